@@ -1,0 +1,154 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes bindings to the CPU oracle (oracle/liboracle.so).
+
+Only tests/, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import this
+package, and only as the checker (or the timed CPU baseline).  The product
+(``mosaic_amd`` / ``libmosaic_hip.so``) never imports it.  See ``oracle/oracle.h`` for the
+reference file:line each restated function follows and how each is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+GRID_H3 = 0
+GRID_BNG = 1
+
+
+def build():
+    """Compile liboracle.so with gcc (oracle/Makefile)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        i64, f64, i32, vp = ctypes.c_int64, ctypes.c_double, ctypes.c_int, ctypes.c_void_p
+        L.oracle_h3_geo_to_h3.restype = i64
+        L.oracle_h3_geo_to_h3.argtypes = [f64, f64, i32]
+        L.oracle_to_radians.restype = f64
+        L.oracle_to_radians.argtypes = [f64, i32]
+        L.oracle_h3_point_to_index.restype = None
+        L.oracle_h3_point_to_index.argtypes = [vp, vp, i64, i32, i32, vp]
+        L.oracle_h3_debug.restype = None
+        L.oracle_h3_debug.argtypes = [f64, f64, i32, vp, vp, vp, vp]
+        L.oracle_bng_point_to_index.restype = i64
+        L.oracle_bng_point_to_index.argtypes = [f64, f64, i32, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_bng_point_to_index_batch.restype = None
+        L.oracle_bng_point_to_index_batch.argtypes = [vp, vp, i64, i32, vp, vp]
+        L.oracle_bng_format.restype = i32
+        L.oracle_bng_format.argtypes = [i64, ctypes.c_char_p, i32]
+        L.oracle_orientation_index.restype = i32
+        L.oracle_orientation_index.argtypes = [f64] * 6
+        L.oracle_wkb_contains.restype = i32
+        L.oracle_wkb_contains.argtypes = [ctypes.c_char_p, i64, f64, f64]
+        L.oracle_pip_join.restype = i64
+        L.oracle_pip_join.argtypes = [vp, i32, i32, i32, vp, vp, i64, vp, i64, vp, vp, i64, i32]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def h3_point_to_index(lon, lat, res, jdk=8):
+    """H3IndexSystem.pointToIndex(lon, lat, res) for arrays (degrees)."""
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    out = np.empty(lon.shape[0], dtype=np.int64)
+    lib().oracle_h3_point_to_index(_ptr(lon), _ptr(lat), lon.shape[0], res, jdk, _ptr(out))
+    return out
+
+
+def h3_geo_to_h3(lat_rad, lng_rad, res):
+    return lib().oracle_h3_geo_to_h3(lat_rad, lng_rad, res)
+
+
+def to_radians(deg, jdk=8):
+    return lib().oracle_to_radians(deg, jdk)
+
+
+def h3_debug(lat_rad, lng_rad, res):
+    face = np.zeros(1, np.int32)
+    x = np.zeros(1)
+    y = np.zeros(1)
+    ijk = np.zeros(3, np.int32)
+    lib().oracle_h3_debug(lat_rad, lng_rad, res, _ptr(face), _ptr(x), _ptr(y), _ptr(ijk))
+    return int(face[0]), float(x[0]), float(y[0]), tuple(int(v) for v in ijk)
+
+
+def bng_point_to_index(e, n, res):
+    """BNGIndexSystem.pointToIndex; raises ValueError for NaN like the reference's IllegalStateException."""
+    err = ctypes.c_int(0)
+    v = lib().oracle_bng_point_to_index(e, n, res, ctypes.byref(err))
+    if err.value == 1:
+        raise ValueError("NaN coordinates are not supported.")
+    if err.value == 2:
+        raise ValueError(f"BNG resolution not supported; found {res}")
+    return v
+
+
+def bng_point_to_index_batch(e, n, res):
+    e = np.ascontiguousarray(e, dtype=np.float64)
+    n = np.ascontiguousarray(n, dtype=np.float64)
+    out = np.empty(e.shape[0], dtype=np.int64)
+    err = np.empty(e.shape[0], dtype=np.uint8)
+    lib().oracle_bng_point_to_index_batch(_ptr(e), _ptr(n), e.shape[0], res, _ptr(out), _ptr(err))
+    return out, err
+
+
+def bng_format(cell_id):
+    buf = ctypes.create_string_buffer(64)
+    n = lib().oracle_bng_format(cell_id, buf, 64)
+    if n < 0:
+        raise ValueError(f"cannot format {cell_id}")
+    return buf.value.decode()
+
+
+def orientation_index(p1, p2, q):
+    return lib().oracle_orientation_index(p1[0], p1[1], p2[0], p2[1], q[0], q[1])
+
+
+def wkb_contains(wkb: bytes, x, y):
+    r = lib().oracle_wkb_contains(wkb, len(wkb), x, y)
+    if r < 0:
+        raise ValueError("unparseable WKB")
+    return bool(r)
+
+
+class _Chips(ctypes.Structure):
+    _fields_ = [("n_chips", ctypes.c_int64), ("index_id", ctypes.c_void_p), ("is_core", ctypes.c_void_p),
+                ("polygon_key", ctypes.c_void_p), ("wkb_offsets", ctypes.c_void_p), ("wkb", ctypes.c_void_p)]
+
+
+def pip_join(chips, grid, res, x, y, n_polygons, jdk=8, pairs=False, threads=1):
+    """Chip join oracle.  ``chips`` is a dict of numpy arrays: index_id (int64), is_core (uint8),
+    polygon_key (int32), wkb_offsets (int64, n+1), wkb (uint8).  Returns (counts, n_pairs[, rows, keys])."""
+    keep = {k: np.ascontiguousarray(v) for k, v in chips.items()}
+    c = _Chips(len(keep["index_id"]), _ptr(keep["index_id"]).value, _ptr(keep["is_core"]).value,
+               _ptr(keep["polygon_key"]).value, _ptr(keep["wkb_offsets"]).value,
+               _ptr(keep["wkb"]).value if len(keep["wkb"]) else None)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    counts = np.zeros(max(n_polygons, 1), dtype=np.int64)
+    if pairs:
+        # first pass to size the output
+        total = lib().oracle_pip_join(ctypes.byref(c), grid, res, jdk, _ptr(x), _ptr(y), len(x), _ptr(counts),
+                                      n_polygons, None, None, 0, 1)
+        rows = np.empty(max(total, 1), np.int64)
+        keys = np.empty(max(total, 1), np.int32)
+        counts[:] = 0
+        lib().oracle_pip_join(ctypes.byref(c), grid, res, jdk, _ptr(x), _ptr(y), len(x), _ptr(counts), n_polygons,
+                              _ptr(rows), _ptr(keys), total, 1)
+        return counts[:n_polygons], total, rows[:total], keys[:total]
+    total = lib().oracle_pip_join(ctypes.byref(c), grid, res, jdk, _ptr(x), _ptr(y), len(x), _ptr(counts),
+                                  n_polygons, None, None, 0, threads)
+    return counts[:n_polygons], total

@@ -1,0 +1,162 @@
+/*
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  CPU restatement of BNGIndexSystem point indexing.
+ *
+ * Follows src/main/scala/com/databricks/labs/mosaic/core/index/BNGIndexSystem.scala with JVM
+ * semantics:
+ *   pointToIndex  :277-291  (Double.toInt truncation/saturation, Int division and remainder)
+ *   getQuadrant   :309-327
+ *   encode        :528-541  (id assembled in f64 from math.pow(10, n) then Double.toLong)
+ *   format        :114-129  (letterMap :84-99, quadrants :36)
+ * Pinned by the reference's golden vectors TestBNGIndexSystem.scala:10-90 (tests/test_oracle_bng.py).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "oracle.h"
+
+/* JVM d2i: NaN -> 0, saturate to [INT_MIN, INT_MAX], truncate toward zero */
+static int32_t jvm_d2i(double d) {
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return 2147483647;
+    if (d <= -2147483648.0) return (-2147483647 - 1);
+    return (int32_t)d;
+}
+/* JVM d2l */
+static int64_t jvm_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+/* java.lang.Math.pow(10, n) is exact for the integer exponents used here (JLS: exact when
+ * representable); n ranges over 0..15. */
+static double pow10i(int n) {
+    static const double t[] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7,
+                               1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                               1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    if (n >= 0 && n <= 22) return t[n];
+    return pow(10.0, (double)n);
+}
+/* JVM Int arithmetic wraps */
+static int32_t imul32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+
+/* BNGIndexSystem.scala:309-327 */
+static int get_quadrant(int res, double e, double n, double divisor) {
+    if (res < -1) {
+        double eQ = e / divisor;
+        double nQ = n / divisor;
+        double eD = eQ - floor(eQ);
+        double nD = nQ - floor(nQ);
+        if (eD < 0.5 && nD < 0.5) return 1; /* SW */
+        if (eD < 0.5) return 2;             /* NW */
+        if (nD < 0.5) return 4;             /* SE */
+        return 3;                           /* NE */
+    }
+    return 0;
+}
+
+/* BNGIndexSystem.scala:528-541 */
+static int64_t encode(int32_t eLetter, int32_t nLetter, int32_t eBin, int32_t nBin, int32_t quadrant,
+                      int32_t nPositions, int32_t res) {
+    double idPlaceholder = pow10i(5 + 2 * nPositions - 2);
+    double eLetterShift = pow10i(3 + 2 * nPositions - 2);
+    double nLetterShift = pow10i(1 + 2 * nPositions - 2);
+    double eShift = pow10i(nPositions);
+    int32_t nShift = 10;
+    double id;
+    if (res == -1) {
+        id = (idPlaceholder + (double)eLetter * eLetterShift) / 100 + (double)quadrant;
+    } else {
+        id = idPlaceholder + (double)eLetter * eLetterShift + (double)nLetter * nLetterShift +
+             (double)eBin * eShift + (double)imul32(nBin, nShift) + (double)quadrant;
+    }
+    return jvm_d2l(id);
+}
+
+static int valid_res(int res) { return res != 0 && res >= -6 && res <= 6; }
+
+/* BNGIndexSystem.scala:277-291 */
+int64_t oracle_bng_point_to_index(double eastings, double northings, int res, int* err) {
+    *err = 0;
+    if (eastings != eastings || northings != northings) {
+        *err = 1; /* IllegalStateException("NaN coordinates are not supported.") */
+        return 0;
+    }
+    if (!valid_res(res)) {
+        *err = 2; /* IllegalStateException("BNG resolution not supported; found ...") */
+        return 0;
+    }
+    int32_t eI = jvm_d2i(eastings);
+    int32_t nI = jvm_d2i(northings);
+    int32_t eLetter = jvm_d2i(floor((double)(eI / 100000)));
+    int32_t nLetter = jvm_d2i(floor((double)(nI / 100000)));
+    int ares = res < 0 ? -res : res;
+    double divisor = res < 0 ? pow10i(6 - ares + 1) : pow10i(6 - res);
+    int32_t quadrant = get_quadrant(res, (double)eI, (double)nI, divisor);
+    int32_t nPositions = res >= -1 ? ares : ares - 1;
+    int32_t eBin = jvm_d2i(floor((double)(eI % 100000) / divisor));
+    int32_t nBin = jvm_d2i(floor((double)(nI % 100000) / divisor));
+    return encode(eLetter, nLetter, eBin, nBin, quadrant, nPositions, res);
+}
+
+void oracle_bng_point_to_index_batch(const double* e, const double* n, int64_t count, int res,
+                                     int64_t* out, uint8_t* err) {
+    for (int64_t i = 0; i < count; i++) {
+        int er;
+        out[i] = oracle_bng_point_to_index(e[i], n[i], res, &er);
+        err[i] = (uint8_t)er;
+    }
+}
+
+/* BNGIndexSystem.scala:84-99 */
+static const char* kLetterMap[13][7] = {
+    {"SV", "SW", "SX", "SY", "SZ", "TV", "TW"}, {"SQ", "SR", "SS", "ST", "SU", "TQ", "TR"},
+    {"SL", "SM", "SN", "SO", "SP", "TL", "TM"}, {"SF", "SG", "SH", "SJ", "SK", "TF", "TG"},
+    {"SA", "SB", "SC", "SD", "SE", "TA", "TB"}, {"NV", "NW", "NX", "NY", "NZ", "OV", "OW"},
+    {"NQ", "NR", "NS", "NT", "NU", "OQ", "OR"}, {"NL", "NM", "NN", "NO", "NP", "OL", "OM"},
+    {"NF", "NG", "NH", "NJ", "NK", "OF", "OG"}, {"NA", "NB", "NC", "ND", "NE", "OA", "OB"},
+    {"HV", "HW", "HX", "HY", "SZ", "JV", "JW"}, {"HQ", "HR", "HS", "HT", "HU", "JQ", "JR"},
+    {"HL", "HM", "HN", "HO", "HP", "JL", "JM"}};
+static const char* kQuadrants[5] = {"", "SW", "NW", "NE", "SE"};
+
+static int digits_to_int(const char* d, int from, int to, int len) {
+    /* Seq.slice(from, to).mkString.toInt */
+    int v = 0;
+    if (from >= len) return -1;
+    if (to > len) to = len;
+    for (int i = from; i < to; i++) v = v * 10 + (d[i] - '0');
+    return v;
+}
+
+/* BNGIndexSystem.scala:114-129 */
+int oracle_bng_format(int64_t id, char* buf, int cap) {
+    char d[32];
+    if (id <= 0) return -1;
+    int len = snprintf(d, sizeof d, "%lld", (long long)id);
+    int row = digits_to_int(d, 3, 5, len);
+    int col = digits_to_int(d, 1, 3, len);
+    if (row < 0 || col < 0 || row > 12 || col > 6) return -1;
+    const char* prefix = kLetterMap[row][col];
+    char out[64];
+    int o = 0;
+    if (len < 6) {
+        out[o++] = prefix[0];
+    } else {
+        int quadrant = d[len - 1] - '0';
+        if (quadrant > 4) return -1;
+        out[o++] = prefix[0];
+        out[o++] = prefix[1];
+        int clen = len - 6; /* digits.drop(5).dropRight(1) */
+        int k = clen / 2;
+        for (int i = 0; i < k; i++) out[o++] = d[5 + i];
+        for (int i = 0; i < k; i++) out[o++] = d[5 + k + i];
+        const char* q = kQuadrants[quadrant];
+        for (int i = 0; q[i]; i++) out[o++] = q[i];
+    }
+    out[o] = 0;
+    if (o + 1 > cap) return -1;
+    memcpy(buf, out, o + 1);
+    return o;
+}

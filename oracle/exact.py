@@ -1,0 +1,88 @@
+"""TEST INFRASTRUCTURE ONLY: exact rational point-in-polygon checker (pure Python, small cases).
+
+Independent of the C oracle's floating-point filter and double-double arithmetic: orientation
+signs are computed with ``fractions.Fraction`` on the exact binary values of the doubles, and the
+location rules follow JTS 1.19 PointLocator / RayCrossingCounter (see oracle/pip.c for the
+reference trail: ST_Contains.scala:34-42 -> MosaicGeometryJTS.scala:101 -> JTS Geometry.contains).
+Used to pin the C oracle's contains() on boundary / near-boundary cases.
+"""
+from fractions import Fraction
+
+INTERIOR, BOUNDARY, EXTERIOR = 0, 1, 2
+
+
+def orientation(p1, p2, q):
+    ax, ay = Fraction(p2[0]) - Fraction(p1[0]), Fraction(p2[1]) - Fraction(p1[1])
+    bx, by = Fraction(q[0]) - Fraction(p2[0]), Fraction(q[1]) - Fraction(p2[1])
+    det = ax * by - ay * bx
+    return (det > 0) - (det < 0)
+
+
+def locate_in_ring(p, ring):
+    px, py = p
+    crossings = 0
+    for i in range(1, len(ring)):
+        p1, p2 = ring[i], ring[i - 1]
+        if p1[0] < px and p2[0] < px:
+            continue
+        if px == p2[0] and py == p2[1]:
+            return BOUNDARY
+        if p1[1] == py and p2[1] == py:
+            if min(p1[0], p2[0]) <= px <= max(p1[0], p2[0]):
+                return BOUNDARY
+            continue
+        if (p1[1] > py and p2[1] <= py) or (p2[1] > py and p1[1] <= py):
+            o = orientation(p1, p2, p)
+            if o == 0:
+                return BOUNDARY
+            if p2[1] < p1[1]:
+                o = -o
+            if o == 1:
+                crossings += 1
+    return INTERIOR if crossings % 2 == 1 else EXTERIOR
+
+
+def _env_excludes(p, ring):
+    xs = [v[0] for v in ring]
+    ys = [v[1] for v in ring]
+    return p[0] < min(xs) or p[0] > max(xs) or p[1] < min(ys) or p[1] > max(ys)
+
+
+def locate_in_polygon(p, rings):
+    if not rings or not rings[0]:
+        return EXTERIOR
+    shell = EXTERIOR if _env_excludes(p, rings[0]) else locate_in_ring(p, rings[0])
+    if shell != INTERIOR:
+        return shell
+    for hole in rings[1:]:
+        if _env_excludes(p, hole):
+            continue
+        h = locate_in_ring(p, hole)
+        if h == INTERIOR:
+            return EXTERIOR
+        if h == BOUNDARY:
+            return BOUNDARY
+    return INTERIOR
+
+
+def contains(parts, p):
+    """parts: list of polygons, each a list of rings (list of (x, y)); True iff JTS contains."""
+    verts = [v for rings in parts for ring in rings for v in ring]
+    if not verts:
+        return False
+    xs = [v[0] for v in verts]
+    ys = [v[1] for v in verts]
+    if p[0] < min(xs) or p[0] > max(xs) or p[1] < min(ys) or p[1] > max(ys):
+        return False
+    if len(parts) == 1:
+        return locate_in_polygon(p, parts[0]) == INTERIOR
+    is_in, nb = False, 0
+    for rings in parts:
+        loc = locate_in_polygon(p, rings)
+        if loc == INTERIOR:
+            is_in = True
+        elif loc == BOUNDARY:
+            nb += 1
+    if nb % 2 == 1:
+        return False
+    return nb > 0 or is_in

@@ -1,0 +1,368 @@
+/*
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  CPU restatement of H3 v3.7 geoToH3.
+ *
+ * Caller in the reference: H3IndexSystem.pointToIndex(lon, lat, res) = h3.geoToH3(lat, lon, res)
+ * (src/main/scala/com/databricks/labs/mosaic/core/index/H3IndexSystem.scala:140-142), reached
+ * from PointIndexGeom.nullSafeEval (expressions/index/PointIndexGeom.scala:32-40) and
+ * PointIndexLonLat.nullSafeEval (PointIndexLonLat.scala:44-51).  h3-java 3.7.0 converts degrees
+ * with java.lang.Math.toRadians and calls H3 C geoToH3 through JNI.
+ *
+ * H3 C v3.7 is third-party and absent here; this file restates its published algorithm
+ * (h3Index.c geoToH3 / _faceIjkToH3, faceijk.c _geoToFaceIjk / _geoToHex2d, coordijk.c
+ * _hex2dToCoordIJK / _upAp7 / _upAp7r / _downAp7 / _downAp7r / _ijkNormalize /
+ * _unitIjkToDigit, geoCoord.c _posAngleRads / _geoAzimuthRads, vec3d.c) with x86-64 gcc
+ * semantics: double arithmetic in SSE2 without contraction, `long double` (x87, 64-bit mantissa)
+ * exactly where H3 uses L-suffixed constants (M_SQRT7, M_SIN60, M_AP7_ROT_RADS, M_2PI,
+ * EPSILON), and glibc libm for the transcendental functions.
+ * Build with -ffp-contract=off (oracle/Makefile).
+ */
+#include <math.h>
+#include <stdint.h>
+
+#include "oracle.h"
+
+#define H3_TABLE static const
+#include "../mosaic_amd/csrc/h3_tables.h"
+
+/* constants.h (v3.7) */
+#define M_2PI_L 6.28318530717958647692528676655900576839433L
+#define M_SQRT7_L 2.6457513110645905905016157536392604257102L
+#define M_SIN60_L 0.8660254037844386467637231707529361834714L
+#define M_AP7_ROT_RADS_L 0.333473172251832115336090755351601070065900389L
+#define RES0_U_GNOMONIC 0.38196601125010500003
+#define EPSILON_L 0.0000000000000001L
+#define MAX_H3_RES 15
+#define MAX_FACE_COORD 2
+
+typedef struct {
+    int i, j, k;
+} CoordIJK;
+
+/* geoCoord.c _posAngleRads */
+static double pos_angle_rads(double rads) {
+    double tmp = ((rads < 0.0L) ? rads + M_2PI_L : rads);
+    if (rads >= M_2PI_L) tmp -= M_2PI_L;
+    return tmp;
+}
+
+/* geoCoord.c _geoAzimuthRads(p1, p2) */
+static double geo_azimuth_rads(double lat1, double lon1, double lat2, double lon2) {
+    return atan2(cos(lat2) * sin(lon2 - lon1),
+                 cos(lat1) * sin(lat2) - sin(lat1) * cos(lat2) * cos(lon2 - lon1));
+}
+
+static double square(double x) { return x * x; }
+
+/* faceijk.c _geoToHex2d */
+static void geo_to_hex2d(double lat, double lon, int res, int* face, double* vx, double* vy) {
+    /* vec3d.c _geoToVec3d */
+    double r0 = cos(lat);
+    double pz = sin(lat);
+    double px = cos(lon) * r0;
+    double py = sin(lon) * r0;
+
+    *face = 0;
+    double sqd = square(kH3FaceCenterPoint[0][0] - px) + square(kH3FaceCenterPoint[0][1] - py) +
+                 square(kH3FaceCenterPoint[0][2] - pz);
+    for (int f = 1; f < 20; f++) {
+        double sqdT = square(kH3FaceCenterPoint[f][0] - px) + square(kH3FaceCenterPoint[f][1] - py) +
+                      square(kH3FaceCenterPoint[f][2] - pz);
+        if (sqdT < sqd) {
+            *face = f;
+            sqd = sqdT;
+        }
+    }
+    double r = acos(1 - sqd / 2);
+    if (r < EPSILON_L) {
+        *vx = *vy = 0.0L;
+        return;
+    }
+    double theta = pos_angle_rads(
+        kH3FaceAxesAzRadsCII[*face][0] -
+        pos_angle_rads(geo_azimuth_rads(kH3FaceCenterGeo[*face][0], kH3FaceCenterGeo[*face][1], lat, lon)));
+    if (res & 1) theta = pos_angle_rads(theta - M_AP7_ROT_RADS_L);
+    r = tan(r);
+    r /= RES0_U_GNOMONIC;
+    for (int i = 0; i < res; i++) r *= M_SQRT7_L;
+    *vx = r * cos(theta);
+    *vy = r * sin(theta);
+}
+
+/* coordijk.c _ijkNormalize */
+static void ijk_normalize(CoordIJK* c) {
+    if (c->i < 0) {
+        c->j -= c->i;
+        c->k -= c->i;
+        c->i = 0;
+    }
+    if (c->j < 0) {
+        c->i -= c->j;
+        c->k -= c->j;
+        c->j = 0;
+    }
+    if (c->k < 0) {
+        c->i -= c->k;
+        c->j -= c->k;
+        c->k = 0;
+    }
+    int min = c->i;
+    if (c->j < min) min = c->j;
+    if (c->k < min) min = c->k;
+    if (min > 0) {
+        c->i -= min;
+        c->j -= min;
+        c->k -= min;
+    }
+}
+
+/* coordijk.c _hex2dToCoordIJK */
+static void hex2d_to_coord_ijk(double vx, double vy, CoordIJK* h) {
+    double a1, a2, x1, x2, r1, r2;
+    int m1, m2;
+    h->k = 0;
+    a1 = fabsl(vx);
+    a2 = fabsl(vy);
+    x2 = a2 / M_SIN60_L;
+    x1 = a1 + x2 / 2.0;
+    m1 = x1;
+    m2 = x2;
+    r1 = x1 - m1;
+    r2 = x2 - m2;
+    if (r1 < 0.5) {
+        if (r1 < 1.0 / 3.0) {
+            if (r2 < (1.0 + r1) / 2.0) {
+                h->i = m1;
+                h->j = m2;
+            } else {
+                h->i = m1;
+                h->j = m2 + 1;
+            }
+        } else {
+            if (r2 < (1.0 - r1)) {
+                h->j = m2;
+            } else {
+                h->j = m2 + 1;
+            }
+            if ((1.0 - r1) <= r2 && r2 < (2.0 * r1)) {
+                h->i = m1 + 1;
+            } else {
+                h->i = m1;
+            }
+        }
+    } else {
+        if (r1 < 2.0 / 3.0) {
+            if (r2 < (1.0 - r1)) {
+                h->j = m2;
+            } else {
+                h->j = m2 + 1;
+            }
+            if ((2.0 * r1 - 1.0) < r2 && r2 < (1.0 - r1)) {
+                h->i = m1;
+            } else {
+                h->i = m1 + 1;
+            }
+        } else {
+            if (r2 < (r1 / 2.0)) {
+                h->i = m1 + 1;
+                h->j = m2;
+            } else {
+                h->i = m1 + 1;
+                h->j = m2 + 1;
+            }
+        }
+    }
+    if (vx < 0.0) {
+        if ((h->j % 2) == 0) {
+            long long int axisi = h->j / 2;
+            long long int diff = h->i - axisi;
+            h->i = h->i - 2.0 * diff;
+        } else {
+            long long int axisi = (h->j + 1) / 2;
+            long long int diff = h->i - axisi;
+            h->i = h->i - (2.0 * diff + 1);
+        }
+    }
+    if (vy < 0.0) {
+        h->i = h->i - (2 * h->j + 1) / 2;
+        h->j = -1 * h->j;
+    }
+    ijk_normalize(h);
+}
+
+/* coordijk.c _upAp7 (Class III parent) / _upAp7r (Class II parent) */
+static void up_ap7(CoordIJK* c) {
+    int i = c->i - c->k;
+    int j = c->j - c->k;
+    c->i = (int)lround((3 * i - j) / 7.0);
+    c->j = (int)lround((i + 2 * j) / 7.0);
+    c->k = 0;
+    ijk_normalize(c);
+}
+static void up_ap7r(CoordIJK* c) {
+    int i = c->i - c->k;
+    int j = c->j - c->k;
+    c->i = (int)lround((2 * i + j) / 7.0);
+    c->j = (int)lround((3 * j - i) / 7.0);
+    c->k = 0;
+    ijk_normalize(c);
+}
+/* coordijk.c _downAp7 / _downAp7r */
+static void down_ap7(CoordIJK* c) {
+    CoordIJK r = {3 * c->i + 1 * c->j + 0 * c->k, 0 * c->i + 3 * c->j + 1 * c->k,
+                  1 * c->i + 0 * c->j + 3 * c->k};
+    *c = r;
+    ijk_normalize(c);
+}
+static void down_ap7r(CoordIJK* c) {
+    CoordIJK r = {3 * c->i + 0 * c->j + 1 * c->k, 1 * c->i + 3 * c->j + 0 * c->k,
+                  0 * c->i + 1 * c->j + 3 * c->k};
+    *c = r;
+    ijk_normalize(c);
+}
+
+/* coordijk.c _unitIjkToDigit: UNIT_VECS[d] = (d>>2 & 1, d>>1 & 1, d & 1) */
+static int unit_ijk_to_digit(CoordIJK c) {
+    ijk_normalize(&c);
+    for (int d = 0; d < 7; d++) {
+        if (c.i == ((d >> 2) & 1) && c.j == ((d >> 1) & 1) && c.k == (d & 1)) return d;
+    }
+    return 7; /* INVALID_DIGIT */
+}
+
+/* h3IndexInlines / h3Index.c bit helpers */
+#define H3_RES_OFFSET 52
+#define H3_BC_OFFSET 45
+#define H3_MODE_OFFSET 59
+#define H3_PER_DIGIT_OFFSET 3
+static int get_digit(uint64_t h, int r) { return (int)((h >> ((MAX_H3_RES - r) * 3)) & 7); }
+static uint64_t set_digit(uint64_t h, int r, int d) {
+    int s = (MAX_H3_RES - r) * 3;
+    return (h & ~((uint64_t)7 << s)) | ((uint64_t)d << s);
+}
+static int get_res(uint64_t h) { return (int)((h >> H3_RES_OFFSET) & 15); }
+
+/* algos.c _rotate60ccw / _rotate60cw */
+static int rotate60ccw(int d) {
+    switch (d) {
+        case 1: return 5;
+        case 5: return 4;
+        case 4: return 6;
+        case 6: return 2;
+        case 2: return 3;
+        case 3: return 1;
+        default: return d;
+    }
+}
+static int rotate60cw(int d) {
+    switch (d) {
+        case 1: return 3;
+        case 3: return 2;
+        case 2: return 6;
+        case 6: return 4;
+        case 4: return 5;
+        case 5: return 1;
+        default: return d;
+    }
+}
+static int leading_nonzero_digit(uint64_t h) {
+    for (int r = 1; r <= get_res(h); r++)
+        if (get_digit(h, r)) return get_digit(h, r);
+    return 0;
+}
+static uint64_t rotate60ccw_h(uint64_t h) {
+    for (int r = 1, res = get_res(h); r <= res; r++) h = set_digit(h, r, rotate60ccw(get_digit(h, r)));
+    return h;
+}
+static uint64_t rotate60cw_h(uint64_t h) {
+    for (int r = 1, res = get_res(h); r <= res; r++) h = set_digit(h, r, rotate60cw(get_digit(h, r)));
+    return h;
+}
+/* h3Index.c _h3RotatePent60ccw */
+static uint64_t rotate_pent60ccw(uint64_t h) {
+    int found = 0;
+    for (int r = 1, res = get_res(h); r <= res; r++) {
+        h = set_digit(h, r, rotate60ccw(get_digit(h, r)));
+        if (!found && get_digit(h, r) != 0) {
+            found = 1;
+            if (leading_nonzero_digit(h) == 1) h = rotate60ccw_h(h);
+        }
+    }
+    return h;
+}
+
+/* h3Index.c _faceIjkToH3 */
+static uint64_t face_ijk_to_h3(int face, CoordIJK ijk, int res) {
+    uint64_t h = 0x00001fffffffffffULL; /* H3_INIT: all digits 7 */
+    h |= (uint64_t)1 << H3_MODE_OFFSET;
+    h |= (uint64_t)res << H3_RES_OFFSET;
+    if (res == 0) {
+        if (ijk.i > MAX_FACE_COORD || ijk.j > MAX_FACE_COORD || ijk.k > MAX_FACE_COORD) return 0;
+        int bc = kH3FaceIjkBaseCells[face][ijk.i][ijk.j][ijk.k] >> 3;
+        return h | ((uint64_t)bc << H3_BC_OFFSET);
+    }
+    for (int r = res - 1; r >= 0; r--) {
+        CoordIJK last = ijk, center;
+        if ((r + 1) & 1) {
+            up_ap7(&ijk);
+            center = ijk;
+            down_ap7(&center);
+        } else {
+            up_ap7r(&ijk);
+            center = ijk;
+            down_ap7r(&center);
+        }
+        CoordIJK diff = {last.i - center.i, last.j - center.j, last.k - center.k};
+        ijk_normalize(&diff);
+        h = set_digit(h, r + 1, unit_ijk_to_digit(diff));
+    }
+    if (ijk.i > MAX_FACE_COORD || ijk.j > MAX_FACE_COORD || ijk.k > MAX_FACE_COORD) return 0;
+    int packed = kH3FaceIjkBaseCells[face][ijk.i][ijk.j][ijk.k];
+    int bc = packed >> 3;
+    int rots = packed & 7;
+    h |= (uint64_t)bc << H3_BC_OFFSET;
+    if (kH3BaseCellData[bc][4]) {
+        if (leading_nonzero_digit(h) == 1) {
+            if (kH3BaseCellData[bc][5] == face || kH3BaseCellData[bc][6] == face)
+                h = rotate60cw_h(h);
+            else
+                h = rotate60ccw_h(h);
+        }
+        for (int i = 0; i < rots; i++) h = rotate_pent60ccw(h);
+    } else {
+        for (int i = 0; i < rots; i++) h = rotate60ccw_h(h);
+    }
+    return h;
+}
+
+/* h3Index.c geoToH3 */
+int64_t oracle_h3_geo_to_h3(double lat, double lon, int res) {
+    if (res < 0 || res > MAX_H3_RES) return 0;
+    if (!isfinite(lat) || !isfinite(lon)) return 0;
+    int face;
+    double vx, vy;
+    geo_to_hex2d(lat, lon, res, &face, &vx, &vy);
+    CoordIJK ijk;
+    hex2d_to_coord_ijk(vx, vy, &ijk);
+    return (int64_t)face_ijk_to_h3(face, ijk, res);
+}
+
+void oracle_h3_debug(double lat, double lon, int res, int* face, double* x, double* y, int* ijk) {
+    geo_to_hex2d(lat, lon, res, face, x, y);
+    CoordIJK c;
+    hex2d_to_coord_ijk(*x, *y, &c);
+    ijk[0] = c.i;
+    ijk[1] = c.j;
+    ijk[2] = c.k;
+}
+
+/* java.lang.Math.toRadians -- JDK 8: angdeg / 180.0 * PI; JDK 9+: angdeg * DEGREES_TO_RADIANS */
+double oracle_to_radians(double deg, int jdk) {
+    if (jdk <= 8) return deg / 180.0 * 3.141592653589793;
+    return deg * 0.017453292519943295;
+}
+
+void oracle_h3_point_to_index(const double* lon, const double* lat, int64_t n, int res, int jdk,
+                              int64_t* out) {
+    for (int64_t i = 0; i < n; i++)
+        out[i] = oracle_h3_geo_to_h3(oracle_to_radians(lat[i], jdk), oracle_to_radians(lon[i], jdk), res);
+}
