@@ -1,0 +1,131 @@
+/*
+ * libmosaic_hip.so -- C ABI of the MI355X engine for Mosaic's point-in-polygon chip-join hot path.
+ *
+ * Plain C: pointers, sizes and status codes; no exceptions cross the boundary; no torch types.
+ * Every entry point is callable from a JNI shim (the Catalyst columnar exec sketched in
+ * INTEGRATION.md) or from Python ctypes (mosaic_amd/_native.py).
+ *
+ * Reference interfaces replaced (bransonf/mosaic @ 0.3.9, paths under
+ * src/main/scala/com/databricks/labs/mosaic/):
+ *   mosaic_point_to_cell      grid_pointascellid / grid_longlatascellid per row:
+ *                             expressions/index/PointIndexGeom.scala:32-40,
+ *                             expressions/index/PointIndexLonLat.scala:44-51 ->
+ *                             core/index/H3IndexSystem.scala:140-142 (pointToIndex) and
+ *                             core/index/BNGIndexSystem.scala:277-291 (pointToIndex)
+ *   mosaic_resolution         H3IndexSystem.getResolution (H3IndexSystem.scala:39-54),
+ *                             BNGIndexSystem.getResolution (BNGIndexSystem.scala:342-353)
+ *   mosaic_bng_format/_parse  BNGIndexSystem.format / parse (BNGIndexSystem.scala:114-129, 391-413)
+ *   mosaic_chip_table_create  the build side of the chip join: rows of ChipType
+ *                             struct<is_core, index_id, wkb> (core/types/ChipType.scala:17-28,
+ *                             core/types/model/MosaicChip.scala:20-74) produced by
+ *                             grid_tessellateexplode (expressions/index/MosaicExplode.scala:70-79)
+ *   mosaic_pip_join_count     the Quickstart join + filter + groupBy(zone).count():
+ *   mosaic_pip_join_pairs       point_cell == chip.index_id && (chip.is_core || st_contains(chip.wkb, point))
+ *                             (notebooks/examples/python/QuickstartNotebook.py:205-219;
+ *                             sql/join/PointInPolygonJoin.scala:68-84)
+ *   mosaic_st_contains        st_contains(geom, point) per row: expressions/geometry/ST_Contains.scala:34-42
+ *                             -> core/geometry/MosaicGeometryJTS.scala:101 (JTS Geometry.contains)
+ *
+ * Conventions
+ *   - Return value: MOSAIC_OK (0) or a mosaic_status code; mosaic_last_error() (thread-local)
+ *     holds the message.  MOSAIC_E_RES / MOSAIC_E_NAN carry the reference's exception messages
+ *     ("H3 resolution has to be between 0 and 15; found N", "BNG resolution not supported; found N",
+ *     "NaN coordinates are not supported.") so a JNI shim can rethrow IllegalStateException.
+ *   - Input arrays are borrowed for the duration of the call and may live in host memory or in
+ *     device memory of the context's GPU (detected per pointer).  Host inputs are staged over PCIe.
+ *   - Calls are synchronous unless the context option "async" is 1, in which case device-pointer
+ *     calls only enqueue work on the context stream (mosaic_sync() waits and reports deferred errors).
+ *   - A context is bound to one GPU; use one context per device (one process per GPU).  Calls on
+ *     one context are serialised on its stream; distinct contexts may be used from distinct threads.
+ */
+#ifndef MOSAIC_HIP_H
+#define MOSAIC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MOSAIC_ABI_VERSION 1
+
+typedef enum {
+    MOSAIC_OK = 0,
+    MOSAIC_E_ARG = 1,      /* invalid argument (null pointer, bad size, bad option) */
+    MOSAIC_E_RES = 2,      /* unsupported resolution (IllegalStateException in the reference) */
+    MOSAIC_E_NAN = 3,      /* NaN coordinate with BNG (IllegalStateException in the reference) */
+    MOSAIC_E_HIP = 4,      /* HIP runtime error / no device */
+    MOSAIC_E_WKB = 5,      /* undecodable or unsupported chip WKB */
+    MOSAIC_E_CAPACITY = 6, /* output buffer too small (pairs) or deferred queue overflow (async) */
+    MOSAIC_E_NOMEM = 7     /* allocation failure */
+} mosaic_status;
+
+typedef enum { MOSAIC_GRID_H3 = 0, MOSAIC_GRID_BNG = 1 } mosaic_grid;
+
+typedef struct mosaic_ctx mosaic_ctx;
+typedef struct mosaic_chips mosaic_chips;
+
+int mosaic_abi_version(void);
+const char* mosaic_last_error(void);
+
+/* ---- context ---- */
+/* Bind a context to HIP device `device` (ordinal as seen by this process). */
+int mosaic_init(int device, mosaic_ctx** out);
+int mosaic_destroy(mosaic_ctx* ctx);
+/* Options: "jdk" (8: Math.toRadians = deg / 180 * PI, the JDK 8 runtime of the reference's CI;
+ * 9+: deg * DEGREES_TO_RADIANS), "async" (0/1), "block" (threads per block, multiple of 64),
+ * "blocks_per_cu" (grid sizing). */
+int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
+/* The hipStream_t work is enqueued on (owned by the context unless set). */
+int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
+int mosaic_set_stream(mosaic_ctx* ctx, void* stream);
+/* Wait for enqueued work; reports deferred errors of async calls. */
+int mosaic_sync(mosaic_ctx* ctx);
+/* Counters of the last join/index call: [0] rows that needed the exact H3 path,
+ * [1] (point, border chip) contains tests, [2] matched pairs.  Filled only by sync calls. */
+int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3);
+
+/* ---- grid systems ---- */
+/* getResolution for an Int resolution; validates the range of the grid system. */
+int mosaic_resolution(int grid, int res, int* out);
+/* getResolution for a String resolution ("9" for H3; "100m", "500m", ... or "4" for BNG). */
+int mosaic_resolution_str(int grid, const char* res, int* out);
+/* grid_pointascellid / grid_longlatascellid: x = lon (H3) or easting (BNG), y = lat or northing.
+ * valid (nullable): 1 = row present; null rows give out_valid 0 and cell 0 (NullIntolerant). */
+int mosaic_point_to_cell(mosaic_ctx* ctx, int grid, int res, const double* x, const double* y,
+                         const uint8_t* valid, int64_t n, int64_t* out_cell, uint8_t* out_valid);
+/* BNG id <-> string (BNGIndexSystem.format / parse).  format returns the string length. */
+int mosaic_bng_format(int64_t id, char* buf, size_t cap);
+int mosaic_bng_parse(const char* s, int64_t* out);
+
+/* ---- chip table (build side) ---- */
+/* n_chips rows of ChipType: is_core[i], index_id[i] (int64 cell id), wkb bytes
+ * wkb[wkb_offsets[i] .. wkb_offsets[i+1]) (Polygon / MultiPolygon, either byte order; empty or
+ * zero-length = no geometry), polygon_key[i] in [0, n_polygons) (the row's zone / group key).
+ * The table is copied to device memory; the caller may free its buffers after the call. */
+int mosaic_chip_table_create(mosaic_ctx* ctx, int grid, int res, int64_t n_chips, const uint8_t* is_core,
+                             const int64_t* index_id, const int64_t* wkb_offsets, const uint8_t* wkb,
+                             const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out);
+int mosaic_chip_table_destroy(mosaic_chips* chips);
+/* out8: n_chips, n_cells, n_border, n_vertices, n_rings, device_bytes, hash_capacity, n_polygons */
+int mosaic_chip_table_info(const mosaic_chips* chips, int64_t* out8);
+
+/* ---- the join ---- */
+/* counts[p] = number of (point, chip) pairs with chip polygon_key p (overwritten). */
+int mosaic_pip_join_count(mosaic_ctx* ctx, const mosaic_chips* chips, const double* x, const double* y,
+                          int64_t n, int64_t* counts);
+/* Emits every matching (row, polygon_key) pair (unordered).  If more than `cap` pairs match,
+ * returns MOSAIC_E_CAPACITY with *n_out = required size. */
+int mosaic_pip_join_pairs(mosaic_ctx* ctx, const mosaic_chips* chips, const double* x, const double* y,
+                          int64_t n, int64_t* out_row, int32_t* out_key, int64_t cap, int64_t* n_out);
+
+/* ---- st_contains per row ---- */
+/* out[i] = JTS contains(geometry[geom_index[i]], POINT(px[i] py[i])); geometries given as WKB. */
+int mosaic_st_contains(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* wkb_offsets, const uint8_t* wkb,
+                       const int32_t* geom_index, const double* px, const double* py, int64_t n, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,114 @@
+"""ctypes binding of libmosaic_hip.so (include/mosaic_hip.h).
+
+The product path always runs through this library; there is no CPU fallback.  Loading fails
+loudly (``NativeUnavailable``) when the in-tree library is missing or no GPU is visible.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmosaic_hip.so")
+
+MOSAIC_OK = 0
+MOSAIC_E_ARG = 1
+MOSAIC_E_RES = 2
+MOSAIC_E_NAN = 3
+MOSAIC_E_HIP = 4
+MOSAIC_E_WKB = 5
+MOSAIC_E_CAPACITY = 6
+MOSAIC_E_NOMEM = 7
+
+GRID_H3 = 0
+GRID_BNG = 1
+
+EXPORTS = [
+    "mosaic_abi_version", "mosaic_last_error", "mosaic_init", "mosaic_destroy", "mosaic_set_option",
+    "mosaic_get_stream", "mosaic_set_stream", "mosaic_sync", "mosaic_last_stats", "mosaic_resolution",
+    "mosaic_resolution_str", "mosaic_point_to_cell", "mosaic_bng_format", "mosaic_bng_parse",
+    "mosaic_chip_table_create", "mosaic_chip_table_destroy", "mosaic_chip_table_info", "mosaic_pip_join_count",
+    "mosaic_pip_join_pairs", "mosaic_st_contains",
+]
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class MosaicError(RuntimeError):
+    """A non-zero mosaic_status.  ``code`` is the status; the message is the library's."""
+
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+class IllegalStateException(MosaicError, ValueError):
+    """Raised where the reference throws java.lang.IllegalStateException (bad resolution, NaN)."""
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc")], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeUnavailable(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i64, i32, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p
+    sig = {
+        "mosaic_abi_version": ([], i32),
+        "mosaic_last_error": ([], cp),
+        "mosaic_init": ([i32, ctypes.POINTER(vp)], i32),
+        "mosaic_destroy": ([vp], i32),
+        "mosaic_set_option": ([vp, cp, i64], i32),
+        "mosaic_get_stream": ([vp, ctypes.POINTER(vp)], i32),
+        "mosaic_set_stream": ([vp, vp], i32),
+        "mosaic_sync": ([vp], i32),
+        "mosaic_last_stats": ([vp, vp], i32),
+        "mosaic_resolution": ([i32, i32, ctypes.POINTER(i32)], i32),
+        "mosaic_resolution_str": ([i32, cp, ctypes.POINTER(i32)], i32),
+        "mosaic_point_to_cell": ([vp, i32, i32, vp, vp, vp, i64, vp, vp], i32),
+        "mosaic_bng_format": ([i64, cp, ctypes.c_size_t], i32),
+        "mosaic_bng_parse": ([cp, ctypes.POINTER(i64)], i32),
+        "mosaic_chip_table_create": ([vp, i32, i32, i64, vp, vp, vp, vp, vp, i32, ctypes.POINTER(vp)], i32),
+        "mosaic_chip_table_destroy": ([vp], i32),
+        "mosaic_chip_table_info": ([vp, vp], i32),
+        "mosaic_pip_join_count": ([vp, vp, vp, vp, i64, vp], i32),
+        "mosaic_pip_join_pairs": ([vp, vp, vp, vp, i64, vp, vp, i64, ctypes.POINTER(i64)], i32),
+        "mosaic_st_contains": ([vp, i64, vp, vp, vp, vp, vp, i64, vp], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc == MOSAIC_OK:
+        return
+    msg = lib().mosaic_last_error().decode(errors="replace")
+    if rc in (MOSAIC_E_RES, MOSAIC_E_NAN):
+        raise IllegalStateException(rc, msg)
+    raise MosaicError(rc, msg)
+
+
+def ptr(a):
+    """Address of a numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    raise TypeError(f"unsupported buffer type {type(a)}")

@@ -1,0 +1,337 @@
+"""Host-side mirror of the reference's function surface for the PIP chip-join path.
+
+Mirrors (bransonf/mosaic 0.3.9, src/main/scala/com/databricks/labs/mosaic/):
+  * ``MosaicContext.build(indexSystem, geometryAPI)``       functions/MosaicContext.scala:796-800
+  * ``functions.grid_pointascellid / grid_longlatascellid``  MosaicContext.scala:655-668
+  * ``functions.st_contains``                                MosaicContext.scala (st_contains) ->
+                                                             expressions/geometry/ST_Contains.scala:21-64
+  * ``H3IndexSystem / BNGIndexSystem.getResolution``         core/index/H3IndexSystem.scala:39-54,
+                                                             core/index/BNGIndexSystem.scala:342-353
+  * the chip join of the Quickstart                         notebooks/examples/python/QuickstartNotebook.py:205-219,
+                                                             sql/join/PointInPolygonJoin.scala:68-84
+Everything computes on the GPU through libmosaic_hip.so; inputs are columnar (numpy arrays or torch
+tensors, host or device), the Spark row wrappers are not reproduced.  Errors follow the reference:
+bad resolutions and NaN BNG coordinates raise ``IllegalStateException`` with the reference's message.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from . import wkb as W
+
+
+class IndexSystem:
+    name = None
+    grid = None
+    cell_id_type = "long"
+
+    def get_resolution(self, res):
+        raise NotImplementedError
+
+
+class H3IndexSystem(IndexSystem):
+    """core/index/H3IndexSystem.scala; cell ids are LongType."""
+
+    name = "H3"
+    grid = N.GRID_H3
+    cell_id_type = "long"
+
+    def get_resolution(self, res):
+        out = ctypes.c_int(0)
+        if isinstance(res, (bool,)):
+            raise ValueError("Resolution must be an Int or String.")
+        if isinstance(res, (int, np.integer)):
+            N.check(N.lib().mosaic_resolution(self.grid, int(res), ctypes.byref(out)))
+        elif isinstance(res, str):
+            N.check(N.lib().mosaic_resolution_str(self.grid, res.encode(), ctypes.byref(out)))
+        else:
+            raise ValueError("Resolution must be an Int or String.")
+        return out.value
+
+    def format(self, cell_id):
+        return format(int(cell_id), "x")
+
+    def parse(self, s):
+        return int(s, 16)
+
+
+class BNGIndexSystem(IndexSystem):
+    """core/index/BNGIndexSystem.scala; cell ids default to StringType (MosaicContext.scala:41-48)."""
+
+    name = "BNG"
+    grid = N.GRID_BNG
+    cell_id_type = "string"
+
+    def get_resolution(self, res):
+        out = ctypes.c_int(0)
+        if isinstance(res, (int, np.integer)) and not isinstance(res, bool):
+            N.check(N.lib().mosaic_resolution(self.grid, int(res), ctypes.byref(out)))
+        elif isinstance(res, str):
+            N.check(N.lib().mosaic_resolution_str(self.grid, res.encode(), ctypes.byref(out)))
+        else:
+            raise N.IllegalStateException(N.MOSAIC_E_RES, f"BNG resolution not supported; found {res}")
+        return out.value
+
+    def format(self, cell_id):
+        buf = ctypes.create_string_buffer(64)
+        rc = N.lib().mosaic_bng_format(int(cell_id), buf, 64)
+        if rc < 0 or rc > 64:
+            N.check(rc if rc > 0 else N.MOSAIC_E_ARG)
+        return buf.value.decode()
+
+    def parse(self, s):
+        out = ctypes.c_int64(0)
+        N.check(N.lib().mosaic_bng_parse(s.encode(), ctypes.byref(out)))
+        return out.value
+
+
+INDEX_SYSTEMS = {"H3": H3IndexSystem, "BNG": BNGIndexSystem}
+
+
+def _f64(a):
+    """Contiguous float64 buffer (numpy or torch, host or device) kept alive by the caller."""
+    if hasattr(a, "data_ptr"):
+        import torch
+
+        if a.dtype != torch.float64:
+            a = a.to(torch.float64)
+        return a.contiguous()
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _is_torch(a):
+    return hasattr(a, "data_ptr") and not isinstance(a, np.ndarray)
+
+
+def _points_xy(points):
+    """Accepts (x, y) arrays, an (n, 2) array, or a sequence of WKT / WKB point geometries."""
+    if isinstance(points, tuple) and len(points) == 2:
+        return _f64(points[0]), _f64(points[1])
+    if isinstance(points, np.ndarray) and points.ndim == 2 and points.shape[1] == 2:
+        return _f64(points[:, 0]), _f64(points[:, 1])
+    if _is_torch(points) and points.dim() == 2:
+        return _f64(points[:, 0]), _f64(points[:, 1])
+    xs, ys = [], []
+    for g in points:
+        kind, v = W.read_wkb(g) if isinstance(g, (bytes, bytearray, memoryview)) else W.read_wkt(g)
+        if kind == "point":
+            if v is None:
+                raise ValueError("POINT EMPTY has no centroid")
+            xs.append(v[0])
+            ys.append(v[1])
+        else:
+            # the reference indexes the centroid of non-point geometries (PointIndexGeom.scala:35-36)
+            raise ValueError("grid_pointascellid expects point geometries in this engine")
+    return np.asarray(xs, np.float64), np.asarray(ys, np.float64)
+
+
+class ChipTable:
+    """Device-resident build side of the chip join: rows of ChipType(is_core, index_id, wkb) plus the
+    key of the polygon each chip belongs to (core/types/ChipType.scala:17-28)."""
+
+    def __init__(self, ctx, is_core, index_id, wkb_list, polygon_key, n_polygons=None):
+        self.ctx = ctx
+        is_core = np.ascontiguousarray(is_core, dtype=np.uint8)
+        index_id = np.ascontiguousarray(index_id, dtype=np.int64)
+        polygon_key = np.ascontiguousarray(polygon_key, dtype=np.int32)
+        if isinstance(wkb_list, tuple) and len(wkb_list) == 2:
+            offsets = np.ascontiguousarray(wkb_list[0], dtype=np.int64)
+            data = np.ascontiguousarray(wkb_list[1], dtype=np.uint8)
+        else:
+            lens = np.array([0 if w is None else len(w) for w in wkb_list], dtype=np.int64)
+            offsets = np.zeros(len(lens) + 1, np.int64)
+            np.cumsum(lens, out=offsets[1:])
+            data = np.frombuffer(b"".join(b"" if w is None else bytes(w) for w in wkb_list), dtype=np.uint8)
+            data = np.ascontiguousarray(data) if len(data) else np.zeros(1, np.uint8)
+        n = len(index_id)
+        if not (len(is_core) == n == len(polygon_key) == len(offsets) - 1):
+            raise ValueError("chip columns have different lengths")
+        if n_polygons is None:
+            n_polygons = int(polygon_key.max()) + 1 if n else 0
+        self.n_polygons = int(n_polygons)
+        self.n_chips = n
+        h = ctypes.c_void_p()
+        N.check(N.lib().mosaic_chip_table_create(
+            ctx.handle, ctx.index_system.grid, ctx.resolution_of_table, n, N.ptr(is_core), N.ptr(index_id),
+            N.ptr(offsets), N.ptr(data), N.ptr(polygon_key), self.n_polygons, ctypes.byref(h)))
+        self.handle = h
+
+    def info(self):
+        out = np.zeros(8, np.int64)
+        N.check(N.lib().mosaic_chip_table_info(self.handle, N.ptr(out)))
+        keys = ["n_chips", "n_cells", "n_border", "n_vertices", "n_rings", "device_bytes", "hash_capacity",
+                "n_polygons"]
+        return dict(zip(keys, (int(v) for v in out)))
+
+    def close(self):
+        if self.handle:
+            N.lib().mosaic_chip_table_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MosaicContext:
+    """``MosaicContext.build(indexSystem, geometryAPI)``; geometry API is JTS semantics only."""
+
+    def __init__(self, index_system="H3", geometry_api="JTS", device=0, jdk=8):
+        if geometry_api.upper() != "JTS":
+            raise ValueError("only JTS semantics are implemented (BASELINE north_star)")
+        if index_system not in INDEX_SYSTEMS:
+            raise ValueError(f"unsupported index system {index_system} (H3, BNG)")
+        self.index_system = INDEX_SYSTEMS[index_system]()
+        self.geometry_api = "JTS"
+        h = ctypes.c_void_p()
+        N.check(N.lib().mosaic_init(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+        self.set_option("jdk", jdk)
+        self.resolution_of_table = None
+
+    @classmethod
+    def build(cls, index_system="H3", geometry_api="JTS", device=0, jdk=8):
+        return cls(index_system, geometry_api, device, jdk)
+
+    def set_option(self, key, value):
+        N.check(N.lib().mosaic_set_option(self.handle, key.encode(), int(value)))
+
+    def stream(self):
+        s = ctypes.c_void_p()
+        N.check(N.lib().mosaic_get_stream(self.handle, ctypes.byref(s)))
+        return s.value
+
+    def set_stream(self, stream_handle):
+        N.check(N.lib().mosaic_set_stream(self.handle, stream_handle))
+
+    def sync(self):
+        N.check(N.lib().mosaic_sync(self.handle))
+
+    def last_stats(self):
+        out = np.zeros(3, np.int64)
+        N.check(N.lib().mosaic_last_stats(self.handle, N.ptr(out)))
+        return {"exact_path_rows": int(out[0]), "contains_tests": int(out[1]), "pairs": int(out[2])}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            N.lib().mosaic_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- grid functions ----
+    def _cells(self, x, y, resolution, valid=None):
+        res = self.index_system.get_resolution(resolution)
+        x, y = _f64(x), _f64(y)
+        n = int(x.shape[0])
+        if _is_torch(x):
+            import torch
+
+            out = torch.empty(n, dtype=torch.int64, device=x.device)
+        else:
+            out = np.empty(n, np.int64)
+        v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+        ov = None if v is None else np.empty(n, np.uint8)
+        N.check(N.lib().mosaic_point_to_cell(self.handle, self.index_system.grid, res, N.ptr(x), N.ptr(y), N.ptr(v), n,
+                                             N.ptr(out), N.ptr(ov)))
+        return (out, ov) if v is not None else out
+
+    def _serialize(self, cells):
+        """IndexSystem.serializeCellId: Long for H3, String for BNG (IndexSystem.scala:37-46)."""
+        if self.index_system.cell_id_type == "string":
+            arr = cells.cpu().numpy() if _is_torch(cells) else cells
+            return [self.index_system.format(c) for c in arr]
+        return cells
+
+    def grid_longlatascellid(self, lon, lat, resolution, raw=False):
+        """PointIndexLonLat (expressions/index/PointIndexLonLat.scala:44-51)."""
+        cells = self._cells(lon, lat, resolution)
+        return cells if raw else self._serialize(cells)
+
+    def grid_pointascellid(self, points, resolution, raw=False):
+        """PointIndexGeom (expressions/index/PointIndexGeom.scala:32-40)."""
+        x, y = _points_xy(points)
+        cells = self._cells(x, y, resolution)
+        return cells if raw else self._serialize(cells)
+
+    # ---- st_contains ----
+    def st_contains(self, geoms, points):
+        """Row-wise st_contains(geom, point): geoms are WKB bytes or WKT strings (one per row, or one
+        for all rows); points as in grid_pointascellid."""
+        x, y = _points_xy(points)
+        x, y = np.asarray(x), np.asarray(y)
+        n = len(x)
+        if isinstance(geoms, (str, bytes, bytearray)):
+            geoms = [geoms]
+            index = np.zeros(n, np.int32)
+        else:
+            geoms = list(geoms)
+            if len(geoms) != n:
+                raise ValueError("one geometry per point row expected")
+            index = np.arange(n, dtype=np.int32)
+        blobs = []
+        for g in geoms:
+            if isinstance(g, str):
+                kind, parts = W.read_wkt(g)
+                if kind != "polygon":
+                    raise ValueError("st_contains left side must be polygonal in this engine")
+                blobs.append(W.geometry_wkb(parts) if parts else b"")
+            else:
+                blobs.append(bytes(g))
+        lens = np.array([len(b) for b in blobs], np.int64)
+        offs = np.zeros(len(blobs) + 1, np.int64)
+        np.cumsum(lens, out=offs[1:])
+        data = np.frombuffer(b"".join(blobs) or b"\0", dtype=np.uint8).copy()
+        out = np.zeros(n, np.uint8)
+        N.check(N.lib().mosaic_st_contains(self.handle, len(blobs), N.ptr(offs), N.ptr(data), N.ptr(index),
+                                           N.ptr(np.ascontiguousarray(x)), N.ptr(np.ascontiguousarray(y)), n,
+                                           N.ptr(out)))
+        return out.astype(bool)
+
+    # ---- the chip join ----
+    def chip_table(self, is_core, index_id, wkb_list, polygon_key, resolution, n_polygons=None):
+        """Build side: rows of grid_tessellateexplode output (MosaicExplode.scala:70-79)."""
+        self.resolution_of_table = self.index_system.get_resolution(resolution)
+        if self.index_system.cell_id_type == "string" and len(index_id) and isinstance(index_id[0], str):
+            index_id = np.array([self.index_system.parse(s) for s in index_id], np.int64)
+        return ChipTable(self, is_core, index_id, wkb_list, polygon_key, n_polygons)
+
+    def pip_join_count(self, chips, x, y):
+        """Quickstart join + filter + groupBy(polygon).count(): int64 count per polygon key."""
+        x, y = _f64(x), _f64(y)
+        n = int(x.shape[0])
+        if _is_torch(x):
+            import torch
+
+            counts = torch.zeros(max(chips.n_polygons, 1), dtype=torch.int64, device=x.device)
+        else:
+            counts = np.zeros(max(chips.n_polygons, 1), np.int64)
+        N.check(N.lib().mosaic_pip_join_count(self.handle, chips.handle, N.ptr(x), N.ptr(y), n, N.ptr(counts)))
+        return counts[:chips.n_polygons]
+
+    def pip_join_pairs(self, chips, x, y, capacity=None):
+        """Quickstart join + filter: (row, polygon_key) pairs sorted by (row, key)."""
+        x, y = _f64(x), _f64(y)
+        n = int(x.shape[0])
+        cap = capacity if capacity is not None else max(2 * n, 1024)
+        while True:
+            rows = np.empty(max(cap, 1), np.int64)
+            keys = np.empty(max(cap, 1), np.int32)
+            n_out = ctypes.c_int64(0)
+            rc = N.lib().mosaic_pip_join_pairs(self.handle, chips.handle, N.ptr(x), N.ptr(y), n, N.ptr(rows),
+                                               N.ptr(keys), cap, ctypes.byref(n_out))
+            if rc == N.MOSAIC_E_CAPACITY:
+                cap = int(n_out.value)
+                continue
+            N.check(rc)
+            k = int(n_out.value)
+            order = np.lexsort((keys[:k], rows[:k]))
+            return rows[:k][order], keys[:k][order]

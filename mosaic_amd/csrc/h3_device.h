@@ -1,0 +1,347 @@
+// H3 v3.7 geoToH3 for gfx950 (and the host, for self-checks): the point -> cell step of
+// grid_pointascellid / grid_longlatascellid (reference H3IndexSystem.pointToIndex,
+// src/main/scala/com/databricks/labs/mosaic/core/index/H3IndexSystem.scala:140-142, which calls
+// h3-java geoToH3(lat, lon, res) -> H3 C geoToH3).
+//
+// Two paths, one answer:
+//  * h3_fast():  the acos/azimuth/tan/sin/cos chain of H3's _geoToHex2d is mathematically the
+//    gnomonic (projective) map  x = S (EI.p)/(FC.p), y = S (EP.p)/(FC.p)  of the unit vector p.
+//    That costs two sincos, 20 face dot products and one division instead of ~11 FP64
+//    transcendentals.  It then checks how far the point is from every decision the integer part
+//    of H3 makes (closest face, the hex-rounding thresholds of _hex2dToCoordIJK, the axis folds):
+//    if every margin exceeds a bound on |fast - H3| (both errors included), H3 on the same input
+//    necessarily takes the same decisions, so the cell is identical.  Otherwise it reports
+//    "ambiguous" and the caller runs
+//  * h3_exact(): a line-by-line restatement of H3 C with x86-64 semantics, including the
+//    x87 long-double operations (x87.h), for the rare ambiguous points (~1e-8 of uniform input).
+// Both share the integer stage (_hex2dToCoordIJK result -> _faceIjkToH3).
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#include "x87.h"
+
+namespace mosaic {
+namespace h3 {
+
+#if defined(__HIPCC__)
+#define H3_TABLE static __constant__ const
+#else
+#define H3_TABLE static const
+#endif
+#include "h3_fast_tables.h"
+#include "h3_tables.h"
+#undef H3_TABLE
+
+static const double kRes0UGnomonic = 0.38196601125010500003;
+
+struct IJK {
+    int i, j, k;
+};
+
+MOSAIC_HD void ijk_normalize(IJK& c) {
+    if (c.i < 0) {
+        c.j -= c.i;
+        c.k -= c.i;
+        c.i = 0;
+    }
+    if (c.j < 0) {
+        c.i -= c.j;
+        c.k -= c.j;
+        c.j = 0;
+    }
+    if (c.k < 0) {
+        c.i -= c.k;
+        c.j -= c.k;
+        c.k = 0;
+    }
+    int mn = c.i;
+    if (c.j < mn) mn = c.j;
+    if (c.k < mn) mn = c.k;
+    if (mn > 0) {
+        c.i -= mn;
+        c.j -= mn;
+        c.k -= mn;
+    }
+}
+
+// lround(n / 7.0) for integer n: no ties are possible (7 is odd), so it is floor((n + 3) / 7).
+MOSAIC_HD int round_div7(int n) {
+    int t = n + 3;
+    int q = t / 7;
+    if ((t % 7 != 0) && (t < 0)) q -= 1;
+    return q;
+}
+
+// coordijk.c _hex2dToCoordIJK, given x2 = |y| / sin60 computed by the caller (exactly as H3 does
+// on the exact path, in plain double on the fast path whose margins cover the difference).
+MOSAIC_HD IJK hex2d_round(double vx, double vy, double a1, double x2) {
+    IJK h;
+    h.k = 0;
+    double x1 = a1 + x2 / 2.0;
+    int m1 = (int)x1;
+    int m2 = (int)x2;
+    double r1 = x1 - m1;
+    double r2 = x2 - m2;
+    if (r1 < 0.5) {
+        if (r1 < 1.0 / 3.0) {
+            h.i = m1;
+            h.j = (r2 < (1.0 + r1) / 2.0) ? m2 : m2 + 1;
+        } else {
+            h.j = (r2 < (1.0 - r1)) ? m2 : m2 + 1;
+            h.i = ((1.0 - r1) <= r2 && r2 < (2.0 * r1)) ? m1 + 1 : m1;
+        }
+    } else {
+        if (r1 < 2.0 / 3.0) {
+            h.j = (r2 < (1.0 - r1)) ? m2 : m2 + 1;
+            h.i = ((2.0 * r1 - 1.0) < r2 && r2 < (1.0 - r1)) ? m1 : m1 + 1;
+        } else {
+            h.i = m1 + 1;
+            h.j = (r2 < (r1 / 2.0)) ? m2 : m2 + 1;
+        }
+    }
+    if (vx < 0.0) {
+        if ((h.j % 2) == 0) {
+            long long axisi = h.j / 2;
+            long long diff = h.i - axisi;
+            h.i = (int)(h.i - 2.0 * diff);
+        } else {
+            long long axisi = (h.j + 1) / 2;
+            long long diff = h.i - axisi;
+            h.i = (int)(h.i - (2.0 * diff + 1));
+        }
+    }
+    if (vy < 0.0) {
+        h.i = h.i - (2 * h.j + 1) / 2;
+        h.j = -1 * h.j;
+    }
+    ijk_normalize(h);
+    return h;
+}
+
+// Distance (in x1/x2 units) from every threshold _hex2dToCoordIJK can compare against.
+MOSAIC_HD double hex2d_margin(double a1, double x2) {
+    double x1 = a1 + x2 / 2.0;
+    double r1 = x1 - floor(x1);
+    double r2 = x2 - floor(x2);
+    double m = fmin(r1, 1.0 - r1);
+    m = fmin(m, fmin(r2, 1.0 - r2));
+    m = fmin(m, fabs(r1 - 1.0 / 3.0));
+    m = fmin(m, fabs(r1 - 0.5));
+    m = fmin(m, fabs(r1 - 2.0 / 3.0));
+    m = fmin(m, fabs(r2 - (1.0 + r1) / 2.0));
+    m = fmin(m, fabs(r2 - (1.0 - r1)));
+    m = fmin(m, fabs(r2 - 2.0 * r1));
+    m = fmin(m, fabs(r2 - (2.0 * r1 - 1.0)));
+    m = fmin(m, fabs(r2 - r1 / 2.0));
+    return m;
+}
+
+// ---- digits / base cell (h3Index.c _faceIjkToH3) ----
+MOSAIC_HD int rotate60ccw(int d) {
+    // 1->5, 5->4, 4->6, 6->2, 2->3, 3->1
+    const int t[8] = {0, 5, 3, 1, 6, 4, 2, 7};
+    return t[d];
+}
+MOSAIC_HD int rotate60cw(int d) {
+    // 1->3, 3->2, 2->6, 6->4, 4->5, 5->1
+    const int t[8] = {0, 3, 6, 2, 5, 1, 4, 7};
+    return t[d];
+}
+MOSAIC_HD int get_digit(uint64_t h, int r) { return (int)((h >> ((15 - r) * 3)) & 7); }
+MOSAIC_HD uint64_t set_digit(uint64_t h, int r, int d) {
+    int s = (15 - r) * 3;
+    return (h & ~((uint64_t)7 << s)) | ((uint64_t)d << s);
+}
+MOSAIC_HD int leading_nonzero_digit(uint64_t h, int res) {
+    for (int r = 1; r <= res; r++) {
+        int d = get_digit(h, r);
+        if (d) return d;
+    }
+    return 0;
+}
+MOSAIC_HD uint64_t rotate_all(uint64_t h, int res, bool ccw) {
+    for (int r = 1; r <= res; r++) h = set_digit(h, r, ccw ? rotate60ccw(get_digit(h, r)) : rotate60cw(get_digit(h, r)));
+    return h;
+}
+MOSAIC_HD uint64_t rotate_pent60ccw(uint64_t h, int res) {
+    bool found = false;
+    for (int r = 1; r <= res; r++) {
+        h = set_digit(h, r, rotate60ccw(get_digit(h, r)));
+        if (!found && get_digit(h, r) != 0) {
+            found = true;
+            if (leading_nonzero_digit(h, res) == 1) h = rotate_all(h, res, true);
+        }
+    }
+    return h;
+}
+
+MOSAIC_HD uint64_t face_ijk_to_h3(int face, IJK ijk, int res) {
+    uint64_t h = 0x00001fffffffffffULL | (1ULL << 59) | ((uint64_t)res << 52);
+    if (res == 0) {
+        if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
+        return h | ((uint64_t)(kH3FaceIjkBaseCells[face][ijk.i][ijk.j][ijk.k] >> 3) << 45);
+    }
+    for (int r = res - 1; r >= 0; r--) {
+        IJK last = ijk;
+        IJK c;
+        int i = ijk.i - ijk.k, j = ijk.j - ijk.k;
+        if ((r + 1) & 1) {  // _upAp7 then _downAp7
+            ijk.i = round_div7(3 * i - j);
+            ijk.j = round_div7(i + 2 * j);
+            ijk.k = 0;
+            ijk_normalize(ijk);
+            c.i = 3 * ijk.i + ijk.j;
+            c.j = 3 * ijk.j + ijk.k;
+            c.k = ijk.i + 3 * ijk.k;
+        } else {  // _upAp7r then _downAp7r
+            ijk.i = round_div7(2 * i + j);
+            ijk.j = round_div7(3 * j - i);
+            ijk.k = 0;
+            ijk_normalize(ijk);
+            c.i = 3 * ijk.i + ijk.k;
+            c.j = ijk.i + 3 * ijk.j;
+            c.k = ijk.j + 3 * ijk.k;
+        }
+        ijk_normalize(c);
+        IJK d = {last.i - c.i, last.j - c.j, last.k - c.k};
+        ijk_normalize(d);
+        // _unitIjkToDigit: UNIT_VECS[digit] = (digit>>2 &1, digit>>1 &1, digit&1)
+        int digit = (d.i <= 1 && d.j <= 1 && d.k <= 1) ? (d.i << 2) | (d.j << 1) | d.k : 7;
+        h = set_digit(h, r + 1, digit);
+    }
+    if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
+    int packed = kH3FaceIjkBaseCells[face][ijk.i][ijk.j][ijk.k];
+    int bc = packed >> 3;
+    int rots = packed & 7;
+    h |= (uint64_t)bc << 45;
+    if (kH3BaseCellData[bc][4]) {
+        if (leading_nonzero_digit(h, res) == 1) {
+            bool cw = kH3BaseCellData[bc][5] == face || kH3BaseCellData[bc][6] == face;
+            h = rotate_all(h, res, !cw);
+        }
+        for (int i = 0; i < rots; i++) h = rotate_pent60ccw(h, res);
+    } else {
+        for (int i = 0; i < rots; i++) h = rotate_all(h, res, true);
+    }
+    return h;
+}
+
+// ---- exact path: H3 C v3.7 with x86-64 double / x87 long double semantics ----
+MOSAIC_HD double pos_angle_rads(double rads) {
+    double tmp = (rads < 0.0) ? x87::add_ld(rads, H3LD_M_2PI_M, H3LD_M_2PI_E, false) : rads;
+    if (rads >= H3LD_M_2PI_DUP) tmp = x87::add_ld(tmp, H3LD_M_2PI_M, H3LD_M_2PI_E, true);
+    return tmp;
+}
+
+MOSAIC_HD double sq(double v) { return v * v; }
+
+MOSAIC_HD uint64_t h3_exact(double lat, double lon, int res) {
+    if (res < 0 || res > 15) return 0;
+    if (!isfinite(lat) || !isfinite(lon)) return 0;
+    double r0 = cos(lat);
+    double pz = sin(lat);
+    double px = cos(lon) * r0;
+    double py = sin(lon) * r0;
+    int face = 0;
+    double sqd = sq(kH3FaceCenterPoint[0][0] - px) + sq(kH3FaceCenterPoint[0][1] - py) +
+                 sq(kH3FaceCenterPoint[0][2] - pz);
+    for (int f = 1; f < 20; f++) {
+        double t = sq(kH3FaceCenterPoint[f][0] - px) + sq(kH3FaceCenterPoint[f][1] - py) +
+                   sq(kH3FaceCenterPoint[f][2] - pz);
+        if (t < sqd) {
+            face = f;
+            sqd = t;
+        }
+    }
+    double vx, vy;
+    double r = acos(1 - sqd / 2);
+    if (r < H3LD_EPSILON_DUP) {
+        vx = vy = 0.0;
+    } else {
+        double lat1 = kH3FaceCenterGeo[face][0], lon1 = kH3FaceCenterGeo[face][1];
+        double az = atan2(cos(lat) * sin(lon - lon1), cos(lat1) * sin(lat) - sin(lat1) * cos(lat) * cos(lon - lon1));
+        double theta = pos_angle_rads(kH3FaceAxesAzRadsCII[face][0] - pos_angle_rads(az));
+        if (res & 1) theta = pos_angle_rads(x87::add_ld(theta, H3LD_M_AP7_ROT_RADS_M, H3LD_M_AP7_ROT_RADS_E, true));
+        r = tan(r);
+        r /= kRes0UGnomonic;
+        for (int i = 0; i < res; i++) r = x87::mul_ld(r, H3LD_M_SQRT7_M, H3LD_M_SQRT7_E);
+        vx = r * cos(theta);
+        vy = r * sin(theta);
+    }
+    double a1 = fabs(vx), a2 = fabs(vy);
+    double x2 = x87::div_ld(a2, H3LD_M_SIN60_M, H3LD_M_SIN60_E);
+    IJK ijk = hex2d_round(vx, vy, a1, x2);
+    return face_ijk_to_h3(face, ijk, res);
+}
+
+// ---- fast path ----
+// Returns the cell, or sets *ambiguous and returns 0 when a decision is too close to call.
+MOSAIC_HD uint64_t h3_fast(double lat, double lon, int res, bool* ambiguous) {
+    *ambiguous = false;
+    if (res < 0 || res > 15) return 0;
+    if (!isfinite(lat) || !isfinite(lon)) return 0;
+    double slat, clat, slon, clon;
+#if defined(__HIP_DEVICE_COMPILE__)
+    sincos(lat, &slat, &clat);
+    sincos(lon, &slon, &clon);
+#else
+    slat = sin(lat);
+    clat = cos(lat);
+    slon = sin(lon);
+    clon = cos(lon);
+#endif
+    double px = clon * clat, py = slon * clat, pz = slat;
+    // closest face = largest dot product with the unit face centre
+    double best = -2.0, second = -2.0;
+    int face = 0;
+#pragma unroll
+    for (int f = 0; f < 20; f++) {
+        const double* b = kH3FastBasis[f];
+        double d = fma(b[0], px, fma(b[1], py, b[2] * pz));
+        if (d > best) {
+            second = best;
+            best = d;
+            face = f;
+        } else if (d > second) {
+            second = d;
+        }
+    }
+    if (best - second < 1e-12) {
+        *ambiguous = true;
+        return 0;
+    }
+    const double* b = kH3FastBasis[face];
+    const double* ei = b + ((res & 1) ? 9 : 3);
+    const double* ep = b + ((res & 1) ? 12 : 6);
+    double s = kH3FastScale[res] / best;
+    double vx = s * fma(ei[0], px, fma(ei[1], py, ei[2] * pz));
+    double vy = s * fma(ep[0], px, fma(ep[1], py, ep[2] * pz));
+    double a1 = fabs(vx), a2 = fabs(vy);
+    // error bound on |fast - H3| in hex units (see DESIGN.md "H3 fast path"): relative terms plus
+    // the acos(1 - sqd/2) ill-conditioning near the face centre.
+    const double eps = 1.1102230246251565e-16;
+    double rh = a1 + a2;
+    double S = kH3FastScale[res];
+    double delta = 64.0 * eps * rh + 32.0 * eps * S * S / fmax(rh, 1e-300) + 1e-300;
+    if (a1 < 8.0 * delta || a2 < 8.0 * delta) {  // axis folds and the r < EPSILON centre case
+        *ambiguous = true;
+        return 0;
+    }
+    double x2 = a2 / 0.86602540378443864676;
+    if (hex2d_margin(a1, x2) < 8.0 * delta) {
+        *ambiguous = true;
+        return 0;
+    }
+    IJK ijk = hex2d_round(vx, vy, a1, x2);
+    return face_ijk_to_h3(face, ijk, res);
+}
+
+// java.lang.Math.toRadians (h3-java converts degrees in Java before calling H3 C)
+MOSAIC_HD double to_radians(double deg, int jdk) {
+    if (jdk <= 8) return deg / 180.0 * 3.141592653589793;
+    return deg * 0.017453292519943295;
+}
+
+}  // namespace h3
+}  // namespace mosaic

@@ -1,0 +1,955 @@
+// libmosaic_hip.so: HIP kernels for gfx950 + the C ABI of include/mosaic_hip.h.
+//
+// Hot path (BASELINE.json north_star): per point
+//   (a) cell = H3 / BNG point index         (h3_device.h fast path, bng_device.h)
+//   (b) probe the chip hash table by cell    (open addressing, 16-byte entries, L2-resident)
+//   (c) core chip -> accept; border chip -> JTS contains on the chip rings (pip_device.h)
+//   and count accepted pairs per polygon key in LDS, flushed once per workgroup.
+// (a)-(c) are fused in one grid-stride kernel so the 16 B/point coordinate stream is read once.
+// Points whose H3 cell the fast path cannot certify are appended to a queue and finished by a
+// second kernel running the exact H3 restatement (h3_exact).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/mosaic_hip.h"
+#include "bng_device.h"
+#include "geom_build.h"
+#include "h3_device.h"
+#include "pip_device.h"
+
+using namespace mosaic;
+
+// ------------------------------------------------------------------------------------------------
+// errors
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t _e = (expr);                                                                         \
+        if (_e != hipSuccess) return fail(MOSAIC_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// device-side data structures
+static const int64_t kEmptyKey = INT64_MIN;
+
+struct HashEntry {  // 16 bytes: one dwordx4 load per probe
+    int64_t key;
+    uint32_t first;
+    uint32_t count;
+};
+
+__host__ __device__ inline uint64_t mix64(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdULL;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ULL;
+    h ^= h >> 33;
+    return h;
+}
+
+struct JoinArgs {
+    const double* x;
+    const double* y;
+    const uint8_t* valid;
+    int64_t n;
+    int res, jdk;
+    const HashEntry* table;
+    uint64_t mask;
+    const uint32_t* chip_meta;  // (polygon_key << 1) | is_core, in table order
+    pip::GeomStore store;       // geometry g == chip g (table order)
+    unsigned long long* counts;  // [n_polygons]
+    int n_polygons;
+    unsigned long long* amb_queue;  // rows for the exact H3 pass
+    unsigned long long* amb_count;
+    unsigned long long amb_cap;
+    long long* pair_row;
+    int* pair_key;
+    unsigned long long* pair_count;
+    long long pair_cap;
+    unsigned long long* tests;  // (point, border chip) contains evaluations
+    unsigned int* flags;        // bit 0: NaN seen (BNG)
+};
+
+template <bool LDS_COUNTS, bool PAIRS>
+__device__ inline void join_point(const JoinArgs& a, int64_t row, double x, double y, int64_t cell, unsigned int* lds,
+                                  unsigned int& tests) {
+    if (cell == kEmptyKey) return;
+    uint64_t slot = mix64((uint64_t)cell) & a.mask;
+    HashEntry e;
+    while (true) {
+        e = a.table[slot];
+        if (e.key == cell) break;
+        if (e.key == kEmptyKey) return;
+        slot = (slot + 1) & a.mask;
+    }
+    for (uint32_t c = e.first; c < e.first + e.count; c++) {
+        uint32_t meta = a.chip_meta[c];
+        bool hit = meta & 1u;
+        if (!hit) {
+            tests++;
+            hit = pip::contains(a.store, c, x, y);
+        }
+        if (hit) {
+            uint32_t key = meta >> 1;
+            if (LDS_COUNTS)
+                atomicAdd(&lds[key], 1u);
+            else
+                atomicAdd(&a.counts[key], 1ULL);
+            if (PAIRS) {
+                unsigned long long idx = atomicAdd(a.pair_count, 1ULL);
+                if ((long long)idx < a.pair_cap) {
+                    a.pair_row[idx] = row;
+                    a.pair_key[idx] = (int)key;
+                }
+            }
+        }
+    }
+}
+
+template <bool LDS_COUNTS>
+__device__ inline void counts_init(const JoinArgs& a, unsigned int* lds) {
+    if (LDS_COUNTS) {
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x) lds[k] = 0;
+        __syncthreads();
+    }
+}
+
+template <bool LDS_COUNTS>
+__device__ inline void counts_flush(const JoinArgs& a, unsigned int* lds, unsigned int tests) {
+    // one wave-level add for the test counter
+    for (int off = 32; off > 0; off >>= 1) tests += __shfl_down(tests, off, 64);
+    if ((threadIdx.x & 63) == 0 && tests) atomicAdd(a.tests, (unsigned long long)tests);
+    if (LDS_COUNTS) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
+    }
+}
+
+// Fused H3 join: fast cell + probe + contains + count.  Ambiguous rows go to the exact pass.
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_h3(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        if (a.valid && !a.valid[i]) continue;
+        double x = a.x[i], y = a.y[i];
+        bool amb;
+        int64_t cell = (int64_t)h3::h3_fast(h3::to_radians(y, a.jdk), h3::to_radians(x, a.jdk), a.res, &amb);
+        if (amb) {
+            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+            continue;
+        }
+        join_point<LDS_COUNTS, PAIRS>(a, i, x, y, cell, lds, tests);
+    }
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
+// Exact H3 for the queued rows (or for every row when all_rows is set: queue overflow fallback).
+template <bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_h3_exact(JoinArgs a, int all_rows) {
+    unsigned int tests = 0;
+    unsigned long long total = all_rows ? (unsigned long long)a.n : min(*a.amb_count, a.amb_cap);
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        int64_t i = all_rows ? (int64_t)t : (int64_t)a.amb_queue[t];
+        if (a.valid && !a.valid[i]) continue;
+        double x = a.x[i], y = a.y[i];
+        int64_t cell = (int64_t)h3::h3_exact(h3::to_radians(y, a.jdk), h3::to_radians(x, a.jdk), a.res);
+        join_point<false, PAIRS>(a, i, x, y, cell, nullptr, tests);
+    }
+    counts_flush<false>(a, nullptr, tests);
+}
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_bng(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    bool nan_seen = false;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        if (a.valid && !a.valid[i]) continue;
+        double x = a.x[i], y = a.y[i];
+        int64_t cell;
+        if (!bng::point_to_index(x, y, a.res, &cell)) {
+            nan_seen = true;
+            continue;
+        }
+        join_point<LDS_COUNTS, PAIRS>(a, i, x, y, cell, lds, tests);
+    }
+    if (nan_seen) atomicOr(a.flags, 1u);
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
+struct CellArgs {
+    const double* x;
+    const double* y;
+    const uint8_t* valid;
+    int64_t n;
+    int res, jdk;
+    long long* out;
+    uint8_t* out_valid;
+    unsigned long long* amb_queue;
+    unsigned long long* amb_count;
+    unsigned long long amb_cap;
+    unsigned int* flags;
+};
+
+__global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        bool v = !a.valid || a.valid[i];
+        if (a.out_valid) a.out_valid[i] = v;
+        if (!v) {
+            a.out[i] = 0;
+            continue;
+        }
+        bool amb;
+        uint64_t cell = h3::h3_fast(h3::to_radians(a.y[i], a.jdk), h3::to_radians(a.x[i], a.jdk), a.res, &amb);
+        if (amb) {
+            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+            else atomicOr(a.flags, 2u);
+        }
+        a.out[i] = (long long)cell;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cell_h3_exact(CellArgs a, int all_rows) {
+    unsigned long long total = all_rows ? (unsigned long long)a.n : min(*a.amb_count, a.amb_cap);
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        int64_t i = all_rows ? (int64_t)t : (int64_t)a.amb_queue[t];
+        if (a.valid && !a.valid[i]) continue;
+        a.out[i] = (long long)h3::h3_exact(h3::to_radians(a.y[i], a.jdk), h3::to_radians(a.x[i], a.jdk), a.res);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cell_bng(CellArgs a) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    bool nan_seen = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        bool v = !a.valid || a.valid[i];
+        if (a.out_valid) a.out_valid[i] = v;
+        int64_t cell = 0;
+        if (v && !bng::point_to_index(a.x[i], a.y[i], a.res, &cell)) nan_seen = true;
+        a.out[i] = v ? cell : 0;
+    }
+    if (nan_seen) atomicOr(a.flags, 1u);
+}
+
+struct ContainsArgs {
+    pip::GeomStore store;
+    int64_t n_geoms;
+    const int* geom_index;
+    const double* px;
+    const double* py;
+    int64_t n;
+    uint8_t* out;
+};
+
+__global__ void __launch_bounds__(256) k_st_contains(ContainsArgs a) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        int g = a.geom_index[i];
+        a.out[i] = (g >= 0 && g < a.n_geoms) ? (uint8_t)pip::contains(a.store, (uint32_t)g, a.px[i], a.py[i]) : 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t n) {
+        if (n <= bytes) return MOSAIC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, n) != hipSuccess) return fail(MOSAIC_E_NOMEM, "hipMalloc(" + std::to_string(n) + ") failed");
+        bytes = n;
+        return MOSAIC_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct mosaic_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int jdk = 8;
+    int async = 0;
+    int block = 256;
+    int blocks_per_cu = 8;
+    DevBuf amb_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
+    int64_t stats[3] = {0, 0, 0};
+    unsigned int deferred_flags = 0;
+};
+
+struct GeomStoreDev {
+    DevBuf verts, ring_start, ring_bbox, part_ring, geom_part, geom_bbox;
+    pip::GeomStore view() const {
+        pip::GeomStore s;
+        s.verts = (const pip::Vec2*)verts.p;
+        s.ring_start = (const uint32_t*)ring_start.p;
+        s.ring_bbox = (const pip::Box*)ring_bbox.p;
+        s.part_ring = (const uint32_t*)part_ring.p;
+        s.geom_part = (const uint32_t*)geom_part.p;
+        s.geom_bbox = (const pip::Box*)geom_bbox.p;
+        return s;
+    }
+    int upload(const GeomBuilder& b, hipStream_t st, size_t* total) {
+        auto up = [&](DevBuf& d, const void* src, size_t bytes) -> int {
+            int rc = d.reserve(std::max<size_t>(bytes, 16));
+            if (rc) return rc;
+            if (bytes) HIP_TRY(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, st));
+            *total += bytes;
+            return MOSAIC_OK;
+        };
+        int rc;
+        if ((rc = up(verts, b.verts.data(), b.verts.size() * sizeof(pip::Vec2)))) return rc;
+        if ((rc = up(ring_start, b.ring_start.data(), b.ring_start.size() * 4))) return rc;
+        if ((rc = up(ring_bbox, b.ring_bbox.data(), b.ring_bbox.size() * sizeof(pip::Box)))) return rc;
+        if ((rc = up(part_ring, b.part_ring.data(), b.part_ring.size() * 4))) return rc;
+        if ((rc = up(geom_part, b.geom_part.data(), b.geom_part.size() * 4))) return rc;
+        if ((rc = up(geom_bbox, b.geom_bbox.data(), b.geom_bbox.size() * sizeof(pip::Box)))) return rc;
+        HIP_TRY(hipStreamSynchronize(st));
+        return MOSAIC_OK;
+    }
+    void release() {
+        verts.release();
+        ring_start.release();
+        ring_bbox.release();
+        part_ring.release();
+        geom_part.release();
+        geom_bbox.release();
+    }
+};
+
+struct mosaic_chips {
+    int grid = 0, res = 0, device = 0;
+    int64_t n_chips = 0, n_cells = 0, n_border = 0, n_vertices = 0, n_rings = 0;
+    int32_t n_polygons = 0;
+    uint64_t capacity = 0;
+    size_t device_bytes = 0;
+    DevBuf table, meta;
+    GeomStoreDev store;
+};
+
+// pointer residency: returns true if p is device-accessible memory of the current device
+static bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+// Make `src` (n_bytes) available on the device: returns the pointer to use.
+static int to_device(mosaic_ctx* c, DevBuf& stage, const void* src, size_t n_bytes, const void** out) {
+    if (!src) {
+        *out = nullptr;
+        return MOSAIC_OK;
+    }
+    if (is_device_ptr(src)) {
+        *out = src;
+        return MOSAIC_OK;
+    }
+    int rc = stage.reserve(std::max<size_t>(n_bytes, 16));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(stage.p, src, n_bytes, hipMemcpyHostToDevice, c->stream));
+    *out = stage.p;
+    return MOSAIC_OK;
+}
+
+static int grid_size(mosaic_ctx* c, int64_t n) {
+    int64_t want = (n + c->block - 1) / c->block;
+    int64_t cap = (int64_t)c->n_cu * c->blocks_per_cu;
+    return (int)std::max<int64_t>(1, std::min(want, cap));
+}
+
+static int res_error(int grid, int res) {
+    if (grid == MOSAIC_GRID_H3)
+        return fail(MOSAIC_E_RES, "H3 resolution has to be between 0 and 15; found " + std::to_string(res));
+    return fail(MOSAIC_E_RES, "BNG resolution not supported; found " + std::to_string(res));
+}
+
+static bool valid_res(int grid, int res) {
+    if (grid == MOSAIC_GRID_H3) return res >= 0 && res <= 15;
+    return bng::valid_resolution(res);
+}
+
+// scalars buffer layout (unsigned long long): [0] amb_count, [1] pair_count, [2] tests, [3] flags
+static const int kScalars = 4;
+
+extern "C" {
+
+int mosaic_abi_version(void) { return MOSAIC_ABI_VERSION; }
+const char* mosaic_last_error(void) { return g_last_error.c_str(); }
+
+int mosaic_init(int device, mosaic_ctx** out) {
+    if (!out) return fail(MOSAIC_E_ARG, "out is null");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(MOSAIC_E_HIP, "no HIP device available");
+    if (device < 0 || device >= count) return fail(MOSAIC_E_ARG, "device ordinal out of range");
+    HIP_TRY(hipSetDevice(device));
+    mosaic_ctx* c = new mosaic_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(MOSAIC_E_HIP, "hipStreamCreate failed");
+    }
+    c->own_stream = true;
+    if (c->scalars.reserve(kScalars * 8)) {
+        delete c;
+        return MOSAIC_E_NOMEM;
+    }
+    *out = c;
+    return MOSAIC_OK;
+}
+
+int mosaic_destroy(mosaic_ctx* c) {
+    if (!c) return MOSAIC_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->amb_queue, &c->scalars, &c->stage_x, &c->stage_y, &c->stage_v, &c->stage_out, &c->stage_out2,
+                      &c->stage_idx})
+        b->release();
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return MOSAIC_OK;
+}
+
+int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
+    if (!c || !key) return fail(MOSAIC_E_ARG, "null argument");
+    std::string k(key);
+    if (k == "jdk") {
+        if (v < 8) return fail(MOSAIC_E_ARG, "jdk must be >= 8");
+        c->jdk = (int)v;
+    } else if (k == "async") {
+        c->async = v ? 1 : 0;
+    } else if (k == "block") {
+        if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "block must be a multiple of 64 in [64, 1024]");
+        c->block = (int)v;
+    } else if (k == "blocks_per_cu") {
+        if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "blocks_per_cu must be in [1, 64]");
+        c->blocks_per_cu = (int)v;
+    } else {
+        return fail(MOSAIC_E_ARG, "unknown option " + k);
+    }
+    return MOSAIC_OK;
+}
+
+int mosaic_get_stream(mosaic_ctx* c, void** s) {
+    if (!c || !s) return fail(MOSAIC_E_ARG, "null argument");
+    *s = (void*)c->stream;
+    return MOSAIC_OK;
+}
+
+int mosaic_set_stream(mosaic_ctx* c, void* s) {
+    if (!c) return fail(MOSAIC_E_ARG, "null argument");
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
+    return MOSAIC_OK;
+}
+
+int mosaic_sync(mosaic_ctx* c) {
+    if (!c) return fail(MOSAIC_E_ARG, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned long long s[kScalars];
+    HIP_TRY(hipMemcpy(s, c->scalars.p, sizeof s, hipMemcpyDeviceToHost));
+    unsigned int flags = c->deferred_flags | (unsigned int)s[3];
+    c->deferred_flags = 0;
+    if (flags & 1u) return fail(MOSAIC_E_NAN, "NaN coordinates are not supported.");
+    if ((flags & 2u) || s[0] > c->amb_queue.bytes / 8)
+        return fail(MOSAIC_E_CAPACITY, "exact-path queue overflowed in an async call; rerun synchronously");
+    return MOSAIC_OK;
+}
+
+int mosaic_last_stats(mosaic_ctx* c, int64_t* out3) {
+    if (!c || !out3) return fail(MOSAIC_E_ARG, "null argument");
+    for (int i = 0; i < 3; i++) out3[i] = c->stats[i];
+    return MOSAIC_OK;
+}
+
+int mosaic_resolution(int grid, int res, int* out) {
+    if (!out) return fail(MOSAIC_E_ARG, "out is null");
+    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
+    if (!valid_res(grid, res)) return res_error(grid, res);
+    *out = res;
+    return MOSAIC_OK;
+}
+
+int mosaic_resolution_str(int grid, const char* s, int* out) {
+    if (!out || !s) return fail(MOSAIC_E_ARG, "null argument");
+    std::string v(s);
+    if (grid == MOSAIC_GRID_H3) {
+        // H3IndexSystem.getResolution: s.toInt (NumberFormatException propagates in the reference)
+        char* end = nullptr;
+        long r = strtol(s, &end, 10);
+        if (v.empty() || *end) return fail(MOSAIC_E_ARG, "For input string: \"" + v + "\"");
+        return mosaic_resolution(grid, (int)r, out);
+    }
+    if (grid == MOSAIC_GRID_BNG) {
+        // BNGIndexSystem.resolutionMap (BNGIndexSystem.scala:43-57); an Int-typed value is checked
+        // against `resolutions` first, a String only against the map.
+        static const char* names[] = {"500km", "100km", "50km", "10km", "5km", "1km",
+                                      "500m",  "100m",  "50m",  "10m",  "5m",  "1m"};
+        static const int vals[] = {-1, 1, -2, 2, -3, 3, -4, 4, -5, 5, -6, 6};
+        for (int i = 0; i < 12; i++)
+            if (v == names[i]) {
+                *out = vals[i];
+                return MOSAIC_OK;
+            }
+        return fail(MOSAIC_E_RES, "BNG resolution not supported; found " + v);
+    }
+    return fail(MOSAIC_E_ARG, "unknown grid");
+}
+
+int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, const double* y, const uint8_t* valid,
+                         int64_t n, int64_t* out_cell, uint8_t* out_valid) {
+    if (!c || (n > 0 && (!x || !y || !out_cell))) return fail(MOSAIC_E_ARG, "null argument");
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
+    if (!valid_res(grid, res)) return res_error(grid, res);
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    const void *dx, *dy, *dv;
+    if ((rc = to_device(c, c->stage_x, x, n * 8, &dx))) return rc;
+    if ((rc = to_device(c, c->stage_y, y, n * 8, &dy))) return rc;
+    if ((rc = to_device(c, c->stage_v, valid, n, &dv))) return rc;
+    bool dev_out = is_device_ptr(out_cell);
+    bool dev_vout = !out_valid || is_device_ptr(out_valid);
+    if (!dev_out && (rc = c->stage_out.reserve(n * 8))) return rc;
+    if (out_valid && !dev_vout && (rc = c->stage_out2.reserve(n))) return rc;
+    long long* dout = dev_out ? (long long*)out_cell : (long long*)c->stage_out.p;
+    uint8_t* dvout = out_valid ? (dev_vout ? out_valid : (uint8_t*)c->stage_out2.p) : nullptr;
+    uint64_t cap = (uint64_t)std::min<int64_t>(n, std::max<int64_t>(n / 8, 1 << 20));
+    if ((rc = c->amb_queue.reserve(cap * 8))) return rc;
+    HIP_TRY(hipMemsetAsync(c->scalars.p, 0, kScalars * 8, c->stream));
+    unsigned long long* sc = (unsigned long long*)c->scalars.p;
+    CellArgs a;
+    a.x = (const double*)dx;
+    a.y = (const double*)dy;
+    a.valid = (const uint8_t*)dv;
+    a.n = n;
+    a.res = res;
+    a.jdk = c->jdk;
+    a.out = dout;
+    a.out_valid = dvout;
+    a.amb_queue = (unsigned long long*)c->amb_queue.p;
+    a.amb_count = sc + 0;
+    a.amb_cap = cap;
+    a.flags = (unsigned int*)(sc + 3);
+    int g = grid_size(c, n);
+    if (grid == MOSAIC_GRID_H3) {
+        hipLaunchKernelGGL(k_cell_h3, dim3(g), dim3(c->block), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_cell_h3_exact, dim3(grid_size(c, (int64_t)cap)), dim3(c->block), 0, c->stream, a, 0);
+        HIP_TRY(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(k_cell_bng, dim3(g), dim3(c->block), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+    }
+    bool host_side = !dev_out || (out_valid && !dev_vout);
+    if (c->async && !host_side) return MOSAIC_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned long long s[kScalars];
+    HIP_TRY(hipMemcpy(s, c->scalars.p, sizeof s, hipMemcpyDeviceToHost));
+    if (grid == MOSAIC_GRID_H3 && s[0] > cap) {  // queue overflow: recompute every row exactly
+        hipLaunchKernelGGL(k_cell_h3_exact, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a, 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    c->stats[0] = (int64_t)s[0];
+    c->stats[1] = 0;
+    c->stats[2] = 0;
+    if (s[3] & 1u) return fail(MOSAIC_E_NAN, "NaN coordinates are not supported.");
+    if (!dev_out) HIP_TRY(hipMemcpy(out_cell, dout, n * 8, hipMemcpyDeviceToHost));
+    if (out_valid && !dev_vout) HIP_TRY(hipMemcpy(out_valid, dvout, n, hipMemcpyDeviceToHost));
+    return MOSAIC_OK;
+}
+
+// BNGIndexSystem.letterMap (BNGIndexSystem.scala:84-99) and quadrants (:36)
+static const char* kLetterMap[13][7] = {
+    {"SV", "SW", "SX", "SY", "SZ", "TV", "TW"}, {"SQ", "SR", "SS", "ST", "SU", "TQ", "TR"},
+    {"SL", "SM", "SN", "SO", "SP", "TL", "TM"}, {"SF", "SG", "SH", "SJ", "SK", "TF", "TG"},
+    {"SA", "SB", "SC", "SD", "SE", "TA", "TB"}, {"NV", "NW", "NX", "NY", "NZ", "OV", "OW"},
+    {"NQ", "NR", "NS", "NT", "NU", "OQ", "OR"}, {"NL", "NM", "NN", "NO", "NP", "OL", "OM"},
+    {"NF", "NG", "NH", "NJ", "NK", "OF", "OG"}, {"NA", "NB", "NC", "ND", "NE", "OA", "OB"},
+    {"HV", "HW", "HX", "HY", "SZ", "JV", "JW"}, {"HQ", "HR", "HS", "HT", "HU", "JQ", "JR"},
+    {"HL", "HM", "HN", "HO", "HP", "JL", "JM"}};
+static const char* kQuadrants[5] = {"", "SW", "NW", "NE", "SE"};
+
+int mosaic_bng_format(int64_t id, char* buf, size_t cap) {
+    if (!buf) return fail(MOSAIC_E_ARG, "null buffer");
+    if (id <= 0) return fail(MOSAIC_E_ARG, "invalid BNG id " + std::to_string(id));
+    std::string d = std::to_string(id);
+    auto num = [&](size_t a, size_t b) -> int {  // digits.slice(a, b).mkString.toInt
+        if (a >= d.size()) return -1;
+        return std::stoi(d.substr(a, std::min(b, d.size()) - a));
+    };
+    int row = num(3, 5), col = num(1, 3);
+    if (row < 0 || col < 0 || row > 12 || col > 6) return fail(MOSAIC_E_ARG, "invalid BNG id " + d);
+    std::string s;
+    if (d.size() < 6) {
+        s = std::string(1, kLetterMap[row][col][0]);
+    } else {
+        int q = d.back() - '0';
+        if (q > 4) return fail(MOSAIC_E_ARG, "invalid BNG id " + d);
+        size_t k = (d.size() - 6) / 2;
+        s = std::string(kLetterMap[row][col]) + d.substr(5, k) + d.substr(5 + k, k) + kQuadrants[q];
+    }
+    if (s.size() + 1 > cap) return fail(MOSAIC_E_CAPACITY, "buffer too small");
+    memcpy(buf, s.c_str(), s.size() + 1);
+    return (int)s.size();
+}
+
+// BNGIndexSystem.parse (BNGIndexSystem.scala:391-413) + encode (:528-541)
+static int64_t bng_encode(int eL, int nL, int eBin, int nBin, int q, int nPos, int res) {
+    double idP = bng::pow10i(5 + 2 * nPos - 2), eLS = bng::pow10i(3 + 2 * nPos - 2), nLS = bng::pow10i(1 + 2 * nPos - 2);
+    double eS = bng::pow10i(nPos);
+    double id = res == -1 ? (idP + (double)eL * eLS) / 100 + q
+                          : idP + (double)eL * eLS + (double)nL * nLS + (double)eBin * eS + (double)(nBin * 10) + q;
+    return bng::jvm_d2l(id);
+}
+
+int mosaic_bng_parse(const char* cs, int64_t* out) {
+    if (!cs || !out) return fail(MOSAIC_E_ARG, "null argument");
+    std::string s(cs);
+    if (s.empty()) return fail(MOSAIC_E_ARG, "empty BNG id");
+    std::string prefix = s.size() >= 2 ? s.substr(0, 2) : s + "V";
+    int eL = -1, nL = -1;
+    for (int r = 0; r < 13 && eL < 0; r++)
+        for (int col = 0; col < 7; col++)
+            if (prefix == kLetterMap[r][col]) {
+                eL = col;
+                nL = r;
+                break;
+            }
+    if (eL < 0) return fail(MOSAIC_E_ARG, "invalid BNG prefix in " + s);
+    if (s.size() == 1) {
+        *out = bng_encode(eL, 0, 0, 0, 0, 1, -1);
+        return MOSAIC_OK;
+    }
+    std::string suffix = s.substr(s.size() - 2);
+    int q = 0;
+    for (int i = 1; i < 5; i++)
+        if (suffix == kQuadrants[i]) q = i;
+    std::string bins = q > 0 ? s.substr(2, s.size() - 4) : s.substr(2);
+    if (bins.empty()) {
+        *out = bng_encode(eL, nL, 0, 0, q, 1, -2);
+        return MOSAIC_OK;
+    }
+    for (char ch : bins)
+        if (ch < '0' || ch > '9') return fail(MOSAIC_E_ARG, "invalid BNG digits in " + s);
+    size_t half = bins.size() / 2;
+    int eBin = std::stoi(bins.substr(0, bins.size() - half));
+    int nBin = std::stoi(bins.substr(bins.size() - half));
+    int nPos = (int)half + 1;
+    int res = q == 0 ? nPos + 1 : -nPos;
+    *out = bng_encode(eL, nL, eBin, nBin, q, nPos, res);
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, const uint8_t* is_core,
+                             const int64_t* index_id, const int64_t* wkb_offsets, const uint8_t* wkb,
+                             const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out) {
+    if (!c || !out || n_chips < 0 || n_polygons < 0) return fail(MOSAIC_E_ARG, "invalid argument");
+    if (n_chips > 0 && (!is_core || !index_id || !wkb_offsets || !polygon_key))
+        return fail(MOSAIC_E_ARG, "null chip column");
+    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
+    if (!valid_res(grid, res)) return res_error(grid, res);
+    if (n_chips >= (int64_t)1 << 31) return fail(MOSAIC_E_ARG, "too many chips");
+    HIP_TRY(hipSetDevice(c->device));
+    // chips grouped by cell, original order kept within a cell
+    std::vector<uint32_t> order(n_chips);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return index_id[a] < index_id[b]; });
+    GeomBuilder gb;
+    std::vector<uint32_t> meta(std::max<int64_t>(n_chips, 1));
+    int64_t n_border = 0;
+    for (int64_t t = 0; t < n_chips; t++) {
+        uint32_t i = order[t];
+        if (polygon_key[i] < 0 || polygon_key[i] >= n_polygons)
+            return fail(MOSAIC_E_ARG, "polygon_key out of range at chip " + std::to_string(i));
+        if (index_id[i] == kEmptyKey) return fail(MOSAIC_E_ARG, "reserved index_id at chip " + std::to_string(i));
+        bool core = is_core[i] != 0;
+        meta[t] = ((uint32_t)polygon_key[i] << 1) | (core ? 1u : 0u);
+        int64_t a = wkb_offsets[i], b = wkb_offsets[i + 1];
+        if (b < a || (b > a && !wkb)) return fail(MOSAIC_E_ARG, "bad wkb offsets at chip " + std::to_string(i));
+        // core chips are accepted without a test: their geometry is never read
+        if (!gb.add(core ? nullptr : wkb + a, core ? 0 : (size_t)(b - a)))
+            return fail(MOSAIC_E_WKB, "chip " + std::to_string(i) + ": " + gb.error);
+        n_border += !core;
+    }
+    // distinct cells -> [first, count)
+    std::vector<std::pair<int64_t, uint32_t>> cells;  // (cell, first)
+    std::vector<uint32_t> counts;
+    for (int64_t t = 0; t < n_chips; t++) {
+        int64_t id = index_id[order[t]];
+        if (cells.empty() || cells.back().first != id) {
+            cells.push_back({id, (uint32_t)t});
+            counts.push_back(0);
+        }
+        counts.back()++;
+    }
+    uint64_t capacity = 16;
+    while (capacity < 2 * cells.size() + 1) capacity <<= 1;
+    std::vector<HashEntry> table(capacity, HashEntry{kEmptyKey, 0, 0});
+    for (size_t k = 0; k < cells.size(); k++) {
+        uint64_t slot = mix64((uint64_t)cells[k].first) & (capacity - 1);
+        while (table[slot].key != kEmptyKey) slot = (slot + 1) & (capacity - 1);
+        table[slot] = HashEntry{cells[k].first, cells[k].second, counts[k]};
+    }
+    mosaic_chips* ch = new mosaic_chips();
+    ch->grid = grid;
+    ch->res = res;
+    ch->device = c->device;
+    ch->n_chips = n_chips;
+    ch->n_cells = (int64_t)cells.size();
+    ch->n_border = n_border;
+    ch->n_vertices = (int64_t)gb.verts.size();
+    ch->n_rings = (int64_t)gb.ring_bbox.size();
+    ch->n_polygons = n_polygons;
+    ch->capacity = capacity;
+    size_t total = 0;
+    int rc;
+    if ((rc = ch->table.reserve(capacity * sizeof(HashEntry))) || (rc = ch->meta.reserve(meta.size() * 4)) ||
+        (rc = ch->store.upload(gb, c->stream, &total))) {
+        ch->table.release();
+        ch->meta.release();
+        ch->store.release();
+        delete ch;
+        return rc;
+    }
+    HIP_TRY(hipMemcpy(ch->table.p, table.data(), capacity * sizeof(HashEntry), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ch->meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
+    ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4;
+    *out = ch;
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_table_destroy(mosaic_chips* ch) {
+    if (!ch) return MOSAIC_OK;
+    (void)hipSetDevice(ch->device);
+    ch->table.release();
+    ch->meta.release();
+    ch->store.release();
+    delete ch;
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_table_info(const mosaic_chips* ch, int64_t* o) {
+    if (!ch || !o) return fail(MOSAIC_E_ARG, "null argument");
+    o[0] = ch->n_chips;
+    o[1] = ch->n_cells;
+    o[2] = ch->n_border;
+    o[3] = ch->n_vertices;
+    o[4] = ch->n_rings;
+    o[5] = (int64_t)ch->device_bytes;
+    o[6] = (int64_t)ch->capacity;
+    o[7] = ch->n_polygons;
+    return MOSAIC_OK;
+}
+
+static const int kLdsCountsMax = 8192;
+
+static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+                    int64_t* counts, int64_t* out_row, int32_t* out_key, int64_t cap, int64_t* n_out) {
+    bool pairs = out_row != nullptr;
+    if (!c || !ch) return fail(MOSAIC_E_ARG, "null context or chip table");
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (n > 0 && (!x || !y)) return fail(MOSAIC_E_ARG, "null coordinates");
+    if (!pairs && !counts && ch->n_polygons > 0) return fail(MOSAIC_E_ARG, "null counts");
+    if (ch->device != c->device) return fail(MOSAIC_E_ARG, "chip table belongs to another device");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    const void *dx, *dy;
+    if ((rc = to_device(c, c->stage_x, x, n * 8, &dx))) return rc;
+    if ((rc = to_device(c, c->stage_y, y, n * 8, &dy))) return rc;
+    bool dev_counts = counts && is_device_ptr(counts);
+    size_t cbytes = (size_t)std::max<int32_t>(ch->n_polygons, 1) * 8;
+    if (!dev_counts && (rc = c->stage_out.reserve(cbytes))) return rc;
+    unsigned long long* dcounts = dev_counts ? (unsigned long long*)counts : (unsigned long long*)c->stage_out.p;
+    HIP_TRY(hipMemsetAsync(dcounts, 0, cbytes, c->stream));
+    HIP_TRY(hipMemsetAsync(c->scalars.p, 0, kScalars * 8, c->stream));
+    uint64_t qcap = (uint64_t)std::max<int64_t>(std::min<int64_t>(n, std::max<int64_t>(n / 8, 1 << 20)), 1);
+    if ((rc = c->amb_queue.reserve(qcap * 8))) return rc;
+    bool dev_pairs = pairs && is_device_ptr(out_row) && is_device_ptr(out_key);
+    if (pairs && !dev_pairs) {
+        if ((rc = c->stage_idx.reserve((size_t)std::max<int64_t>(cap, 1) * 8))) return rc;
+        if ((rc = c->stage_out2.reserve((size_t)std::max<int64_t>(cap, 1) * 4))) return rc;
+    }
+    unsigned long long* sc = (unsigned long long*)c->scalars.p;
+    JoinArgs a;
+    a.x = (const double*)dx;
+    a.y = (const double*)dy;
+    a.valid = nullptr;
+    a.n = n;
+    a.res = ch->res;
+    a.jdk = c->jdk;
+    a.table = (const HashEntry*)ch->table.p;
+    a.mask = ch->capacity - 1;
+    a.chip_meta = (const uint32_t*)ch->meta.p;
+    a.store = ch->store.view();
+    a.counts = dcounts;
+    a.n_polygons = ch->n_polygons;
+    a.amb_queue = (unsigned long long*)c->amb_queue.p;
+    a.amb_count = sc + 0;
+    a.amb_cap = qcap;
+    a.pair_row = pairs ? (long long*)(dev_pairs ? (void*)out_row : c->stage_idx.p) : nullptr;
+    a.pair_key = pairs ? (int*)(dev_pairs ? (void*)out_key : c->stage_out2.p) : nullptr;
+    a.pair_count = sc + 1;
+    a.pair_cap = cap;
+    a.tests = sc + 2;
+    a.flags = (unsigned int*)(sc + 3);
+    bool lds = ch->n_polygons <= kLdsCountsMax;
+    size_t shm = lds ? (size_t)ch->n_polygons * 4 : 0;
+    int g = grid_size(c, n);
+    if (n > 0) {
+        if (ch->grid == MOSAIC_GRID_H3) {
+            if (pairs)
+                hipLaunchKernelGGL((k_join_h3<false, true>), dim3(g), dim3(c->block), 0, c->stream, a);
+            else if (lds)
+                hipLaunchKernelGGL((k_join_h3<true, false>), dim3(g), dim3(c->block), shm, c->stream, a);
+            else
+                hipLaunchKernelGGL((k_join_h3<false, false>), dim3(g), dim3(c->block), 0, c->stream, a);
+            HIP_TRY(hipGetLastError());
+            int ge = grid_size(c, (int64_t)qcap);
+            if (pairs)
+                hipLaunchKernelGGL((k_join_h3_exact<true>), dim3(ge), dim3(c->block), 0, c->stream, a, 0);
+            else
+                hipLaunchKernelGGL((k_join_h3_exact<false>), dim3(ge), dim3(c->block), 0, c->stream, a, 0);
+            HIP_TRY(hipGetLastError());
+        } else {
+            if (pairs)
+                hipLaunchKernelGGL((k_join_bng<false, true>), dim3(g), dim3(c->block), 0, c->stream, a);
+            else if (lds)
+                hipLaunchKernelGGL((k_join_bng<true, false>), dim3(g), dim3(c->block), shm, c->stream, a);
+            else
+                hipLaunchKernelGGL((k_join_bng<false, false>), dim3(g), dim3(c->block), 0, c->stream, a);
+            HIP_TRY(hipGetLastError());
+        }
+    }
+    if (c->async && !pairs && dev_counts) return MOSAIC_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned long long s[kScalars];
+    HIP_TRY(hipMemcpy(s, c->scalars.p, sizeof s, hipMemcpyDeviceToHost));
+    if (ch->grid == MOSAIC_GRID_H3 && s[0] > qcap) {
+        // queue overflow (adversarial input): recompute the whole batch on the exact path
+        HIP_TRY(hipMemsetAsync(dcounts, 0, cbytes, c->stream));
+        HIP_TRY(hipMemsetAsync(sc + 1, 0, 2 * 8, c->stream));
+        if (pairs)
+            hipLaunchKernelGGL((k_join_h3_exact<true>), dim3(g), dim3(c->block), 0, c->stream, a, 1);
+        else
+            hipLaunchKernelGGL((k_join_h3_exact<false>), dim3(g), dim3(c->block), 0, c->stream, a, 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(s + 1, sc + 1, 2 * 8, hipMemcpyDeviceToHost));
+    }
+    c->stats[0] = (int64_t)s[0];
+    c->stats[1] = (int64_t)s[2];
+    c->stats[2] = (int64_t)s[1];
+    if (s[3] & 1u) return fail(MOSAIC_E_NAN, "NaN coordinates are not supported.");
+    if (counts && !dev_counts) HIP_TRY(hipMemcpy(counts, dcounts, (size_t)ch->n_polygons * 8, hipMemcpyDeviceToHost));
+    if (pairs) {
+        *n_out = (int64_t)s[1];
+        if ((int64_t)s[1] > cap) return fail(MOSAIC_E_CAPACITY, "pair buffer too small");
+        if (!dev_pairs && s[1] > 0) {
+            HIP_TRY(hipMemcpy(out_row, c->stage_idx.p, s[1] * 8, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(out_key, c->stage_out2.p, s[1] * 4, hipMemcpyDeviceToHost));
+        }
+    }
+    return MOSAIC_OK;
+}
+
+int mosaic_pip_join_count(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+                          int64_t* counts) {
+    return run_join(c, ch, x, y, n, counts, nullptr, nullptr, 0, nullptr);
+}
+
+int mosaic_pip_join_pairs(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+                          int64_t* out_row, int32_t* out_key, int64_t cap, int64_t* n_out) {
+    if (!out_row || !out_key || !n_out || cap < 0) return fail(MOSAIC_E_ARG, "null pair output");
+    return run_join(c, ch, x, y, n, nullptr, out_row, out_key, cap, n_out);
+}
+
+int mosaic_st_contains(mosaic_ctx* c, int64_t n_geoms, const int64_t* wkb_offsets, const uint8_t* wkb,
+                       const int32_t* geom_index, const double* px, const double* py, int64_t n, uint8_t* out) {
+    if (!c || n < 0 || n_geoms < 0 || (n_geoms > 0 && !wkb_offsets) || (n > 0 && (!geom_index || !px || !py || !out)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    HIP_TRY(hipSetDevice(c->device));
+    GeomBuilder gb;
+    for (int64_t g = 0; g < n_geoms; g++) {
+        int64_t a = wkb_offsets[g], b = wkb_offsets[g + 1];
+        if (b < a || (b > a && !wkb)) return fail(MOSAIC_E_ARG, "bad wkb offsets");
+        if (!gb.add(wkb + a, (size_t)(b - a))) return fail(MOSAIC_E_WKB, "geometry " + std::to_string(g) + ": " + gb.error);
+    }
+    if (n == 0) return MOSAIC_OK;
+    GeomStoreDev st;
+    size_t total = 0;
+    int rc = st.upload(gb, c->stream, &total);
+    if (rc) {
+        st.release();
+        return rc;
+    }
+    const void *dpx, *dpy, *dgi;
+    if ((rc = to_device(c, c->stage_x, px, n * 8, &dpx)) || (rc = to_device(c, c->stage_y, py, n * 8, &dpy)) ||
+        (rc = to_device(c, c->stage_idx, geom_index, n * 4, &dgi))) {
+        st.release();
+        return rc;
+    }
+    bool dev_out = is_device_ptr(out);
+    if (!dev_out && (rc = c->stage_out.reserve(n))) {
+        st.release();
+        return rc;
+    }
+    ContainsArgs a;
+    a.store = st.view();
+    a.n_geoms = n_geoms;
+    a.geom_index = (const int*)dgi;
+    a.px = (const double*)dpx;
+    a.py = (const double*)dpy;
+    a.n = n;
+    a.out = dev_out ? out : (uint8_t*)c->stage_out.p;
+    hipLaunchKernelGGL(k_st_contains, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && !dev_out) e = hipMemcpy(out, a.out, n, hipMemcpyDeviceToHost);
+    st.release();
+    if (e != hipSuccess) return fail(MOSAIC_E_HIP, std::string("st_contains: ") + hipGetErrorString(e));
+    return MOSAIC_OK;
+}
+
+}  // extern "C"

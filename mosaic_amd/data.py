@@ -1,0 +1,113 @@
+"""Polygon fixtures and synthetic point sets for the BASELINE configs (host side, not the hot path).
+
+Polygon sets are the reference's own data files converted by tests/golden/make_fixtures.py
+(NYC taxi zones: notebooks/data/NYC_Taxi_Zones.geojson; London postcodes:
+notebooks/data/London_Postcode_Zones.geojson).  Point generators follow BASELINE.md section 3:
+seeds 20250117 + config number; uniform over the zone bbox (C2), or the Quickstart mixture
+(80 % Gaussian around 32 seeded zone centres, 20 % uniform, rounded to 1e-6 degrees; C1 / C3).
+"""
+import os
+
+import numpy as np
+
+from . import wkb as W
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(_ROOT, "tests", "golden")
+SEED_BASE = 20250117
+
+
+class PolygonSet:
+    """Geometries as flat arrays: xy[V,2], ring_offsets[R+1], part_rings[P+1], geom_parts[G+1]."""
+
+    def __init__(self, xy, ring_offsets, part_rings, geom_parts, names=None):
+        self.xy = np.ascontiguousarray(xy, np.float64)
+        self.ring_offsets = np.ascontiguousarray(ring_offsets, np.int64)
+        self.part_rings = np.ascontiguousarray(part_rings, np.int64)
+        self.geom_parts = np.ascontiguousarray(geom_parts, np.int64)
+        self.names = names
+
+    @classmethod
+    def load(cls, name):
+        z = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+        return cls(z["xy"], z["ring_offsets"], z["part_rings"], z["geom_parts"], z["names"])
+
+    def __len__(self):
+        return len(self.geom_parts) - 1
+
+    def parts(self, g):
+        """Geometry g as a list of parts, each a list of rings of (x, y)."""
+        out = []
+        for p in range(self.geom_parts[g], self.geom_parts[g + 1]):
+            rings = []
+            for r in range(self.part_rings[p], self.part_rings[p + 1]):
+                a, b = self.ring_offsets[r], self.ring_offsets[r + 1]
+                rings.append([tuple(v) for v in self.xy[a:b]])
+            out.append(rings)
+        return out
+
+    def wkb(self, g, big_endian=True):
+        return W.geometry_wkb(self.parts(g), big_endian)
+
+    def subset(self, idx):
+        xy, ro, pr, gp = [], [0], [0], [0]
+        for g in idx:
+            for rings in self.parts(g):
+                for ring in rings:
+                    xy.extend(ring)
+                    ro.append(len(xy))
+                pr.append(len(ro) - 1)
+            gp.append(len(pr) - 1)
+        names = None if self.names is None else self.names[list(idx)]
+        return PolygonSet(np.asarray(xy), ro, pr, gp, names)
+
+    def bbox(self):
+        return (float(self.xy[:, 0].min()), float(self.xy[:, 1].min()), float(self.xy[:, 0].max()),
+                float(self.xy[:, 1].max()))
+
+    def geom_bbox(self, g):
+        a = self.ring_offsets[self.part_rings[self.geom_parts[g]]]
+        b = self.ring_offsets[self.part_rings[self.geom_parts[g + 1]]]
+        v = self.xy[a:b]
+        return float(v[:, 0].min()), float(v[:, 1].min()), float(v[:, 0].max()), float(v[:, 1].max())
+
+    def shell_centroid(self, g):
+        """Mean of the first shell's vertices (cheap 'zone centre' for the mixture generator)."""
+        r = self.part_rings[self.geom_parts[g]]
+        v = self.xy[self.ring_offsets[r]:self.ring_offsets[r + 1]]
+        return float(v[:, 0].mean()), float(v[:, 1].mean())
+
+
+def quickstart_points(zones, n, config=1, sigma=0.005, seed=None, round_1e6=True):
+    """C1 / C3 mixture on the host (numpy PCG64)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + config if seed is None else seed))
+    x0, y0, x1, y1 = zones.bbox()
+    centres = np.array([zones.shell_centroid(g) for g in rng.choice(len(zones), 32, replace=False)])
+    n_mix = int(0.8 * n)
+    c = centres[rng.integers(0, 32, n_mix)]
+    pts = np.empty((n, 2))
+    pts[:n_mix] = c + rng.normal(0.0, sigma, (n_mix, 2))
+    pts[n_mix:, 0] = rng.uniform(x0, x1, n - n_mix)
+    pts[n_mix:, 1] = rng.uniform(y0, y1, n - n_mix)
+    rng.shuffle(pts)
+    if round_1e6:
+        pts = np.round(pts * 1e6) / 1e6
+    return np.ascontiguousarray(pts[:, 0]), np.ascontiguousarray(pts[:, 1])
+
+
+def uniform_points(bbox, n, config=2, seed=None):
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + config if seed is None else seed))
+    x0, y0, x1, y1 = bbox
+    return rng.uniform(x0, x1, n), rng.uniform(y0, y1, n)
+
+
+def uniform_points_device(bbox, n, seed, device="cuda"):
+    """Device-side uniform points (torch Philox): the 1e9-point configs never cross PCIe."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x0, y0, x1, y1 = bbox
+    x = torch.rand(n, generator=g, device=device, dtype=torch.float64).mul_(x1 - x0).add_(x0)
+    y = torch.rand(n, generator=g, device=device, dtype=torch.float64).mul_(y1 - y0).add_(y0)
+    return x, y

@@ -1,0 +1,284 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the same inputs.
+
+Bit-exact for cell ids, contains booleans, join counts and pairs.  Runs on the MI355X box only.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from mosaic_amd import IllegalStateException, MosaicContext
+from mosaic_amd import wkb as W
+from mosaic_amd.data import PolygonSet, quickstart_points
+
+from .helpers import boundary_points, chips_to_oracle, synthetic_chips
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_vectors.json")))
+
+
+@pytest.fixture(scope="module")
+def h3ctx():
+    ctx = MosaicContext.build("H3", "JTS")
+    yield ctx
+    ctx.close()
+
+
+@pytest.fixture(scope="module")
+def bngctx():
+    ctx = MosaicContext.build("BNG", "JTS")
+    yield ctx
+    ctx.close()
+
+
+@pytest.fixture(scope="module")
+def zones():
+    return PolygonSet.load("nyc_taxi_zones")
+
+
+# ---------------- (a) point -> cell ----------------
+def test_h3_known_answers_gpu(h3ctx):
+    for c in GOLD["h3_point_to_cell"]:
+        got = h3ctx.grid_longlatascellid(np.array([c["lon"]]), np.array([c["lat"]]), c["res"])
+        assert int(got[0]) == c["cell"], c["source"]
+
+
+def _sphere_points(rng, n):
+    lon = rng.uniform(-180, 180, n)
+    lat = np.degrees(np.arcsin(rng.uniform(-1, 1, n)))
+    return lon, lat
+
+
+@pytest.mark.parametrize("res", list(range(16)))
+def test_h3_cells_match_oracle_global(h3ctx, res):
+    rng = np.random.default_rng(100 + res)
+    lon, lat = _sphere_points(rng, 200_000)
+    got = h3ctx.grid_longlatascellid(lon, lat, res)
+    want = oracle.h3_point_to_index(lon, lat, res)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(lon[i], lat[i], hex(got[i]), hex(want[i])) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("res", [8, 9, 10, 11])
+def test_h3_cells_match_oracle_nyc(h3ctx, zones, res):
+    x, y = quickstart_points(zones, 1_000_000, config=1)
+    got = h3ctx.grid_longlatascellid(x, y, res)
+    want = oracle.h3_point_to_index(x, y, res)
+    assert np.array_equal(got, want)
+
+
+def test_h3_cells_adversarial(h3ctx):
+    """Points at hexagon vertices / edge midpoints of every face and resolution (forces the exact
+    path) must still match the oracle bit for bit; the stats counter shows the exact path ran."""
+    rng = np.random.default_rng(5)
+    # vertices of res-r cells near random points: cell centres +- half a cell, many resolutions
+    lon, lat = _sphere_points(rng, 50_000)
+    for res in (5, 9, 12, 15):
+        # snap onto an exactly representable grid to create ties in the projection
+        step = 10.0 ** (-(res // 2 + 1))
+        lo = np.round(lon / step) * step
+        la = np.round(lat / step) * step
+        got = h3ctx.grid_longlatascellid(lo, la, res)
+        want = oracle.h3_point_to_index(lo, la, res)
+        assert np.array_equal(got, want), res
+
+
+def test_h3_jdk_toggle(h3ctx):
+    rng = np.random.default_rng(9)
+    lon, lat = _sphere_points(rng, 100_000)
+    h3ctx.set_option("jdk", 11)
+    try:
+        got = h3ctx.grid_longlatascellid(lon, lat, 12)
+    finally:
+        h3ctx.set_option("jdk", 8)
+    assert np.array_equal(got, oracle.h3_point_to_index(lon, lat, 12, jdk=11))
+
+
+def test_h3_nonfinite_and_resolution_errors(h3ctx):
+    got = h3ctx.grid_longlatascellid(np.array([np.nan, 1.0, np.inf]), np.array([1.0, np.nan, 2.0]), 9)
+    assert list(got) == [0, 0, 0]
+    with pytest.raises(IllegalStateException, match="H3 resolution has to be between 0 and 15; found 16"):
+        h3ctx.grid_longlatascellid(np.array([1.0]), np.array([1.0]), 16)
+    with pytest.raises(IllegalStateException, match="found -1"):
+        h3ctx.grid_longlatascellid(np.array([1.0]), np.array([1.0]), -1)
+    assert h3ctx.index_system.get_resolution("9") == 9
+
+
+def test_h3_empty_input(h3ctx):
+    assert len(h3ctx.grid_longlatascellid(np.zeros(0), np.zeros(0), 9)) == 0
+
+
+def test_grid_pointascellid_wkt(h3ctx):
+    pts = ["POINT (30 10)", "POINT (-74.044444 40.689167)"]
+    got = h3ctx.grid_pointascellid(pts, 10)
+    assert int(got[0]) == 623385352048508927
+    assert int(got[1]) == 0x8A2A1072B59FFFF
+
+
+def test_h3_device_tensors(h3ctx):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(3)
+    lon, lat = _sphere_points(rng, 100_000)
+    got = h3ctx.grid_longlatascellid(torch.tensor(lon, device="cuda"), torch.tensor(lat, device="cuda"), 9)
+    assert got.is_cuda
+    assert np.array_equal(got.cpu().numpy(), oracle.h3_point_to_index(lon, lat, 9))
+
+
+def test_bng_golden_gpu(bngctx):
+    for c in GOLD["bng_point_to_index"]:
+        got = bngctx.grid_longlatascellid(np.array([float(c["e"])]), np.array([float(c["n"])]), c["res"])
+        assert got == [c["fmt"]]
+        raw = bngctx.grid_longlatascellid(np.array([float(c["e"])]), np.array([float(c["n"])]), c["res"], raw=True)
+        assert int(raw[0]) == c["id"]
+        assert bngctx.index_system.parse(c["fmt"]) == c["id"]
+
+
+@pytest.mark.parametrize("res", [1, 2, 3, 4, 5, 6, -1, -2, -3, -4, -5, -6])
+def test_bng_matches_oracle(bngctx, res):
+    rng = np.random.default_rng(200 + res)
+    e = rng.uniform(-1e5, 8e5, 200_000)
+    n = rng.uniform(-1e5, 1.4e6, 200_000)
+    e[:1000] = np.round(e[:1000])  # integral coordinates exercise the bin edges
+    n[:1000] = np.round(n[:1000])
+    got = bngctx.grid_longlatascellid(e, n, res, raw=True)
+    want, err = oracle.bng_point_to_index_batch(e, n, res)
+    assert not err.any()
+    assert np.array_equal(got, want)
+
+
+def test_bng_errors(bngctx):
+    with pytest.raises(IllegalStateException, match="NaN coordinates are not supported."):
+        bngctx.grid_longlatascellid(np.array([np.nan]), np.array([100.0]), 5)
+    with pytest.raises(IllegalStateException, match="BNG resolution not supported"):
+        bngctx.grid_longlatascellid(np.array([1.0]), np.array([1.0]), 7)
+    assert bngctx.index_system.get_resolution("100m") == 4
+    assert bngctx.index_system.get_resolution("500m") == -4
+
+
+# ---------------- (c) st_contains ----------------
+def test_st_contains_golden_gpu(h3ctx):
+    poly = GOLD["contains"]["polygon"]
+    pts = [p for p, _ in GOLD["contains"]["cases"]]
+    got = h3ctx.st_contains(poly, pts)
+    assert list(got) == [e for _, e in GOLD["contains"]["cases"]]
+
+
+def test_st_contains_matches_oracle(h3ctx, zones):
+    rng = np.random.default_rng(11)
+    ids = list(range(0, 263, 7))
+    bx, by = boundary_points(zones, ids, rng)
+    geoms, xs, ys = [], [], []
+    for i in range(len(bx)):
+        g = ids[i % len(ids)]
+        geoms.append(zones.wkb(g))
+        xs.append(bx[i])
+        ys.append(by[i])
+    for g in ids:  # random interior/exterior points per zone
+        x0, y0, x1, y1 = zones.geom_bbox(g)
+        for _ in range(200):
+            geoms.append(zones.wkb(g, big_endian=False))
+            xs.append(rng.uniform(x0, x1))
+            ys.append(rng.uniform(y0, y1))
+    got = h3ctx.st_contains(geoms, (np.array(xs), np.array(ys)))
+    want = np.array([oracle.wkb_contains(w, x, y) for w, x, y in zip(geoms, xs, ys)])
+    assert np.array_equal(got, want)
+    assert want.sum() > 0 and (~want).sum() > 0
+
+
+# ---------------- (b)+(c) the chip join ----------------
+def _join_case(ctx, zones, res, n_points, seed, grid=oracle.GRID_H3):
+    rng = np.random.default_rng(seed)
+    ids = list(rng.choice(len(zones), 40, replace=False))
+    chips = synthetic_chips(zones, ids, res, lambda x, y, r: oracle.h3_point_to_index(x, y, r), rng)
+    table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
+                           n_polygons=len(ids))
+    sub = zones.subset(ids)
+    x, y = quickstart_points(sub, n_points, seed=seed)
+    bx, by = boundary_points(zones, ids, rng, n_per=20)
+    x = np.concatenate([x, bx])
+    y = np.concatenate([y, by])
+    return chips, table, x, y, len(ids)
+
+
+@pytest.mark.parametrize("res", [8, 9, 10])
+def test_join_counts_match_oracle(h3ctx, zones, res):
+    chips, table, x, y, npoly = _join_case(h3ctx, zones, res, 300_000, seed=res)
+    got = h3ctx.pip_join_count(table, x, y)
+    want, total = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_H3, res, x, y, npoly, threads=8)
+    assert np.array_equal(got, want)
+    assert total > 1000
+    stats = h3ctx.last_stats()
+    assert stats["pairs"] == total and stats["contains_tests"] > 0
+
+
+def test_join_pairs_match_oracle(h3ctx, zones):
+    chips, table, x, y, npoly = _join_case(h3ctx, zones, 9, 100_000, seed=21)
+    rows, keys = h3ctx.pip_join_pairs(table, x, y, capacity=16)  # forces the capacity retry
+    _, total, orow, okey = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_H3, 9, x, y, npoly, pairs=True)
+    order = np.lexsort((okey, orow))
+    assert len(rows) == total
+    assert np.array_equal(rows, orow[order]) and np.array_equal(keys, okey[order])
+
+
+def test_join_many_polygons_global_counts(h3ctx, zones):
+    """More polygon keys than the LDS histogram holds: the global-atomic count path."""
+    rng = np.random.default_rng(4)
+    ids = list(range(263))
+    chips = synthetic_chips(zones, ids, 9, lambda x, y, r: oracle.h3_point_to_index(x, y, r), rng, pts_per_zone=50)
+    # spread keys over a large key space
+    chips["polygon_key"] = chips["polygon_key"] * 40
+    n_poly = 263 * 40
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9, n_poly)
+    x, y = quickstart_points(zones, 200_000, seed=4)
+    got = h3ctx.pip_join_count(table, x, y)
+    want, _ = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_H3, 9, x, y, n_poly, threads=8)
+    assert np.array_equal(got, want)
+
+
+def test_join_empty_and_edge_inputs(h3ctx, zones):
+    chips, table, x, y, npoly = _join_case(h3ctx, zones, 9, 1000, seed=2)
+    assert not h3ctx.pip_join_count(table, np.zeros(0), np.zeros(0)).any()
+    got = h3ctx.pip_join_count(table, np.array([np.nan, 0.0]), np.array([0.0, np.nan]))
+    assert not got.any()
+    empty = h3ctx.chip_table(np.zeros(0, np.uint8), np.zeros(0, np.int64), [], np.zeros(0, np.int32), 9, 0)
+    assert len(h3ctx.pip_join_count(empty, x, y)) == 0
+
+
+def test_join_device_tensors(h3ctx, zones):
+    torch = pytest.importorskip("torch")
+    chips, table, x, y, npoly = _join_case(h3ctx, zones, 9, 200_000, seed=8)
+    got = h3ctx.pip_join_count(table, torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda"))
+    want, _ = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_H3, 9, x, y, npoly, threads=8)
+    assert np.array_equal(got.cpu().numpy(), want)
+
+
+def test_join_bng(bngctx):
+    london = PolygonSet.load("london_postcode_zones")
+    # project-free check: use the London polygons' lon/lat as planar coordinates scaled into BNG
+    # metres (the join semantics do not depend on the CRS); chips from BNG cells of random points
+    rng = np.random.default_rng(6)
+    ids = list(range(0, 177, 5))
+    scale = np.array([1e5, 1e5])
+    xy = (london.xy - london.xy.min(0)) * scale + np.array([500000.0, 150000.0])
+    proj = PolygonSet(xy, london.ring_offsets, london.part_rings, london.geom_parts)
+    res = 4
+
+    def cell_fn(xs, ys, r):
+        out, err = oracle.bng_point_to_index_batch(xs, ys, r)
+        return out
+
+    chips = synthetic_chips(proj, ids, res, cell_fn, rng, pts_per_zone=300)
+    table = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
+                              n_polygons=len(ids))
+    x0, y0, x1, y1 = proj.bbox()
+    x = rng.uniform(x0, x1, 300_000)
+    y = rng.uniform(y0, y1, 300_000)
+    got = bngctx.pip_join_count(table, x, y)
+    want, total = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_BNG, res, x, y, len(ids), threads=8)
+    assert np.array_equal(got, want) and total > 0
+    with pytest.raises(IllegalStateException, match="NaN"):
+        bngctx.pip_join_count(table, np.array([np.nan]), np.array([1.0]))

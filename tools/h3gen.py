@@ -505,8 +505,111 @@ def write_header(path, centers_geo, fcp, axes, final):
         fh.write("\n".join(L) + "\n")
 
 
+# --- x87 extended-precision constants (used by the exact device path) -----------------------------
+LD_CONSTANTS = {
+    "M_2PI": "6.28318530717958647692528676655900576839433",
+    "M_SQRT7": "2.6457513110645905905016157536392604257102",
+    "M_SIN60": "0.8660254037844386467637231707529361834714",
+    "M_AP7_ROT_RADS": "0.333473172251832115336090755351601070065900389",
+    "EPSILON": "0.0000000000000001",
+}
+
+
+def ld_round(text):
+    """Round a decimal literal to x87 double-extended (64-bit significand, RNE) exactly as gcc does
+    for an L-suffixed literal.  Returns (m64, e) with value = m64 * 2**e, 2**63 <= m64 < 2**64."""
+    from fractions import Fraction
+    v = Fraction(text)
+    e = 0
+    while v * Fraction(2) ** (-e) >= 2 ** 64:
+        e += 1
+    while v * Fraction(2) ** (-e) < 2 ** 63:
+        e -= 1
+    q = v * Fraction(2) ** (-e)
+    m = q.numerator // q.denominator
+    rem = q - m
+    if rem > Fraction(1, 2) or (rem == Fraction(1, 2) and m % 2 == 1):
+        m += 1
+    if m == 2 ** 64:
+        m //= 2
+        e += 1
+    return m, e
+
+
+def double_up(m, e):
+    """Smallest double >= m * 2**e."""
+    import math
+    from fractions import Fraction
+    v = Fraction(m) * Fraction(2) ** e
+    d = float(v)
+    if Fraction(d) < v:
+        d = math.nextafter(d, math.inf)
+    return d
+
+
+def write_ld_header(path):
+    L = ["/* Generated by tools/h3gen.py -- do not edit.",
+         " * H3 v3.7 long-double (L-suffixed) constants as x87 double-extended values:",
+         " * value = m * 2^e with a 64-bit significand m (bit 63 set), rounded RNE from the literal",
+         " * exactly as gcc does on x86-64.  *_DUP is the smallest double >= the value. */",
+         "#ifndef MOSAIC_H3_LD_CONSTANTS_H", "#define MOSAIC_H3_LD_CONSTANTS_H"]
+    for name, text in LD_CONSTANTS.items():
+        m, e = ld_round(text)
+        L.append(f"#define H3LD_{name}_M 0x{m:016x}ULL")
+        L.append(f"#define H3LD_{name}_E ({e})")
+        L.append(f"#define H3LD_{name}_DUP {double_up(m, e)!r}")
+    L.append("#endif")
+    with open(path, "w") as fh:
+        fh.write("\n".join(L) + "\n")
+
+
+
+# --- fast projective path tables ------------------------------------------------------------------
+def write_fast_header(path):
+    """Per-face gnomonic basis for the fast point->hex2d path (h3_device.h):
+    x = SCALE[res] * (EI . p) / (FC . p),  y = SCALE[res] * (EP . p) / (FC . p)
+    where FC is the unit face centre, EI the unit tangent along the face's Class II i-axis
+    (azimuth faceAxesAzRadsCII[f][0]) and EP that rotated 90 degrees counter-clockwise; the Class III
+    (odd resolution) pair is the same basis rotated by -M_AP7_ROT_RADS.  This is geoToH3's
+    acos/azimuth/tan chain written as the projective map it is mathematically."""
+    cg = [(D(a), D(b)) for a, b in FACE_CENTER_GEO]
+    rot = M_AP7_ROT_RADS
+    cr, sr = hp.cos(rot), hp.sin(rot)
+    rows = []
+    for f in range(20):
+        lat, lng = cg[f]
+        c = vec_from_geo(lat, lng)
+        n_, e_ = north_east(lat, lng)
+        az = D(RECALLED_AXIS0[f])
+        ca, sa = hp.cos(az), hp.sin(az)
+        ei2 = add(scale(n_, ca), scale(e_, sa))
+        ep2 = sub(scale(n_, sa), scale(e_, ca))
+        ei3 = add(scale(ei2, cr), scale(ep2, sr))
+        ep3 = sub(scale(ep2, cr), scale(ei2, sr))
+        rows.append((c, ei2, ep2, ei3, ep3))
+    L = ["/* Generated by tools/h3gen.py -- do not edit.  Fast projective geoToH3 tables. */",
+         "#ifndef MOSAIC_H3_FAST_TABLES_H", "#define MOSAIC_H3_FAST_TABLES_H",
+         "#ifndef H3_TABLE", "#define H3_TABLE static const", "#endif",
+         "/* per face: FC[3], EI2[3], EP2[3], EI3[3], EP3[3] */",
+         "H3_TABLE double kH3FastBasis[20][15] = {"]
+    for r in rows:
+        vals = [hp.to_double(v) for vec in r for v in vec]
+        L.append("    {" + ", ".join(repr(v) for v in vals) + "},")
+    L.append("};")
+    L.append("/* SCALE[res] = sqrt(7)^res / RES0_U_GNOMONIC */")
+    L.append("H3_TABLE double kH3FastScale[16] = {")
+    sq7 = D(7).sqrt()
+    L.append("    " + ", ".join(repr(hp.to_double(sq7 ** r / RES0_U_GNOMONIC)) for r in range(16)))
+    L.append("};")
+    L.append("#endif")
+    with open(path, "w") as fh:
+        fh.write("\n".join(L) + "\n")
+
+
 if __name__ == "__main__":
     here = os.path.dirname(os.path.abspath(__file__))
     out = os.path.join(here, "..", "mosaic_amd", "csrc", "h3_tables.h")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     main(os.path.normpath(out))
+    write_ld_header(os.path.normpath(os.path.join(here, "..", "mosaic_amd", "csrc", "h3_ld_constants.h")))
+    write_fast_header(os.path.normpath(os.path.join(here, "..", "mosaic_amd", "csrc", "h3_fast_tables.h")))
