@@ -75,7 +75,7 @@ int mosaic_init(int device, mosaic_ctx** out);
 int mosaic_destroy(mosaic_ctx* ctx);
 /* Options: "jdk" (8: Math.toRadians = deg / 180 * PI, the JDK 8 runtime of the reference's CI;
  * 9+: deg * DEGREES_TO_RADIANS), "async" (0/1), "block" (threads per block, multiple of 64),
- * "blocks_per_cu" (grid sizing). */
+ * "blocks_per_cu" (grid sizing), "timing" (0/1: HIP events around each fused join kernel). */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* The hipStream_t work is enqueued on (owned by the context unless set). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
@@ -83,8 +83,13 @@ int mosaic_set_stream(mosaic_ctx* ctx, void* stream);
 /* Wait for enqueued work; reports deferred errors of async calls. */
 int mosaic_sync(mosaic_ctx* ctx);
 /* Counters of the last join/index call: [0] rows that needed the exact H3 path,
- * [1] (point, border chip) contains tests, [2] matched pairs.  Filled only by sync calls. */
+ * [1] (point, border chip) contains tests, [2] matched pairs (pairs calls only).
+ * Filled only by sync calls. */
 int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3);
+/* With option "timing" = 1, every join call brackets its fused kernel with HIP events on the
+ * context stream.  Waits for the stream, writes up to cap elapsed times (ms) in call order, reports
+ * how many calls were timed in *n_out, and resets the list. */
+int mosaic_kernel_times(mosaic_ctx* ctx, double* out_ms, int64_t cap, int64_t* n_out);
 
 /* ---- grid systems ---- */
 /* getResolution for an Int resolution; validates the range of the grid system. */
@@ -119,6 +124,24 @@ int mosaic_pip_join_count(mosaic_ctx* ctx, const mosaic_chips* chips, const doub
  * returns MOSAIC_E_CAPACITY with *n_out = required size. */
 int mosaic_pip_join_pairs(mosaic_ctx* ctx, const mosaic_chips* chips, const double* x, const double* y,
                           int64_t n, int64_t* out_row, int32_t* out_key, int64_t cap, int64_t* n_out);
+
+/* ---- chip production (host; build side of the join, not the hot path) ---- */
+/* grid_tessellateexplode(geometry, res, keep_core_geom) over n_geoms polygonal geometries given as
+ * flat rings: geometry g = parts [geom_parts[g], geom_parts[g+1]); part p = rings
+ * [part_rings[p], part_rings[p+1]); ring r = vertices xy[2*ring_offsets[r] ..] (x, y interleaved,
+ * lon/lat for H3, BNG metres for BNG).  Chip rows carry the geometry index as their key.
+ * densify >= 1 subdivides H3 cell edges (1 = the 6-vertex h3ToGeoBoundary polygon).
+ * Reference: expressions/index/MosaicExplode.scala:70-79, core/Mosaic.scala:21-87,
+ * core/index/IndexSystem.scala:152-186. */
+typedef struct mosaic_chip_set mosaic_chip_set;
+int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                      const int64_t* ring_offsets, const double* xy, int keep_core_geom, int densify,
+                      mosaic_chip_set** out);
+int mosaic_chip_set_info(const mosaic_chip_set* cs, int64_t* n_chips, int64_t* wkb_bytes);
+/* Copies the chip rows out: is_core[n], index_id[n], key[n], wkb_offsets[n+1], wkb[wkb_bytes]. */
+int mosaic_chip_set_export(const mosaic_chip_set* cs, uint8_t* is_core, int64_t* index_id, int32_t* key,
+                           int64_t* wkb_offsets, uint8_t* wkb);
+int mosaic_chip_set_destroy(mosaic_chip_set* cs);
 
 /* ---- st_contains per row ---- */
 /* out[i] = JTS contains(geometry[geom_index[i]], POINT(px[i] py[i])); geometries given as WKB. */

@@ -29,7 +29,8 @@ EXPORTS = [
     "mosaic_get_stream", "mosaic_set_stream", "mosaic_sync", "mosaic_last_stats", "mosaic_resolution",
     "mosaic_resolution_str", "mosaic_point_to_cell", "mosaic_bng_format", "mosaic_bng_parse",
     "mosaic_chip_table_create", "mosaic_chip_table_destroy", "mosaic_chip_table_info", "mosaic_pip_join_count",
-    "mosaic_pip_join_pairs", "mosaic_st_contains",
+    "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_chip_set_info",
+    "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times",
 ]
 
 
@@ -62,6 +63,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise NativeUnavailable(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as
+    # /opt/rocm's).  Whichever loads first is shared by both; if ours loads first, torch.cuda fails
+    # to initialise later in the process.  So let torch load it first when torch is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, i64, i32, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p
     sig = {
@@ -85,6 +93,11 @@ def lib():
         "mosaic_pip_join_count": ([vp, vp, vp, vp, i64, vp], i32),
         "mosaic_pip_join_pairs": ([vp, vp, vp, vp, i64, vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_st_contains": ([vp, i64, vp, vp, vp, vp, vp, i64, vp], i32),
+        "mosaic_tessellate": ([i32, i32, i64, vp, vp, vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
+        "mosaic_chip_set_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "mosaic_chip_set_export": ([vp, vp, vp, vp, vp, vp], i32),
+        "mosaic_chip_set_destroy": ([vp], i32),
+        "mosaic_kernel_times": ([vp, vp, i64, ctypes.POINTER(i64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -211,6 +211,13 @@ class MosaicContext:
     def sync(self):
         N.check(N.lib().mosaic_sync(self.handle))
 
+    def kernel_times(self, cap=4096):
+        """Elapsed ms of each fused join kernel since option "timing" was set (HIP events)."""
+        out = np.zeros(cap, np.float64)
+        n = ctypes.c_int64(0)
+        N.check(N.lib().mosaic_kernel_times(self.handle, N.ptr(out), cap, ctypes.byref(n)))
+        return out[:min(n.value, cap)]
+
     def last_stats(self):
         out = np.zeros(3, np.int64)
         N.check(N.lib().mosaic_last_stats(self.handle, N.ptr(out)))
@@ -304,11 +311,14 @@ class MosaicContext:
             index_id = np.array([self.index_system.parse(s) for s in index_id], np.int64)
         return ChipTable(self, is_core, index_id, wkb_list, polygon_key, n_polygons)
 
-    def pip_join_count(self, chips, x, y):
-        """Quickstart join + filter + groupBy(polygon).count(): int64 count per polygon key."""
+    def pip_join_count(self, chips, x, y, out=None):
+        """Quickstart join + filter + groupBy(polygon).count(): int64 count per polygon key.
+        ``out`` (optional, >= n_polygons int64, host or device) receives the counts."""
         x, y = _f64(x), _f64(y)
         n = int(x.shape[0])
-        if _is_torch(x):
+        if out is not None:
+            counts = out
+        elif _is_torch(x):
             import torch
 
             counts = torch.zeros(max(chips.n_polygons, 1), dtype=torch.int64, device=x.device)
@@ -335,3 +345,33 @@ class MosaicContext:
             k = int(n_out.value)
             order = np.lexsort((keys[:k], rows[:k]))
             return rows[:k][order], keys[:k][order]
+
+
+def tessellate(index_system, polygons, resolution, keep_core_geom=True, densify=1):
+    """grid_tessellateexplode over a PolygonSet (mosaic_amd.data.PolygonSet) on the host.
+
+    Returns chip columns: dict(is_core uint8, index_id int64, polygon_key int32 (geometry index),
+    wkb=(offsets int64[n+1], data uint8[...])).  MosaicExplode.scala:70-79 / Mosaic.scala:21-87.
+    """
+    if isinstance(index_system, str):
+        index_system = INDEX_SYSTEMS[index_system]()
+    res = index_system.get_resolution(resolution)
+    h = ctypes.c_void_p()
+    N.check(N.lib().mosaic_tessellate(index_system.grid, res, len(polygons), N.ptr(polygons.geom_parts),
+                                      N.ptr(polygons.part_rings), N.ptr(polygons.ring_offsets),
+                                      N.ptr(polygons.xy), int(bool(keep_core_geom)), int(densify), ctypes.byref(h)))
+    try:
+        n = ctypes.c_int64(0)
+        nb = ctypes.c_int64(0)
+        N.check(N.lib().mosaic_chip_set_info(h, ctypes.byref(n), ctypes.byref(nb)))
+        n, nb = n.value, nb.value
+        is_core = np.zeros(n, np.uint8)
+        index_id = np.zeros(n, np.int64)
+        key = np.zeros(n, np.int32)
+        offs = np.zeros(n + 1, np.int64)
+        data = np.zeros(max(nb, 1), np.uint8)
+        N.check(N.lib().mosaic_chip_set_export(h, N.ptr(is_core), N.ptr(index_id), N.ptr(key), N.ptr(offs),
+                                               N.ptr(data)))
+    finally:
+        N.lib().mosaic_chip_set_destroy(h)
+    return dict(is_core=is_core, index_id=index_id, polygon_key=key, wkb=(offs, data))

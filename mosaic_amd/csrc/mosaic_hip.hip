@@ -306,7 +306,28 @@ struct mosaic_ctx {
     DevBuf amb_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
+    // option "timing": HIP events bracket each fused join kernel on the context stream
+    int timing = 0;
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    size_t ev_used = 0;
 };
+
+static int timing_begin(mosaic_ctx* c, hipEvent_t* stop_out) {
+    *stop_out = nullptr;
+    if (!c->timing) return MOSAIC_OK;
+    if (c->ev_used == c->ev_start.size()) {
+        if (c->ev_used >= 4096) return MOSAIC_OK;  // bounded; extra calls are not timed
+        hipEvent_t a, b;
+        HIP_TRY(hipEventCreate(&a));
+        HIP_TRY(hipEventCreate(&b));
+        c->ev_start.push_back(a);
+        c->ev_stop.push_back(b);
+    }
+    HIP_TRY(hipEventRecord(c->ev_start[c->ev_used], c->stream));
+    *stop_out = c->ev_stop[c->ev_used];
+    c->ev_used++;
+    return MOSAIC_OK;
+}
 
 struct GeomStoreDev {
     DevBuf verts, ring_start, ring_bbox, part_ring, geom_part, geom_bbox;
@@ -408,6 +429,8 @@ static const int kScalars = 4;
 
 extern "C" {
 
+int mosaic_tess_fail(int code, const char* msg) { return fail(code, msg); }
+
 int mosaic_abi_version(void) { return MOSAIC_ABI_VERSION; }
 const char* mosaic_last_error(void) { return g_last_error.c_str(); }
 
@@ -441,6 +464,10 @@ int mosaic_destroy(mosaic_ctx* c) {
     for (DevBuf* b : {&c->amb_queue, &c->scalars, &c->stage_x, &c->stage_y, &c->stage_v, &c->stage_out, &c->stage_out2,
                       &c->stage_idx})
         b->release();
+    for (size_t i = 0; i < c->ev_start.size(); i++) {
+        (void)hipEventDestroy(c->ev_start[i]);
+        (void)hipEventDestroy(c->ev_stop[i]);
+    }
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return MOSAIC_OK;
@@ -460,6 +487,9 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "blocks_per_cu") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "blocks_per_cu must be in [1, 64]");
         c->blocks_per_cu = (int)v;
+    } else if (k == "timing") {
+        c->timing = v ? 1 : 0;
+        c->ev_used = 0;
     } else {
         return fail(MOSAIC_E_ARG, "unknown option " + k);
     }
@@ -491,6 +521,21 @@ int mosaic_sync(mosaic_ctx* c) {
     if (flags & 1u) return fail(MOSAIC_E_NAN, "NaN coordinates are not supported.");
     if ((flags & 2u) || s[0] > c->amb_queue.bytes / 8)
         return fail(MOSAIC_E_CAPACITY, "exact-path queue overflowed in an async call; rerun synchronously");
+    return MOSAIC_OK;
+}
+
+int mosaic_kernel_times(mosaic_ctx* c, double* out_ms, int64_t cap, int64_t* n_out) {
+    if (!c || !n_out || (cap > 0 && !out_ms)) return fail(MOSAIC_E_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int64_t n = (int64_t)c->ev_used;
+    for (int64_t i = 0; i < n && i < cap; i++) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev_start[i], c->ev_stop[i]));
+        out_ms[i] = ms;
+    }
+    *n_out = n;
+    c->ev_used = 0;
     return MOSAIC_OK;
 }
 
@@ -638,8 +683,9 @@ int mosaic_bng_format(int64_t id, char* buf, size_t cap) {
 static int64_t bng_encode(int eL, int nL, int eBin, int nBin, int q, int nPos, int res) {
     double idP = bng::pow10i(5 + 2 * nPos - 2), eLS = bng::pow10i(3 + 2 * nPos - 2), nLS = bng::pow10i(1 + 2 * nPos - 2);
     double eS = bng::pow10i(nPos);
+    int32_t nb10 = (int32_t)((uint32_t)nBin * 10u);  // JVM Int multiplication wraps
     double id = res == -1 ? (idP + (double)eL * eLS) / 100 + q
-                          : idP + (double)eL * eLS + (double)nL * nLS + (double)eBin * eS + (double)(nBin * 10) + q;
+                          : idP + (double)eL * eLS + (double)nL * nLS + (double)eBin * eS + (double)nb10 + q;
     return bng::jvm_d2l(id);
 }
 
@@ -838,6 +884,8 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     size_t shm = lds ? (size_t)ch->n_polygons * 4 : 0;
     int g = grid_size(c, n);
     if (n > 0) {
+        hipEvent_t tstop;
+        if ((rc = timing_begin(c, &tstop))) return rc;
         if (ch->grid == MOSAIC_GRID_H3) {
             if (pairs)
                 hipLaunchKernelGGL((k_join_h3<false, true>), dim3(g), dim3(c->block), 0, c->stream, a);
@@ -846,6 +894,7 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
             else
                 hipLaunchKernelGGL((k_join_h3<false, false>), dim3(g), dim3(c->block), 0, c->stream, a);
             HIP_TRY(hipGetLastError());
+            if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
             int ge = grid_size(c, (int64_t)qcap);
             if (pairs)
                 hipLaunchKernelGGL((k_join_h3_exact<true>), dim3(ge), dim3(c->block), 0, c->stream, a, 0);
@@ -860,6 +909,7 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
             else
                 hipLaunchKernelGGL((k_join_bng<false, false>), dim3(g), dim3(c->block), 0, c->stream, a);
             HIP_TRY(hipGetLastError());
+            if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
         }
     }
     if (c->async && !pairs && dev_counts) return MOSAIC_OK;

@@ -1,0 +1,455 @@
+// Chip production (the build side of the chip join) on the host: grid_tessellateexplode.
+//
+// Reference: MosaicExplode.eval (expressions/index/MosaicExplode.scala:70-79) -> Mosaic.getChips /
+// mosaicFill (core/Mosaic.scala:21-87) -> IndexSystem.getBorderChips / getCoreChips
+// (core/index/IndexSystem.scala:152-186).  The reference carves the polygon with JTS
+// buffer(-radius), polyfills, and intersects border cells with JTS overlay.  This producer reaches
+// the same contract -- every cell that meets the polygon gets one chip; a core chip's cell lies in
+// the polygon's interior (so its points are accepted without a test); a border chip carries
+// polygon n cell -- by exact per-cell classification instead:
+//   * H3: the polygon is projected into its icosahedron face's gnomonic hex2d plane at the target
+//     resolution (where H3 cells are exact hexagons); candidate lattice cells come from the
+//     projected bounding box; each ring is clipped against the convex hexagon (Sutherland-Hodgman)
+//     and clip vertices are mapped back to lon/lat.  Original polygon vertices are kept bit-exact.
+//     Hexagon edges are densified (H3 cell edges are great-circle arcs; straight lon/lat chords
+//     would leave slivers).  Cell ids are _faceIjkToH3 of the lattice cell (h3_device.h).
+//   * BNG: cells are axis-aligned squares in the native plane; same clipping.
+// Host-only (not the hot path; §8(f) row 1 lists the GPU producer as next).  Supports polygons
+// that lie on one icosahedron face (true for the NYC / London fixtures); others are rejected.
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/mosaic_hip.h"
+#include "bng_device.h"
+#include "h3_device.h"
+
+using namespace mosaic;
+
+extern "C" int mosaic_tess_fail(int code, const char* msg);  // defined in mosaic_hip.hip
+
+namespace {
+
+struct P2 {
+    double x, y;
+};
+
+// ---- H3 face-plane helpers (host) ----
+struct FacePlane {
+    int face, res;
+    const double *fc, *ei, *ep;
+    double S;
+    void init(int f, int r) {
+        face = f;
+        res = r;
+        const double* b = h3::kH3FastBasis[f];
+        fc = b;
+        ei = b + ((r & 1) ? 9 : 3);
+        ep = b + ((r & 1) ? 12 : 6);
+        S = h3::kH3FastScale[r];
+    }
+    static void unit(double lon_deg, double lat_deg, double p[3]) {
+        double la = lat_deg * (M_PI / 180.0), lo = lon_deg * (M_PI / 180.0);
+        p[0] = cos(lo) * cos(la);
+        p[1] = sin(lo) * cos(la);
+        p[2] = sin(la);
+    }
+    P2 to_hex(double lon, double lat) const {
+        double p[3];
+        unit(lon, lat, p);
+        double d = fc[0] * p[0] + fc[1] * p[1] + fc[2] * p[2];
+        return {S * (ei[0] * p[0] + ei[1] * p[1] + ei[2] * p[2]) / d, S * (ep[0] * p[0] + ep[1] * p[1] + ep[2] * p[2]) / d};
+    }
+    P2 to_geo(P2 h) const {
+        double t[3];
+        for (int k = 0; k < 3; k++) t[k] = fc[k] + (h.x * ei[k] + h.y * ep[k]) / S;
+        double n = sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+        return {atan2(t[1], t[0]) * (180.0 / M_PI), asin(t[2] / n) * (180.0 / M_PI)};
+    }
+};
+
+int face_of(double lon, double lat) {
+    double p[3];
+    FacePlane::unit(lon, lat, p);
+    int best = 0;
+    double bd = -2;
+    for (int f = 0; f < 20; f++) {
+        const double* b = h3::kH3FastBasis[f];
+        double d = b[0] * p[0] + b[1] * p[1] + b[2] * p[2];
+        if (d > bd) {
+            bd = d;
+            best = f;
+        }
+    }
+    return best;
+}
+
+// ---- geometry helpers (plane) ----
+double ring_area(const std::vector<P2>& r) {
+    double a = 0;
+    for (size_t i = 0; i + 1 < r.size(); i++) a += r[i].x * r[i + 1].y - r[i + 1].x * r[i].y;
+    return 0.5 * a;
+}
+
+// Sutherland-Hodgman: clip an (open) vertex list by the half-plane left of edge a->b (ccw convex clip).
+// tag[i] carries, per output vertex, the index of the original vertex (>= 0) or -1 if computed.
+void clip_edge(const std::vector<P2>& in, const std::vector<long>& tin, P2 a, P2 b, std::vector<P2>& out,
+               std::vector<long>& tout) {
+    out.clear();
+    tout.clear();
+    size_t n = in.size();
+    if (!n) return;
+    auto side = [&](P2 p) { return (b.x - a.x) * (p.y - a.y) - (b.y - a.y) * (p.x - a.x); };
+    for (size_t i = 0; i < n; i++) {
+        P2 cur = in[i], prev = in[(i + n - 1) % n];
+        double sc = side(cur), sp = side(prev);
+        bool ic = sc >= 0, ip = sp >= 0;
+        if (ic) {
+            if (!ip) {
+                double t = sp / (sp - sc);
+                out.push_back({prev.x + t * (cur.x - prev.x), prev.y + t * (cur.y - prev.y)});
+                tout.push_back(-1);
+            }
+            out.push_back(cur);
+            tout.push_back(tin[i]);
+        } else if (ip) {
+            double t = sp / (sp - sc);
+            out.push_back({prev.x + t * (cur.x - prev.x), prev.y + t * (cur.y - prev.y)});
+            tout.push_back(-1);
+        }
+    }
+}
+
+bool seg_near_convex(P2 p, P2 q, const std::vector<P2>& poly, double eps) {
+    // true if segment pq comes within eps of the convex polygon (ccw, open vertex list)
+    // test: any endpoint inside expanded poly, or segment intersects an edge, or distance < eps
+    auto inside = [&](P2 r) {
+        for (size_t i = 0; i < poly.size(); i++) {
+            P2 a = poly[i], b = poly[(i + 1) % poly.size()];
+            double ex = b.x - a.x, ey = b.y - a.y, len = sqrt(ex * ex + ey * ey);
+            if ((ex * (r.y - a.y) - ey * (r.x - a.x)) / len < -eps) return false;
+        }
+        return true;
+    };
+    if (inside(p) || inside(q)) return true;
+    auto dist_seg = [](P2 r, P2 a, P2 b) {
+        double ex = b.x - a.x, ey = b.y - a.y;
+        double t = ((r.x - a.x) * ex + (r.y - a.y) * ey) / (ex * ex + ey * ey);
+        t = std::max(0.0, std::min(1.0, t));
+        double dx = a.x + t * ex - r.x, dy = a.y + t * ey - r.y;
+        return sqrt(dx * dx + dy * dy);
+    };
+    for (size_t i = 0; i < poly.size(); i++) {
+        P2 a = poly[i], b = poly[(i + 1) % poly.size()];
+        double d1 = (b.x - a.x) * (p.y - a.y) - (b.y - a.y) * (p.x - a.x);
+        double d2 = (b.x - a.x) * (q.y - a.y) - (b.y - a.y) * (q.x - a.x);
+        double d3 = (q.x - p.x) * (a.y - p.y) - (q.y - p.y) * (a.x - p.x);
+        double d4 = (q.x - p.x) * (b.y - p.y) - (q.y - p.y) * (b.x - p.x);
+        if (((d1 > 0) != (d2 > 0)) && ((d3 > 0) != (d4 > 0))) return true;
+        if (dist_seg(a, p, q) < eps || dist_seg(p, a, b) < eps || dist_seg(q, a, b) < eps) return true;
+    }
+    return false;
+}
+
+bool point_in_rings_evenodd(P2 p, const std::vector<std::vector<P2>>& rings) {
+    bool in = false;
+    for (auto& r : rings) {
+        for (size_t i = 0, j = r.size() - 1; i < r.size(); j = i++) {
+            if (((r[i].y > p.y) != (r[j].y > p.y)) &&
+                (p.x < (r[j].x - r[i].x) * (p.y - r[i].y) / (r[j].y - r[i].y) + r[i].x))
+                in = !in;
+        }
+    }
+    return in;
+}
+
+// ---- WKB writer (JTS WKBWriter default: big-endian, 2D) ----
+struct WkbOut {
+    std::vector<uint8_t> b;
+    void u8(uint8_t v) { b.push_back(v); }
+    void u32(uint32_t v) {
+        for (int i = 3; i >= 0; i--) b.push_back((uint8_t)(v >> (8 * i)));
+    }
+    void f64(double d) {
+        uint64_t u;
+        memcpy(&u, &d, 8);
+        for (int i = 7; i >= 0; i--) b.push_back((uint8_t)(u >> (8 * i)));
+    }
+    void polygon(const std::vector<std::vector<P2>>& rings) {
+        u8(0);
+        u32(3);
+        u32((uint32_t)rings.size());
+        for (auto& r : rings) {
+            u32((uint32_t)r.size());
+            for (auto& p : r) {
+                f64(p.x);
+                f64(p.y);
+            }
+        }
+    }
+};
+
+std::vector<uint8_t> to_wkb(const std::vector<std::vector<std::vector<P2>>>& parts) {
+    WkbOut w;
+    if (parts.size() == 1) {
+        w.polygon(parts[0]);
+    } else {
+        w.u8(0);
+        w.u32(6);
+        w.u32((uint32_t)parts.size());
+        for (auto& p : parts) w.polygon(p);
+    }
+    return w.b;
+}
+
+}  // namespace
+
+struct mosaic_chip_set {
+    std::vector<uint8_t> is_core;
+    std::vector<int64_t> index_id;
+    std::vector<int32_t> key;
+    std::vector<int64_t> wkb_offsets{0};
+    std::vector<uint8_t> wkb;
+    void add(bool core, int64_t id, int32_t k, const std::vector<uint8_t>& blob) {
+        is_core.push_back(core);
+        index_id.push_back(id);
+        key.push_back(k);
+        wkb.insert(wkb.end(), blob.begin(), blob.end());
+        wkb_offsets.push_back((int64_t)wkb.size());
+    }
+};
+
+namespace {
+
+struct Cell {
+    int64_t id;
+    std::vector<P2> clip;     // convex clip polygon in the plane (ccw, open)
+    std::vector<P2> outline;  // densified outline in the plane for core chip output
+};
+
+// Classify one cell against one geometry given in the plane (plane rings + original lon/lat rings).
+// to_geo maps a plane point to output coordinates.
+template <class ToGeo>
+void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::vector<std::vector<std::vector<P2>>>& pl,
+               const std::vector<std::vector<std::vector<P2>>>& geo, double core_eps, int keep_core_geom,
+               ToGeo to_geo, double area_eps) {
+    // 1) any polygon segment near the cell?  2) cell centre inside?
+    bool near = false;
+    for (size_t pi = 0; pi < pl.size() && !near; pi++)
+        for (auto& ring : pl[pi])
+            for (size_t i = 0; i + 1 < ring.size() && !near; i++)
+                if (seg_near_convex(ring[i], ring[i + 1], cell.clip, core_eps)) near = true;
+    P2 c = {0, 0};
+    for (auto& p : cell.clip) {
+        c.x += p.x;
+        c.y += p.y;
+    }
+    c.x /= cell.clip.size();
+    c.y /= cell.clip.size();
+    if (!near) {
+        bool inside = false;
+        for (auto& part : pl) inside = inside || point_in_rings_evenodd(c, part);
+        if (!inside) return;  // disjoint (or inside a hole)
+        std::vector<uint8_t> blob;
+        if (keep_core_geom) {
+            std::vector<P2> ring;
+            for (auto& p : cell.outline) ring.push_back(to_geo(p));
+            ring.push_back(ring.front());
+            blob = to_wkb({{ring}});
+        }
+        cs->add(true, cell.id, key, blob);
+        return;
+    }
+    // border: clip every ring against the cell
+    std::vector<std::vector<std::vector<P2>>> out_parts;
+    std::vector<P2> a, b;
+    std::vector<long> ta, tb;
+    for (size_t pi = 0; pi < pl.size(); pi++) {
+        std::vector<std::vector<P2>> rings_out;
+        double net = 0;
+        for (size_t ri = 0; ri < pl[pi].size(); ri++) {
+            const auto& ring = pl[pi][ri];
+            if (ring.size() < 4) continue;
+            a.assign(ring.begin(), ring.end() - 1);  // open
+            ta.resize(a.size());
+            for (size_t i = 0; i < a.size(); i++) ta[i] = (long)i;
+            for (size_t e = 0; e < cell.clip.size() && !a.empty(); e++) {
+                clip_edge(a, ta, cell.clip[e], cell.clip[(e + 1) % cell.clip.size()], b, tb);
+                a.swap(b);
+                ta.swap(tb);
+            }
+            if (a.size() < 3) {
+                if (ri == 0) break;  // shell misses the cell
+                continue;
+            }
+            std::vector<P2> plane_closed(a);
+            plane_closed.push_back(a.front());
+            double ar = ring_area(plane_closed);
+            if (fabs(ar) <= area_eps) {
+                if (ri == 0) break;
+                continue;
+            }
+            net += ri == 0 ? fabs(ar) : -fabs(ar);
+            std::vector<P2> g;
+            g.reserve(a.size() + 1);
+            for (size_t i = 0; i < a.size(); i++)
+                g.push_back(ta[i] >= 0 ? geo[pi][ri][ta[i]] : to_geo(a[i]));  // original vertices kept exact
+            g.push_back(g.front());
+            rings_out.push_back(std::move(g));
+        }
+        if (!rings_out.empty() && net > area_eps) out_parts.push_back(std::move(rings_out));
+    }
+    if (out_parts.empty()) return;
+    cs->add(false, cell.id, key, to_wkb(out_parts));
+}
+
+}  // namespace
+
+extern "C" {
+
+int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                      const int64_t* ring_offsets, const double* xy, int keep_core_geom, int densify,
+                      mosaic_chip_set** out) {
+    if (!out || n_geoms < 0 || (n_geoms > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy)))
+        return mosaic_tess_fail(MOSAIC_E_ARG, "invalid argument");
+    if (grid == MOSAIC_GRID_H3 && (res < 0 || res > 15))
+        return mosaic_tess_fail(MOSAIC_E_RES, ("H3 resolution has to be between 0 and 15; found " + std::to_string(res)).c_str());
+    if (grid == MOSAIC_GRID_BNG && !(res != 0 && res >= -6 && res <= 6))
+        return mosaic_tess_fail(MOSAIC_E_RES, ("BNG resolution not supported; found " + std::to_string(res)).c_str());
+    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return mosaic_tess_fail(MOSAIC_E_ARG, "unknown grid");
+    if (densify < 1 || densify > 64) return mosaic_tess_fail(MOSAIC_E_ARG, "densify must be in [1, 64]");
+    mosaic_chip_set* cs = new mosaic_chip_set();
+    const int D = densify;  // hexagon edge subdivision (1 = the 6-vertex cell boundary)
+    for (int64_t g = 0; g < n_geoms; g++) {
+        // geometry in lon/lat (or BNG metres)
+        std::vector<std::vector<std::vector<P2>>> geo;
+        for (int64_t p = geom_parts[g]; p < geom_parts[g + 1]; p++) {
+            std::vector<std::vector<P2>> rings;
+            for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
+                std::vector<P2> ring;
+                for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) ring.push_back({xy[2 * v], xy[2 * v + 1]});
+                rings.push_back(std::move(ring));
+            }
+            geo.push_back(std::move(rings));
+        }
+        bool any = false;
+        for (auto& part : geo)
+            for (auto& ring : part) any = any || !ring.empty();
+        if (!any) continue;
+        if (grid == MOSAIC_GRID_H3) {
+            int face = -1;
+            for (auto& part : geo)
+                for (auto& ring : part)
+                    for (auto& p : ring) {
+                        int f = face_of(p.x, p.y);
+                        if (face < 0) face = f;
+                        if (f != face) {
+                            delete cs;
+                            return mosaic_tess_fail(MOSAIC_E_ARG, "geometry spans an icosahedron face edge "
+                                                                  "(unsupported by the host tessellator)");
+                        }
+                    }
+            FacePlane fp;
+            fp.init(face, res);
+            std::vector<std::vector<std::vector<P2>>> pl = geo;
+            double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
+            for (auto& part : pl)
+                for (auto& ring : part)
+                    for (auto& p : ring) {
+                        p = fp.to_hex(p.x, p.y);
+                        x0 = std::min(x0, p.x);
+                        x1 = std::max(x1, p.x);
+                        y0 = std::min(y0, p.y);
+                        y1 = std::max(y1, p.y);
+                    }
+            const double s60 = 0.86602540378443864676, R = 0.57735026918962576451;
+            int jlo = (int)floor(y0 / s60) - 2, jhi = (int)ceil(y1 / s60) + 2;
+            for (int j = jlo; j <= jhi; j++) {
+                int ilo = (int)floor(x0 + j * 0.5) - 2, ihi = (int)ceil(x1 + j * 0.5) + 2;
+                for (int i = ilo; i <= ihi; i++) {
+                    double cx = i - 0.5 * j, cy = j * s60;
+                    if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
+                    Cell cell;
+                    std::vector<P2> corners;
+                    for (int k = 0; k < 6; k++) {
+                        double ang = (30.0 + 60.0 * k) * (M_PI / 180.0);
+                        corners.push_back({cx + R * cos(ang), cy + R * sin(ang)});
+                    }
+                    cell.clip = corners;
+                    for (int k = 0; k < 6; k++) {
+                        P2 a = corners[k], b = corners[(k + 1) % 6];
+                        for (int s = 0; s < D; s++)
+                            cell.outline.push_back({a.x + (b.x - a.x) * s / D, a.y + (b.y - a.y) * s / D});
+                    }
+                    h3::IJK ijk = {i, j, 0};
+                    h3::ijk_normalize(ijk);
+                    cell.id = (int64_t)h3::face_ijk_to_h3(face, ijk, res);
+                    // densified clip polygon: SH on the densified (still convex) hexagon keeps the
+                    // cell boundary within ~1/D^2 of the great-circle arcs once mapped back
+                    cell.clip = cell.outline;
+                    emit_cell(cs, (int32_t)g, cell, pl, geo, 1e-3, keep_core_geom,
+                              [&](P2 h) { return fp.to_geo(h); }, 1e-12);
+                }
+            }
+        } else {
+            static const double edge_by_res[] = {0, 100000, 10000, 1000, 100, 10, 1};
+            int ar = res < 0 ? -res : res;
+            double e = res > 0 ? edge_by_res[ar] : edge_by_res[ar - 1] / 2.0;  // negative res: quadrants
+            if (res == -1) e = 500000;
+            double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
+            for (auto& part : geo)
+                for (auto& ring : part)
+                    for (auto& p : ring) {
+                        x0 = std::min(x0, p.x);
+                        x1 = std::max(x1, p.x);
+                        y0 = std::min(y0, p.y);
+                        y1 = std::max(y1, p.y);
+                    }
+            long ilo = (long)floor(x0 / e), ihi = (long)floor(x1 / e), jlo = (long)floor(y0 / e), jhi = (long)floor(y1 / e);
+            for (long j = jlo; j <= jhi; j++)
+                for (long i = ilo; i <= ihi; i++) {
+                    Cell cell;
+                    double cx0 = i * e, cy0 = j * e;
+                    cell.clip = {{cx0, cy0}, {cx0 + e, cy0}, {cx0 + e, cy0 + e}, {cx0, cy0 + e}};
+                    cell.outline = cell.clip;
+                    int64_t id;
+                    if (!bng::point_to_index(cx0 + 0.5 * e, cy0 + 0.5 * e, res, &id)) continue;
+                    cell.id = id;
+                    emit_cell(cs, (int32_t)g, cell, geo, geo, 1e-9 * e, keep_core_geom, [](P2 h) { return h; },
+                              1e-12 * e * e);
+                }
+        }
+    }
+    *out = cs;
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_set_info(const mosaic_chip_set* cs, int64_t* n_chips, int64_t* wkb_bytes) {
+    if (!cs || !n_chips || !wkb_bytes) return mosaic_tess_fail(MOSAIC_E_ARG, "null argument");
+    *n_chips = (int64_t)cs->index_id.size();
+    *wkb_bytes = (int64_t)cs->wkb.size();
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_set_export(const mosaic_chip_set* cs, uint8_t* is_core, int64_t* index_id, int32_t* key,
+                           int64_t* wkb_offsets, uint8_t* wkb) {
+    if (!cs) return mosaic_tess_fail(MOSAIC_E_ARG, "null chip set");
+    size_t n = cs->index_id.size();
+    if (is_core) memcpy(is_core, cs->is_core.data(), n);
+    if (index_id) memcpy(index_id, cs->index_id.data(), n * 8);
+    if (key) memcpy(key, cs->key.data(), n * 4);
+    if (wkb_offsets) memcpy(wkb_offsets, cs->wkb_offsets.data(), (n + 1) * 8);
+    if (wkb && !cs->wkb.empty()) memcpy(wkb, cs->wkb.data(), cs->wkb.size());
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_set_destroy(mosaic_chip_set* cs) {
+    delete cs;
+    return MOSAIC_OK;
+}
+
+}  // extern "C"

@@ -51,6 +51,8 @@ def lib():
         L.oracle_wkb_contains.argtypes = [ctypes.c_char_p, i64, f64, f64]
         L.oracle_pip_join.restype = i64
         L.oracle_pip_join.argtypes = [vp, i32, i32, i32, vp, vp, i64, vp, i64, vp, vp, i64, i32]
+        L.oracle_brute_force_count.restype = i64
+        L.oracle_brute_force_count.argtypes = [vp, vp, vp, i64, vp, i64]
         _lib = L
     return _lib
 
@@ -127,6 +129,24 @@ def wkb_contains(wkb: bytes, x, y):
 class _Chips(ctypes.Structure):
     _fields_ = [("n_chips", ctypes.c_int64), ("index_id", ctypes.c_void_p), ("is_core", ctypes.c_void_p),
                 ("polygon_key", ctypes.c_void_p), ("wkb_offsets", ctypes.c_void_p), ("wkb", ctypes.c_void_p)]
+
+
+def brute_force_count(polygons, x, y):
+    """Brute-force st_contains counts of a PolygonSet (one key per geometry)."""
+    wkbs = [polygons.wkb(g) for g in range(len(polygons))]
+    lens = np.array([len(w) for w in wkbs], np.int64)
+    offs = np.zeros(len(wkbs) + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    data = np.frombuffer(b"".join(wkbs), np.uint8).copy()
+    keys = np.arange(len(wkbs), dtype=np.int32)
+    core = np.zeros(len(wkbs), np.uint8)
+    ids = np.zeros(len(wkbs), np.int64)
+    c = _Chips(len(wkbs), _ptr(ids).value, _ptr(core).value, _ptr(keys).value, _ptr(offs).value, _ptr(data).value)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    counts = np.zeros(max(len(wkbs), 1), np.int64)
+    total = lib().oracle_brute_force_count(ctypes.byref(c), _ptr(x), _ptr(y), len(x), _ptr(counts), len(wkbs))
+    return counts[:len(wkbs)], total
 
 
 def pip_join(chips, grid, res, x, y, n_polygons, jdk=8, pairs=False, threads=1):

@@ -86,6 +86,26 @@ static void* run_job(void* arg) {
     return NULL;
 }
 
+/* Brute-force st_contains join (the reference's expected count in MosaicFrameBehaviors.scala:157-162):
+ * counts[polygon_key[g]] += #points p with contains(geometry g, p), every geometry tested. */
+int64_t oracle_brute_force_count(const oracle_chips* geoms, const double* x, const double* y, int64_t n,
+                                 int64_t* counts, int64_t n_polygons) {
+    int64_t total = 0;
+    for (int64_t g = 0; g < geoms->n_chips; g++) {
+        void* pg = oracle_wkb_parse(geoms->wkb + geoms->wkb_offsets[g], geoms->wkb_offsets[g + 1] - geoms->wkb_offsets[g]);
+        if (!pg) continue;
+        int32_t key = geoms->polygon_key[g];
+        for (int64_t i = 0; i < n; i++) {
+            if (oracle_parsed_contains(pg, x[i], y[i]) == 1) {
+                if (key >= 0 && key < n_polygons) counts[key]++;
+                total++;
+            }
+        }
+        oracle_parsed_free(pg);
+    }
+    return total;
+}
+
 int64_t oracle_pip_join(const oracle_chips* chips, int grid, int res, int jdk, const double* x,
                         const double* y, int64_t n, int64_t* counts, int64_t n_polygons,
                         int64_t* pair_row, int32_t* pair_key, int64_t cap, int n_threads) {

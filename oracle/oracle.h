@@ -85,6 +85,9 @@ typedef struct {
 int64_t oracle_pip_join(const oracle_chips* chips, int grid, int res, int jdk, const double* x,
                         const double* y, int64_t n, int64_t* counts, int64_t n_polygons,
                         int64_t* pair_row, int32_t* pair_key, int64_t cap, int n_threads);
+/* Brute force: every geometry (chips->wkb, keyed by polygon_key; is_core ignored) against every point. */
+int64_t oracle_brute_force_count(const oracle_chips* geoms, const double* x, const double* y, int64_t n,
+                                 int64_t* counts, int64_t n_polygons);
 
 #ifdef __cplusplus
 }

@@ -211,8 +211,8 @@ def test_join_counts_match_oracle(h3ctx, zones, res):
     want, total = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_H3, res, x, y, npoly, threads=8)
     assert np.array_equal(got, want)
     assert total > 1000
-    stats = h3ctx.last_stats()
-    assert stats["pairs"] == total and stats["contains_tests"] > 0
+    assert int(got.sum()) == total
+    assert h3ctx.last_stats()["contains_tests"] > 0
 
 
 def test_join_pairs_match_oracle(h3ctx, zones):
