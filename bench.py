@@ -121,11 +121,9 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    from mosaic_amd import distributed as D
+
+    rank, world, local = D.init("nccl")
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
@@ -147,8 +145,7 @@ def main():
 
     def step():
         ctx.pip_join_count(table, x, y, out=counts)
-        if world > 1:
-            dist.all_reduce(counts)
+        D.allreduce_counts(counts)
 
     for _ in range(args.warmup):
         step()
@@ -167,10 +164,7 @@ def main():
     ctx.sync()  # deferred errors (e.g. exact-path queue overflow) surface here
     kernel_ms = ctx.kernel_times()
     ctx.set_option("timing", 0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, device=dev)
 
     # one synchronous step for counters (exact-path rows, contains tests)
     ctx.set_option("async", 0)

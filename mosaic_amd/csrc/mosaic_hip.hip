@@ -22,6 +22,7 @@
 #include "bng_device.h"
 #include "geom_build.h"
 #include "h3_device.h"
+#include "pip_coop.h"
 #include "pip_device.h"
 
 using namespace mosaic;
@@ -69,6 +70,7 @@ struct JoinArgs {
     const HashEntry* table;
     uint64_t mask;
     const uint32_t* chip_meta;  // (polygon_key << 1) | is_core, in table order
+    const uint2* chip_ring;     // (first vertex, n vertices) when chip = one Polygon with one ring, else (0, 0)
     pip::GeomStore store;       // geometry g == chip g (table order)
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
@@ -158,6 +160,147 @@ __global__ void __launch_bounds__(256) k_join_h3(JoinArgs a) {
         }
         join_point<LDS_COUNTS, PAIRS>(a, i, x, y, cell, lds, tests);
     }
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
+// ---- wave-cooperative variant (default): lanes own points for (a)+(b); each border-chip test is
+// then evaluated by the whole wave (pip_coop.h), one work item at a time, wave-uniform.
+template <bool LDS_COUNTS, bool PAIRS>
+__device__ inline void emit_hit(const JoinArgs& a, int64_t row, uint32_t key, unsigned int* lds) {
+    if (LDS_COUNTS)
+        atomicAdd(&lds[key], 1u);
+    else
+        atomicAdd(&a.counts[key], 1ULL);
+    if (PAIRS) {
+        unsigned long long idx = atomicAdd(a.pair_count, 1ULL);
+        if ((long long)idx < a.pair_cap) {
+            a.pair_row[idx] = row;
+            a.pair_key[idx] = (int)key;
+        }
+    }
+}
+
+__device__ inline void probe(const JoinArgs& a, int64_t cell, uint32_t& first, uint32_t& end) {
+    first = end = 0;
+    if (cell == kEmptyKey) return;
+    uint64_t slot = mix64((uint64_t)cell) & a.mask;
+    while (true) {
+        HashEntry e = a.table[slot];
+        if (e.key == cell) {
+            first = e.first;
+            end = e.first + e.count;
+            return;
+        }
+        if (e.key == kEmptyKey) return;
+        slot = (slot + 1) & a.mask;
+    }
+}
+
+__device__ inline uint32_t next_border(const JoinArgs& a, uint32_t c, uint32_t end) {
+    while (c < end && (a.chip_meta[c] & 1u)) c++;
+    return c;
+}
+
+// Moves `cur` to this lane's next border chip whose envelope contains (x, y); every border chip
+// passed over (or reached) is one (point, border chip) test.  Loads the reached chip's ring descriptor.
+__device__ inline void advance_border(const JoinArgs& a, uint32_t& cur, uint32_t end, double x, double y,
+                                      unsigned int& tests, uint32_t& vs, uint32_t& nv) {
+    cur = next_border(a, cur, end);
+    while (cur < end) {
+        tests++;
+        if (!pip::box_excludes(a.store.geom_bbox[cur], x, y)) {
+            uint2 d = a.chip_ring[cur];
+            vs = d.x;
+            nv = d.y;
+            return;
+        }
+        cur = next_border(a, cur + 1, end);
+    }
+}
+
+template <int GRID, bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_coop(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    bool nan_seen = false;
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u); base < a.n; base += stride) {
+        int64_t i = base + lane;
+        bool act = i < a.n && (!a.valid || a.valid[i]);
+        double x = 0.0, y = 0.0;
+        int64_t cell = kEmptyKey;
+        if (act) {
+            x = a.x[i];
+            y = a.y[i];
+            if (GRID == MOSAIC_GRID_H3) {
+                bool amb;
+                cell = (int64_t)h3::h3_fast(h3::to_radians(y, a.jdk), h3::to_radians(x, a.jdk), a.res, &amb);
+                if (amb) {
+                    unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+                    if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+                    cell = kEmptyKey;
+                }
+            } else if (!bng::point_to_index(x, y, a.res, &cell)) {
+                nan_seen = true;
+                cell = kEmptyKey;
+            }
+        }
+        uint32_t first, end;
+        probe(a, cell, first, end);
+        for (uint32_t c = first; c < end; c++) {
+            uint32_t meta = a.chip_meta[c];
+            if (meta & 1u) emit_hit<LDS_COUNTS, PAIRS>(a, i, meta >> 1, lds);
+        }
+        // lane-parallel prefilter: a border chip whose envelope excludes the point cannot contain it
+        uint32_t cur = first, vs = 0, nv = 0;
+        advance_border(a, cur, end, x, y, tests, vs, nv);
+        unsigned long long pending = __ballot(cur < end);
+        while (pending) {
+            int s[4] = {0, 0, 0, 0};
+            s[0] = __ffsll(pending) - 1;
+            unsigned long long rest = pending & (pending - 1);
+            uint32_t n0 = pip::readlane_u32(nv, s[0]);
+            if (n0 == 0 || n0 - 1 > 32) {
+                // one item for the whole wave: multi-part / holed chips, or rings over 32 edges
+                uint32_t chip = pip::readlane_u32(cur, s[0]);
+                double qx = pip::readlane_f64(x, s[0]), qy = pip::readlane_f64(y, s[0]);
+                bool hit = n0 == 0 ? pip::coop_contains(a.store, chip, qx, qy)
+                                   : pip::coop_locate_in_ring(a.store, pip::readlane_u32(vs, s[0]), n0, qx, qy) ==
+                                         pip::LOC_INTERIOR;
+                if (lane == s[0]) {
+                    if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                    cur++;
+                    advance_border(a, cur, end, x, y, tests, vs, nv);
+                }
+            } else {
+                // pack 2 (<= 32 edges) or 4 (<= 16 edges) simple items into one wave pass
+                const int G = (n0 - 1 <= 16) ? 16 : 32;
+                int ng = 1;
+                while (ng < 64 / G && rest) {
+                    int c = __ffsll(rest) - 1;
+                    uint32_t nc = pip::readlane_u32(nv, c);
+                    if (nc == 0 || nc - 1 > (uint32_t)G) break;
+                    s[ng++] = c;
+                    rest &= rest - 1;
+                }
+                unsigned long long onm, crm;
+                pip::coop_packed(a.store.verts, ng, G, s[0], s[1], s[2], s[3], x, y, vs, nv, onm, crm);
+                const unsigned long long gmask = G == 32 ? 0xffffffffULL : 0xffffULL;
+                for (int k = 0; k < ng; k++) {
+                    if (lane == s[k]) {
+                        unsigned long long om = (onm >> (k * G)) & gmask, cm = (crm >> (k * G)) & gmask;
+                        if (om == 0 && (__popcll(cm) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                        cur++;
+                        advance_border(a, cur, end, x, y, tests, vs, nv);
+                    }
+                }
+            }
+            pending = __ballot(cur < end);
+        }
+    }
+    if (nan_seen) atomicOr(a.flags, 1u);
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
 
@@ -303,6 +446,7 @@ struct mosaic_ctx {
     int async = 0;
     int block = 256;
     int blocks_per_cu = 8;
+    int pip_mode = 1;  // 1: wave-cooperative contains (default), 0: one lane per point
     DevBuf amb_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
@@ -375,7 +519,7 @@ struct mosaic_chips {
     int32_t n_polygons = 0;
     uint64_t capacity = 0;
     size_t device_bytes = 0;
-    DevBuf table, meta;
+    DevBuf table, meta, ring_desc;
     GeomStoreDev store;
 };
 
@@ -487,6 +631,9 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "blocks_per_cu") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "blocks_per_cu must be in [1, 64]");
         c->blocks_per_cu = (int)v;
+    } else if (k == "pip_mode") {
+        if (v != 0 && v != 1) return fail(MOSAIC_E_ARG, "pip_mode must be 0 or 1");
+        c->pip_mode = (int)v;
     } else if (k == "timing") {
         c->timing = v ? 1 : 0;
         c->ev_used = 0;
@@ -789,19 +936,33 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
     ch->n_rings = (int64_t)gb.ring_bbox.size();
     ch->n_polygons = n_polygons;
     ch->capacity = capacity;
+    // ring descriptors: the common chip (one Polygon, one shell ring) is tested without walking
+    // the part / ring offset arrays
+    std::vector<uint2> ring_desc(meta.size(), make_uint2(0, 0));
+    for (int64_t t = 0; t < n_chips; t++) {
+        uint32_t p0 = gb.geom_part[t], p1 = gb.geom_part[t + 1];
+        if (p1 - p0 != 1) continue;
+        uint32_t r0 = gb.part_ring[p0], r1 = gb.part_ring[p0 + 1];
+        if (r1 - r0 != 1) continue;
+        uint32_t v0 = gb.ring_start[r0], v1 = gb.ring_start[r0 + 1];
+        if (v1 > v0) ring_desc[t] = make_uint2(v0, v1 - v0);
+    }
     size_t total = 0;
     int rc;
     if ((rc = ch->table.reserve(capacity * sizeof(HashEntry))) || (rc = ch->meta.reserve(meta.size() * 4)) ||
+        (rc = ch->ring_desc.reserve(ring_desc.size() * sizeof(uint2))) ||
         (rc = ch->store.upload(gb, c->stream, &total))) {
         ch->table.release();
         ch->meta.release();
+        ch->ring_desc.release();
         ch->store.release();
         delete ch;
         return rc;
     }
     HIP_TRY(hipMemcpy(ch->table.p, table.data(), capacity * sizeof(HashEntry), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
-    ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4;
+    HIP_TRY(hipMemcpy(ch->ring_desc.p, ring_desc.data(), ring_desc.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + ring_desc.size() * sizeof(uint2);
     *out = ch;
     return MOSAIC_OK;
 }
@@ -811,6 +972,7 @@ int mosaic_chip_table_destroy(mosaic_chips* ch) {
     (void)hipSetDevice(ch->device);
     ch->table.release();
     ch->meta.release();
+    ch->ring_desc.release();
     ch->store.release();
     delete ch;
     return MOSAIC_OK;
@@ -868,6 +1030,7 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.table = (const HashEntry*)ch->table.p;
     a.mask = ch->capacity - 1;
     a.chip_meta = (const uint32_t*)ch->meta.p;
+    a.chip_ring = (const uint2*)ch->ring_desc.p;
     a.store = ch->store.view();
     a.counts = dcounts;
     a.n_polygons = ch->n_polygons;
@@ -886,30 +1049,36 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     if (n > 0) {
         hipEvent_t tstop;
         if ((rc = timing_begin(c, &tstop))) return rc;
-        if (ch->grid == MOSAIC_GRID_H3) {
-            if (pairs)
-                hipLaunchKernelGGL((k_join_h3<false, true>), dim3(g), dim3(c->block), 0, c->stream, a);
-            else if (lds)
-                hipLaunchKernelGGL((k_join_h3<true, false>), dim3(g), dim3(c->block), shm, c->stream, a);
-            else
-                hipLaunchKernelGGL((k_join_h3<false, false>), dim3(g), dim3(c->block), 0, c->stream, a);
-            HIP_TRY(hipGetLastError());
-            if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
+        const bool coop = c->pip_mode == 1;
+        const bool h3g = ch->grid == MOSAIC_GRID_H3;
+#define MOSAIC_LAUNCH(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(g), dim3(c->block), SHM, c->stream, a)
+        if (coop && h3g) {
+            if (pairs) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, false, false>), 0);
+        } else if (coop) {
+            if (pairs) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_BNG, false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_BNG, true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_BNG, false, false>), 0);
+        } else if (h3g) {
+            if (pairs) MOSAIC_LAUNCH((k_join_h3<false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_h3<true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_h3<false, false>), 0);
+        } else {
+            if (pairs) MOSAIC_LAUNCH((k_join_bng<false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_bng<true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_bng<false, false>), 0);
+        }
+#undef MOSAIC_LAUNCH
+        HIP_TRY(hipGetLastError());
+        if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
+        if (h3g) {
             int ge = grid_size(c, (int64_t)qcap);
             if (pairs)
                 hipLaunchKernelGGL((k_join_h3_exact<true>), dim3(ge), dim3(c->block), 0, c->stream, a, 0);
             else
                 hipLaunchKernelGGL((k_join_h3_exact<false>), dim3(ge), dim3(c->block), 0, c->stream, a, 0);
             HIP_TRY(hipGetLastError());
-        } else {
-            if (pairs)
-                hipLaunchKernelGGL((k_join_bng<false, true>), dim3(g), dim3(c->block), 0, c->stream, a);
-            else if (lds)
-                hipLaunchKernelGGL((k_join_bng<true, false>), dim3(g), dim3(c->block), shm, c->stream, a);
-            else
-                hipLaunchKernelGGL((k_join_bng<false, false>), dim3(g), dim3(c->block), 0, c->stream, a);
-            HIP_TRY(hipGetLastError());
-            if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
         }
     }
     if (c->async && !pairs && dev_counts) return MOSAIC_OK;

@@ -1,0 +1,75 @@
+"""Multi-process (gloo, world_size 2) test of the sharded join + count all-reduce (CPU only).
+
+Each rank runs the join on its contiguous shard of the points -- here with the CPU oracle standing
+in for the GPU kernel, since this container has no GPU -- and the per-polygon counts are summed
+with one all-reduce: the result must equal the single-process join over all points.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import oracle
+    from mosaic_amd import distributed as D
+    from mosaic_amd.data import PolygonSet, quickstart_points
+    from tests.helpers import chips_to_oracle, synthetic_chips
+
+    D.init("gloo")
+    zones = PolygonSet.load("nyc_taxi_zones_35")
+    rng = np.random.default_rng(0)
+    ids = list(range(35))
+    chips = synthetic_chips(zones, ids, 9, lambda a, b, r: oracle.h3_point_to_index(a, b, r), rng, pts_per_zone=60)
+    oc = chips_to_oracle(chips)
+    x, y = quickstart_points(zones, 40_000, seed=3)
+    counts = D.sharded_join_count(lambda xs, ys: oracle.pip_join(oc, oracle.GRID_H3, 9, xs, ys, 35)[0], x, y, 35)
+    lo, hi = D.shard_bounds(len(x), rank, world)
+    elapsed = D.max_over_ranks(float(rank + 1))
+    if rank == 0:
+        full, _ = oracle.pip_join(oc, oracle.GRID_H3, 9, x, y, 35)
+        q.put((counts.numpy().tolist(), full.tolist(), elapsed, hi - lo))
+    D.finalize()
+
+
+def test_shard_bounds():
+    from mosaic_amd.distributed import shard_bounds
+
+    for n in (0, 1, 7, 100, 10**9 + 3):
+        for w in (1, 2, 3, 8):
+            spans = [shard_bounds(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_sharded_join_equals_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, want, elapsed, shard = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == want
+    assert elapsed == 2.0  # max over ranks
+    assert shard == 20_000
