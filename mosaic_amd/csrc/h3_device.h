@@ -26,12 +26,16 @@ namespace h3 {
 
 #if defined(__HIPCC__)
 #define H3_TABLE static __constant__ const
+#define H3_LUT static __device__ const
 #else
 #define H3_TABLE static const
+#define H3_LUT static const
 #endif
+#include "h3_face_lut.h"
 #include "h3_fast_tables.h"
 #include "h3_tables.h"
 #undef H3_TABLE
+#undef H3_LUT
 
 static const double kRes0UGnomonic = 0.38196601125010500003;
 
@@ -276,26 +280,25 @@ MOSAIC_HD uint64_t h3_exact(double lat, double lon, int res) {
 }
 
 // ---- fast path ----
-// Returns the cell, or sets *ambiguous and returns 0 when a decision is too close to call.
-MOSAIC_HD uint64_t h3_fast(double lat, double lon, int res, bool* ambiguous) {
-    *ambiguous = false;
-    if (res < 0 || res > 15) return 0;
-    if (!isfinite(lat) || !isfinite(lon)) return 0;
-    double slat, clat, slon, clon;
-#if defined(__HIP_DEVICE_COMPILE__)
-    sincos(lat, &slat, &clat);
-    sincos(lon, &slon, &clon);
-#else
-    slat = sin(lat);
-    clat = cos(lat);
-    slon = sin(lon);
-    clon = cos(lon);
-#endif
-    double px = clon * clat, py = slon * clat, pz = slat;
-    // closest face = largest dot product with the unit face centre
+// sin and cos of x, |x| <= pi + 1/128, to ~1 ulp: x = k/64 + r (exact), |r| <= 1/128, table
+// values sin/cos(k/64) correctly rounded, short Taylor polynomials for r (truncation < 1e-21).
+MOSAIC_HD void fast_sincos(double x, double* s, double* c) {
+    double kf = rint(x * 64.0);
+    double r = x - kf * 0.015625;  // exact (Sterbenz-like: r is a multiple of ulp(x), |r| < 2^-7)
+    int k = (int)kf + 201;
+    k = k < 0 ? 0 : (k > 402 ? 402 : k);
+    double sk = kH3SinCos64[k][0], ck = kH3SinCos64[k][1];
+    double r2 = r * r;
+    double sr = fma(r * r2, fma(r2, fma(r2, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), r);
+    double cr = fma(r2, fma(r2, fma(r2, fma(r2, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
+    *s = fma(sk, cr, ck * sr);
+    *c = fma(ck, cr, -(sk * sr));
+}
+
+// Closest face by full search (the 20 face dot products); sets *gap to best - second best.
+MOSAIC_HD int face_search(double px, double py, double pz, double* best_out, double* gap) {
     double best = -2.0, second = -2.0;
     int face = 0;
-#pragma unroll
     for (int f = 0; f < 20; f++) {
         const double* b = kH3FastBasis[f];
         double d = fma(b[0], px, fma(b[1], py, b[2] * pz));
@@ -307,34 +310,149 @@ MOSAIC_HD uint64_t h3_fast(double lat, double lon, int res, bool* ambiguous) {
             second = d;
         }
     }
-    if (best - second < 1e-12) {
-        *ambiguous = true;
-        return 0;
+    *best_out = best;
+    *gap = best - second;
+    return face;
+}
+
+// round(n / 7) for |n| < 2^27: floor((n + 3) / 7), via an unsigned division of a shifted numerator
+MOSAIC_HD int div7r(int n) {
+    const unsigned off = 7u << 25;
+    return (int)((unsigned)(n + 3) + off) / 7 - (1 << 25);
+}
+
+// digit <- axial (i - k, j - k) offset of a child from its parent's centre; 7 = invalid
+MOSAIC_HD int axial_digit(int da, int db) {
+    const unsigned char t[9] = {1, 3, 7, 5, 0, 2, 7, 4, 6};
+    unsigned ia = (unsigned)(da + 1), ib = (unsigned)(db + 1);
+    return (ia < 3 && ib < 3) ? t[ia * 3 + ib] : 7;
+}
+
+// _faceIjkToH3 in axial coordinates (a, b) = (i - k, j - k) of the res-`res` cell on `face`.
+// Same arithmetic as face_ijk_to_h3 (the axial pair is invariant under _ijkNormalize, and
+// _downAp7 / _downAp7r are linear), with the three normalisations per level removed.
+MOSAIC_HD uint64_t face_axial_to_h3(int face, int a, int b, int res) {
+    uint64_t h = 0x00001fffffffffffULL | (1ULL << 59) | ((uint64_t)res << 52);
+    for (int r = res; r >= 1; r--) {
+        int I, J, da, db;
+        if (r & 1) {  // Class III child: _upAp7, centre _downAp7 = axial (2I + J, 3J - I)
+            I = div7r(3 * a - b);
+            J = div7r(a + 2 * b);
+            da = a - (2 * I + J);
+            db = b - (3 * J - I);
+        } else {  // Class II child: _upAp7r, centre _downAp7r = axial (3I - J, I + 2J)
+            I = div7r(2 * a + b);
+            J = div7r(3 * b - a);
+            da = a - (3 * I - J);
+            db = b - (I + 2 * J);
+        }
+        int s = (15 - r) * 3;
+        h = (h & ~((uint64_t)7 << s)) | ((uint64_t)axial_digit(da, db) << s);
+        a = I;
+        b = J;
     }
-    const double* b = kH3FastBasis[face];
-    const double* ei = b + ((res & 1) ? 9 : 3);
-    const double* ep = b + ((res & 1) ? 12 : 6);
-    double s = kH3FastScale[res] / best;
+    IJK ijk = {a, b, 0};
+    ijk_normalize(ijk);
+    if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
+    int packed = kH3FaceIjkBaseCells[face][ijk.i][ijk.j][ijk.k];
+    int bc = packed >> 3;
+    int rots = packed & 7;
+    h |= (uint64_t)bc << 45;
+    if (kH3BaseCellData[bc][4]) {  // pentagon: the reference rotation sequence
+        if (leading_nonzero_digit(h, res) == 1) {
+            bool cw = kH3BaseCellData[bc][5] == face || kH3BaseCellData[bc][6] == face;
+            h = rotate_all(h, res, !cw);
+        }
+        for (int i = 0; i < rots; i++) h = rotate_pent60ccw(h, res);
+    } else if (rots) {
+        for (int i = 0; i < rots; i++) h = rotate_all(h, res, true);
+    }
+    return h;
+}
+
+// Returns the cell of (lat_deg, lon_deg) -- the cell H3 C computes from Math.toRadians of the same
+// degrees -- or sets *ambiguous and returns 0 when a decision is too close to call.
+MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambiguous) {
+    *ambiguous = false;
+    if (res < 0 || res > 15) return 0;
+    if (!isfinite(lat_deg) || !isfinite(lon_deg)) return 0;
+    // radians by one multiply: within 2 ulp of Java's toRadians (covered by the error bound)
+    const double d2r = 0.017453292519943295;
+    double lat = lat_deg * d2r, lon = lon_deg * d2r;
+    double slat, clat, slon, clon;
+    if (fabs(lon) <= 3.15 && fabs(lat) <= 3.15) {
+        fast_sincos(lat, &slat, &clat);
+        fast_sincos(lon, &slon, &clon);
+    } else {
+        slat = sin(lat);
+        clat = cos(lat);
+        slon = sin(lon);
+        clon = cos(lon);
+    }
+    double px = clon * clat, py = slon * clat, pz = slat;
+    // closest face: the lookup cell is wholly inside one face's region (gap > 3e-3), or search
+    int li = (int)floor(lat_deg + 90.0), lj = (int)floor(lon_deg + 180.0);
+    int face = (li >= 0 && li < 180 && lj >= 0 && lj < 360) ? (int)kH3FaceLut[li][lj] : 255;
+    double best;
+    if (face != 255) {
+        const double* fb = kH3FastBasis[face];
+        best = fma(fb[0], px, fma(fb[1], py, fb[2] * pz));
+    } else {
+        double gap;
+        face = face_search(px, py, pz, &best, &gap);
+        if (gap < 1e-12) {
+            *ambiguous = true;
+            return 0;
+        }
+    }
+    const double* fb = kH3FastBasis[face];
+    const double* ei = fb + ((res & 1) ? 9 : 3);
+    const double* ep = fb + ((res & 1) ? 12 : 6);
+    const double S = kH3FastScale[res];
+    double s = S / best;
     double vx = s * fma(ei[0], px, fma(ei[1], py, ei[2] * pz));
     double vy = s * fma(ep[0], px, fma(ep[1], py, ep[2] * pz));
     double a1 = fabs(vx), a2 = fabs(vy);
-    // error bound on |fast - H3| in hex units (see DESIGN.md "H3 fast path"): relative terms plus
-    // the acos(1 - sqd/2) ill-conditioning near the face centre.
+    // bound on |fast - H3| per hex2d coordinate ("H3 fast path"): relative rounding of
+    // both computations, the acos(1 - sqd/2) ill-conditioning near the face centre, and the
+    // 2-ulp radians difference.
     const double eps = 1.1102230246251565e-16;
     double rh = a1 + a2;
-    double S = kH3FastScale[res];
-    double delta = 64.0 * eps * rh + 32.0 * eps * S * S / fmax(rh, 1e-300) + 1e-300;
+    double delta = 64.0 * eps * rh + 32.0 * eps * S * S / fmax(rh, 1e-300) + 8.0 * eps * S;
     if (a1 < 8.0 * delta || a2 < 8.0 * delta) {  // axis folds and the r < EPSILON centre case
         *ambiguous = true;
         return 0;
     }
-    double x2 = a2 / 0.86602540378443864676;
-    if (hex2d_margin(a1, x2) < 8.0 * delta) {
+    // nearest lattice centre (H3's _hex2dToCoordIJK is exact hexagon rounding) and the distance
+    // from the point to that hexagon's boundary
+    const double s60 = 0.86602540378443864676;
+    double bf = rint(vy / s60);
+    double af = rint(vx + 0.5 * bf);
+    int ai = (int)af, bi = (int)bf;
+    double cx = af - 0.5 * bf, cy = bf * s60;
+    // the rounding above is per axis; fix it up to the true nearest centre among the neighbours
+    double dx = vx - cx, dy = vy - cy;
+    double best_d = dx * dx + dy * dy;
+    const int nb[6][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, -1}};
+    int ba = ai, bb = bi;
+    for (int k = 0; k < 6; k++) {
+        int qa = ai + nb[k][0], qb = bi + nb[k][1];
+        double qx = vx - ((double)qa - 0.5 * (double)qb), qy = vy - (double)qb * s60;
+        double d = qx * qx + qy * qy;
+        if (d < best_d) {
+            best_d = d;
+            ba = qa;
+            bb = qb;
+        }
+    }
+    dx = vx - ((double)ba - 0.5 * (double)bb);
+    dy = vy - (double)bb * s60;
+    double m = 0.5 - fmax(fabs(dx), fmax(fabs(0.5 * dx + s60 * dy), fabs(0.5 * dx - s60 * dy)));
+    if (m < 4.0 * delta) {
         *ambiguous = true;
         return 0;
     }
-    IJK ijk = hex2d_round(vx, vy, a1, x2);
-    return face_ijk_to_h3(face, ijk, res);
+    return face_axial_to_h3(face, ba, bb, res);
 }
 
 // java.lang.Math.toRadians (h3-java converts degrees in Java before calling H3 C)

@@ -71,6 +71,10 @@ struct JoinArgs {
     uint64_t mask;
     const uint32_t* chip_meta;  // (polygon_key << 1) | is_core, in table order
     const uint2* chip_ring;     // (first vertex, n vertices) when chip = one Polygon with one ring, else (0, 0)
+    const double2* slab_geo;    // per chip: (y0, slabs / height) of its envelope
+    const uint2* slab_idx;      // per chip: (first slab offset, slab count K); K == 0: general path
+    const uint32_t* slab_off;   // edge-record range of slab s of a chip: [slab_off[b + s], slab_off[b + s + 1])
+    const pip::Edge* edges;     // per-slab segment records
     pip::GeomStore store;       // geometry g == chip g (table order)
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
@@ -152,7 +156,7 @@ __global__ void __launch_bounds__(256) k_join_h3(JoinArgs a) {
         if (a.valid && !a.valid[i]) continue;
         double x = a.x[i], y = a.y[i];
         bool amb;
-        int64_t cell = (int64_t)h3::h3_fast(h3::to_radians(y, a.jdk), h3::to_radians(x, a.jdk), a.res, &amb);
+        int64_t cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
         if (amb) {
             unsigned long long q = atomicAdd(a.amb_count, 1ULL);
             if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
@@ -236,7 +240,7 @@ __global__ void __launch_bounds__(256) k_join_coop(JoinArgs a) {
             y = a.y[i];
             if (GRID == MOSAIC_GRID_H3) {
                 bool amb;
-                cell = (int64_t)h3::h3_fast(h3::to_radians(y, a.jdk), h3::to_radians(x, a.jdk), a.res, &amb);
+                cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
                 if (amb) {
                     unsigned long long q = atomicAdd(a.amb_count, 1ULL);
                     if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
@@ -296,6 +300,155 @@ __global__ void __launch_bounds__(256) k_join_coop(JoinArgs a) {
                         advance_border(a, cur, end, x, y, tests, vs, nv);
                     }
                 }
+            }
+            pending = __ballot(cur < end);
+        }
+    }
+    if (nan_seen) atomicOr(a.flags, 1u);
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
+// ---- slab variant (default): like k_join_coop, but a work item is (point, chip, slab of the
+// chip's envelope containing the point) and only that slab's segment records are evaluated, so
+// most items need 2-8 lanes and one wave pass serves up to 16 of them.
+static const uint32_t kGeneralItem = 0xffffffffu;
+
+// Moves `cur` to this lane's next border chip that may contain (x, y), loading its work item:
+// (e0, m) = its slab's segment records, or m = kGeneralItem for multi-ring / multi-part chips.
+// Chips rejected here (envelope, or a slab no segment crosses) are "not contained".
+__device__ inline void advance_slab(const JoinArgs& a, uint32_t& cur, uint32_t end, double x, double y,
+                                    unsigned int& tests, uint32_t& e0, uint32_t& m) {
+    cur = next_border(a, cur, end);
+    while (cur < end) {
+        tests++;
+        if (!pip::box_excludes(a.store.geom_bbox[cur], x, y)) {
+            uint2 si = a.slab_idx[cur];
+            if (si.y == 0) {
+                e0 = 0;
+                m = kGeneralItem;
+                return;
+            }
+            double2 g = a.slab_geo[cur];
+            int s = (int)floor((y - g.x) * g.y);
+            s = s < 0 ? 0 : (s >= (int)si.y ? (int)si.y - 1 : s);
+            uint32_t o0 = a.slab_off[si.x + s], o1 = a.slab_off[si.x + s + 1];
+            if (o1 > o0) {
+                e0 = o0;
+                m = o1 - o0;
+                return;
+            }
+        }
+        cur = next_border(a, cur + 1, end);
+    }
+}
+
+struct SlabItem {
+    double x, y;
+    uint32_t e0, m;
+};
+
+template <int GRID, bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_slab(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    __shared__ SlabItem items[4][16];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    bool nan_seen = false;
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = (int)(threadIdx.x >> 6) & 3;
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u); base < a.n; base += stride) {
+        int64_t i = base + lane;
+        bool act = i < a.n && (!a.valid || a.valid[i]);
+        double x = 0.0, y = 0.0;
+        int64_t cell = kEmptyKey;
+        if (act) {
+            x = a.x[i];
+            y = a.y[i];
+            if (GRID == MOSAIC_GRID_H3) {
+                bool amb;
+                cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
+                if (amb) {
+                    unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+                    if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+                    cell = kEmptyKey;
+                }
+            } else if (!bng::point_to_index(x, y, a.res, &cell)) {
+                nan_seen = true;
+                cell = kEmptyKey;
+            }
+        }
+        uint32_t first, end;
+        probe(a, cell, first, end);
+        for (uint32_t c = first; c < end; c++) {
+            uint32_t meta = a.chip_meta[c];
+            if (meta & 1u) emit_hit<LDS_COUNTS, PAIRS>(a, i, meta >> 1, lds);
+        }
+        uint32_t cur = first, e0 = 0, m = 0;
+        advance_slab(a, cur, end, x, y, tests, e0, m);
+        unsigned long long pending = __ballot(cur < end);
+        while (pending) {
+            int s0 = __ffsll(pending) - 1;
+            uint32_t m0 = pip::readlane_u32(m, s0);
+            if (m0 > 32) {
+                // one item for the whole wave: general chips, or slabs with more than 32 segments
+                double qx = pip::readlane_f64(x, s0), qy = pip::readlane_f64(y, s0);
+                bool hit;
+                if (m0 == kGeneralItem) {
+                    hit = pip::coop_contains(a.store, pip::readlane_u32(cur, s0), qx, qy);
+                } else {
+                    uint32_t q0 = pip::readlane_u32(e0, s0);
+                    unsigned long long onm = 0;
+                    int cross = 0;
+                    for (uint32_t b = 0; b < m0; b += 64) {
+                        bool on = false, cr = false;
+                        if (b + lane < m0) pip::edge_rec_flags(a.edges[q0 + b + lane], qx, qy, on, cr);
+                        onm |= __ballot(on);
+                        cross += __popcll(__ballot(cr));
+                    }
+                    hit = onm == 0 && (cross & 1);
+                }
+                if (lane == s0) {
+                    if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                    cur++;
+                    advance_slab(a, cur, end, x, y, tests, e0, m);
+                }
+            } else {
+                const int G = m0 <= 4 ? 4 : (m0 <= 8 ? 8 : (m0 <= 16 ? 16 : 32));
+                const int cap = 64 / G;
+                bool cand = cur < end && m <= (uint32_t)G;
+                unsigned long long cmask = __ballot(cand);
+                int rank = __popcll(cmask & lt_mask);
+                bool chosen = cand && rank < cap;
+                if (chosen) {
+                    SlabItem it;
+                    it.x = x;
+                    it.y = y;
+                    it.e0 = e0;
+                    it.m = m;
+                    items[wv][rank] = it;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                int ng = __popcll(cmask);
+                ng = ng < cap ? ng : cap;
+                int k = lane / G, j = lane - k * G;
+                bool on = false, cr = false;
+                if (k < ng) {
+                    SlabItem it = items[wv][k];
+                    if ((uint32_t)j < it.m) pip::edge_rec_flags(a.edges[it.e0 + j], it.x, it.y, on, cr);
+                }
+                unsigned long long onm = __ballot(on), crm = __ballot(cr);
+                if (chosen) {
+                    const unsigned long long gm = (G == 32) ? 0xffffffffULL : ((1ULL << G) - 1ULL);
+                    unsigned long long om = (onm >> (rank * G)) & gm, xm = (crm >> (rank * G)) & gm;
+                    if (om == 0 && (__popcll(xm) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                    cur++;
+                    advance_slab(a, cur, end, x, y, tests, e0, m);
+                }
+                __builtin_amdgcn_wave_barrier();
             }
             pending = __ballot(cur < end);
         }
@@ -365,7 +518,8 @@ __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
             continue;
         }
         bool amb;
-        uint64_t cell = h3::h3_fast(h3::to_radians(a.y[i], a.jdk), h3::to_radians(a.x[i], a.jdk), a.res, &amb);
+        double xd = a.x[i], yd = a.y[i];
+        uint64_t cell = h3::h3_fast(yd, xd, a.res, &amb);
         if (amb) {
             unsigned long long q = atomicAdd(a.amb_count, 1ULL);
             if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
@@ -446,7 +600,7 @@ struct mosaic_ctx {
     int async = 0;
     int block = 256;
     int blocks_per_cu = 8;
-    int pip_mode = 1;  // 1: wave-cooperative contains (default), 0: one lane per point
+    int pip_mode = 2;  // 2: slab-filtered wave-cooperative (default), 1: whole-ring cooperative, 0: lane per point
     DevBuf amb_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
@@ -519,8 +673,13 @@ struct mosaic_chips {
     int32_t n_polygons = 0;
     uint64_t capacity = 0;
     size_t device_bytes = 0;
-    DevBuf table, meta, ring_desc;
+    DevBuf table, meta, ring_desc, slab_geo, slab_idx, slab_off, edges;
+    int64_t n_edge_records = 0;
     GeomStoreDev store;
+    void release_all() {
+        for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges}) b->release();
+        store.release();
+    }
 };
 
 // pointer residency: returns true if p is device-accessible memory of the current device
@@ -626,13 +785,13 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "async") {
         c->async = v ? 1 : 0;
     } else if (k == "block") {
-        if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "block must be a multiple of 64 in [64, 1024]");
+        if (v < 64 || v > 256 || v % 64) return fail(MOSAIC_E_ARG, "block must be 64, 128, 192 or 256");
         c->block = (int)v;
     } else if (k == "blocks_per_cu") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "blocks_per_cu must be in [1, 64]");
         c->blocks_per_cu = (int)v;
     } else if (k == "pip_mode") {
-        if (v != 0 && v != 1) return fail(MOSAIC_E_ARG, "pip_mode must be 0 or 1");
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "pip_mode must be 0, 1 or 2");
         c->pip_mode = (int)v;
     } else if (k == "timing") {
         c->timing = v ? 1 : 0;
@@ -947,22 +1106,64 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
         uint32_t v0 = gb.ring_start[r0], v1 = gb.ring_start[r0 + 1];
         if (v1 > v0) ring_desc[t] = make_uint2(v0, v1 - v0);
     }
+    // slab segment lists for one-ring chips (pip_coop.h "slab-filtered edges"): ~4 segments per
+    // slab; a slab lists every segment whose y-range meets the slab widened by mu
+    std::vector<double2> slab_geo(meta.size(), make_double2(0.0, 0.0));
+    std::vector<uint2> slab_idx(meta.size(), make_uint2(0, 0));
+    std::vector<uint32_t> slab_off;
+    std::vector<pip::Edge> edges;
+    for (int64_t t = 0; t < n_chips; t++) {
+        uint2 d = ring_desc[t];
+        if (d.y < 2 || (meta[t] & 1u)) continue;
+        const pip::Vec2* v = gb.verts.data() + d.x;
+        uint32_t n = d.y;
+        double y0 = INFINITY, y1 = -INFINITY;
+        for (uint32_t k = 0; k < n; k++) {
+            y0 = std::min(y0, v[k].y);
+            y1 = std::max(y1, v[k].y);
+        }
+        uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>(64, (n - 1 + 3) / 4));
+        if (!(y1 > y0)) K = 1;
+        double hgt = y1 - y0;
+        double mu = 1e-7 * hgt + 1e-12 * std::fabs(y0) + 1e-300;
+        slab_geo[t] = make_double2(y0, K > 1 ? (double)K / hgt : 0.0);
+        slab_idx[t] = make_uint2((uint32_t)slab_off.size(), K);
+        for (uint32_t s = 0; s < K; s++) {
+            slab_off.push_back((uint32_t)edges.size());
+            double lo = s == 0 ? -INFINITY : y0 + hgt * s / K - mu;
+            double hi = s + 1 == K ? INFINITY : y0 + hgt * (s + 1) / K + mu;
+            for (uint32_t k = 1; k < n; k++) {
+                double ea = std::min(v[k].y, v[k - 1].y), eb = std::max(v[k].y, v[k - 1].y);
+                if (ea <= hi && eb >= lo) edges.push_back(pip::Edge{v[k].x, v[k].y, v[k - 1].x, v[k - 1].y});
+            }
+        }
+        slab_off.push_back((uint32_t)edges.size());
+    }
+    if (slab_off.empty()) slab_off.push_back(0);
+    if (edges.empty()) edges.push_back(pip::Edge{0, 0, 0, 0});
     size_t total = 0;
     int rc;
     if ((rc = ch->table.reserve(capacity * sizeof(HashEntry))) || (rc = ch->meta.reserve(meta.size() * 4)) ||
         (rc = ch->ring_desc.reserve(ring_desc.size() * sizeof(uint2))) ||
+        (rc = ch->slab_geo.reserve(slab_geo.size() * sizeof(double2))) ||
+        (rc = ch->slab_idx.reserve(slab_idx.size() * sizeof(uint2))) ||
+        (rc = ch->slab_off.reserve(slab_off.size() * 4)) || (rc = ch->edges.reserve(edges.size() * sizeof(pip::Edge))) ||
         (rc = ch->store.upload(gb, c->stream, &total))) {
-        ch->table.release();
-        ch->meta.release();
-        ch->ring_desc.release();
-        ch->store.release();
+        ch->release_all();
         delete ch;
         return rc;
     }
     HIP_TRY(hipMemcpy(ch->table.p, table.data(), capacity * sizeof(HashEntry), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->ring_desc.p, ring_desc.data(), ring_desc.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + ring_desc.size() * sizeof(uint2);
+    HIP_TRY(hipMemcpy(ch->slab_geo.p, slab_geo.data(), slab_geo.size() * sizeof(double2), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ch->slab_idx.p, slab_idx.data(), slab_idx.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ch->slab_off.p, slab_off.data(), slab_off.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ch->edges.p, edges.data(), edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
+    ch->n_edge_records = (int64_t)edges.size();
+    ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + ring_desc.size() * sizeof(uint2) +
+                       slab_geo.size() * sizeof(double2) + slab_idx.size() * sizeof(uint2) + slab_off.size() * 4 +
+                       edges.size() * sizeof(pip::Edge);
     *out = ch;
     return MOSAIC_OK;
 }
@@ -970,10 +1171,7 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
 int mosaic_chip_table_destroy(mosaic_chips* ch) {
     if (!ch) return MOSAIC_OK;
     (void)hipSetDevice(ch->device);
-    ch->table.release();
-    ch->meta.release();
-    ch->ring_desc.release();
-    ch->store.release();
+    ch->release_all();
     delete ch;
     return MOSAIC_OK;
 }
@@ -1031,6 +1229,10 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.mask = ch->capacity - 1;
     a.chip_meta = (const uint32_t*)ch->meta.p;
     a.chip_ring = (const uint2*)ch->ring_desc.p;
+    a.slab_geo = (const double2*)ch->slab_geo.p;
+    a.slab_idx = (const uint2*)ch->slab_idx.p;
+    a.slab_off = (const uint32_t*)ch->slab_off.p;
+    a.edges = (const pip::Edge*)ch->edges.p;
     a.store = ch->store.view();
     a.counts = dcounts;
     a.n_polygons = ch->n_polygons;
@@ -1050,9 +1252,18 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
         hipEvent_t tstop;
         if ((rc = timing_begin(c, &tstop))) return rc;
         const bool coop = c->pip_mode == 1;
+        const bool slab = c->pip_mode == 2;
         const bool h3g = ch->grid == MOSAIC_GRID_H3;
 #define MOSAIC_LAUNCH(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(g), dim3(c->block), SHM, c->stream, a)
-        if (coop && h3g) {
+        if (slab && h3g) {
+            if (pairs) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, false, false>), 0);
+        } else if (slab) {
+            if (pairs) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_BNG, false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_BNG, true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_BNG, false, false>), 0);
+        } else if (coop && h3g) {
             if (pairs) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, true, false>), shm);
             else MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, false, false>), 0);

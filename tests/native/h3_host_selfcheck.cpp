@@ -83,7 +83,7 @@ int main(int argc, char** argv) {
             bad_exact++;
         }
         bool a = false;
-        int64_t fa = (int64_t)mosaic::h3::h3_fast(la, lo, res, &a);
+        int64_t fa = (int64_t)mosaic::h3::h3_fast(lat, lon, res, &a);
         if (a) {
             amb++;
         } else if (fa != want) {

@@ -1,0 +1,97 @@
+"""CPU-only checks of the C ABI: the library loads without a GPU, exports every function that
+include/mosaic_hip.h declares, and its host-only entry points behave like the reference."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from mosaic_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_vectors.json")))
+
+
+def declared_functions():
+    text = open(os.path.join(ROOT, "include", "mosaic_hip.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mosaic_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = N.lib()
+    names = declared_functions()
+    assert len(names) >= 25
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(names) == set(N.EXPORTS)
+    assert lib.mosaic_abi_version() == 1
+
+
+def test_no_gpu_init_fails_cleanly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    rc = N.lib().mosaic_init(0, ctypes.byref(h))
+    assert rc == N.MOSAIC_E_HIP
+    assert b"device" in N.lib().mosaic_last_error()
+
+
+def test_resolution_validation_messages():
+    out = ctypes.c_int(0)
+    lib = N.lib()
+    assert lib.mosaic_resolution(N.GRID_H3, 9, ctypes.byref(out)) == 0 and out.value == 9
+    assert lib.mosaic_resolution(N.GRID_H3, 16, ctypes.byref(out)) == N.MOSAIC_E_RES
+    assert lib.mosaic_last_error() == b"H3 resolution has to be between 0 and 15; found 16"
+    assert lib.mosaic_resolution(N.GRID_BNG, 0, ctypes.byref(out)) == N.MOSAIC_E_RES
+    assert lib.mosaic_last_error() == b"BNG resolution not supported; found 0"
+    assert lib.mosaic_resolution_str(N.GRID_BNG, b"100m", ctypes.byref(out)) == 0 and out.value == 4
+    assert lib.mosaic_resolution_str(N.GRID_BNG, b"500km", ctypes.byref(out)) == 0 and out.value == -1
+    assert lib.mosaic_resolution_str(N.GRID_H3, b"11", ctypes.byref(out)) == 0 and out.value == 11
+    assert lib.mosaic_resolution_str(N.GRID_H3, b"x", ctypes.byref(out)) == N.MOSAIC_E_ARG
+
+
+@pytest.mark.parametrize("case", GOLD["bng_point_to_index"], ids=lambda c: c["fmt"])
+def test_bng_format_parse_golden(case):
+    from mosaic_amd.context import BNGIndexSystem
+
+    bng = BNGIndexSystem()
+    assert bng.format(case["id"]) == case["fmt"]
+    assert bng.parse(case["fmt"]) == case["id"]
+
+
+def test_bng_parse_reference_cases():
+    # TestBNGIndexSystem.scala:75-90
+    from mosaic_amd.context import BNGIndexSystem
+
+    bng = BNGIndexSystem()
+    for s, v in [("T", 1050), ("TQ", 105010), ("TQNW", 105012), ("TQ38827911", 10501388279110),
+                 ("TQ38827911SE", 10501388279114)]:
+        assert bng.parse(s) == v
+        assert bng.format(v) == s
+
+
+def test_bng_format_matches_oracle_random():
+    import oracle
+    from mosaic_amd.context import BNGIndexSystem
+
+    bng = BNGIndexSystem()
+    rng = np.random.default_rng(0)
+    for res in (1, 2, 3, 4, 5, 6, -1, -2, -3, -4, -5, -6):
+        e = rng.uniform(0, 7e5, 200)
+        n = rng.uniform(0, 1.2e6, 200)
+        ids, _ = oracle.bng_point_to_index_batch(e, n, res)
+        for v in ids:
+            s = bng.format(int(v))
+            assert s == oracle.bng_format(int(v))
+            # reference quirks that break the round trip (mirrored, not fixed): letterMap row 10
+            # col 4 repeats "SZ" (BNGIndexSystem.scala:96) and parse takes the first row holding a
+            # prefix (:393); a bare "SW"/"NW"/"NE"/"SE" prefix is read as a quadrant suffix (:400-401)
+            # res -1 formats to the first letter only (:115-118), which parse maps back to column 0
+            if (s.startswith("SZ") and str(int(v))[3:5] == "10") or s in ("SW", "NW", "NE", "SE") or res == -1:
+                continue
+            assert bng.parse(s) == int(v)

@@ -213,6 +213,13 @@ def test_join_counts_match_oracle(h3ctx, zones, res):
     assert total > 1000
     assert int(got.sum()) == total
     assert h3ctx.last_stats()["contains_tests"] > 0
+    # every contains strategy of the fused kernel gives the same counts
+    try:
+        for mode in (0, 1):
+            h3ctx.set_option("pip_mode", mode)
+            assert np.array_equal(h3ctx.pip_join_count(table, x, y), want), mode
+    finally:
+        h3ctx.set_option("pip_mode", 2)
 
 
 def test_join_pairs_match_oracle(h3ctx, zones):

@@ -63,7 +63,8 @@ def main():
     t_cell = timeit(cells)
     print(json.dumps({"variant": "cell_kernel", "ms": t_cell, "pts_per_s": n / t_cell * 1e3}))
     ctx.set_option("async", 1)
-    variants = [("join_all_core", True, 1), ("join_full_lane", False, 0), ("join_full_coop", False, 1)]
+    variants = [("join_all_core", True, 2), ("join_full_lane", False, 0), ("join_full_coop", False, 1),
+                ("join_full_slab", False, 2)]
     for name, core, mode in variants:
         ctx.set_option("pip_mode", mode)
         is_core = np.ones_like(chips["is_core"]) if core else chips["is_core"]
