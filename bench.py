@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_POINT = 16     # two float64 coordinates
+JOIN_KERNEL = "k_join_slab"  # the fused join kernel of the default pip_mode (2)
 
 
 def parse():
@@ -40,7 +41,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--points-per-gpu", type=float, default=1e9)
     p.add_argument("--res", type=int, default=9)
-    p.add_argument("--cpu-sample", type=float, default=2e7, help="points for the CPU baseline (0 = skip)")
+    p.add_argument("--cpu-sample", type=float, default=3e8, help="points for the CPU baseline (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--pmc", type=int, default=1, help="1: measure HBM traffic with a rocprofv3 PMC child pass")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -105,10 +106,10 @@ def pmc_traffic(args):
         for f in files:
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if "k_join_h3" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    if JOIN_KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                         vals.append(float(row["Counter_Value"]))
         if not vals:
-            return None, f"no k_join_h3 rows for {counter}"
+            return None, f"no {JOIN_KERNEL} rows for {counter}"
         res[counter] = float(np.mean(vals))
     # FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reads half of a wide streaming read
     # (MI355X_MICROARCH.md, HBM section): double it.
@@ -213,7 +214,7 @@ def main():
                    "collective": "RCCL all_reduce int64[263] per step" if world > 1 else "none"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
-                     "traffic": traffic, "kernel": "k_join_h3<true,false>",
+                     "traffic": traffic, "kernel": JOIN_KERNEL,
                      "kernel_ms": k_avg_ms, "algorithmic_bytes_per_launch": BYTES_PER_POINT * n,
                      "pmc": pmc_note},
         "cpu_baseline": cpu,
