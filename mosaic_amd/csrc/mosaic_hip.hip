@@ -24,6 +24,7 @@
 #include "h3_device.h"
 #include "pip_coop.h"
 #include "pip_device.h"
+#include "raster.h"
 
 using namespace mosaic;
 
@@ -75,6 +76,10 @@ struct JoinArgs {
     const uint2* slab_idx;      // per chip: (first slab offset, slab count K); K == 0: general path
     const uint32_t* slab_off;   // edge-record range of slab s of a chip: [slab_off[b + s], slab_off[b + s + 1])
     const pip::Edge* edges;     // per-slab segment records
+    const raster::ChipHdr* hdr;     // per chip: envelope + ray-parity raster (raster.h)
+    const raster::CellRec* cells;   // raster cells
+    const pip::Edge* rast_edges;    // raster cell segment lists
+    uint32_t lane_edges;            // cell lists up to this long are evaluated by the owning lane
     pip::GeomStore store;       // geometry g == chip g (table order)
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
@@ -457,6 +462,149 @@ __global__ void __launch_bounds__(256) k_join_slab(JoinArgs a) {
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
 
+// ---- raster variant (default, pip_mode 3): per border chip one ray-parity raster lookup
+// (raster.h); pure cells are decided by the lookup, short cell lists by the owning lane, and only
+// long lists and general (multi-ring / multi-part) chips go to the wave-cooperative evaluation.
+
+// Walks this lane's chips from `cur`: core chips are accepted, border chips decided by the raster
+// where the lane can; stops at the first chip that needs the wave (cur < end on return, with its
+// item (e0, m, par); m == kGeneralItem for general chips).
+template <bool LDS_COUNTS, bool PAIRS>
+__device__ inline void advance_raster(const JoinArgs& a, int64_t row, uint32_t& cur, uint32_t end, double x, double y,
+                                      unsigned int& tests, uint32_t& e0, uint32_t& m, uint32_t& par,
+                                      unsigned int* lds) {
+    for (; cur < end; cur++) {
+        const uint32_t meta = a.chip_meta[cur];
+        if (meta & 1u) {
+            emit_hit<LDS_COUNTS, PAIRS>(a, row, meta >> 1, lds);
+            continue;
+        }
+        tests++;
+        const raster::ChipHdr h = a.hdr[cur];
+        if (pip::box_excludes(h.box, x, y)) continue;
+        if (h.cell_base == raster::kNoRaster) {
+            e0 = 0;
+            m = kGeneralItem;
+            par = 0;
+            return;
+        }
+        const raster::CellRec rec = a.cells[raster::cell_index(h, x, y)];
+        if (rec.m > a.lane_edges) {
+            e0 = rec.word >> 1;
+            m = rec.m;
+            par = rec.word & 1u;
+            return;
+        }
+        if (raster::cell_contains(rec, a.rast_edges, x, y)) emit_hit<LDS_COUNTS, PAIRS>(a, row, meta >> 1, lds);
+    }
+}
+
+template <int GRID, bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    __shared__ SlabItem items[4][16];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    bool nan_seen = false;
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = (int)(threadIdx.x >> 6) & 3;
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u); base < a.n; base += stride) {
+        int64_t i = base + lane;
+        bool act = i < a.n && (!a.valid || a.valid[i]);
+        double x = 0.0, y = 0.0;
+        int64_t cell = kEmptyKey;
+        if (act) {
+            x = a.x[i];
+            y = a.y[i];
+            if (GRID == MOSAIC_GRID_H3) {
+                bool amb;
+                cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
+                if (amb) {
+                    unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+                    if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+                    cell = kEmptyKey;
+                }
+            } else if (!bng::point_to_index(x, y, a.res, &cell)) {
+                nan_seen = true;
+                cell = kEmptyKey;
+            }
+        }
+        uint32_t cur, end;
+        probe(a, cell, cur, end);
+        uint32_t e0 = 0, m = 0, par = 0;
+        advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
+        unsigned long long pending = __ballot(cur < end);
+        while (pending) {
+            int s0 = __ffsll(pending) - 1;
+            uint32_t m0 = pip::readlane_u32(m, s0);
+            if (m0 > 32) {
+                // one item for the whole wave: general chips, or cell lists over 32 records
+                double qx = pip::readlane_f64(x, s0), qy = pip::readlane_f64(y, s0);
+                bool hit;
+                if (m0 == kGeneralItem) {
+                    hit = pip::coop_contains(a.store, pip::readlane_u32(cur, s0), qx, qy);
+                } else {
+                    uint32_t q0 = pip::readlane_u32(e0, s0);
+                    unsigned long long onm = 0;
+                    int cross = (int)pip::readlane_u32(par, s0);
+                    for (uint32_t b = 0; b < m0; b += 64) {
+                        bool on = false, cr = false;
+                        if (b + lane < m0) pip::edge_rec_flags(a.rast_edges[q0 + b + lane], qx, qy, on, cr);
+                        onm |= __ballot(on);
+                        cross += __popcll(__ballot(cr));
+                    }
+                    hit = onm == 0 && (cross & 1);
+                }
+                if (lane == s0) {
+                    if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                    cur++;
+                    advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
+                }
+            } else {
+                const int G = m0 <= 4 ? 4 : (m0 <= 8 ? 8 : (m0 <= 16 ? 16 : 32));
+                const int cap = 64 / G;
+                bool cand = cur < end && m <= (uint32_t)G;
+                unsigned long long cmask = __ballot(cand);
+                int rank = __popcll(cmask & lt_mask);
+                bool chosen = cand && rank < cap;
+                if (chosen) {
+                    SlabItem it;
+                    it.x = x;
+                    it.y = y;
+                    it.e0 = e0;
+                    it.m = m;
+                    items[wv][rank] = it;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                int ng = __popcll(cmask);
+                ng = ng < cap ? ng : cap;
+                int k = lane / G, j = lane - k * G;
+                bool on = false, cr = false;
+                if (k < ng) {
+                    SlabItem it = items[wv][k];
+                    if ((uint32_t)j < it.m) pip::edge_rec_flags(a.rast_edges[it.e0 + j], it.x, it.y, on, cr);
+                }
+                unsigned long long onm = __ballot(on), crm = __ballot(cr);
+                if (chosen) {
+                    const unsigned long long gm = (G == 32) ? 0xffffffffULL : ((1ULL << G) - 1ULL);
+                    unsigned long long om = (onm >> (rank * G)) & gm, xm = (crm >> (rank * G)) & gm;
+                    if (om == 0 && ((__popcll(xm) + par) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                    cur++;
+                    advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            pending = __ballot(cur < end);
+        }
+    }
+    if (nan_seen) atomicOr(a.flags, 1u);
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
 // Exact H3 for the queued rows (or for every row when all_rows is set: queue overflow fallback).
 template <bool PAIRS>
 __global__ void __launch_bounds__(256) k_join_h3_exact(JoinArgs a, int all_rows) {
@@ -600,7 +748,11 @@ struct mosaic_ctx {
     int async = 0;
     int block = 256;
     int blocks_per_cu = 8;
-    int pip_mode = 2;  // 2: slab-filtered wave-cooperative (default), 1: whole-ring cooperative, 0: lane per point
+    // 3: ray-parity raster (default), 2: slab-filtered wave-cooperative, 1: whole-ring cooperative,
+    // 0: lane per point
+    int pip_mode = 3;
+    int raster = 16;      // raster cells per side of a border chip's envelope (chip tables built later)
+    int lane_edges = 8;   // raster cell lists up to this long are evaluated by the owning lane
     DevBuf amb_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
@@ -673,11 +825,14 @@ struct mosaic_chips {
     int32_t n_polygons = 0;
     uint64_t capacity = 0;
     size_t device_bytes = 0;
-    DevBuf table, meta, ring_desc, slab_geo, slab_idx, slab_off, edges;
+    DevBuf table, meta, ring_desc, slab_geo, slab_idx, slab_off, edges, hdr, cells, rast_edges;
     int64_t n_edge_records = 0;
+    int raster = 0;  // raster dims the table was built with (0: none)
+    int64_t raster_cells = 0, raster_pure = 0, raster_records = 0;
     GeomStoreDev store;
     void release_all() {
-        for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges}) b->release();
+        for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges})
+            b->release();
         store.release();
     }
 };
@@ -791,8 +946,14 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "blocks_per_cu must be in [1, 64]");
         c->blocks_per_cu = (int)v;
     } else if (k == "pip_mode") {
-        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "pip_mode must be 0, 1 or 2");
+        if (v < 0 || v > 3) return fail(MOSAIC_E_ARG, "pip_mode must be 0, 1, 2 or 3");
         c->pip_mode = (int)v;
+    } else if (k == "raster") {
+        if (v < 0 || v > 64) return fail(MOSAIC_E_ARG, "raster must be in [0, 64]");
+        c->raster = (int)v;
+    } else if (k == "lane_edges") {
+        if (v < 0 || v > 32) return fail(MOSAIC_E_ARG, "lane_edges must be in [0, 32]");
+        c->lane_edges = (int)v;
     } else if (k == "timing") {
         c->timing = v ? 1 : 0;
         c->ev_used = 0;
@@ -1141,6 +1302,32 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
     }
     if (slab_off.empty()) slab_off.push_back(0);
     if (edges.empty()) edges.push_back(pip::Edge{0, 0, 0, 0});
+    // ray-parity rasters for one-ring border chips (raster.h); other chips take the general path
+    raster::Builder rb;
+    rb.hdr.resize(meta.size());
+    for (int64_t t = 0; t < n_chips; t++) {
+        raster::ChipHdr& h = rb.hdr[t];
+        memset(&h, 0, sizeof h);
+        h.box = gb.geom_bbox[t];
+        h.cell_base = raster::kNoRaster;
+        uint2 d = ring_desc[t];
+        if (!(meta[t] & 1u) && d.y >= 2) rb.add_ring(h, gb.verts.data() + d.x, d.y, c->raster);
+        if (rb.edges.size() >= (1ull << 31)) {
+            ch->release_all();
+            delete ch;
+            return fail(MOSAIC_E_ARG, "chip table too large for the raster record index");
+        }
+    }
+    if (meta.size() > (size_t)n_chips) {
+        memset(&rb.hdr.back(), 0, sizeof(raster::ChipHdr));
+        rb.hdr.back().cell_base = raster::kNoRaster;
+    }
+    if (rb.cells.empty()) rb.cells.push_back(raster::CellRec{0, 0});
+    if (rb.edges.empty()) rb.edges.push_back(pip::Edge{0, 0, 0, 0});
+    ch->raster = c->raster;
+    ch->raster_cells = (int64_t)rb.cells.size();
+    ch->raster_pure = rb.pure_cells;
+    ch->raster_records = (int64_t)rb.edges.size();
     size_t total = 0;
     int rc;
     if ((rc = ch->table.reserve(capacity * sizeof(HashEntry))) || (rc = ch->meta.reserve(meta.size() * 4)) ||
@@ -1148,6 +1335,9 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
         (rc = ch->slab_geo.reserve(slab_geo.size() * sizeof(double2))) ||
         (rc = ch->slab_idx.reserve(slab_idx.size() * sizeof(uint2))) ||
         (rc = ch->slab_off.reserve(slab_off.size() * 4)) || (rc = ch->edges.reserve(edges.size() * sizeof(pip::Edge))) ||
+        (rc = ch->hdr.reserve(rb.hdr.size() * sizeof(raster::ChipHdr))) ||
+        (rc = ch->cells.reserve(rb.cells.size() * sizeof(raster::CellRec))) ||
+        (rc = ch->rast_edges.reserve(rb.edges.size() * sizeof(pip::Edge))) ||
         (rc = ch->store.upload(gb, c->stream, &total))) {
         ch->release_all();
         delete ch;
@@ -1160,10 +1350,14 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
     HIP_TRY(hipMemcpy(ch->slab_idx.p, slab_idx.data(), slab_idx.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->slab_off.p, slab_off.data(), slab_off.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->edges.p, edges.data(), edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ch->hdr.p, rb.hdr.data(), rb.hdr.size() * sizeof(raster::ChipHdr), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
     ch->n_edge_records = (int64_t)edges.size();
     ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + ring_desc.size() * sizeof(uint2) +
                        slab_geo.size() * sizeof(double2) + slab_idx.size() * sizeof(uint2) + slab_off.size() * 4 +
-                       edges.size() * sizeof(pip::Edge);
+                       edges.size() * sizeof(pip::Edge) + rb.hdr.size() * sizeof(raster::ChipHdr) +
+                       rb.cells.size() * sizeof(raster::CellRec) + rb.edges.size() * sizeof(pip::Edge);
     *out = ch;
     return MOSAIC_OK;
 }
@@ -1233,6 +1427,10 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.slab_idx = (const uint2*)ch->slab_idx.p;
     a.slab_off = (const uint32_t*)ch->slab_off.p;
     a.edges = (const pip::Edge*)ch->edges.p;
+    a.hdr = (const raster::ChipHdr*)ch->hdr.p;
+    a.cells = (const raster::CellRec*)ch->cells.p;
+    a.rast_edges = (const pip::Edge*)ch->rast_edges.p;
+    a.lane_edges = (uint32_t)c->lane_edges;
     a.store = ch->store.view();
     a.counts = dcounts;
     a.n_polygons = ch->n_polygons;
@@ -1252,10 +1450,19 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
         hipEvent_t tstop;
         if ((rc = timing_begin(c, &tstop))) return rc;
         const bool coop = c->pip_mode == 1;
-        const bool slab = c->pip_mode == 2;
+        const bool rast = c->pip_mode == 3 && ch->raster > 0;
+        const bool slab = c->pip_mode == 2 || (c->pip_mode == 3 && ch->raster == 0);
         const bool h3g = ch->grid == MOSAIC_GRID_H3;
 #define MOSAIC_LAUNCH(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(g), dim3(c->block), SHM, c->stream, a)
-        if (slab && h3g) {
+        if (rast && h3g) {
+            if (pairs) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, false>), 0);
+        } else if (rast) {
+            if (pairs) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, false, false>), 0);
+        } else if (slab && h3g) {
             if (pairs) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, true, false>), shm);
             else MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, false, false>), 0);

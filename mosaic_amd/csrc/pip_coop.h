@@ -156,30 +156,7 @@ __device__ inline void coop_packed(const Vec2* verts, int ng, int G, int s0, int
 // its envelope, the list of segments whose y-range meets the (slightly widened) slab, as explicit
 // 32-byte records {p1.x, p1.y, p2.x, p2.y}.  Evaluating only the point's slab list gives exactly
 // the flags of the whole ring.
-struct Edge {
-    double p1x, p1y, p2x, p2y;
-};
-
-__device__ inline void edge_rec_flags(const Edge& e, double px, double py, bool& on, bool& cross) {
-    on = false;
-    cross = false;
-    if (e.p1x < px && e.p2x < px) return;
-    if (px == e.p2x && py == e.p2y) {
-        on = true;
-    } else if (e.p1y == py && e.p2y == py) {
-        double minx = e.p1x < e.p2x ? e.p1x : e.p2x;
-        double maxx = e.p1x < e.p2x ? e.p2x : e.p1x;
-        on = (px >= minx && px <= maxx);
-    } else if (((e.p1y > py) && (e.p2y <= py)) || ((e.p2y > py) && (e.p1y <= py))) {
-        int orient = orientation_index(e.p1x, e.p1y, e.p2x, e.p2y, px, py);
-        if (orient == 0) {
-            on = true;
-        } else {
-            if (e.p2y < e.p1y) orient = -orient;
-            cross = orient == 1;
-        }
-    }
-}
+// Edge / edge_rec_flags: pip_device.h (shared with the host-side raster self-check).
 
 }  // namespace pip
 }  // namespace mosaic

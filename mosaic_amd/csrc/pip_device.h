@@ -126,6 +126,34 @@ MOSAIC_HD int orientation_index(double p1x, double p1y, double p2x, double p2y, 
     return 0;
 }
 
+// One RayCrossingCounter.countSegment step on an explicit segment record {p1, p2}
+// (p1 = ring[i], p2 = ring[i-1]): sets `on` for a point on the segment, `cross` for a counted
+// crossing of the rightward ray.
+struct Edge {
+    double p1x, p1y, p2x, p2y;
+};
+
+MOSAIC_HD void edge_rec_flags(const Edge& e, double px, double py, bool& on, bool& cross) {
+    on = false;
+    cross = false;
+    if (e.p1x < px && e.p2x < px) return;
+    if (px == e.p2x && py == e.p2y) {
+        on = true;
+    } else if (e.p1y == py && e.p2y == py) {
+        double minx = e.p1x < e.p2x ? e.p1x : e.p2x;
+        double maxx = e.p1x < e.p2x ? e.p2x : e.p1x;
+        on = (px >= minx && px <= maxx);
+    } else if (((e.p1y > py) && (e.p2y <= py)) || ((e.p2y > py) && (e.p1y <= py))) {
+        int orient = orientation_index(e.p1x, e.p1y, e.p2x, e.p2y, px, py);
+        if (orient == 0) {
+            on = true;
+        } else {
+            if (e.p2y < e.p1y) orient = -orient;
+            cross = orient == 1;
+        }
+    }
+}
+
 enum { LOC_INTERIOR = 0, LOC_BOUNDARY = 1, LOC_EXTERIOR = 2 };
 
 MOSAIC_HD bool box_excludes(const Box& b, double px, double py) {

@@ -215,11 +215,64 @@ def test_join_counts_match_oracle(h3ctx, zones, res):
     assert h3ctx.last_stats()["contains_tests"] > 0
     # every contains strategy of the fused kernel gives the same counts
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             h3ctx.set_option("pip_mode", mode)
             assert np.array_equal(h3ctx.pip_join_count(table, x, y), want), mode
     finally:
-        h3ctx.set_option("pip_mode", 2)
+        h3ctx.set_option("pip_mode", 3)
+
+
+def _chip_boundary_points(chips, rng, limit=4000):
+    """Vertices of border chips, points on their segments, and both 1-3 ulp nudges of each."""
+    from mosaic_amd.wkb import read_wkb
+
+    offs, data = chips["wkb"]
+    xs, ys = [], []
+    border = np.nonzero(chips["is_core"] == 0)[0]
+    for i in rng.choice(border, min(limit, len(border)), replace=False):
+        _, parts = read_wkb(data[offs[i]:offs[i + 1]])
+        ring = np.asarray(parts[0][0])
+        k = int(rng.integers(1, len(ring)))
+        t = rng.uniform()
+        for px, py in (ring[k], ring[k - 1] + t * (ring[k] - ring[k - 1])):
+            for d in (0, 1, -1, 3):
+                xs.append(np.nextafter(px, np.inf) if d == 1 else (np.nextafter(px, -np.inf) if d == -1 else px))
+                ys.append(py if d != 3 else np.nextafter(np.nextafter(py, np.inf), np.inf))
+    return np.array(xs), np.array(ys)
+
+
+def test_join_tessellated_chips_every_strategy(h3ctx):
+    """Real grid_tessellateexplode chips (35 NYC zones, res 9) with points on / next to the chips'
+    own vertices and segments: every contains strategy and raster size matches the oracle."""
+    from mosaic_amd.context import tessellate
+
+    zones35 = PolygonSet.load("nyc_taxi_zones_35")
+    chips = tessellate("H3", zones35, 9)
+    rng = np.random.default_rng(5)
+    x0, y0, x1, y1 = zones35.bbox()
+    bx, by = _chip_boundary_points(chips, rng)
+    x = np.concatenate([rng.uniform(x0, x1, 400_000), bx])
+    y = np.concatenate([rng.uniform(y0, y1, 400_000), by])
+    offs, data = chips["wkb"]
+    oc = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+              wkb_offsets=offs, wkb=data)
+    want, total = oracle.pip_join(oc, oracle.GRID_H3, 9, x, y, len(zones35), threads=8)
+    assert total > 10_000
+    try:
+        for raster, lane_edges in ((16, 8), (1, 8), (5, 0), (32, 32), (0, 8)):
+            h3ctx.set_option("raster", raster)
+            h3ctx.set_option("lane_edges", lane_edges)
+            table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
+                                     n_polygons=len(zones35))
+            for mode in (3, 2, 0):
+                h3ctx.set_option("pip_mode", mode)
+                got = h3ctx.pip_join_count(table, x, y)
+                assert np.array_equal(got, want), (raster, lane_edges, mode)
+            table.close()
+    finally:
+        h3ctx.set_option("raster", 16)
+        h3ctx.set_option("lane_edges", 8)
+        h3ctx.set_option("pip_mode", 3)
 
 
 def test_join_pairs_match_oracle(h3ctx, zones):

@@ -22,6 +22,8 @@ def main():
     p.add_argument("--block", type=int, default=256)
     p.add_argument("--bpc", type=int, default=8)
     p.add_argument("--clustered", action="store_true")
+    p.add_argument("--rasters", type=int, nargs="*", default=[8, 16, 32])
+    p.add_argument("--lane-edges", type=int, nargs="*", default=[0, 4, 8])
     args = p.parse_args()
     import torch
 
@@ -63,10 +65,15 @@ def main():
     t_cell = timeit(cells)
     print(json.dumps({"variant": "cell_kernel", "ms": t_cell, "pts_per_s": n / t_cell * 1e3}))
     ctx.set_option("async", 1)
-    variants = [("join_all_core", True, 2), ("join_full_lane", False, 0), ("join_full_coop", False, 1),
-                ("join_full_slab", False, 2)]
-    for name, core, mode in variants:
+    variants = [("join_all_core", True, 3, 16, 8), ("join_full_coop", False, 1, 16, 8),
+                ("join_full_slab", False, 2, 16, 8)]
+    for r in args.rasters:
+        for le in args.lane_edges:
+            variants.append((f"join_raster{r}_lane{le}", False, 3, r, le))
+    for name, core, mode, raster, lane_edges in variants:
         ctx.set_option("pip_mode", mode)
+        ctx.set_option("raster", raster)
+        ctx.set_option("lane_edges", lane_edges)
         is_core = np.ones_like(chips["is_core"]) if core else chips["is_core"]
         table = ctx.chip_table(is_core, chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
                                n_polygons=len(zones))
