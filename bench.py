@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_POINT = 16     # two float64 coordinates
-JOIN_KERNEL = "k_join_slab"  # the fused join kernel of the default pip_mode (2)
+JOIN_KERNEL = "k_join_raster"  # the fused join kernel of the default pip_mode (3)
 
 
 def parse():

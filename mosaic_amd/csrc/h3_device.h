@@ -19,6 +19,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "crmath.h"
 #include "x87.h"
 
 namespace mosaic {
@@ -168,6 +169,21 @@ MOSAIC_HD uint64_t rotate_all(uint64_t h, int res, bool ccw) {
     for (int r = 1; r <= res; r++) h = set_digit(h, r, ccw ? rotate60ccw(get_digit(h, r)) : rotate60cw(get_digit(h, r)));
     return h;
 }
+
+// rotate_all on all 15 digits at once.  A digit is the unit vector (i, j, k) = its 3 bits; a 60
+// degree rotation maps a single axis to itself plus the next axis (ccw: i->ij, j->jk, k->ki) and
+// a pair to its shared-next axis (ij->j, jk->k, ki->i): d | next(d) or d & next(d), with next the
+// cyclic bit shift.  0 and 7 (unused digits) are fixed points, so no masking by `res` is needed.
+MOSAIC_HD uint64_t rotate_all_digits(uint64_t h, bool ccw) {
+    const uint64_t kDigits = 0x1fffffffffffULL, kLow = 0x1249249249249ULL;
+    uint64_t d = h & kDigits;
+    uint64_t K = d & kLow, J = (d >> 1) & kLow, I = (d >> 2) & kLow;
+    uint64_t single = (I ^ J ^ K) & ~(I & J & K);
+    uint64_t nx = ccw ? ((K << 2) | (I << 1) | J) : ((J << 2) | (K << 1) | I);
+    uint64_t s3 = single * 7u;
+    uint64_t nd = (s3 & (d | nx)) | (~s3 & d & nx);
+    return (h & ~kDigits) | (nd & kDigits);
+}
 MOSAIC_HD uint64_t rotate_pent60ccw(uint64_t h, int res) {
     bool found = false;
     for (int r = 1; r <= res; r++) {
@@ -232,6 +248,21 @@ MOSAIC_HD uint64_t face_ijk_to_h3(int face, IJK ijk, int res) {
 }
 
 // ---- exact path: H3 C v3.7 with x86-64 double / x87 long double semantics ----
+// libm: on the GPU (and in host builds with MOSAIC_H3_CRMATH) the correctly rounded functions of
+// crmath.h; the plain host build uses the system libm, exactly as the oracle does.
+#if defined(__HIP_DEVICE_COMPILE__) || defined(MOSAIC_H3_CRMATH)
+#define H3M_SIN crm::sin_cr
+#define H3M_COS crm::cos_cr
+#define H3M_TAN crm::tan_cr
+#define H3M_ACOS crm::acos_cr
+#define H3M_ATAN2 crm::atan2_cr
+#else
+#define H3M_SIN sin
+#define H3M_COS cos
+#define H3M_TAN tan
+#define H3M_ACOS acos
+#define H3M_ATAN2 atan2
+#endif
 MOSAIC_HD double pos_angle_rads(double rads) {
     double tmp = (rads < 0.0) ? x87::add_ld(rads, H3LD_M_2PI_M, H3LD_M_2PI_E, false) : rads;
     if (rads >= H3LD_M_2PI_DUP) tmp = x87::add_ld(tmp, H3LD_M_2PI_M, H3LD_M_2PI_E, true);
@@ -243,10 +274,10 @@ MOSAIC_HD double sq(double v) { return v * v; }
 MOSAIC_HD uint64_t h3_exact(double lat, double lon, int res) {
     if (res < 0 || res > 15) return 0;
     if (!isfinite(lat) || !isfinite(lon)) return 0;
-    double r0 = cos(lat);
-    double pz = sin(lat);
-    double px = cos(lon) * r0;
-    double py = sin(lon) * r0;
+    double r0 = H3M_COS(lat);
+    double pz = H3M_SIN(lat);
+    double px = H3M_COS(lon) * r0;
+    double py = H3M_SIN(lon) * r0;
     int face = 0;
     double sqd = sq(kH3FaceCenterPoint[0][0] - px) + sq(kH3FaceCenterPoint[0][1] - py) +
                  sq(kH3FaceCenterPoint[0][2] - pz);
@@ -259,19 +290,19 @@ MOSAIC_HD uint64_t h3_exact(double lat, double lon, int res) {
         }
     }
     double vx, vy;
-    double r = acos(1 - sqd / 2);
+    double r = H3M_ACOS(1 - sqd / 2);
     if (r < H3LD_EPSILON_DUP) {
         vx = vy = 0.0;
     } else {
         double lat1 = kH3FaceCenterGeo[face][0], lon1 = kH3FaceCenterGeo[face][1];
-        double az = atan2(cos(lat) * sin(lon - lon1), cos(lat1) * sin(lat) - sin(lat1) * cos(lat) * cos(lon - lon1));
+        double az = H3M_ATAN2(H3M_COS(lat) * H3M_SIN(lon - lon1), H3M_COS(lat1) * H3M_SIN(lat) - H3M_SIN(lat1) * H3M_COS(lat) * H3M_COS(lon - lon1));
         double theta = pos_angle_rads(kH3FaceAxesAzRadsCII[face][0] - pos_angle_rads(az));
         if (res & 1) theta = pos_angle_rads(x87::add_ld(theta, H3LD_M_AP7_ROT_RADS_M, H3LD_M_AP7_ROT_RADS_E, true));
-        r = tan(r);
+        r = H3M_TAN(r);
         r /= kRes0UGnomonic;
         for (int i = 0; i < res; i++) r = x87::mul_ld(r, H3LD_M_SQRT7_M, H3LD_M_SQRT7_E);
-        vx = r * cos(theta);
-        vy = r * sin(theta);
+        vx = r * H3M_COS(theta);
+        vy = r * H3M_SIN(theta);
     }
     double a1 = fabs(vx), a2 = fabs(vy);
     double x2 = x87::div_ld(a2, H3LD_M_SIN60_M, H3LD_M_SIN60_E);
@@ -299,6 +330,7 @@ MOSAIC_HD void fast_sincos(double x, double* s, double* c) {
 MOSAIC_HD int face_search(double px, double py, double pz, double* best_out, double* gap) {
     double best = -2.0, second = -2.0;
     int face = 0;
+#pragma unroll 1
     for (int f = 0; f < 20; f++) {
         const double* b = kH3FastBasis[f];
         double d = fma(b[0], px, fma(b[1], py, b[2] * pz));
@@ -321,11 +353,12 @@ MOSAIC_HD int div7r(int n) {
     return (int)((unsigned)(n + 3) + off) / 7 - (1 << 25);
 }
 
-// digit <- axial (i - k, j - k) offset of a child from its parent's centre; 7 = invalid
+// digit <- axial (i - k, j - k) offset of a child from its parent's centre; 7 = invalid.
+// The 3x3 table {1, 3, 7, 5, 0, 2, 7, 4, 6} packed 3 bits per entry.
 MOSAIC_HD int axial_digit(int da, int db) {
-    const unsigned char t[9] = {1, 3, 7, 5, 0, 2, 7, 4, 6};
+    const unsigned kPacked = 0x69d0bd9u;
     unsigned ia = (unsigned)(da + 1), ib = (unsigned)(db + 1);
-    return (ia < 3 && ib < 3) ? t[ia * 3 + ib] : 7;
+    return (ia < 3 && ib < 3) ? (int)((kPacked >> (3u * (ia * 3u + ib))) & 7u) : 7;
 }
 
 // _faceIjkToH3 in axial coordinates (a, b) = (i - k, j - k) of the res-`res` cell on `face`.
@@ -365,7 +398,7 @@ MOSAIC_HD uint64_t face_axial_to_h3(int face, int a, int b, int res) {
         }
         for (int i = 0; i < rots; i++) h = rotate_pent60ccw(h, res);
     } else if (rots) {
-        for (int i = 0; i < rots; i++) h = rotate_all(h, res, true);
+        for (int i = 0; i < rots; i++) h = rotate_all_digits(h, true);
     }
     return h;
 }
@@ -416,39 +449,35 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
     // bound on |fast - H3| per hex2d coordinate ("H3 fast path"): relative rounding of
     // both computations, the acos(1 - sqd/2) ill-conditioning near the face centre, and the
     // 2-ulp radians difference.
+    // The bound is delta = 64 eps rh + 32 eps S^2 / rh + 8 eps S; every comparison against it is
+    // made multiplied by rh > 0 (drh = delta * rh, widened by 1e-12 for its own rounding), so no
+    // division is needed.  rh == 0 compares 0 < positive: ambiguous, as it must be.
     const double eps = 1.1102230246251565e-16;
     double rh = a1 + a2;
-    double delta = 64.0 * eps * rh + 32.0 * eps * S * S / fmax(rh, 1e-300) + 8.0 * eps * S;
-    if (a1 < 8.0 * delta || a2 < 8.0 * delta) {  // axis folds and the r < EPSILON centre case
+    double drh = (64.0 * eps * rh * rh + 32.0 * eps * S * S + 8.0 * eps * S * rh) * (1.0 + 1e-12);
+    if (a1 * rh < 8.0 * drh || a2 * rh < 8.0 * drh) {  // axis folds and the r < EPSILON centre case
         *ambiguous = true;
         return 0;
     }
     // nearest lattice centre (H3's _hex2dToCoordIJK is exact hexagon rounding) and the distance
     // from the point to that hexagon's boundary
-    const double s60 = 0.86602540378443864676;
-    double bf = rint(vy / s60);
-    double af = rint(vx + 0.5 * bf);
-    int ai = (int)af, bi = (int)bf;
-    double cx = af - 0.5 * bf, cy = bf * s60;
-    // the rounding above is per axis; fix it up to the true nearest centre among the neighbours
-    double dx = vx - cx, dy = vy - cy;
-    double best_d = dx * dx + dy * dy;
-    const int nb[6][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, -1}};
-    int ba = ai, bb = bi;
-    for (int k = 0; k < 6; k++) {
-        int qa = ai + nb[k][0], qb = bi + nb[k][1];
-        double qx = vx - ((double)qa - 0.5 * (double)qb), qy = vy - (double)qb * s60;
-        double d = qx * qx + qy * qy;
-        if (d < best_d) {
-            best_d = d;
-            ba = qa;
-            bb = qb;
-        }
-    }
-    dx = vx - ((double)ba - 0.5 * (double)bb);
-    dy = vy - (double)bb * s60;
+    // Centres are a e1 + b e2 with e1 = (1, 0), e2 = (-1/2, sin60).  Cube rounding in the 60-degree
+    // basis (e1, e1 + e2): u = a - b, w = b, t = -u - w; round all three, recompute the one that
+    // moved most.  The margin test below re-derives the distance to the chosen hexagon's boundary,
+    // so a wrong centre could only ever make the point "ambiguous", never wrong.
+    const double s60 = 0.86602540378443864676, inv_s60 = 1.1547005383792515;
+    double wq = vy * inv_s60;
+    double uq = vx - 0.5 * wq;
+    double tq = -uq - wq;
+    double ru = rint(uq), rw = rint(wq), rt = rint(tq);
+    double du = fabs(ru - uq), dw = fabs(rw - wq), dt = fabs(rt - tq);
+    if (du > dw && du > dt) ru = -rw - rt;
+    else if (dw > dt) rw = -ru - rt;
+    int ba = (int)(ru + rw), bb = (int)rw;
+    double dx = vx - ((double)ba - 0.5 * (double)bb);
+    double dy = vy - (double)bb * s60;
     double m = 0.5 - fmax(fabs(dx), fmax(fabs(0.5 * dx + s60 * dy), fabs(0.5 * dx - s60 * dy)));
-    if (m < 4.0 * delta) {
+    if (m * rh < 4.0 * drh) {
         *ambiguous = true;
         return 0;
     }

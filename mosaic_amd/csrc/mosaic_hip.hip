@@ -752,7 +752,7 @@ struct mosaic_ctx {
     // 0: lane per point
     int pip_mode = 3;
     int raster = 16;      // raster cells per side of a border chip's envelope (chip tables built later)
-    int lane_edges = 8;   // raster cell lists up to this long are evaluated by the owning lane
+    int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
     DevBuf amb_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
