@@ -31,7 +31,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_POINT = 16     # two float64 coordinates
-JOIN_KERNEL = "k_join_raster"  # the fused join kernel of the default pip_mode (3)
+# the fused join kernel of the default pip_mode (3): k_join_tiled when the chip table has an H3 tile
+# directory (tiles.h), else k_join_raster; set in main() from the table
+JOIN_KERNEL = "k_join_tiled"
 
 
 def parse():
@@ -137,6 +139,9 @@ def main():
     ctx.set_option("blocks_per_cu", args.blocks_per_cu)
     table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
                            n_polygons=len(zones))
+    global JOIN_KERNEL
+    tiles = table.tiles()
+    JOIN_KERNEL = ("k_join_stream" if tiles["raster"] else "k_join_tiled") if tiles["built"] else "k_join_raster"
     n = int(args.points_per_gpu)
     x, y = uniform_points_device(zones.bbox(), n, seed=SEED_BASE + 2 + 1000 * rank, device=dev)
     counts = torch.zeros(len(zones), dtype=torch.int64, device=dev)
@@ -210,7 +215,9 @@ def main():
         "config": {"workload": "configs[1]: 1e9 uniform points per GPU vs 263 NYC taxi zones, H3 res "
                                f"{args.res}, Quickstart chip join reduced to per-zone counts",
                    "points_per_gpu": n, "res": args.res, "chips": info["n_chips"], "border_chips": info["n_border"],
-                   "chip_cells": info["n_cells"], "parallelism": f"dp{world}",
+                   "chip_cells": info["n_cells"], "tile_directory": {k: tiles[k] for k in
+                                                                     ("built", "nx", "ny", "records", "entries")},
+                   "parallelism": f"dp{world}",
                    "collective": "RCCL all_reduce int64[263] per step" if world > 1 else "none"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,

@@ -75,7 +75,13 @@ int mosaic_init(int device, mosaic_ctx** out);
 int mosaic_destroy(mosaic_ctx* ctx);
 /* Options: "jdk" (8: Math.toRadians = deg / 180 * PI, the JDK 8 runtime of the reference's CI;
  * 9+: deg * DEGREES_TO_RADIANS), "async" (0/1), "block" (threads per block, multiple of 64),
- * "blocks_per_cu" (grid sizing), "timing" (0/1: HIP events around each fused join kernel). */
+ * "blocks_per_cu" (grid sizing), "timing" (0/1: HIP events around each join's main kernel; 2: the
+ * point-raster join's mixed-cell kernel is timed as a second entry),
+ * "pip_mode" (3 raster, 2 slab, 1 ring-cooperative, 0 lane-per-point contains strategy), "raster"
+ * (raster cells per chip side, for tables built afterwards), "lane_edges", "tiles" (0/1: H3 tile
+ * directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
+ * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
+ * side and cells per sub-block side, for tables built afterwards). */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* The hipStream_t work is enqueued on (owned by the context unless set). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
@@ -115,6 +121,15 @@ int mosaic_chip_table_create(mosaic_ctx* ctx, int grid, int res, int64_t n_chips
 int mosaic_chip_table_destroy(mosaic_chips* chips);
 /* out8: n_chips, n_cells, n_border, n_vertices, n_rings, device_bytes, hash_capacity, n_polygons */
 int mosaic_chip_table_info(const mosaic_chips* chips, int64_t* out8);
+
+/* H3 tile directory of the table (built when option "tiles" = 1, the default): out13 = built (0/1),
+ * tiles along lon, tiles along lat, tile records, window entries, tiles on the generic path, rings;
+ * point raster (option "point_raster" = 1, the default) built (0/1), sub-blocks per tile side,
+ * cells per sub-block side, pure sub-blocks, mixed sub-blocks, mixed cells. */
+int mosaic_chip_table_tiles(const mosaic_chips* chips, int64_t* out13);
+/* out4 = lon, lat of the tile grid origin and tiles per degree along lon, lat (tile i covers
+ * [x0 + i / sx, x0 + (i + 1) / sx)). */
+int mosaic_chip_table_tile_grid(const mosaic_chips* chips, double* out4);
 
 /* ---- the join ---- */
 /* counts[p] = number of (point, chip) pairs with chip polygon_key p (overwritten). */

@@ -403,13 +403,9 @@ MOSAIC_HD uint64_t face_axial_to_h3(int face, int a, int b, int res) {
     return h;
 }
 
-// Returns the cell of (lat_deg, lon_deg) -- the cell H3 C computes from Math.toRadians of the same
-// degrees -- or sets *ambiguous and returns 0 when a decision is too close to call.
-MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambiguous) {
-    *ambiguous = false;
-    if (res < 0 || res > 15) return 0;
-    if (!isfinite(lat_deg) || !isfinite(lon_deg)) return 0;
-    // radians by one multiply: within 2 ulp of Java's toRadians (covered by the error bound)
+// The unit vector of (lat_deg, lon_deg) for the fast path: radians by one multiply (within 2 ulp of
+// Java's toRadians, covered by the error bound) and the table sine / cosine.  Finite inputs only.
+MOSAIC_HD void fast_unit(double lat_deg, double lon_deg, double* px, double* py, double* pz) {
     const double d2r = 0.017453292519943295;
     double lat = lat_deg * d2r, lon = lon_deg * d2r;
     double slat, clat, slon, clon;
@@ -422,29 +418,30 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
         slon = sin(lon);
         clon = cos(lon);
     }
-    double px = clon * clat, py = slon * clat, pz = slat;
-    // closest face: the lookup cell is wholly inside one face's region (gap > 3e-3), or search
-    int li = (int)floor(lat_deg + 90.0), lj = (int)floor(lon_deg + 180.0);
-    int face = (li >= 0 && li < 180 && lj >= 0 && lj < 360) ? (int)kH3FaceLut[li][lj] : 255;
-    double best;
-    if (face != 255) {
-        const double* fb = kH3FastBasis[face];
-        best = fma(fb[0], px, fma(fb[1], py, fb[2] * pz));
-    } else {
-        double gap;
-        face = face_search(px, py, pz, &best, &gap);
-        if (gap < 1e-12) {
-            *ambiguous = true;
-            return 0;
-        }
-    }
+    *px = clon * clat;
+    *py = slon * clat;
+    *pz = slat;
+}
+
+// Face-plane coordinates (res-`res` hex units, Class III rotation included) of the unit vector p on
+// `face`, and best = FC(face) . p.
+MOSAIC_HD void fast_plane(double px, double py, double pz, int face, int res, double* vx, double* vy,
+                          double* best) {
     const double* fb = kH3FastBasis[face];
     const double* ei = fb + ((res & 1) ? 9 : 3);
     const double* ep = fb + ((res & 1) ? 12 : 6);
+    double b = fma(fb[0], px, fma(fb[1], py, fb[2] * pz));
+    double s = kH3FastScale[res] / b;
+    *vx = s * fma(ei[0], px, fma(ei[1], py, ei[2] * pz));
+    *vy = s * fma(ep[0], px, fma(ep[1], py, ep[2] * pz));
+    *best = b;
+}
+
+// The certified integer part of the fast path on a known face: the res-`res` hexagon (axial
+// (ba, bb) = (i - k, j - k)) of face-plane point (vx, vy), or false when a decision is too close to
+// call (the caller then runs h3_exact).
+MOSAIC_HD bool fast_hex(double vx, double vy, int res, int* ba_out, int* bb_out) {
     const double S = kH3FastScale[res];
-    double s = S / best;
-    double vx = s * fma(ei[0], px, fma(ei[1], py, ei[2] * pz));
-    double vy = s * fma(ep[0], px, fma(ep[1], py, ep[2] * pz));
     double a1 = fabs(vx), a2 = fabs(vy);
     // bound on |fast - H3| per hex2d coordinate ("H3 fast path"): relative rounding of
     // both computations, the acos(1 - sqd/2) ill-conditioning near the face centre, and the
@@ -455,10 +452,7 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
     const double eps = 1.1102230246251565e-16;
     double rh = a1 + a2;
     double drh = (64.0 * eps * rh * rh + 32.0 * eps * S * S + 8.0 * eps * S * rh) * (1.0 + 1e-12);
-    if (a1 * rh < 8.0 * drh || a2 * rh < 8.0 * drh) {  // axis folds and the r < EPSILON centre case
-        *ambiguous = true;
-        return 0;
-    }
+    if (a1 * rh < 8.0 * drh || a2 * rh < 8.0 * drh) return false;  // axis folds, r < EPSILON centre
     // nearest lattice centre (H3's _hex2dToCoordIJK is exact hexagon rounding) and the distance
     // from the point to that hexagon's boundary
     // Centres are a e1 + b e2 with e1 = (1, 0), e2 = (-1/2, sin60).  Cube rounding in the 60-degree
@@ -477,7 +471,40 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
     double dx = vx - ((double)ba - 0.5 * (double)bb);
     double dy = vy - (double)bb * s60;
     double m = 0.5 - fmax(fabs(dx), fmax(fabs(0.5 * dx + s60 * dy), fabs(0.5 * dx - s60 * dy)));
-    if (m * rh < 4.0 * drh) {
+    if (m * rh < 4.0 * drh) return false;
+    *ba_out = ba;
+    *bb_out = bb;
+    return true;
+}
+
+// Closest face of unit vector p: the 1-degree lookup cell is wholly inside one face's region
+// (gap > 3e-3), or the full search with a gap check.  Returns -1 when too close to call.
+MOSAIC_HD int fast_face(double lat_deg, double lon_deg, double px, double py, double pz) {
+    int li = (int)floor(lat_deg + 90.0), lj = (int)floor(lon_deg + 180.0);
+    int face = (li >= 0 && li < 180 && lj >= 0 && lj < 360) ? (int)kH3FaceLut[li][lj] : 255;
+    if (face != 255) return face;
+    double best, gap;
+    face = face_search(px, py, pz, &best, &gap);
+    return gap < 1e-12 ? -1 : face;
+}
+
+// Returns the cell of (lat_deg, lon_deg) -- the cell H3 C computes from Math.toRadians of the same
+// degrees -- or sets *ambiguous and returns 0 when a decision is too close to call.
+MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambiguous) {
+    *ambiguous = false;
+    if (res < 0 || res > 15) return 0;
+    if (!isfinite(lat_deg) || !isfinite(lon_deg)) return 0;
+    double px, py, pz;
+    fast_unit(lat_deg, lon_deg, &px, &py, &pz);
+    int face = fast_face(lat_deg, lon_deg, px, py, pz);
+    if (face < 0) {
+        *ambiguous = true;
+        return 0;
+    }
+    double vx, vy, best;
+    fast_plane(px, py, pz, face, res, &vx, &vy, &best);
+    int ba, bb;
+    if (!fast_hex(vx, vy, res, &ba, &bb)) {
         *ambiguous = true;
         return 0;
     }

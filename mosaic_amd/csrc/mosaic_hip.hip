@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mosaic_hip.h"
@@ -25,6 +26,7 @@
 #include "pip_coop.h"
 #include "pip_device.h"
 #include "raster.h"
+#include "tiles.h"
 
 using namespace mosaic;
 
@@ -81,6 +83,15 @@ struct JoinArgs {
     const pip::Edge* rast_edges;    // raster cell segment lists
     uint32_t lane_edges;            // cell lists up to this long are evaluated by the owning lane
     pip::GeomStore store;       // geometry g == chip g (table order)
+    tiles::Grid tgrid;                // tile directory (tiles.h); tile_idx == nullptr: none
+    const uint32_t* tile_idx;
+    const tiles::TileRec* tile_rec;
+    const uint32_t* tile_ent;
+    tiles::PointRaster praster;       // point raster (tiles.h); praster.sub == nullptr: none
+    int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
+    uint32_t* mixq;                   // per stream wave w: rows (- row_lo) in mixed raster cells at
+    uint32_t* mixq_count;             //   mixq[w * mixq_cap ...], mixq_count[w] of them
+    uint64_t mixq_cap;
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
     unsigned long long* amb_queue;  // rows for the exact H3 pass
@@ -499,6 +510,82 @@ __device__ inline void advance_raster(const JoinArgs& a, int64_t row, uint32_t& 
     }
 }
 
+// The chips [cur, end) of every lane's point, raster strategy: lane-local where the raster decides,
+// wave-cooperative for long segment lists and general chips.  Wave-uniform call.
+template <bool LDS_COUNTS, bool PAIRS>
+__device__ inline void raster_chips(const JoinArgs& a, int64_t i, uint32_t cur, uint32_t end, double x, double y,
+                                    unsigned int& tests, unsigned int* lds, SlabItem* items) {
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    uint32_t e0 = 0, m = 0, par = 0;
+    advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
+    unsigned long long pending = __ballot(cur < end);
+    while (pending) {
+        int s0 = __ffsll(pending) - 1;
+        uint32_t m0 = pip::readlane_u32(m, s0);
+        if (m0 > 32) {
+            // one item for the whole wave: general chips, or cell lists over 32 records
+            double qx = pip::readlane_f64(x, s0), qy = pip::readlane_f64(y, s0);
+            bool hit;
+            if (m0 == kGeneralItem) {
+                hit = pip::coop_contains(a.store, pip::readlane_u32(cur, s0), qx, qy);
+            } else {
+                uint32_t q0 = pip::readlane_u32(e0, s0);
+                unsigned long long onm = 0;
+                int cross = (int)pip::readlane_u32(par, s0);
+                for (uint32_t b = 0; b < m0; b += 64) {
+                    bool on = false, cr = false;
+                    if (b + lane < m0) pip::edge_rec_flags(a.rast_edges[q0 + b + lane], qx, qy, on, cr);
+                    onm |= __ballot(on);
+                    cross += __popcll(__ballot(cr));
+                }
+                hit = onm == 0 && (cross & 1);
+            }
+            if (lane == s0) {
+                if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                cur++;
+                advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
+            }
+        } else {
+            const int G = m0 <= 4 ? 4 : (m0 <= 8 ? 8 : (m0 <= 16 ? 16 : 32));
+            const int cap = 64 / G;
+            bool cand = cur < end && m <= (uint32_t)G;
+            unsigned long long cmask = __ballot(cand);
+            int rank = __popcll(cmask & lt_mask);
+            bool chosen = cand && rank < cap;
+            if (chosen) {
+                SlabItem it;
+                it.x = x;
+                it.y = y;
+                it.e0 = e0;
+                it.m = m;
+                items[rank] = it;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int ng = __popcll(cmask);
+            ng = ng < cap ? ng : cap;
+            int k = lane / G, j = lane - k * G;
+            bool on = false, cr = false;
+            if (k < ng) {
+                SlabItem it = items[k];
+                if ((uint32_t)j < it.m) pip::edge_rec_flags(a.rast_edges[it.e0 + j], it.x, it.y, on, cr);
+            }
+            unsigned long long onm = __ballot(on), crm = __ballot(cr);
+            if (chosen) {
+                const unsigned long long gm = (G == 32) ? 0xffffffffULL : ((1ULL << G) - 1ULL);
+                unsigned long long om = (onm >> (rank * G)) & gm, xm = (crm >> (rank * G)) & gm;
+                if (om == 0 && ((__popcll(xm) + par) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
+                cur++;
+                advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        pending = __ballot(cur < end);
+    }
+}
+
 template <int GRID, bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
     extern __shared__ unsigned int lds[];
@@ -508,7 +595,6 @@ __global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
     bool nan_seen = false;
     const int lane = (int)(threadIdx.x & 63);
     const int wv = (int)(threadIdx.x >> 6) & 3;
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u); base < a.n; base += stride) {
         int64_t i = base + lane;
@@ -533,75 +619,218 @@ __global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
         }
         uint32_t cur, end;
         probe(a, cell, cur, end);
-        uint32_t e0 = 0, m = 0, par = 0;
-        advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
-        unsigned long long pending = __ballot(cur < end);
-        while (pending) {
-            int s0 = __ffsll(pending) - 1;
-            uint32_t m0 = pip::readlane_u32(m, s0);
-            if (m0 > 32) {
-                // one item for the whole wave: general chips, or cell lists over 32 records
-                double qx = pip::readlane_f64(x, s0), qy = pip::readlane_f64(y, s0);
-                bool hit;
-                if (m0 == kGeneralItem) {
-                    hit = pip::coop_contains(a.store, pip::readlane_u32(cur, s0), qx, qy);
-                } else {
-                    uint32_t q0 = pip::readlane_u32(e0, s0);
-                    unsigned long long onm = 0;
-                    int cross = (int)pip::readlane_u32(par, s0);
-                    for (uint32_t b = 0; b < m0; b += 64) {
-                        bool on = false, cr = false;
-                        if (b + lane < m0) pip::edge_rec_flags(a.rast_edges[q0 + b + lane], qx, qy, on, cr);
-                        onm |= __ballot(on);
-                        cross += __popcll(__ballot(cr));
-                    }
-                    hit = onm == 0 && (cross & 1);
-                }
-                if (lane == s0) {
-                    if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                    cur++;
-                    advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
-                }
-            } else {
-                const int G = m0 <= 4 ? 4 : (m0 <= 8 ? 8 : (m0 <= 16 ? 16 : 32));
-                const int cap = 64 / G;
-                bool cand = cur < end && m <= (uint32_t)G;
-                unsigned long long cmask = __ballot(cand);
-                int rank = __popcll(cmask & lt_mask);
-                bool chosen = cand && rank < cap;
-                if (chosen) {
-                    SlabItem it;
-                    it.x = x;
-                    it.y = y;
-                    it.e0 = e0;
-                    it.m = m;
-                    items[wv][rank] = it;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                int ng = __popcll(cmask);
-                ng = ng < cap ? ng : cap;
-                int k = lane / G, j = lane - k * G;
-                bool on = false, cr = false;
-                if (k < ng) {
-                    SlabItem it = items[wv][k];
-                    if ((uint32_t)j < it.m) pip::edge_rec_flags(a.rast_edges[it.e0 + j], it.x, it.y, on, cr);
-                }
-                unsigned long long onm = __ballot(on), crm = __ballot(cr);
-                if (chosen) {
-                    const unsigned long long gm = (G == 32) ? 0xffffffffULL : ((1ULL << G) - 1ULL);
-                    unsigned long long om = (onm >> (rank * G)) & gm, xm = (crm >> (rank * G)) & gm;
-                    if (om == 0 && ((__popcll(xm) + par) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                    cur++;
-                    advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            pending = __ballot(cur < end);
-        }
+        raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items[wv]);
     }
     if (nan_seen) atomicOr(a.flags, 1u);
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
+// ---- tiled variant (default for H3 chip tables with a tile directory, tiles.h).  With the point
+// raster (RASTER), one or two L2-resident lookups give the whole answer of most points (no pair, or
+// one pair with a known polygon key).  Otherwise, or for raster cells marked mixed, the point's
+// tile decides whether it can join at all; points that can are compacted per wave in LDS (so the
+// lanes of a wave all carry work), then get their hexagon from the tile's face and window (no
+// index arithmetic, no hash probe) and go through the raster chip loop.
+static const int kQueue = 128;  // per-wave LDS queue (entries)
+
+struct TileQueue {
+    double x[kQueue], y[kQueue];
+    long long row[kQueue];
+    uint32_t code[kQueue];
+};
+
+// Chips of one queued point: tile path (certified hexagon -> window slot) or the generic
+// fast path + probe (kFull tiles, window misses).  Uncertified points go to the exact queue.
+__device__ inline void tiled_cell(const JoinArgs& a, int64_t i, double x, double y, uint32_t code, uint32_t& cur,
+                                  uint32_t& end) {
+    cur = end = 0;
+    int64_t cell;
+    if (code >= 2) {
+        const tiles::TileRec r = a.tile_rec[code - 2];
+        const int face = (int)(r.dims & 0xffu);
+        const int wa = (int)((r.dims >> 8) & 0xfffu), wb = (int)(r.dims >> 20);
+        double px, py, pz, vx, vy, best;
+        h3::fast_unit(y, x, &px, &py, &pz);
+        h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
+        int ba, bb;
+        if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
+            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+            return;
+        }
+        const int ra = ba - r.a0, rb = bb - r.b0;
+        if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
+            const uint32_t e = a.tile_ent[r.off + (uint32_t)(ra * wb + rb)];
+            if (e) {
+                const HashEntry he = a.table[e - 1];
+                cur = he.first;
+                end = he.first + he.count;
+            }
+            return;
+        }
+        cell = (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res);
+    } else {
+        bool amb;
+        cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
+        if (amb) {
+            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+            return;
+        }
+    }
+    probe(a, cell, cur, end);
+}
+
+template <bool LDS_COUNTS, bool PAIRS>
+__device__ inline void tiled_process(const JoinArgs& a, const TileQueue& q, int slot, bool live, unsigned int& tests,
+                                     unsigned int* lds, SlabItem* items) {
+    double x = 0.0, y = 0.0;
+    int64_t i = -1;
+    uint32_t cur = 0, end = 0;
+    if (live) {
+        x = q.x[slot];
+        y = q.y[slot];
+        i = q.row[slot];
+        tiled_cell(a, i, x, y, q.code[slot], cur, end);
+    }
+    raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items);
+}
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_tiled(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    __shared__ SlabItem items[4][16];
+    __shared__ TileQueue queues[4];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = (int)(threadIdx.x >> 6) & 3;
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    TileQueue& q = queues[wv];
+    int qn = 0;  // wave-uniform fill level
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u); base < a.n; base += stride) {
+        const int64_t i = base + lane;
+        bool need = false;
+        double x = 0.0, y = 0.0;
+        uint32_t code = tiles::kSkip;
+        if (i < a.n && (!a.valid || a.valid[i])) {
+            x = a.x[i];
+            y = a.y[i];
+            code = tiles::tile_of(a.tgrid, a.tile_idx, x, y);
+            need = code != tiles::kSkip;
+        }
+        const unsigned long long nm = __ballot(need);
+        if (need) {
+            const int s = qn + __popcll(nm & lt_mask);
+            q.x[s] = x;
+            q.y[s] = y;
+            q.row[s] = i;
+            q.code[s] = code;
+        }
+        qn += __popcll(nm);
+        if (qn >= 64) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            qn -= 64;
+            tiled_process<LDS_COUNTS, PAIRS>(a, q, qn + lane, true, tests, lds, items[wv]);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (qn > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        tiled_process<LDS_COUNTS, PAIRS>(a, q, lane, lane < qn, tests, lds, items[wv]);
+    }
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
+// ---- point-raster stream (default with a point raster, tiles.h): the whole answer of most points
+// from one or two L2 / Infinity-Cache lookups, nothing else in the loop, so the coordinate stream
+// runs near HBM speed.  Four consecutive points per lane (two 16-byte loads per coordinate,
+// VEC: both arrays 16-byte aligned), their lookups issued back to back.  Rows in mixed raster
+// cells are appended to mixq (one atomic per wave) for k_join_mixed.
+template <bool LDS_COUNTS, bool PAIRS, bool VEC>
+__global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    counts_init<LDS_COUNTS>(a, lds);
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    // every wave owns a private queue segment: no atomics, wave-uniform fill level
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    uint32_t* wq = a.mixq + gw * a.mixq_cap;
+    uint32_t wn = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    for (int64_t i0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < a.n; i0 += stride) {
+        double x[4], y[4];
+        bool live[4];
+        if (VEC && i0 + 3 < a.n) {
+            const double2 x01 = *(const double2*)(a.x + i0), x23 = *(const double2*)(a.x + i0 + 2);
+            const double2 y01 = *(const double2*)(a.y + i0), y23 = *(const double2*)(a.y + i0 + 2);
+            x[0] = x01.x;
+            x[1] = x01.y;
+            x[2] = x23.x;
+            x[3] = x23.y;
+            y[0] = y01.x;
+            y[1] = y01.y;
+            y[2] = y23.x;
+            y[3] = y23.y;
+#pragma unroll
+            for (int k = 0; k < 4; k++) live[k] = !a.valid || a.valid[i0 + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                live[k] = i0 + k < a.n && (!a.valid || a.valid[i0 + k]);
+                x[k] = live[k] ? a.x[i0 + k] : 0.0;
+                y[k] = live[k] ? a.y[i0 + k] : 0.0;
+            }
+        }
+        uint16_t rc[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) rc[k] = live[k] ? tiles::raster_code(a.praster, a.tgrid.x0, a.tgrid.y0, x[k], y[k]) : 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (rc[k] != 0 && rc[k] != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, i0 + k, (uint32_t)rc[k] - 1u, lds);
+            const unsigned long long mm = __ballot(rc[k] == tiles::kMixed);
+            if (rc[k] == tiles::kMixed) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(i0 + k - a.row_lo);
+            wn += (uint32_t)__popcll(mm);
+        }
+    }
+    if (lane == 0) a.mixq_count[gw] = wn;
+    counts_flush<LDS_COUNTS>(a, lds, 0u);
+}
+
+// Rows of mixed raster cells: wave w of this launch takes the queue segments of stream waves
+// w, w + W, ... (W = waves here); tile path (certified hexagon -> window -> chips) and the raster
+// chip loop, one queued row per lane.
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a, uint32_t stream_waves) {
+    extern __shared__ unsigned int lds[];
+    __shared__ SlabItem items[4][16];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = (int)(threadIdx.x >> 6) & 3;
+    const uint32_t W = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t sw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); sw < stream_waves; sw += W) {
+        const uint32_t cnt = a.mixq_count[sw];
+        const uint32_t* q = a.mixq + (uint64_t)sw * a.mixq_cap;
+        for (uint32_t b = 0; b < cnt; b += 64) {
+            const bool live = b + lane < cnt;
+            double x = 0.0, y = 0.0;
+            int64_t i = -1;
+            uint32_t cur = 0, end = 0;
+            if (live) {
+                i = a.row_lo + (int64_t)q[b + lane];
+                x = a.x[i];
+                y = a.y[i];
+                tiled_cell(a, i, x, y, tiles::tile_of(a.tgrid, a.tile_idx, x, y), cur, end);
+            }
+            raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items[wv]);
+        }
+    }
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
 
@@ -753,7 +982,11 @@ struct mosaic_ctx {
     int pip_mode = 3;
     int raster = 16;      // raster cells per side of a border chip's envelope (chip tables built later)
     int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
-    DevBuf amb_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
+    int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
+    int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
+    int raster_sub = 16;  // point raster: sub-blocks per tile side
+    int raster_cell = 8;  // point raster: cells per sub-block side
+    DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
     // option "timing": HIP events bracket each fused join kernel on the context stream
@@ -830,8 +1063,18 @@ struct mosaic_chips {
     int raster = 0;  // raster dims the table was built with (0: none)
     int64_t raster_cells = 0, raster_pure = 0, raster_records = 0;
     GeomStoreDev store;
+    // H3 tile directory (tiles.h); tiles_ok == false: none
+    bool tiles_ok = false;
+    tiles::Grid tgrid{};
+    DevBuf tile_idx, tile_rec, tile_ent;
+    int64_t tile_stats[6] = {0, 0, 0, 0, 0, 0};  // nx, ny, records, entries, kFull tiles, rings
+    bool raster_ok = false;                       // point raster (tiles.h)
+    tiles::PointRaster praster{};
+    DevBuf rsub, rblocks;
+    int64_t raster_stats[5] = {0, 0, 0, 0, 0};    // S, C, pure sub-blocks, mixed sub-blocks, mixed cells
     void release_all() {
-        for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges})
+        for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges,
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rblocks})
             b->release();
         store.release();
     }
@@ -919,7 +1162,7 @@ int mosaic_destroy(mosaic_ctx* c) {
     if (!c) return MOSAIC_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->amb_queue, &c->scalars, &c->stage_x, &c->stage_y, &c->stage_v, &c->stage_out, &c->stage_out2,
+    for (DevBuf* b : {&c->amb_queue, &c->mix_queue, &c->scalars, &c->stage_x, &c->stage_y, &c->stage_v, &c->stage_out, &c->stage_out2,
                       &c->stage_idx})
         b->release();
     for (size_t i = 0; i < c->ev_start.size(); i++) {
@@ -954,8 +1197,19 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "lane_edges") {
         if (v < 0 || v > 32) return fail(MOSAIC_E_ARG, "lane_edges must be in [0, 32]");
         c->lane_edges = (int)v;
+    } else if (k == "tiles") {
+        c->tiles = v ? 1 : 0;
+    } else if (k == "point_raster") {
+        c->point_raster = v ? 1 : 0;
+    } else if (k == "raster_sub") {
+        if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "raster_sub must be in [1, 64]");
+        c->raster_sub = (int)v;
+    } else if (k == "raster_cell") {
+        if (v < 1 || v > 32) return fail(MOSAIC_E_ARG, "raster_cell must be in [1, 32]");
+        c->raster_cell = (int)v;
     } else if (k == "timing") {
-        c->timing = v ? 1 : 0;
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
+        c->timing = (int)v;
         c->ev_used = 0;
     } else {
         return fail(MOSAIC_E_ARG, "unknown option " + k);
@@ -1354,6 +1608,80 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
     HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
     ch->n_edge_records = (int64_t)edges.size();
+    if (grid == MOSAIC_GRID_H3 && c->tiles && !cells.empty()) {
+        std::vector<int64_t> cell_ids(cells.size());
+        for (size_t k = 0; k < cells.size(); k++) cell_ids[k] = cells[k].first;
+        const uint64_t cmask = capacity - 1;
+        auto slot_of = [&](int64_t h) -> int64_t {
+            uint64_t slot = mix64((uint64_t)h) & cmask;
+            while (table[slot].key != kEmptyKey) {
+                if (table[slot].key == h) return (int64_t)slot;
+                slot = (slot + 1) & cmask;
+            }
+            return -1;
+        };
+        tiles::Builder tb;
+        if (tb.build(res, cell_ids, slot_of)) {
+            size_t b0 = tb.tile_idx.size() * 4, b1 = tb.recs.size() * sizeof(tiles::TileRec), b2 = tb.entries.size() * 4;
+            if ((rc = ch->tile_idx.reserve(b0)) || (rc = ch->tile_rec.reserve(b1)) || (rc = ch->tile_ent.reserve(b2))) {
+                ch->release_all();
+                delete ch;
+                return rc;
+            }
+            HIP_TRY(hipMemcpy(ch->tile_idx.p, tb.tile_idx.data(), b0, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(ch->tile_rec.p, tb.recs.data(), b1, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(ch->tile_ent.p, tb.entries.data(), b2, hipMemcpyHostToDevice));
+            ch->tiles_ok = true;
+            ch->tgrid = tb.grid;
+            ch->tile_stats[0] = tb.grid.nx;
+            ch->tile_stats[1] = tb.grid.ny;
+            ch->tile_stats[2] = (int64_t)tb.recs.size();
+            ch->tile_stats[3] = (int64_t)tb.entries.size();
+            ch->tile_stats[4] = tb.n_full;
+            ch->tile_stats[5] = tb.rings;
+            total += b0 + b1 + b2;
+            if (c->point_raster) {
+                std::vector<uint32_t> sfirst(capacity, 0), scount(capacity, 0);
+                for (uint64_t q = 0; q < capacity; q++)
+                    if (table[q].key != kEmptyKey) {
+                        sfirst[q] = table[q].first;
+                        scount[q] = table[q].count;
+                    }
+                tiles::Builder::ChipSource src;
+                src.slot_first = sfirst.data();
+                src.slot_count = scount.data();
+                src.meta = meta.data();
+                src.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(),
+                                           gb.part_ring.data(), gb.geom_part.data(), gb.geom_bbox.data()};
+                src.n_polygons = n_polygons;
+                int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+                if (tb.build_raster(src, c->raster_sub, c->raster_cell, threads)) {
+                    size_t r0 = tb.sub.size() * 4, r1 = tb.blocks.size() * 2;
+                    if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1))) {
+                        ch->release_all();
+                        delete ch;
+                        return rc;
+                    }
+                    HIP_TRY(hipMemcpy(ch->rsub.p, tb.sub.data(), r0, hipMemcpyHostToDevice));
+                    HIP_TRY(hipMemcpy(ch->rblocks.p, tb.blocks.data(), r1, hipMemcpyHostToDevice));
+                    ch->raster_ok = true;
+                    ch->praster.sub = (const uint32_t*)ch->rsub.p;
+                    ch->praster.blocks = (const uint16_t*)ch->rblocks.p;
+                    ch->praster.sx = tb.grid.sx * tb.S;
+                    ch->praster.sy = tb.grid.sy * tb.S;
+                    ch->praster.nx = tb.grid.nx * tb.S;
+                    ch->praster.ny = tb.grid.ny * tb.S;
+                    ch->praster.C = tb.C;
+                    ch->raster_stats[0] = tb.S;
+                    ch->raster_stats[1] = tb.C;
+                    ch->raster_stats[2] = tb.n_sub_pure;
+                    ch->raster_stats[3] = tb.n_sub_mixed;
+                    ch->raster_stats[4] = tb.n_cell_mixed;
+                    total += r0 + r1;
+                }
+            }
+        }
+    }
     ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + ring_desc.size() * sizeof(uint2) +
                        slab_geo.size() * sizeof(double2) + slab_idx.size() * sizeof(uint2) + slab_off.size() * 4 +
                        edges.size() * sizeof(pip::Edge) + rb.hdr.size() * sizeof(raster::ChipHdr) +
@@ -1380,6 +1708,24 @@ int mosaic_chip_table_info(const mosaic_chips* ch, int64_t* o) {
     o[5] = (int64_t)ch->device_bytes;
     o[6] = (int64_t)ch->capacity;
     o[7] = ch->n_polygons;
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_table_tiles(const mosaic_chips* ch, int64_t* o) {
+    if (!ch || !o) return fail(MOSAIC_E_ARG, "null argument");
+    o[0] = ch->tiles_ok ? 1 : 0;
+    for (int k = 0; k < 6; k++) o[k + 1] = ch->tile_stats[k];
+    o[7] = ch->raster_ok ? 1 : 0;
+    for (int k = 0; k < 5; k++) o[k + 8] = ch->raster_stats[k];
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_table_tile_grid(const mosaic_chips* ch, double* o) {
+    if (!ch || !o) return fail(MOSAIC_E_ARG, "null argument");
+    o[0] = ch->tgrid.x0;
+    o[1] = ch->tgrid.y0;
+    o[2] = ch->tgrid.sx;
+    o[3] = ch->tgrid.sy;
     return MOSAIC_OK;
 }
 
@@ -1432,6 +1778,15 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.rast_edges = (const pip::Edge*)ch->rast_edges.p;
     a.lane_edges = (uint32_t)c->lane_edges;
     a.store = ch->store.view();
+    a.tgrid = ch->tgrid;
+    a.tile_idx = (const uint32_t*)ch->tile_idx.p;
+    a.tile_rec = (const tiles::TileRec*)ch->tile_rec.p;
+    a.tile_ent = (const uint32_t*)ch->tile_ent.p;
+    a.praster = ch->praster;
+    a.row_lo = 0;
+    a.mixq = nullptr;
+    a.mixq_count = nullptr;
+    a.mixq_cap = 0;
     a.counts = dcounts;
     a.n_polygons = ch->n_polygons;
     a.amb_queue = (unsigned long long*)c->amb_queue.p;
@@ -1454,7 +1809,57 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
         const bool slab = c->pip_mode == 2 || (c->pip_mode == 3 && ch->raster == 0);
         const bool h3g = ch->grid == MOSAIC_GRID_H3;
 #define MOSAIC_LAUNCH(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(g), dim3(c->block), SHM, c->stream, a)
-        if (rast && h3g) {
+        const bool tiled = rast && h3g && c->tiles && ch->tiles_ok;
+        const bool praster = tiled && c->point_raster && ch->raster_ok;
+        if (praster) {
+            // rows in chunks of < 2^32 (uint32 queue entries); one chunk up to 4.29e9 rows.  Each
+            // stream wave gets a queue segment as long as its share of the chunk.
+            const int64_t chunk = ((int64_t)1 << 32) - 1;
+            const int64_t rows = std::min<int64_t>(n, chunk);
+            const int gs = grid_size(c, (rows + 3) / 4);
+            const uint32_t waves = (uint32_t)gs * (uint32_t)(c->block / 64);
+            const uint64_t per_iter = (uint64_t)gs * c->block * 4;
+            const uint64_t cap = ((uint64_t)rows + per_iter - 1) / per_iter * 256;
+            if ((rc = c->mix_queue.reserve((size_t)(cap * waves * 4 + waves * 4)))) return rc;
+            a.mixq = (uint32_t*)c->mix_queue.p;
+            a.mixq_cap = cap;
+            a.mixq_count = (uint32_t*)((char*)c->mix_queue.p + cap * waves * 4);
+            const bool vec = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
+            for (int64_t lo = 0; lo < n; lo += chunk) {
+                JoinArgs ac = a;
+                ac.row_lo = lo;
+                ac.n = std::min<int64_t>(n, lo + chunk);
+#define MOSAIC_STREAM(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(gs), dim3(c->block), SHM, c->stream, ac)
+                if (vec) {
+                    if (pairs) MOSAIC_STREAM((k_join_stream<false, true, true>), 0);
+                    else if (lds) MOSAIC_STREAM((k_join_stream<true, false, true>), shm);
+                    else MOSAIC_STREAM((k_join_stream<false, false, true>), 0);
+                } else {
+                    if (pairs) MOSAIC_STREAM((k_join_stream<false, true, false>), 0);
+                    else if (lds) MOSAIC_STREAM((k_join_stream<true, false, false>), shm);
+                    else MOSAIC_STREAM((k_join_stream<false, false, false>), 0);
+                }
+#undef MOSAIC_STREAM
+                HIP_TRY(hipGetLastError());
+                if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
+                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>(gs, (int64_t)c->n_cu * c->blocks_per_cu));
+#define MOSAIC_MIXED(KERNEL, SHM) \
+    hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac, waves)
+                hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
+                if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
+                if (pairs) MOSAIC_MIXED((k_join_mixed<false, true>), 0);
+                else if (lds) MOSAIC_MIXED((k_join_mixed<true, false>), shm);
+                else MOSAIC_MIXED((k_join_mixed<false, false>), 0);
+#undef MOSAIC_MIXED
+                HIP_TRY(hipGetLastError());
+                if (mstop) HIP_TRY(hipEventRecord(mstop, c->stream));
+            }
+            tstop = nullptr;  // recorded after the first stream launch
+        } else if (tiled) {
+            if (pairs) MOSAIC_LAUNCH((k_join_tiled<false, true>), 0);
+            else if (lds) MOSAIC_LAUNCH((k_join_tiled<true, false>), shm);
+            else MOSAIC_LAUNCH((k_join_tiled<false, false>), 0);
+        } else if (rast && h3g) {
             if (pairs) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, true, false>), shm);
             else MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, false>), 0);

@@ -1,0 +1,373 @@
+// Tile directory: the point side of the H3 chip join without the per-point H3 index arithmetic
+// or the hash probe.
+//
+// The chip join needs, per point, the chips whose index_id equals the point's H3 cell
+// (grid_pointascellid -> H3IndexSystem.pointToIndex, core/index/H3IndexSystem.scala:140-142, then
+// the Quickstart equi-join, notebooks/examples/python/QuickstartNotebook.py:205-219).  The fast
+// path (h3_device.h) certifies the hexagon (face, axial a, b) of a point; turning that into a
+// 64-bit index (15 digit levels) and probing the chip hash is most of its integer work.  Here the
+// lon/lat region around the chip cells is cut into tiles of ~4 hexagons a side.  Per tile the
+// host proves (below) that every point of the tile lies on one icosahedron face, and records the
+// window of axial coordinates its points can round to, with the chip-table slot of every hexagon
+// in the window.  A point then costs: tile lookup, projection, rounding, one window read.
+//
+// Why it is exact (every claim is checked on the host while building; any doubt marks the tile
+// kFull, which runs the unchanged h3_fast + probe path):
+//  * face: the 9 samples (corners, edge midpoints, centre) of the tile all have the same closest
+//    face with a dot-product gap >= 1e-4 to every other face.  The gap is a near-linear function
+//    of position; over a tile of <= 0.25 degrees it deviates from linear by < 3e-6, so the whole
+//    tile is inside the face's region by far more than the fast path's error.
+//  * window: a point's hexagon centre differs from its fractional axial coordinates by < 2/3 in
+//    each axial coordinate; the tile's image is within 0.05 hex units (checked at the edge
+//    midpoints and the centre) of the bilinear patch through its corner images, so the window
+//    [floor(min) - 1, floor(max) + 1] per axis contains every hexagon a tile point can have, under
+//    H3 or the fast path.  A certified point outside the window (impossible by this argument)
+//    still takes the index + probe path.
+//  * skip: a tile whose window holds no chip cell is kSkip: none of its points can join.
+//  * outside the grid: the grid is the region of the chip cells (from a rough cell -> lon/lat
+//    inverse) widened by k tile rings, and every chip cell must be found in the window of a tile
+//    at least k rings inside the grid, where k rings span >= 1.5x the 2.5 hex units from a tile's
+//    image to any point of a cell in its window (measured hex-units-per-degree scales).  So every
+//    point of every chip cell lies inside the grid and a finite point outside joins nothing.
+//    Non-finite points take the full path (H3 returns 0 for them, which a chip could carry).
+//
+// HBM layout (per chip table): tile_idx u32[nx * ny] (kSkip, kFull or record + 2), TileRec 16 B
+// per non-empty tile, u32 window entries (chip-hash slot + 1, 0 = no chips), row-major (a, b).
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#include "h3_device.h"
+#include "raster.h"
+
+#include <algorithm>
+#include <functional>
+#include <vector>
+
+namespace mosaic {
+namespace tiles {
+
+static const uint32_t kSkip = 0;  // no point of the tile can join
+static const uint32_t kFull = 1;  // run the generic fast path + probe
+
+// point raster codes (uint16): 0 = no pair, k + 1 = one pair with polygon key k, kMixed = the
+// points of the cell take the tile path; sub-block entries (uint32) carry kRasterBlock | block.
+static const uint16_t kMixed = 0xffffu;
+static const uint32_t kRasterBlock = 0x80000000u;
+
+struct PointRaster {
+    const uint32_t* sub;     // (nx * S) x (ny * S) sub-block entries; nullptr: no raster
+    const uint16_t* blocks;  // C x C codes per block
+    double sx, sy;           // sub-blocks per degree
+    int32_t nx, ny, C;
+};
+
+// Raster code of (x, y): grid origin (x0, y0) shared with the tile grid.
+MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, double x, double y) {
+    const double gx = (x - x0) * r.sx, gy = (y - y0) * r.sy;
+    if (!(gx >= 0.0 && gx < (double)r.nx && gy >= 0.0 && gy < (double)r.ny))
+        return (isfinite(x) && isfinite(y)) ? (uint16_t)0 : kMixed;
+    const int ix = (int)gx, iy = (int)gy;
+    const uint32_t e = r.sub[(int64_t)iy * r.nx + ix];
+    if (!(e & kRasterBlock)) return (uint16_t)e;
+    int cx = (int)((gx - (double)ix) * (double)r.C), cy = (int)((gy - (double)iy) * (double)r.C);
+    cx = cx < r.C - 1 ? cx : r.C - 1;
+    cy = cy < r.C - 1 ? cy : r.C - 1;
+    return r.blocks[(size_t)(e & ~kRasterBlock) * (size_t)(r.C * r.C) + (size_t)(cy * r.C + cx)];
+}
+
+struct TileRec {
+    int32_t a0, b0;  // window origin (axial)
+    uint32_t off;    // first window entry
+    uint32_t dims;   // face | wa << 8 | wb << 20
+};
+static_assert(sizeof(TileRec) == 16, "TileRec is one 16-byte record");
+
+struct Grid {
+    double x0, y0;  // lon, lat of the grid origin
+    double sx, sy;  // tiles per degree
+    int32_t nx, ny;
+};
+
+// Tile code of (x = lon, y = lat): kSkip outside the grid (finite points), kFull for non-finite.
+MOSAIC_HD uint32_t tile_of(const Grid& g, const uint32_t* idx, double x, double y) {
+    double fx = (x - g.x0) * g.sx, fy = (y - g.y0) * g.sy;
+    if (!(fx >= 0.0 && fx < (double)g.nx && fy >= 0.0 && fy < (double)g.ny))
+        return (isfinite(x) && isfinite(y)) ? kSkip : kFull;
+    return idx[(int64_t)(int)fy * g.nx + (int)fx];
+}
+
+// ---- host-side construction -------------------------------------------------------------------
+// The builder reads the H3 tables as host constants, so its code is compiled by the host compiler
+// only (tiles_build.cpp, g++): hipcc's host pass sees __constant__ tables as uninitialised
+// shadows.  mosaic_hip.hip calls Builder::build across that boundary.
+#if !defined(__HIPCC__)
+// Approximate lon/lat centre of an H3 cell (on its base cell's home face) and its hex-unit scale;
+// used only to place the grid, whose coverage is then verified by the forward path.
+inline bool cell_center(uint64_t h, int res, double* lon, double* lat) {
+    if (((h >> 59) & 15) != 1 || (int)((h >> 52) & 15) != res) return false;
+    int bc = (int)((h >> 45) & 127);
+    if (bc >= 122) return false;
+    const int* bd = h3::kH3BaseCellData[bc];
+    if (bd[4] && h3::leading_nonzero_digit(h, res) == 5) h = h3::rotate_all(h, res, false);
+    int face = bd[0];
+    int a = bd[1] - bd[3], b = bd[2] - bd[3];
+    for (int r = 1; r <= res; r++) {
+        int na, nb;
+        if (r & 1) {
+            na = 2 * a + b;
+            nb = 3 * b - a;
+        } else {
+            na = 3 * a - b;
+            nb = a + 2 * b;
+        }
+        int d = h3::get_digit(h, r);
+        if (d == 7) return false;
+        a = na + (((d >> 2) & 1) - (d & 1));
+        b = nb + (((d >> 1) & 1) - (d & 1));
+    }
+    const double s60 = 0.86602540378443864676;
+    double vx = (double)a - 0.5 * (double)b, vy = (double)b * s60;
+    const double* fb = h3::kH3FastBasis[face];
+    const double* ei = fb + ((res & 1) ? 9 : 3);
+    const double* ep = fb + ((res & 1) ? 12 : 6);
+    double t = vx / h3::kH3FastScale[res], u = vy / h3::kH3FastScale[res];
+    double px = fb[0] + t * ei[0] + u * ep[0], py = fb[1] + t * ei[1] + u * ep[1], pz = fb[2] + t * ei[2] + u * ep[2];
+    double nrm = sqrt(px * px + py * py + pz * pz);
+    *lat = asin(pz / nrm) * 57.29577951308232;
+    *lon = atan2(py, px) * 57.29577951308232;
+    return isfinite(*lat) && isfinite(*lon);
+}
+
+#endif  // !__HIPCC__
+
+struct Builder {
+    Grid grid{};
+    std::vector<uint32_t> tile_idx;
+    std::vector<TileRec> recs;
+    std::vector<uint32_t> entries;
+    int rings = 0;
+    int64_t n_full = 0, n_skip = 0;
+    const char* why = nullptr;  // reason the directory was not built
+    int res_ = 0;
+    std::vector<double> rec_dev;  // per record: patch deviation of the tile (axial units)
+
+    // ---- point raster (second stage, optional): per sub-block of a tile (S x S per tile) a
+    // uint32 entry: kRasterBlock | block, or a code; per block C x C uint16 codes.  Codes: 0 = the
+    // point joins nothing, k + 1 = exactly one pair with polygon key k, kMixed = run the tile path.
+    int S = 0, C = 0;
+    std::vector<uint32_t> sub;
+    std::vector<uint16_t> blocks;
+    int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0;
+    // Chip access for the raster classification (host memory)
+    struct ChipSource {
+        const uint32_t* slot_first;  // per hash slot: first chip, chip count (0 for empty slots)
+        const uint32_t* slot_count;
+        const uint32_t* meta;        // (polygon_key << 1) | is_core
+        pip::GeomStore store;        // chip geometry (border chips), host pointers
+        int32_t n_polygons;
+    };
+    bool build_raster(const ChipSource& src, int S_, int C_, int threads);
+
+    // cells: distinct chip cells; slot_of(cell) -> chip hash slot or -1.  Defined for the host
+    // compiler only (tiles_build.cpp); false (with `why`) when the directory is not built.
+    bool build(int res, const std::vector<int64_t>& cells, const std::function<int64_t(int64_t)>& slot_of);
+
+#if !defined(__HIPCC__)
+    // Sample geometry of one tile: face (or -1) and axial coordinates of the 3 x 3 samples.
+    struct Samples {
+        int face;
+        double a[9], b[9];
+    };
+    static bool sample(double lon0, double lat0, double tw, double th, int res, Samples* s) {
+        s->face = -1;
+        for (int k = 0; k < 9; k++) {
+            double lon = lon0 + 0.5 * (k % 3) * tw, lat = lat0 + 0.5 * (k / 3) * th;
+            double px, py, pz, best, gap;
+            h3::fast_unit(lat, lon, &px, &py, &pz);
+            int f = h3::face_search(px, py, pz, &best, &gap);
+            if (gap < 1e-4 || (s->face >= 0 && f != s->face)) return false;
+            s->face = f;
+            double vx, vy, b;
+            h3::fast_plane(px, py, pz, f, res, &vx, &vy, &b);
+            const double inv_s60 = 1.1547005383792515;
+            s->b[k] = vy * inv_s60;
+            s->a[k] = vx + 0.5 * s->b[k];
+        }
+        return true;
+    }
+
+    bool build_impl(int res, const std::vector<int64_t>& cells, const std::function<int64_t(int64_t)>& slot_of) {
+        why = nullptr;
+        if (cells.empty()) return fail("no chip cells");
+        if (res < 0 || res > 15) return fail("resolution");
+        // region of the chip cells: centres widened by ~3 hex units (measured at the centre)
+        double x0 = INFINITY, y0 = INFINITY, x1 = -INFINITY, y1 = -INFINITY;
+        std::vector<double> cx(cells.size()), cy(cells.size());
+        for (size_t k = 0; k < cells.size(); k++) {
+            if (!cell_center((uint64_t)cells[k], res, &cx[k], &cy[k])) return fail("cell outside the supported set");
+            x0 = std::min(x0, cx[k]);
+            x1 = std::max(x1, cx[k]);
+            y0 = std::min(y0, cy[k]);
+            y1 = std::max(y1, cy[k]);
+        }
+        // hex units per degree at the region centre (lon and lat directions)
+        double mx = 0.5 * (x0 + x1), my = 0.5 * (y0 + y1);
+        Samples c0;
+        double dd = 1e-4;
+        if (!sample(mx - dd, my - dd, 2 * dd, 2 * dd, res, &c0)) return fail("region centre near a face edge");
+        double slon = axis_scale(c0, 3, 5, 2 * dd), slat = axis_scale(c0, 1, 7, 2 * dd);
+        double sig0 = sigma_min(c0, 2 * dd, 2 * dd);
+        if (!(slon > 0 && slat > 0 && sig0 > 0)) return fail("degenerate scale");
+        // pad by 3 hex units (cells are ~0.6 hex units around their centres)
+        x0 -= 6.0 / slon;
+        x1 += 6.0 / slon;
+        y0 -= 6.0 / slat;
+        y1 += 6.0 / slat;
+        if (y0 < -85.0 || y1 > 85.0) return fail("polar region");
+        if (x1 - x0 > 90.0 || y1 - y0 > 60.0) return fail("region too large");
+        double tw = std::min(0.25, 4.0 / slon), th = std::min(0.25, 4.0 / slat);
+        // tile budget: at most 2^24 tiles and 2^26 window entries
+        double ntiles = ((x1 - x0) / tw + 4) * ((y1 - y0) / th + 4);
+        if (ntiles > (double)(1 << 24)) return fail("too many tiles");
+        // rings: 2x the cell reach (2.5 hex units, x1.5) at the centre's scale; verified below
+        int k = std::max(2, (int)ceil(2.0 * 3.75 / (std::min(tw, th) * sig0)));
+        if (k > 64) return fail("ring count");
+        rings = k;
+        int nx = (int)ceil((x1 - x0) / tw) + 2 * k, ny = (int)ceil((y1 - y0) / th) + 2 * k;
+        grid.x0 = x0 - k * tw;
+        grid.y0 = y0 - k * th;
+        grid.sx = 1.0 / tw;
+        grid.sy = 1.0 / th;
+        grid.nx = nx;
+        grid.ny = ny;
+        tile_idx.assign((size_t)nx * ny, kSkip);
+        recs.clear();
+        entries.clear();
+        rec_dev.clear();
+        res_ = res;
+        std::vector<uint8_t> found(cells.size(), 0);
+        std::vector<int64_t> slot_cell;  // slot -> position in cells (for the found flags)
+        double smin = INFINITY;
+        n_full = n_skip = 0;
+        std::vector<uint32_t> win;
+        for (int j = 0; j < ny; j++) {
+            for (int i = 0; i < nx; i++) {
+                // tile bounds exactly as the kernel's index computes them (to rounding)
+                double lon0 = grid.x0 + i * tw, lat0 = grid.y0 + j * th;
+                Samples s;
+                uint32_t code = kFull;
+                double dev = 1.0;
+                if (sample(lon0, lat0, tw, th, res, &s) && (dev = patch_dev(s)) <= 0.05) {
+                    smin = std::min(smin, sigma_min(s, tw, th));
+                    double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+                    for (int q = 0; q < 9; q++) {
+                        amin = std::min(amin, s.a[q]);
+                        amax = std::max(amax, s.a[q]);
+                        bmin = std::min(bmin, s.b[q]);
+                        bmax = std::max(bmax, s.b[q]);
+                    }
+                    int a0 = (int)floor(amin) - 1, a1 = (int)floor(amax) + 1;
+                    int b0 = (int)floor(bmin) - 1, b1 = (int)floor(bmax) + 1;
+                    int wa = a1 - a0 + 1, wb = b1 - b0 + 1;
+                    if (wa <= 255 && wb <= 4095 && wa * wb <= 4096) {
+                        win.assign((size_t)wa * wb, 0);
+                        bool any = false;
+                        bool inner = i >= k && j >= k && i < nx - k && j < ny - k;
+                        for (int ra = 0; ra < wa; ra++) {
+                            for (int rb = 0; rb < wb; rb++) {
+                                int64_t h = (int64_t)h3::face_axial_to_h3(s.face, a0 + ra, b0 + rb, res);
+                                int64_t slot = slot_of(h);
+                                if (slot < 0) continue;
+                                win[(size_t)ra * wb + rb] = (uint32_t)slot + 1;
+                                any = true;
+                                if (inner) mark_found(slot, cells, slot_of, found, slot_cell);
+                            }
+                        }
+                        if (!any) {
+                            code = kSkip;
+                        } else {
+                            if (entries.size() + win.size() >= ((size_t)1 << 26)) return fail("window entries");
+                            TileRec r;
+                            r.a0 = a0;
+                            r.b0 = b0;
+                            r.off = (uint32_t)entries.size();
+                            r.dims = (uint32_t)s.face | ((uint32_t)wa << 8) | ((uint32_t)wb << 20);
+                            entries.insert(entries.end(), win.begin(), win.end());
+                            code = (uint32_t)recs.size() + 2;
+                            recs.push_back(r);
+                            rec_dev.push_back(dev);
+                        }
+                    }
+                }
+                if (code == kFull) n_full++;
+                if (code == kSkip) n_skip++;
+                tile_idx[(size_t)j * nx + i] = code;
+            }
+        }
+        // coverage: every chip cell found in an inner tile, and k rings span the cell reach
+        for (size_t q = 0; q < cells.size(); q++)
+            if (!found[q]) return fail("a chip cell was not found inside the grid");
+        if (!(k * std::min(tw, th) * smin >= 3.75)) return fail("ring margin below the cell reach");
+        if (recs.empty()) recs.push_back(TileRec{0, 0, 0, 0});
+        if (entries.empty()) entries.push_back(0);
+        return true;
+    }
+
+  private:
+    // Euclidean hex units per degree along one sample pair (k0 -> k1 spans `span` degrees)
+    static double axis_scale(const Samples& s, int k0, int k1, double span) {
+        const double s60 = 0.86602540378443864676;
+        double da = s.a[k1] - s.a[k0], db = s.b[k1] - s.b[k0];
+        return hypot(da - 0.5 * db, s60 * db) / span;
+    }
+    // smallest singular value of d(vx, vy)/d(lon, lat) at the tile centre (hex units per degree)
+    static double sigma_min(const Samples& s, double tw, double th) {
+        const double s60 = 0.86602540378443864676;
+        double ax = (s.a[5] - s.a[3]) / tw, bx = (s.b[5] - s.b[3]) / tw;
+        double ay = (s.a[7] - s.a[1]) / th, by = (s.b[7] - s.b[1]) / th;
+        double j00 = ax - 0.5 * bx, j10 = s60 * bx, j01 = ay - 0.5 * by, j11 = s60 * by;
+        double f = j00 * j00 + j01 * j01 + j10 * j10 + j11 * j11, d = fabs(j00 * j11 - j01 * j10);
+        double disc = std::max(0.0, f * f - 4.0 * d * d);
+        return sqrt(std::max(0.0, 0.5 * (f - sqrt(disc))));
+    }
+    bool fail(const char* w) {
+        why = w;
+        tile_idx.clear();
+        recs.clear();
+        entries.clear();
+        return false;
+    }
+    // largest distance (axial units) of the tile's samples from the bilinear patch through its
+    // corner images: the second-order term of the map over the tile
+    static double patch_dev(const Samples& s) {
+        // sample k = (u, v) with u = k % 3, v = k / 3 (0, 1/2, 1); corners 0, 2, 6, 8
+        double d = 0.0;
+        for (int q = 0; q < 9; q++) {
+            double u = 0.5 * (q % 3), v = 0.5 * (q / 3);
+            double pa = (1 - u) * (1 - v) * s.a[0] + u * (1 - v) * s.a[2] + (1 - u) * v * s.a[6] + u * v * s.a[8];
+            double pb = (1 - u) * (1 - v) * s.b[0] + u * (1 - v) * s.b[2] + (1 - u) * v * s.b[6] + u * v * s.b[8];
+            d = std::max(d, std::max(fabs(pa - s.a[q]), fabs(pb - s.b[q])));
+        }
+        return d;
+    }
+    static void mark_found(int64_t slot, const std::vector<int64_t>& cells,
+                           const std::function<int64_t(int64_t)>& slot_of, std::vector<uint8_t>& found,
+                           std::vector<int64_t>& slot_cell) {
+        if (slot_cell.empty()) {
+            int64_t mx = -1;
+            for (size_t q = 0; q < cells.size(); q++) mx = std::max(mx, slot_of(cells[q]));
+            slot_cell.assign((size_t)mx + 1, -1);
+            for (size_t q = 0; q < cells.size(); q++) {
+                int64_t sl = slot_of(cells[q]);
+                if (sl >= 0) slot_cell[(size_t)sl] = (int64_t)q;
+            }
+        }
+        if (slot < (int64_t)slot_cell.size() && slot_cell[(size_t)slot] >= 0) found[(size_t)slot_cell[(size_t)slot]] = 1;
+    }
+#endif  // !__HIPCC__
+};
+
+
+}  // namespace tiles
+}  // namespace mosaic

@@ -1,0 +1,307 @@
+// Host-compiled (g++) half of the H3 tile directory and point raster (tiles.h): the builders read
+// the H3 tables as host constants.  Linked into libmosaic_hip.so next to mosaic_hip.o.
+//
+// Point raster.  Each non-empty tile is cut into S x S sub-blocks and, where needed, each
+// sub-block into C x C cells.  A rectangle R (sub-block or cell, widened by eps) gets a code
+// valid for EVERY point of R:
+//   * the hexagons R can reach: R's image on the tile's face is the quadrilateral of its corner
+//     images to within the tile's measured second-order term (scaled to R's size); every window
+//     hexagon (exact Voronoi hexagon of the face lattice, H3's _hex2dToCoordIJK rounding) that the
+//     quadrilateral meets within a tolerance (separating-axis test) is a candidate.  H3 assigns
+//     each point of R one of them.
+//   * per candidate hexagon h, the answer of its points in R: the keys of h's core chips plus the
+//     keys of h's border chips containing the point.  When no segment of any border chip of h
+//     meets R, each border chip's contains() is constant on R (R is connected and misses the
+//     chip's boundary), so it is evaluated once, at R's centre, with the JTS restatement.
+//   * R's code is that answer if all candidates agree and it is empty or one key; otherwise
+//     kMixed (sub-blocks: split into cells; cells: the tile path runs for their points).
+// Reference semantics followed: the chip join = H3 cell equality (H3IndexSystem.scala:140-142) +
+// is_core || st_contains (QuickstartNotebook.py:205-219, ST_Contains.scala:34-42).
+#include "tiles.h"
+
+#include <atomic>
+#include <thread>
+
+namespace mosaic {
+namespace tiles {
+
+bool Builder::build(int res, const std::vector<int64_t>& cells, const std::function<int64_t(int64_t)>& slot_of) {
+    return build_impl(res, cells, slot_of);
+}
+
+namespace {
+
+const double kS60 = 0.86602540378443864676;
+
+struct P2 {
+    double x, y;
+};
+
+// Convex quadrilateral q[4] meets the Voronoi hexagon of lattice centre c within tolerance t
+// (separating axes: the hexagon's 3 edge normals and the quadrilateral's 4).
+bool quad_meets_hex(const P2* q, P2 c, double t) {
+    // hexagon: vertices at 30 + 60k degrees, radius 1/sqrt(3); apothem 1/2 along 0, 60, 120 degrees
+    static const double ax[3][2] = {{1.0, 0.0}, {0.5, kS60}, {-0.5, kS60}};
+    for (int k = 0; k < 3; k++) {
+        double hc = c.x * ax[k][0] + c.y * ax[k][1];
+        double lo = INFINITY, hi = -INFINITY;
+        for (int v = 0; v < 4; v++) {
+            double d = q[v].x * ax[k][0] + q[v].y * ax[k][1];
+            lo = std::min(lo, d);
+            hi = std::max(hi, d);
+        }
+        if (lo > hc + 0.5 + t || hi < hc - 0.5 - t) return false;
+    }
+    const double r = 0.57735026918962576451;
+    for (int e = 0; e < 4; e++) {
+        P2 a = q[e], b = q[(e + 1) & 3];
+        double nx = -(b.y - a.y), ny = b.x - a.x;
+        double len = sqrt(nx * nx + ny * ny);
+        if (!(len > 0)) continue;
+        nx /= len;
+        ny /= len;
+        double lo = INFINITY, hi = -INFINITY;
+        for (int v = 0; v < 4; v++) {
+            double d = q[v].x * nx + q[v].y * ny;
+            lo = std::min(lo, d);
+            hi = std::max(hi, d);
+        }
+        double hc = c.x * nx + c.y * ny, ext = 0.0;
+        for (int k = 0; k < 6; k++) {
+            double ang = (30.0 + 60.0 * k) * 0.017453292519943295;
+            ext = std::max(ext, fabs(r * (cos(ang) * nx + sin(ang) * ny)));
+        }
+        if (lo > hc + ext + t || hi < hc - ext - t) return false;
+    }
+    return true;
+}
+
+struct Seg {
+    double ax, ay, bx, by;
+};
+
+struct Rect {
+    double x0, y0, x1, y1;
+};
+
+void chip_segments(const pip::GeomStore& s, uint32_t g, std::vector<Seg>& out) {
+    out.clear();
+    for (uint32_t p = s.geom_part[g]; p < s.geom_part[g + 1]; p++)
+        for (uint32_t r = s.part_ring[p]; r < s.part_ring[p + 1]; r++)
+            for (uint32_t v = s.ring_start[r] + 1; v < s.ring_start[r + 1]; v++)
+                out.push_back(Seg{s.verts[v - 1].x, s.verts[v - 1].y, s.verts[v].x, s.verts[v].y});
+}
+
+bool any_seg_meets(const std::vector<Seg>& segs, const Rect& r) {
+    for (const Seg& e : segs)
+        if (raster::seg_meets_rect(e.ax, e.ay, e.bx, e.by, r.x0, r.y0, r.x1, r.y1)) return true;
+    return false;
+}
+
+// One window hexagon's chips, prepared for classification.
+struct Hex {
+    P2 c;                       // lattice centre (face plane, hex units)
+    std::vector<int32_t> core;  // keys of core chips
+    std::vector<uint32_t> border;
+    std::vector<int32_t> border_key;
+    std::vector<std::vector<Seg>> segs;  // per border chip
+    std::vector<pip::Box> bbox;
+};
+
+}  // namespace
+
+bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
+    S = S_;
+    C = C_;
+    sub.clear();
+    blocks.clear();
+    n_sub_pure = n_sub_mixed = n_cell_mixed = 0;
+    if (tile_idx.empty() || S < 1 || C < 1 || S * C > 1024) return false;
+    if (src.n_polygons >= (int32_t)kMixed - 1) return false;
+    const int nx = grid.nx, ny = grid.ny, N = S * C;
+    const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
+    if (NX * NY > ((int64_t)1 << 26)) return false;
+    sub.assign((size_t)(NX * NY), 0u);
+    const double tw = 1.0 / grid.sx, th = 1.0 / grid.sy;
+    // per-tile output blocks, merged afterwards
+    std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
+    std::vector<int> tile_of_rec(recs.size(), -1);
+    for (int64_t t = 0; t < (int64_t)nx * ny; t++)
+        if (tile_idx[(size_t)t] >= 2) tile_of_rec[tile_idx[(size_t)t] - 2] = (int)t;
+    std::atomic<int64_t> next(0), pure(0), mixed(0), cmixed(0);
+
+    auto work = [&]() {
+        std::vector<P2> lat;  // (N + 1)^2 lattice images
+        std::vector<Hex> hexes;
+        std::vector<int> cand, cand2;
+        std::vector<int32_t> ans, ah;
+        std::vector<Seg> segs_tmp;
+        while (true) {
+            int64_t ri = next.fetch_add(1);
+            if (ri >= (int64_t)recs.size()) break;
+            const TileRec& tr = recs[(size_t)ri];
+            int t = tile_of_rec[(size_t)ri];
+            if (t < 0 || tr.dims == 0) continue;
+            const int ti = t % nx, tj = t / nx;
+            const int face = (int)(tr.dims & 0xffu), wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
+            const double lon0 = grid.x0 + ti * tw, lat0 = grid.y0 + tj * th;
+            // lattice images on the tile's face
+            lat.resize((size_t)(N + 1) * (N + 1));
+            for (int j = 0; j <= N; j++)
+                for (int i = 0; i <= N; i++) {
+                    double px, py, pz, vx, vy, b;
+                    h3::fast_unit(lat0 + th * j / N, lon0 + tw * i / N, &px, &py, &pz);
+                    h3::fast_plane(px, py, pz, face, res_, &vx, &vy, &b);
+                    lat[(size_t)j * (N + 1) + i] = P2{vx, vy};
+                }
+            // window hexagons
+            hexes.assign((size_t)wa * wb, Hex());
+            for (int ra = 0; ra < wa; ra++)
+                for (int rb = 0; rb < wb; rb++) {
+                    Hex& h = hexes[(size_t)ra * wb + rb];
+                    int a = tr.a0 + ra, bb = tr.b0 + rb;
+                    h.c = P2{(double)a - 0.5 * (double)bb, (double)bb * kS60};
+                    uint32_t e = entries[tr.off + (uint32_t)(ra * wb + rb)];
+                    if (!e) continue;
+                    uint32_t f0 = src.slot_first[e - 1], n0 = src.slot_count[e - 1];
+                    for (uint32_t cidx = f0; cidx < f0 + n0; cidx++) {
+                        uint32_t m = src.meta[cidx];
+                        if (m & 1u) {
+                            h.core.push_back((int32_t)(m >> 1));
+                        } else {
+                            h.border.push_back(cidx);
+                            h.border_key.push_back((int32_t)(m >> 1));
+                            chip_segments(src.store, cidx, segs_tmp);
+                            h.segs.push_back(segs_tmp);
+                            h.bbox.push_back(src.store.geom_bbox[cidx]);
+                        }
+                    }
+                    std::sort(h.core.begin(), h.core.end());
+                }
+            const double dev = rec_dev[(size_t)ri];
+            const double cell_deg_x = tw / N, cell_deg_y = th / N;
+            // classification of the lattice rectangle [i0, i1] x [j0, j1] (lattice indices)
+            // with candidate hexagons `cin` -> code; `cout` receives the candidates it meets
+            auto classify = [&](int i0, int j0, int i1, int j1, const std::vector<int>& cin, std::vector<int>& cout,
+                                bool& edges_near) -> uint16_t {
+                edges_near = false;
+                P2 q[4] = {lat[(size_t)j0 * (N + 1) + i0], lat[(size_t)j0 * (N + 1) + i1],
+                           lat[(size_t)j1 * (N + 1) + i1], lat[(size_t)j1 * (N + 1) + i0]};
+                double frac = std::max((double)(i1 - i0), (double)(j1 - j0)) / N;
+                double tol = 4.0 * dev * frac * frac + 1e-7;
+                cout.clear();
+                for (int k : cin)
+                    if (quad_meets_hex(q, hexes[(size_t)k].c, tol)) cout.push_back(k);
+                Rect r;
+                double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(lon0) + 1.0);
+                double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(lat0) + 1.0);
+                r.x0 = lon0 + tw * i0 / N - ex;
+                r.x1 = lon0 + tw * i1 / N + ex;
+                r.y0 = lat0 + th * j0 / N - ey;
+                r.y1 = lat0 + th * j1 / N + ey;
+                double cxm = lon0 + tw * (i0 + i1) / (2.0 * N), cym = lat0 + th * (j0 + j1) / (2.0 * N);
+                bool first = true;
+                bool mixed_ans = false;
+                for (int k : cout) {
+                    const Hex& h = hexes[(size_t)k];
+                    ah = h.core;
+                    for (size_t b = 0; b < h.border.size(); b++) {
+                        const pip::Box& bx = h.bbox[b];
+                        if (!(bx.maxx < r.x0 || bx.minx > r.x1 || bx.maxy < r.y0 || bx.miny > r.y1) &&
+                            any_seg_meets(h.segs[b], r)) {
+                            edges_near = true;
+                            return kMixed;
+                        }
+                        if (pip::contains(src.store, h.border[b], cxm, cym)) ah.push_back(h.border_key[b]);
+                    }
+                    std::sort(ah.begin(), ah.end());
+                    if (first) {
+                        ans = ah;
+                        first = false;
+                    } else if (ah != ans) {
+                        mixed_ans = true;
+                    }
+                }
+                if (mixed_ans || cout.empty()) return kMixed;  // no candidate: cannot happen; stay safe
+                if (ans.empty()) return 0;
+                if (ans.size() == 1) return (uint16_t)(ans[0] + 1);
+                return kMixed;
+            };
+            std::vector<int> all((size_t)wa * wb);
+            for (size_t k = 0; k < all.size(); k++) all[k] = (int)k;
+            std::vector<uint16_t>& outb = tile_blocks[(size_t)ri];
+            std::vector<uint16_t> cellc((size_t)C * C);
+            for (int sj = 0; sj < S; sj++)
+                for (int si = 0; si < S; si++) {
+                    bool en;
+                    uint16_t code = classify(si * C, sj * C, (si + 1) * C, (sj + 1) * C, all, cand, en);
+                    uint32_t entry;
+                    if (code != kMixed) {
+                        entry = code;
+                        pure++;
+                    } else {
+                        mixed++;
+                        bool same = true;
+                        for (int cj = 0; cj < C; cj++)
+                            for (int ci = 0; ci < C; ci++) {
+                                int i0 = si * C + ci, j0 = sj * C + cj;
+                                uint16_t cc = classify(i0, j0, i0 + 1, j0 + 1, cand, cand2, en);
+                                cellc[(size_t)cj * C + ci] = cc;
+                                if (cc == kMixed) cmixed++;
+                                same = same && cc == cellc[0];
+                            }
+                        if (same && cellc[0] != kMixed) {
+                            entry = cellc[0];
+                        } else {
+                            entry = kRasterBlock | (uint32_t)(outb.size() / ((size_t)C * C));
+                            outb.insert(outb.end(), cellc.begin(), cellc.end());
+                        }
+                    }
+                    sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
+                }
+        }
+    };
+    int nt = std::max(1, threads);
+    std::vector<std::thread> pool;
+    for (int k = 1; k < nt; k++) pool.emplace_back(work);
+    work();
+    for (auto& th_ : pool) th_.join();
+    // kFull tiles: every point takes the tile path; kSkip tiles: no pair (0, already)
+    for (int64_t t = 0; t < (int64_t)nx * ny; t++) {
+        if (tile_idx[(size_t)t] != kFull) continue;
+        int ti = (int)(t % nx), tj = (int)(t / nx);
+        for (int sj = 0; sj < S; sj++)
+            for (int si = 0; si < S; si++) sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = kMixed;
+    }
+    // merge blocks, rebase the entries
+    std::vector<uint32_t> base(recs.size(), 0);
+    size_t total = 0;
+    for (size_t r = 0; r < recs.size(); r++) {
+        base[r] = (uint32_t)(total / ((size_t)C * C));
+        total += tile_blocks[r].size();
+    }
+    if (total / ((size_t)C * C) >= (size_t)kRasterBlock) {
+        sub.clear();
+        return false;
+    }
+    blocks.reserve(std::max<size_t>(total, 1));
+    for (size_t r = 0; r < recs.size(); r++) blocks.insert(blocks.end(), tile_blocks[r].begin(), tile_blocks[r].end());
+    if (blocks.empty()) blocks.assign((size_t)C * C, kMixed);
+    for (size_t r = 0; r < recs.size(); r++) {
+        int t = tile_of_rec[r];
+        if (t < 0 || !base[r]) continue;
+        int ti = t % nx, tj = t / nx;
+        for (int sj = 0; sj < S; sj++)
+            for (int si = 0; si < S; si++) {
+                uint32_t& e = sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))];
+                if (e & kRasterBlock) e = kRasterBlock | ((e & ~kRasterBlock) + base[r]);
+            }
+    }
+    n_sub_pure = pure.load();
+    n_sub_mixed = mixed.load();
+    n_cell_mixed = cmixed.load();
+    return true;
+}
+
+}  // namespace tiles
+}  // namespace mosaic

@@ -274,17 +274,112 @@ def test_join_tessellated_chips_every_strategy(h3ctx):
             h3ctx.set_option("lane_edges", lane_edges)
             table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
                                      n_polygons=len(zones35))
-            for mode in (3, 2, 0):
+            assert table.tiles()["built"] == 1
+            for mode, tiles, praster in ((3, 1, 1), (3, 1, 0), (3, 0, 0), (2, 1, 1), (0, 1, 1)):
                 h3ctx.set_option("pip_mode", mode)
+                h3ctx.set_option("tiles", tiles)
+                h3ctx.set_option("point_raster", praster)
                 rows, keys = h3ctx.pip_join_pairs(table, x, y)
                 k = ~differ[rows]
                 got = set(zip(rows[k].tolist(), keys[k].tolist()))
-                assert got == want, (raster, lane_edges, mode, len(got ^ want))
+                assert got == want, (raster, lane_edges, mode, tiles, praster, len(got ^ want))
+            h3ctx.set_option("tiles", 1)
+            h3ctx.set_option("point_raster", 1)
             table.close()
     finally:
         h3ctx.set_option("raster", 16)
         h3ctx.set_option("lane_edges", 0)
         h3ctx.set_option("pip_mode", 3)
+        h3ctx.set_option("tiles", 1)
+        h3ctx.set_option("point_raster", 1)
+
+
+def _tile_edge_points(t, rng, n):
+    """Points on and 1 ulp either side of the tile directory's row / column lines."""
+    nx, ny, x0, y0, sx, sy = t["nx"], t["ny"], t["x0"], t["y0"], t["sx"], t["sy"]
+    xs = x0 + rng.integers(0, nx + 1, n) / sx
+    ys = y0 + rng.uniform(0, ny / sy, n)
+    ys2 = y0 + rng.integers(0, ny + 1, n) / sy
+    xs2 = x0 + rng.uniform(0, nx / sx, n)
+    x = np.concatenate([xs, np.nextafter(xs, np.inf), np.nextafter(xs, -np.inf), xs2, xs2])
+    y = np.concatenate([ys, ys, ys, ys2, np.nextafter(ys2, -np.inf)])
+    return x, y
+
+
+def test_join_tiled_nyc_zones_match_oracle(h3ctx, zones):
+    """The bench workload's build side (all 263 zones, grid_tessellateexplode at res 9) with the
+    tile directory: uniform points over and beyond the zones' bbox, clustered points, points on
+    tile lines and on chip boundaries -- counts equal the oracle's and the untiled kernel's."""
+    from mosaic_amd.context import tessellate
+
+    chips = tessellate("H3", zones, 9)
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
+                             n_polygons=len(zones))
+    t = table.tiles()
+    assert t["built"] == 1 and t["records"] > 100, t
+    rng = np.random.default_rng(11)
+    x0, y0, x1, y1 = zones.bbox()
+    wx, wy = x1 - x0, y1 - y0
+    ux = rng.uniform(x0 - 0.2 * wx, x1 + 0.2 * wx, 600_000)
+    uy = rng.uniform(y0 - 0.2 * wy, y1 + 0.2 * wy, 600_000)
+    qx, qy = quickstart_points(zones, 200_000, seed=12)
+    bx, by = _chip_boundary_points(chips, rng, limit=3000)
+    tx, ty = _tile_edge_points(t, rng, 40_000)
+    x = np.concatenate([ux, qx, tx, bx, [np.nan, np.inf, x0]])
+    y = np.concatenate([uy, qy, ty, by, [y0, 0.0, np.nan]])
+    cells = h3ctx.grid_longlatascellid(x, y, 9, raw=True)
+    ocells = oracle.h3_point_to_index(x, y, 9)
+    differ = cells != ocells
+    assert differ[:1_000_000].sum() == 0
+    keep = ~differ
+    offs, data = chips["wkb"]
+    oc = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+              wkb_offsets=offs, wkb=data)
+    want, total = oracle.pip_join(oc, oracle.GRID_H3, 9, x[keep], y[keep], len(zones), threads=8)
+    assert total > 100_000
+    assert t["raster"] == 1 and t["pure_sub_blocks"] > 1000, t
+    got = h3ctx.pip_join_count(table, x[keep], y[keep])
+    assert np.array_equal(got, want)
+    rows, keys = h3ctx.pip_join_pairs(table, x[keep], y[keep])
+    assert len(rows) == total and np.array_equal(np.bincount(keys, minlength=len(zones)), want)
+    try:
+        for tiles, praster in ((1, 0), (0, 0)):
+            h3ctx.set_option("tiles", tiles)
+            h3ctx.set_option("point_raster", praster)
+            assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (tiles, praster)
+    finally:
+        h3ctx.set_option("tiles", 1)
+        h3ctx.set_option("point_raster", 1)
+    table.close()
+
+
+@pytest.mark.parametrize("sub,cell", [(4, 2), (32, 16)])
+def test_join_point_raster_sizes(h3ctx, zones, sub, cell):
+    """Other point-raster sizes (coarse: most points take the tile path; fine) give the oracle's
+    counts on clustered points (the C3 mixture) at res 10."""
+    from mosaic_amd.context import tessellate
+
+    ids = list(range(0, 263, 3))
+    sub_zones = zones.subset(ids)
+    chips = tessellate("H3", sub_zones, 10)
+    h3ctx.set_option("raster_sub", sub)
+    h3ctx.set_option("raster_cell", cell)
+    try:
+        table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 10,
+                                 n_polygons=len(ids))
+    finally:
+        h3ctx.set_option("raster_sub", 16)
+        h3ctx.set_option("raster_cell", 8)
+    t = table.tiles()
+    assert t["raster"] == 1 and t["raster_sub"] == sub and t["raster_cell"] == cell, t
+    x, y = quickstart_points(sub_zones, 400_000, sigma=0.002, seed=31)
+    offs, data = chips["wkb"]
+    oc = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+              wkb_offsets=offs, wkb=data)
+    want, total = oracle.pip_join(oc, oracle.GRID_H3, 10, x, y, len(ids), threads=8)
+    assert total > 100_000
+    assert np.array_equal(h3ctx.pip_join_count(table, x, y), want)
+    table.close()
 
 
 def test_join_pairs_match_oracle(h3ctx, zones):

@@ -1,0 +1,89 @@
+"""CPU-only: the H3 tile directory and point raster (mosaic_amd/csrc/tiles.h, tiles_build.cpp)
+compiled for the host.  The directory gives, for every point it certifies, the chip-table slot of
+the point's exact H3 cell (h3_exact, the oracle's restatement) -- and "skip" only for points whose
+exact cell carries no chip.  Every pure point-raster code equals the exact answer (core chips of
+the exact cell + border chips whose JTS contains holds).  Tessellated NYC zones at several
+resolutions (uniform points, points on / next to tile lines, chip vertices and chip segments),
+plus synthetic cell sets near icosahedron face edges, pentagons, high latitudes and the
+antimeridian (where the builder must either decline or stay exact)."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from mosaic_amd.context import tessellate
+from mosaic_amd.data import PolygonSet
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def exe(tmp_path_factory):
+    out = tmp_path_factory.mktemp("tiles") / "tiles_sc"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wno-unknown-pragmas", "-pthread", "-o", str(out),
+                    os.path.join(ROOT, "tests", "native", "tiles_selfcheck.cpp")], check=True)
+    return out
+
+
+def _run(exe, tmp_path, res, chips, npts=300_000, seed=3, sc=(16, 8)):
+    path = tmp_path / f"chips_{res}.bin"
+    offs, data = chips["wkb"]
+    with open(path, "wb") as f:
+        f.write(struct.pack("<iI", res, len(chips["index_id"])))
+        for i in range(len(chips["index_id"])):
+            w = bytes(data[offs[i]:offs[i + 1]])
+            f.write(struct.pack("<qBiI", int(chips["index_id"][i]), int(chips["is_core"][i]),
+                                int(chips["polygon_key"][i]), len(w)))
+            f.write(w)
+    out = subprocess.run([str(exe), str(path), str(npts), str(seed), str(sc[0]), str(sc[1])], check=True,
+                         capture_output=True, text=True)
+    built, bad, checked, skipped, full, unc, miss, rbuilt, rbad, rpure, rmixed = map(int, out.stdout.split())
+    return dict(built=built, bad=bad, checked=checked, skipped=skipped, full=full, unc=unc, miss=miss,
+                raster=rbuilt, raster_bad=rbad, raster_pure=rpure, raster_mixed=rmixed, log=out.stderr)
+
+
+@pytest.mark.parametrize("res,sc", [(7, (16, 8)), (8, (8, 4)), (9, (16, 8)), (9, (4, 2)), (10, (16, 8)),
+                                    (11, (8, 8))])
+def test_tiles_nyc_tessellation(exe, tmp_path, res, sc):
+    zones = PolygonSet.load("nyc_taxi_zones_35" if res >= 10 else "nyc_taxi_zones")
+    chips = tessellate("H3", zones, res)
+    r = _run(exe, tmp_path, res, chips, sc=sc)
+    assert r["built"] == 1, r["log"]
+    assert r["bad"] == 0, r["log"]
+    assert r["checked"] > 200_000
+    assert r["miss"] == 0
+    assert r["raster"] == 1, r["log"]
+    assert r["raster_bad"] == 0, r["log"]
+    assert r["raster_pure"] > 0.4 * 300_000
+
+
+def _disc_chips(lon, lat, radius_deg, res, n=20000, seed=0):
+    """Core chips (no geometry) for the cells of a disc, with a few polygon keys so that
+    neighbouring cells differ: exercises the raster's hexagon-boundary classification."""
+    rng = np.random.default_rng(seed)
+    x = lon + (rng.random(n) - 0.5) * 2 * radius_deg
+    y = np.clip(lat + (rng.random(n) - 0.5) * 2 * radius_deg, -89.9, 89.9)
+    cells = np.unique(oracle.h3_point_to_index(x, y, res))
+    cells = cells[cells != 0]
+    keys = (cells % 5).astype(np.int32)
+    return dict(index_id=cells, is_core=np.ones(len(cells), np.uint8), polygon_key=keys,
+                wkb=(np.zeros(len(cells) + 1, np.int64), np.zeros(0, np.uint8)))
+
+
+# (lon, lat, radius, res): a face edge crossing (lon -45 between faces 1 / 6 region), a pentagon
+# base cell centre (base cell 4 at about 64.7 N, 10.5 E), Reykjavik-like high latitude, the
+# antimeridian, the equator at the prime meridian, a coarse resolution with huge cells.
+CASES = [(-45.0, 46.0, 1.5, 7), (10.536199, 64.7, 0.4, 6), (-21.9, 64.1, 0.3, 9), (179.95, -16.5, 0.2, 8),
+         (0.0, 0.0, 0.5, 8), (-74.0, 40.7, 3.0, 3), (139.7, 35.7, 0.05, 12)]
+
+
+@pytest.mark.parametrize("lon,lat,radius,res", CASES)
+def test_tiles_synthetic_regions(exe, tmp_path, lon, lat, radius, res):
+    r = _run(exe, tmp_path, res, _disc_chips(lon, lat, radius, res), npts=200_000)
+    assert r["bad"] == 0, r["log"]
+    assert r["raster_bad"] == 0, r["log"]
+    if r["built"]:
+        assert r["checked"] > 0 and r["raster"] == 1

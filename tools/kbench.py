@@ -1,5 +1,5 @@
 """Kernel-level timing breakdown of the join (GPU box): cell kernel alone, join with every chip
-marked core (no contains), full join.  Prints one JSON line per variant.
+marked core (no contains), full join; with and without the H3 tile directory.  Prints one JSON line per variant.
 
     python tools/kbench.py [--n 1e8] [--res 9]
 """
@@ -24,6 +24,11 @@ def main():
     p.add_argument("--clustered", action="store_true")
     p.add_argument("--rasters", type=int, nargs="*", default=[8, 16, 32])
     p.add_argument("--lane-edges", type=int, nargs="*", default=[0, 4, 8])
+    p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*",
+                   default=[(1, 1), (1, 0), (0, 0)], help="TILES:POINT_RASTER pairs")
+    p.add_argument("--point-raster", type=lambda v: tuple(int(q) for q in v.split("x")), nargs="*",
+                   default=[(16, 8)], help="point raster sizes SUBxCELL")
+    p.add_argument("--legacy", action="store_true", help="also time the coop / slab strategies")
     args = p.parse_args()
     import torch
 
@@ -37,7 +42,12 @@ def main():
     ctx.set_option("block", args.block)
     ctx.set_option("blocks_per_cu", args.bpc)
     n = int(args.n)
-    x, y = uniform_points_device(zones.bbox(), n, seed=1)
+    if args.clustered:
+        from mosaic_amd.data import clustered_points_device
+
+        x, y = clustered_points_device(zones, n, seed=1)
+    else:
+        x, y = uniform_points_device(zones.bbox(), n, seed=1)
     out = torch.empty(n, dtype=torch.int64, device="cuda")
     counts = torch.zeros(len(zones), dtype=torch.int64, device="cuda")
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -65,24 +75,49 @@ def main():
     t_cell = timeit(cells)
     print(json.dumps({"variant": "cell_kernel", "ms": t_cell, "pts_per_s": n / t_cell * 1e3}))
     ctx.set_option("async", 1)
-    variants = [("join_all_core", True, 3, 16, 8), ("join_full_coop", False, 1, 16, 8),
-                ("join_full_slab", False, 2, 16, 8)]
-    for r in args.rasters:
-        for le in args.lane_edges:
-            variants.append((f"join_raster{r}_lane{le}", False, 3, r, le))
-    for name, core, mode, raster, lane_edges in variants:
+    # floor: one core chip far from the points -> every point is outside the raster grid (no lookups)
+    far = ctx.grid_longlatascellid(np.array([10.0]), np.array([10.0]), args.res, raw=True)
+    ftab = ctx.chip_table(np.ones(1, np.uint8), far.astype(np.int64), [b""], np.zeros(1, np.int32), args.res,
+                          n_polygons=len(zones))
+    t = timeit(lambda: ctx.pip_join_count(ftab, x, y, out=counts))
+    print(json.dumps({"variant": "stream_floor_no_lookups", "ms": t, "GBps": n * 16 / t / 1e6,
+                      "raster": ftab.tiles()["raster"]}))
+    ftab.close()
+    variants = []
+    for tiles, praster in args.modes:
+        for sub, cell in (args.point_raster if praster else [(16, 8)]):
+            tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}" if praster else "")
+            variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, sub, cell))
+            for r in args.rasters:
+                for le in args.lane_edges:
+                    variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster, sub, cell))
+    if args.legacy:
+        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, 16, 8), ("join_full_slab", False, 2, 16, 8, 0, 0, 16, 8)]
+    for name, core, mode, raster, lane_edges, tiles, praster, sub, cell in variants:
+        ctx.set_option("tiles", tiles)
+        ctx.set_option("point_raster", praster)
+        ctx.set_option("raster_sub", sub)
+        ctx.set_option("raster_cell", cell)
         ctx.set_option("pip_mode", mode)
         ctx.set_option("raster", raster)
         ctx.set_option("lane_edges", lane_edges)
         is_core = np.ones_like(chips["is_core"]) if core else chips["is_core"]
+        tb0 = time.perf_counter()
         table = ctx.chip_table(is_core, chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
                                n_polygons=len(zones))
+        build_s = time.perf_counter() - tb0
         t = timeit(lambda: ctx.pip_join_count(table, x, y, out=counts))
+        ctx.set_option("timing", 2)
+        ctx.pip_join_count(table, x, y, out=counts)
+        kt = [round(v, 4) for v in ctx.kernel_times()]
+        ctx.set_option("timing", 0)
         ctx.set_option("async", 0)
         ctx.pip_join_count(table, x, y, out=counts)
         st = ctx.last_stats()
         ctx.set_option("async", 1)
-        print(json.dumps({"variant": name, "ms": t, "pts_per_s": n / t * 1e3, **st, "info": table.info()}))
+        tl = table.tiles()
+        print(json.dumps({"variant": name, "ms": t, "kernels_ms": kt, "pts_per_s": n / t * 1e3, **st,
+                          "build_s": round(build_s, 2), "raster": {k: tl[k] for k in ("raster", "pure_sub_blocks", "mixed_sub_blocks", "mixed_cells")}}))
         table.close()
 
 
