@@ -89,9 +89,8 @@ struct JoinArgs {
     const uint32_t* tile_ent;
     tiles::PointRaster praster;       // point raster (tiles.h); praster.sub == nullptr: none
     int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
-    uint32_t* mixq;                   // per stream wave w: rows (- row_lo) in mixed raster cells at
-    uint32_t* mixq_count;             //   mixq[w * mixq_cap ...], mixq_count[w] of them
-    uint64_t mixq_cap;
+    uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
+    unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
     unsigned long long* amb_queue;  // rows for the exact H3 pass
@@ -752,84 +751,154 @@ __global__ void __launch_bounds__(256) k_join_tiled(JoinArgs a) {
 // runs near HBM speed.  Four consecutive points per lane (two 16-byte loads per coordinate,
 // VEC: both arrays 16-byte aligned), their lookups issued back to back.  Rows in mixed raster
 // cells are appended to mixq (one atomic per wave) for k_join_mixed.
-template <bool LDS_COUNTS, bool PAIRS, bool VEC>
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+template <bool LDS_COUNTS, bool PAIRS, bool VEC, bool VALID, int G>
 __global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
     extern __shared__ unsigned int lds[];
-    counts_init<LDS_COUNTS>(a, lds);
+    // dynamic LDS: [per-polygon counts (LDS_COUNTS)] [quad level of the raster (if any)]
+    uint16_t* quad = a.praster.quad ? (uint16_t*)(lds + (LDS_COUNTS ? a.n_polygons : 0)) : nullptr;
+    if (quad) {
+        const int nq = a.praster.qnx * a.praster.qny;
+        for (int k = threadIdx.x; k < nq; k += blockDim.x) quad[k] = a.praster.quad[k];
+    }
+    counts_init<LDS_COUNTS>(a, lds);  // (its barrier also publishes the quad level)
+    if (!LDS_COUNTS) __syncthreads();
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    // every wave owns a private queue segment: no atomics, wave-uniform fill level
-    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    uint32_t* wq = a.mixq + gw * a.mixq_cap;
-    uint32_t wn = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    for (int64_t i0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < a.n; i0 += stride) {
-        double x[4], y[4];
-        bool live[4];
-        if (VEC && i0 + 3 < a.n) {
-            const double2 x01 = *(const double2*)(a.x + i0), x23 = *(const double2*)(a.x + i0 + 2);
-            const double2 y01 = *(const double2*)(a.y + i0), y23 = *(const double2*)(a.y + i0 + 2);
-            x[0] = x01.x;
-            x[1] = x01.y;
-            x[2] = x23.x;
-            x[3] = x23.y;
-            y[0] = y01.x;
-            y[1] = y01.y;
-            y[2] = y23.x;
-            y[3] = y23.y;
+    // mixed rows are staged per wave in LDS and flushed to the global queue once 64 or more are
+    // waiting (one atomic per flush: a per-iteration atomic on one counter serialises the grid);
+    // the stage holds < 64 + 256 G rows
+    __shared__ uint32_t stage[4][64 + 256 * G];
+    uint32_t* wq = stage[(threadIdx.x >> 6) & 3];
+    uint32_t wn = 0;  // wave-uniform fill level
+    // G groups of 4 consecutive rows per lane and iteration; group g is a grid-wide slice of
+    // 4 * (threads) rows, so each group's loads stay coalesced across the wave
+    const int64_t gstride = (int64_t)gridDim.x * blockDim.x * 4, stride = gstride * G;
+    // wave-uniform trip count (the ballots, the stage and its flushes need every lane): the loop
+    // runs while the wave's first row is in range; lanes past the end are not live
+    int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 4;
+    int64_t i0 = w0 + lane * 4;
+    // software pipeline (VEC): the next iteration's coordinates load while this iteration's block
+    // gathers and its counting run
+    v2d nx[G][2], ny[G][2];
 #pragma unroll
-            for (int k = 0; k < 4; k++) live[k] = !a.valid || a.valid[i0 + k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                live[k] = i0 + k < a.n && (!a.valid || a.valid[i0 + k]);
-                x[k] = live[k] ? a.x[i0 + k] : 0.0;
-                y[k] = live[k] ? a.y[i0 + k] : 0.0;
-            }
-        }
-        uint16_t rc[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) rc[k] = live[k] ? tiles::raster_code(a.praster, a.tgrid.x0, a.tgrid.y0, x[k], y[k]) : 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (rc[k] != 0 && rc[k] != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, i0 + k, (uint32_t)rc[k] - 1u, lds);
-            const unsigned long long mm = __ballot(rc[k] == tiles::kMixed);
-            if (rc[k] == tiles::kMixed) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(i0 + k - a.row_lo);
-            wn += (uint32_t)__popcll(mm);
+    for (int g = 0; g < G; g++) {
+        const int64_t r = i0 + g * gstride;
+        nx[g][0] = nx[g][1] = ny[g][0] = ny[g][1] = v2d{0.0, 0.0};
+        if (VEC && r + 3 < a.n) {
+            nx[g][0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
+            nx[g][1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 2));
+            ny[g][0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
+            ny[g][1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 2));
         }
     }
-    if (lane == 0) a.mixq_count[gw] = wn;
+    for (; w0 < a.n; w0 += stride, i0 += stride) {
+        tiles::Lookup4 L[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int64_t r = i0 + g * gstride;
+            double x[4], y[4];
+            bool live[4];
+            if (VEC && r + 3 < a.n) {
+                x[0] = nx[g][0].x;
+                x[1] = nx[g][0].y;
+                x[2] = nx[g][1].x;
+                x[3] = nx[g][1].y;
+                y[0] = ny[g][0].x;
+                y[1] = ny[g][0].y;
+                y[2] = ny[g][1].x;
+                y[3] = ny[g][1].y;
+#pragma unroll
+                for (int k = 0; k < 4; k++) live[k] = !VALID || a.valid[r + k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    live[k] = r + k < a.n && (!VALID || a.valid[r + k]);
+                    x[k] = live[k] ? a.x[r + k] : 0.0;
+                    y[k] = live[k] ? a.y[r + k] : 0.0;
+                }
+            }
+            tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L[g], quad);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) tiles::raster_gather4(a.praster, L[g]);
+        if (VEC) {
+            // the next iteration's coordinates, issued after this iteration's gathers (vmcnt
+            // retires in order, so loads issued earlier would be waited for first); unconditional,
+            // since a branch here makes the compiler wait conservatively -- past the end it
+            // re-reads the chunk's first group
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const int64_t r = i0 + stride + g * gstride;
+                const int64_t r1 = (r + 3 < a.n) ? r : a.row_lo;
+                nx[g][0] = __builtin_nontemporal_load((const v2d*)(a.x + r1));
+                nx[g][1] = __builtin_nontemporal_load((const v2d*)(a.x + r1 + 2));
+                ny[g][0] = __builtin_nontemporal_load((const v2d*)(a.y + r1));
+                ny[g][1] = __builtin_nontemporal_load((const v2d*)(a.y + r1 + 2));
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            tiles::raster_select4(L[g]);
+            const int64_t r = i0 + g * gstride;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint16_t rc = L[g].out[k];
+                if (rc != 0 && rc != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, r + k, (uint32_t)rc - 1u, lds);
+                const unsigned long long mm = __ballot(rc == tiles::kMixed);
+                if (rc == tiles::kMixed) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(r + k - a.row_lo);
+                wn += (uint32_t)__popcll(mm);
+            }
+        }
+        if (wn >= 64) {  // flush the whole stage: one atomic per >= 64 rows
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
+            base = __shfl(base, 0, 64);
+            for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
+            __builtin_amdgcn_wave_barrier();
+            wn = 0;
+        }
+    }
+    if (wn) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
+        base = __shfl(base, 0, 64);
+        for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
+    }
     counts_flush<LDS_COUNTS>(a, lds, 0u);
 }
 
-// Rows of mixed raster cells: wave w of this launch takes the queue segments of stream waves
-// w, w + W, ... (W = waves here); tile path (certified hexagon -> window -> chips) and the raster
-// chip loop, one queued row per lane.
+// Rows of mixed raster cells (the dense queue mixq): tile path (certified hexagon -> window ->
+// chips) and the raster chip loop, one queued row per lane.
 template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a, uint32_t stream_waves) {
+__global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     __shared__ SlabItem items[4][16];
     counts_init<LDS_COUNTS>(a, lds);
     unsigned int tests = 0;
-    const int lane = (int)(threadIdx.x & 63);
     const int wv = (int)(threadIdx.x >> 6) & 3;
-    const uint32_t W = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t sw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); sw < stream_waves; sw += W) {
-        const uint32_t cnt = a.mixq_count[sw];
-        const uint32_t* q = a.mixq + (uint64_t)sw * a.mixq_cap;
-        for (uint32_t b = 0; b < cnt; b += 64) {
-            const bool live = b + lane < cnt;
-            double x = 0.0, y = 0.0;
-            int64_t i = -1;
-            uint32_t cur = 0, end = 0;
-            if (live) {
-                i = a.row_lo + (int64_t)q[b + lane];
-                x = a.x[i];
-                y = a.y[i];
-                tiled_cell(a, i, x, y, tiles::tile_of(a.tgrid, a.tile_idx, x, y), cur, end);
-            }
-            raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items[wv]);
+    const unsigned long long total = *a.mixq_count;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total;
+         base += stride) {
+        const unsigned long long t = base + (threadIdx.x & 63);
+        double x = 0.0, y = 0.0;
+        int64_t i = -1;
+        uint32_t cur = 0, end = 0;
+        if (t < total) {
+            i = a.row_lo + (int64_t)a.mixq[t];
+            x = a.x[i];
+            y = a.y[i];
+            tiled_cell(a, i, x, y, tiles::tile_of(a.tgrid, a.tile_idx, x, y), cur, end);
         }
+        raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items[wv]);
     }
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
@@ -984,8 +1053,10 @@ struct mosaic_ctx {
     int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
     int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
     int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
-    int raster_sub = 16;  // point raster: sub-blocks per tile side
-    int raster_cell = 8;  // point raster: cells per sub-block side
+    int raster_sub = 32;  // point raster: sub-blocks per tile side
+    int raster_cell = 16; // point raster: cells per sub-block side
+    int raster_quad = 1;  // point raster: LDS quad level
+    int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
@@ -1070,11 +1141,11 @@ struct mosaic_chips {
     int64_t tile_stats[6] = {0, 0, 0, 0, 0, 0};  // nx, ny, records, entries, kFull tiles, rings
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
-    DevBuf rsub, rblocks;
+    DevBuf rsub, rblocks, rquad;
     int64_t raster_stats[5] = {0, 0, 0, 0, 0};    // S, C, pure sub-blocks, mixed sub-blocks, mixed cells
     void release_all() {
         for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rblocks})
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rblocks, &rquad})
             b->release();
         store.release();
     }
@@ -1125,8 +1196,9 @@ static bool valid_res(int grid, int res) {
     return bng::valid_resolution(res);
 }
 
-// scalars buffer layout (unsigned long long): [0] amb_count, [1] pair_count, [2] tests, [3] flags
-static const int kScalars = 4;
+// scalars buffer layout (unsigned long long): [0] amb_count, [1] pair_count, [2] tests, [3] flags,
+// [4] mixed-raster-cell queue length
+static const int kScalars = 5;
 
 extern "C" {
 
@@ -1204,6 +1276,11 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "raster_sub") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "raster_sub must be in [1, 64]");
         c->raster_sub = (int)v;
+    } else if (k == "stream_groups") {
+        if (v != 1 && v != 2) return fail(MOSAIC_E_ARG, "stream_groups must be 1 or 2");
+        c->stream_groups = (int)v;
+    } else if (k == "raster_quad") {
+        c->raster_quad = v ? 1 : 0;
     } else if (k == "raster_cell") {
         if (v < 1 || v > 32) return fail(MOSAIC_E_ARG, "raster_cell must be in [1, 32]");
         c->raster_cell = (int)v;
@@ -1672,6 +1749,21 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
                     ch->praster.nx = tb.grid.nx * tb.S;
                     ch->praster.ny = tb.grid.ny * tb.S;
                     ch->praster.C = tb.C;
+                    ch->praster.quad = nullptr;
+                    if (!tb.quad.empty() && c->raster_quad) {
+                        size_t r2 = tb.quad.size() * 2;
+                        if ((rc = ch->rquad.reserve(r2))) {
+                            ch->release_all();
+                            delete ch;
+                            return rc;
+                        }
+                        HIP_TRY(hipMemcpy(ch->rquad.p, tb.quad.data(), r2, hipMemcpyHostToDevice));
+                        ch->praster.quad = (const uint16_t*)ch->rquad.p;
+                        ch->praster.qnx = tb.qnx;
+                        ch->praster.qny = tb.qny;
+                        ch->praster.qshift = tb.qshift;
+                        total += r2;
+                    }
                     ch->raster_stats[0] = tb.S;
                     ch->raster_stats[1] = tb.C;
                     ch->raster_stats[2] = tb.n_sub_pure;
@@ -1785,8 +1877,7 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.praster = ch->praster;
     a.row_lo = 0;
     a.mixq = nullptr;
-    a.mixq_count = nullptr;
-    a.mixq_cap = 0;
+    a.mixq_count = sc + 4;
     a.counts = dcounts;
     a.n_polygons = ch->n_polygons;
     a.amb_queue = (unsigned long long*)c->amb_queue.p;
@@ -1812,39 +1903,47 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
         const bool tiled = rast && h3g && c->tiles && ch->tiles_ok;
         const bool praster = tiled && c->point_raster && ch->raster_ok;
         if (praster) {
-            // rows in chunks of < 2^32 (uint32 queue entries); one chunk up to 4.29e9 rows.  Each
-            // stream wave gets a queue segment as long as its share of the chunk.
-            const int64_t chunk = ((int64_t)1 << 32) - 1;
+            // rows in chunks of < 2^32 (uint32 queue entries); one chunk up to 4.29e9 rows
+            const int64_t chunk = ((int64_t)1 << 32) - 4;  // multiple of 4: chunk starts stay 32-byte aligned
             const int64_t rows = std::min<int64_t>(n, chunk);
-            const int gs = grid_size(c, (rows + 3) / 4);
-            const uint32_t waves = (uint32_t)gs * (uint32_t)(c->block / 64);
-            const uint64_t per_iter = (uint64_t)gs * c->block * 4;
-            const uint64_t cap = ((uint64_t)rows + per_iter - 1) / per_iter * 256;
-            if ((rc = c->mix_queue.reserve((size_t)(cap * waves * 4 + waves * 4)))) return rc;
+            const int gs = grid_size(c, (rows + 4 * c->stream_groups - 1) / (4 * c->stream_groups));
+            if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
-            a.mixq_cap = cap;
-            a.mixq_count = (uint32_t*)((char*)c->mix_queue.p + cap * waves * 4);
-            const bool vec = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
+            a.mixq_count = sc + 4;
+            const bool vec = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0 && n >= 4;
             for (int64_t lo = 0; lo < n; lo += chunk) {
                 JoinArgs ac = a;
                 ac.row_lo = lo;
                 ac.n = std::min<int64_t>(n, lo + chunk);
+                const size_t qb = ch->praster.quad ? (size_t)ch->praster.qnx * ch->praster.qny * 2 : 0;
+                const size_t shm_c = (lds ? shm : 0) + qb, shm_n = qb;  // counts (LDS_COUNTS) + quad
 #define MOSAIC_STREAM(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(gs), dim3(c->block), SHM, c->stream, ac)
-                if (vec) {
-                    if (pairs) MOSAIC_STREAM((k_join_stream<false, true, true>), 0);
-                    else if (lds) MOSAIC_STREAM((k_join_stream<true, false, true>), shm);
-                    else MOSAIC_STREAM((k_join_stream<false, false, true>), 0);
+#define MOSAIC_STREAM_G(VEC, VALID, G)                                                  \
+    do {                                                                                \
+        if (pairs) MOSAIC_STREAM((k_join_stream<false, true, VEC, VALID, G>), shm_n);    \
+        else if (lds) MOSAIC_STREAM((k_join_stream<true, false, VEC, VALID, G>), shm_c); \
+        else MOSAIC_STREAM((k_join_stream<false, false, VEC, VALID, G>), shm_n);         \
+    } while (0)
+#define MOSAIC_STREAM_V(VEC, VALID)                                  \
+    do {                                                             \
+        if (c->stream_groups == 2) MOSAIC_STREAM_G(VEC, VALID, 2);   \
+        else MOSAIC_STREAM_G(VEC, VALID, 1);                         \
+    } while (0)
+                if (a.valid) {
+                    MOSAIC_STREAM_V(false, true);
+                } else if (vec && ac.n - lo >= 4) {  // the VEC prefetch re-reads a chunk's first 4 rows
+                    MOSAIC_STREAM_V(true, false);
                 } else {
-                    if (pairs) MOSAIC_STREAM((k_join_stream<false, true, false>), 0);
-                    else if (lds) MOSAIC_STREAM((k_join_stream<true, false, false>), shm);
-                    else MOSAIC_STREAM((k_join_stream<false, false, false>), 0);
+                    MOSAIC_STREAM_V(false, false);
                 }
+#undef MOSAIC_STREAM_V
+#undef MOSAIC_STREAM_G
 #undef MOSAIC_STREAM
                 HIP_TRY(hipGetLastError());
                 if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
                 const int gm = (int)std::max<int64_t>(1, std::min<int64_t>(gs, (int64_t)c->n_cu * c->blocks_per_cu));
 #define MOSAIC_MIXED(KERNEL, SHM) \
-    hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac, waves)
+    hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac)
                 hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
                 if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
                 if (pairs) MOSAIC_MIXED((k_join_mixed<false, true>), 0);

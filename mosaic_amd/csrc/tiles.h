@@ -60,7 +60,76 @@ struct PointRaster {
     const uint16_t* blocks;  // C x C codes per block
     double sx, sy;           // sub-blocks per degree
     int32_t nx, ny, C;
+    // quad level: one uint16 per 2^qshift x 2^qshift sub-blocks, the code they all share or kMixed
+    // (= look at the sub-block); small enough (<= kQuadMax entries) to live in LDS
+    const uint16_t* quad;    // nullptr: no quad level
+    int32_t qnx, qny, qshift;
 };
+static const int kQuadMax = 8192;
+
+// Raster lookups of four points, level by level so the loads of a lane overlap (same result as
+// raster_code() per point): raster_issue4 computes the indices and issues the four sub-block
+// gathers; raster_gather4 issues the block gathers, raster_select4 forms the codes
+// (raster_finish4 = both).  A caller can issue other loads (the next coordinates) in between.
+struct Lookup4 {
+    int64_t si[4];
+    uint32_t fc[4], e[4];
+    bool in[4];
+    uint16_t b[4], out[4];
+};
+MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const double* x, const double* y,
+                             const bool* live, Lookup4& L, const uint16_t* quad_lds = nullptr) {
+    int64_t qi[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const double gx = (x[k] - x0) * r.sx, gy = (y[k] - y0) * r.sy;
+        L.in[k] = live[k] && gx >= 0.0 && gx < (double)r.nx && gy >= 0.0 && gy < (double)r.ny;
+        const int ix = L.in[k] ? (int)gx : 0, iy = L.in[k] ? (int)gy : 0;
+        L.si[k] = (int64_t)iy * r.nx + ix;
+        qi[k] = (int64_t)(iy >> r.qshift) * r.qnx + (ix >> r.qshift);
+        int cx = L.in[k] ? (int)((gx - (double)ix) * (double)r.C) : 0;
+        int cy = L.in[k] ? (int)((gy - (double)iy) * (double)r.C) : 0;
+        cx = cx < r.C - 1 ? cx : r.C - 1;
+        cy = cy < r.C - 1 ? cy : r.C - 1;
+        L.fc[k] = (uint32_t)(cy * r.C + cx);
+        // outside the grid: no pair for finite points, the tile path for non-finite ones
+        L.out[k] = (!live[k] || (isfinite(x[k]) && isfinite(y[k]))) ? (uint16_t)0 : kMixed;
+    }
+    if (quad_lds) {
+        // LDS quad level first; only points in non-uniform quads gather their sub-block (the
+        // others read sub[0], one shared line, so they cost no L2 request)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint16_t q = quad_lds[qi[k]];
+            if (L.in[k] && q != kMixed) {
+                L.out[k] = q;
+                L.in[k] = false;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) L.e[k] = r.sub[L.in[k] ? L.si[k] : 0];
+    } else {
+        // branch-free gathers (index 0 for points outside the grid), so the four issue together
+#pragma unroll
+        for (int k = 0; k < 4; k++) L.e[k] = r.sub[L.si[k]];
+    }
+}
+MOSAIC_HD void raster_gather4(const PointRaster& r, Lookup4& L) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const size_t bi = (L.e[k] & kRasterBlock) ? (size_t)(L.e[k] & ~kRasterBlock) * (size_t)(r.C * r.C) + L.fc[k] : 0;
+        L.b[k] = r.blocks[bi];
+    }
+}
+MOSAIC_HD void raster_select4(Lookup4& L) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (L.in[k]) L.out[k] = (L.e[k] & kRasterBlock) ? L.b[k] : (uint16_t)L.e[k];
+}
+MOSAIC_HD void raster_finish4(const PointRaster& r, Lookup4& L) {
+    raster_gather4(r, L);
+    raster_select4(L);
+}
 
 // Raster code of (x, y): grid origin (x0, y0) shared with the tile grid.
 MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, double x, double y) {
@@ -158,6 +227,8 @@ struct Builder {
     int S = 0, C = 0;
     std::vector<uint32_t> sub;
     std::vector<uint16_t> blocks;
+    std::vector<uint16_t> quad;  // quad level (empty: none)
+    int qshift = 0, qnx = 0, qny = 0;
     int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0;
     // Chip access for the raster classification (host memory)
     struct ChipSource {

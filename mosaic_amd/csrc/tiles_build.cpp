@@ -131,7 +131,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     std::atomic<int64_t> next(0), pure(0), mixed(0), cmixed(0);
 
     auto work = [&]() {
-        std::vector<P2> lat;  // (N + 1)^2 lattice images
+        std::vector<P2> lat;  // (S + 1)^2 sub-block corner images
         std::vector<Hex> hexes;
         std::vector<int> cand, cand2;
         std::vector<int32_t> ans, ah;
@@ -145,15 +145,18 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
             const int ti = t % nx, tj = t / nx;
             const int face = (int)(tr.dims & 0xffu), wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
             const double lon0 = grid.x0 + ti * tw, lat0 = grid.y0 + tj * th;
-            // lattice images on the tile's face
-            lat.resize((size_t)(N + 1) * (N + 1));
-            for (int j = 0; j <= N; j++)
-                for (int i = 0; i <= N; i++) {
-                    double px, py, pz, vx, vy, b;
-                    h3::fast_unit(lat0 + th * j / N, lon0 + tw * i / N, &px, &py, &pz);
-                    h3::fast_plane(px, py, pz, face, res_, &vx, &vy, &b);
-                    lat[(size_t)j * (N + 1) + i] = P2{vx, vy};
-                }
+            // lattice images on the tile's face: sub-block corners now, cell corners of a
+            // sub-block only when it needs its cells
+            auto image = [&](int i, int j) -> P2 {
+                double px, py, pz, vx, vy, b;
+                h3::fast_unit(lat0 + th * j / N, lon0 + tw * i / N, &px, &py, &pz);
+                h3::fast_plane(px, py, pz, face, res_, &vx, &vy, &b);
+                return P2{vx, vy};
+            };
+            lat.resize((size_t)(S + 1) * (S + 1));
+            for (int j = 0; j <= S; j++)
+                for (int i = 0; i <= S; i++) lat[(size_t)j * (S + 1) + i] = image(i * C, j * C);
+            std::vector<P2> clat((size_t)(C + 1) * (C + 1));
             // window hexagons
             hexes.assign((size_t)wa * wb, Hex());
             for (int ra = 0; ra < wa; ra++)
@@ -182,11 +185,10 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
             const double cell_deg_x = tw / N, cell_deg_y = th / N;
             // classification of the lattice rectangle [i0, i1] x [j0, j1] (lattice indices)
             // with candidate hexagons `cin` -> code; `cout` receives the candidates it meets
-            auto classify = [&](int i0, int j0, int i1, int j1, const std::vector<int>& cin, std::vector<int>& cout,
-                                bool& edges_near) -> uint16_t {
+            // (fine-lattice corners i0..i1, j0..j1; q = their images, counter-clockwise)
+            auto classify = [&](int i0, int j0, int i1, int j1, const P2* q, const std::vector<int>& cin,
+                                std::vector<int>& cout, bool& edges_near) -> uint16_t {
                 edges_near = false;
-                P2 q[4] = {lat[(size_t)j0 * (N + 1) + i0], lat[(size_t)j0 * (N + 1) + i1],
-                           lat[(size_t)j1 * (N + 1) + i1], lat[(size_t)j1 * (N + 1) + i0]};
                 double frac = std::max((double)(i1 - i0), (double)(j1 - j0)) / N;
                 double tol = 4.0 * dev * frac * frac + 1e-7;
                 cout.clear();
@@ -234,18 +236,29 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
             for (int sj = 0; sj < S; sj++)
                 for (int si = 0; si < S; si++) {
                     bool en;
-                    uint16_t code = classify(si * C, sj * C, (si + 1) * C, (sj + 1) * C, all, cand, en);
+                    const P2 qs[4] = {lat[(size_t)sj * (S + 1) + si], lat[(size_t)sj * (S + 1) + si + 1],
+                                      lat[(size_t)(sj + 1) * (S + 1) + si + 1], lat[(size_t)(sj + 1) * (S + 1) + si]};
+                    uint16_t code = classify(si * C, sj * C, (si + 1) * C, (sj + 1) * C, qs, all, cand, en);
                     uint32_t entry;
                     if (code != kMixed) {
                         entry = code;
                         pure++;
                     } else {
                         mixed++;
+                        for (int cj = 0; cj <= C; cj++)
+                            for (int ci = 0; ci <= C; ci++)
+                                clat[(size_t)cj * (C + 1) + ci] =
+                                    (ci % C == 0 && cj % C == 0)
+                                        ? lat[(size_t)(sj + cj / C) * (S + 1) + si + ci / C]
+                                        : image(si * C + ci, sj * C + cj);
                         bool same = true;
                         for (int cj = 0; cj < C; cj++)
                             for (int ci = 0; ci < C; ci++) {
                                 int i0 = si * C + ci, j0 = sj * C + cj;
-                                uint16_t cc = classify(i0, j0, i0 + 1, j0 + 1, cand, cand2, en);
+                                const P2 qc[4] = {clat[(size_t)cj * (C + 1) + ci], clat[(size_t)cj * (C + 1) + ci + 1],
+                                                  clat[(size_t)(cj + 1) * (C + 1) + ci + 1],
+                                                  clat[(size_t)(cj + 1) * (C + 1) + ci]};
+                                uint16_t cc = classify(i0, j0, i0 + 1, j0 + 1, qc, cand, cand2, en);
                                 cellc[(size_t)cj * C + ci] = cc;
                                 if (cc == kMixed) cmixed++;
                                 same = same && cc == cellc[0];
@@ -300,6 +313,29 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     n_sub_pure = pure.load();
     n_sub_mixed = mixed.load();
     n_cell_mixed = cmixed.load();
+    // quad level: the smallest power-of-two group of sub-blocks whose table fits kQuadMax entries
+    quad.clear();
+    qshift = 0;
+    while (qshift < 16 && ((NX + (1 << qshift) - 1) >> qshift) * ((NY + (1 << qshift) - 1) >> qshift) > kQuadMax)
+        qshift++;
+    if (qshift < 16) {
+        qnx = (int)((NX + (1 << qshift) - 1) >> qshift);
+        qny = (int)((NY + (1 << qshift) - 1) >> qshift);
+        quad.assign((size_t)qnx * qny, kMixed);
+        std::vector<uint8_t> seen((size_t)qnx * qny, 0);
+        for (int64_t j = 0; j < NY; j++)
+            for (int64_t i = 0; i < NX; i++) {
+                const uint32_t e = sub[(size_t)(j * NX + i)];
+                const size_t q = (size_t)((j >> qshift) * qnx + (i >> qshift));
+                const uint16_t code = (e & kRasterBlock) ? kMixed : (uint16_t)e;
+                if (!seen[q]) {
+                    seen[q] = 1;
+                    quad[q] = code;
+                } else if (quad[q] != code) {
+                    quad[q] = kMixed;
+                }
+            }
+    }
     return true;
 }
 

@@ -110,16 +110,46 @@ int main(int argc, char** argv) {
         pr.nx = tb.grid.nx * S;
         pr.ny = tb.grid.ny * S;
         pr.C = Cc;
+        pr.quad = tb.quad.empty() ? nullptr : tb.quad.data();
+        pr.qnx = tb.qnx;
+        pr.qny = tb.qny;
+        pr.qshift = tb.qshift;
     }
     long rbad = 0, rpure = 0, rmixed = 0, uni = 0, uni_mixed = 0;
     double bx0 = argc > 9 ? atof(argv[6]) : 0, by0 = argc > 9 ? atof(argv[7]) : 0;
     double bx1 = argc > 9 ? atof(argv[8]) : 0, by1 = argc > 9 ? atof(argv[9]) : 0;
+    long st_out = 0, st_skip = 0, st_sub = 0, st_quad = 0;
+    int Q = argc > 10 ? atoi(argv[10]) : 4;
+    // quad level: Q x Q sub-blocks with one shared pure code
+    std::vector<uint8_t> quad_pure;
+    if (rok) {
+        int qx = (pr.nx + Q - 1) / Q, qy = (pr.ny + Q - 1) / Q;
+        quad_pure.assign((size_t)qx * qy, 1);
+        for (int j = 0; j < pr.ny; j++)
+            for (int i = 0; i < pr.nx; i++) {
+                uint32_t e = pr.sub[(size_t)j * pr.nx + i];
+                uint32_t e0 = pr.sub[(size_t)(j / Q * Q) * pr.nx + (i / Q * Q)];
+                if ((e & tiles::kRasterBlock) || e != e0) quad_pure[(size_t)(j / Q) * qx + i / Q] = 0;
+            }
+    }
     if (rok && argc > 9)  // raster hit statistics for uniform points over a bbox
         for (long k = 0; k < npts; k++) {
             double x = bx0 + (bx1 - bx0) * u(rng), y = by0 + (by1 - by0) * u(rng);
             uni++;
             if (tiles::raster_code(pr, tb.grid.x0, tb.grid.y0, x, y) == tiles::kMixed) uni_mixed++;
+            double gx = (x - tb.grid.x0) * pr.sx, gy = (y - tb.grid.y0) * pr.sy;
+            if (!(gx >= 0 && gx < pr.nx && gy >= 0 && gy < pr.ny)) {
+                st_out++;
+                continue;
+            }
+            int ix = (int)gx, iy = (int)gy;
+            if (tb.tile_idx[(size_t)(iy / tb.S) * tb.grid.nx + ix / tb.S] == tiles::kSkip) st_skip++;
+            if (!(pr.sub[(size_t)iy * pr.nx + ix] & tiles::kRasterBlock)) st_sub++;
+            if (quad_pure[(size_t)(iy / Q) * ((pr.nx + Q - 1) / Q) + ix / Q]) st_quad++;
         }
+    if (uni)
+        fprintf(stderr, "uniform: outside %.4f skip-tile %.4f pure-sub %.4f pure-quad(%d) %.4f\n", (double)st_out / uni,
+                (double)st_skip / uni, (double)st_sub / uni, Q, (double)st_quad / uni);
     const tiles::Grid& g = tb.grid;
     double w = g.nx / g.sx, h = g.ny / g.sy;
     long bad = 0, checked = 0, skipped = 0, full = 0, unc = 0, miss = 0;
@@ -130,6 +160,18 @@ int main(int argc, char** argv) {
         int64_t want_slot = slot_of(want);
         if (rok) {
             uint16_t rc = tiles::raster_code(pr, g.x0, g.y0, x, y);
+            // the kernel's batched lookup (with and without the quad level) agrees with it
+            double xs[4] = {x, x, x, x}, ys[4] = {y, y, y, y};
+            bool lv[4] = {true, true, true, true};
+            tiles::Lookup4 L1, L2;
+            tiles::raster_issue4(pr, g.x0, g.y0, xs, ys, lv, L1, tb.quad.empty() ? nullptr : tb.quad.data());
+            tiles::raster_finish4(pr, L1);
+            tiles::raster_issue4(pr, g.x0, g.y0, xs, ys, lv, L2, nullptr);
+            tiles::raster_finish4(pr, L2);
+            if (L1.out[0] != rc || L2.out[0] != rc) {
+                rbad++;
+                if (rbad < 10) fprintf(stderr, "batched lookup: %u %u vs %u\n", L1.out[0], L2.out[0], rc);
+            }
             if (rc == tiles::kMixed) {
                 rmixed++;
             } else {

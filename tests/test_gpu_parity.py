@@ -353,7 +353,7 @@ def test_join_tiled_nyc_zones_match_oracle(h3ctx, zones):
     table.close()
 
 
-@pytest.mark.parametrize("sub,cell", [(4, 2), (32, 16)])
+@pytest.mark.parametrize("sub,cell", [(4, 2), (16, 8)])
 def test_join_point_raster_sizes(h3ctx, zones, sub, cell):
     """Other point-raster sizes (coarse: most points take the tile path; fine) give the oracle's
     counts on clustered points (the C3 mixture) at res 10."""
@@ -368,8 +368,8 @@ def test_join_point_raster_sizes(h3ctx, zones, sub, cell):
         table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 10,
                                  n_polygons=len(ids))
     finally:
-        h3ctx.set_option("raster_sub", 16)
-        h3ctx.set_option("raster_cell", 8)
+        h3ctx.set_option("raster_sub", 32)
+        h3ctx.set_option("raster_cell", 16)
     t = table.tiles()
     assert t["raster"] == 1 and t["raster_sub"] == sub and t["raster_cell"] == cell, t
     x, y = quickstart_points(sub_zones, 400_000, sigma=0.002, seed=31)

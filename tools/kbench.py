@@ -24,10 +24,12 @@ def main():
     p.add_argument("--clustered", action="store_true")
     p.add_argument("--rasters", type=int, nargs="*", default=[8, 16, 32])
     p.add_argument("--lane-edges", type=int, nargs="*", default=[0, 4, 8])
+    p.add_argument("--groups", type=int, nargs="*", default=[1], help="stream_groups values")
     p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*",
                    default=[(1, 1), (1, 0), (0, 0)], help="TILES:POINT_RASTER pairs")
     p.add_argument("--point-raster", type=lambda v: tuple(int(q) for q in v.split("x")), nargs="*",
                    default=[(16, 8)], help="point raster sizes SUBxCELL")
+    p.add_argument("--all-core", action="store_true", help="also time every chip marked core")
     p.add_argument("--legacy", action="store_true", help="also time the coop / slab strategies")
     args = p.parse_args()
     import torch
@@ -86,14 +88,18 @@ def main():
     variants = []
     for tiles, praster in args.modes:
         for sub, cell in (args.point_raster if praster else [(16, 8)]):
-            tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}" if praster else "")
-            variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, sub, cell))
-            for r in args.rasters:
-                for le in args.lane_edges:
-                    variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster, sub, cell))
+            for grp in args.groups:
+                tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}_g{grp}" if praster else "")
+                if args.all_core:
+                    variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, sub, cell, grp))
+                for r in args.rasters:
+                    for le in args.lane_edges:
+                        variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster, sub, cell,
+                                         grp))
     if args.legacy:
-        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, 16, 8), ("join_full_slab", False, 2, 16, 8, 0, 0, 16, 8)]
-    for name, core, mode, raster, lane_edges, tiles, praster, sub, cell in variants:
+        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, 16, 8, 1), ("join_full_slab", False, 2, 16, 8, 0, 0, 16, 8, 1)]
+    for name, core, mode, raster, lane_edges, tiles, praster, sub, cell, grp in variants:
+        ctx.set_option("stream_groups", grp)
         ctx.set_option("tiles", tiles)
         ctx.set_option("point_raster", praster)
         ctx.set_option("raster_sub", sub)

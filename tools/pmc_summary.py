@@ -1,0 +1,26 @@
+"""Summarise rocprofv3 counter CSVs (tools/pmc_stream.sh output): mean per launch, per kernel."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def main():
+    root = sys.argv[1]
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+        per = defaultdict(float)
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = (row["Kernel_Name"].split("(")[0], row["Dispatch_Id"], row["Counter_Name"])
+                per[k] += float(row["Counter_Value"])
+        for (kern, _, ctr), v in per.items():
+            if "k_join" in kern:
+                vals[kern][ctr].append(v)
+    out = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in vals.items()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
