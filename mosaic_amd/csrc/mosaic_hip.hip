@@ -91,6 +91,8 @@ struct JoinArgs {
     int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
     uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
     unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)
+    int probe_mask;                   // measurement only (option "probe_mask"): 1 = k_join_mixed skips
+                                      // the chip loop, 2 = it also skips the cell lookup
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
     unsigned long long* amb_queue;  // rows for the exact H3 pass
@@ -822,6 +824,8 @@ __global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
             tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L[g], quad);
         }
 #pragma unroll
+        for (int g = 0; g < G; g++) tiles::raster_mid4(a.praster, L[g]);
+#pragma unroll
         for (int g = 0; g < G; g++) tiles::raster_gather4(a.praster, L[g]);
         if (VEC) {
             // the next iteration's coordinates, issued after this iteration's gathers (vmcnt
@@ -875,30 +879,92 @@ __global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
     counts_flush<LDS_COUNTS>(a, lds, 0u);
 }
 
-// Rows of mixed raster cells (the dense queue mixq): tile path (certified hexagon -> window ->
-// chips) and the raster chip loop, one queued row per lane.
-template <bool LDS_COUNTS, bool PAIRS>
+// Rows of mixed raster cells (the dense queue mixq), R rows per lane: their chip ranges are found
+// stage by stage for all R rows at once (coordinate gathers, tile codes, tile records, projection,
+// window entries, hash entries -- R independent chains in flight per lane instead of one), then the
+// raster chip loop runs once per row slot (wave-cooperative, so wave-uniform).  Rows the fast path
+// cannot certify, kFull tiles and window misses take tiled_cell (the generic path).
+template <bool LDS_COUNTS, bool PAIRS, int R>
 __global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     __shared__ SlabItem items[4][16];
     counts_init<LDS_COUNTS>(a, lds);
     unsigned int tests = 0;
+    const int lane = (int)(threadIdx.x & 63);
     const int wv = (int)(threadIdx.x >> 6) & 3;
     const unsigned long long total = *a.mixq_count;
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total;
-         base += stride) {
-        const unsigned long long t = base + (threadIdx.x & 63);
-        double x = 0.0, y = 0.0;
-        int64_t i = -1;
-        uint32_t cur = 0, end = 0;
-        if (t < total) {
-            i = a.row_lo + (int64_t)a.mixq[t];
-            x = a.x[i];
-            y = a.y[i];
-            tiled_cell(a, i, x, y, tiles::tile_of(a.tgrid, a.tile_idx, x, y), cur, end);
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x * R;
+    // wave-uniform loop: the wave's rows are [w0, w0 + 64 R), slot k of lane l is w0 + k * 64 + l
+    for (unsigned long long w0 = ((unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * R; w0 < total;
+         w0 += stride) {
+        int64_t row[R];
+        double x[R], y[R];
+        bool live[R];
+        uint32_t code[R], cur[R], end[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const unsigned long long t = w0 + (unsigned long long)(k * 64 + lane);
+            live[k] = t < total;
+            row[k] = a.row_lo + (live[k] ? (int64_t)a.mixq[t] : 0);
         }
-        raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items[wv]);
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            x[k] = a.x[row[k]];
+            y[k] = a.y[row[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < R; k++) code[k] = tiles::tile_of(a.tgrid, a.tile_idx, x[k], y[k]);
+        tiles::TileRec rec[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) rec[k] = a.tile_rec[code[k] >= 2 ? code[k] - 2 : 0];
+        uint32_t ent_idx[R];
+        bool fast[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            fast[k] = false;
+            ent_idx[k] = 0;
+            if (!(a.probe_mask & 2) && live[k] && code[k] >= 2) {
+                const int face = (int)(rec[k].dims & 0xffu);
+                const int wa = (int)((rec[k].dims >> 8) & 0xfffu), wb = (int)(rec[k].dims >> 20);
+                double px, py, pz, vx, vy, best;
+                h3::fast_unit(y[k], x[k], &px, &py, &pz);
+                h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
+                int ba, bb;
+                if (h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
+                    const int ra = ba - rec[k].a0, rb = bb - rec[k].b0;
+                    if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
+                        fast[k] = true;
+                        ent_idx[k] = rec[k].off + (uint32_t)(ra * wb + rb);
+                    }
+                }
+            }
+        }
+        uint32_t ent[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) ent[k] = a.tile_ent[ent_idx[k]];
+        HashEntry he[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) he[k] = a.table[fast[k] && ent[k] ? ent[k] - 1 : 0];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            cur[k] = end[k] = 0;
+            if (!live[k] || (a.probe_mask & 2)) continue;
+            if (fast[k]) {
+                if (ent[k]) {
+                    cur[k] = he[k].first;
+                    end[k] = he[k].first + he[k].count;
+                }
+            } else {
+                tiled_cell(a, row[k], x[k], y[k], code[k], cur[k], end[k]);
+            }
+            if (a.probe_mask & 1) {
+                tests += end[k] - cur[k];
+                cur[k] = end[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < R; k++)
+            raster_chips<LDS_COUNTS, PAIRS>(a, live[k] ? row[k] : -1, cur[k], end[k], x[k], y[k], tests, lds, items[wv]);
     }
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
@@ -1054,9 +1120,13 @@ struct mosaic_ctx {
     int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
     int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
     int raster_sub = 32;  // point raster: sub-blocks per tile side
-    int raster_cell = 16; // point raster: cells per sub-block side
+    int raster_mid = 1;   // point raster: mid cells per sub-block side (1: no mid level)
+    int raster_cell = 16; // point raster: leaf cells per mid cell side
     int raster_quad = 1;  // point raster: LDS quad level
     int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
+    int mixed_blocks_per_cu = 8;  // k_join_mixed grid
+    int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
+    int probe_mask = 0;     // measurement only: see JoinArgs::probe_mask (results are wrong when set)
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
@@ -1141,11 +1211,11 @@ struct mosaic_chips {
     int64_t tile_stats[6] = {0, 0, 0, 0, 0, 0};  // nx, ny, records, entries, kFull tiles, rings
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
-    DevBuf rsub, rblocks, rquad;
+    DevBuf rsub, rmid, rblocks, rquad;
     int64_t raster_stats[5] = {0, 0, 0, 0, 0};    // S, C, pure sub-blocks, mixed sub-blocks, mixed cells
     void release_all() {
         for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rblocks, &rquad})
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad})
             b->release();
         store.release();
     }
@@ -1276,11 +1346,23 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "raster_sub") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "raster_sub must be in [1, 64]");
         c->raster_sub = (int)v;
+    } else if (k == "probe_mask") {
+        if (v < 0 || v > 3) return fail(MOSAIC_E_ARG, "probe_mask must be in [0, 3]");
+        c->probe_mask = (int)v;
+    } else if (k == "mixed_rows") {
+        if (v != 1 && v != 2 && v != 4) return fail(MOSAIC_E_ARG, "mixed_rows must be 1, 2 or 4");
+        c->mixed_rows = (int)v;
+    } else if (k == "mixed_blocks_per_cu") {
+        if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "mixed_blocks_per_cu must be in [1, 64]");
+        c->mixed_blocks_per_cu = (int)v;
     } else if (k == "stream_groups") {
         if (v != 1 && v != 2) return fail(MOSAIC_E_ARG, "stream_groups must be 1 or 2");
         c->stream_groups = (int)v;
     } else if (k == "raster_quad") {
         c->raster_quad = v ? 1 : 0;
+    } else if (k == "raster_mid") {
+        if (v < 1 || v > 16) return fail(MOSAIC_E_ARG, "raster_mid must be in [1, 16]");
+        c->raster_mid = (int)v;
     } else if (k == "raster_cell") {
         if (v < 1 || v > 32) return fail(MOSAIC_E_ARG, "raster_cell must be in [1, 32]");
         c->raster_cell = (int)v;
@@ -1732,17 +1814,21 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
                                            gb.part_ring.data(), gb.geom_part.data(), gb.geom_bbox.data()};
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-                if (tb.build_raster(src, c->raster_sub, c->raster_cell, threads)) {
-                    size_t r0 = tb.sub.size() * 4, r1 = tb.blocks.size() * 2;
-                    if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1))) {
+                if (tb.build_raster(src, c->raster_sub, c->raster_mid, c->raster_cell, threads)) {
+                    size_t r0 = tb.sub.size() * 4, r1 = tb.blocks.size() * 2, rm = tb.mid.size() * 4;
+                    if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
                         ch->release_all();
                         delete ch;
                         return rc;
                     }
                     HIP_TRY(hipMemcpy(ch->rsub.p, tb.sub.data(), r0, hipMemcpyHostToDevice));
+                    HIP_TRY(hipMemcpy(ch->rmid.p, tb.mid.data(), rm, hipMemcpyHostToDevice));
                     HIP_TRY(hipMemcpy(ch->rblocks.p, tb.blocks.data(), r1, hipMemcpyHostToDevice));
+                    total += rm;
                     ch->raster_ok = true;
                     ch->praster.sub = (const uint32_t*)ch->rsub.p;
+                    ch->praster.mid = (const uint32_t*)ch->rmid.p;
+                    ch->praster.M = tb.M;
                     ch->praster.blocks = (const uint16_t*)ch->rblocks.p;
                     ch->praster.sx = tb.grid.sx * tb.S;
                     ch->praster.sy = tb.grid.sy * tb.S;
@@ -1809,6 +1895,7 @@ int mosaic_chip_table_tiles(const mosaic_chips* ch, int64_t* o) {
     for (int k = 0; k < 6; k++) o[k + 1] = ch->tile_stats[k];
     o[7] = ch->raster_ok ? 1 : 0;
     for (int k = 0; k < 5; k++) o[k + 8] = ch->raster_stats[k];
+    o[13] = ch->praster.M;
     return MOSAIC_OK;
 }
 
@@ -1876,6 +1963,7 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.tile_ent = (const uint32_t*)ch->tile_ent.p;
     a.praster = ch->praster;
     a.row_lo = 0;
+    a.probe_mask = c->probe_mask;
     a.mixq = nullptr;
     a.mixq_count = sc + 4;
     a.counts = dcounts;
@@ -1941,14 +2029,24 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
 #undef MOSAIC_STREAM
                 HIP_TRY(hipGetLastError());
                 if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
-                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>(gs, (int64_t)c->n_cu * c->blocks_per_cu));
+                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>(gs, (int64_t)c->n_cu * c->mixed_blocks_per_cu));
 #define MOSAIC_MIXED(KERNEL, SHM) \
     hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac)
                 hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
                 if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
-                if (pairs) MOSAIC_MIXED((k_join_mixed<false, true>), 0);
-                else if (lds) MOSAIC_MIXED((k_join_mixed<true, false>), shm);
-                else MOSAIC_MIXED((k_join_mixed<false, false>), 0);
+                if (c->mixed_rows == 4) {
+                    if (pairs) MOSAIC_MIXED((k_join_mixed<false, true, 4>), 0);
+                    else if (lds) MOSAIC_MIXED((k_join_mixed<true, false, 4>), shm);
+                    else MOSAIC_MIXED((k_join_mixed<false, false, 4>), 0);
+                } else if (c->mixed_rows == 2) {
+                    if (pairs) MOSAIC_MIXED((k_join_mixed<false, true, 2>), 0);
+                    else if (lds) MOSAIC_MIXED((k_join_mixed<true, false, 2>), shm);
+                    else MOSAIC_MIXED((k_join_mixed<false, false, 2>), 0);
+                } else {
+                    if (pairs) MOSAIC_MIXED((k_join_mixed<false, true, 1>), 0);
+                    else if (lds) MOSAIC_MIXED((k_join_mixed<true, false, 1>), shm);
+                    else MOSAIC_MIXED((k_join_mixed<false, false, 1>), 0);
+                }
 #undef MOSAIC_MIXED
                 HIP_TRY(hipGetLastError());
                 if (mstop) HIP_TRY(hipEventRecord(mstop, c->stream));

@@ -28,7 +28,10 @@ def main():
     p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*",
                    default=[(1, 1), (1, 0), (0, 0)], help="TILES:POINT_RASTER pairs")
     p.add_argument("--point-raster", type=lambda v: tuple(int(q) for q in v.split("x")), nargs="*",
-                   default=[(16, 8)], help="point raster sizes SUBxCELL")
+                   default=[(16, 2, 16)], help="point raster sizes SUBxMIDxCELL")
+    p.add_argument("--mixed-rows", type=int, nargs="*", default=[], help="k_join_mixed rows per lane to time")
+    p.add_argument("--mixed-bpc", type=int, nargs="*", default=[], help="k_join_mixed blocks per CU to time")
+    p.add_argument("--probe-mixed", action="store_true", help="time k_join_mixed without its chip loop / cell")
     p.add_argument("--all-core", action="store_true", help="also time every chip marked core")
     p.add_argument("--legacy", action="store_true", help="also time the coop / slab strategies")
     args = p.parse_args()
@@ -87,19 +90,21 @@ def main():
     ftab.close()
     variants = []
     for tiles, praster in args.modes:
-        for sub, cell in (args.point_raster if praster else [(16, 8)]):
+        for sub, mid, cell in (args.point_raster if praster else [(16, 2, 16)]):
             for grp in args.groups:
-                tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}_g{grp}" if praster else "")
+                tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{mid}x{cell}_g{grp}" if praster else "")
                 if args.all_core:
-                    variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, sub, cell, grp))
+                    variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, (sub, mid, cell), grp))
                 for r in args.rasters:
                     for le in args.lane_edges:
-                        variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster, sub, cell,
-                                         grp))
+                        variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster,
+                                         (sub, mid, cell), grp))
     if args.legacy:
-        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, 16, 8, 1), ("join_full_slab", False, 2, 16, 8, 0, 0, 16, 8, 1)]
-    for name, core, mode, raster, lane_edges, tiles, praster, sub, cell, grp in variants:
+        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, (16, 2, 16), 1),
+                     ("join_full_slab", False, 2, 16, 8, 0, 0, (16, 2, 16), 1)]
+    for name, core, mode, raster, lane_edges, tiles, praster, (sub, mid, cell), grp in variants:
         ctx.set_option("stream_groups", grp)
+        ctx.set_option("raster_mid", mid)
         ctx.set_option("tiles", tiles)
         ctx.set_option("point_raster", praster)
         ctx.set_option("raster_sub", sub)
@@ -122,7 +127,32 @@ def main():
         st = ctx.last_stats()
         ctx.set_option("async", 1)
         tl = table.tiles()
-        print(json.dumps({"variant": name, "ms": t, "kernels_ms": kt, "pts_per_s": n / t * 1e3, **st,
+        probes = {}
+        for mr in args.mixed_rows:
+            ctx.set_option("mixed_rows", mr)
+            ctx.set_option("timing", 2)
+            for _ in range(3):
+                ctx.pip_join_count(table, x, y, out=counts)
+            probes[f"mixed_rows{mr}_ms"] = round(float(np.median(ctx.kernel_times()[1::2])), 4)
+            ctx.set_option("timing", 0)
+        ctx.set_option("mixed_rows", 4)
+        for mb in args.mixed_bpc:
+            ctx.set_option("mixed_blocks_per_cu", mb)
+            ctx.set_option("timing", 2)
+            for _ in range(3):
+                ctx.pip_join_count(table, x, y, out=counts)
+            probes[f"mixed_bpc{mb}_ms"] = round(float(np.median(ctx.kernel_times()[1::2])), 4)
+            ctx.set_option("timing", 0)
+        ctx.set_option("mixed_blocks_per_cu", 8)
+        if args.probe_mixed and praster:
+            for pm in (1, 3):
+                ctx.set_option("probe_mask", pm)
+                ctx.set_option("timing", 2)
+                ctx.pip_join_count(table, x, y, out=counts)
+                probes[f"mixed_probe{pm}_ms"] = round(float(ctx.kernel_times()[1]), 4)
+                ctx.set_option("timing", 0)
+            ctx.set_option("probe_mask", 0)
+        print(json.dumps({"variant": name, "ms": t, "kernels_ms": kt, **probes, "pts_per_s": n / t * 1e3, **st,
                           "build_s": round(build_s, 2), "raster": {k: tl[k] for k in ("raster", "pure_sub_blocks", "mixed_sub_blocks", "mixed_cells")}}))
         table.close()
 

@@ -38,11 +38,36 @@ __global__ void __launch_bounds__(256) k_gather(const uint32_t* t, uint32_t mask
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// all lanes gather (random rows of a table of `mask + 1` dwords) while streaming `stream` bytes per
+// lane-iteration (0 or 32: two 16-byte non-temporal loads) of a large array, like k_join_stream
+typedef double v2d __attribute__((ext_vector_type(2)));
+__global__ void __launch_bounds__(256) k_gather_stream(const uint32_t* t, uint32_t mask, int iters, const double* big,
+                                                       size_t big_n, int stream, uint32_t* out) {
+    uint32_t acc = 0, s = blockIdx.x * 256 + threadIdx.x;
+    double dacc = 0.0;
+    size_t pos = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    const size_t step = (size_t)gridDim.x * 256 * 4;
+    for (int it = 0; it < iters; it++) {
+        if (stream) {
+            v2d a = __builtin_nontemporal_load((const v2d*)(big + pos));
+            v2d b = __builtin_nontemporal_load((const v2d*)(big + pos + 2));
+            dacc += a.x + b.y;
+            pos += step;
+            if (pos + 4 > big_n) pos = 0;
+        }
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = t[hash32(s * 4 + k + it * 0x9e3779b9u) & mask];
+        acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    if (acc == 0x12345678u || dacc == 1.2345) out[0] = acc;
+}
+
 int main() {
     const size_t sizes[2] = {(size_t)1 << 19, (size_t)1 << 23};  // 2 MiB, 32 MiB tables
     uint32_t *t, *out;
-    hipMalloc(&t, sizes[1] * 4);
-    hipMemset(t, 1, sizes[1] * 4);
+    hipMalloc(&t, ((size_t)1 << 24) * 4);
+    hipMemset(t, 1, ((size_t)1 << 24) * 4);
     hipMalloc(&out, 4);
     int cus = 256;
     const int blocks = cus * 8, iters = 256;
@@ -71,6 +96,29 @@ int main() {
                        sizes[si] * 4 >> 20, mode ? "masked" : "dummy", act, best,
                        best * 1e-3 * 2.4e9 / instr_per_cu);
             }
+        }
+    }
+    // cost curve over table size, without and with a concurrent streaming read
+    double* big;
+    const size_t big_n = (size_t)1 << 28;  // 2 GiB of doubles
+    hipMalloc(&big, big_n * 8);
+    hipMemset(big, 0, big_n * 8);
+    for (int stream = 0; stream < 2; stream++) {
+        for (int lg = 18; lg <= 24; lg++) {  // 1 MiB .. 64 MiB
+            float best = 1e30f;
+            for (int rep = 0; rep < 4; rep++) {
+                hipEventRecord(a);
+                hipLaunchKernelGGL(k_gather_stream, dim3(blocks), dim3(256), 0, 0, t, (1u << lg) - 1, iters, big, big_n,
+                                   stream, out);
+                hipEventRecord(b);
+                hipEventSynchronize(b);
+                float ms;
+                hipEventElapsedTime(&ms, a, b);
+                if (rep && ms < best) best = ms;
+            }
+            double lanes_per_cu = 32.0 * iters * 4 * 64;
+            printf("table %3d MiB stream %d: %.3f ms  %.2f cyc/lane/CU\n", (1 << lg) * 4 >> 20, stream, best,
+                   best * 1e-3 * 2.4e9 / lanes_per_cu);
         }
     }
     return 0;
