@@ -80,9 +80,9 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * "pip_mode" (3 raster, 2 slab, 1 ring-cooperative, 0 lane-per-point contains strategy), "raster"
  * (raster cells per chip side, for tables built afterwards), "lane_edges", "tiles" (0/1: H3 tile
  * directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
- * raster over the tile directory, likewise), "raster_sub" / "raster_mid" / "raster_cell" (its
- * sub-blocks per tile side, mid cells per sub-block side and leaf cells per mid cell side, for tables
- * built afterwards), "raster_quad" (0/1: its LDS level), "stream_groups" (1/2). */
+ * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
+ * side, a power of two, and cells per sub-block side, for tables built afterwards), "raster_quad"
+ * (0/1: its LDS level), "stream_groups" (1/2), "mixed_rows" (1/2/4), "mixed_blocks_per_cu". */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* The hipStream_t work is enqueued on (owned by the context unless set). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
@@ -123,12 +123,11 @@ int mosaic_chip_table_destroy(mosaic_chips* chips);
 /* out8: n_chips, n_cells, n_border, n_vertices, n_rings, device_bytes, hash_capacity, n_polygons */
 int mosaic_chip_table_info(const mosaic_chips* chips, int64_t* out8);
 
-/* H3 tile directory of the table (built when option "tiles" = 1, the default): out14 = built (0/1),
+/* H3 tile directory of the table (built when option "tiles" = 1, the default): out13 = built (0/1),
  * tiles along lon, tiles along lat, tile records, window entries, tiles on the generic path, rings;
  * point raster (option "point_raster" = 1, the default) built (0/1), sub-blocks per tile side,
- * leaf cells per mid cell side, pure sub-blocks, mixed sub-blocks, mixed leaf cells, mid cells per
- * sub-block side. */
-int mosaic_chip_table_tiles(const mosaic_chips* chips, int64_t* out14);
+ * cells per sub-block side, pure sub-blocks, mixed sub-blocks, mixed cells. */
+int mosaic_chip_table_tiles(const mosaic_chips* chips, int64_t* out13);
 /* out4 = lon, lat of the tile grid origin and tiles per degree along lon, lat (tile i covers
  * [x0 + i / sx, x0 + (i + 1) / sx)). */
 int mosaic_chip_table_tile_grid(const mosaic_chips* chips, double* out4);

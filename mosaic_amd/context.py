@@ -166,10 +166,10 @@ class ChipTable:
 
     def tiles(self):
         """The H3 tile directory of this table (tiles.h): whether it was built, and its size."""
-        out = np.zeros(14, np.int64)
+        out = np.zeros(13, np.int64)
         N.check(N.lib().mosaic_chip_table_tiles(self.handle, N.ptr(out)))
         keys = ["built", "nx", "ny", "records", "entries", "full_tiles", "rings", "raster", "raster_sub",
-                "raster_cell", "pure_sub_blocks", "mixed_sub_blocks", "mixed_cells", "raster_mid"]
+                "raster_cell", "pure_sub_blocks", "mixed_sub_blocks", "mixed_cells"]
         d = dict(zip(keys, (int(v) for v in out)))
         g = np.zeros(4, np.float64)
         N.check(N.lib().mosaic_chip_table_tile_grid(self.handle, N.ptr(g)))

@@ -92,7 +92,8 @@ struct JoinArgs {
     uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
     unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)
     int probe_mask;                   // measurement only (option "probe_mask"): 1 = k_join_mixed skips
-                                      // the chip loop, 2 = it also skips the cell lookup
+                                      // the chip loop, 2 = it also skips the cell lookup; k_join_stream:
+                                      // 4 = no sub-block lookups, 16 = no counting, 32 = no LDS quad
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
     unsigned long long* amb_queue;  // rows for the exact H3 pass
@@ -821,10 +822,15 @@ __global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
                     y[k] = live[k] ? a.y[r + k] : 0.0;
                 }
             }
-            tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L[g], quad);
+            tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L[g],
+                                 (a.probe_mask & 32) ? nullptr : quad);
+            if (a.probe_mask & 4) {  // measurement only: no sub-block lookups
+#pragma unroll
+                for (int k = 0; k < 4; k++) L[g].in[k] = false;
+            }
         }
 #pragma unroll
-        for (int g = 0; g < G; g++) tiles::raster_mid4(a.praster, L[g]);
+        for (int g = 0; g < G; g++) tiles::raster_base4(a.praster, L[g]);
 #pragma unroll
         for (int g = 0; g < G; g++) tiles::raster_gather4(a.praster, L[g]);
         if (VEC) {
@@ -849,7 +855,8 @@ __global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const uint16_t rc = L[g].out[k];
-                if (rc != 0 && rc != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, r + k, (uint32_t)rc - 1u, lds);
+                if (rc != 0 && rc != tiles::kMixed && !(a.probe_mask & 16))
+                    emit_hit<LDS_COUNTS, PAIRS>(a, r + k, (uint32_t)rc - 1u, lds);
                 const unsigned long long mm = __ballot(rc == tiles::kMixed);
                 if (rc == tiles::kMixed) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(r + k - a.row_lo);
                 wn += (uint32_t)__popcll(mm);
@@ -1119,9 +1126,8 @@ struct mosaic_ctx {
     int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
     int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
     int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
-    int raster_sub = 32;  // point raster: sub-blocks per tile side
-    int raster_mid = 1;   // point raster: mid cells per sub-block side (1: no mid level)
-    int raster_cell = 16; // point raster: leaf cells per mid cell side
+    int raster_sub = 32;  // point raster: sub-blocks per tile side (a power of two)
+    int raster_cell = 32; // point raster: leaf cells per sub-block side
     int raster_quad = 1;  // point raster: LDS quad level
     int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
@@ -1211,7 +1217,7 @@ struct mosaic_chips {
     int64_t tile_stats[6] = {0, 0, 0, 0, 0, 0};  // nx, ny, records, entries, kFull tiles, rings
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
-    DevBuf rsub, rmid, rblocks, rquad;
+    DevBuf rsub, rmid, rblocks, rquad;  // rmid: per-tile leaf block bases
     int64_t raster_stats[5] = {0, 0, 0, 0, 0};    // S, C, pure sub-blocks, mixed sub-blocks, mixed cells
     void release_all() {
         for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges,
@@ -1344,10 +1350,10 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "point_raster") {
         c->point_raster = v ? 1 : 0;
     } else if (k == "raster_sub") {
-        if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "raster_sub must be in [1, 64]");
+        if (v < 1 || v > 64 || (v & (v - 1))) return fail(MOSAIC_E_ARG, "raster_sub must be a power of two in [1, 64]");
         c->raster_sub = (int)v;
     } else if (k == "probe_mask") {
-        if (v < 0 || v > 3) return fail(MOSAIC_E_ARG, "probe_mask must be in [0, 3]");
+        if (v < 0 || v > 63) return fail(MOSAIC_E_ARG, "probe_mask must be in [0, 63]");
         c->probe_mask = (int)v;
     } else if (k == "mixed_rows") {
         if (v != 1 && v != 2 && v != 4) return fail(MOSAIC_E_ARG, "mixed_rows must be 1, 2 or 4");
@@ -1360,9 +1366,6 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
         c->stream_groups = (int)v;
     } else if (k == "raster_quad") {
         c->raster_quad = v ? 1 : 0;
-    } else if (k == "raster_mid") {
-        if (v < 1 || v > 16) return fail(MOSAIC_E_ARG, "raster_mid must be in [1, 16]");
-        c->raster_mid = (int)v;
     } else if (k == "raster_cell") {
         if (v < 1 || v > 32) return fail(MOSAIC_E_ARG, "raster_cell must be in [1, 32]");
         c->raster_cell = (int)v;
@@ -1814,21 +1817,22 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
                                            gb.part_ring.data(), gb.geom_part.data(), gb.geom_bbox.data()};
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-                if (tb.build_raster(src, c->raster_sub, c->raster_mid, c->raster_cell, threads)) {
-                    size_t r0 = tb.sub.size() * 4, r1 = tb.blocks.size() * 2, rm = tb.mid.size() * 4;
+                if (tb.build_raster(src, c->raster_sub, c->raster_cell, threads)) {
+                    size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
                     if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
                         ch->release_all();
                         delete ch;
                         return rc;
                     }
                     HIP_TRY(hipMemcpy(ch->rsub.p, tb.sub.data(), r0, hipMemcpyHostToDevice));
-                    HIP_TRY(hipMemcpy(ch->rmid.p, tb.mid.data(), rm, hipMemcpyHostToDevice));
+                    HIP_TRY(hipMemcpy(ch->rmid.p, tb.tile_base.data(), rm, hipMemcpyHostToDevice));
                     HIP_TRY(hipMemcpy(ch->rblocks.p, tb.blocks.data(), r1, hipMemcpyHostToDevice));
                     total += rm;
                     ch->raster_ok = true;
-                    ch->praster.sub = (const uint32_t*)ch->rsub.p;
-                    ch->praster.mid = (const uint32_t*)ch->rmid.p;
-                    ch->praster.M = tb.M;
+                    ch->praster.sub = (const uint16_t*)ch->rsub.p;
+                    ch->praster.tile_base = (const uint32_t*)ch->rmid.p;
+                    ch->praster.sshift = tb.sshift;
+                    ch->praster.tnx = tb.grid.nx;
                     ch->praster.blocks = (const uint16_t*)ch->rblocks.p;
                     ch->praster.sx = tb.grid.sx * tb.S;
                     ch->praster.sy = tb.grid.sy * tb.S;
@@ -1895,7 +1899,6 @@ int mosaic_chip_table_tiles(const mosaic_chips* ch, int64_t* o) {
     for (int k = 0; k < 6; k++) o[k + 1] = ch->tile_stats[k];
     o[7] = ch->raster_ok ? 1 : 0;
     for (int k = 0; k < 5; k++) o[k + 8] = ch->raster_stats[k];
-    o[13] = ch->praster.M;
     return MOSAIC_OK;
 }
 

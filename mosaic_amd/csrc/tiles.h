@@ -50,51 +50,50 @@ namespace tiles {
 static const uint32_t kSkip = 0;  // no point of the tile can join
 static const uint32_t kFull = 1;  // run the generic fast path + probe
 
-// point raster codes (uint16): 0 = no pair, k + 1 = one pair with polygon key k, kMixed = the
-// points of the cell take the tile path; sub-block entries (uint32) carry kRasterBlock | block.
+// point raster codes (uint16): 0 = no pair, k + 1 = one pair with polygon key k (k + 1 < kSubBlock),
+// kMixed = the points of the cell take the tile path.  Sub-block entries (uint16) are a code,
+// kMixed, or kSubBlock | n: leaf block tile_base[tile] + n.
 static const uint16_t kMixed = 0xffffu;
-static const uint32_t kRasterBlock = 0x80000000u;
+static const uint16_t kSubBlock = 0x8000u;
+static const int32_t kMaxRasterKeys = 0x7ffd;  // polygon keys 0 .. kMaxRasterKeys - 1
 
 struct PointRaster {
-    const uint32_t* sub;     // (nx * S) x (ny * S) sub-block entries; nullptr: no raster
-    const uint32_t* mid;     // M x M entries per mixed sub-block (M > 1)
-    const uint16_t* blocks;  // C x C leaf codes per mixed mid cell (per mixed sub-block if M == 1)
-    double sx, sy;           // sub-blocks per degree
-    int32_t nx, ny, M, C;
+    const uint16_t* sub;        // (nx) x (ny) sub-block entries (S x S per tile); nullptr: no raster
+    const uint32_t* tile_base;  // per tile (tnx per row): first leaf block of the tile
+    const uint16_t* blocks;     // C x C leaf codes per mixed sub-block
+    double sx, sy;              // sub-blocks per degree
+    int32_t nx, ny, C, sshift, tnx;  // S = 1 << sshift sub-blocks per tile side
     // quad level: one uint16 per 2^qshift x 2^qshift sub-blocks, the code they all share or kMixed
     // (= look at the sub-block); small enough (<= kQuadMax entries) to live in LDS
-    const uint16_t* quad;    // nullptr: no quad level
+    const uint16_t* quad;       // nullptr: no quad level
     int32_t qnx, qny, qshift;
 };
 static const int kQuadMax = 8192;
 
-// Raster lookups of four points, level by level so the loads of a lane overlap (same result as
-// raster_code() per point): raster_issue4 computes the indices and issues the four sub-block
-// gathers; raster_gather4 issues the block gathers, raster_select4 forms the codes
-// (raster_finish4 = both).  A caller can issue other loads (the next coordinates) in between.
+MOSAIC_HD bool sub_is_block(uint32_t e) { return (e & kSubBlock) && e != kMixed; }
+
 struct Lookup4 {
     int64_t si[4];
-    uint32_t mi[4], fc[4], e[4];
+    uint32_t ti[4], fc[4], e[4], base[4];
     bool in[4];
     uint16_t b[4], out[4];
 };
 MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const double* x, const double* y,
                              const bool* live, Lookup4& L, const uint16_t* quad_lds = nullptr) {
     int64_t qi[4];
-    const int MC = r.M * r.C;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const double gx = (x[k] - x0) * r.sx, gy = (y[k] - y0) * r.sy;
         L.in[k] = live[k] && gx >= 0.0 && gx < (double)r.nx && gy >= 0.0 && gy < (double)r.ny;
         const int ix = L.in[k] ? (int)gx : 0, iy = L.in[k] ? (int)gy : 0;
         L.si[k] = (int64_t)iy * r.nx + ix;
+        L.ti[k] = (uint32_t)((iy >> r.sshift) * r.tnx + (ix >> r.sshift));
         qi[k] = (int64_t)(iy >> r.qshift) * r.qnx + (ix >> r.qshift);
-        int fx = L.in[k] ? (int)((gx - (double)ix) * (double)MC) : 0;
-        int fy = L.in[k] ? (int)((gy - (double)iy) * (double)MC) : 0;
-        fx = fx < MC - 1 ? fx : MC - 1;
-        fy = fy < MC - 1 ? fy : MC - 1;
-        L.mi[k] = (uint32_t)((fy / r.C) * r.M + fx / r.C);
-        L.fc[k] = (uint32_t)((fy % r.C) * r.C + fx % r.C);
+        int cx = L.in[k] ? (int)((gx - (double)ix) * (double)r.C) : 0;
+        int cy = L.in[k] ? (int)((gy - (double)iy) * (double)r.C) : 0;
+        cx = cx < r.C - 1 ? cx : r.C - 1;
+        cy = cy < r.C - 1 ? cy : r.C - 1;
+        L.fc[k] = (uint32_t)(cy * r.C + cx);
         // outside the grid: no pair for finite points, the tile path for non-finite ones
         L.out[k] = (!live[k] || (isfinite(x[k]) && isfinite(y[k]))) ? (uint16_t)0 : kMixed;
     }
@@ -117,32 +116,26 @@ MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const d
         for (int k = 0; k < 4; k++) L.e[k] = r.sub[L.si[k]];
     }
 }
-// mid level (M > 1): entries of points whose sub-block entry is a block (others read mid[0])
-MOSAIC_HD void raster_mid4(const PointRaster& r, Lookup4& L) {
-    if (r.M == 1) return;
+// tile bases of the points whose sub-block entry is a leaf block (others read tile_base[0])
+MOSAIC_HD void raster_base4(const PointRaster& r, Lookup4& L) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const bool blk = L.in[k] && (L.e[k] & kRasterBlock);
-        const size_t mi = blk ? (size_t)(L.e[k] & ~kRasterBlock) * (size_t)(r.M * r.M) + L.mi[k] : 0;
-        const uint32_t m = r.mid[mi];
-        L.e[k] = blk ? m : L.e[k];
-    }
+    for (int k = 0; k < 4; k++) L.base[k] = r.tile_base[(L.in[k] && sub_is_block(L.e[k])) ? L.ti[k] : 0];
 }
 MOSAIC_HD void raster_gather4(const PointRaster& r, Lookup4& L) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const bool blk = L.in[k] && (L.e[k] & kRasterBlock);
-        const size_t bi = blk ? (size_t)(L.e[k] & ~kRasterBlock) * (size_t)(r.C * r.C) + L.fc[k] : 0;
+        const bool blk = L.in[k] && sub_is_block(L.e[k]);
+        const size_t bi = blk ? (size_t)(L.base[k] + (L.e[k] & 0x7fffu)) * (size_t)(r.C * r.C) + L.fc[k] : 0;
         L.b[k] = r.blocks[bi];
     }
 }
 MOSAIC_HD void raster_select4(Lookup4& L) {
 #pragma unroll
     for (int k = 0; k < 4; k++)
-        if (L.in[k]) L.out[k] = (L.e[k] & kRasterBlock) ? L.b[k] : (uint16_t)L.e[k];
+        if (L.in[k]) L.out[k] = sub_is_block(L.e[k]) ? L.b[k] : (uint16_t)L.e[k];
 }
 MOSAIC_HD void raster_finish4(const PointRaster& r, Lookup4& L) {
-    raster_mid4(r, L);
+    raster_base4(r, L);
     raster_gather4(r, L);
     raster_select4(L);
 }
@@ -153,17 +146,13 @@ MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, doubl
     if (!(gx >= 0.0 && gx < (double)r.nx && gy >= 0.0 && gy < (double)r.ny))
         return (isfinite(x) && isfinite(y)) ? (uint16_t)0 : kMixed;
     const int ix = (int)gx, iy = (int)gy;
-    uint32_t e = r.sub[(int64_t)iy * r.nx + ix];
-    if (!(e & kRasterBlock)) return (uint16_t)e;
-    const int MC = r.M * r.C;
-    int fx = (int)((gx - (double)ix) * (double)MC), fy = (int)((gy - (double)iy) * (double)MC);
-    fx = fx < MC - 1 ? fx : MC - 1;
-    fy = fy < MC - 1 ? fy : MC - 1;
-    if (r.M > 1) {
-        e = r.mid[(size_t)(e & ~kRasterBlock) * (size_t)(r.M * r.M) + (size_t)((fy / r.C) * r.M + fx / r.C)];
-        if (!(e & kRasterBlock)) return (uint16_t)e;
-    }
-    return r.blocks[(size_t)(e & ~kRasterBlock) * (size_t)(r.C * r.C) + (size_t)((fy % r.C) * r.C + fx % r.C)];
+    const uint16_t e = r.sub[(int64_t)iy * r.nx + ix];
+    if (!sub_is_block(e)) return e;
+    int cx = (int)((gx - (double)ix) * (double)r.C), cy = (int)((gy - (double)iy) * (double)r.C);
+    cx = cx < r.C - 1 ? cx : r.C - 1;
+    cy = cy < r.C - 1 ? cy : r.C - 1;
+    const uint32_t b = r.tile_base[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)] + (e & 0x7fffu);
+    return r.blocks[(size_t)b * (size_t)(r.C * r.C) + (size_t)(cy * r.C + cx)];
 }
 
 struct TileRec {
@@ -242,13 +231,13 @@ struct Builder {
     int res_ = 0;
     std::vector<double> rec_dev;  // per record: patch deviation of the tile (axial units)
 
-    // ---- point raster (second stage, optional): per sub-block of a tile (S x S per tile) a
-    // uint32 entry: a code, or kRasterBlock | mid block (M > 1: M x M uint32 entries, each a code or
-    // kRasterBlock | leaf block) or leaf block (M == 1); leaf blocks are C x C uint16 codes.  Codes:
-    // 0 = the point joins nothing, k + 1 = exactly one pair with polygon key k, kMixed = run the
-    // tile path.
-    int S = 0, M = 1, C = 0;
-    std::vector<uint32_t> sub, mid;
+    // ---- point raster (second stage, optional): per sub-block of a tile (S x S per tile, S a power
+    // of two) a uint16 entry: a code, kMixed, or kSubBlock | tile-local leaf block; leaf blocks are
+    // C x C uint16 codes, a tile's first at tile_base[tile].  Codes: 0 = the point joins nothing,
+    // k + 1 = exactly one pair with polygon key k, kMixed = run the tile path.
+    int S = 0, C = 0, sshift = 0;
+    std::vector<uint16_t> sub;
+    std::vector<uint32_t> tile_base;
     std::vector<uint16_t> blocks;
     std::vector<uint16_t> quad;  // quad level (empty: none)
     int qshift = 0, qnx = 0, qny = 0;
@@ -261,7 +250,7 @@ struct Builder {
         pip::GeomStore store;        // chip geometry (border chips), host pointers
         int32_t n_polygons;
     };
-    bool build_raster(const ChipSource& src, int S_, int M_, int C_, int threads);
+    bool build_raster(const ChipSource& src, int S_, int C_, int threads);
 
     // cells: distinct chip cells; slot_of(cell) -> chip hash slot or -1.  Defined for the host
     // compiler only (tiles_build.cpp); false (with `why`) when the directory is not built.

@@ -110,24 +110,26 @@ struct Hex {
 
 }  // namespace
 
-bool Builder::build_raster(const ChipSource& src, int S_, int M_, int C_, int threads) {
+bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     S = S_;
-    M = M_;
     C = C_;
     sub.clear();
-    mid.clear();
+    tile_base.clear();
     blocks.clear();
+    quad.clear();
     n_sub_pure = n_sub_mixed = n_cell_mixed = 0;
-    if (tile_idx.empty() || S < 1 || M < 1 || C < 1 || S * M * C > 2048) return false;
-    if (src.n_polygons >= (int32_t)kMixed - 1) return false;
-    const int nx = grid.nx, ny = grid.ny, MC = M * C, N = S * MC;
+    if (tile_idx.empty() || S < 1 || (S & (S - 1)) || C < 1 || S * C > 1024) return false;
+    if (src.n_polygons > (int32_t)kMaxRasterKeys) return false;  // codes must stay below kSubBlock
+    sshift = 0;
+    while ((1 << sshift) < S) sshift++;
+    const int nx = grid.nx, ny = grid.ny, N = S * C;
     const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
-    if (NX * NY > ((int64_t)1 << 26)) return false;
-    sub.assign((size_t)(NX * NY), 0u);
+    if (NX * NY > ((int64_t)1 << 28)) return false;
+    sub.assign((size_t)(NX * NY), (uint16_t)0);
+    tile_base.assign((size_t)nx * ny, 0u);
     const double tw = 1.0 / grid.sx, th = 1.0 / grid.sy;
-    // per-tile output blocks, merged afterwards
+    // per-tile leaf blocks (tile-local numbering in the sub entries), merged afterwards
     std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
-    std::vector<std::vector<uint32_t>> tile_mids(recs.size());
     std::vector<int> tile_of_rec(recs.size(), -1);
     for (int64_t t = 0; t < (int64_t)nx * ny; t++)
         if (tile_idx[(size_t)t] >= 2) tile_of_rec[tile_idx[(size_t)t] - 2] = (int)t;
@@ -158,8 +160,8 @@ bool Builder::build_raster(const ChipSource& src, int S_, int M_, int C_, int th
             };
             lat.resize((size_t)(S + 1) * (S + 1));
             for (int j = 0; j <= S; j++)
-                for (int i = 0; i <= S; i++) lat[(size_t)j * (S + 1) + i] = image(i * MC, j * MC);
-            std::vector<P2> mlat((size_t)(M + 1) * (M + 1)), clat((size_t)(C + 1) * (C + 1));
+                for (int i = 0; i <= S; i++) lat[(size_t)j * (S + 1) + i] = image(i * C, j * C);
+            std::vector<P2> clat((size_t)(C + 1) * (C + 1));
             // window hexagons
             hexes.assign((size_t)wa * wb, Hex());
             for (int ra = 0; ra < wa; ra++)
@@ -186,12 +188,11 @@ bool Builder::build_raster(const ChipSource& src, int S_, int M_, int C_, int th
                 }
             const double dev = rec_dev[(size_t)ri];
             const double cell_deg_x = tw / N, cell_deg_y = th / N;
-            // classification of the lattice rectangle [i0, i1] x [j0, j1] (lattice indices)
-            // with candidate hexagons `cin` -> code; `cout` receives the candidates it meets
-            // (fine-lattice corners i0..i1, j0..j1; q = their images, counter-clockwise)
+            // classification of the fine-lattice rectangle [i0, i1] x [j0, j1] whose corner images
+            // are q (counter-clockwise), with candidate hexagons `cin` -> code; `cout` receives the
+            // candidates it meets
             auto classify = [&](int i0, int j0, int i1, int j1, const P2* q, const std::vector<int>& cin,
-                                std::vector<int>& cout, bool& edges_near) -> uint16_t {
-                edges_near = false;
+                                std::vector<int>& cout) -> uint16_t {
                 double frac = std::max((double)(i1 - i0), (double)(j1 - j0)) / N;
                 double tol = 4.0 * dev * frac * frac + 1e-7;
                 cout.clear();
@@ -213,10 +214,8 @@ bool Builder::build_raster(const ChipSource& src, int S_, int M_, int C_, int th
                     for (size_t b = 0; b < h.border.size(); b++) {
                         const pip::Box& bx = h.bbox[b];
                         if (!(bx.maxx < r.x0 || bx.minx > r.x1 || bx.maxy < r.y0 || bx.miny > r.y1) &&
-                            any_seg_meets(h.segs[b], r)) {
-                            edges_near = true;
+                            any_seg_meets(h.segs[b], r))
                             return kMixed;
-                        }
                         if (pip::contains(src.store, h.border[b], cxm, cym)) ah.push_back(h.border_key[b]);
                     }
                     std::sort(ah.begin(), ah.end());
@@ -235,76 +234,42 @@ bool Builder::build_raster(const ChipSource& src, int S_, int M_, int C_, int th
             std::vector<int> all((size_t)wa * wb);
             for (size_t k = 0; k < all.size(); k++) all[k] = (int)k;
             std::vector<uint16_t>& outb = tile_blocks[(size_t)ri];
-            std::vector<uint32_t>& outm = tile_mids[(size_t)ri];
             std::vector<uint16_t> cellc((size_t)C * C);
-            std::vector<uint32_t> midc((size_t)M * M);
-            std::vector<int> cand3;
-            // q4 holds the corners (0,0) (1,0) (1,1) (0,1)
-            auto corner = [](int cx, int cy) { return cy ? (cx ? 2 : 3) : (cx ? 1 : 0); };
-            // leaf cells of the lattice square [i0, i0 + C] x [j0, j0 + C] (fine units) whose corner
-            // images are q4 -> one code, or a leaf block (returns kRasterBlock | local block index)
-            auto leaf = [&](int i0, int j0, const P2* q4, const std::vector<int>& cin) -> uint32_t {
-                for (int cj = 0; cj <= C; cj++)
-                    for (int ci = 0; ci <= C; ci++)
-                        clat[(size_t)cj * (C + 1) + ci] =
-                            (ci % C == 0 && cj % C == 0) ? q4[corner(ci / C, cj / C)]
-                                                         : image(i0 + ci, j0 + cj);
-                bool same = true, en;
-                for (int cj = 0; cj < C; cj++)
-                    for (int ci = 0; ci < C; ci++) {
-                        const P2 qc[4] = {clat[(size_t)cj * (C + 1) + ci], clat[(size_t)cj * (C + 1) + ci + 1],
-                                          clat[(size_t)(cj + 1) * (C + 1) + ci + 1], clat[(size_t)(cj + 1) * (C + 1) + ci]};
-                        uint16_t cc = classify(i0 + ci, j0 + cj, i0 + ci + 1, j0 + cj + 1, qc, cin, cand3, en);
-                        cellc[(size_t)cj * C + ci] = cc;
-                        if (cc == kMixed) cmixed++;
-                        same = same && cc == cellc[0];
-                    }
-                if (same && cellc[0] != kMixed) return cellc[0];
-                uint32_t e = kRasterBlock | (uint32_t)(outb.size() / ((size_t)C * C));
-                outb.insert(outb.end(), cellc.begin(), cellc.end());
-                return e;
-            };
             for (int sj = 0; sj < S; sj++)
                 for (int si = 0; si < S; si++) {
-                    bool en;
                     const P2 qs[4] = {lat[(size_t)sj * (S + 1) + si], lat[(size_t)sj * (S + 1) + si + 1],
                                       lat[(size_t)(sj + 1) * (S + 1) + si + 1], lat[(size_t)(sj + 1) * (S + 1) + si]};
-                    const int fi = si * MC, fj = sj * MC;  // fine-lattice origin of the sub-block
-                    uint16_t code = classify(fi, fj, fi + MC, fj + MC, qs, all, cand, en);
-                    uint32_t entry;
+                    uint16_t code = classify(si * C, sj * C, (si + 1) * C, (sj + 1) * C, qs, all, cand);
+                    uint16_t entry;
                     if (code != kMixed) {
                         entry = code;
                         pure++;
-                    } else if (M == 1) {
-                        mixed++;
-                        // corner order for leaf(): (0,0) (1,0) (1,1) (0,1) -> q4 index 0, 1, 2, 3
-                        const P2 q4[4] = {qs[0], qs[1], qs[2], qs[3]};
-                        entry = leaf(fi, fj, q4, cand);
                     } else {
                         mixed++;
-                        for (int mj = 0; mj <= M; mj++)
-                            for (int mi = 0; mi <= M; mi++)
-                                mlat[(size_t)mj * (M + 1) + mi] =
-                                    (mi % M == 0 && mj % M == 0)
-                                        ? lat[(size_t)(sj + mj / M) * (S + 1) + si + mi / M]
-                                        : image(fi + mi * C, fj + mj * C);
+                        for (int cj = 0; cj <= C; cj++)
+                            for (int ci = 0; ci <= C; ci++)
+                                clat[(size_t)cj * (C + 1) + ci] =
+                                    (ci % C == 0 && cj % C == 0)
+                                        ? lat[(size_t)(sj + cj / C) * (S + 1) + si + ci / C]
+                                        : image(si * C + ci, sj * C + cj);
                         bool same = true;
-                        for (int mj = 0; mj < M; mj++)
-                            for (int mi = 0; mi < M; mi++) {
-                                const P2 qm[4] = {mlat[(size_t)mj * (M + 1) + mi], mlat[(size_t)mj * (M + 1) + mi + 1],
-                                                  mlat[(size_t)(mj + 1) * (M + 1) + mi + 1],
-                                                  mlat[(size_t)(mj + 1) * (M + 1) + mi]};
-                                const int ci0 = fi + mi * C, cj0 = fj + mj * C;
-                                uint16_t mc = classify(ci0, cj0, ci0 + C, cj0 + C, qm, cand, cand2, en);
-                                uint32_t me = mc != kMixed ? (uint32_t)mc : leaf(ci0, cj0, qm, cand2);
-                                midc[(size_t)mj * M + mi] = me;
-                                same = same && me == midc[0];
+                        for (int cj = 0; cj < C; cj++)
+                            for (int ci = 0; ci < C; ci++) {
+                                int i0 = si * C + ci, j0 = sj * C + cj;
+                                const P2 qc[4] = {clat[(size_t)cj * (C + 1) + ci], clat[(size_t)cj * (C + 1) + ci + 1],
+                                                  clat[(size_t)(cj + 1) * (C + 1) + ci + 1],
+                                                  clat[(size_t)(cj + 1) * (C + 1) + ci]};
+                                uint16_t cc = classify(i0, j0, i0 + 1, j0 + 1, qc, cand, cand2);
+                                cellc[(size_t)cj * C + ci] = cc;
+                                if (cc == kMixed) cmixed++;
+                                same = same && cc == cellc[0];
                             }
-                        if (same && !(midc[0] & kRasterBlock) && midc[0] != kMixed) {
-                            entry = midc[0];
+                        if (same && cellc[0] != kMixed) {
+                            entry = cellc[0];
                         } else {
-                            entry = kRasterBlock | (uint32_t)(outm.size() / ((size_t)M * M));
-                            outm.insert(outm.end(), midc.begin(), midc.end());
+                            // tile-local leaf block number (< S * S <= 0x7fff)
+                            entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / ((size_t)C * C)));
+                            outb.insert(outb.end(), cellc.begin(), cellc.end());
                         }
                     }
                     sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
@@ -323,44 +288,23 @@ bool Builder::build_raster(const ChipSource& src, int S_, int M_, int C_, int th
         for (int sj = 0; sj < S; sj++)
             for (int si = 0; si < S; si++) sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = kMixed;
     }
-    // merge the per-tile leaf blocks and mid blocks, rebase the entries
-    std::vector<uint32_t> lbase(recs.size(), 0), mbase(recs.size(), 0);
-    size_t ltotal = 0, mtotal = 0;
+    // merge the per-tile leaf blocks; a tile's first block goes to tile_base
+    size_t total = 0;
     for (size_t r = 0; r < recs.size(); r++) {
-        lbase[r] = (uint32_t)(ltotal / ((size_t)C * C));
-        ltotal += tile_blocks[r].size();
-        mbase[r] = (uint32_t)(mtotal / ((size_t)M * M));
-        mtotal += tile_mids[r].size();
+        if (tile_of_rec[r] >= 0) tile_base[(size_t)tile_of_rec[r]] = (uint32_t)(total / ((size_t)C * C));
+        total += tile_blocks[r].size();
     }
-    if (ltotal / ((size_t)C * C) >= (size_t)kRasterBlock || mtotal / ((size_t)M * M) >= (size_t)kRasterBlock) {
+    if (total / ((size_t)C * C) >= ((size_t)1 << 31)) {
         sub.clear();
         return false;
     }
-    blocks.reserve(std::max<size_t>(ltotal, 1));
-    mid.reserve(std::max<size_t>(mtotal, 1));
-    for (size_t r = 0; r < recs.size(); r++) {
-        blocks.insert(blocks.end(), tile_blocks[r].begin(), tile_blocks[r].end());
-        for (uint32_t e : tile_mids[r]) mid.push_back((e & kRasterBlock) ? kRasterBlock | ((e & ~kRasterBlock) + lbase[r]) : e);
-    }
+    blocks.reserve(std::max<size_t>(total, 1));
+    for (size_t r = 0; r < recs.size(); r++) blocks.insert(blocks.end(), tile_blocks[r].begin(), tile_blocks[r].end());
     if (blocks.empty()) blocks.assign((size_t)C * C, kMixed);
-    if (mid.empty()) mid.assign((size_t)M * M, kMixed);
-    for (size_t r = 0; r < recs.size(); r++) {
-        int t = tile_of_rec[r];
-        if (t < 0) continue;
-        const uint32_t add = M == 1 ? lbase[r] : mbase[r];
-        if (!add) continue;
-        int ti = t % nx, tj = t / nx;
-        for (int sj = 0; sj < S; sj++)
-            for (int si = 0; si < S; si++) {
-                uint32_t& e = sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))];
-                if (e & kRasterBlock) e = kRasterBlock | ((e & ~kRasterBlock) + add);
-            }
-    }
     n_sub_pure = pure.load();
     n_sub_mixed = mixed.load();
     n_cell_mixed = cmixed.load();
     // quad level: the smallest power-of-two group of sub-blocks whose table fits kQuadMax entries
-    quad.clear();
     qshift = 0;
     while (qshift < 16 && ((NX + (1 << qshift) - 1) >> qshift) * ((NY + (1 << qshift) - 1) >> qshift) > kQuadMax)
         qshift++;
@@ -371,9 +315,9 @@ bool Builder::build_raster(const ChipSource& src, int S_, int M_, int C_, int th
         std::vector<uint8_t> seen((size_t)qnx * qny, 0);
         for (int64_t j = 0; j < NY; j++)
             for (int64_t i = 0; i < NX; i++) {
-                const uint32_t e = sub[(size_t)(j * NX + i)];
+                const uint16_t e = sub[(size_t)(j * NX + i)];
                 const size_t q = (size_t)((j >> qshift) * qnx + (i >> qshift));
-                const uint16_t code = (e & kRasterBlock) ? kMixed : (uint16_t)e;
+                const uint16_t code = (e & kSubBlock) ? kMixed : e;  // blocks and kMixed alike
                 if (!seen[q]) {
                     seen[q] = 1;
                     quad[q] = code;

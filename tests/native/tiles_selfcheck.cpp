@@ -92,9 +92,7 @@ int main(int argc, char** argv) {
         fprintf(stderr, "not built: %s\n", tb.why);
         return 0;
     }
-    // S and C from argv[4], argv[5]; the mid level from MOSAIC_RASTER_MID (default 1: none)
     int S = argc > 5 ? atoi(argv[4]) : 16, Cc = argc > 5 ? atoi(argv[5]) : 8;
-    int Mm = getenv("MOSAIC_RASTER_MID") ? atoi(getenv("MOSAIC_RASTER_MID")) : 1;
     tiles::Builder::ChipSource src;
     src.slot_first = slot_first.data();
     src.slot_count = slot_count.data();
@@ -102,12 +100,13 @@ int main(int argc, char** argv) {
     src.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(), gb.part_ring.data(),
                                gb.geom_part.data(), gb.geom_bbox.data()};
     src.n_polygons = npoly;
-    bool rok = tb.build_raster(src, S, Mm, Cc, 8);
+    bool rok = tb.build_raster(src, S, Cc, 8);
     tiles::PointRaster pr{};
     if (rok) {
         pr.sub = tb.sub.data();
-        pr.mid = tb.mid.data();
-        pr.M = Mm;
+        pr.tile_base = tb.tile_base.data();
+        pr.sshift = tb.sshift;
+        pr.tnx = tb.grid.nx;
         pr.blocks = tb.blocks.data();
         pr.sx = tb.grid.sx * S;
         pr.sy = tb.grid.sy * S;
@@ -131,9 +130,9 @@ int main(int argc, char** argv) {
         quad_pure.assign((size_t)qx * qy, 1);
         for (int j = 0; j < pr.ny; j++)
             for (int i = 0; i < pr.nx; i++) {
-                uint32_t e = pr.sub[(size_t)j * pr.nx + i];
-                uint32_t e0 = pr.sub[(size_t)(j / Q * Q) * pr.nx + (i / Q * Q)];
-                if ((e & tiles::kRasterBlock) || e != e0) quad_pure[(size_t)(j / Q) * qx + i / Q] = 0;
+                uint16_t e = pr.sub[(size_t)j * pr.nx + i];
+                uint16_t e0 = pr.sub[(size_t)(j / Q * Q) * pr.nx + (i / Q * Q)];
+                if (tiles::sub_is_block(e) || e != e0) quad_pure[(size_t)(j / Q) * qx + i / Q] = 0;
             }
     }
     if (rok && argc > 9)  // raster hit statistics for uniform points over a bbox
@@ -148,48 +147,9 @@ int main(int argc, char** argv) {
             }
             int ix = (int)gx, iy = (int)gy;
             if (tb.tile_idx[(size_t)(iy / tb.S) * tb.grid.nx + ix / tb.S] == tiles::kSkip) st_skip++;
-            if (!(pr.sub[(size_t)iy * pr.nx + ix] & tiles::kRasterBlock)) st_sub++;
+            if (!tiles::sub_is_block(pr.sub[(size_t)iy * pr.nx + ix])) st_sub++;
             if (quad_pure[(size_t)(iy / Q) * ((pr.nx + Q - 1) / Q) + ix / Q]) st_quad++;
         }
-    // hypothetical mid level: M x M mid cells per sub-block (each C/M fine cells a side); share of
-    // uniform points in mixed sub-blocks, in mixed mid cells, and the mid-level block count
-    int M = argc > 11 ? atoi(argv[11]) : 0;
-    if (rok && Mm == 1 && M > 0 && Cc % M == 0 && argc > 9) {
-        int f = Cc / M;
-        long in_block = 0, in_mixed_mid = 0, mid_mixed_cells = 0;
-        size_t nblk = tb.blocks.size() / ((size_t)Cc * Cc);
-        std::vector<uint8_t> midmix(nblk * M * M, 0);
-        for (size_t b = 0; b < nblk; b++)
-            for (int my = 0; my < M; my++)
-                for (int mx = 0; mx < M; mx++) {
-                    uint16_t c0 = tb.blocks[b * Cc * Cc + (size_t)(my * f) * Cc + mx * f];
-                    bool mixed = false;
-                    for (int yy = 0; yy < f && !mixed; yy++)
-                        for (int xx = 0; xx < f; xx++) {
-                            uint16_t c = tb.blocks[b * Cc * Cc + (size_t)(my * f + yy) * Cc + mx * f + xx];
-                            if (c != c0 || c == tiles::kMixed) {
-                                mixed = true;
-                                break;
-                            }
-                        }
-                    midmix[(b * M + my) * M + mx] = mixed;
-                    mid_mixed_cells += mixed;
-                }
-        std::mt19937_64 r2(5);
-        for (long k = 0; k < npts; k++) {
-            double x = bx0 + (bx1 - bx0) * u(r2), y = by0 + (by1 - by0) * u(r2);
-            double gx = (x - tb.grid.x0) * pr.sx, gy = (y - tb.grid.y0) * pr.sy;
-            if (!(gx >= 0 && gx < pr.nx && gy >= 0 && gy < pr.ny)) continue;
-            int ix = (int)gx, iy = (int)gy;
-            uint32_t e = pr.sub[(size_t)iy * pr.nx + ix];
-            if (!(e & tiles::kRasterBlock)) continue;
-            in_block++;
-            int cx = std::min((int)((gx - ix) * Cc), Cc - 1), cy = std::min((int)((gy - iy) * Cc), Cc - 1);
-            if (midmix[((size_t)(e & ~tiles::kRasterBlock) * M + cy / f) * M + cx / f]) in_mixed_mid++;
-        }
-        fprintf(stderr, "mid %d: points in blocks %.4f, in mixed mid cells %.4f; blocks %zu, mixed mid cells %ld\n", M,
-                (double)in_block / npts, (double)in_mixed_mid / npts, nblk, mid_mixed_cells);
-    }
     if (uni)
         fprintf(stderr, "uniform: outside %.4f skip-tile %.4f pure-sub %.4f pure-quad(%d) %.4f\n", (double)st_out / uni,
                 (double)st_skip / uni, (double)st_sub / uni, Q, (double)st_quad / uni);

@@ -28,7 +28,7 @@ def exe(tmp_path_factory):
     return out
 
 
-def _run(exe, tmp_path, res, chips, npts=300_000, seed=3, sc=(16, 8), mid=1):
+def _run(exe, tmp_path, res, chips, npts=300_000, seed=3, sc=(16, 8)):
     path = tmp_path / f"chips_{res}.bin"
     offs, data = chips["wkb"]
     with open(path, "wb") as f:
@@ -39,18 +39,18 @@ def _run(exe, tmp_path, res, chips, npts=300_000, seed=3, sc=(16, 8), mid=1):
                                 int(chips["polygon_key"][i]), len(w)))
             f.write(w)
     out = subprocess.run([str(exe), str(path), str(npts), str(seed), str(sc[0]), str(sc[1])], check=True,
-                         capture_output=True, text=True, env={**os.environ, "MOSAIC_RASTER_MID": str(mid)})
+                         capture_output=True, text=True)
     built, bad, checked, skipped, full, unc, miss, rbuilt, rbad, rpure, rmixed = map(int, out.stdout.split())
     return dict(built=built, bad=bad, checked=checked, skipped=skipped, full=full, unc=unc, miss=miss,
                 raster=rbuilt, raster_bad=rbad, raster_pure=rpure, raster_mixed=rmixed, log=out.stderr)
 
 
-@pytest.mark.parametrize("res,sc,mid", [(7, (16, 8), 1), (8, (8, 4), 2), (9, (32, 16), 1), (9, (16, 8), 2),
-                                        (9, (4, 2), 1), (10, (16, 8), 4), (11, (8, 8), 1)])
-def test_tiles_nyc_tessellation(exe, tmp_path, res, sc, mid):
+@pytest.mark.parametrize("res,sc", [(7, (16, 8)), (8, (8, 4)), (9, (32, 16)), (9, (16, 8)), (9, (4, 2)),
+                                    (10, (16, 8)), (11, (8, 8))])
+def test_tiles_nyc_tessellation(exe, tmp_path, res, sc):
     zones = PolygonSet.load("nyc_taxi_zones_35" if res >= 10 else "nyc_taxi_zones")
     chips = tessellate("H3", zones, res)
-    r = _run(exe, tmp_path, res, chips, sc=sc, mid=mid)
+    r = _run(exe, tmp_path, res, chips, sc=sc)
     assert r["built"] == 1, r["log"]
     assert r["bad"] == 0, r["log"]
     assert r["checked"] > 200_000

@@ -1,7 +1,7 @@
 """Profiling driver (GPU box): runs the res-9 NYC chip join on 1e8 resident uniform points a few
 times with one point-raster configuration, nothing else, so PMC passes see only these launches.
 
-    rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -- python tools/joinrun.py 16x2x16
+    rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -- python tools/joinrun.py 32x16
 """
 import os
 import sys
@@ -16,13 +16,12 @@ def main():
     from mosaic_amd.context import tessellate
     from mosaic_amd.data import PolygonSet, uniform_points_device
 
-    sub, mid, cell = (int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "16x2x16").split("x"))
+    sub, cell = (int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "32x16").split("x"))
     n = int(float(sys.argv[2])) if len(sys.argv) > 2 else 100_000_000
     zones = PolygonSet.load("nyc_taxi_zones")
     chips = tessellate("H3", zones, 9)
     ctx = MosaicContext.build("H3")
     ctx.set_option("raster_sub", sub)
-    ctx.set_option("raster_mid", mid)
     ctx.set_option("raster_cell", cell)
     x, y = uniform_points_device(zones.bbox(), n, seed=1)
     counts = torch.zeros(len(zones), dtype=torch.int64, device="cuda")

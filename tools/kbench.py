@@ -28,7 +28,9 @@ def main():
     p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*",
                    default=[(1, 1), (1, 0), (0, 0)], help="TILES:POINT_RASTER pairs")
     p.add_argument("--point-raster", type=lambda v: tuple(int(q) for q in v.split("x")), nargs="*",
-                   default=[(16, 2, 16)], help="point raster sizes SUBxMIDxCELL")
+                   default=[(32, 16)], help="point raster sizes SUBxCELL")
+    p.add_argument("--stream-probes", type=int, nargs="*", default=[],
+                   help="probe_mask values to time k_join_stream with (4 no sub lookups, 16 no counting, 32 no quad)")
     p.add_argument("--mixed-rows", type=int, nargs="*", default=[], help="k_join_mixed rows per lane to time")
     p.add_argument("--mixed-bpc", type=int, nargs="*", default=[], help="k_join_mixed blocks per CU to time")
     p.add_argument("--probe-mixed", action="store_true", help="time k_join_mixed without its chip loop / cell")
@@ -90,21 +92,20 @@ def main():
     ftab.close()
     variants = []
     for tiles, praster in args.modes:
-        for sub, mid, cell in (args.point_raster if praster else [(16, 2, 16)]):
+        for sub, cell in (args.point_raster if praster else [(32, 16)]):
             for grp in args.groups:
-                tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{mid}x{cell}_g{grp}" if praster else "")
+                tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}_g{grp}" if praster else "")
                 if args.all_core:
-                    variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, (sub, mid, cell), grp))
+                    variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, (sub, cell), grp))
                 for r in args.rasters:
                     for le in args.lane_edges:
                         variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster,
-                                         (sub, mid, cell), grp))
+                                         (sub, cell), grp))
     if args.legacy:
-        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, (16, 2, 16), 1),
-                     ("join_full_slab", False, 2, 16, 8, 0, 0, (16, 2, 16), 1)]
-    for name, core, mode, raster, lane_edges, tiles, praster, (sub, mid, cell), grp in variants:
+        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, (32, 16), 1),
+                     ("join_full_slab", False, 2, 16, 8, 0, 0, (32, 16), 1)]
+    for name, core, mode, raster, lane_edges, tiles, praster, (sub, cell), grp in variants:
         ctx.set_option("stream_groups", grp)
-        ctx.set_option("raster_mid", mid)
         ctx.set_option("tiles", tiles)
         ctx.set_option("point_raster", praster)
         ctx.set_option("raster_sub", sub)
@@ -128,6 +129,14 @@ def main():
         ctx.set_option("async", 1)
         tl = table.tiles()
         probes = {}
+        for pm in args.stream_probes:
+            ctx.set_option("probe_mask", pm)
+            ctx.set_option("timing", 2)
+            for _ in range(3):
+                ctx.pip_join_count(table, x, y, out=counts)
+            probes[f"stream_probe{pm}_ms"] = round(float(np.median(ctx.kernel_times()[0::2])), 4)
+            ctx.set_option("timing", 0)
+        ctx.set_option("probe_mask", 0)
         for mr in args.mixed_rows:
             ctx.set_option("mixed_rows", mr)
             ctx.set_option("timing", 2)
