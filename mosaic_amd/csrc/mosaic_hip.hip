@@ -756,8 +756,20 @@ __global__ void __launch_bounds__(256) k_join_tiled(JoinArgs a) {
 // cells are appended to mixq (one atomic per wave) for k_join_mixed.
 typedef double v2d __attribute__((ext_vector_type(2)));
 
+#ifndef MOSAIC_STREAM_NT
+#define MOSAIC_STREAM_NT 1  // k_join_stream: non-temporal coordinate loads
+#endif
+#if MOSAIC_STREAM_NT
+#define MOSAIC_STREAM_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define MOSAIC_STREAM_LOAD(p) (*(p))
+#endif
+#ifndef MOSAIC_STREAM_WAVES
+#define MOSAIC_STREAM_WAVES 6  // k_join_stream: waves per SIMD the register budget must allow
+#endif
 template <bool LDS_COUNTS, bool PAIRS, bool VEC, bool VALID, int G>
-__global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOSAIC_STREAM_WAVES)))
+k_join_stream(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     // dynamic LDS: [per-polygon counts (LDS_COUNTS)] [quad level of the raster (if any)]
     uint16_t* quad = a.praster.quad ? (uint16_t*)(lds + (LDS_COUNTS ? a.n_polygons : 0)) : nullptr;
@@ -790,10 +802,10 @@ __global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
         const int64_t r = i0 + g * gstride;
         nx[g][0] = nx[g][1] = ny[g][0] = ny[g][1] = v2d{0.0, 0.0};
         if (VEC && r + 3 < a.n) {
-            nx[g][0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
-            nx[g][1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 2));
-            ny[g][0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
-            ny[g][1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 2));
+            nx[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r));
+            nx[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r + 2));
+            ny[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r));
+            ny[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r + 2));
         }
     }
     for (; w0 < a.n; w0 += stride, i0 += stride) {
@@ -842,10 +854,10 @@ __global__ void __launch_bounds__(256) k_join_stream(JoinArgs a) {
             for (int g = 0; g < G; g++) {
                 const int64_t r = i0 + stride + g * gstride;
                 const int64_t r1 = (r + 3 < a.n) ? r : a.row_lo;
-                nx[g][0] = __builtin_nontemporal_load((const v2d*)(a.x + r1));
-                nx[g][1] = __builtin_nontemporal_load((const v2d*)(a.x + r1 + 2));
-                ny[g][0] = __builtin_nontemporal_load((const v2d*)(a.y + r1));
-                ny[g][1] = __builtin_nontemporal_load((const v2d*)(a.y + r1 + 2));
+                nx[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1));
+                nx[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1 + 2));
+                ny[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1));
+                ny[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1 + 2));
             }
         }
 #pragma unroll

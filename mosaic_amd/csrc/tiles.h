@@ -73,22 +73,22 @@ static const int kQuadMax = 8192;
 MOSAIC_HD bool sub_is_block(uint32_t e) { return (e & kSubBlock) && e != kMixed; }
 
 struct Lookup4 {
-    int64_t si[4];
+    uint32_t si[4];  // sub-block index (the grid holds < 2^28 sub-blocks)
     uint32_t ti[4], fc[4], e[4], base[4];
     bool in[4];
     uint16_t b[4], out[4];
 };
 MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const double* x, const double* y,
                              const bool* live, Lookup4& L, const uint16_t* quad_lds = nullptr) {
-    int64_t qi[4];
+    uint32_t qi[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const double gx = (x[k] - x0) * r.sx, gy = (y[k] - y0) * r.sy;
         L.in[k] = live[k] && gx >= 0.0 && gx < (double)r.nx && gy >= 0.0 && gy < (double)r.ny;
         const int ix = L.in[k] ? (int)gx : 0, iy = L.in[k] ? (int)gy : 0;
-        L.si[k] = (int64_t)iy * r.nx + ix;
+        L.si[k] = (uint32_t)iy * (uint32_t)r.nx + (uint32_t)ix;
         L.ti[k] = (uint32_t)((iy >> r.sshift) * r.tnx + (ix >> r.sshift));
-        qi[k] = (int64_t)(iy >> r.qshift) * r.qnx + (ix >> r.qshift);
+        qi[k] = (uint32_t)((iy >> r.qshift) * r.qnx + (ix >> r.qshift));
         int cx = L.in[k] ? (int)((gx - (double)ix) * (double)r.C) : 0;
         int cy = L.in[k] ? (int)((gy - (double)iy) * (double)r.C) : 0;
         cx = cx < r.C - 1 ? cx : r.C - 1;
