@@ -88,6 +88,9 @@ struct JoinArgs {
     const tiles::TileRec* tile_rec;
     const uint32_t* tile_ent;
     tiles::PointRaster praster;       // point raster (tiles.h); praster.sub == nullptr: none
+    const uint32_t* bng_cells;        // BNG dense cell table (k_join_stream_bng); nullptr: none
+    const uint16_t* bng_leaf;         // its leaf blocks (C x C codes per border cell)
+    int32_t bng_e0, bng_n0, bng_ne, bng_nn, bng_div, bng_C;
     int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
     uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
     unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)
@@ -754,6 +757,27 @@ __global__ void __launch_bounds__(256) k_join_tiled(JoinArgs a) {
 // runs near HBM speed.  Four consecutive points per lane (two 16-byte loads per coordinate,
 // VEC: both arrays 16-byte aligned), their lookups issued back to back.  Rows in mixed raster
 // cells are appended to mixq (one atomic per wave) for k_join_mixed.
+// Per-wave LDS stage of rows for the mixed-cell queue: rows are appended with a ballot, and the
+// stage goes to the global queue in one atomic once >= 64 rows wait (a per-iteration atomic on one
+// counter serialises the grid).  Wave-uniform calls.
+__device__ inline void stage_push(uint32_t* wq, uint32_t& wn, bool mixed, uint32_t rowoff, unsigned long long lt_mask) {
+    const unsigned long long mm = __ballot(mixed);
+    if (mixed) wq[wn + __popcll(mm & lt_mask)] = rowoff;
+    wn += (uint32_t)__popcll(mm);
+}
+__device__ inline void stage_flush(const JoinArgs& a, uint32_t* wq, uint32_t& wn, int lane, uint32_t min_rows) {
+    if (wn < min_rows || wn == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
+    base = __shfl(base, 0, 64);
+    for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
+    __builtin_amdgcn_wave_barrier();
+    wn = 0;
+}
+
 typedef double v2d __attribute__((ext_vector_type(2)));
 
 #ifndef MOSAIC_STREAM_NT
@@ -894,6 +918,219 @@ k_join_stream(JoinArgs a) {
         if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
         base = __shfl(base, 0, 64);
         for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
+    }
+    counts_flush<LDS_COUNTS>(a, lds, 0u);
+}
+
+// ---- BNG dense cell table (positive resolutions): BNGIndexSystem.pointToIndex
+// (BNGIndexSystem.scala:277-291, 528-541) maps a point with 0 <= toInt(e), toInt(n) < 1e7 to the id
+// of cell (toInt(e) / divisor, toInt(n) / divisor) -- one-to-one there, the two letters being the
+// leading digits of those quotients (100000 is a multiple of every positive-resolution divisor).
+// The host builds a dense table over the chip cells' cell range: 0 = no chip, kBngPure | (k + 1) =
+// exactly one chip, a core chip of polygon k, kBngLeaf | block for other cells (below).  One
+// L2-resident gather per point (two in border cells) decides all but the rows in mixed sub-cells
+// (and rows outside that integer range), which go to the mixed queue and k_join_mixed_bng (the
+// generic point_to_index + probe + chip loop).
+// Border cells carry kBngLeaf | block: C x C codes over the cell (the H3 point raster's codes,
+// tiles_build.cpp bng_leaf_blocks); kMixed codes send the row to the mixed queue.
+static const uint32_t kBngPure = 0x80000000u, kBngLeaf = 0x40000000u;
+
+// Returns a join code (0 none, k + 1 one pair with key k) or tiles::kMixed (queue the row).
+__device__ inline uint32_t bng_dense_code(const JoinArgs& a, double x, double y) {
+    const int32_t eI = bng::jvm_d2i(x), nI = bng::jvm_d2i(y);
+    if (!(eI >= 0 && eI < 10000000 && nI >= 0 && nI < 10000000)) return tiles::kMixed;  // generic path
+    const int32_t qe = eI / a.bng_div, qn = nI / a.bng_div;
+    const int32_t ce = qe - a.bng_e0, cn = qn - a.bng_n0;
+    if ((uint32_t)ce >= (uint32_t)a.bng_ne || (uint32_t)cn >= (uint32_t)a.bng_nn) return 0;  // no chip cell
+    const uint32_t e = a.bng_cells[(int64_t)cn * a.bng_ne + ce];
+    if (e & kBngPure) return e & ~kBngPure;
+    if (!(e & kBngLeaf)) return e ? tiles::kMixed : 0u;
+    // sub-cell of the point inside the cell [qe div, (qe + 1) div) x [qn div, (qn + 1) div)
+    const double f = (double)a.bng_C / (double)a.bng_div;
+    int sx = (int)((x - (double)qe * (double)a.bng_div) * f), sy = (int)((y - (double)qn * (double)a.bng_div) * f);
+    sx = sx < 0 ? 0 : (sx >= a.bng_C ? a.bng_C - 1 : sx);
+    sy = sy < 0 ? 0 : (sy >= a.bng_C ? a.bng_C - 1 : sy);
+    return a.bng_leaf[(size_t)(e & ~kBngLeaf) * (size_t)(a.bng_C * a.bng_C) + (size_t)(sy * a.bng_C + sx)];
+}
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_stream_bng(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    __shared__ uint32_t stage[4][64 + 256];
+    counts_init<LDS_COUNTS>(a, lds);
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    uint32_t* wq = stage[(threadIdx.x >> 6) & 3];
+    uint32_t wn = 0;
+    bool nan_seen = false;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    for (int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 4; w0 < a.n; w0 += stride) {
+        const int64_t r0 = w0 + lane * 4;
+        double x[4], y[4];
+        bool live[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            live[k] = r0 + k < a.n && (!a.valid || a.valid[r0 + k]);
+            x[k] = live[k] ? a.x[r0 + k] : 0.0;
+            y[k] = live[k] ? a.y[r0 + k] : 0.0;
+        }
+        uint32_t code[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            code[k] = 0;
+            if (!live[k]) continue;
+            if (x[k] != x[k] || y[k] != y[k]) {  // the reference throws IllegalStateException
+                nan_seen = true;
+                continue;
+            }
+            code[k] = bng_dense_code(a, x[k], y[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool mixed = code[k] == tiles::kMixed;
+            if (code[k] && !mixed) emit_hit<LDS_COUNTS, PAIRS>(a, r0 + k, code[k] - 1u, lds);
+            stage_push(wq, wn, mixed, (uint32_t)(r0 + k - a.row_lo), lt_mask);
+        }
+        stage_flush(a, wq, wn, lane, 64);
+    }
+    stage_flush(a, wq, wn, lane, 1);
+    if (nan_seen) atomicOr(a.flags, 1u);
+    counts_flush<LDS_COUNTS>(a, lds, 0u);
+}
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_mixed_bng(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    __shared__ SlabItem items[4][16];
+    counts_init<LDS_COUNTS>(a, lds);
+    unsigned int tests = 0;
+    const int wv = (int)(threadIdx.x >> 6) & 3;
+    const unsigned long long total = *a.mixq_count;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total;
+         base += stride) {
+        const unsigned long long t = base + (threadIdx.x & 63);
+        double x = 0.0, y = 0.0;
+        int64_t i = -1, cell = kEmptyKey;
+        if (t < total) {
+            i = a.row_lo + (int64_t)a.mixq[t];
+            x = a.x[i];
+            y = a.y[i];
+            if (!bng::point_to_index(x, y, a.res, &cell)) cell = kEmptyKey;  // NaN: flagged by the stream
+        }
+        uint32_t cur, end;
+        probe(a, cell, cur, end);
+        raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items[wv]);
+    }
+    counts_flush<LDS_COUNTS>(a, lds, tests);
+}
+
+// ---- decoupled variant (option stream_mode = 1): per workgroup of 1024 threads, 4 loader waves
+// stream the coordinates of the next chunk into LDS while 12 worker waves run the raster lookups of
+// the current chunk from LDS.  A wave's vector-memory returns retire in order, so in k_join_stream
+// a wave waiting on its gathers also waits on its stream loads; here the two wait in different
+// waves.  Chunks of kChunkRows rows, double-buffered; one workgroup per CU.
+static const int kLoaderWaves = 4, kWorkerWaves = 12;
+static const int kChunkRows = kWorkerWaves * 64 * 4;  // 3072 rows: 4 per worker lane
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(1024) k_join_stream_dec(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    __shared__ double cx[2][kChunkRows], cy[2][kChunkRows];  // 96 KB
+    __shared__ uint32_t stage[kWorkerWaves][320];
+    uint16_t* quad = a.praster.quad ? (uint16_t*)(lds + (LDS_COUNTS ? a.n_polygons : 0)) : nullptr;
+    if (quad) {
+        const int nq = a.praster.qnx * a.praster.qny;
+        for (int k = threadIdx.x; k < nq; k += blockDim.x) quad[k] = a.praster.quad[k];
+    }
+    counts_init<LDS_COUNTS>(a, lds);
+    if (!LDS_COUNTS) __syncthreads();
+    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const bool loader = wave < kLoaderWaves;
+    const int64_t rows = a.n - a.row_lo;
+    const int64_t nchunks = (rows + kChunkRows - 1) / kChunkRows;
+    // loader lane l (0..255) moves rows [c0 + j * 512 + 2 l, +2) for j < 6, x and y
+    auto load_chunk = [&](int64_t c, int buf) {
+        const int64_t c0 = a.row_lo + c * kChunkRows;
+        const int l = (int)threadIdx.x;  // 0..255 for loader waves
+        v2d vx[6], vy[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const int64_t r = c0 + j * 512 + 2 * l;
+            if (r + 1 < a.n) {
+                vx[j] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r));
+                vy[j] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r));
+            } else {
+                vx[j] = v2d{r < a.n ? a.x[r] : 0.0, 0.0};
+                vy[j] = v2d{r < a.n ? a.y[r] : 0.0, 0.0};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            *(v2d*)&cx[buf][j * 512 + 2 * l] = vx[j];
+            *(v2d*)&cy[buf][j * 512 + 2 * l] = vy[j];
+        }
+    };
+    int64_t c = blockIdx.x;
+    if (loader && c < nchunks) load_chunk(c, 0);
+    __syncthreads();
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    uint32_t* wq = loader ? nullptr : stage[wave - kLoaderWaves];
+    uint32_t wn = 0;
+    for (int k = 0; c < nchunks; c += gridDim.x, k ^= 1) {
+        const int64_t cn = c + gridDim.x;
+        if (loader) {
+            if (cn < nchunks) load_chunk(cn, k ^ 1);
+        } else {
+            const int w = (int)threadIdx.x - kLoaderWaves * 64;  // 0..767
+            const int64_t r0 = a.row_lo + c * kChunkRows + 4 * w;
+            double x[4], y[4];
+            bool live[4];
+            const v2d x01 = *(const v2d*)&cx[k][4 * w], x23 = *(const v2d*)&cx[k][4 * w + 2];
+            const v2d y01 = *(const v2d*)&cy[k][4 * w], y23 = *(const v2d*)&cy[k][4 * w + 2];
+            x[0] = x01.x;
+            x[1] = x01.y;
+            x[2] = x23.x;
+            x[3] = x23.y;
+            y[0] = y01.x;
+            y[1] = y01.y;
+            y[2] = y23.x;
+            y[3] = y23.y;
+#pragma unroll
+            for (int q = 0; q < 4; q++) live[q] = r0 + q < a.n && (!a.valid || a.valid[r0 + q]);
+            tiles::Lookup4 L;
+            tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L, quad);
+            tiles::raster_finish4(a.praster, L);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint16_t rc = L.out[q];
+                if (rc != 0 && rc != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, r0 + q, (uint32_t)rc - 1u, lds);
+                const unsigned long long mm = __ballot(rc == tiles::kMixed);
+                if (rc == tiles::kMixed) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(r0 + q - a.row_lo);
+                wn += (uint32_t)__popcll(mm);
+            }
+            if (wn >= 64) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
+                base = __shfl(base, 0, 64);
+                for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
+                __builtin_amdgcn_wave_barrier();
+                wn = 0;
+            }
+        }
+        __syncthreads();
+    }
+    if (!loader && wn) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
+        base = __shfl(base, 0, 64);
+        for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
     }
     counts_flush<LDS_COUNTS>(a, lds, 0u);
 }
@@ -1144,6 +1381,7 @@ struct mosaic_ctx {
     int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
     int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
+    int stream_mode = 0;          // 0: k_join_stream, 1: k_join_stream_dec (loader / worker waves)
     int probe_mask = 0;     // measurement only: see JoinArgs::probe_mask (results are wrong when set)
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
@@ -1227,13 +1465,16 @@ struct mosaic_chips {
     tiles::Grid tgrid{};
     DevBuf tile_idx, tile_rec, tile_ent;
     int64_t tile_stats[6] = {0, 0, 0, 0, 0, 0};  // nx, ny, records, entries, kFull tiles, rings
+    bool bng_ok = false;  // BNG dense cell table (k_join_stream_bng)
+    int32_t bng_e0 = 0, bng_n0 = 0, bng_ne = 0, bng_nn = 0, bng_div = 1, bng_C = 0;
+    DevBuf bng_cells, bng_leaf;
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
     DevBuf rsub, rmid, rblocks, rquad;  // rmid: per-tile leaf block bases
     int64_t raster_stats[5] = {0, 0, 0, 0, 0};    // S, C, pure sub-blocks, mixed sub-blocks, mixed cells
     void release_all() {
         for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad})
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &bng_cells, &bng_leaf})
             b->release();
         store.release();
     }
@@ -1367,6 +1608,9 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "probe_mask") {
         if (v < 0 || v > 63) return fail(MOSAIC_E_ARG, "probe_mask must be in [0, 63]");
         c->probe_mask = (int)v;
+    } else if (k == "stream_mode") {
+        if (v != 0 && v != 1) return fail(MOSAIC_E_ARG, "stream_mode must be 0 or 1");
+        c->stream_mode = (int)v;
     } else if (k == "mixed_rows") {
         if (v != 1 && v != 2 && v != 4) return fail(MOSAIC_E_ARG, "mixed_rows must be 1, 2 or 4");
         c->mixed_rows = (int)v;
@@ -1782,6 +2026,103 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
     HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
     ch->n_edge_records = (int64_t)edges.size();
+    if (grid == MOSAIC_GRID_BNG && res >= 1 && c->tiles && !cells.empty()) {
+        // BNG dense cell table (see k_join_stream_bng): decode every chip cell id to its cell
+        // coordinates and check the decoding by re-encoding the cell's lower-left corner
+        const int32_t div = (int32_t)bng::pow10i(6 - res), per = 100000 / div;
+        const int64_t p10n = (int64_t)bng::pow10i(res), p10n1 = (int64_t)bng::pow10i(res - 1);
+        std::vector<std::pair<int32_t, int32_t>> cc(cells.size());
+        bool ok = true;
+        int32_t e0 = INT32_MAX, n0 = INT32_MAX, e1 = -1, n1 = -1;
+        for (size_t k = 0; k < cells.size() && ok; k++) {
+            const int64_t id = cells[k].first;
+            if (id < 0) {
+                ok = false;
+                break;
+            }
+            const int64_t nBin = (id / 10) % p10n1, eBin = (id / p10n) % p10n1;
+            // id = 10^(2n+3) + eL 10^(2n+1) + nL 10^(2n-1) + eBin 10^n + nBin 10 + quadrant (n = res)
+            const int64_t sh_nL = (int64_t)bng::pow10i(2 * res - 1), sh_eL = (int64_t)bng::pow10i(2 * res + 1);
+            const int64_t nLet = (id / sh_nL) % 100, eLet = (id / sh_eL) % 100;
+            const int64_t ce = eLet * per + eBin, cn = nLet * per + nBin;
+            int64_t re = 0;
+            if (ce < 0 || cn < 0 || (ce + 1) * div > 10000000 || (cn + 1) * div > 10000000 ||
+                !bng::point_to_index((double)(ce * div), (double)(cn * div), res, &re) || re != id) {
+                ok = false;
+                break;
+            }
+            cc[k] = {(int32_t)ce, (int32_t)cn};
+            e0 = std::min(e0, (int32_t)ce);
+            e1 = std::max(e1, (int32_t)ce);
+            n0 = std::min(n0, (int32_t)cn);
+            n1 = std::max(n1, (int32_t)cn);
+        }
+        const int64_t ne = (int64_t)e1 - e0 + 1, nn = (int64_t)n1 - n0 + 1;
+        if (ok && ne > 0 && nn > 0 && ne * nn <= ((int64_t)1 << 26)) {
+            std::vector<uint32_t> tab((size_t)(ne * nn), 0u);
+            std::vector<tiles::BngBorderCell> border;
+            std::vector<size_t> border_at;
+            for (size_t k = 0; k < cells.size(); k++) {
+                uint64_t slot = mix64((uint64_t)cells[k].first) & (capacity - 1);
+                while (table[slot].key != cells[k].first) slot = (slot + 1) & (capacity - 1);
+                const HashEntry& he = table[slot];
+                uint32_t ent = (uint32_t)slot + 1;
+                const size_t at = (size_t)((cc[k].second - n0) * ne + (cc[k].first - e0));
+                if (he.count == 1 && (meta[he.first] & 1u) && (meta[he.first] >> 1) + 1 < (uint32_t)tiles::kMixed) {
+                    ent = kBngPure | ((meta[he.first] >> 1) + 1);
+                } else if (n_polygons < tiles::kMaxRasterKeys && c->point_raster) {
+                    border.push_back(tiles::BngBorderCell{(double)cc[k].first * div, (double)cc[k].second * div,
+                                                          (uint32_t)slot});
+                    border_at.push_back(at);
+                }
+                tab[at] = ent;
+            }
+            // leaf blocks of the border cells (C x C codes, C = option raster_cell: 3.1 m sub-cells at
+            // 100 m resolution with the default 32)
+            std::vector<uint16_t> leaf;
+            const int C = c->raster_cell;
+            if (!border.empty()) {
+                std::vector<uint32_t> sfirst(capacity, 0), scount(capacity, 0);
+                for (uint64_t q = 0; q < capacity; q++)
+                    if (table[q].key != kEmptyKey) {
+                        sfirst[q] = table[q].first;
+                        scount[q] = table[q].count;
+                    }
+                tiles::Builder::ChipSource src;
+                src.slot_first = sfirst.data();
+                src.slot_count = scount.data();
+                src.meta = meta.data();
+                src.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(),
+                                           gb.part_ring.data(), gb.geom_part.data(), gb.geom_bbox.data()};
+                src.n_polygons = n_polygons;
+                int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+                if (border.size() < ((size_t)1 << 30) && tiles::bng_leaf_blocks(src, border, (double)div, C, threads, leaf)) {
+                    for (size_t b = 0; b < border.size(); b++) tab[border_at[b]] = kBngLeaf | (uint32_t)b;
+                    ch->bng_C = C;
+                } else {
+                    leaf.clear();
+                }
+            }
+            if (leaf.empty()) leaf.assign((size_t)C * C, tiles::kMixed);
+            size_t bb = tab.size() * 4, lb = leaf.size() * 2;
+            if ((rc = ch->bng_cells.reserve(bb)) || (rc = ch->bng_leaf.reserve(lb))) {
+                ch->release_all();
+                delete ch;
+                return rc;
+            }
+            HIP_TRY(hipMemcpy(ch->bng_cells.p, tab.data(), bb, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(ch->bng_leaf.p, leaf.data(), lb, hipMemcpyHostToDevice));
+            total += lb;
+            if (!ch->bng_C) ch->bng_C = C;
+            ch->bng_ok = true;
+            ch->bng_e0 = e0;
+            ch->bng_n0 = n0;
+            ch->bng_ne = (int32_t)ne;
+            ch->bng_nn = (int32_t)nn;
+            ch->bng_div = div;
+            total += bb;
+        }
+    }
     if (grid == MOSAIC_GRID_H3 && c->tiles && !cells.empty()) {
         std::vector<int64_t> cell_ids(cells.size());
         for (size_t k = 0; k < cells.size(); k++) cell_ids[k] = cells[k].first;
@@ -1909,6 +2250,11 @@ int mosaic_chip_table_tiles(const mosaic_chips* ch, int64_t* o) {
     if (!ch || !o) return fail(MOSAIC_E_ARG, "null argument");
     o[0] = ch->tiles_ok ? 1 : 0;
     for (int k = 0; k < 6; k++) o[k + 1] = ch->tile_stats[k];
+    if (ch->grid == MOSAIC_GRID_BNG) {  // BNG dense cell table: built, cells along e, cells along n
+        o[0] = ch->bng_ok ? 1 : 0;
+        o[1] = ch->bng_ne;
+        o[2] = ch->bng_nn;
+    }
     o[7] = ch->raster_ok ? 1 : 0;
     for (int k = 0; k < 5; k++) o[k + 8] = ch->raster_stats[k];
     return MOSAIC_OK;
@@ -1978,6 +2324,11 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.tile_ent = (const uint32_t*)ch->tile_ent.p;
     a.praster = ch->praster;
     a.row_lo = 0;
+    a.bng_cells = nullptr;
+    a.bng_leaf = nullptr;
+    a.bng_e0 = a.bng_n0 = a.bng_ne = a.bng_nn = 0;
+    a.bng_div = 1;
+    a.bng_C = 1;
     a.probe_mask = c->probe_mask;
     a.mixq = nullptr;
     a.mixq_count = sc + 4;
@@ -2005,7 +2356,45 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
 #define MOSAIC_LAUNCH(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(g), dim3(c->block), SHM, c->stream, a)
         const bool tiled = rast && h3g && c->tiles && ch->tiles_ok;
         const bool praster = tiled && c->point_raster && ch->raster_ok;
-        if (praster) {
+        const bool bngdense = !h3g && rast && c->tiles && ch->bng_ok;
+        if (bngdense) {
+            a.bng_cells = (const uint32_t*)ch->bng_cells.p;
+            a.bng_e0 = ch->bng_e0;
+            a.bng_n0 = ch->bng_n0;
+            a.bng_ne = ch->bng_ne;
+            a.bng_nn = ch->bng_nn;
+            a.bng_div = ch->bng_div;
+            a.bng_leaf = (const uint16_t*)ch->bng_leaf.p;
+            a.bng_C = ch->bng_C;
+            const int64_t chunk = ((int64_t)1 << 32) - 4;
+            const int64_t rows = std::min<int64_t>(n, chunk);
+            const int gs = grid_size(c, (rows + 3) / 4);
+            if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
+            a.mixq = (uint32_t*)c->mix_queue.p;
+            for (int64_t lo = 0; lo < n; lo += chunk) {
+                JoinArgs ac = a;
+                ac.row_lo = lo;
+                ac.n = std::min<int64_t>(n, lo + chunk);
+                if (lo > 0) HIP_TRY(hipMemsetAsync(ac.mixq_count, 0, 8, c->stream));
+                if (pairs)
+                    hipLaunchKernelGGL((k_join_stream_bng<false, true>), dim3(gs), dim3(c->block), 0, c->stream, ac);
+                else if (lds)
+                    hipLaunchKernelGGL((k_join_stream_bng<true, false>), dim3(gs), dim3(c->block), shm, c->stream, ac);
+                else
+                    hipLaunchKernelGGL((k_join_stream_bng<false, false>), dim3(gs), dim3(c->block), 0, c->stream, ac);
+                HIP_TRY(hipGetLastError());
+                if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
+                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>(gs, (int64_t)c->n_cu * c->mixed_blocks_per_cu));
+                if (pairs)
+                    hipLaunchKernelGGL((k_join_mixed_bng<false, true>), dim3(gm), dim3(c->block), 0, c->stream, ac);
+                else if (lds)
+                    hipLaunchKernelGGL((k_join_mixed_bng<true, false>), dim3(gm), dim3(c->block), shm, c->stream, ac);
+                else
+                    hipLaunchKernelGGL((k_join_mixed_bng<false, false>), dim3(gm), dim3(c->block), 0, c->stream, ac);
+                HIP_TRY(hipGetLastError());
+            }
+            tstop = nullptr;
+        } else if (praster) {
             // rows in chunks of < 2^32 (uint32 queue entries); one chunk up to 4.29e9 rows
             const int64_t chunk = ((int64_t)1 << 32) - 4;  // multiple of 4: chunk starts stay 32-byte aligned
             const int64_t rows = std::min<int64_t>(n, chunk);
@@ -2032,7 +2421,15 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
         if (c->stream_groups == 2) MOSAIC_STREAM_G(VEC, VALID, 2);   \
         else MOSAIC_STREAM_G(VEC, VALID, 1);                         \
     } while (0)
-                if (a.valid) {
+                if (c->stream_mode == 1 && vec) {
+                    const int gd = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_cu, (ac.n - lo + kChunkRows - 1) / kChunkRows));
+                    if (pairs)
+                        hipLaunchKernelGGL((k_join_stream_dec<false, true>), dim3(gd), dim3(1024), shm_n, c->stream, ac);
+                    else if (lds)
+                        hipLaunchKernelGGL((k_join_stream_dec<true, false>), dim3(gd), dim3(1024), shm_c, c->stream, ac);
+                    else
+                        hipLaunchKernelGGL((k_join_stream_dec<false, false>), dim3(gd), dim3(1024), shm_n, c->stream, ac);
+                } else if (a.valid) {
                     MOSAIC_STREAM_V(false, true);
                 } else if (vec && ac.n - lo >= 4) {  // the VEC prefetch re-reads a chunk's first 4 rows
                     MOSAIC_STREAM_V(true, false);

@@ -452,5 +452,16 @@ struct Builder {
 };
 
 
+// BNG leaf blocks (tiles_build.cpp): for each border cell (lower-left corner x0, y0 in metres,
+// side `side`, chips at hash slot `slot`), C x C uint16 codes over the cell, same codes and same
+// rule as the H3 point raster (the cell is the only candidate: BNG cells are squares in the
+// points' own coordinates).  Host compiler only.
+struct BngBorderCell {
+    double x0, y0;
+    uint32_t slot;
+};
+bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
+                     int threads, std::vector<uint16_t>& blocks);
+
 }  // namespace tiles
 }  // namespace mosaic

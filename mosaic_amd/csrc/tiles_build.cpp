@@ -329,5 +329,64 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     return true;
 }
 
+bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
+                     int threads, std::vector<uint16_t>& blocks) {
+    if (C < 1 || C > 64) return false;
+    blocks.assign(cells.size() * (size_t)C * C, kMixed);
+    std::atomic<int64_t> next(0);
+    auto work = [&]() {
+        std::vector<Seg> segs;
+        std::vector<std::vector<Seg>> csegs;
+        std::vector<int32_t> ans;
+        while (true) {
+            const int64_t k = next.fetch_add(1);
+            if (k >= (int64_t)cells.size()) break;
+            const BngBorderCell& bc = cells[(size_t)k];
+            const uint32_t f0 = src.slot_first[bc.slot], n0 = src.slot_count[bc.slot];
+            std::vector<int32_t> core;
+            std::vector<uint32_t> border;
+            csegs.clear();
+            for (uint32_t c = f0; c < f0 + n0; c++) {
+                if (src.meta[c] & 1u) {
+                    core.push_back((int32_t)(src.meta[c] >> 1));
+                } else {
+                    border.push_back(c);
+                    chip_segments(src.store, c, segs);
+                    csegs.push_back(segs);
+                }
+            }
+            const double h = side / C;
+            for (int j = 0; j < C; j++)
+                for (int i = 0; i < C; i++) {
+                    // the sub-rectangle, widened past the kernel's index rounding
+                    const double ex = 1e-6 * h + 1e-9 * (fabs(bc.x0) + side);
+                    const double ey = 1e-6 * h + 1e-9 * (fabs(bc.y0) + side);
+                    Rect r{bc.x0 + h * i - ex, bc.y0 + h * j - ey, bc.x0 + h * (i + 1) + ex, bc.y0 + h * (j + 1) + ey};
+                    const double cxm = bc.x0 + h * (i + 0.5), cym = bc.y0 + h * (j + 0.5);
+                    ans = core;
+                    bool mixed = false;
+                    for (size_t b = 0; b < border.size() && !mixed; b++) {
+                        const pip::Box& bx = src.store.geom_bbox[border[b]];
+                        if (!(bx.maxx < r.x0 || bx.minx > r.x1 || bx.maxy < r.y0 || bx.miny > r.y1) &&
+                            any_seg_meets(csegs[b], r)) {
+                            mixed = true;
+                            break;
+                        }
+                        if (pip::contains(src.store, border[b], cxm, cym)) ans.push_back((int32_t)(src.meta[border[b]] >> 1));
+                    }
+                    uint16_t code = kMixed;
+                    if (!mixed) code = ans.empty() ? (uint16_t)0 : (ans.size() == 1 ? (uint16_t)(ans[0] + 1) : kMixed);
+                    blocks[(size_t)k * C * C + (size_t)j * C + i] = code;
+                }
+        }
+    };
+    const int nt = std::max(1, threads);
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    return true;
+}
+
 }  // namespace tiles
 }  // namespace mosaic

@@ -343,11 +343,17 @@ def test_join_tiled_nyc_zones_match_oracle(h3ctx, zones):
     rows, keys = h3ctx.pip_join_pairs(table, x[keep], y[keep])
     assert len(rows) == total and np.array_equal(np.bincount(keys, minlength=len(zones)), want)
     try:
+        h3ctx.set_option("stream_mode", 1)  # loader / worker variant of the stream kernel
+        assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want)
+        rows2, keys2 = h3ctx.pip_join_pairs(table, x[keep], y[keep])
+        assert np.array_equal(np.sort(rows2), np.sort(rows))
+        h3ctx.set_option("stream_mode", 0)
         for tiles, praster in ((1, 0), (0, 0)):
             h3ctx.set_option("tiles", tiles)
             h3ctx.set_option("point_raster", praster)
             assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (tiles, praster)
     finally:
+        h3ctx.set_option("stream_mode", 0)
         h3ctx.set_option("tiles", 1)
         h3ctx.set_option("point_raster", 1)
     table.close()
@@ -421,6 +427,62 @@ def test_join_device_tensors(h3ctx, zones):
     got = h3ctx.pip_join_count(table, torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda"))
     want, _ = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_H3, 9, x, y, npoly, threads=8)
     assert np.array_equal(got.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("res", [3, 4])
+def test_join_bng_dense_table(bngctx, res):
+    """BNG dense cell table (k_join_stream_bng): tessellated chips (planar stand-in coordinates in
+    metres), uniform points, points on and 1 ulp around cell lines, negative and >= 1e7 coordinates
+    (outside the one-to-one range: generic path) -- counts equal the oracle's and the generic
+    kernel's."""
+    from mosaic_amd.context import tessellate
+
+    london = PolygonSet.load("london_postcode_zones")
+    ids = list(range(0, 177, 3))
+    xy = (london.xy - london.xy.min(0)) * 1e5 + np.array([500000.0, 150000.0])
+    proj = PolygonSet(xy, london.ring_offsets, london.part_rings, london.geom_parts).subset(ids)
+    chips = tessellate("BNG", proj, res)
+    table = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
+                              n_polygons=len(ids))
+    assert table.tiles()["built"] == 1
+    rng = np.random.default_rng(40 + res)
+    x0, y0, x1, y1 = proj.bbox()
+    x = rng.uniform(x0 - 2000, x1 + 2000, 400_000)
+    y = rng.uniform(y0 - 2000, y1 + 2000, 400_000)
+    step = 10.0 ** (6 - res)
+    lx = np.floor(rng.uniform(x0, x1, 20_000) / step) * step  # on vertical cell lines
+    ly = np.floor(rng.uniform(y0, y1, 20_000) / step) * step  # on horizontal cell lines
+    ux, uy = rng.uniform(x0, x1, 20_000), rng.uniform(y0, y1, 20_000)
+    lines_x = np.concatenate([lx, np.nextafter(lx, -np.inf), np.nextafter(lx, np.inf), ux, ux])
+    lines_y = np.concatenate([uy, uy, uy, ly, np.nextafter(ly, -np.inf)])
+    odd_x = np.array([-0.5, -1.5, -150000.0, 1e7, 2.5e9, x0 + 10.0, 5e6])
+    odd_y = np.array([y0 + 10.0, y0 + 20.0, y0, y0 + 30.0, y0 + 40.0, -0.25, 1.2e7])
+    x = np.concatenate([x, lines_x, odd_x])
+    y = np.concatenate([y, lines_y, odd_y])
+    offs, data = chips["wkb"]
+    oc = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+              wkb_offsets=offs, wkb=data)
+    want, total = oracle.pip_join(oc, oracle.GRID_BNG, res, x, y, len(ids), threads=8)
+    assert total > 10_000
+    assert np.array_equal(bngctx.pip_join_count(table, x, y), want)
+    rows, keys = bngctx.pip_join_pairs(table, x, y)
+    assert len(rows) == total and np.array_equal(np.bincount(keys, minlength=len(ids)), want)
+    bngctx.set_option("tiles", 0)
+    try:
+        assert np.array_equal(bngctx.pip_join_count(table, x, y), want)
+    finally:
+        bngctx.set_option("tiles", 1)
+    bngctx.set_option("point_raster", 0)  # dense cell table without the border-cell leaf blocks
+    try:
+        t2 = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
+                               n_polygons=len(ids))
+    finally:
+        bngctx.set_option("point_raster", 1)
+    assert np.array_equal(bngctx.pip_join_count(t2, x, y), want)
+    t2.close()
+    with pytest.raises(IllegalStateException, match="NaN"):
+        bngctx.pip_join_count(table, np.array([x0 + 5.0, np.nan]), np.array([y0 + 5.0, y0]))
+    table.close()
 
 
 def test_join_bng(bngctx):

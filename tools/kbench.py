@@ -24,6 +24,7 @@ def main():
     p.add_argument("--clustered", action="store_true")
     p.add_argument("--rasters", type=int, nargs="*", default=[8, 16, 32])
     p.add_argument("--lane-edges", type=int, nargs="*", default=[0, 4, 8])
+    p.add_argument("--stream-mode", type=int, default=0, help="0 k_join_stream, 1 loader/worker k_join_stream_dec")
     p.add_argument("--groups", type=int, nargs="*", default=[1], help="stream_groups values")
     p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*",
                    default=[(1, 1), (1, 0), (0, 0)], help="TILES:POINT_RASTER pairs")
@@ -47,6 +48,7 @@ def main():
     chips = tessellate("H3", zones, args.res)
     ctx = MosaicContext.build("H3")
     ctx.set_option("block", args.block)
+    ctx.set_option("stream_mode", args.stream_mode)
     ctx.set_option("blocks_per_cu", args.bpc)
     n = int(args.n)
     if args.clustered:

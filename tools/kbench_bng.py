@@ -1,0 +1,70 @@
+"""BNG chip join timing (GPU box): the C5 shape -- London postcode zones (planar stand-in
+coordinates in metres, as in tests/test_gpu_parity.py::test_join_bng), BNG res 4 (100 m), uniform
+points over the zones' bbox.  Prints one JSON line.
+
+    python tools/kbench_bng.py [--n 1e9] [--res 4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--n", type=float, default=1e9)
+    p.add_argument("--res", type=int, default=4)
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--cells", type=int, default=32, help="leaf sub-cells per border cell side (raster_cell)")
+    args = p.parse_args()
+    import torch
+
+    from mosaic_amd import MosaicContext
+    from mosaic_amd.context import tessellate
+    from mosaic_amd.data import PolygonSet, uniform_points_device
+
+    london = PolygonSet.load("london_postcode_zones")
+    xy = (london.xy - london.xy.min(0)) * 1e5 + np.array([500000.0, 150000.0])
+    proj = PolygonSet(xy, london.ring_offsets, london.part_rings, london.geom_parts)
+    t0 = time.perf_counter()
+    chips = tessellate("BNG", proj, args.res)
+    t_tess = time.perf_counter() - t0
+    ctx = MosaicContext.build("BNG")
+    ctx.set_option("raster_cell", args.cells)
+    t0 = time.perf_counter()
+    table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
+                           n_polygons=len(proj))
+    t_build = time.perf_counter() - t0
+    n = int(args.n)
+    x, y = uniform_points_device(proj.bbox(), n, seed=5)
+    counts = torch.zeros(len(proj), dtype=torch.int64, device="cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.set_option("async", 1)
+    ctx.pip_join_count(table, x, y, out=counts)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(args.reps):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        ctx.pip_join_count(table, x, y, out=counts)
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    ctx.set_option("async", 0)
+    ctx.pip_join_count(table, x, y, out=counts)
+    st = ctx.last_stats()
+    ms = float(np.median(ts))
+    print(json.dumps({"workload": f"BNG res {args.res}, {len(proj)} London zones (planar stand-in), {n} uniform points",
+                      "ms": ms, "points_per_s": n / ms * 1e3, "GBps": n * 16 / ms / 1e6, "chips": table.info(),
+                      "tiles": table.tiles(), "tessellate_s": round(t_tess, 2), "build_s": round(t_build, 2),
+                      "pairs": int(counts.sum().item()), **st}))
+
+
+if __name__ == "__main__":
+    main()
