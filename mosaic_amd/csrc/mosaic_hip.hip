@@ -94,9 +94,12 @@ struct JoinArgs {
     int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
     uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
     unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)
+    int tile_lds_n;                   // k_join_stream: tile_base entries copied to LDS (0: read it
+                                      // from global memory)
     int probe_mask;                   // measurement only (option "probe_mask"): 1 = k_join_mixed skips
                                       // the chip loop, 2 = it also skips the cell lookup; k_join_stream:
-                                      // 4 = no sub-block lookups, 16 = no counting, 32 = no LDS quad
+                                      // 4 = no sub-block lookups, 8 = no leaf-block gathers,
+                                      // 16 = no counting, 32 = no LDS quad
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
     unsigned long long* amb_queue;  // rows for the exact H3 pass
@@ -791,25 +794,31 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 #ifndef MOSAIC_STREAM_WAVES
 #define MOSAIC_STREAM_WAVES 6  // k_join_stream: waves per SIMD the register budget must allow
 #endif
+// k_join_stream dynamic LDS: [per-polygon counts (LDS_COUNTS)] [per-wave mixed-row stages]
+// [tile_base (tile_lds_n words)] [quad level of the raster (if any)]
+static const size_t kStreamLdsTile = 80 * 1024;  // LDS per workgroup up to which tile_base joins it
+static inline size_t stream_stage_words(int block, int G) { return (size_t)(block / 64) * (64 + 256 * (size_t)G); }
+
 template <bool LDS_COUNTS, bool PAIRS, bool VEC, bool VALID, int G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOSAIC_STREAM_WAVES)))
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MOSAIC_STREAM_WAVES)))
 k_join_stream(JoinArgs a) {
     extern __shared__ unsigned int lds[];
-    // dynamic LDS: [per-polygon counts (LDS_COUNTS)] [quad level of the raster (if any)]
-    uint16_t* quad = a.praster.quad ? (uint16_t*)(lds + (LDS_COUNTS ? a.n_polygons : 0)) : nullptr;
+    uint32_t* stage = lds + (LDS_COUNTS ? a.n_polygons : 0);
+    uint32_t* tbase = stage + (blockDim.x >> 6) * (64 + 256 * G);
+    uint16_t* quad = a.praster.quad ? (uint16_t*)(tbase + a.tile_lds_n) : nullptr;
     if (quad) {
         const int nq = a.praster.qnx * a.praster.qny;
         for (int k = threadIdx.x; k < nq; k += blockDim.x) quad[k] = a.praster.quad[k];
     }
-    counts_init<LDS_COUNTS>(a, lds);  // (its barrier also publishes the quad level)
+    for (int k = threadIdx.x; k < a.tile_lds_n; k += blockDim.x) tbase[k] = a.praster.tile_base[k];
+    counts_init<LDS_COUNTS>(a, lds);  // (its barrier also publishes the quad level and tile_base)
     if (!LDS_COUNTS) __syncthreads();
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     // mixed rows are staged per wave in LDS and flushed to the global queue once 64 or more are
     // waiting (one atomic per flush: a per-iteration atomic on one counter serialises the grid);
     // the stage holds < 64 + 256 G rows
-    __shared__ uint32_t stage[4][64 + 256 * G];
-    uint32_t* wq = stage[(threadIdx.x >> 6) & 3];
+    uint32_t* wq = stage + (threadIdx.x >> 6) * (64 + 256 * G);
     uint32_t wn = 0;  // wave-uniform fill level
     // G groups of 4 consecutive rows per lane and iteration; group g is a grid-wide slice of
     // 4 * (threads) rows, so each group's loads stay coalesced across the wave
@@ -864,9 +873,19 @@ k_join_stream(JoinArgs a) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) L[g].in[k] = false;
             }
+            if (a.tile_lds_n) tiles::raster_base4_lds(tbase, L[g]);
         }
+        if (a.probe_mask & 8) {  // measurement only: no leaf-block gathers
 #pragma unroll
-        for (int g = 0; g < G; g++) tiles::raster_base4(a.praster, L[g]);
+            for (int g = 0; g < G; g++)
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (tiles::sub_is_block(L[g].e[k])) L[g].e[k] = 0;
+        }
+        if (!a.tile_lds_n) {
+#pragma unroll
+            for (int g = 0; g < G; g++) tiles::raster_base4(a.praster, L[g]);
+        }
 #pragma unroll
         for (int g = 0; g < G; g++) tiles::raster_gather4(a.praster, L[g]);
         if (VEC) {
@@ -919,6 +938,94 @@ k_join_stream(JoinArgs a) {
         base = __shfl(base, 0, 64);
         for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
     }
+    counts_flush<LDS_COUNTS>(a, lds, 0u);
+}
+
+// ---- k_join_stream_pipe (option stream_mode 2): k_join_stream's lookups software-pipelined over
+// three iterations, so no wait is on a load issued in the same iteration.  Iteration t issues
+// the leaf-block gathers of rows t (their sub-block entries arrived), the sub-block gathers of
+// rows t + 1 (their coordinates arrived) and the coordinate loads of rows t + 2, in that order,
+// and finishes rows t - 1 (their leaf codes arrived): vector-memory returns retire in issue order,
+// which is also the order the next iteration consumes them in.  Four rows per lane, both arrays
+// 16-byte aligned; rows past the last multiple of 4 go to the mixed queue.
+#ifndef MOSAIC_PIPE_WAVES
+#define MOSAIC_PIPE_WAVES 5  // k_join_stream_pipe: waves per SIMD the register budget must allow
+#endif
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MOSAIC_PIPE_WAVES)))
+k_join_stream_pipe(JoinArgs a) {
+    extern __shared__ unsigned int lds[];
+    uint32_t* stage = lds + (LDS_COUNTS ? a.n_polygons : 0);
+    uint32_t* tbase = stage + (blockDim.x >> 6) * (64 + 256);
+    uint16_t* quad = a.praster.quad ? (uint16_t*)(tbase + a.tile_lds_n) : nullptr;
+    if (quad) {
+        const int nq = a.praster.qnx * a.praster.qny;
+        for (int k = threadIdx.x; k < nq; k += blockDim.x) quad[k] = a.praster.quad[k];
+    }
+    for (int k = threadIdx.x; k < a.tile_lds_n; k += blockDim.x) tbase[k] = a.praster.tile_base[k];
+    counts_init<LDS_COUNTS>(a, lds);
+    if (!LDS_COUNTS) __syncthreads();
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    uint32_t* wq = stage + (threadIdx.x >> 6) * (64 + 256);
+    uint32_t wn = 0;
+    const int64_t n4 = a.row_lo + ((a.n - a.row_lo) & ~(int64_t)3);  // rows handled in groups of 4
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    const int64_t i0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 4;
+    auto load = [&](int64_t r, v2d* cx, v2d* cy) {  // unconditional: past the end, the chunk's first rows
+        const int64_t r1 = r < n4 ? r : a.row_lo;
+        cx[0] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1));
+        cx[1] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1 + 2));
+        cy[0] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1));
+        cy[1] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1 + 2));
+    };
+    auto issue = [&](int64_t r, const v2d* cx, const v2d* cy, tiles::Lookup4& L) {
+        const double x[4] = {cx[0].x, cx[0].y, cx[1].x, cx[1].y}, y[4] = {cy[0].x, cy[0].y, cy[1].x, cy[1].y};
+        const bool lv = r < n4;
+        const bool live[4] = {lv, lv, lv, lv};
+        tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L, quad);
+        if (a.tile_lds_n) tiles::raster_base4_lds(tbase, L);
+    };
+    // prologue: rows t = 0 looked up (sub-block gathers out), rows t = 1 loading
+    v2d cx[2], cy[2];
+    tiles::Lookup4 Lc, Lp;
+    load(i0, cx, cy);
+    issue(i0, cx, cy, Lc);
+    load(i0 + stride, cx, cy);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        Lp.in[k] = false;
+        Lp.out[k] = 0;
+        Lp.e[k] = 0;
+        Lp.b[k] = 0;
+    }
+    for (int64_t wp = w0 - stride, r = i0; wp < n4; wp += stride, r += stride) {
+        // rows r (Lc): leaf-block gathers
+        if (!a.tile_lds_n) tiles::raster_base4(a.praster, Lc);
+        tiles::raster_gather4(a.praster, Lc);
+        // rows r - stride (Lp): finish
+        tiles::raster_select4(Lp);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint16_t rc = Lp.out[k];
+            if (rc != 0 && rc != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, r - stride + k, (uint32_t)rc - 1u, lds);
+            stage_push(wq, wn, rc == tiles::kMixed, (uint32_t)(r - stride + k - a.row_lo), lt_mask);
+        }
+        stage_flush(a, wq, wn, lane, 64);
+        // rows r + stride: sub-block gathers; rows r + 2 stride: coordinates
+        tiles::Lookup4 Ln;
+        issue(r + stride, cx, cy, Ln);
+        load(r + 2 * stride, cx, cy);
+        Lp = Lc;
+        Lc = Ln;
+    }
+    // rows past the last multiple of 4 (fewer than 4): the mixed queue
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        const bool tail = n4 + lane < a.n;
+        stage_push(wq, wn, tail, (uint32_t)(n4 + lane - a.row_lo), lt_mask);
+    }
+    stage_flush(a, wq, wn, lane, 1);
     counts_flush<LDS_COUNTS>(a, lds, 0u);
 }
 
@@ -1379,9 +1486,12 @@ struct mosaic_ctx {
     int raster_cell = 32; // point raster: leaf cells per sub-block side
     int raster_quad = 1;  // point raster: LDS quad level
     int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
+    int stream_block = 256; // k_join_stream workgroup size (64 .. 1024, a multiple of 64)
+    int tile_lds = 1;       // k_join_stream: tile_base in LDS when it fits (kStreamLdsTile)
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
     int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
-    int stream_mode = 0;          // 0: k_join_stream, 1: k_join_stream_dec (loader / worker waves)
+    int stream_mode = 0;          // 0: k_join_stream, 1: k_join_stream_dec (loader / worker waves),
+                                  // 2: k_join_stream_pipe (lookups pipelined over iterations)
     int probe_mask = 0;     // measurement only: see JoinArgs::probe_mask (results are wrong when set)
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     int64_t stats[3] = {0, 0, 0};
@@ -1609,7 +1719,7 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
         if (v < 0 || v > 63) return fail(MOSAIC_E_ARG, "probe_mask must be in [0, 63]");
         c->probe_mask = (int)v;
     } else if (k == "stream_mode") {
-        if (v != 0 && v != 1) return fail(MOSAIC_E_ARG, "stream_mode must be 0 or 1");
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "stream_mode must be 0, 1 or 2");
         c->stream_mode = (int)v;
     } else if (k == "mixed_rows") {
         if (v != 1 && v != 2 && v != 4) return fail(MOSAIC_E_ARG, "mixed_rows must be 1, 2 or 4");
@@ -1621,7 +1731,15 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
         if (v != 1 && v != 2) return fail(MOSAIC_E_ARG, "stream_groups must be 1 or 2");
         c->stream_groups = (int)v;
     } else if (k == "raster_quad") {
-        c->raster_quad = v ? 1 : 0;
+        if (v < 0 || v > tiles::kQuadLimit)
+            return fail(MOSAIC_E_ARG, "raster_quad must be 0 (off), 1 (default size) or an entry budget <= " +
+                                          std::to_string(tiles::kQuadLimit));
+        c->raster_quad = (int)v;
+    } else if (k == "tile_lds") {
+        c->tile_lds = v ? 1 : 0;
+    } else if (k == "stream_block") {
+        if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, 1024]");
+        c->stream_block = (int)v;
     } else if (k == "raster_cell") {
         if (v < 1 || v > 32) return fail(MOSAIC_E_ARG, "raster_cell must be in [1, 32]");
         c->raster_cell = (int)v;
@@ -2170,6 +2288,7 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
                                            gb.part_ring.data(), gb.geom_part.data(), gb.geom_bbox.data()};
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+                tb.quad_max = c->raster_quad > 1 ? c->raster_quad : tiles::kQuadMax;
                 if (tb.build_raster(src, c->raster_sub, c->raster_cell, threads)) {
                     size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
                     if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
@@ -2330,6 +2449,7 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.bng_div = 1;
     a.bng_C = 1;
     a.probe_mask = c->probe_mask;
+    a.tile_lds_n = 0;
     a.mixq = nullptr;
     a.mixq_count = sc + 4;
     a.counts = dcounts;
@@ -2398,7 +2518,11 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
             // rows in chunks of < 2^32 (uint32 queue entries); one chunk up to 4.29e9 rows
             const int64_t chunk = ((int64_t)1 << 32) - 4;  // multiple of 4: chunk starts stay 32-byte aligned
             const int64_t rows = std::min<int64_t>(n, chunk);
-            const int gs = grid_size(c, (rows + 4 * c->stream_groups - 1) / (4 * c->stream_groups));
+            // k_join_stream grid: blocks_per_cu x block threads per CU, in stream_block workgroups
+            const int64_t rows_g = (rows + 4 * c->stream_groups - 1) / (4 * c->stream_groups);
+            const int gs = (int)std::max<int64_t>(1, std::min<int64_t>(
+                (rows_g + c->stream_block - 1) / c->stream_block,
+                (int64_t)c->n_cu * std::max(1, c->blocks_per_cu * c->block / c->stream_block)));
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
             a.mixq_count = sc + 4;
@@ -2409,7 +2533,16 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
                 ac.n = std::min<int64_t>(n, lo + chunk);
                 const size_t qb = ch->praster.quad ? (size_t)ch->praster.qnx * ch->praster.qny * 2 : 0;
                 const size_t shm_c = (lds ? shm : 0) + qb, shm_n = qb;  // counts (LDS_COUNTS) + quad
-#define MOSAIC_STREAM(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(gs), dim3(c->block), SHM, c->stream, ac)
+                // k_join_stream: + the per-wave stages (+ tile_base when the workgroup's LDS stays
+                // within kStreamLdsTile)
+                size_t sw = stream_stage_words(c->stream_block, c->stream_groups == 2 ? 2 : 1) * 4;
+                const int64_t ntiles = (int64_t)ch->tgrid.nx * ch->tgrid.ny;
+                if (c->tile_lds && (lds ? shm : 0) + qb + sw + (size_t)ntiles * 4 <= kStreamLdsTile) {
+                    ac.tile_lds_n = (int)ntiles;
+                    sw += (size_t)ntiles * 4;
+                }
+#define MOSAIC_STREAM(KERNEL, SHM) \
+    hipLaunchKernelGGL(KERNEL, dim3(gs), dim3(c->stream_block), (SHM) + sw, c->stream, ac)
 #define MOSAIC_STREAM_G(VEC, VALID, G)                                                  \
     do {                                                                                \
         if (pairs) MOSAIC_STREAM((k_join_stream<false, true, VEC, VALID, G>), shm_n);    \
@@ -2429,6 +2562,14 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
                         hipLaunchKernelGGL((k_join_stream_dec<true, false>), dim3(gd), dim3(1024), shm_c, c->stream, ac);
                     else
                         hipLaunchKernelGGL((k_join_stream_dec<false, false>), dim3(gd), dim3(1024), shm_n, c->stream, ac);
+                } else if (c->stream_mode == 2 && vec && !a.valid && ac.n - lo >= 4) {
+                    const size_t swp = stream_stage_words(c->stream_block, 1) * 4 + (size_t)ac.tile_lds_n * 4;
+                    if (pairs)
+                        hipLaunchKernelGGL((k_join_stream_pipe<false, true>), dim3(gs), dim3(c->stream_block), shm_n + swp, c->stream, ac);
+                    else if (lds)
+                        hipLaunchKernelGGL((k_join_stream_pipe<true, false>), dim3(gs), dim3(c->stream_block), shm_c + swp, c->stream, ac);
+                    else
+                        hipLaunchKernelGGL((k_join_stream_pipe<false, false>), dim3(gs), dim3(c->stream_block), shm_n + swp, c->stream, ac);
                 } else if (a.valid) {
                     MOSAIC_STREAM_V(false, true);
                 } else if (vec && ac.n - lo >= 4) {  // the VEC prefetch re-reads a chunk's first 4 rows
@@ -2441,7 +2582,9 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
 #undef MOSAIC_STREAM
                 HIP_TRY(hipGetLastError());
                 if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
-                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>(gs, (int64_t)c->n_cu * c->mixed_blocks_per_cu));
+                // (the queue holds at most the chunk's rows)
+                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + 4 * c->block - 1) / (4 * c->block),
+                                                                           (int64_t)c->n_cu * c->mixed_blocks_per_cu));
 #define MOSAIC_MIXED(KERNEL, SHM) \
     hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac)
                 hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too

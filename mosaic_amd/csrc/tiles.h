@@ -63,12 +63,15 @@ struct PointRaster {
     const uint16_t* blocks;     // C x C leaf codes per mixed sub-block
     double sx, sy;              // sub-blocks per degree
     int32_t nx, ny, C, sshift, tnx;  // S = 1 << sshift sub-blocks per tile side
-    // quad level: one uint16 per 2^qshift x 2^qshift sub-blocks, the code they all share or kMixed
-    // (= look at the sub-block); small enough (<= kQuadMax entries) to live in LDS
+    // quad level: one uint16 per 2^qshift x 2^qshift sub-blocks, the code they all share, kMixed
+    // (= look at the sub-block) or kSubBlock | r (= look at the sub-block's copy in compact quad r,
+    // sub[nx * ny + (r << 2 qshift) + local]); small enough (<= kQuadMax entries) to live in LDS
     const uint16_t* quad;       // nullptr: no quad level
     int32_t qnx, qny, qshift;
 };
-static const int kQuadMax = 8192;
+static const int kQuadMax = 8192;     // default quad-level entry budget
+static const int kQuadRefMax = 0x7ffe;  // quad entries kSubBlock | r, r <= kQuadRefMax: compact sub-blocks
+static const int kQuadLimit = 65536;  // option raster_quad: largest entry budget
 
 MOSAIC_HD bool sub_is_block(uint32_t e) { return (e & kSubBlock) && e != kMixed; }
 
@@ -80,7 +83,7 @@ struct Lookup4 {
 };
 MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const double* x, const double* y,
                              const bool* live, Lookup4& L, const uint16_t* quad_lds = nullptr) {
-    uint32_t qi[4];
+    uint32_t qi[4], qo[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const double gx = (x[k] - x0) * r.sx, gy = (y[k] - y0) * r.sy;
@@ -89,6 +92,8 @@ MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const d
         L.si[k] = (uint32_t)iy * (uint32_t)r.nx + (uint32_t)ix;
         L.ti[k] = (uint32_t)((iy >> r.sshift) * r.tnx + (ix >> r.sshift));
         qi[k] = (uint32_t)((iy >> r.qshift) * r.qnx + (ix >> r.qshift));
+        const int qm = (1 << r.qshift) - 1;
+        qo[k] = (uint32_t)(((iy & qm) << r.qshift) | (ix & qm));
         int cx = L.in[k] ? (int)((gx - (double)ix) * (double)r.C) : 0;
         int cy = L.in[k] ? (int)((gy - (double)iy) * (double)r.C) : 0;
         cx = cx < r.C - 1 ? cx : r.C - 1;
@@ -103,9 +108,11 @@ MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const d
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint16_t q = quad_lds[qi[k]];
-            if (L.in[k] && q != kMixed) {
+            if (L.in[k] && !(q & kSubBlock)) {
                 L.out[k] = q;
                 L.in[k] = false;
+            } else if (q != kMixed) {  // compact copy
+                L.si[k] = (uint32_t)r.nx * (uint32_t)r.ny + ((uint32_t)(q & 0x7fffu) << (2 * r.qshift)) + qo[k];
             }
         }
 #pragma unroll
@@ -120,6 +127,12 @@ MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const d
 MOSAIC_HD void raster_base4(const PointRaster& r, Lookup4& L) {
 #pragma unroll
     for (int k = 0; k < 4; k++) L.base[k] = r.tile_base[(L.in[k] && sub_is_block(L.e[k])) ? L.ti[k] : 0];
+}
+// the same from an LDS copy of tile_base: every lane reads its tile's base (no dependence on the
+// sub-block entries, so the reads go out beside the sub-block gathers)
+MOSAIC_HD void raster_base4_lds(const uint32_t* tile_base_lds, Lookup4& L) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) L.base[k] = tile_base_lds[L.in[k] ? L.ti[k] : 0];
 }
 MOSAIC_HD void raster_gather4(const PointRaster& r, Lookup4& L) {
 #pragma unroll
@@ -241,6 +254,7 @@ struct Builder {
     std::vector<uint16_t> blocks;
     std::vector<uint16_t> quad;  // quad level (empty: none)
     int qshift = 0, qnx = 0, qny = 0;
+    int quad_max = kQuadMax;  // quad-level entry budget (set before build_raster)
     int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0;
     // Chip access for the raster classification (host memory)
     struct ChipSource {

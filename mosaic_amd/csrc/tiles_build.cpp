@@ -304,9 +304,9 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     n_sub_pure = pure.load();
     n_sub_mixed = mixed.load();
     n_cell_mixed = cmixed.load();
-    // quad level: the smallest power-of-two group of sub-blocks whose table fits kQuadMax entries
+    // quad level: the smallest power-of-two group of sub-blocks whose table fits quad_max entries
     qshift = 0;
-    while (qshift < 16 && ((NX + (1 << qshift) - 1) >> qshift) * ((NY + (1 << qshift) - 1) >> qshift) > kQuadMax)
+    while (qshift < 16 && ((NX + (1 << qshift) - 1) >> qshift) * ((NY + (1 << qshift) - 1) >> qshift) > quad_max)
         qshift++;
     if (qshift < 16) {
         qnx = (int)((NX + (1 << qshift) - 1) >> qshift);
@@ -325,6 +325,31 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                     quad[q] = kMixed;
                 }
             }
+        // compact copies of the non-uniform quads' sub-block entries behind the grid's own
+        // (quad entry kSubBlock | r: quad r's 2^qshift x 2^qshift entries, row-major, from
+        // sub[nx * ny + (r << 2 qshift)]), so the sub-block lookups that pass the quad level
+        // gather from a table the size of the mixed quads rather than of the grid
+        const int64_t QS = (int64_t)1 << qshift, QQ = QS * QS;
+        int64_t nref = 0;
+        for (uint16_t e : quad) nref += e == kMixed;
+        if (qshift <= 6 && nref <= kQuadRefMax + 1 && NX * NY + nref * QQ < ((int64_t)1 << 31)) {
+            const size_t base = sub.size();
+            sub.resize(base + (size_t)(nref * QQ), 0);
+            int64_t r = 0;
+            for (int64_t qj = 0; qj < qny; qj++)
+                for (int64_t qi = 0; qi < qnx; qi++) {
+                    uint16_t& qe = quad[(size_t)(qj * qnx + qi)];
+                    if (qe != kMixed) continue;
+                    uint16_t* dst = sub.data() + base + (size_t)(r * QQ);
+                    for (int64_t dj = 0; dj < QS; dj++)
+                        for (int64_t di = 0; di < QS; di++) {
+                            const int64_t j = qj * QS + dj, i = qi * QS + di;
+                            if (j < NY && i < NX) dst[dj * QS + di] = sub[(size_t)(j * NX + i)];
+                        }
+                    qe = (uint16_t)(kSubBlock | r);
+                    r++;
+                }
+        }
     }
     return true;
 }

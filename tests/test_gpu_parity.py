@@ -343,17 +343,29 @@ def test_join_tiled_nyc_zones_match_oracle(h3ctx, zones):
     rows, keys = h3ctx.pip_join_pairs(table, x[keep], y[keep])
     assert len(rows) == total and np.array_equal(np.bincount(keys, minlength=len(zones)), want)
     try:
-        h3ctx.set_option("stream_mode", 1)  # loader / worker variant of the stream kernel
-        assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want)
-        rows2, keys2 = h3ctx.pip_join_pairs(table, x[keep], y[keep])
-        assert np.array_equal(np.sort(rows2), np.sort(rows))
+        # loader / worker and pipelined variants of the stream kernel, other workgroup sizes
+        for mode, block in ((1, 256), (2, 256), (2, 512), (0, 512), (0, 1024)):
+            h3ctx.set_option("stream_mode", mode)
+            h3ctx.set_option("stream_block", block)
+            assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (mode, block)
+            rows2, keys2 = h3ctx.pip_join_pairs(table, x[keep], y[keep])
+            assert np.array_equal(np.sort(rows2), np.sort(rows)), (mode, block)
+        # row counts that are not multiples of 4 (the pipelined kernel queues the tail rows)
+        xs, ys = x[keep], y[keep]
+        for cut in (1, 2, 3, len(xs) - 5):
+            h3ctx.set_option("stream_mode", 0)
+            ref = h3ctx.pip_join_count(table, xs[:-cut], ys[:-cut])
+            h3ctx.set_option("stream_mode", 2)
+            assert np.array_equal(h3ctx.pip_join_count(table, xs[:-cut], ys[:-cut]), ref), cut
         h3ctx.set_option("stream_mode", 0)
+        h3ctx.set_option("stream_block", 256)
         for tiles, praster in ((1, 0), (0, 0)):
             h3ctx.set_option("tiles", tiles)
             h3ctx.set_option("point_raster", praster)
             assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (tiles, praster)
     finally:
         h3ctx.set_option("stream_mode", 0)
+        h3ctx.set_option("stream_block", 256)
         h3ctx.set_option("tiles", 1)
         h3ctx.set_option("point_raster", 1)
     table.close()

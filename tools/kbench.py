@@ -14,6 +14,10 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+DEFAULTS = {"tile_lds": 1, "stream_mode": 0, "stream_block": 256, "probe_mask": 0, "stream_groups": 1, "mixed_rows": 4,
+            "mixed_blocks_per_cu": 8}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=float, default=1e8)
@@ -26,6 +30,10 @@ def main():
     p.add_argument("--lane-edges", type=int, nargs="*", default=[0, 4, 8])
     p.add_argument("--stream-mode", type=int, default=0, help="0 k_join_stream, 1 loader/worker k_join_stream_dec")
     p.add_argument("--groups", type=int, nargs="*", default=[1], help="stream_groups values")
+    p.add_argument("--quads", type=int, nargs="*", default=[1], help="raster_quad values (1 default, else entry budget)")
+    p.add_argument("--stream-blocks", type=int, nargs="*", default=[], help="k_join_stream workgroup sizes to time")
+    p.add_argument("--sweeps", nargs="*", default=[],
+                   help="launch-option sets to time on each table, e.g. tile_lds=0 stream_block=512,probe_mask=8")
     p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*",
                    default=[(1, 1), (1, 0), (0, 0)], help="TILES:POINT_RASTER pairs")
     p.add_argument("--point-raster", type=lambda v: tuple(int(q) for q in v.split("x")), nargs="*",
@@ -96,18 +104,22 @@ def main():
     for tiles, praster in args.modes:
         for sub, cell in (args.point_raster if praster else [(32, 16)]):
             for grp in args.groups:
-                tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}_g{grp}" if praster else "")
-                if args.all_core:
-                    variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, (sub, cell), grp))
-                for r in args.rasters:
-                    for le in args.lane_edges:
-                        variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster,
-                                         (sub, cell), grp))
+                for quad in (args.quads if praster else [1]):
+                    tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}_g{grp}" if praster else "")
+                    tag += f"_q{quad}" if quad != 1 else ""
+                    if args.all_core:
+                        variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, (sub, cell), grp,
+                                         quad))
+                    for r in args.rasters:
+                        for le in args.lane_edges:
+                            variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster,
+                                             (sub, cell), grp, quad))
     if args.legacy:
-        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, (32, 16), 1),
-                     ("join_full_slab", False, 2, 16, 8, 0, 0, (32, 16), 1)]
-    for name, core, mode, raster, lane_edges, tiles, praster, (sub, cell), grp in variants:
+        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, (32, 16), 1, 1),
+                     ("join_full_slab", False, 2, 16, 8, 0, 0, (32, 16), 1, 1)]
+    for name, core, mode, raster, lane_edges, tiles, praster, (sub, cell), grp, quad in variants:
         ctx.set_option("stream_groups", grp)
+        ctx.set_option("raster_quad", quad)
         ctx.set_option("tiles", tiles)
         ctx.set_option("point_raster", praster)
         ctx.set_option("raster_sub", sub)
@@ -131,6 +143,29 @@ def main():
         ctx.set_option("async", 1)
         tl = table.tiles()
         probes = {}
+        for sb in args.stream_blocks:
+            ctx.set_option("stream_block", sb)
+            ctx.pip_join_count(table, x, y, out=counts)
+            ctx.set_option("timing", 2)
+            for _ in range(3):
+                ctx.pip_join_count(table, x, y, out=counts)
+            kt3 = ctx.kernel_times()
+            probes[f"sblock{sb}_ms"] = [round(float(np.median(kt3[0::2])), 4), round(float(np.median(kt3[1::2])), 4)]
+            ctx.set_option("timing", 0)
+        ctx.set_option("stream_block", 256)
+        for sw in args.sweeps:
+            kv = [(q.split("=")[0], int(q.split("=")[1])) for q in sw.split(",")]
+            for k, v in kv:
+                ctx.set_option(k, v)
+            ctx.pip_join_count(table, x, y, out=counts)
+            ctx.set_option("timing", 2)
+            for _ in range(3):
+                ctx.pip_join_count(table, x, y, out=counts)
+            kt3 = ctx.kernel_times()
+            probes[sw] = [round(float(np.median(kt3[0::2])), 4), round(float(np.median(kt3[1::2])), 4)]
+            ctx.set_option("timing", 0)
+            for k, v in kv:
+                ctx.set_option(k, DEFAULTS[k])
         for pm in args.stream_probes:
             ctx.set_option("probe_mask", pm)
             ctx.set_option("timing", 2)
