@@ -81,10 +81,10 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * (raster cells per chip side, for tables built afterwards), "lane_edges", "tiles" (0/1: H3 tile
  * directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
  * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
- * side, a power of two, and cells per sub-block side, for tables built afterwards), "raster_quad"
- * (its LDS level: 0 off, 1 default budget of 8192 entries, or an entry budget <= 65536),
- * "stream_block" (k_join_stream workgroup size, a multiple of 64; the LDS quad level is held once
- * per workgroup), "tile_lds" (0/1: k_join_stream copies the raster's per-tile leaf-block bases to
+ * side, a power of two, and cells per sub-block side, for tables built afterwards; default 64 /
+ * 16), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768 entries, or an entry budget
+ * <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of 64, default 512; the LDS
+ * quad level is held once per workgroup), "tile_lds" (0/1: k_join_stream copies the raster's per-tile leaf-block bases to
  * LDS when the workgroup's LDS stays within 80 KiB), "stream_groups" (1/2), "mixed_rows" (1/2/4), "mixed_blocks_per_cu". */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* The hipStream_t work is enqueued on (owned by the context unless set). */

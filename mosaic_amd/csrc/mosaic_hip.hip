@@ -1482,11 +1482,11 @@ struct mosaic_ctx {
     int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
     int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
     int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
-    int raster_sub = 32;  // point raster: sub-blocks per tile side (a power of two)
-    int raster_cell = 32; // point raster: leaf cells per sub-block side
+    int raster_sub = 64;  // point raster: sub-blocks per tile side (a power of two)
+    int raster_cell = 16; // point raster: leaf cells per sub-block side
     int raster_quad = 1;  // point raster: LDS quad level
     int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
-    int stream_block = 256; // k_join_stream workgroup size (64 .. 1024, a multiple of 64)
+    int stream_block = 512; // k_join_stream workgroup size (64 .. 1024, a multiple of 64)
     int tile_lds = 1;       // k_join_stream: tile_base in LDS when it fits (kStreamLdsTile)
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
     int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
@@ -2555,6 +2555,9 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
         else MOSAIC_STREAM_G(VEC, VALID, 1);                         \
     } while (0)
                 if (c->stream_mode == 1 && vec) {
+                    // (its chunk buffers take 96 KiB of LDS: a quad level beyond 24 Ki entries stays off)
+                    if (qb > 48 * 1024) ac.praster.quad = nullptr;
+                    const size_t shm_n = ac.praster.quad ? qb : 0, shm_c = (lds ? shm : 0) + shm_n;
                     const int gd = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_cu, (ac.n - lo + kChunkRows - 1) / kChunkRows));
                     if (pairs)
                         hipLaunchKernelGGL((k_join_stream_dec<false, true>), dim3(gd), dim3(1024), shm_n, c->stream, ac);

@@ -69,7 +69,7 @@ struct PointRaster {
     const uint16_t* quad;       // nullptr: no quad level
     int32_t qnx, qny, qshift;
 };
-static const int kQuadMax = 8192;     // default quad-level entry budget
+static const int kQuadMax = 32768;    // default quad-level entry budget
 static const int kQuadRefMax = 0x7ffe;  // quad entries kSubBlock | r, r <= kQuadRefMax: compact sub-blocks
 static const int kQuadLimit = 65536;  // option raster_quad: largest entry budget
 

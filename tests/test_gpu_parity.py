@@ -344,7 +344,7 @@ def test_join_tiled_nyc_zones_match_oracle(h3ctx, zones):
     assert len(rows) == total and np.array_equal(np.bincount(keys, minlength=len(zones)), want)
     try:
         # loader / worker and pipelined variants of the stream kernel, other workgroup sizes
-        for mode, block in ((1, 256), (2, 256), (2, 512), (0, 512), (0, 1024)):
+        for mode, block in ((1, 512), (2, 256), (2, 512), (0, 256), (0, 1024)):
             h3ctx.set_option("stream_mode", mode)
             h3ctx.set_option("stream_block", block)
             assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (mode, block)
@@ -358,14 +358,14 @@ def test_join_tiled_nyc_zones_match_oracle(h3ctx, zones):
             h3ctx.set_option("stream_mode", 2)
             assert np.array_equal(h3ctx.pip_join_count(table, xs[:-cut], ys[:-cut]), ref), cut
         h3ctx.set_option("stream_mode", 0)
-        h3ctx.set_option("stream_block", 256)
+        h3ctx.set_option("stream_block", 512)
         for tiles, praster in ((1, 0), (0, 0)):
             h3ctx.set_option("tiles", tiles)
             h3ctx.set_option("point_raster", praster)
             assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (tiles, praster)
     finally:
         h3ctx.set_option("stream_mode", 0)
-        h3ctx.set_option("stream_block", 256)
+        h3ctx.set_option("stream_block", 512)
         h3ctx.set_option("tiles", 1)
         h3ctx.set_option("point_raster", 1)
     table.close()
@@ -386,8 +386,8 @@ def test_join_point_raster_sizes(h3ctx, zones, sub, cell):
         table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 10,
                                  n_polygons=len(ids))
     finally:
-        h3ctx.set_option("raster_sub", 32)
-        h3ctx.set_option("raster_cell", 32)
+        h3ctx.set_option("raster_sub", 64)
+        h3ctx.set_option("raster_cell", 16)
     t = table.tiles()
     assert t["raster"] == 1 and t["raster_sub"] == sub and t["raster_cell"] == cell, t
     x, y = quickstart_points(sub_zones, 400_000, sigma=0.002, seed=31)

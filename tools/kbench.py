@@ -14,7 +14,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-DEFAULTS = {"tile_lds": 1, "stream_mode": 0, "stream_block": 256, "probe_mask": 0, "stream_groups": 1, "mixed_rows": 4,
+DEFAULTS = {"tile_lds": 1, "stream_mode": 0, "stream_block": 512, "probe_mask": 0, "stream_groups": 1, "mixed_rows": 4,
             "mixed_blocks_per_cu": 8}
 
 
@@ -152,7 +152,7 @@ def main():
             kt3 = ctx.kernel_times()
             probes[f"sblock{sb}_ms"] = [round(float(np.median(kt3[0::2])), 4), round(float(np.median(kt3[1::2])), 4)]
             ctx.set_option("timing", 0)
-        ctx.set_option("stream_block", 256)
+        ctx.set_option("stream_block", 512)
         for sw in args.sweeps:
             kv = [(q.split("=")[0], int(q.split("=")[1])) for q in sw.split(",")]
             for k, v in kv:
