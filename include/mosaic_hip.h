@@ -82,9 +82,12 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
  * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
  * side, a power of two, and cells per sub-block side, for tables built afterwards; default 64 /
- * 16), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768 entries, or an entry budget
+ * 16), "raster_lines" (0/1: sub-blocks crossed by one straight chip edge store a line record instead
+ * of a leaf block; default 1), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768 entries, or an entry budget
  * <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of 64, default 512; the LDS
- * quad level is held once per workgroup), "tile_lds" (0/1: k_join_stream copies the raster's per-tile leaf-block bases to
+ * quad level is held once per workgroup), "stream_persistent" (0/1: k_join_stream launches only the workgroups that
+ * are resident at once; default 0: blocks_per_cu x block threads per CU, measured faster),
+ * "tile_lds" (0/1: k_join_stream copies the raster's per-tile leaf-block bases to
  * LDS when the workgroup's LDS stays within 80 KiB), "stream_groups" (1/2), "mixed_rows" (1/2/4), "mixed_blocks_per_cu". */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* The hipStream_t work is enqueued on (owned by the context unless set). */
@@ -134,6 +137,10 @@ int mosaic_chip_table_tiles(const mosaic_chips* chips, int64_t* out13);
 /* out4 = lon, lat of the tile grid origin and tiles per degree along lon, lat (tile i covers
  * [x0 + i / sx, x0 + (i + 1) / sx)). */
 int mosaic_chip_table_tile_grid(const mosaic_chips* chips, double* out4);
+/* Point raster detail: out4 = sub-blocks stored as line records (option "raster_lines"), LDS quad
+ * level entries (0: none), quad shift (sub-blocks per quad side = 1 << shift), raster bytes on the
+ * device. */
+int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out4);
 
 /* ---- the join ---- */
 /* counts[p] = number of (point, chip) pairs with chip polygon_key p (overwritten). */

@@ -31,7 +31,7 @@ EXPORTS = [
     "mosaic_get_stream", "mosaic_set_stream", "mosaic_sync", "mosaic_last_stats", "mosaic_resolution",
     "mosaic_resolution_str", "mosaic_point_to_cell", "mosaic_bng_format", "mosaic_bng_parse",
     "mosaic_chip_table_create", "mosaic_chip_table_destroy", "mosaic_chip_table_info", "mosaic_chip_table_tiles",
-    "mosaic_chip_table_tile_grid", "mosaic_pip_join_count",
+    "mosaic_chip_table_tile_grid", "mosaic_chip_table_raster", "mosaic_pip_join_count",
     "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_chip_set_info",
     "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times",
 ]
@@ -95,6 +95,7 @@ def lib():
         "mosaic_chip_table_info": ([vp, vp], i32),
         "mosaic_chip_table_tiles": ([vp, vp], i32),
         "mosaic_chip_table_tile_grid": ([vp, vp], i32),
+        "mosaic_chip_table_raster": ([vp, vp], i32),
         "mosaic_pip_join_count": ([vp, vp, vp, vp, i64, vp], i32),
         "mosaic_pip_join_pairs": ([vp, vp, vp, vp, i64, vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_st_contains": ([vp, i64, vp, vp, vp, vp, vp, i64, vp], i32),

@@ -792,7 +792,7 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 #define MOSAIC_STREAM_LOAD(p) (*(p))
 #endif
 #ifndef MOSAIC_STREAM_WAVES
-#define MOSAIC_STREAM_WAVES 6  // k_join_stream: waves per SIMD the register budget must allow
+#define MOSAIC_STREAM_WAVES 4  // k_join_stream: waves per SIMD the register budget must allow (LDS allows 4 at the defaults)
 #endif
 // k_join_stream dynamic LDS: [per-polygon counts (LDS_COUNTS)] [per-wave mixed-row stages]
 // [tile_base (tile_lds_n words)] [quad level of the raster (if any)]
@@ -949,7 +949,7 @@ k_join_stream(JoinArgs a) {
 // which is also the order the next iteration consumes them in.  Four rows per lane, both arrays
 // 16-byte aligned; rows past the last multiple of 4 go to the mixed queue.
 #ifndef MOSAIC_PIPE_WAVES
-#define MOSAIC_PIPE_WAVES 5  // k_join_stream_pipe: waves per SIMD the register budget must allow
+#define MOSAIC_PIPE_WAVES 4  // k_join_stream_pipe: waves per SIMD the register budget must allow
 #endif
 template <bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MOSAIC_PIPE_WAVES)))
@@ -1485,9 +1485,11 @@ struct mosaic_ctx {
     int raster_sub = 64;  // point raster: sub-blocks per tile side (a power of two)
     int raster_cell = 16; // point raster: leaf cells per sub-block side
     int raster_quad = 1;  // point raster: LDS quad level
+    int raster_lines = 1; // point raster: line records for single-edge sub-blocks
     int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
     int stream_block = 512; // k_join_stream workgroup size (64 .. 1024, a multiple of 64)
     int tile_lds = 1;       // k_join_stream: tile_base in LDS when it fits (kStreamLdsTile)
+    int stream_persistent = 0;  // k_join_stream grid: the resident workgroups (1) or blocks_per_cu-based (0)
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
     int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     int stream_mode = 0;          // 0: k_join_stream, 1: k_join_stream_dec (loader / worker waves),
@@ -1581,7 +1583,8 @@ struct mosaic_chips {
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
     DevBuf rsub, rmid, rblocks, rquad;  // rmid: per-tile leaf block bases
-    int64_t raster_stats[5] = {0, 0, 0, 0, 0};    // S, C, pure sub-blocks, mixed sub-blocks, mixed cells
+    int64_t raster_stats[6] = {0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
+                                                   // line sub-blocks
     void release_all() {
         for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges,
                           &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &bng_cells, &bng_leaf})
@@ -1735,6 +1738,10 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
             return fail(MOSAIC_E_ARG, "raster_quad must be 0 (off), 1 (default size) or an entry budget <= " +
                                           std::to_string(tiles::kQuadLimit));
         c->raster_quad = (int)v;
+    } else if (k == "raster_lines") {
+        c->raster_lines = v ? 1 : 0;
+    } else if (k == "stream_persistent") {
+        c->stream_persistent = v ? 1 : 0;
     } else if (k == "tile_lds") {
         c->tile_lds = v ? 1 : 0;
     } else if (k == "stream_block") {
@@ -2289,6 +2296,7 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
                 tb.quad_max = c->raster_quad > 1 ? c->raster_quad : tiles::kQuadMax;
+                tb.lines = c->raster_lines != 0;
                 if (tb.build_raster(src, c->raster_sub, c->raster_cell, threads)) {
                     size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
                     if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
@@ -2331,6 +2339,7 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
                     ch->raster_stats[2] = tb.n_sub_pure;
                     ch->raster_stats[3] = tb.n_sub_mixed;
                     ch->raster_stats[4] = tb.n_cell_mixed;
+                    ch->raster_stats[5] = tb.n_sub_line;
                     total += r0 + r1;
                 }
             }
@@ -2376,6 +2385,15 @@ int mosaic_chip_table_tiles(const mosaic_chips* ch, int64_t* o) {
     }
     o[7] = ch->raster_ok ? 1 : 0;
     for (int k = 0; k < 5; k++) o[k + 8] = ch->raster_stats[k];
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
+    if (!ch || !o) return fail(MOSAIC_E_ARG, "null argument");
+    o[0] = ch->raster_stats[5];
+    o[1] = ch->praster.quad ? (int64_t)ch->praster.qnx * ch->praster.qny : 0;
+    o[2] = ch->praster.quad ? ch->praster.qshift : 0;
+    o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes) : 0;
     return MOSAIC_OK;
 }
 
@@ -2541,8 +2559,20 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
                     ac.tile_lds_n = (int)ntiles;
                     sw += (size_t)ntiles * 4;
                 }
-#define MOSAIC_STREAM(KERNEL, SHM) \
-    hipLaunchKernelGGL(KERNEL, dim3(gs), dim3(c->stream_block), (SHM) + sw, c->stream, ac)
+                // persistent grid (option stream_persistent): exactly the workgroups that are resident
+                // at once, so no second wave of workgroups refills LDS and runs a ragged tail
+                auto grid_for = [&](const void* kernel, size_t shm_bytes) -> int {
+                    if (!c->stream_persistent) return gs;
+                    int nb = 0;
+                    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, c->stream_block, shm_bytes) != hipSuccess ||
+                        nb < 1)
+                        nb = 1;
+                    return (int)std::max<int64_t>(1, std::min<int64_t>((rows_g + c->stream_block - 1) / c->stream_block,
+                                                                       (int64_t)c->n_cu * nb));
+                };
+#define MOSAIC_STREAM(KERNEL, SHM)                                                                        \
+    hipLaunchKernelGGL(KERNEL, dim3(grid_for(reinterpret_cast<const void*>(KERNEL), (SHM) + sw)), dim3(c->stream_block), \
+                       (SHM) + sw, c->stream, ac)
 #define MOSAIC_STREAM_G(VEC, VALID, G)                                                  \
     do {                                                                                \
         if (pairs) MOSAIC_STREAM((k_join_stream<false, true, VEC, VALID, G>), shm_n);    \
@@ -2567,12 +2597,16 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
                         hipLaunchKernelGGL((k_join_stream_dec<false, false>), dim3(gd), dim3(1024), shm_n, c->stream, ac);
                 } else if (c->stream_mode == 2 && vec && !a.valid && ac.n - lo >= 4) {
                     const size_t swp = stream_stage_words(c->stream_block, 1) * 4 + (size_t)ac.tile_lds_n * 4;
+#define MOSAIC_PIPE(KERNEL, SHM)                                                                                \
+    hipLaunchKernelGGL(KERNEL, dim3(grid_for(reinterpret_cast<const void*>(KERNEL), SHM)), dim3(c->stream_block), SHM, \
+                       c->stream, ac)
                     if (pairs)
-                        hipLaunchKernelGGL((k_join_stream_pipe<false, true>), dim3(gs), dim3(c->stream_block), shm_n + swp, c->stream, ac);
+                        MOSAIC_PIPE((k_join_stream_pipe<false, true>), shm_n + swp);
                     else if (lds)
-                        hipLaunchKernelGGL((k_join_stream_pipe<true, false>), dim3(gs), dim3(c->stream_block), shm_c + swp, c->stream, ac);
+                        MOSAIC_PIPE((k_join_stream_pipe<true, false>), shm_c + swp);
                     else
-                        hipLaunchKernelGGL((k_join_stream_pipe<false, false>), dim3(gs), dim3(c->stream_block), shm_n + swp, c->stream, ac);
+                        MOSAIC_PIPE((k_join_stream_pipe<false, false>), shm_n + swp);
+#undef MOSAIC_PIPE
                 } else if (a.valid) {
                     MOSAIC_STREAM_V(false, true);
                 } else if (vec && ac.n - lo >= 4) {  // the VEC prefetch re-reads a chunk's first 4 rows

@@ -52,15 +52,36 @@ static const uint32_t kFull = 1;  // run the generic fast path + probe
 
 // point raster codes (uint16): 0 = no pair, k + 1 = one pair with polygon key k (k + 1 < kSubBlock),
 // kMixed = the points of the cell take the tile path.  Sub-block entries (uint16) are a code,
-// kMixed, or kSubBlock | n: leaf block tile_base[tile] + n.
+// kMixed, kSubBlock | n (n < kLineBit): the C x C leaf block at blocks[tile_base[tile] + n C^2],
+// or kSubBlock | kLineBit | n: the line record at blocks[tile_base[tile] - 8 (n + 1)] (a tile's
+// line records precede its leaf blocks, last first; tile_base counts uint16 elements and is a
+// multiple of 8).
 static const uint16_t kMixed = 0xffffu;
 static const uint16_t kSubBlock = 0x8000u;
+static const uint16_t kLineBit = 0x4000u;
 static const int32_t kMaxRasterKeys = 0x7ffd;  // polygon keys 0 .. kMaxRasterKeys - 1
+
+// A sub-block split by one straight feature (a chip edge: a zone boundary or a hexagon side):
+// s = a u + b v + c over the sub-block's unit square (u, v: the point's offset in sub-block units,
+// (a, b) a unit vector); points with s >= kLineMargin get code pos, s <= -kLineMargin code neg, the
+// band between is mixed.  The host certifies the two half-planes widened by kLineSlack, far more
+// than the float evaluation's error (< 1e-6).
+struct LineRec {
+    float a, b, c;
+    uint16_t pos, neg;
+};
+static_assert(sizeof(LineRec) == 16, "LineRec is one 16-byte record");
+static const float kLineMargin = 1.0f / 128.0f;
+static const double kLineSlack = 1e-4;
+MOSAIC_HD uint16_t line_code(const LineRec& l, float u, float v) {
+    const float sv = fmaf(l.a, u, fmaf(l.b, v, l.c));
+    return sv >= kLineMargin ? l.pos : (sv <= -kLineMargin ? l.neg : kMixed);
+}
 
 struct PointRaster {
     const uint16_t* sub;        // (nx) x (ny) sub-block entries (S x S per tile); nullptr: no raster
-    const uint32_t* tile_base;  // per tile (tnx per row): first leaf block of the tile
-    const uint16_t* blocks;     // C x C leaf codes per mixed sub-block
+    const uint32_t* tile_base;  // per tile (tnx per row): first leaf-block element of the tile
+    const uint16_t* blocks;     // per tile: line records (8 elements each), C x C leaf blocks
     double sx, sy;              // sub-blocks per degree
     int32_t nx, ny, C, sshift, tnx;  // S = 1 << sshift sub-blocks per tile side
     // quad level: one uint16 per 2^qshift x 2^qshift sub-blocks, the code they all share, kMixed
@@ -78,8 +99,10 @@ MOSAIC_HD bool sub_is_block(uint32_t e) { return (e & kSubBlock) && e != kMixed;
 struct Lookup4 {
     uint32_t si[4];  // sub-block index (the grid holds < 2^28 sub-blocks)
     uint32_t ti[4], fc[4], e[4], base[4];
+    float u[4], v[4];  // offset in the sub-block (sub-block units)
     bool in[4];
     uint16_t b[4], out[4];
+    LineRec l[4];
 };
 MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const double* x, const double* y,
                              const bool* live, Lookup4& L, const uint16_t* quad_lds = nullptr) {
@@ -94,6 +117,8 @@ MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const d
         qi[k] = (uint32_t)((iy >> r.qshift) * r.qnx + (ix >> r.qshift));
         const int qm = (1 << r.qshift) - 1;
         qo[k] = (uint32_t)(((iy & qm) << r.qshift) | (ix & qm));
+        L.u[k] = (float)(gx - (double)ix);
+        L.v[k] = (float)(gy - (double)iy);
         int cx = L.in[k] ? (int)((gx - (double)ix) * (double)r.C) : 0;
         int cy = L.in[k] ? (int)((gy - (double)iy) * (double)r.C) : 0;
         cx = cx < r.C - 1 ? cx : r.C - 1;
@@ -134,18 +159,24 @@ MOSAIC_HD void raster_base4_lds(const uint32_t* tile_base_lds, Lookup4& L) {
 #pragma unroll
     for (int k = 0; k < 4; k++) L.base[k] = tile_base_lds[L.in[k] ? L.ti[k] : 0];
 }
+// leaf-code gathers and line-record gathers (lanes that need neither read element 0)
 MOSAIC_HD void raster_gather4(const PointRaster& r, Lookup4& L) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const bool blk = L.in[k] && sub_is_block(L.e[k]);
-        const size_t bi = blk ? (size_t)(L.base[k] + (L.e[k] & 0x7fffu)) * (size_t)(r.C * r.C) + L.fc[k] : 0;
+        const bool line = blk && (L.e[k] & kLineBit);
+        const size_t bi = (blk && !line) ? (size_t)L.base[k] + (size_t)(L.e[k] & 0x3fffu) * (size_t)(r.C * r.C) + L.fc[k] : 0;
+        const size_t li = line ? (size_t)L.base[k] - 8 * (size_t)((L.e[k] & 0x3fffu) + 1) : 0;
         L.b[k] = r.blocks[bi];
+        L.l[k] = *(const LineRec*)(r.blocks + li);
     }
 }
 MOSAIC_HD void raster_select4(Lookup4& L) {
 #pragma unroll
     for (int k = 0; k < 4; k++)
-        if (L.in[k]) L.out[k] = sub_is_block(L.e[k]) ? L.b[k] : (uint16_t)L.e[k];
+        if (L.in[k])
+            L.out[k] = !sub_is_block(L.e[k]) ? (uint16_t)L.e[k]
+                                             : ((L.e[k] & kLineBit) ? line_code(L.l[k], L.u[k], L.v[k]) : L.b[k]);
 }
 MOSAIC_HD void raster_finish4(const PointRaster& r, Lookup4& L) {
     raster_base4(r, L);
@@ -161,11 +192,14 @@ MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, doubl
     const int ix = (int)gx, iy = (int)gy;
     const uint16_t e = r.sub[(int64_t)iy * r.nx + ix];
     if (!sub_is_block(e)) return e;
+    const size_t base = r.tile_base[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)];
+    if (e & kLineBit)
+        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)((e & 0x3fffu) + 1)), (float)(gx - (double)ix),
+                         (float)(gy - (double)iy));
     int cx = (int)((gx - (double)ix) * (double)r.C), cy = (int)((gy - (double)iy) * (double)r.C);
     cx = cx < r.C - 1 ? cx : r.C - 1;
     cy = cy < r.C - 1 ? cy : r.C - 1;
-    const uint32_t b = r.tile_base[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)] + (e & 0x7fffu);
-    return r.blocks[(size_t)b * (size_t)(r.C * r.C) + (size_t)(cy * r.C + cx)];
+    return r.blocks[base + (size_t)(e & 0x3fffu) * (size_t)(r.C * r.C) + (size_t)(cy * r.C + cx)];
 }
 
 struct TileRec {
@@ -245,9 +279,11 @@ struct Builder {
     std::vector<double> rec_dev;  // per record: patch deviation of the tile (axial units)
 
     // ---- point raster (second stage, optional): per sub-block of a tile (S x S per tile, S a power
-    // of two) a uint16 entry: a code, kMixed, or kSubBlock | tile-local leaf block; leaf blocks are
-    // C x C uint16 codes, a tile's first at tile_base[tile].  Codes: 0 = the point joins nothing,
-    // k + 1 = exactly one pair with polygon key k, kMixed = run the tile path.
+    // of two) a uint16 entry: a code, kMixed, kSubBlock | tile-local leaf block, or kSubBlock |
+    // kLineBit | tile-local line record; leaf blocks are C x C uint16 codes, a tile's first at
+    // element tile_base[tile], its line records (LineRec, 8 elements) just below it, last first.
+    // Codes: 0 = the point joins nothing, k + 1 = exactly one pair with polygon key k, kMixed =
+    // run the tile path.
     int S = 0, C = 0, sshift = 0;
     std::vector<uint16_t> sub;
     std::vector<uint32_t> tile_base;
@@ -255,7 +291,8 @@ struct Builder {
     std::vector<uint16_t> quad;  // quad level (empty: none)
     int qshift = 0, qnx = 0, qny = 0;
     int quad_max = kQuadMax;  // quad-level entry budget (set before build_raster)
-    int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0;
+    int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0, n_sub_line = 0;
+    bool lines = true;  // split single-feature sub-blocks by a line (set before build_raster)
     // Chip access for the raster classification (host memory)
     struct ChipSource {
         const uint32_t* slot_first;  // per hash slot: first chip, chip count (0 for empty slots)

@@ -20,6 +20,7 @@
 #include "tiles.h"
 
 #include <atomic>
+#include <cstring>
 #include <thread>
 
 namespace mosaic {
@@ -37,15 +38,15 @@ struct P2 {
     double x, y;
 };
 
-// Convex quadrilateral q[4] meets the Voronoi hexagon of lattice centre c within tolerance t
-// (separating axes: the hexagon's 3 edge normals and the quadrilateral's 4).
-bool quad_meets_hex(const P2* q, P2 c, double t) {
+// Convex polygon q[n] (counter-clockwise) meets the Voronoi hexagon of lattice centre c within
+// tolerance t (separating axes: the hexagon's 3 edge normals and the polygon's n).
+bool poly_meets_hex(const P2* q, int n, P2 c, double t) {
     // hexagon: vertices at 30 + 60k degrees, radius 1/sqrt(3); apothem 1/2 along 0, 60, 120 degrees
     static const double ax[3][2] = {{1.0, 0.0}, {0.5, kS60}, {-0.5, kS60}};
     for (int k = 0; k < 3; k++) {
         double hc = c.x * ax[k][0] + c.y * ax[k][1];
         double lo = INFINITY, hi = -INFINITY;
-        for (int v = 0; v < 4; v++) {
+        for (int v = 0; v < n; v++) {
             double d = q[v].x * ax[k][0] + q[v].y * ax[k][1];
             lo = std::min(lo, d);
             hi = std::max(hi, d);
@@ -53,15 +54,15 @@ bool quad_meets_hex(const P2* q, P2 c, double t) {
         if (lo > hc + 0.5 + t || hi < hc - 0.5 - t) return false;
     }
     const double r = 0.57735026918962576451;
-    for (int e = 0; e < 4; e++) {
-        P2 a = q[e], b = q[(e + 1) & 3];
+    for (int e = 0; e < n; e++) {
+        P2 a = q[e], b = q[(e + 1) % n];
         double nx = -(b.y - a.y), ny = b.x - a.x;
         double len = sqrt(nx * nx + ny * ny);
         if (!(len > 0)) continue;
         nx /= len;
         ny /= len;
         double lo = INFINITY, hi = -INFINITY;
-        for (int v = 0; v < 4; v++) {
+        for (int v = 0; v < n; v++) {
             double d = q[v].x * nx + q[v].y * ny;
             lo = std::min(lo, d);
             hi = std::max(hi, d);
@@ -76,9 +77,81 @@ bool quad_meets_hex(const P2* q, P2 c, double t) {
     return true;
 }
 
+bool quad_meets_hex(const P2* q, P2 c, double t) { return poly_meets_hex(q, 4, c, t); }
+
 struct Seg {
     double ax, ay, bx, by;
 };
+
+double cross(P2 o, P2 a, P2 b) { return (a.x - o.x) * (b.y - o.y) - (a.y - o.y) * (b.x - o.x); }
+
+double seg_point_dist(P2 a, P2 b, P2 p) {
+    const double dx = b.x - a.x, dy = b.y - a.y, l2 = dx * dx + dy * dy;
+    double t = l2 > 0 ? ((p.x - a.x) * dx + (p.y - a.y) * dy) / l2 : 0.0;
+    t = t < 0 ? 0 : (t > 1 ? 1 : t);
+    const double ex = a.x + t * dx - p.x, ey = a.y + t * dy - p.y;
+    return sqrt(ex * ex + ey * ey);
+}
+
+// Segment (a, b) comes within eps of the convex polygon q[n] (counter-clockwise).
+bool seg_meets_poly(P2 a, P2 b, const P2* q, int n, double eps) {
+    auto inside = [&](P2 p) {
+        for (int e = 0; e < n; e++) {
+            P2 u = q[e], v = q[(e + 1) % n];
+            const double len = sqrt((v.x - u.x) * (v.x - u.x) + (v.y - u.y) * (v.y - u.y));
+            if (len > 0 && cross(u, v, p) / len < -eps) return false;
+        }
+        return true;
+    };
+    if (inside(a) || inside(b)) return true;
+    for (int e = 0; e < n; e++) {
+        P2 u = q[e], v = q[(e + 1) % n];
+        const double d1 = cross(a, b, u), d2 = cross(a, b, v), d3 = cross(u, v, a), d4 = cross(u, v, b);
+        if (((d1 <= 0 && d2 >= 0) || (d1 >= 0 && d2 <= 0)) && ((d3 <= 0 && d4 >= 0) || (d3 >= 0 && d4 <= 0))) return true;
+        if (seg_point_dist(a, b, u) <= eps || seg_point_dist(a, b, v) <= eps || seg_point_dist(u, v, a) <= eps ||
+            seg_point_dist(u, v, b) <= eps)
+            return true;
+    }
+    return false;
+}
+
+// Clip the segment to [x0, x1] x [y0, y1] (Liang-Barsky); false when it misses the box.
+bool clip_seg(double& ax, double& ay, double& bx, double& by, double x0, double y0, double x1, double y1) {
+    double t0 = 0.0, t1 = 1.0;
+    const double dx = bx - ax, dy = by - ay;
+    const double p[4] = {-dx, dx, -dy, dy}, qv[4] = {ax - x0, x1 - ax, ay - y0, y1 - ay};
+    for (int k = 0; k < 4; k++) {
+        if (p[k] == 0) {
+            if (qv[k] < 0) return false;
+        } else {
+            const double t = qv[k] / p[k];
+            if (p[k] < 0) t0 = std::max(t0, t);
+            else t1 = std::min(t1, t);
+        }
+    }
+    if (t0 > t1) return false;
+    const double nax = ax + t0 * dx, nay = ay + t0 * dy;
+    bx = ax + t1 * dx;
+    by = ay + t1 * dy;
+    ax = nax;
+    ay = nay;
+    return true;
+}
+
+// Convex polygon q[n] clipped to the half-plane a x + b y + c >= 0 (Sutherland-Hodgman)
+int clip_half(const P2* q, int n, double a, double b, double c, P2* out) {
+    int m = 0;
+    for (int e = 0; e < n; e++) {
+        P2 u = q[e], v = q[(e + 1) % n];
+        const double su = a * u.x + b * u.y + c, sv = a * v.x + b * v.y + c;
+        if (su >= 0) out[m++] = u;
+        if ((su >= 0) != (sv >= 0)) {
+            const double t = su / (su - sv);
+            out[m++] = P2{u.x + t * (v.x - u.x), u.y + t * (v.y - u.y)};
+        }
+    }
+    return m;
+}
 
 struct Rect {
     double x0, y0, x1, y1;
@@ -117,8 +190,8 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     tile_base.clear();
     blocks.clear();
     quad.clear();
-    n_sub_pure = n_sub_mixed = n_cell_mixed = 0;
-    if (tile_idx.empty() || S < 1 || (S & (S - 1)) || C < 1 || S * C > 1024) return false;
+    n_sub_pure = n_sub_mixed = n_cell_mixed = n_sub_line = 0;
+    if (tile_idx.empty() || S < 1 || S > 128 || (S & (S - 1)) || C < 1 || S * C > 1024) return false;
     if (src.n_polygons > (int32_t)kMaxRasterKeys) return false;  // codes must stay below kSubBlock
     sshift = 0;
     while ((1 << sshift) < S) sshift++;
@@ -130,10 +203,11 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     const double tw = 1.0 / grid.sx, th = 1.0 / grid.sy;
     // per-tile leaf blocks (tile-local numbering in the sub entries), merged afterwards
     std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
+    std::vector<std::vector<LineRec>> tile_lines(recs.size());
     std::vector<int> tile_of_rec(recs.size(), -1);
     for (int64_t t = 0; t < (int64_t)nx * ny; t++)
         if (tile_idx[(size_t)t] >= 2) tile_of_rec[tile_idx[(size_t)t] - 2] = (int)t;
-    std::atomic<int64_t> next(0), pure(0), mixed(0), cmixed(0);
+    std::atomic<int64_t> next(0), pure(0), mixed(0), cmixed(0), nline(0);
 
     auto work = [&]() {
         std::vector<P2> lat;  // (S + 1)^2 sub-block corner images
@@ -152,7 +226,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
             const double lon0 = grid.x0 + ti * tw, lat0 = grid.y0 + tj * th;
             // lattice images on the tile's face: sub-block corners now, cell corners of a
             // sub-block only when it needs its cells
-            auto image = [&](int i, int j) -> P2 {
+            auto image = [&](double i, double j) -> P2 {
                 double px, py, pz, vx, vy, b;
                 h3::fast_unit(lat0 + th * j / N, lon0 + tw * i / N, &px, &py, &pz);
                 h3::fast_plane(px, py, pz, face, res_, &vx, &vy, &b);
@@ -231,6 +305,113 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                 if (ans.size() == 1) return (uint16_t)(ans[0] + 1);
                 return kMixed;
             };
+            // classification of the convex region uv[n] (sub-block units, counter-clockwise) of
+            // sub-block (si, sj) with candidate hexagons `cin` (those of the whole sub-block) -> code
+            const double exd = 1e-6 * cell_deg_x + 1e-12 * (fabs(lon0) + 1.0);
+            const double eyd = 1e-6 * cell_deg_y + 1e-12 * (fabs(lat0) + 1.0);
+            auto classify_poly = [&](int si, int sj, const P2* uv, int n, const std::vector<int>& cin) -> uint16_t {
+                P2 img[8], ll[8];
+                double u0 = INFINITY, u1 = -INFINITY, v0 = INFINITY, v1 = -INFINITY;
+                double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY, mx = 0.0, my = 0.0;
+                for (int v = 0; v < n; v++) {
+                    img[v] = image((si + uv[v].x) * C, (sj + uv[v].y) * C);
+                    ll[v] = P2{lon0 + tw * (si + uv[v].x) / S, lat0 + th * (sj + uv[v].y) / S};
+                    u0 = std::min(u0, uv[v].x);
+                    u1 = std::max(u1, uv[v].x);
+                    v0 = std::min(v0, uv[v].y);
+                    v1 = std::max(v1, uv[v].y);
+                    x0 = std::min(x0, ll[v].x);
+                    x1 = std::max(x1, ll[v].x);
+                    y0 = std::min(y0, ll[v].y);
+                    y1 = std::max(y1, ll[v].y);
+                    mx += ll[v].x;
+                    my += ll[v].y;
+                }
+                mx /= n;  // a point inside the (convex) region
+                my /= n;
+                const double frac = std::max(u1 - u0, v1 - v0) / S;
+                const double tol = 4.0 * dev * frac * frac + 1e-7;
+                const double eps = std::max(exd, eyd);
+                bool first = true, mixed_ans = false, any = false;
+                for (int k : cin) {
+                    const Hex& h = hexes[(size_t)k];
+                    if (!poly_meets_hex(img, n, h.c, tol)) continue;
+                    any = true;
+                    ah = h.core;
+                    for (size_t b = 0; b < h.border.size(); b++) {
+                        const pip::Box& bx = h.bbox[b];
+                        if (!(bx.maxx < x0 - eps || bx.minx > x1 + eps || bx.maxy < y0 - eps || bx.miny > y1 + eps))
+                            for (const Seg& e : h.segs[b])
+                                if (seg_meets_poly(P2{e.ax, e.ay}, P2{e.bx, e.by}, ll, n, eps)) return kMixed;
+                        if (pip::contains(src.store, h.border[b], mx, my)) ah.push_back(h.border_key[b]);
+                    }
+                    std::sort(ah.begin(), ah.end());
+                    if (first) {
+                        ans = ah;
+                        first = false;
+                    } else if (ah != ans) {
+                        mixed_ans = true;
+                    }
+                }
+                if (mixed_ans || !any) return kMixed;
+                if (ans.empty()) return 0;
+                if (ans.size() == 1) return (uint16_t)(ans[0] + 1);
+                return kMixed;
+            };
+            // a mixed sub-block whose chip edges all lie along one line: the line through the
+            // longest clipped edge; both sides (beyond the margin, less the slack) must classify
+            std::vector<P2> ends;
+            auto try_line = [&](int si, int sj, const std::vector<int>& cin, LineRec& out) -> bool {
+                const double wR = tw / S, hR = th / S;
+                const double lonR0 = lon0 + tw * si / S, latR0 = lat0 + th * sj / S;
+                const double exu = exd / wR, eyv = eyd / hR;
+                const double bx0 = lonR0 - exd, bx1 = lonR0 + wR + exd, by0 = latR0 - eyd, by1 = latR0 + hR + eyd;
+                double best = 0.0;
+                P2 pa{0, 0}, pb{0, 0};
+                ends.clear();
+                for (int k : cin) {
+                    const Hex& h = hexes[(size_t)k];
+                    for (size_t b = 0; b < h.border.size(); b++) {
+                        const pip::Box& bx = h.bbox[b];
+                        if (bx.maxx < bx0 || bx.minx > bx1 || bx.maxy < by0 || bx.miny > by1) continue;
+                        for (const Seg& e : h.segs[b]) {
+                            double ax = (e.ax - lonR0) / wR, ay = (e.ay - latR0) / hR;
+                            double qx = (e.bx - lonR0) / wR, qy = (e.by - latR0) / hR;
+                            if (!clip_seg(ax, ay, qx, qy, -exu, -eyv, 1.0 + exu, 1.0 + eyv)) continue;
+                            ends.push_back(P2{ax, ay});
+                            ends.push_back(P2{qx, qy});
+                            const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
+                            if (l2 > best) {
+                                best = l2;
+                                pa = P2{ax, ay};
+                                pb = P2{qx, qy};
+                            }
+                        }
+                    }
+                }
+                if (!(best > 1e-6)) return false;
+                const double l = sqrt(best);
+                const double a = -(pb.y - pa.y) / l, b = (pb.x - pa.x) / l;
+                const double c = -(a * 0.5 * (pa.x + pb.x) + b * 0.5 * (pa.y + pb.y));
+                const double lim = (double)kLineMargin - 2.0 * kLineSlack;
+                for (const P2& p : ends)
+                    if (fabs(a * p.x + b * p.y + c) > lim) return false;
+                out.a = (float)a;
+                out.b = (float)b;
+                out.c = (float)c;
+                // certify with the coefficients the device uses
+                const double A = out.a, B = out.b, Cf = out.c, m = (double)kLineMargin - kLineSlack;
+                const P2 sq[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
+                P2 hp[8], hn[8];
+                const int np = clip_half(sq, 4, A, B, Cf - m, hp), nn = clip_half(sq, 4, -A, -B, -Cf - m, hn);
+                const uint16_t cp = np >= 3 ? classify_poly(si, sj, hp, np, cin) : 0;
+                if (cp == kMixed) return false;
+                const uint16_t cn = nn >= 3 ? classify_poly(si, sj, hn, nn, cin) : 0;
+                if (cn == kMixed) return false;
+                out.pos = cp;
+                out.neg = cn;
+                return true;
+            };
             std::vector<int> all((size_t)wa * wb);
             for (size_t k = 0; k < all.size(); k++) all[k] = (int)k;
             std::vector<uint16_t>& outb = tile_blocks[(size_t)ri];
@@ -246,6 +427,15 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                         pure++;
                     } else {
                         mixed++;
+                        LineRec lr;
+                        if (lines && try_line(si, sj, cand, lr)) {
+                            // tile-local line record number (< S * S <= kLineBit)
+                            entry = (uint16_t)(kSubBlock | kLineBit | (uint32_t)tile_lines[(size_t)ri].size());
+                            tile_lines[(size_t)ri].push_back(lr);
+                            nline++;
+                            sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
+                            continue;
+                        }
                         for (int cj = 0; cj <= C; cj++)
                             for (int ci = 0; ci <= C; ci++)
                                 clat[(size_t)cj * (C + 1) + ci] =
@@ -267,7 +457,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                         if (same && cellc[0] != kMixed) {
                             entry = cellc[0];
                         } else {
-                            // tile-local leaf block number (< S * S <= 0x7fff)
+                            // tile-local leaf block number (< S * S <= kLineBit)
                             entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / ((size_t)C * C)));
                             outb.insert(outb.end(), cellc.begin(), cellc.end());
                         }
@@ -288,19 +478,26 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
         for (int sj = 0; sj < S; sj++)
             for (int si = 0; si < S; si++) sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = kMixed;
     }
-    // merge the per-tile leaf blocks; a tile's first block goes to tile_base
+    // merge: per tile [line records, last first][leaf blocks], 16-byte aligned; tile_base = the
+    // element of the tile's first leaf block
     size_t total = 0;
+    std::vector<size_t> at(recs.size());
     for (size_t r = 0; r < recs.size(); r++) {
-        if (tile_of_rec[r] >= 0) tile_base[(size_t)tile_of_rec[r]] = (uint32_t)(total / ((size_t)C * C));
-        total += tile_blocks[r].size();
+        at[r] = total + 8 * tile_lines[r].size();
+        if (tile_of_rec[r] >= 0) tile_base[(size_t)tile_of_rec[r]] = (uint32_t)at[r];
+        total = (at[r] + tile_blocks[r].size() + 7) & ~(size_t)7;
     }
-    if (total / ((size_t)C * C) >= ((size_t)1 << 31)) {
+    if (total >= ((size_t)1 << 32)) {
         sub.clear();
         return false;
     }
-    blocks.reserve(std::max<size_t>(total, 1));
-    for (size_t r = 0; r < recs.size(); r++) blocks.insert(blocks.end(), tile_blocks[r].begin(), tile_blocks[r].end());
-    if (blocks.empty()) blocks.assign((size_t)C * C, kMixed);
+    blocks.assign(std::max<size_t>(total, std::max<size_t>((size_t)C * C, 8)), kMixed);
+    for (size_t r = 0; r < recs.size(); r++) {
+        for (size_t n = 0; n < tile_lines[r].size(); n++)
+            memcpy(blocks.data() + at[r] - 8 * (n + 1), &tile_lines[r][n], sizeof(LineRec));
+        std::copy(tile_blocks[r].begin(), tile_blocks[r].end(), blocks.begin() + (ptrdiff_t)at[r]);
+    }
+    n_sub_line = nline.load();
     n_sub_pure = pure.load();
     n_sub_mixed = mixed.load();
     n_cell_mixed = cmixed.load();

@@ -139,3 +139,78 @@ def clustered_points_device(zones, n, seed, sigma=0.002, device="cuda", chunk=1 
         y[s:s + m] = torch.where(uni, uy, gy)
         del pick, gx, gy, uni, ux, uy
     return x, y
+
+
+NYC_BBOX = (-74.25559136315209, 40.496115395170364, -73.7000090639354, 40.91553277700258)
+
+
+def synthetic_buildings(n, seed=SEED_BASE + 4, bbox=NYC_BBOX, n_centres=64, sigma=0.01):
+    """C4 build side: n OSM-style building footprints -- rotated rectangles (4 vertices) and
+    L-shapes (6 vertices), sides 8-40 m, centres clustered (Gaussian, sigma degrees, around
+    n_centres seeded centres) over the bbox.  One closed shell per geometry, counter-clockwise."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    x0, y0, x1, y1 = bbox
+    cc = np.column_stack([rng.uniform(x0, x1, n_centres), rng.uniform(y0, y1, n_centres)])
+    c = cc[rng.integers(0, n_centres, n)] + rng.normal(0.0, sigma, (n, 2))
+    c[:, 0] = np.clip(c[:, 0], x0, x1)
+    c[:, 1] = np.clip(c[:, 1], y0, y1)
+    w, h = rng.uniform(8.0, 40.0, n), rng.uniform(8.0, 40.0, n)
+    theta = rng.uniform(0.0, 2.0 * np.pi, n)
+    is_l = rng.random(n) < 0.5
+    fa, fb = rng.uniform(0.3, 0.7, n), rng.uniform(0.3, 0.7, n)
+    # local shells in metres, centred
+    rect = np.stack([np.column_stack([-w, -h]), np.column_stack([w, -h]), np.column_stack([w, h]),
+                     np.column_stack([-w, h])], axis=1) * 0.5
+    lsh = np.stack([np.column_stack([-w, -h]) * 0.5, np.column_stack([w, -h]) * 0.5,
+                    np.column_stack([w * 0.5, -h * 0.5 + fb * h]),
+                    np.column_stack([-w * 0.5 + fa * w, -h * 0.5 + fb * h]),
+                    np.column_stack([-w * 0.5 + fa * w, h * 0.5]), np.column_stack([-w, h]) * 0.5], axis=1)
+    ct, st = np.cos(theta)[:, None], np.sin(theta)[:, None]
+    mlon = 1.0 / (111320.0 * np.cos(np.radians(c[:, 1])))[:, None]
+    mlat = 1.0 / 110540.0
+
+    def place(loc, idx):
+        px = (loc[idx, :, 0] * ct[idx] - loc[idx, :, 1] * st[idx]) * mlon[idx] + c[idx, 0:1]
+        py = (loc[idx, :, 0] * st[idx] + loc[idx, :, 1] * ct[idx]) * mlat + c[idx, 1:2]
+        ring = np.stack([px, py], axis=2)
+        return np.concatenate([ring, ring[:, :1]], axis=1)  # closed
+
+    ri, li = np.nonzero(~is_l)[0], np.nonzero(is_l)[0]
+    sizes = np.where(is_l, 7, 5)
+    ro = np.zeros(n + 1, np.int64)
+    ro[1:] = np.cumsum(sizes)
+    xy = np.empty((int(ro[-1]), 2))
+    pr, pl = place(rect, ri), place(lsh, li)
+    for k, g in enumerate(ri):
+        xy[ro[g]:ro[g + 1]] = pr[k]
+    for k, g in enumerate(li):
+        xy[ro[g]:ro[g + 1]] = pl[k]
+    idx = np.arange(n + 1, dtype=np.int64)
+    return PolygonSet(xy, ro, idx, idx)
+
+
+def building_points_device(buildings, n, seed, near=0.7, reach_m=25.0, device="cuda", chunk=1 << 26):
+    """C4 probe side on the device: a fraction `near` of the points uniform within reach_m metres
+    (per axis) of a random building's first vertex, the rest uniform over the buildings' bbox."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    first = torch.tensor(buildings.xy[buildings.ring_offsets[:-1]], dtype=torch.float64, device=device)
+    x0, y0, x1, y1 = buildings.bbox()
+    dlat = reach_m / 110540.0
+    dlon = reach_m / (111320.0 * np.cos(np.radians(0.5 * (y0 + y1))))
+    x = torch.empty(n, dtype=torch.float64, device=device)
+    y = torch.empty(n, dtype=torch.float64, device=device)
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        pick = torch.randint(0, first.shape[0], (m,), generator=g, device=device)
+        nx = torch.rand(m, generator=g, device=device, dtype=torch.float64).mul_(2 * dlon).sub_(dlon).add_(first[pick, 0])
+        ny = torch.rand(m, generator=g, device=device, dtype=torch.float64).mul_(2 * dlat).sub_(dlat).add_(first[pick, 1])
+        uni = torch.rand(m, generator=g, device=device, dtype=torch.float64) >= near
+        ux = torch.rand(m, generator=g, device=device, dtype=torch.float64).mul_(x1 - x0).add_(x0)
+        uy = torch.rand(m, generator=g, device=device, dtype=torch.float64).mul_(y1 - y0).add_(y0)
+        x[s:s + m] = torch.where(uni, ux, nx)
+        y[s:s + m] = torch.where(uni, uy, ny)
+        del pick, nx, ny, uni, ux, uy
+    return x, y

@@ -270,9 +270,9 @@ int main(int argc, char** argv) {
     printf("1 %ld %ld %ld %ld %ld %ld %d %ld %ld %ld\n", bad, checked, skipped, full, unc, miss, rok ? 1 : 0, rbad, rpure,
            rmixed);
     if (uni) fprintf(stderr, "uniform over bbox: %ld points, %.4f mixed\n", uni, (double)uni_mixed / uni);
-    fprintf(stderr, "raster S %d C %d: sub %zu blocks %zu, pure sub %lld mixed sub %lld mixed cells %lld\n", S, Cc,
-            tb.sub.size(), tb.blocks.size() / ((size_t)Cc * Cc), (long long)tb.n_sub_pure, (long long)tb.n_sub_mixed,
-            (long long)tb.n_cell_mixed);
+    fprintf(stderr, "raster S %d C %d: sub %zu block elements %zu, pure sub %lld mixed sub %lld (line %lld) mixed cells %lld\n",
+            S, Cc, tb.sub.size(), tb.blocks.size(), (long long)tb.n_sub_pure, (long long)tb.n_sub_mixed,
+            (long long)tb.n_sub_line, (long long)tb.n_cell_mixed);
     fprintf(stderr, "grid %d x %d, rings %d, records %zu, entries %zu, full tiles %lld\n", g.nx, g.ny, tb.rings,
             tb.recs.size(), tb.entries.size(), (long long)tb.n_full);
     return 0;

@@ -14,7 +14,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-DEFAULTS = {"tile_lds": 1, "stream_mode": 0, "stream_block": 512, "probe_mask": 0, "stream_groups": 1, "mixed_rows": 4,
+DEFAULTS = {"tile_lds": 1, "stream_persistent": 0, "blocks_per_cu": 8, "stream_mode": 0, "stream_block": 512, "probe_mask": 0, "stream_groups": 1, "mixed_rows": 4,
             "mixed_blocks_per_cu": 8}
 
 
@@ -31,6 +31,7 @@ def main():
     p.add_argument("--stream-mode", type=int, default=0, help="0 k_join_stream, 1 loader/worker k_join_stream_dec")
     p.add_argument("--groups", type=int, nargs="*", default=[1], help="stream_groups values")
     p.add_argument("--quads", type=int, nargs="*", default=[1], help="raster_quad values (1 default, else entry budget)")
+    p.add_argument("--lines", type=int, nargs="*", default=[1], help="raster_lines values")
     p.add_argument("--stream-blocks", type=int, nargs="*", default=[], help="k_join_stream workgroup sizes to time")
     p.add_argument("--sweeps", nargs="*", default=[],
                    help="launch-option sets to time on each table, e.g. tile_lds=0 stream_block=512,probe_mask=8")
@@ -105,21 +106,23 @@ def main():
         for sub, cell in (args.point_raster if praster else [(32, 16)]):
             for grp in args.groups:
                 for quad in (args.quads if praster else [1]):
-                    tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}_g{grp}" if praster else "")
-                    tag += f"_q{quad}" if quad != 1 else ""
-                    if args.all_core:
-                        variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, (sub, cell), grp,
-                                         quad))
-                    for r in args.rasters:
-                        for le in args.lane_edges:
-                            variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster,
-                                             (sub, cell), grp, quad))
+                    for ln in (args.lines if praster else [1]):
+                        tag = f"tiles{tiles}_praster{praster}" + (f"_{sub}x{cell}_g{grp}" if praster else "")
+                        tag += (f"_q{quad}" if quad != 1 else "") + ("" if ln else "_nolines")
+                        if args.all_core:
+                            variants.append((f"join_all_core_{tag}", True, 3, 16, 0, tiles, praster, (sub, cell), grp,
+                                             quad, ln))
+                        for r in args.rasters:
+                            for le in args.lane_edges:
+                                variants.append((f"join_raster{r}_lane{le}_{tag}", False, 3, r, le, tiles, praster,
+                                                 (sub, cell), grp, quad, ln))
     if args.legacy:
-        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, (32, 16), 1, 1),
-                     ("join_full_slab", False, 2, 16, 8, 0, 0, (32, 16), 1, 1)]
-    for name, core, mode, raster, lane_edges, tiles, praster, (sub, cell), grp, quad in variants:
+        variants += [("join_full_coop", False, 1, 16, 8, 0, 0, (32, 16), 1, 1, 1),
+                     ("join_full_slab", False, 2, 16, 8, 0, 0, (32, 16), 1, 1, 1)]
+    for name, core, mode, raster, lane_edges, tiles, praster, (sub, cell), grp, quad, ln in variants:
         ctx.set_option("stream_groups", grp)
         ctx.set_option("raster_quad", quad)
+        ctx.set_option("raster_lines", ln)
         ctx.set_option("tiles", tiles)
         ctx.set_option("point_raster", praster)
         ctx.set_option("raster_sub", sub)
@@ -199,7 +202,7 @@ def main():
                 ctx.set_option("timing", 0)
             ctx.set_option("probe_mask", 0)
         print(json.dumps({"variant": name, "ms": t, "kernels_ms": kt, **probes, "pts_per_s": n / t * 1e3, **st,
-                          "build_s": round(build_s, 2), "raster": {k: tl[k] for k in ("raster", "pure_sub_blocks", "mixed_sub_blocks", "mixed_cells")}}))
+                          "build_s": round(build_s, 2), "raster": {k: tl[k] for k in ("raster", "pure_sub_blocks", "mixed_sub_blocks", "line_sub_blocks", "mixed_cells", "raster_bytes")}}))
         table.close()
 
 
