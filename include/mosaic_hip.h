@@ -78,7 +78,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * "blocks_per_cu" (grid sizing), "timing" (0/1: HIP events around each join's main kernel; 2: the
  * point-raster join's mixed-cell kernel is timed as a second entry),
  * "pip_mode" (3 raster, 2 slab, 1 ring-cooperative, 0 lane-per-point contains strategy), "raster"
- * (raster cells per chip side, for tables built afterwards), "lane_edges", "tiles" (0/1: H3 tile
+ * (raster cells per chip side, for tables built afterwards), "raster_adaptive" (0/1: rings with
+ * few segments get 2 ceil(sqrt(segments)) cells a side instead, at most "raster"; default 1), "lane_edges", "tiles" (0/1: H3 tile
  * directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
  * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
  * side, a power of two, and cells per sub-block side, for tables built afterwards; default 64 /

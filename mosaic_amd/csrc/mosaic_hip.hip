@@ -1479,6 +1479,7 @@ struct mosaic_ctx {
     // 0: lane per point
     int pip_mode = 3;
     int raster = 16;      // raster cells per side of a border chip's envelope (chip tables built later)
+    int raster_adaptive = 1;  // fewer raster cells for rings with few segments
     int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
     int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
     int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
@@ -1738,6 +1739,8 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
             return fail(MOSAIC_E_ARG, "raster_quad must be 0 (off), 1 (default size) or an entry budget <= " +
                                           std::to_string(tiles::kQuadLimit));
         c->raster_quad = (int)v;
+    } else if (k == "raster_adaptive") {
+        c->raster_adaptive = v ? 1 : 0;
     } else if (k == "raster_lines") {
         c->raster_lines = v ? 1 : 0;
     } else if (k == "stream_persistent") {
@@ -2108,7 +2111,13 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
         h.box = gb.geom_bbox[t];
         h.cell_base = raster::kNoRaster;
         uint2 d = ring_desc[t];
-        if (!(meta[t] & 1u) && d.y >= 2) rb.add_ring(h, gb.verts.data() + d.x, d.y, c->raster);
+        if (!(meta[t] & 1u) && d.y >= 2) {
+            // option raster_adaptive: small rings get small rasters (2 ceil(sqrt(segments)) cells a
+            // side, at most "raster"), so chip tables of millions of small chips stay compact
+            int dims = c->raster;
+            if (c->raster_adaptive) dims = std::min(dims, std::max(2, 2 * (int)ceil(sqrt((double)(d.y - 1)))));
+            rb.add_ring(h, gb.verts.data() + d.x, d.y, dims);
+        }
         if (rb.edges.size() >= (1ull << 31)) {
             ch->release_all();
             delete ch;

@@ -62,20 +62,20 @@ static const uint16_t kLineBit = 0x4000u;
 static const int32_t kMaxRasterKeys = 0x7ffd;  // polygon keys 0 .. kMaxRasterKeys - 1
 
 // A sub-block split by one straight feature (a chip edge: a zone boundary or a hexagon side):
-// s = a u + b v + c over the sub-block's unit square (u, v: the point's offset in sub-block units,
-// (a, b) a unit vector); points with s >= kLineMargin get code pos, s <= -kLineMargin code neg, the
-// band between is mixed.  The host certifies the two half-planes widened by kLineSlack, far more
-// than the float evaluation's error (< 1e-6).
+// s = a u + b v + c over the sub-block's unit square (u, v: the point's offset in sub-block units),
+// (a, b) scaled to 1 / margin, so points with s >= 1 get code pos, s <= -1 code neg and the band
+// of half-width `margin` (sub-block units, chosen per record) between is mixed.  The host
+// certifies the two half-planes widened by kLineSlack sub-block units, far more than the float
+// evaluation's error.
 struct LineRec {
     float a, b, c;
     uint16_t pos, neg;
 };
 static_assert(sizeof(LineRec) == 16, "LineRec is one 16-byte record");
-static const float kLineMargin = 1.0f / 128.0f;
-static const double kLineSlack = 1e-4;
+static const double kLineSlack = 5e-5;
 MOSAIC_HD uint16_t line_code(const LineRec& l, float u, float v) {
     const float sv = fmaf(l.a, u, fmaf(l.b, v, l.c));
-    return sv >= kLineMargin ? l.pos : (sv <= -kLineMargin ? l.neg : kMixed);
+    return sv >= 1.0f ? l.pos : (sv <= -1.0f ? l.neg : kMixed);
 }
 
 struct PointRaster {

@@ -359,7 +359,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                 return kMixed;
             };
             // a mixed sub-block whose chip edges all lie along one line: the line through the
-            // longest clipped edge; both sides (beyond the margin, less the slack) must classify
+            // longest clipped edge; both sides (beyond a margin, less the slack) must classify
             std::vector<P2> ends;
             auto try_line = [&](int si, int sj, const std::vector<int>& cin, LineRec& out) -> bool {
                 const double wR = tw / S, hR = th / S;
@@ -393,24 +393,29 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                 const double l = sqrt(best);
                 const double a = -(pb.y - pa.y) / l, b = (pb.x - pa.x) / l;
                 const double c = -(a * 0.5 * (pa.x + pb.x) + b * 0.5 * (pa.y + pb.y));
-                const double lim = (double)kLineMargin - 2.0 * kLineSlack;
-                for (const P2& p : ends)
-                    if (fabs(a * p.x + b * p.y + c) > lim) return false;
-                out.a = (float)a;
-                out.b = (float)b;
-                out.c = (float)c;
-                // certify with the coefficients the device uses
-                const double A = out.a, B = out.b, Cf = out.c, m = (double)kLineMargin - kLineSlack;
+                double dev_max = 0.0;
+                for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * p.x + b * p.y + c));
                 const P2 sq[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
-                P2 hp[8], hn[8];
-                const int np = clip_half(sq, 4, A, B, Cf - m, hp), nn = clip_half(sq, 4, -A, -B, -Cf - m, hn);
-                const uint16_t cp = np >= 3 ? classify_poly(si, sj, hp, np, cin) : 0;
-                if (cp == kMixed) return false;
-                const uint16_t cn = nn >= 3 ? classify_poly(si, sj, hn, nn, cin) : 0;
-                if (cn == kMixed) return false;
-                out.pos = cp;
-                out.neg = cn;
-                return true;
+                // the narrowest band (fewest rows to the mixed kernel) whose two sides certify
+                for (double margin : {1.0 / 2048, 1.0 / 512, 1.0 / 128, 1.0 / 32}) {
+                    if (dev_max > margin - 2.0 * kLineSlack) continue;
+                    out.a = (float)(a / margin);
+                    out.b = (float)(b / margin);
+                    out.c = (float)(c / margin);
+                    // certify with the coefficients the device uses: device side + implies
+                    // A u + B v + C >= 1 - (float error) >= 1 - kLineSlack / margin
+                    const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - kLineSlack / margin;
+                    P2 hp[8], hn[8];
+                    const int np = clip_half(sq, 4, A, B, Cf - m, hp), nn = clip_half(sq, 4, -A, -B, -Cf - m, hn);
+                    const uint16_t cp = np >= 3 ? classify_poly(si, sj, hp, np, cin) : 0;
+                    if (cp == kMixed) continue;
+                    const uint16_t cn = nn >= 3 ? classify_poly(si, sj, hn, nn, cin) : 0;
+                    if (cn == kMixed) continue;
+                    out.pos = cp;
+                    out.neg = cn;
+                    return true;
+                }
+                return false;
             };
             std::vector<int> all((size_t)wa * wb);
             for (size_t k = 0; k < all.size(); k++) all[k] = (int)k;

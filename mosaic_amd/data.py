@@ -144,11 +144,14 @@ def clustered_points_device(zones, n, seed, sigma=0.002, device="cuda", chunk=1 
 NYC_BBOX = (-74.25559136315209, 40.496115395170364, -73.7000090639354, 40.91553277700258)
 
 
-def synthetic_buildings(n, seed=SEED_BASE + 4, bbox=NYC_BBOX, n_centres=64, sigma=0.01):
+def synthetic_buildings(n, seed=SEED_BASE + 4, bbox=NYC_BBOX, n_centres=None, sigma=0.004):
     """C4 build side: n OSM-style building footprints -- rotated rectangles (4 vertices) and
     L-shapes (6 vertices), sides 8-40 m, centres clustered (Gaussian, sigma degrees, around
-    n_centres seeded centres) over the bbox.  One closed shell per geometry, counter-clockwise."""
+    n_centres seeded centres; default one per 500 buildings, so clusters stay city-like and
+    footprints rarely overlap) over the bbox.  One closed shell per geometry, counter-clockwise."""
     rng = np.random.Generator(np.random.PCG64(seed))
+    if n_centres is None:
+        n_centres = max(16, n // 500)
     x0, y0, x1, y1 = bbox
     cc = np.column_stack([rng.uniform(x0, x1, n_centres), rng.uniform(y0, y1, n_centres)])
     c = cc[rng.integers(0, n_centres, n)] + rng.normal(0.0, sigma, (n, 2))
