@@ -12,6 +12,10 @@
  *                             expressions/index/PointIndexLonLat.scala:44-51 ->
  *                             core/index/H3IndexSystem.scala:140-142 (pointToIndex) and
  *                             core/index/BNGIndexSystem.scala:277-291 (pointToIndex)
+ *   mosaic_point_geom_to_cell grid_pointascellid over a geometry column (WKB / WKT / hex rows):
+ *   mosaic_point_geom_decode    PointIndexGeom.scala:32-40 -> GeometryAPI.geometry (GeometryAPI.scala:64-72)
+ *                             -> MosaicGeometryJTS.fromWKB / fromWKT / fromHEX (MosaicGeometryJTS.scala:164,
+ *                             195-200) -> getCentroid (:49-53) -> getX / getY (point/MosaicPointJTS.scala:23-25)
  *   mosaic_resolution         H3IndexSystem.getResolution (H3IndexSystem.scala:39-54),
  *                             BNGIndexSystem.getResolution (BNGIndexSystem.scala:342-353)
  *   mosaic_bng_format/_parse  BNGIndexSystem.format / parse (BNGIndexSystem.scala:114-129, 391-413)
@@ -114,6 +118,28 @@ int mosaic_resolution_str(int grid, const char* res, int* out);
  * valid (nullable): 1 = row present; null rows give out_valid 0 and cell 0 (NullIntolerant). */
 int mosaic_point_to_cell(mosaic_ctx* ctx, int grid, int res, const double* x, const double* y,
                          const uint8_t* valid, int64_t n, int64_t* out_cell, uint8_t* out_valid);
+/* grid_pointascellid over a point geometry column in Arrow binary / utf8 layout: row i is
+ * data[offsets[i] .. offsets[i+1]); format = MOSAIC_GEOM_WKB / _WKT / _HEX, | MOSAIC_GEOM_OFFSETS32
+ * for 32-bit offsets (default 64-bit).  Every row JTS 1.19 certainly reads as a non-empty Point is
+ * decoded on the device (Double.parseDouble-exact numbers; either WKB byte order; EWKB / ISO Z, M,
+ * SRID) and indexed: row_status MOSAIC_ROW_OK.  Null rows: MOSAIC_ROW_NULL, cell 0.  Every other
+ * row (other geometry types, whose centroid the reference indexes; POINT EMPTY and malformed rows,
+ * on which the reference throws) gets MOSAIC_ROW_PATH and cell 0: the caller evaluates those rows
+ * with the reference's row-wise expression.  *n_rowpath (nullable) = their number. */
+#define MOSAIC_GEOM_WKB 0
+#define MOSAIC_GEOM_WKT 1
+#define MOSAIC_GEOM_HEX 2
+#define MOSAIC_GEOM_OFFSETS32 0x100
+#define MOSAIC_ROW_NULL 0
+#define MOSAIC_ROW_OK 1
+#define MOSAIC_ROW_PATH 2
+int mosaic_point_geom_to_cell(mosaic_ctx* ctx, int grid, int res, int format, const void* offsets,
+                              const uint8_t* data, const uint8_t* valid, int64_t n, int64_t* out_cell,
+                              uint8_t* row_status, int64_t* n_rowpath);
+/* The decode alone: x / y of MOSAIC_ROW_OK rows (0 elsewhere), row_status as above. */
+int mosaic_point_geom_decode(mosaic_ctx* ctx, int format, const void* offsets, const uint8_t* data,
+                             const uint8_t* valid, int64_t n, double* x, double* y, uint8_t* row_status,
+                             int64_t* n_rowpath);
 /* BNG id <-> string (BNGIndexSystem.format / parse).  format returns the string length. */
 int mosaic_bng_format(int64_t id, char* buf, size_t cap);
 int mosaic_bng_parse(const char* s, int64_t* out);

@@ -33,8 +33,17 @@ EXPORTS = [
     "mosaic_chip_table_create", "mosaic_chip_table_destroy", "mosaic_chip_table_info", "mosaic_chip_table_tiles",
     "mosaic_chip_table_tile_grid", "mosaic_chip_table_raster", "mosaic_pip_join_count",
     "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_chip_set_info",
-    "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times",
+    "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_point_geom_to_cell",
+    "mosaic_point_geom_decode",
 ]
+
+GEOM_WKB = 0
+GEOM_WKT = 1
+GEOM_HEX = 2
+GEOM_OFFSETS32 = 0x100
+ROW_NULL = 0
+ROW_OK = 1
+ROW_PATH = 2
 
 
 class NativeUnavailable(RuntimeError):
@@ -104,6 +113,8 @@ def lib():
         "mosaic_chip_set_export": ([vp, vp, vp, vp, vp, vp], i32),
         "mosaic_chip_set_destroy": ([vp], i32),
         "mosaic_kernel_times": ([vp, vp, i64, ctypes.POINTER(i64)], i32),
+        "mosaic_point_geom_to_cell": ([vp, i32, i32, i32, vp, vp, vp, i64, vp, vp, ctypes.POINTER(i64)], i32),
+        "mosaic_point_geom_decode": ([vp, i32, vp, vp, vp, i64, vp, vp, vp, ctypes.POINTER(i64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

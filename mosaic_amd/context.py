@@ -104,26 +104,49 @@ def _is_torch(a):
     return hasattr(a, "data_ptr") and not isinstance(a, np.ndarray)
 
 
+class RowPathRequired(RuntimeError):
+    """Rows the engine leaves to the reference's row-wise expression (MOSAIC_ROW_PATH): geometry
+    types other than Point (the reference indexes their centroid), POINT EMPTY and malformed rows
+    (on which the reference throws).  ``rows`` holds their indices.  The columnar exec of
+    INTEGRATION.md evaluates them with PointIndexGeom.nullSafeEval; this mirror reports them."""
+
+    def __init__(self, rows):
+        super().__init__(f"{len(rows)} row(s) need the reference row path (first: row {int(rows[0])})")
+        self.rows = rows
+
+
+def geometry_column(geoms):
+    """A sequence of WKB (bytes) / WKT (str) / hex-WKB (str with format="hex") rows, None = null,
+    as an Arrow-layout column: (format, int64 offsets[n+1], uint8 values, uint8 validity or None)."""
+    geoms = list(geoms)
+    kinds = {type(g) for g in geoms if g is not None}
+    if kinds <= {bytes, bytearray, memoryview}:
+        fmt = N.GEOM_WKB
+        rows = [bytes(g) if g is not None else b"" for g in geoms]
+    elif kinds <= {str}:
+        fmt = N.GEOM_WKT
+        rows = [g.encode("utf-8") if g is not None else b"" for g in geoms]
+    else:
+        raise TypeError("a geometry column holds WKB bytes or WKT strings")
+    lens = np.fromiter((len(r) for r in rows), np.int64, len(rows))
+    offsets = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    data = np.frombuffer(b"".join(rows), np.uint8) if offsets[-1] else np.zeros(1, np.uint8)
+    valid = None
+    if any(g is None for g in geoms):
+        valid = np.fromiter((g is not None for g in geoms), np.uint8, len(geoms))
+    return fmt, offsets, data, valid
+
+
 def _points_xy(points):
-    """Accepts (x, y) arrays, an (n, 2) array, or a sequence of WKT / WKB point geometries."""
+    """Accepts (x, y) arrays or an (n, 2) array (host or device)."""
     if isinstance(points, tuple) and len(points) == 2:
         return _f64(points[0]), _f64(points[1])
     if isinstance(points, np.ndarray) and points.ndim == 2 and points.shape[1] == 2:
         return _f64(points[:, 0]), _f64(points[:, 1])
     if _is_torch(points) and points.dim() == 2:
         return _f64(points[:, 0]), _f64(points[:, 1])
-    xs, ys = [], []
-    for g in points:
-        kind, v = W.read_wkb(g) if isinstance(g, (bytes, bytearray, memoryview)) else W.read_wkt(g)
-        if kind == "point":
-            if v is None:
-                raise ValueError("POINT EMPTY has no centroid")
-            xs.append(v[0])
-            ys.append(v[1])
-        else:
-            # the reference indexes the centroid of non-point geometries (PointIndexGeom.scala:35-36)
-            raise ValueError("grid_pointascellid expects point geometries in this engine")
-    return np.asarray(xs, np.float64), np.asarray(ys, np.float64)
+    return None
 
 
 class ChipTable:
@@ -278,17 +301,90 @@ class MosaicContext:
         cells = self._cells(lon, lat, resolution)
         return cells if raw else self._serialize(cells)
 
-    def grid_pointascellid(self, points, resolution, raw=False):
-        """PointIndexGeom (expressions/index/PointIndexGeom.scala:32-40)."""
-        x, y = _points_xy(points)
-        cells = self._cells(x, y, resolution)
-        return cells if raw else self._serialize(cells)
+    def grid_pointascellid(self, points, resolution, raw=False, fmt=None, return_status=False):
+        """PointIndexGeom (expressions/index/PointIndexGeom.scala:32-40).  ``points``: (x, y)
+        arrays / an (n, 2) array, or a geometry column -- a sequence of WKB bytes / WKT strings
+        (None = null) or an Arrow-layout tuple (offsets, values, validity) with ``fmt`` one of
+        "wkb" / "wkt" / "hex" -- decoded on the device (mosaic_point_geom_to_cell).  Rows the
+        engine leaves to the reference row path raise RowPathRequired unless return_status, which
+        returns (cells, row_status) with row_status 0 null / 1 ok / 2 row path."""
+        xy = _points_xy(points)
+        if xy is not None:
+            cells = self._cells(xy[0], xy[1], resolution)
+            return cells if raw else self._serialize(cells)
+        res = self.index_system.get_resolution(resolution)
+        if isinstance(points, tuple) and len(points) == 3:
+            offsets, data, valid = points
+            f = {"wkb": N.GEOM_WKB, "wkt": N.GEOM_WKT, "hex": N.GEOM_HEX}[fmt or "wkb"]
+        else:
+            f, offsets, data, valid = geometry_column(points)
+            if fmt == "hex":
+                f = N.GEOM_HEX
+        if not _is_torch(offsets):
+            offsets = np.ascontiguousarray(offsets)
+            if offsets.dtype == np.int32:
+                f |= N.GEOM_OFFSETS32
+            else:
+                offsets = offsets.astype(np.int64, copy=False)
+        elif str(offsets.dtype) == "torch.int32":
+            f |= N.GEOM_OFFSETS32
+        if valid is not None and not _is_torch(valid):
+            valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        n = int(offsets.shape[0]) - 1
+        if _is_torch(offsets):
+            import torch
+
+            out = torch.empty(n, dtype=torch.int64, device=offsets.device)
+            status = torch.empty(n, dtype=torch.uint8, device=offsets.device)
+        else:
+            out = np.empty(n, np.int64)
+            status = np.empty(n, np.uint8)
+        n_rp = ctypes.c_int64(0)
+        N.check(N.lib().mosaic_point_geom_to_cell(self.handle, self.index_system.grid, res, f, N.ptr(offsets),
+                                                  N.ptr(data), N.ptr(valid), n, N.ptr(out), N.ptr(status),
+                                                  ctypes.byref(n_rp)))
+        if n_rp.value and not return_status:
+            st = status.cpu().numpy() if _is_torch(status) else status
+            raise RowPathRequired(np.flatnonzero(st == N.ROW_PATH))
+        cells = out if raw else self._serialize(out)
+        return (cells, status) if return_status else cells
+
+    def decode_points(self, points, fmt=None):
+        """Point geometry column (as in grid_pointascellid) -> (x, y) on the device decoder
+        (mosaic_point_geom_decode); raises RowPathRequired for rows it does not decode."""
+        if isinstance(points, tuple) and len(points) == 3:
+            offsets, data, valid = points
+            f = {"wkb": N.GEOM_WKB, "wkt": N.GEOM_WKT, "hex": N.GEOM_HEX}[fmt or "wkb"]
+        else:
+            f, offsets, data, valid = geometry_column(points)
+            if fmt == "hex":
+                f = N.GEOM_HEX
+        offsets = np.ascontiguousarray(offsets)
+        if offsets.dtype == np.int32:
+            f |= N.GEOM_OFFSETS32
+        else:
+            offsets = offsets.astype(np.int64, copy=False)
+        n = len(offsets) - 1
+        x, y, status = np.empty(n), np.empty(n), np.empty(n, np.uint8)
+        n_rp = ctypes.c_int64(0)
+        v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+        N.check(N.lib().mosaic_point_geom_decode(self.handle, f, N.ptr(offsets), N.ptr(data), N.ptr(v), n, N.ptr(x),
+                                                 N.ptr(y), N.ptr(status), ctypes.byref(n_rp)))
+        if n_rp.value or (status == N.ROW_NULL).any():
+            raise RowPathRequired(np.flatnonzero(status != N.ROW_OK))
+        return x, y
 
     # ---- st_contains ----
     def st_contains(self, geoms, points):
         """Row-wise st_contains(geom, point): geoms are WKB bytes or WKT strings (one per row, or one
-        for all rows); points as in grid_pointascellid."""
-        x, y = _points_xy(points)
+        for all rows); points as in grid_pointascellid (a point geometry column is decoded on the
+        device; rows it leaves to the row path raise RowPathRequired)."""
+        xy = _points_xy(points)
+        if xy is None:
+            xy = self.decode_points(points)
+        x, y = xy
+        if _is_torch(x):
+            x, y = x.cpu(), y.cpu()
         x, y = np.asarray(x), np.asarray(y)
         n = len(x)
         if isinstance(geoms, (str, bytes, bytearray)):

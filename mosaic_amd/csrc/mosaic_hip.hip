@@ -25,6 +25,7 @@
 #include "h3_device.h"
 #include "pip_coop.h"
 #include "pip_device.h"
+#include "point_decode.h"
 #include "raster.h"
 #include "tiles.h"
 
@@ -1373,6 +1374,7 @@ struct CellArgs {
     const double* x;
     const double* y;
     const uint8_t* valid;
+    const uint8_t* status;  // decoded point rows (k_decode_points): present iff status == kRowOk
     int64_t n;
     int res, jdk;
     long long* out;
@@ -1383,10 +1385,14 @@ struct CellArgs {
     unsigned int* flags;
 };
 
+__device__ __forceinline__ bool cell_row_present(const CellArgs& a, int64_t i) {
+    return (!a.valid || a.valid[i]) && (!a.status || a.status[i] == 1);
+}
+
 __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        bool v = !a.valid || a.valid[i];
+        bool v = cell_row_present(a, i);
         if (a.out_valid) a.out_valid[i] = v;
         if (!v) {
             a.out[i] = 0;
@@ -1409,7 +1415,7 @@ __global__ void __launch_bounds__(256) k_cell_h3_exact(CellArgs a, int all_rows)
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
     for (unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
         int64_t i = all_rows ? (int64_t)t : (int64_t)a.amb_queue[t];
-        if (a.valid && !a.valid[i]) continue;
+        if (!cell_row_present(a, i)) continue;
         a.out[i] = (long long)h3::h3_exact(h3::to_radians(a.y[i], a.jdk), h3::to_radians(a.x[i], a.jdk), a.res);
     }
 }
@@ -1418,13 +1424,89 @@ __global__ void __launch_bounds__(256) k_cell_bng(CellArgs a) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     bool nan_seen = false;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        bool v = !a.valid || a.valid[i];
+        bool v = cell_row_present(a, i);
         if (a.out_valid) a.out_valid[i] = v;
         int64_t cell = 0;
         if (v && !bng::point_to_index(a.x[i], a.y[i], a.res, &cell)) nan_seen = true;
         a.out[i] = v ? cell : 0;
     }
     if (nan_seen) atomicOr(a.flags, 1u);
+}
+
+// ---- point geometry column -> coordinates (grid_pointascellid over WKB / WKT / hex rows) ----
+// One lane per row; rows are [offsets[i], offsets[i+1]) of the value buffer (Arrow binary / utf8
+// layout, 32- or 64-bit offsets).  Status per row: 0 null, 1 decoded, 2 row path (point_decode.h).
+struct DecodeArgs {
+    const void* offsets;
+    int off64;
+    const uint8_t* data;
+    const uint8_t* valid;
+    int64_t n;
+    int format;
+    double* x;
+    double* y;
+    uint8_t* status;
+    unsigned long long* n_rowpath;
+};
+
+// Each wave takes 64 consecutive rows.  Their value bytes -- one contiguous span -- are copied
+// to the wave's LDS slice with coalesced 16-byte loads, and every lane parses its row from LDS
+// (ds_read_u8 at LDS latency instead of a chain of dependent global byte loads).  A wave whose
+// span exceeds the slice parses from global memory.  The copy reads the 16-byte aligned granules
+// around the span: no page is touched that does not hold a byte of the span.
+static const int kDecodeWaveBytes = 4096;
+
+__device__ __forceinline__ int64_t decode_offset(const DecodeArgs& a, int64_t i) {
+    return a.off64 ? ((const int64_t*)a.offsets)[i] : (int64_t)((const int32_t*)a.offsets)[i];
+}
+
+__global__ void __launch_bounds__(256) k_decode_points(DecodeArgs a) {
+    __shared__ uint4 stage[4][kDecodeWaveBytes / 16];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned int rowpath = 0;
+    for (int64_t w0 = (int64_t)blockIdx.x * blockDim.x + wave * 64; w0 < a.n; w0 += stride) {  // wave-uniform
+        const int64_t i = w0 + lane;
+        const bool act = i < a.n;
+        const int64_t wend = w0 + 64 < a.n ? w0 + 64 : a.n;
+        const int64_t sb = decode_offset(a, w0), se = decode_offset(a, wend);
+        const uintptr_t gb = ((uintptr_t)(a.data + sb)) & ~(uintptr_t)15;
+        const int64_t nchunk = se > sb ? (int64_t)(((uintptr_t)(a.data + se) - gb + 15) >> 4) : 0;
+        const bool staged = se >= sb && nchunk <= kDecodeWaveBytes / 16;
+        __builtin_amdgcn_wave_barrier();
+        if (staged) {
+            const uint4* g = (const uint4*)gb;
+            for (int64_t k = lane; k < nchunk; k += 64) stage[wave][k] = g[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        double px = 0.0, py = 0.0;
+        uint8_t st = 0;
+        if (act && (!a.valid || a.valid[i])) {
+            const int64_t b = decode_offset(a, i), e = decode_offset(a, i + 1);
+            int rc = decode::kBadWkb;
+            if (e >= b && b >= sb && e <= se) {
+                if (staged) {
+                    const uint8_t* row = (const uint8_t*)stage[wave] + ((uintptr_t)(a.data + b) - gb);
+                    rc = decode::decode_row(a.format, row, e - b, &px, &py);
+                } else {
+                    rc = decode::decode_row(a.format, a.data + b, e - b, &px, &py);
+                }
+            }
+            st = rc == decode::kOk ? 1 : 2;
+            if (st == 2) {
+                px = py = 0.0;
+                rowpath++;
+            }
+        }
+        if (act) {
+            a.x[i] = px;
+            a.y[i] = py;
+            a.status[i] = st;
+        }
+    }
+    if (rowpath) atomicAdd(a.n_rowpath, (unsigned long long)rowpath);
 }
 
 struct ContainsArgs {
@@ -1497,6 +1579,7 @@ struct mosaic_ctx {
                                   // 2: k_join_stream_pipe (lookups pipelined over iterations)
     int probe_mask = 0;     // measurement only: see JoinArgs::probe_mask (results are wrong when set)
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
+    DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
     // option "timing": HIP events bracket each fused join kernel on the context stream
@@ -1846,14 +1929,10 @@ int mosaic_resolution_str(int grid, const char* s, int* out) {
     return fail(MOSAIC_E_ARG, "unknown grid");
 }
 
-int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, const double* y, const uint8_t* valid,
-                         int64_t n, int64_t* out_cell, uint8_t* out_valid) {
-    if (!c || (n > 0 && (!x || !y || !out_cell))) return fail(MOSAIC_E_ARG, "null argument");
-    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
-    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
-    if (!valid_res(grid, res)) return res_error(grid, res);
-    if (n == 0) return MOSAIC_OK;
-    HIP_TRY(hipSetDevice(c->device));
+// status (device, nullable): rows of a decoded geometry column, present iff status == 1
+static int point_to_cell_impl(mosaic_ctx* c, int grid, int res, const double* x, const double* y,
+                              const uint8_t* valid, const uint8_t* status, int64_t n, int64_t* out_cell,
+                              uint8_t* out_valid) {
     int rc;
     const void *dx, *dy, *dv;
     if ((rc = to_device(c, c->stage_x, x, n * 8, &dx))) return rc;
@@ -1873,6 +1952,7 @@ int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, cons
     a.x = (const double*)dx;
     a.y = (const double*)dy;
     a.valid = (const uint8_t*)dv;
+    a.status = status;
     a.n = n;
     a.res = res;
     a.jdk = c->jdk;
@@ -1909,6 +1989,110 @@ int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, cons
     if (!dev_out) HIP_TRY(hipMemcpy(out_cell, dout, n * 8, hipMemcpyDeviceToHost));
     if (out_valid && !dev_vout) HIP_TRY(hipMemcpy(out_valid, dvout, n, hipMemcpyDeviceToHost));
     return MOSAIC_OK;
+}
+
+int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, const double* y, const uint8_t* valid,
+                         int64_t n, int64_t* out_cell, uint8_t* out_valid) {
+    if (!c || (n > 0 && (!x || !y || !out_cell))) return fail(MOSAIC_E_ARG, "null argument");
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
+    if (!valid_res(grid, res)) return res_error(grid, res);
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    return point_to_cell_impl(c, grid, res, x, y, valid, nullptr, n, out_cell, out_valid);
+}
+
+// Decode a point geometry column into c->dec_x / dec_y / dec_status (device); *n_rowpath = rows
+// left to the reference row path.  Synchronous.
+static int decode_points(mosaic_ctx* c, int format, const void* offsets, const uint8_t* data, const uint8_t* valid,
+                         int64_t n, int64_t* n_rowpath) {
+    const int fmt = format & 0xff;
+    const bool off64 = !(format & MOSAIC_GEOM_OFFSETS32);
+    if (fmt != MOSAIC_GEOM_WKB && fmt != MOSAIC_GEOM_WKT && fmt != MOSAIC_GEOM_HEX)
+        return fail(MOSAIC_E_ARG, "unknown geometry format");
+    if ((format & ~0x1ff) != 0) return fail(MOSAIC_E_ARG, "unknown geometry format flags");
+    const size_t ob = off64 ? 8 : 4;
+    int rc;
+    const void *doff, *ddata = nullptr, *dv;
+    // the value buffer spans [0, offsets[n]) (Arrow: offsets are relative to the buffer start)
+    int64_t end = 0;
+    if (is_device_ptr(offsets)) {
+        int64_t e64 = 0;
+        int32_t e32 = 0;
+        HIP_TRY(hipMemcpy(off64 ? (void*)&e64 : (void*)&e32, (const char*)offsets + n * ob, ob, hipMemcpyDeviceToHost));
+        end = off64 ? e64 : e32;
+    } else {
+        end = off64 ? ((const int64_t*)offsets)[n] : ((const int32_t*)offsets)[n];
+    }
+    if (end < 0) return fail(MOSAIC_E_ARG, "negative offsets");
+    if (end > 0 && !data) return fail(MOSAIC_E_ARG, "null argument");
+    if ((rc = to_device(c, c->geo_off, offsets, (size_t)(n + 1) * ob, &doff))) return rc;
+    if (end > 0 && (rc = to_device(c, c->geo_data, data, (size_t)end, &ddata))) return rc;
+    if ((rc = to_device(c, c->stage_v, valid, n, &dv))) return rc;
+    if ((rc = c->dec_x.reserve(n * 8)) || (rc = c->dec_y.reserve(n * 8)) || (rc = c->dec_status.reserve(n))) return rc;
+    HIP_TRY(hipMemsetAsync(c->scalars.p, 0, kScalars * 8, c->stream));
+    DecodeArgs a;
+    a.offsets = doff;
+    a.off64 = off64 ? 1 : 0;
+    a.data = (const uint8_t*)ddata;
+    a.valid = (const uint8_t*)dv;
+    a.n = n;
+    a.format = fmt;
+    a.x = (double*)c->dec_x.p;
+    a.y = (double*)c->dec_y.p;
+    a.status = (uint8_t*)c->dec_status.p;
+    a.n_rowpath = (unsigned long long*)c->scalars.p + 4;
+    hipLaunchKernelGGL(k_decode_points, dim3(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)c->n_cu * 8))), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    unsigned long long r = 0;
+    HIP_TRY(hipMemcpyAsync(&r, a.n_rowpath, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n_rowpath) *n_rowpath = (int64_t)r;
+    return MOSAIC_OK;
+}
+
+static int copy_out(mosaic_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!dst || !bytes) return MOSAIC_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, is_device_ptr(dst) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MOSAIC_OK;
+}
+
+int mosaic_point_geom_decode(mosaic_ctx* c, int format, const void* offsets, const uint8_t* data, const uint8_t* valid,
+                             int64_t n, double* x, double* y, uint8_t* row_status, int64_t* n_rowpath) {
+    if (!c || !offsets || (n > 0 && (!x || !y || !row_status))) return fail(MOSAIC_E_ARG, "null argument");
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (n_rowpath) *n_rowpath = 0;
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = decode_points(c, format, offsets, data, valid, n, n_rowpath))) return rc;
+    if ((rc = copy_out(c, x, c->dec_x.p, n * 8)) || (rc = copy_out(c, y, c->dec_y.p, n * 8)) ||
+        (rc = copy_out(c, row_status, c->dec_status.p, n)))
+        return rc;
+    return MOSAIC_OK;
+}
+
+int mosaic_point_geom_to_cell(mosaic_ctx* c, int grid, int res, int format, const void* offsets, const uint8_t* data,
+                              const uint8_t* valid, int64_t n, int64_t* out_cell, uint8_t* row_status,
+                              int64_t* n_rowpath) {
+    if (!c || !offsets || (n > 0 && (!out_cell || !row_status))) return fail(MOSAIC_E_ARG, "null argument");
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
+    if (!valid_res(grid, res)) return res_error(grid, res);
+    if (n_rowpath) *n_rowpath = 0;
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = decode_points(c, format, offsets, data, valid, n, n_rowpath))) return rc;
+    const int async = c->async;
+    c->async = 0;
+    rc = point_to_cell_impl(c, grid, res, (const double*)c->dec_x.p, (const double*)c->dec_y.p, nullptr,
+                            (const uint8_t*)c->dec_status.p, n, out_cell, nullptr);
+    c->async = async;
+    if (rc) return rc;
+    return copy_out(c, row_status, c->dec_status.p, n);
 }
 
 // BNGIndexSystem.letterMap (BNGIndexSystem.scala:84-99) and quadrants (:36)

@@ -566,3 +566,102 @@ def test_join_c4_buildings(h3ctx, n_buildings):
     rows, keys = h3ctx.pip_join_pairs(table, x, y)
     assert len(rows) == total and np.array_equal(np.bincount(keys, minlength=n_buildings), want)
     table.close()
+
+
+# ---------------- point geometry column decode ----------------
+def _column(rows):
+    lens = np.array([len(r) for r in rows], np.int64)
+    offs = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    return offs, np.frombuffer(b"".join(rows) or b"\0", np.uint8).copy()
+
+
+@pytest.mark.parametrize("offsets32", [False, True])
+def test_point_decode_corpus(h3ctx, offsets32):
+    """Device decoder vs the oracle restatement (oracle/point_decode.py) on the adversarial corpus:
+    identical decode / row-path split, bit-identical coordinates; null rows stay null."""
+    import ctypes
+    import struct
+
+    from mosaic_amd import _native as N
+    from oracle import point_decode as PD
+    from tests.helpers import point_rows
+
+    rows = point_rows(np.random.default_rng(41))
+    for fmt in (0, 1, 2):
+        sel = [r for f, r in rows if f == fmt]
+        sel = sel + [b""]  # a null row (validity 0) with an empty value
+        offs, data = _column(sel)
+        if offsets32:
+            offs = offs.astype(np.int32)
+        valid = np.ones(len(sel), np.uint8)
+        valid[-1] = 0
+        n = len(sel)
+        x, y, st = np.empty(n), np.empty(n), np.empty(n, np.uint8)
+        n_rp = ctypes.c_int64(0)
+        f = fmt | (N.GEOM_OFFSETS32 if offsets32 else 0)
+        N.check(N.lib().mosaic_point_geom_decode(h3ctx.handle, f, N.ptr(offs), N.ptr(data), N.ptr(valid), n, N.ptr(x),
+                                                 N.ptr(y), N.ptr(st), ctypes.byref(n_rp)))
+        assert st[-1] == N.ROW_NULL
+        n_path = 0
+        for k, r in enumerate(sel[:-1]):
+            want = PD.decode(fmt, r)
+            if want[0] == "ok":
+                assert st[k] == N.ROW_OK, (fmt, r)
+                assert struct.pack("<dd", x[k], y[k]) == struct.pack("<dd", want[1], want[2]), (fmt, r, x[k], y[k])
+            else:
+                assert st[k] == N.ROW_PATH, (fmt, r)
+                n_path += 1
+        assert n_rp.value == n_path > 0
+
+
+def test_grid_pointascellid_geometry_columns(h3ctx, bngctx):
+    """grid_pointascellid over WKT / WKB / hex columns == grid_longlatascellid of the decoded
+    coordinates == the oracle; rows the engine leaves to the row path are reported, not guessed."""
+    from mosaic_amd import RowPathRequired
+    from mosaic_amd.wkb import point_wkb
+
+    rng = np.random.default_rng(43)
+    x = np.round(rng.uniform(-74.3, -73.7, 50_000), 6)
+    y = np.round(rng.uniform(40.5, 40.9, 50_000), 6)
+    want = oracle.h3_point_to_index(x, y, 9)
+    wkt = ["POINT (%r %r)" % (float(a), float(b)) for a, b in zip(x, y)]
+    assert np.array_equal(h3ctx.grid_pointascellid(wkt, 9), want)
+    wkb = [point_wkb(a, b, big_endian=bool(k % 2)) for k, (a, b) in enumerate(zip(x, y))]
+    assert np.array_equal(h3ctx.grid_pointascellid(wkb, 9), want)
+    hexrows = [w.hex() for w in wkb[:5000]]
+    assert np.array_equal(h3ctx.grid_pointascellid(hexrows, 9, fmt="hex"), want[:5000])
+    # nulls and row-path rows
+    mixed = [wkt[0], None, "POLYGON ((0 0, 1 0, 1 1, 0 0))", "POINT EMPTY", wkt[1]]
+    cells, st = h3ctx.grid_pointascellid(mixed, 9, return_status=True)
+    assert list(st) == [1, 0, 2, 2, 1] and cells[0] == want[0] and cells[4] == want[1] and cells[1] == 0
+    with pytest.raises(RowPathRequired) as ei:
+        h3ctx.grid_pointascellid(mixed, 9)
+    assert list(ei.value.rows) == [2, 3]
+    # BNG: metres, string ids; NaN coordinates still raise the reference's exception
+    e = np.round(rng.uniform(0, 700_000, 20_000), 1)
+    nn = np.round(rng.uniform(0, 1_300_000, 20_000), 1)
+    got = bngctx.grid_pointascellid(["POINT (%r %r)" % (float(a), float(b)) for a, b in zip(e, nn)], "100m", raw=True)
+    assert np.array_equal(got, oracle.bng_point_to_index_batch(e, nn, 4)[0])
+    with pytest.raises(IllegalStateException, match="NaN"):
+        bngctx.grid_pointascellid(["POINT (NaN 5)"], 4)
+
+
+def test_point_decode_device_buffers_at_scale(h3ctx):
+    """C1 shape: 10M taxi-GPS WKT rows (1e-6 degree rounding) resident on the device, int32
+    offsets (Spark's Arrow utf8): cells equal the direct lon/lat path on the same doubles."""
+    torch = pytest.importorskip("torch")
+    from mosaic_amd.data import quickstart_points
+
+    zones = PolygonSet.load("nyc_taxi_zones")
+    x, y = quickstart_points(zones, 2_000_000, seed=44)
+    x, y = np.round(x, 6), np.round(y, 6)
+    rows = [("POINT (%.6f %.6f)" % (a, b)).encode() for a, b in zip(x, y)] * 5
+    offs, data = _column(rows)
+    offs32 = torch.tensor(offs.astype(np.int32), device="cuda")
+    dd = torch.tensor(data, device="cuda")
+    cells, st = h3ctx.grid_pointascellid((offs32, dd, None), 9, raw=True, fmt="wkt", return_status=True)
+    assert cells.is_cuda and int((st != 1).sum()) == 0
+    direct = h3ctx.grid_longlatascellid(np.tile(x, 5), np.tile(y, 5), 9, raw=True)
+    assert np.array_equal(cells.cpu().numpy(), direct)
+    assert np.array_equal(direct[:2_000_000], oracle.h3_point_to_index(x, y, 9))
