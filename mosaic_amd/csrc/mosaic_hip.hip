@@ -797,11 +797,17 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 #endif
 // k_join_stream dynamic LDS: [per-polygon counts (LDS_COUNTS)] [per-wave mixed-row stages]
 // [tile_base (tile_lds_n words)] [quad level of the raster (if any)]
-static const size_t kStreamLdsTile = 80 * 1024;  // LDS per workgroup up to which tile_base joins it
+#ifndef MOSAIC_STREAM_LDS_TILE
+#define MOSAIC_STREAM_LDS_TILE (80 * 1024)
+#endif
+static const size_t kStreamLdsTile = MOSAIC_STREAM_LDS_TILE;  // LDS per workgroup up to which tile_base joins it
 static inline size_t stream_stage_words(int block, int G) { return (size_t)(block / 64) * (64 + 256 * (size_t)G); }
 
+#ifndef MOSAIC_STREAM_LB
+#define MOSAIC_STREAM_LB 1024  // k_join_stream: largest workgroup (1024 caps a lane at 128 VGPRs)
+#endif
 template <bool LDS_COUNTS, bool PAIRS, bool VEC, bool VALID, int G>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MOSAIC_STREAM_WAVES)))
+__global__ void __launch_bounds__(MOSAIC_STREAM_LB) __attribute__((amdgpu_waves_per_eu(MOSAIC_STREAM_WAVES)))
 k_join_stream(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     uint32_t* stage = lds + (LDS_COUNTS ? a.n_polygons : 0);
@@ -1831,7 +1837,8 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
     } else if (k == "tile_lds") {
         c->tile_lds = v ? 1 : 0;
     } else if (k == "stream_block") {
-        if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, 1024]");
+        if (v < 64 || v > MOSAIC_STREAM_LB || v % 64)
+            return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, " + std::to_string(MOSAIC_STREAM_LB) + "]");
         c->stream_block = (int)v;
     } else if (k == "raster_cell") {
         if (v < 1 || v > 32) return fail(MOSAIC_E_ARG, "raster_cell must be in [1, 32]");
