@@ -201,6 +201,19 @@ int mosaic_chip_set_destroy(mosaic_chip_set* cs);
 int mosaic_st_contains(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* wkb_offsets, const uint8_t* wkb,
                        const int32_t* geom_index, const double* px, const double* py, int64_t n, uint8_t* out);
 
+/* ---- st_intersects_aggregate over the chip join of two chip tables ---- */
+/* For every (left polygon_key, right polygon_key) pair whose chip sets share at least one cell id,
+ * flag = OR over the chip pairs of the shared cells of (left.is_core || right.is_core ||
+ * JTS 1.19 intersects(left.wkb, right.wkb)).  Groups are written sorted by (left key, right key);
+ * if more than `cap` groups exist, returns MOSAIC_E_CAPACITY with *n_out = the required size.
+ * Both tables must use the same grid and resolution.  Replaces the equi-join + groupBy +
+ * st_intersects_aggregate pattern: ST_IntersectsAggregate.update
+ * (expressions/geometry/ST_IntersectsAggregate.scala:28-39) as used in
+ * ST_IntersectsBehaviors.scala:34-47 / MosaicContext.scala st_intersects_aggregate. */
+int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
+                                int32_t* out_left_key, int32_t* out_right_key, uint8_t* out_flag, int64_t cap,
+                                int64_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

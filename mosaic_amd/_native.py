@@ -34,7 +34,7 @@ EXPORTS = [
     "mosaic_chip_table_tile_grid", "mosaic_chip_table_raster", "mosaic_pip_join_count",
     "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_chip_set_info",
     "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_point_geom_to_cell",
-    "mosaic_point_geom_decode",
+    "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
 ]
 
 GEOM_WKB = 0
@@ -115,6 +115,7 @@ def lib():
         "mosaic_kernel_times": ([vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_point_geom_to_cell": ([vp, i32, i32, i32, vp, vp, vp, i64, vp, vp, ctypes.POINTER(i64)], i32),
         "mosaic_point_geom_decode": ([vp, i32, vp, vp, vp, i64, vp, vp, vp, ctypes.POINTER(i64)], i32),
+        "mosaic_intersects_aggregate": ([vp, vp, vp, vp, vp, vp, i64, ctypes.POINTER(i64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

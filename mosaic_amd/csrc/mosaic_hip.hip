@@ -1036,6 +1036,113 @@ k_join_stream_pipe(JoinArgs a) {
     counts_flush<LDS_COUNTS>(a, lds, 0u);
 }
 
+
+// ---- st_intersects_aggregate over the chip join of two chip tables ----------------------------
+// ST_IntersectsAggregate.update (expressions/geometry/ST_IntersectsAggregate.scala:28-39) folds
+// `left.is_core || right.is_core || left.wkb intersects right.wkb` with OR over the rows of a
+// (left key, right key) group, the rows being the equi-join of the two chip sets on index_id
+// (ST_IntersectsBehaviors.scala:34-47).  One wave per cell of the left table: it probes the right
+// table for the cell and folds every (left chip, right chip) pair of the cell into its group, held
+// in a device hash keyed by (left key << 32 | right key).  A group already true skips the geometry
+// test (the reference's `accumulator || ...`).  The geometry test spreads the segment pairs of two
+// rings over the wave's lanes (any hit ends it), then the shell-vertex containments.
+static const unsigned long long kEmptyGroup = ~0ULL;
+struct IsectArgs {
+    const HashEntry* ta;
+    uint64_t capa;
+    const uint32_t* meta_a;
+    pip::GeomStore sa;
+    const HashEntry* tb;
+    uint64_t maskb;
+    const uint32_t* meta_b;
+    pip::GeomStore sb;
+    int pass;                          // 0: count chip pairs, 1: fold them into groups
+    unsigned long long* pair_count;    // pass 0
+    unsigned long long* gkey;          // pass 1: group hash (kEmptyGroup = free)
+    uint32_t* gflag;
+    uint64_t gmask;
+    int* overflow;
+};
+
+__device__ bool wave_intersects(const pip::GeomStore& sa, uint32_t a, const pip::GeomStore& sb, uint32_t b, int lane) {
+    if (sa.geom_part[a + 1] <= sa.geom_part[a] || sb.geom_part[b + 1] <= sb.geom_part[b]) return false;
+    if (!pip::boxes_meet(sa.geom_bbox[a], sb.geom_bbox[b])) return false;
+    const uint32_t ra0 = sa.part_ring[sa.geom_part[a]], ra1 = sa.part_ring[sa.geom_part[a + 1]];
+    const uint32_t rb0 = sb.part_ring[sb.geom_part[b]], rb1 = sb.part_ring[sb.geom_part[b + 1]];
+    for (uint32_t ra = ra0; ra < ra1; ra++) {
+        if (!pip::boxes_meet(sa.ring_bbox[ra], sb.geom_bbox[b])) continue;
+        const uint32_t ia = sa.ring_start[ra], na = sa.ring_start[ra + 1] - ia;
+        if (na < 2) continue;
+        for (uint32_t rb = rb0; rb < rb1; rb++) {
+            if (!pip::boxes_meet(sa.ring_bbox[ra], sb.ring_bbox[rb])) continue;
+            const uint32_t ib = sb.ring_start[rb], nb = sb.ring_start[rb + 1] - ib;
+            if (nb < 2) continue;
+            const uint64_t total = (uint64_t)(na - 1) * (nb - 1);
+            for (uint64_t base = 0; base < total; base += 64) {  // wave-uniform trip count
+                const uint64_t k = base + (uint64_t)lane;
+                bool hit = false;
+                if (k < total) {
+                    const uint32_t i = (uint32_t)(k / (nb - 1)), j = (uint32_t)(k - (uint64_t)i * (nb - 1));
+                    hit = pip::segments_intersect(sa.verts[ia + i], sa.verts[ia + i + 1], sb.verts[ib + j],
+                                                  sb.verts[ib + j + 1]);
+                }
+                if (__ballot(hit)) return true;
+            }
+        }
+    }
+    return pip::shell_vertex_in(sb, b, sa, a) || pip::shell_vertex_in(sa, a, sb, b);
+}
+
+__device__ inline uint64_t group_slot(const IsectArgs& a, unsigned long long key) {
+    uint64_t s = mix64(key) & a.gmask;
+    for (uint64_t probes = 0; probes <= a.gmask; probes++) {
+        const unsigned long long prev = atomicCAS(&a.gkey[s], kEmptyGroup, key);
+        if (prev == kEmptyGroup || prev == key) return s;
+        s = (s + 1) & a.gmask;
+    }
+    atomicExch(a.overflow, 1);
+    return ~0ULL;
+}
+
+__global__ void __launch_bounds__(256) k_isect_agg(IsectArgs a) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t slot = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; slot < a.capa; slot += nw) {
+        const HashEntry e = a.ta[slot];
+        if (e.key == kEmptyKey) continue;
+        uint32_t fb = 0, eb = 0;
+        for (uint64_t s = mix64((uint64_t)e.key) & a.maskb;; s = (s + 1) & a.maskb) {
+            const HashEntry f = a.tb[s];
+            if (f.key == e.key) {
+                fb = f.first;
+                eb = f.first + f.count;
+                break;
+            }
+            if (f.key == kEmptyKey) break;
+        }
+        if (eb == fb) continue;
+        if (a.pass == 0) {
+            if (lane == 0) atomicAdd(a.pair_count, (unsigned long long)e.count * (eb - fb));
+            continue;
+        }
+        for (uint32_t ca = e.first; ca < e.first + e.count; ca++)
+            for (uint32_t cb = fb; cb < eb; cb++) {
+                const uint32_t ma = a.meta_a[ca], mb = a.meta_b[cb];
+                const unsigned long long key = ((unsigned long long)(ma >> 1) << 32) | (unsigned long long)(mb >> 1);
+                uint64_t gs = 0;
+                uint32_t done = 0;
+                if (lane == 0) {
+                    gs = group_slot(a, key);
+                    done = gs == ~0ULL ? 1u : __hip_atomic_load(&a.gflag[gs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                done = __shfl(done, 0, 64);
+                if (done) continue;
+                const bool hit = ((ma | mb) & 1u) || wave_intersects(a.sa, ca, a.sb, cb, lane);
+                if (lane == 0 && hit) atomicOr(&a.gflag[gs], 1u);
+            }
+    }
+}
+
 // ---- BNG dense cell table (positive resolutions): BNGIndexSystem.pointToIndex
 // (BNGIndexSystem.scala:277-291, 528-541) maps a point with 0 <= toInt(e), toInt(n) < 1e7 to the id
 // of cell (toInt(e) / divisor, toInt(n) / divisor) -- one-to-one there, the two letters being the
@@ -2981,6 +3088,84 @@ int mosaic_st_contains(mosaic_ctx* c, int64_t n_geoms, const int64_t* wkb_offset
     st.release();
     if (e != hipSuccess) return fail(MOSAIC_E_HIP, std::string("st_contains: ") + hipGetErrorString(e));
     return MOSAIC_OK;
+}
+
+
+int mosaic_intersects_aggregate(mosaic_ctx* c, const mosaic_chips* left, const mosaic_chips* right,
+                                int32_t* out_left_key, int32_t* out_right_key, uint8_t* out_flag, int64_t cap,
+                                int64_t* n_out) {
+    if (!c || !left || !right || !n_out || cap < 0 || (cap > 0 && (!out_left_key || !out_right_key || !out_flag)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    if (left->grid != right->grid || left->res != right->res)
+        return fail(MOSAIC_E_ARG, "st_intersects_aggregate: both chip tables must use the same grid and resolution");
+    *n_out = 0;
+    HIP_TRY(hipSetDevice(c->device));
+    if (left->n_chips == 0 || right->n_chips == 0) return MOSAIC_OK;
+    IsectArgs a;
+    a.ta = (const HashEntry*)left->table.p;
+    a.capa = left->capacity;
+    a.meta_a = (const uint32_t*)left->meta.p;
+    a.sa = left->store.view();
+    a.tb = (const HashEntry*)right->table.p;
+    a.maskb = right->capacity - 1;
+    a.meta_b = (const uint32_t*)right->meta.p;
+    a.sb = right->store.view();
+    // pass 0: chip pairs (an upper bound on the groups) size the group hash
+    DevBuf cnt, gkey, gflag, ovf;
+    auto done = [&](int rc) {
+        for (DevBuf* b : {&cnt, &gkey, &gflag, &ovf}) b->release();
+        return rc;
+    };
+    int rc;
+    if ((rc = cnt.reserve(8)) || (rc = ovf.reserve(4))) return done(rc);
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
+    HIP_TRY(hipMemsetAsync(ovf.p, 0, 4, c->stream));
+    a.pass = 0;
+    a.pair_count = (unsigned long long*)cnt.p;
+    a.gkey = nullptr;
+    a.gflag = nullptr;
+    a.gmask = 0;
+    a.overflow = (int*)ovf.p;
+    const int64_t waves = (int64_t)left->capacity;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((waves * 64 + 255) / 256, (int64_t)c->n_cu * 16));
+    hipLaunchKernelGGL(k_isect_agg, dim3(grid), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    unsigned long long pairs = 0;
+    HIP_TRY(hipMemcpyAsync(&pairs, cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (pairs == 0) return done(MOSAIC_OK);
+    uint64_t gcap = 1024;
+    while (gcap < 2 * pairs) gcap <<= 1;
+    if ((rc = gkey.reserve(gcap * 8)) || (rc = gflag.reserve(gcap * 4))) return done(rc);
+    HIP_TRY(hipMemsetAsync(gkey.p, 0xff, gcap * 8, c->stream));
+    HIP_TRY(hipMemsetAsync(gflag.p, 0, gcap * 4, c->stream));
+    a.pass = 1;
+    a.gkey = (unsigned long long*)gkey.p;
+    a.gflag = (uint32_t*)gflag.p;
+    a.gmask = gcap - 1;
+    hipLaunchKernelGGL(k_isect_agg, dim3(grid), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    std::vector<unsigned long long> hk(gcap);
+    std::vector<uint32_t> hf(gcap);
+    int hov = 0;
+    HIP_TRY(hipMemcpyAsync(hk.data(), gkey.p, gcap * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(hf.data(), gflag.p, gcap * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&hov, ovf.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (hov) return done(fail(MOSAIC_E_CAPACITY, "st_intersects_aggregate: group table overflow"));
+    std::vector<std::pair<unsigned long long, uint8_t>> groups;
+    for (uint64_t s = 0; s < gcap; s++)
+        if (hk[s] != kEmptyGroup) groups.push_back({hk[s], (uint8_t)(hf[s] ? 1 : 0)});
+    std::sort(groups.begin(), groups.end());
+    *n_out = (int64_t)groups.size();
+    if ((int64_t)groups.size() > cap)
+        return done(fail(MOSAIC_E_CAPACITY, "st_intersects_aggregate: " + std::to_string(groups.size()) + " groups"));
+    for (size_t i = 0; i < groups.size(); i++) {
+        out_left_key[i] = (int32_t)(groups[i].first >> 32);
+        out_right_key[i] = (int32_t)(groups[i].first & 0xffffffffULL);
+        out_flag[i] = groups[i].second;
+    }
+    return done(MOSAIC_OK);
 }
 
 }  // extern "C"

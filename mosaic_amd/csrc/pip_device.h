@@ -219,5 +219,68 @@ MOSAIC_HD bool contains(const GeomStore& s, uint32_t g, double px, double py) {
     return nb > 0 || is_in;
 }
 
+
+// ---- polygonal intersects (st_intersects_aggregate's chip test) ----
+// JTS 1.19 RobustLineIntersector.computeIntersect's "is there an intersection" part for closed
+// segments p1p2, q1q2: envelope test, the four Orientation.index signs (CGAlgorithmsDD, as above),
+// and for four zero signs computeCollinearIntersection's envelope containments.
+MOSAIC_HD bool in_seg_env(Vec2 a, Vec2 b, Vec2 q) {
+    return q.x >= (a.x < b.x ? a.x : b.x) && q.x <= (a.x > b.x ? a.x : b.x) && q.y >= (a.y < b.y ? a.y : b.y) &&
+           q.y <= (a.y > b.y ? a.y : b.y);
+}
+MOSAIC_HD bool segments_intersect(Vec2 p1, Vec2 p2, Vec2 q1, Vec2 q2) {
+    // Envelope.intersects(p1, p2, q1, q2)
+    const double pminx = p1.x < p2.x ? p1.x : p2.x, pmaxx = p1.x < p2.x ? p2.x : p1.x;
+    const double qminx = q1.x < q2.x ? q1.x : q2.x, qmaxx = q1.x < q2.x ? q2.x : q1.x;
+    if (qminx > pmaxx || qmaxx < pminx) return false;
+    const double pminy = p1.y < p2.y ? p1.y : p2.y, pmaxy = p1.y < p2.y ? p2.y : p1.y;
+    const double qminy = q1.y < q2.y ? q1.y : q2.y, qmaxy = q1.y < q2.y ? q2.y : q1.y;
+    if (qminy > pmaxy || qmaxy < pminy) return false;
+    const int pq1 = orientation_index(p1.x, p1.y, p2.x, p2.y, q1.x, q1.y);
+    const int pq2 = orientation_index(p1.x, p1.y, p2.x, p2.y, q2.x, q2.y);
+    if ((pq1 > 0 && pq2 > 0) || (pq1 < 0 && pq2 < 0)) return false;
+    const int qp1 = orientation_index(q1.x, q1.y, q2.x, q2.y, p1.x, p1.y);
+    const int qp2 = orientation_index(q1.x, q1.y, q2.x, q2.y, p2.x, p2.y);
+    if ((qp1 > 0 && qp2 > 0) || (qp1 < 0 && qp2 < 0)) return false;
+    if (pq1 == 0 && pq2 == 0 && qp1 == 0 && qp2 == 0)
+        return in_seg_env(p1, p2, q1) || in_seg_env(p1, p2, q2) || in_seg_env(q1, q2, p1) || in_seg_env(q1, q2, p2);
+    return true;
+}
+MOSAIC_HD bool boxes_meet(const Box& a, const Box& b) {
+    return !(a.maxx < b.minx || b.maxx < a.minx || a.maxy < b.miny || b.maxy < a.miny);
+}
+// Some vertex of geometry g (the first vertex of each polygon's shell) lies in the interior or on
+// the boundary of geometry h.  Once no boundary segments of g and h meet, every polygon of g lies
+// wholly inside or wholly outside h (and vice versa), so this decides the rest of intersects.
+MOSAIC_HD bool shell_vertex_in(const GeomStore& sg, uint32_t g, const GeomStore& sh, uint32_t h) {
+    for (uint32_t p = sg.geom_part[g]; p < sg.geom_part[g + 1]; p++) {
+        const uint32_t r0 = sg.part_ring[p];
+        if (sg.part_ring[p + 1] <= r0 || sg.ring_start[r0 + 1] <= sg.ring_start[r0]) continue;
+        const Vec2 v = sg.verts[sg.ring_start[r0]];
+        if (box_excludes(sh.geom_bbox[h], v.x, v.y)) continue;
+        for (uint32_t q = sh.geom_part[h]; q < sh.geom_part[h + 1]; q++)
+            if (locate_in_polygon(sh, q, v.x, v.y) != LOC_EXTERIOR) return true;
+    }
+    return false;
+}
+// Geometry.intersects of two polygonal geometries (JTS 1.19 Geometry.intersects -> RelateOp
+// isIntersects: the closed point sets share a point), one thread.
+MOSAIC_HD bool intersects(const GeomStore& sa, uint32_t a, const GeomStore& sb, uint32_t b) {
+    if (sa.geom_part[a + 1] <= sa.geom_part[a] || sb.geom_part[b + 1] <= sb.geom_part[b]) return false;
+    if (!boxes_meet(sa.geom_bbox[a], sb.geom_bbox[b])) return false;
+    const uint32_t ra0 = sa.part_ring[sa.geom_part[a]], ra1 = sa.part_ring[sa.geom_part[a + 1]];
+    const uint32_t rb0 = sb.part_ring[sb.geom_part[b]], rb1 = sb.part_ring[sb.geom_part[b + 1]];
+    for (uint32_t ra = ra0; ra < ra1; ra++) {
+        if (!boxes_meet(sa.ring_bbox[ra], sb.geom_bbox[b])) continue;
+        for (uint32_t rb = rb0; rb < rb1; rb++) {
+            if (!boxes_meet(sa.ring_bbox[ra], sb.ring_bbox[rb])) continue;
+            for (uint32_t i = sa.ring_start[ra]; i + 1 < sa.ring_start[ra + 1]; i++)
+                for (uint32_t j = sb.ring_start[rb]; j + 1 < sb.ring_start[rb + 1]; j++)
+                    if (segments_intersect(sa.verts[i], sa.verts[i + 1], sb.verts[j], sb.verts[j + 1])) return true;
+        }
+    }
+    return shell_vertex_in(sb, b, sa, a) || shell_vertex_in(sa, a, sb, b);
+}
+
 }  // namespace pip
 }  // namespace mosaic

@@ -53,6 +53,10 @@ def lib():
         L.oracle_pip_join.argtypes = [vp, i32, i32, i32, vp, vp, i64, vp, i64, vp, vp, i64, i32]
         L.oracle_brute_force_count.restype = i64
         L.oracle_brute_force_count.argtypes = [vp, vp, vp, i64, vp, i64]
+        L.oracle_segments_intersect.restype = i32
+        L.oracle_segments_intersect.argtypes = [f64] * 8
+        L.oracle_wkb_intersects.restype = i32
+        L.oracle_wkb_intersects.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64]
         _lib = L
     return _lib
 
@@ -124,6 +128,41 @@ def wkb_contains(wkb: bytes, x, y):
     if r < 0:
         raise ValueError("unparseable WKB")
     return bool(r)
+
+
+def segments_intersect(p1, p2, q1, q2):
+    return bool(lib().oracle_segments_intersect(p1[0], p1[1], p2[0], p2[1], q1[0], q1[1], q2[0], q2[1]))
+
+
+def wkb_intersects(wa: bytes, wb: bytes):
+    r = lib().oracle_wkb_intersects(wa, len(wa), wb, len(wb))
+    if r < 0:
+        raise ValueError("unparseable WKB")
+    return bool(r)
+
+
+def intersects_aggregate(left, right):
+    """Reference semantics of left.join(right, index_id).groupBy(left key, right key)
+    .agg(st_intersects_aggregate) (ST_IntersectsAggregate.scala:28-39) over two chip dicts
+    (index_id, is_core, polygon_key, wkb=(offsets, data)): {(left key, right key): flag}."""
+    from collections import defaultdict
+
+    by_cell = defaultdict(list)
+    lo, ld = left["wkb"]
+    for i, c in enumerate(left["index_id"]):
+        by_cell[int(c)].append(i)
+    ro, rd = right["wkb"]
+    out = {}
+    for j, c in enumerate(right["index_id"]):
+        for i in by_cell.get(int(c), ()):
+            g = (int(left["polygon_key"][i]), int(right["polygon_key"][j]))
+            if out.get(g):
+                continue
+            hit = bool(left["is_core"][i]) or bool(right["is_core"][j])
+            if not hit:
+                hit = wkb_intersects(bytes(ld[lo[i]:lo[i + 1]]), bytes(rd[ro[j]:ro[j + 1]]))
+            out[g] = out.get(g, False) or hit
+    return out
 
 
 class _Chips(ctypes.Structure):

@@ -86,3 +86,18 @@ def contains(parts, p):
     if nb % 2 == 1:
         return False
     return nb > 0 or is_in
+
+
+def segments_intersect(p1, p2, q1, q2):
+    """Closed segments p1p2 and q1q2 share a point, in exact rational arithmetic (the predicate
+    JTS RobustLineIntersector.computeIntersect decides with Orientation.index signs)."""
+    o1, o2 = orientation(p1, p2, q1), orientation(p1, p2, q2)
+    o3, o4 = orientation(q1, q2, p1), orientation(q1, q2, p2)
+    if o1 * o2 < 0 and o3 * o4 < 0:
+        return True
+
+    def on(a, b, c):  # c collinear with ab: on the closed segment?
+        return min(a[0], b[0]) <= c[0] <= max(a[0], b[0]) and min(a[1], b[1]) <= c[1] <= max(a[1], b[1])
+
+    return ((o1 == 0 and on(p1, p2, q1)) or (o2 == 0 and on(p1, p2, q2)) or (o3 == 0 and on(q1, q2, p1))
+            or (o4 == 0 and on(q1, q2, p2)))

@@ -69,6 +69,13 @@ int oracle_wkb_contains(const uint8_t* wkb, int64_t len, double px, double py);
 void* oracle_wkb_parse(const uint8_t* wkb, int64_t len);
 int oracle_parsed_contains(const void* parsed, double px, double py);
 void oracle_parsed_free(void* parsed);
+/* JTS RobustLineIntersector: closed segments p1p2 and q1q2 share a point (1) or not (0). */
+int oracle_segments_intersect(double p1x, double p1y, double p2x, double p2y, double q1x, double q1y, double q2x,
+                              double q2y);
+/* JTS Geometry.intersects of two polygonal geometries (closed point sets share a point). */
+int oracle_intersects(const oracle_geom* a, const oracle_geom* b);
+/* The same from two WKBs; -1 on parse error. */
+int oracle_wkb_intersects(const uint8_t* wa, int64_t la, const uint8_t* wb, int64_t lb);
 
 /* ---- chip join ---- */
 typedef struct {

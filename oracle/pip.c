@@ -378,3 +378,91 @@ int oracle_wkb_contains(const uint8_t* wkb, int64_t len, double px, double py) {
     oracle_parsed_free(p);
     return r;
 }
+
+/* ---- JTS 1.19 Geometry.intersects for two polygonal geometries (st_intersects_aggregate) ----
+ * Reached from ST_IntersectsAggregate.update (expressions/geometry/ST_IntersectsAggregate.scala:28-39)
+ * -> MosaicGeometryJTS.intersects -> Geometry.intersects: envelope pre-check, then
+ * RelateOp(...).isIntersects(), i.e. the closed point sets share a point.  Restated as:
+ *   (1) some boundary segment of a meets some boundary segment of b, decided as
+ *       RobustLineIntersector.computeIntersect does: Envelope.intersects(p1, p2, q1, q2), the four
+ *       Orientation.index (CGAlgorithmsDD) signs, and for four zero signs
+ *       computeCollinearIntersection's Envelope.intersects(p1, p2, q) containments;
+ *   (2) otherwise the boundaries are disjoint, so each polygon of one geometry lies wholly inside or
+ *       outside the other: the first shell vertex of each polygon of b located in a (PointLocator,
+ *       INTERIOR or BOUNDARY), and of a in b. */
+static int in_seg_env(double ax, double ay, double bx, double by, double qx, double qy) {
+    return qx >= fmin(ax, bx) && qx <= fmax(ax, bx) && qy >= fmin(ay, by) && qy <= fmax(ay, by);
+}
+
+int oracle_segments_intersect(double p1x, double p1y, double p2x, double p2y, double q1x, double q1y, double q2x,
+                              double q2y) {
+    if (fmin(q1x, q2x) > fmax(p1x, p2x) || fmax(q1x, q2x) < fmin(p1x, p2x)) return 0;
+    if (fmin(q1y, q2y) > fmax(p1y, p2y) || fmax(q1y, q2y) < fmin(p1y, p2y)) return 0;
+    int pq1 = oracle_orientation_index(p1x, p1y, p2x, p2y, q1x, q1y);
+    int pq2 = oracle_orientation_index(p1x, p1y, p2x, p2y, q2x, q2y);
+    if ((pq1 > 0 && pq2 > 0) || (pq1 < 0 && pq2 < 0)) return 0;
+    int qp1 = oracle_orientation_index(q1x, q1y, q2x, q2y, p1x, p1y);
+    int qp2 = oracle_orientation_index(q1x, q1y, q2x, q2y, p2x, p2y);
+    if ((qp1 > 0 && qp2 > 0) || (qp1 < 0 && qp2 < 0)) return 0;
+    if (pq1 == 0 && pq2 == 0 && qp1 == 0 && qp2 == 0)
+        return in_seg_env(p1x, p1y, p2x, p2y, q1x, q1y) || in_seg_env(p1x, p1y, p2x, p2y, q2x, q2y) ||
+               in_seg_env(q1x, q1y, q2x, q2y, p1x, p1y) || in_seg_env(q1x, q1y, q2x, q2y, p2x, p2y);
+    return 1;
+}
+
+static void geom_env(const oracle_geom* g, double* e) {
+    e[0] = e[1] = INFINITY;
+    e[2] = e[3] = -INFINITY;
+    int64_t v0 = g->ring_offsets[g->part_rings[0]], v1 = g->ring_offsets[g->part_rings[g->n_parts]];
+    for (int64_t i = v0; i < v1; i++) {
+        e[0] = fmin(e[0], g->xy[2 * i]);
+        e[1] = fmin(e[1], g->xy[2 * i + 1]);
+        e[2] = fmax(e[2], g->xy[2 * i]);
+        e[3] = fmax(e[3], g->xy[2 * i + 1]);
+    }
+}
+
+static int shell_vertex_in(const oracle_geom* g, const oracle_geom* h) {
+    for (int64_t p = 0; p < g->n_parts; p++) {
+        int64_t r0 = g->part_rings[p];
+        if (g->part_rings[p + 1] <= r0 || g->ring_offsets[r0 + 1] <= g->ring_offsets[r0]) continue;
+        double x = g->xy[2 * g->ring_offsets[r0]], y = g->xy[2 * g->ring_offsets[r0] + 1];
+        for (int64_t q = 0; q < h->n_parts; q++)
+            if (locate_in_polygon(h, q, x, y) != LOC_EXTERIOR) return 1;
+    }
+    return 0;
+}
+
+int oracle_intersects(const oracle_geom* a, const oracle_geom* b) {
+    if (a->n_parts == 0 || b->n_parts == 0) return 0;
+    double ea[4], eb[4];
+    geom_env(a, ea);
+    geom_env(b, eb);
+    if (!(ea[0] <= ea[2]) || !(eb[0] <= eb[2])) return 0; /* empty */
+    if (ea[2] < eb[0] || eb[2] < ea[0] || ea[3] < eb[1] || eb[3] < ea[1]) return 0;
+    int64_t ra1 = a->part_rings[a->n_parts], rb1 = b->part_rings[b->n_parts];
+    for (int64_t ra = a->part_rings[0]; ra < ra1; ra++)
+        for (int64_t rb = b->part_rings[0]; rb < rb1; rb++)
+            for (int64_t i = a->ring_offsets[ra]; i + 1 < a->ring_offsets[ra + 1]; i++)
+                for (int64_t j = b->ring_offsets[rb]; j + 1 < b->ring_offsets[rb + 1]; j++)
+                    if (oracle_segments_intersect(a->xy[2 * i], a->xy[2 * i + 1], a->xy[2 * i + 2], a->xy[2 * i + 3],
+                                                  b->xy[2 * j], b->xy[2 * j + 1], b->xy[2 * j + 2], b->xy[2 * j + 3]))
+                        return 1;
+    return shell_vertex_in(b, a) || shell_vertex_in(a, b);
+}
+
+int oracle_wkb_intersects(const uint8_t* wa, int64_t la, const uint8_t* wb, int64_t lb) {
+    void* pa = oracle_wkb_parse(wa, la);
+    if (!pa) return -1;
+    void* pb = oracle_wkb_parse(wb, lb);
+    if (!pb) {
+        oracle_parsed_free(pa);
+        return -1;
+    }
+    const parsed_geom* ga = (const parsed_geom*)pa;
+    const parsed_geom* gb = (const parsed_geom*)pb;
+    int r = (ga->b.xy && gb->b.xy) ? oracle_intersects(&ga->g, &gb->g) : 0;
+    oracle_parsed_free(pa);
+    oracle_parsed_free(pb);
+    return r;
+}

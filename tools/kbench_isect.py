@@ -1,0 +1,40 @@
+"""Timing of st_intersects_aggregate (mosaic_intersects_aggregate) on the GPU box: the 263 NYC
+zones chipped at H3 res 9 (and the 35-zone set at res 10) joined with a translated copy.  Prints one
+JSON line per case (groups, true groups, chip pairs tested, ms for the whole call incl. D2H)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from mosaic_amd import MosaicContext
+    from mosaic_amd.context import tessellate
+    from mosaic_amd.data import PolygonSet
+
+    ctx = MosaicContext.build("H3")
+    for name, res, shift in (("nyc_taxi_zones", 9, (0.0007, -0.0011)), ("nyc_taxi_zones", 10, (0.0007, -0.0011)),
+                             ("nyc_taxi_zones", 9, (0.0, 0.0))):
+        z = PolygonSet.load(name)
+        m = PolygonSet(z.xy + np.array(shift), z.ring_offsets, z.part_rings, z.geom_parts, z.names)
+        l, r = tessellate("H3", z, res), tessellate("H3", m, res)
+        tl = ctx.chip_table(l["is_core"], l["index_id"], l["wkb"], l["polygon_key"], res)
+        tr = ctx.chip_table(r["is_core"], r["index_id"], r["wkb"], r["polygon_key"], res)
+        ctx.st_intersects_aggregate(tl, tr)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            lk, rk, fl = ctx.st_intersects_aggregate(tl, tr)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        print(json.dumps({"case": f"{name} res {res} shift {shift}", "chips": [len(l["index_id"]), len(r["index_id"])],
+                          "groups": int(len(fl)), "true": int(fl.sum()), "ms_median": float(np.median(ts))}))
+        tl.close()
+        tr.close()
+
+
+if __name__ == "__main__":
+    main()
