@@ -214,6 +214,17 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
                                 int32_t* out_left_key, int32_t* out_right_key, uint8_t* out_flag, int64_t cap,
                                 int64_t* n_out);
 
+/* ---- grid_cellkring / grid_cellkloop over a cell column (BNG) ---- */
+/* loop = 0: kRing(cell, k) = the cell, then the loops 1..k; loop = 1: kLoop(cell, k).  Row i's
+ * cells go to out[i * stride ..] with stride = 8k (loop) or 1 + 4k(k + 1) (ring), in the
+ * reference's order (bottom, right, top, left; cells failing isValid dropped), and
+ * out_count[i] = their number (-1 for null rows, valid[i] == 0).  0 <= k <= 1000.  H3 is not
+ * implemented (MOSAIC_E_ARG).  Reference: BNGIndexSystem.kRing / kLoop / isValid
+ * (core/index/BNGIndexSystem.scala:216-263), grid_cellkring / grid_cellkloop
+ * (functions/MosaicContext.scala). */
+int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k,
+                      int loop, int64_t* out, int32_t* out_count);
+
 #ifdef __cplusplus
 }
 #endif

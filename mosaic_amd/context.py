@@ -458,6 +458,31 @@ class MosaicContext:
             return rows[:k][order], keys[:k][order]
 
 
+    def _kring(self, cells, k, loop, raw):
+        strings = len(cells) and isinstance(cells[0], str)
+        ids = np.array([self.index_system.parse(c) for c in cells] if strings else cells, np.int64)
+        valid = None
+        n = len(ids)
+        stride = 8 * k if loop else 1 + 4 * k * (k + 1)
+        out = np.zeros(max(n * stride, 1), np.int64)
+        cnt = np.zeros(max(n, 1), np.int32)
+        N.check(N.lib().mosaic_cell_kring(self.handle, self.index_system.grid, N.ptr(ids), valid, n, int(k),
+                                          int(loop), N.ptr(out), N.ptr(cnt)))
+        rows = [out[i * stride:i * stride + cnt[i]] for i in range(n)]
+        if raw or self.index_system.cell_id_type != "string":
+            return rows
+        return [[self.index_system.format(c) for c in r] for r in rows]
+
+    def grid_cellkring(self, cells, k, raw=False):
+        """grid_cellkring(cellId, k) (MosaicContext.scala:692-693 -> CellKRing.nullSafeEval ->
+        IndexSystem.kRing; BNG: BNGIndexSystem.scala:216-222): per row the cell and its loops 1..k."""
+        return self._kring(cells, k, False, raw)
+
+    def grid_cellkloop(self, cells, k, raw=False):
+        """grid_cellkloop(cellId, k) (MosaicContext.scala:696-697 -> CellKLoop -> IndexSystem.kLoop;
+        BNG: BNGIndexSystem.scala:234-246): per row the valid cells at distance k."""
+        return self._kring(cells, k, True, raw)
+
     def st_intersects_aggregate(self, left, right):
         """left.join(right, left_index.index_id == right_index.index_id).groupBy(left_key, right_key)
         .agg(st_intersects_aggregate(left_index, right_index)) over two chip tables

@@ -82,5 +82,121 @@ MOSAIC_HD bool point_to_index(double eastings, double northings, int res, int64_
     return true;
 }
 
+
+// ---- k-loops / k-rings: BNGIndexSystem.kLoop / kRing (BNGIndexSystem.scala:216-246) with the
+// cell decoding they use: indexDigits (index.toString digits), getResolution(digits), getEdgeSize
+// (sizeMap), getX / getY, isValid (BNGIndexSystem.scala:248-263).  Int arithmetic as in Scala.
+
+// decimal digits of a positive id, most significant first; returns their count (0 for id <= 0,
+// whose toString the reference would not decode)
+MOSAIC_HD int index_digits(int64_t id, int* d) {
+    if (id <= 0) return 0;
+    int t[20], n = 0;
+    while (id > 0) {
+        t[n++] = (int)(id % 10);
+        id /= 10;
+    }
+    for (int i = 0; i < n; i++) d[i] = t[n - 1 - i];
+    return n;
+}
+MOSAIC_HD int digits_resolution(const int* d, int n) {
+    if (n < 6) return -1;  // 500km
+    const int k = (n - 6) / 2;
+    return d[n - 1] > 0 ? -(k + 2) : k + 1;
+}
+// sizeMap(getResolutionStr(res)); 0 where the reference's map lookup throws
+MOSAIC_HD int32_t edge_size(int res) {
+    switch (res) {
+        case -1: return 500000;
+        case 1: return 100000;
+        case -2: return 50000;
+        case 2: return 10000;
+        case -3: return 5000;
+        case 3: return 1000;
+        case -4: return 500;
+        case 4: return 100;
+        case -5: return 50;
+        case 5: return 10;
+        case -6: return 5;
+        case 6: return 1;
+        default: return 0;
+    }
+}
+// getX (y = 0) / getY (y = 1): the letter digits then k coordinate digits, as one Int, times the
+// (quadrant-adjusted) edge size, plus the quadrant's offset
+MOSAIC_HD int32_t digits_coord(const int* d, int n, int32_t edge, int y) {
+    const int k = (n - 6) / 2;  // JVM Int division: truncates toward zero (0 for n = 5)
+    const int a = y ? 3 : 1, b = y ? 5 + k : 5;
+    int32_t v = 0;
+    for (int i = a; i < a + 2 && i < n; i++) v = v * 10 + d[i];  // at most 2 + 6 digits: no overflow
+    for (int i = b; i < b + k && i < n; i++) v = v * 10 + d[i];
+    const int q = d[n - 1];
+    const int32_t adj = q > 0 ? 2 * edge : edge;
+    const int32_t off = y ? ((q == 2 || q == 3) ? edge : 0) : ((q == 3 || q == 4) ? edge : 0);
+    return (int32_t)((uint32_t)v * (uint32_t)adj + (uint32_t)off);  // Int * and + wrap
+}
+// cell -> (resolution, edge size, x, y); false if the reference could not decode it
+MOSAIC_HD bool cell_origin(int64_t id, int* res, int32_t* edge, int32_t* x, int32_t* y) {
+    int d[20];
+    const int n = index_digits(id, d);
+    if (n < 4) return false;  // the reference's digit slices would be empty (NumberFormatException)
+    *res = digits_resolution(d, n);
+    *edge = edge_size(*res);
+    if (*edge == 0) return false;
+    *x = digits_coord(d, n, *edge, 0);
+    *y = digits_coord(d, n, *edge, 1);
+    return true;
+}
+MOSAIC_HD bool is_valid(int64_t id) {
+    int res;
+    int32_t e, x, y;
+    if (!cell_origin(id, &res, &e, &x, &y)) return false;
+    return x >= 0 && x <= 700000 && y >= 0 && y <= 1300000;
+}
+// kLoop(id, k): the 8k cells of the square loop at distance k, bottom, right, top, left, each
+// side from its first corner, keeping the isValid ones (order kept).  Returns the count, or -1 if
+// the id cannot be decoded.
+MOSAIC_HD int kloop(int64_t id, int k, int64_t* out) {
+    int res;
+    int32_t e, x, y;
+    if (!cell_origin(id, &res, &e, &x, &y)) return -1;
+    int m = 0;
+    for (int side = 0; side < 4; side++)
+        for (int c = 0; c < 2 * k; c++) {
+            // Int arithmetic, wrapping as the JVM's does (exact in int64 for |k| < 2^20, then
+            // truncated to 32 bits)
+            const int64_t X = x, Y = y, E = e, K = k, C = c;
+            int64_t qx, qy;
+            if (side == 0) {
+                qx = X + (C - K) * E;
+                qy = Y - K * E;
+            } else if (side == 1) {
+                qx = X + K * E;
+                qy = Y + (C - K) * E;
+            } else if (side == 2) {
+                qx = X + (K - C) * E;
+                qy = Y + K * E;
+            } else {
+                qx = X - K * E;
+                qy = Y + (K - C) * E;
+            }
+            const int32_t px = (int32_t)(uint32_t)(uint64_t)qx, py = (int32_t)(uint32_t)(uint64_t)qy;
+            int64_t cell = 0;
+            point_to_index((double)px, (double)py, res, &cell);
+            if (is_valid(cell)) out[m++] = cell;
+        }
+    return m;
+}
+// kRing(id, n) = id, then kLoop(id, 1 .. n)
+MOSAIC_HD int kring(int64_t id, int n, int64_t* out) {
+    int res;
+    int32_t e, x, y;
+    if (!cell_origin(id, &res, &e, &x, &y)) return -1;
+    int m = 0;
+    out[m++] = id;
+    for (int k = 1; k <= n; k++) m += kloop(id, k, out + m);
+    return m;
+}
+
 }  // namespace bng
 }  // namespace mosaic

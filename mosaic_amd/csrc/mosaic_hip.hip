@@ -1143,6 +1143,36 @@ __global__ void __launch_bounds__(256) k_isect_agg(IsectArgs a) {
     }
 }
 
+
+// ---- grid_cellkring / grid_cellkloop over a BNG cell column (BNGIndexSystem.kRing / kLoop,
+// BNGIndexSystem.scala:216-246): one lane per row writes its cells to a fixed-stride slot
+// (8k for a loop, 1 + 4k(k + 1) for a ring) and the count; null rows get count -1 (NullIntolerant).
+struct KringArgs {
+    const int64_t* cells;
+    const uint8_t* valid;
+    int64_t n;
+    int k, loop;
+    int64_t stride;
+    int64_t* out;
+    int32_t* count;
+    unsigned int* flags;  // bit 0: an id the reference cannot decode
+};
+__global__ void __launch_bounds__(256) k_bng_kring(KringArgs a) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+        if (a.valid && !a.valid[i]) {
+            a.count[i] = -1;
+            continue;
+        }
+        int64_t* o = a.out + i * a.stride;
+        const int m = a.loop ? bng::kloop(a.cells[i], a.k, o) : bng::kring(a.cells[i], a.k, o);
+        if (m < 0) bad = true;
+        a.count[i] = m < 0 ? 0 : m;
+    }
+    if (bad) atomicOr(a.flags, 1u);
+}
+
 // ---- BNG dense cell table (positive resolutions): BNGIndexSystem.pointToIndex
 // (BNGIndexSystem.scala:277-291, 528-541) maps a point with 0 <= toInt(e), toInt(n) < 1e7 to the id
 // of cell (toInt(e) / divisor, toInt(n) / divisor) -- one-to-one there, the two letters being the
@@ -3165,6 +3195,53 @@ int mosaic_intersects_aggregate(mosaic_ctx* c, const mosaic_chips* left, const m
         out_right_key[i] = (int32_t)(groups[i].first & 0xffffffffULL);
         out_flag[i] = groups[i].second;
     }
+    return done(MOSAIC_OK);
+}
+
+
+int mosaic_cell_kring(mosaic_ctx* c, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k, int loop,
+                      int64_t* out, int32_t* out_count) {
+    if (!c || n < 0 || (n > 0 && (!cells || !out || !out_count))) return fail(MOSAIC_E_ARG, "invalid argument");
+    if (grid != MOSAIC_GRID_BNG)
+        return fail(MOSAIC_E_ARG, "grid_cellkring / grid_cellkloop: only the BNG grid is implemented by this engine");
+    if (k < 0 || k > 1000) return fail(MOSAIC_E_ARG, "k must be in [0, 1000]");
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t stride = loop ? 8 * (int64_t)k : 1 + 4 * (int64_t)k * (k + 1);
+    const int64_t slots = stride * n;  // 0 for a k = 0 loop: nothing to copy back
+    DevBuf s_cells, s_valid, s_out, s_cnt, s_flags;
+    auto done = [&](int rc) {
+        for (DevBuf* b : {&s_cells, &s_valid, &s_out, &s_cnt, &s_flags}) b->release();
+        return rc;
+    };
+    int rc;
+    const void *dc, *dv;
+    if ((rc = to_device(c, s_cells, cells, (size_t)n * 8, &dc)) || (rc = to_device(c, s_valid, valid, (size_t)n, &dv)))
+        return done(rc);
+    const bool dev_out = is_device_ptr(out), dev_cnt = is_device_ptr(out_count);
+    if ((!dev_out && (rc = s_out.reserve(std::max<size_t>((size_t)slots * 8, 16)))) || (!dev_cnt && (rc = s_cnt.reserve((size_t)n * 4))) ||
+        (rc = s_flags.reserve(4)))
+        return done(rc);
+    HIP_TRY(hipMemsetAsync(s_flags.p, 0, 4, c->stream));
+    KringArgs a;
+    a.cells = (const int64_t*)dc;
+    a.valid = (const uint8_t*)dv;
+    a.n = n;
+    a.k = k;
+    a.loop = loop ? 1 : 0;
+    a.stride = stride;
+    a.out = dev_out ? out : (int64_t*)s_out.p;
+    a.count = dev_cnt ? out_count : (int32_t*)s_cnt.p;
+    a.flags = (unsigned int*)s_flags.p;
+    hipLaunchKernelGGL(k_bng_kring, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    unsigned int flags = 0;
+    HIP_TRY(hipMemcpyAsync(&flags, s_flags.p, 4, hipMemcpyDeviceToHost, c->stream));
+    if (!dev_out && slots > 0)
+        HIP_TRY(hipMemcpyAsync(out, s_out.p, (size_t)slots * 8, hipMemcpyDeviceToHost, c->stream));
+    if (!dev_cnt) HIP_TRY(hipMemcpyAsync(out_count, s_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (flags & 1u) return done(fail(MOSAIC_E_ARG, "invalid BNG cell id"));
     return done(MOSAIC_OK);
 }
 

@@ -57,6 +57,11 @@ def lib():
         L.oracle_segments_intersect.argtypes = [f64] * 8
         L.oracle_wkb_intersects.restype = i32
         L.oracle_wkb_intersects.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64]
+        for fn in ("oracle_bng_kloop", "oracle_bng_kring"):
+            getattr(L, fn).restype = i32
+            getattr(L, fn).argtypes = [i64, i32, vp]
+        L.oracle_bng_is_valid.restype = i32
+        L.oracle_bng_is_valid.argtypes = [i64]
         _lib = L
     return _lib
 
@@ -128,6 +133,26 @@ def wkb_contains(wkb: bytes, x, y):
     if r < 0:
         raise ValueError("unparseable WKB")
     return bool(r)
+
+
+def bng_kloop(cell, k):
+    out = np.zeros(max(8 * k, 1), np.int64)
+    m = lib().oracle_bng_kloop(int(cell), int(k), _ptr(out))
+    if m < 0:
+        raise ValueError("undecodable BNG id")
+    return out[:m]
+
+
+def bng_kring(cell, k):
+    out = np.zeros(1 + 4 * k * (k + 1), np.int64)
+    m = lib().oracle_bng_kring(int(cell), int(k), _ptr(out))
+    if m < 0:
+        raise ValueError("undecodable BNG id")
+    return out[:m]
+
+
+def bng_is_valid(cell):
+    return bool(lib().oracle_bng_is_valid(int(cell)))
 
 
 def segments_intersect(p1, p2, q1, q2):

@@ -12,6 +12,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "oracle.h"
@@ -159,4 +160,85 @@ int oracle_bng_format(int64_t id, char* buf, int cap) {
     if (o + 1 > cap) return -1;
     memcpy(buf, out, o + 1);
     return o;
+}
+
+/* ---- BNGIndexSystem.kLoop / kRing / isValid (BNGIndexSystem.scala:216-263) ----
+ * The id's decimal string (indexDigits), getResolution(digits), sizeMap, getX / getY (Int
+ * arithmetic, wrapping), then pointToIndex of the loop's cell origins filtered by isValid. */
+static int bng_digits(int64_t id, int* d) {
+    char buf[32];
+    if (id <= 0) return 0;
+    int n = snprintf(buf, sizeof buf, "%lld", (long long)id);
+    for (int i = 0; i < n; i++) d[i] = buf[i] - '0';
+    return n;
+}
+
+/* (slice(a0, a1) ++ slice(b0, b1)).mkString.toInt of the digit sequence (at most 8 digits here) */
+static int32_t bng_slices_int(const int* d, int n, int a0, int a1, int b0, int b1) {
+    char s[40];
+    int m = 0;
+    for (int i = a0; i < a1 && i < n; i++) s[m++] = (char)('0' + d[i]);
+    for (int i = b0; i < b1 && i < n; i++) s[m++] = (char)('0' + d[i]);
+    s[m] = 0;
+    return (int32_t)strtol(s, NULL, 10);
+}
+
+/* 0 if the reference cannot decode the id */
+static int bng_origin(int64_t id, int* res, int32_t* edge, int32_t* x, int32_t* y) {
+    static const int sizes_pos[7] = {0, 100000, 10000, 1000, 100, 10, 1};
+    static const int sizes_neg[7] = {0, 500000, 50000, 5000, 500, 50, 5};
+    int d[32];
+    int n = bng_digits(id, d);
+    if (n < 4) return 0;
+    int q = d[n - 1];
+    int k = (n - 6) / 2; /* C and JVM Int division both truncate toward zero */
+    *res = n < 6 ? -1 : (q > 0 ? -(k + 2) : k + 1);
+    if (*res < -6 || *res > 6 || *res == 0) return 0;
+    *edge = *res > 0 ? sizes_pos[*res] : sizes_neg[-*res];
+    uint32_t adj = (uint32_t)(q > 0 ? 2 * *edge : *edge);
+    int32_t xd = bng_slices_int(d, n, 1, 3, 5, 5 + k), yd = bng_slices_int(d, n, 3, 5, 5 + k, 5 + 2 * k);
+    *x = (int32_t)((uint32_t)xd * adj + (uint32_t)((q == 3 || q == 4) ? *edge : 0));
+    *y = (int32_t)((uint32_t)yd * adj + (uint32_t)((q == 2 || q == 3) ? *edge : 0));
+    return 1;
+}
+
+int oracle_bng_is_valid(int64_t id) {
+    int res;
+    int32_t e, x, y;
+    if (!bng_origin(id, &res, &e, &x, &y)) return 0;
+    return x >= 0 && x <= 700000 && y >= 0 && y <= 1300000;
+}
+
+int oracle_bng_kloop(int64_t id, int k, int64_t* out) {
+    int res;
+    int32_t e, x, y;
+    if (!bng_origin(id, &res, &e, &x, &y)) return -1;
+    int m = 0;
+    /* bottom, right, top, left (BNGIndexSystem.scala:238-241) */
+    for (int side = 0; side < 4; side++) {
+        for (int c = 0; c < 2 * k; c++) {
+            uint32_t ux = (uint32_t)x, uy = (uint32_t)y, ue = (uint32_t)e, uk = (uint32_t)k, uc = (uint32_t)c;
+            uint32_t qx, qy;
+            switch (side) {
+                case 0: qx = ux + (uc - uk) * ue; qy = uy - uk * ue; break;
+                case 1: qx = ux + uk * ue; qy = uy + (uc - uk) * ue; break;
+                case 2: qx = ux + (uk - uc) * ue; qy = uy + uk * ue; break;
+                default: qx = ux - uk * ue; qy = uy + (uk - uc) * ue; break;
+            }
+            int err = 0;
+            int64_t cell = oracle_bng_point_to_index((double)(int32_t)qx, (double)(int32_t)qy, res, &err);
+            if (oracle_bng_is_valid(cell)) out[m++] = cell;
+        }
+    }
+    return m;
+}
+
+int oracle_bng_kring(int64_t id, int n, int64_t* out) {
+    int res;
+    int32_t e, x, y;
+    if (!bng_origin(id, &res, &e, &x, &y)) return -1;
+    int m = 0;
+    out[m++] = id;
+    for (int k = 1; k <= n; k++) m += oracle_bng_kloop(id, k, out + m);
+    return m;
 }

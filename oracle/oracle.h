@@ -50,6 +50,11 @@ void oracle_bng_point_to_index_batch(const double* e, const double* n, int64_t c
                                      int64_t* out, uint8_t* err);
 /* BNGIndexSystem.format: writes a NUL-terminated string; returns its length or -1. */
 int oracle_bng_format(int64_t id, char* buf, int cap);
+/* BNGIndexSystem.isValid / kLoop / kRing: cell count written to out (<= 8k / 1 + 4k(k+1)), -1 if
+ * the id cannot be decoded. */
+int oracle_bng_is_valid(int64_t id);
+int oracle_bng_kloop(int64_t id, int k, int64_t* out);
+int oracle_bng_kring(int64_t id, int n, int64_t* out);
 
 /* ---- JTS contains ---- */
 /* Geometry described as rings: ring_offsets[r]..ring_offsets[r+1] index into xy (pairs);
