@@ -92,6 +92,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of 64, default 512; the LDS
  * quad level is held once per workgroup), "stream_persistent" (0/1: k_join_stream launches only the workgroups that
  * are resident at once; default 0: blocks_per_cu x block threads per CU, measured faster),
+ * "host_chunk" (rows per chunk when mosaic_pip_join_count gets host-resident coordinates: the next
+ * chunk's copy overlaps the current chunk's join; 0 = stage the whole batch; default 2^25),
  * "tile_lds" (0/1: k_join_stream copies the raster's per-tile leaf-block bases to
  * LDS when the workgroup's LDS stays within 80 KiB), "stream_groups" (1/2), "mixed_rows" (1/2/4), "mixed_blocks_per_cu". */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);

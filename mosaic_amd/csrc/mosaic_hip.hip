@@ -1723,6 +1723,11 @@ struct mosaic_ctx {
     int probe_mask = 0;     // measurement only: see JoinArgs::probe_mask (results are wrong when set)
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
+    // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
+    // copy on copy_stream overlapping the current chunk's join (0: stage the whole batch first)
+    int64_t host_chunk = (int64_t)1 << 25;
+    hipStream_t copy_stream = nullptr;
+    DevBuf hx[2], hy[2], hcounts;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
     // option "timing": HIP events bracket each fused join kernel on the context stream
@@ -1904,8 +1909,10 @@ int mosaic_destroy(mosaic_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->amb_queue, &c->mix_queue, &c->scalars, &c->stage_x, &c->stage_y, &c->stage_v, &c->stage_out, &c->stage_out2,
-                      &c->stage_idx})
+                      &c->stage_idx, &c->geo_off, &c->geo_data, &c->dec_x, &c->dec_y, &c->dec_status, &c->hx[0], &c->hx[1],
+                      &c->hy[0], &c->hy[1], &c->hcounts})
         b->release();
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     for (size_t i = 0; i < c->ev_start.size(); i++) {
         (void)hipEventDestroy(c->ev_start[i]);
         (void)hipEventDestroy(c->ev_stop[i]);
@@ -1969,6 +1976,9 @@ int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
         c->raster_adaptive = v ? 1 : 0;
     } else if (k == "raster_lines") {
         c->raster_lines = v ? 1 : 0;
+    } else if (k == "host_chunk") {
+        if (v < 0) return fail(MOSAIC_E_ARG, "host_chunk must be >= 0");
+        c->host_chunk = v;
     } else if (k == "stream_persistent") {
         c->stream_persistent = v ? 1 : 0;
     } else if (k == "tile_lds") {
@@ -3062,8 +3072,75 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     return MOSAIC_OK;
 }
 
+// Host-resident coordinates: the batch is joined in chunks of host_chunk rows.  Chunk i's join
+// runs (asynchronously, counts on the device) while chunk i + 1 is copied on copy_stream into the
+// other pair of device buffers; then chunk i is finished exactly as a synchronous call would be
+// (NaN -> MOSAIC_E_NAN; an exact-path queue overflow reruns the chunk synchronously) and its counts
+// are added on the host.  The PCIe copy and the join overlap instead of adding.
+static int join_count_host_chunked(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+                                   int64_t* counts) {
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t CH = c->host_chunk;
+    int rc;
+    for (int b = 0; b < 2; b++)
+        if ((rc = c->hx[b].reserve((size_t)CH * 8)) || (rc = c->hy[b].reserve((size_t)CH * 8))) return rc;
+    const int32_t np = std::max<int32_t>(ch->n_polygons, 1);
+    if ((rc = c->hcounts.reserve((size_t)np * 8))) return rc;
+    if (!c->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    std::vector<int64_t> total((size_t)np, 0), part((size_t)np, 0);
+    int64_t st0 = 0, st1 = 0;
+    const int64_t nch = (n + CH - 1) / CH;
+    auto copy = [&](int64_t i) -> int {
+        const int64_t lo = i * CH, m = std::min(CH, n - lo);
+        HIP_TRY(hipMemcpyAsync(c->hx[i & 1].p, x + lo, (size_t)m * 8, hipMemcpyHostToDevice, c->copy_stream));
+        HIP_TRY(hipMemcpyAsync(c->hy[i & 1].p, y + lo, (size_t)m * 8, hipMemcpyHostToDevice, c->copy_stream));
+        return MOSAIC_OK;
+    };
+    if ((rc = copy(0))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->copy_stream));
+    const int saved_async = c->async;
+    for (int64_t i = 0; i < nch; i++) {
+        const int64_t m = std::min(CH, n - i * CH);
+        const double* dx = (const double*)c->hx[i & 1].p;
+        const double* dy = (const double*)c->hy[i & 1].p;
+        c->async = 1;
+        rc = run_join(c, ch, dx, dy, m, (int64_t*)c->hcounts.p, nullptr, nullptr, 0, nullptr);
+        c->async = saved_async;
+        if (rc) return rc;
+        if (i + 1 < nch && (rc = copy(i + 1))) return rc;
+        rc = mosaic_sync(c);
+        if (rc == MOSAIC_E_CAPACITY) {
+            c->async = 0;
+            rc = run_join(c, ch, dx, dy, m, (int64_t*)c->hcounts.p, nullptr, nullptr, 0, nullptr);
+            c->async = saved_async;
+            if (rc) return rc;
+        } else if (rc) {
+            HIP_TRY(hipStreamSynchronize(c->copy_stream));
+            return rc;
+        } else {
+            unsigned long long s[kScalars];
+            HIP_TRY(hipMemcpy(s, c->scalars.p, sizeof s, hipMemcpyDeviceToHost));
+            c->stats[0] = (int64_t)s[0];
+            c->stats[1] = (int64_t)s[2];
+        }
+        st0 += c->stats[0];
+        st1 += c->stats[1];
+        HIP_TRY(hipMemcpy(part.data(), c->hcounts.p, (size_t)np * 8, hipMemcpyDeviceToHost));
+        for (int32_t k = 0; k < np; k++) total[(size_t)k] += part[(size_t)k];
+        HIP_TRY(hipStreamSynchronize(c->copy_stream));
+    }
+    c->stats[0] = st0;
+    c->stats[1] = st1;
+    c->stats[2] = 0;
+    if (ch->n_polygons > 0) memcpy(counts, total.data(), (size_t)ch->n_polygons * 8);
+    return MOSAIC_OK;
+}
+
 int mosaic_pip_join_count(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
                           int64_t* counts) {
+    if (c && ch && x && y && counts && c->host_chunk > 0 && n > c->host_chunk && ch->device == c->device &&
+        !is_device_ptr(x) && !is_device_ptr(y) && !is_device_ptr(counts))
+        return join_count_host_chunked(c, ch, x, y, n, counts);
     return run_join(c, ch, x, y, n, counts, nullptr, nullptr, 0, nullptr);
 }
 
