@@ -145,6 +145,13 @@ int mosaic_point_geom_decode(mosaic_ctx* ctx, int format, const void* offsets, c
 /* BNG id <-> string (BNGIndexSystem.format / parse).  format returns the string length. */
 int mosaic_bng_format(int64_t id, char* buf, size_t cap);
 int mosaic_bng_parse(const char* s, int64_t* out);
+/* serializeCellId over a BNG cell column (IndexSystem.scala:37-46 -> BNGIndexSystem.format
+ * :114-129), computed on the GPU, in Arrow utf8 layout: offsets[n + 1] (int64) and the characters.
+ * Null rows (valid[i] == 0; valid may be null) are empty strings.  If the characters exceed
+ * chars_cap, returns MOSAIC_E_CAPACITY with *chars_needed set (offsets are written either way);
+ * an id the reference cannot format gives MOSAIC_E_ARG. */
+int mosaic_bng_format_column(mosaic_ctx* ctx, const int64_t* ids, const uint8_t* valid, int64_t n, int64_t* offsets,
+                             char* chars, int64_t chars_cap, int64_t* chars_needed);
 
 /* ---- chip table (build side) ---- */
 /* n_chips rows of ChipType: is_core[i], index_id[i] (int64 cell id), wkb bytes

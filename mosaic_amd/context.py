@@ -292,9 +292,23 @@ class MosaicContext:
     def _serialize(self, cells):
         """IndexSystem.serializeCellId: Long for H3, String for BNG (IndexSystem.scala:37-46)."""
         if self.index_system.cell_id_type == "string":
-            arr = cells.cpu().numpy() if _is_torch(cells) else cells
-            return [self.index_system.format(c) for c in arr]
+            offs, chars = self.bng_format_column(cells)
+            return [chars[offs[i]:offs[i + 1]].decode() for i in range(len(offs) - 1)]
         return cells
+
+    def bng_format_column(self, cells, valid=None):
+        """BNG ids -> Arrow utf8 column (int64 offsets[n + 1], bytes), formatted on the GPU
+        (BNGIndexSystem.format, BNGIndexSystem.scala:114-129)."""
+        ids = cells.contiguous() if _is_torch(cells) else np.ascontiguousarray(cells, np.int64)
+        n = int(ids.shape[0])
+        offs = np.zeros(n + 1, np.int64)
+        need = ctypes.c_int64(0)
+        v = None if valid is None else np.ascontiguousarray(valid, np.uint8)
+        cap = 16 * n
+        chars = np.zeros(max(cap, 1), np.uint8)
+        N.check(N.lib().mosaic_bng_format_column(self.handle, N.ptr(ids), None if v is None else N.ptr(v), n,
+                                                 N.ptr(offs), N.ptr(chars), cap, ctypes.byref(need)))
+        return offs, chars[:need.value].tobytes()
 
     def grid_longlatascellid(self, lon, lat, resolution, raw=False):
         """PointIndexLonLat (expressions/index/PointIndexLonLat.scala:44-51)."""

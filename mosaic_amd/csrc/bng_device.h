@@ -198,5 +198,47 @@ MOSAIC_HD int kring(int64_t id, int n, int64_t* out) {
     return m;
 }
 
+
+// ---- BNGIndexSystem.format (BNGIndexSystem.scala:114-129) for one id, device and host: the two
+// letters of letterMap(nLetter digits)(eLetter digits) (row 10 col 4 is "SZ" as in the reference,
+// :96), then the k easting and k northing digits and the quadrant's name.  Writes at most 16 chars
+// to out (may be null: length only); returns the length, or -1 for an id the reference cannot format.
+MOSAIC_HD int format_id(int64_t id, char* out) {
+    const char* const kLetters =
+        "SVSWSXSYSZTVTWSQSRSSSTSUTQTRSLSMSNSOSPTLTMSFSGSHSJSKTFTGSASBSCSDSETATBNVNWNXNYNZOVOW"
+        "NQNRNSNTNUOQORNLNMNNNONPOLOMNFNGNHNJNKOFOGNANBNCNDNEOAOBHVHWHXHYSZJVJWHQHRHSHTHUJQJR"
+        "HLHMHNHOHPJLJM";
+    const char* const kQuad = "  SWNWNESE";
+    int d[20];
+    const int n = index_digits(id, d);
+    if (n < 4) return -1;  // slice(3, 5) would be empty (NumberFormatException)
+    const int col = d[1] * 10 + d[2], row = n == 4 ? d[3] : d[3] * 10 + d[4];
+    if (row > 12 || col > 6) return -1;
+    const char* lt = kLetters + 2 * (row * 7 + col);
+    if (n < 6) {
+        if (out) out[0] = lt[0];
+        return 1;
+    }
+    const int q = d[n - 1];
+    if (q > 4) return -1;
+    const int k = (n - 6) / 2;
+    int m = 0;
+    if (out) {
+        out[0] = lt[0];
+        out[1] = lt[1];
+    }
+    m = 2;
+    for (int i = 5; i < 5 + 2 * k; i++, m++)
+        if (out) out[m] = (char)('0' + d[i]);
+    if (q > 0) {
+        if (out) {
+            out[m] = kQuad[2 * q];
+            out[m + 1] = kQuad[2 * q + 1];
+        }
+        m += 2;
+    }
+    return m;
+}
+
 }  // namespace bng
 }  // namespace mosaic

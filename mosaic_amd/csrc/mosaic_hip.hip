@@ -9,6 +9,7 @@
 // Points whose H3 cell the fast path cannot certify are appended to a queue and finished by a
 // second kernel running the exact H3 restatement (h3_exact).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -1172,6 +1173,47 @@ __global__ void __launch_bounds__(256) k_bng_kring(KringArgs a) {
     }
     if (bad) atomicOr(a.flags, 1u);
 }
+
+
+// ---- serializeCellId for BNG (IndexSystem.scala:37-46 -> BNGIndexSystem.format :114-129) over a
+// cell column, output in Arrow utf8 layout: k_bng_format_len writes each row's length (0 for null
+// rows) to offsets[i + 1], an inclusive scan turns them into offsets, k_bng_format_write writes the
+// characters.  Ids the reference cannot format set flags bit 0.
+struct FormatArgs {
+    const int64_t* ids;
+    const uint8_t* valid;
+    int64_t n;
+    int64_t* offsets;  // n + 1
+    char* chars;
+    unsigned int* flags;
+};
+__global__ void __launch_bounds__(256) k_bng_format_len(FormatArgs a) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+        int len = 0;
+        if (!a.valid || a.valid[i]) {
+            len = bng::format_id(a.ids[i], nullptr);
+            if (len < 0) {
+                bad = true;
+                len = 0;
+            }
+        }
+        a.offsets[i + 1] = len;
+    }
+    if (bad) atomicOr(a.flags, 1u);
+}
+__global__ void __launch_bounds__(256) k_bng_format_write(FormatArgs a) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+        if (a.valid && !a.valid[i]) continue;
+        char buf[16];
+        const int len = bng::format_id(a.ids[i], buf);
+        char* o = a.chars + a.offsets[i];
+        for (int j = 0; j < len; j++) o[j] = buf[j];
+    }
+}
+__global__ void k_add_prev(int64_t* first, const int64_t* prev_total) { *first += *prev_total; }
 
 // ---- BNG dense cell table (positive resolutions): BNGIndexSystem.pointToIndex
 // (BNGIndexSystem.scala:277-291, 528-541) maps a point with 0 <= toInt(e), toInt(n) < 1e7 to the id
@@ -3319,6 +3361,73 @@ int mosaic_cell_kring(mosaic_ctx* c, int grid, const int64_t* cells, const uint8
     if (!dev_cnt) HIP_TRY(hipMemcpyAsync(out_count, s_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (flags & 1u) return done(fail(MOSAIC_E_ARG, "invalid BNG cell id"));
+    return done(MOSAIC_OK);
+}
+
+
+int mosaic_bng_format_column(mosaic_ctx* c, const int64_t* ids, const uint8_t* valid, int64_t n, int64_t* offsets,
+                             char* chars, int64_t chars_cap, int64_t* chars_needed) {
+    if (!c || n < 0 || !offsets || !chars_needed || (n > 0 && !ids) || chars_cap < 0 || (chars_cap > 0 && !chars))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf s_ids, s_valid, s_off, s_chars, s_flags, s_tmp;
+    auto done = [&](int rc) {
+        for (DevBuf* b : {&s_ids, &s_valid, &s_off, &s_chars, &s_flags, &s_tmp}) b->release();
+        return rc;
+    };
+    int rc;
+    const void *di, *dv;
+    if ((rc = to_device(c, s_ids, ids, (size_t)n * 8, &di)) || (rc = to_device(c, s_valid, valid, (size_t)n, &dv)))
+        return done(rc);
+    const bool dev_off = is_device_ptr(offsets);
+    if ((!dev_off && (rc = s_off.reserve((size_t)(n + 1) * 8))) || (rc = s_flags.reserve(4))) return done(rc);
+    int64_t* doff = dev_off ? offsets : (int64_t*)s_off.p;
+    HIP_TRY(hipMemsetAsync(doff, 0, 8, c->stream));
+    HIP_TRY(hipMemsetAsync(s_flags.p, 0, 4, c->stream));
+    FormatArgs a;
+    a.ids = (const int64_t*)di;
+    a.valid = (const uint8_t*)dv;
+    a.n = n;
+    a.offsets = doff;
+    a.chars = nullptr;
+    a.flags = (unsigned int*)s_flags.p;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_bng_format_len, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        size_t tmp_bytes = 0;
+        // n may exceed INT_MAX: scan in pieces of 2^30 rows, carrying the running total
+        const int64_t piece = (int64_t)1 << 30;
+        HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, doff + 1, doff + 1, (int)std::min(n, piece),
+                                                 c->stream));
+        if ((rc = s_tmp.reserve(std::max<size_t>(tmp_bytes, 16)))) return done(rc);
+        for (int64_t lo = 0; lo < n; lo += piece) {
+            const int m = (int)std::min(piece, n - lo);
+            if (lo > 0) {
+                // add the previous pieces' total to this piece's first length
+                hipLaunchKernelGGL(k_add_prev, dim3(1), dim3(1), 0, c->stream, doff + 1 + lo, doff + lo);
+                HIP_TRY(hipGetLastError());
+            }
+            size_t tb = s_tmp.bytes;
+            HIP_TRY(hipcub::DeviceScan::InclusiveSum(s_tmp.p, tb, doff + 1 + lo, doff + 1 + lo, m, c->stream));
+        }
+    }
+    int64_t total = 0;
+    unsigned int flags = 0;
+    HIP_TRY(hipMemcpyAsync(&total, doff + n, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&flags, s_flags.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (flags & 1u) return done(fail(MOSAIC_E_ARG, "invalid BNG id in the column"));
+    *chars_needed = total;
+    if (!dev_off) HIP_TRY(hipMemcpy(offsets, doff, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost));
+    if (total > chars_cap) return done(fail(MOSAIC_E_CAPACITY, "chars buffer too small"));
+    if (total == 0) return done(MOSAIC_OK);
+    const bool dev_chars = is_device_ptr(chars);
+    if (!dev_chars && (rc = s_chars.reserve((size_t)total))) return done(rc);
+    a.chars = dev_chars ? chars : (char*)s_chars.p;
+    hipLaunchKernelGGL(k_bng_format_write, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    if (!dev_chars) HIP_TRY(hipMemcpyAsync(chars, s_chars.p, (size_t)total, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return done(MOSAIC_OK);
 }
 
