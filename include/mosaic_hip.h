@@ -234,6 +234,15 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
 int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k,
                       int loop, int64_t* out, int32_t* out_count);
 
+/* ---- grid_boundaryaswkb over a cell column (BNG) ---- */
+/* out[93 i .. 93 i + 92] = the WKB JTS writes for BNGIndexSystem.indexToGeometry(ids[i])
+ * (core/index/BNGIndexSystem.scala indexToGeometry; functions/MosaicContext.scala
+ * grid_boundaryaswkb -> expressions/index/IndexGeometry.scala:65-75): big-endian 2D Polygon of the
+ * cell square, 5 points.  Null rows (valid[i] == 0) are left zero.  H3 is not implemented
+ * (MOSAIC_E_ARG). */
+int mosaic_cell_boundary_wkb(mosaic_ctx* ctx, int grid, const int64_t* ids, const uint8_t* valid, int64_t n,
+                             uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,7 +35,7 @@ EXPORTS = [
     "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_chip_set_info",
     "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_point_geom_to_cell",
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
-    "mosaic_cell_kring", "mosaic_bng_format_column",
+    "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb",
 ]
 
 GEOM_WKB = 0
@@ -119,6 +119,7 @@ def lib():
         "mosaic_intersects_aggregate": ([vp, vp, vp, vp, vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_cell_kring": ([vp, i32, vp, vp, i64, i32, i32, vp, vp], i32),
         "mosaic_bng_format_column": ([vp, vp, vp, i64, vp, vp, i64, ctypes.POINTER(i64)], i32),
+        "mosaic_cell_boundary_wkb": ([vp, i32, vp, vp, i64, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -497,6 +497,16 @@ class MosaicContext:
         BNG: BNGIndexSystem.scala:234-246): per row the valid cells at distance k."""
         return self._kring(cells, k, True, raw)
 
+    def grid_boundaryaswkb(self, cells):
+        """grid_boundaryaswkb(cellId) (IndexGeometry.scala:65-75 -> IndexSystem.indexToGeometry ->
+        toWKB); BNG only: per row the cell square as big-endian WKB (93 bytes)."""
+        strings = len(cells) and isinstance(cells[0], str)
+        ids = np.array([self.index_system.parse(c) for c in cells] if strings else cells, np.int64)
+        out = np.zeros(max(93 * len(ids), 1), np.uint8)
+        N.check(N.lib().mosaic_cell_boundary_wkb(self.handle, self.index_system.grid, N.ptr(ids), None, len(ids),
+                                                 N.ptr(out)))
+        return [out[93 * i:93 * (i + 1)].tobytes() for i in range(len(ids))]
+
     def st_intersects_aggregate(self, left, right):
         """left.join(right, left_index.index_id == right_index.index_id).groupBy(left_key, right_key)
         .agg(st_intersects_aggregate(left_index, right_index)) over two chip tables

@@ -7,6 +7,7 @@
 #pragma once
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #if !defined(MOSAIC_HD)
 #if defined(__HIPCC__)
@@ -91,10 +92,21 @@ MOSAIC_HD bool point_to_index(double eastings, double northings, int res, int64_
 // whose toString the reference would not decode)
 MOSAIC_HD int index_digits(int64_t id, int* d) {
     if (id <= 0) return 0;
+    // 64-bit division only to split off 9-digit groups; the digits come from 32-bit arithmetic
     int t[20], n = 0;
-    while (id > 0) {
-        t[n++] = (int)(id % 10);
-        id /= 10;
+    uint64_t u = (uint64_t)id;
+    while (u >= 1000000000ull) {
+        uint32_t lo = (uint32_t)(u % 1000000000ull);
+        u /= 1000000000ull;
+        for (int i = 0; i < 9; i++) {
+            t[n++] = (int)(lo % 10u);
+            lo /= 10u;
+        }
+    }
+    uint32_t hi = (uint32_t)u;
+    while (hi > 0) {
+        t[n++] = (int)(hi % 10u);
+        hi /= 10u;
     }
     for (int i = 0; i < n; i++) d[i] = t[n - 1 - i];
     return n;
@@ -238,6 +250,39 @@ MOSAIC_HD int format_id(int64_t id, char* out) {
         m += 2;
     }
     return m;
+}
+
+
+// ---- BNGIndexSystem.indexToGeometry (BNGIndexSystem.scala:420-431 area: the cell square
+// (x, y) (x + e, y) (x + e, y + e) (x, y + e) (x, y) in Int arithmetic) as JTS WKBWriter writes it
+// for grid_boundaryaswkb: big-endian, 2D Polygon, one ring of 5 points = 93 bytes.
+static const int kCellWkbBytes = 93;
+MOSAIC_HD void put_be_u32(uint8_t* o, uint32_t v) {
+    o[0] = (uint8_t)(v >> 24);
+    o[1] = (uint8_t)(v >> 16);
+    o[2] = (uint8_t)(v >> 8);
+    o[3] = (uint8_t)v;
+}
+MOSAIC_HD void put_be_f64(uint8_t* o, double d) {
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    for (int i = 0; i < 8; i++) o[i] = (uint8_t)(u >> (56 - 8 * i));
+}
+MOSAIC_HD bool cell_wkb(int64_t id, uint8_t* o) {
+    int res;
+    int32_t e, x, y;
+    if (!cell_origin(id, &res, &e, &x, &y)) return false;
+    const int32_t x1 = (int32_t)((uint32_t)x + (uint32_t)e), y1 = (int32_t)((uint32_t)y + (uint32_t)e);
+    const int32_t px[5] = {x, x1, x1, x, x}, py[5] = {y, y, y1, y1, y};
+    o[0] = 0;  // big-endian
+    put_be_u32(o + 1, 3);
+    put_be_u32(o + 5, 1);
+    put_be_u32(o + 9, 5);
+    for (int i = 0; i < 5; i++) {
+        put_be_f64(o + 13 + 16 * i, (double)px[i]);
+        put_be_f64(o + 21 + 16 * i, (double)py[i]);
+    }
+    return true;
 }
 
 }  // namespace bng

@@ -1210,10 +1210,33 @@ __global__ void __launch_bounds__(256) k_bng_format_write(FormatArgs a) {
         char buf[16];
         const int len = bng::format_id(a.ids[i], buf);
         char* o = a.chars + a.offsets[i];
-        for (int j = 0; j < len; j++) o[j] = buf[j];
+        int j = 0;
+        // whole aligned 4-byte words where the row's start allows (a column of one resolution has
+        // equal lengths, so its rows start 4-aligned whenever the length is a multiple of 4)
+        if ((((uintptr_t)o) & 3) == 0)
+            for (; j + 4 <= len; j += 4) {
+                uint32_t w = (uint32_t)(uint8_t)buf[j] | ((uint32_t)(uint8_t)buf[j + 1] << 8) |
+                             ((uint32_t)(uint8_t)buf[j + 2] << 16) | ((uint32_t)(uint8_t)buf[j + 3] << 24);
+                *(uint32_t*)(o + j) = w;
+            }
+        for (; j < len; j++) o[j] = buf[j];
     }
 }
 __global__ void k_add_prev(int64_t* first, const int64_t* prev_total) { *first += *prev_total; }
+
+
+// ---- grid_boundaryaswkb over a BNG cell column (IndexGeometry -> BNGIndexSystem.indexToGeometry,
+// toWKB): 93 bytes per row at out + 93 i; null rows are left untouched (the caller's validity).
+__global__ void __launch_bounds__(256) k_bng_cell_wkb(const int64_t* ids, const uint8_t* valid, int64_t n,
+                                                      uint8_t* out, unsigned int* flags) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+        if (valid && !valid[i]) continue;
+        if (!bng::cell_wkb(ids[i], out + i * bng::kCellWkbBytes)) bad = true;
+    }
+    if (bad) atomicOr(flags, 1u);
+}
 
 // ---- BNG dense cell table (positive resolutions): BNGIndexSystem.pointToIndex
 // (BNGIndexSystem.scala:277-291, 528-541) maps a point with 0 <= toInt(e), toInt(n) < 1e7 to the id
@@ -3428,6 +3451,40 @@ int mosaic_bng_format_column(mosaic_ctx* c, const int64_t* ids, const uint8_t* v
     HIP_TRY(hipGetLastError());
     if (!dev_chars) HIP_TRY(hipMemcpyAsync(chars, s_chars.p, (size_t)total, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return done(MOSAIC_OK);
+}
+
+
+int mosaic_cell_boundary_wkb(mosaic_ctx* c, int grid, const int64_t* ids, const uint8_t* valid, int64_t n,
+                             uint8_t* out) {
+    if (!c || n < 0 || (n > 0 && (!ids || !out))) return fail(MOSAIC_E_ARG, "invalid argument");
+    if (grid != MOSAIC_GRID_BNG)
+        return fail(MOSAIC_E_ARG, "grid_boundaryaswkb: only the BNG grid is implemented by this engine");
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf s_ids, s_valid, s_out, s_flags;
+    auto done = [&](int rc) {
+        for (DevBuf* b : {&s_ids, &s_valid, &s_out, &s_flags}) b->release();
+        return rc;
+    };
+    int rc;
+    const void *di, *dv;
+    if ((rc = to_device(c, s_ids, ids, (size_t)n * 8, &di)) || (rc = to_device(c, s_valid, valid, (size_t)n, &dv)))
+        return done(rc);
+    const size_t bytes = (size_t)n * bng::kCellWkbBytes;
+    const bool dev_out = is_device_ptr(out);
+    if ((!dev_out && (rc = s_out.reserve(bytes))) || (rc = s_flags.reserve(4))) return done(rc);
+    uint8_t* dout = dev_out ? out : (uint8_t*)s_out.p;
+    if (!dev_out && valid) HIP_TRY(hipMemsetAsync(dout, 0, bytes, c->stream));
+    HIP_TRY(hipMemsetAsync(s_flags.p, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_bng_cell_wkb, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, (const int64_t*)di,
+                       (const uint8_t*)dv, n, dout, (unsigned int*)s_flags.p);
+    HIP_TRY(hipGetLastError());
+    unsigned int flags = 0;
+    HIP_TRY(hipMemcpyAsync(&flags, s_flags.p, 4, hipMemcpyDeviceToHost, c->stream));
+    if (!dev_out) HIP_TRY(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (flags & 1u) return done(fail(MOSAIC_E_ARG, "invalid BNG cell id"));
     return done(MOSAIC_OK);
 }
 

@@ -62,6 +62,8 @@ def lib():
             getattr(L, fn).argtypes = [i64, i32, vp]
         L.oracle_bng_is_valid.restype = i32
         L.oracle_bng_is_valid.argtypes = [i64]
+        L.oracle_bng_cell_origin.restype = i32
+        L.oracle_bng_cell_origin.argtypes = [i64, vp]
         _lib = L
     return _lib
 
@@ -153,6 +155,21 @@ def bng_kring(cell, k):
 
 def bng_is_valid(cell):
     return bool(lib().oracle_bng_is_valid(int(cell)))
+
+
+def bng_cell_wkb(cell):
+    """grid_boundaryaswkb for a BNG cell: BNGIndexSystem.indexToGeometry's square (x, y), (x + e, y),
+    (x + e, y + e), (x, y + e), (x, y) as JTS WKBWriter's default big-endian 2D Polygon."""
+    import struct
+
+    o = np.zeros(4, np.int32)
+    if not lib().oracle_bng_cell_origin(int(cell), _ptr(o)):
+        raise ValueError("undecodable BNG id")
+    _, e, x, y = (int(v) for v in o)
+    x1 = int(np.int32(np.uint32((x + e) & 0xffffffff)))
+    y1 = int(np.int32(np.uint32((y + e) & 0xffffffff)))
+    pts = [(x, y), (x1, y), (x1, y1), (x, y1), (x, y)]
+    return struct.pack(">BIII", 0, 3, 1, 5) + b"".join(struct.pack(">dd", float(a), float(b)) for a, b in pts)
 
 
 def segments_intersect(p1, p2, q1, q2):

@@ -242,3 +242,16 @@ int oracle_bng_kring(int64_t id, int n, int64_t* out) {
     for (int k = 1; k <= n; k++) m += oracle_bng_kloop(id, k, out + m);
     return m;
 }
+
+/* BNGIndexSystem.indexToGeometry's square: origin (x, y) and edge of the cell (Int arithmetic as
+ * getX / getY); 0 if the id cannot be decoded. */
+int oracle_bng_cell_origin(int64_t id, int32_t* out4) {
+    int res;
+    int32_t e, x, y;
+    if (!bng_origin(id, &res, &e, &x, &y)) return 0;
+    out4[0] = res;
+    out4[1] = e;
+    out4[2] = x;
+    out4[3] = y;
+    return 1;
+}

@@ -55,6 +55,8 @@ int oracle_bng_format(int64_t id, char* buf, int cap);
 int oracle_bng_is_valid(int64_t id);
 int oracle_bng_kloop(int64_t id, int k, int64_t* out);
 int oracle_bng_kring(int64_t id, int n, int64_t* out);
+/* (resolution, edge, x, y) of a cell for indexToGeometry; 0 if undecodable. */
+int oracle_bng_cell_origin(int64_t id, int32_t* out4);
 
 /* ---- JTS contains ---- */
 /* Geometry described as rings: ring_offsets[r]..ring_offsets[r+1] index into xy (pairs);
