@@ -497,6 +497,23 @@ class MosaicContext:
         BNG: BNGIndexSystem.scala:234-246): per row the valid cells at distance k."""
         return self._kring(cells, k, True, raw)
 
+    def grid_cellkringexplode(self, cells, k):
+        """grid_cellkringexplode (MosaicContext.scala:694-695, CellKRingExplode): one output row per
+        (input row, ring cell) -- (row index array, cell array), in the reference's order."""
+        return self._explode(self.grid_cellkring(cells, k, raw=True))
+
+    def grid_cellkloopexplode(self, cells, k):
+        """grid_cellkloopexplode (CellKLoopExplode): one output row per (input row, loop cell)."""
+        return self._explode(self.grid_cellkloop(cells, k, raw=True))
+
+    def _explode(self, rows):
+        lens = np.array([len(r) for r in rows], np.int64)
+        idx = np.repeat(np.arange(len(rows), dtype=np.int64), lens)
+        cells = np.concatenate(rows) if len(rows) else np.zeros(0, np.int64)
+        if self.index_system.cell_id_type == "string":
+            return idx, self._serialize(cells)
+        return idx, cells
+
     def grid_boundaryaswkb(self, cells):
         """grid_boundaryaswkb(cellId) (IndexGeometry.scala:65-75 -> IndexSystem.indexToGeometry ->
         toWKB); BNG only: per row the cell square as big-endian WKB (93 bytes)."""

@@ -82,9 +82,10 @@ def quickstart_points(zones, n, config=1, sigma=0.005, seed=None, round_1e6=True
     """C1 / C3 mixture on the host (numpy PCG64)."""
     rng = np.random.Generator(np.random.PCG64(SEED_BASE + config if seed is None else seed))
     x0, y0, x1, y1 = zones.bbox()
-    centres = np.array([zones.shell_centroid(g) for g in rng.choice(len(zones), 32, replace=False)])
+    k = min(32, len(zones))  # 32 mixture centres (fewer for small zone sets)
+    centres = np.array([zones.shell_centroid(g) for g in rng.choice(len(zones), k, replace=False)])
     n_mix = int(0.8 * n)
-    c = centres[rng.integers(0, 32, n_mix)]
+    c = centres[rng.integers(0, k, n_mix)]
     pts = np.empty((n, 2))
     pts[:n_mix] = c + rng.normal(0.0, sigma, (n_mix, 2))
     pts[n_mix:, 0] = rng.uniform(x0, x1, n - n_mix)

@@ -155,3 +155,15 @@ def test_gpu_agg_matches_oracle(ctx, name, res, shift):
     want = oracle.intersects_aggregate(_chips_dict(left), _chips_dict(right))
     assert got == want
     assert list(zip(lk, rk)) == sorted(zip(lk, rk))
+
+
+def test_quickstart_points_small_zone_sets():
+    """__graft_entry__.smoke() draws its points from 21 zones: fewer than the 32 mixture centres."""
+    from mosaic_amd.data import quickstart_points
+
+    zones = PolygonSet.load("nyc_taxi_zones")
+    x, y = quickstart_points(zones.subset(list(range(0, 263, 13))), 20000, seed=1)
+    assert len(x) == len(y) == 20000 and np.isfinite(x).all()
+    a = quickstart_points(zones, 1000, seed=3)
+    b = quickstart_points(zones, 1000, seed=3)
+    assert np.array_equal(a[0], b[0])

@@ -89,6 +89,11 @@ def test_gpu_kring_matches_oracle(loop):
         assert sorted(ctx.grid_cellkloop([POS], k)[0]) == sorted(want)
     for k, want in GOLD_NEG.items():
         assert sorted(ctx.grid_cellkloop(["TQ3879SE"], k)[0]) == sorted(want)
+    # the explode variants: one row per (input row, cell), same cells in the same order
+    idx, cells_out = ctx.grid_cellkringexplode([POS, NEG], 2)
+    rings = ctx.grid_cellkring([POS, NEG], 2)
+    assert list(idx) == [0] * len(rings[0]) + [1] * len(rings[1])
+    assert list(cells_out) == rings[0] + rings[1]
     ctx.close()
 
 
