@@ -32,7 +32,8 @@ EXPORTS = [
     "mosaic_resolution_str", "mosaic_point_to_cell", "mosaic_bng_format", "mosaic_bng_parse",
     "mosaic_chip_table_create", "mosaic_chip_table_destroy", "mosaic_chip_table_info", "mosaic_chip_table_tiles",
     "mosaic_chip_table_tile_grid", "mosaic_chip_table_raster", "mosaic_pip_join_count",
-    "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_chip_set_info",
+    "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_tessellate_gpu",
+    "mosaic_tess_last_classify_ms", "mosaic_chip_set_info",
     "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_point_geom_to_cell",
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
     "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb",
@@ -120,6 +121,8 @@ def lib():
         "mosaic_cell_kring": ([vp, i32, vp, vp, i64, i32, i32, vp, vp], i32),
         "mosaic_bng_format_column": ([vp, vp, vp, i64, vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_cell_boundary_wkb": ([vp, i32, vp, vp, i64, vp], i32),
+        "mosaic_tessellate_gpu": ([vp, i32, i32, i64, vp, vp, vp, vp, i32, ctypes.POINTER(vp)], i32),
+        "mosaic_tess_last_classify_ms": ([vp], ctypes.c_double),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

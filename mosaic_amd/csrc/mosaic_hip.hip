@@ -1771,6 +1771,7 @@ struct mosaic_ctx {
     int raster = 16;      // raster cells per side of a border chip's envelope (chip tables built later)
     int raster_adaptive = 1;  // fewer raster cells for rings with few segments
     int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
+    double last_tess_classify_ms = 0;  // k_bng_tess_classify duration of the last mosaic_tessellate_gpu
     int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
     int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
     int raster_sub = 64;  // point raster: sub-blocks per tile side (a power of two)
@@ -3487,5 +3488,172 @@ int mosaic_cell_boundary_wkb(mosaic_ctx* c, int grid, const int64_t* ids, const 
     if (flags & 1u) return done(fail(MOSAIC_E_ARG, "invalid BNG cell id"));
     return done(MOSAIC_OK);
 }
+
+}  // extern "C"
+
+// ---- grid_tessellateexplode (BNG): per-cell classification on the GPU ----
+// Reference: IndexSystem.getCoreChips / getBorderChips (core/index/IndexSystem.scala:152-186) via
+// Mosaic.mosaicFill (core/Mosaic.scala:60-87).  The producer's contract (tessellate.cpp emit_cell):
+// a candidate cell is a BORDER cell if any polygon segment comes within eps of the cell square,
+// else a CORE cell if its centre is inside a part (even-odd over the part's rings), else it is
+// dropped.  That test is O(segments) per cell and dominates chip production; one wave per
+// candidate cell runs it here, lanes strided over each ring's segments (HBM/L2-resident rings,
+// read once per wave; the rings of one geometry stay in L2 across its candidates).  Arithmetic is
+// the host test's, operation for operation (no contraction), so the classes are bit-identical.
+namespace tessgpu {
+
+__device__ inline bool seg_near_square(double px, double py, double qx, double qy, const double* sx,
+                                       const double* sy, double eps) {
+    // tessellate.cpp seg_near_convex with the 4-vertex ccw square (sx[k], sy[k])
+    auto inside = [&](double rx, double ry) {
+        for (int i = 0; i < 4; i++) {
+            double ax = sx[i], ay = sy[i], bx = sx[(i + 1) & 3], by = sy[(i + 1) & 3];
+            double ex = bx - ax, ey = by - ay, len = sqrt(ex * ex + ey * ey);
+            if ((ex * (ry - ay) - ey * (rx - ax)) / len < -eps) return false;
+        }
+        return true;
+    };
+    if (inside(px, py) || inside(qx, qy)) return true;
+    auto dist_seg = [](double rx, double ry, double ax, double ay, double bx, double by) {
+        double ex = bx - ax, ey = by - ay;
+        double t = ((rx - ax) * ex + (ry - ay) * ey) / (ex * ex + ey * ey);
+        t = fmax(0.0, fmin(1.0, t));
+        double dx = ax + t * ex - rx, dy = ay + t * ey - ry;
+        return sqrt(dx * dx + dy * dy);
+    };
+    for (int i = 0; i < 4; i++) {
+        double ax = sx[i], ay = sy[i], bx = sx[(i + 1) & 3], by = sy[(i + 1) & 3];
+        double d1 = (bx - ax) * (py - ay) - (by - ay) * (px - ax);
+        double d2 = (bx - ax) * (qy - ay) - (by - ay) * (qx - ax);
+        double d3 = (qx - px) * (ay - py) - (qy - py) * (ax - px);
+        double d4 = (qx - px) * (by - py) - (qy - py) * (bx - px);
+        if (((d1 > 0) != (d2 > 0)) && ((d3 > 0) != (d4 > 0))) return true;
+        if (dist_seg(ax, ay, px, py, qx, qy) < eps || dist_seg(px, py, ax, ay, bx, by) < eps ||
+            dist_seg(qx, qy, ax, ay, bx, by) < eps)
+            return true;
+    }
+    return false;
+}
+
+struct ClassifyArgs {
+    const double* xy;             // interleaved vertices (x, y)
+    const int64_t* ring_offsets;  // [n_rings + 1]
+    const int64_t* part_rings;    // [n_parts + 1]
+    const int64_t* geom_parts;    // [n_geoms + 1]
+    const int32_t* cand_geom;     // [n_cand]
+    const int64_t* cand_ij;       // [2 n_cand] lower-left cell corner / e
+    int64_t n_cand;
+    double e, eps;
+    uint8_t* cls;  // 0 dropped, 1 core, 2 border
+};
+
+__global__ void __launch_bounds__(256) k_bng_tess_classify(ClassifyArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < a.n_cand; c += n_waves) {
+        const int g = a.cand_geom[c];
+        const double cx0 = (double)a.cand_ij[2 * c] * a.e, cy0 = (double)a.cand_ij[2 * c + 1] * a.e;
+        double sx[4] = {cx0, cx0 + a.e, cx0 + a.e, cx0};
+        double sy[4] = {cy0, cy0, cy0 + a.e, cy0 + a.e};
+        const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
+        bool near = false;
+        for (int64_t p = p0; p < p1 && !near; p++)
+            for (int64_t r = a.part_rings[p]; r < a.part_rings[p + 1]; r++) {
+                const int64_t b = a.ring_offsets[r], n = a.ring_offsets[r + 1] - b;
+                bool hit = false;
+                for (int64_t v = lane; v + 1 < n && !hit; v += 64) {
+                    const double* s = a.xy + 2 * (b + v);
+                    hit = seg_near_square(s[0], s[1], s[2], s[3], sx, sy, a.eps);
+                }
+                if (__ballot(hit)) {
+                    near = true;
+                    break;
+                }
+            }
+        uint8_t out = 2;
+        if (!near) {
+            // centre = ((((0 + x0) + x1) + x2) + x3) / 4 as the host sums the clip square
+            const double cx = (((0.0 + sx[0]) + sx[1]) + sx[2] + sx[3]) / 4.0;
+            const double cy = (((0.0 + sy[0]) + sy[1]) + sy[2] + sy[3]) / 4.0;
+            bool inside = false;
+            for (int64_t p = p0; p < p1 && !inside; p++) {
+                bool par = false;
+                for (int64_t r = a.part_rings[p]; r < a.part_rings[p + 1]; r++) {
+                    const int64_t b = a.ring_offsets[r], n = a.ring_offsets[r + 1] - b;
+                    for (int64_t i = lane; i < n; i += 64) {
+                        const int64_t j = i == 0 ? n - 1 : i - 1;
+                        const double ix = a.xy[2 * (b + i)], iy = a.xy[2 * (b + i) + 1];
+                        const double jx = a.xy[2 * (b + j)], jy = a.xy[2 * (b + j) + 1];
+                        if (((iy > cy) != (jy > cy)) && (cx < (jx - ix) * (cy - iy) / (jy - iy) + ix)) par = !par;
+                    }
+                }
+                inside = (__popcll(__ballot(par)) & 1) != 0;
+            }
+            out = inside ? 1 : 0;
+        }
+        if (lane == 0) a.cls[c] = out;
+    }
+}
+
+}  // namespace tessgpu
+
+extern "C" {
+
+// Classification step of mosaic_tessellate_gpu (tessellate.cpp); not part of the public header.
+int mosaic_tess_classify_bng(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                             const int64_t* ring_offsets, const double* xy, int64_t n_cand, const int32_t* cand_geom,
+                             const int64_t* cand_ij, double e, double eps, uint8_t* cls) {
+    if (!c || n_geoms < 0 || n_cand < 0 || (n_cand > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy ||
+                                                            !cand_geom || !cand_ij || !cls)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    if (n_cand == 0) return MOSAIC_OK;
+    for (int64_t k = 0; k < n_cand; k++)  // the kernel indexes geom_parts[g + 1]
+        if (cand_geom[k] < 0 || cand_geom[k] >= n_geoms) return fail(MOSAIC_E_ARG, "candidate geometry out of range");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t n_parts = geom_parts[n_geoms], n_rings = part_rings[n_parts], n_verts = ring_offsets[n_rings];
+    DevBuf s_gp, s_pr, s_ro, s_xy, s_cg, s_ij, s_cls;
+    auto done = [&](int rc) {
+        for (DevBuf* b : {&s_gp, &s_pr, &s_ro, &s_xy, &s_cg, &s_ij, &s_cls}) b->release();
+        return rc;
+    };
+    int rc;
+    const void *dgp, *dpr, *dro, *dxy, *dcg, *dij;
+    if ((rc = to_device(c, s_gp, geom_parts, (size_t)(n_geoms + 1) * 8, &dgp)) ||
+        (rc = to_device(c, s_pr, part_rings, (size_t)(n_parts + 1) * 8, &dpr)) ||
+        (rc = to_device(c, s_ro, ring_offsets, (size_t)(n_rings + 1) * 8, &dro)) ||
+        (rc = to_device(c, s_xy, xy, (size_t)std::max<int64_t>(n_verts, 1) * 16, &dxy)) ||
+        (rc = to_device(c, s_cg, cand_geom, (size_t)n_cand * 4, &dcg)) ||
+        (rc = to_device(c, s_ij, cand_ij, (size_t)n_cand * 16, &dij)) || (rc = s_cls.reserve((size_t)n_cand)))
+        return done(rc);
+    tessgpu::ClassifyArgs a;
+    a.xy = (const double*)dxy;
+    a.ring_offsets = (const int64_t*)dro;
+    a.part_rings = (const int64_t*)dpr;
+    a.geom_parts = (const int64_t*)dgp;
+    a.cand_geom = (const int32_t*)dcg;
+    a.cand_ij = (const int64_t*)dij;
+    a.n_cand = n_cand;
+    a.e = e;
+    a.eps = eps;
+    a.cls = (uint8_t*)s_cls.p;
+    const int64_t blocks = std::min<int64_t>((n_cand + 3) / 4, (int64_t)c->n_cu * 16);  // 4 waves per block
+    hipEvent_t t0, t1;
+    HIP_TRY(hipEventCreate(&t0));
+    HIP_TRY(hipEventCreate(&t1));
+    HIP_TRY(hipEventRecord(t0, c->stream));
+    hipLaunchKernelGGL(tessgpu::k_bng_tess_classify, dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(t1, c->stream));
+    HIP_TRY(hipMemcpyAsync(cls, s_cls.p, (size_t)n_cand, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, t0, t1);
+    c->last_tess_classify_ms = ms;
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    return done(MOSAIC_OK);
+}
+
+double mosaic_tess_last_classify_ms(const mosaic_ctx* c) { return c ? c->last_tess_classify_ms : -1.0; }
 
 }  // extern "C"

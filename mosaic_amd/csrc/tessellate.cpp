@@ -31,6 +31,10 @@
 using namespace mosaic;
 
 extern "C" int mosaic_tess_fail(int code, const char* msg);  // defined in mosaic_hip.hip
+extern "C" int mosaic_tess_classify_bng(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom_parts,
+                                        const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
+                                        int64_t n_cand, const int32_t* cand_geom, const int64_t* cand_ij, double e,
+                                        double eps, uint8_t* cls);  // mosaic_hip.hip
 
 namespace {
 
@@ -236,10 +240,12 @@ struct Cell {
 template <class ToGeo>
 void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::vector<std::vector<std::vector<P2>>>& pl,
                const std::vector<std::vector<std::vector<P2>>>& geo, double core_eps, int keep_core_geom,
-               ToGeo to_geo, double area_eps) {
+               ToGeo to_geo, double area_eps, int pre = -1) {
     // 1) any polygon segment near the cell?  2) cell centre inside?
-    bool near = false;
-    for (size_t pi = 0; pi < pl.size() && !near; pi++)
+    // pre >= 0: the class was computed on the GPU (k_bng_tess_classify: 0 dropped, 1 core, 2 border)
+    if (pre == 0) return;
+    bool near = pre == 2;
+    for (size_t pi = 0; pre < 0 && pi < pl.size() && !near; pi++)
         for (auto& ring : pl[pi])
             for (size_t i = 0; i + 1 < ring.size() && !near; i++)
                 if (seg_near_convex(ring[i], ring[i + 1], cell.clip, core_eps)) near = true;
@@ -251,8 +257,8 @@ void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::ve
     c.x /= cell.clip.size();
     c.y /= cell.clip.size();
     if (!near) {
-        bool inside = false;
-        for (auto& part : pl) inside = inside || point_in_rings_evenodd(c, part);
+        bool inside = pre == 1;
+        for (size_t pi = 0; pre < 0 && pi < pl.size(); pi++) inside = inside || point_in_rings_evenodd(c, pl[pi]);
         if (!inside) return;  // disjoint (or inside a hole)
         std::vector<uint8_t> blob;
         if (keep_core_geom) {
@@ -423,6 +429,85 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                               1e-12 * e * e);
                 }
         }
+    }
+    *out = cs;
+    return MOSAIC_OK;
+}
+
+// grid_tessellateexplode for the BNG grid with the per-cell classification (the O(segments x cells)
+// part of the producer) on the GPU (k_bng_tess_classify); border cells are clipped on the host
+// exactly as mosaic_tessellate does, so the chip set is identical row for row and byte for byte.
+int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
+                          const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
+                          int keep_core_geom, mosaic_chip_set** out) {
+    if (!ctx || !out || n_geoms < 0 || (n_geoms > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy)))
+        return mosaic_tess_fail(MOSAIC_E_ARG, "invalid argument");
+    if (grid != MOSAIC_GRID_BNG)
+        return mosaic_tess_fail(MOSAIC_E_ARG, "mosaic_tessellate_gpu: only the BNG grid is implemented");
+    if (!(res != 0 && res >= -6 && res <= 6))
+        return mosaic_tess_fail(MOSAIC_E_RES, ("BNG resolution not supported; found " + std::to_string(res)).c_str());
+    static const double edge_by_res[] = {0, 100000, 10000, 1000, 100, 10, 1};
+    const int ar = res < 0 ? -res : res;
+    double e = res > 0 ? edge_by_res[ar] : edge_by_res[ar - 1] / 2.0;  // negative res: quadrants
+    if (res == -1) e = 500000;
+    // candidates in mosaic_tessellate's order: geometry, then row j, then column i
+    std::vector<int32_t> cg;
+    std::vector<int64_t> cij, cid;
+    for (int64_t g = 0; g < n_geoms; g++) {
+        double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
+        bool any = false;
+        for (int64_t p = geom_parts[g]; p < geom_parts[g + 1]; p++)
+            for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++)
+                for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) {
+                    any = true;
+                    x0 = std::min(x0, xy[2 * v]);
+                    x1 = std::max(x1, xy[2 * v]);
+                    y0 = std::min(y0, xy[2 * v + 1]);
+                    y1 = std::max(y1, xy[2 * v + 1]);
+                }
+        if (!any) continue;
+        long ilo = (long)floor(x0 / e), ihi = (long)floor(x1 / e), jlo = (long)floor(y0 / e), jhi = (long)floor(y1 / e);
+        for (long j = jlo; j <= jhi; j++)
+            for (long i = ilo; i <= ihi; i++) {
+                double cx0 = i * e, cy0 = j * e;
+                int64_t id;
+                if (!bng::point_to_index(cx0 + 0.5 * e, cy0 + 0.5 * e, res, &id)) continue;
+                cg.push_back((int32_t)g);
+                cij.push_back(i);
+                cij.push_back(j);
+                cid.push_back(id);
+            }
+    }
+    const int64_t n_cand = (int64_t)cg.size();
+    std::vector<uint8_t> cls(n_cand);
+    int rc = mosaic_tess_classify_bng(ctx, n_geoms, geom_parts, part_rings, ring_offsets, xy, n_cand, cg.data(),
+                                      cij.data(), e, 1e-9 * e, cls.data());
+    if (rc) return rc;
+    mosaic_chip_set* cs = new mosaic_chip_set();
+    std::vector<std::vector<std::vector<P2>>> geo;
+    int64_t cur = -1;
+    for (int64_t k = 0; k < n_cand; k++) {
+        if (!cls[k]) continue;
+        if (cg[k] != cur) {
+            cur = cg[k];
+            geo.clear();
+            for (int64_t p = geom_parts[cur]; p < geom_parts[cur + 1]; p++) {
+                std::vector<std::vector<P2>> rings;
+                for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
+                    std::vector<P2> ring;
+                    for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) ring.push_back({xy[2 * v], xy[2 * v + 1]});
+                    rings.push_back(std::move(ring));
+                }
+                geo.push_back(std::move(rings));
+            }
+        }
+        Cell cell;
+        const double cx0 = cij[2 * k] * e, cy0 = cij[2 * k + 1] * e;
+        cell.clip = {{cx0, cy0}, {cx0 + e, cy0}, {cx0 + e, cy0 + e}, {cx0, cy0 + e}};
+        cell.outline = cell.clip;
+        cell.id = cid[k];
+        emit_cell(cs, (int32_t)cur, cell, geo, geo, 1e-9 * e, keep_core_geom, [](P2 h) { return h; }, 1e-12 * e * e,
+                  (int)cls[k]);
     }
     *out = cs;
     return MOSAIC_OK;

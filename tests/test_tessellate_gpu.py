@@ -1,0 +1,101 @@
+"""grid_tessellateexplode (BNG) with the cell classification on the GPU: parity with the host producer.
+
+mosaic_tessellate_gpu classifies every candidate cell (border / core / dropped) with
+k_bng_tess_classify and clips border cells on the host; mosaic_tessellate does all of it on the
+host.  The chip sets must agree row for row and byte for byte (is_core, index_id, polygon key,
+WKB).  The host producer itself is pinned against the reference's chip-join == brute-force
+invariant (MosaicFrameBehaviors.scala:136-223) in test_tessellate.py, and the chip join over the
+GPU-produced chips is checked against the brute-force oracle here as well.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+from mosaic_amd import MosaicContext
+from mosaic_amd.context import tessellate
+from mosaic_amd.data import PolygonSet
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = MosaicContext.build("BNG", "JTS")
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def london_m():
+    # planar stand-in coordinates (metres) for the BNG grid, as in test_tessellate.py
+    lon = PolygonSet.load("london_postcode_zones")
+    xy = (lon.xy - lon.xy.min(0)) * 1e5 + np.array([500000.0, 150000.0])
+    return PolygonSet(xy, lon.ring_offsets, lon.part_rings, lon.geom_parts)
+
+
+def _same(a, b):
+    assert len(a["index_id"]) == len(b["index_id"])
+    for k in ("is_core", "index_id", "polygon_key"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["wkb"][0], b["wkb"][0])
+    assert np.array_equal(a["wkb"][1], b["wkb"][1])
+
+
+@pytest.mark.parametrize("res", [3, -3, 4])
+def test_bng_gpu_tessellation_equals_host(ctx, london_m, res):
+    polys = london_m if res != 4 else london_m.subset(range(0, 177, 4))
+    t0 = time.perf_counter()
+    host = tessellate("BNG", polys, res)
+    t1 = time.perf_counter()
+    gpu = tessellate("BNG", polys, res, ctx=ctx)
+    t2 = time.perf_counter()
+    _same(host, gpu)
+    assert len(host["index_id"]) > 100 and (host["is_core"] == 0).sum() > 0
+    if res == 4:  # 100 m cells: postcode interiors hold core cells
+        assert host["is_core"].sum() > 0
+    from mosaic_amd import _native as N
+
+    ms = N.lib().mosaic_tess_last_classify_ms(ctx.handle)
+    print(f"res {res}: {len(host['index_id'])} chips, host {t1 - t0:.3f} s, gpu path {t2 - t1:.3f} s "
+          f"(classify kernel {ms:.3f} ms)")
+
+
+def test_bng_gpu_tessellation_join_invariant(ctx, london_m):
+    polys = london_m.subset(range(0, 177, 5))
+    chips = tessellate("BNG", polys, 3, ctx=ctx)
+    rng = np.random.default_rng(7)
+    x0, y0, x1, y1 = polys.bbox()
+    x = rng.uniform(x0, x1, 40_000)
+    y = rng.uniform(y0, y1, 40_000)
+    want, total_bf = oracle.brute_force_count(polys, x, y)
+    offs, data = chips["wkb"]
+    o = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+             wkb_offsets=offs, wkb=data)
+    got, _ = oracle.pip_join(o, oracle.GRID_BNG, 3, x, y, len(polys), threads=8)
+    assert np.array_equal(got, want) and total_bf > 1000
+
+
+def test_bng_gpu_tessellation_holes_multipart_empty(ctx):
+    # geometry 0: 3.5 km square with a 1.2 km hole; geometry 1: empty; geometry 2: two parts
+    sq = lambda x0, y0, s: [(x0, y0), (x0 + s, y0), (x0 + s, y0 + s), (x0, y0 + s), (x0, y0)]
+    rings = [sq(530250.0, 180250.0, 3500.0), sq(531100.0, 181100.0, 1200.0)[::-1],
+             sq(540000.0, 170000.0, 900.0), sq(542500.0, 171500.0, 2100.0)]
+    xy = np.array([p for r in rings for p in r], np.float64)
+    ring_offsets = np.cumsum([0] + [len(r) for r in rings]).astype(np.int64)
+    part_rings = np.array([0, 2, 3, 4], np.int64)
+    geom_parts = np.array([0, 1, 1, 3], np.int64)
+    polys = PolygonSet(xy, ring_offsets, part_rings, geom_parts)
+    for res in (3, 4, -4):
+        for keep in (True, False):
+            _same(tessellate("BNG", polys, res, keep_core_geom=keep),
+                  tessellate("BNG", polys, res, keep_core_geom=keep, ctx=ctx))
+    chips = tessellate("BNG", polys, 3, ctx=ctx)
+    assert set(chips["polygon_key"].tolist()) == {0, 2}
+
+
+def test_gpu_tessellation_rejects_h3(ctx):
+    z = PolygonSet.load("nyc_taxi_zones_35").subset([0])
+    with pytest.raises(Exception, match="only the BNG grid"):
+        tessellate("H3", z, 9, ctx=ctx)
