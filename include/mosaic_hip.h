@@ -204,16 +204,18 @@ int mosaic_chip_set_info(const mosaic_chip_set* cs, int64_t* n_chips, int64_t* w
 int mosaic_chip_set_export(const mosaic_chip_set* cs, uint8_t* is_core, int64_t* index_id, int32_t* key,
                            int64_t* wkb_offsets, uint8_t* wkb);
 int mosaic_chip_set_destroy(mosaic_chip_set* cs);
-/* grid_tessellateexplode (BNG) with the cell classification on the GPU: the same chip set as
- * mosaic_tessellate (BNG), row for row.  Each candidate cell of a geometry's envelope is classified
- * by k_bng_tess_classify (border: a segment within 1e-9 e of the cell square; core: centre inside;
- * else dropped), replacing the per-cell JTS buffer/intersects of IndexSystem.getBorderChips /
- * getCoreChips (core/index/IndexSystem.scala:152-186, via Mosaic.mosaicFill core/Mosaic.scala:60-87);
- * border cells are clipped on the host.  H3 returns MOSAIC_E_ARG. */
+/* grid_tessellateexplode with the cell classification on the GPU: the same chip set as
+ * mosaic_tessellate, row for row and byte for byte.  Each candidate cell of a geometry's envelope is
+ * classified on the GPU (border: a ring segment within eps of the cell; core: cell centre inside
+ * the part, even-odd; else dropped), replacing the per-cell JTS buffer / intersects of
+ * IndexSystem.getBorderChips / getCoreChips (core/index/IndexSystem.scala:152-186, via
+ * Mosaic.mosaicFill core/Mosaic.scala:60-87).  BNG: k_bng_tess_classify on the cell squares; H3:
+ * k_tess_classify_poly on the (densify-subdivided) hexagons in the icosahedron face plane.  Border
+ * cells are clipped on the host.  Errors as mosaic_tessellate. */
 int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
                           const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
-                          int keep_core_geom, mosaic_chip_set** out);
-/* Duration (HIP events on the context stream) of the last k_bng_tess_classify launch, ms. */
+                          int keep_core_geom, int densify, mosaic_chip_set** out);
+/* Duration (HIP events on the context stream) of the last classification launch, ms. */
 double mosaic_tess_last_classify_ms(const mosaic_ctx* ctx);
 
 /* ---- st_contains per row ---- */

@@ -121,7 +121,7 @@ def lib():
         "mosaic_cell_kring": ([vp, i32, vp, vp, i64, i32, i32, vp, vp], i32),
         "mosaic_bng_format_column": ([vp, vp, vp, i64, vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_cell_boundary_wkb": ([vp, i32, vp, vp, i64, vp], i32),
-        "mosaic_tessellate_gpu": ([vp, i32, i32, i64, vp, vp, vp, vp, i32, ctypes.POINTER(vp)], i32),
+        "mosaic_tessellate_gpu": ([vp, i32, i32, i64, vp, vp, vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
         "mosaic_tess_last_classify_ms": ([vp], ctypes.c_double),
     }
     for name, (args, res) in sig.items():

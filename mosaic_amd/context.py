@@ -548,8 +548,8 @@ class MosaicContext:
 def tessellate(index_system, polygons, resolution, keep_core_geom=True, densify=1, ctx=None):
     """grid_tessellateexplode over a PolygonSet (mosaic_amd.data.PolygonSet).
 
-    ctx=None: the host producer (mosaic_tessellate).  ctx=MosaicContext (BNG only): the cell
-    classification runs on the context's GPU (mosaic_tessellate_gpu), same chip set row for row.
+    ctx=None: the host producer (mosaic_tessellate).  ctx=MosaicContext: the cell classification
+    runs on the context's GPU (mosaic_tessellate_gpu), same chip set row for row.
 
     Returns chip columns: dict(is_core uint8, index_id int64, polygon_key int32 (geometry index),
     wkb=(offsets int64[n+1], data uint8[...])).  MosaicExplode.scala:70-79 / Mosaic.scala:21-87.
@@ -562,7 +562,7 @@ def tessellate(index_system, polygons, resolution, keep_core_geom=True, densify=
         N.check(N.lib().mosaic_tessellate_gpu(ctx.handle, index_system.grid, res, len(polygons),
                                               N.ptr(polygons.geom_parts), N.ptr(polygons.part_rings),
                                               N.ptr(polygons.ring_offsets), N.ptr(polygons.xy),
-                                              int(bool(keep_core_geom)), ctypes.byref(h)))
+                                              int(bool(keep_core_geom)), int(densify), ctypes.byref(h)))
     else:
         N.check(N.lib().mosaic_tessellate(index_system.grid, res, len(polygons), N.ptr(polygons.geom_parts),
                                           N.ptr(polygons.part_rings), N.ptr(polygons.ring_offsets),

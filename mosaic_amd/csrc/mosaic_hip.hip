@@ -3657,3 +3657,169 @@ int mosaic_tess_classify_bng(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom
 double mosaic_tess_last_classify_ms(const mosaic_ctx* c) { return c ? c->last_tess_classify_ms : -1.0; }
 
 }  // extern "C"
+
+// ---- grid_tessellateexplode (H3): the same classification against a per-cell convex clip polygon ----
+// The host producer classifies an H3 cell in its icosahedron face's gnomonic hex2d plane against the
+// (densified) hexagon (tessellate.cpp, mosaic_tessellate H3 branch).  The hexagon vertices are
+// computed on the host (glibc cos/sin) and passed per candidate, so the device test reads exactly the
+// host's operands; rings arrive already projected into the face plane.
+namespace tessgpu {
+
+__device__ inline bool seg_near_poly(double px, double py, double qx, double qy, const double* P, int nv, double eps) {
+    // tessellate.cpp seg_near_convex over the open ccw vertex list P[0..nv)
+    auto inside = [&](double rx, double ry) {
+        for (int i = 0; i < nv; i++) {
+            const int k = i + 1 == nv ? 0 : i + 1;
+            double ax = P[2 * i], ay = P[2 * i + 1], bx = P[2 * k], by = P[2 * k + 1];
+            double ex = bx - ax, ey = by - ay, len = sqrt(ex * ex + ey * ey);
+            if ((ex * (ry - ay) - ey * (rx - ax)) / len < -eps) return false;
+        }
+        return true;
+    };
+    if (inside(px, py) || inside(qx, qy)) return true;
+    auto dist_seg = [](double rx, double ry, double ax, double ay, double bx, double by) {
+        double ex = bx - ax, ey = by - ay;
+        double t = ((rx - ax) * ex + (ry - ay) * ey) / (ex * ex + ey * ey);
+        t = fmax(0.0, fmin(1.0, t));
+        double dx = ax + t * ex - rx, dy = ay + t * ey - ry;
+        return sqrt(dx * dx + dy * dy);
+    };
+    for (int i = 0; i < nv; i++) {
+        const int k = i + 1 == nv ? 0 : i + 1;
+        double ax = P[2 * i], ay = P[2 * i + 1], bx = P[2 * k], by = P[2 * k + 1];
+        double d1 = (bx - ax) * (py - ay) - (by - ay) * (px - ax);
+        double d2 = (bx - ax) * (qy - ay) - (by - ay) * (qx - ax);
+        double d3 = (qx - px) * (ay - py) - (qy - py) * (ax - px);
+        double d4 = (qx - px) * (by - py) - (qy - py) * (bx - px);
+        if (((d1 > 0) != (d2 > 0)) && ((d3 > 0) != (d4 > 0))) return true;
+        if (dist_seg(ax, ay, px, py, qx, qy) < eps || dist_seg(px, py, ax, ay, bx, by) < eps ||
+            dist_seg(qx, qy, ax, ay, bx, by) < eps)
+            return true;
+    }
+    return false;
+}
+
+struct ClassifyPolyArgs {
+    const double* xy;  // ring vertices in the clip plane, interleaved
+    const int64_t* ring_offsets;
+    const int64_t* part_rings;
+    const int64_t* geom_parts;
+    const int32_t* cand_geom;
+    const double* clip;  // [n_cand][nv][2]
+    int nv;
+    int64_t n_cand;
+    double eps;
+    uint8_t* cls;
+};
+
+__global__ void __launch_bounds__(256) k_tess_classify_poly(ClassifyPolyArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < a.n_cand; c += n_waves) {
+        const int g = a.cand_geom[c];
+        const double* P = a.clip + 2 * (int64_t)a.nv * c;
+        const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
+        bool near = false;
+        for (int64_t p = p0; p < p1 && !near; p++)
+            for (int64_t r = a.part_rings[p]; r < a.part_rings[p + 1]; r++) {
+                const int64_t b = a.ring_offsets[r], n = a.ring_offsets[r + 1] - b;
+                bool hit = false;
+                for (int64_t v = lane; v + 1 < n && !hit; v += 64) {
+                    const double* s = a.xy + 2 * (b + v);
+                    hit = seg_near_poly(s[0], s[1], s[2], s[3], P, a.nv, a.eps);
+                }
+                if (__ballot(hit)) {
+                    near = true;
+                    break;
+                }
+            }
+        uint8_t out = 2;
+        if (!near) {
+            double cx = 0, cy = 0;  // centroid of the clip vertex list, summed in order as the host does
+            for (int i = 0; i < a.nv; i++) {
+                cx += P[2 * i];
+                cy += P[2 * i + 1];
+            }
+            cx /= (double)a.nv;
+            cy /= (double)a.nv;
+            bool inside = false;
+            for (int64_t p = p0; p < p1 && !inside; p++) {
+                bool par = false;
+                for (int64_t r = a.part_rings[p]; r < a.part_rings[p + 1]; r++) {
+                    const int64_t b = a.ring_offsets[r], n = a.ring_offsets[r + 1] - b;
+                    for (int64_t i = lane; i < n; i += 64) {
+                        const int64_t j = i == 0 ? n - 1 : i - 1;
+                        const double ix = a.xy[2 * (b + i)], iy = a.xy[2 * (b + i) + 1];
+                        const double jx = a.xy[2 * (b + j)], jy = a.xy[2 * (b + j) + 1];
+                        if (((iy > cy) != (jy > cy)) && (cx < (jx - ix) * (cy - iy) / (jy - iy) + ix)) par = !par;
+                    }
+                }
+                inside = (__popcll(__ballot(par)) & 1) != 0;
+            }
+            out = inside ? 1 : 0;
+        }
+        if (lane == 0) a.cls[c] = out;
+    }
+}
+
+}  // namespace tessgpu
+
+extern "C" {
+
+// Classification step of mosaic_tessellate_gpu for per-cell convex clip polygons (H3 hexagons in the
+// face plane); not part of the public header.  xy holds the rings already in the clip plane.
+int mosaic_tess_classify_poly(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                              const int64_t* ring_offsets, const double* xy, int64_t n_cand, const int32_t* cand_geom,
+                              const double* clip, int nv, double eps, uint8_t* cls) {
+    if (!c || n_geoms < 0 || n_cand < 0 || nv < 3 ||
+        (n_cand > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy || !cand_geom || !clip || !cls)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    if (n_cand == 0) return MOSAIC_OK;
+    for (int64_t k = 0; k < n_cand; k++)
+        if (cand_geom[k] < 0 || cand_geom[k] >= n_geoms) return fail(MOSAIC_E_ARG, "candidate geometry out of range");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t n_parts = geom_parts[n_geoms], n_rings = part_rings[n_parts], n_verts = ring_offsets[n_rings];
+    DevBuf s_gp, s_pr, s_ro, s_xy, s_cg, s_clip, s_cls;
+    auto done = [&](int rc) {
+        for (DevBuf* b : {&s_gp, &s_pr, &s_ro, &s_xy, &s_cg, &s_clip, &s_cls}) b->release();
+        return rc;
+    };
+    int rc;
+    const void *dgp, *dpr, *dro, *dxy, *dcg, *dclip;
+    if ((rc = to_device(c, s_gp, geom_parts, (size_t)(n_geoms + 1) * 8, &dgp)) ||
+        (rc = to_device(c, s_pr, part_rings, (size_t)(n_parts + 1) * 8, &dpr)) ||
+        (rc = to_device(c, s_ro, ring_offsets, (size_t)(n_rings + 1) * 8, &dro)) ||
+        (rc = to_device(c, s_xy, xy, (size_t)std::max<int64_t>(n_verts, 1) * 16, &dxy)) ||
+        (rc = to_device(c, s_cg, cand_geom, (size_t)n_cand * 4, &dcg)) ||
+        (rc = to_device(c, s_clip, clip, (size_t)n_cand * nv * 16, &dclip)) || (rc = s_cls.reserve((size_t)n_cand)))
+        return done(rc);
+    tessgpu::ClassifyPolyArgs a;
+    a.xy = (const double*)dxy;
+    a.ring_offsets = (const int64_t*)dro;
+    a.part_rings = (const int64_t*)dpr;
+    a.geom_parts = (const int64_t*)dgp;
+    a.cand_geom = (const int32_t*)dcg;
+    a.clip = (const double*)dclip;
+    a.nv = nv;
+    a.n_cand = n_cand;
+    a.eps = eps;
+    a.cls = (uint8_t*)s_cls.p;
+    const int64_t blocks = std::min<int64_t>((n_cand + 3) / 4, (int64_t)c->n_cu * 16);
+    hipEvent_t t0, t1;
+    HIP_TRY(hipEventCreate(&t0));
+    HIP_TRY(hipEventCreate(&t1));
+    HIP_TRY(hipEventRecord(t0, c->stream));
+    hipLaunchKernelGGL(tessgpu::k_tess_classify_poly, dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(t1, c->stream));
+    HIP_TRY(hipMemcpyAsync(cls, s_cls.p, (size_t)n_cand, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, t0, t1);
+    c->last_tess_classify_ms = ms;
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    return done(MOSAIC_OK);
+}
+
+}  // extern "C"

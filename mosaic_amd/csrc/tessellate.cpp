@@ -35,6 +35,10 @@ extern "C" int mosaic_tess_classify_bng(mosaic_ctx* c, int64_t n_geoms, const in
                                         const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
                                         int64_t n_cand, const int32_t* cand_geom, const int64_t* cand_ij, double e,
                                         double eps, uint8_t* cls);  // mosaic_hip.hip
+extern "C" int mosaic_tess_classify_poly(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom_parts,
+                                         const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
+                                         int64_t n_cand, const int32_t* cand_geom, const double* clip, int nv,
+                                         double eps, uint8_t* cls);  // mosaic_hip.hip
 
 namespace {
 
@@ -434,16 +438,127 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
     return MOSAIC_OK;
 }
 
-// grid_tessellateexplode for the BNG grid with the per-cell classification (the O(segments x cells)
+// H3 branch of mosaic_tessellate_gpu: candidates, hexagon clip polygons and face-plane rings exactly as
+// mosaic_tessellate's H3 branch builds them; the classification runs in k_tess_classify_poly.
+static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const int64_t* geom_parts,
+                             const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
+                             int keep_core_geom, int densify, mosaic_chip_set** out) {
+    if (res < 0 || res > 15)
+        return mosaic_tess_fail(MOSAIC_E_RES, ("H3 resolution has to be between 0 and 15; found " + std::to_string(res)).c_str());
+    if (densify < 1 || densify > 64) return mosaic_tess_fail(MOSAIC_E_ARG, "densify must be in [1, 64]");
+    const int D = densify, nv = 6 * D;
+    const int64_t n_verts = n_geoms ? ring_offsets[part_rings[geom_parts[n_geoms]]] : 0;
+    std::vector<double> pxy((size_t)std::max<int64_t>(n_verts, 1) * 2);
+    std::vector<int> gface(n_geoms, -1);
+    std::vector<int32_t> cg;
+    std::vector<double> clip;
+    std::vector<int64_t> cid;
+    const double s60 = 0.86602540378443864676, R = 0.57735026918962576451;
+    for (int64_t g = 0; g < n_geoms; g++) {
+        const int64_t v0 = ring_offsets[part_rings[geom_parts[g]]], v1 = ring_offsets[part_rings[geom_parts[g + 1]]];
+        if (v0 == v1) continue;
+        int face = -1;
+        for (int64_t v = v0; v < v1; v++) {
+            int f = face_of(xy[2 * v], xy[2 * v + 1]);
+            if (face < 0) face = f;
+            if (f != face)
+                return mosaic_tess_fail(MOSAIC_E_ARG, "geometry spans an icosahedron face edge "
+                                                      "(unsupported by the host tessellator)");
+        }
+        gface[g] = face;
+        FacePlane fp;
+        fp.init(face, res);
+        double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
+        for (int64_t v = v0; v < v1; v++) {
+            P2 p = fp.to_hex(xy[2 * v], xy[2 * v + 1]);
+            pxy[2 * v] = p.x;
+            pxy[2 * v + 1] = p.y;
+            x0 = std::min(x0, p.x);
+            x1 = std::max(x1, p.x);
+            y0 = std::min(y0, p.y);
+            y1 = std::max(y1, p.y);
+        }
+        int jlo = (int)floor(y0 / s60) - 2, jhi = (int)ceil(y1 / s60) + 2;
+        for (int j = jlo; j <= jhi; j++) {
+            int ilo = (int)floor(x0 + j * 0.5) - 2, ihi = (int)ceil(x1 + j * 0.5) + 2;
+            for (int i = ilo; i <= ihi; i++) {
+                double cx = i - 0.5 * j, cy = j * s60;
+                if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
+                P2 corners[6];
+                for (int k = 0; k < 6; k++) {
+                    double ang = (30.0 + 60.0 * k) * (M_PI / 180.0);
+                    corners[k] = {cx + R * cos(ang), cy + R * sin(ang)};
+                }
+                for (int k = 0; k < 6; k++) {
+                    P2 a = corners[k], b = corners[(k + 1) % 6];
+                    for (int s = 0; s < D; s++) {
+                        clip.push_back(a.x + (b.x - a.x) * s / D);
+                        clip.push_back(a.y + (b.y - a.y) * s / D);
+                    }
+                }
+                h3::IJK ijk = {i, j, 0};
+                h3::ijk_normalize(ijk);
+                cg.push_back((int32_t)g);
+                cid.push_back((int64_t)h3::face_ijk_to_h3(face, ijk, res));
+            }
+        }
+    }
+    const int64_t n_cand = (int64_t)cg.size();
+    std::vector<uint8_t> cls(n_cand);
+    int rc = mosaic_tess_classify_poly(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), n_cand,
+                                       cg.data(), clip.data(), nv, 1e-3, cls.data());
+    if (rc) return rc;
+    mosaic_chip_set* cs = new mosaic_chip_set();
+    std::vector<std::vector<std::vector<P2>>> geo, pl;
+    FacePlane fp;
+    fp.init(0, res);  // re-initialised per geometry below
+    int64_t cur = -1;
+    for (int64_t k = 0; k < n_cand; k++) {
+        if (!cls[k]) continue;
+        if (cg[k] != cur) {
+            cur = cg[k];
+            fp.init(gface[cur], res);
+            geo.clear();
+            pl.clear();
+            for (int64_t p = geom_parts[cur]; p < geom_parts[cur + 1]; p++) {
+                std::vector<std::vector<P2>> rings, prings;
+                for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
+                    std::vector<P2> ring, pring;
+                    for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) {
+                        ring.push_back({xy[2 * v], xy[2 * v + 1]});
+                        pring.push_back({pxy[2 * v], pxy[2 * v + 1]});
+                    }
+                    rings.push_back(std::move(ring));
+                    prings.push_back(std::move(pring));
+                }
+                geo.push_back(std::move(rings));
+                pl.push_back(std::move(prings));
+            }
+        }
+        Cell cell;
+        const double* P = clip.data() + 2 * (size_t)nv * k;
+        for (int v = 0; v < nv; v++) cell.outline.push_back({P[2 * v], P[2 * v + 1]});
+        cell.clip = cell.outline;
+        cell.id = cid[k];
+        emit_cell(cs, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); }, 1e-12,
+                  (int)cls[k]);
+    }
+    *out = cs;
+    return MOSAIC_OK;
+}
+
+// grid_tessellateexplode with the per-cell classification (the O(segments x cells)
 // part of the producer) on the GPU (k_bng_tess_classify); border cells are clipped on the host
 // exactly as mosaic_tessellate does, so the chip set is identical row for row and byte for byte.
 int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
                           const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
-                          int keep_core_geom, mosaic_chip_set** out) {
+                          int keep_core_geom, int densify, mosaic_chip_set** out) {
     if (!ctx || !out || n_geoms < 0 || (n_geoms > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy)))
         return mosaic_tess_fail(MOSAIC_E_ARG, "invalid argument");
-    if (grid != MOSAIC_GRID_BNG)
-        return mosaic_tess_fail(MOSAIC_E_ARG, "mosaic_tessellate_gpu: only the BNG grid is implemented");
+    if (grid == MOSAIC_GRID_H3)
+        return tessellate_gpu_h3(ctx, res, n_geoms, geom_parts, part_rings, ring_offsets, xy, keep_core_geom, densify,
+                                 out);
+    if (grid != MOSAIC_GRID_BNG) return mosaic_tess_fail(MOSAIC_E_ARG, "unknown grid");
     if (!(res != 0 && res >= -6 && res <= 6))
         return mosaic_tess_fail(MOSAIC_E_RES, ("BNG resolution not supported; found " + std::to_string(res)).c_str());
     static const double edge_by_res[] = {0, 100000, 10000, 1000, 100, 10, 1};

@@ -95,7 +95,41 @@ def test_bng_gpu_tessellation_holes_multipart_empty(ctx):
     assert set(chips["polygon_key"].tolist()) == {0, 2}
 
 
-def test_gpu_tessellation_rejects_h3(ctx):
+@pytest.mark.parametrize("res,densify", [(8, 1), (9, 1), (9, 4), (10, 1)])
+def test_h3_gpu_tessellation_equals_host(ctx, res, densify):
+    zones = PolygonSet.load("nyc_taxi_zones")
+    polys = zones if res < 10 else zones.subset(range(0, 263, 3))
+    t0 = time.perf_counter()
+    host = tessellate("H3", polys, res, densify=densify)
+    t1 = time.perf_counter()
+    gpu = tessellate("H3", polys, res, densify=densify, ctx=ctx)
+    t2 = time.perf_counter()
+    _same(host, gpu)
+    assert host["is_core"].sum() > 0 and (host["is_core"] == 0).sum() > 0
+    from mosaic_amd import _native as N
+
+    ms = N.lib().mosaic_tess_last_classify_ms(ctx.handle)
+    print(f"H3 res {res} densify {densify}: {len(host['index_id'])} chips, host {t1 - t0:.3f} s, "
+          f"gpu path {t2 - t1:.3f} s (classify kernel {ms:.3f} ms)")
+
+
+def test_h3_gpu_tessellation_join_invariant(ctx):
+    z35 = PolygonSet.load("nyc_taxi_zones_35")
+    trips = np.load("tests/golden/nyctaxi_yellow_trips_pickups.npy")
+    chips = tessellate("H3", z35, 8, ctx=ctx)
+    want, total_bf = oracle.brute_force_count(z35, trips[:, 0], trips[:, 1])
+    offs, data = chips["wkb"]
+    o = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+             wkb_offsets=offs, wkb=data)
+    got, _ = oracle.pip_join(o, oracle.GRID_H3, 8, trips[:, 0], trips[:, 1], len(z35))
+    assert np.array_equal(got, want) and total_bf > 0
+
+
+def test_gpu_tessellation_errors(ctx):
+    from mosaic_amd import IllegalStateException
+
     z = PolygonSet.load("nyc_taxi_zones_35").subset([0])
-    with pytest.raises(Exception, match="only the BNG grid"):
-        tessellate("H3", z, 9, ctx=ctx)
+    with pytest.raises(IllegalStateException, match="found 16"):
+        tessellate("H3", z, 16, ctx=ctx)
+    with pytest.raises(IllegalStateException, match="BNG resolution not supported"):
+        tessellate("BNG", z, 0, ctx=ctx)
