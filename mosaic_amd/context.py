@@ -429,6 +429,13 @@ class MosaicContext:
         return out.astype(bool)
 
     # ---- the chip join ----
+    def grid_tessellateexplode(self, polygons, resolution, keep_core_geom=True, densify=1):
+        """grid_tessellateexplode(geom, res, keepCoreGeom) (MosaicContext.scala functions ->
+        MosaicExplode.scala:70-79 -> Mosaic.getChips core/Mosaic.scala:21-87) over a PolygonSet:
+        chip columns (is_core, index_id, polygon_key, wkb) with the cell classification on this
+        context's GPU (mosaic_tessellate_gpu)."""
+        return tessellate(self.index_system, polygons, resolution, keep_core_geom, densify, ctx=self)
+
     def chip_table(self, is_core, index_id, wkb_list, polygon_key, resolution, n_polygons=None):
         """Build side: rows of grid_tessellateexplode output (MosaicExplode.scala:70-79)."""
         self.resolution_of_table = self.index_system.get_resolution(resolution)

@@ -113,16 +113,25 @@ def test_h3_gpu_tessellation_equals_host(ctx, res, densify):
           f"gpu path {t2 - t1:.3f} s (classify kernel {ms:.3f} ms)")
 
 
-def test_h3_gpu_tessellation_join_invariant(ctx):
+def test_h3_gpu_tessellation_join_invariant():
+    # MosaicFrameBehaviors.scala:136-223 shape: 98 trips x 35 zones, H3 res 8, through the
+    # MosaicContext mirror (grid_tessellateexplode) and the GPU chip join
     z35 = PolygonSet.load("nyc_taxi_zones_35")
     trips = np.load("tests/golden/nyctaxi_yellow_trips_pickups.npy")
-    chips = tessellate("H3", z35, 8, ctx=ctx)
+    h3 = MosaicContext.build("H3", "JTS")
+    chips = h3.grid_tessellateexplode(z35, 8)
+    table = h3.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 8,
+                          n_polygons=len(z35))
+    gpu_counts = h3.pip_join_count(table, trips[:, 0], trips[:, 1])
+    table.close()
+    h3.close()
     want, total_bf = oracle.brute_force_count(z35, trips[:, 0], trips[:, 1])
     offs, data = chips["wkb"]
     o = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
              wkb_offsets=offs, wkb=data)
     got, _ = oracle.pip_join(o, oracle.GRID_H3, 8, trips[:, 0], trips[:, 1], len(z35))
     assert np.array_equal(got, want) and total_bf > 0
+    assert np.array_equal(np.asarray(gpu_counts), want)
 
 
 def test_gpu_tessellation_errors(ctx):
