@@ -41,6 +41,16 @@ def test_no_gpu_init_fails_cleanly():
     assert b"device" in N.lib().mosaic_last_error()
 
 
+def test_tessellate_gpu_argument_checks():
+    # no context (no GPU here): the GPU producer refuses before any device work
+    h = ctypes.c_void_p()
+    z = np.zeros(2, np.int64)
+    rc = N.lib().mosaic_tessellate_gpu(None, N.GRID_BNG, 3, 1, N.ptr(z), N.ptr(z), N.ptr(z),
+                                       N.ptr(np.zeros(2)), 1, 1, ctypes.byref(h))
+    assert rc == N.MOSAIC_E_ARG and b"invalid argument" in N.lib().mosaic_last_error()
+    assert N.lib().mosaic_tess_last_classify_ms(None) == -1.0
+
+
 def test_resolution_validation_messages():
     out = ctypes.c_int(0)
     lib = N.lib()
