@@ -120,6 +120,15 @@ int mosaic_resolution_str(int grid, const char* res, int* out);
  * valid (nullable): 1 = row present; null rows give out_valid 0 and cell 0 (NullIntolerant). */
 int mosaic_point_to_cell(mosaic_ctx* ctx, int grid, int res, const double* x, const double* y,
                          const uint8_t* valid, int64_t n, int64_t* out_cell, uint8_t* out_valid);
+/* H3 cells from the exact path alone (h3_exact: the line-by-line H3 C v3.7 restatement with the
+ * glibc 2.35 libm restatement glibc_math.h) for every row, skipping the certified fast path;
+ * x = lon, y = lat (degrees).  Same answer as mosaic_point_to_cell; exists so the exact path can be
+ * checked against the reference on arbitrarily many rows. */
+int mosaic_point_to_cell_exact(mosaic_ctx* ctx, int res, const double* x, const double* y, int64_t n,
+                               int64_t* out_cell);
+/* Diagnostics: out[i] = the device's glibc restatement of fn(a[i]) / atan2(a[i], b[i]);
+ * fn 0 = sin, 1 = cos (both via sincos), 2 = tan, 3 = acos, 4 = atan2. */
+int mosaic_diag_libm(mosaic_ctx* ctx, int fn, const double* a, const double* b, int64_t n, double* out);
 /* grid_pointascellid over a point geometry column in Arrow binary / utf8 layout: row i is
  * data[offsets[i] .. offsets[i+1]); format = MOSAIC_GEOM_WKB / _WKT / _HEX, | MOSAIC_GEOM_OFFSETS32
  * for 32-bit offsets (default 64-bit).  Every row JTS 1.19 certainly reads as a non-empty Point is

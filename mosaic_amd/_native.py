@@ -36,7 +36,8 @@ EXPORTS = [
     "mosaic_tess_last_classify_ms", "mosaic_chip_set_info",
     "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_point_geom_to_cell",
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
-    "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb",
+    "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb", "mosaic_point_to_cell_exact",
+    "mosaic_diag_libm",
 ]
 
 GEOM_WKB = 0
@@ -123,6 +124,8 @@ def lib():
         "mosaic_cell_boundary_wkb": ([vp, i32, vp, vp, i64, vp], i32),
         "mosaic_tessellate_gpu": ([vp, i32, i32, i64, vp, vp, vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
         "mosaic_tess_last_classify_ms": ([vp], ctypes.c_double),
+        "mosaic_point_to_cell_exact": ([vp, i32, vp, vp, i64, vp], i32),
+        "mosaic_diag_libm": ([vp, i32, vp, vp, i64, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -19,7 +19,7 @@
 #include <math.h>
 #include <stdint.h>
 
-#include "crmath.h"
+#include "glibc_math.h"
 #include "x87.h"
 
 namespace mosaic {
@@ -248,21 +248,9 @@ MOSAIC_HD uint64_t face_ijk_to_h3(int face, IJK ijk, int res) {
 }
 
 // ---- exact path: H3 C v3.7 with x86-64 double / x87 long double semantics ----
-// libm: on the GPU (and in host builds with MOSAIC_H3_CRMATH) the correctly rounded functions of
-// crmath.h; the plain host build uses the system libm, exactly as the oracle does.
-#if defined(__HIP_DEVICE_COMPILE__) || defined(MOSAIC_H3_CRMATH)
-#define H3M_SIN crm::sin_cr
-#define H3M_COS crm::cos_cr
-#define H3M_TAN crm::tan_cr
-#define H3M_ACOS crm::acos_cr
-#define H3M_ATAN2 crm::atan2_cr
-#else
-#define H3M_SIN sin
-#define H3M_COS cos
-#define H3M_TAN tan
-#define H3M_ACOS acos
-#define H3M_ATAN2 atan2
-#endif
+// libm: glibc_math.h, the bit-exact restatement of the glibc 2.35 functions H3 C reaches on an
+// x86-64 host (sincos for every sin / cos pair, FMA-build acos / atan2 / tan), on the device and
+// in host builds alike.
 MOSAIC_HD double pos_angle_rads(double rads) {
     double tmp = (rads < 0.0) ? x87::add_ld(rads, H3LD_M_2PI_M, H3LD_M_2PI_E, false) : rads;
     if (rads >= H3LD_M_2PI_DUP) tmp = x87::add_ld(tmp, H3LD_M_2PI_M, H3LD_M_2PI_E, true);
@@ -274,10 +262,12 @@ MOSAIC_HD double sq(double v) { return v * v; }
 MOSAIC_HD uint64_t h3_exact(double lat, double lon, int res) {
     if (res < 0 || res > 15) return 0;
     if (!isfinite(lat) || !isfinite(lon)) return 0;
-    double r0 = H3M_COS(lat);
-    double pz = H3M_SIN(lat);
-    double px = H3M_COS(lon) * r0;
-    double py = H3M_SIN(lon) * r0;
+    // vec3d.c _geoToVec3d: r = cos(lat); z = sin(lat); x = cos(lon) * r; y = sin(lon) * r
+    double pz, r0, slon, clon;
+    glibc::sincos(lat, &pz, &r0);
+    glibc::sincos(lon, &slon, &clon);
+    double px = clon * r0;
+    double py = slon * r0;
     int face = 0;
     double sqd = sq(kH3FaceCenterPoint[0][0] - px) + sq(kH3FaceCenterPoint[0][1] - py) +
                  sq(kH3FaceCenterPoint[0][2] - pz);
@@ -290,19 +280,26 @@ MOSAIC_HD uint64_t h3_exact(double lat, double lon, int res) {
         }
     }
     double vx, vy;
-    double r = H3M_ACOS(1 - sqd / 2);
+    double r = glibc::acos(1 - sqd / 2);
     if (r < H3LD_EPSILON_DUP) {
         vx = vy = 0.0;
     } else {
+        // geoCoord.c _geoAzimuthRads(faceCenterGeo[face], g):
+        // atan2(cos(lat2) sin(lon2 - lon1), cos(lat1) sin(lat2) - sin(lat1) cos(lat2) cos(lon2 - lon1))
         double lat1 = kH3FaceCenterGeo[face][0], lon1 = kH3FaceCenterGeo[face][1];
-        double az = H3M_ATAN2(H3M_COS(lat) * H3M_SIN(lon - lon1), H3M_COS(lat1) * H3M_SIN(lat) - H3M_SIN(lat1) * H3M_COS(lat) * H3M_COS(lon - lon1));
+        double sdl, cdl, slat1, clat1;
+        glibc::sincos(lon - lon1, &sdl, &cdl);
+        glibc::sincos(lat1, &slat1, &clat1);
+        double az = glibc::atan2(r0 * sdl, clat1 * pz - slat1 * r0 * cdl);
         double theta = pos_angle_rads(kH3FaceAxesAzRadsCII[face][0] - pos_angle_rads(az));
         if (res & 1) theta = pos_angle_rads(x87::add_ld(theta, H3LD_M_AP7_ROT_RADS_M, H3LD_M_AP7_ROT_RADS_E, true));
-        r = H3M_TAN(r);
+        r = glibc::tan(r);  // r <= 0.6524 (face circumradius): inside glibc::tan's restated domain
         r /= kRes0UGnomonic;
         for (int i = 0; i < res; i++) r = x87::mul_ld(r, H3LD_M_SQRT7_M, H3LD_M_SQRT7_E);
-        vx = r * H3M_COS(theta);
-        vy = r * H3M_SIN(theta);
+        double st, ct;
+        glibc::sincos(theta, &st, &ct);
+        vx = r * ct;
+        vy = r * st;
     }
     double a1 = fabs(vx), a2 = fabs(vy);
     double x2 = x87::div_ld(a2, H3LD_M_SIN60_M, H3LD_M_SIN60_E);
@@ -311,7 +308,7 @@ MOSAIC_HD uint64_t h3_exact(double lat, double lon, int res) {
 }
 
 // ---- fast path ----
-// sin and cos of x, |x| <= pi + 1/128, to ~1 ulp: x = k/64 + r (exact), |r| <= 1/128, table
+// sin and cos of x, |x| < 201.5 / 64 (= pi + 0.0068), to ~1 ulp: x = k/64 + r (exact), |r| <= 1/128, table
 // values sin/cos(k/64) correctly rounded, short Taylor polynomials for r (truncation < 1e-21).
 MOSAIC_HD void fast_sincos(double x, double* s, double* c) {
     double kf = rint(x * 64.0);
@@ -409,14 +406,13 @@ MOSAIC_HD void fast_unit(double lat_deg, double lon_deg, double* px, double* py,
     const double d2r = 0.017453292519943295;
     double lat = lat_deg * d2r, lon = lon_deg * d2r;
     double slat, clat, slon, clon;
-    if (fabs(lon) <= 3.15 && fabs(lat) <= 3.15) {
+    // fast_sincos's table spans k / 64 for |k| <= 201, i.e. |x| < 201.5 / 64 = 3.1484375 (180.39 deg)
+    if (fabs(lon) < 3.1484375 && fabs(lat) < 3.1484375) {
         fast_sincos(lat, &slat, &clat);
         fast_sincos(lon, &slon, &clon);
-    } else {
-        slat = sin(lat);
-        clat = cos(lat);
-        slon = sin(lon);
-        clon = cos(lon);
+    } else {  // |lon| beyond 180.39 deg (or |lat| beyond): glibc's sincos, < 0.55 ulp on host and device
+        glibc::sincos(lat, &slat, &clat);
+        glibc::sincos(lon, &slon, &clon);
     }
     *px = clon * clat;
     *py = slon * clat;

@@ -1628,6 +1628,22 @@ __global__ void __launch_bounds__(256) k_cell_h3_exact(CellArgs a, int all_rows)
     }
 }
 
+// Diagnostics (mosaic_diag_libm): the exact path's libm restatement (glibc_math.h) per row.
+__global__ void __launch_bounds__(256) k_diag_libm(int fn, const double* a, const double* b, int64_t n, double* out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double s, c, r = 0.0;
+        switch (fn) {
+            case 0: glibc::sincos(a[i], &s, &c); r = s; break;
+            case 1: glibc::sincos(a[i], &s, &c); r = c; break;
+            case 2: r = glibc::tan(a[i]); break;
+            case 3: r = glibc::acos(a[i]); break;
+            default: r = glibc::atan2(a[i], b[i]); break;
+        }
+        out[i] = r;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_cell_bng(CellArgs a) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     bool nan_seen = false;
@@ -2220,6 +2236,52 @@ int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, cons
     if (n == 0) return MOSAIC_OK;
     HIP_TRY(hipSetDevice(c->device));
     return point_to_cell_impl(c, grid, res, x, y, valid, nullptr, n, out_cell, out_valid);
+}
+
+int mosaic_point_to_cell_exact(mosaic_ctx* c, int res, const double* x, const double* y, int64_t n,
+                               int64_t* out_cell) {
+    if (!c || (n > 0 && (!x || !y || !out_cell))) return fail(MOSAIC_E_ARG, "null argument");
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (!valid_res(MOSAIC_GRID_H3, res)) return res_error(MOSAIC_GRID_H3, res);
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    const void *dx, *dy;
+    if ((rc = to_device(c, c->stage_x, x, n * 8, &dx))) return rc;
+    if ((rc = to_device(c, c->stage_y, y, n * 8, &dy))) return rc;
+    bool dev_out = is_device_ptr(out_cell);
+    if (!dev_out && (rc = c->stage_out.reserve(n * 8))) return rc;
+    CellArgs a{};
+    a.x = (const double*)dx;
+    a.y = (const double*)dy;
+    a.n = n;
+    a.res = res;
+    a.jdk = c->jdk;
+    a.out = dev_out ? (long long*)out_cell : (long long*)c->stage_out.p;
+    hipLaunchKernelGGL(k_cell_h3_exact, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a, 1);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!dev_out) HIP_TRY(hipMemcpy(out_cell, a.out, n * 8, hipMemcpyDeviceToHost));
+    return MOSAIC_OK;
+}
+
+int mosaic_diag_libm(mosaic_ctx* c, int fn, const double* a, const double* b, int64_t n, double* out) {
+    if (!c || fn < 0 || fn > 4 || (n > 0 && (!a || !out || (fn == 4 && !b)))) return fail(MOSAIC_E_ARG, "bad argument");
+    if (n <= 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    const void *da, *db = nullptr;
+    if ((rc = to_device(c, c->stage_x, a, n * 8, &da))) return rc;
+    if (fn == 4 && (rc = to_device(c, c->stage_y, b, n * 8, &db))) return rc;
+    bool dev_out = is_device_ptr(out);
+    if (!dev_out && (rc = c->stage_out.reserve(n * 8))) return rc;
+    double* dout = dev_out ? out : (double*)c->stage_out.p;
+    hipLaunchKernelGGL(k_diag_libm, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, fn, (const double*)da,
+                       (const double*)db, n, dout);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!dev_out) HIP_TRY(hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost));
+    return MOSAIC_OK;
 }
 
 // Decode a point geometry column into c->dec_x / dec_y / dec_status (device); *n_rowpath = rows

@@ -37,6 +37,8 @@ def lib():
         L.oracle_to_radians.argtypes = [f64, i32]
         L.oracle_h3_point_to_index.restype = None
         L.oracle_h3_point_to_index.argtypes = [vp, vp, i64, i32, i32, vp]
+        L.oracle_libm_eval.restype = None
+        L.oracle_libm_eval.argtypes = [i32, vp, vp, i64, vp]
         L.oracle_h3_debug.restype = None
         L.oracle_h3_debug.argtypes = [f64, f64, i32, vp, vp, vp, vp]
         L.oracle_bng_point_to_index.restype = i64
@@ -87,6 +89,15 @@ def h3_geo_to_h3(lat_rad, lng_rad, res):
 
 def to_radians(deg, jdk=8):
     return lib().oracle_to_radians(deg, jdk)
+
+
+def libm_eval(fn, a, b=None):
+    """The host glibc functions H3 C calls: fn 0 sin, 1 cos (sincos), 2 tan, 3 acos, 4 atan2(a, b)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(a if b is None else b, dtype=np.float64)
+    out = np.empty_like(a)
+    lib().oracle_libm_eval(fn, _ptr(a), _ptr(b), a.shape[0], _ptr(out))
+    return out
 
 
 def h3_debug(lat_rad, lng_rad, res):

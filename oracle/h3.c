@@ -16,6 +16,7 @@
  * EPSILON), and glibc libm for the transcendental functions.
  * Build with -ffp-contract=off (oracle/Makefile).
  */
+#define _GNU_SOURCE /* sincos */
 #include <math.h>
 #include <stdint.h>
 
@@ -365,4 +366,23 @@ void oracle_h3_point_to_index(const double* lon, const double* lat, int64_t n, i
                               int64_t* out) {
     for (int64_t i = 0; i < n; i++)
         out[i] = oracle_h3_geo_to_h3(oracle_to_radians(lat[i], jdk), oracle_to_radians(lon[i], jdk), res);
+}
+
+/* The host libm H3 C reaches (glibc: sincos, tan, acos, atan2), row by row: the reference side of
+ * the device glibc restatement's parity test (mosaic_amd/csrc/glibc_math.h).
+ * fn 0 = sin and 1 = cos (both via sincos, as gcc compiles H3's sin / cos pairs), 2 = tan,
+ * 3 = acos, 4 = atan2(a, b). */
+void oracle_libm_eval(int fn, const double* a, const double* b, int64_t n, double* out) {
+    /* through a volatile pointer: with one output unused, gcc would rewrite sincos as sin / cos */
+    void (*volatile sc)(double, double*, double*) = sincos;
+    for (int64_t i = 0; i < n; i++) {
+        double s, c;
+        switch (fn) {
+            case 0: sc(a[i], &s, &c); out[i] = s; break;
+            case 1: sc(a[i], &s, &c); out[i] = c; break;
+            case 2: out[i] = tan(a[i]); break;
+            case 3: out[i] = acos(a[i]); break;
+            default: out[i] = atan2(a[i], b[i]); break;
+        }
+    }
 }

@@ -40,6 +40,8 @@ double oracle_to_radians(double deg, int jdk);
 void oracle_h3_point_to_index(const double* lon, const double* lat, int64_t n, int res, int jdk,
                               int64_t* out);
 /* Intermediate state of geoToH3 for diagnostics: face, hex2d x/y, res ijk. */
+/* The host libm H3 C reaches: fn 0 sin, 1 cos (via sincos), 2 tan, 3 acos, 4 atan2(a, b). */
+void oracle_libm_eval(int fn, const double* a, const double* b, int64_t n, double* out);
 void oracle_h3_debug(double lat_rad, double lng_rad, int res, int* face, double* x, double* y,
                      int* ijk);
 

@@ -163,3 +163,32 @@ def point_rows(rng, n=3000):
     rows += [(2, s) for s in [b"0101000000000000000000F03F00000000000000400", b"01010000000000000000000F03G000000000000000040",
                               b"", b"0"]]
     return rows
+
+
+def h3_cell_boundary_points(rng, n, res, lon_range=(-180.0, 180.0), lat_range=(-90.0, 90.0), iters=60):
+    """Points within an ulp of H3 cell boundaries at `res`, by bisection on the oracle's cells.
+
+    Pairs (p, p + d) with |d| about one cell edge that land in different cells are bisected until
+    the two ends are adjacent doubles (or `iters` halvings): both ends are returned, so every pair
+    straddles a boundary of the reference's own cells (edges, vertices where three cells meet, the
+    fold axes and face edges at coarse resolutions).  Returns (lon, lat) arrays (degrees)."""
+    import oracle
+
+    edge_deg = 0.0019 * 7 ** ((9 - res) / 2.0)  # ~ res-r hexagon edge in degrees of latitude
+    lon = rng.uniform(*lon_range, n)
+    lat = rng.uniform(*lat_range, n)
+    ang = rng.uniform(0, 2 * np.pi, n)
+    span = edge_deg * rng.uniform(0.3, 1.5, n)
+    lon2 = lon + span * np.cos(ang) / np.maximum(np.cos(np.radians(lat)), 0.05)
+    lat2 = np.clip(lat + span * np.sin(ang), -90.0, 90.0)
+    c0 = oracle.h3_point_to_index(lon, lat, res)
+    c1 = oracle.h3_point_to_index(lon2, lat2, res)
+    k = c0 != c1
+    ax, ay, bx, by, ca = lon[k], lat[k], lon2[k], lat2[k], c0[k]
+    for _ in range(iters):
+        mx, my = 0.5 * (ax + bx), 0.5 * (ay + by)
+        cm = oracle.h3_point_to_index(mx, my, res)
+        same = cm == ca
+        ax, ay = np.where(same, mx, ax), np.where(same, my, ay)
+        bx, by = np.where(same, bx, mx), np.where(same, by, my)
+    return np.concatenate([ax, bx]), np.concatenate([ay, by])

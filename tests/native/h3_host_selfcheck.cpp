@@ -21,8 +21,8 @@ int main(int argc, char** argv) {
     for (long i = 0; i < n; i++) {
         double lon, lat;
         int mode = i % 4;
-        if (mode == 0) {  // global uniform on the sphere
-            lon = -180.0 + 360.0 * u(rng);
+        if (mode == 0) {  // global uniform on the sphere, longitudes also beyond +-180 (valid input)
+            lon = (i & 8) ? -200.0 + 400.0 * u(rng) : -180.0 + 360.0 * u(rng);
             lat = asin(2.0 * u(rng) - 1.0) * 57.29577951308232;
         } else if (mode == 1) {  // NYC bbox
             lon = -74.25559136315209 + 0.5556 * u(rng);

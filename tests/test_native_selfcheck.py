@@ -1,6 +1,6 @@
 """CPU-only: the device H3 code (mosaic_amd/csrc/h3_device.h) compiled for the host must match the
-oracle bit for bit -- h3_exact everywhere (same glibc libm on both sides; validates the x87
-long-double emulation), h3_fast wherever it does not flag the point as ambiguous (validates the
+oracle bit for bit -- h3_exact everywhere (glibc_math.h's restatement of libm against the oracle's
+real glibc; validates the restatement and the x87 long-double emulation), h3_fast wherever it does not flag the point as ambiguous (validates the
 projective fast path, the face lookup table, the table sine/cosine and the margin bounds).
 Includes adversarial points built within 1e-9 hex units of cell edges, vertices and face centres."""
 import os
@@ -21,18 +21,17 @@ def test_device_h3_code_on_host(tmp_path, oracle_lib):
     assert ambiguous > 1000  # the adversarial quarter does exercise the exact path
 
 
-def test_device_exact_path_libm_divergence_is_bounded(tmp_path, oracle_lib):
-    """The GPU's exact path uses crmath.h (correctly rounded); the oracle uses glibc, which is not
-    correctly rounded for ~0.1-0.25 % of arguments.  Built with MOSAIC_H3_CRMATH on the host, the
-    device code must still agree with the oracle on every point the fast path certifies, and on
-    all but a small fraction of the (adversarial) points that reach the exact path."""
-    exe = tmp_path / "h3sc_cr"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wno-unknown-pragmas", "-DMOSAIC_H3_CRMATH",
-                    "-o", str(exe), os.path.join(ROOT, "tests", "native", "h3_host_selfcheck.cpp"),
-                    os.path.join(ROOT, "oracle", "liboracle.so"), f"-Wl,-rpath,{os.path.join(ROOT, 'oracle')}"],
-                   check=True)
-    out = subprocess.run([str(exe), "400000", "11"], check=True, capture_output=True, text=True).stdout.split()
-    bad_exact, bad_fast, ambiguous = map(int, out)
-    assert bad_fast == 0
-    assert ambiguous > 1000
-    assert bad_exact <= 0.002 * ambiguous, (bad_exact, ambiguous)
+def test_glibc_math_restatement_is_bit_exact(tmp_path):
+    """mosaic_amd/csrc/glibc_math.h (the exact path's sincos / tan / acos / atan2 on the device)
+    compiled for the host equals this image's glibc 2.35 libm bit for bit on 2e6 arguments per
+    function: H3's argument ranges, thresholds between glibc's branches, huge arguments
+    (__branred), zeros, infinities, NaN and random bit patterns."""
+    exe = tmp_path / "gmsc"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "native", "glibc_math_selfcheck.cpp"), "-lm"], check=True)
+    res = subprocess.run([str(exe), "2000000", "3"], capture_output=True, text=True)
+    rows = [line.split() for line in res.stdout.split("\n") if line.strip()]
+    assert {r[0] for r in rows} == {"sin", "cos", "tan", "acos", "atan2"}
+    for name, n, bad in rows:
+        assert int(n) > 1000000 and int(bad) == 0, (name, n, bad, res.stderr)
+    assert res.returncode == 0
