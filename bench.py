@@ -2,24 +2,29 @@
 
 Workload (BASELINE.json configs[1], the single-GPU config): 1e9 uniform synthetic points per GPU
 over the NYC taxi-zone bounding box, joined to the 263 taxi zones' res-9 chips
-(grid_tessellateexplode output, built once on the host), Quickstart semantics
+(grid_tessellateexplode output), Quickstart semantics
 (cell == chip.index_id && (is_core || st_contains(chip.wkb, point))), reduced to per-zone counts.
-A step = one pass of the fused join kernel over the resident batch (+ the exact-H3 pass for the
-rare ambiguous points); with N > 1 GPUs each rank owns its own 1e9-point shard (weak scaling) and
-the step ends with one RCCL all-reduce of the int64[263] counts.
+A step = one pass of the join over the resident batch (stream kernel, mixed-row kernel, exact-H3
+pass for the rare ambiguous points); with N > 1 GPUs each rank owns its own 1e9-point shard (weak
+scaling) and the step ends with one RCCL all-reduce of the int64[263] counts.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Rank 0 prints one JSON line.  `roofline` prices the fused join kernel against the HBM roofline of
-its 16 B/point algorithmic input stream (kernel time from HIP events on the launch stream);
-`cpu_baseline` times the CPU restatement (oracle/, "port") of the same join on a bounded sample.
+Without a torchrun environment, --gpus N > 1 relaunches itself under torch.distributed.run (before
+touching the GPU) and exits with its status.  Rank 0 prints one JSON line.  `roofline` prices the
+stream kernel against the HBM roofline of its 16 B/point algorithmic input stream (kernel time from
+HIP events on the launch stream); `cpu_baseline` times the CPU restatement (oracle/, "port") on a
+bounded prefix of the SAME device points, whose counts must equal the GPU's on that prefix
+(`parity`; the bench fails otherwise); `config.build_s` is the build side (tessellation + chip
+table with tile directory and point raster) and `end_to_end_points_per_s` one pass including it.
 """
 import argparse
 import glob
 import json
 import os
+import platform
 import subprocess
 import sys
 import time
@@ -31,57 +36,97 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_POINT = 16     # two float64 coordinates
-# the fused join kernel of the default pip_mode (3): k_join_tiled when the chip table has an H3 tile
-# directory (tiles.h), else k_join_raster; set in main() from the table
-JOIN_KERNEL = "k_join_tiled"
+JOIN_KERNEL = "k_join_stream"  # set in main() from the chip table
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--points-per-gpu", type=float, default=1e9)
     p.add_argument("--res", type=int, default=9)
-    p.add_argument("--cpu-sample", type=float, default=3e8, help="points for the CPU baseline (0 = skip)")
+    p.add_argument("--cpu-sample", type=float, default=2e8,
+                   help="prefix of the device points joined by the CPU oracle (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--pmc", type=int, default=1, help="1: measure HBM traffic with a rocprofv3 PMC child pass")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    p.add_argument("--block", type=int, default=256)
-    p.add_argument("--blocks-per-cu", type=int, default=8)
     return p.parse_args()
 
 
-def build_chips(res):
+def relaunch(args):
+    """--gpus N > 1 outside torchrun: run this script under torch.distributed.run as a child."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def host_info():
+    cpu = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    rocm = None
+    for path in ("/opt/rocm/.info/version", "/opt/rocm/.info/version-dev"):
+        try:
+            with open(path) as f:
+                rocm = f.read().strip()
+                break
+        except OSError:
+            pass
+    return {"cpu_model": cpu, "nproc": os.cpu_count(), "rocm": rocm}
+
+
+def build_chips(res, rank, world):
+    """Rank 0 tessellates; the chip rows go to the other ranks over the process group (one build
+    per node instead of one per rank)."""
     from mosaic_amd.context import tessellate
     from mosaic_amd.data import PolygonSet
 
     zones = PolygonSet.load("nyc_taxi_zones")
-    chips = tessellate("H3", zones, res)
-    return zones, chips
+    t0 = time.perf_counter()
+    chips = None
+    if rank == 0:
+        chips = tessellate("H3", zones, res)
+    if world > 1:
+        import torch.distributed as dist
+
+        obj = [chips]
+        dist.broadcast_object_list(obj, src=0)
+        chips = obj[0]
+    return zones, chips, time.perf_counter() - t0
 
 
-def cpu_baseline(zones, chips, res, n, threads):
-    """The oracle (C restatement of the reference's algorithm, pthreads) on a bounded sample."""
+def cpu_baseline(chips, res, n_zones, x, y, threads):
+    """The oracle (C restatement of the reference's algorithm, pthreads) on the given host points."""
     import oracle
-    from mosaic_amd.data import uniform_points
 
-    x, y = uniform_points(zones.bbox(), int(n), config=2)
     offs, data = chips["wkb"]
     oc = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
               wkb_offsets=offs, wkb=data)
     oracle.lib()
     t0 = time.perf_counter()
-    counts, total = oracle.pip_join(oc, oracle.GRID_H3, res, x, y, len(zones), threads=threads)
+    counts, total = oracle.pip_join(oc, oracle.GRID_H3, res, x, y, n_zones, threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": len(x) / dt, "unit": "points/s", "cores": threads, "kind": "port",
-            "sample": f"{len(x):.0f} uniform points over the NYC zone bbox, H3 res {res}, same chips "
-                      f"({total} pairs), {dt:.1f} s, CPU restatement (oracle/join.c), not Spark"}
+    return counts, total, dt
 
 
 def pmc_traffic(args):
-    """rocprofv3 PMC child pass (FETCH_SIZE / WRITE_SIZE only, its own run) on the same launch shape;
-    returns HBM bytes per fused-kernel launch with the gfx950 FETCH_SIZE x2 correction."""
+    """rocprofv3 PMC child pass (FETCH_SIZE / WRITE_SIZE only, each its own run) on the same launch
+    shape; returns HBM bytes per stream-kernel launch with the gfx950 FETCH_SIZE x2 correction."""
+    import csv
     import shutil
 
     exe = shutil.which("rocprofv3")
@@ -103,8 +148,6 @@ def pmc_traffic(args):
         if not files:
             return None, f"no counter csv for {counter}"
         vals = []
-        import csv
-
         for f in files:
             with open(f) as fh:
                 for row in csv.DictReader(fh):
@@ -121,27 +164,32 @@ def pmc_traffic(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
     import torch
     import torch.distributed as dist
 
     from mosaic_amd import distributed as D
 
     rank, world, local = D.init("nccl")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
     from mosaic_amd import MosaicContext
     from mosaic_amd.data import SEED_BASE, uniform_points_device
 
-    zones, chips = build_chips(args.res)
+    zones, chips, tess_s = build_chips(args.res, rank, world)
     ctx = MosaicContext.build("H3", "JTS", device=local)
-    ctx.set_option("block", args.block)
-    ctx.set_option("blocks_per_cu", args.blocks_per_cu)
+    t0 = time.perf_counter()
     table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
                            n_polygons=len(zones))
+    table_s = time.perf_counter() - t0
     global JOIN_KERNEL
     tiles = table.tiles()
-    JOIN_KERNEL = ("k_join_stream" if tiles["raster"] else "k_join_tiled") if tiles["built"] else "k_join_raster"
+    JOIN_KERNEL = ("k_join_stream" if tiles["stream"] else "k_join_tiled") if tiles["built"] else "k_join_raster"
     n = int(args.points_per_gpu)
     x, y = uniform_points_device(zones.bbox(), n, seed=SEED_BASE + 2 + 1000 * rank, device=dev)
     counts = torch.zeros(len(zones), dtype=torch.int64, device=dev)
@@ -153,6 +201,12 @@ def main():
         ctx.pip_join_count(table, x, y, out=counts)
         D.allreduce_counts(counts)
 
+    # one untimed first pass: the end-to-end (build + one join) figure
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    step()
+    torch.cuda.synchronize(dev)
+    first_pass_s = time.perf_counter() - t0
     for _ in range(args.warmup):
         step()
     ctx.sync()
@@ -178,11 +232,31 @@ def main():
     stats = ctx.last_stats()
     if args.pmc_child:
         return
+    # parity on the full-size workload: the CPU oracle on a prefix of the same device points
+    parity = None
+    cpu = None
+    if args.cpu_sample > 0 and rank == 0:
+        m = int(min(args.cpu_sample, n))
+        gpu_prefix = ctx.pip_join_count(table, x[:m], y[:m]).cpu().numpy()
+        hx, hy = x[:m].cpu().numpy(), y[:m].cpu().numpy()
+        want, total, dt = cpu_baseline(chips, args.res, len(zones), hx, hy, args.cpu_threads)
+        match = bool(np.array_equal(gpu_prefix, want))
+        parity = {"points": m, "pairs": int(total), "match": match,
+                  "against": "oracle/join.c (CPU restatement of the reference's join) on the first "
+                             f"{m} of this rank's device points"}
+        cpu = {"value": m / dt, "unit": "points/s", "cores": args.cpu_threads, "kind": "port",
+               "sample": f"the first {m:.0f} of the benchmarked device points (uniform over the NYC zone bbox), "
+                         f"H3 res {args.res}, same chips ({total} pairs), {dt:.1f} s, CPU restatement "
+                         "(oracle/join.c), not Spark"}
+        del hx, hy
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
+    if parity is not None and not parity["match"]:
+        print(json.dumps({"error": "GPU counts differ from the oracle on the parity prefix", "parity": parity}))
+        sys.exit(3)
 
     total_points = world * n * args.steps
     value = total_points / elapsed
@@ -194,10 +268,8 @@ def main():
             traffic, pmc_note = pmc_traffic(args)
         except Exception as e:  # the measurement is optional; never fail the bench on it
             traffic, pmc_note = None, f"pmc error: {e}"
-    cpu = None
-    if args.cpu_sample > 0 and world == 1:
-        cpu = cpu_baseline(zones, chips, args.res, args.cpu_sample, args.cpu_threads)
     info = table.info()
+    build_s = tess_s + table_s
     line = {
         "metric": "PIP-join points/sec (whole node) at H3 res 9, 1/2/4/8 MI355X vs CPU host",
         "value": value,
@@ -215,16 +287,23 @@ def main():
         "config": {"workload": "configs[1]: 1e9 uniform points per GPU vs 263 NYC taxi zones, H3 res "
                                f"{args.res}, Quickstart chip join reduced to per-zone counts",
                    "points_per_gpu": n, "res": args.res, "chips": info["n_chips"], "border_chips": info["n_border"],
-                   "chip_cells": info["n_cells"], "tile_directory": {k: tiles[k] for k in
-                                                                     ("built", "nx", "ny", "records", "entries")},
+                   "chip_cells": info["n_cells"],
+                   "tile_directory": {k: tiles[k] for k in ("built", "nx", "ny", "records", "entries")},
+                   "point_raster": {k: tiles[k] for k in ("raster", "raster_sub", "raster_cell", "quad_entries",
+                                                          "raster_bytes", "stream")},
                    "parallelism": f"dp{world}",
-                   "collective": "RCCL all_reduce int64[263] per step" if world > 1 else "none"},
+                   "collective": "RCCL all_reduce int64[263] per step" if world > 1 else "none",
+                   "build_s": round(build_s, 3), "tessellate_s": round(tess_s, 3), "chip_table_s": round(table_s, 3),
+                   "first_pass_s": round(first_pass_s, 4),
+                   "end_to_end_points_per_s": world * n / (build_s + elapsed / args.steps)},
+        "host": host_info(),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                      "traffic": traffic, "kernel": JOIN_KERNEL,
                      "kernel_ms": k_avg_ms, "algorithmic_bytes_per_launch": BYTES_PER_POINT * n,
                      "pmc": pmc_note},
         "cpu_baseline": cpu,
+        "parity": parity,
         "stats": {"exact_path_rows_per_step": stats["exact_path_rows"],
                   "contains_tests_per_step": stats["contains_tests"],
                   "pairs_per_step": int(check.sum().item())},

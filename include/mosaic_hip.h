@@ -38,9 +38,15 @@
  *   - Input arrays are borrowed for the duration of the call and may live in host memory or in
  *     device memory of the context's GPU (detected per pointer).  Host inputs are staged over PCIe.
  *   - Calls are synchronous unless the context option "async" is 1, in which case device-pointer
- *     calls only enqueue work on the context stream (mosaic_sync() waits and reports deferred errors).
- *   - A context is bound to one GPU; use one context per device (one process per GPU).  Calls on
- *     one context are serialised on its stream; distinct contexts may be used from distinct threads.
+ *     calls only enqueue work on the calling thread's stream (mosaic_sync() waits and reports
+ *     deferred errors).
+ *   - Threads: a context is bound to one GPU and every entry point is thread-safe (SURVEY.md §8(b),
+ *     the executor's task threads sharing one context; the reference's index systems are JVM
+ *     singletons, H3IndexSystem.scala:22-27).  Each calling thread gets its own HIP stream (created
+ *     on first use; mosaic_set_stream / mosaic_get_stream act on the calling thread's), scratch
+ *     buffers, counters (mosaic_last_stats) and timing events, so concurrent calls never share
+ *     state.  Options are shared by the context and copied once at the start of every call.  Chip
+ *     tables are immutable once created and may be joined from any thread.
  */
 #ifndef MOSAIC_HIP_H
 #define MOSAIC_HIP_H
@@ -78,31 +84,28 @@ const char* mosaic_last_error(void);
 int mosaic_init(int device, mosaic_ctx** out);
 int mosaic_destroy(mosaic_ctx* ctx);
 /* Options: "jdk" (8: Math.toRadians = deg / 180 * PI, the JDK 8 runtime of the reference's CI;
- * 9+: deg * DEGREES_TO_RADIANS), "async" (0/1), "block" (threads per block, multiple of 64),
- * "blocks_per_cu" (grid sizing), "timing" (0/1: HIP events around each join's main kernel; 2: the
- * point-raster join's mixed-cell kernel is timed as a second entry),
- * "pip_mode" (3 raster, 2 slab, 1 ring-cooperative, 0 lane-per-point contains strategy), "raster"
- * (raster cells per chip side, for tables built afterwards), "raster_adaptive" (0/1: rings with
- * few segments get 2 ceil(sqrt(segments)) cells a side instead, at most "raster"; default 1), "lane_edges", "tiles" (0/1: H3 tile
- * directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
+ * 9+: deg * DEGREES_TO_RADIANS), "async" (0/1), "block" (threads per block of the row kernels,
+ * multiple of 64), "blocks_per_cu" (grid sizing), "timing" (0/1: HIP events around each join's main
+ * kernel; 2: the point-raster join's mixed-cell kernel is timed as a second entry), "raster" (ray-parity
+ * raster cells per border chip side, 1..64, for tables built afterwards), "raster_adaptive" (0/1: rings
+ * with few segments get 2 ceil(sqrt(segments)) cells a side instead, at most "raster"; default 1),
+ * "lane_edges" (raster cell lists up to this long are evaluated by the owning lane), "tiles" (0/1: H3
+ * tile directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
  * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
- * side, a power of two, and cells per sub-block side, for tables built afterwards; default 64 /
+ * side and leaf cells per sub-block side, powers of two, for tables built afterwards; default 64 /
  * 16), "raster_lines" (0/1: sub-blocks crossed by one straight chip edge store a line record instead
- * of a leaf block; default 1), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768 entries, or an entry budget
- * <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of 64, default 512; the LDS
- * quad level is held once per workgroup), "stream_persistent" (0/1: k_join_stream launches only the workgroups that
- * are resident at once; default 0: blocks_per_cu x block threads per CU, measured faster),
- * "host_chunk" (rows per chunk when mosaic_pip_join_count gets host-resident coordinates: the next
- * chunk's copy overlaps the current chunk's join; 0 = stage the whole batch; default 2^25),
- * "tile_lds" (0/1: k_join_stream copies the raster's per-tile leaf-block bases to
- * LDS when the workgroup's LDS stays within 80 KiB), "stream_groups" (1/2), "mixed_rows" (1/2/4), "mixed_blocks_per_cu". */
+ * of a leaf block; default 1), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768
+ * entries, or an entry budget <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of
+ * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
+ * host-resident coordinates: the next chunk's copy overlaps the current chunk's join; 0 = stage the
+ * whole batch; default 2^25), "mixed_rows" (1/2/4), "mixed_blocks_per_cu". */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
-/* The hipStream_t work is enqueued on (owned by the context unless set). */
+/* The calling thread's hipStream_t (created by the context unless set by this thread). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
 int mosaic_set_stream(mosaic_ctx* ctx, void* stream);
 /* Wait for enqueued work; reports deferred errors of async calls. */
 int mosaic_sync(mosaic_ctx* ctx);
-/* Counters of the last join/index call: [0] rows that needed the exact H3 path,
+/* Counters of the calling thread's last join/index call: [0] rows that needed the exact H3 path,
  * [1] (point, border chip) contains tests, [2] matched pairs (pairs calls only).
  * Filled only by sync calls. */
 int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3);
@@ -182,10 +185,10 @@ int mosaic_chip_table_tiles(const mosaic_chips* chips, int64_t* out13);
 /* out4 = lon, lat of the tile grid origin and tiles per degree along lon, lat (tile i covers
  * [x0 + i / sx, x0 + (i + 1) / sx)). */
 int mosaic_chip_table_tile_grid(const mosaic_chips* chips, double* out4);
-/* Point raster detail: out4 = sub-blocks stored as line records (option "raster_lines"), LDS quad
+/* Point raster detail: out5 = sub-blocks stored as line records (option "raster_lines"), LDS quad
  * level entries (0: none), quad shift (sub-blocks per quad side = 1 << shift), raster bytes on the
- * device. */
-int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out4);
+ * device, 1 if joins run the stream kernel on it (quad level with compact copies, edges clamp-safe). */
+int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out5);
 
 /* ---- the join ---- */
 /* counts[p] = number of (point, chip) pairs with chip polygon_key p (overwritten). */

@@ -15,9 +15,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/mosaic_hip.h"
@@ -75,11 +78,6 @@ struct JoinArgs {
     const HashEntry* table;
     uint64_t mask;
     const uint32_t* chip_meta;  // (polygon_key << 1) | is_core, in table order
-    const uint2* chip_ring;     // (first vertex, n vertices) when chip = one Polygon with one ring, else (0, 0)
-    const double2* slab_geo;    // per chip: (y0, slabs / height) of its envelope
-    const uint2* slab_idx;      // per chip: (first slab offset, slab count K); K == 0: general path
-    const uint32_t* slab_off;   // edge-record range of slab s of a chip: [slab_off[b + s], slab_off[b + s + 1])
-    const pip::Edge* edges;     // per-slab segment records
     const raster::ChipHdr* hdr;     // per chip: envelope + ray-parity raster (raster.h)
     const raster::CellRec* cells;   // raster cells
     const pip::Edge* rast_edges;    // raster cell segment lists
@@ -96,12 +94,6 @@ struct JoinArgs {
     int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
     uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
     unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)
-    int tile_lds_n;                   // k_join_stream: tile_base entries copied to LDS (0: read it
-                                      // from global memory)
-    int probe_mask;                   // measurement only (option "probe_mask"): 1 = k_join_mixed skips
-                                      // the chip loop, 2 = it also skips the cell lookup; k_join_stream:
-                                      // 4 = no sub-block lookups, 8 = no leaf-block gathers,
-                                      // 16 = no counting, 32 = no LDS quad
     unsigned long long* counts;  // [n_polygons]
     int n_polygons;
     unsigned long long* amb_queue;  // rows for the exact H3 pass
@@ -171,30 +163,7 @@ __device__ inline void counts_flush(const JoinArgs& a, unsigned int* lds, unsign
     }
 }
 
-// Fused H3 join: fast cell + probe + contains + count.  Ambiguous rows go to the exact pass.
-template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(256) k_join_h3(JoinArgs a) {
-    extern __shared__ unsigned int lds[];
-    counts_init<LDS_COUNTS>(a, lds);
-    unsigned int tests = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        if (a.valid && !a.valid[i]) continue;
-        double x = a.x[i], y = a.y[i];
-        bool amb;
-        int64_t cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
-        if (amb) {
-            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-            continue;
-        }
-        join_point<LDS_COUNTS, PAIRS>(a, i, x, y, cell, lds, tests);
-    }
-    counts_flush<LDS_COUNTS>(a, lds, tests);
-}
-
-// ---- wave-cooperative variant (default): lanes own points for (a)+(b); each border-chip test is
-// then evaluated by the whole wave (pip_coop.h), one work item at a time, wave-uniform.
+// One (row, key) pair: the count, and the pair itself for the pairs output.
 template <bool LDS_COUNTS, bool PAIRS>
 __device__ inline void emit_hit(const JoinArgs& a, int64_t row, uint32_t key, unsigned int* lds) {
     if (LDS_COUNTS)
@@ -226,264 +195,16 @@ __device__ inline void probe(const JoinArgs& a, int64_t cell, uint32_t& first, u
     }
 }
 
-__device__ inline uint32_t next_border(const JoinArgs& a, uint32_t c, uint32_t end) {
-    while (c < end && (a.chip_meta[c] & 1u)) c++;
-    return c;
-}
-
-// Moves `cur` to this lane's next border chip whose envelope contains (x, y); every border chip
-// passed over (or reached) is one (point, border chip) test.  Loads the reached chip's ring descriptor.
-__device__ inline void advance_border(const JoinArgs& a, uint32_t& cur, uint32_t end, double x, double y,
-                                      unsigned int& tests, uint32_t& vs, uint32_t& nv) {
-    cur = next_border(a, cur, end);
-    while (cur < end) {
-        tests++;
-        if (!pip::box_excludes(a.store.geom_bbox[cur], x, y)) {
-            uint2 d = a.chip_ring[cur];
-            vs = d.x;
-            nv = d.y;
-            return;
-        }
-        cur = next_border(a, cur + 1, end);
-    }
-}
-
-template <int GRID, bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(256) k_join_coop(JoinArgs a) {
-    extern __shared__ unsigned int lds[];
-    counts_init<LDS_COUNTS>(a, lds);
-    unsigned int tests = 0;
-    bool nan_seen = false;
-    const int lane = (int)(threadIdx.x & 63);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u); base < a.n; base += stride) {
-        int64_t i = base + lane;
-        bool act = i < a.n && (!a.valid || a.valid[i]);
-        double x = 0.0, y = 0.0;
-        int64_t cell = kEmptyKey;
-        if (act) {
-            x = a.x[i];
-            y = a.y[i];
-            if (GRID == MOSAIC_GRID_H3) {
-                bool amb;
-                cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
-                if (amb) {
-                    unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-                    if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-                    cell = kEmptyKey;
-                }
-            } else if (!bng::point_to_index(x, y, a.res, &cell)) {
-                nan_seen = true;
-                cell = kEmptyKey;
-            }
-        }
-        uint32_t first, end;
-        probe(a, cell, first, end);
-        for (uint32_t c = first; c < end; c++) {
-            uint32_t meta = a.chip_meta[c];
-            if (meta & 1u) emit_hit<LDS_COUNTS, PAIRS>(a, i, meta >> 1, lds);
-        }
-        // lane-parallel prefilter: a border chip whose envelope excludes the point cannot contain it
-        uint32_t cur = first, vs = 0, nv = 0;
-        advance_border(a, cur, end, x, y, tests, vs, nv);
-        unsigned long long pending = __ballot(cur < end);
-        while (pending) {
-            int s[4] = {0, 0, 0, 0};
-            s[0] = __ffsll(pending) - 1;
-            unsigned long long rest = pending & (pending - 1);
-            uint32_t n0 = pip::readlane_u32(nv, s[0]);
-            if (n0 == 0 || n0 - 1 > 32) {
-                // one item for the whole wave: multi-part / holed chips, or rings over 32 edges
-                uint32_t chip = pip::readlane_u32(cur, s[0]);
-                double qx = pip::readlane_f64(x, s[0]), qy = pip::readlane_f64(y, s[0]);
-                bool hit = n0 == 0 ? pip::coop_contains(a.store, chip, qx, qy)
-                                   : pip::coop_locate_in_ring(a.store, pip::readlane_u32(vs, s[0]), n0, qx, qy) ==
-                                         pip::LOC_INTERIOR;
-                if (lane == s[0]) {
-                    if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                    cur++;
-                    advance_border(a, cur, end, x, y, tests, vs, nv);
-                }
-            } else {
-                // pack 2 (<= 32 edges) or 4 (<= 16 edges) simple items into one wave pass
-                const int G = (n0 - 1 <= 16) ? 16 : 32;
-                int ng = 1;
-                while (ng < 64 / G && rest) {
-                    int c = __ffsll(rest) - 1;
-                    uint32_t nc = pip::readlane_u32(nv, c);
-                    if (nc == 0 || nc - 1 > (uint32_t)G) break;
-                    s[ng++] = c;
-                    rest &= rest - 1;
-                }
-                unsigned long long onm, crm;
-                pip::coop_packed(a.store.verts, ng, G, s[0], s[1], s[2], s[3], x, y, vs, nv, onm, crm);
-                const unsigned long long gmask = G == 32 ? 0xffffffffULL : 0xffffULL;
-                for (int k = 0; k < ng; k++) {
-                    if (lane == s[k]) {
-                        unsigned long long om = (onm >> (k * G)) & gmask, cm = (crm >> (k * G)) & gmask;
-                        if (om == 0 && (__popcll(cm) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                        cur++;
-                        advance_border(a, cur, end, x, y, tests, vs, nv);
-                    }
-                }
-            }
-            pending = __ballot(cur < end);
-        }
-    }
-    if (nan_seen) atomicOr(a.flags, 1u);
-    counts_flush<LDS_COUNTS>(a, lds, tests);
-}
-
-// ---- slab variant (default): like k_join_coop, but a work item is (point, chip, slab of the
-// chip's envelope containing the point) and only that slab's segment records are evaluated, so
-// most items need 2-8 lanes and one wave pass serves up to 16 of them.
+// Work items of the wave-cooperative chip evaluation (raster_chips): a general chip (multi-ring /
+// multi-part) or a raster cell's segment list.
 static const uint32_t kGeneralItem = 0xffffffffu;
-
-// Moves `cur` to this lane's next border chip that may contain (x, y), loading its work item:
-// (e0, m) = its slab's segment records, or m = kGeneralItem for multi-ring / multi-part chips.
-// Chips rejected here (envelope, or a slab no segment crosses) are "not contained".
-__device__ inline void advance_slab(const JoinArgs& a, uint32_t& cur, uint32_t end, double x, double y,
-                                    unsigned int& tests, uint32_t& e0, uint32_t& m) {
-    cur = next_border(a, cur, end);
-    while (cur < end) {
-        tests++;
-        if (!pip::box_excludes(a.store.geom_bbox[cur], x, y)) {
-            uint2 si = a.slab_idx[cur];
-            if (si.y == 0) {
-                e0 = 0;
-                m = kGeneralItem;
-                return;
-            }
-            double2 g = a.slab_geo[cur];
-            int s = (int)floor((y - g.x) * g.y);
-            s = s < 0 ? 0 : (s >= (int)si.y ? (int)si.y - 1 : s);
-            uint32_t o0 = a.slab_off[si.x + s], o1 = a.slab_off[si.x + s + 1];
-            if (o1 > o0) {
-                e0 = o0;
-                m = o1 - o0;
-                return;
-            }
-        }
-        cur = next_border(a, cur + 1, end);
-    }
-}
 
 struct SlabItem {
     double x, y;
     uint32_t e0, m;
 };
 
-template <int GRID, bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(256) k_join_slab(JoinArgs a) {
-    extern __shared__ unsigned int lds[];
-    __shared__ SlabItem items[4][16];
-    counts_init<LDS_COUNTS>(a, lds);
-    unsigned int tests = 0;
-    bool nan_seen = false;
-    const int lane = (int)(threadIdx.x & 63);
-    const int wv = (int)(threadIdx.x >> 6) & 3;
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (int64_t)(threadIdx.x & ~63u); base < a.n; base += stride) {
-        int64_t i = base + lane;
-        bool act = i < a.n && (!a.valid || a.valid[i]);
-        double x = 0.0, y = 0.0;
-        int64_t cell = kEmptyKey;
-        if (act) {
-            x = a.x[i];
-            y = a.y[i];
-            if (GRID == MOSAIC_GRID_H3) {
-                bool amb;
-                cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
-                if (amb) {
-                    unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-                    if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-                    cell = kEmptyKey;
-                }
-            } else if (!bng::point_to_index(x, y, a.res, &cell)) {
-                nan_seen = true;
-                cell = kEmptyKey;
-            }
-        }
-        uint32_t first, end;
-        probe(a, cell, first, end);
-        for (uint32_t c = first; c < end; c++) {
-            uint32_t meta = a.chip_meta[c];
-            if (meta & 1u) emit_hit<LDS_COUNTS, PAIRS>(a, i, meta >> 1, lds);
-        }
-        uint32_t cur = first, e0 = 0, m = 0;
-        advance_slab(a, cur, end, x, y, tests, e0, m);
-        unsigned long long pending = __ballot(cur < end);
-        while (pending) {
-            int s0 = __ffsll(pending) - 1;
-            uint32_t m0 = pip::readlane_u32(m, s0);
-            if (m0 > 32) {
-                // one item for the whole wave: general chips, or slabs with more than 32 segments
-                double qx = pip::readlane_f64(x, s0), qy = pip::readlane_f64(y, s0);
-                bool hit;
-                if (m0 == kGeneralItem) {
-                    hit = pip::coop_contains(a.store, pip::readlane_u32(cur, s0), qx, qy);
-                } else {
-                    uint32_t q0 = pip::readlane_u32(e0, s0);
-                    unsigned long long onm = 0;
-                    int cross = 0;
-                    for (uint32_t b = 0; b < m0; b += 64) {
-                        bool on = false, cr = false;
-                        if (b + lane < m0) pip::edge_rec_flags(a.edges[q0 + b + lane], qx, qy, on, cr);
-                        onm |= __ballot(on);
-                        cross += __popcll(__ballot(cr));
-                    }
-                    hit = onm == 0 && (cross & 1);
-                }
-                if (lane == s0) {
-                    if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                    cur++;
-                    advance_slab(a, cur, end, x, y, tests, e0, m);
-                }
-            } else {
-                const int G = m0 <= 4 ? 4 : (m0 <= 8 ? 8 : (m0 <= 16 ? 16 : 32));
-                const int cap = 64 / G;
-                bool cand = cur < end && m <= (uint32_t)G;
-                unsigned long long cmask = __ballot(cand);
-                int rank = __popcll(cmask & lt_mask);
-                bool chosen = cand && rank < cap;
-                if (chosen) {
-                    SlabItem it;
-                    it.x = x;
-                    it.y = y;
-                    it.e0 = e0;
-                    it.m = m;
-                    items[wv][rank] = it;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                int ng = __popcll(cmask);
-                ng = ng < cap ? ng : cap;
-                int k = lane / G, j = lane - k * G;
-                bool on = false, cr = false;
-                if (k < ng) {
-                    SlabItem it = items[wv][k];
-                    if ((uint32_t)j < it.m) pip::edge_rec_flags(a.edges[it.e0 + j], it.x, it.y, on, cr);
-                }
-                unsigned long long onm = __ballot(on), crm = __ballot(cr);
-                if (chosen) {
-                    const unsigned long long gm = (G == 32) ? 0xffffffffULL : ((1ULL << G) - 1ULL);
-                    unsigned long long om = (onm >> (rank * G)) & gm, xm = (crm >> (rank * G)) & gm;
-                    if (om == 0 && (__popcll(xm) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                    cur++;
-                    advance_slab(a, cur, end, x, y, tests, e0, m);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            pending = __ballot(cur < end);
-        }
-    }
-    if (nan_seen) atomicOr(a.flags, 1u);
-    counts_flush<LDS_COUNTS>(a, lds, tests);
-}
-
-// ---- raster variant (default, pip_mode 3): per border chip one ray-parity raster lookup
+// ---- raster chip loop: per border chip one ray-parity raster lookup
 // (raster.h); pure cells are decided by the lookup, short cell lists by the owning lane, and only
 // long lists and general (multi-ring / multi-part) chips go to the wave-cooperative evaluation.
 
@@ -757,11 +478,6 @@ __global__ void __launch_bounds__(256) k_join_tiled(JoinArgs a) {
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
 
-// ---- point-raster stream (default with a point raster, tiles.h): the whole answer of most points
-// from one or two L2 / Infinity-Cache lookups, nothing else in the loop, so the coordinate stream
-// runs near HBM speed.  Four consecutive points per lane (two 16-byte loads per coordinate,
-// VEC: both arrays 16-byte aligned), their lookups issued back to back.  Rows in mixed raster
-// cells are appended to mixq (one atomic per wave) for k_join_mixed.
 // Per-wave LDS stage of rows for the mixed-cell queue: rows are appended with a ballot, and the
 // stage goes to the global queue in one atomic once >= 64 rows wait (a per-iteration atomic on one
 // counter serialises the grid).  Wave-uniform calls.
@@ -783,158 +499,191 @@ __device__ inline void stage_flush(const JoinArgs& a, uint32_t* wq, uint32_t& wn
     wn = 0;
 }
 
+// ---- k_join_stream (default with a point raster, tiles.h): the point raster's answer for every
+// point of the batch, branch-free.  Per point: fine-cell coordinates (two f64 ops per axis, clamped
+// to the grid), the LDS quad level, and -- only for points whose quad is not uniform -- one 2-byte
+// gather of the sub-block entry from the compact copies; points whose sub-block is a leaf block or
+// a line record gather that (2 or 16 bytes).  Gathers go through buffer descriptors: a lane that
+// needs no gather passes an out-of-range offset, which the hardware drops without a memory access,
+// so no lane branches.  Answers: 0 (no pair), k + 1 (one pair with key k: an LDS atomic), kMixed
+// (the row goes to the mixed queue for k_join_mixed).  tiles::raster_code is the same computation
+// for one point on the host.
+//
+// Rows: each wave handles 256 consecutive rows per iteration; lane l holds rows 2l, 2l + 1,
+// 128 + 2l, 129 + 2l, so each 16-byte coordinate load instruction reads 1 KiB contiguous.  The
+// next iteration's coordinates are loaded after this iteration's gathers are issued (vector-memory
+// returns retire in order: waiting for the gathers does not wait for them).
+struct StreamArgs {
+    double x0, y0, sxC, syC;  // fine-cell coordinates g = (x - x0) sxC, (y - y0) syC (C per sub-block)
+    double gxmax, gymax;      // clamp: NX C - 1, NY C - 1
+    int32_t cs, qsh, tsh, qs;  // log2 C; cs + quad shift; cs + tile shift (sub-blocks per tile); quad shift
+    int32_t qnx, tnx;         // quad-level entries per row, tiles per row
+    int32_t n_quad_words, n_tiles;  // LDS copies: quad level (uint32 words), tile_base (if tb_lds)
+    int32_t tb_lds;           // 1: tile_base in LDS; 0: gathered through its descriptor
+    int32_t stage_words;      // per-wave mixed-row stage
+    const uint32_t* quad;     // quad level, uint16 entries packed in uint32 words
+    const uint32_t* tile_base;
+    const uint16_t* csub;     // compact sub-block copies (PointRaster::sub + nx * ny)
+    const uint16_t* blocks;   // line records and leaf blocks
+    uint32_t csub_bytes, blocks_bytes, tile_base_bytes;
+};
+static const uint32_t kNoLoad = 0x7ffffff0u;  // out-of-range buffer offset (every table is < 2 GiB)
+
 typedef double v2d __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
-#ifndef MOSAIC_STREAM_NT
-#define MOSAIC_STREAM_NT 1  // k_join_stream: non-temporal coordinate loads
-#endif
-#if MOSAIC_STREAM_NT
-#define MOSAIC_STREAM_LOAD(p) __builtin_nontemporal_load(p)
-#else
-#define MOSAIC_STREAM_LOAD(p) (*(p))
-#endif
-#ifndef MOSAIC_STREAM_WAVES
-#define MOSAIC_STREAM_WAVES 4  // k_join_stream: waves per SIMD the register budget must allow (LDS allows 4 at the defaults)
-#endif
-// k_join_stream dynamic LDS: [per-polygon counts (LDS_COUNTS)] [per-wave mixed-row stages]
-// [tile_base (tile_lds_n words)] [quad level of the raster (if any)]
-#ifndef MOSAIC_STREAM_LDS_TILE
-#define MOSAIC_STREAM_LDS_TILE (80 * 1024)
-#endif
-static const size_t kStreamLdsTile = MOSAIC_STREAM_LDS_TILE;  // LDS per workgroup up to which tile_base joins it
-static inline size_t stream_stage_words(int block, int G) { return (size_t)(block / 64) * (64 + 256 * (size_t)G); }
+__device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t bytes) {
+    // wave-uniform inputs made provably uniform (no waterfall loops around the loads)
+    const uint64_t u = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 
-#ifndef MOSAIC_STREAM_LB
-#define MOSAIC_STREAM_LB 1024  // k_join_stream: largest workgroup (1024 caps a lane at 128 VGPRs)
-#endif
-template <bool LDS_COUNTS, bool PAIRS, bool VEC, bool VALID, int G>
-__global__ void __launch_bounds__(MOSAIC_STREAM_LB) __attribute__((amdgpu_waves_per_eu(MOSAIC_STREAM_WAVES)))
-k_join_stream(JoinArgs a) {
+template <bool LDS_COUNTS, bool PAIRS, bool VEC>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream(JoinArgs a, StreamArgs s) {
     extern __shared__ unsigned int lds[];
-    uint32_t* stage = lds + (LDS_COUNTS ? a.n_polygons : 0);
-    uint32_t* tbase = stage + (blockDim.x >> 6) * (64 + 256 * G);
-    uint16_t* quad = a.praster.quad ? (uint16_t*)(tbase + a.tile_lds_n) : nullptr;
-    if (quad) {
-        const int nq = a.praster.qnx * a.praster.qny;
-        for (int k = threadIdx.x; k < nq; k += blockDim.x) quad[k] = a.praster.quad[k];
-    }
-    for (int k = threadIdx.x; k < a.tile_lds_n; k += blockDim.x) tbase[k] = a.praster.tile_base[k];
-    counts_init<LDS_COUNTS>(a, lds);  // (its barrier also publishes the quad level and tile_base)
-    if (!LDS_COUNTS) __syncthreads();
+    const int nwaves = (int)(blockDim.x >> 6);
+    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;  // counts + one spill word per lane
+    uint32_t* stage = lds + ncw;
+    uint32_t* tb = stage + nwaves * s.stage_words;
+    uint32_t* quadw = tb + (s.tb_lds ? s.n_tiles : 0);
+    const uint16_t* quad = (const uint16_t*)quadw;
+    for (int k = threadIdx.x; k < s.n_quad_words; k += blockDim.x) quadw[k] = s.quad[k];
+    if (s.tb_lds)
+        for (int k = threadIdx.x; k < s.n_tiles; k += blockDim.x) tb[k] = s.tile_base[k];
+    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
+    const __amdgpu_buffer_rsrc_t rblk = stream_rsrc(s.blocks, s.blocks_bytes);
+    const __amdgpu_buffer_rsrc_t rtb = stream_rsrc(s.tile_base, s.tile_base_bytes);
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    // mixed rows are staged per wave in LDS and flushed to the global queue once 64 or more are
-    // waiting (one atomic per flush: a per-iteration atomic on one counter serialises the grid);
-    // the stage holds < 64 + 256 G rows
-    uint32_t* wq = stage + (threadIdx.x >> 6) * (64 + 256 * G);
-    uint32_t wn = 0;  // wave-uniform fill level
-    // G groups of 4 consecutive rows per lane and iteration; group g is a grid-wide slice of
-    // 4 * (threads) rows, so each group's loads stay coalesced across the wave
-    const int64_t gstride = (int64_t)gridDim.x * blockDim.x * 4, stride = gstride * G;
-    // wave-uniform trip count (the ballots, the stage and its flushes need every lane): the loop
-    // runs while the wave's first row is in range; lanes past the end are not live
-    int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 4;
-    int64_t i0 = w0 + lane * 4;
-    // software pipeline (VEC): the next iteration's coordinates load while this iteration's block
-    // gathers and its counting run
-    v2d nx[G][2], ny[G][2];
+    // the wave index through readfirstlane: w0 and every branch on it are provably wave-uniform
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t* wq = stage + wave * s.stage_words;
+    uint32_t wn = 0;  // wave-uniform fill level of the stage
+    const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
+    // rows of slot k: w0 + (k >> 1) 128 + 2 lane + (k & 1)
+    auto row_of = [&](int64_t wb, int k) -> int64_t { return wb + (k >> 1) * 128 + 2 * lane + (k & 1); };
+    v2d px[2], py[2];
+    auto load4 = [&](int64_t wb) {  // unconditional: past the end, the chunk's first rows (VEC: >= 256 of them)
+        const int64_t r = (wb + 256 <= a.n) ? wb + 2 * lane : a.row_lo;
+        px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
+        px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
+        py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
+        py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
+    };
+    if (VEC) load4(w0);
+    for (; w0 < a.n; w0 += stride) {
+        const bool full = VEC && w0 + 256 <= a.n;  // wave-uniform
+        double x[4], y[4];
+        bool live[4];
+        if (full) {
+            x[0] = px[0].x, x[1] = px[0].y, x[2] = px[1].x, x[3] = px[1].y;
+            y[0] = py[0].x, y[1] = py[0].y, y[2] = py[1].x, y[3] = py[1].y;
 #pragma unroll
-    for (int g = 0; g < G; g++) {
-        const int64_t r = i0 + g * gstride;
-        nx[g][0] = nx[g][1] = ny[g][0] = ny[g][1] = v2d{0.0, 0.0};
-        if (VEC && r + 3 < a.n) {
-            nx[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r));
-            nx[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r + 2));
-            ny[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r));
-            ny[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r + 2));
-        }
-    }
-    for (; w0 < a.n; w0 += stride, i0 += stride) {
-        tiles::Lookup4 L[G];
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            const int64_t r = i0 + g * gstride;
-            double x[4], y[4];
-            bool live[4];
-            if (VEC && r + 3 < a.n) {
-                x[0] = nx[g][0].x;
-                x[1] = nx[g][0].y;
-                x[2] = nx[g][1].x;
-                x[3] = nx[g][1].y;
-                y[0] = ny[g][0].x;
-                y[1] = ny[g][0].y;
-                y[2] = ny[g][1].x;
-                y[3] = ny[g][1].y;
-#pragma unroll
-                for (int k = 0; k < 4; k++) live[k] = !VALID || a.valid[r + k];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    live[k] = r + k < a.n && (!VALID || a.valid[r + k]);
-                    x[k] = live[k] ? a.x[r + k] : 0.0;
-                    y[k] = live[k] ? a.y[r + k] : 0.0;
-                }
-            }
-            tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L[g],
-                                 (a.probe_mask & 32) ? nullptr : quad);
-            if (a.probe_mask & 4) {  // measurement only: no sub-block lookups
-#pragma unroll
-                for (int k = 0; k < 4; k++) L[g].in[k] = false;
-            }
-            if (a.tile_lds_n) tiles::raster_base4_lds(tbase, L[g]);
-        }
-        if (a.probe_mask & 8) {  // measurement only: no leaf-block gathers
-#pragma unroll
-            for (int g = 0; g < G; g++)
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (tiles::sub_is_block(L[g].e[k])) L[g].e[k] = 0;
-        }
-        if (!a.tile_lds_n) {
-#pragma unroll
-            for (int g = 0; g < G; g++) tiles::raster_base4(a.praster, L[g]);
-        }
-#pragma unroll
-        for (int g = 0; g < G; g++) tiles::raster_gather4(a.praster, L[g]);
-        if (VEC) {
-            // the next iteration's coordinates, issued after this iteration's gathers (vmcnt
-            // retires in order, so loads issued earlier would be waited for first); unconditional,
-            // since a branch here makes the compiler wait conservatively -- past the end it
-            // re-reads the chunk's first group
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                const int64_t r = i0 + stride + g * gstride;
-                const int64_t r1 = (r + 3 < a.n) ? r : a.row_lo;
-                nx[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1));
-                nx[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1 + 2));
-                ny[g][0] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1));
-                ny[g][1] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1 + 2));
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            tiles::raster_select4(L[g]);
-            const int64_t r = i0 + g * gstride;
+            for (int k = 0; k < 4; k++) live[k] = true;
+        } else {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint16_t rc = L[g].out[k];
-                if (rc != 0 && rc != tiles::kMixed && !(a.probe_mask & 16))
-                    emit_hit<LDS_COUNTS, PAIRS>(a, r + k, (uint32_t)rc - 1u, lds);
-                const unsigned long long mm = __ballot(rc == tiles::kMixed);
-                if (rc == tiles::kMixed) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(r + k - a.row_lo);
-                wn += (uint32_t)__popcll(mm);
+                const int64_t r = row_of(w0, k);
+                live[k] = r < a.n;
+                x[k] = live[k] ? a.x[r] : 0.0;
+                y[k] = live[k] ? a.y[r] : 0.0;
             }
         }
-        if (wn >= 64) {  // flush the whole stage: one atomic per >= 64 rows
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
-            base = __shfl(base, 0, 64);
-            for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
-            __builtin_amdgcn_wave_barrier();
-            wn = 0;
+        // stage A: fine-cell coordinates, quad level (LDS), tile base (LDS)
+        double gx[4], gy[4];
+        uint32_t ixC[4], iyC[4], qv[4], tbv[4], ta[4];
+        bool fin[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            fin[k] = __builtin_isfinite(x[k] + y[k]);
+            gx[k] = fmin(fmax((x[k] - s.x0) * s.sxC, 0.0), s.gxmax);  // NaN -> 0
+            gy[k] = fmin(fmax((y[k] - s.y0) * s.syC, 0.0), s.gymax);
+            ixC[k] = (uint32_t)(int)gx[k];
+            iyC[k] = (uint32_t)(int)gy[k];
+            // (indices < 2^24: 24-bit multiplies)
+            qv[k] = quad[__umul24(iyC[k] >> s.qsh, (uint32_t)s.qnx) + (ixC[k] >> s.qsh)];
+            ta[k] = __umul24(iyC[k] >> s.tsh, (uint32_t)s.tnx) + (ixC[k] >> s.tsh);
+            tbv[k] = s.tb_lds ? tb[ta[k]] : 0u;
+        }
+        // stage B: sub-block entries of the points in non-uniform quads
+        uint32_t code[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t local = (((iyC[k] >> s.cs) & qm) << s.qs) | ((ixC[k] >> s.cs) & qm);
+            const uint32_t off = ((((qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
+            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, qv[k] >= 0x8000u ? off : kNoLoad, 0, 0);
+        }
+        // stage C: leaf codes and line records of the points in mixed sub-blocks
+        uint32_t leaf[4];
+        v4u lrec[4];
+        bool blk[4], line[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            code[k] = qv[k] >= 0x8000u ? code[k] : qv[k];
+            blk[k] = code[k] - 0x8000u < 0x7fffu;  // kSubBlock | n, not kMixed
+            line[k] = blk[k] && (code[k] & 0x4000u);
+            if (!s.tb_lds) tbv[k] = __builtin_amdgcn_raw_buffer_load_b32(rtb, blk[k] ? ta[k] << 2 : kNoLoad, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t n = code[k] & 0x3fffu;
+            const uint32_t lf = ((iyC[k] & cm) << s.cs) | (ixC[k] & cm);
+            const uint32_t loff = (tbv[k] + (n << (2 * s.cs)) + lf) << 1;
+            const uint32_t roff = (tbv[k] - 8u * (n + 1u)) << 1;
+            leaf[k] = __builtin_amdgcn_raw_buffer_load_b16(rblk, (blk[k] && !line[k]) ? loff : kNoLoad, 0, 0);
+            lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rblk, line[k] ? roff : kNoLoad, 0, 0);
+        }
+        if (VEC) load4(w0 + stride);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            // tiles::line_code, as selects
+            const float u = (float)(gx[k] - (double)(ixC[k] & ~cm)), v = (float)(gy[k] - (double)(iyC[k] & ~cm));
+            const float sv = fmaf(__uint_as_float(lrec[k].x), u, fmaf(__uint_as_float(lrec[k].y), v, __uint_as_float(lrec[k].z)));
+            const uint32_t pos = lrec[k].w & 0xffffu, neg = lrec[k].w >> 16;
+            uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
+            lc = sv <= -1.0f ? neg : lc;
+            uint32_t c = line[k] ? lc : (blk[k] ? leaf[k] : code[k]);
+            c = fin[k] ? c : (uint32_t)tiles::kMixed;
+            code[k] = live[k] ? c : 0u;
+        }
+        // counts: one LDS add per point (points without a pair add to the lane's spill word)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (LDS_COUNTS && !PAIRS) {
+                const uint32_t slot = code[k] - 1u < 0xfffeu ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
+                atomicAdd(&lds[slot], 1u);
+            } else if (code[k] - 1u < 0xfffeu) {
+                emit_hit<LDS_COUNTS, PAIRS>(a, row_of(w0, k), code[k] - 1u, lds);
+            }
+        }
+        // mixed rows to the per-wave stage (rare: one wave-uniform test per iteration)
+        const bool anym = code[0] == tiles::kMixed || code[1] == tiles::kMixed || code[2] == tiles::kMixed ||
+                          code[3] == tiles::kMixed;
+        if (__ballot(anym)) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool m = code[k] == tiles::kMixed;
+                const unsigned long long mm = __ballot(m);
+                if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(w0, k) - a.row_lo);
+                wn += (uint32_t)__popcll(mm);
+            }
+            if (wn >= 64) {  // flush: one atomic per >= 64 rows
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
+                base = __shfl(base, 0, 64);
+                for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
+                __builtin_amdgcn_wave_barrier();
+                wn = 0;
+            }
         }
     }
     if (wn) {
@@ -944,97 +693,13 @@ k_join_stream(JoinArgs a) {
         unsigned long long base = 0;
         if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
         base = __shfl(base, 0, 64);
-        for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
+        for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
     }
-    counts_flush<LDS_COUNTS>(a, lds, 0u);
-}
-
-// ---- k_join_stream_pipe (option stream_mode 2): k_join_stream's lookups software-pipelined over
-// three iterations, so no wait is on a load issued in the same iteration.  Iteration t issues
-// the leaf-block gathers of rows t (their sub-block entries arrived), the sub-block gathers of
-// rows t + 1 (their coordinates arrived) and the coordinate loads of rows t + 2, in that order,
-// and finishes rows t - 1 (their leaf codes arrived): vector-memory returns retire in issue order,
-// which is also the order the next iteration consumes them in.  Four rows per lane, both arrays
-// 16-byte aligned; rows past the last multiple of 4 go to the mixed queue.
-#ifndef MOSAIC_PIPE_WAVES
-#define MOSAIC_PIPE_WAVES 4  // k_join_stream_pipe: waves per SIMD the register budget must allow
-#endif
-template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MOSAIC_PIPE_WAVES)))
-k_join_stream_pipe(JoinArgs a) {
-    extern __shared__ unsigned int lds[];
-    uint32_t* stage = lds + (LDS_COUNTS ? a.n_polygons : 0);
-    uint32_t* tbase = stage + (blockDim.x >> 6) * (64 + 256);
-    uint16_t* quad = a.praster.quad ? (uint16_t*)(tbase + a.tile_lds_n) : nullptr;
-    if (quad) {
-        const int nq = a.praster.qnx * a.praster.qny;
-        for (int k = threadIdx.x; k < nq; k += blockDim.x) quad[k] = a.praster.quad[k];
+    if (LDS_COUNTS) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
     }
-    for (int k = threadIdx.x; k < a.tile_lds_n; k += blockDim.x) tbase[k] = a.praster.tile_base[k];
-    counts_init<LDS_COUNTS>(a, lds);
-    if (!LDS_COUNTS) __syncthreads();
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    uint32_t* wq = stage + (threadIdx.x >> 6) * (64 + 256);
-    uint32_t wn = 0;
-    const int64_t n4 = a.row_lo + ((a.n - a.row_lo) & ~(int64_t)3);  // rows handled in groups of 4
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    const int64_t i0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    const int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 4;
-    auto load = [&](int64_t r, v2d* cx, v2d* cy) {  // unconditional: past the end, the chunk's first rows
-        const int64_t r1 = r < n4 ? r : a.row_lo;
-        cx[0] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1));
-        cx[1] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r1 + 2));
-        cy[0] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1));
-        cy[1] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r1 + 2));
-    };
-    auto issue = [&](int64_t r, const v2d* cx, const v2d* cy, tiles::Lookup4& L) {
-        const double x[4] = {cx[0].x, cx[0].y, cx[1].x, cx[1].y}, y[4] = {cy[0].x, cy[0].y, cy[1].x, cy[1].y};
-        const bool lv = r < n4;
-        const bool live[4] = {lv, lv, lv, lv};
-        tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L, quad);
-        if (a.tile_lds_n) tiles::raster_base4_lds(tbase, L);
-    };
-    // prologue: rows t = 0 looked up (sub-block gathers out), rows t = 1 loading
-    v2d cx[2], cy[2];
-    tiles::Lookup4 Lc, Lp;
-    load(i0, cx, cy);
-    issue(i0, cx, cy, Lc);
-    load(i0 + stride, cx, cy);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        Lp.in[k] = false;
-        Lp.out[k] = 0;
-        Lp.e[k] = 0;
-        Lp.b[k] = 0;
-    }
-    for (int64_t wp = w0 - stride, r = i0; wp < n4; wp += stride, r += stride) {
-        // rows r (Lc): leaf-block gathers
-        if (!a.tile_lds_n) tiles::raster_base4(a.praster, Lc);
-        tiles::raster_gather4(a.praster, Lc);
-        // rows r - stride (Lp): finish
-        tiles::raster_select4(Lp);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint16_t rc = Lp.out[k];
-            if (rc != 0 && rc != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, r - stride + k, (uint32_t)rc - 1u, lds);
-            stage_push(wq, wn, rc == tiles::kMixed, (uint32_t)(r - stride + k - a.row_lo), lt_mask);
-        }
-        stage_flush(a, wq, wn, lane, 64);
-        // rows r + stride: sub-block gathers; rows r + 2 stride: coordinates
-        tiles::Lookup4 Ln;
-        issue(r + stride, cx, cy, Ln);
-        load(r + 2 * stride, cx, cy);
-        Lp = Lc;
-        Lc = Ln;
-    }
-    // rows past the last multiple of 4 (fewer than 4): the mixed queue
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-        const bool tail = n4 + lane < a.n;
-        stage_push(wq, wn, tail, (uint32_t)(n4 + lane - a.row_lo), lt_mask);
-    }
-    stage_flush(a, wq, wn, lane, 1);
-    counts_flush<LDS_COUNTS>(a, lds, 0u);
 }
 
 
@@ -1341,116 +1006,6 @@ __global__ void __launch_bounds__(256) k_join_mixed_bng(JoinArgs a) {
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
 
-// ---- decoupled variant (option stream_mode = 1): per workgroup of 1024 threads, 4 loader waves
-// stream the coordinates of the next chunk into LDS while 12 worker waves run the raster lookups of
-// the current chunk from LDS.  A wave's vector-memory returns retire in order, so in k_join_stream
-// a wave waiting on its gathers also waits on its stream loads; here the two wait in different
-// waves.  Chunks of kChunkRows rows, double-buffered; one workgroup per CU.
-static const int kLoaderWaves = 4, kWorkerWaves = 12;
-static const int kChunkRows = kWorkerWaves * 64 * 4;  // 3072 rows: 4 per worker lane
-
-template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(1024) k_join_stream_dec(JoinArgs a) {
-    extern __shared__ unsigned int lds[];
-    __shared__ double cx[2][kChunkRows], cy[2][kChunkRows];  // 96 KB
-    __shared__ uint32_t stage[kWorkerWaves][320];
-    uint16_t* quad = a.praster.quad ? (uint16_t*)(lds + (LDS_COUNTS ? a.n_polygons : 0)) : nullptr;
-    if (quad) {
-        const int nq = a.praster.qnx * a.praster.qny;
-        for (int k = threadIdx.x; k < nq; k += blockDim.x) quad[k] = a.praster.quad[k];
-    }
-    counts_init<LDS_COUNTS>(a, lds);
-    if (!LDS_COUNTS) __syncthreads();
-    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-    const bool loader = wave < kLoaderWaves;
-    const int64_t rows = a.n - a.row_lo;
-    const int64_t nchunks = (rows + kChunkRows - 1) / kChunkRows;
-    // loader lane l (0..255) moves rows [c0 + j * 512 + 2 l, +2) for j < 6, x and y
-    auto load_chunk = [&](int64_t c, int buf) {
-        const int64_t c0 = a.row_lo + c * kChunkRows;
-        const int l = (int)threadIdx.x;  // 0..255 for loader waves
-        v2d vx[6], vy[6];
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const int64_t r = c0 + j * 512 + 2 * l;
-            if (r + 1 < a.n) {
-                vx[j] = MOSAIC_STREAM_LOAD((const v2d*)(a.x + r));
-                vy[j] = MOSAIC_STREAM_LOAD((const v2d*)(a.y + r));
-            } else {
-                vx[j] = v2d{r < a.n ? a.x[r] : 0.0, 0.0};
-                vy[j] = v2d{r < a.n ? a.y[r] : 0.0, 0.0};
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            *(v2d*)&cx[buf][j * 512 + 2 * l] = vx[j];
-            *(v2d*)&cy[buf][j * 512 + 2 * l] = vy[j];
-        }
-    };
-    int64_t c = blockIdx.x;
-    if (loader && c < nchunks) load_chunk(c, 0);
-    __syncthreads();
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    uint32_t* wq = loader ? nullptr : stage[wave - kLoaderWaves];
-    uint32_t wn = 0;
-    for (int k = 0; c < nchunks; c += gridDim.x, k ^= 1) {
-        const int64_t cn = c + gridDim.x;
-        if (loader) {
-            if (cn < nchunks) load_chunk(cn, k ^ 1);
-        } else {
-            const int w = (int)threadIdx.x - kLoaderWaves * 64;  // 0..767
-            const int64_t r0 = a.row_lo + c * kChunkRows + 4 * w;
-            double x[4], y[4];
-            bool live[4];
-            const v2d x01 = *(const v2d*)&cx[k][4 * w], x23 = *(const v2d*)&cx[k][4 * w + 2];
-            const v2d y01 = *(const v2d*)&cy[k][4 * w], y23 = *(const v2d*)&cy[k][4 * w + 2];
-            x[0] = x01.x;
-            x[1] = x01.y;
-            x[2] = x23.x;
-            x[3] = x23.y;
-            y[0] = y01.x;
-            y[1] = y01.y;
-            y[2] = y23.x;
-            y[3] = y23.y;
-#pragma unroll
-            for (int q = 0; q < 4; q++) live[q] = r0 + q < a.n && (!a.valid || a.valid[r0 + q]);
-            tiles::Lookup4 L;
-            tiles::raster_issue4(a.praster, a.tgrid.x0, a.tgrid.y0, x, y, live, L, quad);
-            tiles::raster_finish4(a.praster, L);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint16_t rc = L.out[q];
-                if (rc != 0 && rc != tiles::kMixed) emit_hit<LDS_COUNTS, PAIRS>(a, r0 + q, (uint32_t)rc - 1u, lds);
-                const unsigned long long mm = __ballot(rc == tiles::kMixed);
-                if (rc == tiles::kMixed) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(r0 + q - a.row_lo);
-                wn += (uint32_t)__popcll(mm);
-            }
-            if (wn >= 64) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
-                base = __shfl(base, 0, 64);
-                for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
-                __builtin_amdgcn_wave_barrier();
-                wn = 0;
-            }
-        }
-        __syncthreads();
-    }
-    if (!loader && wn) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
-        base = __shfl(base, 0, 64);
-        for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
-    }
-    counts_flush<LDS_COUNTS>(a, lds, 0u);
-}
-
 // Rows of mixed raster cells (the dense queue mixq), R rows per lane: their chip ranges are found
 // stage by stage for all R rows at once (coordinate gathers, tile codes, tile records, projection,
 // window entries, hash entries -- R independent chains in flight per lane instead of one), then the
@@ -1495,7 +1050,7 @@ __global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a) {
         for (int k = 0; k < R; k++) {
             fast[k] = false;
             ent_idx[k] = 0;
-            if (!(a.probe_mask & 2) && live[k] && code[k] >= 2) {
+            if (live[k] && code[k] >= 2) {
                 const int face = (int)(rec[k].dims & 0xffu);
                 const int wa = (int)((rec[k].dims >> 8) & 0xfffu), wb = (int)(rec[k].dims >> 20);
                 double px, py, pz, vx, vy, best;
@@ -1520,7 +1075,7 @@ __global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a) {
 #pragma unroll
         for (int k = 0; k < R; k++) {
             cur[k] = end[k] = 0;
-            if (!live[k] || (a.probe_mask & 2)) continue;
+            if (!live[k]) continue;
             if (fast[k]) {
                 if (ent[k]) {
                     cur[k] = he[k].first;
@@ -1528,10 +1083,6 @@ __global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a) {
                 }
             } else {
                 tiled_cell(a, row[k], x[k], y[k], code[k], cur[k], end[k]);
-            }
-            if (a.probe_mask & 1) {
-                tests += end[k] - cur[k];
-                cur[k] = end[k];
             }
         }
 #pragma unroll
@@ -1555,27 +1106,6 @@ __global__ void __launch_bounds__(256) k_join_h3_exact(JoinArgs a, int all_rows)
         join_point<false, PAIRS>(a, i, x, y, cell, nullptr, tests);
     }
     counts_flush<false>(a, nullptr, tests);
-}
-
-template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(256) k_join_bng(JoinArgs a) {
-    extern __shared__ unsigned int lds[];
-    counts_init<LDS_COUNTS>(a, lds);
-    unsigned int tests = 0;
-    bool nan_seen = false;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        if (a.valid && !a.valid[i]) continue;
-        double x = a.x[i], y = a.y[i];
-        int64_t cell;
-        if (!bng::point_to_index(x, y, a.res, &cell)) {
-            nan_seen = true;
-            continue;
-        }
-        join_point<LDS_COUNTS, PAIRS>(a, i, x, y, cell, lds, tests);
-    }
-    if (nan_seen) atomicOr(a.flags, 1u);
-    counts_flush<LDS_COUNTS>(a, lds, tests);
 }
 
 struct CellArgs {
@@ -1772,53 +1302,108 @@ struct DevBuf {
     }
 };
 
-struct mosaic_ctx {
-    int device = 0;
-    int n_cu = 256;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
+// Options of a context (mosaic_set_option).  Every call copies them once at entry, so a call runs
+// with one consistent set even while another thread changes them.
+struct Options {
     int jdk = 8;
     int async = 0;
     int block = 256;
     int blocks_per_cu = 8;
-    // 3: ray-parity raster (default), 2: slab-filtered wave-cooperative, 1: whole-ring cooperative,
-    // 0: lane per point
-    int pip_mode = 3;
-    int raster = 16;      // raster cells per side of a border chip's envelope (chip tables built later)
+    int raster = 16;          // ray-parity raster cells per side of a border chip (chip tables built later)
     int raster_adaptive = 1;  // fewer raster cells for rings with few segments
-    int lane_edges = 0;   // raster cell lists up to this long are evaluated by the owning lane
-    double last_tess_classify_ms = 0;  // k_bng_tess_classify duration of the last mosaic_tessellate_gpu
-    int tiles = 1;        // build / use the H3 tile directory (tiles.h) with pip_mode 3
-    int point_raster = 1; // build / use the point raster over the tile directory (tiles.h)
-    int raster_sub = 64;  // point raster: sub-blocks per tile side (a power of two)
-    int raster_cell = 16; // point raster: leaf cells per sub-block side
-    int raster_quad = 1;  // point raster: LDS quad level
-    int raster_lines = 1; // point raster: line records for single-edge sub-blocks
-    int stream_groups = 1;  // k_join_stream: groups of 4 rows per lane and iteration (1 or 2)
-    int stream_block = 512; // k_join_stream workgroup size (64 .. 1024, a multiple of 64)
-    int tile_lds = 1;       // k_join_stream: tile_base in LDS when it fits (kStreamLdsTile)
-    int stream_persistent = 0;  // k_join_stream grid: the resident workgroups (1) or blocks_per_cu-based (0)
+    int lane_edges = 0;       // raster cell lists up to this long are evaluated by the owning lane
+    int tiles = 1;            // build / use the H3 tile directory (tiles.h)
+    int point_raster = 1;     // build / use the point raster over the tile directory (tiles.h)
+    int raster_sub = 64;      // point raster: sub-blocks per tile side (a power of two)
+    int raster_cell = 16;     // point raster: leaf cells per sub-block side (a power of two)
+    int raster_quad = 1;      // point raster: LDS quad level
+    int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
+    int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
     int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
-    int stream_mode = 0;          // 0: k_join_stream, 1: k_join_stream_dec (loader / worker waves),
-                                  // 2: k_join_stream_pipe (lookups pipelined over iterations)
-    int probe_mask = 0;     // measurement only: see JoinArgs::probe_mask (results are wrong when set)
-    DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
-    DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
     // copy on copy_stream overlapping the current chunk's join (0: stage the whole batch first)
     int64_t host_chunk = (int64_t)1 << 25;
+    int timing = 0;           // HIP events bracket each fused join kernel on the calling thread's stream
+};
+
+// Execution state of one calling thread on one context: its HIP stream (created on first use, or
+// set with mosaic_set_stream), its scratch buffers, counters, deferred errors and timing events.
+// Threads never share one, so concurrent calls on a context do not touch each other's scratch
+// ("Concurrent callers are multiplexed onto per-thread HIP streams").
+struct ThreadCtx : Options {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    double last_tess_classify_ms = 0;  // tessellation classification kernel of the last mosaic_tessellate_gpu
+    DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
+    DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
     hipStream_t copy_stream = nullptr;
     DevBuf hx[2], hy[2], hcounts;
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
-    // option "timing": HIP events bracket each fused join kernel on the context stream
-    int timing = 0;
     std::vector<hipEvent_t> ev_start, ev_stop;
     size_t ev_used = 0;
+    void release() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (DevBuf* b : {&amb_queue, &mix_queue, &scalars, &stage_x, &stage_y, &stage_v, &stage_out, &stage_out2,
+                          &stage_idx, &geo_off, &geo_data, &dec_x, &dec_y, &dec_status, &hx[0], &hx[1], &hy[0], &hy[1],
+                          &hcounts})
+            b->release();
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
+        for (size_t i = 0; i < ev_start.size(); i++) {
+            (void)hipEventDestroy(ev_start[i]);
+            (void)hipEventDestroy(ev_stop[i]);
+        }
+        if (own_stream && stream) (void)hipStreamDestroy(stream);
+    }
 };
 
-static int timing_begin(mosaic_ctx* c, hipEvent_t* stop_out) {
+// The ABI handle: a device, the shared options and the per-thread execution states.  Chip tables
+// are immutable after mosaic_chip_table_create and may be joined from any number of threads.
+struct mosaic_ctx {
+    int device = 0;
+    int n_cu = 256;
+    std::mutex mu;
+    Options opt;
+    std::unordered_map<std::thread::id, std::unique_ptr<ThreadCtx>> threads;
+};
+
+static const int kScalars = 5;
+
+// The calling thread's execution state, options refreshed from the context (created on first use).
+static ThreadCtx* enter(mosaic_ctx* ctx) {
+    if (!ctx) return nullptr;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    std::unique_ptr<ThreadCtx>& t = ctx->threads[std::this_thread::get_id()];
+    if (!t) {
+        std::unique_ptr<ThreadCtx> n(new ThreadCtx());
+        n->device = ctx->device;
+        n->n_cu = ctx->n_cu;
+        if (hipSetDevice(ctx->device) != hipSuccess ||
+            hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking) != hipSuccess) {
+            fail(MOSAIC_E_HIP, "hipStreamCreate failed");
+            ctx->threads.erase(std::this_thread::get_id());
+            return nullptr;
+        }
+        n->own_stream = true;
+        if (n->scalars.reserve(kScalars * 8)) {
+            n->release();
+            ctx->threads.erase(std::this_thread::get_id());
+            return nullptr;
+        }
+        t = std::move(n);
+    }
+    static_cast<Options&>(*t) = ctx->opt;
+    return t.get();
+}
+#define ENTER(CTX)                                                                 \
+    ThreadCtx* c = enter(CTX);                                                     \
+    if (!c) return (CTX) ? MOSAIC_E_HIP : fail(MOSAIC_E_ARG, "null context");
+
+static int timing_begin(ThreadCtx* c, hipEvent_t* stop_out) {
     *stop_out = nullptr;
     if (!c->timing) return MOSAIC_OK;
     if (c->ev_used == c->ev_start.size()) {
@@ -1881,8 +1466,7 @@ struct mosaic_chips {
     int32_t n_polygons = 0;
     uint64_t capacity = 0;
     size_t device_bytes = 0;
-    DevBuf table, meta, ring_desc, slab_geo, slab_idx, slab_off, edges, hdr, cells, rast_edges;
-    int64_t n_edge_records = 0;
+    DevBuf table, meta, hdr, cells, rast_edges;
     int raster = 0;  // raster dims the table was built with (0: none)
     int64_t raster_cells = 0, raster_pure = 0, raster_records = 0;
     GeomStoreDev store;
@@ -1896,11 +1480,13 @@ struct mosaic_chips {
     DevBuf bng_cells, bng_leaf;
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
+    bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
+    StreamArgs stream{};
     DevBuf rsub, rmid, rblocks, rquad;  // rmid: per-tile leaf block bases
     int64_t raster_stats[6] = {0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
                                                    // line sub-blocks
     void release_all() {
-        for (DevBuf* b : {&table, &meta, &ring_desc, &slab_geo, &slab_idx, &slab_off, &edges, &hdr, &cells, &rast_edges,
+        for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
                           &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &bng_cells, &bng_leaf})
             b->release();
         store.release();
@@ -1919,7 +1505,7 @@ static bool is_device_ptr(const void* p) {
 }
 
 // Make `src` (n_bytes) available on the device: returns the pointer to use.
-static int to_device(mosaic_ctx* c, DevBuf& stage, const void* src, size_t n_bytes, const void** out) {
+static int to_device(ThreadCtx* c, DevBuf& stage, const void* src, size_t n_bytes, const void** out) {
     if (!src) {
         *out = nullptr;
         return MOSAIC_OK;
@@ -1935,7 +1521,7 @@ static int to_device(mosaic_ctx* c, DevBuf& stage, const void* src, size_t n_byt
     return MOSAIC_OK;
 }
 
-static int grid_size(mosaic_ctx* c, int64_t n) {
+static int grid_size(ThreadCtx* c, int64_t n) {
     int64_t want = (n + c->block - 1) / c->block;
     int64_t cap = (int64_t)c->n_cu * c->blocks_per_cu;
     return (int)std::max<int64_t>(1, std::min(want, cap));
@@ -1954,7 +1540,6 @@ static bool valid_res(int grid, int res) {
 
 // scalars buffer layout (unsigned long long): [0] amb_count, [1] pair_count, [2] tests, [3] flags,
 // [4] mixed-raster-cell queue length
-static const int kScalars = 5;
 
 extern "C" {
 
@@ -1973,131 +1558,124 @@ int mosaic_init(int device, mosaic_ctx** out) {
     c->device = device;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (!enter(c)) {  // the creating thread's state: fails early if the device cannot make a stream
         delete c;
-        return fail(MOSAIC_E_HIP, "hipStreamCreate failed");
-    }
-    c->own_stream = true;
-    if (c->scalars.reserve(kScalars * 8)) {
-        delete c;
-        return MOSAIC_E_NOMEM;
+        return MOSAIC_E_HIP;
     }
     *out = c;
     return MOSAIC_OK;
 }
 
-int mosaic_destroy(mosaic_ctx* c) {
-    if (!c) return MOSAIC_OK;
-    (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->amb_queue, &c->mix_queue, &c->scalars, &c->stage_x, &c->stage_y, &c->stage_v, &c->stage_out, &c->stage_out2,
-                      &c->stage_idx, &c->geo_off, &c->geo_data, &c->dec_x, &c->dec_y, &c->dec_status, &c->hx[0], &c->hx[1],
-                      &c->hy[0], &c->hy[1], &c->hcounts})
-        b->release();
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    for (size_t i = 0; i < c->ev_start.size(); i++) {
-        (void)hipEventDestroy(c->ev_start[i]);
-        (void)hipEventDestroy(c->ev_stop[i]);
+int mosaic_destroy(mosaic_ctx* ctx) {
+    if (!ctx) return MOSAIC_OK;
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        for (auto& kv : ctx->threads) kv.second->release();
+        ctx->threads.clear();
     }
-    if (c->own_stream) (void)hipStreamDestroy(c->stream);
-    delete c;
+    delete ctx;
     return MOSAIC_OK;
 }
 
-int mosaic_set_option(mosaic_ctx* c, const char* key, int64_t v) {
-    if (!c || !key) return fail(MOSAIC_E_ARG, "null argument");
+int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
+    if (!ctx || !key) return fail(MOSAIC_E_ARG, "null argument");
     std::string k(key);
+    Options o;
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        o = ctx->opt;
+    }
+    auto pow2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
     if (k == "jdk") {
         if (v < 8) return fail(MOSAIC_E_ARG, "jdk must be >= 8");
-        c->jdk = (int)v;
+        o.jdk = (int)v;
     } else if (k == "async") {
-        c->async = v ? 1 : 0;
+        o.async = v ? 1 : 0;
     } else if (k == "block") {
         if (v < 64 || v > 256 || v % 64) return fail(MOSAIC_E_ARG, "block must be 64, 128, 192 or 256");
-        c->block = (int)v;
+        o.block = (int)v;
     } else if (k == "blocks_per_cu") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "blocks_per_cu must be in [1, 64]");
-        c->blocks_per_cu = (int)v;
-    } else if (k == "pip_mode") {
-        if (v < 0 || v > 3) return fail(MOSAIC_E_ARG, "pip_mode must be 0, 1, 2 or 3");
-        c->pip_mode = (int)v;
+        o.blocks_per_cu = (int)v;
     } else if (k == "raster") {
-        if (v < 0 || v > 64) return fail(MOSAIC_E_ARG, "raster must be in [0, 64]");
-        c->raster = (int)v;
+        if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "raster must be in [1, 64]");
+        o.raster = (int)v;
     } else if (k == "lane_edges") {
         if (v < 0 || v > 32) return fail(MOSAIC_E_ARG, "lane_edges must be in [0, 32]");
-        c->lane_edges = (int)v;
+        o.lane_edges = (int)v;
     } else if (k == "tiles") {
-        c->tiles = v ? 1 : 0;
+        o.tiles = v ? 1 : 0;
     } else if (k == "point_raster") {
-        c->point_raster = v ? 1 : 0;
+        o.point_raster = v ? 1 : 0;
     } else if (k == "raster_sub") {
-        if (v < 1 || v > 64 || (v & (v - 1))) return fail(MOSAIC_E_ARG, "raster_sub must be a power of two in [1, 64]");
-        c->raster_sub = (int)v;
-    } else if (k == "probe_mask") {
-        if (v < 0 || v > 63) return fail(MOSAIC_E_ARG, "probe_mask must be in [0, 63]");
-        c->probe_mask = (int)v;
-    } else if (k == "stream_mode") {
-        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "stream_mode must be 0, 1 or 2");
-        c->stream_mode = (int)v;
+        if (v > 64 || !pow2(v)) return fail(MOSAIC_E_ARG, "raster_sub must be a power of two in [1, 64]");
+        o.raster_sub = (int)v;
+    } else if (k == "raster_cell") {
+        if (v > 32 || !pow2(v)) return fail(MOSAIC_E_ARG, "raster_cell must be a power of two in [1, 32]");
+        o.raster_cell = (int)v;
     } else if (k == "mixed_rows") {
         if (v != 1 && v != 2 && v != 4) return fail(MOSAIC_E_ARG, "mixed_rows must be 1, 2 or 4");
-        c->mixed_rows = (int)v;
+        o.mixed_rows = (int)v;
     } else if (k == "mixed_blocks_per_cu") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "mixed_blocks_per_cu must be in [1, 64]");
-        c->mixed_blocks_per_cu = (int)v;
-    } else if (k == "stream_groups") {
-        if (v != 1 && v != 2) return fail(MOSAIC_E_ARG, "stream_groups must be 1 or 2");
-        c->stream_groups = (int)v;
+        o.mixed_blocks_per_cu = (int)v;
     } else if (k == "raster_quad") {
         if (v < 0 || v > tiles::kQuadLimit)
             return fail(MOSAIC_E_ARG, "raster_quad must be 0 (off), 1 (default size) or an entry budget <= " +
                                           std::to_string(tiles::kQuadLimit));
-        c->raster_quad = (int)v;
+        o.raster_quad = (int)v;
     } else if (k == "raster_adaptive") {
-        c->raster_adaptive = v ? 1 : 0;
+        o.raster_adaptive = v ? 1 : 0;
     } else if (k == "raster_lines") {
-        c->raster_lines = v ? 1 : 0;
+        o.raster_lines = v ? 1 : 0;
     } else if (k == "host_chunk") {
         if (v < 0) return fail(MOSAIC_E_ARG, "host_chunk must be >= 0");
-        c->host_chunk = v;
-    } else if (k == "stream_persistent") {
-        c->stream_persistent = v ? 1 : 0;
-    } else if (k == "tile_lds") {
-        c->tile_lds = v ? 1 : 0;
+        o.host_chunk = v;
     } else if (k == "stream_block") {
-        if (v < 64 || v > MOSAIC_STREAM_LB || v % 64)
-            return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, " + std::to_string(MOSAIC_STREAM_LB) + "]");
-        c->stream_block = (int)v;
-    } else if (k == "raster_cell") {
-        if (v < 1 || v > 32) return fail(MOSAIC_E_ARG, "raster_cell must be in [1, 32]");
-        c->raster_cell = (int)v;
+        if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, 1024]");
+        o.stream_block = (int)v;
     } else if (k == "timing") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
-        c->timing = (int)v;
-        c->ev_used = 0;
+        o.timing = (int)v;
     } else {
         return fail(MOSAIC_E_ARG, "unknown option " + k);
+    }
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ctx->opt = o;
+    }
+    if (k == "timing") {  // the calling thread's timed-call list starts over
+        ENTER(ctx);
+        c->ev_used = 0;
     }
     return MOSAIC_OK;
 }
 
-int mosaic_get_stream(mosaic_ctx* c, void** s) {
-    if (!c || !s) return fail(MOSAIC_E_ARG, "null argument");
+int mosaic_get_stream(mosaic_ctx* ctx, void** s) {
+    if (!ctx || !s) return fail(MOSAIC_E_ARG, "null argument");
+    ENTER(ctx);
     *s = (void*)c->stream;
     return MOSAIC_OK;
 }
 
-int mosaic_set_stream(mosaic_ctx* c, void* s) {
-    if (!c) return fail(MOSAIC_E_ARG, "null argument");
-    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+int mosaic_set_stream(mosaic_ctx* ctx, void* s) {
+    ENTER(ctx);
+    if (c->own_stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+    }
     c->stream = (hipStream_t)s;
     c->own_stream = false;
     return MOSAIC_OK;
 }
 
-int mosaic_sync(mosaic_ctx* c) {
-    if (!c) return fail(MOSAIC_E_ARG, "null context");
+static int sync_impl(ThreadCtx* c);
+int mosaic_sync(mosaic_ctx* ctx) {
+    ENTER(ctx);
+    return sync_impl(c);
+}
+
+static int sync_impl(ThreadCtx* c) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned long long s[kScalars];
@@ -2110,8 +1688,9 @@ int mosaic_sync(mosaic_ctx* c) {
     return MOSAIC_OK;
 }
 
-int mosaic_kernel_times(mosaic_ctx* c, double* out_ms, int64_t cap, int64_t* n_out) {
-    if (!c || !n_out || (cap > 0 && !out_ms)) return fail(MOSAIC_E_ARG, "null argument");
+int mosaic_kernel_times(mosaic_ctx* ctx, double* out_ms, int64_t cap, int64_t* n_out) {
+    if (!ctx || !n_out || (cap > 0 && !out_ms)) return fail(MOSAIC_E_ARG, "null argument");
+    ENTER(ctx);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     int64_t n = (int64_t)c->ev_used;
@@ -2125,8 +1704,9 @@ int mosaic_kernel_times(mosaic_ctx* c, double* out_ms, int64_t cap, int64_t* n_o
     return MOSAIC_OK;
 }
 
-int mosaic_last_stats(mosaic_ctx* c, int64_t* out3) {
-    if (!c || !out3) return fail(MOSAIC_E_ARG, "null argument");
+int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3) {
+    if (!ctx || !out3) return fail(MOSAIC_E_ARG, "null argument");
+    ENTER(ctx);
     for (int i = 0; i < 3; i++) out3[i] = c->stats[i];
     return MOSAIC_OK;
 }
@@ -2166,7 +1746,7 @@ int mosaic_resolution_str(int grid, const char* s, int* out) {
 }
 
 // status (device, nullable): rows of a decoded geometry column, present iff status == 1
-static int point_to_cell_impl(mosaic_ctx* c, int grid, int res, const double* x, const double* y,
+static int point_to_cell_impl(ThreadCtx* c, int grid, int res, const double* x, const double* y,
                               const uint8_t* valid, const uint8_t* status, int64_t n, int64_t* out_cell,
                               uint8_t* out_valid) {
     int rc;
@@ -2227,8 +1807,9 @@ static int point_to_cell_impl(mosaic_ctx* c, int grid, int res, const double* x,
     return MOSAIC_OK;
 }
 
-int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, const double* y, const uint8_t* valid,
+int mosaic_point_to_cell(mosaic_ctx* ctx, int grid, int res, const double* x, const double* y, const uint8_t* valid,
                          int64_t n, int64_t* out_cell, uint8_t* out_valid) {
+    ENTER(ctx);
     if (!c || (n > 0 && (!x || !y || !out_cell))) return fail(MOSAIC_E_ARG, "null argument");
     if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
     if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
@@ -2238,8 +1819,9 @@ int mosaic_point_to_cell(mosaic_ctx* c, int grid, int res, const double* x, cons
     return point_to_cell_impl(c, grid, res, x, y, valid, nullptr, n, out_cell, out_valid);
 }
 
-int mosaic_point_to_cell_exact(mosaic_ctx* c, int res, const double* x, const double* y, int64_t n,
+int mosaic_point_to_cell_exact(mosaic_ctx* ctx, int res, const double* x, const double* y, int64_t n,
                                int64_t* out_cell) {
+    ENTER(ctx);
     if (!c || (n > 0 && (!x || !y || !out_cell))) return fail(MOSAIC_E_ARG, "null argument");
     if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
     if (!valid_res(MOSAIC_GRID_H3, res)) return res_error(MOSAIC_GRID_H3, res);
@@ -2265,7 +1847,8 @@ int mosaic_point_to_cell_exact(mosaic_ctx* c, int res, const double* x, const do
     return MOSAIC_OK;
 }
 
-int mosaic_diag_libm(mosaic_ctx* c, int fn, const double* a, const double* b, int64_t n, double* out) {
+int mosaic_diag_libm(mosaic_ctx* ctx, int fn, const double* a, const double* b, int64_t n, double* out) {
+    ENTER(ctx);
     if (!c || fn < 0 || fn > 4 || (n > 0 && (!a || !out || (fn == 4 && !b)))) return fail(MOSAIC_E_ARG, "bad argument");
     if (n <= 0) return MOSAIC_OK;
     HIP_TRY(hipSetDevice(c->device));
@@ -2286,7 +1869,7 @@ int mosaic_diag_libm(mosaic_ctx* c, int fn, const double* a, const double* b, in
 
 // Decode a point geometry column into c->dec_x / dec_y / dec_status (device); *n_rowpath = rows
 // left to the reference row path.  Synchronous.
-static int decode_points(mosaic_ctx* c, int format, const void* offsets, const uint8_t* data, const uint8_t* valid,
+static int decode_points(ThreadCtx* c, int format, const void* offsets, const uint8_t* data, const uint8_t* valid,
                          int64_t n, int64_t* n_rowpath) {
     const int fmt = format & 0xff;
     const bool off64 = !(format & MOSAIC_GEOM_OFFSETS32);
@@ -2333,7 +1916,7 @@ static int decode_points(mosaic_ctx* c, int format, const void* offsets, const u
     return MOSAIC_OK;
 }
 
-static int copy_out(mosaic_ctx* c, void* dst, const void* src, size_t bytes) {
+static int copy_out(ThreadCtx* c, void* dst, const void* src, size_t bytes) {
     if (!dst || !bytes) return MOSAIC_OK;
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, is_device_ptr(dst) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
                            c->stream));
@@ -2341,8 +1924,9 @@ static int copy_out(mosaic_ctx* c, void* dst, const void* src, size_t bytes) {
     return MOSAIC_OK;
 }
 
-int mosaic_point_geom_decode(mosaic_ctx* c, int format, const void* offsets, const uint8_t* data, const uint8_t* valid,
+int mosaic_point_geom_decode(mosaic_ctx* ctx, int format, const void* offsets, const uint8_t* data, const uint8_t* valid,
                              int64_t n, double* x, double* y, uint8_t* row_status, int64_t* n_rowpath) {
+    ENTER(ctx);
     if (!c || !offsets || (n > 0 && (!x || !y || !row_status))) return fail(MOSAIC_E_ARG, "null argument");
     if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
     if (n_rowpath) *n_rowpath = 0;
@@ -2356,9 +1940,10 @@ int mosaic_point_geom_decode(mosaic_ctx* c, int format, const void* offsets, con
     return MOSAIC_OK;
 }
 
-int mosaic_point_geom_to_cell(mosaic_ctx* c, int grid, int res, int format, const void* offsets, const uint8_t* data,
+int mosaic_point_geom_to_cell(mosaic_ctx* ctx, int grid, int res, int format, const void* offsets, const uint8_t* data,
                               const uint8_t* valid, int64_t n, int64_t* out_cell, uint8_t* row_status,
                               int64_t* n_rowpath) {
+    ENTER(ctx);
     if (!c || !offsets || (n > 0 && (!out_cell || !row_status))) return fail(MOSAIC_E_ARG, "null argument");
     if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
     if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
@@ -2460,9 +2045,10 @@ int mosaic_bng_parse(const char* cs, int64_t* out) {
     return MOSAIC_OK;
 }
 
-int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, const uint8_t* is_core,
+int mosaic_chip_table_create(mosaic_ctx* ctx, int grid, int res, int64_t n_chips, const uint8_t* is_core,
                              const int64_t* index_id, const int64_t* wkb_offsets, const uint8_t* wkb,
                              const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out) {
+    ENTER(ctx);
     if (!c || !out || n_chips < 0 || n_polygons < 0) return fail(MOSAIC_E_ARG, "invalid argument");
     if (n_chips > 0 && (!is_core || !index_id || !wkb_offsets || !polygon_key))
         return fail(MOSAIC_E_ARG, "null chip column");
@@ -2533,41 +2119,6 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
         uint32_t v0 = gb.ring_start[r0], v1 = gb.ring_start[r0 + 1];
         if (v1 > v0) ring_desc[t] = make_uint2(v0, v1 - v0);
     }
-    // slab segment lists for one-ring chips (pip_coop.h "slab-filtered edges"): ~4 segments per
-    // slab; a slab lists every segment whose y-range meets the slab widened by mu
-    std::vector<double2> slab_geo(meta.size(), make_double2(0.0, 0.0));
-    std::vector<uint2> slab_idx(meta.size(), make_uint2(0, 0));
-    std::vector<uint32_t> slab_off;
-    std::vector<pip::Edge> edges;
-    for (int64_t t = 0; t < n_chips; t++) {
-        uint2 d = ring_desc[t];
-        if (d.y < 2 || (meta[t] & 1u)) continue;
-        const pip::Vec2* v = gb.verts.data() + d.x;
-        uint32_t n = d.y;
-        double y0 = INFINITY, y1 = -INFINITY;
-        for (uint32_t k = 0; k < n; k++) {
-            y0 = std::min(y0, v[k].y);
-            y1 = std::max(y1, v[k].y);
-        }
-        uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>(64, (n - 1 + 3) / 4));
-        if (!(y1 > y0)) K = 1;
-        double hgt = y1 - y0;
-        double mu = 1e-7 * hgt + 1e-12 * std::fabs(y0) + 1e-300;
-        slab_geo[t] = make_double2(y0, K > 1 ? (double)K / hgt : 0.0);
-        slab_idx[t] = make_uint2((uint32_t)slab_off.size(), K);
-        for (uint32_t s = 0; s < K; s++) {
-            slab_off.push_back((uint32_t)edges.size());
-            double lo = s == 0 ? -INFINITY : y0 + hgt * s / K - mu;
-            double hi = s + 1 == K ? INFINITY : y0 + hgt * (s + 1) / K + mu;
-            for (uint32_t k = 1; k < n; k++) {
-                double ea = std::min(v[k].y, v[k - 1].y), eb = std::max(v[k].y, v[k - 1].y);
-                if (ea <= hi && eb >= lo) edges.push_back(pip::Edge{v[k].x, v[k].y, v[k - 1].x, v[k - 1].y});
-            }
-        }
-        slab_off.push_back((uint32_t)edges.size());
-    }
-    if (slab_off.empty()) slab_off.push_back(0);
-    if (edges.empty()) edges.push_back(pip::Edge{0, 0, 0, 0});
     // ray-parity rasters for one-ring border chips (raster.h); other chips take the general path
     raster::Builder rb;
     rb.hdr.resize(meta.size());
@@ -2603,10 +2154,6 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
     size_t total = 0;
     int rc;
     if ((rc = ch->table.reserve(capacity * sizeof(HashEntry))) || (rc = ch->meta.reserve(meta.size() * 4)) ||
-        (rc = ch->ring_desc.reserve(ring_desc.size() * sizeof(uint2))) ||
-        (rc = ch->slab_geo.reserve(slab_geo.size() * sizeof(double2))) ||
-        (rc = ch->slab_idx.reserve(slab_idx.size() * sizeof(uint2))) ||
-        (rc = ch->slab_off.reserve(slab_off.size() * 4)) || (rc = ch->edges.reserve(edges.size() * sizeof(pip::Edge))) ||
         (rc = ch->hdr.reserve(rb.hdr.size() * sizeof(raster::ChipHdr))) ||
         (rc = ch->cells.reserve(rb.cells.size() * sizeof(raster::CellRec))) ||
         (rc = ch->rast_edges.reserve(rb.edges.size() * sizeof(pip::Edge))) ||
@@ -2617,15 +2164,9 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
     }
     HIP_TRY(hipMemcpy(ch->table.p, table.data(), capacity * sizeof(HashEntry), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->ring_desc.p, ring_desc.data(), ring_desc.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->slab_geo.p, slab_geo.data(), slab_geo.size() * sizeof(double2), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->slab_idx.p, slab_idx.data(), slab_idx.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->slab_off.p, slab_off.data(), slab_off.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->edges.p, edges.data(), edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->hdr.p, rb.hdr.data(), rb.hdr.size() * sizeof(raster::ChipHdr), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
-    ch->n_edge_records = (int64_t)edges.size();
     if (grid == MOSAIC_GRID_BNG && res >= 1 && c->tiles && !cells.empty()) {
         // BNG dense cell table (see k_join_stream_bng): decode every chip cell id to its cell
         // coordinates and check the decoding by re-encoding the cell's lower-left corner
@@ -2794,20 +2335,52 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
                     ch->praster.nx = tb.grid.nx * tb.S;
                     ch->praster.ny = tb.grid.ny * tb.S;
                     ch->praster.C = tb.C;
+                    ch->praster.cshift = tb.cshift;
                     ch->praster.quad = nullptr;
                     if (!tb.quad.empty() && c->raster_quad) {
-                        size_t r2 = tb.quad.size() * 2;
+                        size_t r2 = (tb.quad.size() + 1) / 2 * 4;  // read as uint32 words by k_join_stream
                         if ((rc = ch->rquad.reserve(r2))) {
                             ch->release_all();
                             delete ch;
                             return rc;
                         }
-                        HIP_TRY(hipMemcpy(ch->rquad.p, tb.quad.data(), r2, hipMemcpyHostToDevice));
+                        HIP_TRY(hipMemcpy(ch->rquad.p, tb.quad.data(), tb.quad.size() * 2, hipMemcpyHostToDevice));
                         ch->praster.quad = (const uint16_t*)ch->rquad.p;
                         ch->praster.qnx = tb.qnx;
                         ch->praster.qny = tb.qny;
                         ch->praster.qshift = tb.qshift;
                         total += r2;
+                    }
+                    // k_join_stream's view of the raster (tiles::raster_code, lane-parallel)
+                    const size_t nsub = (size_t)ch->praster.nx * ch->praster.ny;
+                    const size_t csub_bytes = (tb.sub.size() - nsub) * 2, blocks_bytes = tb.blocks.size() * 2;
+                    if (ch->praster.quad && tb.edge_ok && csub_bytes < kNoLoad && blocks_bytes < kNoLoad &&
+                        rm < kNoLoad && (int64_t)ch->praster.nx * tb.C < (1 << 30) && (int64_t)ch->praster.ny * tb.C < (1 << 30)) {
+                        StreamArgs& sa = ch->stream;
+                        sa.x0 = tb.grid.x0;
+                        sa.y0 = tb.grid.y0;
+                        sa.sxC = ch->praster.sx * tb.C;
+                        sa.syC = ch->praster.sy * tb.C;
+                        sa.gxmax = (double)ch->praster.nx * tb.C - 1.0;
+                        sa.gymax = (double)ch->praster.ny * tb.C - 1.0;
+                        sa.cs = tb.cshift;
+                        sa.qs = tb.qshift;
+                        sa.qsh = tb.cshift + tb.qshift;
+                        sa.tsh = tb.cshift + tb.sshift;
+                        sa.qnx = tb.qnx;
+                        sa.tnx = tb.grid.nx;
+                        sa.n_quad_words = (int32_t)((tb.quad.size() + 1) / 2);
+                        sa.n_tiles = (int32_t)tb.tile_base.size();
+                        sa.tb_lds = 0;
+                        sa.stage_words = 64 + 256;
+                        sa.quad = (const uint32_t*)ch->rquad.p;
+                        sa.tile_base = (const uint32_t*)ch->rmid.p;
+                        sa.csub = (const uint16_t*)ch->rsub.p + nsub;
+                        sa.blocks = (const uint16_t*)ch->rblocks.p;
+                        sa.csub_bytes = (uint32_t)csub_bytes;
+                        sa.blocks_bytes = (uint32_t)blocks_bytes;
+                        sa.tile_base_bytes = (uint32_t)rm;
+                        ch->stream_ok = true;
                     }
                     ch->raster_stats[0] = tb.S;
                     ch->raster_stats[1] = tb.C;
@@ -2820,9 +2393,7 @@ int mosaic_chip_table_create(mosaic_ctx* c, int grid, int res, int64_t n_chips, 
             }
         }
     }
-    ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + ring_desc.size() * sizeof(uint2) +
-                       slab_geo.size() * sizeof(double2) + slab_idx.size() * sizeof(uint2) + slab_off.size() * 4 +
-                       edges.size() * sizeof(pip::Edge) + rb.hdr.size() * sizeof(raster::ChipHdr) +
+    ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + rb.hdr.size() * sizeof(raster::ChipHdr) +
                        rb.cells.size() * sizeof(raster::CellRec) + rb.edges.size() * sizeof(pip::Edge);
     *out = ch;
     return MOSAIC_OK;
@@ -2869,6 +2440,7 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
     o[1] = ch->praster.quad ? (int64_t)ch->praster.qnx * ch->praster.qny : 0;
     o[2] = ch->praster.quad ? ch->praster.qshift : 0;
     o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes) : 0;
+    o[4] = ch->stream_ok ? 1 : 0;
     return MOSAIC_OK;
 }
 
@@ -2882,8 +2454,9 @@ int mosaic_chip_table_tile_grid(const mosaic_chips* ch, double* o) {
 }
 
 static const int kLdsCountsMax = 8192;
+static const size_t kStreamLdsMax = 160 * 1024;  // LDS per CU (MI355X): one k_join_stream workgroup's budget
 
-static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
                     int64_t* counts, int64_t* out_row, int32_t* out_key, int64_t cap, int64_t* n_out) {
     bool pairs = out_row != nullptr;
     if (!c || !ch) return fail(MOSAIC_E_ARG, "null context or chip table");
@@ -2920,11 +2493,6 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.table = (const HashEntry*)ch->table.p;
     a.mask = ch->capacity - 1;
     a.chip_meta = (const uint32_t*)ch->meta.p;
-    a.chip_ring = (const uint2*)ch->ring_desc.p;
-    a.slab_geo = (const double2*)ch->slab_geo.p;
-    a.slab_idx = (const uint2*)ch->slab_idx.p;
-    a.slab_off = (const uint32_t*)ch->slab_off.p;
-    a.edges = (const pip::Edge*)ch->edges.p;
     a.hdr = (const raster::ChipHdr*)ch->hdr.p;
     a.cells = (const raster::CellRec*)ch->cells.p;
     a.rast_edges = (const pip::Edge*)ch->rast_edges.p;
@@ -2941,8 +2509,6 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     a.bng_e0 = a.bng_n0 = a.bng_ne = a.bng_nn = 0;
     a.bng_div = 1;
     a.bng_C = 1;
-    a.probe_mask = c->probe_mask;
-    a.tile_lds_n = 0;
     a.mixq = nullptr;
     a.mixq_count = sc + 4;
     a.counts = dcounts;
@@ -2962,14 +2528,19 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
     if (n > 0) {
         hipEvent_t tstop;
         if ((rc = timing_begin(c, &tstop))) return rc;
-        const bool coop = c->pip_mode == 1;
-        const bool rast = c->pip_mode == 3 && ch->raster > 0;
-        const bool slab = c->pip_mode == 2 || (c->pip_mode == 3 && ch->raster == 0);
         const bool h3g = ch->grid == MOSAIC_GRID_H3;
 #define MOSAIC_LAUNCH(KERNEL, SHM) hipLaunchKernelGGL(KERNEL, dim3(g), dim3(c->block), SHM, c->stream, a)
-        const bool tiled = rast && h3g && c->tiles && ch->tiles_ok;
+        const bool tiled = h3g && c->tiles && ch->tiles_ok;
         const bool praster = tiled && c->point_raster && ch->raster_ok;
-        const bool bngdense = !h3g && rast && c->tiles && ch->bng_ok;
+        const bool bngdense = !h3g && c->tiles && ch->bng_ok;
+        // k_join_stream's LDS: [counts + 64 spill words] [per-wave stages] [tile_base if it fits] [quad]
+        StreamArgs sa = ch->stream;
+        const int blk = c->stream_block;
+        size_t shm_s = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blk / 64) * sa.stage_words * 4 +
+                       (size_t)sa.n_quad_words * 4;
+        sa.tb_lds = shm_s + (size_t)sa.n_tiles * 4 <= kStreamLdsMax ? 1 : 0;
+        if (sa.tb_lds) shm_s += (size_t)sa.n_tiles * 4;
+        const bool stream = praster && ch->stream_ok && shm_s <= kStreamLdsMax;
         if (bngdense) {
             a.bng_cells = (const uint32_t*)ch->bng_cells.p;
             a.bng_e0 = ch->bng_e0;
@@ -3007,92 +2578,35 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
                 HIP_TRY(hipGetLastError());
             }
             tstop = nullptr;
-        } else if (praster) {
-            // rows in chunks of < 2^32 (uint32 queue entries); one chunk up to 4.29e9 rows
-            const int64_t chunk = ((int64_t)1 << 32) - 4;  // multiple of 4: chunk starts stay 32-byte aligned
+        } else if (stream) {
+            // k_join_stream + k_join_mixed over rows in chunks of < 2^32 (uint32 queue entries)
+            const int64_t chunk = ((int64_t)1 << 32) - 256;  // multiple of 256: chunk starts stay aligned
             const int64_t rows = std::min<int64_t>(n, chunk);
-            // k_join_stream grid: blocks_per_cu x block threads per CU, in stream_block workgroups
-            const int64_t rows_g = (rows + 4 * c->stream_groups - 1) / (4 * c->stream_groups);
-            const int gs = (int)std::max<int64_t>(1, std::min<int64_t>(
-                (rows_g + c->stream_block - 1) / c->stream_block,
-                (int64_t)c->n_cu * std::max(1, c->blocks_per_cu * c->block / c->stream_block)));
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
             a.mixq_count = sc + 4;
-            const bool vec = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0 && n >= 4;
+            const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
+            auto kernel_for = [&](bool vec) -> const void* {
+                if (pairs) return vec ? (const void*)k_join_stream<false, true, true> : (const void*)k_join_stream<false, true, false>;
+                if (lds) return vec ? (const void*)k_join_stream<true, false, true> : (const void*)k_join_stream<true, false, false>;
+                return vec ? (const void*)k_join_stream<false, false, true> : (const void*)k_join_stream<false, false, false>;
+            };
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blk, shm_s) != hipSuccess || per_cu < 1)
+                per_cu = 1;
             for (int64_t lo = 0; lo < n; lo += chunk) {
                 JoinArgs ac = a;
                 ac.row_lo = lo;
                 ac.n = std::min<int64_t>(n, lo + chunk);
-                const size_t qb = ch->praster.quad ? (size_t)ch->praster.qnx * ch->praster.qny * 2 : 0;
-                const size_t shm_c = (lds ? shm : 0) + qb, shm_n = qb;  // counts (LDS_COUNTS) + quad
-                // k_join_stream: + the per-wave stages (+ tile_base when the workgroup's LDS stays
-                // within kStreamLdsTile)
-                size_t sw = stream_stage_words(c->stream_block, c->stream_groups == 2 ? 2 : 1) * 4;
-                const int64_t ntiles = (int64_t)ch->tgrid.nx * ch->tgrid.ny;
-                if (c->tile_lds && (lds ? shm : 0) + qb + sw + (size_t)ntiles * 4 <= kStreamLdsTile) {
-                    ac.tile_lds_n = (int)ntiles;
-                    sw += (size_t)ntiles * 4;
-                }
-                // persistent grid (option stream_persistent): exactly the workgroups that are resident
-                // at once, so no second wave of workgroups refills LDS and runs a ragged tail
-                auto grid_for = [&](const void* kernel, size_t shm_bytes) -> int {
-                    if (!c->stream_persistent) return gs;
-                    int nb = 0;
-                    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, c->stream_block, shm_bytes) != hipSuccess ||
-                        nb < 1)
-                        nb = 1;
-                    return (int)std::max<int64_t>(1, std::min<int64_t>((rows_g + c->stream_block - 1) / c->stream_block,
-                                                                       (int64_t)c->n_cu * nb));
-                };
-#define MOSAIC_STREAM(KERNEL, SHM)                                                                        \
-    hipLaunchKernelGGL(KERNEL, dim3(grid_for(reinterpret_cast<const void*>(KERNEL), (SHM) + sw)), dim3(c->stream_block), \
-                       (SHM) + sw, c->stream, ac)
-#define MOSAIC_STREAM_G(VEC, VALID, G)                                                  \
-    do {                                                                                \
-        if (pairs) MOSAIC_STREAM((k_join_stream<false, true, VEC, VALID, G>), shm_n);    \
-        else if (lds) MOSAIC_STREAM((k_join_stream<true, false, VEC, VALID, G>), shm_c); \
-        else MOSAIC_STREAM((k_join_stream<false, false, VEC, VALID, G>), shm_n);         \
-    } while (0)
-#define MOSAIC_STREAM_V(VEC, VALID)                                  \
-    do {                                                             \
-        if (c->stream_groups == 2) MOSAIC_STREAM_G(VEC, VALID, 2);   \
-        else MOSAIC_STREAM_G(VEC, VALID, 1);                         \
-    } while (0)
-                if (c->stream_mode == 1 && vec) {
-                    // (its chunk buffers take 96 KiB of LDS: a quad level beyond 24 Ki entries stays off)
-                    if (qb > 48 * 1024) ac.praster.quad = nullptr;
-                    const size_t shm_n = ac.praster.quad ? qb : 0, shm_c = (lds ? shm : 0) + shm_n;
-                    const int gd = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_cu, (ac.n - lo + kChunkRows - 1) / kChunkRows));
-                    if (pairs)
-                        hipLaunchKernelGGL((k_join_stream_dec<false, true>), dim3(gd), dim3(1024), shm_n, c->stream, ac);
-                    else if (lds)
-                        hipLaunchKernelGGL((k_join_stream_dec<true, false>), dim3(gd), dim3(1024), shm_c, c->stream, ac);
-                    else
-                        hipLaunchKernelGGL((k_join_stream_dec<false, false>), dim3(gd), dim3(1024), shm_n, c->stream, ac);
-                } else if (c->stream_mode == 2 && vec && !a.valid && ac.n - lo >= 4) {
-                    const size_t swp = stream_stage_words(c->stream_block, 1) * 4 + (size_t)ac.tile_lds_n * 4;
-#define MOSAIC_PIPE(KERNEL, SHM)                                                                                \
-    hipLaunchKernelGGL(KERNEL, dim3(grid_for(reinterpret_cast<const void*>(KERNEL), SHM)), dim3(c->stream_block), SHM, \
-                       c->stream, ac)
-                    if (pairs)
-                        MOSAIC_PIPE((k_join_stream_pipe<false, true>), shm_n + swp);
-                    else if (lds)
-                        MOSAIC_PIPE((k_join_stream_pipe<true, false>), shm_c + swp);
-                    else
-                        MOSAIC_PIPE((k_join_stream_pipe<false, false>), shm_n + swp);
-#undef MOSAIC_PIPE
-                } else if (a.valid) {
-                    MOSAIC_STREAM_V(false, true);
-                } else if (vec && ac.n - lo >= 4) {  // the VEC prefetch re-reads a chunk's first 4 rows
-                    MOSAIC_STREAM_V(true, false);
-                } else {
-                    MOSAIC_STREAM_V(false, false);
-                }
-#undef MOSAIC_STREAM_V
-#undef MOSAIC_STREAM_G
-#undef MOSAIC_STREAM
-                HIP_TRY(hipGetLastError());
+                // 16-byte loads need aligned columns and >= 256 rows (the prefetch past the end
+                // re-reads the chunk's first 256)
+                const void* kfn = kernel_for(aligned && ac.n - lo >= 256);
+                if (lo > 0) HIP_TRY(hipMemsetAsync(ac.mixq_count, 0, 8, c->stream));
+                // persistent grid: the workgroups resident at once (each fills its LDS once)
+                const int gs = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + 4 * blk - 1) / (4 * blk),
+                                                                           (int64_t)c->n_cu * per_cu));
+                void* kargs[] = {&ac, &sa};
+                HIP_TRY(hipLaunchKernel(kfn, dim3(gs), dim3(blk), kargs, shm_s, c->stream));
                 if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
                 // (the queue holds at most the chunk's rows)
                 const int gm = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + 4 * c->block - 1) / (4 * c->block),
@@ -3123,38 +2637,14 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
             if (pairs) MOSAIC_LAUNCH((k_join_tiled<false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_tiled<true, false>), shm);
             else MOSAIC_LAUNCH((k_join_tiled<false, false>), 0);
-        } else if (rast && h3g) {
+        } else if (h3g) {
             if (pairs) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, true, false>), shm);
             else MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, false>), 0);
-        } else if (rast) {
+        } else {
             if (pairs) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, true, false>), shm);
             else MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, false, false>), 0);
-        } else if (slab && h3g) {
-            if (pairs) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, false, true>), 0);
-            else if (lds) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, true, false>), shm);
-            else MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_H3, false, false>), 0);
-        } else if (slab) {
-            if (pairs) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_BNG, false, true>), 0);
-            else if (lds) MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_BNG, true, false>), shm);
-            else MOSAIC_LAUNCH((k_join_slab<MOSAIC_GRID_BNG, false, false>), 0);
-        } else if (coop && h3g) {
-            if (pairs) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, false, true>), 0);
-            else if (lds) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, true, false>), shm);
-            else MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_H3, false, false>), 0);
-        } else if (coop) {
-            if (pairs) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_BNG, false, true>), 0);
-            else if (lds) MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_BNG, true, false>), shm);
-            else MOSAIC_LAUNCH((k_join_coop<MOSAIC_GRID_BNG, false, false>), 0);
-        } else if (h3g) {
-            if (pairs) MOSAIC_LAUNCH((k_join_h3<false, true>), 0);
-            else if (lds) MOSAIC_LAUNCH((k_join_h3<true, false>), shm);
-            else MOSAIC_LAUNCH((k_join_h3<false, false>), 0);
-        } else {
-            if (pairs) MOSAIC_LAUNCH((k_join_bng<false, true>), 0);
-            else if (lds) MOSAIC_LAUNCH((k_join_bng<true, false>), shm);
-            else MOSAIC_LAUNCH((k_join_bng<false, false>), 0);
         }
 #undef MOSAIC_LAUNCH
         HIP_TRY(hipGetLastError());
@@ -3205,7 +2695,7 @@ static int run_join(mosaic_ctx* c, const mosaic_chips* ch, const double* x, cons
 // other pair of device buffers; then chunk i is finished exactly as a synchronous call would be
 // (NaN -> MOSAIC_E_NAN; an exact-path queue overflow reruns the chunk synchronously) and its counts
 // are added on the host.  The PCIe copy and the join overlap instead of adding.
-static int join_count_host_chunked(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+static int join_count_host_chunked(ThreadCtx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
                                    int64_t* counts) {
     HIP_TRY(hipSetDevice(c->device));
     const int64_t CH = c->host_chunk;
@@ -3236,7 +2726,7 @@ static int join_count_host_chunked(mosaic_ctx* c, const mosaic_chips* ch, const 
         c->async = saved_async;
         if (rc) return rc;
         if (i + 1 < nch && (rc = copy(i + 1))) return rc;
-        rc = mosaic_sync(c);
+        rc = sync_impl(c);
         if (rc == MOSAIC_E_CAPACITY) {
             c->async = 0;
             rc = run_join(c, ch, dx, dy, m, (int64_t*)c->hcounts.p, nullptr, nullptr, 0, nullptr);
@@ -3264,22 +2754,25 @@ static int join_count_host_chunked(mosaic_ctx* c, const mosaic_chips* ch, const 
     return MOSAIC_OK;
 }
 
-int mosaic_pip_join_count(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+int mosaic_pip_join_count(mosaic_ctx* ctx, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
                           int64_t* counts) {
+    ENTER(ctx);
     if (c && ch && x && y && counts && c->host_chunk > 0 && n > c->host_chunk && ch->device == c->device &&
         !is_device_ptr(x) && !is_device_ptr(y) && !is_device_ptr(counts))
         return join_count_host_chunked(c, ch, x, y, n, counts);
     return run_join(c, ch, x, y, n, counts, nullptr, nullptr, 0, nullptr);
 }
 
-int mosaic_pip_join_pairs(mosaic_ctx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
+int mosaic_pip_join_pairs(mosaic_ctx* ctx, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
                           int64_t* out_row, int32_t* out_key, int64_t cap, int64_t* n_out) {
+    ENTER(ctx);
     if (!out_row || !out_key || !n_out || cap < 0) return fail(MOSAIC_E_ARG, "null pair output");
     return run_join(c, ch, x, y, n, nullptr, out_row, out_key, cap, n_out);
 }
 
-int mosaic_st_contains(mosaic_ctx* c, int64_t n_geoms, const int64_t* wkb_offsets, const uint8_t* wkb,
+int mosaic_st_contains(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* wkb_offsets, const uint8_t* wkb,
                        const int32_t* geom_index, const double* px, const double* py, int64_t n, uint8_t* out) {
+    ENTER(ctx);
     if (!c || n < 0 || n_geoms < 0 || (n_geoms > 0 && !wkb_offsets) || (n > 0 && (!geom_index || !px || !py || !out)))
         return fail(MOSAIC_E_ARG, "invalid argument");
     HIP_TRY(hipSetDevice(c->device));
@@ -3326,9 +2819,10 @@ int mosaic_st_contains(mosaic_ctx* c, int64_t n_geoms, const int64_t* wkb_offset
 }
 
 
-int mosaic_intersects_aggregate(mosaic_ctx* c, const mosaic_chips* left, const mosaic_chips* right,
+int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
                                 int32_t* out_left_key, int32_t* out_right_key, uint8_t* out_flag, int64_t cap,
                                 int64_t* n_out) {
+    ENTER(ctx);
     if (!c || !left || !right || !n_out || cap < 0 || (cap > 0 && (!out_left_key || !out_right_key || !out_flag)))
         return fail(MOSAIC_E_ARG, "invalid argument");
     if (left->grid != right->grid || left->res != right->res)
@@ -3404,8 +2898,9 @@ int mosaic_intersects_aggregate(mosaic_ctx* c, const mosaic_chips* left, const m
 }
 
 
-int mosaic_cell_kring(mosaic_ctx* c, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k, int loop,
+int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k, int loop,
                       int64_t* out, int32_t* out_count) {
+    ENTER(ctx);
     if (!c || n < 0 || (n > 0 && (!cells || !out || !out_count))) return fail(MOSAIC_E_ARG, "invalid argument");
     if (grid != MOSAIC_GRID_BNG)
         return fail(MOSAIC_E_ARG, "grid_cellkring / grid_cellkloop: only the BNG grid is implemented by this engine");
@@ -3451,8 +2946,9 @@ int mosaic_cell_kring(mosaic_ctx* c, int grid, const int64_t* cells, const uint8
 }
 
 
-int mosaic_bng_format_column(mosaic_ctx* c, const int64_t* ids, const uint8_t* valid, int64_t n, int64_t* offsets,
+int mosaic_bng_format_column(mosaic_ctx* ctx, const int64_t* ids, const uint8_t* valid, int64_t n, int64_t* offsets,
                              char* chars, int64_t chars_cap, int64_t* chars_needed) {
+    ENTER(ctx);
     if (!c || n < 0 || !offsets || !chars_needed || (n > 0 && !ids) || chars_cap < 0 || (chars_cap > 0 && !chars))
         return fail(MOSAIC_E_ARG, "invalid argument");
     HIP_TRY(hipSetDevice(c->device));
@@ -3518,8 +3014,9 @@ int mosaic_bng_format_column(mosaic_ctx* c, const int64_t* ids, const uint8_t* v
 }
 
 
-int mosaic_cell_boundary_wkb(mosaic_ctx* c, int grid, const int64_t* ids, const uint8_t* valid, int64_t n,
+int mosaic_cell_boundary_wkb(mosaic_ctx* ctx, int grid, const int64_t* ids, const uint8_t* valid, int64_t n,
                              uint8_t* out) {
+    ENTER(ctx);
     if (!c || n < 0 || (n > 0 && (!ids || !out))) return fail(MOSAIC_E_ARG, "invalid argument");
     if (grid != MOSAIC_GRID_BNG)
         return fail(MOSAIC_E_ARG, "grid_boundaryaswkb: only the BNG grid is implemented by this engine");
@@ -3662,9 +3159,10 @@ __global__ void __launch_bounds__(256) k_bng_tess_classify(ClassifyArgs a) {
 extern "C" {
 
 // Classification step of mosaic_tessellate_gpu (tessellate.cpp); not part of the public header.
-int mosaic_tess_classify_bng(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+int mosaic_tess_classify_bng(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                              const int64_t* ring_offsets, const double* xy, int64_t n_cand, const int32_t* cand_geom,
                              const int64_t* cand_ij, double e, double eps, uint8_t* cls) {
+    ENTER(ctx);
     if (!c || n_geoms < 0 || n_cand < 0 || (n_cand > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy ||
                                                             !cand_geom || !cand_ij || !cls)))
         return fail(MOSAIC_E_ARG, "invalid argument");
@@ -3716,7 +3214,10 @@ int mosaic_tess_classify_bng(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom
     return done(MOSAIC_OK);
 }
 
-double mosaic_tess_last_classify_ms(const mosaic_ctx* c) { return c ? c->last_tess_classify_ms : -1.0; }
+double mosaic_tess_last_classify_ms(const mosaic_ctx* ctx) {
+    ThreadCtx* c = enter(const_cast<mosaic_ctx*>(ctx));
+    return c ? c->last_tess_classify_ms : -1.0;
+}
 
 }  // extern "C"
 
@@ -3830,9 +3331,10 @@ extern "C" {
 
 // Classification step of mosaic_tessellate_gpu for per-cell convex clip polygons (H3 hexagons in the
 // face plane); not part of the public header.  xy holds the rings already in the clip plane.
-int mosaic_tess_classify_poly(mosaic_ctx* c, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+int mosaic_tess_classify_poly(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                               const int64_t* ring_offsets, const double* xy, int64_t n_cand, const int32_t* cand_geom,
                               const double* clip, int nv, double eps, uint8_t* cls) {
+    ENTER(ctx);
     if (!c || n_geoms < 0 || n_cand < 0 || nv < 3 ||
         (n_cand > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy || !cand_geom || !clip || !cls)))
         return fail(MOSAIC_E_ARG, "invalid argument");

@@ -62,11 +62,11 @@ static const uint16_t kLineBit = 0x4000u;
 static const int32_t kMaxRasterKeys = 0x7ffd;  // polygon keys 0 .. kMaxRasterKeys - 1
 
 // A sub-block split by one straight feature (a chip edge: a zone boundary or a hexagon side):
-// s = a u + b v + c over the sub-block's unit square (u, v: the point's offset in sub-block units),
-// (a, b) scaled to 1 / margin, so points with s >= 1 get code pos, s <= -1 code neg and the band
-// of half-width `margin` (sub-block units, chosen per record) between is mixed.  The host
-// certifies the two half-planes widened by kLineSlack sub-block units, far more than the float
-// evaluation's error.
+// s = a u + b v + c with (u, v) the point's offset from the sub-block's lower-left corner in leaf
+// cells (0 <= u, v < C), (a, b) scaled to 1 / (margin C), so points with s >= 1 get code pos,
+// s <= -1 code neg and the band of half-width `margin` (sub-block units, chosen per record)
+// between is mixed.  The host certifies the two half-planes widened by kLineSlack sub-block units,
+// far more than the float evaluation's error.
 struct LineRec {
     float a, b, c;
     uint16_t pos, neg;
@@ -79,13 +79,15 @@ MOSAIC_HD uint16_t line_code(const LineRec& l, float u, float v) {
 }
 
 struct PointRaster {
-    const uint16_t* sub;        // (nx) x (ny) sub-block entries (S x S per tile); nullptr: no raster
+    const uint16_t* sub;        // (nx) x (ny) sub-block entries (S x S per tile), then the compact
+                                // copies of the non-uniform quads; nullptr: no raster
     const uint32_t* tile_base;  // per tile (tnx per row): first leaf-block element of the tile
     const uint16_t* blocks;     // per tile: line records (8 elements each), C x C leaf blocks
     double sx, sy;              // sub-blocks per degree
     int32_t nx, ny, C, sshift, tnx;  // S = 1 << sshift sub-blocks per tile side
-    // quad level: one uint16 per 2^qshift x 2^qshift sub-blocks, the code they all share, kMixed
-    // (= look at the sub-block) or kSubBlock | r (= look at the sub-block's copy in compact quad r,
+    int32_t cshift;             // C = 1 << cshift leaf cells per sub-block side
+    // quad level: one uint16 per 2^qshift x 2^qshift sub-blocks: the code they all share (< 0x8000)
+    // or kSubBlock | r (= look at the sub-block's copy in compact quad r,
     // sub[nx * ny + (r << 2 qshift) + local]); small enough (<= kQuadMax entries) to live in LDS
     const uint16_t* quad;       // nullptr: no quad level
     int32_t qnx, qny, qshift;
@@ -96,110 +98,37 @@ static const int kQuadLimit = 65536;  // option raster_quad: largest entry budge
 
 MOSAIC_HD bool sub_is_block(uint32_t e) { return (e & kSubBlock) && e != kMixed; }
 
-struct Lookup4 {
-    uint32_t si[4];  // sub-block index (the grid holds < 2^28 sub-blocks)
-    uint32_t ti[4], fc[4], e[4], base[4];
-    float u[4], v[4];  // offset in the sub-block (sub-block units)
-    bool in[4];
-    uint16_t b[4], out[4];
-    LineRec l[4];
-};
-MOSAIC_HD void raster_issue4(const PointRaster& r, double x0, double y0, const double* x, const double* y,
-                             const bool* live, Lookup4& L, const uint16_t* quad_lds = nullptr) {
-    uint32_t qi[4], qo[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const double gx = (x[k] - x0) * r.sx, gy = (y[k] - y0) * r.sy;
-        L.in[k] = live[k] && gx >= 0.0 && gx < (double)r.nx && gy >= 0.0 && gy < (double)r.ny;
-        const int ix = L.in[k] ? (int)gx : 0, iy = L.in[k] ? (int)gy : 0;
-        L.si[k] = (uint32_t)iy * (uint32_t)r.nx + (uint32_t)ix;
-        L.ti[k] = (uint32_t)((iy >> r.sshift) * r.tnx + (ix >> r.sshift));
-        qi[k] = (uint32_t)((iy >> r.qshift) * r.qnx + (ix >> r.qshift));
+// The point raster's code of (x, y), grid origin (x0, y0) shared with the tile grid; the kernel
+// k_join_stream computes exactly this, lane-parallel.  Fine-cell coordinates g = (x - x0) sx C
+// (C a power of two, so g is the sub-block coordinate scaled exactly) are clamped to the grid:
+// a finite point outside lands on an edge sub-block, whose entry the builder has checked to be 0
+// (no pair; every chip cell lies well inside the grid) or kMixed.  Non-finite points: kMixed.
+// With use_quad the sub-block entry is read through the quad level and its compact copies, as the
+// kernel does; the answer is the same.
+MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, double x, double y, bool use_quad = false) {
+    if (!isfinite(x + y)) return kMixed;
+    const int C = 1 << r.cshift, cm = C - 1;
+    double gx = (x - x0) * (r.sx * (double)C), gy = (y - y0) * (r.sy * (double)C);
+    gx = fmin(fmax(gx, 0.0), (double)r.nx * C - 1.0);
+    gy = fmin(fmax(gy, 0.0), (double)r.ny * C - 1.0);
+    const int ixC = (int)gx, iyC = (int)gy, ix = ixC >> r.cshift, iy = iyC >> r.cshift;
+    uint32_t e;
+    if (use_quad && r.quad) {
+        const uint32_t q = r.quad[(uint32_t)(iy >> r.qshift) * (uint32_t)r.qnx + (uint32_t)(ix >> r.qshift)];
         const int qm = (1 << r.qshift) - 1;
-        qo[k] = (uint32_t)(((iy & qm) << r.qshift) | (ix & qm));
-        L.u[k] = (float)(gx - (double)ix);
-        L.v[k] = (float)(gy - (double)iy);
-        int cx = L.in[k] ? (int)((gx - (double)ix) * (double)r.C) : 0;
-        int cy = L.in[k] ? (int)((gy - (double)iy) * (double)r.C) : 0;
-        cx = cx < r.C - 1 ? cx : r.C - 1;
-        cy = cy < r.C - 1 ? cy : r.C - 1;
-        L.fc[k] = (uint32_t)(cy * r.C + cx);
-        // outside the grid: no pair for finite points, the tile path for non-finite ones
-        L.out[k] = (!live[k] || (isfinite(x[k]) && isfinite(y[k]))) ? (uint16_t)0 : kMixed;
-    }
-    if (quad_lds) {
-        // LDS quad level first; only points in non-uniform quads gather their sub-block (the
-        // others read sub[0], one shared line, so they cost no L2 request)
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint16_t q = quad_lds[qi[k]];
-            if (L.in[k] && !(q & kSubBlock)) {
-                L.out[k] = q;
-                L.in[k] = false;
-            } else if (q != kMixed) {  // compact copy
-                L.si[k] = (uint32_t)r.nx * (uint32_t)r.ny + ((uint32_t)(q & 0x7fffu) << (2 * r.qshift)) + qo[k];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) L.e[k] = r.sub[L.in[k] ? L.si[k] : 0];
+        e = q < kSubBlock ? q
+                          : r.sub[(size_t)r.nx * r.ny + ((size_t)(q & 0x7fffu) << (2 * r.qshift)) +
+                                  (size_t)(((iy & qm) << r.qshift) | (ix & qm))];
     } else {
-        // branch-free gathers (index 0 for points outside the grid), so the four issue together
-#pragma unroll
-        for (int k = 0; k < 4; k++) L.e[k] = r.sub[L.si[k]];
+        e = r.sub[(size_t)iy * r.nx + ix];
     }
-}
-// tile bases of the points whose sub-block entry is a leaf block (others read tile_base[0])
-MOSAIC_HD void raster_base4(const PointRaster& r, Lookup4& L) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) L.base[k] = r.tile_base[(L.in[k] && sub_is_block(L.e[k])) ? L.ti[k] : 0];
-}
-// the same from an LDS copy of tile_base: every lane reads its tile's base (no dependence on the
-// sub-block entries, so the reads go out beside the sub-block gathers)
-MOSAIC_HD void raster_base4_lds(const uint32_t* tile_base_lds, Lookup4& L) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) L.base[k] = tile_base_lds[L.in[k] ? L.ti[k] : 0];
-}
-// leaf-code gathers and line-record gathers (lanes that need neither read element 0)
-MOSAIC_HD void raster_gather4(const PointRaster& r, Lookup4& L) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const bool blk = L.in[k] && sub_is_block(L.e[k]);
-        const bool line = blk && (L.e[k] & kLineBit);
-        const size_t bi = (blk && !line) ? (size_t)L.base[k] + (size_t)(L.e[k] & 0x3fffu) * (size_t)(r.C * r.C) + L.fc[k] : 0;
-        const size_t li = line ? (size_t)L.base[k] - 8 * (size_t)((L.e[k] & 0x3fffu) + 1) : 0;
-        L.b[k] = r.blocks[bi];
-        L.l[k] = *(const LineRec*)(r.blocks + li);
-    }
-}
-MOSAIC_HD void raster_select4(Lookup4& L) {
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (L.in[k])
-            L.out[k] = !sub_is_block(L.e[k]) ? (uint16_t)L.e[k]
-                                             : ((L.e[k] & kLineBit) ? line_code(L.l[k], L.u[k], L.v[k]) : L.b[k]);
-}
-MOSAIC_HD void raster_finish4(const PointRaster& r, Lookup4& L) {
-    raster_base4(r, L);
-    raster_gather4(r, L);
-    raster_select4(L);
-}
-
-// Raster code of (x, y): grid origin (x0, y0) shared with the tile grid.
-MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, double x, double y) {
-    const double gx = (x - x0) * r.sx, gy = (y - y0) * r.sy;
-    if (!(gx >= 0.0 && gx < (double)r.nx && gy >= 0.0 && gy < (double)r.ny))
-        return (isfinite(x) && isfinite(y)) ? (uint16_t)0 : kMixed;
-    const int ix = (int)gx, iy = (int)gy;
-    const uint16_t e = r.sub[(int64_t)iy * r.nx + ix];
-    if (!sub_is_block(e)) return e;
+    if (!sub_is_block(e)) return (uint16_t)e;
     const size_t base = r.tile_base[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)];
+    const uint32_t n = e & 0x3fffu;
     if (e & kLineBit)
-        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)((e & 0x3fffu) + 1)), (float)(gx - (double)ix),
-                         (float)(gy - (double)iy));
-    int cx = (int)((gx - (double)ix) * (double)r.C), cy = (int)((gy - (double)iy) * (double)r.C);
-    cx = cx < r.C - 1 ? cx : r.C - 1;
-    cy = cy < r.C - 1 ? cy : r.C - 1;
-    return r.blocks[base + (size_t)(e & 0x3fffu) * (size_t)(r.C * r.C) + (size_t)(cy * r.C + cx)];
+        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)(gx - (double)(ixC & ~cm)),
+                         (float)(gy - (double)(iyC & ~cm)));
+    return r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
 }
 
 struct TileRec {
@@ -284,7 +213,8 @@ struct Builder {
     // element tile_base[tile], its line records (LineRec, 8 elements) just below it, last first.
     // Codes: 0 = the point joins nothing, k + 1 = exactly one pair with polygon key k, kMixed =
     // run the tile path.
-    int S = 0, C = 0, sshift = 0;
+    int S = 0, C = 0, sshift = 0, cshift = 0;
+    bool edge_ok = false;  // every edge sub-block is 0 or kMixed (raster_code clamps onto them)
     std::vector<uint16_t> sub;
     std::vector<uint32_t> tile_base;
     std::vector<uint16_t> blocks;

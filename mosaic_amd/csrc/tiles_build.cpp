@@ -191,10 +191,12 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     blocks.clear();
     quad.clear();
     n_sub_pure = n_sub_mixed = n_cell_mixed = n_sub_line = 0;
-    if (tile_idx.empty() || S < 1 || S > 128 || (S & (S - 1)) || C < 1 || S * C > 1024) return false;
+    if (tile_idx.empty() || S < 1 || S > 128 || (S & (S - 1)) || C < 1 || (C & (C - 1)) || S * C > 1024) return false;
     if (src.n_polygons > (int32_t)kMaxRasterKeys) return false;  // codes must stay below kSubBlock
     sshift = 0;
     while ((1 << sshift) < S) sshift++;
+    cshift = 0;
+    while ((1 << cshift) < C) cshift++;
     const int nx = grid.nx, ny = grid.ny, N = S * C;
     const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
     if (NX * NY > ((int64_t)1 << 28)) return false;
@@ -413,6 +415,10 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                     if (cn == kMixed) continue;
                     out.pos = cp;
                     out.neg = cn;
+                    // the device evaluates the line at leaf-cell offsets u C, v C: a / C, b / C
+                    // (C a power of two: the same products, bit for bit)
+                    out.a = (float)((double)out.a / C);
+                    out.b = (float)((double)out.b / C);
                     return true;
                 }
                 return false;
@@ -502,6 +508,20 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
             memcpy(blocks.data() + at[r] - 8 * (n + 1), &tile_lines[r][n], sizeof(LineRec));
         std::copy(tile_blocks[r].begin(), tile_blocks[r].end(), blocks.begin() + (ptrdiff_t)at[r]);
     }
+    // clamping (raster_code, k_join_stream): a finite point outside the grid is looked up at the
+    // nearest edge sub-block, so every edge sub-block must answer "no pair" (0) or kMixed (the
+    // tile path, which finds no chip outside the grid); chip cells lie >= k tile rings inside
+    edge_ok = true;
+    for (int64_t i = 0; i < NX && edge_ok; i++)
+        for (int64_t j : {(int64_t)0, NY - 1}) {
+            const uint16_t e = sub[(size_t)(j * NX + i)];
+            if (e != 0 && e != kMixed) edge_ok = false;
+        }
+    for (int64_t j = 0; j < NY && edge_ok; j++)
+        for (int64_t i : {(int64_t)0, NX - 1}) {
+            const uint16_t e = sub[(size_t)(j * NX + i)];
+            if (e != 0 && e != kMixed) edge_ok = false;
+        }
     n_sub_line = nline.load();
     n_sub_pure = pure.load();
     n_sub_mixed = mixed.load();
@@ -551,6 +571,8 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                     qe = (uint16_t)(kSubBlock | r);
                     r++;
                 }
+        } else {
+            quad.clear();  // no quad level: k_join_stream needs one (the tile path serves)
         }
     }
     return true;

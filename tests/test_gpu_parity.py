@@ -213,13 +213,15 @@ def test_join_counts_match_oracle(h3ctx, zones, res):
     assert total > 1000
     assert int(got.sum()) == total
     assert h3ctx.last_stats()["contains_tests"] > 0
-    # every contains strategy of the fused kernel gives the same counts
+    # the tile path and the generic path (no tile directory) give the same counts
     try:
-        for mode in (0, 1, 2):
-            h3ctx.set_option("pip_mode", mode)
-            assert np.array_equal(h3ctx.pip_join_count(table, x, y), want), mode
+        for tiles, praster in ((1, 0), (0, 0)):
+            h3ctx.set_option("tiles", tiles)
+            h3ctx.set_option("point_raster", praster)
+            assert np.array_equal(h3ctx.pip_join_count(table, x, y), want), (tiles, praster)
     finally:
-        h3ctx.set_option("pip_mode", 3)
+        h3ctx.set_option("tiles", 1)
+        h3ctx.set_option("point_raster", 1)
 
 
 def _chip_boundary_points(chips, rng, limit=4000):
@@ -243,7 +245,7 @@ def _chip_boundary_points(chips, rng, limit=4000):
 
 def test_join_tessellated_chips_every_strategy(h3ctx):
     """Real grid_tessellateexplode chips (35 NYC zones, res 9) with points on / next to the chips'
-    own vertices and segments: every contains strategy and raster size gives the oracle's pairs.
+    own vertices and segments: every join path and raster size gives the oracle's pairs.
 
     Chip vertices include H3 cell corners, where H3's answer hangs on the last bit of libm: the
     exact path's glibc restatement makes every row's cell equal the oracle's."""
@@ -266,26 +268,26 @@ def test_join_tessellated_chips_every_strategy(h3ctx):
     assert total > 10_000
     want = set(zip(orow.tolist(), okey.tolist()))
     try:
-        for raster, lane_edges in ((16, 8), (1, 8), (5, 0), (32, 32), (0, 8)):
+        for raster, lane_edges in ((16, 8), (1, 8), (5, 0), (32, 32), (2, 0)):
             h3ctx.set_option("raster", raster)
             h3ctx.set_option("lane_edges", lane_edges)
             table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
                                      n_polygons=len(zones35))
             assert table.tiles()["built"] == 1
-            for mode, tiles, praster in ((3, 1, 1), (3, 1, 0), (3, 0, 0), (2, 1, 1), (0, 1, 1)):
-                h3ctx.set_option("pip_mode", mode)
+            for tiles, praster in ((1, 1), (1, 0), (0, 0)):
                 h3ctx.set_option("tiles", tiles)
                 h3ctx.set_option("point_raster", praster)
                 rows, keys = h3ctx.pip_join_pairs(table, x, y)
                 got = set(zip(rows.tolist(), keys.tolist()))
-                assert got == want, (raster, lane_edges, mode, tiles, praster, len(got ^ want))
+                assert got == want, (raster, lane_edges, tiles, praster, len(got ^ want))
+                counts = h3ctx.pip_join_count(table, x, y)
+                assert np.array_equal(counts, np.bincount(okey, minlength=len(zones35))), (raster, tiles, praster)
             h3ctx.set_option("tiles", 1)
             h3ctx.set_option("point_raster", 1)
             table.close()
     finally:
         h3ctx.set_option("raster", 16)
         h3ctx.set_option("lane_edges", 0)
-        h3ctx.set_option("pip_mode", 3)
         h3ctx.set_option("tiles", 1)
         h3ctx.set_option("point_raster", 1)
 
@@ -338,29 +340,32 @@ def test_join_tiled_nyc_zones_match_oracle(h3ctx, zones):
     rows, keys = h3ctx.pip_join_pairs(table, x[keep], y[keep])
     assert len(rows) == total and np.array_equal(np.bincount(keys, minlength=len(zones)), want)
     try:
-        # loader / worker and pipelined variants of the stream kernel, other workgroup sizes
-        for mode, block in ((1, 512), (2, 256), (2, 512), (0, 256), (0, 1024)):
-            h3ctx.set_option("stream_mode", mode)
+        # other workgroup sizes of the stream kernel
+        for block in (256, 512, 64):
             h3ctx.set_option("stream_block", block)
-            assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (mode, block)
+            assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), block
             rows2, keys2 = h3ctx.pip_join_pairs(table, x[keep], y[keep])
-            assert np.array_equal(np.sort(rows2), np.sort(rows)), (mode, block)
-        # row counts that are not multiples of 4 (the pipelined kernel queues the tail rows)
+            assert np.array_equal(np.sort(rows2), np.sort(rows)), block
+        h3ctx.set_option("stream_block", 1024)
+        # row counts that are not multiples of 256 (the wave's tail iteration), misaligned columns
+        # (the scalar-load variant) and the tiled kernel agree with the oracle on every prefix
+        import torch
+
         xs, ys = x[keep], y[keep]
-        for cut in (1, 2, 3, len(xs) - 5):
-            h3ctx.set_option("stream_mode", 0)
-            ref = h3ctx.pip_join_count(table, xs[:-cut], ys[:-cut])
-            h3ctx.set_option("stream_mode", 2)
+        xt, yt = torch.from_numpy(xs).cuda(), torch.from_numpy(ys).cuda()
+        for cut in (1, 2, 3, 255, 257, len(xs) - 5):
+            ref, _ = oracle.pip_join(oc, oracle.GRID_H3, 9, xs[:-cut], ys[:-cut], len(zones), threads=8)
             assert np.array_equal(h3ctx.pip_join_count(table, xs[:-cut], ys[:-cut]), ref), cut
-        h3ctx.set_option("stream_mode", 0)
-        h3ctx.set_option("stream_block", 512)
+            # device columns starting 8 bytes past a 16-byte boundary
+            ref1, _ = oracle.pip_join(oc, oracle.GRID_H3, 9, xs[1:-cut], ys[1:-cut], len(zones), threads=8)
+            got1 = h3ctx.pip_join_count(table, xt[1:-cut], yt[1:-cut]).cpu().numpy()
+            assert np.array_equal(got1, ref1), cut
         for tiles, praster in ((1, 0), (0, 0)):
             h3ctx.set_option("tiles", tiles)
             h3ctx.set_option("point_raster", praster)
             assert np.array_equal(h3ctx.pip_join_count(table, x[keep], y[keep]), want), (tiles, praster)
     finally:
-        h3ctx.set_option("stream_mode", 0)
-        h3ctx.set_option("stream_block", 512)
+        h3ctx.set_option("stream_block", 1024)
         h3ctx.set_option("tiles", 1)
         h3ctx.set_option("point_raster", 1)
     table.close()

@@ -1,0 +1,76 @@
+"""GPU: one context shared by concurrent caller threads ("All entry points are
+thread-safe.  Concurrent callers are multiplexed onto per-thread HIP streams"; INTEGRATION.md: one
+context per executor, used by its task threads).  Four Python threads (ctypes releases the GIL, so
+the calls overlap) join different point sets against the same chip table, counts and pairs, host
+and device inputs, with different options changing underneath them; every result equals the oracle."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from mosaic_amd.context import tessellate
+from mosaic_amd.data import PolygonSet, quickstart_points
+from tests.helpers import chips_to_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def h3ctx():
+    from mosaic_amd import MosaicContext
+
+    ctx = MosaicContext.build("H3", "JTS")
+    yield ctx
+    ctx.close()
+
+
+def test_concurrent_joins_on_one_context(h3ctx):
+    import torch
+
+    zones = PolygonSet.load("nyc_taxi_zones_35")
+    chips = tessellate("H3", zones, 9)
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
+                             n_polygons=len(zones))
+    assert table.tiles()["stream"] == 1
+    oc = chips_to_oracle(chips)
+    cases = []
+    for t in range(4):
+        x, y = quickstart_points(zones, 150_000 + 7919 * t, seed=100 + t)
+        want, total = oracle.pip_join(oc, oracle.GRID_H3, 9, x, y, len(zones), threads=4)
+        _, _, orow, okey = oracle.pip_join(oc, oracle.GRID_H3, 9, x, y, len(zones), pairs=True)
+        cases.append((x, y, want, set(zip(orow.tolist(), okey.tolist()))))
+    errors = []
+    barrier = threading.Barrier(4)
+
+    def worker(t):
+        try:
+            x, y, want, pairs = cases[t]
+            xt = torch.from_numpy(x).cuda() if t % 2 else x
+            yt = torch.from_numpy(y).cuda() if t % 2 else y
+            barrier.wait()
+            for it in range(6):
+                got = h3ctx.pip_join_count(table, xt, yt)
+                got = got.cpu().numpy() if hasattr(got, "cpu") else got
+                if not np.array_equal(got, want):
+                    errors.append((t, it, "counts"))
+                if it % 3 == 2:
+                    rows, keys = h3ctx.pip_join_pairs(table, x, y)
+                    if set(zip(rows.tolist(), keys.tolist())) != pairs:
+                        errors.append((t, it, "pairs"))
+                # options change under the other threads; each call copies them once at entry
+                h3ctx.set_option("stream_block", 512 if (t + it) % 2 else 1024)
+                h3ctx.set_option("mixed_rows", (1, 2, 4)[(t + it) % 3])
+        except Exception as e:  # surfaced below
+            errors.append((t, "exception", repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=300)
+    h3ctx.set_option("stream_block", 1024)
+    h3ctx.set_option("mixed_rows", 4)
+    table.close()
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors[:5]

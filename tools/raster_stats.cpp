@@ -1,0 +1,199 @@
+// Measurement tool (not product code): builds the H3 tile directory + point raster of
+// mosaic_amd/csrc/tiles_build.cpp on the host for a chip set and reports, for uniform points over a
+// box, which level of the raster decides them -- and what finer LDS quad levels would decide.
+// Input: the chips.bin format of tests/native/tiles_selfcheck.cpp.
+// Usage: raster_stats <chips.bin> <points> <x0> <y0> <x1> <y1> [S C threads]
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <chrono>
+#include <random>
+#include <set>
+#include <unordered_map>
+#include <vector>
+
+#include "../mosaic_amd/csrc/geom_build.h"
+#include "../mosaic_amd/csrc/tiles_build.cpp"
+
+using namespace mosaic;
+
+int main(int argc, char** argv) {
+    if (argc < 7) return 2;
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) return 2;
+    int32_t res = 0;
+    uint32_t nchips = 0;
+    if (fread(&res, 4, 1, f) != 1 || fread(&nchips, 4, 1, f) != 1) return 2;
+    struct Row {
+        int64_t cell;
+        uint8_t core;
+        int32_t key;
+        std::vector<uint8_t> wkb;
+    };
+    std::vector<Row> rows(nchips);
+    int32_t npoly = 0;
+    for (auto& r : rows) {
+        uint32_t len = 0;
+        if (fread(&r.cell, 8, 1, f) != 1 || fread(&r.core, 1, 1, f) != 1 || fread(&r.key, 4, 1, f) != 1 ||
+            fread(&len, 4, 1, f) != 1)
+            return 2;
+        r.wkb.resize(len);
+        if (len && fread(r.wkb.data(), 1, len, f) != len) return 2;
+        npoly = std::max(npoly, r.key + 1);
+    }
+    fclose(f);
+    std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) { return a.cell < b.cell; });
+    GeomBuilder gb;
+    std::vector<uint32_t> meta(nchips);
+    for (uint32_t k = 0; k < nchips; k++) {
+        meta[k] = ((uint32_t)rows[k].key << 1) | (rows[k].core ? 1u : 0u);
+        if (!gb.add(rows[k].core ? nullptr : rows[k].wkb.data(), rows[k].core ? 0 : rows[k].wkb.size())) return 3;
+    }
+    std::vector<int64_t> cells;
+    std::vector<uint32_t> first, count;
+    for (uint32_t k = 0; k < nchips; k++) {
+        if (cells.empty() || cells.back() != rows[k].cell) {
+            cells.push_back(rows[k].cell);
+            first.push_back(k);
+            count.push_back(0);
+        }
+        count.back()++;
+    }
+    const uint32_t n = (uint32_t)cells.size();
+    std::unordered_map<int64_t, int64_t> slot;
+    std::vector<uint32_t> slot_first(n), slot_count(n);
+    for (uint32_t k = 0; k < n; k++) {
+        slot.emplace(cells[k], (int64_t)k);
+        slot_first[k] = first[k];
+        slot_count[k] = count[k];
+    }
+    auto slot_of = [&](int64_t h) -> int64_t {
+        auto it = slot.find(h);
+        return it == slot.end() ? -1 : it->second;
+    };
+    const long npts = atol(argv[2]);
+    const double bx0 = atof(argv[3]), by0 = atof(argv[4]), bx1 = atof(argv[5]), by1 = atof(argv[6]);
+    const int S = argc > 8 ? atoi(argv[7]) : 64, C = argc > 8 ? atoi(argv[8]) : 16;
+    const int threads = argc > 9 ? atoi(argv[9]) : 8;
+    auto t0 = std::chrono::steady_clock::now();
+    tiles::Builder tb;
+    if (!tb.build(res, cells, slot_of)) {
+        fprintf(stderr, "directory not built: %s\n", tb.why);
+        return 1;
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    tiles::Builder::ChipSource src;
+    src.slot_first = slot_first.data();
+    src.slot_count = slot_count.data();
+    src.meta = meta.data();
+    src.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(), gb.part_ring.data(),
+                               gb.geom_part.data(), gb.geom_bbox.data()};
+    src.n_polygons = npoly;
+    if (!tb.build_raster(src, S, C, threads)) {
+        fprintf(stderr, "raster not built\n");
+        return 1;
+    }
+    auto t2 = std::chrono::steady_clock::now();
+    printf("directory %.3f s, raster %.3f s (%d threads)\n", std::chrono::duration<double>(t1 - t0).count(),
+           std::chrono::duration<double>(t2 - t1).count(), threads);
+    const int64_t NX = (int64_t)tb.grid.nx * S, NY = (int64_t)tb.grid.ny * S;
+    printf("grid %d x %d tiles, %lld x %lld sub-blocks, records %zu; sub pure %lld mixed %lld line %lld; "
+           "blocks %zu elements; quad %d x %d shift %d\n",
+           tb.grid.nx, tb.grid.ny, (long long)NX, (long long)NY, tb.recs.size(), (long long)tb.n_sub_pure,
+           (long long)tb.n_sub_mixed, (long long)tb.n_sub_line, tb.blocks.size(), tb.qnx, tb.qny, tb.qshift);
+    const uint16_t* sub = tb.sub.data();
+    auto sub_at = [&](int64_t i, int64_t j) { return sub[(size_t)(j * NX + i)]; };
+    // per quad shift q: uniform quads (one pure code over all their sub-blocks)
+    for (int q = 1; q <= 5; q++) {
+        const int64_t qnx = (NX + (1 << q) - 1) >> q, qny = (NY + (1 << q) - 1) >> q;
+        std::vector<uint16_t> qc((size_t)(qnx * qny), 0xfffe);
+        for (int64_t j = 0; j < NY; j++)
+            for (int64_t i = 0; i < NX; i++) {
+                uint16_t e = sub_at(i, j);
+                uint16_t c = (e & tiles::kSubBlock) ? tiles::kMixed : e;
+                uint16_t& d = qc[(size_t)((j >> q) * qnx + (i >> q))];
+                if (d == 0xfffe) d = c;
+                else if (d != c) d = tiles::kMixed;
+            }
+        int64_t nonu = 0;
+        for (uint16_t c : qc) nonu += c == tiles::kMixed;
+        // super-tiles of 16 x 16 quads: distinct codes
+        const int64_t snx = (qnx + 15) / 16, sny = (qny + 15) / 16;
+        std::vector<std::set<uint16_t>> pal((size_t)(snx * sny));
+        for (int64_t j = 0; j < NY; j++)
+            for (int64_t i = 0; i < NX; i++) {
+                uint16_t e = sub_at(i, j);
+                if (e & tiles::kSubBlock) continue;
+                pal[(size_t)(((j >> q) / 16) * snx + ((i >> q) / 16))].insert(e);
+            }
+        size_t pmax = 0, over14 = 0, over6 = 0;
+        for (auto& s : pal) {
+            pmax = std::max(pmax, s.size());
+            over14 += s.size() > 14;
+            over6 += s.size() > 6;
+        }
+        // uniform points
+        std::mt19937_64 rng(7);
+        std::uniform_real_distribution<double> u(0.0, 1.0);
+        long in_uni = 0, in_grid = 0;
+        for (long k = 0; k < npts / 4; k++) {
+            double x = bx0 + (bx1 - bx0) * u(rng), y = by0 + (by1 - by0) * u(rng);
+            double gx = (x - tb.grid.x0) * tb.grid.sx * S, gy = (y - tb.grid.y0) * tb.grid.sy * S;
+            if (!(gx >= 0 && gx < NX && gy >= 0 && gy < NY)) {
+                in_uni++;
+                continue;
+            }
+            in_grid++;
+            if (qc[(size_t)(((int64_t)gy >> q) * qnx + ((int64_t)gx >> q))] != tiles::kMixed) in_uni++;
+        }
+        printf("q %d: %lld x %lld quads (%lld), non-uniform %lld (%.1f%%); points decided by the quad level %.4f; "
+               "super-tiles %lld, palette max %zu, >6 codes %zu, >14 codes %zu; LDS nibbles %.1f KB\n",
+               q, (long long)qnx, (long long)qny, (long long)(qnx * qny), (long long)nonu,
+               100.0 * nonu / (qnx * qny), (double)in_uni / (npts / 4), (long long)(snx * sny), pmax, over6, over14,
+               qnx * qny / 2048.0);
+    }
+    // point categories under the built raster (its own quad level)
+    std::mt19937_64 rng(11);
+    std::uniform_real_distribution<double> u(0.0, 1.0);
+    long c_out = 0, c_quad = 0, c_sub = 0, c_line = 0, c_line_mixed = 0, c_leaf = 0, c_leaf_mixed = 0, c_submixed = 0;
+    const int qs = tb.qshift;
+    for (long k = 0; k < npts; k++) {
+        double x = bx0 + (bx1 - bx0) * u(rng), y = by0 + (by1 - by0) * u(rng);
+        double gx = (x - tb.grid.x0) * tb.grid.sx * S, gy = (y - tb.grid.y0) * tb.grid.sy * S;
+        if (!(gx >= 0 && gx < NX && gy >= 0 && gy < NY)) {
+            c_out++;
+            continue;
+        }
+        int64_t ix = (int64_t)gx, iy = (int64_t)gy;
+        uint16_t qe = tb.quad.empty() ? tiles::kMixed : tb.quad[(size_t)((iy >> qs) * tb.qnx + (ix >> qs))];
+        if (!(qe & tiles::kSubBlock)) {
+            c_quad++;
+            continue;
+        }
+        uint16_t e = sub_at(ix, iy);
+        if (!tiles::sub_is_block(e)) {
+            if (e == tiles::kMixed) c_submixed++;
+            else c_sub++;
+            continue;
+        }
+        uint16_t code = tiles::raster_code(
+            tiles::PointRaster{sub, tb.tile_base.data(), tb.blocks.data(), tb.grid.sx * S, tb.grid.sy * S, (int32_t)NX,
+                               (int32_t)NY, C, tb.sshift, tb.grid.nx, tb.cshift, nullptr, 0, 0, 0},
+            tb.grid.x0, tb.grid.y0, x, y);
+        if (e & tiles::kLineBit) {
+            c_line++;
+            c_line_mixed += code == tiles::kMixed;
+        } else {
+            c_leaf++;
+            c_leaf_mixed += code == tiles::kMixed;
+        }
+    }
+    printf("uniform points %ld: outside grid %.4f, quad level %.4f, sub-block pure %.4f, sub-block mixed %.4f, "
+           "line %.4f (mixed band %.5f), leaf %.4f (mixed cell %.5f)\n",
+           npts, (double)c_out / npts, (double)c_quad / npts, (double)c_sub / npts, (double)c_submixed / npts,
+           (double)c_line / npts, (double)c_line_mixed / npts, (double)c_leaf / npts, (double)c_leaf_mixed / npts);
+    return 0;
+}
