@@ -154,6 +154,26 @@ int mosaic_point_geom_to_cell(mosaic_ctx* ctx, int grid, int res, int format, co
 int mosaic_point_geom_decode(mosaic_ctx* ctx, int format, const void* offsets, const uint8_t* data,
                              const uint8_t* valid, int64_t n, double* x, double* y, uint8_t* row_status,
                              int64_t* n_rowpath);
+/* grid_pointascellid over the COORDS form of points: InternalGeometryType rows
+ * struct<typeId: int, srid: int, boundaries: array<array<array<double>>>, holes: ...>
+ * (core/types/model/InternalGeometry.scala; st_point's output, expressions/constructors/ST_Point.scala:27-32)
+ * as Arrow columns: type_id[n]; boundary_offsets[n + 1] (row -> boundaries), coord_offsets
+ * (boundary -> coordinates), value_offsets (coordinate -> values), all int32 (Arrow list); values
+ * (float64).  Rows with type_id 1 (POINT) whose first boundary's first coordinate has 2 values, or
+ * 3 or more (z ignored), are decoded as MosaicPointJTS.fromInternal does
+ * (core/geometry/point/MosaicPointJTS.scala:82-89) and indexed: MOSAIC_ROW_OK.  Null rows:
+ * MOSAIC_ROW_NULL.  Other types (the reference indexes their centroid) and rows the reference throws
+ * on (no boundary, no coordinate, a 1-value coordinate): MOSAIC_ROW_PATH.  Child arrays must not
+ * hold nulls.  The holes column is not read (a Point has none). */
+int mosaic_point_coords_to_cell(mosaic_ctx* ctx, int grid, int res, const int32_t* type_id,
+                                const int32_t* boundary_offsets, const int32_t* coord_offsets,
+                                const int32_t* value_offsets, const double* values, const uint8_t* valid, int64_t n,
+                                int64_t* out_cell, uint8_t* row_status, int64_t* n_rowpath);
+/* The decode alone: x / y of MOSAIC_ROW_OK rows (0 elsewhere), row_status as above. */
+int mosaic_point_coords_decode(mosaic_ctx* ctx, const int32_t* type_id, const int32_t* boundary_offsets,
+                               const int32_t* coord_offsets, const int32_t* value_offsets, const double* values,
+                               const uint8_t* valid, int64_t n, double* x, double* y, uint8_t* row_status,
+                               int64_t* n_rowpath);
 /* BNG id <-> string (BNGIndexSystem.format / parse).  format returns the string length. */
 int mosaic_bng_format(int64_t id, char* buf, size_t cap);
 int mosaic_bng_parse(const char* s, int64_t* out);
@@ -165,6 +185,15 @@ int mosaic_bng_parse(const char* s, int64_t* out);
 int mosaic_bng_format_column(mosaic_ctx* ctx, const int64_t* ids, const uint8_t* valid, int64_t n, int64_t* offsets,
                              char* chars, int64_t chars_cap, int64_t* chars_needed);
 
+/* BNGIndexSystem.parse (BNGIndexSystem.scala:391-413) over a string column on the GPU: the
+ * StringType cell ids of BNG chips (BNGIndexSystem.scala:28, serializeCellId IndexSystem.scala:37-46)
+ * back to the long ids mosaic_chip_table_create takes.  Arrow utf8 (offsets32 = 1: int32 offsets) or
+ * large_utf8 (int64 offsets) layout, offsets[n + 1] + chars; null rows (valid[i] == 0) give 0.
+ * A row the reference cannot parse (its letterMap lookup or Integer.parseInt throws) gives
+ * MOSAIC_E_ARG naming the first such row. */
+int mosaic_bng_parse_column(mosaic_ctx* ctx, int offsets32, const void* offsets, const uint8_t* chars,
+                            const uint8_t* valid, int64_t n, int64_t* out_ids);
+
 /* ---- chip table (build side) ---- */
 /* n_chips rows of ChipType: is_core[i], index_id[i] (int64 cell id), wkb bytes
  * wkb[wkb_offsets[i] .. wkb_offsets[i+1]) (Polygon / MultiPolygon, either byte order; empty or
@@ -173,6 +202,13 @@ int mosaic_bng_format_column(mosaic_ctx* ctx, const int64_t* ids, const uint8_t*
 int mosaic_chip_table_create(mosaic_ctx* ctx, int grid, int res, int64_t n_chips, const uint8_t* is_core,
                              const int64_t* index_id, const int64_t* wkb_offsets, const uint8_t* wkb,
                              const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out);
+/* The same over Arrow columns as a JNI shim hands them over: wkb_offsets are int32 (Arrow binary)
+ * when wkb_offsets32 != 0, else int64 (large_binary).  BNG StringType ids: parse them first with
+ * mosaic_bng_parse_column. */
+int mosaic_chip_table_create_arrow(mosaic_ctx* ctx, int grid, int res, int64_t n_chips, const uint8_t* is_core,
+                                   const int64_t* index_id, const void* wkb_offsets, int wkb_offsets32,
+                                   const uint8_t* wkb, const int32_t* polygon_key, int32_t n_polygons,
+                                   mosaic_chips** out);
 int mosaic_chip_table_destroy(mosaic_chips* chips);
 /* out8: n_chips, n_cells, n_border, n_vertices, n_rings, device_bytes, hash_capacity, n_polygons */
 int mosaic_chip_table_info(const mosaic_chips* chips, int64_t* out8);

@@ -37,7 +37,8 @@ EXPORTS = [
     "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_point_geom_to_cell",
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
     "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb", "mosaic_point_to_cell_exact",
-    "mosaic_diag_libm",
+    "mosaic_diag_libm", "mosaic_point_coords_to_cell", "mosaic_point_coords_decode", "mosaic_bng_parse_column",
+    "mosaic_chip_table_create_arrow",
 ]
 
 GEOM_WKB = 0
@@ -126,6 +127,10 @@ def lib():
         "mosaic_tess_last_classify_ms": ([vp], ctypes.c_double),
         "mosaic_point_to_cell_exact": ([vp, i32, vp, vp, i64, vp], i32),
         "mosaic_diag_libm": ([vp, i32, vp, vp, i64, vp], i32),
+        "mosaic_point_coords_to_cell": ([vp, i32, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, ctypes.POINTER(i64)], i32),
+        "mosaic_point_coords_decode": ([vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, ctypes.POINTER(i64)], i32),
+        "mosaic_bng_parse_column": ([vp, i32, vp, vp, vp, i64, vp], i32),
+        "mosaic_chip_table_create_arrow": ([vp, i32, i32, i64, vp, vp, vp, i32, vp, vp, i32, ctypes.POINTER(vp)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

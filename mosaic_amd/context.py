@@ -138,6 +138,58 @@ def geometry_column(geoms):
     return fmt, offsets, data, valid
 
 
+class CoordsColumn:
+    """The COORDS geometry form (InternalGeometryType: struct<typeId, srid, boundaries:
+    array<array<array<double>>>, holes: array<array<array<array<double>>>>>,
+    core/types/model/InternalGeometry.scala) as Arrow columns: type_id int32[n], srid int32[n],
+    boundary_offsets int32[n + 1] (row -> boundaries), coord_offsets int32 (boundary -> coordinates),
+    value_offsets int32 (coordinate -> values), values float64, validity uint8 or None.  The holes
+    column is not kept (no point has one)."""
+
+    def __init__(self, type_id, srid, boundary_offsets, coord_offsets, value_offsets, values, valid=None):
+        self.type_id = np.ascontiguousarray(type_id, np.int32)
+        self.srid = np.ascontiguousarray(srid, np.int32)
+        self.boundary_offsets = np.ascontiguousarray(boundary_offsets, np.int32)
+        self.coord_offsets = np.ascontiguousarray(coord_offsets, np.int32)
+        self.value_offsets = np.ascontiguousarray(value_offsets, np.int32)
+        self.values = np.ascontiguousarray(values, np.float64)
+        self.valid = None if valid is None else np.ascontiguousarray(valid, np.uint8)
+
+    def __len__(self):
+        return len(self.type_id)
+
+    @classmethod
+    def from_rows(cls, rows):
+        """rows: (type_id, srid, boundaries, holes) tuples -- boundaries a list of coordinate lists,
+        a coordinate a list of 2 or 3 floats -- or None for a null row."""
+        tid, srid, bo, co, vo, vals, valid = [], [], [0], [0], [0], [], []
+        for r in rows:
+            valid.append(r is not None)
+            t, sr, bnds = (r[0], r[1], r[2]) if r is not None else (0, 0, [])
+            tid.append(t)
+            srid.append(sr)
+            for b in bnds:
+                for c in b:
+                    vals.extend(float(v) for v in c)
+                    vo.append(len(vals))
+                co.append(len(vo) - 1)
+            bo.append(len(co) - 1)
+        return cls(tid, srid, bo, co, vo, vals, np.array(valid, np.uint8))
+
+
+def st_point(x, y):
+    """ST_Point (expressions/constructors/ST_Point.scala:27-32): InternalGeometry(POINT, 0,
+    [[[x, y]]], [[]]) per row, as a CoordsColumn."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    n = len(x)
+    vals = np.empty(2 * n, np.float64)
+    vals[0::2] = x
+    vals[1::2] = y
+    ar = np.arange(n + 1, dtype=np.int32)
+    return CoordsColumn(np.ones(n, np.int32), np.zeros(n, np.int32), ar, ar, 2 * ar, vals)
+
+
 def _points_xy(points):
     """Accepts (x, y) arrays or an (n, 2) array (host or device)."""
     if isinstance(points, tuple) and len(points) == 2:
@@ -156,10 +208,16 @@ class ChipTable:
     def __init__(self, ctx, is_core, index_id, wkb_list, polygon_key, n_polygons=None):
         self.ctx = ctx
         is_core = np.ascontiguousarray(is_core, dtype=np.uint8)
+        if isinstance(index_id, tuple) or (len(index_id) and isinstance(index_id[0], str)):
+            # StringType ids (the BNG default, BNGIndexSystem.scala:28): parsed on the GPU
+            index_id = ctx.bng_parse_column(index_id)
         index_id = np.ascontiguousarray(index_id, dtype=np.int64)
         polygon_key = np.ascontiguousarray(polygon_key, dtype=np.int32)
         if isinstance(wkb_list, tuple) and len(wkb_list) == 2:
-            offsets = np.ascontiguousarray(wkb_list[0], dtype=np.int64)
+            # Arrow binary (int32 offsets) or large_binary (int64)
+            offsets = np.ascontiguousarray(wkb_list[0])
+            if offsets.dtype != np.int32:
+                offsets = offsets.astype(np.int64, copy=False)
             data = np.ascontiguousarray(wkb_list[1], dtype=np.uint8)
         else:
             lens = np.array([0 if w is None else len(w) for w in wkb_list], dtype=np.int64)
@@ -175,9 +233,10 @@ class ChipTable:
         self.n_polygons = int(n_polygons)
         self.n_chips = n
         h = ctypes.c_void_p()
-        N.check(N.lib().mosaic_chip_table_create(
+        N.check(N.lib().mosaic_chip_table_create_arrow(
             ctx.handle, ctx.index_system.grid, ctx.resolution_of_table, n, N.ptr(is_core), N.ptr(index_id),
-            N.ptr(offsets), N.ptr(data), N.ptr(polygon_key), self.n_polygons, ctypes.byref(h)))
+            N.ptr(offsets), 1 if offsets.dtype == np.int32 else 0, N.ptr(data), N.ptr(polygon_key), self.n_polygons,
+            ctypes.byref(h)))
         self.handle = h
 
     def info(self):
@@ -311,6 +370,30 @@ class MosaicContext:
                                                  N.ptr(offs), N.ptr(chars), cap, ctypes.byref(need)))
         return offs, chars[:need.value].tobytes()
 
+    def bng_parse_column(self, strings, valid=None):
+        """BNG string ids -> long ids, parsed on the GPU (BNGIndexSystem.parse,
+        BNGIndexSystem.scala:391-413).  ``strings``: a sequence of str (None = null) or an Arrow utf8
+        tuple (offsets int32 / int64, chars)."""
+        if isinstance(strings, tuple) and len(strings) == 2:
+            offs, chars = strings
+            offs = np.ascontiguousarray(offs)
+            chars = np.frombuffer(chars, np.uint8) if isinstance(chars, (bytes, bytearray)) else np.ascontiguousarray(chars, np.uint8)
+        else:
+            enc = [b"" if v is None else v.encode() for v in strings]
+            if valid is None and any(v is None for v in strings):
+                valid = np.array([v is not None for v in strings], np.uint8)
+            offs = np.zeros(len(enc) + 1, np.int32)
+            np.cumsum([len(e) for e in enc], out=offs[1:])
+            chars = np.frombuffer(b"".join(enc) or b"\0", np.uint8)
+        o32 = 1 if offs.dtype == np.int32 else 0
+        if not o32:
+            offs = offs.astype(np.int64, copy=False)
+        n = len(offs) - 1
+        out = np.zeros(max(n, 1), np.int64)
+        v = None if valid is None else np.ascontiguousarray(valid, np.uint8)
+        N.check(N.lib().mosaic_bng_parse_column(self.handle, o32, N.ptr(offs), N.ptr(chars), N.ptr(v), n, N.ptr(out)))
+        return out[:n]
+
     def grid_longlatascellid(self, lon, lat, resolution, raw=False):
         """PointIndexLonLat (expressions/index/PointIndexLonLat.scala:44-51)."""
         cells = self._cells(lon, lat, resolution)
@@ -328,6 +411,20 @@ class MosaicContext:
             cells = self._cells(xy[0], xy[1], resolution)
             return cells if raw else self._serialize(cells)
         res = self.index_system.get_resolution(resolution)
+        if isinstance(points, CoordsColumn):
+            n = len(points)
+            out = np.empty(n, np.int64)
+            status = np.empty(n, np.uint8)
+            n_rp = ctypes.c_int64(0)
+            N.check(N.lib().mosaic_point_coords_to_cell(
+                self.handle, self.index_system.grid, res, N.ptr(points.type_id), N.ptr(points.boundary_offsets),
+                N.ptr(points.coord_offsets), N.ptr(points.value_offsets),
+                N.ptr(points.values) if len(points.values) else None, N.ptr(points.valid), n, N.ptr(out),
+                N.ptr(status), ctypes.byref(n_rp)))
+            if n_rp.value and not return_status:
+                raise RowPathRequired(np.flatnonzero(status == N.ROW_PATH))
+            cells = out if raw else self._serialize(out)
+            return (cells, status) if return_status else cells
         if isinstance(points, tuple) and len(points) == 3:
             offsets, data, valid = points
             f = {"wkb": N.GEOM_WKB, "wkt": N.GEOM_WKT, "hex": N.GEOM_HEX}[fmt or "wkb"]

@@ -84,6 +84,79 @@ MOSAIC_HD bool point_to_index(double eastings, double northings, int res, int64_
 }
 
 
+// ---- BNGIndexSystem.parse (BNGIndexSystem.scala:391-413) + encode (:528-541): a string id (the
+// StringType cell ids BNG chips carry by default, BNGIndexSystem.scala:28) -> the long id.
+// letterMap (:84-99, row 10 repeats "SZ": find() takes the first row, row 0) and quadrants (:36).
+MOSAIC_HD int letter_code(char a, char b) {
+    // letterMap as a table of the two characters; returns row * 8 + column of the first match
+    const char* rows = "SVSWSXSYSZTVTW" "SQSRSSSTSUTQTR" "SLSMSNSOSPTLTM" "SFSGSHSJSKTFTG" "SASBSCSDSETATB"
+                       "NVNWNXNYNZOVOW" "NQNRNSNTNUOQOR" "NLNMNNNONPOLOM" "NFNGNHNJNKOFOG" "NANBNCNDNEOAOB"
+                       "HVHWHXHYSZJVJW" "HQHRHSHTHUJQJR" "HLHMHNHOHPJLJM";
+    for (int r = 0; r < 13; r++)
+        for (int c = 0; c < 7; c++)
+            if (rows[r * 14 + 2 * c] == a && rows[r * 14 + 2 * c + 1] == b) return r * 8 + c;
+    return -1;
+}
+// Integer.parseInt over s[0 .. n): optional sign, then at least one ASCII digit, within Int range
+// (Java also accepts non-ASCII Unicode digits, which this does not: such ids are rejected)
+MOSAIC_HD bool java_parse_int(const char* s, int n, int32_t* out) {
+    if (n <= 0) return false;
+    int i = 0;
+    bool neg = false;
+    if (s[0] == '-' || s[0] == '+') {
+        neg = s[0] == '-';
+        i = 1;
+        if (n == 1) return false;
+    }
+    int64_t v = 0;
+    for (; i < n; i++) {
+        if (s[i] < '0' || s[i] > '9') return false;
+        v = v * 10 + (s[i] - '0');
+        if (v > 2147483648LL) return false;
+    }
+    if (!neg && v > 2147483647LL) return false;
+    *out = (int32_t)(neg ? -v : v);
+    return true;
+}
+MOSAIC_HD int64_t encode(int eLetter, int nLetter, int32_t eBin, int32_t nBin, int quadrant, int nPositions, int res) {
+    const double idP = pow10i(5 + 2 * nPositions - 2), eLS = pow10i(3 + 2 * nPositions - 2),
+                 nLS = pow10i(1 + 2 * nPositions - 2), eS = pow10i(nPositions);
+    const int32_t nb10 = (int32_t)((uint32_t)nBin * 10u);  // Int * Int wraps
+    const double id = res == -1 ? (idP + (double)eLetter * eLS) / 100 + (double)quadrant
+                                : idP + (double)eLetter * eLS + (double)nLetter * nLS + (double)eBin * eS + (double)nb10 +
+                                      (double)quadrant;
+    return jvm_d2l(id);
+}
+// Returns false where the reference throws (no letter pair, non-numeric bins, Int overflow).
+MOSAIC_HD bool parse(const char* s, int n, int64_t* out) {
+    const int lc = n >= 2 ? letter_code(s[0], s[1]) : (n == 1 ? letter_code(s[0], 'V') : -1);
+    if (lc < 0) return false;
+    const int eLetter = lc & 7, nLetter = lc >> 3;
+    if (n == 1) {
+        *out = encode(eLetter, 0, 0, 0, 0, 1, -1);
+        return true;
+    }
+    // suffix = the last two characters; quadrants = ("", "SW", "NW", "NE", "SE")
+    const char a = s[n - 2], b = s[n - 1];
+    int quadrant = 0;
+    if (b == 'W' && (a == 'S' || a == 'N')) quadrant = a == 'S' ? 1 : 2;
+    else if (b == 'E' && (a == 'N' || a == 'S')) quadrant = a == 'N' ? 3 : 4;
+    // binDigits = drop(2) (then dropRight(2) with a quadrant); may be empty or, for "SW"-like ids of
+    // length 2 or 3, start past its end
+    const int d0 = 2, d1 = quadrant > 0 ? n - 2 : n;
+    const int L = d1 > d0 ? d1 - d0 : 0;
+    if (L == 0) {
+        *out = encode(eLetter, nLetter, 0, 0, quadrant, 1, -2);
+        return true;
+    }
+    int32_t eBin, nBin;
+    if (!java_parse_int(s + d0, L - L / 2, &eBin) || !java_parse_int(s + d0 + L / 2, L - L / 2, &nBin)) return false;
+    const int nPositions = L / 2 + 1;
+    const int res = quadrant == 0 ? nPositions + 1 : -nPositions;
+    *out = encode(eLetter, nLetter, eBin, nBin, quadrant, nPositions, res);
+    return true;
+}
+
 // ---- k-loops / k-rings: BNGIndexSystem.kLoop / kRing (BNGIndexSystem.scala:216-246) with the
 // cell decoding they use: indexDigits (index.toString digits), getResolution(digits), getEdgeSize
 // (sizeMap), getX / getY, isValid (BNGIndexSystem.scala:248-263).  Int arithmetic as in Scala.

@@ -889,6 +889,96 @@ __global__ void __launch_bounds__(256) k_bng_format_write(FormatArgs a) {
 }
 __global__ void k_add_prev(int64_t* first, const int64_t* prev_total) { *first += *prev_total; }
 
+// BNGIndexSystem.parse over a string column (Arrow utf8 / large_utf8): one lane per row, the row's
+// characters read from global memory (ids are <= 16 characters).  Rows the reference cannot parse
+// get id 0 and set flags bit 0; null rows (valid[i] == 0) get 0.
+struct ParseArgs {
+    const void* offsets;
+    int off64;
+    const uint8_t* chars;
+    const uint8_t* valid;
+    int64_t n;
+    int64_t* ids;
+    unsigned long long* first_bad;  // smallest unparseable row (atomicMin), ~0 if none
+};
+__global__ void __launch_bounds__(256) k_bng_parse(ParseArgs a) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+        int64_t id = 0;
+        if (!a.valid || a.valid[i]) {
+            const int64_t o0 = a.off64 ? ((const int64_t*)a.offsets)[i] : ((const int32_t*)a.offsets)[i];
+            const int64_t o1 = a.off64 ? ((const int64_t*)a.offsets)[i + 1] : ((const int32_t*)a.offsets)[i + 1];
+            char buf[24];
+            const int len = (int)(o1 - o0);
+            bool ok = len >= 0 && len <= 24;
+            if (ok) {
+                for (int j = 0; j < len; j++) buf[j] = (char)a.chars[o0 + j];
+                ok = bng::parse(buf, len, &id);
+            }
+            if (!ok) {
+                id = 0;
+                atomicMin(a.first_bad, (unsigned long long)i);
+            }
+        }
+        a.ids[i] = id;
+    }
+}
+
+// The COORDS form of a point (InternalGeometryType, core/types/model/InternalGeometry.scala,
+// the output of st_point: expressions/constructors/ST_Point.scala:27-32) as Arrow columns:
+// type_id[n] (int32), boundaries list offsets bnd[n + 1] (rows -> boundaries), ring offsets
+// ring[] (boundaries -> coordinates), coordinate offsets crd[] (coordinates -> values), values
+// (float64).  MosaicPointJTS.fromInternal (core/geometry/point/MosaicPointJTS.scala:82-89) reads
+// boundaries.head.head: x = values[0], y = values[1] of the first coordinate of the first
+// boundary; InternalCoord(ArrayData) (InternalCoord.scala) needs 2 values, or >= 3 (z ignored).
+// Rows of other types (their centroid) and rows the reference would throw on (no boundary, no
+// coordinate, a 1-value coordinate) go to the row path.
+struct CoordsArgs {
+    const int32_t* type_id;
+    const int32_t* bnd;
+    const int32_t* ring;
+    const int32_t* crd;
+    const double* values;
+    const uint8_t* valid;
+    int64_t n, n_bnd, n_ring, n_values;  // lengths of ring[] and crd[] offset arrays (+1), values
+    double* x;
+    double* y;
+    uint8_t* status;
+    unsigned long long* n_rowpath;
+};
+__global__ void __launch_bounds__(256) k_decode_coords(CoordsArgs a) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    unsigned int rowpath = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+        uint8_t st = MOSAIC_ROW_NULL;
+        double x = 0.0, y = 0.0;
+        if (!a.valid || a.valid[i]) {
+            st = MOSAIC_ROW_PATH;
+            if (a.type_id[i] == 1) {  // GeometryTypeEnum.POINT
+                const int64_t b0 = a.bnd[i], b1 = a.bnd[i + 1];
+                if (b1 > b0 && b0 >= 0 && b0 + 1 < a.n_bnd) {
+                    const int64_t r0 = a.ring[b0], r1 = a.ring[b0 + 1];
+                    if (r1 > r0 && r0 >= 0 && r0 + 1 < a.n_ring) {
+                        const int64_t c0 = a.crd[r0], c1 = a.crd[r0 + 1];
+                        const int64_t len = c1 - c0;
+                        if ((len == 2 || len >= 3) && c0 >= 0 && c0 + 1 < a.n_values) {
+                            x = a.values[c0];
+                            y = a.values[c0 + 1];
+                            st = MOSAIC_ROW_OK;
+                        }
+                    }
+                }
+            }
+        }
+        rowpath += st == MOSAIC_ROW_PATH;
+        a.x[i] = x;
+        a.y[i] = y;
+        a.status[i] = st;
+    }
+    for (int off = 32; off > 0; off >>= 1) rowpath += __shfl_down(rowpath, off, 64);
+    if ((threadIdx.x & 63) == 0 && rowpath) atomicAdd(a.n_rowpath, (unsigned long long)rowpath);
+}
+
 
 // ---- grid_boundaryaswkb over a BNG cell column (IndexGeometry -> BNGIndexSystem.indexToGeometry,
 // toWKB): 93 bytes per row at out + 93 i; null rows are left untouched (the caller's validity).
@@ -1962,6 +2052,153 @@ int mosaic_point_geom_to_cell(mosaic_ctx* ctx, int grid, int res, int format, co
     return copy_out(c, row_status, c->dec_status.p, n);
 }
 
+// element idx of an int32 array in host or device memory
+static int read_i32(ThreadCtx* c, const int32_t* p, int64_t idx, int32_t* out) {
+    if (is_device_ptr(p)) {
+        HIP_TRY(hipMemcpy(out, p + idx, 4, hipMemcpyDeviceToHost));
+    } else {
+        *out = p[idx];
+    }
+    (void)c;
+    return MOSAIC_OK;
+}
+
+// Decode a COORDS point column into c->dec_x / dec_y / dec_status (device).  Synchronous.
+static int decode_coords(ThreadCtx* c, const int32_t* type_id, const int32_t* bnd, const int32_t* ring,
+                         const int32_t* crd, const double* values, const uint8_t* valid, int64_t n, int64_t* n_rowpath) {
+    if (!type_id || !bnd || !ring || !crd) return fail(MOSAIC_E_ARG, "null argument");
+    int rc;
+    int32_t nb = 0, nr = 0, nv = 0;
+    if ((rc = read_i32(c, bnd, n, &nb))) return rc;
+    if (nb < 0) return fail(MOSAIC_E_ARG, "negative offsets");
+    if ((rc = read_i32(c, ring, nb, &nr))) return rc;
+    if (nr < 0) return fail(MOSAIC_E_ARG, "negative offsets");
+    if ((rc = read_i32(c, crd, nr, &nv))) return rc;
+    if (nv < 0 || (nv > 0 && !values)) return fail(MOSAIC_E_ARG, "bad coordinate values");
+    const void *dt, *db, *dr, *dc, *dvals = nullptr, *dv;
+    if ((rc = to_device(c, c->stage_idx, type_id, (size_t)n * 4, &dt)) ||
+        (rc = to_device(c, c->geo_off, bnd, (size_t)(n + 1) * 4, &db)) ||
+        (rc = to_device(c, c->stage_out, ring, (size_t)(nb + 1) * 4, &dr)) ||
+        (rc = to_device(c, c->stage_out2, crd, (size_t)(nr + 1) * 4, &dc)) ||
+        (nv > 0 && (rc = to_device(c, c->geo_data, values, (size_t)nv * 8, &dvals))) ||
+        (rc = to_device(c, c->stage_v, valid, (size_t)n, &dv)))
+        return rc;
+    if ((rc = c->dec_x.reserve(n * 8)) || (rc = c->dec_y.reserve(n * 8)) || (rc = c->dec_status.reserve(n))) return rc;
+    HIP_TRY(hipMemsetAsync(c->scalars.p, 0, kScalars * 8, c->stream));
+    CoordsArgs a;
+    a.type_id = (const int32_t*)dt;
+    a.bnd = (const int32_t*)db;
+    a.ring = (const int32_t*)dr;
+    a.crd = (const int32_t*)dc;
+    a.values = (const double*)dvals;
+    a.valid = (const uint8_t*)dv;
+    a.n = n;
+    a.n_bnd = (int64_t)nb + 1;
+    a.n_ring = (int64_t)nr + 1;
+    a.n_values = nv;
+    a.x = (double*)c->dec_x.p;
+    a.y = (double*)c->dec_y.p;
+    a.status = (uint8_t*)c->dec_status.p;
+    a.n_rowpath = (unsigned long long*)c->scalars.p + 4;
+    hipLaunchKernelGGL(k_decode_coords, dim3(grid_size(c, n)), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    unsigned long long r = 0;
+    HIP_TRY(hipMemcpyAsync(&r, a.n_rowpath, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n_rowpath) *n_rowpath = (int64_t)r;
+    return MOSAIC_OK;
+}
+
+int mosaic_point_coords_decode(mosaic_ctx* ctx, const int32_t* type_id, const int32_t* boundary_offsets,
+                               const int32_t* coord_offsets, const int32_t* value_offsets, const double* values,
+                               const uint8_t* valid, int64_t n, double* x, double* y, uint8_t* row_status,
+                               int64_t* n_rowpath) {
+    ENTER(ctx);
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (n > 0 && (!x || !y || !row_status)) return fail(MOSAIC_E_ARG, "null argument");
+    if (n_rowpath) *n_rowpath = 0;
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = decode_coords(c, type_id, boundary_offsets, coord_offsets, value_offsets, values, valid, n, n_rowpath)))
+        return rc;
+    if ((rc = copy_out(c, x, c->dec_x.p, n * 8)) || (rc = copy_out(c, y, c->dec_y.p, n * 8)) ||
+        (rc = copy_out(c, row_status, c->dec_status.p, n)))
+        return rc;
+    return MOSAIC_OK;
+}
+
+int mosaic_point_coords_to_cell(mosaic_ctx* ctx, int grid, int res, const int32_t* type_id,
+                                const int32_t* boundary_offsets, const int32_t* coord_offsets,
+                                const int32_t* value_offsets, const double* values, const uint8_t* valid, int64_t n,
+                                int64_t* out_cell, uint8_t* row_status, int64_t* n_rowpath) {
+    ENTER(ctx);
+    if (n < 0) return fail(MOSAIC_E_ARG, "negative n");
+    if (n > 0 && (!out_cell || !row_status)) return fail(MOSAIC_E_ARG, "null argument");
+    if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
+    if (!valid_res(grid, res)) return res_error(grid, res);
+    if (n_rowpath) *n_rowpath = 0;
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    if ((rc = decode_coords(c, type_id, boundary_offsets, coord_offsets, value_offsets, values, valid, n, n_rowpath)))
+        return rc;
+    c->async = 0;
+    rc = point_to_cell_impl(c, grid, res, (const double*)c->dec_x.p, (const double*)c->dec_y.p, nullptr,
+                            (const uint8_t*)c->dec_status.p, n, out_cell, nullptr);
+    if (rc) return rc;
+    return copy_out(c, row_status, c->dec_status.p, n);
+}
+
+int mosaic_bng_parse_column(mosaic_ctx* ctx, int offsets32, const void* offsets, const uint8_t* chars,
+                            const uint8_t* valid, int64_t n, int64_t* out_ids) {
+    ENTER(ctx);
+    if (n < 0 || (n > 0 && (!offsets || !out_ids))) return fail(MOSAIC_E_ARG, "invalid argument");
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t ob = offsets32 ? 4 : 8;
+    int64_t end = 0;
+    if (is_device_ptr(offsets)) {
+        int64_t e64 = 0;
+        int32_t e32 = 0;
+        HIP_TRY(hipMemcpy(offsets32 ? (void*)&e32 : (void*)&e64, (const char*)offsets + n * ob, ob, hipMemcpyDeviceToHost));
+        end = offsets32 ? e32 : e64;
+    } else {
+        end = offsets32 ? ((const int32_t*)offsets)[n] : ((const int64_t*)offsets)[n];
+    }
+    if (end < 0 || (end > 0 && !chars)) return fail(MOSAIC_E_ARG, "bad string column");
+    DevBuf s_off, s_chars, s_valid, s_ids, s_bad;
+    auto done = [&](int rc) {
+        for (DevBuf* b : {&s_off, &s_chars, &s_valid, &s_ids, &s_bad}) b->release();
+        return rc;
+    };
+    int rc;
+    const void *doff, *dchars = nullptr, *dv;
+    if ((rc = to_device(c, s_off, offsets, (size_t)(n + 1) * ob, &doff)) ||
+        (end > 0 && (rc = to_device(c, s_chars, chars, (size_t)end, &dchars))) ||
+        (rc = to_device(c, s_valid, valid, (size_t)n, &dv)) || (rc = s_bad.reserve(8)))
+        return done(rc);
+    const bool dev_out = is_device_ptr(out_ids);
+    if (!dev_out && (rc = s_ids.reserve((size_t)n * 8))) return done(rc);
+    HIP_TRY(hipMemsetAsync(s_bad.p, 0xff, 8, c->stream));
+    ParseArgs a;
+    a.offsets = doff;
+    a.off64 = offsets32 ? 0 : 1;
+    a.chars = (const uint8_t*)dchars;
+    a.valid = (const uint8_t*)dv;
+    a.n = n;
+    a.ids = dev_out ? out_ids : (int64_t*)s_ids.p;
+    a.first_bad = (unsigned long long*)s_bad.p;
+    hipLaunchKernelGGL(k_bng_parse, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    unsigned long long bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, s_bad.p, 8, hipMemcpyDeviceToHost, c->stream));
+    if (!dev_out) HIP_TRY(hipMemcpyAsync(out_ids, s_ids.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (bad != ~0ULL) return done(fail(MOSAIC_E_ARG, "invalid BNG id at row " + std::to_string(bad)));
+    return done(MOSAIC_OK);
+}
+
 // BNGIndexSystem.letterMap (BNGIndexSystem.scala:84-99) and quadrants (:36)
 static const char* kLetterMap[13][7] = {
     {"SV", "SW", "SX", "SY", "SZ", "TV", "TW"}, {"SQ", "SR", "SS", "ST", "SU", "TQ", "TR"},
@@ -1997,60 +2234,44 @@ int mosaic_bng_format(int64_t id, char* buf, size_t cap) {
     return (int)s.size();
 }
 
-// BNGIndexSystem.parse (BNGIndexSystem.scala:391-413) + encode (:528-541)
-static int64_t bng_encode(int eL, int nL, int eBin, int nBin, int q, int nPos, int res) {
-    double idP = bng::pow10i(5 + 2 * nPos - 2), eLS = bng::pow10i(3 + 2 * nPos - 2), nLS = bng::pow10i(1 + 2 * nPos - 2);
-    double eS = bng::pow10i(nPos);
-    int32_t nb10 = (int32_t)((uint32_t)nBin * 10u);  // JVM Int multiplication wraps
-    double id = res == -1 ? (idP + (double)eL * eLS) / 100 + q
-                          : idP + (double)eL * eLS + (double)nL * nLS + (double)eBin * eS + (double)nb10 + q;
-    return bng::jvm_d2l(id);
-}
 
 int mosaic_bng_parse(const char* cs, int64_t* out) {
     if (!cs || !out) return fail(MOSAIC_E_ARG, "null argument");
-    std::string s(cs);
-    if (s.empty()) return fail(MOSAIC_E_ARG, "empty BNG id");
-    std::string prefix = s.size() >= 2 ? s.substr(0, 2) : s + "V";
-    int eL = -1, nL = -1;
-    for (int r = 0; r < 13 && eL < 0; r++)
-        for (int col = 0; col < 7; col++)
-            if (prefix == kLetterMap[r][col]) {
-                eL = col;
-                nL = r;
-                break;
-            }
-    if (eL < 0) return fail(MOSAIC_E_ARG, "invalid BNG prefix in " + s);
-    if (s.size() == 1) {
-        *out = bng_encode(eL, 0, 0, 0, 0, 1, -1);
-        return MOSAIC_OK;
-    }
-    std::string suffix = s.substr(s.size() - 2);
-    int q = 0;
-    for (int i = 1; i < 5; i++)
-        if (suffix == kQuadrants[i]) q = i;
-    std::string bins = q > 0 ? s.substr(2, s.size() - 4) : s.substr(2);
-    if (bins.empty()) {
-        *out = bng_encode(eL, nL, 0, 0, q, 1, -2);
-        return MOSAIC_OK;
-    }
-    for (char ch : bins)
-        if (ch < '0' || ch > '9') return fail(MOSAIC_E_ARG, "invalid BNG digits in " + s);
-    size_t half = bins.size() / 2;
-    int eBin = std::stoi(bins.substr(0, bins.size() - half));
-    int nBin = std::stoi(bins.substr(bins.size() - half));
-    int nPos = (int)half + 1;
-    int res = q == 0 ? nPos + 1 : -nPos;
-    *out = bng_encode(eL, nL, eBin, nBin, q, nPos, res);
+    const size_t len = strlen(cs);
+    if (len > 64 || !bng::parse(cs, (int)len, out)) return fail(MOSAIC_E_ARG, std::string("invalid BNG id ") + cs);
     return MOSAIC_OK;
 }
+
+static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, const uint8_t* is_core,
+                             const int64_t* index_id, const void* wkb_off, bool off32, const uint8_t* wkb,
+                             const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out);
 
 int mosaic_chip_table_create(mosaic_ctx* ctx, int grid, int res, int64_t n_chips, const uint8_t* is_core,
                              const int64_t* index_id, const int64_t* wkb_offsets, const uint8_t* wkb,
                              const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out) {
     ENTER(ctx);
+    return chip_table_create(c, grid, res, n_chips, is_core, index_id, wkb_offsets, false, wkb, polygon_key, n_polygons,
+                             out);
+}
+
+int mosaic_chip_table_create_arrow(mosaic_ctx* ctx, int grid, int res, int64_t n_chips, const uint8_t* is_core,
+                                   const int64_t* index_id, const void* wkb_offsets, int wkb_offsets32,
+                                   const uint8_t* wkb, const int32_t* polygon_key, int32_t n_polygons,
+                                   mosaic_chips** out) {
+    ENTER(ctx);
+    return chip_table_create(c, grid, res, n_chips, is_core, index_id, wkb_offsets, wkb_offsets32 != 0, wkb,
+                             polygon_key, n_polygons, out);
+}
+
+static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, const uint8_t* is_core,
+                             const int64_t* index_id, const void* wkb_off, bool off32, const uint8_t* wkb,
+                             const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out) {
+    // Arrow binary (int32 offsets) or large_binary (int64)
+    auto wkb_offsets = [&](int64_t i) -> int64_t {
+        return off32 ? (int64_t)((const int32_t*)wkb_off)[i] : ((const int64_t*)wkb_off)[i];
+    };
     if (!c || !out || n_chips < 0 || n_polygons < 0) return fail(MOSAIC_E_ARG, "invalid argument");
-    if (n_chips > 0 && (!is_core || !index_id || !wkb_offsets || !polygon_key))
+    if (n_chips > 0 && (!is_core || !index_id || !wkb_off || !polygon_key))
         return fail(MOSAIC_E_ARG, "null chip column");
     if (grid != MOSAIC_GRID_H3 && grid != MOSAIC_GRID_BNG) return fail(MOSAIC_E_ARG, "unknown grid");
     if (!valid_res(grid, res)) return res_error(grid, res);
@@ -2071,7 +2292,7 @@ int mosaic_chip_table_create(mosaic_ctx* ctx, int grid, int res, int64_t n_chips
         if (index_id[i] == kEmptyKey) return fail(MOSAIC_E_ARG, "reserved index_id at chip " + std::to_string(i));
         bool core = is_core[i] != 0;
         meta[t] = ((uint32_t)polygon_key[i] << 1) | (core ? 1u : 0u);
-        int64_t a = wkb_offsets[i], b = wkb_offsets[i + 1];
+        int64_t a = wkb_offsets(i), b = wkb_offsets(i + 1);
         if (b < a || (b > a && !wkb)) return fail(MOSAIC_E_ARG, "bad wkb offsets at chip " + std::to_string(i));
         // core chips are accepted without a test: their geometry is never read
         if (!gb.add(core ? nullptr : wkb + a, core ? 0 : (size_t)(b - a)))

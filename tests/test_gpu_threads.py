@@ -11,7 +11,6 @@ import pytest
 import oracle
 from mosaic_amd.context import tessellate
 from mosaic_amd.data import PolygonSet, quickstart_points
-from tests.helpers import chips_to_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +32,9 @@ def test_concurrent_joins_on_one_context(h3ctx):
     table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
                              n_polygons=len(zones))
     assert table.tiles()["stream"] == 1
-    oc = chips_to_oracle(chips)
+    offs, data = chips["wkb"]
+    oc = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+              wkb_offsets=offs, wkb=data)
     cases = []
     for t in range(4):
         x, y = quickstart_points(zones, 150_000 + 7919 * t, seed=100 + t)
