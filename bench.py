@@ -89,17 +89,16 @@ def host_info():
     return {"cpu_model": cpu, "nproc": os.cpu_count(), "rocm": rocm}
 
 
-def build_chips(res, rank, world):
-    """Rank 0 tessellates; the chip rows go to the other ranks over the process group (one build
-    per node instead of one per rank)."""
-    from mosaic_amd.context import tessellate
+def build_chips(ctx, res, rank, world):
+    """Rank 0 tessellates (grid_tessellateexplode, cell classification on its GPU); the chip rows go
+    to the other ranks over the process group (one build per node instead of one per rank)."""
     from mosaic_amd.data import PolygonSet
 
     zones = PolygonSet.load("nyc_taxi_zones")
     t0 = time.perf_counter()
     chips = None
     if rank == 0:
-        chips = tessellate("H3", zones, res)
+        chips = ctx.grid_tessellateexplode(zones, res)
     if world > 1:
         import torch.distributed as dist
 
@@ -181,8 +180,8 @@ def main():
     from mosaic_amd import MosaicContext
     from mosaic_amd.data import SEED_BASE, uniform_points_device
 
-    zones, chips, tess_s = build_chips(args.res, rank, world)
     ctx = MosaicContext.build("H3", "JTS", device=local)
+    zones, chips, tess_s = build_chips(ctx, args.res, rank, world)
     t0 = time.perf_counter()
     table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
                            n_polygons=len(zones))

@@ -537,8 +537,6 @@ class MosaicContext:
     def chip_table(self, is_core, index_id, wkb_list, polygon_key, resolution, n_polygons=None):
         """Build side: rows of grid_tessellateexplode output (MosaicExplode.scala:70-79)."""
         self.resolution_of_table = self.index_system.get_resolution(resolution)
-        if self.index_system.cell_id_type == "string" and len(index_id) and isinstance(index_id[0], str):
-            index_id = np.array([self.index_system.parse(s) for s in index_id], np.int64)
         return ChipTable(self, is_core, index_id, wkb_list, polygon_key, n_polygons)
 
     def pip_join_count(self, chips, x, y, out=None):

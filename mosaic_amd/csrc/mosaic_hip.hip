@@ -2242,6 +2242,9 @@ int mosaic_bng_parse(const char* cs, int64_t* out) {
     return MOSAIC_OK;
 }
 
+static const int kLdsCountsMax = 8192;
+static const size_t kStreamLdsMax = 160 * 1024;  // LDS per CU (MI355X): one k_join_stream workgroup's budget
+
 static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, const uint8_t* is_core,
                              const int64_t* index_id, const void* wkb_off, bool off32, const uint8_t* wkb,
                              const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out);
@@ -2532,7 +2535,13 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                                            gb.part_ring.data(), gb.geom_part.data(), gb.geom_bbox.data()};
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-                tb.quad_max = c->raster_quad > 1 ? c->raster_quad : tiles::kQuadMax;
+                // LDS quad level: by default as many entries as one k_join_stream workgroup's LDS holds
+                // beside its counts, its per-wave stages (1024 threads) and, when small, tile_base
+                size_t avail = kStreamLdsMax - 16 * 320 * 4 - 1024 -
+                               (n_polygons <= kLdsCountsMax ? ((size_t)n_polygons + 64) * 4 : 0);
+                const size_t tbytes = tb.tile_idx.size() * 4;
+                if (tbytes <= avail / 3) avail -= tbytes;
+                tb.quad_max = c->raster_quad > 1 ? c->raster_quad : (int)std::min<size_t>(tiles::kQuadLimit, avail / 2);
                 tb.lines = c->raster_lines != 0;
                 if (tb.build_raster(src, c->raster_sub, c->raster_cell, threads)) {
                     size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
@@ -2674,8 +2683,6 @@ int mosaic_chip_table_tile_grid(const mosaic_chips* ch, double* o) {
     return MOSAIC_OK;
 }
 
-static const int kLdsCountsMax = 8192;
-static const size_t kStreamLdsMax = 160 * 1024;  // LDS per CU (MI355X): one k_join_stream workgroup's budget
 
 static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const double* y, int64_t n,
                     int64_t* counts, int64_t* out_row, int32_t* out_key, int64_t cap, int64_t* n_out) {

@@ -47,6 +47,8 @@ def lib():
         L.oracle_bng_point_to_index_batch.argtypes = [vp, vp, i64, i32, vp, vp]
         L.oracle_bng_format.restype = i32
         L.oracle_bng_format.argtypes = [i64, ctypes.c_char_p, i32]
+        L.oracle_bng_parse.restype = i32
+        L.oracle_bng_parse.argtypes = [ctypes.c_char_p, i32, ctypes.POINTER(i64)]
         L.oracle_orientation_index.restype = i32
         L.oracle_orientation_index.argtypes = [f64] * 6
         L.oracle_wkb_contains.restype = i32
@@ -127,6 +129,13 @@ def bng_point_to_index_batch(e, n, res):
     err = np.empty(e.shape[0], dtype=np.uint8)
     lib().oracle_bng_point_to_index_batch(_ptr(e), _ptr(n), e.shape[0], res, _ptr(out), _ptr(err))
     return out, err
+
+
+def bng_parse(text):
+    """BNGIndexSystem.parse; None where the reference throws."""
+    b = text.encode()
+    out = ctypes.c_int64(0)
+    return out.value if lib().oracle_bng_parse(b, len(b), ctypes.byref(out)) else None
 
 
 def bng_format(cell_id):

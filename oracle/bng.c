@@ -162,6 +162,82 @@ int oracle_bng_format(int64_t id, char* buf, int cap) {
     return o;
 }
 
+/* ---- BNGIndexSystem.parse (BNGIndexSystem.scala:391-413) + encode (:528-541) ----
+ * letterMap.find(_.contains(prefix)).get: the first row holding the pair (row 0 for "SZ"), its
+ * first column; Integer.parseInt for the bins (sign, ASCII digits, Int range; Java's non-ASCII
+ * Unicode digits are not restated).  Returns 1 and the id, or 0 where the reference throws. */
+static int java_parse_int(const char* s, int n, int32_t* out) {
+    if (n <= 0) return 0;
+    int i = 0, neg = 0;
+    if (s[0] == '-' || s[0] == '+') {
+        neg = s[0] == '-';
+        i = 1;
+        if (n == 1) return 0;
+    }
+    long long v = 0;
+    for (; i < n; i++) {
+        if (s[i] < '0' || s[i] > '9') return 0;
+        v = v * 10 + (s[i] - '0');
+        if (v > 2147483648LL) return 0;
+    }
+    if (!neg && v > 2147483647LL) return 0;
+    *out = (int32_t)(neg ? -v : v);
+    return 1;
+}
+
+static int64_t bng_encode(int eL, int nL, int32_t eBin, int32_t nBin, int q, int nPos, int res) {
+    double idP = pow(10.0, 5 + 2 * nPos - 2), eLS = pow(10.0, 3 + 2 * nPos - 2), nLS = pow(10.0, 1 + 2 * nPos - 2);
+    double eS = pow(10.0, nPos);
+    int32_t nb10 = (int32_t)((uint32_t)nBin * 10u);
+    double id = res == -1 ? (idP + eL * eLS) / 100 + q : idP + eL * eLS + nL * nLS + eBin * eS + nb10 + q;
+    return jvm_d2l(id);
+}
+
+int oracle_bng_parse(const char* s, int n, int64_t* out) {
+    char prefix[3] = {0, 0, 0};
+    if (n >= 2) {
+        prefix[0] = s[0];
+        prefix[1] = s[1];
+    } else if (n == 1) {
+        prefix[0] = s[0];
+        prefix[1] = 'V';
+    } else {
+        return 0;
+    }
+    int eL = -1, nL = -1;
+    for (int r = 0; r < 13 && eL < 0; r++)
+        for (int c = 0; c < 7; c++)
+            if (strcmp(kLetterMap[r][c], prefix) == 0) {
+                eL = c;
+                nL = r;
+                break;
+            }
+    if (eL < 0) return 0;
+    if (n == 1) {
+        *out = bng_encode(eL, 0, 0, 0, 0, 1, -1);
+        return 1;
+    }
+    char suffix[3] = {s[n - 2], s[n - 1], 0};
+    int q = 0;
+    for (int i = 1; i < 5; i++)
+        if (strcmp(kQuadrants[i], suffix) == 0) q = i;
+    /* drop(2), then dropRight(2) with a quadrant */
+    int from = 2, to = q > 0 ? n - 2 : n;
+    int L = to > from ? to - from : 0;
+    if (L == 0) {
+        *out = bng_encode(eL, nL, 0, 0, q, 1, -2);
+        return 1;
+    }
+    int32_t eBin, nBin;
+    int half = L / 2;
+    if (!java_parse_int(s + from, L - half, &eBin)) return 0;  /* dropRight(half) */
+    if (!java_parse_int(s + from + half, L - half, &nBin)) return 0;  /* drop(half) */
+    int nPos = half + 1;
+    int res = q == 0 ? nPos + 1 : -nPos;
+    *out = bng_encode(eL, nL, eBin, nBin, q, nPos, res);
+    return 1;
+}
+
 /* ---- BNGIndexSystem.kLoop / kRing / isValid (BNGIndexSystem.scala:216-263) ----
  * The id's decimal string (indexDigits), getResolution(digits), sizeMap, getX / getY (Int
  * arithmetic, wrapping), then pointToIndex of the loop's cell origins filtered by isValid. */

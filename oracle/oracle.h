@@ -52,6 +52,8 @@ void oracle_bng_point_to_index_batch(const double* e, const double* n, int64_t c
                                      int64_t* out, uint8_t* err);
 /* BNGIndexSystem.format: writes a NUL-terminated string; returns its length or -1. */
 int oracle_bng_format(int64_t id, char* buf, int cap);
+/* BNGIndexSystem.parse: 1 and *out, or 0 where the reference throws. */
+int oracle_bng_parse(const char* s, int n, int64_t* out);
 /* BNGIndexSystem.isValid / kLoop / kRing: cell count written to out (<= 8k / 1 + 4k(k+1)), -1 if
  * the id cannot be decoded. */
 int oracle_bng_is_valid(int64_t id);

@@ -142,3 +142,19 @@ def hex_point(text):
 
 def decode(fmt, row):
     return (wkb_point, wkt_point, hex_point)[fmt](row)
+
+
+def coords_point(row):
+    """The COORDS form (core/types/model/InternalGeometry.scala): row = (type_id, srid, boundaries,
+    holes) or None.  MosaicPointJTS.fromInternal (core/geometry/point/MosaicPointJTS.scala:82-89)
+    reads boundaries.head.head; InternalCoord(ArrayData) takes 2 values or the first 3.  Returns
+    ("null",), ("ok", x, y) or ("path",) (other types: the centroid; rows the reference throws on)."""
+    if row is None:
+        return ("null",)
+    type_id, _srid, boundaries = row[0], row[1], row[2]
+    if type_id != 1 or not boundaries or not boundaries[0]:
+        return ("path",)
+    c = boundaries[0][0]
+    if len(c) == 2 or len(c) >= 3:
+        return ("ok", float(c[0]), float(c[1]))
+    return ("path",)

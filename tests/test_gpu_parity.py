@@ -443,16 +443,14 @@ def test_join_device_tensors(h3ctx, zones):
 
 @pytest.mark.parametrize("res", [3, 4])
 def test_join_bng_dense_table(bngctx, res):
-    """BNG dense cell table (k_join_stream_bng): tessellated chips (planar stand-in coordinates in
-    metres), uniform points, points on and 1 ulp around cell lines, negative and >= 1e7 coordinates
-    (outside the one-to-one range: generic path) -- counts equal the oracle's and the generic
-    kernel's."""
+    """BNG dense cell table (k_join_stream_bng): tessellated chips of the London postcode zones in
+    EPSG:27700 metres (tests/golden/make_bng_fixture.py), uniform points, points on and 1 ulp around
+    cell lines, negative and >= 1e7 coordinates (outside the one-to-one range: generic path) --
+    counts equal the oracle's and the generic kernel's."""
     from mosaic_amd.context import tessellate
 
-    london = PolygonSet.load("london_postcode_zones")
     ids = list(range(0, 177, 3))
-    xy = (london.xy - london.xy.min(0)) * 1e5 + np.array([500000.0, 150000.0])
-    proj = PolygonSet(xy, london.ring_offsets, london.part_rings, london.geom_parts).subset(ids)
+    proj = PolygonSet.load("london_postcodes_bng").subset(ids)
     chips = tessellate("BNG", proj, res)
     table = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
                               n_polygons=len(ids))
@@ -498,14 +496,10 @@ def test_join_bng_dense_table(bngctx, res):
 
 
 def test_join_bng(bngctx):
-    london = PolygonSet.load("london_postcode_zones")
-    # project-free check: use the London polygons' lon/lat as planar coordinates scaled into BNG
-    # metres (the join semantics do not depend on the CRS); chips from BNG cells of random points
+    # the London postcode zones in EPSG:27700 metres; chips from BNG cells of random points
+    proj = PolygonSet.load("london_postcodes_bng")
     rng = np.random.default_rng(6)
     ids = list(range(0, 177, 5))
-    scale = np.array([1e5, 1e5])
-    xy = (london.xy - london.xy.min(0)) * scale + np.array([500000.0, 150000.0])
-    proj = PolygonSet(xy, london.ring_offsets, london.part_rings, london.geom_parts)
     res = 4
 
     def cell_fn(xs, ys, r):

@@ -73,10 +73,8 @@ def test_keep_core_geom_false(zones35):
 
 
 def test_bng_tessellation_invariant():
-    london = PolygonSet.load("london_postcode_zones")
-    # planar stand-in coordinates (metres) for the BNG grid; projection is not on the hot path
-    xy = (london.xy - london.xy.min(0)) * 1e5 + np.array([500000.0, 150000.0])
-    proj = PolygonSet(xy, london.ring_offsets, london.part_rings, london.geom_parts).subset(range(0, 177, 6))
+    # the London postcode zones in EPSG:27700 metres (tests/golden/make_bng_fixture.py)
+    proj = PolygonSet.load("london_postcodes_bng").subset(range(0, 177, 6))
     chips = tessellate("BNG", proj, 3)
     rng = np.random.default_rng(0)
     x0, y0, x1, y1 = proj.bbox()

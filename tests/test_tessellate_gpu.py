@@ -29,10 +29,8 @@ def ctx():
 
 @pytest.fixture(scope="module")
 def london_m():
-    # planar stand-in coordinates (metres) for the BNG grid, as in test_tessellate.py
-    lon = PolygonSet.load("london_postcode_zones")
-    xy = (lon.xy - lon.xy.min(0)) * 1e5 + np.array([500000.0, 150000.0])
-    return PolygonSet(xy, lon.ring_offsets, lon.part_rings, lon.geom_parts)
+    # the London postcode zones in EPSG:27700 metres (tests/golden/make_bng_fixture.py)
+    return PolygonSet.load("london_postcodes_bng")
 
 
 def _same(a, b):

@@ -16,6 +16,21 @@ if [[ $STEP == all || $STEP == kbench ]]; then
       || { echo "kbench failed"; tail -20 gpurun_out/kbench.log; exit 1; }
   cat gpurun_out/kbench.log
 fi
+if [[ $STEP == configs ]]; then
+  timeout -k 10 300 python -u tools/kbench.py --n 1e9 --res 10 --clustered > gpurun_out/kbench_c3.log 2>&1 \
+      || { echo "kbench c3 failed"; tail -20 gpurun_out/kbench_c3.log; exit 1; }
+  cat gpurun_out/kbench_c3.log
+  timeout -k 10 300 python -u tools/kbench_bng.py --n 1e9 --res 4 > gpurun_out/kbench_c5.log 2>&1 \
+      || { echo "kbench c5 failed"; tail -20 gpurun_out/kbench_c5.log; exit 1; }
+  cat gpurun_out/kbench_c5.log
+fi
+if [[ $STEP == newtests ]]; then
+  timeout -k 10 600 python -u -m pytest tests/test_coords.py tests/test_bng_parse.py tests/test_tessellate_gpu.py \
+      "tests/test_gpu_parity.py::test_join_bng_dense_table" "tests/test_gpu_parity.py::test_join_bng" -m gpu -v \
+      --timeout 300 --timeout-method thread > gpurun_out/gpu_newtests.log 2>&1 \
+      || { echo "new gpu tests failed"; tail -40 gpurun_out/gpu_newtests.log; exit 1; }
+  tail -3 gpurun_out/gpu_newtests.log
+fi
 if [[ $STEP == all || $STEP == bench ]]; then
   timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err \
       || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
