@@ -703,6 +703,185 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 }
 
 
+// ---- k_join_stream_pipe: k_join_stream's per-point computation as a three-stage software
+// pipeline over the wave's groups of 256 rows, so that the gathers of one group overlap the
+// coordinate loads of the next instead of adding to them.  Iteration t: finish group t - 2 (its leaf
+// codes / line records arrived), turn group t - 1's sub-block entries into leaf and line gathers,
+// run group t's coordinates through the quad level and issue its sub-block gathers, and load group
+// t + 1's coordinates -- issued in that order, so every wait is on the oldest loads in flight
+// (vector-memory returns retire in order per wave).  Needs 16-byte aligned columns, tile_base in
+// LDS and at least one full group; the wave's last partial group runs unpipelined.  Same answers
+// as k_join_stream, point for point.
+struct PipeGroup {
+    float u[4], v[4];     // offset in the sub-block, leaf cells
+    uint32_t lf[4];       // leaf cell index within the leaf block
+    uint32_t tbv[4];      // tile base
+    uint32_t qv[4];       // quad-level entry
+    uint32_t code[4];     // sub-block entry (gathered), then the answer
+    uint32_t leaf[4];     // gathered leaf code
+    v4u lrec[4];          // gathered line record
+};
+// quad-level value standing for "non-finite coordinates" in a group (never a code: codes are
+// <= kMaxRasterKeys + 1 or >= kSubBlock): the row takes the tile path
+static const uint32_t kPipeNonFinite = 0x7fffu;
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_pipe(JoinArgs a, StreamArgs s) {
+    extern __shared__ unsigned int lds[];
+    const int nwaves = (int)(blockDim.x >> 6);
+    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
+    uint32_t* stage = lds + ncw;
+    uint32_t* tb = stage + nwaves * s.stage_words;
+    uint32_t* quadw = tb + s.n_tiles;
+    const uint16_t* quad = (const uint16_t*)quadw;
+    for (int k = threadIdx.x; k < s.n_quad_words; k += blockDim.x) quadw[k] = s.quad[k];
+    for (int k = threadIdx.x; k < s.n_tiles; k += blockDim.x) tb[k] = s.tile_base[k];
+    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
+    const __amdgpu_buffer_rsrc_t rblk = stream_rsrc(s.blocks, s.blocks_bytes);
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t* wq = stage + wave * s.stage_words;
+    uint32_t wn = 0;
+    const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
+    // full groups of this wave: wbase + t stride, t < T
+    const int64_t T = wbase + 256 <= a.n ? (a.n - 256 - wbase) / stride + 1 : 0;
+    auto row_of = [&](int64_t wb, int k) -> int64_t { return wb + (k >> 1) * 128 + 2 * lane + (k & 1); };
+    // stage A: coordinates -> fine cell, quad level and tile base (LDS) -> sub-block gathers
+    auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, PipeGroup& g) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool lv = valid && live[k];
+            const double gx = fmin(fmax((x[k] - s.x0) * s.sxC, 0.0), s.gxmax);  // NaN -> 0
+            const double gy = fmin(fmax((y[k] - s.y0) * s.syC, 0.0), s.gymax);
+            const uint32_t ixC = (uint32_t)(int)gx, iyC = (uint32_t)(int)gy;
+            g.u[k] = (float)(gx - (double)(ixC & ~cm));
+            g.v[k] = (float)(gy - (double)(iyC & ~cm));
+            g.lf[k] = ((iyC & cm) << s.cs) | (ixC & cm);
+            const uint32_t q = quad[__umul24(iyC >> s.qsh, (uint32_t)s.qnx) + (ixC >> s.qsh)];
+            // dead rows answer 0, non-finite ones kPipeNonFinite (-> kMixed)
+            g.qv[k] = !lv ? 0u : (__builtin_isfinite(x[k] + y[k]) ? q : kPipeNonFinite);
+            g.tbv[k] = tb[__umul24(iyC >> s.tsh, (uint32_t)s.tnx) + (ixC >> s.tsh)];
+            const uint32_t local = (((iyC >> s.cs) & qm) << s.qs) | ((ixC >> s.cs) & qm);
+            const uint32_t off = ((((g.qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
+            g.code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, g.qv[k] >= 0x8000u ? off : kNoLoad, 0, 0);
+        }
+    };
+    // stage B: sub-block entries -> leaf and line gathers
+    auto stage_b = [&](PipeGroup& g) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t c = g.qv[k] >= 0x8000u ? g.code[k] : g.qv[k];
+            g.code[k] = c;
+            const bool blk = c - 0x8000u < 0x7fffu;  // kSubBlock | n, not kMixed
+            const bool line = blk && (c & 0x4000u);
+            const uint32_t n = c & 0x3fffu;
+            const uint32_t loff = (g.tbv[k] + (n << (2 * s.cs)) + g.lf[k]) << 1;
+            const uint32_t roff = (g.tbv[k] - 8u * (n + 1u)) << 1;
+            g.leaf[k] = __builtin_amdgcn_raw_buffer_load_b16(rblk, (blk && !line) ? loff : kNoLoad, 0, 0);
+            g.lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rblk, line ? roff : kNoLoad, 0, 0);
+        }
+    };
+    // stage D: the answers -> counts and the mixed-row stage
+    auto stage_d = [&](PipeGroup& g, int64_t wb) {
+        uint32_t code[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float sv = fmaf(__uint_as_float(g.lrec[k].x), g.u[k],
+                                  fmaf(__uint_as_float(g.lrec[k].y), g.v[k], __uint_as_float(g.lrec[k].z)));
+            const uint32_t pos = g.lrec[k].w & 0xffffu, neg = g.lrec[k].w >> 16;
+            uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
+            lc = sv <= -1.0f ? neg : lc;
+            const uint32_t gc = g.code[k];
+            const bool blk = gc - 0x8000u < 0x7fffu, line = blk && (gc & 0x4000u);
+            uint32_t c = line ? lc : (blk ? g.leaf[k] : gc);
+            code[k] = c == kPipeNonFinite ? (uint32_t)tiles::kMixed : c;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (LDS_COUNTS && !PAIRS) {
+                const uint32_t slot = code[k] - 1u < 0xfffeu ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
+                atomicAdd(&lds[slot], 1u);
+            } else if (code[k] - 1u < 0xfffeu) {
+                emit_hit<LDS_COUNTS, PAIRS>(a, row_of(wb, k), code[k] - 1u, lds);
+            }
+        }
+        const bool anym = code[0] == tiles::kMixed || code[1] == tiles::kMixed || code[2] == tiles::kMixed ||
+                          code[3] == tiles::kMixed;
+        if (__ballot(anym)) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool m = code[k] == tiles::kMixed;
+                const unsigned long long mm = __ballot(m);
+                if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(wb, k) - a.row_lo);
+                wn += (uint32_t)__popcll(mm);
+            }
+            stage_flush(a, wq, wn, lane, 64);
+        }
+    };
+    v2d px[2], py[2];
+    auto load4 = [&](int64_t wb, bool valid) {  // unconditional: invalid groups re-read the wave's first rows
+        const int64_t r = valid ? wb + 2 * lane : wbase + 2 * lane;
+        px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
+        px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
+        py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
+        py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
+    };
+    // two group slots used in turn (no copies of registers that loads are still landing in):
+    // iteration t finishes the slot holding t - 2, advances the one holding t - 1, refills the first
+    PipeGroup g0, g1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        g0.qv[k] = g1.qv[k] = 0u;
+        g0.code[k] = g1.code[k] = 0u;
+        g0.tbv[k] = g1.tbv[k] = g0.lf[k] = g1.lf[k] = 0u;
+        g0.u[k] = g1.u[k] = g0.v[k] = g1.v[k] = 0.0f;
+    }
+    auto step = [&](int64_t t, PipeGroup& gfin, PipeGroup& gadv) {
+        const bool all[4] = {true, true, true, true};
+        if (t >= 2) stage_d(gfin, wbase + (t - 2) * stride);
+        stage_b(gadv);  // (invalid groups gather nothing)
+        const double x[4] = {px[0].x, px[0].y, px[1].x, px[1].y}, y[4] = {py[0].x, py[0].y, py[1].x, py[1].y};
+        stage_a(x, y, all, t < T, gfin);
+        load4(wbase + (t + 1) * stride, t + 1 < T);
+    };
+    if (T > 0) {
+        load4(wbase, true);
+        for (int64_t t = 0; t < T + 2; t += 2) {
+            step(t, g0, g1);
+            if (t + 1 >= T + 2) break;
+            step(t + 1, g1, g0);
+        }
+    }
+    // the wave's partial group (rows past its last full group), unpipelined
+    const int64_t wt = wbase + T * stride;
+    if (wt < a.n) {
+        double x[4], y[4];
+        bool live[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int64_t r = row_of(wt, k);
+            live[k] = r < a.n;
+            x[k] = live[k] ? a.x[r] : 0.0;
+            y[k] = live[k] ? a.y[r] : 0.0;
+        }
+        PipeGroup g;
+        stage_a(x, y, live, true, g);
+        stage_b(g);
+        stage_d(g, wt);
+    }
+    stage_flush(a, wq, wn, lane, 1);
+    if (LDS_COUNTS) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
+    }
+}
+
 // ---- st_intersects_aggregate over the chip join of two chip tables ----------------------------
 // ST_IntersectsAggregate.update (expressions/geometry/ST_IntersectsAggregate.scala:28-39) folds
 // `left.is_core || right.is_core || left.wkb intersects right.wkb` with OR over the rows of a
@@ -1006,67 +1185,128 @@ __global__ void __launch_bounds__(256) k_bng_cell_wkb(const int64_t* ids, const 
 // tiles_build.cpp bng_leaf_blocks); kMixed codes send the row to the mixed queue.
 static const uint32_t kBngPure = 0x80000000u, kBngLeaf = 0x40000000u;
 
-// Returns a join code (0 none, k + 1 one pair with key k) or tiles::kMixed (queue the row).
-__device__ inline uint32_t bng_dense_code(const JoinArgs& a, double x, double y) {
-    const int32_t eI = bng::jvm_d2i(x), nI = bng::jvm_d2i(y);
-    if (!(eI >= 0 && eI < 10000000 && nI >= 0 && nI < 10000000)) return tiles::kMixed;  // generic path
-    const int32_t qe = eI / a.bng_div, qn = nI / a.bng_div;
-    const int32_t ce = qe - a.bng_e0, cn = qn - a.bng_n0;
-    if ((uint32_t)ce >= (uint32_t)a.bng_ne || (uint32_t)cn >= (uint32_t)a.bng_nn) return 0;  // no chip cell
-    const uint32_t e = a.bng_cells[(int64_t)cn * a.bng_ne + ce];
-    if (e & kBngPure) return e & ~kBngPure;
-    if (!(e & kBngLeaf)) return e ? tiles::kMixed : 0u;
-    // sub-cell of the point inside the cell [qe div, (qe + 1) div) x [qn div, (qn + 1) div)
-    const double f = (double)a.bng_C / (double)a.bng_div;
-    int sx = (int)((x - (double)qe * (double)a.bng_div) * f), sy = (int)((y - (double)qn * (double)a.bng_div) * f);
-    sx = sx < 0 ? 0 : (sx >= a.bng_C ? a.bng_C - 1 : sx);
-    sy = sy < 0 ? 0 : (sy >= a.bng_C ? a.bng_C - 1 : sy);
-    return a.bng_leaf[(size_t)(e & ~kBngLeaf) * (size_t)(a.bng_C * a.bng_C) + (size_t)(sy * a.bng_C + sx)];
-}
-
-template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(256) k_join_stream_bng(JoinArgs a) {
+// k_join_stream_bng: the dense table's answer for every point, branch-free, in the layout of
+// k_join_stream (256 rows per wave and iteration, 1 KiB coalesced coordinate loads, the next
+// iteration's coordinates loaded behind this iteration's gathers).  Per point: JVM toInt of both
+// coordinates, the cell (exact quotients: (int)(a / div + 1e-7) from one f64 multiply-add -- for
+// a < 1e7 and div <= 1e5 a non-integer quotient is >= 1 / div below the next integer, far more than
+// the 2e-9 the reciprocal and the offset move it), one 4-byte cell gather and, in border cells, one
+// 2-byte leaf gather, both through buffer descriptors (lanes that need none pass an out-of-range
+// offset).  NaN coordinates set flags bit 0 (the reference throws IllegalStateException).
+struct BngStreamArgs {
+    int32_t e0, n0, ne, nn, C;
+    double inv_div, div, f;  // 1 / divisor (rounded), divisor, C / divisor
+    const uint32_t* cells;
+    const uint16_t* leaf;
+    uint32_t cells_bytes, leaf_bytes;
+};
+template <bool LDS_COUNTS, bool PAIRS, bool VEC>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_bng(JoinArgs a, BngStreamArgs s) {
     extern __shared__ unsigned int lds[];
-    __shared__ uint32_t stage[4][64 + 256];
-    counts_init<LDS_COUNTS>(a, lds);
+    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
+    uint32_t* stage = lds + ncw;
+    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rcell = stream_rsrc(s.cells, s.cells_bytes);
+    const __amdgpu_buffer_rsrc_t rleaf = stream_rsrc(s.leaf, s.leaf_bytes);
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    uint32_t* wq = stage[(threadIdx.x >> 6) & 3];
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t* wq = stage + wave * 320;
     uint32_t wn = 0;
     bool nan_seen = false;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    for (int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 4; w0 < a.n; w0 += stride) {
-        const int64_t r0 = w0 + lane * 4;
+    int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
+    auto row_of = [&](int64_t wb, int k) -> int64_t { return wb + (k >> 1) * 128 + 2 * lane + (k & 1); };
+    v2d px[2], py[2];
+    auto load4 = [&](int64_t wb) {
+        const int64_t r = (wb + 256 <= a.n) ? wb + 2 * lane : a.row_lo;
+        px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
+        px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
+        py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
+        py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
+    };
+    if (VEC) load4(w0);
+    const uint32_t C = (uint32_t)s.C;
+    for (; w0 < a.n; w0 += stride) {
+        const bool full = VEC && w0 + 256 <= a.n;
         double x[4], y[4];
         bool live[4];
+        if (full) {
+            x[0] = px[0].x, x[1] = px[0].y, x[2] = px[1].x, x[3] = px[1].y;
+            y[0] = py[0].x, y[1] = py[0].y, y[2] = py[1].x, y[3] = py[1].y;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            live[k] = r0 + k < a.n && (!a.valid || a.valid[r0 + k]);
-            x[k] = live[k] ? a.x[r0 + k] : 0.0;
-            y[k] = live[k] ? a.y[r0 + k] : 0.0;
-        }
-        uint32_t code[4];
+            for (int k = 0; k < 4; k++) live[k] = true;
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            code[k] = 0;
-            if (!live[k]) continue;
-            if (x[k] != x[k] || y[k] != y[k]) {  // the reference throws IllegalStateException
-                nan_seen = true;
-                continue;
+            for (int k = 0; k < 4; k++) {
+                const int64_t r = row_of(w0, k);
+                live[k] = r < a.n;
+                x[k] = live[k] ? a.x[r] : 0.0;
+                y[k] = live[k] ? a.y[r] : 0.0;
             }
-            code[k] = bng_dense_code(a, x[k], y[k]);
+        }
+        uint32_t code[4], e[4], loff[4];
+        bool inr[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool nan = x[k] != x[k] || y[k] != y[k];
+            nan_seen |= live[k] && nan;
+            const int32_t eI = bng::jvm_d2i(x[k]), nI = bng::jvm_d2i(y[k]);
+            inr[k] = (uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u;
+            const int32_t qe = (int32_t)fma((double)eI, s.inv_div, 1e-7), qn = (int32_t)fma((double)nI, s.inv_div, 1e-7);
+            const int32_t ce = qe - s.e0, cn = qn - s.n0;
+            const bool cell_in = inr[k] && (uint32_t)ce < (uint32_t)s.ne && (uint32_t)cn < (uint32_t)s.nn;
+            e[k] = __builtin_amdgcn_raw_buffer_load_b32(rcell, cell_in ? (uint32_t)(cn * s.ne + ce) << 2 : kNoLoad, 0, 0);
+            // sub-cell of the point inside the cell [qe div, (qe + 1) div) x [qn div, (qn + 1) div)
+            int sx = (int)((x[k] - (double)qe * s.div) * s.f), sy = (int)((y[k] - (double)qn * s.div) * s.f);
+            sx = min(max(sx, 0), (int)C - 1);
+            sy = min(max(sy, 0), (int)C - 1);
+            loff[k] = (uint32_t)(sy * (int)C + sx);
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const bool mixed = code[k] == tiles::kMixed;
-            if (code[k] && !mixed) emit_hit<LDS_COUNTS, PAIRS>(a, r0 + k, code[k] - 1u, lds);
-            stage_push(wq, wn, mixed, (uint32_t)(r0 + k - a.row_lo), lt_mask);
+            const bool leafc = (e[k] & (kBngPure | kBngLeaf)) == kBngLeaf;
+            const uint32_t off = (((e[k] & ~kBngLeaf) * C * C) + loff[k]) << 1;
+            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rleaf, leafc ? off : kNoLoad, 0, 0);
         }
-        stage_flush(a, wq, wn, lane, 64);
+        if (VEC) load4(w0 + stride);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t c = (e[k] & kBngPure) ? (e[k] & ~kBngPure) : ((e[k] & kBngLeaf) ? code[k] : (e[k] ? (uint32_t)tiles::kMixed : 0u));
+            c = inr[k] ? c : (uint32_t)tiles::kMixed;      // outside the one-to-one range: generic path
+            c = (x[k] != x[k] || y[k] != y[k]) ? 0u : c;  // NaN: flagged, no pair
+            code[k] = live[k] ? c : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (LDS_COUNTS && !PAIRS) {
+                const uint32_t slot = code[k] - 1u < 0xfffeu ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
+                atomicAdd(&lds[slot], 1u);
+            } else if (code[k] - 1u < 0xfffeu) {
+                emit_hit<LDS_COUNTS, PAIRS>(a, row_of(w0, k), code[k] - 1u, lds);
+            }
+        }
+        const bool anym = code[0] == tiles::kMixed || code[1] == tiles::kMixed || code[2] == tiles::kMixed ||
+                          code[3] == tiles::kMixed;
+        if (__ballot(anym)) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool m = code[k] == tiles::kMixed;
+                const unsigned long long mm = __ballot(m);
+                if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(w0, k) - a.row_lo);
+                wn += (uint32_t)__popcll(mm);
+            }
+            stage_flush(a, wq, wn, lane, 64);
+        }
     }
     stage_flush(a, wq, wn, lane, 1);
-    if (nan_seen) atomicOr(a.flags, 1u);
-    counts_flush<LDS_COUNTS>(a, lds, 0u);
+    if (__ballot(nan_seen) && lane == 0) atomicOr(a.flags, 1u);
+    if (LDS_COUNTS) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
+    }
 }
 
 template <bool LDS_COUNTS, bool PAIRS>
@@ -1409,6 +1649,7 @@ struct Options {
     int raster_quad = 1;      // point raster: LDS quad level
     int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
+    int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
     int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
@@ -1568,6 +1809,7 @@ struct mosaic_chips {
     bool bng_ok = false;  // BNG dense cell table (k_join_stream_bng)
     int32_t bng_e0 = 0, bng_n0 = 0, bng_ne = 0, bng_nn = 0, bng_div = 1, bng_C = 0;
     DevBuf bng_cells, bng_leaf;
+    size_t bng_leaf_bytes = 0;
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
     bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
@@ -1724,6 +1966,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "stream_block") {
         if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, 1024]");
         o.stream_block = (int)v;
+    } else if (k == "stream_pipe") {
+        o.stream_pipe = v ? 1 : 0;
     } else if (k == "timing") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
         o.timing = (int)v;
@@ -2461,7 +2705,9 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                                            gb.part_ring.data(), gb.geom_part.data(), gb.geom_bbox.data()};
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-                if (border.size() < ((size_t)1 << 30) && tiles::bng_leaf_blocks(src, border, (double)div, C, threads, leaf)) {
+                // (leaf offsets are 32-bit buffer offsets in k_join_stream_bng)
+                if (border.size() * C * C * 2 < (size_t)kNoLoad &&
+                    tiles::bng_leaf_blocks(src, border, (double)div, C, threads, leaf)) {
                     for (size_t b = 0; b < border.size(); b++) tab[border_at[b]] = kBngLeaf | (uint32_t)b;
                     ch->bng_C = C;
                 } else {
@@ -2477,6 +2723,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             }
             HIP_TRY(hipMemcpy(ch->bng_cells.p, tab.data(), bb, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(ch->bng_leaf.p, leaf.data(), lb, hipMemcpyHostToDevice));
+            ch->bng_leaf_bytes = lb;
             total += lb;
             if (!ch->bng_C) ch->bng_C = C;
             ch->bng_ok = true;
@@ -2778,25 +3025,47 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             a.bng_div = ch->bng_div;
             a.bng_leaf = (const uint16_t*)ch->bng_leaf.p;
             a.bng_C = ch->bng_C;
-            const int64_t chunk = ((int64_t)1 << 32) - 4;
+            BngStreamArgs bs;
+            bs.e0 = ch->bng_e0;
+            bs.n0 = ch->bng_n0;
+            bs.ne = ch->bng_ne;
+            bs.nn = ch->bng_nn;
+            bs.C = ch->bng_C;
+            bs.div = (double)ch->bng_div;
+            bs.inv_div = 1.0 / (double)ch->bng_div;
+            bs.f = (double)ch->bng_C / (double)ch->bng_div;
+            bs.cells = (const uint32_t*)ch->bng_cells.p;
+            bs.leaf = (const uint16_t*)ch->bng_leaf.p;
+            bs.cells_bytes = (uint32_t)((size_t)ch->bng_ne * ch->bng_nn * 4);
+            bs.leaf_bytes = (uint32_t)std::min<size_t>(ch->bng_leaf_bytes, kNoLoad);
+            const int64_t chunk = ((int64_t)1 << 32) - 256;
             const int64_t rows = std::min<int64_t>(n, chunk);
-            const int gs = grid_size(c, (rows + 3) / 4);
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
+            const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
+            const int blkb = c->stream_block;
+            const size_t shm_b = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blkb / 64) * 320 * 4;
+            auto kernel_for = [&](bool vec) -> const void* {
+                if (pairs) return vec ? (const void*)k_join_stream_bng<false, true, true> : (const void*)k_join_stream_bng<false, true, false>;
+                if (lds) return vec ? (const void*)k_join_stream_bng<true, false, true> : (const void*)k_join_stream_bng<true, false, false>;
+                return vec ? (const void*)k_join_stream_bng<false, false, true> : (const void*)k_join_stream_bng<false, false, false>;
+            };
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blkb, shm_b) != hipSuccess || per_cu < 1)
+                per_cu = 1;
             for (int64_t lo = 0; lo < n; lo += chunk) {
                 JoinArgs ac = a;
                 ac.row_lo = lo;
                 ac.n = std::min<int64_t>(n, lo + chunk);
                 if (lo > 0) HIP_TRY(hipMemsetAsync(ac.mixq_count, 0, 8, c->stream));
-                if (pairs)
-                    hipLaunchKernelGGL((k_join_stream_bng<false, true>), dim3(gs), dim3(c->block), 0, c->stream, ac);
-                else if (lds)
-                    hipLaunchKernelGGL((k_join_stream_bng<true, false>), dim3(gs), dim3(c->block), shm, c->stream, ac);
-                else
-                    hipLaunchKernelGGL((k_join_stream_bng<false, false>), dim3(gs), dim3(c->block), 0, c->stream, ac);
-                HIP_TRY(hipGetLastError());
+                const void* kfn = kernel_for(aligned && ac.n - lo >= 256);
+                const int gs = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + 4 * blkb - 1) / (4 * blkb),
+                                                                           (int64_t)c->n_cu * per_cu));
+                void* kargs[] = {&ac, &bs};
+                HIP_TRY(hipLaunchKernel(kfn, dim3(gs), dim3(blkb), kargs, shm_b, c->stream));
                 if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
-                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>(gs, (int64_t)c->n_cu * c->mixed_blocks_per_cu));
+                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + c->block - 1) / c->block,
+                                                                           (int64_t)c->n_cu * c->mixed_blocks_per_cu));
                 if (pairs)
                     hipLaunchKernelGGL((k_join_mixed_bng<false, true>), dim3(gm), dim3(c->block), 0, c->stream, ac);
                 else if (lds)
@@ -2815,6 +3084,11 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             a.mixq_count = sc + 4;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             auto kernel_for = [&](bool vec) -> const void* {
+                if (vec && sa.tb_lds && c->stream_pipe) {  // the pipelined form (k_join_stream_pipe)
+                    if (pairs) return (const void*)k_join_stream_pipe<false, true>;
+                    if (lds) return (const void*)k_join_stream_pipe<true, false>;
+                    return (const void*)k_join_stream_pipe<false, false>;
+                }
                 if (pairs) return vec ? (const void*)k_join_stream<false, true, true> : (const void*)k_join_stream<false, true, false>;
                 if (lds) return vec ? (const void*)k_join_stream<true, false, true> : (const void*)k_join_stream<true, false, false>;
                 return vec ? (const void*)k_join_stream<false, false, true> : (const void*)k_join_stream<false, false, false>;

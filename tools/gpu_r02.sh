@@ -24,6 +24,27 @@ if [[ $STEP == configs ]]; then
       || { echo "kbench c5 failed"; tail -20 gpurun_out/kbench_c5.log; exit 1; }
   cat gpurun_out/kbench_c5.log
 fi
+if [[ $STEP == pipe ]]; then
+  timeout -k 10 600 python -u -m pytest "tests/test_gpu_parity.py::test_join_tiled_nyc_zones_match_oracle" \
+      "tests/test_gpu_parity.py::test_join_tessellated_chips_every_strategy" "tests/test_gpu_parity.py::test_join_point_raster_sizes" \
+      "tests/test_gpu_parity.py::test_join_counts_match_oracle" tests/test_gpu_threads.py -m gpu -v \
+      --timeout 300 --timeout-method thread > gpurun_out/gpu_pipetests.log 2>&1 \
+      || { echo "pipe gpu tests failed"; tail -40 gpurun_out/gpu_pipetests.log; exit 1; }
+  tail -3 gpurun_out/gpu_pipetests.log
+  timeout -k 10 300 python -u tools/kbench.py --n 1e9 --sweep stream_pipe=0 stream_pipe=1 > gpurun_out/kbench_pipe.log 2>&1 \
+      || { echo "kbench failed"; tail -20 gpurun_out/kbench_pipe.log; exit 1; }
+  cat gpurun_out/kbench_pipe.log
+  timeout -k 10 300 python -u tools/kbench.py --n 1e9 --res 10 --clustered --sweep stream_pipe=0 stream_pipe=1 > gpurun_out/kbench_pipe_c3.log 2>&1 \
+      || { echo "kbench c3 failed"; tail -20 gpurun_out/kbench_pipe_c3.log; exit 1; }
+  cat gpurun_out/kbench_pipe_c3.log
+  timeout -k 10 300 python -u tools/kbench_bng.py --n 1e9 --res 4 > gpurun_out/kbench_c5.log 2>&1 \
+      || { echo "kbench c5 failed"; tail -20 gpurun_out/kbench_c5.log; exit 1; }
+  cat gpurun_out/kbench_c5.log
+  timeout -k 10 600 python -u -m pytest "tests/test_gpu_parity.py::test_join_bng_dense_table" "tests/test_gpu_parity.py::test_join_bng" \
+      tests/test_bng_parse.py -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/gpu_bngtests.log 2>&1 \
+      || { echo "bng gpu tests failed"; tail -40 gpurun_out/gpu_bngtests.log; exit 1; }
+  tail -3 gpurun_out/gpu_bngtests.log
+fi
 if [[ $STEP == newtests ]]; then
   timeout -k 10 600 python -u -m pytest tests/test_coords.py tests/test_bng_parse.py tests/test_tessellate_gpu.py \
       "tests/test_gpu_parity.py::test_join_bng_dense_table" "tests/test_gpu_parity.py::test_join_bng" -m gpu -v \

@@ -28,6 +28,7 @@ def main():
     p.add_argument("--quads", type=int, nargs="*", default=[1], help="raster_quad values (1 default, else entry budget)")
     p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*", default=[(1, 1)],
                    help="TILES:POINT_RASTER pairs")
+    p.add_argument("--sweep", nargs="*", default=[""], help="option sets to time, e.g. stream_pipe=0 stream_pipe=1")
     args = p.parse_args()
     import torch
 
@@ -61,8 +62,11 @@ def main():
             for tiles, praster in args.modes:
                 ctx.set_option("tiles", tiles)
                 ctx.set_option("point_raster", praster)
-                for sb in args.stream_blocks:
+                for sb, sw in [(b, w) for b in args.stream_blocks for w in args.sweep]:
                     ctx.set_option("stream_block", sb)
+                    for kv in filter(None, sw.split(",")):
+                        k, v = kv.split("=")
+                        ctx.set_option(k, int(v))
                     ctx.pip_join_count(table, x, y, out=counts)
                     torch.cuda.synchronize()
                     ctx.set_option("timing", 2)
@@ -83,7 +87,7 @@ def main():
                     stats = ctx.last_stats()
                     step = float(np.median(ts))
                     line = {"res": args.res, "clustered": args.clustered, "n": n, "raster": f"{sub}x{cell}",
-                            "quad": quad, "tiles": tiles, "point_raster": praster, "stream_block": sb,
+                            "quad": quad, "tiles": tiles, "point_raster": praster, "stream_block": sb, "options": sw,
                             "call_ms": round(step, 4), "points_per_s": n / (step * 1e-3),
                             "same_counts": bool(np.array_equal(got, ref)), "pairs": int(got.sum()),
                             "tess_s": round(tess_s, 2), "build_s": round(build_s, 2),
