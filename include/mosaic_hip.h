@@ -94,7 +94,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
  * side and leaf cells per sub-block side, powers of two, for tables built afterwards; default 64 /
  * 16), "raster_lines" (0/1: sub-blocks crossed by one straight chip edge store a line record instead
- * of a leaf block; default 1), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768
+ * of a leaf block; default 1), "raster_build" (1: the point raster is classified on the GPU, the
+ * default; 0: on host threads -- identical bytes), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768
  * entries, or an entry budget <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of
  * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
  * host-resident coordinates: the next chunk's copy overlaps the current chunk's join; 0 = stage the
@@ -225,6 +226,11 @@ int mosaic_chip_table_tile_grid(const mosaic_chips* chips, double* out4);
  * level entries (0: none), quad shift (sub-blocks per quad side = 1 << shift), raster bytes on the
  * device, 1 if joins run the stream kernel on it (quad level with compact copies, edges clamp-safe). */
 int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out5);
+/* Build cost of the table in ms (ms4): chip hash + geometry + chip rasters, tile directory (host),
+ * point-raster classification (GPU with option "raster_build" = 1, the default; host threads with
+ * 0), point-raster assembly (host); *digest = FNV-1a 64 of the point raster's arrays (0: no raster),
+ * equal for both classification builds. */
+int mosaic_chip_table_build_info(const mosaic_chips* chips, double* ms4, uint64_t* digest);
 
 /* ---- the join ---- */
 /* counts[p] = number of (point, chip) pairs with chip polygon_key p (overwritten). */

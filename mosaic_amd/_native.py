@@ -38,7 +38,7 @@ EXPORTS = [
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
     "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb", "mosaic_point_to_cell_exact",
     "mosaic_diag_libm", "mosaic_point_coords_to_cell", "mosaic_point_coords_decode", "mosaic_bng_parse_column",
-    "mosaic_chip_table_create_arrow",
+    "mosaic_chip_table_create_arrow", "mosaic_chip_table_build_info",
 ]
 
 GEOM_WKB = 0
@@ -131,6 +131,7 @@ def lib():
         "mosaic_point_coords_decode": ([vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, ctypes.POINTER(i64)], i32),
         "mosaic_bng_parse_column": ([vp, i32, vp, vp, vp, i64, vp], i32),
         "mosaic_chip_table_create_arrow": ([vp, i32, i32, i64, vp, vp, vp, i32, vp, vp, i32, ctypes.POINTER(vp)], i32),
+        "mosaic_chip_table_build_info": ([vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -262,6 +262,15 @@ class ChipTable:
                  stream=int(r[4]))
         return d
 
+    def build_info(self):
+        """Build cost of this table in ms (chip core, tile directory, point-raster classification,
+        point-raster assembly) and the point raster's FNV-1a digest (0: no raster)."""
+        ms = np.zeros(4, np.float64)
+        dig = np.zeros(1, np.uint64)
+        N.check(N.lib().mosaic_chip_table_build_info(self.handle, N.ptr(ms), N.ptr(dig)))
+        return dict(core_ms=float(ms[0]), directory_ms=float(ms[1]), raster_classify_ms=float(ms[2]),
+                    raster_assemble_ms=float(ms[3]), raster_digest=int(dig[0]))
+
     def close(self):
         if self.handle:
             N.lib().mosaic_chip_table_destroy(self.handle)

@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -31,6 +32,7 @@
 #include "pip_device.h"
 #include "point_decode.h"
 #include "raster.h"
+#include "raster_build.h"
 #include "tiles.h"
 
 using namespace mosaic;
@@ -882,6 +884,333 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     }
 }
 
+// ---- point-raster build on the GPU: phase 1 of tiles::Builder::build_raster (tiles_build.cpp,
+// classify_raster_host), the same classification with the same arithmetic (raster_build.h), so the
+// raster is identical bit for bit.  k_raster_sub: one lane per sub-block of every tile record ->
+// its code or kMixed; k_raster_line: one lane per mixed sub-block -> a line record, if one
+// certifies; k_raster_cells: one lane per leaf cell of the other mixed sub-blocks.  Candidate
+// hexagons are recomputed per lane (a window holds a few dozen).  The host assembles (phase 2).
+struct RBuildArgs {
+    const tiles::TileRec* recs;
+    const int32_t* tile_of_rec;
+    const double* rec_dev;
+    const uint32_t* entries;  // tile-window entries: chip-hash slot + 1
+    int32_t n_recs, tnx;
+    double gx0, gy0, tw, th;
+    int32_t S, C, N, res, lines;
+    const HashEntry* table;
+    const uint32_t* meta;
+    pip::GeomStore store;
+    rbuild::HexTable ht;
+    uint16_t* code;             // n_recs x S x S
+    const uint32_t* mixed;      // k_raster_line: mixed sub-blocks (index into code)
+    int64_t n_mixed;
+    uint8_t* kind;              // per mixed sub-block: 1 line record, 0 cells
+    tiles::LineRec* line;
+    const uint32_t* cell_sb;    // k_raster_cells: the kind-0 mixed sub-blocks (index into code)
+    int64_t n_cell_sb;
+    uint16_t* cells;            // n_cell_sb x C x C
+};
+
+struct RTile {  // one tile record, as the builder's per-record lambda sees it
+    int face, wa, wb, a0, b0;
+    uint32_t off;
+    double lon0, lat0, dev, exd, eyd;
+};
+
+__device__ inline bool rtile_of(const RBuildArgs& a, int r, RTile& t) {
+    const tiles::TileRec tr = a.recs[r];
+    const int ti_ = a.tile_of_rec[r];
+    if (ti_ < 0 || tr.dims == 0) return false;
+    const int ti = ti_ % a.tnx, tj = ti_ / a.tnx;
+    t.face = (int)(tr.dims & 0xffu);
+    t.wa = (int)((tr.dims >> 8) & 0xfffu);
+    t.wb = (int)(tr.dims >> 20);
+    t.a0 = tr.a0;
+    t.b0 = tr.b0;
+    t.off = tr.off;
+    t.lon0 = a.gx0 + ti * a.tw;
+    t.lat0 = a.gy0 + tj * a.th;
+    t.dev = a.rec_dev[r];
+    const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
+    t.exd = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
+    t.eyd = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
+    return true;
+}
+
+__device__ inline rbuild::P2 rimage(const RBuildArgs& a, const RTile& t, double i, double j) {
+    double px, py, pz, vx, vy, b;
+    h3::fast_unit(t.lat0 + a.th * j / a.N, t.lon0 + a.tw * i / a.N, &px, &py, &pz);
+    h3::fast_plane(px, py, pz, t.face, a.res, &vx, &vy, &b);
+    return rbuild::P2{vx, vy};
+}
+
+__device__ inline rbuild::P2 rhex_centre(const RTile& t, int k) {
+    const int ra = k / t.wb, rb = k - ra * t.wb;
+    const int aa = t.a0 + ra, bb = t.b0 + rb;
+    return rbuild::P2{(double)aa - 0.5 * (double)bb, (double)bb * rbuild::kS60};
+}
+
+// The answer of window hexagon k's points in a region: the keys of its core chips plus those of
+// its border chips containing (cx, cy) -- as (count, key of a single one) -- or -1 when a border
+// chip's boundary meets the region (rect: [x0, x1] x [y0, y1]; poly: ll[n] within eps).
+__device__ inline int rhex_answer(const RBuildArgs& a, const RTile& t, int k, bool poly, double x0, double y0,
+                                  double x1, double y1, const rbuild::P2* ll, int n, double eps, double cx, double cy,
+                                  int* key) {
+    const uint32_t e = a.entries[t.off + (uint32_t)k];
+    int cnt = 0;
+    *key = -1;
+    if (!e) return 0;
+    const HashEntry he = a.table[e - 1];
+    for (uint32_t c = he.first; c < he.first + he.count; c++) {
+        const uint32_t m = a.meta[c];
+        if (!(m & 1u)) {
+            const pip::Box bx = a.store.geom_bbox[c];
+            const bool meets_box = poly ? !(bx.maxx < x0 - eps || bx.minx > x1 + eps || bx.maxy < y0 - eps || bx.miny > y1 + eps)
+                                        : !(bx.maxx < x0 || bx.minx > x1 || bx.maxy < y0 || bx.miny > y1);
+            if (meets_box) {
+                for (uint32_t p = a.store.geom_part[c]; p < a.store.geom_part[c + 1]; p++)
+                    for (uint32_t r = a.store.part_ring[p]; r < a.store.part_ring[p + 1]; r++)
+                        for (uint32_t v = a.store.ring_start[r] + 1; v < a.store.ring_start[r + 1]; v++) {
+                            const pip::Vec2 s0 = a.store.verts[v - 1], s1 = a.store.verts[v];
+                            const bool hit = poly ? rbuild::seg_meets_poly(rbuild::P2{s0.x, s0.y}, rbuild::P2{s1.x, s1.y}, ll, n, eps)
+                                                  : raster::seg_meets_rect(s0.x, s0.y, s1.x, s1.y, x0, y0, x1, y1);
+                            if (hit) return -1;
+                        }
+            }
+            if (!pip::contains(a.store, c, cx, cy)) continue;
+        }
+        if (cnt == 0) *key = (int)(m >> 1);
+        cnt++;
+    }
+    return cnt;
+}
+
+// tiles_build.cpp classify(): the code of fine-lattice rectangle [i0, i1] x [j0, j1] with corner
+// images q; candidates: window hexagons meeting q (and, for cells, meeting the sub-block quad sq
+// with the sub-block's tolerance).
+__device__ inline uint16_t rclassify_rect(const RBuildArgs& a, const RTile& t, int i0, int j0, int i1, int j1,
+                                          const rbuild::P2* q, const rbuild::P2* sq, double stol) {
+    const double frac = rbuild::dmax((double)(i1 - i0), (double)(j1 - j0)) / a.N;
+    const double tol = 4.0 * t.dev * frac * frac + 1e-7;
+    const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
+    const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
+    const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
+    const double x0 = t.lon0 + a.tw * i0 / a.N - ex, x1 = t.lon0 + a.tw * i1 / a.N + ex;
+    const double y0 = t.lat0 + a.th * j0 / a.N - ey, y1 = t.lat0 + a.th * j1 / a.N + ey;
+    const double cxm = t.lon0 + a.tw * (i0 + i1) / (2.0 * a.N), cym = t.lat0 + a.th * (j0 + j1) / (2.0 * a.N);
+    bool any = false;
+    int acnt = 0, akey = -1;
+    for (int k = 0; k < t.wa * t.wb; k++) {
+        const rbuild::P2 c = rhex_centre(t, k);
+        if (sq && !rbuild::poly_meets_hex(sq, 4, c, stol, a.ht)) continue;
+        if (!rbuild::poly_meets_hex(q, 4, c, tol, a.ht)) continue;
+        int key;
+        const int cnt = rhex_answer(a, t, k, false, x0, y0, x1, y1, nullptr, 0, 0.0, cxm, cym, &key);
+        if (cnt < 0 || cnt > 1) return tiles::kMixed;
+        if (!any) {
+            any = true;
+            acnt = cnt;
+            akey = key;
+        } else if (cnt != acnt || key != akey) {
+            return tiles::kMixed;
+        }
+    }
+    if (!any) return tiles::kMixed;
+    return acnt == 0 ? (uint16_t)0 : (uint16_t)(akey + 1);
+}
+
+// the sub-block quad (corner images) of sub-block (si, sj) and its tolerance
+__device__ inline double rsub_quad(const RBuildArgs& a, const RTile& t, int si, int sj, rbuild::P2* q) {
+    const int C = a.C;
+    q[0] = rimage(a, t, si * C, sj * C);
+    q[1] = rimage(a, t, (si + 1) * C, sj * C);
+    q[2] = rimage(a, t, (si + 1) * C, (sj + 1) * C);
+    q[3] = rimage(a, t, si * C, (sj + 1) * C);
+    const double frac = rbuild::dmax((double)C, (double)C) / a.N;
+    return 4.0 * t.dev * frac * frac + 1e-7;
+}
+
+// tiles_build.cpp classify_poly(): convex region uv[n] of sub-block (si, sj), candidates those
+// of the sub-block (sq, stol)
+__device__ inline uint16_t rclassify_poly(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* uv,
+                                          int n, const rbuild::P2* sq, double stol) {
+    using rbuild::dmax;
+    using rbuild::dmin;
+    rbuild::P2 img[8], ll[8];
+    double u0 = INFINITY, u1 = -INFINITY, v0 = INFINITY, v1 = -INFINITY;
+    double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY, mx = 0.0, my = 0.0;
+    const int S = a.S, C = a.C;
+    for (int v = 0; v < n; v++) {
+        img[v] = rimage(a, t, (si + uv[v].x) * C, (sj + uv[v].y) * C);
+        ll[v] = rbuild::P2{t.lon0 + a.tw * (si + uv[v].x) / S, t.lat0 + a.th * (sj + uv[v].y) / S};
+        u0 = dmin(u0, uv[v].x);
+        u1 = dmax(u1, uv[v].x);
+        v0 = dmin(v0, uv[v].y);
+        v1 = dmax(v1, uv[v].y);
+        x0 = dmin(x0, ll[v].x);
+        x1 = dmax(x1, ll[v].x);
+        y0 = dmin(y0, ll[v].y);
+        y1 = dmax(y1, ll[v].y);
+        mx += ll[v].x;
+        my += ll[v].y;
+    }
+    mx /= n;
+    my /= n;
+    const double frac = dmax(u1 - u0, v1 - v0) / S;
+    const double tol = 4.0 * t.dev * frac * frac + 1e-7;
+    const double eps = dmax(t.exd, t.eyd);
+    bool any = false;
+    int acnt = 0, akey = -1;
+    for (int k = 0; k < t.wa * t.wb; k++) {
+        const rbuild::P2 c = rhex_centre(t, k);
+        if (!rbuild::poly_meets_hex(sq, 4, c, stol, a.ht)) continue;
+        if (!rbuild::poly_meets_hex(img, n, c, tol, a.ht)) continue;
+        int key;
+        const int cnt = rhex_answer(a, t, k, true, x0, y0, x1, y1, ll, n, eps, mx, my, &key);
+        if (cnt < 0 || cnt > 1) return tiles::kMixed;
+        if (!any) {
+            any = true;
+            acnt = cnt;
+            akey = key;
+        } else if (cnt != acnt || key != akey) {
+            return tiles::kMixed;
+        }
+    }
+    if (!any) return tiles::kMixed;
+    return acnt == 0 ? (uint16_t)0 : (uint16_t)(akey + 1);
+}
+
+__global__ void __launch_bounds__(256) k_raster_sub(RBuildArgs a) {
+    const int64_t SS = (int64_t)a.S * a.S;
+    const int64_t total = (int64_t)a.n_recs * SS;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
+        RTile t;
+        uint16_t code = 0;
+        if (rtile_of(a, r, t)) {
+            rbuild::P2 q[4];
+            rsub_quad(a, t, si, sj, q);
+            code = rclassify_rect(a, t, si * a.C, sj * a.C, (si + 1) * a.C, (sj + 1) * a.C, q, nullptr, 0.0);
+        }
+        a.code[g] = code;
+    }
+}
+
+// tiles_build.cpp try_line()
+__device__ inline bool rtry_line(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* sq, double stol,
+                                 tiles::LineRec& out) {
+    const int S = a.S;
+    const double wR = a.tw / S, hR = a.th / S;
+    const double lonR0 = t.lon0 + a.tw * si / S, latR0 = t.lat0 + a.th * sj / S;
+    const double exu = t.exd / wR, eyv = t.eyd / hR;
+    const double bx0 = lonR0 - t.exd, bx1 = lonR0 + wR + t.exd, by0 = latR0 - t.eyd, by1 = latR0 + hR + t.eyd;
+    // pass 0: the longest clipped border-chip segment; pass 1: the largest distance of any clipped
+    // end from its line
+    double best = 0.0, dev_max = 0.0, la = 0.0, lb = 0.0, lc = 0.0;
+    rbuild::P2 pa{0, 0}, pb{0, 0};
+    for (int pass = 0; pass < 2; pass++) {
+        for (int k = 0; k < t.wa * t.wb; k++) {
+            if (!rbuild::poly_meets_hex(sq, 4, rhex_centre(t, k), stol, a.ht)) continue;
+            const uint32_t e = a.entries[t.off + (uint32_t)k];
+            if (!e) continue;
+            const HashEntry he = a.table[e - 1];
+            for (uint32_t c = he.first; c < he.first + he.count; c++) {
+                if (a.meta[c] & 1u) continue;
+                const pip::Box bx = a.store.geom_bbox[c];
+                if (bx.maxx < bx0 || bx.minx > bx1 || bx.maxy < by0 || bx.miny > by1) continue;
+                for (uint32_t p = a.store.geom_part[c]; p < a.store.geom_part[c + 1]; p++)
+                    for (uint32_t r = a.store.part_ring[p]; r < a.store.part_ring[p + 1]; r++)
+                        for (uint32_t v = a.store.ring_start[r] + 1; v < a.store.ring_start[r + 1]; v++) {
+                            const pip::Vec2 s0 = a.store.verts[v - 1], s1 = a.store.verts[v];
+                            double ax = (s0.x - lonR0) / wR, ay = (s0.y - latR0) / hR;
+                            double qx = (s1.x - lonR0) / wR, qy = (s1.y - latR0) / hR;
+                            if (!rbuild::clip_seg(ax, ay, qx, qy, -exu, -eyv, 1.0 + exu, 1.0 + eyv)) continue;
+                            if (pass == 0) {
+                                const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
+                                if (l2 > best) {
+                                    best = l2;
+                                    pa = rbuild::P2{ax, ay};
+                                    pb = rbuild::P2{qx, qy};
+                                }
+                            } else {
+                                dev_max = rbuild::dmax(dev_max, fabs(la * ax + lb * ay + lc));
+                                dev_max = rbuild::dmax(dev_max, fabs(la * qx + lb * qy + lc));
+                            }
+                        }
+            }
+        }
+        if (pass == 0) {
+            if (!(best > 1e-6)) return false;
+            const double l = sqrt(best);
+            la = -(pb.y - pa.y) / l;
+            lb = (pb.x - pa.x) / l;
+            lc = -(la * 0.5 * (pa.x + pb.x) + lb * 0.5 * (pa.y + pb.y));
+        }
+    }
+    const rbuild::P2 sqb[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
+    for (int mk = 0; mk < 4; mk++) {
+        const double margin = rbuild::line_margin(mk);
+        if (dev_max > margin - 2.0 * tiles::kLineSlack) continue;
+        out.a = (float)(la / margin);
+        out.b = (float)(lb / margin);
+        out.c = (float)(lc / margin);
+        const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - tiles::kLineSlack / margin;
+        rbuild::P2 hp[8], hn[8];
+        const int np = rbuild::clip_half(sqb, 4, A, B, Cf - m, hp), nn = rbuild::clip_half(sqb, 4, -A, -B, -Cf - m, hn);
+        const uint16_t cp = np >= 3 ? rclassify_poly(a, t, si, sj, hp, np, sq, stol) : (uint16_t)0;
+        if (cp == tiles::kMixed) continue;
+        const uint16_t cn = nn >= 3 ? rclassify_poly(a, t, si, sj, hn, nn, sq, stol) : (uint16_t)0;
+        if (cn == tiles::kMixed) continue;
+        out.pos = cp;
+        out.neg = cn;
+        out.a = (float)((double)out.a / a.C);
+        out.b = (float)((double)out.b / a.C);
+        return true;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(256) k_raster_line(RBuildArgs a) {
+    const int64_t SS = (int64_t)a.S * a.S;
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < a.n_mixed; m += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = a.mixed[m];
+        const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
+        RTile t;
+        tiles::LineRec lr{0, 0, 0, 0, 0};
+        bool ok = false;
+        if (a.lines && rtile_of(a, r, t)) {
+            rbuild::P2 sq[4];
+            const double stol = rsub_quad(a, t, si, sj, sq);
+            ok = rtry_line(a, t, si, sj, sq, stol, lr);
+        }
+        a.kind[m] = ok ? 1 : 0;
+        a.line[m] = ok ? lr : tiles::LineRec{0, 0, 0, 0, 0};
+    }
+}
+
+__global__ void __launch_bounds__(256) k_raster_cells(RBuildArgs a) {
+    const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
+    const int64_t total = a.n_cell_sb * CC;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = w / CC;
+        const int cc = (int)(w - m * CC), cj = cc / a.C, ci = cc - cj * a.C;
+        const int64_t g = a.cell_sb[m];
+        const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
+        RTile t;
+        uint16_t code = tiles::kMixed;
+        if (rtile_of(a, r, t)) {
+            rbuild::P2 sq[4];
+            const double stol = rsub_quad(a, t, si, sj, sq);
+            const int i0 = si * a.C + ci, j0 = sj * a.C + cj;
+            const rbuild::P2 qc[4] = {rimage(a, t, i0, j0), rimage(a, t, i0 + 1, j0), rimage(a, t, i0 + 1, j0 + 1),
+                                      rimage(a, t, i0, j0 + 1)};
+            code = rclassify_rect(a, t, i0, j0, i0 + 1, j0 + 1, qc, sq, stol);
+        }
+        a.cells[w] = code;
+    }
+}
+
 // ---- st_intersects_aggregate over the chip join of two chip tables ----------------------------
 // ST_IntersectsAggregate.update (expressions/geometry/ST_IntersectsAggregate.scala:28-39) folds
 // `left.is_core || right.is_core || left.wkb intersects right.wkb` with OR over the rows of a
@@ -1648,6 +1977,7 @@ struct Options {
     int raster_cell = 16;     // point raster: leaf cells per sub-block side (a power of two)
     int raster_quad = 1;      // point raster: LDS quad level
     int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
+    int raster_build = 1;     // point raster classification: 1 on the GPU (k_raster_*), 0 on host threads
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
     int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
@@ -1817,6 +2147,10 @@ struct mosaic_chips {
     DevBuf rsub, rmid, rblocks, rquad;  // rmid: per-tile leaf block bases
     int64_t raster_stats[6] = {0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
                                                    // line sub-blocks
+    // build cost (ms): chip table core (hash, geometry, chip rasters), tile directory, point-raster
+    // classification (GPU or host), point-raster assembly; FNV-1a digest of the point raster
+    double build_ms[4] = {0, 0, 0, 0};
+    uint64_t raster_digest = 0;
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
                           &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &bng_cells, &bng_leaf})
@@ -1960,6 +2294,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.raster_adaptive = v ? 1 : 0;
     } else if (k == "raster_lines") {
         o.raster_lines = v ? 1 : 0;
+    } else if (k == "raster_build") {
+        o.raster_build = v ? 1 : 0;
     } else if (k == "host_chunk") {
         if (v < 0) return fail(MOSAIC_E_ARG, "host_chunk must be >= 0");
         o.host_chunk = v;
@@ -2510,9 +2846,114 @@ int mosaic_chip_table_create_arrow(mosaic_ctx* ctx, int grid, int res, int64_t n
                              polygon_key, n_polygons, out);
 }
 
+struct TmpBuf : DevBuf {  // scratch released on every return path
+    ~TmpBuf() { release(); }
+};
+
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Phase 1 of tiles::Builder::build_raster on the GPU (k_raster_sub, k_raster_line, k_raster_cells)
+// over the chip table already on the device; the host then assembles the raster from `rc` exactly
+// as after classify_raster_host, so both builds give the same bytes (raster_digest).
+static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles::Builder& tb,
+                               tiles::Builder::RasterClass& rc) {
+    const size_t n_recs = tb.recs.size(), SS = (size_t)tb.S * tb.S, CC = (size_t)tb.C * tb.C;
+    const int64_t n_sub = (int64_t)(n_recs * SS);
+    if (tb.tile_of_rec.size() != n_recs || tb.rec_dev.size() != n_recs || !ch->tile_rec.p || !ch->tile_ent.p)
+        return fail(MOSAIC_E_ARG, "raster build: tile directory not on the device");
+    TmpBuf d_tor, d_dev, d_code, d_list, d_kind, d_line, d_cells;
+    int e;
+    if ((e = d_tor.reserve(std::max<size_t>(n_recs * 4, 16))) || (e = d_dev.reserve(std::max<size_t>(n_recs * 8, 16))) ||
+        (e = d_code.reserve(std::max<size_t>((size_t)n_sub * 2, 16))))
+        return e;
+    HIP_TRY(hipMemcpyAsync(d_tor.p, tb.tile_of_rec.data(), n_recs * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_dev.p, tb.rec_dev.data(), n_recs * 8, hipMemcpyHostToDevice, c->stream));
+    RBuildArgs a{};
+    a.recs = (const tiles::TileRec*)ch->tile_rec.p;
+    a.tile_of_rec = (const int32_t*)d_tor.p;
+    a.rec_dev = (const double*)d_dev.p;
+    a.entries = (const uint32_t*)ch->tile_ent.p;
+    a.n_recs = (int32_t)n_recs;
+    a.tnx = tb.grid.nx;
+    a.gx0 = tb.grid.x0;
+    a.gy0 = tb.grid.y0;
+    a.tw = 1.0 / tb.grid.sx;
+    a.th = 1.0 / tb.grid.sy;
+    a.S = tb.S;
+    a.C = tb.C;
+    a.N = tb.S * tb.C;
+    a.res = tb.res_;
+    a.lines = tb.lines ? 1 : 0;
+    a.table = (const HashEntry*)ch->table.p;
+    a.meta = (const uint32_t*)ch->meta.p;
+    a.store = ch->store.view();
+    a.ht = tiles::Builder::hex_table_values();
+    a.code = (uint16_t*)d_code.p;
+    auto grid_of = [](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1 << 22))); };
+    rc.code.resize((size_t)n_sub);
+    if (n_sub) {
+        hipLaunchKernelGGL(k_raster_sub, grid_of(n_sub), dim3(256), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(rc.code.data(), d_code.p, (size_t)n_sub * 2, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    // mixed sub-blocks in record, then scan order (the order assemble_raster consumes them)
+    std::vector<uint32_t> list;
+    for (int64_t g = 0; g < n_sub; g++)
+        if (rc.code[(size_t)g] == tiles::kMixed) list.push_back((uint32_t)g);
+    const int64_t n_mixed = (int64_t)list.size();
+    rc.kind.assign((size_t)n_mixed, 0);
+    rc.line.assign((size_t)n_mixed, tiles::LineRec{0, 0, 0, 0, 0});
+    rc.cell_at.assign((size_t)n_mixed, 0);
+    rc.cells.clear();
+    if (!n_mixed) return MOSAIC_OK;
+    if ((e = d_list.reserve(list.size() * 4)) || (e = d_kind.reserve(list.size())) ||
+        (e = d_line.reserve(list.size() * sizeof(tiles::LineRec))))
+        return e;
+    HIP_TRY(hipMemcpyAsync(d_list.p, list.data(), list.size() * 4, hipMemcpyHostToDevice, c->stream));
+    a.mixed = (const uint32_t*)d_list.p;
+    a.n_mixed = n_mixed;
+    a.kind = (uint8_t*)d_kind.p;
+    a.line = (tiles::LineRec*)d_line.p;
+    hipLaunchKernelGGL(k_raster_line, grid_of(n_mixed), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(rc.kind.data(), d_kind.p, list.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(rc.line.data(), d_line.p, list.size() * sizeof(tiles::LineRec), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // the other mixed sub-blocks: C x C leaf cells each
+    std::vector<uint32_t> cell_sb;
+    for (int64_t m = 0; m < n_mixed; m++)
+        if (!rc.kind[(size_t)m]) {
+            rc.cell_at[(size_t)m] = (uint32_t)cell_sb.size();
+            cell_sb.push_back(list[(size_t)m]);
+        }
+    if (cell_sb.empty()) return MOSAIC_OK;
+    const int64_t n_cells = (int64_t)(cell_sb.size() * CC);
+    if ((e = d_cells.reserve((size_t)n_cells * 2))) return e;
+    HIP_TRY(hipMemcpyAsync(d_list.p, cell_sb.data(), cell_sb.size() * 4, hipMemcpyHostToDevice, c->stream));
+    a.cell_sb = (const uint32_t*)d_list.p;
+    a.n_cell_sb = (int64_t)cell_sb.size();
+    a.cells = (uint16_t*)d_cells.p;
+    hipLaunchKernelGGL(k_raster_cells, grid_of(n_cells), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    rc.cells.resize((size_t)n_cells);
+    HIP_TRY(hipMemcpyAsync(rc.cells.data(), d_cells.p, (size_t)n_cells * 2, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MOSAIC_OK;
+}
+
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    for (size_t i = 0; i < n; i++) h = (h ^ ((const uint8_t*)p)[i]) * 1099511628211ull;
+    return h;
+}
+
 static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, const uint8_t* is_core,
                              const int64_t* index_id, const void* wkb_off, bool off32, const uint8_t* wkb,
                              const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out) {
+    const auto t_begin = std::chrono::steady_clock::now();
     // Arrow binary (int32 offsets) or large_binary (int64)
     auto wkb_offsets = [&](int64_t i) -> int64_t {
         return off32 ? (int64_t)((const int32_t*)wkb_off)[i] : ((const int64_t*)wkb_off)[i];
@@ -2748,7 +3189,11 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             return -1;
         };
         tiles::Builder tb;
-        if (tb.build(res, cell_ids, slot_of)) {
+        ch->build_ms[0] = ms_since(t_begin);
+        auto t_dir = std::chrono::steady_clock::now();
+        const bool dir_ok = tb.build(res, cell_ids, slot_of);
+        ch->build_ms[1] = ms_since(t_dir);
+        if (dir_ok) {
             size_t b0 = tb.tile_idx.size() * 4, b1 = tb.recs.size() * sizeof(tiles::TileRec), b2 = tb.entries.size() * 4;
             if ((rc = ch->tile_idx.reserve(b0)) || (rc = ch->tile_rec.reserve(b1)) || (rc = ch->tile_ent.reserve(b2))) {
                 ch->release_all();
@@ -2790,7 +3235,31 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 if (tbytes <= avail / 3) avail -= tbytes;
                 tb.quad_max = c->raster_quad > 1 ? c->raster_quad : (int)std::min<size_t>(tiles::kQuadLimit, avail / 2);
                 tb.lines = c->raster_lines != 0;
-                if (tb.build_raster(src, c->raster_sub, c->raster_cell, threads)) {
+                bool raster_built = false;
+                auto t_cls = std::chrono::steady_clock::now();
+                if (tb.raster_setup(src, c->raster_sub, c->raster_cell)) {
+                    tiles::Builder::RasterClass cls;
+                    if (c->raster_build) {
+                        if ((rc = raster_classify_gpu(c, ch, tb, cls))) {
+                            ch->release_all();
+                            delete ch;
+                            return rc;
+                        }
+                    } else {
+                        tb.classify_raster_host(src, threads, cls);
+                    }
+                    ch->build_ms[2] = ms_since(t_cls);
+                    auto t_asm = std::chrono::steady_clock::now();
+                    raster_built = tb.assemble_raster(cls);
+                    ch->build_ms[3] = ms_since(t_asm);
+                }
+                if (raster_built) {
+                    uint64_t h = 1469598103934665603ull;
+                    h = fnv1a(h, tb.sub.data(), tb.sub.size() * 2);
+                    h = fnv1a(h, tb.blocks.data(), tb.blocks.size() * 2);
+                    h = fnv1a(h, tb.tile_base.data(), tb.tile_base.size() * 4);
+                    h = fnv1a(h, tb.quad.data(), tb.quad.size() * 2);
+                    ch->raster_digest = h;
                     size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
                     if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
                         ch->release_all();
@@ -2918,6 +3387,13 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
     o[2] = ch->praster.quad ? ch->praster.qshift : 0;
     o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes) : 0;
     o[4] = ch->stream_ok ? 1 : 0;
+    return MOSAIC_OK;
+}
+
+int mosaic_chip_table_build_info(const mosaic_chips* ch, double* ms4, uint64_t* digest) {
+    if (!ch || !ms4 || !digest) return fail(MOSAIC_E_ARG, "null argument");
+    for (int k = 0; k < 4; k++) ms4[k] = ch->build_ms[k];
+    *digest = ch->raster_ok ? ch->raster_digest : 0;
     return MOSAIC_OK;
 }
 

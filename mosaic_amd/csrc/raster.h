@@ -74,7 +74,7 @@ MOSAIC_HD bool cell_contains(const CellRec& rec, const pip::Edge* edges, double 
 
 // ---- host-side construction -------------------------------------------------------------------
 // Closed-segment vs closed-rectangle test (Liang-Barsky), double precision.
-inline bool seg_meets_rect(double ax, double ay, double bx, double by, double x0, double y0, double x1, double y1) {
+MOSAIC_HD bool seg_meets_rect(double ax, double ay, double bx, double by, double x0, double y0, double x1, double y1) {
     double t0 = 0.0, t1 = 1.0;
     const double dx = bx - ax, dy = by - ay;
     auto clip = [&](double p, double q) -> bool {  // constraint p * t <= q

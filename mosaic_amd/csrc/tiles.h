@@ -39,6 +39,7 @@
 
 #include "h3_device.h"
 #include "raster.h"
+#include "raster_build.h"
 
 #include <algorithm>
 #include <functional>
@@ -232,6 +233,23 @@ struct Builder {
         int32_t n_polygons;
     };
     bool build_raster(const ChipSource& src, int S_, int C_, int threads);
+    // build_raster in two phases, so the classification can run on the GPU (k_raster_* in
+    // mosaic_hip.hip) and the assembly on the host:
+    //   phase 1: every sub-block's code (kMixed for mixed ones); per mixed sub-block (in record,
+    //            then scan order) a line record (kind 1) or its C x C cell codes (kind 0);
+    //   phase 2: sub-block entries, per-tile line records and leaf blocks, quad level.
+    struct RasterClass {
+        std::vector<uint16_t> code;     // records x S x S (scan order sj S + si)
+        std::vector<uint8_t> kind;      // per mixed sub-block
+        std::vector<LineRec> line;      // per mixed sub-block (kind 1)
+        std::vector<uint32_t> cell_at;  // per mixed sub-block (kind 0): its block of C x C codes in cells
+        std::vector<uint16_t> cells;
+    };
+    std::vector<int> tile_of_rec;  // record -> tile (raster_setup)
+    bool raster_setup(const ChipSource& src, int S_, int C_);
+    void classify_raster_host(const ChipSource& src, int threads, RasterClass& rc);
+    bool assemble_raster(const RasterClass& rc);
+    static rbuild::HexTable hex_table_values();
 
     // cells: distinct chip cells; slot_of(cell) -> chip hash slot or -1.  Defined for the host
     // compiler only (tiles_build.cpp); false (with `why`) when the directory is not built.

@@ -18,6 +18,7 @@
 // Reference semantics followed: the chip join = H3 cell equality (H3IndexSystem.scala:140-142) +
 // is_core || st_contains (QuickstartNotebook.py:205-219, ST_Contains.scala:34-42).
 #include "tiles.h"
+#include "raster_build.h"
 
 #include <atomic>
 #include <cstring>
@@ -32,126 +33,15 @@ bool Builder::build(int res, const std::vector<int64_t>& cells, const std::funct
 
 namespace {
 
-const double kS60 = 0.86602540378443864676;
-
-struct P2 {
-    double x, y;
-};
-
-// Convex polygon q[n] (counter-clockwise) meets the Voronoi hexagon of lattice centre c within
-// tolerance t (separating axes: the hexagon's 3 edge normals and the polygon's n).
-bool poly_meets_hex(const P2* q, int n, P2 c, double t) {
-    // hexagon: vertices at 30 + 60k degrees, radius 1/sqrt(3); apothem 1/2 along 0, 60, 120 degrees
-    static const double ax[3][2] = {{1.0, 0.0}, {0.5, kS60}, {-0.5, kS60}};
-    for (int k = 0; k < 3; k++) {
-        double hc = c.x * ax[k][0] + c.y * ax[k][1];
-        double lo = INFINITY, hi = -INFINITY;
-        for (int v = 0; v < n; v++) {
-            double d = q[v].x * ax[k][0] + q[v].y * ax[k][1];
-            lo = std::min(lo, d);
-            hi = std::max(hi, d);
-        }
-        if (lo > hc + 0.5 + t || hi < hc - 0.5 - t) return false;
-    }
-    const double r = 0.57735026918962576451;
-    for (int e = 0; e < n; e++) {
-        P2 a = q[e], b = q[(e + 1) % n];
-        double nx = -(b.y - a.y), ny = b.x - a.x;
-        double len = sqrt(nx * nx + ny * ny);
-        if (!(len > 0)) continue;
-        nx /= len;
-        ny /= len;
-        double lo = INFINITY, hi = -INFINITY;
-        for (int v = 0; v < n; v++) {
-            double d = q[v].x * nx + q[v].y * ny;
-            lo = std::min(lo, d);
-            hi = std::max(hi, d);
-        }
-        double hc = c.x * nx + c.y * ny, ext = 0.0;
-        for (int k = 0; k < 6; k++) {
-            double ang = (30.0 + 60.0 * k) * 0.017453292519943295;
-            ext = std::max(ext, fabs(r * (cos(ang) * nx + sin(ang) * ny)));
-        }
-        if (lo > hc + ext + t || hi < hc - ext - t) return false;
-    }
-    return true;
-}
-
-bool quad_meets_hex(const P2* q, P2 c, double t) { return poly_meets_hex(q, 4, c, t); }
+using rbuild::clip_half;
+using rbuild::clip_seg;
+using rbuild::kS60;
+using rbuild::P2;
+using rbuild::seg_meets_poly;
 
 struct Seg {
     double ax, ay, bx, by;
 };
-
-double cross(P2 o, P2 a, P2 b) { return (a.x - o.x) * (b.y - o.y) - (a.y - o.y) * (b.x - o.x); }
-
-double seg_point_dist(P2 a, P2 b, P2 p) {
-    const double dx = b.x - a.x, dy = b.y - a.y, l2 = dx * dx + dy * dy;
-    double t = l2 > 0 ? ((p.x - a.x) * dx + (p.y - a.y) * dy) / l2 : 0.0;
-    t = t < 0 ? 0 : (t > 1 ? 1 : t);
-    const double ex = a.x + t * dx - p.x, ey = a.y + t * dy - p.y;
-    return sqrt(ex * ex + ey * ey);
-}
-
-// Segment (a, b) comes within eps of the convex polygon q[n] (counter-clockwise).
-bool seg_meets_poly(P2 a, P2 b, const P2* q, int n, double eps) {
-    auto inside = [&](P2 p) {
-        for (int e = 0; e < n; e++) {
-            P2 u = q[e], v = q[(e + 1) % n];
-            const double len = sqrt((v.x - u.x) * (v.x - u.x) + (v.y - u.y) * (v.y - u.y));
-            if (len > 0 && cross(u, v, p) / len < -eps) return false;
-        }
-        return true;
-    };
-    if (inside(a) || inside(b)) return true;
-    for (int e = 0; e < n; e++) {
-        P2 u = q[e], v = q[(e + 1) % n];
-        const double d1 = cross(a, b, u), d2 = cross(a, b, v), d3 = cross(u, v, a), d4 = cross(u, v, b);
-        if (((d1 <= 0 && d2 >= 0) || (d1 >= 0 && d2 <= 0)) && ((d3 <= 0 && d4 >= 0) || (d3 >= 0 && d4 <= 0))) return true;
-        if (seg_point_dist(a, b, u) <= eps || seg_point_dist(a, b, v) <= eps || seg_point_dist(u, v, a) <= eps ||
-            seg_point_dist(u, v, b) <= eps)
-            return true;
-    }
-    return false;
-}
-
-// Clip the segment to [x0, x1] x [y0, y1] (Liang-Barsky); false when it misses the box.
-bool clip_seg(double& ax, double& ay, double& bx, double& by, double x0, double y0, double x1, double y1) {
-    double t0 = 0.0, t1 = 1.0;
-    const double dx = bx - ax, dy = by - ay;
-    const double p[4] = {-dx, dx, -dy, dy}, qv[4] = {ax - x0, x1 - ax, ay - y0, y1 - ay};
-    for (int k = 0; k < 4; k++) {
-        if (p[k] == 0) {
-            if (qv[k] < 0) return false;
-        } else {
-            const double t = qv[k] / p[k];
-            if (p[k] < 0) t0 = std::max(t0, t);
-            else t1 = std::min(t1, t);
-        }
-    }
-    if (t0 > t1) return false;
-    const double nax = ax + t0 * dx, nay = ay + t0 * dy;
-    bx = ax + t1 * dx;
-    by = ay + t1 * dy;
-    ax = nax;
-    ay = nay;
-    return true;
-}
-
-// Convex polygon q[n] clipped to the half-plane a x + b y + c >= 0 (Sutherland-Hodgman)
-int clip_half(const P2* q, int n, double a, double b, double c, P2* out) {
-    int m = 0;
-    for (int e = 0; e < n; e++) {
-        P2 u = q[e], v = q[(e + 1) % n];
-        const double su = a * u.x + b * u.y + c, sv = a * v.x + b * v.y + c;
-        if (su >= 0) out[m++] = u;
-        if ((su >= 0) != (sv >= 0)) {
-            const double t = su / (su - sv);
-            out[m++] = P2{u.x + t * (v.x - u.x), u.y + t * (v.y - u.y)};
-        }
-    }
-    return m;
-}
 
 struct Rect {
     double x0, y0, x1, y1;
@@ -181,9 +71,16 @@ struct Hex {
     std::vector<pip::Box> bbox;
 };
 
+const rbuild::HexTable& hex_table() {
+    static const rbuild::HexTable t = rbuild::hex_table();
+    return t;
+}
+
 }  // namespace
 
-bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
+rbuild::HexTable Builder::hex_table_values() { return hex_table(); }
+
+bool Builder::raster_setup(const ChipSource& src, int S_, int C_) {
     S = S_;
     C = C_;
     sub.clear();
@@ -197,19 +94,33 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     while ((1 << sshift) < S) sshift++;
     cshift = 0;
     while ((1 << cshift) < C) cshift++;
-    const int nx = grid.nx, ny = grid.ny, N = S * C;
-    const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
-    if (NX * NY > ((int64_t)1 << 28)) return false;
-    sub.assign((size_t)(NX * NY), (uint16_t)0);
-    tile_base.assign((size_t)nx * ny, 0u);
-    const double tw = 1.0 / grid.sx, th = 1.0 / grid.sy;
-    // per-tile leaf blocks (tile-local numbering in the sub entries), merged afterwards
-    std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
-    std::vector<std::vector<LineRec>> tile_lines(recs.size());
-    std::vector<int> tile_of_rec(recs.size(), -1);
-    for (int64_t t = 0; t < (int64_t)nx * ny; t++)
+    if ((int64_t)grid.nx * S * grid.ny * S > ((int64_t)1 << 28)) return false;
+    tile_of_rec.assign(recs.size(), -1);
+    for (int64_t t = 0; t < (int64_t)grid.nx * grid.ny; t++)
         if (tile_idx[(size_t)t] >= 2) tile_of_rec[tile_idx[(size_t)t] - 2] = (int)t;
-    std::atomic<int64_t> next(0), pure(0), mixed(0), cmixed(0), nline(0);
+    return true;
+}
+
+bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
+    if (!raster_setup(src, S_, C_)) return false;
+    RasterClass rc;
+    classify_raster_host(src, threads, rc);
+    return assemble_raster(rc);
+}
+
+// Phase 1 on the host: every sub-block's code (kMixed for mixed ones), and for the mixed ones a
+// line record or their C x C cell codes.
+void Builder::classify_raster_host(const ChipSource& src, int threads, RasterClass& rc) {
+    const int nx = grid.nx, N = S * C;
+    const double tw = 1.0 / grid.sx, th = 1.0 / grid.sy;
+    const rbuild::HexTable& ht = hex_table();
+    const size_t SS = (size_t)S * S;
+    rc.code.assign(recs.size() * SS, (uint16_t)0);
+    // per record: its mixed sub-blocks' results (concatenated in record order afterwards)
+    std::vector<std::vector<uint8_t>> r_kind(recs.size());
+    std::vector<std::vector<LineRec>> r_line(recs.size());
+    std::vector<std::vector<uint16_t>> r_cells(recs.size());
+    std::atomic<int64_t> next(0);
 
     auto work = [&]() {
         std::vector<P2> lat;  // (S + 1)^2 sub-block corner images
@@ -273,7 +184,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                 double tol = 4.0 * dev * frac * frac + 1e-7;
                 cout.clear();
                 for (int k : cin)
-                    if (quad_meets_hex(q, hexes[(size_t)k].c, tol)) cout.push_back(k);
+                    if (rbuild::poly_meets_hex(q, 4, hexes[(size_t)k].c, tol, ht)) cout.push_back(k);
                 Rect r;
                 double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(lon0) + 1.0);
                 double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(lat0) + 1.0);
@@ -337,7 +248,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                 bool first = true, mixed_ans = false, any = false;
                 for (int k : cin) {
                     const Hex& h = hexes[(size_t)k];
-                    if (!poly_meets_hex(img, n, h.c, tol)) continue;
+                    if (!rbuild::poly_meets_hex(img, n, h.c, tol, ht)) continue;
                     any = true;
                     ah = h.core;
                     for (size_t b = 0; b < h.border.size(); b++) {
@@ -399,7 +310,8 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
                 for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * p.x + b * p.y + c));
                 const P2 sq[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
                 // the narrowest band (fewest rows to the mixed kernel) whose two sides certify
-                for (double margin : {1.0 / 2048, 1.0 / 512, 1.0 / 128, 1.0 / 32}) {
+                for (int mk = 0; mk < 4; mk++) {
+                    const double margin = rbuild::line_margin(mk);
                     if (dev_max > margin - 2.0 * kLineSlack) continue;
                     out.a = (float)(a / margin);
                     out.b = (float)(b / margin);
@@ -425,55 +337,36 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
             };
             std::vector<int> all((size_t)wa * wb);
             for (size_t k = 0; k < all.size(); k++) all[k] = (int)k;
-            std::vector<uint16_t>& outb = tile_blocks[(size_t)ri];
+            uint16_t* rcode = rc.code.data() + (size_t)ri * SS;
             std::vector<uint16_t> cellc((size_t)C * C);
             for (int sj = 0; sj < S; sj++)
                 for (int si = 0; si < S; si++) {
                     const P2 qs[4] = {lat[(size_t)sj * (S + 1) + si], lat[(size_t)sj * (S + 1) + si + 1],
                                       lat[(size_t)(sj + 1) * (S + 1) + si + 1], lat[(size_t)(sj + 1) * (S + 1) + si]};
                     uint16_t code = classify(si * C, sj * C, (si + 1) * C, (sj + 1) * C, qs, all, cand);
-                    uint16_t entry;
-                    if (code != kMixed) {
-                        entry = code;
-                        pure++;
-                    } else {
-                        mixed++;
-                        LineRec lr;
-                        if (lines && try_line(si, sj, cand, lr)) {
-                            // tile-local line record number (< S * S <= kLineBit)
-                            entry = (uint16_t)(kSubBlock | kLineBit | (uint32_t)tile_lines[(size_t)ri].size());
-                            tile_lines[(size_t)ri].push_back(lr);
-                            nline++;
-                            sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
-                            continue;
-                        }
-                        for (int cj = 0; cj <= C; cj++)
-                            for (int ci = 0; ci <= C; ci++)
-                                clat[(size_t)cj * (C + 1) + ci] =
-                                    (ci % C == 0 && cj % C == 0)
-                                        ? lat[(size_t)(sj + cj / C) * (S + 1) + si + ci / C]
-                                        : image(si * C + ci, sj * C + cj);
-                        bool same = true;
-                        for (int cj = 0; cj < C; cj++)
-                            for (int ci = 0; ci < C; ci++) {
-                                int i0 = si * C + ci, j0 = sj * C + cj;
-                                const P2 qc[4] = {clat[(size_t)cj * (C + 1) + ci], clat[(size_t)cj * (C + 1) + ci + 1],
-                                                  clat[(size_t)(cj + 1) * (C + 1) + ci + 1],
-                                                  clat[(size_t)(cj + 1) * (C + 1) + ci]};
-                                uint16_t cc = classify(i0, j0, i0 + 1, j0 + 1, qc, cand, cand2);
-                                cellc[(size_t)cj * C + ci] = cc;
-                                if (cc == kMixed) cmixed++;
-                                same = same && cc == cellc[0];
-                            }
-                        if (same && cellc[0] != kMixed) {
-                            entry = cellc[0];
-                        } else {
-                            // tile-local leaf block number (< S * S <= kLineBit)
-                            entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / ((size_t)C * C)));
-                            outb.insert(outb.end(), cellc.begin(), cellc.end());
-                        }
+                    rcode[(size_t)sj * S + si] = code;
+                    if (code != kMixed) continue;
+                    LineRec lr;
+                    if (lines && try_line(si, sj, cand, lr)) {
+                        r_kind[(size_t)ri].push_back(1);
+                        r_line[(size_t)ri].push_back(lr);
+                        continue;
                     }
-                    sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
+                    for (int cj = 0; cj <= C; cj++)
+                        for (int ci = 0; ci <= C; ci++)
+                            clat[(size_t)cj * (C + 1) + ci] =
+                                (ci % C == 0 && cj % C == 0) ? lat[(size_t)(sj + cj / C) * (S + 1) + si + ci / C]
+                                                             : image(si * C + ci, sj * C + cj);
+                    for (int cj = 0; cj < C; cj++)
+                        for (int ci = 0; ci < C; ci++) {
+                            int i0 = si * C + ci, j0 = sj * C + cj;
+                            const P2 qc[4] = {clat[(size_t)cj * (C + 1) + ci], clat[(size_t)cj * (C + 1) + ci + 1],
+                                              clat[(size_t)(cj + 1) * (C + 1) + ci + 1], clat[(size_t)(cj + 1) * (C + 1) + ci]};
+                            cellc[(size_t)cj * C + ci] = classify(i0, j0, i0 + 1, j0 + 1, qc, cand, cand2);
+                        }
+                    r_kind[(size_t)ri].push_back(0);
+                    r_line[(size_t)ri].push_back(LineRec{0, 0, 0, 0, 0});
+                    r_cells[(size_t)ri].insert(r_cells[(size_t)ri].end(), cellc.begin(), cellc.end());
                 }
         }
     };
@@ -482,6 +375,79 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     for (int k = 1; k < nt; k++) pool.emplace_back(work);
     work();
     for (auto& th_ : pool) th_.join();
+    rc.kind.clear();
+    rc.line.clear();
+    rc.cell_at.clear();
+    rc.cells.clear();
+    for (size_t r = 0; r < recs.size(); r++) {
+        size_t c0 = 0;
+        for (size_t k = 0; k < r_kind[r].size(); k++) {
+            rc.kind.push_back(r_kind[r][k]);
+            rc.line.push_back(r_line[r][k]);
+            if (r_kind[r][k]) {
+                rc.cell_at.push_back(0);
+            } else {
+                rc.cell_at.push_back((uint32_t)(rc.cells.size() / ((size_t)C * C)));
+                rc.cells.insert(rc.cells.end(), r_cells[r].begin() + (ptrdiff_t)c0, r_cells[r].begin() + (ptrdiff_t)(c0 + (size_t)C * C));
+                c0 += (size_t)C * C;
+            }
+        }
+    }
+}
+
+// Phase 2 (host, either classification): sub-block entries, per-tile line records and leaf blocks,
+// the quad level with its compact copies.
+bool Builder::assemble_raster(const RasterClass& rc) {
+    const int nx = grid.nx, ny = grid.ny;
+    const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
+    const size_t SS = (size_t)S * S, CC = (size_t)C * C;
+    sub.assign((size_t)(NX * NY), (uint16_t)0);
+    tile_base.assign((size_t)nx * ny, 0u);
+    std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
+    std::vector<std::vector<LineRec>> tile_lines(recs.size());
+    int64_t pure = 0, mixed = 0, cmixed = 0, nline = 0;
+    size_t mk = 0;  // next mixed sub-block
+    for (size_t ri = 0; ri < recs.size(); ri++) {
+        const int t = tile_of_rec[ri];
+        if (t < 0 || recs[ri].dims == 0) continue;
+        const int ti = t % nx, tj = t / nx;
+        const uint16_t* rcode = rc.code.data() + ri * SS;
+        std::vector<uint16_t>& outb = tile_blocks[ri];
+        for (int sj = 0; sj < S; sj++)
+            for (int si = 0; si < S; si++) {
+                const uint16_t code = rcode[(size_t)sj * S + si];
+                uint16_t entry;
+                if (code != kMixed) {
+                    entry = code;
+                    pure++;
+                } else {
+                    mixed++;
+                    if (mk >= rc.kind.size()) return false;
+                    if (rc.kind[mk]) {
+                        // tile-local line record number (< S * S <= kLineBit)
+                        entry = (uint16_t)(kSubBlock | kLineBit | (uint32_t)tile_lines[ri].size());
+                        tile_lines[ri].push_back(rc.line[mk]);
+                        nline++;
+                    } else {
+                        const uint16_t* cellc = rc.cells.data() + (size_t)rc.cell_at[mk] * CC;
+                        bool same = true;
+                        for (size_t q = 0; q < CC; q++) {
+                            if (cellc[q] == kMixed) cmixed++;
+                            same = same && cellc[q] == cellc[0];
+                        }
+                        if (same && cellc[0] != kMixed) {
+                            entry = cellc[0];
+                        } else {
+                            // tile-local leaf block number (< S * S <= kLineBit)
+                            entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / CC));
+                            outb.insert(outb.end(), cellc, cellc + CC);
+                        }
+                    }
+                    mk++;
+                }
+                sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
+            }
+    }
     // kFull tiles: every point takes the tile path; kSkip tiles: no pair (0, already)
     for (int64_t t = 0; t < (int64_t)nx * ny; t++) {
         if (tile_idx[(size_t)t] != kFull) continue;
@@ -502,7 +468,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
         sub.clear();
         return false;
     }
-    blocks.assign(std::max<size_t>(total, std::max<size_t>((size_t)C * C, 8)), kMixed);
+    blocks.assign(std::max<size_t>(total, std::max<size_t>(CC, 8)), kMixed);
     for (size_t r = 0; r < recs.size(); r++) {
         for (size_t n = 0; n < tile_lines[r].size(); n++)
             memcpy(blocks.data() + at[r] - 8 * (n + 1), &tile_lines[r][n], sizeof(LineRec));
@@ -522,10 +488,10 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
             const uint16_t e = sub[(size_t)(j * NX + i)];
             if (e != 0 && e != kMixed) edge_ok = false;
         }
-    n_sub_line = nline.load();
-    n_sub_pure = pure.load();
-    n_sub_mixed = mixed.load();
-    n_cell_mixed = cmixed.load();
+    n_sub_line = nline;
+    n_sub_pure = pure;
+    n_sub_mixed = mixed;
+    n_cell_mixed = cmixed;
     // quad level: the smallest power-of-two group of sub-blocks whose table fits quad_max entries
     qshift = 0;
     while (qshift < 16 && ((NX + (1 << qshift) - 1) >> qshift) * ((NY + (1 << qshift) - 1) >> qshift) > quad_max)

@@ -99,6 +99,16 @@ int main(int argc, char** argv) {
     auto t2 = std::chrono::steady_clock::now();
     printf("directory %.3f s, raster %.3f s (%d threads)\n", std::chrono::duration<double>(t1 - t0).count(),
            std::chrono::duration<double>(t2 - t1).count(), threads);
+    {
+        auto fnv = [](const void* p, size_t n) {
+            uint64_t h = 1469598103934665603ull;
+            for (size_t i = 0; i < n; i++) h = (h ^ ((const uint8_t*)p)[i]) * 1099511628211ull;
+            return (unsigned long long)h;
+        };
+        printf("hash sub %016llx blocks %016llx tile_base %016llx quad %016llx\n", fnv(tb.sub.data(), tb.sub.size() * 2),
+               fnv(tb.blocks.data(), tb.blocks.size() * 2), fnv(tb.tile_base.data(), tb.tile_base.size() * 4),
+               fnv(tb.quad.data(), tb.quad.size() * 2));
+    }
     const int64_t NX = (int64_t)tb.grid.nx * S, NY = (int64_t)tb.grid.ny * S;
     printf("grid %d x %d tiles, %lld x %lld sub-blocks, records %zu; sub pure %lld mixed %lld line %lld; "
            "blocks %zu elements; quad %d x %d shift %d\n",
