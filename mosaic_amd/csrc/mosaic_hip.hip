@@ -528,6 +528,10 @@ struct StreamArgs {
     const uint16_t* csub;     // compact sub-block copies (PointRaster::sub + nx * ny)
     const uint16_t* blocks;   // line records and leaf blocks
     uint32_t csub_bytes, blocks_bytes, tile_base_bytes;
+    // quad records (tiles::PointRaster::qrec_*), copied to LDS behind the quad level: 2 n_qrec mask
+    // words, then the n_qrec uint16 codes; n_qrec_words >= 2 (index 0 is always readable)
+    const uint32_t* qrec;
+    int32_t n_qrec, n_qrec_words, qrl;
 };
 static const uint32_t kNoLoad = 0x7ffffff0u;  // out-of-range buffer offset (every table is < 2 GiB)
 
@@ -542,6 +546,19 @@ __device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t byt
                                              (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// The LDS quad level's entry for fine cell (ixC, iyC), resolved through the quad's record when the
+// point's sub-quad is uniform with the record's code (tiles::raster_code with use_quad, branch-free)
+__device__ inline uint32_t quad_lookup(const StreamArgs& s, const uint16_t* quad, const uint32_t* qmask,
+                                       const uint16_t* qcode, uint32_t ixC, uint32_t iyC) {
+    const uint32_t q = quad[__umul24(iyC >> s.qsh, (uint32_t)s.qnx) + (ixC >> s.qsh)];
+    const uint32_t r = q & 0x7fffu;
+    const bool rec = q >= 0x8000u && r < (uint32_t)s.n_qrec;
+    const uint32_t b = (((iyC >> (s.cs + s.qrl)) & 7u) << 3) | ((ixC >> (s.cs + s.qrl)) & 7u);
+    const uint32_t w = qmask[rec ? 2u * r + (b >> 5) : 0u];
+    const uint32_t c = qcode[rec ? r : 0u];
+    return (rec && ((w >> (b & 31u)) & 1u)) ? c : q;
+}
+
 template <bool LDS_COUNTS, bool PAIRS, bool VEC>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream(JoinArgs a, StreamArgs s) {
     extern __shared__ unsigned int lds[];
@@ -551,7 +568,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     uint32_t* tb = stage + nwaves * s.stage_words;
     uint32_t* quadw = tb + (s.tb_lds ? s.n_tiles : 0);
     const uint16_t* quad = (const uint16_t*)quadw;
+    uint32_t* qmask = quadw + s.n_quad_words;
+    const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
     for (int k = threadIdx.x; k < s.n_quad_words; k += blockDim.x) quadw[k] = s.quad[k];
+    for (int k = threadIdx.x; k < s.n_qrec_words; k += blockDim.x) qmask[k] = s.qrec[k];
     if (s.tb_lds)
         for (int k = threadIdx.x; k < s.n_tiles; k += blockDim.x) tb[k] = s.tile_base[k];
     for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
@@ -609,7 +629,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             ixC[k] = (uint32_t)(int)gx[k];
             iyC[k] = (uint32_t)(int)gy[k];
             // (indices < 2^24: 24-bit multiplies)
-            qv[k] = quad[__umul24(iyC[k] >> s.qsh, (uint32_t)s.qnx) + (ixC[k] >> s.qsh)];
+            qv[k] = quad_lookup(s, quad, qmask, qcode, ixC[k], iyC[k]);
             ta[k] = __umul24(iyC[k] >> s.tsh, (uint32_t)s.tnx) + (ixC[k] >> s.tsh);
             tbv[k] = s.tb_lds ? tb[ta[k]] : 0u;
         }
@@ -736,7 +756,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     uint32_t* tb = stage + nwaves * s.stage_words;
     uint32_t* quadw = tb + s.n_tiles;
     const uint16_t* quad = (const uint16_t*)quadw;
+    uint32_t* qmask = quadw + s.n_quad_words;
+    const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
     for (int k = threadIdx.x; k < s.n_quad_words; k += blockDim.x) quadw[k] = s.quad[k];
+    for (int k = threadIdx.x; k < s.n_qrec_words; k += blockDim.x) qmask[k] = s.qrec[k];
     for (int k = threadIdx.x; k < s.n_tiles; k += blockDim.x) tb[k] = s.tile_base[k];
     for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
     __syncthreads();
@@ -764,7 +787,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             g.u[k] = (float)(gx - (double)(ixC & ~cm));
             g.v[k] = (float)(gy - (double)(iyC & ~cm));
             g.lf[k] = ((iyC & cm) << s.cs) | (ixC & cm);
-            const uint32_t q = quad[__umul24(iyC >> s.qsh, (uint32_t)s.qnx) + (ixC >> s.qsh)];
+            const uint32_t q = quad_lookup(s, quad, qmask, qcode, ixC, iyC);
             // dead rows answer 0, non-finite ones kPipeNonFinite (-> kMixed)
             g.qv[k] = !lv ? 0u : (__builtin_isfinite(x[k] + y[k]) ? q : kPipeNonFinite);
             g.tbv[k] = tb[__umul24(iyC >> s.tsh, (uint32_t)s.tnx) + (ixC >> s.tsh)];
@@ -1978,6 +2001,7 @@ struct Options {
     int raster_quad = 1;      // point raster: LDS quad level
     int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
     int raster_build = 1;     // point raster classification: 1 on the GPU (k_raster_*), 0 on host threads
+    int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
     int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
@@ -2144,7 +2168,7 @@ struct mosaic_chips {
     tiles::PointRaster praster{};
     bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
     StreamArgs stream{};
-    DevBuf rsub, rmid, rblocks, rquad;  // rmid: per-tile leaf block bases
+    DevBuf rsub, rmid, rblocks, rquad, rqrec;  // rmid: per-tile leaf block bases; rqrec: quad records
     int64_t raster_stats[6] = {0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
                                                    // line sub-blocks
     // build cost (ms): chip table core (hash, geometry, chip rasters), tile directory, point-raster
@@ -2153,7 +2177,7 @@ struct mosaic_chips {
     uint64_t raster_digest = 0;
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &bng_cells, &bng_leaf})
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf})
             b->release();
         store.release();
     }
@@ -2294,6 +2318,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.raster_adaptive = v ? 1 : 0;
     } else if (k == "raster_lines") {
         o.raster_lines = v ? 1 : 0;
+    } else if (k == "raster_quad_records") {
+        o.raster_quad_records = v ? 1 : 0;
     } else if (k == "raster_build") {
         o.raster_build = v ? 1 : 0;
     } else if (k == "host_chunk") {
@@ -3233,7 +3259,14 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                                (n_polygons <= kLdsCountsMax ? ((size_t)n_polygons + 64) * 4 : 0);
                 const size_t tbytes = tb.tile_idx.size() * 4;
                 if (tbytes <= avail / 3) avail -= tbytes;
-                tb.quad_max = c->raster_quad > 1 ? c->raster_quad : (int)std::min<size_t>(tiles::kQuadLimit, avail / 2);
+                // quad level in at most half of it, quad records in the rest (option raster_quad_records)
+                if (c->raster_quad_records && c->raster_quad == 1) {
+                    tb.quad_max = (int)std::min<size_t>(tiles::kQuadLimit, avail / 4);
+                    tb.quad_lds_bytes = avail;
+                } else {
+                    tb.quad_max = c->raster_quad > 1 ? c->raster_quad : (int)std::min<size_t>(tiles::kQuadLimit, avail / 2);
+                    tb.quad_lds_bytes = 0;
+                }
                 tb.lines = c->raster_lines != 0;
                 bool raster_built = false;
                 auto t_cls = std::chrono::steady_clock::now();
@@ -3259,6 +3292,8 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     h = fnv1a(h, tb.blocks.data(), tb.blocks.size() * 2);
                     h = fnv1a(h, tb.tile_base.data(), tb.tile_base.size() * 4);
                     h = fnv1a(h, tb.quad.data(), tb.quad.size() * 2);
+                    h = fnv1a(h, tb.qrec_mask.data(), tb.qrec_mask.size() * 4);
+                    h = fnv1a(h, tb.qrec_code.data(), tb.qrec_code.size() * 2);
                     ch->raster_digest = h;
                     size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
                     if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
@@ -3326,6 +3361,26 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         sa.csub_bytes = (uint32_t)csub_bytes;
                         sa.blocks_bytes = (uint32_t)blocks_bytes;
                         sa.tile_base_bytes = (uint32_t)rm;
+                        // quad records: mask words, then the codes (>= 2 words, so index 0 is readable)
+                        std::vector<uint32_t> qw(tb.qrec_mask);
+                        const size_t nrec = tb.qrec_code.size();
+                        qw.resize(2 * nrec + (nrec + 1) / 2, 0u);
+                        if (nrec) memcpy(qw.data() + 2 * nrec, tb.qrec_code.data(), nrec * 2);
+                        if (qw.size() < 2) qw.resize(2, 0u);
+                        if ((rc = ch->rqrec.reserve(qw.size() * 4))) {
+                            ch->release_all();
+                            delete ch;
+                            return rc;
+                        }
+                        HIP_TRY(hipMemcpy(ch->rqrec.p, qw.data(), qw.size() * 4, hipMemcpyHostToDevice));
+                        sa.qrec = (const uint32_t*)ch->rqrec.p;
+                        sa.n_qrec = (int32_t)nrec;
+                        sa.n_qrec_words = (int32_t)qw.size();
+                        sa.qrl = tb.qrec_shift;
+                        ch->praster.qrec_mask = nrec ? (const uint32_t*)ch->rqrec.p : nullptr;
+                        ch->praster.qrec_code = nrec ? (const uint16_t*)((const uint32_t*)ch->rqrec.p + 2 * nrec) : nullptr;
+                        ch->praster.n_qrec = (int32_t)nrec;
+                        ch->praster.qrec_shift = tb.qrec_shift;
                         ch->stream_ok = true;
                     }
                     ch->raster_stats[0] = tb.S;
@@ -3385,7 +3440,7 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
     o[0] = ch->raster_stats[5];
     o[1] = ch->praster.quad ? (int64_t)ch->praster.qnx * ch->praster.qny : 0;
     o[2] = ch->praster.quad ? ch->praster.qshift : 0;
-    o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes) : 0;
+    o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes + ch->rqrec.bytes) : 0;
     o[4] = ch->stream_ok ? 1 : 0;
     return MOSAIC_OK;
 }
@@ -3488,7 +3543,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
         StreamArgs sa = ch->stream;
         const int blk = c->stream_block;
         size_t shm_s = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blk / 64) * sa.stage_words * 4 +
-                       (size_t)sa.n_quad_words * 4;
+                       (size_t)sa.n_quad_words * 4 + (size_t)sa.n_qrec_words * 4;
         sa.tb_lds = shm_s + (size_t)sa.n_tiles * 4 <= kStreamLdsMax ? 1 : 0;
         if (sa.tb_lds) shm_s += (size_t)sa.n_tiles * 4;
         const bool stream = praster && ch->stream_ok && shm_s <= kStreamLdsMax;

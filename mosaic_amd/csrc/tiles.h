@@ -92,6 +92,14 @@ struct PointRaster {
     // sub[nx * ny + (r << 2 qshift) + local]); small enough (<= kQuadMax entries) to live in LDS
     const uint16_t* quad;       // nullptr: no quad level
     int32_t qnx, qny, qshift;
+    // quad records (LDS-resident beside the quad level): for compact quad r < n_qrec, 8 x 8
+    // sub-quads of 2^qrec_shift sub-blocks a side (qrec_shift = qshift - 3); bit
+    // (sy & 7) 8 + (sx & 7) of qrec_mask[2 r], [2 r + 1] (sx, sy = sub-block >> qrec_shift) set
+    // when every sub-block of that sub-quad holds the code qrec_code[r] -- the quad's most common
+    // uniform sub-quad code -- so such points need no sub-block lookup
+    const uint32_t* qrec_mask;
+    const uint16_t* qrec_code;
+    int32_t n_qrec, qrec_shift;
 };
 static const int kQuadMax = 32768;    // default quad-level entry budget
 static const int kQuadRefMax = 0x7ffe;  // quad entries kSubBlock | r, r <= kQuadRefMax: compact sub-blocks
@@ -115,7 +123,12 @@ MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, doubl
     const int ixC = (int)gx, iyC = (int)gy, ix = ixC >> r.cshift, iy = iyC >> r.cshift;
     uint32_t e;
     if (use_quad && r.quad) {
-        const uint32_t q = r.quad[(uint32_t)(iy >> r.qshift) * (uint32_t)r.qnx + (uint32_t)(ix >> r.qshift)];
+        uint32_t q = r.quad[(uint32_t)(iy >> r.qshift) * (uint32_t)r.qnx + (uint32_t)(ix >> r.qshift)];
+        if (q >= kSubBlock && (q & 0x7fffu) < (uint32_t)r.n_qrec) {
+            const uint32_t rr = q & 0x7fffu;
+            const uint32_t b = (uint32_t)((((iy >> r.qrec_shift) & 7) << 3) | ((ix >> r.qrec_shift) & 7));
+            if ((r.qrec_mask[2 * rr + (b >> 5)] >> (b & 31)) & 1u) q = r.qrec_code[rr];
+        }
         const int qm = (1 << r.qshift) - 1;
         e = q < kSubBlock ? q
                           : r.sub[(size_t)r.nx * r.ny + ((size_t)(q & 0x7fffu) << (2 * r.qshift)) +
@@ -222,6 +235,12 @@ struct Builder {
     std::vector<uint16_t> quad;  // quad level (empty: none)
     int qshift = 0, qnx = 0, qny = 0;
     int quad_max = kQuadMax;  // quad-level entry budget (set before build_raster)
+    // quad records (PointRaster::qrec_*): LDS bytes for the quad level and the records together
+    // (0: no records); set before build_raster
+    size_t quad_lds_bytes = 0;
+    std::vector<uint32_t> qrec_mask;
+    std::vector<uint16_t> qrec_code;
+    int qrec_shift = 0;
     int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0, n_sub_line = 0;
     bool lines = true;  // split single-feature sub-blocks by a line (set before build_raster)
     // Chip access for the raster classification (host memory)

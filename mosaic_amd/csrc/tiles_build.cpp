@@ -87,6 +87,9 @@ bool Builder::raster_setup(const ChipSource& src, int S_, int C_) {
     tile_base.clear();
     blocks.clear();
     quad.clear();
+    qrec_mask.clear();
+    qrec_code.clear();
+    qrec_shift = 0;
     n_sub_pure = n_sub_mixed = n_cell_mixed = n_sub_line = 0;
     if (tile_idx.empty() || S < 1 || S > 128 || (S & (S - 1)) || C < 1 || (C & (C - 1)) || S * C > 1024) return false;
     if (src.n_polygons > (int32_t)kMaxRasterKeys) return false;  // codes must stay below kSubBlock
@@ -537,6 +540,55 @@ bool Builder::assemble_raster(const RasterClass& rc) {
                     qe = (uint16_t)(kSubBlock | r);
                     r++;
                 }
+            // quad records for as many compact quads as the LDS budget holds (10 bytes each)
+            qrec_mask.clear();
+            qrec_code.clear();
+            qrec_shift = 0;
+            const int64_t qbytes = ((int64_t)quad.size() + 1) / 2 * 4;
+            const int64_t nrec = qshift >= 3 && (int64_t)quad_lds_bytes > qbytes + 16
+                                     ? std::min<int64_t>(nref, ((int64_t)quad_lds_bytes - qbytes - 16) / 10)
+                                     : 0;
+            if (nrec > 0) {
+                qrec_shift = qshift - 3;
+                const int64_t G = (int64_t)1 << qrec_shift;
+                qrec_mask.assign((size_t)(2 * nrec), 0u);
+                qrec_code.assign((size_t)nrec, 0);
+                for (int64_t rr = 0; rr < nrec; rr++) {
+                    // the compact copy (out-of-grid entries are 0 there; points never reach them, and a
+                    // sub-quad counts as uniform only if they agree too)
+                    const uint16_t* src = sub.data() + base + (size_t)(rr * QQ);
+                    uint16_t code[64];
+                    bool uni[64];
+                    for (int b = 0; b < 64; b++) {
+                        const int64_t i0 = (b & 7) * G, j0 = (b >> 3) * G;
+                        const uint16_t c = src[j0 * QS + i0];
+                        bool u = !(c & kSubBlock);
+                        for (int64_t dj = 0; dj < G && u; dj++)
+                            for (int64_t di = 0; di < G; di++)
+                                if (src[(j0 + dj) * QS + i0 + di] != c) {
+                                    u = false;
+                                    break;
+                                }
+                        code[b] = c;
+                        uni[b] = u;
+                    }
+                    // the most common uniform code (ties: the smallest)
+                    int best_n = 0;
+                    uint16_t best = 0;
+                    for (int b = 0; b < 64; b++) {
+                        if (!uni[b]) continue;
+                        int cnt = 0;
+                        for (int b2 = 0; b2 < 64; b2++) cnt += uni[b2] && code[b2] == code[b];
+                        if (cnt > best_n || (cnt == best_n && code[b] < best)) {
+                            best_n = cnt;
+                            best = code[b];
+                        }
+                    }
+                    qrec_code[(size_t)rr] = best;
+                    for (int b = 0; b < 64; b++)
+                        if (uni[b] && code[b] == best) qrec_mask[(size_t)(2 * rr + (b >> 5))] |= 1u << (b & 31);
+                }
+            }
         } else {
             quad.clear();  // no quad level: k_join_stream needs one (the tile path serves)
         }

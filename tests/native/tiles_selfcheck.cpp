@@ -100,6 +100,9 @@ int main(int argc, char** argv) {
     src.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(), gb.part_ring.data(),
                                gb.geom_part.data(), gb.geom_bbox.data()};
     src.n_polygons = npoly;
+    // the stream kernel's LDS shape: quad level in half of ~130 KB, quad records in the rest
+    tb.quad_max = 16384;
+    tb.quad_lds_bytes = 130 * 1024;
     bool rok = tb.build_raster(src, S, Cc, 8);
     tiles::PointRaster pr{};
     if (rok) {
@@ -118,6 +121,11 @@ int main(int argc, char** argv) {
         pr.qnx = tb.qnx;
         pr.qny = tb.qny;
         pr.qshift = tb.qshift;
+        pr.qrec_mask = tb.qrec_mask.empty() ? nullptr : tb.qrec_mask.data();
+        pr.qrec_code = tb.qrec_code.empty() ? nullptr : tb.qrec_code.data();
+        pr.n_qrec = (int32_t)tb.qrec_code.size();
+        pr.qrec_shift = tb.qrec_shift;
+        fprintf(stderr, "quad level %d x %d shift %d, %d quad records\n", tb.qnx, tb.qny, tb.qshift, pr.n_qrec);
     }
     long rbad = 0, rpure = 0, rmixed = 0, uni = 0, uni_mixed = 0;
     double bx0 = argc > 9 ? atof(argv[6]) : 0, by0 = argc > 9 ? atof(argv[7]) : 0;

@@ -29,6 +29,8 @@ def main():
     p.add_argument("--modes", type=lambda v: tuple(int(q) for q in v.split(":")), nargs="*", default=[(1, 1)],
                    help="TILES:POINT_RASTER pairs")
     p.add_argument("--sweep", nargs="*", default=[""], help="option sets to time, e.g. stream_pipe=0 stream_pipe=1")
+    p.add_argument("--build-opts", nargs="*", default=[""],
+                   help="option sets applied before each table build, e.g. raster_quad_records=0")
     args = p.parse_args()
     import torch
 
@@ -48,8 +50,13 @@ def main():
         x, y = uniform_points_device(zones.bbox(), n, seed=1)
     counts = torch.zeros(len(zones), dtype=torch.int64, device="cuda")
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    for sub, cell in args.point_raster:
-        for quad in args.quads:
+    ref = None
+    for sub, cell, quad, bo in [(s_, c_, q_, b_) for s_, c_ in args.point_raster for q_ in args.quads
+                                for b_ in args.build_opts]:
+        if True:
+            for kv in filter(None, bo.split(",")):
+                k, v = kv.split("=")
+                ctx.set_option(k, int(v))
             ctx.set_option("raster_sub", sub)
             ctx.set_option("raster_cell", cell)
             ctx.set_option("raster_quad", quad)
@@ -58,7 +65,7 @@ def main():
                                    n_polygons=len(zones))
             build_s = time.perf_counter() - t0
             tl = table.tiles()
-            ref = None
+            binfo = table.build_info()
             for tiles, praster in args.modes:
                 ctx.set_option("tiles", tiles)
                 ctx.set_option("point_raster", praster)
@@ -87,7 +94,8 @@ def main():
                     stats = ctx.last_stats()
                     step = float(np.median(ts))
                     line = {"res": args.res, "clustered": args.clustered, "n": n, "raster": f"{sub}x{cell}",
-                            "quad": quad, "tiles": tiles, "point_raster": praster, "stream_block": sb, "options": sw,
+                            "quad": quad, "build_opts": bo, "build_ms": {k: round(v, 1) for k, v in binfo.items()
+                                                                          if k.endswith("_ms")}, "tiles": tiles, "point_raster": praster, "stream_block": sb, "options": sw,
                             "call_ms": round(step, 4), "points_per_s": n / (step * 1e-3),
                             "same_counts": bool(np.array_equal(got, ref)), "pairs": int(got.sum()),
                             "tess_s": round(tess_s, 2), "build_s": round(build_s, 2),
@@ -102,6 +110,9 @@ def main():
             ctx.set_option("tiles", 1)
             ctx.set_option("point_raster", 1)
             table.close()
+            for kv in filter(None, bo.split(",")):  # build options back to their defaults
+                k, _ = kv.split("=")
+                ctx.set_option(k, {"raster_quad_records": 1, "raster_build": 1, "raster_lines": 1}.get(k, 1))
 
 
 if __name__ == "__main__":

@@ -165,6 +165,69 @@ int main(int argc, char** argv) {
                100.0 * nonu / (qnx * qny), (double)in_uni / (npts / 4), (long long)(snx * sny), pmax, over6, over14,
                qnx * qny / 2048.0);
     }
+    // LDS records for the non-uniform quads of the q = 4 level: a 2^(4-L) x 2^(4-L) grid of
+    // sub-quads (2^L x 2^L sub-blocks) each naming one of the quad's K most frequent uniform codes
+    // (or "gather"): share of the uniform points such a record decides.
+    {
+        const int q = 4;
+        const int64_t qnx = (NX + (1 << q) - 1) >> q, qny = (NY + (1 << q) - 1) >> q;
+        auto code_at = [&](int64_t i, int64_t j) -> uint16_t {
+            if (i >= NX || j >= NY) return 0;
+            uint16_t e = sub_at(i, j);
+            return (e & tiles::kSubBlock) ? tiles::kMixed : e;
+        };
+        for (int L = 1; L <= 2; L++)
+            for (int K = 1; K <= 3; K++) {
+                const int g = 1 << (q - L);  // sub-quads per quad side
+                // per quad: its sub-quad codes (kMixed: not uniform) and its top-K codes
+                std::vector<uint16_t> sq((size_t)(qnx * qny * g * g));
+                std::vector<std::vector<uint16_t>> top((size_t)(qnx * qny));
+                int64_t nonu = 0;
+                for (int64_t qj = 0; qj < qny; qj++)
+                    for (int64_t qi = 0; qi < qnx; qi++) {
+                        std::unordered_map<uint16_t, int> cnt;
+                        bool uni = true;
+                        uint16_t first = code_at(qi << q, qj << q);
+                        for (int b = 0; b < g; b++)
+                            for (int a = 0; a < g; a++) {
+                                uint16_t c = 0xfffe;
+                                for (int dj = 0; dj < (1 << L); dj++)
+                                    for (int di = 0; di < (1 << L); di++) {
+                                        uint16_t e = code_at((qi << q) + (a << L) + di, (qj << q) + (b << L) + dj);
+                                        if (c == 0xfffe) c = e;
+                                        else if (c != e) c = tiles::kMixed;
+                                        uni = uni && e == first && e != tiles::kMixed;
+                                    }
+                                sq[(size_t)((qj * qnx + qi) * g * g + b * g + a)] = c;
+                                if (c != tiles::kMixed) cnt[c]++;
+                            }
+                        if (uni) continue;
+                        nonu++;
+                        std::vector<std::pair<int, uint16_t>> v;
+                        for (auto& kv : cnt) v.push_back({-kv.second, kv.first});
+                        std::sort(v.begin(), v.end());
+                        for (int k = 0; k < K && k < (int)v.size(); k++) top[(size_t)(qj * qnx + qi)].push_back(v[k].second);
+                    }
+                std::mt19937_64 rng(7);
+                std::uniform_real_distribution<double> u(0.0, 1.0);
+                long dec = 0, tot = 0;
+                for (long k = 0; k < npts / 4; k++) {
+                    double x = bx0 + (bx1 - bx0) * u(rng), y = by0 + (by1 - by0) * u(rng);
+                    double gx = (x - tb.grid.x0) * tb.grid.sx * S, gy = (y - tb.grid.y0) * tb.grid.sy * S;
+                    tot++;
+                    if (!(gx >= 0 && gx < NX && gy >= 0 && gy < NY)) { dec++; continue; }
+                    const int64_t ix = (int64_t)gx, iy = (int64_t)gy, qq = (iy >> q) * qnx + (ix >> q);
+                    const auto& t = top[(size_t)qq];
+                    if (t.empty()) { dec++; continue; }
+                    const uint16_t c = sq[(size_t)(qq * g * g + ((iy >> L) & (g - 1)) * g + ((ix >> L) & (g - 1)))];
+                    if (c != tiles::kMixed && std::find(t.begin(), t.end(), c) != t.end()) dec++;
+                }
+                const int bits = K == 1 ? 1 : 2;
+                printf("q4 records: sub-quads %dx%d (L %d), top-%d codes: decided %.4f; %lld records x %d B = %.1f KB\n",
+                       g, g, L, K, (double)dec / tot, (long long)nonu, (g * g * bits + 7) / 8 + 2 * K,
+                       nonu * ((g * g * bits + 7) / 8 + 2 * K) / 1024.0);
+            }
+    }
     // point categories under the built raster (its own quad level)
     std::mt19937_64 rng(11);
     std::uniform_real_distribution<double> u(0.0, 1.0);
