@@ -99,7 +99,7 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * entries, or an entry budget <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of
  * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
  * host-resident coordinates: the next chunk's copy overlaps the current chunk's join; 0 = stage the
- * whole batch; default 2^25), "mixed_rows" (1/2/4), "mixed_blocks_per_cu". */
+ * whole batch; default 2^25), "mixed_rows" (1/2/4, default 2), "mixed_blocks_per_cu". */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* The calling thread's hipStream_t (created by the context unless set by this thread). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);

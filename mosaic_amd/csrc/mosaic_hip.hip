@@ -2005,7 +2005,7 @@ struct Options {
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
     int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
-    int mixed_rows = 4;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
+    int mixed_rows = 2;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
     // copy on copy_stream overlapping the current chunk's join (0: stage the whole batch first)
     int64_t host_chunk = (int64_t)1 << 25;
@@ -2971,8 +2971,16 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     return MOSAIC_OK;
 }
 
+// FNV-1a over 8-byte words (then the tail bytes): a fingerprint of the raster arrays
 static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
-    for (size_t i = 0; i < n; i++) h = (h ^ ((const uint8_t*)p)[i]) * 1099511628211ull;
+    const uint8_t* b = (const uint8_t*)p;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, b + i, 8);
+        h = (h ^ w) * 1099511628211ull;
+    }
+    for (; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
     return h;
 }
 
@@ -3055,25 +3063,50 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
         if (v1 > v0) ring_desc[t] = make_uint2(v0, v1 - v0);
     }
     // ray-parity rasters for one-ring border chips (raster.h); other chips take the general path
+    // (contiguous chip ranges on host threads, concatenated in chip order: the same arrays as one
+    // sequential pass)
     raster::Builder rb;
     rb.hdr.resize(meta.size());
-    for (int64_t t = 0; t < n_chips; t++) {
-        raster::ChipHdr& h = rb.hdr[t];
-        memset(&h, 0, sizeof h);
-        h.box = gb.geom_bbox[t];
-        h.cell_base = raster::kNoRaster;
-        uint2 d = ring_desc[t];
-        if (!(meta[t] & 1u) && d.y >= 2) {
-            // option raster_adaptive: small rings get small rasters (2 ceil(sqrt(segments)) cells a
-            // side, at most "raster"), so chip tables of millions of small chips stay compact
-            int dims = c->raster;
-            if (c->raster_adaptive) dims = std::min(dims, std::max(2, 2 * (int)ceil(sqrt((double)(d.y - 1)))));
-            rb.add_ring(h, gb.verts.data() + d.x, d.y, dims);
-        }
-        if (rb.edges.size() >= (1ull << 31)) {
-            ch->release_all();
-            delete ch;
-            return fail(MOSAIC_E_ARG, "chip table too large for the raster record index");
+    {
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
+            std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), n_chips / 256));
+        std::vector<raster::Builder> part((size_t)nt);
+        auto work = [&](int k) {
+            raster::Builder& pb = part[(size_t)k];
+            for (int64_t t = n_chips * k / nt; t < n_chips * (k + 1) / nt; t++) {
+                raster::ChipHdr& h = rb.hdr[t];
+                memset(&h, 0, sizeof h);
+                h.box = gb.geom_bbox[t];
+                h.cell_base = raster::kNoRaster;
+                uint2 d = ring_desc[t];
+                if (!(meta[t] & 1u) && d.y >= 2) {
+                    // option raster_adaptive: small rings get small rasters (2 ceil(sqrt(segments))
+                    // cells a side, at most "raster"), so tables of millions of small chips stay compact
+                    int dims = c->raster;
+                    if (c->raster_adaptive) dims = std::min(dims, std::max(2, 2 * (int)ceil(sqrt((double)(d.y - 1)))));
+                    pb.add_ring(h, gb.verts.data() + d.x, d.y, dims);
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int k = 1; k < nt; k++) pool.emplace_back(work, k);
+        work(0);
+        for (auto& th : pool) th.join();
+        for (int k = 0; k < nt; k++) {
+            const size_t c0 = rb.cells.size(), e0 = rb.edges.size();
+            for (int64_t t = n_chips * k / nt; t < n_chips * (k + 1) / nt; t++)
+                if (rb.hdr[t].cell_base != raster::kNoRaster) rb.hdr[t].cell_base += (uint32_t)c0;
+            for (raster::CellRec cr : part[(size_t)k].cells) {
+                if (cr.m) cr.word += (uint32_t)(e0 << 1);
+                rb.cells.push_back(cr);
+            }
+            rb.edges.insert(rb.edges.end(), part[(size_t)k].edges.begin(), part[(size_t)k].edges.end());
+            rb.pure_cells += part[(size_t)k].pure_cells;
+            if (rb.edges.size() >= (1ull << 31) || rb.cells.size() >= (size_t)raster::kNoRaster) {
+                ch->release_all();
+                delete ch;
+                return fail(MOSAIC_E_ARG, "chip table too large for the raster record index");
+            }
         }
     }
     if (meta.size() > (size_t)n_chips) {
@@ -3283,7 +3316,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     }
                     ch->build_ms[2] = ms_since(t_cls);
                     auto t_asm = std::chrono::steady_clock::now();
-                    raster_built = tb.assemble_raster(cls);
+                    raster_built = tb.assemble_raster(cls, threads);
                     ch->build_ms[3] = ms_since(t_asm);
                 }
                 if (raster_built) {

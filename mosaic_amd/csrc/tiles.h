@@ -267,7 +267,7 @@ struct Builder {
     std::vector<int> tile_of_rec;  // record -> tile (raster_setup)
     bool raster_setup(const ChipSource& src, int S_, int C_);
     void classify_raster_host(const ChipSource& src, int threads, RasterClass& rc);
-    bool assemble_raster(const RasterClass& rc);
+    bool assemble_raster(const RasterClass& rc, int threads = 1);
     static rbuild::HexTable hex_table_values();
 
     // cells: distinct chip cells; slot_of(cell) -> chip hash slot or -1.  Defined for the host

@@ -108,7 +108,7 @@ bool Builder::build_raster(const ChipSource& src, int S_, int C_, int threads) {
     if (!raster_setup(src, S_, C_)) return false;
     RasterClass rc;
     classify_raster_host(src, threads, rc);
-    return assemble_raster(rc);
+    return assemble_raster(rc, threads);
 }
 
 // Phase 1 on the host: every sub-block's code (kMixed for mixed ones), and for the mixed ones a
@@ -400,7 +400,22 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
 
 // Phase 2 (host, either classification): sub-block entries, per-tile line records and leaf blocks,
 // the quad level with its compact copies.
-bool Builder::assemble_raster(const RasterClass& rc) {
+namespace {
+// fn(begin, end) over [0, n) in contiguous chunks on up to `threads` threads
+template <class F>
+void parallel_for(int64_t n, int threads, F fn) {
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n / 64));
+    if (nt <= 1) {
+        if (n > 0) fn((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int k = 0; k < nt; k++) pool.emplace_back([=, &fn]() { fn(n * k / nt, n * (k + 1) / nt); });
+    for (auto& t : pool) t.join();
+}
+}  // namespace
+
+bool Builder::assemble_raster(const RasterClass& rc, int threads) {
     const int nx = grid.nx, ny = grid.ny;
     const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
     const size_t SS = (size_t)S * S, CC = (size_t)C * C;
@@ -408,49 +423,72 @@ bool Builder::assemble_raster(const RasterClass& rc) {
     tile_base.assign((size_t)nx * ny, 0u);
     std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
     std::vector<std::vector<LineRec>> tile_lines(recs.size());
-    int64_t pure = 0, mixed = 0, cmixed = 0, nline = 0;
-    size_t mk = 0;  // next mixed sub-block
-    for (size_t ri = 0; ri < recs.size(); ri++) {
-        const int t = tile_of_rec[ri];
-        if (t < 0 || recs[ri].dims == 0) continue;
-        const int ti = t % nx, tj = t / nx;
-        const uint16_t* rcode = rc.code.data() + ri * SS;
-        std::vector<uint16_t>& outb = tile_blocks[ri];
-        for (int sj = 0; sj < S; sj++)
-            for (int si = 0; si < S; si++) {
-                const uint16_t code = rcode[(size_t)sj * S + si];
-                uint16_t entry;
-                if (code != kMixed) {
-                    entry = code;
-                    pure++;
-                } else {
-                    mixed++;
-                    if (mk >= rc.kind.size()) return false;
-                    if (rc.kind[mk]) {
-                        // tile-local line record number (< S * S <= kLineBit)
-                        entry = (uint16_t)(kSubBlock | kLineBit | (uint32_t)tile_lines[ri].size());
-                        tile_lines[ri].push_back(rc.line[mk]);
-                        nline++;
-                    } else {
-                        const uint16_t* cellc = rc.cells.data() + (size_t)rc.cell_at[mk] * CC;
-                        bool same = true;
-                        for (size_t q = 0; q < CC; q++) {
-                            if (cellc[q] == kMixed) cmixed++;
-                            same = same && cellc[q] == cellc[0];
-                        }
-                        if (same && cellc[0] != kMixed) {
-                            entry = cellc[0];
-                        } else {
-                            // tile-local leaf block number (< S * S <= kLineBit)
-                            entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / CC));
-                            outb.insert(outb.end(), cellc, cellc + CC);
-                        }
-                    }
-                    mk++;
-                }
-                sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
+    // each record's first mixed sub-block (records are independent after that)
+    const int64_t nrec = (int64_t)recs.size();
+    std::vector<size_t> mk0((size_t)nrec + 1, 0);
+    auto rec_ok = [&](int64_t ri) { return tile_of_rec[(size_t)ri] >= 0 && recs[(size_t)ri].dims != 0; };
+    parallel_for(nrec, threads, [&](int64_t b, int64_t e) {
+        for (int64_t ri = b; ri < e; ri++) {
+            size_t m = 0;
+            if (rec_ok(ri)) {
+                const uint16_t* rcode = rc.code.data() + (size_t)ri * SS;
+                for (size_t k = 0; k < SS; k++) m += rcode[k] == kMixed;
             }
-    }
+            mk0[(size_t)ri + 1] = m;
+        }
+    });
+    for (int64_t ri = 0; ri < nrec; ri++) mk0[(size_t)ri + 1] += mk0[(size_t)ri];
+    if (mk0[(size_t)nrec] > rc.kind.size()) return false;
+    std::atomic<int64_t> pure(0), mixed(0), cmixed(0), nline(0);
+    parallel_for(nrec, threads, [&](int64_t b, int64_t e) {
+        int64_t l_pure = 0, l_mixed = 0, l_cmixed = 0, l_line = 0;
+        for (int64_t ri = b; ri < e; ri++) {
+            if (!rec_ok(ri)) continue;
+            const int t = tile_of_rec[(size_t)ri];
+            const int ti = t % nx, tj = t / nx;
+            const uint16_t* rcode = rc.code.data() + (size_t)ri * SS;
+            std::vector<uint16_t>& outb = tile_blocks[(size_t)ri];
+            std::vector<LineRec>& outl = tile_lines[(size_t)ri];
+            size_t mk = mk0[(size_t)ri];  // next mixed sub-block
+            for (int sj = 0; sj < S; sj++)
+                for (int si = 0; si < S; si++) {
+                    const uint16_t code = rcode[(size_t)sj * S + si];
+                    uint16_t entry;
+                    if (code != kMixed) {
+                        entry = code;
+                        l_pure++;
+                    } else {
+                        l_mixed++;
+                        if (rc.kind[mk]) {
+                            // tile-local line record number (< S * S <= kLineBit)
+                            entry = (uint16_t)(kSubBlock | kLineBit | (uint32_t)outl.size());
+                            outl.push_back(rc.line[mk]);
+                            l_line++;
+                        } else {
+                            const uint16_t* cellc = rc.cells.data() + (size_t)rc.cell_at[mk] * CC;
+                            bool same = true;
+                            for (size_t q = 0; q < CC; q++) {
+                                if (cellc[q] == kMixed) l_cmixed++;
+                                same = same && cellc[q] == cellc[0];
+                            }
+                            if (same && cellc[0] != kMixed) {
+                                entry = cellc[0];
+                            } else {
+                                // tile-local leaf block number (< S * S <= kLineBit)
+                                entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / CC));
+                                outb.insert(outb.end(), cellc, cellc + CC);
+                            }
+                        }
+                        mk++;
+                    }
+                    sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = entry;
+                }
+        }
+        pure += l_pure;
+        mixed += l_mixed;
+        cmixed += l_cmixed;
+        nline += l_line;
+    });
     // kFull tiles: every point takes the tile path; kSkip tiles: no pair (0, already)
     for (int64_t t = 0; t < (int64_t)nx * ny; t++) {
         if (tile_idx[(size_t)t] != kFull) continue;
@@ -472,11 +510,13 @@ bool Builder::assemble_raster(const RasterClass& rc) {
         return false;
     }
     blocks.assign(std::max<size_t>(total, std::max<size_t>(CC, 8)), kMixed);
-    for (size_t r = 0; r < recs.size(); r++) {
-        for (size_t n = 0; n < tile_lines[r].size(); n++)
-            memcpy(blocks.data() + at[r] - 8 * (n + 1), &tile_lines[r][n], sizeof(LineRec));
-        std::copy(tile_blocks[r].begin(), tile_blocks[r].end(), blocks.begin() + (ptrdiff_t)at[r]);
-    }
+    parallel_for(nrec, threads, [&](int64_t b, int64_t e) {
+        for (int64_t r = b; r < e; r++) {
+            for (size_t n = 0; n < tile_lines[(size_t)r].size(); n++)
+                memcpy(blocks.data() + at[(size_t)r] - 8 * (n + 1), &tile_lines[(size_t)r][n], sizeof(LineRec));
+            std::copy(tile_blocks[(size_t)r].begin(), tile_blocks[(size_t)r].end(), blocks.begin() + (ptrdiff_t)at[(size_t)r]);
+        }
+    });
     // clamping (raster_code, k_join_stream): a finite point outside the grid is looked up at the
     // nearest edge sub-block, so every edge sub-block must answer "no pair" (0) or kMixed (the
     // tile path, which finds no chip outside the grid); chip cells lie >= k tile rings inside
@@ -491,10 +531,10 @@ bool Builder::assemble_raster(const RasterClass& rc) {
             const uint16_t e = sub[(size_t)(j * NX + i)];
             if (e != 0 && e != kMixed) edge_ok = false;
         }
-    n_sub_line = nline;
-    n_sub_pure = pure;
-    n_sub_mixed = mixed;
-    n_cell_mixed = cmixed;
+    n_sub_line = nline.load();
+    n_sub_pure = pure.load();
+    n_sub_mixed = mixed.load();
+    n_cell_mixed = cmixed.load();
     // quad level: the smallest power-of-two group of sub-blocks whose table fits quad_max entries
     qshift = 0;
     while (qshift < 16 && ((NX + (1 << qshift) - 1) >> qshift) * ((NY + (1 << qshift) - 1) >> qshift) > quad_max)
@@ -504,18 +544,20 @@ bool Builder::assemble_raster(const RasterClass& rc) {
         qny = (int)((NY + (1 << qshift) - 1) >> qshift);
         quad.assign((size_t)qnx * qny, kMixed);
         std::vector<uint8_t> seen((size_t)qnx * qny, 0);
-        for (int64_t j = 0; j < NY; j++)
-            for (int64_t i = 0; i < NX; i++) {
-                const uint16_t e = sub[(size_t)(j * NX + i)];
-                const size_t q = (size_t)((j >> qshift) * qnx + (i >> qshift));
-                const uint16_t code = (e & kSubBlock) ? kMixed : e;  // blocks and kMixed alike
-                if (!seen[q]) {
-                    seen[q] = 1;
-                    quad[q] = code;
-                } else if (quad[q] != code) {
-                    quad[q] = kMixed;
+        parallel_for(qny, threads, [&](int64_t qb, int64_t qe) {  // quad rows [qb, qe)
+            for (int64_t j = qb << qshift; j < std::min<int64_t>(NY, qe << qshift); j++)
+                for (int64_t i = 0; i < NX; i++) {
+                    const uint16_t e = sub[(size_t)(j * NX + i)];
+                    const size_t q = (size_t)((j >> qshift) * qnx + (i >> qshift));
+                    const uint16_t code = (e & kSubBlock) ? kMixed : e;  // blocks and kMixed alike
+                    if (!seen[q]) {
+                        seen[q] = 1;
+                        quad[q] = code;
+                    } else if (quad[q] != code) {
+                        quad[q] = kMixed;
+                    }
                 }
-            }
+        });
         // compact copies of the non-uniform quads' sub-block entries behind the grid's own
         // (quad entry kSubBlock | r: quad r's 2^qshift x 2^qshift entries, row-major, from
         // sub[nx * ny + (r << 2 qshift)]), so the sub-block lookups that pass the quad level
@@ -526,20 +568,22 @@ bool Builder::assemble_raster(const RasterClass& rc) {
         if (qshift <= 6 && nref <= kQuadRefMax + 1 && NX * NY + nref * QQ < ((int64_t)1 << 31)) {
             const size_t base = sub.size();
             sub.resize(base + (size_t)(nref * QQ), 0);
-            int64_t r = 0;
-            for (int64_t qj = 0; qj < qny; qj++)
-                for (int64_t qi = 0; qi < qnx; qi++) {
-                    uint16_t& qe = quad[(size_t)(qj * qnx + qi)];
-                    if (qe != kMixed) continue;
+            std::vector<int64_t> refq;  // compact quad r -> quad (row-major order)
+            refq.reserve((size_t)nref);
+            for (int64_t q = 0; q < (int64_t)quad.size(); q++)
+                if (quad[(size_t)q] == kMixed) refq.push_back(q);
+            parallel_for(nref, threads, [&](int64_t b, int64_t e) {
+                for (int64_t r = b; r < e; r++) {
+                    const int64_t qj = refq[(size_t)r] / qnx, qi = refq[(size_t)r] % qnx;
                     uint16_t* dst = sub.data() + base + (size_t)(r * QQ);
                     for (int64_t dj = 0; dj < QS; dj++)
                         for (int64_t di = 0; di < QS; di++) {
                             const int64_t j = qj * QS + dj, i = qi * QS + di;
                             if (j < NY && i < NX) dst[dj * QS + di] = sub[(size_t)(j * NX + i)];
                         }
-                    qe = (uint16_t)(kSubBlock | r);
-                    r++;
+                    quad[(size_t)refq[(size_t)r]] = (uint16_t)(kSubBlock | r);
                 }
+            });
             // quad records for as many compact quads as the LDS budget holds (10 bytes each)
             qrec_mask.clear();
             qrec_code.clear();
@@ -553,7 +597,8 @@ bool Builder::assemble_raster(const RasterClass& rc) {
                 const int64_t G = (int64_t)1 << qrec_shift;
                 qrec_mask.assign((size_t)(2 * nrec), 0u);
                 qrec_code.assign((size_t)nrec, 0);
-                for (int64_t rr = 0; rr < nrec; rr++) {
+                parallel_for(nrec, threads, [&](int64_t rb, int64_t re) {
+                for (int64_t rr = rb; rr < re; rr++) {
                     // the compact copy (out-of-grid entries are 0 there; points never reach them, and a
                     // sub-quad counts as uniform only if they agree too)
                     const uint16_t* src = sub.data() + base + (size_t)(rr * QQ);
@@ -588,6 +633,7 @@ bool Builder::assemble_raster(const RasterClass& rc) {
                     for (int b = 0; b < 64; b++)
                         if (uni[b] && code[b] == best) qrec_mask[(size_t)(2 * rr + (b >> 5))] |= 1u << (b & 31);
                 }
+                });
             }
         } else {
             quad.clear();  // no quad level: k_join_stream needs one (the tile path serves)

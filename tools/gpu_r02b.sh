@@ -21,6 +21,29 @@ case $STEP in
     run kb_qrec_c2 300 python -u tools/kbench.py --n 1e9 --build-opts raster_quad_records=0 raster_quad_records=1
     run kb_qrec_c3 300 python -u tools/kbench.py --n 1e9 --res 10 --clustered --build-opts raster_quad_records=0 raster_quad_records=1
     ;;
+  probe)
+    run stream_probe 120 ./tools/probes/stream_probe 1e9
+    ;;
+  sweep1)
+    run kb_sweep1 400 python -u tools/kbench.py --n 1e9 --reps 6 --stream-blocks 1024 512 --sweep stream_pipe=0 stream_pipe=1 \
+        stream_pipe=1,mixed_rows=1 stream_pipe=1,mixed_rows=2 stream_pipe=1,mixed_blocks_per_cu=16
+    ;;
+  bprof0)
+    run build_prof 300 python -u tools/build_prof.py
+    cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/bprof -o bp -- \
+        python3 $GRAFT_REPO_ROOT/tools/build_prof.py > $GRAFT_REPO_ROOT/gpurun_out/bprof.log 2>&1 \
+        || { echo "rocprof failed"; tail -20 $GRAFT_REPO_ROOT/gpurun_out/bprof.log; exit 1; }
+    cd $GRAFT_REPO_ROOT && find gpurun_out/bprof -name "*kernel_stats.csv" -exec head -20 {} \;
+    ;;
+  bprof)
+    run t_bprof 600 $PYT tests/test_raster_build.py "tests/test_gpu_parity.py::test_join_counts_match_oracle" \
+        "tests/test_gpu_parity.py::test_join_c4_buildings" -s
+    run build_prof 300 python -u tools/build_prof.py
+    cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/bprof -o bp -- \
+        python3 $GRAFT_REPO_ROOT/tools/build_prof.py > $GRAFT_REPO_ROOT/gpurun_out/bprof.log 2>&1 \
+        || { echo "rocprof failed"; tail -20 $GRAFT_REPO_ROOT/gpurun_out/bprof.log; exit 1; }
+    cd $GRAFT_REPO_ROOT && find gpurun_out/bprof -name "*kernel_stats.csv" -exec head -20 {} \;
+    ;;
   tests)
     run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
     ;;

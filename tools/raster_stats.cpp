@@ -168,16 +168,16 @@ int main(int argc, char** argv) {
     // LDS records for the non-uniform quads of the q = 4 level: a 2^(4-L) x 2^(4-L) grid of
     // sub-quads (2^L x 2^L sub-blocks) each naming one of the quad's K most frequent uniform codes
     // (or "gather"): share of the uniform points such a record decides.
-    {
-        const int q = 4;
+    for (int q = 3; q <= 6; q++) {
         const int64_t qnx = (NX + (1 << q) - 1) >> q, qny = (NY + (1 << q) - 1) >> q;
         auto code_at = [&](int64_t i, int64_t j) -> uint16_t {
             if (i >= NX || j >= NY) return 0;
             uint16_t e = sub_at(i, j);
             return (e & tiles::kSubBlock) ? tiles::kMixed : e;
         };
-        for (int L = 1; L <= 2; L++)
-            for (int K = 1; K <= 3; K++) {
+        for (int L = q - 4; L <= q - 2; L++)
+            for (int K = 1; K <= 2; K++) {
+                if (L < 0) continue;
                 const int g = 1 << (q - L);  // sub-quads per quad side
                 // per quad: its sub-quad codes (kMixed: not uniform) and its top-K codes
                 std::vector<uint16_t> sq((size_t)(qnx * qny * g * g));
@@ -223,9 +223,11 @@ int main(int argc, char** argv) {
                     if (c != tiles::kMixed && std::find(t.begin(), t.end(), c) != t.end()) dec++;
                 }
                 const int bits = K == 1 ? 1 : 2;
-                printf("q4 records: sub-quads %dx%d (L %d), top-%d codes: decided %.4f; %lld records x %d B = %.1f KB\n",
-                       g, g, L, K, (double)dec / tot, (long long)nonu, (g * g * bits + 7) / 8 + 2 * K,
-                       nonu * ((g * g * bits + 7) / 8 + 2 * K) / 1024.0);
+                const double kb = nonu * ((g * g * bits + 7) / 8 + 2 * K) / 1024.0;
+                printf("q%d records: sub-quads %dx%d (L %d), top-%d codes: decided %.4f; %lld records x %d B = %.1f KB"
+                       " + quad table %.1f KB = %.1f KB\n",
+                       q, g, g, L, K, (double)dec / tot, (long long)nonu, (g * g * bits + 7) / 8 + 2 * K, kb,
+                       qnx * qny * 2 / 1024.0, kb + qnx * qny * 2 / 1024.0);
             }
     }
     // point categories under the built raster (its own quad level)
