@@ -1212,6 +1212,231 @@ __global__ void __launch_bounds__(256) k_raster_line(RBuildArgs a) {
     }
 }
 
+// ---- k_raster_line_wave: k_raster_line with one wave per mixed sub-block -- the candidate
+// hexagons, chips and rings wave-uniform, their segments spread over the lanes (ballot for "any
+// segment meets", wave reductions for the longest clipped segment and the largest deviation,
+// coop_contains for JTS contains).  Every decision is order-independent or reduced in the
+// sequential order, so the line records are those of k_raster_line / try_line, bit for bit.
+__device__ inline double wave_max_f64(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = rbuild::dmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// rhex_answer for a convex region ll[n] (within eps), wave-uniform result
+__device__ inline int rhex_answer_wave(const RBuildArgs& a, const RTile& t, int k, double x0, double y0, double x1,
+                                       double y1, const rbuild::P2* ll, int n, double eps, double cx, double cy, int* key) {
+    const uint32_t e = a.entries[t.off + (uint32_t)k];
+    int cnt = 0;
+    *key = -1;
+    if (!e) return 0;
+    const HashEntry he = a.table[e - 1];
+    const int lane = (int)(threadIdx.x & 63);
+    for (uint32_t c = he.first; c < he.first + he.count; c++) {
+        const uint32_t m = a.meta[c];
+        if (!(m & 1u)) {
+            const pip::Box bx = a.store.geom_bbox[c];
+            if (!(bx.maxx < x0 - eps || bx.minx > x1 + eps || bx.maxy < y0 - eps || bx.miny > y1 + eps)) {
+                for (uint32_t p = a.store.geom_part[c]; p < a.store.geom_part[c + 1]; p++)
+                    for (uint32_t r = a.store.part_ring[p]; r < a.store.part_ring[p + 1]; r++) {
+                        const uint32_t v0 = a.store.ring_start[r] + 1, v1 = a.store.ring_start[r + 1];
+                        for (uint32_t base = v0; base < v1; base += 64) {
+                            const uint32_t v = base + (uint32_t)lane;
+                            bool hit = false;
+                            if (v < v1) {
+                                const pip::Vec2 s0 = a.store.verts[v - 1], s1 = a.store.verts[v];
+                                hit = rbuild::seg_meets_poly(rbuild::P2{s0.x, s0.y}, rbuild::P2{s1.x, s1.y}, ll, n, eps);
+                            }
+                            if (__ballot(hit)) return -1;
+                        }
+                    }
+            }
+            if (!pip::coop_contains(a.store, c, cx, cy)) continue;
+        }
+        if (cnt == 0) *key = (int)(m >> 1);
+        cnt++;
+    }
+    return cnt;
+}
+
+__device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* uv,
+                                               int n, const rbuild::P2* sq, double stol) {
+    using rbuild::dmax;
+    using rbuild::dmin;
+    rbuild::P2 img[8], ll[8];
+    double u0 = INFINITY, u1 = -INFINITY, v0 = INFINITY, v1 = -INFINITY;
+    double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY, mx = 0.0, my = 0.0;
+    const int S = a.S, C = a.C;
+    for (int v = 0; v < n; v++) {
+        img[v] = rimage(a, t, (si + uv[v].x) * C, (sj + uv[v].y) * C);
+        ll[v] = rbuild::P2{t.lon0 + a.tw * (si + uv[v].x) / S, t.lat0 + a.th * (sj + uv[v].y) / S};
+        u0 = dmin(u0, uv[v].x);
+        u1 = dmax(u1, uv[v].x);
+        v0 = dmin(v0, uv[v].y);
+        v1 = dmax(v1, uv[v].y);
+        x0 = dmin(x0, ll[v].x);
+        x1 = dmax(x1, ll[v].x);
+        y0 = dmin(y0, ll[v].y);
+        y1 = dmax(y1, ll[v].y);
+        mx += ll[v].x;
+        my += ll[v].y;
+    }
+    mx /= n;
+    my /= n;
+    const double frac = dmax(u1 - u0, v1 - v0) / S;
+    const double tol = 4.0 * t.dev * frac * frac + 1e-7;
+    const double eps = dmax(t.exd, t.eyd);
+    bool any = false;
+    int acnt = 0, akey = -1;
+    const int W = t.wa * t.wb, lane = (int)(threadIdx.x & 63);
+    for (int k0 = 0; k0 < W; k0 += 64) {
+        // the window hexagons of this chunk that are candidates, one lane each, in order
+        const int kl = k0 + lane;
+        bool is_c = false;
+        if (kl < W) {
+            const rbuild::P2 c = rhex_centre(t, kl);
+            is_c = rbuild::poly_meets_hex(sq, 4, c, stol, a.ht) && rbuild::poly_meets_hex(img, n, c, tol, a.ht);
+        }
+        for (unsigned long long mask = __ballot(is_c); mask; mask &= mask - 1) {
+            const int k = k0 + __builtin_ctzll(mask);
+            int key;
+            const int cnt = rhex_answer_wave(a, t, k, x0, y0, x1, y1, ll, n, eps, mx, my, &key);
+            if (cnt < 0 || cnt > 1) return tiles::kMixed;
+            if (!any) {
+                any = true;
+                acnt = cnt;
+                akey = key;
+            } else if (cnt != acnt || key != akey) {
+                return tiles::kMixed;
+            }
+        }
+    }
+    if (!any) return tiles::kMixed;
+    return acnt == 0 ? (uint16_t)0 : (uint16_t)(akey + 1);
+}
+
+__device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* sq,
+                                      double stol, tiles::LineRec& out) {
+    const int S = a.S, lane = (int)(threadIdx.x & 63);
+    const double wR = a.tw / S, hR = a.th / S;
+    const double lonR0 = t.lon0 + a.tw * si / S, latR0 = t.lat0 + a.th * sj / S;
+    const double exu = t.exd / wR, eyv = t.eyd / hR;
+    const double bx0 = lonR0 - t.exd, bx1 = lonR0 + wR + t.exd, by0 = latR0 - t.eyd, by1 = latR0 + hR + t.eyd;
+    // pass 0: this lane's longest clipped segment (first in (hexagon, vertex) order on ties); pass
+    // 1: this lane's largest deviation; then wave reductions
+    double best = 0.0, dev_max = 0.0, la = 0.0, lb = 0.0, lc = 0.0;
+    uint64_t best_key = ~0ull;
+    rbuild::P2 pa{0, 0}, pb{0, 0};
+    const int W = t.wa * t.wb;
+    if (W <= 0) return false;
+    for (int pass = 0; pass < 2; pass++)
+        for (int k0 = 0; k0 < W; k0 += 64) {
+        const int kl = k0 + lane;
+        const bool is_c = kl < W && a.entries[t.off + (uint32_t)kl] &&
+                          rbuild::poly_meets_hex(sq, 4, rhex_centre(t, kl), stol, a.ht);
+        for (unsigned long long mask = __ballot(is_c); mask; mask &= mask - 1) {
+            const int k = k0 + __builtin_ctzll(mask);
+            const uint32_t e = a.entries[t.off + (uint32_t)k];
+            const HashEntry he = a.table[e - 1];
+            for (uint32_t c = he.first; c < he.first + he.count; c++) {
+                if (a.meta[c] & 1u) continue;
+                const pip::Box bx = a.store.geom_bbox[c];
+                if (bx.maxx < bx0 || bx.minx > bx1 || bx.maxy < by0 || bx.miny > by1) continue;
+                for (uint32_t p = a.store.geom_part[c]; p < a.store.geom_part[c + 1]; p++)
+                    for (uint32_t r = a.store.part_ring[p]; r < a.store.part_ring[p + 1]; r++) {
+                        const uint32_t vend = a.store.ring_start[r + 1];
+                        for (uint32_t v = a.store.ring_start[r] + 1 + (uint32_t)lane; v < vend; v += 64) {
+                            const pip::Vec2 s0 = a.store.verts[v - 1], s1 = a.store.verts[v];
+                            double ax = (s0.x - lonR0) / wR, ay = (s0.y - latR0) / hR;
+                            double qx = (s1.x - lonR0) / wR, qy = (s1.y - latR0) / hR;
+                            if (!rbuild::clip_seg(ax, ay, qx, qy, -exu, -eyv, 1.0 + exu, 1.0 + eyv)) continue;
+                            if (pass == 0) {
+                                const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
+                                if (l2 > best) {  // a lane's segments come in increasing order
+                                    best = l2;
+                                    best_key = ((uint64_t)(uint32_t)k << 32) | v;
+                                    pa = rbuild::P2{ax, ay};
+                                    pb = rbuild::P2{qx, qy};
+                                }
+                            } else {
+                                dev_max = rbuild::dmax(dev_max, fabs(la * ax + lb * ay + lc));
+                                dev_max = rbuild::dmax(dev_max, fabs(la * qx + lb * qy + lc));
+                            }
+                        }
+                    }
+            }
+        }
+        if (pass == 0 && k0 + 64 >= W) {
+            // the sequential choice: the largest l2, and of equal ones the first in order
+            double bl = best;
+            uint64_t bk = best_key;
+            int bw = lane;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const double ol = __shfl_xor(bl, o, 64);
+                const uint64_t ok = __shfl_xor(bk, o, 64);
+                const int ow = __shfl_xor(bw, o, 64);
+                if (ol > bl || (ol == bl && ok < bk)) {
+                    bl = ol;
+                    bk = ok;
+                    bw = ow;
+                }
+            }
+            best = bl;
+            if (!(best > 1e-6)) return false;
+            pa = rbuild::P2{__shfl(pa.x, bw, 64), __shfl(pa.y, bw, 64)};
+            pb = rbuild::P2{__shfl(pb.x, bw, 64), __shfl(pb.y, bw, 64)};
+            const double l = sqrt(best);
+            la = -(pb.y - pa.y) / l;
+            lb = (pb.x - pa.x) / l;
+            lc = -(la * 0.5 * (pa.x + pb.x) + lb * 0.5 * (pa.y + pb.y));
+        }
+    }
+    dev_max = wave_max_f64(dev_max);
+    const rbuild::P2 sqb[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
+    for (int mk = 0; mk < 4; mk++) {
+        const double margin = rbuild::line_margin(mk);
+        if (dev_max > margin - 2.0 * tiles::kLineSlack) continue;
+        out.a = (float)(la / margin);
+        out.b = (float)(lb / margin);
+        out.c = (float)(lc / margin);
+        const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - tiles::kLineSlack / margin;
+        rbuild::P2 hp[8], hn[8];
+        const int np = rbuild::clip_half(sqb, 4, A, B, Cf - m, hp), nn = rbuild::clip_half(sqb, 4, -A, -B, -Cf - m, hn);
+        const uint16_t cp = np >= 3 ? rclassify_poly_wave(a, t, si, sj, hp, np, sq, stol) : (uint16_t)0;
+        if (cp == tiles::kMixed) continue;
+        const uint16_t cn = nn >= 3 ? rclassify_poly_wave(a, t, si, sj, hn, nn, sq, stol) : (uint16_t)0;
+        if (cn == tiles::kMixed) continue;
+        out.pos = cp;
+        out.neg = cn;
+        out.a = (float)((double)out.a / a.C);
+        out.b = (float)((double)out.b / a.C);
+        return true;
+    }
+    return false;
+}
+
+// one wave per mixed sub-block (waves past the end exit together)
+__global__ void __launch_bounds__(256) k_raster_line_wave(RBuildArgs a) {
+    const int64_t SS = (int64_t)a.S * a.S;
+    const int64_t m = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (m >= a.n_mixed) return;
+    const int64_t g = a.mixed[m];
+    const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
+    RTile t;
+    tiles::LineRec lr{0, 0, 0, 0, 0};
+    bool ok = false;
+    if (a.lines && rtile_of(a, r, t)) {
+        rbuild::P2 sq[4];
+        const double stol = rsub_quad(a, t, si, sj, sq);
+        ok = rtry_line_wave(a, t, si, sj, sq, stol, lr);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        a.kind[m] = ok ? 1 : 0;
+        a.line[m] = ok ? lr : tiles::LineRec{0, 0, 0, 0, 0};
+    }
+}
+
 __global__ void __launch_bounds__(256) k_raster_cells(RBuildArgs a) {
     const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
     const int64_t total = a.n_cell_sb * CC;
@@ -2321,7 +2546,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "raster_quad_records") {
         o.raster_quad_records = v ? 1 : 0;
     } else if (k == "raster_build") {
-        o.raster_build = v ? 1 : 0;
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "raster_build must be 0 (host), 1 (GPU) or 2 (GPU, lane-per-sub-block lines)");
+        o.raster_build = (int)v;
     } else if (k == "host_chunk") {
         if (v < 0) return fail(MOSAIC_E_ARG, "host_chunk must be >= 0");
         o.host_chunk = v;
@@ -2943,7 +3169,10 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     a.n_mixed = n_mixed;
     a.kind = (uint8_t*)d_kind.p;
     a.line = (tiles::LineRec*)d_line.p;
-    hipLaunchKernelGGL(k_raster_line, grid_of(n_mixed), dim3(256), 0, c->stream, a);
+    if (c->raster_build == 2)  // one lane per sub-block (the first GPU form, kept for comparison)
+        hipLaunchKernelGGL(k_raster_line, grid_of(n_mixed), dim3(256), 0, c->stream, a);
+    else  // one wave per sub-block
+        hipLaunchKernelGGL(k_raster_line_wave, dim3((unsigned)((n_mixed + 3) / 4)), dim3(256), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(rc.kind.data(), d_kind.p, list.size(), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(rc.line.data(), d_line.p, list.size() * sizeof(tiles::LineRec), hipMemcpyDeviceToHost,

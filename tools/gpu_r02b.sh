@@ -28,6 +28,10 @@ case $STEP in
     run kb_sweep1 400 python -u tools/kbench.py --n 1e9 --reps 6 --stream-blocks 1024 512 --sweep stream_pipe=0 stream_pipe=1 \
         stream_pipe=1,mixed_rows=1 stream_pipe=1,mixed_rows=2 stream_pipe=1,mixed_blocks_per_cu=16
     ;;
+  rbw)
+    run t_rbw 600 $PYT tests/test_raster_build.py -s
+    run build_prof 300 python -u tools/build_prof.py
+    ;;
   bprof0)
     run build_prof 300 python -u tools/build_prof.py
     cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/bprof -o bp -- \
