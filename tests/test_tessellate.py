@@ -93,3 +93,25 @@ def test_tessellate_errors():
         tessellate("H3", z, 16)
     with pytest.raises(IllegalStateException, match="BNG resolution not supported"):
         tessellate("BNG", z, 0)
+
+
+def _one_polygon(coords):
+    xy = np.array(coords, np.float64)
+    return PolygonSet(xy, [0, len(xy)], [0, 1], [0, 1])
+
+
+# The reference's own tessellation regression fixtures (WKT coordinates copied as data):
+# issue #243, core/TestMosaic.scala:9-16 -- mosaicFill at H3 res 7 gives 10 chips, all distinct
+REF_243 = [(4.42, 51.78), (4.38, 51.78), (4.39, 51.83), (4.40, 51.83), (4.41, 51.8303), (4.417, 51.8295),
+           (4.42, 51.83), (4.44, 51.81), (4.42, 51.78)]
+# issue #260, expressions/index/MosaicFillBehaviors.scala:177-195 -- grid_tessellate at res 3 has > 0 chips
+REF_260 = [(5.26, 52.72), (5.20, 52.71), (5.21, 52.75), (5.26, 52.75), (5.26, 52.72)]
+
+
+def test_reference_tessellation_fixtures():
+    c = tessellate("H3", _one_polygon(REF_243), 7)
+    assert len(c["index_id"]) == 10 and len(set(c["index_id"].tolist())) == 10
+    c = tessellate("H3", _one_polygon(REF_260), 3)
+    assert len(c["index_id"]) > 0
+    # every chip's polygon key is the input geometry and its cell holds part of the polygon
+    assert set(c["polygon_key"].tolist()) == {0}

@@ -140,3 +140,18 @@ def test_gpu_tessellation_errors(ctx):
         tessellate("H3", z, 16, ctx=ctx)
     with pytest.raises(IllegalStateException, match="BNG resolution not supported"):
         tessellate("BNG", z, 0, ctx=ctx)
+
+
+def test_h3_gpu_reference_tessellation_fixtures():
+    # the reference's regression polygons (issue #243 at res 7: 10 distinct chips; issue #260 at res
+    # 3: > 0 chips) through the GPU producer, equal to the host producer
+    from .test_tessellate import REF_243, REF_260, _one_polygon
+
+    h3 = MosaicContext.build("H3", "JTS")
+    for coords, res in ((REF_243, 7), (REF_260, 3)):
+        p = _one_polygon(coords)
+        host = tessellate("H3", p, res)
+        gpu = h3.grid_tessellateexplode(p, res)
+        _same(host, gpu)
+    assert len(set(gpu["index_id"].tolist())) >= 1
+    h3.close()

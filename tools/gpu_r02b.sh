@@ -32,6 +32,9 @@ case $STEP in
     run t_rbw 600 $PYT tests/test_raster_build.py -s
     run build_prof 300 python -u tools/build_prof.py
     ;;
+  cfg)
+    run t_cfg 900 $PYT tests/test_gpu_configs.py tests/test_tessellate_gpu.py -s
+    ;;
   bprof0)
     run build_prof 300 python -u tools/build_prof.py
     cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/bprof -o bp -- \
