@@ -33,6 +33,7 @@
 #include "point_decode.h"
 #include "raster.h"
 #include "raster_build.h"
+#include "tess_gpu.h"
 #include "tiles.h"
 
 using namespace mosaic;
@@ -4620,7 +4621,327 @@ __global__ void __launch_bounds__(256) k_tess_classify_poly(ClassifyPolyArgs a) 
     }
 }
 
+// ---- k_tess_clip: border chips of mosaic_tessellate_gpu (tess_gpu.h), one wave per task.  Per ring
+// of the candidate's geometry: Sutherland-Hodgman against each edge of the clip polygon as a
+// wave-parallel pass (lane i emits the output of input vertex i -- intersection and / or the vertex,
+// as tessellate.cpp's clip_edge -- at its ballot prefix, so the output order is the sequential
+// one), ping-ponging between two scratch buffers of the wave; then the ring's area (summed in order,
+// redundantly on every lane), the degenerate / net-area tests and the output vertices (original
+// vertices copied, computed ones mapped back).
+struct ClipArgs {
+    const double* pxy;  // rings in the clip plane
+    const double* gxy;  // rings in output coordinates (lon / lat or metres)
+    const int64_t *ring_offsets, *part_rings, *geom_parts;
+    const int32_t* cand_geom;
+    const int32_t* gface;
+    const double* clip;
+    int nv, res, mode;
+    double area_eps;
+    const int64_t* tasks;
+    int64_t n_tasks;
+    double* sxy;      // per wave: 2 x cap points
+    int32_t* stag;    // per wave: 2 x cap tags
+    int64_t cap;
+    double* out;      // output vertices (interleaved)
+    unsigned long long* counters;  // [0] vertices, [1] rings, [2] parts
+    int64_t out_cap, ring_cap, part_cap;
+    tessclip::ClipRing* rings;
+    tessclip::ClipPart* parts;
+    uint8_t* redo;  // per task
+};
+
+__device__ inline void wave_sync_global() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// tessellate.cpp FacePlane::to_geo (mode 0) / identity (mode 1)
+__device__ inline void clip_to_geo(const ClipArgs& a, int face, double hx, double hy, double* ox, double* oy) {
+    if (a.mode == 1) {
+        *ox = hx;
+        *oy = hy;
+        return;
+    }
+    const double* b = h3::kH3FastBasis[face];
+    const double* ei = b + ((a.res & 1) ? 9 : 3);
+    const double* ep = b + ((a.res & 1) ? 12 : 6);
+    const double S = h3::kH3FastScale[a.res];
+    double t[3];
+    for (int k = 0; k < 3; k++) t[k] = b[k] + (hx * ei[k] + hy * ep[k]) / S;
+    *ox = glibc::atan2(t[1], t[0]) * (180.0 / M_PI);
+    *oy = glibc::atan2(t[2], sqrt(t[0] * t[0] + t[1] * t[1])) * (180.0 / M_PI);
+}
+
+// one Sutherland-Hodgman pass (clip_edge): returns the output size, or -1 when it exceeds cap
+__device__ inline int64_t clip_pass(const double* ixy, const int32_t* itag, int64_t n, double ax, double ay, double bx,
+                                    double by, double* oxy, int32_t* otag, int64_t cap) {
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int64_t m = 0;
+    for (int64_t base = 0; base < n; base += 64) {
+        const int64_t i = base + lane;
+        int cnt = 0;
+        double qx = 0, qy = 0, cx = 0, cy = 0;
+        int32_t ct = -1;
+        if (i < n) {
+            const int64_t j = i == 0 ? n - 1 : i - 1;
+            cx = ixy[2 * i];
+            cy = ixy[2 * i + 1];
+            ct = itag[i];
+            const double px = ixy[2 * j], py = ixy[2 * j + 1];
+            const double sc = (bx - ax) * (cy - ay) - (by - ay) * (cx - ax);
+            const double sp = (bx - ax) * (py - ay) - (by - ay) * (px - ax);
+            const bool ic = sc >= 0, ip = sp >= 0;
+            if (ic != ip) {
+                const double t = sp / (sp - sc);
+                qx = px + t * (cx - px);
+                qy = py + t * (cy - py);
+            }
+            cnt = ic ? (ip ? 1 : 2) : (ip ? 1 : 0);
+            // emitted: ic && !ip: [q, cur]; ic && ip: [cur]; !ic && ip: [q]
+            if (!ic && ip) {
+                cx = qx;
+                cy = qy;
+                ct = -1;
+            }
+        }
+        const unsigned long long b1 = __ballot(cnt >= 1), b2 = __ballot(cnt == 2);
+        const int64_t pre = m + __popcll(b1 & lt) + __popcll(b2 & lt);
+        const int64_t tot = __popcll(b1) + __popcll(b2);
+        if (m + tot > cap) return -1;
+        if (cnt == 2) {
+            oxy[2 * pre] = qx;
+            oxy[2 * pre + 1] = qy;
+            otag[pre] = -1;
+            oxy[2 * pre + 2] = cx;
+            oxy[2 * pre + 3] = cy;
+            otag[pre + 1] = ct;
+        } else if (cnt == 1) {
+            oxy[2 * pre] = cx;
+            oxy[2 * pre + 1] = cy;
+            otag[pre] = ct;
+        }
+        m += tot;
+    }
+    return m;
+}
+
+__global__ void __launch_bounds__(256) k_tess_clip(ClipArgs a) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    double* bxy[2] = {a.sxy + wave * 4 * a.cap, a.sxy + wave * 4 * a.cap + 2 * a.cap};
+    int32_t* btag[2] = {a.stag + wave * 2 * a.cap, a.stag + wave * 2 * a.cap + a.cap};
+    for (int64_t t = wave; t < a.n_tasks; t += n_waves) {
+        const int64_t k = a.tasks[t];
+        const int g = a.cand_geom[k];
+        const double* P = a.clip + 2 * (int64_t)a.nv * k;
+        const int face = a.mode == 0 ? a.gface[g] : 0;
+        bool redo = false;
+        const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
+        for (int64_t p = p0; p < p1 && !redo; p++) {
+            bool any = false;
+            double net = 0;
+            const int64_t r0 = a.part_rings[p];
+            for (int64_t r = r0; r < a.part_rings[p + 1]; r++) {
+                const int64_t vb = a.ring_offsets[r], n_closed = a.ring_offsets[r + 1] - vb;
+                if (n_closed < 4) continue;
+                const int64_t n = n_closed - 1;  // open vertex list
+                if (n > a.cap) {
+                    redo = true;
+                    break;
+                }
+                for (int64_t i = lane; i < n; i += 64) {
+                    bxy[0][2 * i] = a.pxy[2 * (vb + i)];
+                    bxy[0][2 * i + 1] = a.pxy[2 * (vb + i) + 1];
+                    btag[0][i] = (int32_t)i;
+                }
+                wave_sync_global();
+                int cur = 0;
+                int64_t m = n;
+                for (int e = 0; e < a.nv && m > 0; e++) {
+                    const int f = e + 1 == a.nv ? 0 : e + 1;
+                    m = clip_pass(bxy[cur], btag[cur], m, P[2 * e], P[2 * e + 1], P[2 * f], P[2 * f + 1], bxy[cur ^ 1],
+                                  btag[cur ^ 1], a.cap);
+                    wave_sync_global();
+                    if (m < 0) break;
+                    cur ^= 1;
+                }
+                if (m < 0) {
+                    redo = true;
+                    break;
+                }
+                const bool shell = r == r0;
+                if (m < 3) {
+                    if (shell) break;  // the shell misses the cell
+                    continue;
+                }
+                const double* vx = bxy[cur];
+                double ar = 0;  // ring_area of the closed ring, in order
+                for (int64_t i = 0; i < m; i++) {
+                    const int64_t j = i + 1 == m ? 0 : i + 1;
+                    ar += vx[2 * i] * vx[2 * j + 1] - vx[2 * j] * vx[2 * i + 1];
+                }
+                ar = 0.5 * ar;
+                if (fabs(ar) <= a.area_eps) {
+                    if (shell) break;
+                    continue;
+                }
+                net += shell ? fabs(ar) : -fabs(ar);
+                any = true;
+                unsigned long long off = 0, rid = 0;
+                if (lane == 0) {
+                    off = atomicAdd(&a.counters[0], (unsigned long long)(m + 1));
+                    rid = atomicAdd(&a.counters[1], 1ull);
+                }
+                off = __shfl(off, 0, 64);
+                rid = __shfl(rid, 0, 64);
+                if ((int64_t)(off + m + 1) > a.out_cap || (int64_t)rid >= a.ring_cap) {
+                    redo = true;
+                    break;
+                }
+                const int32_t* tg = btag[cur];
+                for (int64_t i = lane; i <= m; i += 64) {
+                    const int64_t s_ = i == m ? 0 : i;
+                    double ox, oy;
+                    if (tg[s_] >= 0) {
+                        ox = a.gxy[2 * (vb + tg[s_])];
+                        oy = a.gxy[2 * (vb + tg[s_]) + 1];
+                    } else {
+                        clip_to_geo(a, face, vx[2 * s_], vx[2 * s_ + 1], &ox, &oy);
+                    }
+                    a.out[2 * (off + i)] = ox;
+                    a.out[2 * (off + i) + 1] = oy;
+                }
+                if (lane == 0) a.rings[rid] = tessclip::ClipRing{k, (int32_t)(p - p0), (int32_t)(r - r0), (int64_t)off, (int32_t)(m + 1), 0};
+            }
+            if (any && !redo) {
+                unsigned long long pid = 0;
+                if (lane == 0) pid = atomicAdd(&a.counters[2], 1ull);
+                pid = __shfl(pid, 0, 64);
+                if ((int64_t)pid >= a.part_cap) {
+                    redo = true;
+                } else if (lane == 0) {
+                    a.parts[pid] = tessclip::ClipPart{k, (int32_t)(p - p0), net > a.area_eps ? 1 : 0};
+                }
+            }
+        }
+        if (lane == 0) a.redo[t] = redo ? 1 : 0;
+    }
+}
+
 }  // namespace tessgpu
+
+// host side of the border clipping (tess_gpu.h)
+int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                         const int64_t* ring_offsets, const double* pxy, const double* gxy, const int32_t* gface, int res,
+                         int mode, int64_t n_tasks, const int64_t* tasks, const int32_t* cand_geom, int64_t n_cand,
+                         const double* clip, int nv, double area_eps, ClipResult* out) {
+    ENTER(ctx);
+    if (!out || n_geoms < 0 || n_tasks < 0 || nv < 3 || (mode == 0 && (res < 0 || res > 15)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    out->redo.assign((size_t)n_tasks, 0);
+    out->rings.clear();
+    out->parts.clear();
+    out->verts.clear();
+    out->kernel_ms = 0;
+    if (n_tasks == 0) return MOSAIC_OK;
+    const int64_t n_parts = geom_parts[n_geoms], n_rings = part_rings[n_parts], n_verts = ring_offsets[n_rings];
+    int64_t maxn = 1, ring_cap = 0, part_cap = 0;
+    for (int64_t r = 0; r < n_rings; r++) maxn = std::max<int64_t>(maxn, ring_offsets[r + 1] - ring_offsets[r]);
+    for (int64_t t = 0; t < n_tasks; t++) {
+        if (tasks[t] < 0 || tasks[t] >= n_cand) return fail(MOSAIC_E_ARG, "task out of range");
+        const int g = cand_geom[tasks[t]];
+        if (g < 0 || g >= n_geoms || (mode == 0 && (gface[g] < 0 || gface[g] >= 20)))
+            return fail(MOSAIC_E_ARG, "candidate geometry out of range");
+        part_cap += geom_parts[g + 1] - geom_parts[g];
+        ring_cap += part_rings[geom_parts[g + 1]] - part_rings[geom_parts[g]];
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    // per-wave scratch: 2 buffers of cap points; as many waves as a 2 GiB budget holds
+    const int64_t cap = 2 * maxn + 4 * (int64_t)nv + 64, per_wave = 2 * cap * (16 + 4);
+    const int64_t n_waves = std::max<int64_t>(1, std::min<int64_t>({n_tasks, (int64_t)c->n_cu * 8, ((int64_t)2 << 30) / per_wave}));
+    const int64_t out_cap = 2 * n_verts + n_tasks * (3 * (int64_t)nv + 8) + 1024;
+    TmpBuf s_gp, s_pr, s_ro, s_pxy, s_gxy, s_gf, s_cg, s_clip, s_tasks, s_sxy, s_stag, s_out, s_cnt, s_rings, s_parts, s_redo;
+    int rc;
+    auto up = [&](TmpBuf& b, const void* src, size_t bytes) -> int {
+        int e = b.reserve(std::max<size_t>(bytes, 16));
+        if (e) return e;
+        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        return MOSAIC_OK;
+    };
+    if ((rc = up(s_gp, geom_parts, (size_t)(n_geoms + 1) * 8)) || (rc = up(s_pr, part_rings, (size_t)(n_parts + 1) * 8)) ||
+        (rc = up(s_ro, ring_offsets, (size_t)(n_rings + 1) * 8)) || (rc = up(s_pxy, pxy, (size_t)n_verts * 16)) ||
+        (rc = up(s_gxy, gxy, (size_t)n_verts * 16)) || (rc = up(s_gf, gface, mode == 0 ? (size_t)n_geoms * 4 : 0)) ||
+        (rc = up(s_cg, cand_geom, (size_t)n_cand * 4)) || (rc = up(s_clip, clip, (size_t)n_cand * nv * 16)) ||
+        (rc = up(s_tasks, tasks, (size_t)n_tasks * 8)) || (rc = s_sxy.reserve((size_t)(n_waves * 4 * cap) * 8)) ||
+        (rc = s_stag.reserve((size_t)(n_waves * 2 * cap) * 4)) || (rc = s_out.reserve((size_t)out_cap * 16)) ||
+        (rc = s_cnt.reserve(32)) || (rc = s_rings.reserve((size_t)std::max<int64_t>(ring_cap, 1) * sizeof(tessclip::ClipRing))) ||
+        (rc = s_parts.reserve((size_t)std::max<int64_t>(part_cap, 1) * sizeof(tessclip::ClipPart))) ||
+        (rc = s_redo.reserve((size_t)n_tasks)))
+        return rc;
+    HIP_TRY(hipMemsetAsync(s_cnt.p, 0, 32, c->stream));
+    tessgpu::ClipArgs a;
+    a.pxy = (const double*)s_pxy.p;
+    a.gxy = (const double*)s_gxy.p;
+    a.ring_offsets = (const int64_t*)s_ro.p;
+    a.part_rings = (const int64_t*)s_pr.p;
+    a.geom_parts = (const int64_t*)s_gp.p;
+    a.cand_geom = (const int32_t*)s_cg.p;
+    a.gface = (const int32_t*)s_gf.p;
+    a.clip = (const double*)s_clip.p;
+    a.nv = nv;
+    a.res = res;
+    a.mode = mode;
+    a.area_eps = area_eps;
+    a.tasks = (const int64_t*)s_tasks.p;
+    a.n_tasks = n_tasks;
+    a.sxy = (double*)s_sxy.p;
+    a.stag = (int32_t*)s_stag.p;
+    a.cap = cap;
+    a.out = (double*)s_out.p;
+    a.counters = (unsigned long long*)s_cnt.p;
+    a.out_cap = out_cap;
+    a.ring_cap = ring_cap;
+    a.part_cap = part_cap;
+    a.rings = (tessclip::ClipRing*)s_rings.p;
+    a.parts = (tessclip::ClipPart*)s_parts.p;
+    a.redo = (uint8_t*)s_redo.p;
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return fail(MOSAIC_E_HIP, "hipEventCreate failed");
+    }
+    auto run = [&]() -> int {
+        HIP_TRY(hipEventRecord(e0, c->stream));
+        hipLaunchKernelGGL(tessgpu::k_tess_clip, dim3((unsigned)((n_waves + 3) / 4)), dim3(256), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(e1, c->stream));
+        unsigned long long cnt[3];
+        HIP_TRY(hipMemcpyAsync(cnt, s_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(out->redo.data(), s_redo.p, (size_t)n_tasks, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        const int64_t nv_out = std::min<int64_t>((int64_t)cnt[0], out_cap), nr = std::min<int64_t>((int64_t)cnt[1], ring_cap),
+                      np = std::min<int64_t>((int64_t)cnt[2], part_cap);
+        out->verts.resize((size_t)nv_out * 2);
+        out->rings.resize((size_t)nr);
+        out->parts.resize((size_t)np);
+        if (nv_out) HIP_TRY(hipMemcpyAsync(out->verts.data(), s_out.p, (size_t)nv_out * 16, hipMemcpyDeviceToHost, c->stream));
+        if (nr) HIP_TRY(hipMemcpyAsync(out->rings.data(), s_rings.p, (size_t)nr * sizeof(tessclip::ClipRing), hipMemcpyDeviceToHost, c->stream));
+        if (np) HIP_TRY(hipMemcpyAsync(out->parts.data(), s_parts.p, (size_t)np * sizeof(tessclip::ClipPart), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        out->kernel_ms = ms;
+        return MOSAIC_OK;
+    };
+    rc = run();
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
 
 extern "C" {
 

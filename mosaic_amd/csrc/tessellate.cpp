@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/mosaic_hip.h"
+#include "tess_gpu.h"
 #include "bng_device.h"
 #include "h3_device.h"
 
@@ -75,8 +76,9 @@ struct FacePlane {
     P2 to_geo(P2 h) const {
         double t[3];
         for (int k = 0; k < 3; k++) t[k] = fc[k] + (h.x * ei[k] + h.y * ep[k]) / S;
-        double n = sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
-        return {atan2(t[1], t[0]) * (180.0 / M_PI), asin(t[2] / n) * (180.0 / M_PI)};
+        // (latitude as atan2(z, |xy|): the same function as the longitude, so the GPU clipper's
+        // restatement of glibc atan2 (glibc_math.h) maps computed vertices bit for bit)
+        return {atan2(t[1], t[0]) * (180.0 / M_PI), atan2(t[2], sqrt(t[0] * t[0] + t[1] * t[1])) * (180.0 / M_PI)};
     }
 };
 
@@ -317,6 +319,47 @@ void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::ve
     cs->add(false, cell.id, key, to_wkb(out_parts));
 }
 
+// The border chips the GPU clipped (tess_gpu.h), indexed by candidate: rings sorted by (candidate,
+// part, ring), parts by (candidate, part).
+struct ClippedChips {
+    tessclip::ClipResult r;
+    std::vector<int64_t> task_of;  // candidate -> task (-1: not a border task)
+    size_t ir = 0, ip = 0;
+    void index(int64_t n_cand, const std::vector<int64_t>& tasks) {
+        std::sort(r.rings.begin(), r.rings.end(), [](const tessclip::ClipRing& a, const tessclip::ClipRing& b) {
+            return a.cand != b.cand ? a.cand < b.cand : (a.part != b.part ? a.part < b.part : a.ring < b.ring);
+        });
+        std::sort(r.parts.begin(), r.parts.end(), [](const tessclip::ClipPart& a, const tessclip::ClipPart& b) {
+            return a.cand != b.cand ? a.cand < b.cand : a.part < b.part;
+        });
+        task_of.assign((size_t)n_cand, -1);
+        for (size_t t = 0; t < tasks.size(); t++) task_of[(size_t)tasks[t]] = (int64_t)t;
+    }
+    bool redo(int64_t k) const { return task_of[(size_t)k] < 0 || r.redo[(size_t)task_of[(size_t)k]]; }
+    // candidate k's chip (candidates are visited in increasing order); false: no chip
+    bool chip(int64_t k, std::vector<uint8_t>& wkb) {
+        while (ir < r.rings.size() && r.rings[ir].cand < k) ir++;
+        while (ip < r.parts.size() && r.parts[ip].cand < k) ip++;
+        std::vector<std::vector<std::vector<P2>>> parts;
+        size_t jr = ir;
+        for (size_t jp = ip; jp < r.parts.size() && r.parts[jp].cand == k; jp++) {
+            const int32_t part = r.parts[jp].part;
+            while (jr < r.rings.size() && r.rings[jr].cand == k && r.rings[jr].part < part) jr++;
+            std::vector<std::vector<P2>> rings;
+            for (; jr < r.rings.size() && r.rings[jr].cand == k && r.rings[jr].part == part; jr++) {
+                const tessclip::ClipRing& cr = r.rings[jr];
+                std::vector<P2> ring((size_t)cr.n);
+                for (int32_t i = 0; i < cr.n; i++) ring[(size_t)i] = P2{r.verts[2 * (cr.off + i)], r.verts[2 * (cr.off + i) + 1]};
+                rings.push_back(std::move(ring));
+            }
+            if (r.parts[jp].keep && !rings.empty()) parts.push_back(std::move(rings));
+        }
+        if (parts.empty()) return false;
+        wkb = to_wkb(parts);
+        return true;
+    }
+};
+
 }  // namespace
 
 extern "C" {
@@ -508,13 +551,28 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     int rc = mosaic_tess_classify_poly(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), n_cand,
                                        cg.data(), clip.data(), nv, 1e-3, cls.data());
     if (rc) return rc;
+    // border cells clipped on the GPU (k_tess_clip); a cell the kernel could not finish is clipped here
+    std::vector<int64_t> tasks;
+    for (int64_t k = 0; k < n_cand; k++)
+        if (cls[k] == 2) tasks.push_back(k);
+    ClippedChips cc;
+    if ((rc = tessclip::clip_border(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), xy, gface.data(), res, 0,
+                                    (int64_t)tasks.size(), tasks.data(), cg.data(), n_cand, clip.data(), nv, 1e-12,
+                                    &cc.r)))
+        return rc;
+    cc.index(n_cand, tasks);
     mosaic_chip_set* cs = new mosaic_chip_set();
     std::vector<std::vector<std::vector<P2>>> geo, pl;
     FacePlane fp;
     fp.init(0, res);  // re-initialised per geometry below
     int64_t cur = -1;
+    std::vector<uint8_t> blob;
     for (int64_t k = 0; k < n_cand; k++) {
         if (!cls[k]) continue;
+        if (cls[k] == 2 && !cc.redo(k)) {
+            if (cc.chip(k, blob)) cs->add(false, cid[k], cg[k], blob);
+            continue;
+        }
         if (cg[k] != cur) {
             cur = cg[k];
             fp.init(gface[cur], res);
@@ -598,11 +656,32 @@ int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, c
     int rc = mosaic_tess_classify_bng(ctx, n_geoms, geom_parts, part_rings, ring_offsets, xy, n_cand, cg.data(),
                                       cij.data(), e, 1e-9 * e, cls.data());
     if (rc) return rc;
+    // border cells clipped on the GPU (k_tess_clip, identity mapping) against the squares emit_cell uses
+    std::vector<int64_t> tasks;
+    for (int64_t k = 0; k < n_cand; k++)
+        if (cls[k] == 2) tasks.push_back(k);
+    std::vector<double> sq((size_t)n_cand * 8);
+    for (int64_t k = 0; k < n_cand; k++) {
+        const double cx0 = cij[2 * k] * e, cy0 = cij[2 * k + 1] * e;
+        const double v[8] = {cx0, cy0, cx0 + e, cy0, cx0 + e, cy0 + e, cx0, cy0 + e};
+        memcpy(sq.data() + 8 * k, v, sizeof v);
+    }
+    ClippedChips cc;
+    if ((rc = tessclip::clip_border(ctx, n_geoms, geom_parts, part_rings, ring_offsets, xy, xy, nullptr, 0, 1,
+                                    (int64_t)tasks.size(), tasks.data(), cg.data(), n_cand, sq.data(), 4, 1e-12 * e * e,
+                                    &cc.r)))
+        return rc;
+    cc.index(n_cand, tasks);
     mosaic_chip_set* cs = new mosaic_chip_set();
     std::vector<std::vector<std::vector<P2>>> geo;
+    std::vector<uint8_t> blob;
     int64_t cur = -1;
     for (int64_t k = 0; k < n_cand; k++) {
         if (!cls[k]) continue;
+        if (cls[k] == 2 && !cc.redo(k)) {
+            if (cc.chip(k, blob)) cs->add(false, cid[k], cg[k], blob);
+            continue;
+        }
         if (cg[k] != cur) {
             cur = cg[k];
             geo.clear();

@@ -32,6 +32,11 @@ case $STEP in
     run t_rbw 600 $PYT tests/test_raster_build.py -s
     run build_prof 300 python -u tools/build_prof.py
     ;;
+  clip)
+    run t_clip 900 $PYT tests/test_tessellate_gpu.py tests/test_raster_build.py -s
+    run build_prof 300 python -u tools/build_prof.py
+    run kb_tess 300 python -u tools/kbench_tess.py
+    ;;
   cfg)
     run t_cfg 900 $PYT tests/test_gpu_configs.py tests/test_tessellate_gpu.py -s
     ;;
