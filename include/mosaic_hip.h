@@ -99,7 +99,10 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * entries, or an entry budget <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of
  * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
  * host-resident coordinates: the next chunk's copy overlaps the current chunk's join; 0 = stage the
- * whole batch; default 2^25), "mixed_rows" (1/2/4, default 2), "mixed_blocks_per_cu". */
+ * whole batch; default 2^25), "mixed_rows" (1/2/4, default 2), "mixed_blocks_per_cu", "stream_pipe"
+ * (0/1: the software-pipelined stream kernel where it applies; default 1), "bng_lds" (0/1: BNG tables
+ * built afterwards carry an LDS cell level for the BNG stream kernel; default 1), "bng_cell" (sub-cells
+ * per BNG border cell side in those tables, a power of two <= 64; default 32). */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* The calling thread's hipStream_t (created by the context unless set by this thread). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
@@ -217,7 +220,9 @@ int mosaic_chip_table_info(const mosaic_chips* chips, int64_t* out8);
 /* H3 tile directory of the table (built when option "tiles" = 1, the default): out13 = built (0/1),
  * tiles along lon, tiles along lat, tile records, window entries, tiles on the generic path, rings;
  * point raster (option "point_raster" = 1, the default) built (0/1), sub-blocks per tile side,
- * cells per sub-block side, pure sub-blocks, mixed sub-blocks, mixed cells. */
+ * cells per sub-block side, pure sub-blocks, mixed sub-blocks, mixed cells.  BNG tables report their
+ * dense cell table instead in the first five: built (0/1), cells along e, cells along n, bytes of the
+ * LDS cell level (option "bng_lds"), its block shift, mixed border-cell sub-cells, line-record sub-cells. */
 int mosaic_chip_table_tiles(const mosaic_chips* chips, int64_t* out13);
 /* out4 = lon, lat of the tile grid origin and tiles per degree along lon, lat (tile i covers
  * [x0 + i / sx, x0 + (i + 1) / sx)). */

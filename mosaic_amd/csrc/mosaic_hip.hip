@@ -534,7 +534,28 @@ struct StreamArgs {
     const uint32_t* qrec;
     int32_t n_qrec, n_qrec_words, qrl;
 };
+// per-wave mixed-row stage of the stream kernels (words): rows are appended one slot (<= 64 rows)
+// at a time and flushed at >= 64
+static const int kStageWords = 128;
 static const uint32_t kNoLoad = 0x7ffffff0u;  // out-of-range buffer offset (every table is < 2 GiB)
+// cache-policy bits (aux) of the stream kernels' gathers: sub-block entries, line records, leaf
+// codes, BNG sub-cell entries (build-time A/B knobs; 2 = nt)
+#ifndef MOSAIC_AUX_SUB
+#define MOSAIC_AUX_SUB 0
+#endif
+#ifndef MOSAIC_AUX_LINE
+#define MOSAIC_AUX_LINE 0
+#endif
+#ifndef MOSAIC_AUX_LEAF
+#define MOSAIC_AUX_LEAF 0
+#endif
+#ifndef MOSAIC_AUX_BNG
+#define MOSAIC_AUX_BNG 0
+#endif
+// k_join_stream_pipe: groups of coordinates in flight ahead of the one being looked up (1 or 2)
+#ifndef MOSAIC_PIPE_DEPTH
+#define MOSAIC_PIPE_DEPTH 1
+#endif
 
 typedef double v2d __attribute__((ext_vector_type(2)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -640,7 +661,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         for (int k = 0; k < 4; k++) {
             const uint32_t local = (((iyC[k] >> s.cs) & qm) << s.qs) | ((ixC[k] >> s.cs) & qm);
             const uint32_t off = ((((qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
-            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, qv[k] >= 0x8000u ? off : kNoLoad, 0, 0);
+            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, qv[k] >= 0x8000u ? off : kNoLoad, 0, MOSAIC_AUX_SUB);
         }
         // stage C: leaf codes and line records of the points in mixed sub-blocks
         uint32_t leaf[4];
@@ -695,29 +716,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
                 const unsigned long long mm = __ballot(m);
                 if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(w0, k) - a.row_lo);
                 wn += (uint32_t)__popcll(mm);
-            }
-            if (wn >= 64) {  // flush: one atomic per >= 64 rows
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
-                base = __shfl(base, 0, 64);
-                for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
-                __builtin_amdgcn_wave_barrier();
-                wn = 0;
+                stage_flush(a, wq, wn, lane, 64);  // one atomic per >= 64 rows; the stage holds < 128
             }
         }
     }
-    if (wn) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
-        base = __shfl(base, 0, 64);
-        for (uint32_t q = (uint32_t)lane; q < wn; q += 64) a.mixq[base + q] = wq[q];
-    }
+    stage_flush(a, wq, wn, lane, 1);
     if (LDS_COUNTS) {
         __syncthreads();
         for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
@@ -794,7 +797,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             g.tbv[k] = tb[__umul24(iyC >> s.tsh, (uint32_t)s.tnx) + (ixC >> s.tsh)];
             const uint32_t local = (((iyC >> s.cs) & qm) << s.qs) | ((ixC >> s.cs) & qm);
             const uint32_t off = ((((g.qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
-            g.code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, g.qv[k] >= 0x8000u ? off : kNoLoad, 0, 0);
+            g.code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, g.qv[k] >= 0x8000u ? off : kNoLoad, 0, MOSAIC_AUX_SUB);
         }
     };
     // stage B: sub-block entries -> leaf and line gathers
@@ -808,8 +811,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const uint32_t n = c & 0x3fffu;
             const uint32_t loff = (g.tbv[k] + (n << (2 * s.cs)) + g.lf[k]) << 1;
             const uint32_t roff = (g.tbv[k] - 8u * (n + 1u)) << 1;
-            g.leaf[k] = __builtin_amdgcn_raw_buffer_load_b16(rblk, (blk && !line) ? loff : kNoLoad, 0, 0);
-            g.lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rblk, line ? roff : kNoLoad, 0, 0);
+            g.leaf[k] = __builtin_amdgcn_raw_buffer_load_b16(rblk, (blk && !line) ? loff : kNoLoad, 0, MOSAIC_AUX_LEAF);
+            g.lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rblk, line ? roff : kNoLoad, 0, MOSAIC_AUX_LINE);
         }
     };
     // stage D: the answers -> counts and the mixed-row stage
@@ -845,18 +848,22 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
                 const unsigned long long mm = __ballot(m);
                 if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(wb, k) - a.row_lo);
                 wn += (uint32_t)__popcll(mm);
+                stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
             }
-            stage_flush(a, wq, wn, lane, 64);
         }
     };
-    v2d px[2], py[2];
-    auto load4 = [&](int64_t wb, bool valid) {  // unconditional: invalid groups re-read the wave's first rows
-        const int64_t r = valid ? wb + 2 * lane : wbase + 2 * lane;
-        px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
-        px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
-        py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
-        py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
+    // coordinates of the next MOSAIC_PIPE_DEPTH groups (1: loaded one iteration ahead; 2: two)
+    struct Coords {
+        v2d px[2], py[2];
     };
+    auto load4 = [&](Coords& cb, int64_t wb, bool valid) {  // unconditional: invalid groups re-read the wave's first rows
+        const int64_t r = valid ? wb + 2 * lane : wbase + 2 * lane;
+        cb.px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
+        cb.px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
+        cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
+        cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
+    };
+    Coords cb0, cb1;
     // two group slots used in turn (no copies of registers that loads are still landing in):
     // iteration t finishes the slot holding t - 2, advances the one holding t - 1, refills the first
     PipeGroup g0, g1;
@@ -867,20 +874,23 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         g0.tbv[k] = g1.tbv[k] = g0.lf[k] = g1.lf[k] = 0u;
         g0.u[k] = g1.u[k] = g0.v[k] = g1.v[k] = 0.0f;
     }
-    auto step = [&](int64_t t, PipeGroup& gfin, PipeGroup& gadv) {
+    auto step = [&](int64_t t, PipeGroup& gfin, PipeGroup& gadv, Coords& cb, Coords& cn) {
         const bool all[4] = {true, true, true, true};
         if (t >= 2) stage_d(gfin, wbase + (t - 2) * stride);
         stage_b(gadv);  // (invalid groups gather nothing)
-        const double x[4] = {px[0].x, px[0].y, px[1].x, px[1].y}, y[4] = {py[0].x, py[0].y, py[1].x, py[1].y};
+        const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
+        const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
         stage_a(x, y, all, t < T, gfin);
-        load4(wbase + (t + 1) * stride, t + 1 < T);
+        if (MOSAIC_PIPE_DEPTH == 2) load4(cb, wbase + (t + 2) * stride, t + 2 < T);  // cb is free again
+        else load4(cn, wbase + (t + 1) * stride, t + 1 < T);
     };
     if (T > 0) {
-        load4(wbase, true);
+        load4(cb0, wbase, true);
+        if (MOSAIC_PIPE_DEPTH == 2) load4(cb1, wbase + stride, 1 < T);
         for (int64_t t = 0; t < T + 2; t += 2) {
-            step(t, g0, g1);
+            step(t, g0, g1, cb0, cb1);
             if (t + 1 >= T + 2) break;
-            step(t + 1, g1, g0);
+            step(t + 1, g1, g0, cb1, cb0);
         }
     }
     // the wave's partial group (rows past its last full group), unpipelined
@@ -1759,8 +1769,10 @@ __global__ void __launch_bounds__(256) k_bng_cell_wkb(const int64_t* ids, const 
 // L2-resident gather per point (two in border cells) decides all but the rows in mixed sub-cells
 // (and rows outside that integer range), which go to the mixed queue and k_join_mixed_bng (the
 // generic point_to_index + probe + chip loop).
-// Border cells carry kBngLeaf | block: C x C codes over the cell (the H3 point raster's codes,
-// tiles_build.cpp bng_leaf_blocks); kMixed codes send the row to the mixed queue.
+// Border cells carry kBngLeaf | base: C x C sub-cell entries at leaf[base] (the H3 point raster's
+// codes, tiles_build.cpp bng_leaf_blocks) -- a code, kMixed (the row goes to the mixed queue) or
+// kSubBlock | kLineBit | n: the sub-cell is split by one straight chip edge, LineRec n of the cell at
+// leaf[base - 8 (n + 1)] decides the point from its offset in the sub-cell.
 static const uint32_t kBngPure = 0x80000000u, kBngLeaf = 0x40000000u;
 
 // k_join_stream_bng: the dense table's answer for every point, branch-free, in the layout of
@@ -1771,26 +1783,38 @@ static const uint32_t kBngPure = 0x80000000u, kBngLeaf = 0x40000000u;
 // the 2e-9 the reciprocal and the offset move it), one 4-byte cell gather and, in border cells, one
 // 2-byte leaf gather, both through buffer descriptors (lanes that need none pass an out-of-range
 // offset).  NaN coordinates set flags bit 0 (the reference throws IllegalStateException).
+//
+// LDS cell level (when the table is built with one and it fits the workgroup's LDS): one byte per
+// 2^lsh x 2^lsh block of table cells, copied to LDS at kernel start -- 0: no chip cell in the block,
+// 1..0xFE: every cell of the block is a pure cell whose answer is that code (key + 1), 0xFF: gather
+// the cell's table entry.  Points in pure and empty cells then need no gather at all.
+static const uint32_t kBngLdsGather = 0xFFu;
 struct BngStreamArgs {
     int32_t e0, n0, ne, nn, C;
     double inv_div, div, f;  // 1 / divisor (rounded), divisor, C / divisor
     const uint32_t* cells;
     const uint16_t* leaf;
     uint32_t cells_bytes, leaf_bytes;
+    const uint32_t* lcell;   // LDS cell level (bytes packed in words); nullptr / lcell_words == 0: none
+    int32_t lcell_words, lsh, lnx;
 };
 template <bool LDS_COUNTS, bool PAIRS, bool VEC>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_bng(JoinArgs a, BngStreamArgs s) {
     extern __shared__ unsigned int lds[];
     const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
     uint32_t* stage = lds + ncw;
+    uint32_t* lcw = stage + (int)(blockDim.x >> 6) * kStageWords;
+    const uint8_t* lcell = (const uint8_t*)lcw;
+    const bool use_lc = s.lcell_words > 0;  // (uniform)
     for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
+    for (int k = threadIdx.x; k < s.lcell_words; k += blockDim.x) lcw[k] = s.lcell[k];
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rcell = stream_rsrc(s.cells, s.cells_bytes);
     const __amdgpu_buffer_rsrc_t rleaf = stream_rsrc(s.leaf, s.leaf_bytes);
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint32_t* wq = stage + wave * 320;
+    uint32_t* wq = stage + wave * kStageWords;
     uint32_t wn = 0;
     bool nan_seen = false;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
@@ -1825,6 +1849,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             }
         }
         uint32_t code[4], e[4], loff[4];
+        float su[4], sv[4];
         bool inr[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -1835,22 +1860,43 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const int32_t qe = (int32_t)fma((double)eI, s.inv_div, 1e-7), qn = (int32_t)fma((double)nI, s.inv_div, 1e-7);
             const int32_t ce = qe - s.e0, cn = qn - s.n0;
             const bool cell_in = inr[k] && (uint32_t)ce < (uint32_t)s.ne && (uint32_t)cn < (uint32_t)s.nn;
-            e[k] = __builtin_amdgcn_raw_buffer_load_b32(rcell, cell_in ? (uint32_t)(cn * s.ne + ce) << 2 : kNoLoad, 0, 0);
+            // LDS cell level first: only cells it marks kBngLdsGather gather their table entry
+            const uint32_t li = cell_in ? __umul24((uint32_t)cn >> s.lsh, (uint32_t)s.lnx) + ((uint32_t)ce >> s.lsh) : 0u;
+            const uint32_t lb = use_lc ? (uint32_t)lcell[li] : kBngLdsGather;
+            const bool gth = cell_in && lb == kBngLdsGather;
+            e[k] = __builtin_amdgcn_raw_buffer_load_b32(rcell, gth ? (uint32_t)(cn * s.ne + ce) << 2 : kNoLoad, 0, 0);
+            e[k] = (gth || !cell_in) ? e[k] : (lb ? (kBngPure | lb) : 0u);
             // sub-cell of the point inside the cell [qe div, (qe + 1) div) x [qn div, (qn + 1) div)
-            int sx = (int)((x[k] - (double)qe * s.div) * s.f), sy = (int)((y[k] - (double)qn * s.div) * s.f);
+            const double gxs = (x[k] - (double)qe * s.div) * s.f, gys = (y[k] - (double)qn * s.div) * s.f;
+            int sx = (int)gxs, sy = (int)gys;
             sx = min(max(sx, 0), (int)C - 1);
             sy = min(max(sy, 0), (int)C - 1);
+            su[k] = (float)(gxs - (double)sx);  // offset in the sub-cell (sub-cell units)
+            sv[k] = (float)(gys - (double)sy);
             loff[k] = (uint32_t)(sy * (int)C + sx);
         }
+        bool leafc[4], line[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const bool leafc = (e[k] & (kBngPure | kBngLeaf)) == kBngLeaf;
-            const uint32_t off = (((e[k] & ~kBngLeaf) * C * C) + loff[k]) << 1;
-            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rleaf, leafc ? off : kNoLoad, 0, 0);
+            leafc[k] = (e[k] & (kBngPure | kBngLeaf)) == kBngLeaf;
+            const uint32_t off = ((e[k] & ~kBngLeaf) + loff[k]) << 1;
+            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rleaf, leafc[k] ? off : kNoLoad, 0, MOSAIC_AUX_BNG);
+        }
+        v4u lrec[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            line[k] = leafc[k] && (code[k] & 0xC000u) == 0xC000u && code[k] != (uint32_t)tiles::kMixed;
+            const uint32_t roff = ((e[k] & ~kBngLeaf) - 8u * ((code[k] & 0x3fffu) + 1u)) << 1;
+            lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rleaf, line[k] ? roff : kNoLoad, 0, 0);
         }
         if (VEC) load4(w0 + stride);
 #pragma unroll
         for (int k = 0; k < 4; k++) {
+            // tiles::line_code, as selects
+            const float lv = fmaf(__uint_as_float(lrec[k].x), su[k], fmaf(__uint_as_float(lrec[k].y), sv[k], __uint_as_float(lrec[k].z)));
+            uint32_t lc = lv >= 1.0f ? (lrec[k].w & 0xffffu) : (uint32_t)tiles::kMixed;
+            lc = lv <= -1.0f ? (lrec[k].w >> 16) : lc;
+            code[k] = line[k] ? lc : code[k];
             uint32_t c = (e[k] & kBngPure) ? (e[k] & ~kBngPure) : ((e[k] & kBngLeaf) ? code[k] : (e[k] ? (uint32_t)tiles::kMixed : 0u));
             c = inr[k] ? c : (uint32_t)tiles::kMixed;      // outside the one-to-one range: generic path
             c = (x[k] != x[k] || y[k] != y[k]) ? 0u : c;  // NaN: flagged, no pair
@@ -1874,8 +1920,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
                 const unsigned long long mm = __ballot(m);
                 if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(w0, k) - a.row_lo);
                 wn += (uint32_t)__popcll(mm);
+                stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
             }
-            stage_flush(a, wq, wn, lane, 64);
         }
     }
     stage_flush(a, wq, wn, lane, 1);
@@ -1887,29 +1933,62 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     }
 }
 
-template <bool LDS_COUNTS, bool PAIRS>
+// Rows of the BNG dense table's mixed sub-cells (and rows outside its one-to-one range), R rows per
+// lane: coordinates, cell (BNGIndexSystem.pointToIndex), first hash probe of all R rows issued
+// together (R independent chains per lane, as k_join_mixed), then the raster chip loop per row slot.
+template <bool LDS_COUNTS, bool PAIRS, int R>
 __global__ void __launch_bounds__(256) k_join_mixed_bng(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     __shared__ SlabItem items[4][16];
     counts_init<LDS_COUNTS>(a, lds);
     unsigned int tests = 0;
+    const int lane = (int)(threadIdx.x & 63);
     const int wv = (int)(threadIdx.x >> 6) & 3;
     const unsigned long long total = *a.mixq_count;
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total;
-         base += stride) {
-        const unsigned long long t = base + (threadIdx.x & 63);
-        double x = 0.0, y = 0.0;
-        int64_t i = -1, cell = kEmptyKey;
-        if (t < total) {
-            i = a.row_lo + (int64_t)a.mixq[t];
-            x = a.x[i];
-            y = a.y[i];
-            if (!bng::point_to_index(x, y, a.res, &cell)) cell = kEmptyKey;  // NaN: flagged by the stream
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x * R;
+    for (unsigned long long w0 = ((unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * R; w0 < total;
+         w0 += stride) {
+        int64_t row[R], cell[R];
+        double x[R], y[R];
+        bool live[R];
+        uint32_t cur[R], end[R];
+        uint64_t slot[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const unsigned long long t = w0 + (unsigned long long)(k * 64 + lane);
+            live[k] = t < total;
+            row[k] = a.row_lo + (live[k] ? (int64_t)a.mixq[t] : 0);
         }
-        uint32_t cur, end;
-        probe(a, cell, cur, end);
-        raster_chips<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, lds, items[wv]);
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            x[k] = a.x[row[k]];
+            y[k] = a.y[row[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            // NaN: flagged by the stream kernel, no pair
+            if (!live[k] || !bng::point_to_index(x[k], y[k], a.res, &cell[k])) cell[k] = kEmptyKey;
+            slot[k] = mix64((uint64_t)cell[k]) & a.mask;
+        }
+        HashEntry he[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) he[k] = a.table[slot[k]];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            cur[k] = end[k] = 0;
+            if (cell[k] == kEmptyKey) continue;
+            while (he[k].key != cell[k] && he[k].key != kEmptyKey) {  // linear probing (rare)
+                slot[k] = (slot[k] + 1) & a.mask;
+                he[k] = a.table[slot[k]];
+            }
+            if (he[k].key == cell[k]) {
+                cur[k] = he[k].first;
+                end[k] = he[k].first + he[k].count;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < R; k++)
+            raster_chips<LDS_COUNTS, PAIRS>(a, live[k] ? row[k] : -1, cur[k], end[k], x[k], y[k], tests, lds, items[wv]);
     }
     counts_flush<LDS_COUNTS>(a, lds, tests);
 }
@@ -2230,6 +2309,8 @@ struct Options {
     int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
     int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
+    int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
+    int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
     int mixed_blocks_per_cu = 8;  // k_join_mixed grid
     int mixed_rows = 2;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
@@ -2388,8 +2469,10 @@ struct mosaic_chips {
     int64_t tile_stats[6] = {0, 0, 0, 0, 0, 0};  // nx, ny, records, entries, kFull tiles, rings
     bool bng_ok = false;  // BNG dense cell table (k_join_stream_bng)
     int32_t bng_e0 = 0, bng_n0 = 0, bng_ne = 0, bng_nn = 0, bng_div = 1, bng_C = 0;
-    DevBuf bng_cells, bng_leaf;
+    DevBuf bng_cells, bng_leaf, bng_lcell;
     size_t bng_leaf_bytes = 0;
+    int32_t bng_lwords = 0, bng_lsh = 0, bng_lnx = 0;  // LDS cell level (BngStreamArgs::lcell); 0 words: none
+    int64_t bng_sub_stats[2] = {0, 0};                 // border-cell sub-cells: kMixed, line records
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
     bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
@@ -2403,7 +2486,7 @@ struct mosaic_chips {
     uint64_t raster_digest = 0;
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf})
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell})
             b->release();
         store.release();
     }
@@ -2557,6 +2640,11 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.stream_block = (int)v;
     } else if (k == "stream_pipe") {
         o.stream_pipe = v ? 1 : 0;
+    } else if (k == "bng_lds") {
+        o.bng_lds = v ? 1 : 0;
+    } else if (k == "bng_cell") {
+        if (v > 64 || !pow2(v)) return fail(MOSAIC_E_ARG, "bng_cell must be a power of two in [1, 64]");
+        o.bng_cell = (int)v;
     } else if (k == "timing") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
         o.timing = (int)v;
@@ -3416,10 +3504,10 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 }
                 tab[at] = ent;
             }
-            // leaf blocks of the border cells (C x C codes, C = option raster_cell: 3.1 m sub-cells at
-            // 100 m resolution with the default 32)
+            // leaf blocks of the border cells (C x C sub-cell entries, C = option bng_cell: 3.1 m
+            // sub-cells at 100 m resolution with the default 32; line records with option raster_lines)
             std::vector<uint16_t> leaf;
-            const int C = c->raster_cell;
+            const int C = c->bng_cell;
             if (!border.empty()) {
                 std::vector<uint32_t> sfirst(capacity, 0), scount(capacity, 0);
                 for (uint64_t q = 0; q < capacity; q++)
@@ -3436,23 +3524,71 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
                 // (leaf offsets are 32-bit buffer offsets in k_join_stream_bng)
-                if (border.size() * C * C * 2 < (size_t)kNoLoad &&
-                    tiles::bng_leaf_blocks(src, border, (double)div, C, threads, leaf)) {
-                    for (size_t b = 0; b < border.size(); b++) tab[border_at[b]] = kBngLeaf | (uint32_t)b;
+                std::vector<uint32_t> lbase;
+                // (leaf element offsets < 2^30, byte offsets below kNoLoad)
+                if (tiles::bng_leaf_blocks(src, border, (double)div, C, c->raster_lines != 0, threads, leaf, lbase) &&
+                    leaf.size() * 2 < (size_t)kNoLoad) {
+                    for (size_t b = 0; b < border.size(); b++) {
+                        tab[border_at[b]] = kBngLeaf | lbase[b];
+                        for (int q = 0; q < C * C; q++) {
+                            const uint16_t v = leaf[lbase[b] + q];
+                            ch->bng_sub_stats[0] += v == tiles::kMixed;
+                            ch->bng_sub_stats[1] += v != tiles::kMixed && (v & 0xC000u) == 0xC000u;
+                        }
+                    }
                     ch->bng_C = C;
                 } else {
                     leaf.clear();
                 }
             }
             if (leaf.empty()) leaf.assign((size_t)C * C, tiles::kMixed);
+            // LDS cell level (BngStreamArgs::lcell): the finest block size 2^lsh whose byte table fits
+            // the stream kernel's LDS beside its counts and 16 per-wave stages
+            std::vector<uint8_t> lcell;
+            int lsh = 0;
+            int64_t lnx = 0;
+            if (c->bng_lds) {
+                const size_t other = (n_polygons <= kLdsCountsMax ? ((size_t)n_polygons + 64) * 4 : 0) + 16 * kStageWords * 4;
+                const size_t budget = kStreamLdsMax > other ? (kStreamLdsMax - other) & ~(size_t)3 : 0;
+                int64_t lny = 0;
+                for (; lsh <= 16; lsh++) {
+                    lnx = (ne + (1 << lsh) - 1) >> lsh;
+                    lny = (nn + (1 << lsh) - 1) >> lsh;
+                    if ((size_t)((lnx * lny + 3) & ~3) <= budget) break;
+                }
+                if (lsh <= 16) {
+                    auto byte_of = [](uint32_t t) -> uint8_t {
+                        if (t == 0) return 0;
+                        if ((t & kBngPure) && (t & ~kBngPure) < kBngLdsGather) return (uint8_t)(t & ~kBngPure);
+                        return (uint8_t)kBngLdsGather;
+                    };
+                    lcell.assign((size_t)((lnx * lny + 3) & ~3), 0);
+                    std::vector<uint8_t> seen(lcell.size(), 0);
+                    for (int64_t j = 0; j < nn; j++)
+                        for (int64_t i = 0; i < ne; i++) {
+                            const size_t b = (size_t)((j >> lsh) * lnx + (i >> lsh));
+                            const uint8_t v = byte_of(tab[(size_t)(j * ne + i)]);
+                            if (!seen[b]) lcell[b] = v, seen[b] = 1;
+                            else if (lcell[b] != v) lcell[b] = (uint8_t)kBngLdsGather;
+                        }
+                }
+            }
             size_t bb = tab.size() * 4, lb = leaf.size() * 2;
-            if ((rc = ch->bng_cells.reserve(bb)) || (rc = ch->bng_leaf.reserve(lb))) {
+            if ((rc = ch->bng_cells.reserve(bb)) || (rc = ch->bng_leaf.reserve(lb)) ||
+                (!lcell.empty() && (rc = ch->bng_lcell.reserve(lcell.size())))) {
                 ch->release_all();
                 delete ch;
                 return rc;
             }
             HIP_TRY(hipMemcpy(ch->bng_cells.p, tab.data(), bb, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(ch->bng_leaf.p, leaf.data(), lb, hipMemcpyHostToDevice));
+            if (!lcell.empty()) {
+                HIP_TRY(hipMemcpy(ch->bng_lcell.p, lcell.data(), lcell.size(), hipMemcpyHostToDevice));
+                ch->bng_lwords = (int32_t)(lcell.size() / 4);
+                ch->bng_lsh = lsh;
+                ch->bng_lnx = (int32_t)lnx;
+                total += lcell.size();
+            }
             ch->bng_leaf_bytes = lb;
             total += lb;
             if (!ch->bng_C) ch->bng_C = C;
@@ -3518,7 +3654,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
                 // LDS quad level: by default as many entries as one k_join_stream workgroup's LDS holds
                 // beside its counts, its per-wave stages (1024 threads) and, when small, tile_base
-                size_t avail = kStreamLdsMax - 16 * 320 * 4 - 1024 -
+                size_t avail = kStreamLdsMax - 16 * kStageWords * 4 - 1024 -
                                (n_polygons <= kLdsCountsMax ? ((size_t)n_polygons + 64) * 4 : 0);
                 const size_t tbytes = tb.tile_idx.size() * 4;
                 if (tbytes <= avail / 3) avail -= tbytes;
@@ -3616,7 +3752,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         sa.n_quad_words = (int32_t)((tb.quad.size() + 1) / 2);
                         sa.n_tiles = (int32_t)tb.tile_base.size();
                         sa.tb_lds = 0;
-                        sa.stage_words = 64 + 256;
+                        sa.stage_words = kStageWords;
                         sa.quad = (const uint32_t*)ch->rquad.p;
                         sa.tile_base = (const uint32_t*)ch->rmid.p;
                         sa.csub = (const uint16_t*)ch->rsub.p + nsub;
@@ -3642,6 +3778,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         sa.qrl = tb.qrec_shift;
                         ch->praster.qrec_mask = nrec ? (const uint32_t*)ch->rqrec.p : nullptr;
                         ch->praster.qrec_code = nrec ? (const uint16_t*)((const uint32_t*)ch->rqrec.p + 2 * nrec) : nullptr;
+
                         ch->praster.n_qrec = (int32_t)nrec;
                         ch->praster.qrec_shift = tb.qrec_shift;
                         ch->stream_ok = true;
@@ -3692,6 +3829,10 @@ int mosaic_chip_table_tiles(const mosaic_chips* ch, int64_t* o) {
         o[0] = ch->bng_ok ? 1 : 0;
         o[1] = ch->bng_ne;
         o[2] = ch->bng_nn;
+        o[3] = (int64_t)ch->bng_lwords * 4;  // LDS cell level: bytes, block shift
+        o[4] = ch->bng_lsh;
+        o[5] = ch->bng_sub_stats[0];  // mixed sub-cells, line sub-cells
+        o[6] = ch->bng_sub_stats[1];
     }
     o[7] = ch->raster_ok ? 1 : 0;
     for (int k = 0; k < 5; k++) o[k + 8] = ch->raster_stats[k];
@@ -3838,7 +3979,13 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             a.mixq = (uint32_t*)c->mix_queue.p;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             const int blkb = c->stream_block;
-            const size_t shm_b = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blkb / 64) * 320 * 4;
+            size_t shm_b = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blkb / 64) * kStageWords * 4;
+            // the LDS cell level when it fits this launch's LDS
+            bs.lcell = (const uint32_t*)ch->bng_lcell.p;
+            bs.lsh = ch->bng_lsh;
+            bs.lnx = ch->bng_lnx;
+            bs.lcell_words = shm_b + (size_t)ch->bng_lwords * 4 <= kStreamLdsMax ? ch->bng_lwords : 0;
+            shm_b += (size_t)bs.lcell_words * 4;
             auto kernel_for = [&](bool vec) -> const void* {
                 if (pairs) return vec ? (const void*)k_join_stream_bng<false, true, true> : (const void*)k_join_stream_bng<false, true, false>;
                 if (lds) return vec ? (const void*)k_join_stream_bng<true, false, true> : (const void*)k_join_stream_bng<true, false, false>;
@@ -3858,14 +4005,21 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 void* kargs[] = {&ac, &bs};
                 HIP_TRY(hipLaunchKernel(kfn, dim3(gs), dim3(blkb), kargs, shm_b, c->stream));
                 if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
-                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + c->block - 1) / c->block,
+                const int gm = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + 4 * c->block - 1) / (4 * c->block),
                                                                            (int64_t)c->n_cu * c->mixed_blocks_per_cu));
-                if (pairs)
-                    hipLaunchKernelGGL((k_join_mixed_bng<false, true>), dim3(gm), dim3(c->block), 0, c->stream, ac);
-                else if (lds)
-                    hipLaunchKernelGGL((k_join_mixed_bng<true, false>), dim3(gm), dim3(c->block), shm, c->stream, ac);
-                else
-                    hipLaunchKernelGGL((k_join_mixed_bng<false, false>), dim3(gm), dim3(c->block), 0, c->stream, ac);
+#define MOSAIC_MIXED_BNG(R_)                                                                                     \
+    do {                                                                                                         \
+        if (pairs) hipLaunchKernelGGL((k_join_mixed_bng<false, true, R_>), dim3(gm), dim3(c->block), 0, c->stream, ac); \
+        else if (lds) hipLaunchKernelGGL((k_join_mixed_bng<true, false, R_>), dim3(gm), dim3(c->block), shm, c->stream, ac); \
+        else hipLaunchKernelGGL((k_join_mixed_bng<false, false, R_>), dim3(gm), dim3(c->block), 0, c->stream, ac); \
+    } while (0)
+                hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
+                if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
+                if (c->mixed_rows == 4) MOSAIC_MIXED_BNG(4);
+                else if (c->mixed_rows == 2) MOSAIC_MIXED_BNG(2);
+                else MOSAIC_MIXED_BNG(1);
+#undef MOSAIC_MIXED_BNG
+                if (mstop) HIP_TRY(hipEventRecord(mstop, c->stream));
                 HIP_TRY(hipGetLastError());
             }
             tstop = nullptr;

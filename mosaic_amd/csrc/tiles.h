@@ -478,8 +478,12 @@ struct BngBorderCell {
     double x0, y0;
     uint32_t slot;
 };
+// BNG border cells (k_join_stream_bng): per cell a C x C block of sub-cell entries -- a code,
+// kMixed, or kSubBlock | kLineBit | n for a sub-cell split by one straight chip edge (LineRec n of
+// the cell, evaluated at the point's offset in the sub-cell in sub-cell units, stored at
+// blocks[base - 8 (n + 1)]); base[k] = element offset of cell k's block (a multiple of 8).
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
-                     int threads, std::vector<uint16_t>& blocks);
+                     bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base);
 
 }  // namespace tiles
 }  // namespace mosaic

@@ -643,14 +643,17 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
 }
 
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
-                     int threads, std::vector<uint16_t>& blocks) {
+                     bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base) {
     if (C < 1 || C > 64) return false;
-    blocks.assign(cells.size() * (size_t)C * C, kMixed);
+    const size_t CC = (size_t)C * C, CCp = (CC + 7) & ~(size_t)7;  // leaf block padded to 16 bytes
+    std::vector<std::vector<uint16_t>> ent(cells.size());
+    std::vector<std::vector<LineRec>> lrec(cells.size());
     std::atomic<int64_t> next(0);
     auto work = [&]() {
         std::vector<Seg> segs;
         std::vector<std::vector<Seg>> csegs;
         std::vector<int32_t> ans;
+        std::vector<P2> ends;
         while (true) {
             const int64_t k = next.fetch_add(1);
             if (k >= (int64_t)cells.size()) break;
@@ -669,11 +672,92 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                 }
             }
             const double h = side / C;
+            // the sub-rectangles are widened past the kernel's index rounding
+            const double ex = 1e-6 * h + 1e-9 * (fabs(bc.x0) + side);
+            const double ey = 1e-6 * h + 1e-9 * (fabs(bc.y0) + side);
+            // answer of the convex polygon q[n] (metres): kMixed when a border chip's segment comes
+            // within ex of it, else the keys containing its vertex mean (contains() is constant on it)
+            auto classify_poly = [&](const P2* q, int n) -> uint16_t {
+                double mx = 0, my = 0, x0 = INFINITY, y0 = INFINITY, x1 = -INFINITY, y1 = -INFINITY;
+                for (int v = 0; v < n; v++) {
+                    mx += q[v].x;
+                    my += q[v].y;
+                    x0 = rbuild::dmin(x0, q[v].x);
+                    y0 = rbuild::dmin(y0, q[v].y);
+                    x1 = rbuild::dmax(x1, q[v].x);
+                    y1 = rbuild::dmax(y1, q[v].y);
+                }
+                mx /= n;
+                my /= n;
+                ans = core;
+                for (size_t b = 0; b < border.size(); b++) {
+                    const pip::Box& bx = src.store.geom_bbox[border[b]];
+                    if (!(bx.maxx < x0 - ex || bx.minx > x1 + ex || bx.maxy < y0 - ey || bx.miny > y1 + ey))
+                        for (const Seg& e : csegs[b])
+                            if (seg_meets_poly(P2{e.ax, e.ay}, P2{e.bx, e.by}, q, n, ex)) return kMixed;
+                    if (pip::contains(src.store, border[b], mx, my)) ans.push_back((int32_t)(src.meta[border[b]] >> 1));
+                }
+                return ans.empty() ? (uint16_t)0 : (ans.size() == 1 ? (uint16_t)(ans[0] + 1) : kMixed);
+            };
+            // a mixed sub-cell whose chip edges all lie along one line (tiles_build try_line, in
+            // sub-cell units): the line through the longest clipped edge, both sides certified
+            auto try_line = [&](int i, int j, LineRec& out) -> bool {
+                const double rx0 = bc.x0 + h * i, ry0 = bc.y0 + h * j;
+                const double exu = ex / h, eyv = ey / h;
+                const double bx0 = rx0 - ex, bx1 = rx0 + h + ex, by0 = ry0 - ey, by1 = ry0 + h + ey;
+                double best = 0.0;
+                P2 pa{0, 0}, pb{0, 0};
+                ends.clear();
+                for (size_t b = 0; b < border.size(); b++) {
+                    const pip::Box& bx = src.store.geom_bbox[border[b]];
+                    if (bx.maxx < bx0 || bx.minx > bx1 || bx.maxy < by0 || bx.miny > by1) continue;
+                    for (const Seg& e : csegs[b]) {
+                        double ax = (e.ax - rx0) / h, ay = (e.ay - ry0) / h;
+                        double qx = (e.bx - rx0) / h, qy = (e.by - ry0) / h;
+                        if (!clip_seg(ax, ay, qx, qy, -exu, -eyv, 1.0 + exu, 1.0 + eyv)) continue;
+                        ends.push_back(P2{ax, ay});
+                        ends.push_back(P2{qx, qy});
+                        const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
+                        if (l2 > best) {
+                            best = l2;
+                            pa = P2{ax, ay};
+                            pb = P2{qx, qy};
+                        }
+                    }
+                }
+                if (!(best > 1e-6)) return false;
+                const double l = sqrt(best);
+                const double a = -(pb.y - pa.y) / l, b = (pb.x - pa.x) / l;
+                const double c = -(a * 0.5 * (pa.x + pb.x) + b * 0.5 * (pa.y + pb.y));
+                double dev_max = 0.0;
+                for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * p.x + b * p.y + c));
+                const P2 sq[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
+                for (int mk = 0; mk < 4; mk++) {
+                    const double margin = rbuild::line_margin(mk);
+                    if (dev_max > margin - 2.0 * kLineSlack) continue;
+                    out.a = (float)(a / margin);
+                    out.b = (float)(b / margin);
+                    out.c = (float)(c / margin);
+                    // certify with the coefficients the device uses (as try_line)
+                    const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - kLineSlack / margin;
+                    P2 hp[8], hn[8];
+                    const int np = clip_half(sq, 4, A, B, Cf - m, hp), nn = clip_half(sq, 4, -A, -B, -Cf - m, hn);
+                    for (int v = 0; v < np; v++) hp[v] = P2{rx0 + h * hp[v].x, ry0 + h * hp[v].y};
+                    for (int v = 0; v < nn; v++) hn[v] = P2{rx0 + h * hn[v].x, ry0 + h * hn[v].y};
+                    const uint16_t cp = np >= 3 ? classify_poly(hp, np) : 0;
+                    if (cp == kMixed) continue;
+                    const uint16_t cn = nn >= 3 ? classify_poly(hn, nn) : 0;
+                    if (cn == kMixed) continue;
+                    out.pos = cp;
+                    out.neg = cn;
+                    return true;
+                }
+                return false;
+            };
+            std::vector<uint16_t>& e = ent[(size_t)k];
+            e.assign(CCp, 0);
             for (int j = 0; j < C; j++)
                 for (int i = 0; i < C; i++) {
-                    // the sub-rectangle, widened past the kernel's index rounding
-                    const double ex = 1e-6 * h + 1e-9 * (fabs(bc.x0) + side);
-                    const double ey = 1e-6 * h + 1e-9 * (fabs(bc.y0) + side);
                     Rect r{bc.x0 + h * i - ex, bc.y0 + h * j - ey, bc.x0 + h * (i + 1) + ex, bc.y0 + h * (j + 1) + ey};
                     const double cxm = bc.x0 + h * (i + 0.5), cym = bc.y0 + h * (j + 0.5);
                     ans = core;
@@ -689,7 +773,12 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                     }
                     uint16_t code = kMixed;
                     if (!mixed) code = ans.empty() ? (uint16_t)0 : (ans.size() == 1 ? (uint16_t)(ans[0] + 1) : kMixed);
-                    blocks[(size_t)k * C * C + (size_t)j * C + i] = code;
+                    LineRec lr;
+                    if (code == kMixed && lines && try_line(i, j, lr)) {
+                        code = (uint16_t)(kSubBlock | kLineBit | lrec[(size_t)k].size());
+                        lrec[(size_t)k].push_back(lr);
+                    }
+                    e[(size_t)j * C + i] = code;
                 }
         }
     };
@@ -698,6 +787,22 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
     for (int t = 1; t < nt; t++) pool.emplace_back(work);
     work();
     for (auto& t : pool) t.join();
+    // layout per border cell: its line records (8 elements each, record n at base - 8 (n + 1)),
+    // then its leaf block at base
+    size_t total = 0;
+    for (size_t k = 0; k < cells.size(); k++) total += lrec[k].size() * 8 + CCp;
+    if (total >= ((size_t)1 << 30)) return false;  // element offsets share a word with the table's flags
+    blocks.assign(total, kMixed);
+    base.assign(cells.size(), 0);
+    size_t at = 0;
+    for (size_t k = 0; k < cells.size(); k++) {
+        const size_t nl = lrec[k].size();
+        for (size_t n = 0; n < nl; n++) memcpy(&blocks[at + 8 * (nl - 1 - n)], &lrec[k][n], sizeof(LineRec));
+        at += 8 * nl;
+        base[k] = (uint32_t)at;
+        memcpy(&blocks[at], ent[k].data(), CCp * 2);
+        at += CCp;
+    }
     return true;
 }
 

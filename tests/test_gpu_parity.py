@@ -441,20 +441,25 @@ def test_join_device_tensors(h3ctx, zones):
     assert np.array_equal(got.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("res", [3, 4])
-def test_join_bng_dense_table(bngctx, res):
+@pytest.mark.parametrize("res,every", [(3, 3), (4, 3), (5, 25)])
+def test_join_bng_dense_table(bngctx, res, every):
     """BNG dense cell table (k_join_stream_bng): tessellated chips of the London postcode zones in
     EPSG:27700 metres (tests/golden/make_bng_fixture.py), uniform points, points on and 1 ulp around
     cell lines, negative and >= 1e7 coordinates (outside the one-to-one range: generic path) --
-    counts equal the oracle's and the generic kernel's."""
+    counts equal the oracle's and the generic kernel's, with and without the LDS cell level (res 5:
+    the level holds blocks of cells, block shift > 0)."""
     from mosaic_amd.context import tessellate
 
-    ids = list(range(0, 177, 3))
+    ids = list(range(0, 177, every))
     proj = PolygonSet.load("london_postcodes_bng").subset(ids)
     chips = tessellate("BNG", proj, res)
     table = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
                               n_polygons=len(ids))
-    assert table.tiles()["built"] == 1
+    ti = table.tiles()
+    assert ti["built"] == 1 and ti["records"] > 0  # LDS cell level bytes
+    lds_budget = 160 * 1024 - (len(ids) + 64) * 4 - 16 * 320 * 4
+    assert (ti["entries"] > 0) == (ti["nx"] * ti["ny"] > lds_budget)  # block shift
+    assert ti["rings"] > 0  # border-cell sub-cells split by one straight edge (line records)
     rng = np.random.default_rng(40 + res)
     x0, y0, x1, y1 = proj.bbox()
     x = rng.uniform(x0 - 2000, x1 + 2000, 400_000)
@@ -490,6 +495,20 @@ def test_join_bng_dense_table(bngctx, res):
         bngctx.set_option("point_raster", 1)
     assert np.array_equal(bngctx.pip_join_count(t2, x, y), want)
     t2.close()
+    # dense cell table without the LDS cell level and line records, 8 x 8 sub-cells
+    for k, v in (("bng_lds", 0), ("raster_lines", 0), ("bng_cell", 8)):
+        bngctx.set_option(k, v)
+    try:
+        t3 = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
+                               n_polygons=len(ids))
+    finally:
+        for k, v in (("bng_lds", 1), ("raster_lines", 1), ("bng_cell", 32)):
+            bngctx.set_option(k, v)
+    assert t3.tiles()["records"] == 0 and t3.tiles()["rings"] == 0
+    assert np.array_equal(bngctx.pip_join_count(t3, x, y), want)
+    r3, k3 = bngctx.pip_join_pairs(t3, x, y)
+    assert np.array_equal(np.sort(r3 * len(ids) + k3), np.sort(rows * len(ids) + keys))
+    t3.close()
     with pytest.raises(IllegalStateException, match="NaN"):
         bngctx.pip_join_count(table, np.array([x0 + 5.0, np.nan]), np.array([y0 + 5.0, y0]))
     table.close()

@@ -20,7 +20,8 @@ def main():
     p.add_argument("--n", type=float, default=1e9)
     p.add_argument("--res", type=int, default=4)
     p.add_argument("--reps", type=int, default=5)
-    p.add_argument("--cells", type=int, default=32, help="leaf sub-cells per border cell side (raster_cell)")
+    p.add_argument("--cells", type=int, default=32, help="sub-cells per border cell side (bng_cell)")
+    p.add_argument("--build-opts", default="", help="comma-separated key=value options set before the table build")
     args = p.parse_args()
     import torch
 
@@ -33,7 +34,10 @@ def main():
     chips = tessellate("BNG", proj, args.res)
     t_tess = time.perf_counter() - t0
     ctx = MosaicContext.build("BNG")
-    ctx.set_option("raster_cell", args.cells)
+    ctx.set_option("bng_cell", args.cells)
+    for kv in filter(None, args.build_opts.split(",")):
+        k, v = kv.split("=")
+        ctx.set_option(k, int(v))
     t0 = time.perf_counter()
     table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
                            n_polygons=len(proj))
@@ -55,11 +59,19 @@ def main():
         torch.cuda.synchronize()
         ts.append(s.elapsed_time(e))
     ctx.set_option("async", 0)
+    ctx.set_option("timing", 2)
+    for _ in range(args.reps):
+        ctx.pip_join_count(table, x, y, out=counts)
+    kt = ctx.kernel_times()
+    ctx.set_option("timing", 0)
     ctx.pip_join_count(table, x, y, out=counts)
     st = ctx.last_stats()
     ms = float(np.median(ts))
     print(json.dumps({"workload": f"BNG res {args.res}, {len(proj)} London zones (EPSG:27700), {n} uniform points",
-                      "ms": ms, "points_per_s": n / ms * 1e3, "GBps": n * 16 / ms / 1e6, "chips": table.info(),
+                      "build_opts": args.build_opts, "raster_cell": args.cells,
+                      "ms": ms, "stream_ms": round(float(np.median(kt[0::2])), 4), "mixed_ms": round(float(np.median(kt[1::2])), 4),
+                      "stream_frac_of_8TBps": round(16.0 * n / (float(np.median(kt[0::2])) * 1e-3) / 8e12, 4),
+                      "points_per_s": n / ms * 1e3, "GBps": n * 16 / ms / 1e6, "chips": table.info(),
                       "tiles": table.tiles(), "tessellate_s": round(t_tess, 2), "build_s": round(t_build, 2),
                       "pair_count": int(counts.sum().item()), "exact_path_rows": st["exact_path_rows"],
                       "contains_tests": st["contains_tests"]}))
