@@ -540,7 +540,11 @@ class MosaicContext:
         """grid_tessellateexplode(geom, res, keepCoreGeom) (MosaicContext.scala functions ->
         MosaicExplode.scala:70-79 -> Mosaic.getChips core/Mosaic.scala:21-87) over a PolygonSet:
         chip columns (is_core, index_id, polygon_key, wkb) with the cell classification on this
-        context's GPU (mosaic_tessellate_gpu)."""
+        context's GPU (mosaic_tessellate_gpu).
+
+        H3 restriction: each geometry must lie on one icosahedron face (true for city- and
+        country-scale inputs such as the NYC and London fixtures); a geometry spanning a face edge
+        raises IllegalArgumentException (MOSAIC_E_ARG), where the reference would tessellate it."""
         return tessellate(self.index_system, polygons, resolution, keep_core_geom, densify, ctx=self)
 
     def chip_table(self, is_core, index_id, wkb_list, polygon_key, resolution, n_polygons=None):

@@ -2328,7 +2328,8 @@ struct ThreadCtx : Options {
     int n_cu = 256;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    double last_tess_classify_ms = 0;  // tessellation classification kernel of the last mosaic_tessellate_gpu
+    double last_tess_classify_ms = 0;  // classification kernel (k_bng_tess_classify / k_tess_classify_poly) of the
+                                       // last mosaic_tessellate_gpu; 0 when it had no candidates
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
     hipStream_t copy_stream = nullptr;
@@ -4609,6 +4610,26 @@ __global__ void __launch_bounds__(256) k_bng_tess_classify(ClassifyArgs a) {
 extern "C" {
 
 // Classification step of mosaic_tessellate_gpu (tessellate.cpp); not part of the public header.
+}  // extern "C"
+
+// Scope guards of the classification entry points: staged buffers and timing events are released
+// on every return path (errors after allocation included)
+struct DevBufGuard {
+    std::vector<DevBuf*> bufs;
+    ~DevBufGuard() {
+        for (DevBuf* b : bufs) b->release();
+    }
+};
+struct EventGuard {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~EventGuard() {
+        for (hipEvent_t x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+};
+
+extern "C" {
+
 int mosaic_tess_classify_bng(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                              const int64_t* ring_offsets, const double* xy, int64_t n_cand, const int32_t* cand_geom,
                              const int64_t* cand_ij, double e, double eps, uint8_t* cls) {
@@ -4616,16 +4637,17 @@ int mosaic_tess_classify_bng(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* ge
     if (!c || n_geoms < 0 || n_cand < 0 || (n_cand > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy ||
                                                             !cand_geom || !cand_ij || !cls)))
         return fail(MOSAIC_E_ARG, "invalid argument");
-    if (n_cand == 0) return MOSAIC_OK;
+    if (n_cand == 0) {
+        c->last_tess_classify_ms = 0;  // (no kernel ran)
+        return MOSAIC_OK;
+    }
     for (int64_t k = 0; k < n_cand; k++)  // the kernel indexes geom_parts[g + 1]
         if (cand_geom[k] < 0 || cand_geom[k] >= n_geoms) return fail(MOSAIC_E_ARG, "candidate geometry out of range");
     HIP_TRY(hipSetDevice(c->device));
     const int64_t n_parts = geom_parts[n_geoms], n_rings = part_rings[n_parts], n_verts = ring_offsets[n_rings];
     DevBuf s_gp, s_pr, s_ro, s_xy, s_cg, s_ij, s_cls;
-    auto done = [&](int rc) {
-        for (DevBuf* b : {&s_gp, &s_pr, &s_ro, &s_xy, &s_cg, &s_ij, &s_cls}) b->release();
-        return rc;
-    };
+    DevBufGuard guard{{&s_gp, &s_pr, &s_ro, &s_xy, &s_cg, &s_ij, &s_cls}};
+    auto done = [&](int rc) { return rc; };  // (the guard releases the buffers)
     int rc;
     const void *dgp, *dpr, *dro, *dxy, *dcg, *dij;
     if ((rc = to_device(c, s_gp, geom_parts, (size_t)(n_geoms + 1) * 8, &dgp)) ||
@@ -4647,9 +4669,10 @@ int mosaic_tess_classify_bng(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* ge
     a.eps = eps;
     a.cls = (uint8_t*)s_cls.p;
     const int64_t blocks = std::min<int64_t>((n_cand + 3) / 4, (int64_t)c->n_cu * 16);  // 4 waves per block
-    hipEvent_t t0, t1;
-    HIP_TRY(hipEventCreate(&t0));
-    HIP_TRY(hipEventCreate(&t1));
+    EventGuard ev;
+    HIP_TRY(hipEventCreate(&ev.e[0]));
+    HIP_TRY(hipEventCreate(&ev.e[1]));
+    hipEvent_t t0 = ev.e[0], t1 = ev.e[1];
     HIP_TRY(hipEventRecord(t0, c->stream));
     hipLaunchKernelGGL(tessgpu::k_bng_tess_classify, dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
@@ -4659,8 +4682,6 @@ int mosaic_tess_classify_bng(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* ge
     float ms = 0;
     (void)hipEventElapsedTime(&ms, t0, t1);
     c->last_tess_classify_ms = ms;
-    (void)hipEventDestroy(t0);
-    (void)hipEventDestroy(t1);
     return done(MOSAIC_OK);
 }
 
@@ -5108,16 +5129,17 @@ int mosaic_tess_classify_poly(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* g
     if (!c || n_geoms < 0 || n_cand < 0 || nv < 3 ||
         (n_cand > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy || !cand_geom || !clip || !cls)))
         return fail(MOSAIC_E_ARG, "invalid argument");
-    if (n_cand == 0) return MOSAIC_OK;
+    if (n_cand == 0) {
+        c->last_tess_classify_ms = 0;  // (no kernel ran)
+        return MOSAIC_OK;
+    }
     for (int64_t k = 0; k < n_cand; k++)
         if (cand_geom[k] < 0 || cand_geom[k] >= n_geoms) return fail(MOSAIC_E_ARG, "candidate geometry out of range");
     HIP_TRY(hipSetDevice(c->device));
     const int64_t n_parts = geom_parts[n_geoms], n_rings = part_rings[n_parts], n_verts = ring_offsets[n_rings];
     DevBuf s_gp, s_pr, s_ro, s_xy, s_cg, s_clip, s_cls;
-    auto done = [&](int rc) {
-        for (DevBuf* b : {&s_gp, &s_pr, &s_ro, &s_xy, &s_cg, &s_clip, &s_cls}) b->release();
-        return rc;
-    };
+    DevBufGuard guard{{&s_gp, &s_pr, &s_ro, &s_xy, &s_cg, &s_clip, &s_cls}};
+    auto done = [&](int rc) { return rc; };  // (the guard releases the buffers)
     int rc;
     const void *dgp, *dpr, *dro, *dxy, *dcg, *dclip;
     if ((rc = to_device(c, s_gp, geom_parts, (size_t)(n_geoms + 1) * 8, &dgp)) ||
@@ -5139,9 +5161,10 @@ int mosaic_tess_classify_poly(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* g
     a.eps = eps;
     a.cls = (uint8_t*)s_cls.p;
     const int64_t blocks = std::min<int64_t>((n_cand + 3) / 4, (int64_t)c->n_cu * 16);
-    hipEvent_t t0, t1;
-    HIP_TRY(hipEventCreate(&t0));
-    HIP_TRY(hipEventCreate(&t1));
+    EventGuard ev;
+    HIP_TRY(hipEventCreate(&ev.e[0]));
+    HIP_TRY(hipEventCreate(&ev.e[1]));
+    hipEvent_t t0 = ev.e[0], t1 = ev.e[1];
     HIP_TRY(hipEventRecord(t0, c->stream));
     hipLaunchKernelGGL(tessgpu::k_tess_classify_poly, dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
@@ -5151,8 +5174,6 @@ int mosaic_tess_classify_poly(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* g
     float ms = 0;
     (void)hipEventElapsedTime(&ms, t0, t1);
     c->last_tess_classify_ms = ms;
-    (void)hipEventDestroy(t0);
-    (void)hipEventDestroy(t1);
     return done(MOSAIC_OK);
 }
 

@@ -494,9 +494,26 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     std::vector<double> pxy((size_t)std::max<int64_t>(n_verts, 1) * 2);
     std::vector<int> gface(n_geoms, -1);
     std::vector<int32_t> cg;
-    std::vector<double> clip;
+    std::vector<double> cxy;  // candidate hexagon centres in the face plane
     std::vector<int64_t> cid;
     const double s60 = 0.86602540378443864676, R = 0.57735026918962576451;
+    // candidate k's (densified) hexagon clip polygon, nv points: the host producer's arithmetic
+    auto fill_clip = [&](int64_t k, double* out_pts) {
+        const double cx = cxy[2 * (size_t)k], cy = cxy[2 * (size_t)k + 1];
+        P2 corners[6];
+        for (int q = 0; q < 6; q++) {
+            double ang = (30.0 + 60.0 * q) * (M_PI / 180.0);
+            corners[q] = {cx + R * cos(ang), cy + R * sin(ang)};
+        }
+        int m = 0;
+        for (int q = 0; q < 6; q++) {
+            P2 a = corners[q], b = corners[(q + 1) % 6];
+            for (int t = 0; t < D; t++) {
+                out_pts[m++] = a.x + (b.x - a.x) * t / D;
+                out_pts[m++] = a.y + (b.y - a.y) * t / D;
+            }
+        }
+    };
     for (int64_t g = 0; g < n_geoms; g++) {
         const int64_t v0 = ring_offsets[part_rings[geom_parts[g]]], v1 = ring_offsets[part_rings[geom_parts[g + 1]]];
         if (v0 == v1) continue;
@@ -527,18 +544,8 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             for (int i = ilo; i <= ihi; i++) {
                 double cx = i - 0.5 * j, cy = j * s60;
                 if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
-                P2 corners[6];
-                for (int k = 0; k < 6; k++) {
-                    double ang = (30.0 + 60.0 * k) * (M_PI / 180.0);
-                    corners[k] = {cx + R * cos(ang), cy + R * sin(ang)};
-                }
-                for (int k = 0; k < 6; k++) {
-                    P2 a = corners[k], b = corners[(k + 1) % 6];
-                    for (int s = 0; s < D; s++) {
-                        clip.push_back(a.x + (b.x - a.x) * s / D);
-                        clip.push_back(a.y + (b.y - a.y) * s / D);
-                    }
-                }
+                cxy.push_back(cx);
+                cxy.push_back(cy);
                 h3::IJK ijk = {i, j, 0};
                 h3::ijk_normalize(ijk);
                 cg.push_back((int32_t)g);
@@ -546,60 +553,77 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             }
         }
     }
+    // candidates in chunks, so the clip polygons staged on the host and the device stay bounded
+    // (<= 64 MB of them per chunk) for any densify and envelope; chips come out in candidate order
     const int64_t n_cand = (int64_t)cg.size();
-    std::vector<uint8_t> cls(n_cand);
-    int rc = mosaic_tess_classify_poly(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), n_cand,
-                                       cg.data(), clip.data(), nv, 1e-3, cls.data());
-    if (rc) return rc;
-    // border cells clipped on the GPU (k_tess_clip); a cell the kernel could not finish is clipped here
+    const int64_t chunk = std::max<int64_t>(1, ((int64_t)64 << 20) / ((int64_t)nv * 16));
+    std::vector<double> clip;
+    std::vector<uint8_t> cls;
     std::vector<int64_t> tasks;
-    for (int64_t k = 0; k < n_cand; k++)
-        if (cls[k] == 2) tasks.push_back(k);
-    ClippedChips cc;
-    if ((rc = tessclip::clip_border(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), xy, gface.data(), res, 0,
-                                    (int64_t)tasks.size(), tasks.data(), cg.data(), n_cand, clip.data(), nv, 1e-12,
-                                    &cc.r)))
-        return rc;
-    cc.index(n_cand, tasks);
     mosaic_chip_set* cs = new mosaic_chip_set();
     std::vector<std::vector<std::vector<P2>>> geo, pl;
     FacePlane fp;
     fp.init(0, res);  // re-initialised per geometry below
     int64_t cur = -1;
     std::vector<uint8_t> blob;
-    for (int64_t k = 0; k < n_cand; k++) {
-        if (!cls[k]) continue;
-        if (cls[k] == 2 && !cc.redo(k)) {
-            if (cc.chip(k, blob)) cs->add(false, cid[k], cg[k], blob);
-            continue;
+    for (int64_t k0 = 0; k0 < n_cand; k0 += chunk) {
+        const int64_t nc = std::min<int64_t>(chunk, n_cand - k0);
+        clip.resize((size_t)nc * nv * 2);
+        for (int64_t k = 0; k < nc; k++) fill_clip(k0 + k, clip.data() + 2 * (size_t)nv * k);
+        cls.assign((size_t)nc, 0);
+        int rc = mosaic_tess_classify_poly(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), nc,
+                                           cg.data() + k0, clip.data(), nv, 1e-3, cls.data());
+        if (rc) {
+            delete cs;
+            return rc;
         }
-        if (cg[k] != cur) {
-            cur = cg[k];
-            fp.init(gface[cur], res);
-            geo.clear();
-            pl.clear();
-            for (int64_t p = geom_parts[cur]; p < geom_parts[cur + 1]; p++) {
-                std::vector<std::vector<P2>> rings, prings;
-                for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
-                    std::vector<P2> ring, pring;
-                    for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) {
-                        ring.push_back({xy[2 * v], xy[2 * v + 1]});
-                        pring.push_back({pxy[2 * v], pxy[2 * v + 1]});
-                    }
-                    rings.push_back(std::move(ring));
-                    prings.push_back(std::move(pring));
-                }
-                geo.push_back(std::move(rings));
-                pl.push_back(std::move(prings));
+        // border cells clipped on the GPU (k_tess_clip); a cell the kernel could not finish is clipped here
+        tasks.clear();
+        for (int64_t k = 0; k < nc; k++)
+            if (cls[k] == 2) tasks.push_back(k);
+        ClippedChips cc;
+        if ((rc = tessclip::clip_border(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), xy, gface.data(), res,
+                                        0, (int64_t)tasks.size(), tasks.data(), cg.data() + k0, nc, clip.data(), nv, 1e-12,
+                                        &cc.r))) {
+            delete cs;
+            return rc;
+        }
+        cc.index(nc, tasks);
+        for (int64_t kk = 0; kk < nc; kk++) {
+            const int64_t k = k0 + kk;
+            if (!cls[kk]) continue;
+            if (cls[kk] == 2 && !cc.redo(kk)) {
+                if (cc.chip(kk, blob)) cs->add(false, cid[k], cg[k], blob);
+                continue;
             }
+            if (cg[k] != cur) {
+                cur = cg[k];
+                fp.init(gface[cur], res);
+                geo.clear();
+                pl.clear();
+                for (int64_t p = geom_parts[cur]; p < geom_parts[cur + 1]; p++) {
+                    std::vector<std::vector<P2>> rings, prings;
+                    for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
+                        std::vector<P2> ring, pring;
+                        for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) {
+                            ring.push_back({xy[2 * v], xy[2 * v + 1]});
+                            pring.push_back({pxy[2 * v], pxy[2 * v + 1]});
+                        }
+                        rings.push_back(std::move(ring));
+                        prings.push_back(std::move(pring));
+                    }
+                    geo.push_back(std::move(rings));
+                    pl.push_back(std::move(prings));
+                }
+            }
+            Cell cell;
+            const double* P = clip.data() + 2 * (size_t)nv * kk;
+            for (int v = 0; v < nv; v++) cell.outline.push_back({P[2 * v], P[2 * v + 1]});
+            cell.clip = cell.outline;
+            cell.id = cid[k];
+            emit_cell(cs, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); }, 1e-12,
+                      (int)cls[kk]);
         }
-        Cell cell;
-        const double* P = clip.data() + 2 * (size_t)nv * k;
-        for (int v = 0; v < nv; v++) cell.outline.push_back({P[2 * v], P[2 * v + 1]});
-        cell.clip = cell.outline;
-        cell.id = cid[k];
-        emit_cell(cs, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); }, 1e-12,
-                  (int)cls[k]);
     }
     *out = cs;
     return MOSAIC_OK;

@@ -155,3 +155,28 @@ def test_h3_gpu_reference_tessellation_fixtures():
         _same(host, gpu)
     assert len(set(gpu["index_id"].tolist())) >= 1
     h3.close()
+
+
+@pytest.mark.parametrize("res,densify", [(9, 1), (9, 16), (10, 64)])
+def test_h3_gpu_tessellation_holes_multipart_duplicates(ctx, res, densify):
+    # H3 chips of a holed, two-part geometry whose rings repeat consecutive vertices (zero-length
+    # segments), an empty geometry and a plain square, at large densify: GPU producer == host producer
+    def sq(x0, y0, s, dup=False):
+        r = [(x0, y0), (x0 + s, y0), (x0 + s, y0 + s), (x0, y0 + s), (x0, y0)]
+        return r[:2] + [r[1]] + r[2:] if dup else r
+
+    rings = [sq(-73.99, 40.70, 0.045, dup=True), sq(-73.975, 40.715, 0.012)[::-1],
+             sq(-73.93, 40.76, 0.02), sq(-73.90, 40.78, 0.015, dup=True), sq(-74.02, 40.62, 0.01)]
+    xy = np.array([p for r in rings for p in r], np.float64)
+    ring_offsets = np.cumsum([0] + [len(r) for r in rings]).astype(np.int64)
+    part_rings = np.array([0, 2, 3, 4, 5], np.int64)
+    geom_parts = np.array([0, 2, 2, 3], np.int64)  # geometry 0: holed part + part; 1: empty; 2: square
+    polys = PolygonSet(xy, ring_offsets, part_rings, geom_parts)
+    h3 = MosaicContext.build("H3", "JTS")
+    for keep in (True, False):
+        host = tessellate("H3", polys, res, densify=densify, keep_core_geom=keep)
+        gpu = tessellate("H3", polys, res, densify=densify, keep_core_geom=keep, ctx=h3)
+        _same(host, gpu)
+    assert set(gpu["polygon_key"].tolist()) == {0, 2}
+    assert gpu["is_core"].sum() > 0 and (gpu["is_core"] == 0).sum() > 0
+    h3.close()

@@ -43,6 +43,9 @@ case $STEP in
     run kb_qc_c3 300 python -u tools/kbench.py --n 1e9 --res 10 --clustered --reps 8
     run kb_qc_c5 300 python -u tools/kbench_bng.py --cells 32
     ;;
+  tess)
+    run t_tess 900 $PYT tests/test_tessellate_gpu.py -s
+    ;;
   tests)
     run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
     ;;
