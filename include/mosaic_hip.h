@@ -295,14 +295,16 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
                                 int32_t* out_left_key, int32_t* out_right_key, uint8_t* out_flag, int64_t cap,
                                 int64_t* n_out);
 
-/* ---- grid_cellkring / grid_cellkloop over a cell column (BNG) ---- */
-/* loop = 0: kRing(cell, k) = the cell, then the loops 1..k; loop = 1: kLoop(cell, k).  Row i's
- * cells go to out[i * stride ..] with stride = 8k (loop) or 1 + 4k(k + 1) (ring), in the
- * reference's order (bottom, right, top, left; cells failing isValid dropped), and
- * out_count[i] = their number (-1 for null rows, valid[i] == 0).  0 <= k <= 1000.  H3 is not
- * implemented (MOSAIC_E_ARG).  Reference: BNGIndexSystem.kRing / kLoop / isValid
- * (core/index/BNGIndexSystem.scala:216-263), grid_cellkring / grid_cellkloop
- * (functions/MosaicContext.scala). */
+/* ---- grid_cellkring / grid_cellkloop over a cell column (BNG, H3) ---- */
+/* loop = 0: kRing(cell, k); loop = 1: kLoop(cell, k).  Row i's cells go to out[i * stride ..] and
+ * out_count[i] = their number (-1 for null rows, valid[i] == 0).  0 <= k <= 1000.
+ * BNG: stride = 8k (loop) or 1 + 4k(k + 1) (ring), the cell then the loops 1..k, in the reference's
+ * order (bottom, right, top, left; cells failing isValid dropped).  Reference: BNGIndexSystem.kRing /
+ * kLoop / isValid (core/index/BNGIndexSystem.scala:216-263).
+ * H3: stride = max(6k, 1) (loop) or 1 + 3k(k + 1) (ring), in H3 v3.7's hexRange / hexRing order
+ * (reference H3IndexSystem.kRing / kLoop, core/index/H3IndexSystem.scala:154-177); a row whose
+ * ring walk reaches a pentagon (where H3 falls back to its hash-ordered _kRingInternal) or whose id
+ * is not a valid cell gets out_count[i] = -2 (unsupported, no cells written). */
 int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k,
                       int loop, int64_t* out, int32_t* out_count);
 

@@ -544,7 +544,7 @@ class MosaicContext:
 
         H3 restriction: each geometry must lie on one icosahedron face (true for city- and
         country-scale inputs such as the NYC and London fixtures); a geometry spanning a face edge
-        raises IllegalArgumentException (MOSAIC_E_ARG), where the reference would tessellate it."""
+        raises MosaicError (MOSAIC_E_ARG), where the reference would tessellate it."""
         return tessellate(self.index_system, polygons, resolution, keep_core_geom, densify, ctx=self)
 
     def chip_table(self, is_core, index_id, wkb_list, polygon_key, resolution, n_polygons=None):
@@ -593,11 +593,19 @@ class MosaicContext:
         ids = np.array([self.index_system.parse(c) for c in cells] if strings else cells, np.int64)
         valid = None
         n = len(ids)
-        stride = 8 * k if loop else 1 + 4 * k * (k + 1)
+        if self.index_system.grid == N.GRID_H3:
+            stride = max(6 * k, 1) if loop else 1 + 3 * k * (k + 1)
+        else:
+            stride = 8 * k if loop else 1 + 4 * k * (k + 1)
         out = np.zeros(max(n * stride, 1), np.int64)
         cnt = np.zeros(max(n, 1), np.int32)
         N.check(N.lib().mosaic_cell_kring(self.handle, self.index_system.grid, N.ptr(ids), valid, n, int(k),
                                           int(loop), N.ptr(out), N.ptr(cnt)))
+        bad = np.nonzero(cnt[:n] == -2)[0]
+        if len(bad):
+            raise N.MosaicError(
+                N.MOSAIC_E_ARG, f"grid_cellkring / grid_cellkloop: the H3 ring of row {int(bad[0])} (cell {int(ids[bad[0]])}) reaches a "
+                "pentagon, where H3 falls back to its hash-ordered kRing; not supported by this engine")
         rows = [out[i * stride:i * stride + cnt[i]] for i in range(n)]
         if raw or self.index_system.cell_id_type != "string":
             return rows
@@ -605,12 +613,14 @@ class MosaicContext:
 
     def grid_cellkring(self, cells, k, raw=False):
         """grid_cellkring(cellId, k) (MosaicContext.scala:692-693 -> CellKRing.nullSafeEval ->
-        IndexSystem.kRing; BNG: BNGIndexSystem.scala:216-222): per row the cell and its loops 1..k."""
+        IndexSystem.kRing; BNG: BNGIndexSystem.scala:216-222, the cell and its loops 1..k; H3:
+        H3IndexSystem.scala:154-160, h3.kRing in hexRange order -- rings reaching a pentagon raise)."""
         return self._kring(cells, k, False, raw)
 
     def grid_cellkloop(self, cells, k, raw=False):
         """grid_cellkloop(cellId, k) (MosaicContext.scala:696-697 -> CellKLoop -> IndexSystem.kLoop;
-        BNG: BNGIndexSystem.scala:234-246): per row the valid cells at distance k."""
+        BNG: BNGIndexSystem.scala:234-246, the valid cells at distance k; H3: H3IndexSystem.scala:
+        171-177, h3.hexRing order)."""
         return self._kring(cells, k, True, raw)
 
     def grid_cellkringexplode(self, cells, k):

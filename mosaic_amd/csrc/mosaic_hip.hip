@@ -28,6 +28,7 @@
 #include "bng_device.h"
 #include "geom_build.h"
 #include "h3_device.h"
+#include "h3_grid.h"
 #include "pip_coop.h"
 #include "pip_device.h"
 #include "point_decode.h"
@@ -1604,6 +1605,19 @@ __global__ void __launch_bounds__(256) k_bng_kring(KringArgs a) {
         a.count[i] = m < 0 ? 0 : m;
     }
     if (bad) atomicOr(a.flags, 1u);
+}
+
+// grid_cellkring / grid_cellkloop over H3 cells (h3_grid.h): one lane per row, H3's hexRange /
+// hexRing order; rows whose walk reaches a pentagon (or an invalid id) get count -2.
+__global__ void __launch_bounds__(256) k_h3_kring(KringArgs a) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+        if (a.valid && !a.valid[i]) {
+            a.count[i] = -1;
+            continue;
+        }
+        a.count[i] = h3grid::kring((uint64_t)a.cells[i], a.k, a.loop, a.out + i * a.stride);
+    }
 }
 
 
@@ -4353,12 +4367,13 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
                       int64_t* out, int32_t* out_count) {
     ENTER(ctx);
     if (!c || n < 0 || (n > 0 && (!cells || !out || !out_count))) return fail(MOSAIC_E_ARG, "invalid argument");
-    if (grid != MOSAIC_GRID_BNG)
-        return fail(MOSAIC_E_ARG, "grid_cellkring / grid_cellkloop: only the BNG grid is implemented by this engine");
+    if (grid != MOSAIC_GRID_BNG && grid != MOSAIC_GRID_H3) return fail(MOSAIC_E_ARG, "unknown grid");
     if (k < 0 || k > 1000) return fail(MOSAIC_E_ARG, "k must be in [0, 1000]");
     if (n == 0) return MOSAIC_OK;
     HIP_TRY(hipSetDevice(c->device));
-    const int64_t stride = loop ? 8 * (int64_t)k : 1 + 4 * (int64_t)k * (k + 1);
+    const bool h3g = grid == MOSAIC_GRID_H3;
+    const int64_t stride = h3g ? (loop ? std::max<int64_t>(6 * (int64_t)k, 1) : 1 + 3 * (int64_t)k * (k + 1))
+                               : (loop ? 8 * (int64_t)k : 1 + 4 * (int64_t)k * (k + 1));
     const int64_t slots = stride * n;  // 0 for a k = 0 loop: nothing to copy back
     DevBuf s_cells, s_valid, s_out, s_cnt, s_flags;
     auto done = [&](int rc) {
@@ -4384,7 +4399,8 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
     a.out = dev_out ? out : (int64_t*)s_out.p;
     a.count = dev_cnt ? out_count : (int32_t*)s_cnt.p;
     a.flags = (unsigned int*)s_flags.p;
-    hipLaunchKernelGGL(k_bng_kring, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
+    if (h3g) hipLaunchKernelGGL(k_h3_kring, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
+    else hipLaunchKernelGGL(k_bng_kring, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     unsigned int flags = 0;
     HIP_TRY(hipMemcpyAsync(&flags, s_flags.p, 4, hipMemcpyDeviceToHost, c->stream));

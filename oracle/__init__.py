@@ -68,6 +68,12 @@ def lib():
         L.oracle_bng_is_valid.argtypes = [i64]
         L.oracle_bng_cell_origin.restype = i32
         L.oracle_bng_cell_origin.argtypes = [i64, vp]
+        L.oracle_h3_to_geo.restype = None
+        L.oracle_h3_to_geo.argtypes = [i64, vp, vp]
+        L.oracle_h3_kring_set.restype = i64
+        L.oracle_h3_kring_set.argtypes = [i64, i32, vp, vp, i64]
+        L.oracle_h3_is_pentagon.restype = i32
+        L.oracle_h3_is_pentagon.argtypes = [i64]
         _lib = L
     return _lib
 
@@ -83,6 +89,28 @@ def h3_point_to_index(lon, lat, res, jdk=8):
     out = np.empty(lon.shape[0], dtype=np.int64)
     lib().oracle_h3_point_to_index(_ptr(lon), _ptr(lat), lon.shape[0], res, jdk, _ptr(out))
     return out
+
+
+def h3_to_geo(cell):
+    """h3ToGeo: the cell centre (lat, lng) in radians (H3 C v3.7 _faceIjkToGeo)."""
+    lat = np.zeros(1)
+    lon = np.zeros(1)
+    lib().oracle_h3_to_geo(int(cell), _ptr(lat), _ptr(lon))
+    return float(lat[0]), float(lon[0])
+
+
+def h3_kring_set(cell, k):
+    """kRing(cell, k) as {cell: ring distance}, found on the sphere (oracle/h3.c)."""
+    cap = 1 + 3 * k * (k + 1) + 64
+    out = np.zeros(cap, np.int64)
+    dist = np.zeros(cap, np.int32)
+    n = lib().oracle_h3_kring_set(int(cell), k, _ptr(out), _ptr(dist), cap)
+    assert n >= 0
+    return dict(zip(out[:n].tolist(), dist[:n].tolist()))
+
+
+def h3_is_pentagon(cell):
+    return bool(lib().oracle_h3_is_pentagon(int(cell)))
 
 
 def h3_geo_to_h3(lat_rad, lng_rad, res):

@@ -386,3 +386,204 @@ void oracle_libm_eval(int fn, const double* a, const double* b, int64_t n, doubl
         }
     }
 }
+
+/* ---- h3ToGeo (cell centre) and a geometric k-ring: the oracle of the H3 grid_cellkring /
+ * grid_cellkloop kernels (mosaic_amd/csrc/h3_grid.h).  Reference: H3IndexSystem.kRing / kLoop
+ * (core/index/H3IndexSystem.scala:154-177) = h3-java kRing / hexRing (H3 C v3.7 algos.c).  The
+ * oracle does not restate H3's traversal: a cell's neighbours are found on the sphere, as the cells
+ * geoToH3 gives just beyond the cell's boundary along 48 bearings from its centre, and the k-ring
+ * set is their breadth-first closure -- independent of the kernel's FaceIJK walk. */
+#include "../mosaic_amd/csrc/h3_face_tables.h"
+
+#define M_SQRT3_2_L 0.8660254037844386467637231707529361834714L
+
+typedef struct {
+    int face;
+    CoordIJK coord;
+} FaceIJK;
+
+static const int kMaxDimByCIIres[17] = {2, -1, 14, -1, 98, -1, 686, -1, 4802, -1, 33614, -1, 235298, -1, 1647086, -1, 11529602};
+static const int kUnitScaleByCIIres[17] = {1, -1, 7, -1, 49, -1, 343, -1, 2401, -1, 16807, -1, 117649, -1, 823543, -1, 5764801};
+
+/* coordijk.c _ijkRotate60ccw */
+static void ijk_rotate60ccw(CoordIJK* c) {
+    CoordIJK r = {c->i + c->k, c->i + c->j, c->j + c->k};
+    *c = r;
+    ijk_normalize(c);
+}
+/* coordijk.c _ijkRotate60cw: i -> (1, 0, 1), j -> (1, 1, 0), k -> (0, 1, 1) */
+static void ijk_rotate60cw(CoordIJK* c) {
+    CoordIJK r = {c->i + c->j, c->j + c->k, c->i + c->k};
+    *c = r;
+    ijk_normalize(c);
+}
+
+/* faceijk.c _adjustOverageClassII (substrate 0): 0 none, 1 new face */
+static int adjust_overage_class2(FaceIJK* fijk, int res, int pent_leading4) {
+    CoordIJK* ijk = &fijk->coord;
+    int max_dim = kMaxDimByCIIres[res];
+    if (ijk->i + ijk->j + ijk->k <= max_dim) return 0;
+    const int* o;
+    if (ijk->k > 0) {
+        if (ijk->j > 0) {
+            o = kH3FaceNeighbors[fijk->face][3];
+        } else {
+            o = kH3FaceNeighbors[fijk->face][2];
+            if (pent_leading4) {
+                CoordIJK tmp = {ijk->i - max_dim, ijk->j, ijk->k};
+                ijk_rotate60cw(&tmp);
+                ijk->i = tmp.i + max_dim;
+                ijk->j = tmp.j;
+                ijk->k = tmp.k;
+            }
+        }
+    } else {
+        o = kH3FaceNeighbors[fijk->face][1];
+    }
+    fijk->face = o[0];
+    for (int r = 0; r < o[4]; r++) ijk_rotate60ccw(ijk);
+    int s = kUnitScaleByCIIres[res];
+    ijk->i += o[1] * s;
+    ijk->j += o[2] * s;
+    ijk->k += o[3] * s;
+    ijk_normalize(ijk);
+    return 1;
+}
+
+/* h3Index.c _h3ToFaceIjk (with _h3ToFaceIjkWithInitializedFijk) */
+static void h3_to_faceijk(uint64_t h, FaceIJK* fijk) {
+    int bc = (int)((h >> H3_BC_OFFSET) & 127), res = get_res(h);
+    int pent = kH3BaseCellData[bc][4];
+    if (pent && leading_nonzero_digit(h) == 5) h = rotate60cw_h(h);
+    fijk->face = kH3BaseCellData[bc][0];
+    fijk->coord.i = kH3BaseCellData[bc][1];
+    fijk->coord.j = kH3BaseCellData[bc][2];
+    fijk->coord.k = kH3BaseCellData[bc][3];
+    int possible = !(!pent && (res == 0 || (fijk->coord.i == 0 && fijk->coord.j == 0 && fijk->coord.k == 0)));
+    for (int r = 1; r <= res; r++) {
+        if (r & 1) down_ap7(&fijk->coord);
+        else down_ap7r(&fijk->coord);
+        int d = get_digit(h, r);
+        if (d > 0 && d < 7) {
+            fijk->coord.i += (d >> 2) & 1;
+            fijk->coord.j += (d >> 1) & 1;
+            fijk->coord.k += d & 1;
+            ijk_normalize(&fijk->coord);
+        }
+    }
+    if (!possible) return;
+    CoordIJK orig = fijk->coord;
+    int r2 = res;
+    if (res & 1) {
+        down_ap7r(&fijk->coord);
+        r2++;
+    }
+    int pent4 = pent && leading_nonzero_digit(h) == 4;
+    if (adjust_overage_class2(fijk, r2, pent4)) {
+        if (pent)
+            while (adjust_overage_class2(fijk, r2, 0)) {
+            }
+        if (r2 != res) up_ap7r(&fijk->coord);
+    } else if (r2 != res) {
+        fijk->coord = orig;
+    }
+}
+
+/* geoCoord.c _geoAzDistanceRads (the oracle's own use: points along a bearing) */
+static void geo_az_distance(double lat1, double lon1, double az, double dist, double* lat2, double* lon2) {
+    double sl = sin(lat1) * cos(dist) + cos(lat1) * sin(dist) * cos(az);
+    if (sl > 1.0) sl = 1.0;
+    if (sl < -1.0) sl = -1.0;
+    *lat2 = asin(sl);
+    double sn = sin(az) * sin(dist) / cos(*lat2);
+    double cs = (cos(dist) - sin(lat1) * sin(*lat2)) / cos(lat1) / cos(*lat2);
+    if (sn > 1.0) sn = 1.0;
+    if (sn < -1.0) sn = -1.0;
+    if (cs > 1.0) cs = 1.0;
+    if (cs < -1.0) cs = -1.0;
+    double lon = lon1 + atan2(sn, cs);
+    while (lon > M_PI) lon -= 2 * M_PI;
+    while (lon < -M_PI) lon += 2 * M_PI;
+    *lon2 = lon;
+}
+
+/* faceijk.c _faceIjkToGeo: _ijkToHex2d + _hex2dToGeo (substrate 0) -- the cell centre (radians) */
+void oracle_h3_to_geo(int64_t h3, double* lat, double* lon) {
+    FaceIJK f;
+    h3_to_faceijk((uint64_t)h3, &f);
+    int res = get_res((uint64_t)h3);
+    int i = f.coord.i - f.coord.k, j = f.coord.j - f.coord.k;
+    double vx = i - 0.5 * j, vy = j * M_SQRT3_2_L;
+    double r = sqrt(vx * vx + vy * vy);
+    const double* c = kH3FaceCenterGeo[f.face];
+    if (r < EPSILON_L) {
+        *lat = c[0];
+        *lon = c[1];
+        return;
+    }
+    double theta = atan2(vy, vx);
+    for (int q = 0; q < res; q++) r /= M_SQRT7_L;
+    r *= RES0_U_GNOMONIC;
+    r = atan(r);
+    if (res & 1) theta = pos_angle_rads(theta + M_AP7_ROT_RADS_L);
+    theta = pos_angle_rads(kH3FaceAxesAzRadsCII[f.face][0] - theta);
+    geo_az_distance(c[0], c[1], theta, r, lat, lon);
+}
+
+/* neighbours of h (sphere search): out[0..n), n <= 12 */
+static int oracle_h3_neighbors(uint64_t h, uint64_t* out) {
+    int res = get_res(h), n = 0;
+    double lat, lon;
+    oracle_h3_to_geo((int64_t)h, &lat, &lon);
+    double step = 0.02;
+    for (int q = 0; q < res; q++) step /= 2.6457513110645906;
+    for (int d = 0; d < 48; d++) {
+        double az = (d + 0.37) * (2 * M_PI / 48), lo = 0, hi = step, la, ln;
+        for (int it = 0; it < 60; it++) {
+            geo_az_distance(lat, lon, az, hi, &la, &ln);
+            if ((uint64_t)oracle_h3_geo_to_h3(la, ln, res) != h) break;
+            lo = hi;
+            hi *= 1.5;
+        }
+        for (int it = 0; it < 60; it++) {
+            double mid = 0.5 * (lo + hi);
+            geo_az_distance(lat, lon, az, mid, &la, &ln);
+            if ((uint64_t)oracle_h3_geo_to_h3(la, ln, res) == h) lo = mid;
+            else hi = mid;
+        }
+        geo_az_distance(lat, lon, az, hi * 1.3, &la, &ln);
+        uint64_t c = (uint64_t)oracle_h3_geo_to_h3(la, ln, res);
+        if (c == h || c == 0) continue;
+        int seen = 0;
+        for (int m = 0; m < n; m++) seen |= out[m] == c;
+        if (!seen && n < 12) out[n++] = c;
+    }
+    return n;
+}
+
+/* kRing(h, k) as a set (breadth-first over the sphere neighbours), with each cell's ring
+ * distance: out / dist hold up to cap cells; returns the count (-1: cap too small) */
+int64_t oracle_h3_kring_set(int64_t h3, int k, int64_t* out, int32_t* dist, int64_t cap) {
+    if (cap < 1) return -1;
+    int64_t n = 0, head = 0;
+    out[n] = h3;
+    dist[n++] = 0;
+    while (head < n) {
+        uint64_t cur = (uint64_t)out[head];
+        int dcur = dist[head++];
+        if (dcur == k) continue;
+        uint64_t nb[12];
+        int m = oracle_h3_neighbors(cur, nb);
+        for (int q = 0; q < m; q++) {
+            int seen = 0;
+            for (int64_t t = 0; t < n && !seen; t++) seen = (uint64_t)out[t] == nb[q];
+            if (seen) continue;
+            if (n >= cap) return -1;
+            out[n] = (int64_t)nb[q];
+            dist[n++] = dcur + 1;
+        }
+    }
+    return n;
+}
+
+int oracle_h3_is_pentagon(int64_t h3) { return kH3BaseCellData[(h3 >> H3_BC_OFFSET) & 127][4]; }

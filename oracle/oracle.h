@@ -42,6 +42,10 @@ void oracle_h3_point_to_index(const double* lon, const double* lat, int64_t n, i
 /* Intermediate state of geoToH3 for diagnostics: face, hex2d x/y, res ijk. */
 /* The host libm H3 C reaches: fn 0 sin, 1 cos (via sincos), 2 tan, 3 acos, 4 atan2(a, b). */
 void oracle_libm_eval(int fn, const double* a, const double* b, int64_t n, double* out);
+/* h3ToGeo (radians) and kRing as a set found on the sphere (oracle of the H3 k-ring kernels) */
+void oracle_h3_to_geo(int64_t h3, double* lat, double* lon);
+int64_t oracle_h3_kring_set(int64_t h3, int k, int64_t* out, int32_t* dist, int64_t cap);
+int oracle_h3_is_pentagon(int64_t h3);
 void oracle_h3_debug(double lat_rad, double lng_rad, int res, int* face, double* x, double* y,
                      int* ijk);
 

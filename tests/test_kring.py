@@ -5,8 +5,8 @@ reached from CellKRing / CellKLoop.nullSafeEval (expressions/index/CellKRing.sca
 The oracle (oracle/bng.c) is pinned by the reference's golden vectors
 (TestBNGIndexSystem.scala:92-161: k-loops 1..3 around "TQ3879SE" (res -4) and "TQ3879" (res 3),
 k-rings = the cell and its loops, isValid); the GPU path (mosaic_cell_kring through the C ABI,
-marked gpu) must equal the oracle element for element, order included.  H3 k-rings are not
-implemented by this engine (the ABI says so)."""
+marked gpu) must equal the oracle element for element, order included.  H3 k-rings:
+tests/test_h3_kring.py."""
 import numpy as np
 import pytest
 

@@ -46,6 +46,9 @@ case $STEP in
   tess)
     run t_tess 900 $PYT tests/test_tessellate_gpu.py -s
     ;;
+  kring)
+    run t_kring 600 $PYT tests/test_h3_kring.py tests/test_kring.py -s
+    ;;
   tests)
     run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
     ;;
