@@ -308,6 +308,22 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
 int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k,
                       int loop, int64_t* out, int32_t* out_count);
 
+/* ---- H3 cell geometry over a cell column ---- */
+/* H3 C v3.7 h3ToGeo / h3ToGeoBoundary bit for bit (x87 long-double steps and glibc libm restated),
+ * in degrees through java.lang.Math.toDegrees (option "jdk"), x = lng, y = lat.
+ * mode 0 (h3ToGeo): out = double[2 n], the cell centre (x, y); out_count[i] = 1.
+ * mode 1 (h3ToGeoBoundary): out = double[20 n], row i's vertices from out + 20 i as (x, y) pairs;
+ *   out_count[i] = their number (5..10: Class III cells crossing an icosahedron edge and pentagons
+ *   carry extra edge vertices).
+ * mode 2 (grid_boundaryaswkb: IndexGeometry -> H3IndexSystem.indexToGeometry -> toWKB): out =
+ *   uint8[189 n], row i's JTS big-endian 2D WKB polygon (the boundary closed with its first vertex)
+ *   from out + 189 i; out_count[i] = its byte length (13 + 16 (vertices + 1)).
+ * Null rows (valid[i] == 0): out_count[i] = -1.  An id that is not a valid H3 cell: MOSAIC_E_ARG.
+ * Reference: H3IndexSystem.indexToGeometry / getBufferRadius / polyfill
+ * (core/index/H3IndexSystem.scala:73-126), expressions/index/IndexGeometry.scala:65-75. */
+int mosaic_h3_cell_geometry(mosaic_ctx* ctx, int mode, const int64_t* cells, const uint8_t* valid, int64_t n,
+                            void* out, int32_t* out_count);
+
 /* ---- grid_boundaryaswkb over a cell column (BNG) ---- */
 /* out[93 i .. 93 i + 92] = the WKB JTS writes for BNGIndexSystem.indexToGeometry(ids[i])
  * (core/index/BNGIndexSystem.scala indexToGeometry; functions/MosaicContext.scala

@@ -38,7 +38,7 @@ EXPORTS = [
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
     "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb", "mosaic_point_to_cell_exact",
     "mosaic_diag_libm", "mosaic_point_coords_to_cell", "mosaic_point_coords_decode", "mosaic_bng_parse_column",
-    "mosaic_chip_table_create_arrow", "mosaic_chip_table_build_info",
+    "mosaic_chip_table_create_arrow", "mosaic_chip_table_build_info", "mosaic_h3_cell_geometry",
 ]
 
 GEOM_WKB = 0
@@ -123,6 +123,7 @@ def lib():
         "mosaic_cell_kring": ([vp, i32, vp, vp, i64, i32, i32, vp, vp], i32),
         "mosaic_bng_format_column": ([vp, vp, vp, i64, vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_cell_boundary_wkb": ([vp, i32, vp, vp, i64, vp], i32),
+        "mosaic_h3_cell_geometry": ([vp, i32, vp, vp, i64, vp, vp], i32),
         "mosaic_tessellate_gpu": ([vp, i32, i32, i64, vp, vp, vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
         "mosaic_tess_last_classify_ms": ([vp], ctypes.c_double),
         "mosaic_point_to_cell_exact": ([vp, i32, vp, vp, i64, vp], i32),

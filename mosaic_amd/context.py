@@ -640,9 +640,34 @@ class MosaicContext:
             return idx, self._serialize(cells)
         return idx, cells
 
+    def _h3_geometry(self, cells, mode):
+        ids = np.ascontiguousarray(cells, np.int64)
+        n = len(ids)
+        width = (2, 20, 189)[mode]
+        out = np.zeros(max(n * width, 1), np.uint8 if mode == 2 else np.float64)
+        cnt = np.zeros(max(n, 1), np.int32)
+        N.check(N.lib().mosaic_h3_cell_geometry(self.handle, mode, N.ptr(ids), None, n, N.ptr(out), N.ptr(cnt)))
+        return out, cnt[:n], width
+
+    def grid_cellcenter(self, cells):
+        """H3 h3ToGeo over a cell column (the cell centres polyfill tests, H3IndexSystem.scala:113-126):
+        array [n, 2] of (lng, lat) degrees."""
+        out, _, _ = self._h3_geometry(cells, 0)
+        return out[:2 * len(cells)].reshape(-1, 2)
+
+    def grid_boundary(self, cells):
+        """H3IndexSystem.indexToGeometry's vertices (h3.h3ToGeoBoundary, H3IndexSystem.scala:93-100):
+        per row an array [k, 2] of (lng, lat) degrees, k = 5..10 (the ring is not closed)."""
+        out, cnt, w = self._h3_geometry(cells, 1)
+        return [out[w * i:w * i + 2 * cnt[i]].reshape(-1, 2) for i in range(len(cells))]
+
     def grid_boundaryaswkb(self, cells):
         """grid_boundaryaswkb(cellId) (IndexGeometry.scala:65-75 -> IndexSystem.indexToGeometry ->
-        toWKB); BNG only: per row the cell square as big-endian WKB (93 bytes)."""
+        toWKB): per row the cell polygon as JTS big-endian WKB -- BNG: the cell square (93 bytes);
+        H3: the h3ToGeoBoundary ring closed with its first vertex."""
+        if self.index_system.grid == N.GRID_H3:
+            out, cnt, w = self._h3_geometry(cells, 2)
+            return [out[w * i:w * i + cnt[i]].tobytes() for i in range(len(cells))]
         strings = len(cells) and isinstance(cells[0], str)
         ids = np.array([self.index_system.parse(c) for c in cells] if strings else cells, np.int64)
         out = np.zeros(max(93 * len(ids), 1), np.uint8)

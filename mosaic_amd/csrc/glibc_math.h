@@ -470,5 +470,113 @@ MOSAIC_HD double atan2(double y, double x) {
     return copysign(r, y);
 }
 
+// ---- atan: s_atan.c __atan (FMA build, s_atan-fma.o), table cij shared with atan2 ----
+// Thresholds A = 0x1.bb67ap-27 (.LC6), B = 1/16, C = 1, D = 16, E = 0x1.49ff2p+53; the shipped
+// object contracts TWO52 + TWO8 u, the EMULV products and the Horner steps into fused ops.
+MOSAIC_HD double atan(double x) {
+    const double hp0 = kHp0, hp1 = kHp1;
+    const uint32_t ux = (uint32_t)hi32(x), dx = lo32(x);
+    if ((ux & 0x7ff00000) == 0x7ff00000 && ((ux & 0x000fffff) | dx) != 0) return x + x;
+    const double u = (x < 0) ? -x : x;
+    const double A = 0x1.bb67ap-27, E = 0x1.49ff2p+53;
+    if (u < 1.0) {
+        if (u < 0.0625) {
+            if (u < A) return x;
+            const double v = x * x;
+            return fma(x * v, atan2_poly(v), x);
+        }
+        const double* c = atan2_row(u);
+        const double z = u - c[0];
+        const double yy = fma(fma(fma(fma(c[6], z, c[5]), z, c[4]), z, c[3]), z, c[2]);
+        return copysign(fma(yy, z, c[1]), x);
+    }
+    if (u < 16.0) {
+        const double w = 1.0 / u;
+        const double t1 = u * w, t2 = fma(u, w, -t1);
+        const double* c = atan2_row(w);
+        const double z = fma((1.0 - t1) - t2, w, w - c[0]);
+        const double yy = fma(-z, atan2_tpoly(c, z), hp1);
+        return copysign((hp0 - c[1]) + yy, x);
+    }
+    if (u < E) {
+        const double w = 1.0 / u;
+        const double v = w * w, t1 = u * w;
+        const double yy = (w * v) * atan2_poly(v);
+        const double t2 = fma(u, w, -t1);
+        const double ww = ((1.0 - t1) - t2) * w;
+        const double t3 = hp0 - w;
+        const double cor = (hp0 > fabs(w)) ? (hp0 - t3) - w : hp0 - (w + t3);
+        return copysign(((((cor + hp1) - ww) - yy) + t3), x);
+    }
+    return (x < 0) ? -hp0 : hp0;
+}
+
+// ---- asin: e_asin.c __ieee754_asin (FMA build, e_asin-fma.o), tables asncs / inroot / powtwo ----
+MOSAIC_HD double asin(double x) {
+    const double hp0 = kHp0, hp1 = kHp1;
+    const double f1 = 0x1.55555555554f9p-3, f2 = 0x1.333333336127dp-4, f3 = 0x1.6db6dae42c0e4p-5,
+                 f4 = 0x1.f1c7e04f4ad99p-6, f5 = 0x1.6e442c822d419p-6, f6 = 0x1.292d80f453c72p-6;
+    const double rt0 = 0x1.fffffffecc1ddp-1, rt1 = 0x1.fffffff757304p-2, rt2 = 0x1.800496769c91ap-2,
+                 rt3 = 0x1.4006318d1dab9p-2;
+    const double t24 = 0x1p+24;
+    const int32_t m = hi32(x);
+    const int32_t k = m & 0x7fffffff;
+    if (k < 0x3e500000) return x;
+    if (k < 0x3fc00000) {  // |x| < 0.125
+        const double x2 = x * x;
+        const double p = fma(fma(fma(fma(fma(f6, x2, f5), x2, f4), x2, f3), x2, f2), x2, f1);
+        return fma(x * x2, p, x);
+    }
+    if (k < 0x3fef0000) {  // 0.125 <= |x| < 0.96875: per-interval polynomial in |x| - x0
+        int n, top;
+        if (k < 0x3fd00000) {
+            n = 11 * ((k >> 15) & 0x1f);
+            top = 6;
+        } else if (k < 0x3fe00000) {
+            n = 352 + 11 * ((k >> 14) & 0x3f);
+            top = 6;
+        } else if (k < 0x3fe80000) {
+            n = 1056 + 12 * ((k >> 13) & 0x7f);
+            top = 7;
+        } else if (k < 0x3fed8000) {
+            n = 992 + 13 * ((k >> 13) & 0x7f);
+            top = 8;
+        } else if (k < 0x3fee8000) {
+            n = 884 + 14 * ((k >> 13) & 0x7f);
+            top = 9;
+        } else {
+            n = 768 + 15 * ((k >> 13) & 0x7f);
+            top = 10;
+        }
+        const double* T = kAsnCs + n;
+        const double xx = ((m > 0) ? x : -x) - T[0];
+        const double xx2 = xx * xx;
+        double p = T[top];
+        for (int j = top - 1; j >= 2; j--) p = fma(xx, p, T[j]);
+        p = fma(xx2, p, T[top + 1]);
+        const double res = fma(xx, T[1], p) + T[top + 2];
+        return (m > 0) ? res : -res;
+    }
+    if (k < 0x3ff00000) {  // 0.96875 <= |x| < 1: pi/2 - 2 asin(sqrt((1 - |x|) / 2))
+        const double z = ((m > 0) ? (1.0 - x) : (x + 1.0)) * 0.5;
+        const int64_t zb = (int64_t)bits(z);
+        double t = kInRoot[(int)((zb >> 46) & 0x7f)] * kPowTwo[0x1ff - (int)(zb >> 53)];
+        const double r = fma(-(t * t), z, 1.0);
+        t = fma(fma(fma(rt3, r, rt2), r, rt1), r, rt0) * t;
+        const double c = z * t;
+        const double y = (c + t24) - t24;
+        const double den = fma(fma(-c, t * 0.5, 1.5), c, y);
+        const double cc = fma(-y, y, z) / den;
+        const double p = fma(fma(fma(fma(fma(f6, z, f5), z, f4), z, f3), z, f2), z, f1) * z;
+        const double cor = fma(-((y + cc) + (y + cc)), p, fma(-2.0, cc, hp1));
+        const double res = cor + fma(-2.0, y, hp0);
+        return (m > 0) ? res : -res;
+    }
+    if (k == 0x3ff00000 && lo32(x) == 0) return (m > 0) ? hp0 : -hp0;
+    if (k > 0x7ff00000 || (k == 0x7ff00000 && lo32(x) != 0)) return x + x;
+    const double zz = x - x;
+    return zz / zz;
+}
+
 }  // namespace glibc
 }  // namespace mosaic

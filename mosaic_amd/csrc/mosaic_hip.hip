@@ -28,6 +28,7 @@
 #include "bng_device.h"
 #include "geom_build.h"
 #include "h3_device.h"
+#include "h3_geom.h"
 #include "h3_grid.h"
 #include "pip_coop.h"
 #include "pip_device.h"
@@ -1774,6 +1775,56 @@ __global__ void __launch_bounds__(256) k_bng_cell_wkb(const int64_t* ids, const 
     if (bad) atomicOr(flags, 1u);
 }
 
+// ---- H3 cell geometry over a cell column (h3_geom.h): mode 0 h3ToGeo centres, 1 h3ToGeoBoundary
+// vertices, 2 grid_boundaryaswkb (IndexGeometry -> H3IndexSystem.indexToGeometry -> toWKB: the
+// boundary closed with its first vertex, JTS big-endian 2D WKB, x = lng, y = lat in degrees through
+// java.lang.Math.toDegrees).  One lane per row; invalid ids set flags bit 0.
+static const int kH3WkbStride = 13 + 16 * 11;  // <= 10 boundary vertices + the closing point
+__global__ void __launch_bounds__(256) k_h3_geom(const int64_t* ids, const uint8_t* valid, int64_t n, int mode,
+                                                 int jdk, void* out, int32_t* count, unsigned int* flags) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+        if (valid && !valid[i]) {
+            count[i] = -1;
+            continue;
+        }
+        double v[20];
+        int nv;
+        if (mode == 0) {
+            nv = h3geom::h3_to_geo((uint64_t)ids[i], &v[0], &v[1]) ? 1 : -1;
+        } else {
+            nv = h3geom::h3_to_geo_boundary((uint64_t)ids[i], v);
+        }
+        if (nv < 0) {
+            bad = true;
+            count[i] = 0;
+            continue;
+        }
+        if (mode < 2) {
+            double* o = (double*)out + (mode == 0 ? 2 : 20) * i;
+            for (int k = 0; k < nv; k++) {
+                o[2 * k] = h3geom::to_degrees(v[2 * k + 1], jdk);  // x = lng
+                o[2 * k + 1] = h3geom::to_degrees(v[2 * k], jdk);  // y = lat
+            }
+            count[i] = nv;
+        } else {
+            uint8_t* o = (uint8_t*)out + (int64_t)kH3WkbStride * i;
+            o[0] = 0;  // big-endian
+            bng::put_be_u32(o + 1, 3);
+            bng::put_be_u32(o + 5, 1);
+            bng::put_be_u32(o + 9, (uint32_t)(nv + 1));
+            for (int k = 0; k <= nv; k++) {
+                const int q = k == nv ? 0 : k;
+                bng::put_be_f64(o + 13 + 16 * k, h3geom::to_degrees(v[2 * q + 1], jdk));
+                bng::put_be_f64(o + 21 + 16 * k, h3geom::to_degrees(v[2 * q], jdk));
+            }
+            count[i] = 13 + 16 * (nv + 1);
+        }
+    }
+    if (bad) atomicOr(flags, 1u);
+}
+
 // ---- BNG dense cell table (positive resolutions): BNGIndexSystem.pointToIndex
 // (BNGIndexSystem.scala:277-291, 528-541) maps a point with 0 <= toInt(e), toInt(n) < 1e7 to the id
 // of cell (toInt(e) / divisor, toInt(n) / divisor) -- one-to-one there, the two letters being the
@@ -2300,6 +2351,22 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
+    }
+};
+
+// Scope guards of entry points: staged buffers and timing events are released
+// on every return path (errors after allocation included)
+struct DevBufGuard {
+    std::vector<DevBuf*> bufs;
+    ~DevBufGuard() {
+        for (DevBuf* b : bufs) b->release();
+    }
+};
+struct EventGuard {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~EventGuard() {
+        for (hipEvent_t x : e)
+            if (x) (void)hipEventDestroy(x);
     }
 };
 
@@ -4481,6 +4548,40 @@ int mosaic_bng_format_column(mosaic_ctx* ctx, const int64_t* ids, const uint8_t*
 }
 
 
+int mosaic_h3_cell_geometry(mosaic_ctx* ctx, int mode, const int64_t* ids, const uint8_t* valid, int64_t n,
+                            void* out, int32_t* out_count) {
+    ENTER(ctx);
+    if (!c || n < 0 || mode < 0 || mode > 2 || (n > 0 && (!ids || !out || !out_count)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf s_ids, s_valid, s_out, s_cnt, s_flags;
+    DevBufGuard guard{{&s_ids, &s_valid, &s_out, &s_cnt, &s_flags}};
+    int rc;
+    const void *di, *dv;
+    if ((rc = to_device(c, s_ids, ids, (size_t)n * 8, &di)) || (rc = to_device(c, s_valid, valid, (size_t)n, &dv)))
+        return rc;
+    const size_t bytes = (size_t)n * (mode == 0 ? 16 : (mode == 1 ? 160 : (size_t)kH3WkbStride));
+    const bool dev_out = is_device_ptr(out), dev_cnt = is_device_ptr(out_count);
+    if ((!dev_out && (rc = s_out.reserve(bytes))) || (!dev_cnt && (rc = s_cnt.reserve((size_t)n * 4))) ||
+        (rc = s_flags.reserve(4)))
+        return rc;
+    void* dout = dev_out ? out : s_out.p;
+    int32_t* dcnt = dev_cnt ? out_count : (int32_t*)s_cnt.p;
+    HIP_TRY(hipMemsetAsync(dout, 0, bytes, c->stream));
+    HIP_TRY(hipMemsetAsync(s_flags.p, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_h3_geom, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, (const int64_t*)di,
+                       (const uint8_t*)dv, n, mode, c->jdk, dout, dcnt, (unsigned int*)s_flags.p);
+    HIP_TRY(hipGetLastError());
+    unsigned int flags = 0;
+    HIP_TRY(hipMemcpyAsync(&flags, s_flags.p, 4, hipMemcpyDeviceToHost, c->stream));
+    if (!dev_out) HIP_TRY(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, c->stream));
+    if (!dev_cnt) HIP_TRY(hipMemcpyAsync(out_count, dcnt, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (flags & 1u) return fail(MOSAIC_E_ARG, "invalid H3 cell id");
+    return MOSAIC_OK;
+}
+
 int mosaic_cell_boundary_wkb(mosaic_ctx* ctx, int grid, const int64_t* ids, const uint8_t* valid, int64_t n,
                              uint8_t* out) {
     ENTER(ctx);
@@ -4626,25 +4727,6 @@ __global__ void __launch_bounds__(256) k_bng_tess_classify(ClassifyArgs a) {
 extern "C" {
 
 // Classification step of mosaic_tessellate_gpu (tessellate.cpp); not part of the public header.
-}  // extern "C"
-
-// Scope guards of the classification entry points: staged buffers and timing events are released
-// on every return path (errors after allocation included)
-struct DevBufGuard {
-    std::vector<DevBuf*> bufs;
-    ~DevBufGuard() {
-        for (DevBuf* b : bufs) b->release();
-    }
-};
-struct EventGuard {
-    hipEvent_t e[2] = {nullptr, nullptr};
-    ~EventGuard() {
-        for (hipEvent_t x : e)
-            if (x) (void)hipEventDestroy(x);
-    }
-};
-
-extern "C" {
 
 int mosaic_tess_classify_bng(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                              const int64_t* ring_offsets, const double* xy, int64_t n_cand, const int32_t* cand_geom,

@@ -72,6 +72,8 @@ def lib():
         L.oracle_h3_to_geo.argtypes = [i64, vp, vp]
         L.oracle_h3_kring_set.restype = i64
         L.oracle_h3_kring_set.argtypes = [i64, i32, vp, vp, i64]
+        L.oracle_h3_to_geo_boundary.restype = i32
+        L.oracle_h3_to_geo_boundary.argtypes = [i64, vp]
         L.oracle_h3_is_pentagon.restype = i32
         L.oracle_h3_is_pentagon.argtypes = [i64]
         _lib = L
@@ -107,6 +109,13 @@ def h3_kring_set(cell, k):
     n = lib().oracle_h3_kring_set(int(cell), k, _ptr(out), _ptr(dist), cap)
     assert n >= 0
     return dict(zip(out[:n].tolist(), dist[:n].tolist()))
+
+
+def h3_to_geo_boundary(cell):
+    """h3ToGeoBoundary: [(lat, lng)] radians, 5..10 vertices (H3 C v3.7 _faceIjkToGeoBoundary)."""
+    out = np.zeros(20)
+    n = lib().oracle_h3_to_geo_boundary(int(cell), _ptr(out))
+    return [(float(out[2 * i]), float(out[2 * i + 1])) for i in range(n)]
 
 
 def h3_is_pentagon(cell):

@@ -507,27 +507,14 @@ static void geo_az_distance(double lat1, double lon1, double az, double dist, do
     *lon2 = lon;
 }
 
-/* faceijk.c _faceIjkToGeo: _ijkToHex2d + _hex2dToGeo (substrate 0) -- the cell centre (radians) */
+static void hex2d_to_geo(double vx, double vy, int face, int res, int substrate, double* lat, double* lon);
+
+/* h3Index.c h3ToGeo = faceijk.c _faceIjkToGeo: _ijkToHex2d + _hex2dToGeo (substrate 0), radians */
 void oracle_h3_to_geo(int64_t h3, double* lat, double* lon) {
     FaceIJK f;
     h3_to_faceijk((uint64_t)h3, &f);
-    int res = get_res((uint64_t)h3);
     int i = f.coord.i - f.coord.k, j = f.coord.j - f.coord.k;
-    double vx = i - 0.5 * j, vy = j * M_SQRT3_2_L;
-    double r = sqrt(vx * vx + vy * vy);
-    const double* c = kH3FaceCenterGeo[f.face];
-    if (r < EPSILON_L) {
-        *lat = c[0];
-        *lon = c[1];
-        return;
-    }
-    double theta = atan2(vy, vx);
-    for (int q = 0; q < res; q++) r /= M_SQRT7_L;
-    r *= RES0_U_GNOMONIC;
-    r = atan(r);
-    if (res & 1) theta = pos_angle_rads(theta + M_AP7_ROT_RADS_L);
-    theta = pos_angle_rads(kH3FaceAxesAzRadsCII[f.face][0] - theta);
-    geo_az_distance(c[0], c[1], theta, r, lat, lon);
+    hex2d_to_geo(i - 0.5 * j, j * M_SQRT3_2_L, f.face, get_res((uint64_t)h3), 0, lat, lon);
 }
 
 /* neighbours of h (sphere search): out[0..n), n <= 12 */
@@ -587,3 +574,246 @@ int64_t oracle_h3_kring_set(int64_t h3, int k, int64_t* out, int32_t* dist, int6
 }
 
 int oracle_h3_is_pentagon(int64_t h3) { return kH3BaseCellData[(h3 >> H3_BC_OFFSET) & 127][4]; }
+
+/* ---- h3ToGeoBoundary (H3 C v3.7 faceijk.c _faceIjkToGeoBoundary / _faceIjkPentToGeoBoundary):
+ * the oracle of the grid_boundaryaswkb / indexToGeometry kernels (reference
+ * H3IndexSystem.indexToGeometry, core/index/H3IndexSystem.scala:93-100).  Restated from the
+ * published H3 C algorithm with x86-64 semantics: `long double` where H3 uses L constants
+ * (M_SQRT7, M_SQRT3_2, EPSILON, M_2PI, M_AP7_ROT_RADS), `float t` in _v2dIntersect, glibc libm. */
+#define NUM_HEX_VERTS 6
+#define NUM_PENT_VERTS 5
+
+/* geoCoord.c constrainLng */
+static double constrain_lng(double lng) {
+    while (lng > M_PI) lng = lng - (2 * M_PI);
+    while (lng < -M_PI) lng = lng + (2 * M_PI);
+    return lng;
+}
+
+/* geoCoord.c _geoAzDistanceRads */
+static void geo_az_distance_rads(double lat1, double lon1, double az, double distance, double* lat2, double* lon2) {
+    if (distance < EPSILON_L) {
+        *lat2 = lat1;
+        *lon2 = lon1;
+        return;
+    }
+    double sinlat, sinlon, coslon;
+    az = pos_angle_rads(az);
+    if (az < EPSILON_L || fabs(az - M_PI) < EPSILON_L) {
+        if (az < EPSILON_L) *lat2 = lat1 + distance;
+        else *lat2 = lat1 - distance;
+        if (fabs(*lat2 - M_PI_2) < EPSILON_L) {
+            *lat2 = M_PI_2;
+            *lon2 = 0.0;
+        } else if (fabs(*lat2 + M_PI_2) < EPSILON_L) {
+            *lat2 = -M_PI_2;
+            *lon2 = 0.0;
+        } else {
+            *lon2 = constrain_lng(lon1);
+        }
+    } else {
+        sinlat = sin(lat1) * cos(distance) + cos(lat1) * sin(distance) * cos(az);
+        if (sinlat > 1.0) sinlat = 1.0;
+        if (sinlat < -1.0) sinlat = -1.0;
+        *lat2 = asin(sinlat);
+        if (fabs(*lat2 - M_PI_2) < EPSILON_L) {
+            *lat2 = M_PI_2;
+            *lon2 = 0.0;
+        } else if (fabs(*lat2 + M_PI_2) < EPSILON_L) {
+            *lat2 = -M_PI_2;
+            *lon2 = 0.0;
+        } else {
+            sinlon = sin(az) * sin(distance) / cos(*lat2);
+            coslon = (cos(distance) - sin(lat1) * sin(*lat2)) / cos(lat1) / cos(*lat2);
+            if (sinlon > 1.0) sinlon = 1.0;
+            if (sinlon < -1.0) sinlon = -1.0;
+            if (coslon > 1.0) coslon = 1.0;
+            if (coslon < -1.0) coslon = -1.0;
+            *lon2 = constrain_lng(lon1 + atan2(sinlon, coslon));
+        }
+    }
+}
+
+/* faceijk.c _hex2dToGeo */
+static void hex2d_to_geo(double vx, double vy, int face, int res, int substrate, double* lat, double* lon) {
+    double r = sqrt(vx * vx + vy * vy);
+    if (r < EPSILON_L) {
+        *lat = kH3FaceCenterGeo[face][0];
+        *lon = kH3FaceCenterGeo[face][1];
+        return;
+    }
+    double theta = atan2(vy, vx);
+    for (int i = 0; i < res; i++) r /= M_SQRT7_L;
+    if (substrate) {
+        r /= 3.0;
+        if (res & 1) r /= M_SQRT7_L;
+    }
+    r *= RES0_U_GNOMONIC;
+    r = atan(r);
+    if (!substrate && (res & 1)) theta = pos_angle_rads(theta + M_AP7_ROT_RADS_L);
+    theta = pos_angle_rads(kH3FaceAxesAzRadsCII[face][0] - theta);
+    geo_az_distance_rads(kH3FaceCenterGeo[face][0], kH3FaceCenterGeo[face][1], theta, r, lat, lon);
+}
+
+/* coordijk.c _ijkToHex2d */
+static void ijk_to_hex2d(CoordIJK c, double* x, double* y) {
+    int i = c.i - c.k, j = c.j - c.k;
+    *x = i - 0.5 * j;
+    *y = j * M_SQRT3_2_L;
+}
+
+/* coordijk.c _downAp3 / _downAp3r */
+static void down_ap3(CoordIJK* c) {
+    CoordIJK r = {2 * c->i + 1 * c->j + 0 * c->k, 0 * c->i + 2 * c->j + 1 * c->k, 1 * c->i + 0 * c->j + 2 * c->k};
+    *c = r;
+    ijk_normalize(c);
+}
+static void down_ap3r(CoordIJK* c) {
+    CoordIJK r = {2 * c->i + 0 * c->j + 1 * c->k, 1 * c->i + 2 * c->j + 0 * c->k, 0 * c->i + 1 * c->j + 2 * c->k};
+    *c = r;
+    ijk_normalize(c);
+}
+
+/* faceijk.c _adjustOverageClassII with substrate: 0 NO_OVERAGE, 1 FACE_EDGE, 2 NEW_FACE */
+static int adjust_overage_sub(FaceIJK* fijk, int res) {
+    CoordIJK* ijk = &fijk->coord;
+    int max_dim = kMaxDimByCIIres[res] * 3;
+    int sum = ijk->i + ijk->j + ijk->k;
+    if (sum == max_dim) return 1;
+    if (sum <= max_dim) return 0;
+    const int* o;
+    if (ijk->k > 0) o = ijk->j > 0 ? kH3FaceNeighbors[fijk->face][3] : kH3FaceNeighbors[fijk->face][2];
+    else o = kH3FaceNeighbors[fijk->face][1];
+    fijk->face = o[0];
+    for (int r = 0; r < o[4]; r++) ijk_rotate60ccw(ijk);
+    int s = kUnitScaleByCIIres[res] * 3;
+    ijk->i += o[1] * s;
+    ijk->j += o[2] * s;
+    ijk->k += o[3] * s;
+    ijk_normalize(ijk);
+    return (ijk->i + ijk->j + ijk->k == max_dim) ? 1 : 2;
+}
+
+/* vec2d.c _v2dIntersect (note `float t`, as H3 v3.7 declares it) */
+static void v2d_intersect(double p0x, double p0y, double p1x, double p1y, double p2x, double p2y, double p3x,
+                          double p3y, double* ix, double* iy) {
+    double s1x = p1x - p0x, s1y = p1y - p0y, s2x = p3x - p2x, s2y = p3y - p2y;
+    float t = (s2x * (p0y - p2y) - s2y * (p0x - p2x)) / (-s2x * s1y + s1x * s2y);
+    *ix = p0x + (t * s1x);
+    *iy = p0y + (t * s1y);
+}
+
+static void face_edge(int dir, int max_dim, double e[4]) {
+    double v0x = 3.0 * max_dim, v0y = 0.0;
+    double v1x = -1.5 * max_dim, v1y = 3.0 * M_SQRT3_2_L * max_dim;
+    double v2x = -1.5 * max_dim, v2y = -3.0 * M_SQRT3_2_L * max_dim;
+    if (dir == 1) { /* IJ */
+        e[0] = v0x; e[1] = v0y; e[2] = v1x; e[3] = v1y;
+    } else if (dir == 3) { /* JK */
+        e[0] = v1x; e[1] = v1y; e[2] = v2x; e[3] = v2y;
+    } else { /* KI */
+        e[0] = v2x; e[1] = v2y; e[2] = v0x; e[3] = v0y;
+    }
+}
+
+/* h3ToGeoBoundary: verts (lat, lon radians) -> out[2 n], returns n (<= 10) */
+int oracle_h3_to_geo_boundary(int64_t h3, double* out) {
+    static const CoordIJK vertsCII[6] = {{2, 1, 0}, {1, 2, 0}, {0, 2, 1}, {0, 1, 2}, {1, 0, 2}, {2, 0, 1}};
+    static const CoordIJK vertsCIII[6] = {{5, 4, 0}, {1, 5, 0}, {0, 5, 4}, {0, 1, 5}, {4, 0, 5}, {5, 0, 1}};
+    uint64_t h = (uint64_t)h3;
+    int res = get_res(h);
+    FaceIJK center;
+    h3_to_faceijk(h, &center);
+    int pent = kH3BaseCellData[(h >> H3_BC_OFFSET) & 127][4] && leading_nonzero_digit(h) == 0;
+    int nverts = pent ? NUM_PENT_VERTS : NUM_HEX_VERTS;
+    /* _faceIjkToVerts / _faceIjkPentToVerts */
+    int adj_res = res;
+    FaceIJK c = center;
+    const CoordIJK* verts = (res & 1) ? vertsCIII : vertsCII;
+    down_ap3(&c.coord);
+    down_ap3r(&c.coord);
+    if (res & 1) {
+        down_ap7r(&c.coord);
+        adj_res++;
+    }
+    FaceIJK fv[6];
+    for (int v = 0; v < nverts; v++) {
+        fv[v].face = c.face;
+        fv[v].coord.i = c.coord.i + verts[v].i;
+        fv[v].coord.j = c.coord.j + verts[v].j;
+        fv[v].coord.k = c.coord.k + verts[v].k;
+        ijk_normalize(&fv[v].coord);
+    }
+    int n = 0;
+    if (!pent) {
+        int last_face = -1, last_overage = 0;
+        for (int vert = 0; vert < NUM_HEX_VERTS + 1; vert++) {
+            int v = vert % NUM_HEX_VERTS;
+            FaceIJK fijk = fv[v];
+            int overage = adjust_overage_sub(&fijk, adj_res);
+            if ((res & 1) && vert > 0 && fijk.face != last_face && last_overage != 1) {
+                int last_v = (v + 5) % NUM_HEX_VERTS;
+                double o0x, o0y, o1x, o1y;
+                ijk_to_hex2d(fv[last_v].coord, &o0x, &o0y);
+                ijk_to_hex2d(fv[v].coord, &o1x, &o1y);
+                int max_dim = kMaxDimByCIIres[adj_res];
+                int face2 = (last_face == center.face) ? fijk.face : last_face;
+                double e[4];
+                face_edge(kH3AdjacentFaceDir[center.face][face2], max_dim, e);
+                double ix, iy;
+                v2d_intersect(o0x, o0y, o1x, o1y, e[0], e[1], e[2], e[3], &ix, &iy);
+                int at_vertex = (o0x == ix && o0y == iy) || (o1x == ix && o1y == iy);
+                if (!at_vertex) {
+                    hex2d_to_geo(ix, iy, center.face, adj_res, 1, &out[2 * n], &out[2 * n + 1]);
+                    n++;
+                }
+            }
+            if (vert < NUM_HEX_VERTS) {
+                double vx, vy;
+                ijk_to_hex2d(fijk.coord, &vx, &vy);
+                hex2d_to_geo(vx, vy, fijk.face, adj_res, 1, &out[2 * n], &out[2 * n + 1]);
+                n++;
+            }
+            last_face = fijk.face;
+            last_overage = overage;
+        }
+    } else {
+        FaceIJK last = fv[0];
+        for (int vert = 0; vert < NUM_PENT_VERTS + 1; vert++) {
+            int v = vert % NUM_PENT_VERTS;
+            FaceIJK fijk = fv[v];
+            while (adjust_overage_sub(&fijk, adj_res) == 2) {
+            }
+            if ((res & 1) && vert > 0) {
+                FaceIJK tmp = fijk;
+                double o0x, o0y, o1x, o1y;
+                ijk_to_hex2d(last.coord, &o0x, &o0y);
+                int dir = kH3AdjacentFaceDir[tmp.face][last.face];
+                const int* o = kH3FaceNeighbors[tmp.face][dir];
+                tmp.face = o[0];
+                for (int r = 0; r < o[4]; r++) ijk_rotate60ccw(&tmp.coord);
+                int s = kUnitScaleByCIIres[adj_res] * 3;
+                tmp.coord.i += o[1] * s;
+                tmp.coord.j += o[2] * s;
+                tmp.coord.k += o[3] * s;
+                ijk_normalize(&tmp.coord);
+                ijk_to_hex2d(tmp.coord, &o1x, &o1y);
+                int max_dim = kMaxDimByCIIres[adj_res];
+                double e[4];
+                face_edge(kH3AdjacentFaceDir[tmp.face][fijk.face], max_dim, e);
+                double ix, iy;
+                v2d_intersect(o0x, o0y, o1x, o1y, e[0], e[1], e[2], e[3], &ix, &iy);
+                hex2d_to_geo(ix, iy, tmp.face, adj_res, 1, &out[2 * n], &out[2 * n + 1]);
+                n++;
+            }
+            if (vert < NUM_PENT_VERTS) {
+                double vx, vy;
+                ijk_to_hex2d(fijk.coord, &vx, &vy);
+                hex2d_to_geo(vx, vy, fijk.face, adj_res, 1, &out[2 * n], &out[2 * n + 1]);
+                n++;
+            }
+            last = fijk;
+        }
+    }
+    return n;
+}

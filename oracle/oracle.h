@@ -46,6 +46,7 @@ void oracle_libm_eval(int fn, const double* a, const double* b, int64_t n, doubl
 void oracle_h3_to_geo(int64_t h3, double* lat, double* lon);
 int64_t oracle_h3_kring_set(int64_t h3, int k, int64_t* out, int32_t* dist, int64_t cap);
 int oracle_h3_is_pentagon(int64_t h3);
+int oracle_h3_to_geo_boundary(int64_t h3, double* out);
 void oracle_h3_debug(double lat_rad, double lng_rad, int res, int* face, double* x, double* y,
                      int* ijk);
 

@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
         }
     };
 
-    Tally ts{"sin"}, tc{"cos"}, tt{"tan"}, ta{"acos"}, t2{"atan2"};
+    Tally ts{"sin"}, tc{"cos"}, tt{"tan"}, ta{"acos"}, t2{"atan2"}, tat{"atan"}, tas{"asin"};
     const double thresholds[] = {0.126, 0.855469, 2.426265, 105414350.0, 0x1p-27, 0x1p-26};
     for (long i = 0; i < n; i++) {
         // ---- sincos ----
@@ -115,9 +115,52 @@ int main(int argc, char** argv) {
         }
         double b0 = ::atan2(y, xx), b1 = g::atan2(y, xx);
         t2.check(same(b0, b1), y, xx, b1, b0);
+
+        // ---- atan (h3ToGeo / h3ToGeoBoundary: atan of the gnomonic radius) ----
+        double at;
+        switch (i % 7) {
+            case 0: at = u01(rng) * 0.76; break;  // H3: r RES0_U_GNOMONIC over a face
+            case 1: at = sgn() * logu(1e-300, 1e300); break;
+            case 2: at = sgn() * u01(rng); break;
+            case 3: at = sgn() * (1.0 + u01(rng) * 15.0); break;
+            case 4: {
+                const double th[] = {0x1.bb67ap-27, 0.0625, 1.0, 16.0, 0x1.49ff2p+53, 0x1p-1022};
+                at = sgn() * th[rng() % 6] * (1.0 + (u01(rng) - 0.5) * 1e-12);
+                break;
+            }
+            case 5: {
+                const double sp[] = {0.0, -0.0, INFINITY, -INFINITY, NAN, 5e-324};
+                at = sp[rng() % 6];
+                break;
+            }
+            default: at = rbits(); break;
+        }
+        double q0 = ::atan(at), q1 = g::atan(at);
+        tat.check(same(q0, q1), at, 0, q1, q0);
+
+        // ---- asin (_geoAzDistanceRads: asin of the destination's sin(lat)) ----
+        double as;
+        switch (i % 6) {
+            case 0: as = (u01(rng) - 0.5) * 2.0; break;
+            case 1: as = sgn() * (1.0 - logu(1e-17, 0.04)); break;  // the sqrt branch
+            case 2: as = sgn() * logu(1e-300, 0.5); break;
+            case 3: {
+                const double th[] = {0x1p-26, 0.125, 0.25, 0.5, 0.75, 0.921875, 0.953125, 0.96875, 1.0};
+                as = sgn() * th[rng() % 9] * (1.0 + (u01(rng) - 0.5) * 1e-12);
+                break;
+            }
+            case 4: {
+                const double sp[] = {0.0, -0.0, 1.0, -1.0, INFINITY, NAN, 1.5, 5e-324};
+                as = sp[rng() % 8];
+                break;
+            }
+            default: as = (rng() % 16 == 0) ? rbits() : sgn() * u01(rng); break;
+        }
+        double e0 = ::asin(as), e1 = g::asin(as);
+        tas.check(same(e0, e1), as, 0, e1, e0);
     }
     long bad = 0;
-    for (Tally* t : {&ts, &tc, &tt, &ta, &t2}) {
+    for (Tally* t : {&ts, &tc, &tt, &ta, &t2, &tat, &tas}) {
         printf("%s %ld %ld\n", t->name, t->n, t->bad);
         bad += t->bad;
     }

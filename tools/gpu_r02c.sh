@@ -49,6 +49,9 @@ case $STEP in
   kring)
     run t_kring 600 $PYT tests/test_h3_kring.py tests/test_kring.py -s
     ;;
+  geom)
+    run t_geom 600 $PYT tests/test_h3_geom.py tests/test_h3_kring.py tests/test_bng_boundary.py -s
+    ;;
   tests)
     run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
     ;;
