@@ -324,6 +324,37 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
 int mosaic_h3_cell_geometry(mosaic_ctx* ctx, int mode, const int64_t* cells, const uint8_t* valid, int64_t n,
                             void* out, int32_t* out_count);
 
+/* ---- grid_polyfill ---- */
+/* grid_polyfill(geometry, res) over n_geoms polygonal geometries in the flat-ring layout of
+ * mosaic_tessellate (x = lon, y = lat for H3; BNG metres), on the GPU.  Row g's cells are
+ * cells[offsets[g] .. offsets[g + 1]) of the result (mosaic_cell_lists_export).
+ * H3: per polygon part, H3 C v3.7 polyfill(shell, holes, res) as h3-java 3.7.0 is called by
+ * H3IndexSystem.polyfill (core/index/H3IndexSystem.scala:113-126): the cells whose h3ToGeo centre
+ * H3's pointInsidePolygon accepts, reached from the cells of the sampled ring edges; the parts' lists
+ * concatenated, each in the order h3-java returns (H3's output-table slot order).  Vertices through
+ * Math.toRadians (option "jdk").
+ * BNG: BNGIndexSystem.polyfill (core/index/BNGIndexSystem.scala:185-204): the cells reached from
+ * the vertex and centroid cells whose square's centroid the geometry contains (JTS), ordered as
+ * the reference's Scala immutable HashSet iterates them.
+ * status[g]: MOSAIC_POLYFILL_OK, or MOSAIC_POLYFILL_UNSUPPORTED (no cells written) for an H3 row
+ * whose search meets a pentagon or holds a non-finite vertex, or a BNG row without area.  An empty
+ * geometry gives no cells.  Errors: MOSAIC_E_RES, MOSAIC_E_NAN (BNG NaN vertex), MOSAIC_E_CAPACITY. */
+#define MOSAIC_POLYFILL_OK 0
+#define MOSAIC_POLYFILL_UNSUPPORTED (-2)
+typedef struct mosaic_cell_lists mosaic_cell_lists;
+int mosaic_polyfill(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
+                    const int64_t* part_rings, const int64_t* ring_offsets, const double* xy, mosaic_cell_lists** out);
+int mosaic_cell_lists_info(const mosaic_cell_lists* lists, int64_t* n_rows, int64_t* n_cells);
+/* offsets[n_rows + 1], cells[n_cells], status[n_rows] (any may be null) */
+int mosaic_cell_lists_export(const mosaic_cell_lists* lists, int64_t* offsets, int64_t* cells, int32_t* status);
+int mosaic_cell_lists_destroy(mosaic_cell_lists* lists);
+/* Device time (HIP events on the calling thread's stream) of the calling thread's last mosaic_polyfill, ms. */
+double mosaic_polyfill_last_ms(void);
+
+/* Execution state of the calling thread on ctx (its device, stream, the "jdk" option and the
+ * device's CU count), for the library's own translation units. */
+int mosaic_ctx_exec(mosaic_ctx* ctx, int* device, void** stream, int* jdk, int* n_cu);
+
 /* ---- grid_boundaryaswkb over a cell column (BNG) ---- */
 /* out[93 i .. 93 i + 92] = the WKB JTS writes for BNGIndexSystem.indexToGeometry(ids[i])
  * (core/index/BNGIndexSystem.scala indexToGeometry; functions/MosaicContext.scala

@@ -39,6 +39,8 @@ EXPORTS = [
     "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb", "mosaic_point_to_cell_exact",
     "mosaic_diag_libm", "mosaic_point_coords_to_cell", "mosaic_point_coords_decode", "mosaic_bng_parse_column",
     "mosaic_chip_table_create_arrow", "mosaic_chip_table_build_info", "mosaic_h3_cell_geometry",
+    "mosaic_polyfill", "mosaic_cell_lists_info", "mosaic_cell_lists_export", "mosaic_cell_lists_destroy",
+    "mosaic_polyfill_last_ms", "mosaic_ctx_exec",
 ]
 
 GEOM_WKB = 0
@@ -133,6 +135,13 @@ def lib():
         "mosaic_bng_parse_column": ([vp, i32, vp, vp, vp, i64, vp], i32),
         "mosaic_chip_table_create_arrow": ([vp, i32, i32, i64, vp, vp, vp, i32, vp, vp, i32, ctypes.POINTER(vp)], i32),
         "mosaic_chip_table_build_info": ([vp, vp, vp], i32),
+        "mosaic_polyfill": ([vp, i32, i32, i64, vp, vp, vp, vp, ctypes.POINTER(vp)], i32),
+        "mosaic_cell_lists_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "mosaic_cell_lists_export": ([vp, vp, vp, vp], i32),
+        "mosaic_cell_lists_destroy": ([vp], i32),
+        "mosaic_polyfill_last_ms": ([], ctypes.c_double),
+        "mosaic_ctx_exec": ([vp, ctypes.POINTER(i32), ctypes.POINTER(vp), ctypes.POINTER(i32), ctypes.POINTER(i32)],
+                            i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -675,6 +675,37 @@ class MosaicContext:
                                                  N.ptr(out)))
         return [out[93 * i:93 * (i + 1)].tobytes() for i in range(len(ids))]
 
+    def grid_polyfill(self, polygons, resolution, raw=False):
+        """grid_polyfill(geometry, res) (expressions/index/Polyfill.scala nullSafeEval ->
+        IndexSystem.polyfill: H3IndexSystem.scala:113-126, BNGIndexSystem.scala:185-204) over a
+        PolygonSet, on this context's GPU (mosaic_polyfill).  Returns one list per geometry: int64
+        cells (H3), or BNG ids formatted as the reference's StringType ids unless raw=True.  A row the
+        engine does not answer (an H3 search meeting a pentagon, a non-finite vertex, a BNG geometry
+        without area) raises MosaicError."""
+        res = self.index_system.get_resolution(resolution)
+        h = ctypes.c_void_p()
+        N.check(N.lib().mosaic_polyfill(self.handle, self.index_system.grid, res, len(polygons),
+                                        N.ptr(polygons.geom_parts), N.ptr(polygons.part_rings),
+                                        N.ptr(polygons.ring_offsets), N.ptr(polygons.xy), ctypes.byref(h)))
+        try:
+            n_rows, n_cells = ctypes.c_int64(0), ctypes.c_int64(0)
+            N.check(N.lib().mosaic_cell_lists_info(h, ctypes.byref(n_rows), ctypes.byref(n_cells)))
+            offs = np.zeros(n_rows.value + 1, np.int64)
+            cells = np.zeros(max(n_cells.value, 1), np.int64)
+            status = np.zeros(max(n_rows.value, 1), np.int32)
+            N.check(N.lib().mosaic_cell_lists_export(h, N.ptr(offs), N.ptr(cells), N.ptr(status)))
+        finally:
+            N.lib().mosaic_cell_lists_destroy(h)
+        bad = np.nonzero(status[:n_rows.value] != 0)[0]
+        if len(bad):
+            raise N.MosaicError(N.MOSAIC_E_ARG, f"grid_polyfill: rows {bad[:8].tolist()} are not supported by this "
+                                                "engine (H3 search meeting a pentagon, non-finite vertex, or a "
+                                                "BNG geometry without area)")
+        out = [cells[offs[g]:offs[g + 1]].copy() for g in range(n_rows.value)]
+        if raw or self.index_system.grid == N.GRID_H3:
+            return out
+        return [list(self._serialize(c)) for c in out]
+
     def st_intersects_aggregate(self, left, right):
         """left.join(right, left_index.index_id == right_index.index_id).groupBy(left_key, right_key)
         .agg(st_intersects_aggregate(left_index, right_index)) over two chip tables

@@ -2626,6 +2626,16 @@ extern "C" {
 
 int mosaic_tess_fail(int code, const char* msg) { return fail(code, msg); }
 
+int mosaic_ctx_exec(mosaic_ctx* ctx, int* device, void** stream, int* jdk, int* n_cu) {
+    ENTER(ctx);
+    HIP_TRY(hipSetDevice(c->device));
+    *device = c->device;
+    *stream = (void*)c->stream;
+    *jdk = c->jdk;
+    *n_cu = c->n_cu;
+    return MOSAIC_OK;
+}
+
 int mosaic_abi_version(void) { return MOSAIC_ABI_VERSION; }
 const char* mosaic_last_error(void) { return g_last_error.c_str(); }
 

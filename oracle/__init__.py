@@ -76,6 +76,14 @@ def lib():
         L.oracle_h3_to_geo_boundary.argtypes = [i64, vp]
         L.oracle_h3_is_pentagon.restype = i32
         L.oracle_h3_is_pentagon.argtypes = [i64]
+        L.oracle_h3_polyfill.restype = i64
+        L.oracle_h3_polyfill.argtypes = [vp, vp, vp, i32, i32, vp, i64, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_h3_ring1.restype = i32
+        L.oracle_h3_ring1.argtypes = [i64, vp]
+        L.oracle_jts_centroid.restype = i32
+        L.oracle_jts_centroid.argtypes = [vp, vp, vp]
+        L.oracle_bng_polyfill.restype = i64
+        L.oracle_bng_polyfill.argtypes = [vp, i32, vp, i64]
         _lib = L
     return _lib
 
@@ -310,3 +318,74 @@ def pip_join(chips, grid, res, x, y, n_polygons, jdk=8, pairs=False, threads=1):
     total = lib().oracle_pip_join(ctypes.byref(c), grid, res, jdk, _ptr(x), _ptr(y), len(x), _ptr(counts),
                                   n_polygons, None, None, 0, threads)
     return counts[:n_polygons], total
+
+
+class _Geom(ctypes.Structure):
+    _fields_ = [("xy", ctypes.c_void_p), ("ring_offsets", ctypes.c_void_p), ("part_rings", ctypes.c_void_p),
+                ("n_parts", ctypes.c_int64)]
+
+
+def _geom_arrays(parts):
+    """parts: list of parts, each a list of rings of (x, y) -> (xy, ring_offsets, part_rings)."""
+    rings = [np.asarray(r, np.float64).reshape(-1, 2) for part in parts for r in part]
+    xy = np.ascontiguousarray(np.concatenate(rings) if rings else np.zeros((0, 2)), np.float64)
+    ro = np.zeros(len(rings) + 1, np.int64)
+    np.cumsum([len(r) for r in rings], out=ro[1:])
+    pr = np.zeros(len(parts) + 1, np.int64)
+    np.cumsum([len(p) for p in parts], out=pr[1:])
+    return xy, ro, pr
+
+
+def h3_polyfill_part(rings, res, jdk=8, cap=1 << 22):
+    """H3 polyfill of one polygon part (rings of (lon, lat) degrees, shell first): (cells in H3's
+    output order, collision_free)."""
+    lat = np.ascontiguousarray(np.concatenate([[to_radians(v[1], jdk) for v in r] for r in rings]), np.float64)
+    lon = np.ascontiguousarray(np.concatenate([[to_radians(v[0], jdk) for v in r] for r in rings]), np.float64)
+    ro = np.zeros(len(rings) + 1, np.int64)
+    np.cumsum([len(r) for r in rings], out=ro[1:])
+    out = np.zeros(cap, np.int64)
+    cf = ctypes.c_int(0)
+    n = lib().oracle_h3_polyfill(_ptr(lat), _ptr(lon), _ptr(ro), len(rings), res, _ptr(out), cap, ctypes.byref(cf))
+    if n < 0:
+        raise RuntimeError("oracle_h3_polyfill failed")
+    return out[:n].copy(), bool(cf.value)
+
+
+def h3_polyfill(parts, res, jdk=8):
+    """grid_polyfill (H3) of a geometry given as parts: the parts' cells concatenated, plus whether
+    every part's order is certain (collision-free)."""
+    cells, ok = [], True
+    for rings in parts:
+        if not rings or len(rings[0]) == 0:
+            continue
+        c, cf = h3_polyfill_part(rings, res, jdk)
+        cells.append(c)
+        ok &= cf
+    return (np.concatenate(cells) if cells else np.zeros(0, np.int64)), ok
+
+
+def h3_ring1(cell):
+    out = np.zeros(16, np.int64)
+    n = lib().oracle_h3_ring1(int(cell), _ptr(out))
+    return out[:n].copy()
+
+
+def jts_centroid(parts):
+    xy, ro, pr = _geom_arrays(parts)
+    g = _Geom(_ptr(xy).value, _ptr(ro).value, _ptr(pr).value, len(parts))
+    c = np.zeros(2, np.float64)
+    if not lib().oracle_jts_centroid(ctypes.byref(g), _ptr(c), _ptr(c[1:])):
+        return None
+    return float(c[0]), float(c[1])
+
+
+def bng_polyfill(parts, res, cap=1 << 22):
+    """grid_polyfill (BNG) of a geometry given as parts (eastings / northings): the cell set, as a
+    sorted array."""
+    xy, ro, pr = _geom_arrays(parts)
+    g = _Geom(_ptr(xy).value, _ptr(ro).value, _ptr(pr).value, len(parts))
+    out = np.zeros(cap, np.int64)
+    n = lib().oracle_bng_polyfill(ctypes.byref(g), res, _ptr(out), cap)
+    if n < 0:
+        raise RuntimeError("oracle_bng_polyfill failed")
+    return np.sort(out[:n])

@@ -93,6 +93,19 @@ int oracle_intersects(const oracle_geom* a, const oracle_geom* b);
 /* The same from two WKBs; -1 on parse error. */
 int oracle_wkb_intersects(const uint8_t* wa, int64_t la, const uint8_t* wb, int64_t lb);
 
+/* ---- grid_polyfill (polyfill.c) ---- */
+/* H3 polyfill of one polygon part (rings [0, n_rings) in lat / lon radians, ring_off[n_rings + 1]);
+ * cells in H3's output-slot order; *collision_free = 0 when probing displaced a cell (then only the
+ * set is certain).  -1: cap too small. */
+int64_t oracle_h3_polyfill(const double* lat, const double* lon, const int64_t* ring_off, int n_rings, int res,
+                           int64_t* out, int64_t cap, int* collision_free);
+/* kRing(h, 1) as a set from the cell geometry (h first). */
+int oracle_h3_ring1(int64_t h, int64_t* out);
+/* JTS Centroid of a polygonal geometry (area-weighted); 0 when its area is 0. */
+int oracle_jts_centroid(const oracle_geom* g, double* cx, double* cy);
+/* BNG polyfill of a geometry: cells in breadth-first order; -1 on cap overflow / NaN / no area. */
+int64_t oracle_bng_polyfill(const oracle_geom* g, int res, int64_t* out, int64_t cap);
+
 /* ---- chip join ---- */
 typedef struct {
     int64_t n_chips;

@@ -58,6 +58,9 @@ case $STEP in
   bench)
     run bench 900 python -u bench.py
     ;;
+  t)  # TESTS="tests/a.py tests/b.py" bash tools/gpu_r02d.sh t
+    run t_sel 900 $PYT $TESTS -s
+    ;;
   full)  # whole GPU suite, smoke, bench line, kernel stats of the bench
     run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
     run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
