@@ -351,6 +351,14 @@ int mosaic_cell_lists_destroy(mosaic_cell_lists* lists);
 /* Device time (HIP events on the calling thread's stream) of the calling thread's last mosaic_polyfill, ms. */
 double mosaic_polyfill_last_ms(void);
 
+/* getBufferRadius(geometry, res) per geometry (the radius mosaicFill buffers by, core/Mosaic.scala:68):
+ * H3 (H3IndexSystem.scala:73-80): the largest distance (degrees) from the centroid of the cell
+ * holding the geometry's JTS centroid (its indexToGeometry polygon's JTS centroid) to that polygon's
+ * ring points; NaN for a geometry without area.  BNG (BNGIndexSystem.scala:146-149): edge * sqrt(2) / 2.
+ * Geometries in the flat-ring layout of mosaic_polyfill; out[n_geoms]. */
+int mosaic_buffer_radius(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
+                         const int64_t* part_rings, const int64_t* ring_offsets, const double* xy, double* out);
+
 /* Execution state of the calling thread on ctx (its device, stream, the "jdk" option and the
  * device's CU count), for the library's own translation units. */
 int mosaic_ctx_exec(mosaic_ctx* ctx, int* device, void** stream, int* jdk, int* n_cu);

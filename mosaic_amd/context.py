@@ -706,6 +706,17 @@ class MosaicContext:
             return out
         return [list(self._serialize(c)) for c in out]
 
+    def buffer_radius(self, polygons, resolution):
+        """IndexSystem.getBufferRadius(geometry, res) per geometry of a PolygonSet (the radius
+        Mosaic.mosaicFill buffers by, core/Mosaic.scala:68; H3IndexSystem.scala:73-80,
+        BNGIndexSystem.scala:146-149), computed on this context's GPU (H3).  float64[n]."""
+        res = self.index_system.get_resolution(resolution)
+        out = np.zeros(max(len(polygons), 1), np.float64)
+        N.check(N.lib().mosaic_buffer_radius(self.handle, self.index_system.grid, res, len(polygons),
+                                             N.ptr(polygons.geom_parts), N.ptr(polygons.part_rings),
+                                             N.ptr(polygons.ring_offsets), N.ptr(polygons.xy), N.ptr(out)))
+        return out[:len(polygons)]
+
     def st_intersects_aggregate(self, left, right):
         """left.join(right, left_index.index_id == right_index.index_id).groupBy(left_key, right_key)
         .agg(st_intersects_aggregate(left_index, right_index)) over two chip tables

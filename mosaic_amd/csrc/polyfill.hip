@@ -396,7 +396,7 @@ uint64_t scala_set_order_key(int64_t v) {
 }
 
 // JTS 1.19 Orientation.isCCW of a closed ring
-bool jts_is_ccw(const double* xy, int64_t n) {
+__host__ __device__ inline bool jts_is_ccw(const double* xy, int64_t n) {
     const int64_t npts = n - 1;
     if (npts < 3) return false;
     int64_t up_hi = 0, up_low = -1;
@@ -416,9 +416,10 @@ bool jts_is_ccw(const double* xy, int64_t n) {
         down_low = (down_low + 1) % npts;
     } while (down_low != up_hi && xy[2 * down_low + 1] == hi_y);
     const int64_t down_hi = down_low > 0 ? down_low - 1 : npts - 1;
-    auto eq = [&](int64_t a, int64_t b) { return xy[2 * a] == xy[2 * b] && xy[2 * a + 1] == xy[2 * b + 1]; };
-    if (eq(up_hi, down_hi)) {
-        if (eq(up_low, up_hi) || eq(down_low, up_hi) || eq(up_low, down_low)) return false;
+#define PF_EQ2(a, b) (xy[2 * (a)] == xy[2 * (b)] && xy[2 * (a) + 1] == xy[2 * (b) + 1])
+    if (PF_EQ2(up_hi, down_hi)) {
+        if (PF_EQ2(up_low, up_hi) || PF_EQ2(down_low, up_hi) || PF_EQ2(up_low, down_low)) return false;
+#undef PF_EQ2
         return pip::orientation_index(xy[2 * up_low], xy[2 * up_low + 1], xy[2 * up_hi], xy[2 * up_hi + 1],
                                       xy[2 * down_low], xy[2 * down_low + 1]) == 1;
     }
@@ -454,6 +455,53 @@ bool jts_centroid(int64_t g, const int64_t* geom_parts, const int64_t* part_ring
     *cx = sx / 3 / a2;
     *cy = sy / 3 / a2;
     return true;
+}
+
+// getBufferRadius (H3IndexSystem.scala:73-80) from the geometry's centroid: the centroid's cell
+// (geoToH3 after Math.toRadians), its indexToGeometry ring (h3ToGeoBoundary in degrees, closed with
+// the first vertex), that polygon's JTS centroid, and the largest distance (Coordinate.distance) of
+// a ring point from it
+__global__ void __launch_bounds__(256) k_buffer_radius_h3(const double* cx, const double* cy, const uint8_t* ok,
+                                                          int64_t n, int res, int jdk, double* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!ok[i]) {
+            out[i] = NAN;
+            continue;
+        }
+        const uint64_t cell = h3::h3_exact(h3::to_radians(cy[i], jdk), h3::to_radians(cx[i], jdk), res);
+        double v[20], xy[22];
+        const int nv = h3geom::h3_to_geo_boundary(cell, v);
+        if (nv <= 0) {
+            out[i] = NAN;
+            continue;
+        }
+        for (int k = 0; k < nv; k++) {
+            xy[2 * k] = h3geom::to_degrees(v[2 * k + 1], jdk);
+            xy[2 * k + 1] = h3geom::to_degrees(v[2 * k], jdk);
+        }
+        xy[2 * nv] = xy[0];
+        xy[2 * nv + 1] = xy[1];
+        const int64_t m = nv + 1;
+        // JTS Centroid of the polygon (shell only)
+        const double bx = xy[0], by = xy[1];
+        const double sign = !jts_is_ccw(xy, m) ? 1.0 : -1.0;
+        double sx = 0, sy = 0, a2 = 0;
+        for (int64_t k = 0; k + 1 < m; k++) {
+            const double p1x = xy[2 * k], p1y = xy[2 * k + 1], p2x = xy[2 * k + 2], p2y = xy[2 * k + 3];
+            const double area2 = (p1x - bx) * (p2y - by) - (p2x - bx) * (p1y - by);
+            sx += sign * area2 * (bx + p1x + p2x);
+            sy += sign * area2 * (by + p1y + p2y);
+            a2 += sign * area2;
+        }
+        const double gx = sx / 3 / a2, gy = sy / 3 / a2;
+        double r = 0;
+        for (int64_t k = 0; k < m; k++) {
+            const double dx = xy[2 * k] - gx, dy = xy[2 * k + 1] - gy;
+            const double d = sqrt(dx * dx + dy * dy);
+            r = d > r ? d : r;
+        }
+        out[i] = r;
+    }
 }
 
 struct Input {
@@ -911,5 +959,39 @@ int mosaic_cell_lists_destroy(mosaic_cell_lists* l) {
 }
 
 double mosaic_polyfill_last_ms(void) { return g_last_polyfill_ms; }
+
+int mosaic_buffer_radius(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
+                         const int64_t* part_rings, const int64_t* ring_offsets, const double* xy, double* out) {
+    if (!ctx || !out || n_geoms < 0 || (n_geoms > 0 && (!geom_parts || !part_rings || !ring_offsets)))
+        return mosaic_tess_fail(MOSAIC_E_ARG, "invalid argument");
+    if (grid == MOSAIC_GRID_BNG) {
+        if (!bng::valid_resolution(res)) return mosaic_tess_fail(MOSAIC_E_RES, "invalid BNG resolution");
+        const double r = (double)bng::edge_size(res) * 1.4142135623730951 / 2;  // size * math.sqrt(2) / 2
+        for (int64_t g = 0; g < n_geoms; g++) out[g] = r;
+        return MOSAIC_OK;
+    }
+    if (grid != MOSAIC_GRID_H3 || res < 0 || res > 15)
+        return mosaic_tess_fail(grid == MOSAIC_GRID_H3 ? MOSAIC_E_RES : MOSAIC_E_ARG, "invalid grid or resolution");
+    if (n_geoms == 0) return MOSAIC_OK;
+    int device = 0, jdk = 8, n_cu = 256;
+    void* stream = nullptr;
+    PF_RC(mosaic_ctx_exec(ctx, &device, &stream, &jdk, &n_cu));
+    hipStream_t st = (hipStream_t)stream;
+    std::vector<double> cx((size_t)n_geoms, 0), cy((size_t)n_geoms, 0);
+    std::vector<uint8_t> ok((size_t)n_geoms, 0);
+    for (int64_t g = 0; g < n_geoms; g++)
+        ok[g] = jts_centroid(g, geom_parts, part_rings, ring_offsets, xy, &cx[g], &cy[g]) ? 1 : 0;
+    Buf d_cx, d_cy, d_ok, d_out;
+    PF_RC(upload(d_cx, cx, st));
+    PF_RC(upload(d_cy, cy, st));
+    PF_RC(upload(d_ok, ok, st));
+    PF_RC(d_out.reserve((size_t)n_geoms * 8));
+    hipLaunchKernelGGL(k_buffer_radius_h3, dim3(blocks_for(n_geoms, n_cu)), dim3(256), 0, st, d_cx.as<double>(),
+                       d_cy.as<double>(), d_ok.as<uint8_t>(), n_geoms, res, jdk, d_out.as<double>());
+    PF_TRY(hipGetLastError());
+    PF_TRY(hipMemcpyAsync(out, d_out.p, (size_t)n_geoms * 8, hipMemcpyDeviceToHost, st));
+    PF_TRY(hipStreamSynchronize(st));
+    return MOSAIC_OK;
+}
 
 }  // extern "C"

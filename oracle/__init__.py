@@ -82,6 +82,8 @@ def lib():
         L.oracle_h3_ring1.argtypes = [i64, vp]
         L.oracle_jts_centroid.restype = i32
         L.oracle_jts_centroid.argtypes = [vp, vp, vp]
+        L.oracle_h3_buffer_radius.restype = f64
+        L.oracle_h3_buffer_radius.argtypes = [vp, i32, i32]
         L.oracle_bng_polyfill.restype = i64
         L.oracle_bng_polyfill.argtypes = [vp, i32, vp, i64]
         _lib = L
@@ -389,3 +391,10 @@ def bng_polyfill(parts, res, cap=1 << 22):
     if n < 0:
         raise RuntimeError("oracle_bng_polyfill failed")
     return np.sort(out[:n])
+
+
+def h3_buffer_radius(parts, res, jdk=8):
+    """H3IndexSystem.getBufferRadius of a geometry given as parts of (lon, lat) rings."""
+    xy, ro, pr = _geom_arrays(parts)
+    g = _Geom(_ptr(xy).value, _ptr(ro).value, _ptr(pr).value, len(parts))
+    return lib().oracle_h3_buffer_radius(ctypes.byref(g), res, jdk)

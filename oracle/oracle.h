@@ -103,6 +103,8 @@ int64_t oracle_h3_polyfill(const double* lat, const double* lon, const int64_t* 
 int oracle_h3_ring1(int64_t h, int64_t* out);
 /* JTS Centroid of a polygonal geometry (area-weighted); 0 when its area is 0. */
 int oracle_jts_centroid(const oracle_geom* g, double* cx, double* cy);
+/* H3 getBufferRadius of a geometry (degrees); NaN without area. */
+double oracle_h3_buffer_radius(const oracle_geom* g, int res, int jdk);
 /* BNG polyfill of a geometry: cells in breadth-first order; -1 on cap overflow / NaN / no area. */
 int64_t oracle_bng_polyfill(const oracle_geom* g, int res, int64_t* out, int64_t cap);
 

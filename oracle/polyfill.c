@@ -450,3 +450,33 @@ fail:
     free(visited.k);
     return -1;
 }
+
+/* getBufferRadius (H3IndexSystem.scala:73-80): the cell of the geometry's JTS centroid
+ * (h3.geoToH3(centroid.y, centroid.x) through Math.toRadians), its indexToGeometry polygon
+ * (h3ToGeoBoundary through Math.toDegrees, closed with the first vertex), that polygon's JTS
+ * centroid, the largest Coordinate.distance of a ring point from it.  NaN without area. */
+static double to_degrees(double rad, int jdk) { return jdk <= 8 ? rad * 180.0 / M_PI : rad * 57.29577951308232; }
+
+double oracle_h3_buffer_radius(const oracle_geom* g, int res, int jdk) {
+    double cx, cy;
+    if (!oracle_jts_centroid(g, &cx, &cy)) return NAN;
+    int64_t cell = oracle_h3_geo_to_h3(oracle_to_radians(cy, jdk), oracle_to_radians(cx, jdk), res);
+    double v[20], xy[22];
+    int nv = oracle_h3_to_geo_boundary(cell, v);
+    for (int k = 0; k < nv; k++) {
+        xy[2 * k] = to_degrees(v[2 * k + 1], jdk);
+        xy[2 * k + 1] = to_degrees(v[2 * k], jdk);
+    }
+    xy[2 * nv] = xy[0];
+    xy[2 * nv + 1] = xy[1];
+    int64_t ro[2] = {0, nv + 1}, pr[2] = {0, 1};
+    oracle_geom hex = {xy, ro, pr, 1};
+    double hx, hy;
+    if (!oracle_jts_centroid(&hex, &hx, &hy)) return NAN;
+    double r = 0;
+    for (int k = 0; k <= nv; k++) {
+        double dx = xy[2 * k] - hx, dy = xy[2 * k + 1] - hy, d = sqrt(dx * dx + dy * dy);
+        if (d > r) r = d;
+    }
+    return r;
+}

@@ -311,3 +311,36 @@ def test_gpu_bng_london(bngctx, res):
         assert keys == sorted(keys)
     s = bngctx.grid_polyfill(sub.subset([0]), res)
     assert all(isinstance(v, str) for v in s[0])
+
+
+# ---- getBufferRadius (H3IndexSystem.scala:73-80, BNGIndexSystem.scala:146-149) ----
+def test_oracle_jts_centroid_cases():
+    """JTS 1.19 Centroid (area-weighted triangle fan, shells reset the base point, holes subtract).
+    The docs' st_centroid2D example (docs/source/api/spatial-functions.rst:258-262) shows
+    {25.454545454545453, 26.96969696969697}; JTS 1.19's cg3.y / 3 / areasum2 rounds y one ulp higher
+    (the docs were rendered with another geometry API), so only x is compared with it."""
+    cx, cy = oracle.jts_centroid([[[(30, 10), (40, 40), (20, 40), (10, 20), (30, 10)]]])
+    assert cx == 25.454545454545453 and abs(cy - 26.96969696969697) <= 4e-15
+    assert oracle.jts_centroid([[[(0, 0), (4, 0), (4, 4), (0, 4), (0, 0)]]]) == (2.0, 2.0)
+    # a hole removes its area: square 0..4 minus square 0..2 -> centroid (7/3, 7/3)
+    cx, cy = oracle.jts_centroid([[[(0, 0), (4, 0), (4, 4), (0, 4), (0, 0)], [(0, 0), (0, 2), (2, 2), (2, 0), (0, 0)]]])
+    assert abs(cx - 7 / 3) < 1e-12 and abs(cy - 7 / 3) < 1e-12
+    assert oracle.jts_centroid([[[(0, 0), (1, 1), (2, 2), (0, 0)]]]) is None
+
+
+def test_oracle_buffer_radius_scale():
+    zones = PolygonSet.load("nyc_taxi_zones")
+    r9 = oracle.h3_buffer_radius(zones.parts(0), 9)
+    r10 = oracle.h3_buffer_radius(zones.parts(0), 10)
+    assert 0.0015 < r9 < 0.003 and abs(r9 / r10 - math.sqrt(7)) < 0.2
+
+
+@pytest.mark.gpu
+def test_gpu_buffer_radius_matches_oracle(h3ctx, bngctx):
+    zones = PolygonSet.load("nyc_taxi_zones")
+    for res in (0, 5, 9, 11, 13):
+        got = h3ctx.buffer_radius(zones, res)
+        want = np.array([oracle.h3_buffer_radius(zones.parts(g), res) for g in range(len(zones))])
+        assert np.array_equal(got, want), res
+    london = PolygonSet.load("london_postcodes_bng")
+    assert np.all(bngctx.buffer_radius(london, 4) == 100 * math.sqrt(2) / 2)
