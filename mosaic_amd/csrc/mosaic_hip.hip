@@ -575,12 +575,15 @@ __device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t byt
 __device__ inline uint32_t quad_lookup(const StreamArgs& s, const uint16_t* quad, const uint32_t* qmask,
                                        const uint16_t* qcode, uint32_t ixC, uint32_t iyC) {
     const uint32_t q = quad[__umul24(iyC >> s.qsh, (uint32_t)s.qnx) + (ixC >> s.qsh)];
-    const uint32_t r = q & 0x7fffu;
-    const bool rec = q >= 0x8000u && r < (uint32_t)s.n_qrec;
-    const uint32_t b = (((iyC >> (s.cs + s.qrl)) & 7u) << 3) | ((ixC >> (s.cs + s.qrl)) & 7u);
-    const uint32_t w = qmask[rec ? 2u * r + (b >> 5) : 0u];
-    const uint32_t c = qcode[rec ? r : 0u];
-    return (rec && ((w >> (b & 31u)) & 1u)) ? c : q;
+    // q >= 0x8000 with record index q & 0x7fff < n_qrec, as one unsigned compare (q < 0x8000 wraps)
+    const uint32_t r = q - 0x8000u;
+    const bool rec = r < (uint32_t)s.n_qrec;
+    const uint32_t sh = (uint32_t)(s.cs + s.qrl);
+    const uint32_t b = (__builtin_amdgcn_ubfe(iyC, sh, 3u) << 3) | __builtin_amdgcn_ubfe(ixC, sh, 3u);
+    const uint32_t rr = rec ? r : 0u;  // record 0 (mask words 0 and 1) is always readable
+    const uint32_t w = qmask[2u * rr + (b >> 5)];
+    const uint32_t c = qcode[rr];
+    return (rec && __builtin_amdgcn_ubfe(w, b & 31u, 1u)) ? c : q;
 }
 
 template <bool LDS_COUNTS, bool PAIRS, bool VEC>
@@ -752,6 +755,9 @@ struct PipeGroup {
 // quad-level value standing for "non-finite coordinates" in a group (never a code: codes are
 // <= kMaxRasterKeys + 1 or >= kSubBlock): the row takes the tile path
 static const uint32_t kPipeNonFinite = 0x7fffu;
+static_assert(tiles::kMaxRasterKeys + 1 < 0x7fff, "key codes stay below kPipeNonFinite");
+// stage B -> D marker of a row in a line sub-block (above every code)
+static const uint32_t kPipeLine = 0x10000u;
 
 template <bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_pipe(JoinArgs a, StreamArgs s) {
@@ -777,6 +783,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     uint32_t* wq = stage + wave * s.stage_words;
     uint32_t wn = 0;
     const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u;
+    const double gx0 = -s.x0 * s.sxC, gy0 = -s.y0 * s.syC;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
     const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
     // full groups of this wave: wbase + t stride, t < T
@@ -787,17 +794,20 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const bool lv = valid && live[k];
-            const double gx = fmin(fmax((x[k] - s.x0) * s.sxC, 0.0), s.gxmax);  // NaN -> 0
-            const double gy = fmin(fmax((y[k] - s.y0) * s.syC, 0.0), s.gymax);
+            // (x - x0) sxC as one fma (x sxC - x0 sxC): within the raster's 1e-6-cell widening
+            const double gx = fmin(fmax(fma(x[k], s.sxC, gx0), 0.0), s.gxmax);  // NaN -> 0
+            const double gy = fmin(fmax(fma(y[k], s.syC, gy0), 0.0), s.gymax);
             const uint32_t ixC = (uint32_t)(int)gx, iyC = (uint32_t)(int)gy;
-            g.u[k] = (float)(gx - (double)(ixC & ~cm));
-            g.v[k] = (float)(gy - (double)(iyC & ~cm));
+            // the offset in the sub-block, leaf cells: (ixC & cm) + fract(gx) (gx >= 0)
+            g.u[k] = (float)(ixC & cm) + (float)__builtin_amdgcn_fract(gx);
+            g.v[k] = (float)(iyC & cm) + (float)__builtin_amdgcn_fract(gy);
             g.lf[k] = ((iyC & cm) << s.cs) | (ixC & cm);
             const uint32_t q = quad_lookup(s, quad, qmask, qcode, ixC, iyC);
             // dead rows answer 0, non-finite ones kPipeNonFinite (-> kMixed)
             g.qv[k] = !lv ? 0u : (__builtin_isfinite(x[k] + y[k]) ? q : kPipeNonFinite);
             g.tbv[k] = tb[__umul24(iyC >> s.tsh, (uint32_t)s.tnx) + (ixC >> s.tsh)];
-            const uint32_t local = (((iyC >> s.cs) & qm) << s.qs) | ((ixC >> s.cs) & qm);
+            const uint32_t local = (__builtin_amdgcn_ubfe(iyC, (uint32_t)s.cs, (uint32_t)s.qs) << s.qs) |
+                                   __builtin_amdgcn_ubfe(ixC, (uint32_t)s.cs, (uint32_t)s.qs);
             const uint32_t off = ((((g.qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
             g.code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, g.qv[k] >= 0x8000u ? off : kNoLoad, 0, MOSAIC_AUX_SUB);
         }
@@ -807,7 +817,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t c = g.qv[k] >= 0x8000u ? g.code[k] : g.qv[k];
-            g.code[k] = c;
             const bool blk = c - 0x8000u < 0x7fffu;  // kSubBlock | n, not kMixed
             const bool line = blk && (c & 0x4000u);
             const uint32_t n = c & 0x3fffu;
@@ -815,6 +824,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const uint32_t roff = (g.tbv[k] - 8u * (n + 1u)) << 1;
             g.leaf[k] = __builtin_amdgcn_raw_buffer_load_b16(rblk, (blk && !line) ? loff : kNoLoad, 0, MOSAIC_AUX_LEAF);
             g.lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rblk, line ? roff : kNoLoad, 0, MOSAIC_AUX_LINE);
+            // for stage D: kPipeLine for a line row, else the code to OR with the gathered leaf code
+            // (0 for leaf rows; out-of-range gathers return 0)
+            g.code[k] = line ? kPipeLine : (blk ? 0u : c);
         }
     };
     // stage D: the answers -> counts and the mixed-row stage
@@ -827,26 +839,25 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const uint32_t pos = g.lrec[k].w & 0xffffu, neg = g.lrec[k].w >> 16;
             uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
             lc = sv <= -1.0f ? neg : lc;
-            const uint32_t gc = g.code[k];
-            const bool blk = gc - 0x8000u < 0x7fffu, line = blk && (gc & 0x4000u);
-            uint32_t c = line ? lc : (blk ? g.leaf[k] : gc);
-            code[k] = c == kPipeNonFinite ? (uint32_t)tiles::kMixed : c;
+            // answers: 0, key + 1 (<= kMaxRasterKeys), or >= kPipeNonFinite (kMixed, non-finite):
+            // the tile path
+            code[k] = g.code[k] == kPipeLine ? lc : (g.code[k] | g.leaf[k]);
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (LDS_COUNTS && !PAIRS) {
-                const uint32_t slot = code[k] - 1u < 0xfffeu ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
+                const uint32_t slot = code[k] - 1u < kPipeNonFinite - 1u ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
                 atomicAdd(&lds[slot], 1u);
-            } else if (code[k] - 1u < 0xfffeu) {
+            } else if (code[k] - 1u < kPipeNonFinite - 1u) {
                 emit_hit<LDS_COUNTS, PAIRS>(a, row_of(wb, k), code[k] - 1u, lds);
             }
         }
-        const bool anym = code[0] == tiles::kMixed || code[1] == tiles::kMixed || code[2] == tiles::kMixed ||
-                          code[3] == tiles::kMixed;
+        const bool anym = code[0] >= kPipeNonFinite || code[1] >= kPipeNonFinite || code[2] >= kPipeNonFinite ||
+                          code[3] >= kPipeNonFinite;
         if (__ballot(anym)) {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const bool m = code[k] == tiles::kMixed;
+                const bool m = code[k] >= kPipeNonFinite;
                 const unsigned long long mm = __ballot(m);
                 if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(wb, k) - a.row_lo);
                 wn += (uint32_t)__popcll(mm);

@@ -61,6 +61,12 @@ case $STEP in
   t)  # TESTS="tests/a.py tests/b.py" bash tools/gpu_r02d.sh t
     run t_sel 900 $PYT $TESTS -s
     ;;
+  perf)  # stream-kernel change: parity subset, C2 / C3 kernel bench, SQ instruction counters
+    run t_perf 900 $PYT "tests/test_gpu_parity.py::test_join_counts_match_oracle" "tests/test_gpu_parity.py::test_join_tiled_nyc_zones_match_oracle" "tests/test_gpu_parity.py::test_join_point_raster_sizes" -s
+    run kb_c2 300 python -u tools/kbench.py --n 1e9 --reps 8
+    run kb_c3 300 python -u tools/kbench.py --n 1e9 --res 10 --clustered --reps 8
+    bash tools/pmc_sq.sh
+    ;;
   full)  # whole GPU suite, smoke, bench line, kernel stats of the bench
     run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
     run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
