@@ -213,6 +213,14 @@ int mosaic_chip_table_create_arrow(mosaic_ctx* ctx, int grid, int res, int64_t n
                                    const int64_t* index_id, const void* wkb_offsets, int wkb_offsets32,
                                    const uint8_t* wkb, const int32_t* polygon_key, int32_t n_polygons,
                                    mosaic_chips** out);
+/* The array form (PointInPolygonJoin.joinArrayRows, sql/join/PointInPolygonJoin.scala:39-66): polygon
+ * row p's chip array (grid_tessellate's chips) is rows [chip_offsets[p], chip_offsets[p + 1]) of the
+ * flattened columns is_core / index_id / wkb (wkb_offsets indexed from chip_offsets[0], n + 1 entries);
+ * joins then count at most one pair per (point, polygon row), from the first chip of the row with
+ * the point's cell (array_position + element_at), as the reference does. */
+int mosaic_chip_table_create_arrays(mosaic_ctx* ctx, int grid, int res, int32_t n_polygons, const int64_t* chip_offsets,
+                                    const uint8_t* is_core, const int64_t* index_id, const int64_t* wkb_offsets,
+                                    const uint8_t* wkb, mosaic_chips** out);
 int mosaic_chip_table_destroy(mosaic_chips* chips);
 /* out8: n_chips, n_cells, n_border, n_vertices, n_rings, device_bytes, hash_capacity, n_polygons */
 int mosaic_chip_table_info(const mosaic_chips* chips, int64_t* out8);

@@ -239,6 +239,31 @@ class ChipTable:
             ctypes.byref(h)))
         self.handle = h
 
+    @classmethod
+    def from_arrays(cls, ctx, chip_offsets, is_core, index_id, wkb_list):
+        """The array form of the build side (PointInPolygonJoin.joinArrayRows,
+        sql/join/PointInPolygonJoin.scala:39-66): polygon row p's chip array (grid_tessellate output)
+        is rows [chip_offsets[p], chip_offsets[p + 1]) of the flattened chip columns; a point joins a
+        row at most once, through the row's first chip with the point's cell."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        chip_offsets = np.ascontiguousarray(chip_offsets, dtype=np.int64)
+        is_core = np.ascontiguousarray(is_core, dtype=np.uint8)
+        index_id = np.ascontiguousarray(index_id, dtype=np.int64)
+        lens = np.array([0 if w is None else len(w) for w in wkb_list], dtype=np.int64)
+        offsets = np.zeros(len(lens) + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        data = np.frombuffer(b"".join(b"" if w is None else bytes(w) for w in wkb_list), dtype=np.uint8)
+        data = np.ascontiguousarray(data) if len(data) else np.zeros(1, np.uint8)
+        self.n_polygons = len(chip_offsets) - 1
+        self.n_chips = len(index_id)
+        h = ctypes.c_void_p()
+        N.check(N.lib().mosaic_chip_table_create_arrays(
+            ctx.handle, ctx.index_system.grid, ctx.resolution_of_table, self.n_polygons, N.ptr(chip_offsets),
+            N.ptr(is_core), N.ptr(index_id), N.ptr(offsets), N.ptr(data), ctypes.byref(h)))
+        self.handle = h
+        return self
+
     def info(self):
         out = np.zeros(8, np.int64)
         N.check(N.lib().mosaic_chip_table_info(self.handle, N.ptr(out)))
@@ -551,6 +576,12 @@ class MosaicContext:
         """Build side: rows of grid_tessellateexplode output (MosaicExplode.scala:70-79)."""
         self.resolution_of_table = self.index_system.get_resolution(resolution)
         return ChipTable(self, is_core, index_id, wkb_list, polygon_key, n_polygons)
+
+    def chip_table_arrays(self, chip_offsets, is_core, index_id, wkb_list, resolution):
+        """Build side from grid_tessellate chip arrays, one array per polygon row (the array form of
+        PointInPolygonJoin, sql/join/PointInPolygonJoin.scala:39-66); see ChipTable.from_arrays."""
+        self.resolution_of_table = self.index_system.get_resolution(resolution)
+        return ChipTable.from_arrays(self, chip_offsets, is_core, index_id, wkb_list)
 
     def pip_join_count(self, chips, x, y, out=None):
         """Quickstart join + filter + groupBy(polygon).count(): int64 count per polygon key.
