@@ -803,8 +803,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             g.v[k] = (float)(iyC & cm) + (float)__builtin_amdgcn_fract(gy);
             g.lf[k] = ((iyC & cm) << s.cs) | (ixC & cm);
             const uint32_t q = quad_lookup(s, quad, qmask, qcode, ixC, iyC);
-            // dead rows answer 0, non-finite ones kPipeNonFinite (-> kMixed)
-            g.qv[k] = !lv ? 0u : (__builtin_isfinite(x[k] + y[k]) ? q : kPipeNonFinite);
+            // dead rows answer 0.  Non-finite coordinates need no test: fmax / fmin clamp them onto
+            // the grid's edge ring, whose sub-blocks are all 0 or kMixed (PointRaster edge_ok, a
+            // precondition of this kernel), and a non-finite point joins nothing in the reference
+            // (geoToH3 gives H3_NULL) -- 0 is its answer, kMixed sends it to the exact path.
+            g.qv[k] = lv ? q : 0u;
             g.tbv[k] = tb[__umul24(iyC >> s.tsh, (uint32_t)s.tnx) + (ixC >> s.tsh)];
             const uint32_t local = (__builtin_amdgcn_ubfe(iyC, (uint32_t)s.cs, (uint32_t)s.qs) << s.qs) |
                                    __builtin_amdgcn_ubfe(ixC, (uint32_t)s.cs, (uint32_t)s.qs);
@@ -843,6 +846,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             // the tile path
             code[k] = g.code[k] == kPipeLine ? lc : (g.code[k] | g.leaf[k]);
         }
+        // counts: one LDS add per point (points without a pair add to the lane's spill word: a
+        // masked add measured slower on clustered input)
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (LDS_COUNTS && !PAIRS) {
@@ -852,9 +857,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
                 emit_hit<LDS_COUNTS, PAIRS>(a, row_of(wb, k), code[k] - 1u, lds);
             }
         }
-        const bool anym = code[0] >= kPipeNonFinite || code[1] >= kPipeNonFinite || code[2] >= kPipeNonFinite ||
-                          code[3] >= kPipeNonFinite;
-        if (__ballot(anym)) {
+        const uint32_t cmax = max(max(code[0], code[1]), max(code[2], code[3]));
+        if (__ballot(cmax >= kPipeNonFinite)) {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const bool m = code[k] >= kPipeNonFinite;
