@@ -303,6 +303,19 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
                                 int32_t* out_left_key, int32_t* out_right_key, uint8_t* out_flag, int64_t cap,
                                 int64_t* n_out);
 
+/* ---- st_intersection_aggregate over the chip join of two chip tables (area) ---- */
+/* For every (left polygon_key, right polygon_key) pair whose chip sets share a cell id: the area of
+ * the geometry ST_IntersectionAggregate.update / merge (expressions/geometry/
+ * ST_IntersectionAggregate.scala) builds as the union of, per joined chip pair, the cell (both core),
+ * the other chip (one core) or the two chips' intersection -- st_area(st_intersection_aggregate(..)),
+ * the quantity the reference's tests check (ST_IntersectionBehaviors.scala:22-135, 1e-8).  out_status
+ * 1 marks groups the engine does not answer (a cell holding several chip pairs of the group without a
+ * (core, core) pair, a core chip without geometry): evaluate those on the row path.  Sorted by key
+ * pair; MOSAIC_E_CAPACITY with *n_out set when more than cap groups exist. */
+int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
+                                  int32_t* out_left_key, int32_t* out_right_key, double* out_area, uint8_t* out_status,
+                                  int64_t cap, int64_t* n_out);
+
 /* ---- grid_cellkring / grid_cellkloop over a cell column (BNG, H3) ---- */
 /* loop = 0: kRing(cell, k); loop = 1: kLoop(cell, k).  Row i's cells go to out[i * stride ..] and
  * out_count[i] = their number (-1 for null rows, valid[i] == 0).  0 <= k <= 1000.

@@ -769,6 +769,29 @@ class MosaicContext:
             k = int(n_out.value)
             return lk[:k], rk[:k], fl[:k].astype(bool)
 
+    def st_intersection_aggregate_area(self, left, right):
+        """st_area(st_intersection_aggregate(left_index, right_index)) per (left_key, right_key) group of
+        the chip join (ST_IntersectionAggregate.scala; the quantity ST_IntersectionBehaviors.scala:22-135
+        checks): arrays (left_key, right_key, area float64, status uint8) sorted by key pair; status 1
+        marks groups the engine does not answer (several chip pairs of the group in one cell without a
+        (core, core) pair, or a core chip without geometry)."""
+        cap = 1024
+        while True:
+            lk = np.empty(cap, np.int32)
+            rk = np.empty(cap, np.int32)
+            ar = np.empty(cap, np.float64)
+            st = np.empty(cap, np.uint8)
+            n_out = ctypes.c_int64(0)
+            rc = N.lib().mosaic_intersection_aggregate(self.handle, left.handle, right.handle, N.ptr(lk), N.ptr(rk),
+                                                       N.ptr(ar), N.ptr(st), cap, ctypes.byref(n_out))
+            if rc == N.MOSAIC_E_CAPACITY and n_out.value > cap:
+                cap = int(n_out.value)
+                continue
+            N.check(rc)
+            k = int(n_out.value)
+            return lk[:k], rk[:k], ar[:k], st[:k]
+
+
 def tessellate(index_system, polygons, resolution, keep_core_geom=True, densify=1, ctx=None):
     """grid_tessellateexplode over a PolygonSet (mosaic_amd.data.PolygonSet).
 

@@ -30,6 +30,7 @@
 #include "h3_device.h"
 #include "h3_geom.h"
 #include "h3_grid.h"
+#include "isect_area.h"
 #include "pip_coop.h"
 #include "pip_device.h"
 #include "point_decode.h"
@@ -1589,6 +1590,156 @@ __global__ void __launch_bounds__(256) k_isect_agg(IsectArgs a) {
                 if (done) continue;
                 const bool hit = ((ma | mb) & 1u) || wave_intersects(a.sa, ca, a.sb, cb, lane);
                 if (lane == 0 && hit) atomicOr(&a.gflag[gs], 1u);
+            }
+    }
+}
+
+
+// ---- st_intersection_aggregate's area over the chip join of two chip tables (isect_area.h) ----
+// Per (left key, right key) group: the area of the union of the chip-pair pieces the reference's
+// ST_IntersectionAggregate.update folds (expressions/geometry/ST_IntersectionAggregate.scala).  One
+// wave per cell of the left table, as k_isect_agg; pieces of different cells meet in zero area, so
+// a group's area is the sum over its cells.  Within a cell: a (core, core) pair makes the piece the
+// whole cell (every other piece lies inside it); otherwise the cell must hold one pair of the group
+// (the usual case: one chip per polygon and cell), whose piece is the other chip (one core side) or
+// the intersection of the two chips (wave-parallel sum of triangle overlaps, isect_area.h).  A cell
+// with several pairs and no (core, core) pair sets the group's status bit (the caller evaluates such
+// groups on the row path); a (core, core) pair's cell is the cell polygon (indexToGeometry, as the
+// reference's getCellGeom): H3 h3ToGeoBoundary in degrees, BNG the cell square.
+struct IsectAreaArgs {
+    IsectArgs base;
+    double* garea;
+    int grid, jdk;
+};
+
+// indexToGeometry(cell).getArea (the reference's getCellGeom for a (core, core) pair): H3 the
+// h3ToGeoBoundary ring in degrees (h3-java's Math.toDegrees), BNG the cell square
+__device__ double cell_area(int grid, int64_t id, int jdk) {
+    if (grid == MOSAIC_GRID_BNG) {
+        int r;
+        int32_t e, x, y;
+        if (!bng::cell_origin(id, &r, &e, &x, &y)) return NAN;
+        return (double)e * (double)e;
+    }
+    double v[20];
+    const int n = h3geom::h3_to_geo_boundary((uint64_t)id, v);
+    if (n <= 0) return NAN;
+    const double ox = h3geom::to_degrees(v[1], jdk), oy = h3geom::to_degrees(v[0], jdk);
+    double a = 0, px = 0, py = 0;
+    for (int k = 1; k <= n; k++) {
+        const double x = k == n ? 0.0 : h3geom::to_degrees(v[2 * k + 1], jdk) - ox;
+        const double y = k == n ? 0.0 : h3geom::to_degrees(v[2 * k], jdk) - oy;
+        a += px * y - x * py;
+        px = x;
+        py = y;
+    }
+    return 0.5 * fabs(a);
+}
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Area of geometry g (shells counter-clockwise positive, holes negative): JTS getArea
+__device__ double wave_geom_area(const pip::GeomStore& s, uint32_t g, int lane) {
+    const uint32_t ne = isect::edge_count(s, g);
+    if (ne == 0) return 0.0;
+    const pip::Vec2 o = s.verts[s.ring_start[s.part_ring[s.geom_part[g]]]];
+    double sum = 0;
+    for (uint32_t e = (uint32_t)lane; e < ne; e += 64) {
+        uint32_t r, v;
+        bool shell;
+        isect::edge_at(s, g, e, &r, &v, &shell);
+        const double sg = isect::ring_sign(s, r, shell);
+        const pip::Vec2 a = s.verts[v], b = s.verts[v + 1];
+        sum += sg * ((a.x - o.x) * (b.y - o.y) - (b.x - o.x) * (a.y - o.y));
+    }
+    return 0.5 * wave_sum(sum);
+}
+
+// area(A n B): lanes over A's edges, each against every edge of B (isect_area.h)
+__device__ double wave_isect_area(const pip::GeomStore& sa, uint32_t a, const pip::GeomStore& sb, uint32_t b, int lane) {
+    if (sa.geom_part[a + 1] <= sa.geom_part[a] || sb.geom_part[b + 1] <= sb.geom_part[b]) return 0.0;
+    if (!pip::boxes_meet(sa.geom_bbox[a], sb.geom_bbox[b])) return 0.0;
+    const uint32_t na = isect::edge_count(sa, a);
+    if (na == 0) return 0.0;
+    const pip::Vec2 o = sa.verts[sa.ring_start[sa.part_ring[sa.geom_part[a]]]];
+    double sum = 0;
+    for (uint32_t e = (uint32_t)lane; e < na; e += 64) {
+        uint32_t r, v;
+        bool shell;
+        isect::edge_at(sa, a, e, &r, &v, &shell);
+        const double sga = isect::ring_sign(sa, r, shell);
+        const double p0x = sa.verts[v].x - o.x, p0y = sa.verts[v].y - o.y;
+        const double p1x = sa.verts[v + 1].x - o.x, p1y = sa.verts[v + 1].y - o.y;
+        for (uint32_t p = sb.geom_part[b]; p < sb.geom_part[b + 1]; p++)
+            for (uint32_t rb = sb.part_ring[p]; rb < sb.part_ring[p + 1]; rb++) {
+                const double sgb = isect::ring_sign(sb, rb, rb == sb.part_ring[p]);
+                for (uint32_t i = sb.ring_start[rb]; i + 1 < sb.ring_start[rb + 1]; i++)
+                    sum += isect::pair_term(p0x, p0y, p1x, p1y, sga, sb.verts[i].x - o.x, sb.verts[i].y - o.y,
+                                            sb.verts[i + 1].x - o.x, sb.verts[i + 1].y - o.y, sgb);
+            }
+    }
+    return wave_sum(sum);
+}
+
+__global__ void __launch_bounds__(256) k_isect_area(IsectAreaArgs x) {
+    const IsectArgs& a = x.base;
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t slot = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; slot < a.capa; slot += nw) {
+        const HashEntry e = a.ta[slot];
+        if (e.key == kEmptyKey) continue;
+        uint32_t fb = 0, eb = 0;
+        for (uint64_t s = mix64((uint64_t)e.key) & a.maskb;; s = (s + 1) & a.maskb) {
+            const HashEntry f = a.tb[s];
+            if (f.key == e.key) {
+                fb = f.first;
+                eb = f.first + f.count;
+                break;
+            }
+            if (f.key == kEmptyKey) break;
+        }
+        for (uint32_t ca = e.first; ca < e.first + e.count; ca++)
+            for (uint32_t cb = fb; cb < eb; cb++) {
+                const uint32_t ma = a.meta_a[ca], mb = a.meta_b[cb];
+                const unsigned long long key = ((unsigned long long)(ma >> 1) << 32) | (unsigned long long)(mb >> 1);
+                // the group's pairs in this cell: is this the first, how many, a (core, core) one
+                bool first = true;
+                uint32_t n = 0, cc = ~0u;
+                for (uint32_t ca2 = e.first; ca2 < e.first + e.count; ca2++)
+                    for (uint32_t cb2 = fb; cb2 < eb; cb2++) {
+                        const uint32_t ma2 = a.meta_a[ca2], mb2 = a.meta_b[cb2];
+                        if (((unsigned long long)(ma2 >> 1) << 32 | (unsigned long long)(mb2 >> 1)) != key) continue;
+                        n++;
+                        if ((ma2 & mb2 & 1u) && cc == ~0u) cc = ca2;
+                        if (ca2 < ca || (ca2 == ca && cb2 < cb)) first = false;
+                    }
+                if (!first) continue;
+                uint64_t gs = 0;
+                if (lane == 0) gs = group_slot(a, key);
+                gs = __shfl(gs, 0, 64);
+                if (gs == ~0ULL) continue;
+                double area = 0;
+                uint32_t flag = 0;
+                if (cc != ~0u) {
+                    area = cell_area(x.grid, e.key, x.jdk);
+                } else if (n > 1) {
+                    flag = 1;
+                } else if (ma & 1u) {
+                    area = wave_geom_area(a.sb, cb, lane);
+                } else if (mb & 1u) {
+                    area = wave_geom_area(a.sa, ca, lane);
+                } else {
+                    area = wave_isect_area(a.sa, ca, a.sb, cb, lane);
+                }
+                if (area != area) flag = 1;
+                if (lane == 0) {
+                    if (flag) atomicOr(&a.gflag[gs], flag);
+                    else atomicAdd(&x.garea[gs], area);
+                }
             }
     }
 }
@@ -4452,6 +4603,86 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
         out_flag[i] = groups[i].second;
     }
     return done(MOSAIC_OK);
+}
+
+int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
+                                  int32_t* out_left_key, int32_t* out_right_key, double* out_area, uint8_t* out_status,
+                                  int64_t cap, int64_t* n_out) {
+    ENTER(ctx);
+    if (!c || !left || !right || !n_out || cap < 0 ||
+        (cap > 0 && (!out_left_key || !out_right_key || !out_area || !out_status)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    if (left->grid != right->grid || left->res != right->res)
+        return fail(MOSAIC_E_ARG, "st_intersection_aggregate: both chip tables must use the same grid and resolution");
+    *n_out = 0;
+    HIP_TRY(hipSetDevice(c->device));
+    if (left->n_chips == 0 || right->n_chips == 0) return MOSAIC_OK;
+    IsectArgs a;
+    a.ta = (const HashEntry*)left->table.p;
+    a.capa = left->capacity;
+    a.meta_a = (const uint32_t*)left->meta.p;
+    a.sa = left->store.view();
+    a.tb = (const HashEntry*)right->table.p;
+    a.maskb = right->capacity - 1;
+    a.meta_b = (const uint32_t*)right->meta.p;
+    a.sb = right->store.view();
+    DevBuf cnt, gkey, gflag, garea, ovf;
+    DevBufGuard guard{{&cnt, &gkey, &gflag, &garea, &ovf}};
+    int rc;
+    if ((rc = cnt.reserve(8)) || (rc = ovf.reserve(4))) return rc;
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
+    HIP_TRY(hipMemsetAsync(ovf.p, 0, 4, c->stream));
+    a.pass = 0;
+    a.pair_count = (unsigned long long*)cnt.p;
+    a.gkey = nullptr;
+    a.gflag = nullptr;
+    a.gmask = 0;
+    a.overflow = (int*)ovf.p;
+    const int64_t waves = (int64_t)left->capacity;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((waves * 64 + 255) / 256, (int64_t)c->n_cu * 16));
+    hipLaunchKernelGGL(k_isect_agg, dim3(grid), dim3(256), 0, c->stream, a);  // pass 0: chip pairs
+    HIP_TRY(hipGetLastError());
+    unsigned long long pairs = 0;
+    HIP_TRY(hipMemcpyAsync(&pairs, cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (pairs == 0) return MOSAIC_OK;
+    uint64_t gcap = 1024;
+    while (gcap < 2 * pairs) gcap <<= 1;
+    if ((rc = gkey.reserve(gcap * 8)) || (rc = gflag.reserve(gcap * 4)) || (rc = garea.reserve(gcap * 8))) return rc;
+    HIP_TRY(hipMemsetAsync(gkey.p, 0xff, gcap * 8, c->stream));
+    HIP_TRY(hipMemsetAsync(gflag.p, 0, gcap * 4, c->stream));
+    HIP_TRY(hipMemsetAsync(garea.p, 0, gcap * 8, c->stream));
+    a.pass = 1;
+    a.gkey = (unsigned long long*)gkey.p;
+    a.gflag = (uint32_t*)gflag.p;
+    a.gmask = gcap - 1;
+    IsectAreaArgs x{a, (double*)garea.p, left->grid, c->jdk};
+    hipLaunchKernelGGL(k_isect_area, dim3(grid), dim3(256), 0, c->stream, x);
+    HIP_TRY(hipGetLastError());
+    std::vector<unsigned long long> hk(gcap);
+    std::vector<uint32_t> hf(gcap);
+    std::vector<double> ha(gcap);
+    int hov = 0;
+    HIP_TRY(hipMemcpyAsync(hk.data(), gkey.p, gcap * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(hf.data(), gflag.p, gcap * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ha.data(), garea.p, gcap * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&hov, ovf.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (hov) return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: group table overflow");
+    std::vector<std::pair<unsigned long long, uint64_t>> groups;
+    for (uint64_t s = 0; s < gcap; s++)
+        if (hk[s] != kEmptyGroup) groups.push_back({hk[s], s});
+    std::sort(groups.begin(), groups.end());
+    *n_out = (int64_t)groups.size();
+    if ((int64_t)groups.size() > cap)
+        return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: " + std::to_string(groups.size()) + " groups");
+    for (size_t i = 0; i < groups.size(); i++) {
+        out_left_key[i] = (int32_t)(groups[i].first >> 32);
+        out_right_key[i] = (int32_t)(groups[i].first & 0xffffffffULL);
+        out_area[i] = ha[groups[i].second];
+        out_status[i] = (uint8_t)(hf[groups[i].second] ? 1 : 0);
+    }
+    return MOSAIC_OK;
 }
 
 

@@ -101,3 +101,87 @@ def segments_intersect(p1, p2, q1, q2):
 
     return ((o1 == 0 and on(p1, p2, q1)) or (o2 == 0 and on(p1, p2, q2)) or (o3 == 0 and on(q1, q2, p1))
             or (o4 == 0 and on(q1, q2, p2)))
+
+
+# ---- area of A n B by vertical slabs (exact rationals): the checker of the engine's
+# st_intersection_aggregate areas (a different algorithm from the engine's boundary integral).
+# Between consecutive x-coordinates of all vertices and all edge crossings, the edges crossing a
+# slab keep their vertical order, so the length of {y : (x, y) in A n B} is linear in x and the
+# midpoint rule is exact.  Rings: lists of (x, y), closed (last == first); parts: lists of rings
+# (shell first); inside = odd crossing count per part (valid polygons), any part.
+def _edges(parts):
+    out = []
+    for rings in parts:
+        for r in rings:
+            pts = [(Fraction(x), Fraction(y)) for x, y in r]
+            out.extend((pts[i], pts[i + 1]) for i in range(len(pts) - 1) if pts[i] != pts[i + 1])
+    return out
+
+
+def _crossings_x(ea, eb):
+    xs = set()
+    for (p, q) in ea:
+        for (r, s) in eb:
+            d = (q[0] - p[0]) * (s[1] - r[1]) - (q[1] - p[1]) * (s[0] - r[0])
+            if d == 0:
+                continue
+            t = ((r[0] - p[0]) * (s[1] - r[1]) - (r[1] - p[1]) * (s[0] - r[0])) / d
+            u = ((r[0] - p[0]) * (q[1] - p[1]) - (r[1] - p[1]) * (q[0] - p[0])) / d
+            if 0 <= t <= 1 and 0 <= u <= 1:
+                xs.add(p[0] + t * (q[0] - p[0]))
+    return xs
+
+
+def _section(edges_by_part, x):
+    """per part: sorted y where the vertical line x crosses its edges (x strictly inside a slab)"""
+    out = []
+    for edges in edges_by_part:
+        ys = []
+        for (p, q) in edges:
+            if (p[0] < x < q[0]) or (q[0] < x < p[0]):
+                ys.append(p[1] + (x - p[0]) * (q[1] - p[1]) / (q[0] - p[0]))
+        out.append(sorted(ys))
+    return out
+
+
+def _inside_len(sec_a, sec_b):
+    """length of the y-set inside some part of A and some part of B"""
+    def intervals(sec):
+        iv = []
+        for ys in sec:
+            iv.extend((ys[i], ys[i + 1]) for i in range(0, len(ys) - 1, 2))
+        return iv
+    ia, ib = intervals(sec_a), intervals(sec_b)
+    total = Fraction(0)
+    for (a0, a1) in ia:
+        for (b0, b1) in ib:
+            lo, hi = max(a0, b0), min(a1, b1)
+            if hi > lo:
+                total += hi - lo
+    return total
+
+
+def intersection_area(parts_a, parts_b):
+    ea = [_edges([p]) for p in parts_a]
+    eb = [_edges([p]) for p in parts_b]
+    fa = [e for es in ea for e in es]
+    fb = [e for es in eb for e in es]
+    xs = {p[0] for e in fa + fb for p in e} | _crossings_x(fa, fb)
+    xs = sorted(xs)
+    area = Fraction(0)
+    for i in range(len(xs) - 1):
+        x0, x1 = xs[i], xs[i + 1]
+        xm = (x0 + x1) / 2
+        area += (x1 - x0) * _inside_len(_section(ea, xm), _section(eb, xm))
+    return area
+
+
+def polygon_area(parts):
+    """JTS getArea: per part |shell| - sum |holes| (shoelace, exact)"""
+    total = Fraction(0)
+    for rings in parts:
+        for k, r in enumerate(rings):
+            pts = [(Fraction(x), Fraction(y)) for x, y in r]
+            a = sum(pts[i][0] * pts[i + 1][1] - pts[i + 1][0] * pts[i][1] for i in range(len(pts) - 1)) / 2
+            total += abs(a) if k == 0 else -abs(a)
+    return total
