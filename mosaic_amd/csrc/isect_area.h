@@ -12,8 +12,9 @@
 // pairs of sign_a sign_b |T_a n T_b| -- two triangles, one convex clip each (Sutherland-Hodgman,
 // at most 9 vertices).  Zero-width bridges a clipped ring can carry (an edge and its reverse)
 // cancel term by term, coincident sides of two chips need no special case, and the pairs spread
-// over a wave's lanes without sorting or point location.  Coordinates are relative to O (A's first
-// vertex) to keep the terms small.
+// over a wave's lanes without sorting or point location.  O is the lower-left corner of the two
+// bounding boxes: coordinates stay small, and every triangle is a sector within 90 degrees, so
+// pairs of disjoint sectors are rejected with two cross products.
 #pragma once
 #include <math.h>
 #include <stdint.h>
@@ -113,6 +114,9 @@ MOSAIC_HD double pair_term(double p0x, double p0y, double p1x, double p1y, doubl
     // both triangles counter-clockwise; the orientations went into the sign
     const double ax0 = ca > 0 ? p0x : p1x, ay0 = ca > 0 ? p0y : p1y, ax1 = ca > 0 ? p1x : p0x, ay1 = ca > 0 ? p1y : p0y;
     const double bx0 = cb > 0 ? q0x : q1x, by0 = cb > 0 ? q0y : q1y, bx1 = cb > 0 ? q1x : q0x, by1 = cb > 0 ? q1y : q0y;
+    // with the origin at the lower-left corner of both bounding boxes every vertex lies within 90
+    // degrees of +x, so two triangles overlap only where their angular sectors do
+    if (ax0 * by1 - ay0 * bx1 <= 0.0 || bx0 * ay1 - by0 * ax1 <= 0.0) return 0.0;
     return s * tri_overlap(ax0, ay0, ax1, ay1, bx0, by0, bx1, by1);
 }
 

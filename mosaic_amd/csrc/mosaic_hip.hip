@@ -1665,7 +1665,7 @@ __device__ double wave_isect_area(const pip::GeomStore& sa, uint32_t a, const pi
     if (!pip::boxes_meet(sa.geom_bbox[a], sb.geom_bbox[b])) return 0.0;
     const uint32_t na = isect::edge_count(sa, a);
     if (na == 0) return 0.0;
-    const pip::Vec2 o = sa.verts[sa.ring_start[sa.part_ring[sa.geom_part[a]]]];
+    const pip::Vec2 o{fmin(sa.geom_bbox[a].minx, sb.geom_bbox[b].minx), fmin(sa.geom_bbox[a].miny, sb.geom_bbox[b].miny)};
     double sum = 0;
     for (uint32_t e = (uint32_t)lane; e < na; e += 64) {
         uint32_t r, v;

@@ -47,7 +47,7 @@ extern "C" double isect_area_host(const double* xa, const int64_t* ra, int nra, 
     Store A(xa, ra, nra, pa, npa), B(xb, rb, nrb, pb, npb);
     const pip::GeomStore sa = A.view(), sb = B.view();
     const uint32_t na = isect::edge_count(sa, 0);
-    const pip::Vec2 o = sa.verts[0];
+    const pip::Vec2 o{fmin(sa.geom_bbox[0].minx, sb.geom_bbox[0].minx), fmin(sa.geom_bbox[0].miny, sb.geom_bbox[0].miny)};
     double sum = 0;
     for (uint32_t e = 0; e < na; e++) {
         uint32_t r, v;

@@ -1,6 +1,7 @@
-"""Timing of st_intersects_aggregate (mosaic_intersects_aggregate) on the GPU box: the 263 NYC
-zones chipped at H3 res 9 (and the 35-zone set at res 10) joined with a translated copy.  Prints one
-JSON line per case (groups, true groups, chip pairs tested, ms for the whole call incl. D2H)."""
+"""Timing of st_intersects_aggregate (mosaic_intersects_aggregate) and of st_intersection_aggregate's
+area (mosaic_intersection_aggregate) on the GPU box: the 263 NYC zones chipped at H3 res 9 and 10
+joined with a translated copy.  Prints one JSON line per case (groups, true groups, refused groups,
+ms for each whole call incl. D2H)."""
 import json
 import os
 import sys
@@ -30,8 +31,16 @@ def main():
             t0 = time.perf_counter()
             lk, rk, fl = ctx.st_intersects_aggregate(tl, tr)
             ts.append((time.perf_counter() - t0) * 1e3)
+        ctx.st_intersection_aggregate_area(tl, tr)
+        ta = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            _, _, area, st = ctx.st_intersection_aggregate_area(tl, tr)
+            ta.append((time.perf_counter() - t0) * 1e3)
         print(json.dumps({"case": f"{name} res {res} shift {shift}", "chips": [len(l["index_id"]), len(r["index_id"])],
-                          "groups": int(len(fl)), "true": int(fl.sum()), "ms_median": float(np.median(ts))}))
+                          "groups": int(len(fl)), "true": int(fl.sum()), "ms_median": float(np.median(ts)),
+                          "area_ms_median": float(np.median(ta)), "area_refused_groups": int(st.sum()),
+                          "area_total": float(area[st == 0].sum())}), flush=True)
         tl.close()
         tr.close()
 
