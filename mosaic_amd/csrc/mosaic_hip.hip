@@ -563,6 +563,22 @@ static const uint32_t kNoLoad = 0x7ffffff0u;  // out-of-range buffer offset (eve
 typedef double v2d __attribute__((ext_vector_type(2)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
+// A stream kernel's LDS fill: n words from global memory, 8 coalesced loads per thread in flight
+// before the stores (a plain strided loop waits for each load in turn: ~40 serial round trips for
+// a full quad level)
+__device__ inline void lds_fill(uint32_t* dst, const uint32_t* __restrict__ src, int n) {
+    const int nt = (int)blockDim.x;
+    int k = (int)threadIdx.x;
+    for (; k + 7 * nt < n; k += 8 * nt) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = src[k + j * nt];
+#pragma unroll
+        for (int j = 0; j < 8; j++) dst[k + j * nt] = v[j];
+    }
+    for (; k < n; k += nt) dst[k] = src[k];
+}
+
 __device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t bytes) {
     // wave-uniform inputs made provably uniform (no waterfall loops around the loads)
     const uint64_t u = (uint64_t)p;
@@ -598,10 +614,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint16_t* quad = (const uint16_t*)quadw;
     uint32_t* qmask = quadw + s.n_quad_words;
     const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
-    for (int k = threadIdx.x; k < s.n_quad_words; k += blockDim.x) quadw[k] = s.quad[k];
-    for (int k = threadIdx.x; k < s.n_qrec_words; k += blockDim.x) qmask[k] = s.qrec[k];
+    lds_fill(quadw, s.quad, s.n_quad_words);
+    lds_fill(qmask, s.qrec, s.n_qrec_words);
     if (s.tb_lds)
-        for (int k = threadIdx.x; k < s.n_tiles; k += blockDim.x) tb[k] = s.tile_base[k];
+        lds_fill(tb, s.tile_base, s.n_tiles);
     for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
@@ -771,9 +787,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint16_t* quad = (const uint16_t*)quadw;
     uint32_t* qmask = quadw + s.n_quad_words;
     const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
-    for (int k = threadIdx.x; k < s.n_quad_words; k += blockDim.x) quadw[k] = s.quad[k];
-    for (int k = threadIdx.x; k < s.n_qrec_words; k += blockDim.x) qmask[k] = s.qrec[k];
-    for (int k = threadIdx.x; k < s.n_tiles; k += blockDim.x) tb[k] = s.tile_base[k];
+    lds_fill(quadw, s.quad, s.n_quad_words);
+    lds_fill(qmask, s.qrec, s.n_qrec_words);
+    lds_fill(tb, s.tile_base, s.n_tiles);
     for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
@@ -2038,7 +2054,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint8_t* lcell = (const uint8_t*)lcw;
     const bool use_lc = s.lcell_words > 0;  // (uniform)
     for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
-    for (int k = threadIdx.x; k < s.lcell_words; k += blockDim.x) lcw[k] = s.lcell[k];
+    lds_fill(lcw, s.lcell, s.lcell_words);
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rcell = stream_rsrc(s.cells, s.cells_bytes);
     const __amdgpu_buffer_rsrc_t rleaf = stream_rsrc(s.leaf, s.leaf_bytes);
@@ -2229,8 +2245,11 @@ __global__ void __launch_bounds__(256) k_join_mixed_bng(JoinArgs a) {
 // window entries, hash entries -- R independent chains in flight per lane instead of one), then the
 // raster chip loop runs once per row slot (wave-cooperative, so wave-uniform).  Rows the fast path
 // cannot certify, kFull tiles and window misses take tiled_cell (the generic path).
+#ifndef MOSAIC_MIXED_WPE
+#define MOSAIC_MIXED_WPE 4
+#endif
 template <bool LDS_COUNTS, bool PAIRS, int R>
-__global__ void __launch_bounds__(256) k_join_mixed(JoinArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOSAIC_MIXED_WPE))) k_join_mixed(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     __shared__ SlabItem items[4][16];
     counts_init<LDS_COUNTS>(a, lds);
@@ -4358,7 +4377,9 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
         HIP_TRY(hipGetLastError());
         if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
         if (h3g) {
-            int ge = grid_size(c, (int64_t)qcap);
+            // the margin queue is nearly always a handful of rows: a grid of 2 workgroups per CU keeps
+            // the launch short (a 2048-workgroup grid cost ~40 us of dispatch for ~1 row)
+            int ge = std::min(grid_size(c, (int64_t)qcap), std::max(1, c->n_cu * 2));
             if (pairs)
                 hipLaunchKernelGGL((k_join_h3_exact<true>), dim3(ge), dim3(c->block), 0, c->stream, a, 0);
             else

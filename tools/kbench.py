@@ -99,7 +99,8 @@ def main():
                             "call_ms": round(step, 4), "points_per_s": n / (step * 1e-3),
                             "same_counts": bool(np.array_equal(got, ref)), "pairs": int(got.sum()),
                             "tess_s": round(tess_s, 2), "build_s": round(build_s, 2),
-                            "raster_bytes": tl.get("raster_bytes"), "quad_entries": tl.get("quad_entries")}
+                            "raster_bytes": tl.get("raster_bytes"), "quad_entries": tl.get("quad_entries"),
+                            "stats": stats}
                     if tiles and praster and len(kt) >= 2:
                         line["stream_ms"] = round(float(np.median(kt[0::2])), 4)
                         line["mixed_ms"] = round(float(np.median(kt[1::2])), 4)
