@@ -2607,7 +2607,7 @@ struct Options {
     int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
     int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
     int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
-    int mixed_blocks_per_cu = 8;  // k_join_mixed grid
+    int mixed_blocks_per_cu = 4;  // k_join_mixed grid: the workgroups resident at once (~120 VGPRs: 4 per CU)
     int mixed_rows = 2;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
     // copy on copy_stream overlapping the current chunk's join (0: stage the whole batch first)
