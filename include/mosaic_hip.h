@@ -102,8 +102,21 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * whole batch; default 2^25), "mixed_rows" (1/2/4, default 2), "mixed_blocks_per_cu", "stream_pipe"
  * (0/1: the software-pipelined stream kernel where it applies; default 1), "bng_lds" (0/1: BNG tables
  * built afterwards carry an LDS cell level for the BNG stream kernel; default 1), "bng_cell" (sub-cells
- * per BNG border cell side in those tables, a power of two <= 64; default 32). */
+ * per BNG border cell side in those tables, a power of two <= 64; default 32), "scratch_limit" (see
+ * the per-thread state below). */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
+/* Per-thread state.  Each calling thread gets its own execution state on a context (HIP stream,
+ * copy stream, timing events, scratch queues and staging sized by its largest call).  It is freed
+ * by mosaic_thread_release (the calling thread's state), by mosaic_destroy (all), or when a thread
+ * other than the process's main thread exits (a thread_local guard), so an executor whose worker
+ * pool retires and creates threads does not accumulate streams or scratch.  States are keyed by a
+ * per-thread serial number, never by pthread ids (which the runtime reuses).  Option
+ * "scratch_limit" (bytes, 0 = keep; default 0) frees a thread's scratch when a call returns holding
+ * more than that.  mosaic_thread_count reports the live states and the scratch they hold.
+ * (Replaces no reference interface: the JVM side's H3Core / index-system singletons hold no device
+ * state, H3IndexSystem.scala:22-27; this is the multiplexing SURVEY.md §8(b) asks of the ABI.) */
+int mosaic_thread_release(mosaic_ctx* ctx);
+int mosaic_thread_count(mosaic_ctx* ctx, int64_t* n_threads, int64_t* scratch_bytes);
 /* The calling thread's hipStream_t (created by the context unless set by this thread). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
 int mosaic_set_stream(mosaic_ctx* ctx, void* stream);
@@ -278,7 +291,8 @@ int mosaic_chip_set_destroy(mosaic_chip_set* cs);
  * IndexSystem.getBorderChips / getCoreChips (core/index/IndexSystem.scala:152-186, via
  * Mosaic.mosaicFill core/Mosaic.scala:60-87).  BNG: k_bng_tess_classify on the cell squares; H3:
  * k_tess_classify_poly on the (densify-subdivided) hexagons in the icosahedron face plane.  Border
- * cells are clipped on the host.  Errors as mosaic_tessellate. */
+ * cells are clipped on the GPU as well (k_tess_clip); candidate enumeration and the chip WKB
+ * assembly are host code.  Errors as mosaic_tessellate. */
 int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
                           const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
                           int keep_core_geom, int densify, mosaic_chip_set** out);
@@ -311,7 +325,9 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
  * the quantity the reference's tests check (ST_IntersectionBehaviors.scala:22-135, 1e-8).  out_status
  * 1 marks groups the engine does not answer (a cell holding several chip pairs of the group without a
  * (core, core) pair, a core chip without geometry): evaluate those on the row path.  Sorted by key
- * pair; MOSAIC_E_CAPACITY with *n_out set when more than cap groups exist. */
+ * pair; MOSAIC_E_CAPACITY with *n_out set when more than cap groups exist.  A group's area is summed
+ * over its cells with float64 atomics in completion order, so repeated calls can differ in the last
+ * bits (always within the reference's 1e-8); the set of groups and their status are deterministic. */
 int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
                                   int32_t* out_left_key, int32_t* out_right_key, double* out_area, uint8_t* out_status,
                                   int64_t cap, int64_t* n_out);
@@ -388,8 +404,9 @@ int mosaic_ctx_exec(mosaic_ctx* ctx, int* device, void** stream, int* jdk, int* 
 /* out[93 i .. 93 i + 92] = the WKB JTS writes for BNGIndexSystem.indexToGeometry(ids[i])
  * (core/index/BNGIndexSystem.scala indexToGeometry; functions/MosaicContext.scala
  * grid_boundaryaswkb -> expressions/index/IndexGeometry.scala:65-75): big-endian 2D Polygon of the
- * cell square, 5 points.  Null rows (valid[i] == 0) are left zero.  H3 is not implemented
- * (MOSAIC_E_ARG). */
+ * cell square, 5 points.  Null rows (valid[i] == 0) are left zero.  H3 cells are served by
+ * mosaic_h3_cell_geometry mode 2 (variable-length rings); with grid H3 this entry returns
+ * MOSAIC_E_ARG. */
 int mosaic_cell_boundary_wkb(mosaic_ctx* ctx, int grid, const int64_t* ids, const uint8_t* valid, int64_t n,
                              uint8_t* out);
 

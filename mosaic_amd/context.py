@@ -190,6 +190,15 @@ def st_point(x, y):
     return CoordsColumn(np.ones(n, np.int32), np.zeros(n, np.int32), ar, ar, 2 * ar, vals)
 
 
+def _is_arrow_utf8(v):
+    """An Arrow utf8 column given explicitly as (offsets int32 / int64 array, chars bytes / uint8 array)."""
+    if not (isinstance(v, tuple) and len(v) == 2):
+        return False
+    offs, chars = v
+    return (isinstance(offs, np.ndarray) and offs.dtype in (np.int32, np.int64) and
+            (isinstance(chars, (bytes, bytearray)) or (isinstance(chars, np.ndarray) and chars.dtype == np.uint8)))
+
+
 def _points_xy(points):
     """Accepts (x, y) arrays or an (n, 2) array (host or device)."""
     if isinstance(points, tuple) and len(points) == 2:
@@ -208,9 +217,15 @@ class ChipTable:
     def __init__(self, ctx, is_core, index_id, wkb_list, polygon_key, n_polygons=None):
         self.ctx = ctx
         is_core = np.ascontiguousarray(is_core, dtype=np.uint8)
-        if isinstance(index_id, tuple) or (len(index_id) and isinstance(index_id[0], str)):
+        strings = not _is_arrow_utf8(index_id) and len(index_id) and isinstance(index_id[0], str)
+        if ctx.index_system.cell_id_type == "string" and (_is_arrow_utf8(index_id) or strings):
             # StringType ids (the BNG default, BNGIndexSystem.scala:28): parsed on the GPU
             index_id = ctx.bng_parse_column(index_id)
+        elif strings:
+            # string ids of a LongType index system (H3 hex strings, H3IndexSystem.parse)
+            index_id = [ctx.index_system.parse(v) for v in index_id]
+        elif _is_arrow_utf8(index_id):
+            raise ValueError(f"an Arrow utf8 id column needs a StringType index system, not {ctx.index_system.name}")
         index_id = np.ascontiguousarray(index_id, dtype=np.int64)
         polygon_key = np.ascontiguousarray(polygon_key, dtype=np.int32)
         if isinstance(wkb_list, tuple) and len(wkb_list) == 2:
@@ -350,6 +365,17 @@ class MosaicContext:
         N.check(N.lib().mosaic_kernel_times(self.handle, N.ptr(out), cap, ctypes.byref(n)))
         return out[:min(n.value, cap)]
 
+    def thread_release(self):
+        """Free the calling thread's execution state on this context (its stream, scratch, events);
+        a later call from the thread creates a fresh one (mosaic_thread_release)."""
+        N.check(N.lib().mosaic_thread_release(self.handle))
+
+    def thread_states(self):
+        """(live per-thread states, scratch bytes they hold) (mosaic_thread_count)."""
+        n, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(N.lib().mosaic_thread_count(self.handle, ctypes.byref(n), ctypes.byref(b)))
+        return n.value, b.value
+
     def last_stats(self):
         out = np.zeros(3, np.int64)
         N.check(N.lib().mosaic_last_stats(self.handle, N.ptr(out)))
@@ -408,7 +434,7 @@ class MosaicContext:
         """BNG string ids -> long ids, parsed on the GPU (BNGIndexSystem.parse,
         BNGIndexSystem.scala:391-413).  ``strings``: a sequence of str (None = null) or an Arrow utf8
         tuple (offsets int32 / int64, chars)."""
-        if isinstance(strings, tuple) and len(strings) == 2:
+        if _is_arrow_utf8(strings):
             offs, chars = strings
             offs = np.ascontiguousarray(offs)
             chars = np.frombuffer(chars, np.uint8) if isinstance(chars, (bytes, bytearray)) else np.ascontiguousarray(chars, np.uint8)

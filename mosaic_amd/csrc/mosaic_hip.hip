@@ -14,7 +14,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <memory>
 #include <mutex>
@@ -31,6 +35,7 @@
 #include "h3_geom.h"
 #include "h3_grid.h"
 #include "isect_area.h"
+#include "join_common.h"
 #include "pip_coop.h"
 #include "pip_device.h"
 #include "point_decode.h"
@@ -55,63 +60,6 @@ static int fail(int code, const std::string& msg) {
         hipError_t _e = (expr);                                                                         \
         if (_e != hipSuccess) return fail(MOSAIC_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
-
-// ------------------------------------------------------------------------------------------------
-// device-side data structures
-static const int64_t kEmptyKey = INT64_MIN;
-
-struct HashEntry {  // 16 bytes: one dwordx4 load per probe
-    int64_t key;
-    uint32_t first;
-    uint32_t count;
-};
-
-__host__ __device__ inline uint64_t mix64(uint64_t h) {
-    h ^= h >> 33;
-    h *= 0xff51afd7ed558ccdULL;
-    h ^= h >> 33;
-    h *= 0xc4ceb9fe1a85ec53ULL;
-    h ^= h >> 33;
-    return h;
-}
-
-struct JoinArgs {
-    const double* x;
-    const double* y;
-    const uint8_t* valid;
-    int64_t n;
-    int res, jdk;
-    const HashEntry* table;
-    uint64_t mask;
-    const uint32_t* chip_meta;  // (polygon_key << 1) | is_core, in table order
-    const raster::ChipHdr* hdr;     // per chip: envelope + ray-parity raster (raster.h)
-    const raster::CellRec* cells;   // raster cells
-    const pip::Edge* rast_edges;    // raster cell segment lists
-    uint32_t lane_edges;            // cell lists up to this long are evaluated by the owning lane
-    pip::GeomStore store;       // geometry g == chip g (table order)
-    tiles::Grid tgrid;                // tile directory (tiles.h); tile_idx == nullptr: none
-    const uint32_t* tile_idx;
-    const tiles::TileRec* tile_rec;
-    const uint32_t* tile_ent;
-    tiles::PointRaster praster;       // point raster (tiles.h); praster.sub == nullptr: none
-    const uint32_t* bng_cells;        // BNG dense cell table (k_join_stream_bng); nullptr: none
-    const uint16_t* bng_leaf;         // its leaf blocks (C x C codes per border cell)
-    int32_t bng_e0, bng_n0, bng_ne, bng_nn, bng_div, bng_C;
-    int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
-    uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
-    unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)
-    unsigned long long* counts;  // [n_polygons]
-    int n_polygons;
-    unsigned long long* amb_queue;  // rows for the exact H3 pass
-    unsigned long long* amb_count;
-    unsigned long long amb_cap;
-    long long* pair_row;
-    int* pair_key;
-    unsigned long long* pair_count;
-    long long pair_cap;
-    unsigned long long* tests;  // (point, border chip) contains evaluations
-    unsigned int* flags;        // bit 0: NaN seen (BNG)
-};
 
 template <bool LDS_COUNTS, bool PAIRS>
 __device__ inline void join_point(const JoinArgs& a, int64_t row, double x, double y, int64_t cell, unsigned int* lds,
@@ -166,22 +114,6 @@ __device__ inline void counts_flush(const JoinArgs& a, unsigned int* lds, unsign
         __syncthreads();
         for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
             if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
-    }
-}
-
-// One (row, key) pair: the count, and the pair itself for the pairs output.
-template <bool LDS_COUNTS, bool PAIRS>
-__device__ inline void emit_hit(const JoinArgs& a, int64_t row, uint32_t key, unsigned int* lds) {
-    if (LDS_COUNTS)
-        atomicAdd(&lds[key], 1u);
-    else
-        atomicAdd(&a.counts[key], 1ULL);
-    if (PAIRS) {
-        unsigned long long idx = atomicAdd(a.pair_count, 1ULL);
-        if ((long long)idx < a.pair_cap) {
-            a.pair_row[idx] = row;
-            a.pair_key[idx] = (int)key;
-        }
     }
 }
 
@@ -482,474 +414,6 @@ __global__ void __launch_bounds__(256) k_join_tiled(JoinArgs a) {
         tiled_process<LDS_COUNTS, PAIRS>(a, q, lane, lane < qn, tests, lds, items[wv]);
     }
     counts_flush<LDS_COUNTS>(a, lds, tests);
-}
-
-// Per-wave LDS stage of rows for the mixed-cell queue: rows are appended with a ballot, and the
-// stage goes to the global queue in one atomic once >= 64 rows wait (a per-iteration atomic on one
-// counter serialises the grid).  Wave-uniform calls.
-__device__ inline void stage_push(uint32_t* wq, uint32_t& wn, bool mixed, uint32_t rowoff, unsigned long long lt_mask) {
-    const unsigned long long mm = __ballot(mixed);
-    if (mixed) wq[wn + __popcll(mm & lt_mask)] = rowoff;
-    wn += (uint32_t)__popcll(mm);
-}
-__device__ inline void stage_flush(const JoinArgs& a, uint32_t* wq, uint32_t& wn, int lane, uint32_t min_rows) {
-    if (wn < min_rows || wn == 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(a.mixq_count, (unsigned long long)wn);
-    base = __shfl(base, 0, 64);
-    for (uint32_t k = (uint32_t)lane; k < wn; k += 64) a.mixq[base + k] = wq[k];
-    __builtin_amdgcn_wave_barrier();
-    wn = 0;
-}
-
-// ---- k_join_stream (default with a point raster, tiles.h): the point raster's answer for every
-// point of the batch, branch-free.  Per point: fine-cell coordinates (two f64 ops per axis, clamped
-// to the grid), the LDS quad level, and -- only for points whose quad is not uniform -- one 2-byte
-// gather of the sub-block entry from the compact copies; points whose sub-block is a leaf block or
-// a line record gather that (2 or 16 bytes).  Gathers go through buffer descriptors: a lane that
-// needs no gather passes an out-of-range offset, which the hardware drops without a memory access,
-// so no lane branches.  Answers: 0 (no pair), k + 1 (one pair with key k: an LDS atomic), kMixed
-// (the row goes to the mixed queue for k_join_mixed).  tiles::raster_code is the same computation
-// for one point on the host.
-//
-// Rows: each wave handles 256 consecutive rows per iteration; lane l holds rows 2l, 2l + 1,
-// 128 + 2l, 129 + 2l, so each 16-byte coordinate load instruction reads 1 KiB contiguous.  The
-// next iteration's coordinates are loaded after this iteration's gathers are issued (vector-memory
-// returns retire in order: waiting for the gathers does not wait for them).
-struct StreamArgs {
-    double x0, y0, sxC, syC;  // fine-cell coordinates g = (x - x0) sxC, (y - y0) syC (C per sub-block)
-    double gxmax, gymax;      // clamp: NX C - 1, NY C - 1
-    int32_t cs, qsh, tsh, qs;  // log2 C; cs + quad shift; cs + tile shift (sub-blocks per tile); quad shift
-    int32_t qnx, tnx;         // quad-level entries per row, tiles per row
-    int32_t n_quad_words, n_tiles;  // LDS copies: quad level (uint32 words), tile_base (if tb_lds)
-    int32_t tb_lds;           // 1: tile_base in LDS; 0: gathered through its descriptor
-    int32_t stage_words;      // per-wave mixed-row stage
-    const uint32_t* quad;     // quad level, uint16 entries packed in uint32 words
-    const uint32_t* tile_base;
-    const uint16_t* csub;     // compact sub-block copies (PointRaster::sub + nx * ny)
-    const uint16_t* blocks;   // line records and leaf blocks
-    uint32_t csub_bytes, blocks_bytes, tile_base_bytes;
-    // quad records (tiles::PointRaster::qrec_*), copied to LDS behind the quad level: 2 n_qrec mask
-    // words, then the n_qrec uint16 codes; n_qrec_words >= 2 (index 0 is always readable)
-    const uint32_t* qrec;
-    int32_t n_qrec, n_qrec_words, qrl;
-};
-// per-wave mixed-row stage of the stream kernels (words): rows are appended one slot (<= 64 rows)
-// at a time and flushed at >= 64
-static const int kStageWords = 128;
-static const uint32_t kNoLoad = 0x7ffffff0u;  // out-of-range buffer offset (every table is < 2 GiB)
-// cache-policy bits (aux) of the stream kernels' gathers: sub-block entries, line records, leaf
-// codes, BNG sub-cell entries (build-time A/B knobs; 2 = nt)
-#ifndef MOSAIC_AUX_SUB
-#define MOSAIC_AUX_SUB 0
-#endif
-#ifndef MOSAIC_AUX_LINE
-#define MOSAIC_AUX_LINE 0
-#endif
-#ifndef MOSAIC_AUX_LEAF
-#define MOSAIC_AUX_LEAF 0
-#endif
-#ifndef MOSAIC_AUX_BNG
-#define MOSAIC_AUX_BNG 0
-#endif
-// k_join_stream_pipe: groups of coordinates in flight ahead of the one being looked up (1 or 2)
-#ifndef MOSAIC_PIPE_DEPTH
-#define MOSAIC_PIPE_DEPTH 1
-#endif
-
-typedef double v2d __attribute__((ext_vector_type(2)));
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-
-// A stream kernel's LDS fill: n words from global memory, 8 coalesced loads per thread in flight
-// before the stores (a plain strided loop waits for each load in turn: ~40 serial round trips for
-// a full quad level)
-__device__ inline void lds_fill(uint32_t* dst, const uint32_t* __restrict__ src, int n) {
-    const int nt = (int)blockDim.x;
-    int k = (int)threadIdx.x;
-    for (; k + 7 * nt < n; k += 8 * nt) {
-        uint32_t v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = src[k + j * nt];
-#pragma unroll
-        for (int j = 0; j < 8; j++) dst[k + j * nt] = v[j];
-    }
-    for (; k < n; k += nt) dst[k] = src[k];
-}
-
-__device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t bytes) {
-    // wave-uniform inputs made provably uniform (no waterfall loops around the loads)
-    const uint64_t u = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
-                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-// The LDS quad level's entry for fine cell (ixC, iyC), resolved through the quad's record when the
-// point's sub-quad is uniform with the record's code (tiles::raster_code with use_quad, branch-free)
-__device__ inline uint32_t quad_lookup(const StreamArgs& s, const uint16_t* quad, const uint32_t* qmask,
-                                       const uint16_t* qcode, uint32_t ixC, uint32_t iyC) {
-    const uint32_t q = quad[__umul24(iyC >> s.qsh, (uint32_t)s.qnx) + (ixC >> s.qsh)];
-    // q >= 0x8000 with record index q & 0x7fff < n_qrec, as one unsigned compare (q < 0x8000 wraps)
-    const uint32_t r = q - 0x8000u;
-    const bool rec = r < (uint32_t)s.n_qrec;
-    const uint32_t sh = (uint32_t)(s.cs + s.qrl);
-    const uint32_t b = (__builtin_amdgcn_ubfe(iyC, sh, 3u) << 3) | __builtin_amdgcn_ubfe(ixC, sh, 3u);
-    const uint32_t rr = rec ? r : 0u;  // record 0 (mask words 0 and 1) is always readable
-    const uint32_t w = qmask[2u * rr + (b >> 5)];
-    const uint32_t c = qcode[rr];
-    return (rec && __builtin_amdgcn_ubfe(w, b & 31u, 1u)) ? c : q;
-}
-
-template <bool LDS_COUNTS, bool PAIRS, bool VEC>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream(JoinArgs a, StreamArgs s) {
-    extern __shared__ unsigned int lds[];
-    const int nwaves = (int)(blockDim.x >> 6);
-    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;  // counts + one spill word per lane
-    uint32_t* stage = lds + ncw;
-    uint32_t* tb = stage + nwaves * s.stage_words;
-    uint32_t* quadw = tb + (s.tb_lds ? s.n_tiles : 0);
-    const uint16_t* quad = (const uint16_t*)quadw;
-    uint32_t* qmask = quadw + s.n_quad_words;
-    const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
-    lds_fill(quadw, s.quad, s.n_quad_words);
-    lds_fill(qmask, s.qrec, s.n_qrec_words);
-    if (s.tb_lds)
-        lds_fill(tb, s.tile_base, s.n_tiles);
-    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
-    const __amdgpu_buffer_rsrc_t rblk = stream_rsrc(s.blocks, s.blocks_bytes);
-    const __amdgpu_buffer_rsrc_t rtb = stream_rsrc(s.tile_base, s.tile_base_bytes);
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    // the wave index through readfirstlane: w0 and every branch on it are provably wave-uniform
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint32_t* wq = stage + wave * s.stage_words;
-    uint32_t wn = 0;  // wave-uniform fill level of the stage
-    const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
-    // rows of slot k: w0 + (k >> 1) 128 + 2 lane + (k & 1)
-    auto row_of = [&](int64_t wb, int k) -> int64_t { return wb + (k >> 1) * 128 + 2 * lane + (k & 1); };
-    v2d px[2], py[2];
-    auto load4 = [&](int64_t wb) {  // unconditional: past the end, the chunk's first rows (VEC: >= 256 of them)
-        const int64_t r = (wb + 256 <= a.n) ? wb + 2 * lane : a.row_lo;
-        px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
-        px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
-        py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
-        py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
-    };
-    if (VEC) load4(w0);
-    for (; w0 < a.n; w0 += stride) {
-        const bool full = VEC && w0 + 256 <= a.n;  // wave-uniform
-        double x[4], y[4];
-        bool live[4];
-        if (full) {
-            x[0] = px[0].x, x[1] = px[0].y, x[2] = px[1].x, x[3] = px[1].y;
-            y[0] = py[0].x, y[1] = py[0].y, y[2] = py[1].x, y[3] = py[1].y;
-#pragma unroll
-            for (int k = 0; k < 4; k++) live[k] = true;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int64_t r = row_of(w0, k);
-                live[k] = r < a.n;
-                x[k] = live[k] ? a.x[r] : 0.0;
-                y[k] = live[k] ? a.y[r] : 0.0;
-            }
-        }
-        // stage A: fine-cell coordinates, quad level (LDS), tile base (LDS)
-        double gx[4], gy[4];
-        uint32_t ixC[4], iyC[4], qv[4], tbv[4], ta[4];
-        bool fin[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            fin[k] = __builtin_isfinite(x[k] + y[k]);
-            gx[k] = fmin(fmax((x[k] - s.x0) * s.sxC, 0.0), s.gxmax);  // NaN -> 0
-            gy[k] = fmin(fmax((y[k] - s.y0) * s.syC, 0.0), s.gymax);
-            ixC[k] = (uint32_t)(int)gx[k];
-            iyC[k] = (uint32_t)(int)gy[k];
-            // (indices < 2^24: 24-bit multiplies)
-            qv[k] = quad_lookup(s, quad, qmask, qcode, ixC[k], iyC[k]);
-            ta[k] = __umul24(iyC[k] >> s.tsh, (uint32_t)s.tnx) + (ixC[k] >> s.tsh);
-            tbv[k] = s.tb_lds ? tb[ta[k]] : 0u;
-        }
-        // stage B: sub-block entries of the points in non-uniform quads
-        uint32_t code[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t local = (((iyC[k] >> s.cs) & qm) << s.qs) | ((ixC[k] >> s.cs) & qm);
-            const uint32_t off = ((((qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
-            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, qv[k] >= 0x8000u ? off : kNoLoad, 0, MOSAIC_AUX_SUB);
-        }
-        // stage C: leaf codes and line records of the points in mixed sub-blocks
-        uint32_t leaf[4];
-        v4u lrec[4];
-        bool blk[4], line[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            code[k] = qv[k] >= 0x8000u ? code[k] : qv[k];
-            blk[k] = code[k] - 0x8000u < 0x7fffu;  // kSubBlock | n, not kMixed
-            line[k] = blk[k] && (code[k] & 0x4000u);
-            if (!s.tb_lds) tbv[k] = __builtin_amdgcn_raw_buffer_load_b32(rtb, blk[k] ? ta[k] << 2 : kNoLoad, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t n = code[k] & 0x3fffu;
-            const uint32_t lf = ((iyC[k] & cm) << s.cs) | (ixC[k] & cm);
-            const uint32_t loff = (tbv[k] + (n << (2 * s.cs)) + lf) << 1;
-            const uint32_t roff = (tbv[k] - 8u * (n + 1u)) << 1;
-            leaf[k] = __builtin_amdgcn_raw_buffer_load_b16(rblk, (blk[k] && !line[k]) ? loff : kNoLoad, 0, 0);
-            lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rblk, line[k] ? roff : kNoLoad, 0, 0);
-        }
-        if (VEC) load4(w0 + stride);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            // tiles::line_code, as selects
-            const float u = (float)(gx[k] - (double)(ixC[k] & ~cm)), v = (float)(gy[k] - (double)(iyC[k] & ~cm));
-            const float sv = fmaf(__uint_as_float(lrec[k].x), u, fmaf(__uint_as_float(lrec[k].y), v, __uint_as_float(lrec[k].z)));
-            const uint32_t pos = lrec[k].w & 0xffffu, neg = lrec[k].w >> 16;
-            uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
-            lc = sv <= -1.0f ? neg : lc;
-            uint32_t c = line[k] ? lc : (blk[k] ? leaf[k] : code[k]);
-            c = fin[k] ? c : (uint32_t)tiles::kMixed;
-            code[k] = live[k] ? c : 0u;
-        }
-        // counts: one LDS add per point (points without a pair add to the lane's spill word)
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (LDS_COUNTS && !PAIRS) {
-                const uint32_t slot = code[k] - 1u < 0xfffeu ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
-                atomicAdd(&lds[slot], 1u);
-            } else if (code[k] - 1u < 0xfffeu) {
-                emit_hit<LDS_COUNTS, PAIRS>(a, row_of(w0, k), code[k] - 1u, lds);
-            }
-        }
-        // mixed rows to the per-wave stage (rare: one wave-uniform test per iteration)
-        const bool anym = code[0] == tiles::kMixed || code[1] == tiles::kMixed || code[2] == tiles::kMixed ||
-                          code[3] == tiles::kMixed;
-        if (__ballot(anym)) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool m = code[k] == tiles::kMixed;
-                const unsigned long long mm = __ballot(m);
-                if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(w0, k) - a.row_lo);
-                wn += (uint32_t)__popcll(mm);
-                stage_flush(a, wq, wn, lane, 64);  // one atomic per >= 64 rows; the stage holds < 128
-            }
-        }
-    }
-    stage_flush(a, wq, wn, lane, 1);
-    if (LDS_COUNTS) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
-            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
-    }
-}
-
-
-// ---- k_join_stream_pipe: k_join_stream's per-point computation as a three-stage software
-// pipeline over the wave's groups of 256 rows, so that the gathers of one group overlap the
-// coordinate loads of the next instead of adding to them.  Iteration t: finish group t - 2 (its leaf
-// codes / line records arrived), turn group t - 1's sub-block entries into leaf and line gathers,
-// run group t's coordinates through the quad level and issue its sub-block gathers, and load group
-// t + 1's coordinates -- issued in that order, so every wait is on the oldest loads in flight
-// (vector-memory returns retire in order per wave).  Needs 16-byte aligned columns, tile_base in
-// LDS and at least one full group; the wave's last partial group runs unpipelined.  Same answers
-// as k_join_stream, point for point.
-struct PipeGroup {
-    float u[4], v[4];     // offset in the sub-block, leaf cells
-    uint32_t lf[4];       // leaf cell index within the leaf block
-    uint32_t tbv[4];      // tile base
-    uint32_t qv[4];       // quad-level entry
-    uint32_t code[4];     // sub-block entry (gathered), then the answer
-    uint32_t leaf[4];     // gathered leaf code
-    v4u lrec[4];          // gathered line record
-};
-// quad-level value standing for "non-finite coordinates" in a group (never a code: codes are
-// <= kMaxRasterKeys + 1 or >= kSubBlock): the row takes the tile path
-static const uint32_t kPipeNonFinite = 0x7fffu;
-static_assert(tiles::kMaxRasterKeys + 1 < 0x7fff, "key codes stay below kPipeNonFinite");
-// stage B -> D marker of a row in a line sub-block (above every code)
-static const uint32_t kPipeLine = 0x10000u;
-
-template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_pipe(JoinArgs a, StreamArgs s) {
-    extern __shared__ unsigned int lds[];
-    const int nwaves = (int)(blockDim.x >> 6);
-    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
-    uint32_t* stage = lds + ncw;
-    uint32_t* tb = stage + nwaves * s.stage_words;
-    uint32_t* quadw = tb + s.n_tiles;
-    const uint16_t* quad = (const uint16_t*)quadw;
-    uint32_t* qmask = quadw + s.n_quad_words;
-    const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
-    lds_fill(quadw, s.quad, s.n_quad_words);
-    lds_fill(qmask, s.qrec, s.n_qrec_words);
-    lds_fill(tb, s.tile_base, s.n_tiles);
-    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
-    const __amdgpu_buffer_rsrc_t rblk = stream_rsrc(s.blocks, s.blocks_bytes);
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint32_t* wq = stage + wave * s.stage_words;
-    uint32_t wn = 0;
-    const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u;
-    const double gx0 = -s.x0 * s.sxC, gy0 = -s.y0 * s.syC;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
-    // full groups of this wave: wbase + t stride, t < T
-    const int64_t T = wbase + 256 <= a.n ? (a.n - 256 - wbase) / stride + 1 : 0;
-    auto row_of = [&](int64_t wb, int k) -> int64_t { return wb + (k >> 1) * 128 + 2 * lane + (k & 1); };
-    // stage A: coordinates -> fine cell, quad level and tile base (LDS) -> sub-block gathers
-    auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, PipeGroup& g) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool lv = valid && live[k];
-            // (x - x0) sxC as one fma (x sxC - x0 sxC): within the raster's 1e-6-cell widening
-            const double gx = fmin(fmax(fma(x[k], s.sxC, gx0), 0.0), s.gxmax);  // NaN -> 0
-            const double gy = fmin(fmax(fma(y[k], s.syC, gy0), 0.0), s.gymax);
-            const uint32_t ixC = (uint32_t)(int)gx, iyC = (uint32_t)(int)gy;
-            // the offset in the sub-block, leaf cells: (ixC & cm) + fract(gx) (gx >= 0)
-            g.u[k] = (float)(ixC & cm) + (float)__builtin_amdgcn_fract(gx);
-            g.v[k] = (float)(iyC & cm) + (float)__builtin_amdgcn_fract(gy);
-            g.lf[k] = ((iyC & cm) << s.cs) | (ixC & cm);
-            const uint32_t q = quad_lookup(s, quad, qmask, qcode, ixC, iyC);
-            // dead rows answer 0.  Non-finite coordinates need no test: fmax / fmin clamp them onto
-            // the grid's edge ring, whose sub-blocks are all 0 or kMixed (PointRaster edge_ok, a
-            // precondition of this kernel), and a non-finite point joins nothing in the reference
-            // (geoToH3 gives H3_NULL) -- 0 is its answer, kMixed sends it to the exact path.
-            g.qv[k] = lv ? q : 0u;
-            g.tbv[k] = tb[__umul24(iyC >> s.tsh, (uint32_t)s.tnx) + (ixC >> s.tsh)];
-            const uint32_t local = (__builtin_amdgcn_ubfe(iyC, (uint32_t)s.cs, (uint32_t)s.qs) << s.qs) |
-                                   __builtin_amdgcn_ubfe(ixC, (uint32_t)s.cs, (uint32_t)s.qs);
-            const uint32_t off = ((((g.qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
-            g.code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, g.qv[k] >= 0x8000u ? off : kNoLoad, 0, MOSAIC_AUX_SUB);
-        }
-    };
-    // stage B: sub-block entries -> leaf and line gathers
-    auto stage_b = [&](PipeGroup& g) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t c = g.qv[k] >= 0x8000u ? g.code[k] : g.qv[k];
-            const bool blk = c - 0x8000u < 0x7fffu;  // kSubBlock | n, not kMixed
-            const bool line = blk && (c & 0x4000u);
-            const uint32_t n = c & 0x3fffu;
-            const uint32_t loff = (g.tbv[k] + (n << (2 * s.cs)) + g.lf[k]) << 1;
-            const uint32_t roff = (g.tbv[k] - 8u * (n + 1u)) << 1;
-            g.leaf[k] = __builtin_amdgcn_raw_buffer_load_b16(rblk, (blk && !line) ? loff : kNoLoad, 0, MOSAIC_AUX_LEAF);
-            g.lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rblk, line ? roff : kNoLoad, 0, MOSAIC_AUX_LINE);
-            // for stage D: kPipeLine for a line row, else the code to OR with the gathered leaf code
-            // (0 for leaf rows; out-of-range gathers return 0)
-            g.code[k] = line ? kPipeLine : (blk ? 0u : c);
-        }
-    };
-    // stage D: the answers -> counts and the mixed-row stage
-    auto stage_d = [&](PipeGroup& g, int64_t wb) {
-        uint32_t code[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float sv = fmaf(__uint_as_float(g.lrec[k].x), g.u[k],
-                                  fmaf(__uint_as_float(g.lrec[k].y), g.v[k], __uint_as_float(g.lrec[k].z)));
-            const uint32_t pos = g.lrec[k].w & 0xffffu, neg = g.lrec[k].w >> 16;
-            uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
-            lc = sv <= -1.0f ? neg : lc;
-            // answers: 0, key + 1 (<= kMaxRasterKeys), or >= kPipeNonFinite (kMixed, non-finite):
-            // the tile path
-            code[k] = g.code[k] == kPipeLine ? lc : (g.code[k] | g.leaf[k]);
-        }
-        // counts: one LDS add per point (points without a pair add to the lane's spill word: a
-        // masked add measured slower on clustered input)
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (LDS_COUNTS && !PAIRS) {
-                const uint32_t slot = code[k] - 1u < kPipeNonFinite - 1u ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
-                atomicAdd(&lds[slot], 1u);
-            } else if (code[k] - 1u < kPipeNonFinite - 1u) {
-                emit_hit<LDS_COUNTS, PAIRS>(a, row_of(wb, k), code[k] - 1u, lds);
-            }
-        }
-        const uint32_t cmax = max(max(code[0], code[1]), max(code[2], code[3]));
-        if (__ballot(cmax >= kPipeNonFinite)) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool m = code[k] >= kPipeNonFinite;
-                const unsigned long long mm = __ballot(m);
-                if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(wb, k) - a.row_lo);
-                wn += (uint32_t)__popcll(mm);
-                stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
-            }
-        }
-    };
-    // coordinates of the next MOSAIC_PIPE_DEPTH groups (1: loaded one iteration ahead; 2: two)
-    struct Coords {
-        v2d px[2], py[2];
-    };
-    auto load4 = [&](Coords& cb, int64_t wb, bool valid) {  // unconditional: invalid groups re-read the wave's first rows
-        const int64_t r = valid ? wb + 2 * lane : wbase + 2 * lane;
-        cb.px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
-        cb.px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
-        cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
-        cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
-    };
-    Coords cb0, cb1;
-    // two group slots used in turn (no copies of registers that loads are still landing in):
-    // iteration t finishes the slot holding t - 2, advances the one holding t - 1, refills the first
-    PipeGroup g0, g1;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        g0.qv[k] = g1.qv[k] = 0u;
-        g0.code[k] = g1.code[k] = 0u;
-        g0.tbv[k] = g1.tbv[k] = g0.lf[k] = g1.lf[k] = 0u;
-        g0.u[k] = g1.u[k] = g0.v[k] = g1.v[k] = 0.0f;
-    }
-    auto step = [&](int64_t t, PipeGroup& gfin, PipeGroup& gadv, Coords& cb, Coords& cn) {
-        const bool all[4] = {true, true, true, true};
-        if (t >= 2) stage_d(gfin, wbase + (t - 2) * stride);
-        stage_b(gadv);  // (invalid groups gather nothing)
-        const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
-        const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
-        stage_a(x, y, all, t < T, gfin);
-        if (MOSAIC_PIPE_DEPTH == 2) load4(cb, wbase + (t + 2) * stride, t + 2 < T);  // cb is free again
-        else load4(cn, wbase + (t + 1) * stride, t + 1 < T);
-    };
-    if (T > 0) {
-        load4(cb0, wbase, true);
-        if (MOSAIC_PIPE_DEPTH == 2) load4(cb1, wbase + stride, 1 < T);
-        for (int64_t t = 0; t < T + 2; t += 2) {
-            step(t, g0, g1, cb0, cb1);
-            if (t + 1 >= T + 2) break;
-            step(t + 1, g1, g0, cb1, cb0);
-        }
-    }
-    // the wave's partial group (rows past its last full group), unpipelined
-    const int64_t wt = wbase + T * stride;
-    if (wt < a.n) {
-        double x[4], y[4];
-        bool live[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int64_t r = row_of(wt, k);
-            live[k] = r < a.n;
-            x[k] = live[k] ? a.x[r] : 0.0;
-            y[k] = live[k] ? a.y[r] : 0.0;
-        }
-        PipeGroup g;
-        stage_a(x, y, live, true, g);
-        stage_b(g);
-        stage_d(g, wt);
-    }
-    stage_flush(a, wq, wn, lane, 1);
-    if (LDS_COUNTS) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
-            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
-    }
 }
 
 // ---- point-raster build on the GPU: phase 1 of tiles::Builder::build_raster (tiles_build.cpp,
@@ -2007,179 +1471,6 @@ __global__ void __launch_bounds__(256) k_h3_geom(const int64_t* ids, const uint8
     if (bad) atomicOr(flags, 1u);
 }
 
-// ---- BNG dense cell table (positive resolutions): BNGIndexSystem.pointToIndex
-// (BNGIndexSystem.scala:277-291, 528-541) maps a point with 0 <= toInt(e), toInt(n) < 1e7 to the id
-// of cell (toInt(e) / divisor, toInt(n) / divisor) -- one-to-one there, the two letters being the
-// leading digits of those quotients (100000 is a multiple of every positive-resolution divisor).
-// The host builds a dense table over the chip cells' cell range: 0 = no chip, kBngPure | (k + 1) =
-// exactly one chip, a core chip of polygon k, kBngLeaf | block for other cells (below).  One
-// L2-resident gather per point (two in border cells) decides all but the rows in mixed sub-cells
-// (and rows outside that integer range), which go to the mixed queue and k_join_mixed_bng (the
-// generic point_to_index + probe + chip loop).
-// Border cells carry kBngLeaf | base: C x C sub-cell entries at leaf[base] (the H3 point raster's
-// codes, tiles_build.cpp bng_leaf_blocks) -- a code, kMixed (the row goes to the mixed queue) or
-// kSubBlock | kLineBit | n: the sub-cell is split by one straight chip edge, LineRec n of the cell at
-// leaf[base - 8 (n + 1)] decides the point from its offset in the sub-cell.
-static const uint32_t kBngPure = 0x80000000u, kBngLeaf = 0x40000000u;
-
-// k_join_stream_bng: the dense table's answer for every point, branch-free, in the layout of
-// k_join_stream (256 rows per wave and iteration, 1 KiB coalesced coordinate loads, the next
-// iteration's coordinates loaded behind this iteration's gathers).  Per point: JVM toInt of both
-// coordinates, the cell (exact quotients: (int)(a / div + 1e-7) from one f64 multiply-add -- for
-// a < 1e7 and div <= 1e5 a non-integer quotient is >= 1 / div below the next integer, far more than
-// the 2e-9 the reciprocal and the offset move it), one 4-byte cell gather and, in border cells, one
-// 2-byte leaf gather, both through buffer descriptors (lanes that need none pass an out-of-range
-// offset).  NaN coordinates set flags bit 0 (the reference throws IllegalStateException).
-//
-// LDS cell level (when the table is built with one and it fits the workgroup's LDS): one byte per
-// 2^lsh x 2^lsh block of table cells, copied to LDS at kernel start -- 0: no chip cell in the block,
-// 1..0xFE: every cell of the block is a pure cell whose answer is that code (key + 1), 0xFF: gather
-// the cell's table entry.  Points in pure and empty cells then need no gather at all.
-static const uint32_t kBngLdsGather = 0xFFu;
-struct BngStreamArgs {
-    int32_t e0, n0, ne, nn, C;
-    double inv_div, div, f;  // 1 / divisor (rounded), divisor, C / divisor
-    const uint32_t* cells;
-    const uint16_t* leaf;
-    uint32_t cells_bytes, leaf_bytes;
-    const uint32_t* lcell;   // LDS cell level (bytes packed in words); nullptr / lcell_words == 0: none
-    int32_t lcell_words, lsh, lnx;
-};
-template <bool LDS_COUNTS, bool PAIRS, bool VEC>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_bng(JoinArgs a, BngStreamArgs s) {
-    extern __shared__ unsigned int lds[];
-    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
-    uint32_t* stage = lds + ncw;
-    uint32_t* lcw = stage + (int)(blockDim.x >> 6) * kStageWords;
-    const uint8_t* lcell = (const uint8_t*)lcw;
-    const bool use_lc = s.lcell_words > 0;  // (uniform)
-    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
-    lds_fill(lcw, s.lcell, s.lcell_words);
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t rcell = stream_rsrc(s.cells, s.cells_bytes);
-    const __amdgpu_buffer_rsrc_t rleaf = stream_rsrc(s.leaf, s.leaf_bytes);
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint32_t* wq = stage + wave * kStageWords;
-    uint32_t wn = 0;
-    bool nan_seen = false;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
-    auto row_of = [&](int64_t wb, int k) -> int64_t { return wb + (k >> 1) * 128 + 2 * lane + (k & 1); };
-    v2d px[2], py[2];
-    auto load4 = [&](int64_t wb) {
-        const int64_t r = (wb + 256 <= a.n) ? wb + 2 * lane : a.row_lo;
-        px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
-        px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
-        py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
-        py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
-    };
-    if (VEC) load4(w0);
-    const uint32_t C = (uint32_t)s.C;
-    for (; w0 < a.n; w0 += stride) {
-        const bool full = VEC && w0 + 256 <= a.n;
-        double x[4], y[4];
-        bool live[4];
-        if (full) {
-            x[0] = px[0].x, x[1] = px[0].y, x[2] = px[1].x, x[3] = px[1].y;
-            y[0] = py[0].x, y[1] = py[0].y, y[2] = py[1].x, y[3] = py[1].y;
-#pragma unroll
-            for (int k = 0; k < 4; k++) live[k] = true;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int64_t r = row_of(w0, k);
-                live[k] = r < a.n;
-                x[k] = live[k] ? a.x[r] : 0.0;
-                y[k] = live[k] ? a.y[r] : 0.0;
-            }
-        }
-        uint32_t code[4], e[4], loff[4];
-        float su[4], sv[4];
-        bool inr[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool nan = x[k] != x[k] || y[k] != y[k];
-            nan_seen |= live[k] && nan;
-            const int32_t eI = bng::jvm_d2i(x[k]), nI = bng::jvm_d2i(y[k]);
-            inr[k] = (uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u;
-            const int32_t qe = (int32_t)fma((double)eI, s.inv_div, 1e-7), qn = (int32_t)fma((double)nI, s.inv_div, 1e-7);
-            const int32_t ce = qe - s.e0, cn = qn - s.n0;
-            const bool cell_in = inr[k] && (uint32_t)ce < (uint32_t)s.ne && (uint32_t)cn < (uint32_t)s.nn;
-            // LDS cell level first: only cells it marks kBngLdsGather gather their table entry
-            const uint32_t li = cell_in ? __umul24((uint32_t)cn >> s.lsh, (uint32_t)s.lnx) + ((uint32_t)ce >> s.lsh) : 0u;
-            const uint32_t lb = use_lc ? (uint32_t)lcell[li] : kBngLdsGather;
-            const bool gth = cell_in && lb == kBngLdsGather;
-            e[k] = __builtin_amdgcn_raw_buffer_load_b32(rcell, gth ? (uint32_t)(cn * s.ne + ce) << 2 : kNoLoad, 0, 0);
-            e[k] = (gth || !cell_in) ? e[k] : (lb ? (kBngPure | lb) : 0u);
-            // sub-cell of the point inside the cell [qe div, (qe + 1) div) x [qn div, (qn + 1) div)
-            const double gxs = (x[k] - (double)qe * s.div) * s.f, gys = (y[k] - (double)qn * s.div) * s.f;
-            int sx = (int)gxs, sy = (int)gys;
-            sx = min(max(sx, 0), (int)C - 1);
-            sy = min(max(sy, 0), (int)C - 1);
-            su[k] = (float)(gxs - (double)sx);  // offset in the sub-cell (sub-cell units)
-            sv[k] = (float)(gys - (double)sy);
-            loff[k] = (uint32_t)(sy * (int)C + sx);
-        }
-        bool leafc[4], line[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            leafc[k] = (e[k] & (kBngPure | kBngLeaf)) == kBngLeaf;
-            const uint32_t off = ((e[k] & ~kBngLeaf) + loff[k]) << 1;
-            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rleaf, leafc[k] ? off : kNoLoad, 0, MOSAIC_AUX_BNG);
-        }
-        v4u lrec[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            line[k] = leafc[k] && (code[k] & 0xC000u) == 0xC000u && code[k] != (uint32_t)tiles::kMixed;
-            const uint32_t roff = ((e[k] & ~kBngLeaf) - 8u * ((code[k] & 0x3fffu) + 1u)) << 1;
-            lrec[k] = __builtin_amdgcn_raw_buffer_load_b128(rleaf, line[k] ? roff : kNoLoad, 0, 0);
-        }
-        if (VEC) load4(w0 + stride);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            // tiles::line_code, as selects
-            const float lv = fmaf(__uint_as_float(lrec[k].x), su[k], fmaf(__uint_as_float(lrec[k].y), sv[k], __uint_as_float(lrec[k].z)));
-            uint32_t lc = lv >= 1.0f ? (lrec[k].w & 0xffffu) : (uint32_t)tiles::kMixed;
-            lc = lv <= -1.0f ? (lrec[k].w >> 16) : lc;
-            code[k] = line[k] ? lc : code[k];
-            uint32_t c = (e[k] & kBngPure) ? (e[k] & ~kBngPure) : ((e[k] & kBngLeaf) ? code[k] : (e[k] ? (uint32_t)tiles::kMixed : 0u));
-            c = inr[k] ? c : (uint32_t)tiles::kMixed;      // outside the one-to-one range: generic path
-            c = (x[k] != x[k] || y[k] != y[k]) ? 0u : c;  // NaN: flagged, no pair
-            code[k] = live[k] ? c : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (LDS_COUNTS && !PAIRS) {
-                const uint32_t slot = code[k] - 1u < 0xfffeu ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
-                atomicAdd(&lds[slot], 1u);
-            } else if (code[k] - 1u < 0xfffeu) {
-                emit_hit<LDS_COUNTS, PAIRS>(a, row_of(w0, k), code[k] - 1u, lds);
-            }
-        }
-        const bool anym = code[0] == tiles::kMixed || code[1] == tiles::kMixed || code[2] == tiles::kMixed ||
-                          code[3] == tiles::kMixed;
-        if (__ballot(anym)) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool m = code[k] == tiles::kMixed;
-                const unsigned long long mm = __ballot(m);
-                if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(w0, k) - a.row_lo);
-                wn += (uint32_t)__popcll(mm);
-                stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
-            }
-        }
-    }
-    stage_flush(a, wq, wn, lane, 1);
-    if (__ballot(nan_seen) && lane == 0) atomicOr(a.flags, 1u);
-    if (LDS_COUNTS) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
-            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
-    }
-}
-
 // Rows of the BNG dense table's mixed sub-cells (and rows outside its one-to-one range), R rows per
 // lane: coordinates, cell (BNGIndexSystem.pointToIndex), first hash probe of all R rows issued
 // together (R independent chains per lane, as k_join_mixed), then the raster chip loop per row slot.
@@ -2613,6 +1904,9 @@ struct Options {
     // copy on copy_stream overlapping the current chunk's join (0: stage the whole batch first)
     int64_t host_chunk = (int64_t)1 << 25;
     int timing = 0;           // HIP events bracket each fused join kernel on the calling thread's stream
+    // a calling thread keeps its scratch (queues, staging) between calls up to this many bytes; above
+    // it the scratch is freed when the call returns (0: always kept, the default)
+    int64_t scratch_limit = 0;
 };
 
 // Execution state of one calling thread on one context: its HIP stream (created on first use, or
@@ -2634,13 +1928,29 @@ struct ThreadCtx : Options {
     unsigned int deferred_flags = 0;
     std::vector<hipEvent_t> ev_start, ev_stop;
     size_t ev_used = 0;
+    // the scratch buffers sized by the calls (not `scalars`, which every call needs)
+    std::vector<DevBuf*> scratch() {
+        return {&amb_queue, &mix_queue, &stage_x, &stage_y, &stage_v, &stage_out, &stage_out2, &stage_idx, &geo_off,
+                &geo_data, &dec_x, &dec_y, &dec_status, &hx[0], &hx[1], &hy[0], &hy[1], &hcounts};
+    }
+    size_t held() {
+        size_t n = 0;
+        for (DevBuf* b : scratch()) n += b->bytes;
+        return n;
+    }
+    // free the scratch once the thread's queued work is done (scratch_limit)
+    void trim() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+        for (DevBuf* b : scratch()) b->release();
+    }
     void release() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
-        for (DevBuf* b : {&amb_queue, &mix_queue, &scalars, &stage_x, &stage_y, &stage_v, &stage_out, &stage_out2,
-                          &stage_idx, &geo_off, &geo_data, &dec_x, &dec_y, &dec_status, &hx[0], &hx[1], &hy[0], &hy[1],
-                          &hcounts})
-            b->release();
+        if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+        for (DevBuf* b : scratch()) b->release();
+        scalars.release();
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         for (size_t i = 0; i < ev_start.size(); i++) {
             (void)hipEventDestroy(ev_start[i]);
@@ -2655,18 +1965,60 @@ struct ThreadCtx : Options {
 struct mosaic_ctx {
     int device = 0;
     int n_cu = 256;
+    uint64_t serial = 0;  // unique per context for the process's lifetime (never reused, unlike pointers)
     std::mutex mu;
     Options opt;
-    std::unordered_map<std::thread::id, std::unique_ptr<ThreadCtx>> threads;
+    // keyed by the thread's serial (this_thread_serial), never by pthread / std::thread ids, which
+    // the runtime reuses: a new thread must not inherit a dead thread's state (its stream)
+    std::unordered_map<uint64_t, std::unique_ptr<ThreadCtx>> threads;
 };
 
 static const int kScalars = 5;
 
+// Lifetime of per-thread states.  A thread's state on a context is freed by mosaic_thread_release,
+// by mosaic_destroy, or when the thread exits (ThreadExit below) -- so an executor whose worker pool
+// retires threads does not accumulate streams and scratch.  Live contexts are registered by serial;
+// lock order: g_live_mu, then ctx->mu.
+static std::mutex g_live_mu;
+static std::unordered_map<mosaic_ctx*, uint64_t> g_live;
+static std::atomic<uint64_t> g_serial{1};
+
+static uint64_t this_thread_serial() {
+    static thread_local uint64_t id = g_serial.fetch_add(1);
+    return id;
+}
+
+struct ThreadExit {
+    std::vector<std::pair<mosaic_ctx*, uint64_t>> ctxs;  // contexts this thread entered
+    ~ThreadExit() {
+        // the process's main thread exits with the process: its states go with mosaic_destroy or the
+        // process, never from a thread_local destructor racing the HIP runtime's own teardown
+        if ((pid_t)syscall(SYS_gettid) == getpid()) return;
+        const uint64_t me = this_thread_serial();
+        std::lock_guard<std::mutex> live(g_live_mu);
+        for (auto& e : ctxs) {
+            auto it = g_live.find(e.first);
+            if (it == g_live.end() || it->second != e.second) continue;  // destroyed since
+            std::unique_ptr<ThreadCtx> t;
+            {
+                std::lock_guard<std::mutex> lock(e.first->mu);
+                auto f = e.first->threads.find(me);
+                if (f == e.first->threads.end()) continue;
+                t = std::move(f->second);
+                e.first->threads.erase(f);
+            }
+            t->release();
+        }
+    }
+};
+static thread_local ThreadExit g_thread_exit;
+
 // The calling thread's execution state, options refreshed from the context (created on first use).
 static ThreadCtx* enter(mosaic_ctx* ctx) {
     if (!ctx) return nullptr;
+    const uint64_t me = this_thread_serial();
     std::lock_guard<std::mutex> lock(ctx->mu);
-    std::unique_ptr<ThreadCtx>& t = ctx->threads[std::this_thread::get_id()];
+    std::unique_ptr<ThreadCtx>& t = ctx->threads[me];
     if (!t) {
         std::unique_ptr<ThreadCtx> n(new ThreadCtx());
         n->device = ctx->device;
@@ -2674,23 +2026,38 @@ static ThreadCtx* enter(mosaic_ctx* ctx) {
         if (hipSetDevice(ctx->device) != hipSuccess ||
             hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking) != hipSuccess) {
             fail(MOSAIC_E_HIP, "hipStreamCreate failed");
-            ctx->threads.erase(std::this_thread::get_id());
+            ctx->threads.erase(me);
             return nullptr;
         }
         n->own_stream = true;
         if (n->scalars.reserve(kScalars * 8)) {
             n->release();
-            ctx->threads.erase(std::this_thread::get_id());
+            ctx->threads.erase(me);
             return nullptr;
         }
         t = std::move(n);
+        auto& v = g_thread_exit.ctxs;
+        v.erase(std::remove_if(v.begin(), v.end(), [&](const std::pair<mosaic_ctx*, uint64_t>& e) {
+                    return e.first == ctx;
+                }), v.end());
+        v.emplace_back(ctx, ctx->serial);
     }
     static_cast<Options&>(*t) = ctx->opt;
     return t.get();
 }
+
+// Frees the calling thread's scratch on the way out of an entry point when it holds more than the
+// option scratch_limit (bytes; 0 keeps it).
+struct ScratchTrim {
+    ThreadCtx* c;
+    ~ScratchTrim() {
+        if (c && c->scratch_limit > 0 && (int64_t)c->held() > c->scratch_limit) c->trim();
+    }
+};
 #define ENTER(CTX)                                                                 \
     ThreadCtx* c = enter(CTX);                                                     \
-    if (!c) return (CTX) ? MOSAIC_E_HIP : fail(MOSAIC_E_ARG, "null context");
+    if (!c) return (CTX) ? MOSAIC_E_HIP : fail(MOSAIC_E_ARG, "null context");      \
+    ScratchTrim scratch_trim_{c};
 
 static int timing_begin(ThreadCtx* c, hipEvent_t* stop_out) {
     *stop_out = nullptr;
@@ -2862,10 +2229,15 @@ int mosaic_init(int device, mosaic_ctx** out) {
     HIP_TRY(hipSetDevice(device));
     mosaic_ctx* c = new mosaic_ctx();
     c->device = device;
+    c->serial = g_serial.fetch_add(1);
+    {
+        std::lock_guard<std::mutex> live(g_live_mu);
+        g_live[c] = c->serial;
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (!enter(c)) {  // the creating thread's state: fails early if the device cannot make a stream
-        delete c;
+        mosaic_destroy(c);
         return MOSAIC_E_HIP;
     }
     *out = c;
@@ -2875,11 +2247,44 @@ int mosaic_init(int device, mosaic_ctx** out) {
 int mosaic_destroy(mosaic_ctx* ctx) {
     if (!ctx) return MOSAIC_OK;
     {
+        std::lock_guard<std::mutex> live(g_live_mu);  // waits for an exiting thread's release
+        g_live.erase(ctx);
+    }
+    {
         std::lock_guard<std::mutex> lock(ctx->mu);
         for (auto& kv : ctx->threads) kv.second->release();
         ctx->threads.clear();
     }
     delete ctx;
+    return MOSAIC_OK;
+}
+
+int mosaic_thread_release(mosaic_ctx* ctx) {
+    if (!ctx) return fail(MOSAIC_E_ARG, "null context");
+    std::unique_ptr<ThreadCtx> t;
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        auto f = ctx->threads.find(this_thread_serial());
+        if (f == ctx->threads.end()) return MOSAIC_OK;
+        t = std::move(f->second);
+        ctx->threads.erase(f);
+    }
+    t->release();
+    auto& v = g_thread_exit.ctxs;
+    v.erase(std::remove_if(v.begin(), v.end(), [&](const std::pair<mosaic_ctx*, uint64_t>& e) { return e.first == ctx; }),
+            v.end());
+    return MOSAIC_OK;
+}
+
+int mosaic_thread_count(mosaic_ctx* ctx, int64_t* n_threads, int64_t* scratch_bytes) {
+    if (!ctx || !n_threads) return fail(MOSAIC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    *n_threads = (int64_t)ctx->threads.size();
+    if (scratch_bytes) {
+        int64_t b = 0;
+        for (auto& kv : ctx->threads) b += (int64_t)kv.second->held();
+        *scratch_bytes = b;
+    }
     return MOSAIC_OK;
 }
 
@@ -2955,6 +2360,9 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "timing") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
         o.timing = (int)v;
+    } else if (k == "scratch_limit") {
+        if (v < 0) return fail(MOSAIC_E_ARG, "scratch_limit must be >= 0");
+        o.scratch_limit = v;
     } else {
         return fail(MOSAIC_E_ARG, "unknown option " + k);
     }
@@ -4294,9 +3702,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             bs.lcell_words = shm_b + (size_t)ch->bng_lwords * 4 <= kStreamLdsMax ? ch->bng_lwords : 0;
             shm_b += (size_t)bs.lcell_words * 4;
             auto kernel_for = [&](bool vec) -> const void* {
-                if (pairs) return vec ? (const void*)k_join_stream_bng<false, true, true> : (const void*)k_join_stream_bng<false, true, false>;
-                if (lds) return vec ? (const void*)k_join_stream_bng<true, false, true> : (const void*)k_join_stream_bng<true, false, false>;
-                return vec ? (const void*)k_join_stream_bng<false, false, true> : (const void*)k_join_stream_bng<false, false, false>;
+                return stream_kernel_bng(lds, pairs, vec);
             };
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blkb, shm_b) != hipSuccess || per_cu < 1)
@@ -4339,14 +3745,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             a.mixq_count = sc + 4;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             auto kernel_for = [&](bool vec) -> const void* {
-                if (vec && sa.tb_lds && c->stream_pipe) {  // the pipelined form (k_join_stream_pipe)
-                    if (pairs) return (const void*)k_join_stream_pipe<false, true>;
-                    if (lds) return (const void*)k_join_stream_pipe<true, false>;
-                    return (const void*)k_join_stream_pipe<false, false>;
-                }
-                if (pairs) return vec ? (const void*)k_join_stream<false, true, true> : (const void*)k_join_stream<false, true, false>;
-                if (lds) return vec ? (const void*)k_join_stream<true, false, true> : (const void*)k_join_stream<true, false, false>;
-                return vec ? (const void*)k_join_stream<false, false, true> : (const void*)k_join_stream<false, false, false>;
+                // the pipelined form (k_join_stream_pipe) where it applies
+                return stream_kernel_h3(vec && sa.tb_lds && c->stream_pipe, lds, pairs, vec);
             };
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blk, shm_s) != hipSuccess || per_cu < 1)

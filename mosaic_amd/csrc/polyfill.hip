@@ -709,6 +709,10 @@ int h3_batch(hipStream_t st, int n_cu, int jdk, int res, const Input& in, int64_
         if (fails[q]) part_bad[q] = 1;
         if (part_bad[q] || seq[q].empty()) continue;
         const uint64_t M = (uint64_t)part_m[q];
+        // H3 v3.7 _polyfillInternal gives up when its table of maxPolyfillSize slots is full (its
+        // probe loop stops at loopCount > numHexagons) and polyfill returns no cells for the part;
+        // the placement below would otherwise probe forever
+        if (seq[q].size() > M) continue;
         std::unordered_set<uint64_t> used;
         used.reserve(seq[q].size() * 2);
         std::vector<std::pair<uint64_t, uint64_t>> placed;
