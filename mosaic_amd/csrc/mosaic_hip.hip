@@ -3693,7 +3693,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
-            const int blkb = c->stream_block;
+            const bool bpipe = c->stream_pipe && aligned;  // k_join_stream_bng_pipe (768-thread workgroups)
+            const int blkb = bpipe ? std::min(c->stream_block, kBngPipeBlock) : c->stream_block;
             size_t shm_b = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blkb / 64) * kStageWords * 4;
             // the LDS cell level when it fits this launch's LDS
             bs.lcell = (const uint32_t*)ch->bng_lcell.p;
@@ -3702,7 +3703,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             bs.lcell_words = shm_b + (size_t)ch->bng_lwords * 4 <= kStreamLdsMax ? ch->bng_lwords : 0;
             shm_b += (size_t)bs.lcell_words * 4;
             auto kernel_for = [&](bool vec) -> const void* {
-                return stream_kernel_bng(lds, pairs, vec);
+                return stream_kernel_bng(lds, pairs, vec, bpipe);
             };
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blkb, shm_b) != hipSuccess || per_cu < 1)
