@@ -12,7 +12,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmosaic_hip.so")
 # A/B measurement of alternative builds (tools/): an explicit library path overrides the in-tree one
-LIB_PATH = os.environ.get("MOSAIC_HIP_LIB", LIB_PATH)
+LIB_PATH = os.environ.get("MOSAIC_HIP_LIB") or LIB_PATH
 
 MOSAIC_OK = 0
 MOSAIC_E_ARG = 1

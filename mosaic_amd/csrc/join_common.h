@@ -123,6 +123,10 @@ struct StreamArgs {
     // words, then the n_qrec uint16 codes; n_qrec_words >= 2 (index 0 is always readable)
     const uint32_t* qrec;
     int32_t n_qrec, n_qrec_words, qrl;
+    // fixed-point fine-cell coordinates of k_join_stream_pipe (tiles::raster_code_fixed): g =
+    // clamp(cvt_i32(fma(x, sxF, gx0F)), 0, gxmaxF) with F = tiles::kFixBits fraction bits
+    double sxF, syF, gx0F, gy0F;
+    int32_t gxmaxF, gymaxF, fix_ok;  // fix_ok: (NX C) 2^F and (NY C) 2^F fit an int32
 };
 // per-wave mixed-row stage of the stream kernels (words): rows are appended one slot (<= 64 rows)
 // at a time and flushed at >= 64
@@ -176,13 +180,16 @@ __device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t byt
 
 // The LDS quad level's entry for fine cell (ixC, iyC), resolved through the quad's record when the
 // point's sub-quad is uniform with the record's code (tiles::raster_code with use_quad, branch-free)
+// (SH0: fraction bits below the fine-cell coordinates ixC, iyC -- 0, or kFixBits for the
+// fixed-point coordinates of k_join_stream_pipe)
+template <int SH0 = 0>
 __device__ inline uint32_t quad_lookup(const StreamArgs& s, const uint16_t* quad, const uint32_t* qmask,
                                        const uint16_t* qcode, uint32_t ixC, uint32_t iyC) {
-    const uint32_t q = quad[__umul24(iyC >> s.qsh, (uint32_t)s.qnx) + (ixC >> s.qsh)];
+    const uint32_t q = quad[__umul24(iyC >> (s.qsh + SH0), (uint32_t)s.qnx) + (ixC >> (s.qsh + SH0))];
     // q >= 0x8000 with record index q & 0x7fff < n_qrec, as one unsigned compare (q < 0x8000 wraps)
     const uint32_t r = q - 0x8000u;
     const bool rec = r < (uint32_t)s.n_qrec;
-    const uint32_t sh = (uint32_t)(s.cs + s.qrl);
+    const uint32_t sh = (uint32_t)(s.cs + s.qrl + SH0);
     const uint32_t b = (__builtin_amdgcn_ubfe(iyC, sh, 3u) << 3) | __builtin_amdgcn_ubfe(ixC, sh, 3u);
     const uint32_t rr = rec ? r : 0u;  // record 0 (mask words 0 and 1) is always readable
     const uint32_t w = qmask[2u * rr + (b >> 5)];

@@ -210,9 +210,19 @@ __device__ inline v4u gather_b128(__amdgpu_buffer_rsrc_t r, bool need, uint32_t 
 // (vector-memory returns retire in order per wave).  Needs 16-byte aligned columns, tile_base in
 // LDS and at least one full group; the wave's last partial group runs unpipelined.  Same answers
 // as k_join_stream, point for point.
+// MOSAIC_FIXED 1 (default): fine-cell coordinates in fixed point (tiles::raster_code_fixed) -- one
+// f64 fma, one saturating conversion and an integer clamp per axis, every index a bit-field of the
+// result; 0: the f64 clamp / floor / fract form (tiles::raster_code; measurement builds)
+#ifndef MOSAIC_FIXED
+#define MOSAIC_FIXED 1
+#endif
 struct PipeGroup {
+#if MOSAIC_FIXED
+    uint32_t gx[4], gy[4];  // fixed-point fine-cell coordinates (kFixBits fraction bits)
+#else
     float u[4], v[4];     // offset in the sub-block, leaf cells
     uint32_t lf[4];       // leaf cell index within the leaf block
+#endif
     uint32_t tbv[4];      // tile base
     uint32_t qv[4];       // quad-level entry
     uint32_t code[4];     // sub-block entry (gathered), then the answer
@@ -262,6 +272,15 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const bool lv = valid && live[k];
+#if MOSAIC_FIXED
+            // fixed point (tiles::raster_code_fixed): saturating conversion (negative, NaN -> 0), clamp
+            const uint32_t ixC = min(tiles::fix_cvt(fma(x[k], s.sxF, s.gx0F)), (uint32_t)s.gxmaxF);
+            const uint32_t iyC = min(tiles::fix_cvt(fma(y[k], s.syF, s.gy0F)), (uint32_t)s.gymaxF);
+            g.gx[k] = ixC;
+            g.gy[k] = iyC;
+            constexpr int SH0 = tiles::kFixBits;
+#else
+            constexpr int SH0 = 0;
             // (x - x0) sxC as one fma (x sxC - x0 sxC): within the raster's 1e-6-cell widening
             const double gx = fmin(fmax(fma(x[k], s.sxC, gx0), 0.0), s.gxmax);  // NaN -> 0
             const double gy = fmin(fmax(fma(y[k], s.syC, gy0), 0.0), s.gymax);
@@ -270,10 +289,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             g.u[k] = (float)(ixC & cm) + (float)__builtin_amdgcn_fract(gx);
             g.v[k] = (float)(iyC & cm) + (float)__builtin_amdgcn_fract(gy);
             g.lf[k] = ((iyC & cm) << s.cs) | (ixC & cm);
+#endif
 #if MOSAIC_ABL == 1
             const uint32_t q = (ixC ^ iyC) & 7u;  // ablation: no LDS lookups
 #else
-            const uint32_t q = quad_lookup(s, quad, qmask, qcode, ixC, iyC);
+            const uint32_t q = quad_lookup<SH0>(s, quad, qmask, qcode, ixC, iyC);
 #endif
             // dead rows answer 0.  Non-finite coordinates need no test: fmax / fmin clamp them onto
             // the grid's edge ring, whose sub-blocks are all 0 or kMixed (PointRaster edge_ok, a
@@ -283,10 +303,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #if MOSAIC_ABL == 1
             g.tbv[k] = ixC;
 #else
-            g.tbv[k] = tb[__umul24(iyC >> s.tsh, (uint32_t)s.tnx) + (ixC >> s.tsh)];
+            g.tbv[k] = tb[__umul24(iyC >> (s.tsh + SH0), (uint32_t)s.tnx) + (ixC >> (s.tsh + SH0))];
 #endif
-            const uint32_t local = (__builtin_amdgcn_ubfe(iyC, (uint32_t)s.cs, (uint32_t)s.qs) << s.qs) |
-                                   __builtin_amdgcn_ubfe(ixC, (uint32_t)s.cs, (uint32_t)s.qs);
+            const uint32_t local = (__builtin_amdgcn_ubfe(iyC, (uint32_t)(s.cs + SH0), (uint32_t)s.qs) << s.qs) |
+                                   __builtin_amdgcn_ubfe(ixC, (uint32_t)(s.cs + SH0), (uint32_t)s.qs);
             const uint32_t off = ((((g.qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
 #if MOSAIC_ABL == 1 || MOSAIC_ABL == 2
             g.code[k] = off & 1u;  // ablation: no sub-block gathers
@@ -303,7 +323,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const bool blk = c - 0x8000u < 0x7fffu;  // kSubBlock | n, not kMixed
             const bool line = blk && (c & 0x4000u);
             const uint32_t n = c & 0x3fffu;
-            const uint32_t loff = (g.tbv[k] + (n << (2 * s.cs)) + g.lf[k]) << 1;
+#if MOSAIC_FIXED
+            const uint32_t lf = (__builtin_amdgcn_ubfe(g.gy[k], (uint32_t)tiles::kFixBits, (uint32_t)s.cs) << s.cs) |
+                                __builtin_amdgcn_ubfe(g.gx[k], (uint32_t)tiles::kFixBits, (uint32_t)s.cs);
+#else
+            const uint32_t lf = g.lf[k];
+#endif
+            const uint32_t loff = (g.tbv[k] + (n << (2 * s.cs)) + lf) << 1;
             const uint32_t roff = (g.tbv[k] - 8u * (n + 1u)) << 1;
 #if MOSAIC_ABL >= 1 && MOSAIC_ABL <= 3
             g.leaf[k] = loff & 1u;  // ablation: no leaf / line gathers
@@ -322,8 +348,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         uint32_t code[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const float sv = fmaf(__uint_as_float(g.lrec[k].x), g.u[k],
-                                  fmaf(__uint_as_float(g.lrec[k].y), g.v[k], __uint_as_float(g.lrec[k].z)));
+#if MOSAIC_FIXED
+            // the offset in the sub-block, leaf cells, truncated to 2^-kFixBits (exact in f32)
+            const uint32_t fb = (uint32_t)(s.cs + tiles::kFixBits);
+            const float u = (float)__builtin_amdgcn_ubfe(g.gx[k], 0u, fb) * (1.0f / (float)(1 << tiles::kFixBits));
+            const float v = (float)__builtin_amdgcn_ubfe(g.gy[k], 0u, fb) * (1.0f / (float)(1 << tiles::kFixBits));
+#else
+            const float u = g.u[k], v = g.v[k];
+#endif
+            const float sv = fmaf(__uint_as_float(g.lrec[k].x), u,
+                                  fmaf(__uint_as_float(g.lrec[k].y), v, __uint_as_float(g.lrec[k].z)));
             const uint32_t pos = g.lrec[k].w & 0xffffu, neg = g.lrec[k].w >> 16;
             uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
             lc = sv <= -1.0f ? neg : lc;
@@ -377,8 +411,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     for (int k = 0; k < 4; k++) {
         g0.qv[k] = g1.qv[k] = 0u;
         g0.code[k] = g1.code[k] = 0u;
-        g0.tbv[k] = g1.tbv[k] = g0.lf[k] = g1.lf[k] = 0u;
+        g0.tbv[k] = g1.tbv[k] = 0u;
+#if MOSAIC_FIXED
+        g0.gx[k] = g1.gx[k] = g0.gy[k] = g1.gy[k] = 0u;
+#else
+        g0.lf[k] = g1.lf[k] = 0u;
         g0.u[k] = g1.u[k] = g0.v[k] = g1.v[k] = 0.0f;
+#endif
     }
     auto step = [&](int64_t t, PipeGroup& gfin, PipeGroup& gadv, Coords& cb, Coords& cn) {
         const bool all[4] = {true, true, true, true};

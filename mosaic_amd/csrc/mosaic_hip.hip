@@ -1086,9 +1086,15 @@ __global__ void __launch_bounds__(256) k_isect_agg(IsectArgs a) {
 // with several pairs and no (core, core) pair sets the group's status bit (the caller evaluates such
 // groups on the row path); a (core, core) pair's cell is the cell polygon (indexToGeometry, as the
 // reference's getCellGeom): H3 h3ToGeoBoundary in degrees, BNG the cell square.
+// Each (group, cell) piece is written as one record (group slot << 32 | left cell slot, area); the
+// host sums a group's records in (group, cell) order, so the area is the same bits on every run
+// (an atomic float add would sum in the order the waves finish).
 struct IsectAreaArgs {
     IsectArgs base;
-    double* garea;
+    unsigned long long* rkey;
+    double* rarea;
+    unsigned long long* rcount;
+    unsigned long long rcap;
     int grid, jdk;
 };
 
@@ -1217,8 +1223,17 @@ __global__ void __launch_bounds__(256) k_isect_area(IsectAreaArgs x) {
                 }
                 if (area != area) flag = 1;
                 if (lane == 0) {
-                    if (flag) atomicOr(&a.gflag[gs], flag);
-                    else atomicAdd(&x.garea[gs], area);
+                    if (flag) {
+                        atomicOr(&a.gflag[gs], flag);
+                    } else {
+                        const unsigned long long r = atomicAdd(x.rcount, 1ULL);
+                        if (r < x.rcap) {
+                            x.rkey[r] = (gs << 32) | slot;
+                            x.rarea[r] = area;
+                        } else {
+                            atomicOr(a.overflow, 1);
+                        }
+                    }
                 }
             }
     }
@@ -3458,6 +3473,17 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         sa.syC = ch->praster.sy * tb.C;
                         sa.gxmax = (double)ch->praster.nx * tb.C - 1.0;
                         sa.gymax = (double)ch->praster.ny * tb.C - 1.0;
+                        // fixed-point coordinates of k_join_stream_pipe (tiles::raster_code_fixed):
+                        // power-of-two scalings of the same products
+                        const double fs = (double)(1 << tiles::kFixBits);
+                        sa.sxF = sa.sxC * fs;
+                        sa.syF = sa.syC * fs;
+                        sa.gx0F = (-sa.x0 * sa.sxC) * fs;
+                        sa.gy0F = (-sa.y0 * sa.syC) * fs;
+                        sa.fix_ok = ((int64_t)ch->praster.nx * tb.C << tiles::kFixBits) < ((int64_t)1 << 31) &&
+                                    ((int64_t)ch->praster.ny * tb.C << tiles::kFixBits) < ((int64_t)1 << 31);
+                        sa.gxmaxF = sa.fix_ok ? (int32_t)(((int64_t)ch->praster.nx * tb.C - 1) << tiles::kFixBits) : 0;
+                        sa.gymaxF = sa.fix_ok ? (int32_t)(((int64_t)ch->praster.ny * tb.C - 1) << tiles::kFixBits) : 0;
                         sa.cs = tb.cshift;
                         sa.qs = tb.qshift;
                         sa.qsh = tb.cshift + tb.qshift;
@@ -3747,7 +3773,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             auto kernel_for = [&](bool vec) -> const void* {
                 // the pipelined form (k_join_stream_pipe) where it applies
-                return stream_kernel_h3(vec && sa.tb_lds && c->stream_pipe, lds, pairs, vec);
+                return stream_kernel_h3(vec && sa.tb_lds && sa.fix_ok && c->stream_pipe, lds, pairs, vec);
             };
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blk, shm_s) != hipSuccess || per_cu < 1)
@@ -4078,8 +4104,8 @@ int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, con
     a.maskb = right->capacity - 1;
     a.meta_b = (const uint32_t*)right->meta.p;
     a.sb = right->store.view();
-    DevBuf cnt, gkey, gflag, garea, ovf;
-    DevBufGuard guard{{&cnt, &gkey, &gflag, &garea, &ovf}};
+    DevBuf cnt, gkey, gflag, rkey, rarea, ovf;
+    DevBufGuard guard{{&cnt, &gkey, &gflag, &rkey, &rarea, &ovf}};
     int rc;
     if ((rc = cnt.reserve(8)) || (rc = ovf.reserve(4))) return rc;
     HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
@@ -4100,27 +4126,46 @@ int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, con
     if (pairs == 0) return MOSAIC_OK;
     uint64_t gcap = 1024;
     while (gcap < 2 * pairs) gcap <<= 1;
-    if ((rc = gkey.reserve(gcap * 8)) || (rc = gflag.reserve(gcap * 4)) || (rc = garea.reserve(gcap * 8))) return rc;
+    if (gcap > ((uint64_t)1 << 32) || left->capacity > ((uint64_t)1 << 32))
+        return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: too many chip pairs");
+    if ((rc = gkey.reserve(gcap * 8)) || (rc = gflag.reserve(gcap * 4)) || (rc = rkey.reserve(pairs * 8)) ||
+        (rc = rarea.reserve(pairs * 8)))
+        return rc;
     HIP_TRY(hipMemsetAsync(gkey.p, 0xff, gcap * 8, c->stream));
     HIP_TRY(hipMemsetAsync(gflag.p, 0, gcap * 4, c->stream));
-    HIP_TRY(hipMemsetAsync(garea.p, 0, gcap * 8, c->stream));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
     a.pass = 1;
     a.gkey = (unsigned long long*)gkey.p;
     a.gflag = (uint32_t*)gflag.p;
     a.gmask = gcap - 1;
-    IsectAreaArgs x{a, (double*)garea.p, left->grid, c->jdk};
+    // (pieces <= chip pairs: the record buffer cannot overflow)
+    IsectAreaArgs x{a, (unsigned long long*)rkey.p, (double*)rarea.p, (unsigned long long*)cnt.p, pairs, left->grid, c->jdk};
     hipLaunchKernelGGL(k_isect_area, dim3(grid), dim3(256), 0, c->stream, x);
     HIP_TRY(hipGetLastError());
     std::vector<unsigned long long> hk(gcap);
     std::vector<uint32_t> hf(gcap);
-    std::vector<double> ha(gcap);
     int hov = 0;
+    unsigned long long nrec = 0;
     HIP_TRY(hipMemcpyAsync(hk.data(), gkey.p, gcap * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(hf.data(), gflag.p, gcap * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(ha.data(), garea.p, gcap * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&nrec, cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&hov, ovf.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (hov) return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: group table overflow");
+    if (hov || nrec > pairs) return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: group table overflow");
+    std::vector<std::pair<unsigned long long, double>> rec(nrec);
+    {
+        std::vector<unsigned long long> rk(nrec);
+        std::vector<double> ra(nrec);
+        HIP_TRY(hipMemcpyAsync(rk.data(), rkey.p, nrec * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(ra.data(), rarea.p, nrec * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (size_t i = 0; i < nrec; i++) rec[i] = {rk[i], ra[i]};
+    }
+    // per group, its pieces summed in cell-slot order: the same bits on every run
+    std::sort(rec.begin(), rec.end(), [](const std::pair<unsigned long long, double>& p,
+                                         const std::pair<unsigned long long, double>& q) { return p.first < q.first; });
+    std::vector<double> ha(gcap, 0.0);
+    for (const auto& r : rec) ha[r.first >> 32] += r.second;
     std::vector<std::pair<unsigned long long, uint64_t>> groups;
     for (uint64_t s = 0; s < gcap; s++)
         if (hk[s] != kEmptyGroup) groups.push_back({hk[s], s});

@@ -14,8 +14,9 @@
 //     Hexagon edges are densified (H3 cell edges are great-circle arcs; straight lon/lat chords
 //     would leave slivers).  Cell ids are _faceIjkToH3 of the lattice cell (h3_device.h).
 //   * BNG: cells are axis-aligned squares in the native plane; same clipping.
-// Host-only (not the hot path; §8(f) row 1 lists the GPU producer as next).  Supports polygons
-// that lie on one icosahedron face (true for the NYC / London fixtures); others are rejected.
+// Polygons spanning icosahedron faces are cut into per-face pieces (tessellate_h3_multiface); the
+// GPU producer (mosaic_tessellate_gpu) classifies and clips single-face geometries on the device and
+// runs the same host routine for face-spanning ones, so both give the same chip set.
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -241,20 +242,14 @@ struct Cell {
     std::vector<P2> outline;  // densified outline in the plane for core chip output
 };
 
-// Classify one cell against one geometry given in the plane (plane rings + original lon/lat rings).
-// to_geo maps a plane point to output coordinates.
-template <class ToGeo>
-void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::vector<std::vector<std::vector<P2>>>& pl,
-               const std::vector<std::vector<std::vector<P2>>>& geo, double core_eps, int keep_core_geom,
-               ToGeo to_geo, double area_eps, int pre = -1) {
+// The class of one cell (convex clip region) for one geometry given in the plane: 0 disjoint (or in a
+// hole), 1 core (no polygon segment within core_eps, centre inside), 2 border.
+int classify_cell(const Cell& cell, const std::vector<std::vector<std::vector<P2>>>& pl, double core_eps) {
     // 1) any polygon segment near the cell?  2) cell centre inside?
-    // pre >= 0: the class was computed on the GPU (k_bng_tess_classify: 0 dropped, 1 core, 2 border)
-    if (pre == 0) return;
-    bool near = pre == 2;
-    for (size_t pi = 0; pre < 0 && pi < pl.size() && !near; pi++)
+    for (size_t pi = 0; pi < pl.size(); pi++)
         for (auto& ring : pl[pi])
-            for (size_t i = 0; i + 1 < ring.size() && !near; i++)
-                if (seg_near_convex(ring[i], ring[i + 1], cell.clip, core_eps)) near = true;
+            for (size_t i = 0; i + 1 < ring.size(); i++)
+                if (seg_near_convex(ring[i], ring[i + 1], cell.clip, core_eps)) return 2;
     P2 c = {0, 0};
     for (auto& p : cell.clip) {
         c.x += p.x;
@@ -262,22 +257,26 @@ void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::ve
     }
     c.x /= cell.clip.size();
     c.y /= cell.clip.size();
-    if (!near) {
-        bool inside = pre == 1;
-        for (size_t pi = 0; pre < 0 && pi < pl.size(); pi++) inside = inside || point_in_rings_evenodd(c, pl[pi]);
-        if (!inside) return;  // disjoint (or inside a hole)
-        std::vector<uint8_t> blob;
-        if (keep_core_geom) {
-            std::vector<P2> ring;
-            for (auto& p : cell.outline) ring.push_back(to_geo(p));
-            ring.push_back(ring.front());
-            blob = to_wkb({{ring}});
-        }
-        cs->add(true, cell.id, key, blob);
-        return;
-    }
-    // border: clip every ring against the cell
-    std::vector<std::vector<std::vector<P2>>> out_parts;
+    bool inside = false;
+    for (size_t pi = 0; pi < pl.size(); pi++) inside = inside || point_in_rings_evenodd(c, pl[pi]);
+    return inside ? 1 : 0;
+}
+
+// A core cell's outline mapped to output coordinates, closed.
+template <class ToGeo>
+std::vector<P2> cell_ring(const Cell& cell, ToGeo to_geo) {
+    std::vector<P2> ring;
+    for (auto& p : cell.outline) ring.push_back(to_geo(p));
+    ring.push_back(ring.front());
+    return ring;
+}
+
+// Border cell: every ring of the geometry clipped against the cell, appended to out_parts (polygon
+// parts, shells first); original vertices kept exact, computed ones mapped by to_geo.
+template <class ToGeo>
+void clip_cell(const Cell& cell, const std::vector<std::vector<std::vector<P2>>>& pl,
+               const std::vector<std::vector<std::vector<P2>>>& geo, ToGeo to_geo, double area_eps,
+               std::vector<std::vector<std::vector<P2>>>& out_parts) {
     std::vector<P2> a, b;
     std::vector<long> ta, tb;
     for (size_t pi = 0; pi < pl.size(); pi++) {
@@ -315,8 +314,251 @@ void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::ve
         }
         if (!rings_out.empty() && net > area_eps) out_parts.push_back(std::move(rings_out));
     }
+}
+
+// Classify one cell against one geometry given in the plane (plane rings + original lon/lat rings)
+// and emit its chip.  to_geo maps a plane point to output coordinates.
+template <class ToGeo>
+void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::vector<std::vector<std::vector<P2>>>& pl,
+               const std::vector<std::vector<std::vector<P2>>>& geo, double core_eps, int keep_core_geom,
+               ToGeo to_geo, double area_eps, int pre = -1) {
+    // pre >= 0: the class was computed on the GPU (k_bng_tess_classify: 0 dropped, 1 core, 2 border)
+    const int cls = pre >= 0 ? pre : classify_cell(cell, pl, core_eps);
+    if (cls == 0) return;
+    if (cls == 1) {
+        std::vector<uint8_t> blob;
+        if (keep_core_geom) blob = to_wkb({{cell_ring(cell, to_geo)}});
+        cs->add(true, cell.id, key, blob);
+        return;
+    }
+    std::vector<std::vector<std::vector<P2>>> out_parts;
+    clip_cell(cell, pl, geo, to_geo, area_eps, out_parts);
     if (out_parts.empty()) return;
     cs->add(false, cell.id, key, to_wkb(out_parts));
+}
+
+// ---- H3 polygons that span icosahedron faces ----
+// geoToH3 projects a point onto its closest face (largest fc . p) and rounds in that face's
+// gnomonic plane, so a cell is, on the sphere, the union over faces f of (hexagon of its lattice
+// position on f) n territory(f), where territory(f) = {p : fc_f . p >= fc_g . p for every g} is the
+// face's spherical triangle, a straight-edged triangle in f's gnomonic plane (the three bisector
+// planes (fc_f - fc_g) . p = 0 of its edge neighbours g).  Per face f whose territory meets the
+// polygon, candidate lattice cells are clipped to the triangle; face_ijk_to_h3(f, ijk) is H3's id of
+// the points of that piece (what _faceIjkToH3 computes for them).  A cell's pieces are then merged:
+// core when every piece is core, else a border chip holding the core pieces' outlines and the
+// border pieces' clips (a MultiPolygon whose parts meet along the face edge).
+struct FaceTerritory {
+    double A[3], B[3], C[3];  // A x + B y + C >= 0 in the face plane (hex2d units at res)
+    void init(int f, const FacePlane& fp) {
+        const double* fc = h3::kH3FastBasis[f];
+        int nb[3] = {-1, -1, -1};
+        double nd[3] = {-2, -2, -2};
+        for (int g = 0; g < 20; g++) {  // the three edge neighbours: the closest face centres
+            if (g == f) continue;
+            const double* fg = h3::kH3FastBasis[g];
+            double d = fc[0] * fg[0] + fc[1] * fg[1] + fc[2] * fg[2];
+            for (int q = 0; q < 3; q++)
+                if (d > nd[q]) {
+                    for (int r = 2; r > q; r--) {
+                        nd[r] = nd[r - 1];
+                        nb[r] = nb[r - 1];
+                    }
+                    nd[q] = d;
+                    nb[q] = g;
+                    break;
+                }
+        }
+        for (int q = 0; q < 3; q++) {
+            const double* fg = h3::kH3FastBasis[nb[q]];
+            double w[3] = {fc[0] - fg[0], fc[1] - fg[1], fc[2] - fg[2]};
+            // p ~ fc + (x ei + y ep) / S
+            C[q] = w[0] * fc[0] + w[1] * fc[1] + w[2] * fc[2];
+            A[q] = (w[0] * fp.ei[0] + w[1] * fp.ei[1] + w[2] * fp.ei[2]) / fp.S;
+            B[q] = (w[0] * fp.ep[0] + w[1] * fp.ep[1] + w[2] * fp.ep[2]) / fp.S;
+        }
+    }
+    // the triangle's corners (pairwise intersections of its edge lines)
+    void corners(P2 out[3]) const {
+        for (int q = 0; q < 3; q++) {
+            const int a = (q + 1) % 3, b = (q + 2) % 3;
+            const double det = A[a] * B[b] - A[b] * B[a];
+            out[q] = {(-C[a] * B[b] + C[b] * B[a]) / det, (-A[a] * C[b] + A[b] * C[a]) / det};
+        }
+    }
+};
+
+// keep A x + B y + C >= 0 of a convex (open) polygon
+void clip_halfplane(const std::vector<P2>& in, double A, double B, double C, std::vector<P2>& out) {
+    out.clear();
+    const size_t n = in.size();
+    for (size_t i = 0; i < n; i++) {
+        const P2 cur = in[i], prev = in[(i + n - 1) % n];
+        const double sc = A * cur.x + B * cur.y + C, sp = A * prev.x + B * prev.y + C;
+        if (sc >= 0) {
+            if (sp < 0) {
+                const double t = sp / (sp - sc);
+                out.push_back({prev.x + t * (cur.x - prev.x), prev.y + t * (cur.y - prev.y)});
+            }
+            out.push_back(cur);
+        } else if (sp >= 0) {
+            const double t = sp / (sp - sc);
+            out.push_back({prev.x + t * (cur.x - prev.x), prev.y + t * (cur.y - prev.y)});
+        }
+    }
+}
+
+double open_area(const std::vector<P2>& r) {
+    double a = 0;
+    for (size_t i = 0; i < r.size(); i++) {
+        const P2 p = r[i], q = r[(i + 1) % r.size()];
+        a += p.x * q.y - q.x * p.y;
+    }
+    return 0.5 * a;
+}
+
+// Chips of geometry g (lon/lat rings geo) that spans faces: 0, or MOSAIC_E_ARG for geometries no
+// face plane can hold (a vertex more than ~78 degrees from a face centre whose territory it meets).
+int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, int keep_core_geom,
+                            const std::vector<std::vector<std::vector<P2>>>& geo) {
+    struct Piece {
+        int face, cls;
+        Cell cell;
+        std::vector<std::vector<std::vector<P2>>> parts;  // border: the clipped geometry
+    };
+    std::vector<int64_t> order;  // cell ids in first-seen order (faces ascending, lattice order)
+    std::vector<std::vector<Piece>> pieces;
+    std::vector<std::pair<int64_t, size_t>> index;  // id -> slot (sorted at the end of each face)
+    auto slot_of = [&](int64_t id) -> size_t {
+        for (auto& e : index)
+            if (e.first == id) return e.second;
+        index.push_back({id, order.size()});
+        order.push_back(id);
+        pieces.emplace_back();
+        return order.size() - 1;
+    };
+    const double s60 = 0.86602540378443864676, R = 0.57735026918962576451;
+    int faces_used = 0;
+    for (int f = 0; f < 20; f++) {
+        FacePlane fp;
+        fp.init(f, res);
+        const double* fc = fp.fc;
+        // the gnomonic projection must hold every vertex (fc . p >= 0.2, ~78 degrees)
+        bool valid = true;
+        for (auto& part : geo)
+            for (auto& ring : part)
+                for (auto& p : ring) {
+                    double u[3];
+                    FacePlane::unit(p.x, p.y, u);
+                    if (fc[0] * u[0] + fc[1] * u[1] + fc[2] * u[2] < 0.2) valid = false;
+                }
+        FaceTerritory ft;
+        ft.init(f, fp);
+        std::vector<std::vector<std::vector<P2>>> pl = geo;
+        for (auto& part : pl)
+            for (auto& ring : part)
+                for (auto& p : ring) p = fp.to_hex(p.x, p.y);
+        // does the territory meet the geometry? (the shells clipped to the triangle keep area)
+        double met = 0;
+        if (valid) {
+            std::vector<P2> a, b;
+            for (auto& part : pl) {
+                if (part.empty() || part[0].size() < 4) continue;
+                a.assign(part[0].begin(), part[0].end() - 1);
+                for (int q = 0; q < 3 && !a.empty(); q++) {
+                    clip_halfplane(a, ft.A[q], ft.B[q], ft.C[q], b);
+                    a.swap(b);
+                }
+                if (a.size() >= 3) met += fabs(open_area(a));
+            }
+        } else {
+            // refuse only when the geometry could reach this face: some vertex on it
+            for (auto& part : geo)
+                for (auto& ring : part)
+                    for (auto& p : ring)
+                        if (face_of(p.x, p.y) == f) return MOSAIC_E_ARG;
+            continue;
+        }
+        if (!(met > 1e-12)) continue;
+        faces_used++;
+        P2 tc[3];
+        ft.corners(tc);
+        double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
+        for (auto& part : pl)
+            for (auto& ring : part)
+                for (auto& p : ring) {
+                    x0 = std::min(x0, p.x);
+                    x1 = std::max(x1, p.x);
+                    y0 = std::min(y0, p.y);
+                    y1 = std::max(y1, p.y);
+                }
+        double tx0 = std::min(tc[0].x, std::min(tc[1].x, tc[2].x)), tx1 = std::max(tc[0].x, std::max(tc[1].x, tc[2].x));
+        double ty0 = std::min(tc[0].y, std::min(tc[1].y, tc[2].y)), ty1 = std::max(tc[0].y, std::max(tc[1].y, tc[2].y));
+        x0 = std::max(x0, tx0);
+        x1 = std::min(x1, tx1);
+        y0 = std::max(y0, ty0);
+        y1 = std::min(y1, ty1);
+        if (x0 > x1 || y0 > y1) continue;
+        int jlo = (int)floor(y0 / s60) - 2, jhi = (int)ceil(y1 / s60) + 2;
+        std::vector<P2> hex, tmp;
+        for (int j = jlo; j <= jhi; j++) {
+            int ilo = (int)floor(x0 + j * 0.5) - 2, ihi = (int)ceil(x1 + j * 0.5) + 2;
+            for (int i = ilo; i <= ihi; i++) {
+                double cx = i - 0.5 * j, cy = j * s60;
+                if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
+                P2 corners[6];
+                for (int k = 0; k < 6; k++) {
+                    double ang = (30.0 + 60.0 * k) * (M_PI / 180.0);
+                    corners[k] = {cx + R * cos(ang), cy + R * sin(ang)};
+                }
+                hex.clear();
+                for (int k = 0; k < 6; k++) {
+                    P2 a = corners[k], b = corners[(k + 1) % 6];
+                    for (int t = 0; t < D; t++) hex.push_back({a.x + (b.x - a.x) * t / D, a.y + (b.y - a.y) * t / D});
+                }
+                // the piece of the cell on this face
+                for (int q = 0; q < 3 && !hex.empty(); q++) {
+                    clip_halfplane(hex, ft.A[q], ft.B[q], ft.C[q], tmp);
+                    hex.swap(tmp);
+                }
+                if (hex.size() < 3 || !(fabs(open_area(hex)) > 1e-9)) continue;
+                h3::IJK ijk = {i, j, 0};
+                h3::ijk_normalize(ijk);
+                const int64_t id = (int64_t)h3::face_ijk_to_h3(f, ijk, res);
+                if (id == 0) return MOSAIC_E_ARG;  // (a lattice cell H3 has no id for: not expected)
+                Piece pc;
+                pc.face = f;
+                pc.cell.id = id;
+                pc.cell.clip = hex;
+                pc.cell.outline = hex;
+                pc.cls = classify_cell(pc.cell, pl, 1e-3);
+                if (pc.cls == 2) clip_cell(pc.cell, pl, geo, [&](P2 h) { return fp.to_geo(h); }, 1e-12, pc.parts);
+                pieces[slot_of(id)].push_back(std::move(pc));
+            }
+        }
+    }
+    if (faces_used == 0) return MOSAIC_OK;
+    for (size_t k = 0; k < order.size(); k++) {
+        const std::vector<Piece>& ps = pieces[k];
+        bool all_core = true, any = false;
+        for (const Piece& p : ps) {
+            all_core = all_core && p.cls == 1;
+            any = any || p.cls == 1 || (p.cls == 2 && !p.parts.empty());
+        }
+        if (!any) continue;
+        std::vector<std::vector<std::vector<P2>>> parts;
+        for (const Piece& p : ps) {
+            if (p.cls == 1 && (keep_core_geom || !all_core)) {
+                FacePlane fp;
+                fp.init(p.face, res);
+                parts.push_back({cell_ring(p.cell, [&](P2 h) { return fp.to_geo(h); })});
+            } else if (p.cls == 2) {
+                for (auto& q : p.parts) parts.push_back(q);
+            }
+        }
+        if (all_core) cs->add(true, order[k], key, keep_core_geom ? to_wkb(parts) : std::vector<uint8_t>());
+        else if (!parts.empty()) cs->add(false, order[k], key, to_wkb(parts));
+    }
+    return MOSAIC_OK;
 }
 
 // The border chips the GPU clipped (tess_gpu.h), indexed by candidate: rings sorted by (candidate,
@@ -395,17 +637,22 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
         if (!any) continue;
         if (grid == MOSAIC_GRID_H3) {
             int face = -1;
+            bool multi = false;
             for (auto& part : geo)
                 for (auto& ring : part)
                     for (auto& p : ring) {
                         int f = face_of(p.x, p.y);
                         if (face < 0) face = f;
-                        if (f != face) {
-                            delete cs;
-                            return mosaic_tess_fail(MOSAIC_E_ARG, "geometry spans an icosahedron face edge "
-                                                                  "(unsupported by the host tessellator)");
-                        }
+                        multi = multi || f != face;
                     }
+            if (multi) {  // cells on several faces: per-face pieces (tessellate_h3_multiface)
+                if (tessellate_h3_multiface(cs, (int32_t)g, res, D, keep_core_geom, geo)) {
+                    delete cs;
+                    return mosaic_tess_fail(MOSAIC_E_ARG, "geometry too large for a gnomonic face plane "
+                                                          "(a vertex more than 78 degrees from a face centre it meets)");
+                }
+                continue;
+            }
             FacePlane fp;
             fp.init(face, res);
             std::vector<std::vector<std::vector<P2>>> pl = geo;
@@ -496,6 +743,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     std::vector<int32_t> cg;
     std::vector<double> cxy;  // candidate hexagon centres in the face plane
     std::vector<int64_t> cid;
+    std::vector<int64_t> multi_geoms;  // geometries spanning icosahedron faces
     const double s60 = 0.86602540378443864676, R = 0.57735026918962576451;
     // candidate k's (densified) hexagon clip polygon, nv points: the host producer's arithmetic
     auto fill_clip = [&](int64_t k, double* out_pts) {
@@ -518,12 +766,15 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         const int64_t v0 = ring_offsets[part_rings[geom_parts[g]]], v1 = ring_offsets[part_rings[geom_parts[g + 1]]];
         if (v0 == v1) continue;
         int face = -1;
+        bool multi = false;
         for (int64_t v = v0; v < v1; v++) {
             int f = face_of(xy[2 * v], xy[2 * v + 1]);
             if (face < 0) face = f;
-            if (f != face)
-                return mosaic_tess_fail(MOSAIC_E_ARG, "geometry spans an icosahedron face edge "
-                                                      "(unsupported by the host tessellator)");
+            multi = multi || f != face;
+        }
+        if (multi) {  // spans faces: the host's per-face pieces (tessellate_h3_multiface), in geometry order
+            multi_geoms.push_back(g);
+            continue;
         }
         gface[g] = face;
         FacePlane fp;
@@ -566,6 +817,27 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     fp.init(0, res);  // re-initialised per geometry below
     int64_t cur = -1;
     std::vector<uint8_t> blob;
+    // the face-spanning geometries before geometry `upto`, emitted where the host producer emits them
+    size_t next_multi = 0;
+    auto flush_multi = [&](int64_t upto) -> int {
+        for (; next_multi < multi_geoms.size() && multi_geoms[next_multi] < upto; next_multi++) {
+            const int64_t g = multi_geoms[next_multi];
+            std::vector<std::vector<std::vector<P2>>> mg;
+            for (int64_t p = geom_parts[g]; p < geom_parts[g + 1]; p++) {
+                std::vector<std::vector<P2>> rings;
+                for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
+                    std::vector<P2> ring;
+                    for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) ring.push_back({xy[2 * v], xy[2 * v + 1]});
+                    rings.push_back(std::move(ring));
+                }
+                mg.push_back(std::move(rings));
+            }
+            if (tessellate_h3_multiface(cs, (int32_t)g, res, D, keep_core_geom, mg))
+                return mosaic_tess_fail(MOSAIC_E_ARG, "geometry too large for a gnomonic face plane "
+                                                      "(a vertex more than 78 degrees from a face centre it meets)");
+        }
+        return MOSAIC_OK;
+    };
     for (int64_t k0 = 0; k0 < n_cand; k0 += chunk) {
         const int64_t nc = std::min<int64_t>(chunk, n_cand - k0);
         clip.resize((size_t)nc * nv * 2);
@@ -591,6 +863,10 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         cc.index(nc, tasks);
         for (int64_t kk = 0; kk < nc; kk++) {
             const int64_t k = k0 + kk;
+            if (!multi_geoms.empty() && (rc = flush_multi(cg[k]))) {
+                delete cs;
+                return rc;
+            }
             if (!cls[kk]) continue;
             if (cls[kk] == 2 && !cc.redo(kk)) {
                 if (cc.chip(kk, blob)) cs->add(false, cid[k], cg[k], blob);
@@ -624,6 +900,10 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             emit_cell(cs, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); }, 1e-12,
                       (int)cls[kk]);
         }
+    }
+    if (int rc = flush_multi(n_geoms)) {
+        delete cs;
+        return rc;
     }
     *out = cs;
     return MOSAIC_OK;

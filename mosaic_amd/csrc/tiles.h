@@ -145,6 +145,56 @@ MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, doubl
     return r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
 }
 
+// Fixed-point fine-cell coordinates (k_join_stream_pipe): gi = floor(g 2^kFixBits) with g the
+// fine-cell coordinate, computed as the saturating conversion of fma(x, sxC 2^F, -x0 sxC 2^F) (a
+// power-of-two scaling of the kernel's fma(x, sxC, -x0 sxC): the same rounding, so floor(gi / 2^F)
+// is the same leaf cell; negative and NaN -> 0) clamped to gmax 2^F.  The line test then sees the point's offset
+// truncated to 2^-F leaf cells (< 2^-16 sub-blocks per axis with C = 16): far inside the
+// kLineSlack sub-block units the line records are certified with.  Needs (N C) 2^F < 2^31.
+static const int kFixBits = 12;
+MOSAIC_HD uint32_t fix_cvt(double v) {  // v_cvt_u32_f64: saturating (negative and NaN -> 0)
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    __asm__("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+#else
+    if (!(v > 0.0)) return 0u;
+    if (v >= 4294967295.0) return 4294967295u;
+    return (uint32_t)v;
+#endif
+}
+// the host statement of k_join_stream_pipe's lookup (quad level, compact copies, leaf blocks and line
+// records with fixed-point offsets); ax = sxC 2^F, bx = -x0 sxC 2^F (likewise y), gmax = (N C - 1) 2^F
+MOSAIC_HD uint16_t raster_code_fixed(const PointRaster& r, double ax, double bx, double ay, double by, uint32_t gxmax,
+                                     uint32_t gymax, double x, double y) {
+    const int F = kFixBits;
+    uint32_t gix = fix_cvt(fma(x, ax, bx)), giy = fix_cvt(fma(y, ay, by));
+    gix = gix > gxmax ? gxmax : gix;
+    giy = giy > gymax ? gymax : giy;
+    const int cm = (1 << r.cshift) - 1;
+    const int ixC = gix >> F, iyC = giy >> F, ix = ixC >> r.cshift, iy = iyC >> r.cshift;
+    uint32_t q = r.quad[(uint32_t)(iy >> r.qshift) * (uint32_t)r.qnx + (uint32_t)(ix >> r.qshift)];
+    if (q >= kSubBlock && (q & 0x7fffu) < (uint32_t)r.n_qrec) {
+        const uint32_t rr = q & 0x7fffu;
+        const uint32_t b = (uint32_t)((((iy >> r.qrec_shift) & 7) << 3) | ((ix >> r.qrec_shift) & 7));
+        if ((r.qrec_mask[2 * rr + (b >> 5)] >> (b & 31)) & 1u) q = r.qrec_code[rr];
+    }
+    const int qm = (1 << r.qshift) - 1;
+    const uint32_t e = q < kSubBlock ? q
+                                     : r.sub[(size_t)r.nx * r.ny + ((size_t)(q & 0x7fffu) << (2 * r.qshift)) +
+                                             (size_t)(((iy & qm) << r.qshift) | (ix & qm))];
+    if (!sub_is_block(e)) return (uint16_t)e;
+    const size_t base = r.tile_base[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)];
+    const uint32_t n = e & 0x3fffu;
+    if (e & kLineBit) {
+        const uint32_t fm = (1u << (r.cshift + F)) - 1u;
+        const float sc = 1.0f / (float)(1 << F);
+        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)((uint32_t)gix & fm) * sc,
+                         (float)((uint32_t)giy & fm) * sc);
+    }
+    return r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
+}
+
 struct TileRec {
     int32_t a0, b0;  // window origin (axial)
     uint32_t off;    // first window entry

@@ -185,10 +185,8 @@ def synthetic_buildings(n, seed=SEED_BASE + 4, bbox=NYC_BBOX, n_centres=None, si
     ro[1:] = np.cumsum(sizes)
     xy = np.empty((int(ro[-1]), 2))
     pr, pl = place(rect, ri), place(lsh, li)
-    for k, g in enumerate(ri):
-        xy[ro[g]:ro[g + 1]] = pr[k]
-    for k, g in enumerate(li):
-        xy[ro[g]:ro[g + 1]] = pl[k]
+    xy[(ro[ri][:, None] + np.arange(5)).ravel()] = pr.reshape(-1, 2)
+    xy[(ro[li][:, None] + np.arange(7)).ravel()] = pl.reshape(-1, 2)
     idx = np.arange(n + 1, dtype=np.int64)
     return PolygonSet(xy, ro, idx, idx)
 

@@ -127,7 +127,7 @@ int main(int argc, char** argv) {
         pr.qrec_shift = tb.qrec_shift;
         fprintf(stderr, "quad level %d x %d shift %d, %d quad records\n", tb.qnx, tb.qny, tb.qshift, pr.n_qrec);
     }
-    long rbad = 0, rpure = 0, rmixed = 0, uni = 0, uni_mixed = 0;
+    long rbad = 0, rpure = 0, rfpure = 0, rmixed = 0, uni = 0, uni_mixed = 0;
     double bx0 = argc > 9 ? atof(argv[6]) : 0, by0 = argc > 9 ? atof(argv[7]) : 0;
     double bx1 = argc > 9 ? atof(argv[8]) : 0, by1 = argc > 9 ? atof(argv[9]) : 0;
     long st_out = 0, st_skip = 0, st_sub = 0, st_quad = 0;
@@ -178,20 +178,33 @@ int main(int argc, char** argv) {
                 rbad++;
                 if (rbad < 10) fprintf(stderr, "quad lookup: %u vs %u\n", rq, rc);
             }
-            if (rc == tiles::kMixed) {
+            // k_join_stream_pipe's fixed-point form: every pure code it gives is the exact answer too
+            const double fs = (double)(1 << tiles::kFixBits), sxC = pr.sx * pr.C, syC = pr.sy * pr.C;
+            const uint16_t rf = !pr.quad ? (uint16_t)tiles::kMixed : tiles::raster_code_fixed(
+                pr, sxC * fs, (-g.x0 * sxC) * fs, syC * fs, (-g.y0 * syC) * fs,
+                (uint32_t)(((int64_t)pr.nx * pr.C - 1) << tiles::kFixBits), (uint32_t)(((int64_t)pr.ny * pr.C - 1) << tiles::kFixBits),
+                x, y);
+            if (rf != tiles::kMixed) rfpure++;
+            if (rc == tiles::kMixed && rf == tiles::kMixed) {
                 rmixed++;
             } else {
-                rpure++;
+                if (rc != tiles::kMixed) rpure++;
                 std::vector<int32_t> keys;
                 if (want_slot >= 0)
                     for (uint32_t c = slot_first[want_slot]; c < slot_first[want_slot] + slot_count[want_slot]; c++)
                         if ((meta[c] & 1u) || pip::contains(src.store, c, x, y)) keys.push_back((int32_t)(meta[c] >> 1));
                 uint16_t wc = keys.empty() ? 0 : (keys.size() == 1 ? (uint16_t)(keys[0] + 1) : tiles::kMixed);
-                if (wc != rc) {
+                if (rc != tiles::kMixed && wc != rc) {
                     rbad++;
                     if (rbad < 10)
                         fprintf(stderr, "raster: %.17g %.17g code %u want %u (cell %llx)\n", x, y, rc, wc,
                                 (unsigned long long)want);
+                }
+                if (rf != tiles::kMixed && wc != rf) {
+                    rbad++;
+                    if (rbad < 10)
+                        fprintf(stderr, "raster (fixed point): %.17g %.17g code %u want %u (cell %llx)\n", x, y, rf,
+                                wc, (unsigned long long)want);
                 }
             }
         }
@@ -274,6 +287,7 @@ int main(int argc, char** argv) {
         rbad++;
         fprintf(stderr, "an edge sub-block answers a pair\n");
     }
+    fprintf(stderr, "pure codes: float form %ld, fixed-point form %ld\n", rpure, rfpure);
     printf("1 %ld %ld %ld %ld %ld %ld %d %ld %ld %ld\n", bad, checked, skipped, full, unc, miss, rok ? 1 : 0, rbad, rpure,
            rmixed);
     if (uni) fprintf(stderr, "uniform over bbox: %ld points, %.4f mixed\n", uni, (double)uni_mixed / uni);

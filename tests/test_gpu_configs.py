@@ -9,6 +9,14 @@
   (sigma 0.002 deg) -- counts equal the oracle's.
 * C4 shape at scale: 1e6 OSM-style buildings chipped at H3 res 11 (~2.4 M chips), 1e7 points
   (70 % near buildings) -- counts equal the oracle's.
+Full size (VERDICT r2 "full-size checks"), each the raster / dense-table path against the generic
+path (tile directory and point raster off) on every point plus the oracle on a prefix:
+* C3: 1e9 clustered device points (80 % around 32 zone centres, sigma 0.002 deg), all 263 zones at
+  H3 res 10; oracle on the first 1e8.
+* C5: 1e9 uniform points over the 177 London postcode zones in EPSG:27700, BNG res 4 (dense cell
+  table + LDS cell level + line records); oracle on the first 1e8.
+* C4: 5e6 buildings chipped at H3 res 11, 2.5e8 points (70 % within 25 m of a building); oracle on
+  the first 1e7 (reference: notebooks/examples/python/QuickstartNotebook.py:207-219).
 Runs on the MI355X box only.
 """
 import numpy as np
@@ -104,4 +112,112 @@ def test_c4_million_buildings_vs_oracle(h3ctx):
     want, total = oracle.pip_join(chips_to_oracle(chips), oracle.GRID_H3, 11, x, y, nb, threads=16)
     assert total > 1_000_000
     assert np.array_equal(got, want)
+    table.close()
+
+
+def _fast_vs_generic(ctx, table, x, y):
+    """Counts of the default path and of the generic path (tile directory / dense table and point
+    raster off: hash probe + per-chip rasters) on the same device points."""
+    fast = ctx.pip_join_count(table, x, y).cpu().numpy()
+    try:
+        ctx.set_option("tiles", 0)
+        ctx.set_option("point_raster", 0)
+        generic = ctx.pip_join_count(table, x, y).cpu().numpy()
+    finally:
+        ctx.set_option("tiles", 1)
+        ctx.set_option("point_raster", 1)
+    return fast, generic
+
+
+def _oracle_prefix(ctx, table, chips, grid, res, x, y, m, n_polygons):
+    import torch
+
+    got = ctx.pip_join_count(table, x[:m], y[:m]).cpu().numpy()
+    hx, hy = x[:m].cpu().numpy(), y[:m].cpu().numpy()
+    torch.cuda.empty_cache()
+    want, total = oracle.pip_join(chips_to_oracle(chips), grid, res, hx, hy, n_polygons, threads=16)
+    return got, want, total
+
+
+def test_c3_full_size_clustered_res10(h3ctx, zones):
+    import torch
+
+    from mosaic_amd.data import SEED_BASE, clustered_points_device
+
+    chips = h3ctx.grid_tessellateexplode(zones, 10)
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 10,
+                             n_polygons=len(zones))
+    t = table.tiles()
+    assert t["raster"] == 1 and t["stream"] == 1, t
+    n = 1_000_000_000
+    x, y = clustered_points_device(zones, n, seed=SEED_BASE + 3, sigma=0.002, device=torch.device("cuda:0"))
+    fast, generic = _fast_vs_generic(h3ctx, table, x, y)
+    assert fast.sum() > 5e8
+    assert np.array_equal(fast, generic)
+    got, want, total = _oracle_prefix(h3ctx, table, chips, oracle.GRID_H3, 10, x, y, 100_000_000, len(zones))
+    del x, y
+    torch.cuda.empty_cache()
+    assert total > 5e7 and np.array_equal(got, want)
+    table.close()
+
+
+def test_c5_full_size_bng_res4():
+    import torch
+
+    from mosaic_amd.context import tessellate
+    from mosaic_amd.data import uniform_points_device
+
+    proj = PolygonSet.load("london_postcodes_bng")
+    assert len(proj) == 177
+    ctx = MosaicContext.build("BNG")
+    try:
+        chips = tessellate("BNG", proj, 4)
+        table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 4,
+                               n_polygons=len(proj))
+        assert table.tiles()["built"] == 1
+        n = 1_000_000_000
+        x, y = uniform_points_device(proj.bbox(), n, seed=5, device=torch.device("cuda:0"))
+        fast, generic = _fast_vs_generic(ctx, table, x, y)
+        assert fast.sum() > 3e8
+        assert np.array_equal(fast, generic)
+        got, want, total = _oracle_prefix(ctx, table, chips, oracle.GRID_BNG, 4, x, y, 100_000_000, len(proj))
+        del x, y
+        torch.cuda.empty_cache()
+        assert total > 3e7 and np.array_equal(got, want)
+        table.close()
+    finally:
+        ctx.close()
+
+
+def test_c4_full_size_five_million_buildings(h3ctx):
+    import time
+
+    import torch
+
+    from mosaic_amd.data import building_points_device, synthetic_buildings
+
+    nb = 5_000_000
+    b = synthetic_buildings(nb, bbox=(-74.05, 40.60, -73.80, 40.85), n_centres=320, sigma=0.02)
+    t0 = time.perf_counter()
+    chips = h3ctx.grid_tessellateexplode(b, 11)
+    t_tess = time.perf_counter() - t0
+    assert len(chips["index_id"]) > 7_500_000
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    t0 = time.perf_counter()
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 11,
+                             n_polygons=nb)
+    t_table = time.perf_counter() - t0
+    dev_bytes = free0 - torch.cuda.mem_get_info()[0]
+    print(f"C4 full size: {len(chips['index_id'])} chips, tessellate {t_tess:.2f} s, table {t_table:.2f} s, "
+          f"device {dev_bytes / 2**30:.2f} GiB, info {table.info()}")
+    n = 250_000_000
+    x, y = building_points_device(b, n, seed=81)
+    fast, generic = _fast_vs_generic(h3ctx, table, x, y)
+    assert fast.sum() > 5e7
+    assert np.array_equal(fast, generic)
+    got, want, total = _oracle_prefix(h3ctx, table, chips, oracle.GRID_H3, 11, x, y, 10_000_000, nb)
+    del x, y
+    torch.cuda.empty_cache()
+    assert total > 2e6 and np.array_equal(got, want)
     table.close()

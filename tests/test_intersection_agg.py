@@ -225,6 +225,11 @@ def test_gpu_intersection_agg_nyc_zones(h3ctx):
             assert abs(v - float(flat)) <= 1e-8, (a, v, float(flat))
             checked += 1
     assert checked >= 4
+    # each group's pieces are summed on the host in cell order: the same bits on every call
+    for _ in range(3):
+        lk2, rk2, area2, st2 = h3ctx.st_intersection_aggregate_area(left, right)
+        assert np.array_equal(lk2, lk) and np.array_equal(rk2, rk) and np.array_equal(st2, st)
+        assert np.array_equal(area2.view(np.uint64), area.view(np.uint64))
     left.close()
     right.close()
 

@@ -7,6 +7,7 @@ resolutions (uniform points, points on / next to tile lines, chip vertices and c
 plus synthetic cell sets near icosahedron face edges, pentagons, high latitudes and the
 antimeridian (where the builder must either decline or stay exact)."""
 import os
+import re
 import struct
 import subprocess
 
@@ -58,6 +59,10 @@ def test_tiles_nyc_tessellation(exe, tmp_path, res, sc):
     assert r["raster"] == 1, r["log"]
     assert r["raster_bad"] == 0, r["log"]
     assert r["raster_pure"] > 0.4 * 300_000
+    # k_join_stream_pipe's fixed-point lookup (tiles::raster_code_fixed; its pure codes are checked
+    # against the exact answer like the float form's) decides as many points
+    m = re.search(r"pure codes: float form (\d+), fixed-point form (\d+)", r["log"])
+    assert m and int(m.group(2)) >= 0.999 * int(m.group(1)), r["log"]
 
 
 def _disc_chips(lon, lat, radius_deg, res, n=20000, seed=0):
