@@ -37,6 +37,9 @@
  *     "NaN coordinates are not supported.") so a JNI shim can rethrow IllegalStateException.
  *   - Input arrays are borrowed for the duration of the call and may live in host memory or in
  *     device memory of the context's GPU (detected per pointer).  Host inputs are staged over PCIe.
+ *     Device inputs must be complete when the call's work starts: the context's own streams are
+ *     non-blocking (no implicit order with the null stream), so a caller producing columns on another
+ *     stream either binds that stream with mosaic_set_stream or synchronises it first.
  *   - Calls are synchronous unless the context option "async" is 1, in which case device-pointer
  *     calls only enqueue work on the calling thread's stream (mosaic_sync() waits and reports
  *     deferred errors).
@@ -100,7 +103,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
  * host-resident coordinates: the next chunk's copy overlaps the current chunk's join; 0 = stage the
  * whole batch; default 2^25), "mixed_rows" (1/2/4, default 2), "mixed_blocks_per_cu", "stream_pipe"
- * (0/1: the software-pipelined stream kernel where it applies; default 1), "bng_lds" (0/1: BNG tables
+ * (0/1: the software-pipelined H3 stream kernel where it applies; default 1), "bng_pipe" (0/1: the
+ * software-pipelined BNG stream kernel; default 0, slower at C5), "bng_lds" (0/1: BNG tables
  * built afterwards carry an LDS cell level for the BNG stream kernel; default 1), "bng_cell" (sub-cells
  * per BNG border cell side in those tables, a power of two <= 64; default 32), "scratch_limit" (see
  * the per-thread state below). */
@@ -272,7 +276,11 @@ int mosaic_pip_join_pairs(mosaic_ctx* ctx, const mosaic_chips* chips, const doub
  * flat rings: geometry g = parts [geom_parts[g], geom_parts[g+1]); part p = rings
  * [part_rings[p], part_rings[p+1]); ring r = vertices xy[2*ring_offsets[r] ..] (x, y interleaved,
  * lon/lat for H3, BNG metres for BNG).  Chip rows carry the geometry index as their key.
- * densify >= 1 subdivides H3 cell edges (1 = the 6-vertex h3ToGeoBoundary polygon).
+ * densify >= 1 subdivides H3 cell edges (1 = the 6-vertex h3ToGeoBoundary polygon; border chips keep
+ * straight sides between hexagon corners either way).  H3 geometries spanning icosahedron faces are
+ * cut into per-face pieces merged per cell (a border chip may then be a MultiPolygon whose parts meet
+ * along the face edge); MOSAIC_E_ARG for a geometry with a vertex more than ~78 degrees from the
+ * centre of a face it meets.
  * Reference: expressions/index/MosaicExplode.scala:70-79, core/Mosaic.scala:21-87,
  * core/index/IndexSystem.scala:152-186. */
 typedef struct mosaic_chip_set mosaic_chip_set;
@@ -292,7 +300,8 @@ int mosaic_chip_set_destroy(mosaic_chip_set* cs);
  * Mosaic.mosaicFill core/Mosaic.scala:60-87).  BNG: k_bng_tess_classify on the cell squares; H3:
  * k_tess_classify_poly on the (densify-subdivided) hexagons in the icosahedron face plane.  Border
  * cells are clipped on the GPU as well (k_tess_clip); candidate enumeration and the chip WKB
- * assembly are host code.  Errors as mosaic_tessellate. */
+ * assembly are host code, as is the per-face routine for H3 geometries spanning faces.  Errors as
+ * mosaic_tessellate. */
 int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
                           const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
                           int keep_core_geom, int densify, mosaic_chip_set** out);

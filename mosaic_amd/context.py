@@ -14,6 +14,7 @@ tensors, host or device), the Spark row wrappers are not reproduced.  Errors fol
 bad resolutions and NaN BNG coordinates raise ``IllegalStateException`` with the reference's message.
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -339,6 +340,7 @@ class MosaicContext:
         self.device = device
         self.set_option("jdk", jdk)
         self.resolution_of_table = None
+        self._bound = threading.local()  # per calling thread: the stream set with set_stream
 
     @classmethod
     def build(cls, index_system="H3", geometry_api="JTS", device=0, jdk=8):
@@ -354,6 +356,20 @@ class MosaicContext:
 
     def set_stream(self, stream_handle):
         N.check(N.lib().mosaic_set_stream(self.handle, stream_handle))
+        self._bound.stream = stream_handle
+
+    def _order(self, *arrays):
+        """Device columns written on torch's current stream are complete before the engine's own
+        (non-blocking) stream reads them: without a stream bound with set_stream, wait for torch's
+        current stream (a bound stream orders the work itself)."""
+        if getattr(self._bound, "stream", None) is not None:
+            return
+        for a in arrays:
+            if _is_torch(a) and a.is_cuda:
+                import torch
+
+                torch.cuda.current_stream(a.device).synchronize()
+                return
 
     def sync(self):
         N.check(N.lib().mosaic_sync(self.handle))
@@ -396,6 +412,7 @@ class MosaicContext:
     def _cells(self, x, y, resolution, valid=None):
         res = self.index_system.get_resolution(resolution)
         x, y = _f64(x), _f64(y)
+        self._order(x, y, valid)
         n = int(x.shape[0])
         if _is_torch(x):
             import torch
@@ -420,6 +437,7 @@ class MosaicContext:
         """BNG ids -> Arrow utf8 column (int64 offsets[n + 1], bytes), formatted on the GPU
         (BNGIndexSystem.format, BNGIndexSystem.scala:114-129)."""
         ids = cells.contiguous() if _is_torch(cells) else np.ascontiguousarray(cells, np.int64)
+        self._order(ids, valid)
         n = int(ids.shape[0])
         offs = np.zeros(n + 1, np.int64)
         need = ctypes.c_int64(0)
@@ -503,6 +521,7 @@ class MosaicContext:
         if valid is not None and not _is_torch(valid):
             valid = np.ascontiguousarray(valid, dtype=np.uint8)
         n = int(offsets.shape[0]) - 1
+        self._order(offsets, data, valid)
         if _is_torch(offsets):
             import torch
 
@@ -593,9 +612,9 @@ class MosaicContext:
         chip columns (is_core, index_id, polygon_key, wkb) with the cell classification on this
         context's GPU (mosaic_tessellate_gpu).
 
-        H3 restriction: each geometry must lie on one icosahedron face (true for city- and
-        country-scale inputs such as the NYC and London fixtures); a geometry spanning a face edge
-        raises MosaicError (MOSAIC_E_ARG), where the reference would tessellate it."""
+        H3 geometries spanning icosahedron faces are cut into per-face pieces; only a
+        geometry with a vertex more than ~78 degrees from the centre of a face it meets (no gnomonic
+        face plane holds it) raises MosaicError (MOSAIC_E_ARG)."""
         return tessellate(self.index_system, polygons, resolution, keep_core_geom, densify, ctx=self)
 
     def chip_table(self, is_core, index_id, wkb_list, polygon_key, resolution, n_polygons=None):
@@ -613,6 +632,7 @@ class MosaicContext:
         """Quickstart join + filter + groupBy(polygon).count(): int64 count per polygon key.
         ``out`` (optional, >= n_polygons int64, host or device) receives the counts."""
         x, y = _f64(x), _f64(y)
+        self._order(x, y, out)
         n = int(x.shape[0])
         if out is not None:
             counts = out
@@ -628,6 +648,7 @@ class MosaicContext:
     def pip_join_pairs(self, chips, x, y, capacity=None):
         """Quickstart join + filter: (row, polygon_key) pairs sorted by (row, key)."""
         x, y = _f64(x), _f64(y)
+        self._order(x, y)
         n = int(x.shape[0])
         cap = capacity if capacity is not None else max(2 * n, 1024)
         while True:

@@ -1911,6 +1911,7 @@ struct Options {
     int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
     int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
+    int bng_pipe = 0;         // k_join_stream_bng_pipe (measured slower at C5: 6.30 vs 4.53 ms, profiles/r03_kbench_bng_pipe.txt)
     int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
     int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
     int mixed_blocks_per_cu = 4;  // k_join_mixed grid: the workgroups resident at once (~120 VGPRs: 4 per CU)
@@ -2162,7 +2163,8 @@ struct mosaic_chips {
     // build cost (ms): chip table core (hash, geometry, chip rasters), tile directory, point-raster
     // classification (GPU or host), point-raster assembly; FNV-1a digest of the point raster
     double build_ms[4] = {0, 0, 0, 0};
-    uint64_t raster_digest = 0;
+    uint64_t raster_digest = 0;  // computed on first request (mosaic_chip_table_build_info), not in the build
+    size_t raster_parts[6] = {0, 0, 0, 0, 0, 0};  // bytes of sub, blocks, tile_base, quad, qrec masks, qrec codes
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
                           &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell})
@@ -2367,6 +2369,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.stream_block = (int)v;
     } else if (k == "stream_pipe") {
         o.stream_pipe = v ? 1 : 0;
+    } else if (k == "bng_pipe") {
+        o.bng_pipe = v ? 1 : 0;
     } else if (k == "bng_lds") {
         o.bng_lds = v ? 1 : 0;
     } else if (k == "bng_cell") {
@@ -2925,11 +2929,24 @@ static double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// Build-side phase trace (measurement only): MOSAIC_BUILD_TRACE=1 prints each phase's wall time of
+// a chip-table build to stderr.
+struct BuildTrace {
+    bool on = getenv("MOSAIC_BUILD_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        fprintf(stderr, "[build] %-28s %8.3f ms\n", what, ms_since(t));
+        t = std::chrono::steady_clock::now();
+    }
+};
+
 // Phase 1 of tiles::Builder::build_raster on the GPU (k_raster_sub, k_raster_line, k_raster_cells)
 // over the chip table already on the device; the host then assembles the raster from `rc` exactly
 // as after classify_raster_host, so both builds give the same bytes (raster_digest).
 static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles::Builder& tb,
                                tiles::Builder::RasterClass& rc) {
+    BuildTrace trace;
     const size_t n_recs = tb.recs.size(), SS = (size_t)tb.S * tb.S, CC = (size_t)tb.C * tb.C;
     const int64_t n_sub = (int64_t)(n_recs * SS);
     if (tb.tile_of_rec.size() != n_recs || tb.rec_dev.size() != n_recs || !ch->tile_rec.p || !ch->tile_ent.p)
@@ -2970,6 +2987,7 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
         HIP_TRY(hipMemcpyAsync(rc.code.data(), d_code.p, (size_t)n_sub * 2, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
     }
+    trace.mark("  k_raster_sub + copy");
     // mixed sub-blocks in record, then scan order (the order assemble_raster consumes them)
     std::vector<uint32_t> list;
     for (int64_t g = 0; g < n_sub; g++)
@@ -2997,6 +3015,7 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     HIP_TRY(hipMemcpyAsync(rc.line.data(), d_line.p, list.size() * sizeof(tiles::LineRec), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    trace.mark("  mixed list + line kernel");
     // the other mixed sub-blocks: C x C leaf cells each
     std::vector<uint32_t> cell_sb;
     for (int64_t m = 0; m < n_mixed; m++)
@@ -3016,6 +3035,7 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     rc.cells.resize((size_t)n_cells);
     HIP_TRY(hipMemcpyAsync(rc.cells.data(), d_cells.p, (size_t)n_cells * 2, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    trace.mark("  k_raster_cells + copy");
     return MOSAIC_OK;
 }
 
@@ -3036,6 +3056,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                              const int64_t* index_id, const void* wkb_off, bool off32, const uint8_t* wkb,
                              const int32_t* polygon_key, int32_t n_polygons, mosaic_chips** out) {
     const auto t_begin = std::chrono::steady_clock::now();
+    BuildTrace trace;
     // Arrow binary (int32 offsets) or large_binary (int64)
     auto wkb_offsets = [&](int64_t i) -> int64_t {
         return off32 ? (int64_t)((const int32_t*)wkb_off)[i] : ((const int64_t*)wkb_off)[i];
@@ -3052,6 +3073,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     std::iota(order.begin(), order.end(), 0u);
     std::stable_sort(order.begin(), order.end(),
                      [&](uint32_t a, uint32_t b) { return index_id[a] < index_id[b]; });
+    trace.mark("sort by cell");
     GeomBuilder gb;
     std::vector<uint32_t> meta(std::max<int64_t>(n_chips, 1));
     int64_t n_border = 0;
@@ -3069,6 +3091,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             return fail(MOSAIC_E_WKB, "chip " + std::to_string(i) + ": " + gb.error);
         n_border += !core;
     }
+    trace.mark("wkb parse");
     // distinct cells -> [first, count)
     std::vector<std::pair<int64_t, uint32_t>> cells;  // (cell, first)
     std::vector<uint32_t> counts;
@@ -3157,6 +3180,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             }
         }
     }
+    trace.mark("hash + chip rasters");
     if (meta.size() > (size_t)n_chips) {
         memset(&rb.hdr.back(), 0, sizeof(raster::ChipHdr));
         rb.hdr.back().cell_base = raster::kNoRaster;
@@ -3183,6 +3207,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     HIP_TRY(hipMemcpy(ch->hdr.p, rb.hdr.data(), rb.hdr.size() * sizeof(raster::ChipHdr), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
+    trace.mark("core uploads");
     if (grid == MOSAIC_GRID_BNG && res >= 1 && c->tiles && !cells.empty()) {
         // BNG dense cell table (see k_join_stream_bng): decode every chip cell id to its cell
         // coordinates and check the decoding by re-encoding the cell's lower-left corner
@@ -3346,8 +3371,10 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
         tiles::Builder tb;
         ch->build_ms[0] = ms_since(t_begin);
         auto t_dir = std::chrono::steady_clock::now();
+        trace.mark("(core)");
         const bool dir_ok = tb.build(res, cell_ids, slot_of);
         ch->build_ms[1] = ms_since(t_dir);
+        trace.mark("tile directory");
         if (dir_ok) {
             size_t b0 = tb.tile_idx.size() * 4, b1 = tb.recs.size() * sizeof(tiles::TileRec), b2 = tb.entries.size() * 4;
             if ((rc = ch->tile_idx.reserve(b0)) || (rc = ch->tile_rec.reserve(b1)) || (rc = ch->tile_ent.reserve(b2))) {
@@ -3411,19 +3438,19 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         tb.classify_raster_host(src, threads, cls);
                     }
                     ch->build_ms[2] = ms_since(t_cls);
+                    trace.mark("raster setup + classify");
                     auto t_asm = std::chrono::steady_clock::now();
                     raster_built = tb.assemble_raster(cls, threads);
                     ch->build_ms[3] = ms_since(t_asm);
+                    trace.mark("raster assemble");
                 }
                 if (raster_built) {
-                    uint64_t h = 1469598103934665603ull;
-                    h = fnv1a(h, tb.sub.data(), tb.sub.size() * 2);
-                    h = fnv1a(h, tb.blocks.data(), tb.blocks.size() * 2);
-                    h = fnv1a(h, tb.tile_base.data(), tb.tile_base.size() * 4);
-                    h = fnv1a(h, tb.quad.data(), tb.quad.size() * 2);
-                    h = fnv1a(h, tb.qrec_mask.data(), tb.qrec_mask.size() * 4);
-                    h = fnv1a(h, tb.qrec_code.data(), tb.qrec_code.size() * 2);
-                    ch->raster_digest = h;
+                    ch->raster_parts[0] = tb.sub.size() * 2;
+                    ch->raster_parts[1] = tb.blocks.size() * 2;
+                    ch->raster_parts[2] = tb.tile_base.size() * 4;
+                    ch->raster_parts[3] = tb.quad.size() * 2;
+                    ch->raster_parts[4] = tb.qrec_mask.size() * 4;
+                    ch->raster_parts[5] = tb.qrec_code.size() * 2;
                     size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
                     if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
                         ch->release_all();
@@ -3535,6 +3562,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             }
         }
     }
+    trace.mark("raster uploads + stream args");
     ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + rb.hdr.size() * sizeof(raster::ChipHdr) +
                        rb.cells.size() * sizeof(raster::CellRec) + rb.edges.size() * sizeof(pip::Edge);
     *out = ch;
@@ -3593,7 +3621,24 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
 int mosaic_chip_table_build_info(const mosaic_chips* ch, double* ms4, uint64_t* digest) {
     if (!ch || !ms4 || !digest) return fail(MOSAIC_E_ARG, "null argument");
     for (int k = 0; k < 4; k++) ms4[k] = ch->build_ms[k];
-    *digest = ch->raster_ok ? ch->raster_digest : 0;
+    *digest = 0;
+    if (!ch->raster_ok) return MOSAIC_OK;
+    if (!ch->raster_digest) {
+        // FNV-1a over the raster arrays as uploaded (sub-block table, blocks, tile bases, quad level,
+        // quad-record masks and codes): read back from the device on request, off the build's path
+        HIP_TRY(hipSetDevice(ch->device));
+        const void* src[6] = {ch->rsub.p, ch->rblocks.p, ch->rmid.p, ch->rquad.p, ch->rqrec.p,
+                              ch->rqrec.p ? (const void*)((const uint8_t*)ch->rqrec.p + ch->raster_parts[4]) : nullptr};
+        uint64_t h = 1469598103934665603ull;
+        std::vector<uint8_t> buf;
+        for (int k = 0; k < 6; k++) {
+            buf.resize(src[k] ? ch->raster_parts[k] : 0);  // (parts not uploaded: quad level or records off)
+            if (!buf.empty()) HIP_TRY(hipMemcpy(buf.data(), src[k], buf.size(), hipMemcpyDeviceToHost));
+            h = fnv1a(h, buf.data(), buf.size());
+        }
+        const_cast<mosaic_chips*>(ch)->raster_digest = h;
+    }
+    *digest = ch->raster_digest;
     return MOSAIC_OK;
 }
 
@@ -3719,7 +3764,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
-            const bool bpipe = c->stream_pipe && aligned;  // k_join_stream_bng_pipe (768-thread workgroups)
+            const bool bpipe = c->bng_pipe && aligned;  // k_join_stream_bng_pipe (768-thread workgroups)
             const int blkb = bpipe ? std::min(c->stream_block, kBngPipeBlock) : c->stream_block;
             size_t shm_b = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blkb / 64) * kStageWords * 4;
             // the LDS cell level when it fits this launch's LDS

@@ -21,7 +21,11 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -43,6 +47,24 @@ extern "C" int mosaic_tess_classify_poly(mosaic_ctx* c, int64_t n_geoms, const i
                                          double eps, uint8_t* cls);  // mosaic_hip.hip
 
 namespace {
+
+// phase trace (measurement only): MOSAIC_BUILD_TRACE=1 prints phase wall times to stderr
+struct TessTrace {
+    bool on = getenv("MOSAIC_BUILD_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    double acc[4] = {0, 0, 0, 0};
+    void mark(const char* what) {
+        if (!on) return;
+        fprintf(stderr, "[tess] %-28s %8.3f ms\n", what,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
+        t = std::chrono::steady_clock::now();
+    }
+    void add(int k) {  // accumulate the time since the last mark into acc[k]
+        if (!on) return;
+        acc[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+        t = std::chrono::steady_clock::now();
+    }
+};
 
 struct P2 {
     double x, y;
@@ -736,6 +758,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     if (res < 0 || res > 15)
         return mosaic_tess_fail(MOSAIC_E_RES, ("H3 resolution has to be between 0 and 15; found " + std::to_string(res)).c_str());
     if (densify < 1 || densify > 64) return mosaic_tess_fail(MOSAIC_E_ARG, "densify must be in [1, 64]");
+    TessTrace trace;
     const int D = densify, nv = 6 * D;
     const int64_t n_verts = n_geoms ? ring_offsets[part_rings[geom_parts[n_geoms]]] : 0;
     std::vector<double> pxy((size_t)std::max<int64_t>(n_verts, 1) * 2);
@@ -804,6 +827,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             }
         }
     }
+    trace.mark("h3 candidates (host)");
     // candidates in chunks, so the clip polygons staged on the host and the device stay bounded
     // (<= 64 MB of them per chunk) for any densify and envelope; chips come out in candidate order
     const int64_t n_cand = (int64_t)cg.size();
@@ -843,8 +867,10 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         clip.resize((size_t)nc * nv * 2);
         for (int64_t k = 0; k < nc; k++) fill_clip(k0 + k, clip.data() + 2 * (size_t)nv * k);
         cls.assign((size_t)nc, 0);
+        trace.add(0);
         int rc = mosaic_tess_classify_poly(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), nc,
                                            cg.data() + k0, clip.data(), nv, 1e-3, cls.data());
+        trace.add(1);
         if (rc) {
             delete cs;
             return rc;
@@ -860,6 +886,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             delete cs;
             return rc;
         }
+        trace.add(2);
         cc.index(nc, tasks);
         for (int64_t kk = 0; kk < nc; kk++) {
             const int64_t k = k0 + kk;
@@ -905,6 +932,10 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         delete cs;
         return rc;
     }
+    trace.add(3);
+    if (trace.on)
+        fprintf(stderr, "[tess] clip polygons %.3f ms, classify %.3f ms, gpu clip %.3f ms, chip assembly %.3f ms\n",
+                trace.acc[0], trace.acc[1], trace.acc[2], trace.acc[3]);
     *out = cs;
     return MOSAIC_OK;
 }

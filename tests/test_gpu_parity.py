@@ -274,22 +274,26 @@ def test_join_tessellated_chips_every_strategy(h3ctx):
             table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
                                      n_polygons=len(zones35))
             assert table.tiles()["built"] == 1
-            for tiles, praster in ((1, 1), (1, 0), (0, 0)):
+            # (stream_pipe 0: k_join_stream, the unpipelined float-coordinate stream kernel)
+            for tiles, praster, pipe in ((1, 1, 1), (1, 1, 0), (1, 0, 1), (0, 0, 1)):
                 h3ctx.set_option("tiles", tiles)
                 h3ctx.set_option("point_raster", praster)
+                h3ctx.set_option("stream_pipe", pipe)
                 rows, keys = h3ctx.pip_join_pairs(table, x, y)
                 got = set(zip(rows.tolist(), keys.tolist()))
-                assert got == want, (raster, lane_edges, tiles, praster, len(got ^ want))
+                assert got == want, (raster, lane_edges, tiles, praster, pipe, len(got ^ want))
                 counts = h3ctx.pip_join_count(table, x, y)
-                assert np.array_equal(counts, np.bincount(okey, minlength=len(zones35))), (raster, tiles, praster)
+                assert np.array_equal(counts, np.bincount(okey, minlength=len(zones35))), (raster, tiles, praster, pipe)
             h3ctx.set_option("tiles", 1)
             h3ctx.set_option("point_raster", 1)
+            h3ctx.set_option("stream_pipe", 1)
             table.close()
     finally:
         h3ctx.set_option("raster", 16)
         h3ctx.set_option("lane_edges", 0)
         h3ctx.set_option("tiles", 1)
         h3ctx.set_option("point_raster", 1)
+        h3ctx.set_option("stream_pipe", 1)
 
 
 def _tile_edge_points(t, rng, n):
@@ -487,6 +491,13 @@ def test_join_bng_dense_table(bngctx, res, every):
         assert np.array_equal(bngctx.pip_join_count(table, x, y), want)
     finally:
         bngctx.set_option("tiles", 1)
+    bngctx.set_option("bng_pipe", 1)  # the software-pipelined BNG stream kernel (not the default)
+    try:
+        assert np.array_equal(bngctx.pip_join_count(table, x, y), want)
+        r1, k1 = bngctx.pip_join_pairs(table, x, y)
+        assert np.array_equal(np.sort(r1 * len(ids) + k1), np.sort(rows * len(ids) + keys))
+    finally:
+        bngctx.set_option("bng_pipe", 0)
     bngctx.set_option("point_raster", 0)  # dense cell table without the border-cell leaf blocks
     try:
         t2 = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,
