@@ -21,10 +21,17 @@ namespace mosaic {
 namespace bng {
 
 MOSAIC_HD int32_t jvm_d2i(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // v_cvt_i32_f64 is Double.toInt: truncation toward zero, NaN -> 0, saturation at Int bounds
+    int32_t r;
+    __asm__("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(d));
+    return r;
+#else
     if (d != d) return 0;
     if (d >= 2147483647.0) return 2147483647;
     if (d <= -2147483648.0) return (-2147483647 - 1);
     return (int32_t)d;
+#endif
 }
 MOSAIC_HD int64_t jvm_d2l(double d) {
     if (d != d) return 0;

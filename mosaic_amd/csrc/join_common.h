@@ -215,6 +215,8 @@ static const uint32_t kBngLdsGather = 0xFFu;
 struct BngStreamArgs {
     int32_t e0, n0, ne, nn, C;
     double inv_div, div, f;  // 1 / divisor (rounded), divisor, C / divisor
+    int32_t idiv;            // divisor
+    float ff;                // C / divisor (f32)
     const uint32_t* cells;
     const uint16_t* leaf;
     uint32_t cells_bytes, leaf_bytes;

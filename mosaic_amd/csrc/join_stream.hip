@@ -537,7 +537,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             nan_seen |= live[k] && nan;
             const int32_t eI = bng::jvm_d2i(x[k]), nI = bng::jvm_d2i(y[k]);
             inr[k] = (uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u;
-            const int32_t qe = (int32_t)fma((double)eI, s.inv_div, 1e-7), qn = (int32_t)fma((double)nI, s.inv_div, 1e-7);
+            const double xe = (double)eI, ye = (double)nI;
+            const int32_t qe = (int32_t)fma(xe, s.inv_div, 1e-7), qn = (int32_t)fma(ye, s.inv_div, 1e-7);
             const int32_t ce = qe - s.e0, cn = qn - s.n0;
             const bool cell_in = inr[k] && (uint32_t)ce < (uint32_t)s.ne && (uint32_t)cn < (uint32_t)s.nn;
             // LDS cell level first: only cells it marks kBngLdsGather gather their table entry
@@ -546,13 +547,18 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const bool gth = cell_in && lb == kBngLdsGather;
             e[k] = __builtin_amdgcn_raw_buffer_load_b32(rcell, gth ? (uint32_t)(cn * s.ne + ce) << 2 : kNoLoad, 0, 0);
             e[k] = (gth || !cell_in) ? e[k] : (lb ? (kBngPure | lb) : 0u);
-            // sub-cell of the point inside the cell [qe div, (qe + 1) div) x [qn div, (qn + 1) div)
-            const double gxs = (x[k] - (double)qe * s.div) * s.f, gys = (y[k] - (double)qn * s.div) * s.f;
+            // sub-cell of the point inside the cell [qe div, (qe + 1) div) x [qn div, (qn + 1) div):
+            // the offset in the cell is (toInt(e) - qe div) (exact integer) + (e - toInt(e)) (exact in
+            // f64), in f32 sub-cell units (relative error ~1e-7, far inside the builder's sub-cell
+            // widening); one f64 add per axis instead of the f64 offset / scale / fract chain
+            // (qe, qn < 2^24 wherever the cell is used: 24-bit multiplies)
+            const float gxs = fmaf((float)(eI - (int32_t)__umul24((uint32_t)qe, (uint32_t)s.idiv)), s.ff, (float)(x[k] - xe) * s.ff);
+            const float gys = fmaf((float)(nI - (int32_t)__umul24((uint32_t)qn, (uint32_t)s.idiv)), s.ff, (float)(y[k] - ye) * s.ff);
             int sx = (int)gxs, sy = (int)gys;
             sx = min(max(sx, 0), (int)C - 1);
             sy = min(max(sy, 0), (int)C - 1);
-            su[k] = (float)(gxs - (double)sx);  // offset in the sub-cell (sub-cell units)
-            sv[k] = (float)(gys - (double)sy);
+            su[k] = gxs - (float)sx;  // offset in the sub-cell (sub-cell units)
+            sv[k] = gys - (float)sy;
             loff[k] = (uint32_t)(sy * (int)C + sx);
         }
         bool leafc[4], line[4];

@@ -3135,10 +3135,12 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     }
     // ray-parity rasters for one-ring border chips (raster.h); other chips take the general path
     // (contiguous chip ranges on host threads, concatenated in chip order: the same arrays as one
-    // sequential pass)
+    // sequential pass).  Built on a background thread while the tile directory is built and the
+    // point raster is classified on the GPU (neither reads them); joined before their upload.
     raster::Builder rb;
     rb.hdr.resize(meta.size());
-    {
+    bool rb_overflow = false;
+    auto chip_rasters = [&]() {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
             std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), n_chips / 256));
         std::vector<raster::Builder> part((size_t)nt);
@@ -3174,29 +3176,28 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             rb.edges.insert(rb.edges.end(), part[(size_t)k].edges.begin(), part[(size_t)k].edges.end());
             rb.pure_cells += part[(size_t)k].pure_cells;
             if (rb.edges.size() >= (1ull << 31) || rb.cells.size() >= (size_t)raster::kNoRaster) {
-                ch->release_all();
-                delete ch;
-                return fail(MOSAIC_E_ARG, "chip table too large for the raster record index");
+                rb_overflow = true;
+                return;
             }
         }
-    }
-    trace.mark("hash + chip rasters");
-    if (meta.size() > (size_t)n_chips) {
-        memset(&rb.hdr.back(), 0, sizeof(raster::ChipHdr));
-        rb.hdr.back().cell_base = raster::kNoRaster;
-    }
-    if (rb.cells.empty()) rb.cells.push_back(raster::CellRec{0, 0});
-    if (rb.edges.empty()) rb.edges.push_back(pip::Edge{0, 0, 0, 0});
+        if (meta.size() > (size_t)n_chips) {
+            memset(&rb.hdr.back(), 0, sizeof(raster::ChipHdr));
+            rb.hdr.back().cell_base = raster::kNoRaster;
+        }
+        if (rb.cells.empty()) rb.cells.push_back(raster::CellRec{0, 0});
+        if (rb.edges.empty()) rb.edges.push_back(pip::Edge{0, 0, 0, 0});
+    };
+    struct JoinOnExit {  // every return path waits for the background build first
+        std::thread t;
+        ~JoinOnExit() {
+            if (t.joinable()) t.join();
+        }
+    } rb_job;
+    rb_job.t = std::thread(chip_rasters);
     ch->raster = c->raster;
-    ch->raster_cells = (int64_t)rb.cells.size();
-    ch->raster_pure = rb.pure_cells;
-    ch->raster_records = (int64_t)rb.edges.size();
     size_t total = 0;
     int rc;
     if ((rc = ch->table.reserve(capacity * sizeof(HashEntry))) || (rc = ch->meta.reserve(meta.size() * 4)) ||
-        (rc = ch->hdr.reserve(rb.hdr.size() * sizeof(raster::ChipHdr))) ||
-        (rc = ch->cells.reserve(rb.cells.size() * sizeof(raster::CellRec))) ||
-        (rc = ch->rast_edges.reserve(rb.edges.size() * sizeof(pip::Edge))) ||
         (rc = ch->store.upload(gb, c->stream, &total))) {
         ch->release_all();
         delete ch;
@@ -3204,9 +3205,27 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     }
     HIP_TRY(hipMemcpy(ch->table.p, table.data(), capacity * sizeof(HashEntry), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ch->meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->hdr.p, rb.hdr.data(), rb.hdr.size() * sizeof(raster::ChipHdr), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
+    // the chip rasters: joined here when the build has no point raster to classify, else after it
+    bool rb_uploaded = false;
+    auto upload_chip_rasters = [&]() -> int {
+        if (rb_uploaded) return MOSAIC_OK;
+        rb_uploaded = true;
+        if (rb_job.t.joinable()) rb_job.t.join();
+        trace.mark("chip rasters (joined)");
+        if (rb_overflow) return fail(MOSAIC_E_ARG, "chip table too large for the raster record index");
+        ch->raster_cells = (int64_t)rb.cells.size();
+        ch->raster_pure = rb.pure_cells;
+        ch->raster_records = (int64_t)rb.edges.size();
+        int e;
+        if ((e = ch->hdr.reserve(rb.hdr.size() * sizeof(raster::ChipHdr))) ||
+            (e = ch->cells.reserve(rb.cells.size() * sizeof(raster::CellRec))) ||
+            (e = ch->rast_edges.reserve(rb.edges.size() * sizeof(pip::Edge))))
+            return e;
+        HIP_TRY(hipMemcpy(ch->hdr.p, rb.hdr.data(), rb.hdr.size() * sizeof(raster::ChipHdr), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
+        return MOSAIC_OK;
+    };
     trace.mark("core uploads");
     if (grid == MOSAIC_GRID_BNG && res >= 1 && c->tiles && !cells.empty()) {
         // BNG dense cell table (see k_join_stream_bng): decode every chip cell id to its cell
@@ -3439,6 +3458,11 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     }
                     ch->build_ms[2] = ms_since(t_cls);
                     trace.mark("raster setup + classify");
+                    if ((rc = upload_chip_rasters())) {
+                        ch->release_all();
+                        delete ch;
+                        return rc;
+                    }
                     auto t_asm = std::chrono::steady_clock::now();
                     raster_built = tb.assemble_raster(cls, threads);
                     ch->build_ms[3] = ms_since(t_asm);
@@ -3457,9 +3481,11 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         delete ch;
                         return rc;
                     }
+                    trace.mark("  raster reserve");
                     HIP_TRY(hipMemcpy(ch->rsub.p, tb.sub.data(), r0, hipMemcpyHostToDevice));
                     HIP_TRY(hipMemcpy(ch->rmid.p, tb.tile_base.data(), rm, hipMemcpyHostToDevice));
                     HIP_TRY(hipMemcpy(ch->rblocks.p, tb.blocks.data(), r1, hipMemcpyHostToDevice));
+                    trace.mark("  raster copies (sub, blocks)");
                     total += rm;
                     ch->raster_ok = true;
                     ch->praster.sub = (const uint16_t*)ch->rsub.p;
@@ -3563,6 +3589,11 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
         }
     }
     trace.mark("raster uploads + stream args");
+    if ((rc = upload_chip_rasters())) {
+        ch->release_all();
+        delete ch;
+        return rc;
+    }
     ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + rb.hdr.size() * sizeof(raster::ChipHdr) +
                        rb.cells.size() * sizeof(raster::CellRec) + rb.edges.size() * sizeof(pip::Edge);
     *out = ch;
@@ -3755,6 +3786,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             bs.div = (double)ch->bng_div;
             bs.inv_div = 1.0 / (double)ch->bng_div;
             bs.f = (double)ch->bng_C / (double)ch->bng_div;
+            bs.idiv = ch->bng_div;
+            bs.ff = (float)bs.f;
             bs.cells = (const uint32_t*)ch->bng_cells.p;
             bs.leaf = (const uint16_t*)ch->bng_leaf.p;
             bs.cells_bytes = (uint32_t)((size_t)ch->bng_ne * ch->bng_nn * 4);

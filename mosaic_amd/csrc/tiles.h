@@ -195,6 +195,26 @@ MOSAIC_HD uint16_t raster_code_fixed(const PointRaster& r, double ax, double bx,
     return r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
 }
 
+// std::vector allocator whose resize() leaves trivial elements uninitialised (host builders only)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+
 struct TileRec {
     int32_t a0, b0;  // window origin (axial)
     uint32_t off;    // first window entry
@@ -279,9 +299,11 @@ struct Builder {
     // run the tile path.
     int S = 0, C = 0, sshift = 0, cshift = 0;
     bool edge_ok = false;  // every edge sub-block is 0 or kMixed (raster_code clamps onto them)
-    std::vector<uint16_t> sub;
+    // (sub and blocks are resized without value-initialisation: assemble_raster writes every
+    // element, in parallel, so the pages are first touched by the threads that fill them)
+    std::vector<uint16_t, NoInitAlloc<uint16_t>> sub;
     std::vector<uint32_t> tile_base;
-    std::vector<uint16_t> blocks;
+    std::vector<uint16_t, NoInitAlloc<uint16_t>> blocks;
     std::vector<uint16_t> quad;  // quad level (empty: none)
     int qshift = 0, qnx = 0, qny = 0;
     int quad_max = kQuadMax;  // quad-level entry budget (set before build_raster)

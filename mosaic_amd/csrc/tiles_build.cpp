@@ -20,6 +20,9 @@
 #include "tiles.h"
 #include "raster_build.h"
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <atomic>
 #include <cstring>
 #include <thread>
@@ -415,11 +418,27 @@ void parallel_for(int64_t n, int threads, F fn) {
 }
 }  // namespace
 
+// phase trace of the assembly (measurement only): MOSAIC_BUILD_TRACE=1
+namespace {
+struct AsmTrace {
+    bool on = getenv("MOSAIC_BUILD_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        fprintf(stderr, "[asm]   %-26s %8.3f ms\n", what,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
+        t = std::chrono::steady_clock::now();
+    }
+};
+}  // namespace
+
 bool Builder::assemble_raster(const RasterClass& rc, int threads) {
+    AsmTrace trace;
     const int nx = grid.nx, ny = grid.ny;
     const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
     const size_t SS = (size_t)S * S, CC = (size_t)C * C;
-    sub.assign((size_t)(NX * NY), (uint16_t)0);
+    sub.clear();
+    sub.resize((size_t)(NX * NY));  // (uninitialised: every tile's entries are written below)
     tile_base.assign((size_t)nx * ny, 0u);
     std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
     std::vector<std::vector<LineRec>> tile_lines(recs.size());
@@ -439,6 +458,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
     });
     for (int64_t ri = 0; ri < nrec; ri++) mk0[(size_t)ri + 1] += mk0[(size_t)ri];
     if (mk0[(size_t)nrec] > rc.kind.size()) return false;
+    trace.mark("alloc + mixed counts");
     std::atomic<int64_t> pure(0), mixed(0), cmixed(0), nline(0);
     parallel_for(nrec, threads, [&](int64_t b, int64_t e) {
         int64_t l_pure = 0, l_mixed = 0, l_cmixed = 0, l_line = 0;
@@ -489,13 +509,20 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
         cmixed += l_cmixed;
         nline += l_line;
     });
-    // kFull tiles: every point takes the tile path; kSkip tiles: no pair (0, already)
-    for (int64_t t = 0; t < (int64_t)nx * ny; t++) {
-        if (tile_idx[(size_t)t] != kFull) continue;
-        int ti = (int)(t % nx), tj = (int)(t / nx);
-        for (int sj = 0; sj < S; sj++)
-            for (int si = 0; si < S; si++) sub[(size_t)((int64_t)(tj * S + sj) * NX + (ti * S + si))] = kMixed;
-    }
+    trace.mark("sub entries");
+    // tiles without a record: kFull (every point takes the tile path) or kSkip (no pair: 0)
+    std::vector<uint8_t> has_rec((size_t)nx * ny, 0);
+    for (int64_t ri = 0; ri < nrec; ri++)
+        if (rec_ok(ri)) has_rec[(size_t)tile_of_rec[(size_t)ri]] = 1;
+    parallel_for((int64_t)nx * ny, threads, [&](int64_t b, int64_t e) {
+        for (int64_t t = b; t < e; t++) {
+            if (has_rec[(size_t)t]) continue;
+            const uint16_t v = tile_idx[(size_t)t] == kFull ? kMixed : (uint16_t)0;
+            int ti = (int)(t % nx), tj = (int)(t / nx);
+            for (int sj = 0; sj < S; sj++)
+                std::fill_n(sub.data() + (size_t)((int64_t)(tj * S + sj) * NX + ti * S), S, v);
+        }
+    });
     // merge: per tile [line records, last first][leaf blocks], 16-byte aligned; tile_base = the
     // element of the tile's first leaf block
     size_t total = 0;
@@ -509,14 +536,24 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
         sub.clear();
         return false;
     }
-    blocks.assign(std::max<size_t>(total, std::max<size_t>(CC, 8)), kMixed);
+    const size_t nblocks = std::max<size_t>(total, std::max<size_t>(CC, 8));
+    blocks.clear();
+    blocks.resize(nblocks);  // (uninitialised: each record's span and the padding are written below)
     parallel_for(nrec, threads, [&](int64_t b, int64_t e) {
         for (int64_t r = b; r < e; r++) {
+            // [span start, line records, leaf blocks, padding to the next record's span)
+            const size_t lo = at[(size_t)r] - 8 * tile_lines[(size_t)r].size();
+            const size_t hi = (size_t)r + 1 < recs.size() ? at[(size_t)r + 1] - 8 * tile_lines[(size_t)r + 1].size() : nblocks;
             for (size_t n = 0; n < tile_lines[(size_t)r].size(); n++)
                 memcpy(blocks.data() + at[(size_t)r] - 8 * (n + 1), &tile_lines[(size_t)r][n], sizeof(LineRec));
             std::copy(tile_blocks[(size_t)r].begin(), tile_blocks[(size_t)r].end(), blocks.begin() + (ptrdiff_t)at[(size_t)r]);
+            std::fill(blocks.begin() + (ptrdiff_t)(at[(size_t)r] + tile_blocks[(size_t)r].size()), blocks.begin() + (ptrdiff_t)hi,
+                      kMixed);
+            if (r == 0) std::fill(blocks.begin(), blocks.begin() + (ptrdiff_t)lo, kMixed);
         }
     });
+    if (nrec == 0) std::fill(blocks.begin(), blocks.end(), kMixed);
+    trace.mark("full tiles + merge blocks");
     // clamping (raster_code, k_join_stream): a finite point outside the grid is looked up at the
     // nearest edge sub-block, so every edge sub-block must answer "no pair" (0) or kMixed (the
     // tile path, which finds no chip outside the grid); chip cells lie >= k tile rings inside
@@ -543,21 +580,26 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
         qnx = (int)((NX + (1 << qshift) - 1) >> qshift);
         qny = (int)((NY + (1 << qshift) - 1) >> qshift);
         quad.assign((size_t)qnx * qny, kMixed);
-        std::vector<uint8_t> seen((size_t)qnx * qny, 0);
-        parallel_for(qny, threads, [&](int64_t qb, int64_t qe) {  // quad rows [qb, qe)
-            for (int64_t j = qb << qshift; j < std::min<int64_t>(NY, qe << qshift); j++)
-                for (int64_t i = 0; i < NX; i++) {
-                    const uint16_t e = sub[(size_t)(j * NX + i)];
-                    const size_t q = (size_t)((j >> qshift) * qnx + (i >> qshift));
-                    const uint16_t code = (e & kSubBlock) ? kMixed : e;  // blocks and kMixed alike
-                    if (!seen[q]) {
-                        seen[q] = 1;
-                        quad[q] = code;
-                    } else if (quad[q] != code) {
-                        quad[q] = kMixed;
-                    }
+        // per quad: the code all its (in-grid) sub-blocks share, else kMixed (blocks and kMixed alike)
+        parallel_for((int64_t)qnx * qny, threads, [&](int64_t qb, int64_t qe) {
+            for (int64_t q = qb; q < qe; q++) {
+                const int64_t i0 = (q % qnx) << qshift, j0 = (q / qnx) << qshift;
+                const int64_t i1 = std::min<int64_t>(NX, i0 + ((int64_t)1 << qshift));
+                const int64_t j1 = std::min<int64_t>(NY, j0 + ((int64_t)1 << qshift));
+                const uint16_t first = sub[(size_t)(j0 * NX + i0)];
+                uint16_t code = (first & kSubBlock) ? kMixed : first;
+                for (int64_t j = j0; j < j1 && code != kMixed; j++) {
+                    const uint16_t* row = sub.data() + (size_t)(j * NX);
+                    for (int64_t i = i0; i < i1; i++)
+                        if (row[i] != code) {
+                            code = kMixed;
+                            break;
+                        }
                 }
+                quad[(size_t)q] = code;
+            }
         });
+        trace.mark("edge check + quad level");
         // compact copies of the non-uniform quads' sub-block entries behind the grid's own
         // (quad entry kSubBlock | r: quad r's 2^qshift x 2^qshift entries, row-major, from
         // sub[nx * ny + (r << 2 qshift)]), so the sub-block lookups that pass the quad level
@@ -584,6 +626,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
                     quad[(size_t)refq[(size_t)r]] = (uint16_t)(kSubBlock | r);
                 }
             });
+            trace.mark("compact copies");
             // quad records for as many compact quads as the LDS budget holds (10 bytes each)
             qrec_mask.clear();
             qrec_code.clear();
@@ -635,6 +678,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
                 }
                 });
             }
+            trace.mark("quad records");
         } else {
             quad.clear();  // no quad level: k_join_stream needs one (the tile path serves)
         }
