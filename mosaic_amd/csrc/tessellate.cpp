@@ -25,8 +25,10 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mosaic_hip.h"
@@ -52,7 +54,7 @@ namespace {
 struct TessTrace {
     bool on = getenv("MOSAIC_BUILD_TRACE") != nullptr;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-    double acc[4] = {0, 0, 0, 0};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
     void mark(const char* what) {
         if (!on) return;
         fprintf(stderr, "[tess] %-28s %8.3f ms\n", what,
@@ -119,6 +121,24 @@ int face_of(double lon, double lat) {
         }
     }
     return best;
+}
+
+// The hexagon corner offsets R cos(30 + 60 k deg), R sin(...), k = 0..5: the same expressions as the
+// per-cell loops used to evaluate (so the same doubles), computed once.
+struct HexCorners {
+    double dx[6], dy[6];
+    HexCorners() {
+        const double R = 0.57735026918962576451;
+        for (int k = 0; k < 6; k++) {
+            double ang = (30.0 + 60.0 * k) * (M_PI / 180.0);
+            dx[k] = R * cos(ang);
+            dy[k] = R * sin(ang);
+        }
+    }
+};
+const HexCorners& hex_corners() {
+    static const HexCorners h;
+    return h;
 }
 
 // ---- geometry helpers (plane) ----
@@ -528,10 +548,7 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
                 double cx = i - 0.5 * j, cy = j * s60;
                 if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
                 P2 corners[6];
-                for (int k = 0; k < 6; k++) {
-                    double ang = (30.0 + 60.0 * k) * (M_PI / 180.0);
-                    corners[k] = {cx + R * cos(ang), cy + R * sin(ang)};
-                }
+                for (int k = 0; k < 6; k++) corners[k] = {cx + hex_corners().dx[k], cy + hex_corners().dy[k]};
                 hex.clear();
                 for (int k = 0; k < 6; k++) {
                     P2 a = corners[k], b = corners[(k + 1) % 6];
@@ -588,7 +605,6 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
 struct ClippedChips {
     tessclip::ClipResult r;
     std::vector<int64_t> task_of;  // candidate -> task (-1: not a border task)
-    size_t ir = 0, ip = 0;
     void index(int64_t n_cand, const std::vector<int64_t>& tasks) {
         std::sort(r.rings.begin(), r.rings.end(), [](const tessclip::ClipRing& a, const tessclip::ClipRing& b) {
             return a.cand != b.cand ? a.cand < b.cand : (a.part != b.part ? a.part < b.part : a.ring < b.ring);
@@ -600,10 +616,14 @@ struct ClippedChips {
         for (size_t t = 0; t < tasks.size(); t++) task_of[(size_t)tasks[t]] = (int64_t)t;
     }
     bool redo(int64_t k) const { return task_of[(size_t)k] < 0 || r.redo[(size_t)task_of[(size_t)k]]; }
-    // candidate k's chip (candidates are visited in increasing order); false: no chip
-    bool chip(int64_t k, std::vector<uint8_t>& wkb) {
-        while (ir < r.rings.size() && r.rings[ir].cand < k) ir++;
-        while (ip < r.parts.size() && r.parts[ip].cand < k) ip++;
+    // candidate k's chip (any order: its first ring and part by binary search); false: no chip
+    bool chip(int64_t k, std::vector<uint8_t>& wkb) const {
+        const size_t ir = (size_t)(std::lower_bound(r.rings.begin(), r.rings.end(), k,
+                                                    [](const tessclip::ClipRing& a, int64_t c) { return a.cand < c; }) -
+                                   r.rings.begin());
+        const size_t ip = (size_t)(std::lower_bound(r.parts.begin(), r.parts.end(), k,
+                                                    [](const tessclip::ClipPart& a, int64_t c) { return a.cand < c; }) -
+                                   r.parts.begin());
         std::vector<std::vector<std::vector<P2>>> parts;
         size_t jr = ir;
         for (size_t jp = ip; jp < r.parts.size() && r.parts[jp].cand == k; jp++) {
@@ -697,10 +717,7 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                     if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
                     Cell cell;
                     std::vector<P2> corners;
-                    for (int k = 0; k < 6; k++) {
-                        double ang = (30.0 + 60.0 * k) * (M_PI / 180.0);
-                        corners.push_back({cx + R * cos(ang), cy + R * sin(ang)});
-                    }
+                    for (int k = 0; k < 6; k++) corners.push_back({cx + hex_corners().dx[k], cy + hex_corners().dy[k]});
                     cell.clip = corners;
                     for (int k = 0; k < 6; k++) {
                         P2 a = corners[k], b = corners[(k + 1) % 6];
@@ -772,10 +789,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     auto fill_clip = [&](int64_t k, double* out_pts) {
         const double cx = cxy[2 * (size_t)k], cy = cxy[2 * (size_t)k + 1];
         P2 corners[6];
-        for (int q = 0; q < 6; q++) {
-            double ang = (30.0 + 60.0 * q) * (M_PI / 180.0);
-            corners[q] = {cx + R * cos(ang), cy + R * sin(ang)};
-        }
+        for (int q = 0; q < 6; q++) corners[q] = {cx + hex_corners().dx[q], cy + hex_corners().dy[q]};
         int m = 0;
         for (int q = 0; q < 6; q++) {
             P2 a = corners[q], b = corners[(q + 1) % 6];
@@ -785,21 +799,27 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             }
         }
     };
-    for (int64_t g = 0; g < n_geoms; g++) {
-        const int64_t v0 = ring_offsets[part_rings[geom_parts[g]]], v1 = ring_offsets[part_rings[geom_parts[g + 1]]];
-        if (v0 == v1) continue;
-        int face = -1;
+    // per geometry (host threads, independent): face check, face-plane vertices (disjoint ranges of
+    // pxy), candidate lattice cells; concatenated in geometry order afterwards
+    struct GeomCands {
         bool multi = false;
+        int face = -1;
+        std::vector<double> cxy;
+        std::vector<int64_t> cid;
+    };
+    std::vector<GeomCands> gc((size_t)n_geoms);
+    auto cands_of = [&](int64_t g) {
+        GeomCands& out = gc[(size_t)g];
+        const int64_t v0 = ring_offsets[part_rings[geom_parts[g]]], v1 = ring_offsets[part_rings[geom_parts[g + 1]]];
+        if (v0 == v1) return;
+        int face = -1;
         for (int64_t v = v0; v < v1; v++) {
             int f = face_of(xy[2 * v], xy[2 * v + 1]);
             if (face < 0) face = f;
-            multi = multi || f != face;
+            out.multi = out.multi || f != face;
         }
-        if (multi) {  // spans faces: the host's per-face pieces (tessellate_h3_multiface), in geometry order
-            multi_geoms.push_back(g);
-            continue;
-        }
-        gface[g] = face;
+        if (out.multi) return;  // spans faces: the host's per-face pieces (tessellate_h3_multiface)
+        out.face = face;
         FacePlane fp;
         fp.init(face, res);
         double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
@@ -818,15 +838,35 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             for (int i = ilo; i <= ihi; i++) {
                 double cx = i - 0.5 * j, cy = j * s60;
                 if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
-                cxy.push_back(cx);
-                cxy.push_back(cy);
+                out.cxy.push_back(cx);
+                out.cxy.push_back(cy);
                 h3::IJK ijk = {i, j, 0};
                 h3::ijk_normalize(ijk);
-                cg.push_back((int32_t)g);
-                cid.push_back((int64_t)h3::face_ijk_to_h3(face, ijk, res));
+                out.cid.push_back((int64_t)h3::face_ijk_to_h3(face, ijk, res));
             }
         }
+    };
+    {
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
+            std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), n_geoms / 8));
+        std::atomic<int64_t> next(0);
+        auto work = [&]() {
+            for (int64_t g; (g = next.fetch_add(1)) < n_geoms;) cands_of(g);
+        };
+        std::vector<std::thread> pool;
+        for (int k = 1; k < nt; k++) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
     }
+    for (int64_t g = 0; g < n_geoms; g++) {
+        GeomCands& q = gc[(size_t)g];
+        if (q.multi) multi_geoms.push_back(g);
+        gface[g] = q.face;
+        cxy.insert(cxy.end(), q.cxy.begin(), q.cxy.end());
+        cid.insert(cid.end(), q.cid.begin(), q.cid.end());
+        cg.insert(cg.end(), q.cid.size(), (int32_t)g);
+    }
+    gc.clear();
     trace.mark("h3 candidates (host)");
     // candidates in chunks, so the clip polygons staged on the host and the device stay bounded
     // (<= 64 MB of them per chunk) for any densify and envelope; chips come out in candidate order
@@ -836,11 +876,6 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     std::vector<uint8_t> cls;
     std::vector<int64_t> tasks;
     mosaic_chip_set* cs = new mosaic_chip_set();
-    std::vector<std::vector<std::vector<P2>>> geo, pl;
-    FacePlane fp;
-    fp.init(0, res);  // re-initialised per geometry below
-    int64_t cur = -1;
-    std::vector<uint8_t> blob;
     // the face-spanning geometries before geometry `upto`, emitted where the host producer emits them
     size_t next_multi = 0;
     auto flush_multi = [&](int64_t upto) -> int {
@@ -888,54 +923,95 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         }
         trace.add(2);
         cc.index(nc, tasks);
+        trace.add(3);
+        // the chunk's chips on host threads (each candidate's chip is independent: GPU-clipped border
+        // chips to WKB, core chips' outlines, cells the GPU clipper left to the host), then appended
+        // in candidate order
+        struct OneChip {
+            bool has = false, core = false;
+            std::vector<uint8_t> blob;
+        };
+        std::vector<OneChip> chips((size_t)nc);
+        {
+            const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
+                std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), nc / 256));
+            auto work = [&](int t) {
+                std::vector<std::vector<std::vector<P2>>> geo, pl;
+                FacePlane fp;
+                fp.init(0, res);
+                int64_t cur = -1;
+                mosaic_chip_set tmp;
+                for (int64_t kk = nc * t / nt; kk < nc * (t + 1) / nt; kk++) {
+                    const int64_t k = k0 + kk;
+                    OneChip& o = chips[(size_t)kk];
+                    if (!cls[kk]) continue;
+                    if (cls[kk] == 2 && !cc.redo(kk)) {
+                        o.has = cc.chip(kk, o.blob);
+                        continue;
+                    }
+                    if (cg[k] != cur) {
+                        cur = cg[k];
+                        fp.init(gface[cur], res);
+                        geo.clear();
+                        pl.clear();
+                        for (int64_t p = geom_parts[cur]; p < geom_parts[cur + 1]; p++) {
+                            std::vector<std::vector<P2>> rings, prings;
+                            for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
+                                std::vector<P2> ring, pring;
+                                for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) {
+                                    ring.push_back({xy[2 * v], xy[2 * v + 1]});
+                                    pring.push_back({pxy[2 * v], pxy[2 * v + 1]});
+                                }
+                                rings.push_back(std::move(ring));
+                                prings.push_back(std::move(pring));
+                            }
+                            geo.push_back(std::move(rings));
+                            pl.push_back(std::move(prings));
+                        }
+                    }
+                    Cell cell;
+                    const double* P = clip.data() + 2 * (size_t)nv * kk;
+                    for (int v = 0; v < nv; v++) cell.outline.push_back({P[2 * v], P[2 * v + 1]});
+                    cell.clip = cell.outline;
+                    cell.id = cid[k];
+                    tmp.is_core.clear();
+                    tmp.index_id.clear();
+                    tmp.key.clear();
+                    tmp.wkb_offsets.assign(1, 0);
+                    tmp.wkb.clear();
+                    emit_cell(&tmp, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); },
+                              1e-12, (int)cls[kk]);
+                    if (!tmp.index_id.empty()) {
+                        o.has = true;
+                        o.core = tmp.is_core[0] != 0;
+                        o.blob.assign(tmp.wkb.begin(), tmp.wkb.end());
+                    }
+                }
+            };
+            std::vector<std::thread> pool;
+            for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
+            work(0);
+            for (auto& th : pool) th.join();
+        }
+        trace.add(4);
         for (int64_t kk = 0; kk < nc; kk++) {
             const int64_t k = k0 + kk;
             if (!multi_geoms.empty() && (rc = flush_multi(cg[k]))) {
                 delete cs;
                 return rc;
             }
-            if (!cls[kk]) continue;
-            if (cls[kk] == 2 && !cc.redo(kk)) {
-                if (cc.chip(kk, blob)) cs->add(false, cid[k], cg[k], blob);
-                continue;
-            }
-            if (cg[k] != cur) {
-                cur = cg[k];
-                fp.init(gface[cur], res);
-                geo.clear();
-                pl.clear();
-                for (int64_t p = geom_parts[cur]; p < geom_parts[cur + 1]; p++) {
-                    std::vector<std::vector<P2>> rings, prings;
-                    for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
-                        std::vector<P2> ring, pring;
-                        for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) {
-                            ring.push_back({xy[2 * v], xy[2 * v + 1]});
-                            pring.push_back({pxy[2 * v], pxy[2 * v + 1]});
-                        }
-                        rings.push_back(std::move(ring));
-                        prings.push_back(std::move(pring));
-                    }
-                    geo.push_back(std::move(rings));
-                    pl.push_back(std::move(prings));
-                }
-            }
-            Cell cell;
-            const double* P = clip.data() + 2 * (size_t)nv * kk;
-            for (int v = 0; v < nv; v++) cell.outline.push_back({P[2 * v], P[2 * v + 1]});
-            cell.clip = cell.outline;
-            cell.id = cid[k];
-            emit_cell(cs, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); }, 1e-12,
-                      (int)cls[kk]);
+            if (chips[(size_t)kk].has) cs->add(chips[(size_t)kk].core, cid[k], cg[k], chips[(size_t)kk].blob);
         }
     }
     if (int rc = flush_multi(n_geoms)) {
         delete cs;
         return rc;
     }
-    trace.add(3);
+    trace.add(5);
     if (trace.on)
-        fprintf(stderr, "[tess] clip polygons %.3f ms, classify %.3f ms, gpu clip %.3f ms, chip assembly %.3f ms\n",
-                trace.acc[0], trace.acc[1], trace.acc[2], trace.acc[3]);
+        fprintf(stderr, "[tess] clip polygons %.3f ms, classify %.3f ms, gpu clip %.3f ms, index clips %.3f ms, "
+                        "chip WKB (threads) %.3f ms, append %.3f ms\n",
+                trace.acc[0], trace.acc[1], trace.acc[2], trace.acc[3], trace.acc[4], trace.acc[5]);
     *out = cs;
     return MOSAIC_OK;
 }

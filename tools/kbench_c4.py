@@ -49,6 +49,9 @@ def main():
     for v in args.variants:
         ctx.set_option("tiles", 0 if v == "tiles0" else 1)
         ctx.set_option("point_raster", 0 if v == "praster0" else 1)
+        for kv in (v.split(",") if "=" in v else []):  # option sets, e.g. raster_min_segments=8
+            k_, v_ = kv.split("=")
+            ctx.set_option(k_, int(v_))
         t0 = time.perf_counter()
         table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], args.res,
                                n_polygons=nb)
