@@ -968,109 +968,6 @@ __global__ void __launch_bounds__(256) k_raster_cells(RBuildArgs a) {
     }
 }
 
-// k_raster_cells with one workgroup per sub-block: the sub-block's quad, its candidate hexagons
-// (the window hexagons meeting it, in window order) and the (C + 1)^2 leaf-cell corner images are
-// computed once into LDS, then each thread classifies its cells against that short list -- the same
-// tests in the same order as rclassify_rect, so the same codes bit for bit.
-static const int kRasterCellsMaxCand = 512;   // window hexagons a workgroup can list (else per-lane)
-static const int kRasterCellsMaxC = 32;       // leaf cells per sub-block side held in LDS
-__global__ void __launch_bounds__(256) k_raster_cells_wg(RBuildArgs a) {
-    __shared__ rbuild::P2 lat[(kRasterCellsMaxC + 1) * (kRasterCellsMaxC + 1)];
-    __shared__ rbuild::P2 sq_s[4];
-    __shared__ double stol_s;
-    __shared__ int cand[kRasterCellsMaxCand];
-    __shared__ int ncand_s;
-    const int64_t m = blockIdx.x;
-    if (m >= a.n_cell_sb) return;  // (uniform)
-    const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
-    const int64_t g = a.cell_sb[m];
-    const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
-    RTile t;
-    const bool ok = rtile_of(a, r, t);  // (uniform)
-    const int W = ok ? t.wa * t.wb : 0;
-    const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
-    if (!ok || W > kRasterCellsMaxCand || a.C > kRasterCellsMaxC) {
-        // per-lane fallback (k_raster_cells' body)
-        for (int64_t cc = tid; cc < CC; cc += nt) {
-            uint16_t code = tiles::kMixed;
-            if (ok) {
-                const int cj = (int)(cc / a.C), ci = (int)(cc - (int64_t)cj * a.C);
-                rbuild::P2 sq[4];
-                const double stol = rsub_quad(a, t, si, sj, sq);
-                const int i0 = si * a.C + ci, j0 = sj * a.C + cj;
-                const rbuild::P2 qc[4] = {rimage(a, t, i0, j0), rimage(a, t, i0 + 1, j0), rimage(a, t, i0 + 1, j0 + 1),
-                                          rimage(a, t, i0, j0 + 1)};
-                code = rclassify_rect(a, t, i0, j0, i0 + 1, j0 + 1, qc, sq, stol);
-            }
-            a.cells[m * CC + cc] = code;
-        }
-        return;
-    }
-    if (tid == 0) {
-        stol_s = rsub_quad(a, t, si, sj, sq_s);
-        ncand_s = 0;
-    }
-    const int C = a.C, L = C + 1;
-    for (int q = tid; q < L * L; q += nt) {
-        const int lj = q / L, li = q - lj * L;
-        lat[q] = rimage(a, t, si * C + li, sj * C + lj);
-    }
-    __syncthreads();
-    // the sub-block's candidate hexagons, in window order (a block-wide ordered compaction)
-    __shared__ int wcount[16];
-    for (int k0 = 0; k0 < W; k0 += nt) {
-        const int k = k0 + tid;
-        const bool is_c = k < W && rbuild::poly_meets_hex(sq_s, 4, rhex_centre(t, k), stol_s, a.ht);
-        const unsigned long long bal = __ballot(is_c);
-        const int wave = tid >> 6, lane = tid & 63;
-        if (lane == 0) wcount[wave] = __popcll(bal);
-        __syncthreads();
-        int base = ncand_s;
-        for (int w = 0; w < wave; w++) base += wcount[w];
-        if (is_c) cand[base + __popcll(bal & ((1ull << lane) - 1ull))] = k;
-        __syncthreads();
-        if (tid == 0) {
-            int tot = 0;
-            for (int w = 0; w < (nt + 63) / 64; w++) tot += wcount[w];
-            ncand_s += tot;
-        }
-        __syncthreads();
-    }
-    const int ncand = ncand_s;
-    const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
-    const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
-    const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
-    for (int64_t cc = tid; cc < CC; cc += nt) {
-        const int cj = (int)(cc / C), ci = (int)(cc - (int64_t)cj * C);
-        const int i0 = si * C + ci, j0 = sj * C + cj, i1 = i0 + 1, j1 = j0 + 1;
-        const rbuild::P2 q[4] = {lat[cj * L + ci], lat[cj * L + ci + 1], lat[(cj + 1) * L + ci + 1], lat[(cj + 1) * L + ci]};
-        // rclassify_rect over the pre-filtered candidates
-        const double frac = rbuild::dmax((double)(i1 - i0), (double)(j1 - j0)) / a.N;
-        const double tol = 4.0 * t.dev * frac * frac + 1e-7;
-        const double x0 = t.lon0 + a.tw * i0 / a.N - ex, x1 = t.lon0 + a.tw * i1 / a.N + ex;
-        const double y0 = t.lat0 + a.th * j0 / a.N - ey, y1 = t.lat0 + a.th * j1 / a.N + ey;
-        const double cxm = t.lon0 + a.tw * (i0 + i1) / (2.0 * a.N), cym = t.lat0 + a.th * (j0 + j1) / (2.0 * a.N);
-        bool any = false, mixed = false;
-        int acnt = 0, akey = -1;
-        for (int n = 0; n < ncand && !mixed; n++) {
-            const int k = cand[n];
-            if (!rbuild::poly_meets_hex(q, 4, rhex_centre(t, k), tol, a.ht)) continue;
-            int key;
-            const int cnt = rhex_answer(a, t, k, false, x0, y0, x1, y1, nullptr, 0, 0.0, cxm, cym, &key);
-            if (cnt < 0 || cnt > 1) {
-                mixed = true;
-            } else if (!any) {
-                any = true;
-                acnt = cnt;
-                akey = key;
-            } else if (cnt != acnt || key != akey) {
-                mixed = true;
-            }
-        }
-        a.cells[m * CC + cc] = (mixed || !any) ? tiles::kMixed : (acnt == 0 ? (uint16_t)0 : (uint16_t)(akey + 1));
-    }
-}
-
 // ---- st_intersects_aggregate over the chip join of two chip tables ----------------------------
 // ST_IntersectsAggregate.update (expressions/geometry/ST_IntersectsAggregate.scala:28-39) folds
 // `left.is_core || right.is_core || left.wkb intersects right.wkb` with OR over the rows of a
@@ -3145,10 +3042,9 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     a.cell_sb = (const uint32_t*)d_list.p;
     a.n_cell_sb = (int64_t)cell_sb.size();
     a.cells = (uint16_t*)d_cells.p;
-    if (c->raster_build == 2)  // one lane per leaf cell (the first GPU form, kept for comparison)
-        hipLaunchKernelGGL(k_raster_cells, grid_of(n_cells), dim3(256), 0, c->stream, a);
-    else  // one workgroup per sub-block
-        hipLaunchKernelGGL(k_raster_cells_wg, dim3((unsigned)cell_sb.size()), dim3(256), 0, c->stream, a);
+    // (one lane per leaf cell; a workgroup-per-sub-block form with the candidate hexagons and corner
+    // images in LDS measured slower: 7.4 -> 9.6 ms for NYC res 9, profiles/r03_build_trace_v4.txt)
+    hipLaunchKernelGGL(k_raster_cells, grid_of(n_cells), dim3(256), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     rc.cells.resize((size_t)n_cells);
     HIP_TRY(hipMemcpyAsync(rc.cells.data(), d_cells.p, (size_t)n_cells * 2, hipMemcpyDeviceToHost, c->stream));
@@ -3718,6 +3614,9 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     trace.mark("chip rasters uploaded");
     ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + rb.hdr.size() * sizeof(raster::ChipHdr) +
                        rb.cells.size() * sizeof(raster::CellRec) + rb.edges.size() * sizeof(pip::Edge);
+    // the host-side build arrays (chip rasters, geometry store) are released off the return path
+    defer_free(std::move(rb));
+    defer_free(std::move(gb));
     *out = ch;
     return MOSAIC_OK;
 }
