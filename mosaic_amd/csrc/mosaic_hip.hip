@@ -4852,6 +4852,29 @@ __device__ inline int64_t clip_pass(const double* ixy, const int32_t* itag, int6
     return m;
 }
 
+// mosaic_tessellate_gpu's H3 clip polygons generated on the device: candidate k's hexagon around its
+// face-plane centre (cxy), each side cut into D pieces -- tessellate.cpp fill_clip's arithmetic
+// (corner = centre + offset; a + (b - a) t / D, no contraction), so the same doubles.
+struct FillClipArgs {
+    const double* cxy;
+    int64_t n_cand;
+    int D;
+    double dx[6], dy[6];
+    double* clip;  // [n_cand][6 D][2]
+};
+__global__ void __launch_bounds__(256) k_tess_fill_clip(FillClipArgs a) {
+    const int nv = 6 * a.D;
+    const int64_t total = a.n_cand * nv;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = w / nv;
+        const int v = (int)(w - k * nv), q = v / a.D, t = v - q * a.D, q1 = q + 1 == 6 ? 0 : q + 1;
+        const double cx = a.cxy[2 * k], cy = a.cxy[2 * k + 1];
+        const double ax = cx + a.dx[q], ay = cy + a.dy[q], bx = cx + a.dx[q1], by = cy + a.dy[q1];
+        a.clip[2 * w] = ax + (bx - ax) * t / a.D;
+        a.clip[2 * w + 1] = ay + (by - ay) * t / a.D;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_tess_clip(ClipArgs a) {
     const int lane = (int)(threadIdx.x & 63);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -5066,6 +5089,214 @@ int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return rc;
+}
+
+// ---- mosaic_tessellate_gpu's H3 branch as one device session: the geometry batch is uploaded once,
+// each chunk of candidates uploads only its centres (16 B each); clip polygons are generated on the
+// device (k_tess_fill_clip), classified (k_tess_classify_poly) and the border ones clipped
+// (k_tess_clip) from the same device arrays.
+struct tessclip::H3Session {
+    mosaic_ctx* ctx;
+    int64_t n_geoms, n_parts, n_rings, n_verts, maxn;
+    const int64_t *geom_parts, *part_rings, *ring_offsets;
+    int res, D;
+    double dx[6], dy[6];
+    DevBuf d_gp, d_pr, d_ro, d_pxy, d_gxy, d_gf, d_cg, d_cxy, d_clip, d_cls, d_tasks;
+    DevBuf d_sxy, d_stag, d_out, d_cnt, d_rings, d_parts, d_redo;
+    void release() {
+        for (DevBuf* b : {&d_gp, &d_pr, &d_ro, &d_pxy, &d_gxy, &d_gf, &d_cg, &d_cxy, &d_clip, &d_cls, &d_tasks, &d_sxy, &d_stag,
+                          &d_out, &d_cnt, &d_rings, &d_parts, &d_redo})
+            b->release();
+    }
+};
+
+int tessclip::h3_session_begin(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                               const int64_t* ring_offsets, const double* pxy, const double* gxy, const int32_t* gface,
+                               int res, int D, const double* dx, const double* dy, H3Session** out) {
+    ENTER(ctx);
+    if (!out || n_geoms < 0 || D < 1 || D > 64 || res < 0 || res > 15) return fail(MOSAIC_E_ARG, "invalid argument");
+    H3Session* S = new H3Session();
+    S->ctx = ctx;
+    S->n_geoms = n_geoms;
+    S->n_parts = geom_parts[n_geoms];
+    S->n_rings = part_rings[S->n_parts];
+    S->n_verts = ring_offsets[S->n_rings];
+    S->geom_parts = geom_parts;
+    S->part_rings = part_rings;
+    S->ring_offsets = ring_offsets;
+    S->res = res;
+    S->D = D;
+    for (int q = 0; q < 6; q++) {
+        S->dx[q] = dx[q];
+        S->dy[q] = dy[q];
+    }
+    S->maxn = 1;
+    for (int64_t r = 0; r < S->n_rings; r++) S->maxn = std::max<int64_t>(S->maxn, ring_offsets[r + 1] - ring_offsets[r]);
+    HIP_TRY(hipSetDevice(c->device));
+    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+        int e = b.reserve(std::max<size_t>(bytes, 16));
+        if (e) return e;
+        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        return MOSAIC_OK;
+    };
+    int rc;
+    if ((rc = up(S->d_gp, geom_parts, (size_t)(n_geoms + 1) * 8)) || (rc = up(S->d_pr, part_rings, (size_t)(S->n_parts + 1) * 8)) ||
+        (rc = up(S->d_ro, ring_offsets, (size_t)(S->n_rings + 1) * 8)) || (rc = up(S->d_pxy, pxy, (size_t)S->n_verts * 16)) ||
+        (rc = up(S->d_gxy, gxy, (size_t)S->n_verts * 16)) || (rc = up(S->d_gf, gface, (size_t)n_geoms * 4)) ||
+        (rc = S->d_cnt.reserve(32))) {
+        S->release();
+        delete S;
+        return rc;
+    }
+    *out = S;
+    return MOSAIC_OK;
+}
+
+void tessclip::h3_session_end(H3Session* S) {
+    if (!S) return;
+    ThreadCtx* c = enter(S->ctx);
+    if (c) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+    }
+    S->release();
+    delete S;
+}
+
+int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geom, const double* cxy, double eps,
+                               double area_eps, uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out) {
+    ENTER(S->ctx);
+    const int nv = 6 * S->D;
+    tasks.clear();
+    out->redo.clear();
+    out->rings.clear();
+    out->parts.clear();
+    out->verts.clear();
+    out->kernel_ms = 0;
+    if (nc <= 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+        int e = b.reserve(std::max<size_t>(bytes, 16));
+        if (e) return e;
+        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        return MOSAIC_OK;
+    };
+    if ((rc = up(S->d_cg, cand_geom, (size_t)nc * 4)) || (rc = up(S->d_cxy, cxy, (size_t)nc * 16)) ||
+        (rc = S->d_clip.reserve((size_t)nc * nv * 16)) || (rc = S->d_cls.reserve((size_t)nc)))
+        return rc;
+    tessgpu::FillClipArgs fa;
+    fa.cxy = (const double*)S->d_cxy.p;
+    fa.n_cand = nc;
+    fa.D = S->D;
+    for (int q = 0; q < 6; q++) {
+        fa.dx[q] = S->dx[q];
+        fa.dy[q] = S->dy[q];
+    }
+    fa.clip = (double*)S->d_clip.p;
+    const int64_t nfill = nc * nv;
+    hipLaunchKernelGGL(tessgpu::k_tess_fill_clip, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((nfill + 255) / 256, 1 << 20))),
+                       dim3(256), 0, c->stream, fa);
+    HIP_TRY(hipGetLastError());
+    tessgpu::ClassifyPolyArgs ca;
+    ca.xy = (const double*)S->d_pxy.p;
+    ca.ring_offsets = (const int64_t*)S->d_ro.p;
+    ca.part_rings = (const int64_t*)S->d_pr.p;
+    ca.geom_parts = (const int64_t*)S->d_gp.p;
+    ca.cand_geom = (const int32_t*)S->d_cg.p;
+    ca.clip = (const double*)S->d_clip.p;
+    ca.nv = nv;
+    ca.n_cand = nc;
+    ca.eps = eps;
+    ca.cls = (uint8_t*)S->d_cls.p;
+    const int64_t blocks = std::min<int64_t>((nc + 3) / 4, (int64_t)c->n_cu * 16);
+    EventGuard ev;
+    HIP_TRY(hipEventCreate(&ev.e[0]));
+    HIP_TRY(hipEventCreate(&ev.e[1]));
+    HIP_TRY(hipEventRecord(ev.e[0], c->stream));
+    hipLaunchKernelGGL(tessgpu::k_tess_classify_poly, dim3((unsigned)blocks), dim3(256), 0, c->stream, ca);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.e[1], c->stream));
+    HIP_TRY(hipMemcpyAsync(cls, S->d_cls.p, (size_t)nc, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    float cms = 0;
+    (void)hipEventElapsedTime(&cms, ev.e[0], ev.e[1]);
+    c->last_tess_classify_ms = cms;
+    // the border candidates, clipped on the device (tessclip::clip_border's kernel and sizing)
+    int64_t ring_cap = 0, part_cap = 0;
+    for (int64_t k = 0; k < nc; k++) {
+        if (cls[k] != 2) continue;
+        tasks.push_back(k);
+        const int g = cand_geom[k];
+        part_cap += S->geom_parts[g + 1] - S->geom_parts[g];
+        ring_cap += S->part_rings[S->geom_parts[g + 1]] - S->part_rings[S->geom_parts[g]];
+    }
+    const int64_t n_tasks = (int64_t)tasks.size();
+    out->redo.assign((size_t)n_tasks, 0);
+    if (n_tasks == 0) return MOSAIC_OK;
+    const int64_t cap = 2 * S->maxn + 4 * (int64_t)nv + 64, per_wave = 2 * cap * (16 + 4);
+    const int64_t n_waves = std::max<int64_t>(1, std::min<int64_t>({n_tasks, (int64_t)c->n_cu * 8, ((int64_t)2 << 30) / per_wave}));
+    // output bound: every ring of a task's geometry clipped by a convex nv-gon
+    int64_t task_verts = 0;
+    for (int64_t t = 0; t < n_tasks; t++) {
+        const int g = cand_geom[tasks[(size_t)t]];
+        task_verts += S->ring_offsets[S->part_rings[S->geom_parts[g + 1]]] - S->ring_offsets[S->part_rings[S->geom_parts[g]]];
+    }
+    const int64_t out_cap = 2 * task_verts + n_tasks * (3 * (int64_t)nv + 8) + 1024;
+    if ((rc = up(S->d_tasks, tasks.data(), (size_t)n_tasks * 8)) || (rc = S->d_sxy.reserve((size_t)(n_waves * 4 * cap) * 8)) ||
+        (rc = S->d_stag.reserve((size_t)(n_waves * 2 * cap) * 4)) || (rc = S->d_out.reserve((size_t)out_cap * 16)) ||
+        (rc = S->d_rings.reserve((size_t)std::max<int64_t>(ring_cap, 1) * sizeof(ClipRing))) ||
+        (rc = S->d_parts.reserve((size_t)std::max<int64_t>(part_cap, 1) * sizeof(ClipPart))) ||
+        (rc = S->d_redo.reserve((size_t)n_tasks)))
+        return rc;
+    HIP_TRY(hipMemsetAsync(S->d_cnt.p, 0, 32, c->stream));
+    tessgpu::ClipArgs a;
+    a.pxy = (const double*)S->d_pxy.p;
+    a.gxy = (const double*)S->d_gxy.p;
+    a.ring_offsets = (const int64_t*)S->d_ro.p;
+    a.part_rings = (const int64_t*)S->d_pr.p;
+    a.geom_parts = (const int64_t*)S->d_gp.p;
+    a.cand_geom = (const int32_t*)S->d_cg.p;
+    a.gface = (const int32_t*)S->d_gf.p;
+    a.clip = (const double*)S->d_clip.p;
+    a.nv = nv;
+    a.res = S->res;
+    a.mode = 0;
+    a.area_eps = area_eps;
+    a.tasks = (const int64_t*)S->d_tasks.p;
+    a.n_tasks = n_tasks;
+    a.sxy = (double*)S->d_sxy.p;
+    a.stag = (int32_t*)S->d_stag.p;
+    a.cap = cap;
+    a.out = (double*)S->d_out.p;
+    a.counters = (unsigned long long*)S->d_cnt.p;
+    a.out_cap = out_cap;
+    a.ring_cap = ring_cap;
+    a.part_cap = part_cap;
+    a.rings = (ClipRing*)S->d_rings.p;
+    a.parts = (ClipPart*)S->d_parts.p;
+    a.redo = (uint8_t*)S->d_redo.p;
+    HIP_TRY(hipEventRecord(ev.e[0], c->stream));
+    hipLaunchKernelGGL(tessgpu::k_tess_clip, dim3((unsigned)((n_waves + 3) / 4)), dim3(256), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.e[1], c->stream));
+    unsigned long long cnt[3];
+    HIP_TRY(hipMemcpyAsync(cnt, S->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out->redo.data(), S->d_redo.p, (size_t)n_tasks, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int64_t nv_out = std::min<int64_t>((int64_t)cnt[0], out_cap), nr = std::min<int64_t>((int64_t)cnt[1], ring_cap),
+                  np = std::min<int64_t>((int64_t)cnt[2], part_cap);
+    out->verts.resize((size_t)nv_out * 2);
+    out->rings.resize((size_t)nr);
+    out->parts.resize((size_t)np);
+    if (nv_out) HIP_TRY(hipMemcpyAsync(out->verts.data(), S->d_out.p, (size_t)nv_out * 16, hipMemcpyDeviceToHost, c->stream));
+    if (nr) HIP_TRY(hipMemcpyAsync(out->rings.data(), S->d_rings.p, (size_t)nr * sizeof(ClipRing), hipMemcpyDeviceToHost, c->stream));
+    if (np) HIP_TRY(hipMemcpyAsync(out->parts.data(), S->d_parts.p, (size_t)np * sizeof(ClipPart), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ev.e[0], ev.e[1]);
+    out->kernel_ms = ms;
+    return MOSAIC_OK;
 }
 
 extern "C" {

@@ -41,5 +41,18 @@ int clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, con
                 int64_t n_tasks, const int64_t* tasks, const int32_t* cand_geom, int64_t n_cand, const double* clip, int nv,
                 double area_eps, ClipResult* out);
 
+// mosaic_tessellate_gpu's H3 branch as one device session (mosaic_hip.hip): the geometry batch (rings
+// in the face plane and in lon / lat, each geometry's face) is uploaded once; per chunk of candidates
+// (geometry, face-plane centre) the hexagon clip polygons (D pieces per side, corner offsets dx / dy)
+// are generated on the device, classified (cls: 0 dropped, 1 core, 2 border) and the border ones
+// clipped (tasks: their candidate indices; out as clip_border's).
+struct H3Session;
+int h3_session_begin(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                     const int64_t* ring_offsets, const double* pxy, const double* gxy, const int32_t* gface, int res, int D,
+                     const double* dx, const double* dy, H3Session** out);
+int h3_session_chunk(H3Session* s, int64_t n_cand, const int32_t* cand_geom, const double* cxy, double eps,
+                     double area_eps, uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out);
+void h3_session_end(H3Session* s);
+
 }  // namespace tessclip
 }  // namespace mosaic

@@ -95,6 +95,9 @@ struct FacePlane {
     P2 to_hex(double lon, double lat) const {
         double p[3];
         unit(lon, lat, p);
+        return to_hex_unit(p);
+    }
+    P2 to_hex_unit(const double p[3]) const {
         double d = fc[0] * p[0] + fc[1] * p[1] + fc[2] * p[2];
         return {S * (ei[0] * p[0] + ei[1] * p[1] + ei[2] * p[2]) / d, S * (ep[0] * p[0] + ep[1] * p[1] + ep[2] * p[2]) / d};
     }
@@ -107,9 +110,7 @@ struct FacePlane {
     }
 };
 
-int face_of(double lon, double lat) {
-    double p[3];
-    FacePlane::unit(lon, lat, p);
+int face_of_unit(const double p[3]) {
     int best = 0;
     double bd = -2;
     for (int f = 0; f < 20; f++) {
@@ -121,6 +122,11 @@ int face_of(double lon, double lat) {
         }
     }
     return best;
+}
+int face_of(double lon, double lat) {
+    double p[3];
+    FacePlane::unit(lon, lat, p);
+    return face_of_unit(p);
 }
 
 // The hexagon corner offsets R cos(30 + 60 k deg), R sin(...), k = 0..5: the same expressions as the
@@ -225,12 +231,18 @@ struct WkbOut {
     std::vector<uint8_t> b;
     void u8(uint8_t v) { b.push_back(v); }
     void u32(uint32_t v) {
-        for (int i = 3; i >= 0; i--) b.push_back((uint8_t)(v >> (8 * i)));
+        const size_t n = b.size();
+        b.resize(n + 4);
+        v = __builtin_bswap32(v);
+        memcpy(b.data() + n, &v, 4);
     }
     void f64(double d) {
         uint64_t u;
         memcpy(&u, &d, 8);
-        for (int i = 7; i >= 0; i--) b.push_back((uint8_t)(u >> (8 * i)));
+        const size_t n = b.size();
+        b.resize(n + 8);
+        u = __builtin_bswap64(u);
+        memcpy(b.data() + n, &u, 8);
     }
     void polygon(const std::vector<std::vector<P2>>& rings) {
         u8(0);
@@ -606,40 +618,72 @@ struct ClippedChips {
     tessclip::ClipResult r;
     std::vector<int64_t> task_of;  // candidate -> task (-1: not a border task)
     void index(int64_t n_cand, const std::vector<int64_t>& tasks) {
-        std::sort(r.rings.begin(), r.rings.end(), [](const tessclip::ClipRing& a, const tessclip::ClipRing& b) {
-            return a.cand != b.cand ? a.cand < b.cand : (a.part != b.part ? a.part < b.part : a.ring < b.ring);
+        // stable counting sort by candidate (the kernel appends each candidate's rings / parts in
+        // (part, ring) order from one wave; a candidate whose entries are not is sorted on its own)
+        auto by_cand = [&](auto& v, auto less) {
+            std::vector<int64_t> start((size_t)n_cand + 1, 0);
+            for (auto& e : v) start[(size_t)e.cand + 1]++;
+            for (int64_t c = 0; c < n_cand; c++) start[(size_t)c + 1] += start[(size_t)c];
+            std::remove_reference_t<decltype(v)> out(v.size());
+            std::vector<int64_t> pos(start.begin(), start.end() - 1);
+            for (auto& e : v) out[(size_t)pos[(size_t)e.cand]++] = e;
+            for (int64_t c = 0; c < n_cand; c++) {
+                auto b = out.begin() + start[(size_t)c], e = out.begin() + start[(size_t)c + 1];
+                if (!std::is_sorted(b, e, less)) std::sort(b, e, less);
+            }
+            v.swap(out);
+        };
+        by_cand(r.rings, [](const tessclip::ClipRing& a, const tessclip::ClipRing& b) {
+            return a.part != b.part ? a.part < b.part : a.ring < b.ring;
         });
-        std::sort(r.parts.begin(), r.parts.end(), [](const tessclip::ClipPart& a, const tessclip::ClipPart& b) {
-            return a.cand != b.cand ? a.cand < b.cand : a.part < b.part;
-        });
+        by_cand(r.parts, [](const tessclip::ClipPart& a, const tessclip::ClipPart& b) { return a.part < b.part; });
         task_of.assign((size_t)n_cand, -1);
         for (size_t t = 0; t < tasks.size(); t++) task_of[(size_t)tasks[t]] = (int64_t)t;
     }
     bool redo(int64_t k) const { return task_of[(size_t)k] < 0 || r.redo[(size_t)task_of[(size_t)k]]; }
-    // candidate k's chip (any order: its first ring and part by binary search); false: no chip
-    bool chip(int64_t k, std::vector<uint8_t>& wkb) const {
+    // candidate k's chip as WKB appended to w (to_wkb's bytes); false (nothing written): no chip
+    bool chip(int64_t k, WkbOut& w) const {
         const size_t ir = (size_t)(std::lower_bound(r.rings.begin(), r.rings.end(), k,
                                                     [](const tessclip::ClipRing& a, int64_t c) { return a.cand < c; }) -
                                    r.rings.begin());
         const size_t ip = (size_t)(std::lower_bound(r.parts.begin(), r.parts.end(), k,
                                                     [](const tessclip::ClipPart& a, int64_t c) { return a.cand < c; }) -
                                    r.parts.begin());
-        std::vector<std::vector<std::vector<P2>>> parts;
-        size_t jr = ir;
+        // the kept parts that have rings: (first ring, ring count)
+        std::pair<size_t, size_t> kept[64];
+        std::vector<std::pair<size_t, size_t>> more;
+        size_t n_kept = 0, jr = ir;
         for (size_t jp = ip; jp < r.parts.size() && r.parts[jp].cand == k; jp++) {
             const int32_t part = r.parts[jp].part;
             while (jr < r.rings.size() && r.rings[jr].cand == k && r.rings[jr].part < part) jr++;
-            std::vector<std::vector<P2>> rings;
-            for (; jr < r.rings.size() && r.rings[jr].cand == k && r.rings[jr].part == part; jr++) {
-                const tessclip::ClipRing& cr = r.rings[jr];
-                std::vector<P2> ring((size_t)cr.n);
-                for (int32_t i = 0; i < cr.n; i++) ring[(size_t)i] = P2{r.verts[2 * (cr.off + i)], r.verts[2 * (cr.off + i) + 1]};
-                rings.push_back(std::move(ring));
-            }
-            if (r.parts[jp].keep && !rings.empty()) parts.push_back(std::move(rings));
+            const size_t r0 = jr;
+            while (jr < r.rings.size() && r.rings[jr].cand == k && r.rings[jr].part == part) jr++;
+            if (!r.parts[jp].keep || jr == r0) continue;
+            if (n_kept < 64) kept[n_kept] = {r0, jr - r0};
+            else more.push_back({r0, jr - r0});
+            n_kept++;
         }
-        if (parts.empty()) return false;
-        wkb = to_wkb(parts);
+        if (n_kept == 0) return false;
+        auto part_at = [&](size_t i) { return i < 64 ? kept[i] : more[i - 64]; };
+        if (n_kept > 1) {
+            w.u8(0);
+            w.u32(6);
+            w.u32((uint32_t)n_kept);
+        }
+        for (size_t i = 0; i < n_kept; i++) {
+            const auto pr = part_at(i);
+            w.u8(0);
+            w.u32(3);
+            w.u32((uint32_t)pr.second);
+            for (size_t q = pr.first; q < pr.first + pr.second; q++) {
+                const tessclip::ClipRing& cr = r.rings[q];
+                w.u32((uint32_t)cr.n);
+                for (int32_t v = 0; v < cr.n; v++) {
+                    w.f64(r.verts[2 * (cr.off + v)]);
+                    w.f64(r.verts[2 * (cr.off + v) + 1]);
+                }
+            }
+        }
         return true;
     }
 };
@@ -813,8 +857,12 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         const int64_t v0 = ring_offsets[part_rings[geom_parts[g]]], v1 = ring_offsets[part_rings[geom_parts[g + 1]]];
         if (v0 == v1) return;
         int face = -1;
+        // unit vectors once per vertex (face test and projection: the same doubles as face_of / to_hex)
+        std::vector<double> u((size_t)(v1 - v0) * 3);
         for (int64_t v = v0; v < v1; v++) {
-            int f = face_of(xy[2 * v], xy[2 * v + 1]);
+            double* pu = u.data() + 3 * (v - v0);
+            FacePlane::unit(xy[2 * v], xy[2 * v + 1], pu);
+            int f = face_of_unit(pu);
             if (face < 0) face = f;
             out.multi = out.multi || f != face;
         }
@@ -824,7 +872,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         fp.init(face, res);
         double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
         for (int64_t v = v0; v < v1; v++) {
-            P2 p = fp.to_hex(xy[2 * v], xy[2 * v + 1]);
+            P2 p = fp.to_hex_unit(u.data() + 3 * (v - v0));
             pxy[2 * v] = p.x;
             pxy[2 * v + 1] = p.y;
             x0 = std::min(x0, p.x);
@@ -872,7 +920,6 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     // (<= 64 MB of them per chunk) for any densify and envelope; chips come out in candidate order
     const int64_t n_cand = (int64_t)cg.size();
     const int64_t chunk = std::max<int64_t>(1, ((int64_t)64 << 20) / ((int64_t)nv * 16));
-    std::vector<double> clip;
     std::vector<uint8_t> cls;
     std::vector<int64_t> tasks;
     mosaic_chip_set* cs = new mosaic_chip_set();
@@ -897,27 +944,32 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         }
         return MOSAIC_OK;
     };
-    for (int64_t k0 = 0; k0 < n_cand; k0 += chunk) {
-        const int64_t nc = std::min<int64_t>(chunk, n_cand - k0);
-        clip.resize((size_t)nc * nv * 2);
-        for (int64_t k = 0; k < nc; k++) fill_clip(k0 + k, clip.data() + 2 * (size_t)nv * k);
-        cls.assign((size_t)nc, 0);
-        trace.add(0);
-        int rc = mosaic_tess_classify_poly(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), nc,
-                                           cg.data() + k0, clip.data(), nv, 1e-3, cls.data());
-        trace.add(1);
-        if (rc) {
+    // one device session for the batch: geometry uploaded once, per chunk only the candidate centres;
+    // clip polygons generated, classified and the border ones clipped on the device
+    tessclip::H3Session* S = nullptr;
+    struct SessionEnd {
+        tessclip::H3Session*& s;
+        ~SessionEnd() { tessclip::h3_session_end(s); }
+    } session_end{S};
+    if (n_cand > 0) {
+        if (int rc = tessclip::h3_session_begin(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), xy,
+                                                gface.data(), res, D, hex_corners().dx, hex_corners().dy, &S)) {
             delete cs;
             return rc;
         }
-        // border cells clipped on the GPU (k_tess_clip); a cell the kernel could not finish is clipped here
-        tasks.clear();
-        for (int64_t k = 0; k < nc; k++)
-            if (cls[k] == 2) tasks.push_back(k);
+    }
+    trace.mark("h3 session upload");
+    double clip_kernel_ms = 0;
+    for (int64_t k0 = 0; k0 < n_cand; k0 += chunk) {
+        const int64_t nc = std::min<int64_t>(chunk, n_cand - k0);
+        cls.assign((size_t)nc, 0);
+        trace.add(0);
         ClippedChips cc;
-        if ((rc = tessclip::clip_border(ctx, n_geoms, geom_parts, part_rings, ring_offsets, pxy.data(), xy, gface.data(), res,
-                                        0, (int64_t)tasks.size(), tasks.data(), cg.data() + k0, nc, clip.data(), nv, 1e-12,
-                                        &cc.r))) {
+        int rc = tessclip::h3_session_chunk(S, nc, cg.data() + k0, cxy.data() + 2 * (size_t)k0, 1e-3, 1e-12, cls.data(),
+                                            tasks, &cc.r);
+        trace.add(1);
+        clip_kernel_ms += cc.r.kernel_ms;
+        if (rc) {
             delete cs;
             return rc;
         }
@@ -927,26 +979,33 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         // the chunk's chips on host threads (each candidate's chip is independent: GPU-clipped border
         // chips to WKB, core chips' outlines, cells the GPU clipper left to the host), then appended
         // in candidate order
+        // thread t takes candidates [nc t / nt, nc (t + 1) / nt) and appends their WKB to its own buffer,
+        // so the buffers concatenated in thread order are the chunk's WKB in candidate order
         struct OneChip {
-            bool has = false, core = false;
-            std::vector<uint8_t> blob;
+            int64_t off = 0;  // in the thread's buffer
+            int32_t len = -1;  // -1: no chip
+            uint8_t core = 0;
         };
         std::vector<OneChip> chips((size_t)nc);
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
+            std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), nc / 256));
+        std::vector<WkbOut> bufs((size_t)nt);
         {
-            const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
-                std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), nc / 256));
             auto work = [&](int t) {
                 std::vector<std::vector<std::vector<P2>>> geo, pl;
                 FacePlane fp;
                 fp.init(0, res);
                 int64_t cur = -1;
                 mosaic_chip_set tmp;
+                std::vector<double> P((size_t)nv * 2);  // the cell's clip polygon (core / host-clipped cells)
+                WkbOut& w = bufs[(size_t)t];
                 for (int64_t kk = nc * t / nt; kk < nc * (t + 1) / nt; kk++) {
                     const int64_t k = k0 + kk;
                     OneChip& o = chips[(size_t)kk];
                     if (!cls[kk]) continue;
+                    o.off = (int64_t)w.b.size();
                     if (cls[kk] == 2 && !cc.redo(kk)) {
-                        o.has = cc.chip(kk, o.blob);
+                        if (cc.chip(kk, w)) o.len = (int32_t)((int64_t)w.b.size() - o.off);
                         continue;
                     }
                     if (cg[k] != cur) {
@@ -970,7 +1029,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
                         }
                     }
                     Cell cell;
-                    const double* P = clip.data() + 2 * (size_t)nv * kk;
+                    fill_clip(k, P.data());
                     for (int v = 0; v < nv; v++) cell.outline.push_back({P[2 * v], P[2 * v + 1]});
                     cell.clip = cell.outline;
                     cell.id = cid[k];
@@ -982,9 +1041,9 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
                     emit_cell(&tmp, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); },
                               1e-12, (int)cls[kk]);
                     if (!tmp.index_id.empty()) {
-                        o.has = true;
                         o.core = tmp.is_core[0] != 0;
-                        o.blob.assign(tmp.wkb.begin(), tmp.wkb.end());
+                        w.b.insert(w.b.end(), tmp.wkb.begin(), tmp.wkb.end());
+                        o.len = (int32_t)tmp.wkb.size();
                     }
                 }
             };
@@ -994,14 +1053,40 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             for (auto& th : pool) th.join();
         }
         trace.add(4);
-        for (int64_t kk = 0; kk < nc; kk++) {
-            const int64_t k = k0 + kk;
-            if (!multi_geoms.empty() && (rc = flush_multi(cg[k]))) {
-                delete cs;
-                return rc;
+        int64_t n_chips = 0, n_bytes = 0;
+        for (auto& o : chips)
+            if (o.len >= 0) n_chips++, n_bytes += o.len;
+        cs->is_core.reserve(cs->is_core.size() + (size_t)n_chips);
+        cs->index_id.reserve(cs->index_id.size() + (size_t)n_chips);
+        cs->key.reserve(cs->key.size() + (size_t)n_chips);
+        cs->wkb_offsets.reserve(cs->wkb_offsets.size() + (size_t)n_chips);
+        cs->wkb.reserve(cs->wkb.size() + (size_t)n_bytes);
+        for (int t = 0; t < nt; t++) {
+            const std::vector<uint8_t>& b = bufs[(size_t)t].b;
+            const size_t wkb0 = cs->wkb.size();
+            // face-spanning geometries are emitted between chips: then chip by chip
+            const bool interleaved = !multi_geoms.empty();
+            for (int64_t kk = nc * t / nt; kk < nc * (t + 1) / nt; kk++) {
+                const int64_t k = k0 + kk;
+                if (interleaved && (rc = flush_multi(cg[k]))) {
+                    delete cs;
+                    return rc;
+                }
+                const OneChip& o = chips[(size_t)kk];
+                if (o.len < 0) continue;
+                cs->is_core.push_back(o.core);
+                cs->index_id.push_back(cid[k]);
+                cs->key.push_back(cg[k]);
+                if (interleaved) {
+                    cs->wkb.insert(cs->wkb.end(), b.begin() + o.off, b.begin() + o.off + o.len);
+                    cs->wkb_offsets.push_back((int64_t)cs->wkb.size());
+                } else {
+                    cs->wkb_offsets.push_back((int64_t)(wkb0 + (size_t)o.off + (size_t)o.len));
+                }
             }
-            if (chips[(size_t)kk].has) cs->add(chips[(size_t)kk].core, cid[k], cg[k], chips[(size_t)kk].blob);
+            if (!interleaved) cs->wkb.insert(cs->wkb.end(), b.begin(), b.end());
         }
+        trace.add(5);
     }
     if (int rc = flush_multi(n_geoms)) {
         delete cs;
@@ -1009,9 +1094,9 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     }
     trace.add(5);
     if (trace.on)
-        fprintf(stderr, "[tess] clip polygons %.3f ms, classify %.3f ms, gpu clip %.3f ms, index clips %.3f ms, "
+        fprintf(stderr, "[tess] chunk setup %.3f ms, device classify + clip %.3f ms (clip kernel %.3f ms), index clips %.3f ms, "
                         "chip WKB (threads) %.3f ms, append %.3f ms\n",
-                trace.acc[0], trace.acc[1], trace.acc[2], trace.acc[3], trace.acc[4], trace.acc[5]);
+                trace.acc[0], trace.acc[1], clip_kernel_ms, trace.acc[3], trace.acc[4], trace.acc[5]);
     *out = cs;
     return MOSAIC_OK;
 }
@@ -1090,7 +1175,8 @@ int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, c
     for (int64_t k = 0; k < n_cand; k++) {
         if (!cls[k]) continue;
         if (cls[k] == 2 && !cc.redo(k)) {
-            if (cc.chip(k, blob)) cs->add(false, cid[k], cg[k], blob);
+            WkbOut w;
+            if (cc.chip(k, w)) cs->add(false, cid[k], cg[k], w.b);
             continue;
         }
         if (cg[k] != cur) {
