@@ -216,6 +216,11 @@ __device__ inline v4u gather_b128(__amdgpu_buffer_rsrc_t r, bool need, uint32_t 
 #ifndef MOSAIC_FIXED
 #define MOSAIC_FIXED 1
 #endif
+// MOSAIC_LATE_ISSUE 1: every gather issued at the end of the iteration (see issue_leaf); measured
+// slower (C2 stream 3.33 -> 3.47 ms, profiles/r03_kbench_late_issue.txt), kept for measurement builds
+#ifndef MOSAIC_LATE_ISSUE
+#define MOSAIC_LATE_ISSUE 0
+#endif
 struct PipeGroup {
 #if MOSAIC_FIXED
     uint32_t gx[4], gy[4];  // fixed-point fine-cell coordinates (kFixBits fraction bits)
@@ -262,6 +267,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     uint32_t wn = 0;
     const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u;
     const double gx0 = -s.x0 * s.sxC, gy0 = -s.y0 * s.syC;
+    const uint32_t spill = (uint32_t)(a.n_polygons + lane);  // the lane's spill word (LDS counts)
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
     const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
     // full groups of this wave: wbase + t stride, t < T
@@ -310,6 +316,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const uint32_t off = ((((g.qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
 #if MOSAIC_ABL == 1 || MOSAIC_ABL == 2
             g.code[k] = off & 1u;  // ablation: no sub-block gathers
+#elif MOSAIC_LATE_ISSUE
+            g.code[k] = g.qv[k] >= 0x8000u ? off : kNoLoad;  // gathered by issue_gathers
 #else
             g.code[k] = gather_b16<MOSAIC_AUX_SUB>(rsub, g.qv[k] >= 0x8000u, off);
 #endif
@@ -334,6 +342,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #if MOSAIC_ABL >= 1 && MOSAIC_ABL <= 3
             g.leaf[k] = loff & 1u;  // ablation: no leaf / line gathers
             g.lrec[k] = v4u{roff, loff, 0u, 0u};
+#elif MOSAIC_LATE_ISSUE
+            g.leaf[k] = blk && !line ? loff : kNoLoad;  // gathered by issue_gathers
+            g.lrec[k].x = line ? roff : kNoLoad;
 #else
             g.leaf[k] = gather_b16<MOSAIC_AUX_LEAF>(rblk, blk && !line, loff);
             g.lrec[k] = gather_b128<MOSAIC_AUX_LINE>(rblk, line, roff);
@@ -370,8 +381,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (LDS_COUNTS && !PAIRS) {
-                const uint32_t slot = code[k] - 1u < kPipeNonFinite - 1u ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
-                #if MOSAIC_ABL == 4
+                // keys are < n_polygons <= 8192; 0 (no pair) wraps to 0xffffffff and kMixed / non-finite
+                // codes are >= kPipeNonFinite: both land on the lane's spill word
+                const uint32_t slot = min(code[k] - 1u, spill);
+#if MOSAIC_ABL == 4
                 abl_acc += slot;  // ablation: no LDS count atomics
 #else
                 atomicAdd(&lds[slot], 1u);
@@ -419,23 +432,63 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         g0.u[k] = g1.u[k] = g0.v[k] = g1.v[k] = 0.0f;
 #endif
     }
-    auto step = [&](int64_t t, PipeGroup& gfin, PipeGroup& gadv, Coords& cb, Coords& cn) {
+    // MOSAIC_LATE_ISSUE: stages B and A only compute their gather offsets (kNoLoad: none); the
+    // gathers of both are issued here, after every wait of the iteration.  A gather issued only by
+    // the lanes that need it is a branch, so the compiler cannot count it in vmcnt: any wait placed
+    // after one becomes vmcnt(0).  Issued in the middle of the iteration (stage B before stage A),
+    // the leaf / line gathers were waited for by stage A's wait on the coordinates, i.e. they had no
+    // latency budget at all; issued last, every load has the whole next iteration's latency budget.
+    auto issue_leaf = [&](PipeGroup& g) {
+#if MOSAIC_LATE_ISSUE && MOSAIC_ABL == 0
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t lo = g.leaf[k], ro = g.lrec[k].x;
+            g.leaf[k] = gather_b16<MOSAIC_AUX_LEAF>(rblk, lo != kNoLoad, lo);
+            g.lrec[k] = gather_b128<MOSAIC_AUX_LINE>(rblk, ro != kNoLoad, ro);
+        }
+#endif
+    };
+    auto issue_sub = [&](PipeGroup& g) {
+#if MOSAIC_LATE_ISSUE && MOSAIC_ABL == 0
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t so = g.code[k];
+            g.code[k] = gather_b16<MOSAIC_AUX_SUB>(rsub, so != kNoLoad, so);
+        }
+#endif
+    };
+    // VALID: group t is a full group of this wave (t < T) -- a compile-time constant, so the main loop
+    // carries no per-point validity test (only the two drain steps run with VALID false)
+    auto step = [&](auto VALID, int64_t t, PipeGroup& gfin, PipeGroup& gadv, Coords& cb, Coords& cn) {
         const bool all[4] = {true, true, true, true};
         if (t >= 2) stage_d(gfin, wbase + (t - 2) * stride);
         stage_b(gadv);  // (invalid groups gather nothing)
         const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
         const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
-        stage_a(x, y, all, t < T, gfin);
+        stage_a(x, y, all, decltype(VALID)::value, gfin);
+        issue_leaf(gadv);
+        issue_sub(gfin);
         if (MOSAIC_PIPE_DEPTH == 2) load4(cb, wbase + (t + 2) * stride, t + 2 < T);  // cb is free again
         else load4(cn, wbase + (t + 1) * stride, t + 1 < T);
     };
     if (T > 0) {
         load4(cb0, wbase, true);
         if (MOSAIC_PIPE_DEPTH == 2) load4(cb1, wbase + stride, 1 < T);
-        for (int64_t t = 0; t < T + 2; t += 2) {
-            step(t, g0, g1, cb0, cb1);
-            if (t + 1 >= T + 2) break;
-            step(t + 1, g1, g0, cb1, cb0);
+        const std::true_type full;
+        const std::false_type drain;
+        int64_t t = 0;
+        for (; t + 2 <= T; t += 2) {
+            step(full, t, g0, g1, cb0, cb1);
+            step(full, t + 1, g1, g0, cb1, cb0);
+        }
+        // groups t .. T - 1 (none or one) and the two drain steps (t = T, T + 1)
+        if (t < T) {
+            step(full, t, g0, g1, cb0, cb1);
+            step(drain, t + 1, g1, g0, cb1, cb0);
+            step(drain, t + 2, g0, g1, cb0, cb1);
+        } else {
+            step(drain, t, g0, g1, cb0, cb1);
+            step(drain, t + 1, g1, g0, cb1, cb0);
         }
     }
     // the wave's partial group (rows past its last full group), unpipelined
@@ -452,7 +505,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         }
         PipeGroup g;
         stage_a(x, y, live, true, g);
+        issue_sub(g);
         stage_b(g);
+        issue_leaf(g);
         stage_d(g, wt);
     }
     if (MOSAIC_ABL == 4 && abl_acc == 0xdeadbeefu) lds[0] = 1u;
@@ -464,6 +519,248 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     }
 }
 
+
+// ---- k_join_stream_cpt: k_join_stream_pipe with the rows that need gathers compacted.  87.6 % of
+// uniform NYC points are decided by the LDS levels alone (the quad level and its records), yet the
+// pipe kernel runs the sub-block / leaf / line stages -- about half of its VALU instructions -- on all
+// 256 rows of every group, since a wave instruction costs the same however few lanes need it.  Here
+// stage A decides and counts the LDS-resolved rows at once and moves the others ("pending": quad entry
+// >= 0x8000) into one 64-lane set with ds_permute (no LDS memory: per row slot k, a rotation of the
+// stable partition pending / not pending, so every lane sends and receives exactly one value); the
+// set's sub-block gather, leaf / line gathers and answers then take one lane per pending row.  The
+// set is software-pipelined like the pipe kernel's groups (iteration t: finish the set of t - 2, turn
+// the set of t - 1's sub-block entries into leaf / line gathers, run group t through the LDS levels,
+// compact it and gather its sub-block entries, load group t + 1).  Pending rows beyond 64 in a group
+// (clustered input) are finished at once, unpipelined.  Per pending row the set carries: the low L =
+// cs + kFixBits + qs bits of both fixed-point fine-cell coordinates (leaf cell, line offsets and the
+// sub-block within the quad; L <= 20), the source lane and row slot, the quad entry and the tile.
+// Same answers as k_join_stream_pipe, point for point.
+struct CptSet {
+    uint32_t a;     // ix low bits | source lane << 20 | row slot k << 26
+    uint32_t b;     // iy low bits
+    uint32_t c;     // quad entry | tile index << 16
+    uint32_t code;  // A -> B: gathered sub-block entry; B -> D: the answer, 0 for leaf rows, or kPipeLine
+    uint32_t leaf;  // gathered leaf code
+    v4u lrec;       // gathered line record
+};
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_cpt(JoinArgs a, StreamArgs s) {
+    extern __shared__ unsigned int lds[];
+    const int nwaves = (int)(blockDim.x >> 6);
+    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
+    uint32_t* stage = lds + ncw;
+    uint32_t* tb = stage + nwaves * s.stage_words;
+    uint32_t* quadw = tb + s.n_tiles;
+    const uint16_t* quad = (const uint16_t*)quadw;
+    uint32_t* qmask = quadw + s.n_quad_words;
+    const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
+    lds_fill(quadw, s.quad, s.n_quad_words);
+    lds_fill(qmask, s.qrec, s.n_qrec_words);
+    lds_fill(tb, s.tile_base, s.n_tiles);
+    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
+    const __amdgpu_buffer_rsrc_t rblk = stream_rsrc(s.blocks, s.blocks_bytes);
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t* wq = stage + wave * s.stage_words;
+    uint32_t wn = 0;
+    constexpr int F = tiles::kFixBits;
+    const uint32_t cs = (uint32_t)s.cs, qs = (uint32_t)s.qs;
+    const uint32_t lowm = (1u << (cs + F + qs)) - 1u;
+    const uint32_t spill = (uint32_t)(a.n_polygons + lane);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
+    const int64_t T = wbase + 256 <= a.n ? (a.n - 256 - wbase) / stride + 1 : 0;
+    // a row's answer: count it (LDS) or emit the pair; kMixed / non-finite rows (>= kPipeNonFinite)
+    // are returned to the caller's mixed-row stage
+    auto answer = [&](uint32_t code, int64_t row) {
+        if (LDS_COUNTS && !PAIRS) {
+            atomicAdd(&lds[min(code - 1u, spill)], 1u);  // 0 wraps, mixed codes >= kPipeNonFinite: spill
+        } else if (code - 1u < kPipeNonFinite - 1u) {
+            emit_hit<LDS_COUNTS, PAIRS>(a, row, code - 1u, lds);
+        }
+    };
+    // --- set stages
+    // A: the sub-block gather (pending rows: quad entry >= 0x8000)
+    auto set_a = [&](CptSet& z) {
+        const uint32_t q = z.c & 0xffffu;
+        const uint32_t local = (__builtin_amdgcn_ubfe(z.b, cs + F, qs) << qs) | __builtin_amdgcn_ubfe(z.a, cs + F, qs);
+        const uint32_t off = (((q & 0x7fffu) << (2 * qs)) + local) << 1;
+        z.code = gather_b16<MOSAIC_AUX_SUB>(rsub, q >= 0x8000u, off);
+    };
+    // B: sub-block entry -> leaf / line gather
+    auto set_b = [&](CptSet& z) {
+        const uint32_t q = z.c & 0xffffu;
+        const uint32_t c = q >= 0x8000u ? z.code : q;
+        const bool blk = c - 0x8000u < 0x7fffu;
+        const bool line = blk && (c & 0x4000u);
+        const uint32_t n = c & 0x3fffu;
+        const uint32_t lf = (__builtin_amdgcn_ubfe(z.b, (uint32_t)F, cs) << cs) | __builtin_amdgcn_ubfe(z.a, (uint32_t)F, cs);
+        const uint32_t tbv = tb[z.c >> 16];
+        const uint32_t loff = (tbv + (n << (2 * cs)) + lf) << 1;
+        const uint32_t roff = (tbv - 8u * (n + 1u)) << 1;
+        z.leaf = gather_b16<MOSAIC_AUX_LEAF>(rblk, blk && !line, loff);
+        z.lrec = gather_b128<MOSAIC_AUX_LINE>(rblk, line, roff);
+        z.code = line ? kPipeLine : (blk ? 0u : c);
+    };
+    // D: answers of the set's rows (group base wb)
+    auto set_d = [&](CptSet& z, int64_t wb) {
+        const uint32_t fb = cs + (uint32_t)F;
+        const float u = (float)__builtin_amdgcn_ubfe(z.a, 0u, fb) * (1.0f / (float)(1 << F));
+        const float v = (float)__builtin_amdgcn_ubfe(z.b, 0u, fb) * (1.0f / (float)(1 << F));
+        const float sv = fmaf(__uint_as_float(z.lrec.x), u, fmaf(__uint_as_float(z.lrec.y), v, __uint_as_float(z.lrec.z)));
+        const uint32_t pos = z.lrec.w & 0xffffu, neg = z.lrec.w >> 16;
+        uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
+        lc = sv <= -1.0f ? neg : lc;
+        const uint32_t code = z.code == kPipeLine ? lc : (z.code | z.leaf);
+        const uint32_t src = (z.a >> 20) & 63u, k = z.a >> 26;
+        const int64_t row = wb + (int64_t)((k >> 1) * 128u + 2u * src + (k & 1u));
+        answer(code, row);
+        const bool m = code >= kPipeNonFinite;
+        if (__ballot(m)) {
+            const unsigned long long mm = __ballot(m);
+            if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row - a.row_lo);
+            wn += (uint32_t)__popcll(mm);
+            stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
+        }
+    };
+    // --- stage A of a group: LDS levels, resolved rows answered, pending rows compacted into z (the
+    // first 64); more than 64 pending rows: the rest finished here
+    auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, CptSet& z, int64_t wb) {
+        uint32_t fa[4], fb[4], fc[4];
+        bool pend[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t ixC = min(tiles::fix_cvt(fma(x[k], s.sxF, s.gx0F)), (uint32_t)s.gxmaxF);
+            const uint32_t iyC = min(tiles::fix_cvt(fma(y[k], s.syF, s.gy0F)), (uint32_t)s.gymaxF);
+            const uint32_t q0 = quad_lookup<F>(s, quad, qmask, qcode, ixC, iyC);
+            const uint32_t q = valid && live[k] ? q0 : 0u;
+            const uint32_t tile = __umul24(iyC >> (s.tsh + F), (uint32_t)s.tnx) + (ixC >> (s.tsh + F));
+            // resolved rows (codes < 0x8000: 0 or key + 1); pending rows add to the spill word now
+            // and are counted when their answer is known
+            if (LDS_COUNTS && !PAIRS) atomicAdd(&lds[min(q - 1u, spill)], 1u);
+            else if (q - 1u < kPipeNonFinite - 1u) emit_hit<LDS_COUNTS, PAIRS>(a, wb + (k >> 1) * 128 + 2 * lane + (k & 1), q - 1u, lds);
+            pend[k] = q >= 0x8000u;
+            fa[k] = (ixC & lowm) | ((uint32_t)lane << 20) | ((uint32_t)k << 26);
+            fb[k] = iyC & lowm;
+            fc[k] = q | (tile << 16);
+        }
+        // compaction: row slot k's pending rows go to set slots base_k .. base_k + n_k - 1 (lane =
+        // slot mod 64), its other rows behind them (a rotation of the stable partition: a permutation)
+        uint32_t va[4], vb[4], vc[4], bases[4];
+        uint32_t base = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned long long m = __ballot(pend[k]);
+            const uint32_t n = (uint32_t)__popcll(m);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            // (a select written as bit operations: pending iff bit 15 of the quad entry, a u16)
+            const uint32_t alt = n + ((uint32_t)lane - rank), pm = 0u - ((fc[k] >> 15) & 1u);
+            const uint32_t dst = ((base + (alt ^ ((rank ^ alt) & pm))) & 63u) << 2;
+            va[k] = (uint32_t)__builtin_amdgcn_ds_permute((int)dst, (int)fa[k]);
+            vb[k] = (uint32_t)__builtin_amdgcn_ds_permute((int)dst, (int)fb[k]);
+            vc[k] = (uint32_t)__builtin_amdgcn_ds_permute((int)dst, (int)fc[k]);
+            bases[k] = base;
+            base += n;
+        }
+        const uint32_t P = base;  // pending rows of the group (wave-uniform)
+        // set sv (slots 64 sv .. 64 sv + 63): lane j takes slot 64 sv + j from the row slot whose range holds it
+        auto gather_set = [&](uint32_t sv, CptSet& o) {
+            const uint32_t slot = 64u * sv + (uint32_t)lane;
+            uint32_t ra = va[0], rb = vb[0], rc = vc[0];
+#pragma unroll
+            for (int k = 1; k < 4; k++) {
+                const bool tk = slot >= bases[k];
+                ra = tk ? va[k] : ra;
+                rb = tk ? vb[k] : rb;
+                rc = tk ? vc[k] : rc;
+            }
+            const bool ok = slot < P;  // empty slots: quad entry 0, answer 0 (the spill word)
+            o.a = ok ? ra : 0u;
+            o.b = ok ? rb : 0u;
+            o.c = ok ? rc : 0u;
+        };
+        gather_set(0u, z);
+        set_a(z);
+        if (P > 64u) {  // (wave-uniform) the group's further sets, unpipelined
+            for (uint32_t sv = 1; sv * 64u < P; sv++) {
+                CptSet o;
+                gather_set(sv, o);
+                set_a(o);
+                set_b(o);
+                set_d(o, wb);
+            }
+        }
+    };
+    struct Coords {
+        v2d px[2], py[2];
+    };
+    auto load4 = [&](Coords& cb, int64_t wb, bool valid) {
+        const int64_t r = valid ? wb + 2 * lane : wbase + 2 * lane;
+        cb.px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
+        cb.px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
+        cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
+        cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
+    };
+    Coords cb0, cb1;
+    CptSet z0, z1;
+    z0.a = z1.a = z0.b = z1.b = z0.c = z1.c = z0.code = z1.code = z0.leaf = z1.leaf = 0u;
+    z0.lrec = z1.lrec = v4u{0u, 0u, 0u, 0u};
+    // zfin: the set of t - 2, refilled with group t; zadv: the set of t - 1
+    auto step = [&](auto VALID, int64_t t, CptSet& zfin, CptSet& zadv, Coords& cb, Coords& cn) {
+        const bool all[4] = {true, true, true, true};
+        if (t >= 2) set_d(zfin, wbase + (t - 2) * stride);
+        set_b(zadv);
+        const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
+        const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
+        stage_a(x, y, all, decltype(VALID)::value, zfin, wbase + t * stride);
+        load4(cn, wbase + (t + 1) * stride, t + 1 < T);
+    };
+    if (T > 0) {
+        load4(cb0, wbase, true);
+        const std::true_type full;
+        const std::false_type drain;
+        int64_t t = 0;
+        for (; t + 2 <= T; t += 2) {
+            step(full, t, z0, z1, cb0, cb1);
+            step(full, t + 1, z1, z0, cb1, cb0);
+        }
+        if (t < T) {
+            step(full, t, z0, z1, cb0, cb1);
+            step(drain, t + 1, z1, z0, cb1, cb0);
+            step(drain, t + 2, z0, z1, cb0, cb1);
+        } else {
+            step(drain, t, z0, z1, cb0, cb1);
+            step(drain, t + 1, z1, z0, cb1, cb0);
+        }
+    }
+    // the wave's partial group (rows past its last full group), unpipelined
+    const int64_t wt = wbase + T * stride;
+    if (wt < a.n) {
+        double x[4], y[4];
+        bool live[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int64_t r = wt + (k >> 1) * 128 + 2 * lane + (k & 1);
+            live[k] = r < a.n;
+            x[k] = live[k] ? a.x[r] : 0.0;
+            y[k] = live[k] ? a.y[r] : 0.0;
+        }
+        CptSet z;
+        stage_a(x, y, live, true, z, wt);
+        set_b(z);
+        set_d(z, wt);
+    }
+    stage_flush(a, wq, wn, lane, 1);
+    if (LDS_COUNTS) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
+    }
+}
 
 // k_join_stream_bng: the dense table's answer for every point, branch-free, in the layout of
 // k_join_stream (256 rows per wave and iteration, 1 KiB coalesced coordinate loads, the next
@@ -833,7 +1130,12 @@ __global__ void __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) k
     }
 }
 
-const void* stream_kernel_h3(bool pipe, bool lds, bool pairs, bool vec) {
+const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec) {
+    if (pipe == 2 && vec) {
+        if (pairs) return (const void*)k_join_stream_cpt<false, true>;
+        if (lds) return (const void*)k_join_stream_cpt<true, false>;
+        return (const void*)k_join_stream_cpt<false, false>;
+    }
     if (pipe && vec) {
         if (pairs) return (const void*)k_join_stream_pipe<false, true>;
         if (lds) return (const void*)k_join_stream_pipe<true, false>;

@@ -1911,7 +1911,7 @@ struct Options {
     int raster_build = 1;     // point raster classification: 1 on the GPU (k_raster_*), 0 on host threads
     int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
-    int stream_pipe = 1;      // k_join_stream_pipe (software-pipelined) where it applies
+    int stream_pipe = 2;      // 1: k_join_stream_pipe (software-pipelined), 2: k_join_stream_cpt (+ compacted gathers)
     int bng_pipe = 0;         // k_join_stream_bng_pipe (measured slower at C5: 6.30 vs 4.53 ms, profiles/r03_kbench_bng_pipe.txt)
     int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
     int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
@@ -2380,7 +2380,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, 1024]");
         o.stream_block = (int)v;
     } else if (k == "stream_pipe") {
-        o.stream_pipe = v ? 1 : 0;
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "stream_pipe must be 0, 1 or 2");
+        o.stream_pipe = (int)v;
     } else if (k == "bng_pipe") {
         o.bng_pipe = v ? 1 : 0;
     } else if (k == "bng_lds") {
@@ -3872,7 +3873,11 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             auto kernel_for = [&](bool vec) -> const void* {
                 // the pipelined form (k_join_stream_pipe) where it applies
-                return stream_kernel_h3(vec && sa.tb_lds && sa.fix_ok && c->stream_pipe, lds, pairs, vec);
+                // (the compacted form, k_join_stream_cpt, carries cs + kFixBits + qs <= 20 low bits of
+                // the fine-cell coordinates and a 16-bit tile index per pending row)
+                int mode = vec && sa.tb_lds && sa.fix_ok ? c->stream_pipe : 0;
+                if (mode == 2 && !(sa.cs + sa.qs <= 8 && sa.n_tiles <= 65536)) mode = 1;
+                return stream_kernel_h3(mode, lds, pairs, vec);
             };
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blk, shm_s) != hipSuccess || per_cu < 1)
