@@ -136,6 +136,10 @@ int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3);
  * context stream.  Waits for the stream, writes up to cap elapsed times (ms) in call order, reports
  * how many calls were timed in *n_out, and resets the list. */
 int mosaic_kernel_times(mosaic_ctx* ctx, double* out_ms, int64_t cap, int64_t* n_out);
+/* Name of the dominant kernel of the calling thread's last join call ("k_join_stream_cpt",
+ * "k_join_stream_pipe", "k_join_stream_bng", ...; "" before any): what a profile of that call
+ * should be filtered on.  Static storage; never freed. */
+const char* mosaic_last_kernel(mosaic_ctx* ctx);
 
 /* ---- grid systems ---- */
 /* getResolution for an Int resolution; validates the range of the grid system. */

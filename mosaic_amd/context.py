@@ -374,6 +374,10 @@ class MosaicContext:
     def sync(self):
         N.check(N.lib().mosaic_sync(self.handle))
 
+    def last_kernel(self):
+        """name of the dominant kernel of this thread's last join call (mosaic_last_kernel)"""
+        return N.lib().mosaic_last_kernel(self.handle).decode()
+
     def kernel_times(self, cap=4096):
         """Elapsed ms of each fused join kernel since option "timing" was set (HIP events)."""
         out = np.zeros(cap, np.float64)

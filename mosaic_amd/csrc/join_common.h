@@ -131,6 +131,8 @@ struct StreamArgs {
 // per-wave mixed-row stage of the stream kernels (words): rows are appended one slot (<= 64 rows)
 // at a time and flushed at >= 64
 static const int kStageWords = 128;
+// k_join_stream_cpt's per-wave compaction buffer (words): 64 slots x 3 words
+static const int kCptBufWords = 192;
 static const uint32_t kNoLoad = 0x7ffffff0u;  // out-of-range buffer offset (every table is < 2 GiB)
 // cache-policy bits (aux) of the stream kernels' gathers: sub-block entries, line records, leaf
 // codes, BNG sub-cell entries (build-time A/B knobs; 2 = nt)
@@ -178,6 +180,15 @@ __device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t byt
                                              (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// a * b + c for a, b < 2^24 as one v_mad_u32_u24 (b wave-uniform).  Written out because the compiler
+// turns __umul24(a, b) + c into v_mad_u64_u32 (a quarter-rate instruction) or a multiply, two
+// shifts and an add when the sum is an address
+__device__ inline uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+}
+
 // The LDS quad level's entry for fine cell (ixC, iyC), resolved through the quad's record when the
 // point's sub-quad is uniform with the record's code (tiles::raster_code with use_quad, branch-free)
 // (SH0: fraction bits below the fine-cell coordinates ixC, iyC -- 0, or kFixBits for the
@@ -185,7 +196,7 @@ __device__ inline __amdgpu_buffer_rsrc_t stream_rsrc(const void* p, uint32_t byt
 template <int SH0 = 0>
 __device__ inline uint32_t quad_lookup(const StreamArgs& s, const uint16_t* quad, const uint32_t* qmask,
                                        const uint16_t* qcode, uint32_t ixC, uint32_t iyC) {
-    const uint32_t q = quad[__umul24(iyC >> (s.qsh + SH0), (uint32_t)s.qnx) + (ixC >> (s.qsh + SH0))];
+    const uint32_t q = quad[mad_u24(iyC >> (s.qsh + SH0), (uint32_t)s.qnx, ixC >> (s.qsh + SH0))];
     // q >= 0x8000 with record index q & 0x7fff < n_qrec, as one unsigned compare (q < 0x8000 wraps)
     const uint32_t r = q - 0x8000u;
     const bool rec = r < (uint32_t)s.n_qrec;

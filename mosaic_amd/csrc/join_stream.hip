@@ -535,6 +535,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 // cs + kFixBits + qs bits of both fixed-point fine-cell coordinates (leaf cell, line offsets and the
 // sub-block within the quad; L <= 20), the source lane and row slot, the quad entry and the tile.
 // Same answers as k_join_stream_pipe, point for point.
+#ifndef MOSAIC_CPT_DEPTH
+#define MOSAIC_CPT_DEPTH 1
+#endif
+// 1: compaction through a per-wave LDS buffer; 0: ds_permute (no LDS memory)
+#ifndef MOSAIC_CPT_LDS
+#define MOSAIC_CPT_LDS 1
+#endif
 struct CptSet {
     uint32_t a;     // ix low bits | source lane << 20 | row slot k << 26
     uint32_t b;     // iy low bits
@@ -550,7 +557,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const int nwaves = (int)(blockDim.x >> 6);
     const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
     uint32_t* stage = lds + ncw;
-    uint32_t* tb = stage + nwaves * s.stage_words;
+    // per-wave compaction buffers (MOSAIC_CPT_LDS): 64 slots x 3 words, structure of arrays
+    uint32_t* cbuf_all = stage + nwaves * s.stage_words;
+    uint32_t* tb = cbuf_all + nwaves * kCptBufWords;
     uint32_t* quadw = tb + s.n_tiles;
     const uint16_t* quad = (const uint16_t*)quadw;
     uint32_t* qmask = quadw + s.n_quad_words;
@@ -566,11 +575,17 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     uint32_t* wq = stage + wave * s.stage_words;
+    uint32_t* cbuf = cbuf_all + wave * kCptBufWords;
     uint32_t wn = 0;
     constexpr int F = tiles::kFixBits;
     const uint32_t cs = (uint32_t)s.cs, qs = (uint32_t)s.qs;
     const uint32_t lowm = (1u << (cs + F + qs)) - 1u;
     const uint32_t spill = (uint32_t)(a.n_polygons + lane);
+    // the fixed-point offsets in VGPRs for the whole kernel (an fma reads one scalar operand; as
+    // scalars they would be copied into VGPRs at every point)
+    double gx0v, gy0v;
+    __asm__("v_mov_b64 %0, %1" : "=v"(gx0v) : "s"(s.gx0F));
+    __asm__("v_mov_b64 %0, %1" : "=v"(gy0v) : "s"(s.gy0F));
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
     const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
     const int64_t T = wbase + 256 <= a.n ? (a.n - 256 - wbase) / stride + 1 : 0;
@@ -634,11 +649,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         bool pend[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint32_t ixC = min(tiles::fix_cvt(fma(x[k], s.sxF, s.gx0F)), (uint32_t)s.gxmaxF);
-            const uint32_t iyC = min(tiles::fix_cvt(fma(y[k], s.syF, s.gy0F)), (uint32_t)s.gymaxF);
+            const uint32_t ixC = min(tiles::fix_cvt(fma(x[k], s.sxF, gx0v)), (uint32_t)s.gxmaxF);
+            const uint32_t iyC = min(tiles::fix_cvt(fma(y[k], s.syF, gy0v)), (uint32_t)s.gymaxF);
             const uint32_t q0 = quad_lookup<F>(s, quad, qmask, qcode, ixC, iyC);
             const uint32_t q = valid && live[k] ? q0 : 0u;
-            const uint32_t tile = __umul24(iyC >> (s.tsh + F), (uint32_t)s.tnx) + (ixC >> (s.tsh + F));
+            const uint32_t tile = mad_u24(iyC >> (s.tsh + F), (uint32_t)s.tnx, ixC >> (s.tsh + F));
             // resolved rows (codes < 0x8000: 0 or key + 1); pending rows add to the spill word now
             // and are counted when their answer is known
             if (LDS_COUNTS && !PAIRS) atomicAdd(&lds[min(q - 1u, spill)], 1u);
@@ -648,6 +663,38 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             fb[k] = iyC & lowm;
             fc[k] = q | (tile << 16);
         }
+#if MOSAIC_CPT_LDS
+        // compaction through the wave's LDS buffer: row slot k's pending rows take set slots base_k ..
+        // base_k + n_k - 1; the rows of set sv (slots 64 sv .. 64 sv + 63) are stored, then read back
+        // one per lane
+        uint32_t ranks[4], bases[4];
+        uint32_t base = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned long long m = __ballot(pend[k]);
+            ranks[k] = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            bases[k] = base;
+            base += (uint32_t)__popcll(m);
+        }
+        const uint32_t P = base;  // pending rows of the group (wave-uniform)
+        auto gather_set = [&](uint32_t sv, CptSet& o) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t slot = ranks[k] - 64u * sv;
+                if (pend[k] && slot < 64u) {
+                    cbuf[slot] = fa[k];
+                    cbuf[64 + slot] = fb[k];
+                    cbuf[128 + slot] = fc[k];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            const bool ok = 64u * sv + (uint32_t)lane < P;  // empty slots: quad entry 0, answer 0
+            o.a = ok ? cbuf[lane] : 0u;
+            o.b = ok ? cbuf[64 + lane] : 0u;
+            o.c = ok ? cbuf[128 + lane] : 0u;
+            __builtin_amdgcn_wave_barrier();
+        };
+#else
         // compaction: row slot k's pending rows go to set slots base_k .. base_k + n_k - 1 (lane =
         // slot mod 64), its other rows behind them (a rotation of the stable partition: a permutation)
         uint32_t va[4], vb[4], vc[4], bases[4];
@@ -683,6 +730,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             o.b = ok ? rb : 0u;
             o.c = ok ? rc : 0u;
         };
+#endif
         gather_set(0u, z);
         set_a(z);
         if (P > 64u) {  // (wave-uniform) the group's further sets, unpipelined
@@ -705,11 +753,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
         cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
     };
-    Coords cb0, cb1;
+    Coords cb0, cb1, cb2;
     CptSet z0, z1;
     z0.a = z1.a = z0.b = z1.b = z0.c = z1.c = z0.code = z1.code = z0.leaf = z1.leaf = 0u;
     z0.lrec = z1.lrec = v4u{0u, 0u, 0u, 0u};
-    // zfin: the set of t - 2, refilled with group t; zadv: the set of t - 1
+    // zfin: the set of t - 2, refilled with group t; zadv: the set of t - 1.  Coordinates are loaded
+    // MOSAIC_CPT_DEPTH groups ahead: cb holds group t, cn is loaded with group t + DEPTH (with depth
+    // 1, cn is the other buffer; with depth 2, the buffers rotate over three)
     auto step = [&](auto VALID, int64_t t, CptSet& zfin, CptSet& zadv, Coords& cb, Coords& cn) {
         const bool all[4] = {true, true, true, true};
         if (t >= 2) set_d(zfin, wbase + (t - 2) * stride);
@@ -717,13 +767,50 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
         const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
         stage_a(x, y, all, decltype(VALID)::value, zfin, wbase + t * stride);
-        load4(cn, wbase + (t + 1) * stride, t + 1 < T);
+        load4(cn, wbase + (t + MOSAIC_CPT_DEPTH) * stride, t + MOSAIC_CPT_DEPTH < T);
+    };
+    auto step_rt = [&](bool valid, int64_t t, CptSet& zfin, CptSet& zadv, Coords& cb, Coords& cn) {
+        const bool all[4] = {true, true, true, true};
+        if (t >= 2) set_d(zfin, wbase + (t - 2) * stride);
+        set_b(zadv);
+        const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
+        const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
+        stage_a(x, y, all, valid, zfin, wbase + t * stride);
+        load4(cn, wbase + (t + MOSAIC_CPT_DEPTH) * stride, t + MOSAIC_CPT_DEPTH < T);
     };
     if (T > 0) {
-        load4(cb0, wbase, true);
         const std::true_type full;
         const std::false_type drain;
         int64_t t = 0;
+#if MOSAIC_CPT_DEPTH == 2
+        load4(cb0, wbase, true);
+        load4(cb1, wbase + stride, 1 < T);
+        // slots: set t % 2, coordinates t % 3 (six steps per turn)
+        for (; t + 6 <= T; t += 6) {
+            step(full, t, z0, z1, cb0, cb2);
+            step(full, t + 1, z1, z0, cb1, cb0);
+            step(full, t + 2, z0, z1, cb2, cb1);
+            step(full, t + 3, z1, z0, cb0, cb2);
+            step(full, t + 4, z0, z1, cb1, cb0);
+            step(full, t + 5, z1, z0, cb2, cb1);
+        }
+        // the remaining groups (<= 5) and the two drain steps, in the same slot sequence (validity
+        // tested at run time here)
+#define MOSAIC_CPT_TAIL(ZF, ZA, CB, CN) \
+    if (t < T + 2) {                    \
+        step_rt(t < T, t, ZF, ZA, CB, CN); \
+        t++;                            \
+    }
+        MOSAIC_CPT_TAIL(z0, z1, cb0, cb2)
+        MOSAIC_CPT_TAIL(z1, z0, cb1, cb0)
+        MOSAIC_CPT_TAIL(z0, z1, cb2, cb1)
+        MOSAIC_CPT_TAIL(z1, z0, cb0, cb2)
+        MOSAIC_CPT_TAIL(z0, z1, cb1, cb0)
+        MOSAIC_CPT_TAIL(z1, z0, cb2, cb1)
+        MOSAIC_CPT_TAIL(z0, z1, cb0, cb2)
+#undef MOSAIC_CPT_TAIL
+#else
+        load4(cb0, wbase, true);
         for (; t + 2 <= T; t += 2) {
             step(full, t, z0, z1, cb0, cb1);
             step(full, t + 1, z1, z0, cb1, cb0);
@@ -736,6 +823,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             step(drain, t, z0, z1, cb0, cb1);
             step(drain, t + 1, z1, z0, cb1, cb0);
         }
+#endif
     }
     // the wave's partial group (rows past its last full group), unpipelined
     const int64_t wt = wbase + T * stride;

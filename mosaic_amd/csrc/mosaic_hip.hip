@@ -1935,6 +1935,7 @@ struct ThreadCtx : Options {
     int n_cu = 256;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    const char* last_kernel = "";      // the dominant kernel of the last join call (mosaic_last_kernel)
     double last_tess_classify_ms = 0;  // classification kernel (k_bng_tess_classify / k_tess_classify_poly) of the
                                        // last mosaic_tessellate_gpu; 0 when it had no candidates
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
@@ -2460,6 +2461,11 @@ int mosaic_kernel_times(mosaic_ctx* ctx, double* out_ms, int64_t cap, int64_t* n
     *n_out = n;
     c->ev_used = 0;
     return MOSAIC_OK;
+}
+
+const char* mosaic_last_kernel(mosaic_ctx* ctx) {
+    ThreadCtx* c = ctx ? enter(ctx) : nullptr;
+    return c ? c->last_kernel : "";
 }
 
 int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3) {
@@ -3831,6 +3837,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             auto kernel_for = [&](bool vec) -> const void* {
                 return stream_kernel_bng(lds, pairs, vec, bpipe);
             };
+            c->last_kernel = bpipe ? "k_join_stream_bng_pipe" : "k_join_stream_bng";
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blkb, shm_b) != hipSuccess || per_cu < 1)
                 per_cu = 1;
@@ -3871,16 +3878,24 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             a.mixq = (uint32_t*)c->mix_queue.p;
             a.mixq_count = sc + 4;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
-            auto kernel_for = [&](bool vec) -> const void* {
-                // the pipelined form (k_join_stream_pipe) where it applies
-                // (the compacted form, k_join_stream_cpt, carries cs + kFixBits + qs <= 20 low bits of
-                // the fine-cell coordinates and a 16-bit tile index per pending row)
+            auto mode_for = [&](bool vec) -> int {
+                // the pipelined forms where they apply (the compacted one, k_join_stream_cpt, carries
+                // cs + kFixBits + qs <= 20 low bits of the fine-cell coordinates and a 16-bit tile index
+                // per pending row)
+                // per pending row, and per wave a kCptBufWords compaction buffer in LDS)
                 int mode = vec && sa.tb_lds && sa.fix_ok ? c->stream_pipe : 0;
-                if (mode == 2 && !(sa.cs + sa.qs <= 8 && sa.n_tiles <= 65536)) mode = 1;
-                return stream_kernel_h3(mode, lds, pairs, vec);
+                if (mode == 2 && !(sa.cs + sa.qs <= 8 && sa.n_tiles <= 65536 &&
+                                   shm_s + (size_t)(blk / 64) * kCptBufWords * 4 <= kStreamLdsMax))
+                    mode = 1;
+                return mode;
+            };
+            auto kernel_for = [&](bool vec) -> const void* { return stream_kernel_h3(mode_for(vec), lds, pairs, vec); };
+            auto shm_for = [&](bool vec) -> size_t {
+                return shm_s + (mode_for(vec) == 2 ? (size_t)(blk / 64) * kCptBufWords * 4 : 0);
             };
             int per_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blk, shm_s) != hipSuccess || per_cu < 1)
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blk, shm_for(true)) != hipSuccess ||
+                per_cu < 1)
                 per_cu = 1;
             for (int64_t lo = 0; lo < n; lo += chunk) {
                 JoinArgs ac = a;
@@ -3889,12 +3904,16 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 // 16-byte loads need aligned columns and >= 256 rows (the prefetch past the end
                 // re-reads the chunk's first 256)
                 const void* kfn = kernel_for(aligned && ac.n - lo >= 256);
+                if (lo == 0) {
+                    static const char* const names[3] = {"k_join_stream", "k_join_stream_pipe", "k_join_stream_cpt"};
+                    c->last_kernel = names[mode_for(aligned && ac.n - lo >= 256)];
+                }
                 if (lo > 0) HIP_TRY(hipMemsetAsync(ac.mixq_count, 0, 8, c->stream));
                 // persistent grid: the workgroups resident at once (each fills its LDS once)
                 const int gs = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + 4 * blk - 1) / (4 * blk),
                                                                            (int64_t)c->n_cu * per_cu));
                 void* kargs[] = {&ac, &sa};
-                HIP_TRY(hipLaunchKernel(kfn, dim3(gs), dim3(blk), kargs, shm_s, c->stream));
+                HIP_TRY(hipLaunchKernel(kfn, dim3(gs), dim3(blk), kargs, shm_for(aligned && ac.n - lo >= 256), c->stream));
                 if (tstop && lo == 0) HIP_TRY(hipEventRecord(tstop, c->stream));
                 // (the queue holds at most the chunk's rows)
                 const int gm = (int)std::max<int64_t>(1, std::min<int64_t>((ac.n - lo + 4 * c->block - 1) / (4 * c->block),
@@ -3922,14 +3941,17 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             }
             tstop = nullptr;  // recorded after the first stream launch
         } else if (tiled) {
+            c->last_kernel = "k_join_tiled";
             if (pairs) MOSAIC_LAUNCH((k_join_tiled<false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_tiled<true, false>), shm);
             else MOSAIC_LAUNCH((k_join_tiled<false, false>), 0);
         } else if (h3g) {
+            c->last_kernel = "k_join_raster";
             if (pairs) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, true, false>), shm);
             else MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_H3, false, false>), 0);
         } else {
+            c->last_kernel = "k_join_raster";
             if (pairs) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, false, true>), 0);
             else if (lds) MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, true, false>), shm);
             else MOSAIC_LAUNCH((k_join_raster<MOSAIC_GRID_BNG, false, false>), 0);
