@@ -190,6 +190,11 @@ __device__ inline uint32_t gather_b16(__amdgpu_buffer_rsrc_t r, bool need, uint3
     if (MOSAIC_GATHER_MODE == 1 && !__ballot(need)) return 0u;
     return __builtin_amdgcn_raw_buffer_load_b16(r, need ? off : kNoLoad, 0, aux);
 }
+__device__ inline uint32_t gather_b32(__amdgpu_buffer_rsrc_t r, bool need, uint32_t off) {
+    uint32_t v = 0u;
+    if (need) v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    return v;
+}
 template <int aux>
 __device__ inline v4u gather_b128(__amdgpu_buffer_rsrc_t r, bool need, uint32_t off) {
     if (MOSAIC_GATHER_MODE == 2) {
@@ -1005,6 +1010,267 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 }
 
 
+// ---- k_join_stream_bng_cpt: k_join_stream_bng with the rows that need gathers compacted (the H3
+// k_join_stream_cpt scheme).  Stage A runs every row through the integer cell arithmetic and the LDS
+// cell level; rows in empty or pure blocks (82 % of uniform C5 points), rows outside the one-to-one
+// range (kMixed) and NaN rows (flagged) are answered there.  The others ("pending": in a border cell)
+// go through a per-wave LDS buffer into one 64-lane set -- per row the cell index with the source
+// lane and row slot, and the f32 sub-cell coordinates -- whose cell-entry, sub-cell-code and
+// line-record gathers and answers take one lane per pending row, as a four-stage software pipeline
+// over the sets (iteration t: answers of the set of t - 3, line-record gathers of t - 2, sub-cell
+// gathers of t - 1, group t's LDS level + compaction + cell-entry gathers, coordinates of t + 1).
+// More than 64 pending rows in a group are finished at once.  Needs ne nn < 2^24 (cell index in 24
+// bits).  The sub-cell arithmetic is k_join_stream_bng's, so the answers are the same point for point.
+struct BngCptSet {
+    uint32_t a;     // cell index | source lane << 24 | row slot k << 30
+    uint32_t b, c;  // f32 sub-cell coordinates gxs, gys
+    uint32_t e;     // A -> B: gathered cell entry; B -> C: gathered sub-cell code
+    uint32_t p;     // 0: empty slot; B -> C: the answer, or kBngLeaf; C -> D: the answer or kPipeLine
+};
+// (the cell's leaf base, B -> C, and the line record, C -> D, are held by one set at a time: one
+// register copy each instead of one per set slot)
+
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_bng_cpt(JoinArgs a, BngStreamArgs s) {
+    extern __shared__ unsigned int lds[];
+    const int nwaves = (int)(blockDim.x >> 6);
+    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
+    uint32_t* stage = lds + ncw;
+    uint32_t* cbuf_all = stage + nwaves * kStageWords;
+    uint32_t* lcw = cbuf_all + nwaves * kCptBufWords;
+    const uint8_t* lcell = (const uint8_t*)lcw;
+    const bool use_lc = s.lcell_words > 0;  // (uniform)
+    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
+    lds_fill(lcw, s.lcell, s.lcell_words);
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rcell = stream_rsrc(s.cells, s.cells_bytes);
+    const __amdgpu_buffer_rsrc_t rleaf = stream_rsrc(s.leaf, s.leaf_bytes);
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t* wq = stage + wave * kStageWords;
+    uint32_t* cbuf = cbuf_all + wave * kCptBufWords;
+    uint32_t wn = 0;
+    bool nan_seen = false;
+    const uint32_t C = (uint32_t)s.C;
+    const uint32_t spill = (uint32_t)(a.n_polygons + lane);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
+    const int64_t T = wbase + 256 <= a.n ? (a.n - 256 - wbase) / stride + 1 : 0;
+    auto count = [&](uint32_t code, int64_t row) {
+        if (LDS_COUNTS && !PAIRS) atomicAdd(&lds[min(code - 1u, spill)], 1u);  // 0 and kMixed: spill
+        else if (code - 1u < 0xfffeu) emit_hit<LDS_COUNTS, PAIRS>(a, row, code - 1u, lds);
+    };
+    auto push_mixed = [&](bool m, int64_t row) {
+        if (__ballot(m)) {
+            const unsigned long long mm = __ballot(m);
+            if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row - a.row_lo);
+            wn += (uint32_t)__popcll(mm);
+            stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
+        }
+    };
+    // the sub-cell of set row z: index, and the offset in it (k_join_stream_bng's clamp)
+    auto subcell = [&](const BngCptSet& z, float* su, float* sv) -> uint32_t {
+        const float gxs = __uint_as_float(z.b), gys = __uint_as_float(z.c);
+        int sx = (int)gxs, sy = (int)gys;
+        sx = min(max(sx, 0), (int)C - 1);
+        sy = min(max(sy, 0), (int)C - 1);
+        *su = gxs - (float)sx;
+        *sv = gys - (float)sy;
+        return (uint32_t)(sy * (int)C + sx);
+    };
+    // A': cell-entry gathers
+    auto set_a = [&](BngCptSet& z) {
+        z.e = gather_b32(rcell, z.p != 0u, (z.a & 0xffffffu) << 2);
+    };
+    // B': cell entry -> sub-cell code gather
+    auto set_b = [&](BngCptSet& z, uint32_t& base) {
+        const uint32_t e = z.e;
+        const bool leafc = z.p != 0u && (e & (kBngPure | kBngLeaf)) == kBngLeaf;
+        base = e & ~kBngLeaf;
+        float su, sv;
+        const uint32_t q = subcell(z, &su, &sv);
+        z.e = gather_b16<MOSAIC_AUX_BNG>(rleaf, leafc, (base + q) << 1);
+        z.p = z.p == 0u ? 0u : ((e & kBngPure) ? (e & ~kBngPure) : (leafc ? kBngLeaf : (e ? (uint32_t)tiles::kMixed : 0u)));
+    };
+    // C': sub-cell code -> line-record gather
+    auto set_c = [&](BngCptSet& z, uint32_t base, v4u& lrec) {
+        const uint32_t code = z.e;
+        const bool leafc = z.p == kBngLeaf;
+        const bool line = leafc && (code & 0xC000u) == 0xC000u && code != (uint32_t)tiles::kMixed;
+        lrec = gather_b128<0>(rleaf, line, (base - 8u * ((code & 0x3fffu) + 1u)) << 1);
+        z.p = line ? kPipeLine : (leafc ? code : z.p);
+    };
+    // D': answers of the set's rows (group base wb)
+    auto set_d = [&](BngCptSet& z, const v4u& lrec, int64_t wb) {
+        float su, sv;
+        (void)subcell(z, &su, &sv);
+        const float lv = fmaf(__uint_as_float(lrec.x), su, fmaf(__uint_as_float(lrec.y), sv, __uint_as_float(lrec.z)));
+        uint32_t lc = lv >= 1.0f ? (lrec.w & 0xffffu) : (uint32_t)tiles::kMixed;
+        lc = lv <= -1.0f ? (lrec.w >> 16) : lc;
+        const uint32_t code = z.p == kPipeLine ? lc : z.p;
+        const uint32_t src = (z.a >> 24) & 63u, k = z.a >> 30;
+        const int64_t row = wb + (int64_t)((k >> 1) * 128u + 2u * src + (k & 1u));
+        count(code, row);
+        push_mixed(code == (uint32_t)tiles::kMixed, row);
+    };
+    // A: a group through the cell arithmetic and the LDS level, resolved rows answered, pending rows
+    // compacted into z (the first 64) through the wave's LDS buffer
+    auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, BngCptSet& z, int64_t wb) {
+        uint32_t fa[4], fb[4], fc[4];
+        bool pend[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool lv = valid && live[k];
+            const bool nan = x[k] != x[k] || y[k] != y[k];
+            nan_seen |= lv && nan;
+            const int32_t eI = bng::jvm_d2i(x[k]), nI = bng::jvm_d2i(y[k]);
+            const bool inr = (uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u;
+            const double xe = (double)eI, ye = (double)nI;
+            const int32_t qe = (int32_t)fma(xe, s.inv_div, 1e-7), qn = (int32_t)fma(ye, s.inv_div, 1e-7);
+            const int32_t ce = qe - s.e0, cn = qn - s.n0;
+            const bool cell_in = inr && (uint32_t)ce < (uint32_t)s.ne && (uint32_t)cn < (uint32_t)s.nn;
+            const uint32_t li = cell_in ? __umul24((uint32_t)cn >> s.lsh, (uint32_t)s.lnx) + ((uint32_t)ce >> s.lsh) : 0u;
+            const uint32_t lb = use_lc ? (uint32_t)lcell[li] : kBngLdsGather;
+            pend[k] = lv && !nan && cell_in && lb == kBngLdsGather;
+            // resolved rows: outside the one-to-one range kMixed, else the LDS block's code (0 outside
+            // the table); NaN and dead rows 0
+            uint32_t code = !inr ? (uint32_t)tiles::kMixed : (cell_in ? (lb == kBngLdsGather ? 0u : lb) : 0u);
+            code = (lv && !nan && !pend[k]) ? code : 0u;
+            const int64_t row = wb + (k >> 1) * 128 + 2 * lane + (k & 1);
+            count(code, row);
+            push_mixed(code == (uint32_t)tiles::kMixed, row);
+            // k_join_stream_bng's f32 sub-cell coordinates
+            const float gxs = fmaf((float)(eI - (int32_t)__umul24((uint32_t)qe, (uint32_t)s.idiv)), s.ff, (float)(x[k] - xe) * s.ff);
+            const float gys = fmaf((float)(nI - (int32_t)__umul24((uint32_t)qn, (uint32_t)s.idiv)), s.ff, (float)(y[k] - ye) * s.ff);
+            fa[k] = ((uint32_t)(cn * s.ne + ce) & 0xffffffu) | ((uint32_t)lane << 24) | ((uint32_t)k << 30);
+            fb[k] = __float_as_uint(gxs);
+            fc[k] = __float_as_uint(gys);
+        }
+        uint32_t ranks[4];
+        uint32_t P = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned long long m = __ballot(pend[k]);
+            ranks[k] = P + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            P += (uint32_t)__popcll(m);
+        }
+        auto gather_set = [&](uint32_t sv, BngCptSet& o) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t slot = ranks[k] - 64u * sv;
+                if (pend[k] && slot < 64u) {
+                    cbuf[slot] = fa[k];
+                    cbuf[64 + slot] = fb[k];
+                    cbuf[128 + slot] = fc[k];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            const bool ok = 64u * sv + (uint32_t)lane < P;
+            o.a = ok ? cbuf[lane] : 0u;
+            o.b = ok ? cbuf[64 + lane] : 0u;
+            o.c = ok ? cbuf[128 + lane] : 0u;
+            o.p = ok ? 1u : 0u;  // (a pending row: 1 until stage B' gives its answer)
+            __builtin_amdgcn_wave_barrier();
+        };
+        gather_set(0u, z);
+        set_a(z);
+        if (P > 64u) {  // (wave-uniform) the group's further sets, unpipelined
+            for (uint32_t sv = 1; sv * 64u < P; sv++) {
+                BngCptSet o;
+                uint32_t ob;
+                v4u orec;
+                gather_set(sv, o);
+                set_a(o);
+                set_b(o, ob);
+                set_c(o, ob, orec);
+                set_d(o, orec, wb);
+            }
+        }
+    };
+    struct Coords {
+        v2d px[2], py[2];
+    };
+    auto load4 = [&](Coords& cb, int64_t wb, bool valid) {
+        const int64_t r = valid ? wb + 2 * lane : wbase + 2 * lane;
+        cb.px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
+        cb.px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
+        cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
+        cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
+    };
+    BngCptSet z0, z1, z2;
+    z0.a = z1.a = z2.a = z0.b = z1.b = z2.b = z0.c = z1.c = z2.c = 0u;
+    z0.e = z1.e = z2.e = z0.p = z1.p = z2.p = 0u;
+    uint32_t base_bc = 0u;            // the leaf base of the set between stages B and C
+    v4u lrec_cd = {0u, 0u, 0u, 0u};   // the line record of the set between stages C and D
+    // zd: the set of t - 3, refilled with group t; zc: t - 2; zb: t - 1
+    auto step = [&](bool valid, int64_t t, BngCptSet& zd, BngCptSet& zc, BngCptSet& zb, Coords& cb, Coords& cn) {
+        const bool all[4] = {true, true, true, true};
+        if (t >= 3) set_d(zd, lrec_cd, wbase + (t - 3) * stride);
+        set_c(zc, base_bc, lrec_cd);
+        set_b(zb, base_bc);
+        const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
+        const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
+        stage_a(x, y, all, valid, zd, wbase + t * stride);
+        load4(cn, wbase + (t + 1) * stride, t + 1 < T);
+    };
+    if (T > 0) {
+        Coords cb0, cb1;
+        load4(cb0, wbase, true);
+        int64_t t = 0;
+        for (; t + 6 <= T; t += 6) {
+            step(true, t, z0, z1, z2, cb0, cb1);
+            step(true, t + 1, z1, z2, z0, cb1, cb0);
+            step(true, t + 2, z2, z0, z1, cb0, cb1);
+            step(true, t + 3, z0, z1, z2, cb1, cb0);
+            step(true, t + 4, z1, z2, z0, cb0, cb1);
+            step(true, t + 5, z2, z0, z1, cb1, cb0);
+        }
+        // the remaining groups (<= 5) and the three drain steps, in the same slot sequence
+#define MOSAIC_BCPT_TAIL(ZD, ZC, ZB, CB, CN) \
+    if (t < T + 3) {                       \
+        step(t < T, t, ZD, ZC, ZB, CB, CN); \
+        t++;                               \
+    }
+        MOSAIC_BCPT_TAIL(z0, z1, z2, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z1, z2, z0, cb1, cb0)
+        MOSAIC_BCPT_TAIL(z2, z0, z1, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z0, z1, z2, cb1, cb0)
+        MOSAIC_BCPT_TAIL(z1, z2, z0, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z2, z0, z1, cb1, cb0)
+        MOSAIC_BCPT_TAIL(z0, z1, z2, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z1, z2, z0, cb1, cb0)
+#undef MOSAIC_BCPT_TAIL
+    }
+    // the wave's partial group, unpipelined
+    const int64_t wt = wbase + T * stride;
+    if (wt < a.n) {
+        double x[4], y[4];
+        bool live[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int64_t r = wt + (k >> 1) * 128 + 2 * lane + (k & 1);
+            live[k] = r < a.n;
+            x[k] = live[k] ? a.x[r] : 0.0;
+            y[k] = live[k] ? a.y[r] : 0.0;
+        }
+        BngCptSet z;
+        uint32_t zb;
+        v4u zrec;
+        stage_a(x, y, live, true, z, wt);
+        set_b(z, zb);
+        set_c(z, zb, zrec);
+        set_d(z, zrec, wt);
+    }
+    stage_flush(a, wq, wn, lane, 1);
+    if (__ballot(nan_seen) && lane == 0) atomicOr(a.flags, 1u);
+    if (LDS_COUNTS) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
+    }
+}
+
 // ---- k_join_stream_bng_pipe: k_join_stream_bng as a four-stage software pipeline over each wave's
 // groups of 256 rows (the H3 kernel's scheme, one stage longer: the BNG answer can take three
 // dependent gathers).  Iteration t: D finishes group t - 3 (its line records arrived), C turns group
@@ -1234,7 +1500,12 @@ const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec) {
     return vec ? (const void*)k_join_stream<false, false, true> : (const void*)k_join_stream<false, false, false>;
 }
 
-const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool pipe) {
+const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool pipe, bool cpt) {
+    if (cpt && vec) {
+        if (pairs) return (const void*)k_join_stream_bng_cpt<false, true>;
+        if (lds) return (const void*)k_join_stream_bng_cpt<true, false>;
+        return (const void*)k_join_stream_bng_cpt<false, false>;
+    }
     if (pipe && vec) {
         if (pairs) return (const void*)k_join_stream_bng_pipe<false, true>;
         if (lds) return (const void*)k_join_stream_bng_pipe<true, false>;

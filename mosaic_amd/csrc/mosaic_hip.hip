@@ -1911,6 +1911,7 @@ struct Options {
     int raster_build = 1;     // point raster classification: 1 on the GPU (k_raster_*), 0 on host threads
     int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
+    int bng_cpt = 1;          // k_join_stream_bng_cpt (rows needing gathers compacted) where it applies
     int stream_pipe = 2;      // 1: k_join_stream_pipe (software-pipelined), 2: k_join_stream_cpt (+ compacted gathers)
     int bng_pipe = 0;         // k_join_stream_bng_pipe (measured slower at C5: 6.30 vs 4.53 ms, profiles/r03_kbench_bng_pipe.txt)
     int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
@@ -2385,6 +2386,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.stream_pipe = (int)v;
     } else if (k == "bng_pipe") {
         o.bng_pipe = v ? 1 : 0;
+    } else if (k == "bng_cpt") {
+        o.bng_cpt = v ? 1 : 0;
     } else if (k == "bng_lds") {
         o.bng_lds = v ? 1 : 0;
     } else if (k == "bng_cell") {
@@ -3834,10 +3837,16 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             bs.lnx = ch->bng_lnx;
             bs.lcell_words = shm_b + (size_t)ch->bng_lwords * 4 <= kStreamLdsMax ? ch->bng_lwords : 0;
             shm_b += (size_t)bs.lcell_words * 4;
+            // k_join_stream_bng_cpt (option bng_cpt): with the LDS cell level, a 24-bit cell index and
+            // room for its per-wave compaction buffers
+            const size_t cpt_bytes = (size_t)(blkb / 64) * kCptBufWords * 4;
+            const bool bcpt = c->bng_cpt && !bpipe && aligned && bs.lcell_words > 0 &&
+                              (int64_t)ch->bng_ne * ch->bng_nn < ((int64_t)1 << 24) && shm_b + cpt_bytes <= kStreamLdsMax;
+            if (bcpt) shm_b += cpt_bytes;
             auto kernel_for = [&](bool vec) -> const void* {
-                return stream_kernel_bng(lds, pairs, vec, bpipe);
+                return stream_kernel_bng(lds, pairs, vec, bpipe, bcpt);
             };
-            c->last_kernel = bpipe ? "k_join_stream_bng_pipe" : "k_join_stream_bng";
+            c->last_kernel = bcpt ? "k_join_stream_bng_cpt" : (bpipe ? "k_join_stream_bng_pipe" : "k_join_stream_bng");
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blkb, shm_b) != hipSuccess || per_cu < 1)
                 per_cu = 1;
