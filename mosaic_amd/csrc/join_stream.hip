@@ -1119,6 +1119,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, BngCptSet& z, int64_t wb) {
         uint32_t fa[4], fb[4], fc[4];
         bool pend[4];
+        uint32_t mixed_k = 0;  // row slots whose row goes to the mixed queue (outside the one-to-one range)
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const bool lv = valid && live[k];
@@ -1137,15 +1138,18 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             // the table); NaN and dead rows 0
             uint32_t code = !inr ? (uint32_t)tiles::kMixed : (cell_in ? (lb == kBngLdsGather ? 0u : lb) : 0u);
             code = (lv && !nan && !pend[k]) ? code : 0u;
-            const int64_t row = wb + (k >> 1) * 128 + 2 * lane + (k & 1);
-            count(code, row);
-            push_mixed(code == (uint32_t)tiles::kMixed, row);
+            if (LDS_COUNTS && !PAIRS) atomicAdd(&lds[min(code - 1u, spill)], 1u);  // 0 and kMixed: spill
+            else count(code, wb + (k >> 1) * 128 + 2 * lane + (k & 1));
+            mixed_k |= (code == (uint32_t)tiles::kMixed ? 1u : 0u) << k;
             // k_join_stream_bng's f32 sub-cell coordinates
             const float gxs = fmaf((float)(eI - (int32_t)__umul24((uint32_t)qe, (uint32_t)s.idiv)), s.ff, (float)(x[k] - xe) * s.ff);
             const float gys = fmaf((float)(nI - (int32_t)__umul24((uint32_t)qn, (uint32_t)s.idiv)), s.ff, (float)(y[k] - ye) * s.ff);
             fa[k] = ((uint32_t)(cn * s.ne + ce) & 0xffffffu) | ((uint32_t)lane << 24) | ((uint32_t)k << 30);
             fb[k] = __float_as_uint(gxs);
             fc[k] = __float_as_uint(gys);
+        }
+        if (__ballot(mixed_k != 0u)) {  // (rare: one wave-uniform test per group)
+            for (int k = 0; k < 4; k++) push_mixed((mixed_k >> k) & 1u, wb + (k >> 1) * 128 + 2 * lane + (k & 1));
         }
         uint32_t ranks[4];
         uint32_t P = 0;

@@ -4800,6 +4800,8 @@ struct ClipArgs {
     double area_eps;
     const int64_t* tasks;
     int64_t n_tasks;
+    const int64_t* tsel;  // when set: the kernel takes the tasks tsel[0 .. n_sel) (positions in tasks)
+    int64_t n_sel;
     double* sxy;      // per wave: 2 x cap points
     int32_t* stag;    // per wave: 2 x cap tags
     int64_t cap;
@@ -4917,7 +4919,9 @@ __global__ void __launch_bounds__(256) k_tess_clip(ClipArgs a) {
     const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     double* bxy[2] = {a.sxy + wave * 4 * a.cap, a.sxy + wave * 4 * a.cap + 2 * a.cap};
     int32_t* btag[2] = {a.stag + wave * 2 * a.cap, a.stag + wave * 2 * a.cap + a.cap};
-    for (int64_t t = wave; t < a.n_tasks; t += n_waves) {
+    const int64_t n_work = a.tsel ? a.n_sel : a.n_tasks;
+    for (int64_t u = wave; u < n_work; u += n_waves) {
+        const int64_t t = a.tsel ? a.tsel[u] : u;
         const int64_t k = a.tasks[t];
         const int g = a.cand_geom[k];
         const double* P = a.clip + 2 * (int64_t)a.nv * k;
@@ -5015,9 +5019,180 @@ __global__ void __launch_bounds__(256) k_tess_clip(ClipArgs a) {
     }
 }
 
+// ---- k_tess_clip_lane: k_tess_clip for small tasks (every ring of the geometry <= kClipLaneRing
+// vertices, clip polygon <= kClipLaneClip vertices: building-scale inputs), one LANE per task -- the
+// same Sutherland-Hodgman passes run sequentially in the lane's private buffers, so the output
+// vertices, their order, the area sums and the tests are k_tess_clip's (and clip_edge's) exactly.
+// (k_tess_clip spends a wave, global scratch and an agent-scope fence per pass on rings of ~5-13
+// vertices there.)
+static constexpr int kClipLaneRing = 24, kClipLaneClip = 12, kClipLaneCap = kClipLaneRing + kClipLaneClip + 2;
+__global__ void __launch_bounds__(256) k_tess_clip_lane(ClipArgs a) {
+    const int64_t n_work = a.tsel ? a.n_sel : a.n_tasks;
+    double bx[2][kClipLaneCap], by[2][kClipLaneCap];
+    int32_t bt[2][kClipLaneCap];
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_work; u += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = a.tsel ? a.tsel[u] : u;
+        const int64_t k = a.tasks[t];
+        const int g = a.cand_geom[k];
+        const double* P = a.clip + 2 * (int64_t)a.nv * k;
+        const int face = a.mode == 0 ? a.gface[g] : 0;
+        bool redo = a.nv > kClipLaneClip;
+        const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
+        for (int64_t p = p0; p < p1 && !redo; p++) {
+            bool any = false;
+            double net = 0;
+            const int64_t r0 = a.part_rings[p];
+            for (int64_t r = r0; r < a.part_rings[p + 1]; r++) {
+                const int64_t vb = a.ring_offsets[r], n_closed = a.ring_offsets[r + 1] - vb;
+                if (n_closed < 4) continue;
+                const int64_t n = n_closed - 1;  // open vertex list
+                if (n > kClipLaneRing) {
+                    redo = true;
+                    break;
+                }
+                for (int64_t i = 0; i < n; i++) {
+                    bx[0][i] = a.pxy[2 * (vb + i)];
+                    by[0][i] = a.pxy[2 * (vb + i) + 1];
+                    bt[0][i] = (int32_t)i;
+                }
+                int cur = 0;
+                int64_t m = n;
+                for (int e = 0; e < a.nv && m > 0; e++) {
+                    const int f = e + 1 == a.nv ? 0 : e + 1;
+                    const double ax = P[2 * e], ay = P[2 * e + 1], bx_ = P[2 * f], by_ = P[2 * f + 1];
+                    int64_t o = 0;
+                    for (int64_t i = 0; i < m; i++) {
+                        const int64_t j = i == 0 ? m - 1 : i - 1;
+                        double cx = bx[cur][i], cy = by[cur][i];
+                        int32_t ct = bt[cur][i];
+                        const double px = bx[cur][j], py = by[cur][j];
+                        const double sc = (bx_ - ax) * (cy - ay) - (by_ - ay) * (cx - ax);
+                        const double sp = (bx_ - ax) * (py - ay) - (by_ - ay) * (px - ax);
+                        const bool ic = sc >= 0, ip = sp >= 0;
+                        double qx = 0, qy = 0;
+                        if (ic != ip) {
+                            const double tt = sp / (sp - sc);
+                            qx = px + tt * (cx - px);
+                            qy = py + tt * (cy - py);
+                        }
+                        const int cnt = ic ? (ip ? 1 : 2) : (ip ? 1 : 0);
+                        if (!ic && ip) {
+                            cx = qx;
+                            cy = qy;
+                            ct = -1;
+                        }
+                        if (o + cnt > kClipLaneCap) {
+                            o = -1;
+                            break;
+                        }
+                        if (cnt == 2) {
+                            bx[cur ^ 1][o] = qx;
+                            by[cur ^ 1][o] = qy;
+                            bt[cur ^ 1][o] = -1;
+                            o++;
+                        }
+                        if (cnt >= 1) {
+                            bx[cur ^ 1][o] = cx;
+                            by[cur ^ 1][o] = cy;
+                            bt[cur ^ 1][o] = ct;
+                            o++;
+                        }
+                    }
+                    m = o;
+                    if (m < 0) break;
+                    cur ^= 1;
+                }
+                if (m < 0) {
+                    redo = true;
+                    break;
+                }
+                const bool shell = r == r0;
+                if (m < 3) {
+                    if (shell) break;  // the shell misses the cell
+                    continue;
+                }
+                double ar = 0;  // ring_area of the closed ring, in order
+                for (int64_t i = 0; i < m; i++) {
+                    const int64_t j = i + 1 == m ? 0 : i + 1;
+                    ar += bx[cur][i] * by[cur][j] - bx[cur][j] * by[cur][i];
+                }
+                ar = 0.5 * ar;
+                if (fabs(ar) <= a.area_eps) {
+                    if (shell) break;
+                    continue;
+                }
+                net += shell ? fabs(ar) : -fabs(ar);
+                any = true;
+                const unsigned long long off = atomicAdd(&a.counters[0], (unsigned long long)(m + 1));
+                const unsigned long long rid = atomicAdd(&a.counters[1], 1ull);
+                if ((int64_t)(off + m + 1) > a.out_cap || (int64_t)rid >= a.ring_cap) {
+                    redo = true;
+                    break;
+                }
+                for (int64_t i = 0; i <= m; i++) {
+                    const int64_t s_ = i == m ? 0 : i;
+                    double ox, oy;
+                    if (bt[cur][s_] >= 0) {
+                        ox = a.gxy[2 * (vb + bt[cur][s_])];
+                        oy = a.gxy[2 * (vb + bt[cur][s_]) + 1];
+                    } else {
+                        clip_to_geo(a, face, bx[cur][s_], by[cur][s_], &ox, &oy);
+                    }
+                    a.out[2 * (off + i)] = ox;
+                    a.out[2 * (off + i) + 1] = oy;
+                }
+                a.rings[rid] = tessclip::ClipRing{k, (int32_t)(p - p0), (int32_t)(r - r0), (int64_t)off, (int32_t)(m + 1), 0};
+            }
+            if (any && !redo) {
+                const unsigned long long pid = atomicAdd(&a.counters[2], 1ull);
+                if ((int64_t)pid >= a.part_cap) redo = true;
+                else a.parts[pid] = tessclip::ClipPart{k, (int32_t)(p - p0), net > a.area_eps ? 1 : 0};
+            }
+        }
+        a.redo[t] = redo ? 1 : 0;
+    }
+}
+
 }  // namespace tessgpu
 
 // host side of the border clipping (tess_gpu.h)
+
+// The tasks split for k_tess_clip_lane (every ring of the geometry and the clip polygon small) and
+// k_tess_clip (the rest), uploaded as one selection list [small..., large...]; both kernels launched
+// (they append to the same outputs).
+static int launch_clip_kernels(ThreadCtx* c, tessgpu::ClipArgs a, int64_t n_tasks, const int64_t* tasks,
+                               const int32_t* cand_geom, const int64_t* geom_parts, const int64_t* part_rings,
+                               const int64_t* ring_offsets, int nv, int64_t n_waves, DevBuf& d_sel) {
+    std::vector<int64_t> sel((size_t)n_tasks);
+    int64_t n_small = 0, n_large = 0;
+    for (int64_t t = 0; t < n_tasks; t++) {
+        const int g = cand_geom[tasks[t]];
+        bool small = nv <= tessgpu::kClipLaneClip;
+        for (int64_t r = part_rings[geom_parts[g]]; small && r < part_rings[geom_parts[g + 1]]; r++)
+            small = ring_offsets[r + 1] - ring_offsets[r] - 1 <= tessgpu::kClipLaneRing;
+        if (small) sel[(size_t)n_small++] = t;
+        else sel[(size_t)(n_tasks - 1 - n_large++)] = t;
+    }
+    std::reverse(sel.begin() + n_small, sel.end());  // large ones in task order
+    int e = d_sel.reserve(std::max<size_t>((size_t)n_tasks * 8, 16));
+    if (e) return e;
+    if (n_tasks) HIP_TRY(hipMemcpyAsync(d_sel.p, sel.data(), (size_t)n_tasks * 8, hipMemcpyHostToDevice, c->stream));
+    if (n_small) {
+        a.tsel = (const int64_t*)d_sel.p;
+        a.n_sel = n_small;
+        const int64_t blocks = std::min<int64_t>((n_small + 255) / 256, (int64_t)c->n_cu * 8);
+        hipLaunchKernelGGL(tessgpu::k_tess_clip_lane, dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+    }
+    if (n_large) {
+        a.tsel = (const int64_t*)d_sel.p + n_small;
+        a.n_sel = n_large;
+        const int64_t w = std::max<int64_t>(1, std::min<int64_t>(n_waves, n_large));
+        hipLaunchKernelGGL(tessgpu::k_tess_clip, dim3((unsigned)((w + 3) / 4)), dim3(256), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+    }
+    return MOSAIC_OK;
+}
 int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                          const int64_t* ring_offsets, const double* pxy, const double* gxy, const int32_t* gface, int res,
                          int mode, int64_t n_tasks, const int64_t* tasks, const int32_t* cand_geom, int64_t n_cand,
@@ -5047,7 +5222,7 @@ int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_
     const int64_t cap = 2 * maxn + 4 * (int64_t)nv + 64, per_wave = 2 * cap * (16 + 4);
     const int64_t n_waves = std::max<int64_t>(1, std::min<int64_t>({n_tasks, (int64_t)c->n_cu * 8, ((int64_t)2 << 30) / per_wave}));
     const int64_t out_cap = 2 * n_verts + n_tasks * (3 * (int64_t)nv + 8) + 1024;
-    TmpBuf s_gp, s_pr, s_ro, s_pxy, s_gxy, s_gf, s_cg, s_clip, s_tasks, s_sxy, s_stag, s_out, s_cnt, s_rings, s_parts, s_redo;
+    TmpBuf s_gp, s_pr, s_ro, s_pxy, s_gxy, s_gf, s_cg, s_clip, s_tasks, s_sxy, s_stag, s_out, s_cnt, s_rings, s_parts, s_redo, s_sel;
     int rc;
     auto up = [&](TmpBuf& b, const void* src, size_t bytes) -> int {
         int e = b.reserve(std::max<size_t>(bytes, 16));
@@ -5098,10 +5273,12 @@ int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_
         (void)hipEventDestroy(e0);
         return fail(MOSAIC_E_HIP, "hipEventCreate failed");
     }
+    a.tsel = nullptr;
+    a.n_sel = 0;
     auto run = [&]() -> int {
         HIP_TRY(hipEventRecord(e0, c->stream));
-        hipLaunchKernelGGL(tessgpu::k_tess_clip, dim3((unsigned)((n_waves + 3) / 4)), dim3(256), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
+        int le = launch_clip_kernels(c, a, n_tasks, tasks, cand_geom, geom_parts, part_rings, ring_offsets, nv, n_waves, s_sel);
+        if (le) return le;
         HIP_TRY(hipEventRecord(e1, c->stream));
         unsigned long long cnt[3];
         HIP_TRY(hipMemcpyAsync(cnt, s_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
@@ -5138,10 +5315,10 @@ struct tessclip::H3Session {
     int res, D;
     double dx[6], dy[6];
     DevBuf d_gp, d_pr, d_ro, d_pxy, d_gxy, d_gf, d_cg, d_cxy, d_clip, d_cls, d_tasks;
-    DevBuf d_sxy, d_stag, d_out, d_cnt, d_rings, d_parts, d_redo;
+    DevBuf d_sxy, d_stag, d_out, d_cnt, d_rings, d_parts, d_redo, d_sel;
     void release() {
         for (DevBuf* b : {&d_gp, &d_pr, &d_ro, &d_pxy, &d_gxy, &d_gf, &d_cg, &d_cxy, &d_clip, &d_cls, &d_tasks, &d_sxy, &d_stag,
-                          &d_out, &d_cnt, &d_rings, &d_parts, &d_redo})
+                          &d_out, &d_cnt, &d_rings, &d_parts, &d_redo, &d_sel})
             b->release();
     }
 };
@@ -5312,9 +5489,12 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     a.rings = (ClipRing*)S->d_rings.p;
     a.parts = (ClipPart*)S->d_parts.p;
     a.redo = (uint8_t*)S->d_redo.p;
+    a.tsel = nullptr;
+    a.n_sel = 0;
     HIP_TRY(hipEventRecord(ev.e[0], c->stream));
-    hipLaunchKernelGGL(tessgpu::k_tess_clip, dim3((unsigned)((n_waves + 3) / 4)), dim3(256), 0, c->stream, a);
-    HIP_TRY(hipGetLastError());
+    if ((rc = launch_clip_kernels(c, a, n_tasks, tasks.data(), cand_geom, S->geom_parts, S->part_rings, S->ring_offsets, nv,
+                                  n_waves, S->d_sel)))
+        return rc;
     HIP_TRY(hipEventRecord(ev.e[1], c->stream));
     unsigned long long cnt[3];
     HIP_TRY(hipMemcpyAsync(cnt, S->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));

@@ -180,3 +180,37 @@ def test_h3_gpu_tessellation_holes_multipart_duplicates(ctx, res, densify):
     assert set(gpu["polygon_key"].tolist()) == {0, 2}
     assert gpu["is_core"].sum() > 0 and (gpu["is_core"] == 0).sum() > 0
     h3.close()
+
+
+def test_gpu_tessellation_small_rings_lane_kernel(ctx):
+    """Building-scale inputs go to k_tess_clip_lane (one lane per border cell: every ring <= 24
+    vertices, clip polygon <= 12 vertices); rings beyond that, or a densified hexagon of 18 sides,
+    to the wave kernel -- both must give the host producer's chip set byte for byte."""
+    from mosaic_amd.data import synthetic_buildings
+
+    bld = synthetic_buildings(20_000)
+    for res, densify in ((11, 1), (12, 2), (11, 3)):
+        host = tessellate("H3", bld, res, densify=densify)
+        gpu = tessellate("H3", bld, res, densify=densify, ctx=ctx)
+        _same(host, gpu)
+        assert (host["is_core"] == 0).sum() > 10_000
+    # BNG (clip squares, mode 1): small random polygons in London metres at 10 m cells, some with
+    # more than 24 vertices (wave kernel) beside the small ones
+    rng = np.random.default_rng(11)
+    rings = []
+    for i in range(3000):
+        cx, cy = rng.uniform(525000, 535000), rng.uniform(175000, 185000)
+        nvx = int(rng.integers(3, 40))
+        ang = np.sort(rng.uniform(0, 2 * np.pi, nvx))
+        rad = rng.uniform(8.0, 40.0, nvx)
+        ring = [(cx + r * np.cos(a), cy + r * np.sin(a)) for a, r in zip(ang, rad)]
+        rings.append(ring + ring[:1])
+    xy = np.array([p for r in rings for p in r], np.float64)
+    ring_offsets = np.cumsum([0] + [len(r) for r in rings]).astype(np.int64)
+    part_rings = np.arange(len(rings) + 1, dtype=np.int64)
+    geom_parts = np.arange(len(rings) + 1, dtype=np.int64)
+    polys = PolygonSet(xy, ring_offsets, part_rings, geom_parts)
+    host = tessellate("BNG", polys, 5)
+    gpu = tessellate("BNG", polys, 5, ctx=ctx)
+    _same(host, gpu)
+    assert (host["is_core"] == 0).sum() > 10_000
