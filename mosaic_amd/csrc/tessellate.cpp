@@ -258,6 +258,31 @@ struct WkbOut {
     }
 };
 
+// to a preallocated span (same bytes as WkbOut)
+struct WkbPtr {
+    uint8_t* b;
+    void u8(uint8_t v) { *b++ = v; }
+    void u32(uint32_t v) {
+        v = __builtin_bswap32(v);
+        memcpy(b, &v, 4);
+        b += 4;
+    }
+    void f64(double d) {
+        uint64_t u;
+        memcpy(&u, &d, 8);
+        u = __builtin_bswap64(u);
+        memcpy(b, &u, 8);
+        b += 8;
+    }
+};
+// counts bytes only
+struct WkbSize {
+    int64_t n = 0;
+    void u8(uint8_t) { n += 1; }
+    void u32(uint32_t) { n += 4; }
+    void f64(double) { n += 8; }
+};
+
 std::vector<uint8_t> to_wkb(const std::vector<std::vector<std::vector<P2>>>& parts) {
     WkbOut w;
     if (parts.size() == 1) {
@@ -273,12 +298,32 @@ std::vector<uint8_t> to_wkb(const std::vector<std::vector<std::vector<P2>>>& par
 
 }  // namespace
 
+// an allocator whose resize() leaves new bytes uninitialised (the writers fill them, in parallel)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... args) {
+        ::new ((void*)p) U(std::forward<A>(args)...);
+    }
+};
+
 struct mosaic_chip_set {
     std::vector<uint8_t> is_core;
     std::vector<int64_t> index_id;
     std::vector<int32_t> key;
     std::vector<int64_t> wkb_offsets{0};
-    std::vector<uint8_t> wkb;
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> wkb;
     void add(bool core, int64_t id, int32_t k, const std::vector<uint8_t>& blob) {
         is_core.push_back(core);
         index_id.push_back(id);
@@ -642,7 +687,8 @@ struct ClippedChips {
     }
     bool redo(int64_t k) const { return task_of[(size_t)k] < 0 || r.redo[(size_t)task_of[(size_t)k]]; }
     // candidate k's chip as WKB appended to w (to_wkb's bytes); false (nothing written): no chip
-    bool chip(int64_t k, WkbOut& w) const {
+    template <class W>
+    bool chip(int64_t k, W& w) const {
         const size_t ir = (size_t)(std::lower_bound(r.rings.begin(), r.rings.end(), k,
                                                     [](const tessclip::ClipRing& a, int64_t c) { return a.cand < c; }) -
                                    r.rings.begin());
@@ -844,30 +890,31 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         }
     };
     // per geometry (host threads, independent): face check, face-plane vertices (disjoint ranges of
-    // pxy), candidate lattice cells; concatenated in geometry order afterwards
-    struct GeomCands {
+    // pxy) and the lattice window; then the candidates counted, offsets by a prefix sum, and filled in
+    // place (geometry order) by the threads again -- no per-geometry vectors, no concatenation
+    struct GeomWin {
+        int face = -1, jlo = 0, jhi = -1;
         bool multi = false;
-        int face = -1;
-        std::vector<double> cxy;
-        std::vector<int64_t> cid;
+        double x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+        int64_t count = 0;
     };
-    std::vector<GeomCands> gc((size_t)n_geoms);
-    auto cands_of = [&](int64_t g) {
-        GeomCands& out = gc[(size_t)g];
+    std::vector<GeomWin> gw((size_t)n_geoms);
+    auto window_of = [&](int64_t g, std::vector<double>& u) {
+        GeomWin& w = gw[(size_t)g];
         const int64_t v0 = ring_offsets[part_rings[geom_parts[g]]], v1 = ring_offsets[part_rings[geom_parts[g + 1]]];
         if (v0 == v1) return;
         int face = -1;
         // unit vectors once per vertex (face test and projection: the same doubles as face_of / to_hex)
-        std::vector<double> u((size_t)(v1 - v0) * 3);
+        u.resize((size_t)(v1 - v0) * 3);
         for (int64_t v = v0; v < v1; v++) {
             double* pu = u.data() + 3 * (v - v0);
             FacePlane::unit(xy[2 * v], xy[2 * v + 1], pu);
             int f = face_of_unit(pu);
             if (face < 0) face = f;
-            out.multi = out.multi || f != face;
+            w.multi = w.multi || f != face;
         }
-        if (out.multi) return;  // spans faces: the host's per-face pieces (tessellate_h3_multiface)
-        out.face = face;
+        if (w.multi) return;  // spans faces: the host's per-face pieces (tessellate_h3_multiface)
+        w.face = face;
         FacePlane fp;
         fp.init(face, res);
         double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
@@ -880,41 +927,68 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             y0 = std::min(y0, p.y);
             y1 = std::max(y1, p.y);
         }
-        int jlo = (int)floor(y0 / s60) - 2, jhi = (int)ceil(y1 / s60) + 2;
-        for (int j = jlo; j <= jhi; j++) {
+        w.x0 = x0, w.y0 = y0, w.x1 = x1, w.y1 = y1;
+        w.jlo = (int)floor(y0 / s60) - 2;
+        w.jhi = (int)ceil(y1 / s60) + 2;
+        int64_t cnt = 0;
+        for (int j = w.jlo; j <= w.jhi; j++) {
             int ilo = (int)floor(x0 + j * 0.5) - 2, ihi = (int)ceil(x1 + j * 0.5) + 2;
             for (int i = ilo; i <= ihi; i++) {
                 double cx = i - 0.5 * j, cy = j * s60;
                 if (cx + R < x0 || cx - R > x1 || cy + R < y0 || cy - R > y1) continue;
-                out.cxy.push_back(cx);
-                out.cxy.push_back(cy);
+                cnt++;
+            }
+        }
+        w.count = cnt;
+    };
+    std::vector<int64_t> cand0((size_t)n_geoms + 1, 0);
+    auto fill_of = [&](int64_t g) {
+        const GeomWin& w = gw[(size_t)g];
+        if (w.multi || w.face < 0) return;
+        int64_t o = cand0[(size_t)g];
+        for (int j = w.jlo; j <= w.jhi; j++) {
+            int ilo = (int)floor(w.x0 + j * 0.5) - 2, ihi = (int)ceil(w.x1 + j * 0.5) + 2;
+            for (int i = ilo; i <= ihi; i++) {
+                double cx = i - 0.5 * j, cy = j * s60;
+                if (cx + R < w.x0 || cx - R > w.x1 || cy + R < w.y0 || cy - R > w.y1) continue;
+                cxy[2 * (size_t)o] = cx;
+                cxy[2 * (size_t)o + 1] = cy;
                 h3::IJK ijk = {i, j, 0};
                 h3::ijk_normalize(ijk);
-                out.cid.push_back((int64_t)h3::face_ijk_to_h3(face, ijk, res));
+                cid[(size_t)o] = (int64_t)h3::face_ijk_to_h3(w.face, ijk, res);
+                cg[(size_t)o] = (int32_t)g;
+                o++;
             }
         }
     };
     {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
             std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), n_geoms / 8));
-        std::atomic<int64_t> next(0);
-        auto work = [&]() {
-            for (int64_t g; (g = next.fetch_add(1)) < n_geoms;) cands_of(g);
+        auto pool_run = [&](auto body) {
+            std::atomic<int64_t> next(0);
+            auto work = [&]() {
+                std::vector<double> u;
+                for (int64_t g0; (g0 = next.fetch_add(64)) < n_geoms;)
+                    for (int64_t g = g0; g < std::min<int64_t>(g0 + 64, n_geoms); g++) body(g, u);
+            };
+            std::vector<std::thread> pool;
+            for (int k = 1; k < nt; k++) pool.emplace_back(work);
+            work();
+            for (auto& th : pool) th.join();
         };
-        std::vector<std::thread> pool;
-        for (int k = 1; k < nt; k++) pool.emplace_back(work);
-        work();
-        for (auto& th : pool) th.join();
+        pool_run([&](int64_t g, std::vector<double>& u) { window_of(g, u); });
+        for (int64_t g = 0; g < n_geoms; g++) {
+            cand0[(size_t)g + 1] = cand0[(size_t)g] + gw[(size_t)g].count;
+            if (gw[(size_t)g].multi) multi_geoms.push_back(g);
+            gface[g] = gw[(size_t)g].face;
+        }
+        const int64_t total = cand0[(size_t)n_geoms];
+        cxy.resize((size_t)total * 2);
+        cid.resize((size_t)total);
+        cg.resize((size_t)total);
+        pool_run([&](int64_t g, std::vector<double>&) { fill_of(g); });
     }
-    for (int64_t g = 0; g < n_geoms; g++) {
-        GeomCands& q = gc[(size_t)g];
-        if (q.multi) multi_geoms.push_back(g);
-        gface[g] = q.face;
-        cxy.insert(cxy.end(), q.cxy.begin(), q.cxy.end());
-        cid.insert(cid.end(), q.cid.begin(), q.cid.end());
-        cg.insert(cg.end(), q.cid.size(), (int32_t)g);
-    }
-    gc.clear();
+    gw.clear();
     trace.mark("h3 candidates (host)");
     // candidates in chunks, so the clip polygons staged on the host and the device stay bounded
     // (<= 64 MB of them per chunk) for any densify and envelope; chips come out in candidate order
@@ -977,19 +1051,21 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         cc.index(nc, tasks);
         trace.add(3);
         // the chunk's chips on host threads (each candidate's chip is independent: GPU-clipped border
-        // chips to WKB, core chips' outlines, cells the GPU clipper left to the host), then appended
-        // in candidate order
-        // thread t takes candidates [nc t / nt, nc (t + 1) / nt) and appends their WKB to its own buffer,
-        // so the buffers concatenated in thread order are the chunk's WKB in candidate order
+        // chips to WKB, core chips' outlines, cells the GPU clipper left to the host).  Thread t takes
+        // candidates [nc t / nt, nc (t + 1) / nt): GPU-clipped chips are sized first and written in
+        // place into the chip set afterwards (offsets by a prefix sum); the others are built into the
+        // thread's buffer and copied.  (With face-spanning geometries in the batch, whose chips are
+        // emitted between these, every chip goes through the thread buffers and is appended in order.)
         struct OneChip {
-            int64_t off = 0;  // in the thread's buffer
+            int64_t off = 0;   // in the thread's buffer (built chips), then in the chip set's wkb
             int32_t len = -1;  // -1: no chip
-            uint8_t core = 0;
+            uint8_t core = 0, built = 0;
         };
         std::vector<OneChip> chips((size_t)nc);
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
             std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), nc / 256));
         std::vector<WkbOut> bufs((size_t)nt);
+        const bool direct = multi_geoms.empty();
         {
             auto work = [&](int t) {
                 std::vector<std::vector<std::vector<P2>>> geo, pl;
@@ -1005,9 +1081,16 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
                     if (!cls[kk]) continue;
                     o.off = (int64_t)w.b.size();
                     if (cls[kk] == 2 && !cc.redo(kk)) {
-                        if (cc.chip(kk, w)) o.len = (int32_t)((int64_t)w.b.size() - o.off);
+                        if (direct) {
+                            WkbSize z;
+                            if (cc.chip(kk, z)) o.len = (int32_t)z.n;
+                        } else {
+                            o.built = 1;
+                            if (cc.chip(kk, w)) o.len = (int32_t)((int64_t)w.b.size() - o.off);
+                        }
                         continue;
                     }
+                    o.built = 1;
                     if (cg[k] != cur) {
                         cur = cg[k];
                         fp.init(gface[cur], res);
@@ -1051,6 +1134,51 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
             for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
             work(0);
             for (auto& th : pool) th.join();
+        }
+        if (direct) {
+            // offsets, index columns, then the WKB written in place by the threads
+            int64_t n_chips = 0, n_bytes = 0;
+            for (auto& o : chips)
+                if (o.len >= 0) n_chips++, n_bytes += o.len;
+            const size_t c0 = cs->index_id.size(), w0 = cs->wkb.size();
+            cs->is_core.resize(c0 + (size_t)n_chips);
+            cs->index_id.resize(c0 + (size_t)n_chips);
+            cs->key.resize(c0 + (size_t)n_chips);
+            cs->wkb_offsets.resize(c0 + 1 + (size_t)n_chips);
+            cs->wkb.resize(w0 + (size_t)n_bytes);
+            std::vector<int64_t> src_off((size_t)nc, 0);
+            size_t ci = c0;
+            int64_t wo = (int64_t)w0;
+            for (int64_t kk = 0; kk < nc; kk++) {
+                OneChip& o = chips[(size_t)kk];
+                if (o.len < 0) continue;
+                cs->is_core[ci] = o.core;
+                cs->index_id[ci] = cid[k0 + kk];
+                cs->key[ci] = cg[k0 + kk];
+                src_off[(size_t)kk] = o.off;
+                o.off = wo;
+                wo += o.len;
+                cs->wkb_offsets[++ci] = wo;
+            }
+            trace.add(4);
+            auto write = [&](int t) {
+                for (int64_t kk = nc * t / nt; kk < nc * (t + 1) / nt; kk++) {
+                    const OneChip& o = chips[(size_t)kk];
+                    if (o.len <= 0) continue;
+                    if (o.built) {
+                        memcpy(cs->wkb.data() + o.off, bufs[(size_t)t].b.data() + src_off[(size_t)kk], (size_t)o.len);
+                    } else {
+                        WkbPtr w{cs->wkb.data() + o.off};
+                        cc.chip(kk, w);
+                    }
+                }
+            };
+            std::vector<std::thread> pool;
+            for (int t = 1; t < nt; t++) pool.emplace_back(write, t);
+            write(0);
+            for (auto& th : pool) th.join();
+            trace.add(5);
+            continue;
         }
         trace.add(4);
         int64_t n_chips = 0, n_bytes = 0;
