@@ -662,11 +662,13 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
 struct ClippedChips {
     tessclip::ClipResult r;
     std::vector<int64_t> task_of;  // candidate -> task (-1: not a border task)
+    std::vector<int64_t> ring_at, part_at;  // candidate c's rings / parts: [ring_at[c], ring_at[c + 1])
     void index(int64_t n_cand, const std::vector<int64_t>& tasks) {
-        // stable counting sort by candidate (the kernel appends each candidate's rings / parts in
-        // (part, ring) order from one wave; a candidate whose entries are not is sorted on its own)
-        auto by_cand = [&](auto& v, auto less) {
-            std::vector<int64_t> start((size_t)n_cand + 1, 0);
+        // stable counting sort by candidate (the kernels append each candidate's rings / parts in
+        // (part, ring) order from one wave or lane; a candidate whose entries are not is sorted on
+        // its own), keeping each candidate's start
+        auto by_cand = [&](auto& v, auto less, std::vector<int64_t>& start) {
+            start.assign((size_t)n_cand + 1, 0);
             for (auto& e : v) start[(size_t)e.cand + 1]++;
             for (int64_t c = 0; c < n_cand; c++) start[(size_t)c + 1] += start[(size_t)c];
             std::remove_reference_t<decltype(v)> out(v.size());
@@ -674,14 +676,14 @@ struct ClippedChips {
             for (auto& e : v) out[(size_t)pos[(size_t)e.cand]++] = e;
             for (int64_t c = 0; c < n_cand; c++) {
                 auto b = out.begin() + start[(size_t)c], e = out.begin() + start[(size_t)c + 1];
-                if (!std::is_sorted(b, e, less)) std::sort(b, e, less);
+                if (e - b > 1 && !std::is_sorted(b, e, less)) std::sort(b, e, less);
             }
             v.swap(out);
         };
         by_cand(r.rings, [](const tessclip::ClipRing& a, const tessclip::ClipRing& b) {
             return a.part != b.part ? a.part < b.part : a.ring < b.ring;
-        });
-        by_cand(r.parts, [](const tessclip::ClipPart& a, const tessclip::ClipPart& b) { return a.part < b.part; });
+        }, ring_at);
+        by_cand(r.parts, [](const tessclip::ClipPart& a, const tessclip::ClipPart& b) { return a.part < b.part; }, part_at);
         task_of.assign((size_t)n_cand, -1);
         for (size_t t = 0; t < tasks.size(); t++) task_of[(size_t)tasks[t]] = (int64_t)t;
     }
@@ -689,12 +691,7 @@ struct ClippedChips {
     // candidate k's chip as WKB appended to w (to_wkb's bytes); false (nothing written): no chip
     template <class W>
     bool chip(int64_t k, W& w) const {
-        const size_t ir = (size_t)(std::lower_bound(r.rings.begin(), r.rings.end(), k,
-                                                    [](const tessclip::ClipRing& a, int64_t c) { return a.cand < c; }) -
-                                   r.rings.begin());
-        const size_t ip = (size_t)(std::lower_bound(r.parts.begin(), r.parts.end(), k,
-                                                    [](const tessclip::ClipPart& a, int64_t c) { return a.cand < c; }) -
-                                   r.parts.begin());
+        const size_t ir = (size_t)ring_at[(size_t)k], ip = (size_t)part_at[(size_t)k];
         // the kept parts that have rings: (first ring, ring count)
         std::pair<size_t, size_t> kept[64];
         std::vector<std::pair<size_t, size_t>> more;
