@@ -295,6 +295,11 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                       mosaic_chip_set** out);
 int mosaic_chip_set_info(const mosaic_chip_set* cs, int64_t* n_chips, int64_t* wkb_bytes);
 /* Copies the chip rows out: is_core[n], index_id[n], key[n], wkb_offsets[n+1], wkb[wkb_bytes]. */
+/* Zero-copy view of the same columns: pointers into the chip set, valid until mosaic_chip_set_destroy
+ * (what mosaic_chip_set_export copies; the Python binding wraps them and destroys the set with the
+ * last array). */
+int mosaic_chip_set_columns(const mosaic_chip_set* cs, const uint8_t** is_core, const int64_t** index_id,
+                            const int32_t** key, const int64_t** wkb_offsets, const uint8_t** wkb);
 int mosaic_chip_set_export(const mosaic_chip_set* cs, uint8_t* is_core, int64_t* index_id, int32_t* key,
                            int64_t* wkb_offsets, uint8_t* wkb);
 int mosaic_chip_set_destroy(mosaic_chip_set* cs);

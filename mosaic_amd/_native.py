@@ -34,7 +34,7 @@ EXPORTS = [
     "mosaic_chip_table_tile_grid", "mosaic_chip_table_raster", "mosaic_pip_join_count",
     "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_tessellate_gpu",
     "mosaic_tess_last_classify_ms", "mosaic_chip_set_info",
-    "mosaic_chip_set_export", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_last_kernel", "mosaic_point_geom_to_cell",
+    "mosaic_chip_set_export", "mosaic_chip_set_columns", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_last_kernel", "mosaic_point_geom_to_cell",
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
     "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb", "mosaic_point_to_cell_exact",
     "mosaic_diag_libm", "mosaic_point_coords_to_cell", "mosaic_point_coords_decode", "mosaic_bng_parse_column",
@@ -118,6 +118,8 @@ def lib():
         "mosaic_tessellate": ([i32, i32, i64, vp, vp, vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
         "mosaic_chip_set_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
         "mosaic_chip_set_export": ([vp, vp, vp, vp, vp, vp], i32),
+        "mosaic_chip_set_columns": ([vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                     ctypes.POINTER(vp)], i32),
         "mosaic_chip_set_destroy": ([vp], i32),
         "mosaic_kernel_times": ([vp, vp, i64, ctypes.POINTER(i64)], i32),
         "mosaic_last_kernel": ([vp], ctypes.c_char_p),

@@ -866,18 +866,37 @@ def tessellate(index_system, polygons, resolution, keep_core_geom=True, densify=
                                           N.ptr(polygons.part_rings), N.ptr(polygons.ring_offsets),
                                           N.ptr(polygons.xy), int(bool(keep_core_geom)), int(densify),
                                           ctypes.byref(h)))
-    try:
-        n = ctypes.c_int64(0)
-        nb = ctypes.c_int64(0)
-        N.check(N.lib().mosaic_chip_set_info(h, ctypes.byref(n), ctypes.byref(nb)))
-        n, nb = n.value, nb.value
-        is_core = np.zeros(n, np.uint8)
-        index_id = np.zeros(n, np.int64)
-        key = np.zeros(n, np.int32)
-        offs = np.zeros(n + 1, np.int64)
-        data = np.zeros(max(nb, 1), np.uint8)
-        N.check(N.lib().mosaic_chip_set_export(h, N.ptr(is_core), N.ptr(index_id), N.ptr(key), N.ptr(offs),
-                                               N.ptr(data)))
-    finally:
-        N.lib().mosaic_chip_set_destroy(h)
+    # zero-copy: the arrays view the chip set's own columns, which live until the last of them is
+    # collected (_ChipSetOwner destroys the set)
+    owner = _ChipSetOwner(h)
+    n = ctypes.c_int64(0)
+    nb = ctypes.c_int64(0)
+    N.check(N.lib().mosaic_chip_set_info(h, ctypes.byref(n), ctypes.byref(nb)))
+    n, nb = n.value, nb.value
+    p = [ctypes.c_void_p() for _ in range(5)]
+    N.check(N.lib().mosaic_chip_set_columns(h, *[ctypes.byref(q) for q in p]))
+    is_core = owner.view(p[0], n, ctypes.c_uint8, np.uint8)
+    index_id = owner.view(p[1], n, ctypes.c_int64, np.int64)
+    key = owner.view(p[2], n, ctypes.c_int32, np.int32)
+    offs = owner.view(p[3], n + 1, ctypes.c_int64, np.int64)
+    data = owner.view(p[4], nb, ctypes.c_uint8, np.uint8) if nb else np.zeros(1, np.uint8)
     return dict(is_core=is_core, index_id=index_id, polygon_key=key, wkb=(offs, data))
+
+
+class _ChipSetOwner:
+    """Holds a mosaic_chip_set whose columns numpy arrays view; destroyed with the last of them."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def view(self, ptr, n, ctype, dtype):
+        if n == 0 or not ptr.value:
+            return np.zeros(0, dtype)
+        buf = (ctype * n).from_address(ptr.value)
+        buf._owner = self  # the arrays' base keeps the set alive
+        return np.frombuffer(buf, dtype=dtype)
+
+    def __del__(self):
+        if self.h:
+            N.lib().mosaic_chip_set_destroy(self.h)
+            self.h = None

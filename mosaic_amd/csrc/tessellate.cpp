@@ -1336,6 +1336,17 @@ int mosaic_chip_set_info(const mosaic_chip_set* cs, int64_t* n_chips, int64_t* w
     return MOSAIC_OK;
 }
 
+int mosaic_chip_set_columns(const mosaic_chip_set* cs, const uint8_t** is_core, const int64_t** index_id,
+                            const int32_t** key, const int64_t** wkb_offsets, const uint8_t** wkb) {
+    if (!cs || !is_core || !index_id || !key || !wkb_offsets || !wkb) return mosaic_tess_fail(MOSAIC_E_ARG, "null argument");
+    *is_core = cs->is_core.data();
+    *index_id = cs->index_id.data();
+    *key = cs->key.data();
+    *wkb_offsets = cs->wkb_offsets.data();
+    *wkb = cs->wkb.data();
+    return MOSAIC_OK;
+}
+
 int mosaic_chip_set_export(const mosaic_chip_set* cs, uint8_t* is_core, int64_t* index_id, int32_t* key,
                            int64_t* wkb_offsets, uint8_t* wkb) {
     if (!cs) return mosaic_tess_fail(MOSAIC_E_ARG, "null chip set");
