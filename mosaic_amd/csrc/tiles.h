@@ -330,11 +330,12 @@ struct Builder {
     //            then scan order) a line record (kind 1) or its C x C cell codes (kind 0);
     //   phase 2: sub-block entries, per-tile line records and leaf blocks, quad level.
     struct RasterClass {
-        std::vector<uint16_t> code;     // records x S x S (scan order sj S + si)
+        // (code and cells are filled by device-to-host copies: not value-initialised)
+        std::vector<uint16_t, NoInitAlloc<uint16_t>> code;  // records x S x S (scan order sj S + si)
         std::vector<uint8_t> kind;      // per mixed sub-block
         std::vector<LineRec> line;      // per mixed sub-block (kind 1)
         std::vector<uint32_t> cell_at;  // per mixed sub-block (kind 0): its block of C x C codes in cells
-        std::vector<uint16_t> cells;
+        std::vector<uint16_t, NoInitAlloc<uint16_t>> cells;
     };
     std::vector<int> tile_of_rec;  // record -> tile (raster_setup)
     bool raster_setup(const ChipSource& src, int S_, int C_);
