@@ -540,8 +540,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 // cs + kFixBits + qs bits of both fixed-point fine-cell coordinates (leaf cell, line offsets and the
 // sub-block within the quad; L <= 20), the source lane and row slot, the quad entry and the tile.
 // Same answers as k_join_stream_pipe, point for point.
-#ifndef MOSAIC_CPT_DEPTH
-#define MOSAIC_CPT_DEPTH 1
+// 1: a group's second set of pending rows (65 - 128) is pipelined like the first
+#ifndef MOSAIC_CPT_TWO
+#define MOSAIC_CPT_TWO 1
 #endif
 // 1: compaction through a per-wave LDS buffer; 0: ds_permute (no LDS memory)
 #ifndef MOSAIC_CPT_LDS
@@ -649,7 +650,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     };
     // --- stage A of a group: LDS levels, resolved rows answered, pending rows compacted into z (the
     // first 64); more than 64 pending rows: the rest finished here
-    auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, CptSet& z, int64_t wb) {
+    auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, CptSet& z, CptSet& z2, bool& two,
+                       int64_t wb) {
         uint32_t fa[4], fb[4], fc[4];
         bool pend[4];
 #pragma unroll
@@ -738,8 +740,14 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #endif
         gather_set(0u, z);
         set_a(z);
-        if (P > 64u) {  // (wave-uniform) the group's further sets, unpipelined
-            for (uint32_t sv = 1; sv * 64u < P; sv++) {
+        // a second set (65 - 128 pending rows, clustered input) is pipelined too (MOSAIC_CPT_TWO)
+        two = MOSAIC_CPT_TWO && P > 64u;
+        if (two) {
+            gather_set(1u, z2);
+            set_a(z2);
+        }
+        if (P > (two ? 128u : 64u)) {  // (wave-uniform) the group's further sets, unpipelined
+            for (uint32_t sv = two ? 2 : 1; sv * 64u < P; sv++) {
                 CptSet o;
                 gather_set(sv, o);
                 set_a(o);
@@ -758,77 +766,43 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
         cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
     };
-    Coords cb0, cb1, cb2;
-    CptSet z0, z1;
+    CptSet z0, z1, y0, y1;  // y: the second set of the same group
+    bool two0 = false, two1 = false;
     z0.a = z1.a = z0.b = z1.b = z0.c = z1.c = z0.code = z1.code = z0.leaf = z1.leaf = 0u;
     z0.lrec = z1.lrec = v4u{0u, 0u, 0u, 0u};
-    // zfin: the set of t - 2, refilled with group t; zadv: the set of t - 1.  Coordinates are loaded
-    // MOSAIC_CPT_DEPTH groups ahead: cb holds group t, cn is loaded with group t + DEPTH (with depth
-    // 1, cn is the other buffer; with depth 2, the buffers rotate over three)
-    auto step = [&](auto VALID, int64_t t, CptSet& zfin, CptSet& zadv, Coords& cb, Coords& cn) {
+    // zfin (yfin): the set(s) of t - 2, refilled with group t; zadv (yadv): the set(s) of t - 1
+    auto step = [&](auto VALID, int64_t t, CptSet& zfin, CptSet& yfin, bool& tfin, CptSet& zadv, CptSet& yadv, bool tadv,
+                    Coords& cb, Coords& cn) {
         const bool all[4] = {true, true, true, true};
-        if (t >= 2) set_d(zfin, wbase + (t - 2) * stride);
+        if (t >= 2) {
+            set_d(zfin, wbase + (t - 2) * stride);
+            if (tfin) set_d(yfin, wbase + (t - 2) * stride);
+        }
         set_b(zadv);
+        if (tadv) set_b(yadv);
         const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
         const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
-        stage_a(x, y, all, decltype(VALID)::value, zfin, wbase + t * stride);
-        load4(cn, wbase + (t + MOSAIC_CPT_DEPTH) * stride, t + MOSAIC_CPT_DEPTH < T);
-    };
-    auto step_rt = [&](bool valid, int64_t t, CptSet& zfin, CptSet& zadv, Coords& cb, Coords& cn) {
-        const bool all[4] = {true, true, true, true};
-        if (t >= 2) set_d(zfin, wbase + (t - 2) * stride);
-        set_b(zadv);
-        const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
-        const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
-        stage_a(x, y, all, valid, zfin, wbase + t * stride);
-        load4(cn, wbase + (t + MOSAIC_CPT_DEPTH) * stride, t + MOSAIC_CPT_DEPTH < T);
+        stage_a(x, y, all, decltype(VALID)::value, zfin, yfin, tfin, wbase + t * stride);
+        load4(cn, wbase + (t + 1) * stride, t + 1 < T);
     };
     if (T > 0) {
+        Coords cb0, cb1;
         const std::true_type full;
         const std::false_type drain;
         int64_t t = 0;
-#if MOSAIC_CPT_DEPTH == 2
-        load4(cb0, wbase, true);
-        load4(cb1, wbase + stride, 1 < T);
-        // slots: set t % 2, coordinates t % 3 (six steps per turn)
-        for (; t + 6 <= T; t += 6) {
-            step(full, t, z0, z1, cb0, cb2);
-            step(full, t + 1, z1, z0, cb1, cb0);
-            step(full, t + 2, z0, z1, cb2, cb1);
-            step(full, t + 3, z1, z0, cb0, cb2);
-            step(full, t + 4, z0, z1, cb1, cb0);
-            step(full, t + 5, z1, z0, cb2, cb1);
-        }
-        // the remaining groups (<= 5) and the two drain steps, in the same slot sequence (validity
-        // tested at run time here)
-#define MOSAIC_CPT_TAIL(ZF, ZA, CB, CN) \
-    if (t < T + 2) {                    \
-        step_rt(t < T, t, ZF, ZA, CB, CN); \
-        t++;                            \
-    }
-        MOSAIC_CPT_TAIL(z0, z1, cb0, cb2)
-        MOSAIC_CPT_TAIL(z1, z0, cb1, cb0)
-        MOSAIC_CPT_TAIL(z0, z1, cb2, cb1)
-        MOSAIC_CPT_TAIL(z1, z0, cb0, cb2)
-        MOSAIC_CPT_TAIL(z0, z1, cb1, cb0)
-        MOSAIC_CPT_TAIL(z1, z0, cb2, cb1)
-        MOSAIC_CPT_TAIL(z0, z1, cb0, cb2)
-#undef MOSAIC_CPT_TAIL
-#else
         load4(cb0, wbase, true);
         for (; t + 2 <= T; t += 2) {
-            step(full, t, z0, z1, cb0, cb1);
-            step(full, t + 1, z1, z0, cb1, cb0);
+            step(full, t, z0, y0, two0, z1, y1, two1, cb0, cb1);
+            step(full, t + 1, z1, y1, two1, z0, y0, two0, cb1, cb0);
         }
         if (t < T) {
-            step(full, t, z0, z1, cb0, cb1);
-            step(drain, t + 1, z1, z0, cb1, cb0);
-            step(drain, t + 2, z0, z1, cb0, cb1);
+            step(full, t, z0, y0, two0, z1, y1, two1, cb0, cb1);
+            step(drain, t + 1, z1, y1, two1, z0, y0, two0, cb1, cb0);
+            step(drain, t + 2, z0, y0, two0, z1, y1, two1, cb0, cb1);
         } else {
-            step(drain, t, z0, z1, cb0, cb1);
-            step(drain, t + 1, z1, z0, cb1, cb0);
+            step(drain, t, z0, y0, two0, z1, y1, two1, cb0, cb1);
+            step(drain, t + 1, z1, y1, two1, z0, y0, two0, cb1, cb0);
         }
-#endif
     }
     // the wave's partial group (rows past its last full group), unpipelined
     const int64_t wt = wbase + T * stride;
@@ -842,10 +816,15 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             x[k] = live[k] ? a.x[r] : 0.0;
             y[k] = live[k] ? a.y[r] : 0.0;
         }
-        CptSet z;
-        stage_a(x, y, live, true, z, wt);
+        CptSet z, z2;
+        bool two = false;
+        stage_a(x, y, live, true, z, z2, two, wt);
         set_b(z);
         set_d(z, wt);
+        if (two) {
+            set_b(z2);
+            set_d(z2, wt);
+        }
     }
     stage_flush(a, wq, wn, lane, 1);
     if (LDS_COUNTS) {
