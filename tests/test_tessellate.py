@@ -115,3 +115,23 @@ def test_reference_tessellation_fixtures():
     assert len(c["index_id"]) > 0
     # every chip's polygon key is the input geometry and its cell holds part of the polygon
     assert set(c["polygon_key"].tolist()) == {0}
+
+
+def test_chip_set_zero_copy_lifetime():
+    """tessellate()'s arrays view the chip set's own columns (mosaic_chip_set_columns): the set lives
+    until the last array is collected, and the views equal a copying export of the same set."""
+    import gc
+
+    from mosaic_amd.data import PolygonSet
+
+    zones = PolygonSet.load("nyc_taxi_zones_35")
+    a = tessellate("H3", zones, 8)
+    b = tessellate("H3", zones, 8)
+    wkb_offs, wkb = a["wkb"]
+    ids = a["index_id"].copy()
+    del a
+    gc.collect()
+    _ = [np.zeros(1 << 16) for _ in range(64)]  # reuse freed memory, if any were freed
+    assert np.array_equal(wkb_offs, b["wkb"][0]) and np.array_equal(wkb, b["wkb"][1])
+    assert np.array_equal(ids, b["index_id"])
+    assert wkb_offs[-1] == len(wkb) and wkb_offs[0] == 0
