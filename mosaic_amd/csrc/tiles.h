@@ -42,7 +42,9 @@
 #include "raster_build.h"
 
 #include <algorithm>
+#include <atomic>
 #include <functional>
+#include <thread>
 #include <vector>
 
 namespace mosaic {
@@ -421,11 +423,32 @@ struct Builder {
         rec_dev.clear();
         res_ = res;
         std::vector<uint8_t> found(cells.size(), 0);
-        std::vector<int64_t> slot_cell;  // slot -> position in cells (for the found flags)
-        double smin = INFINITY;
+        // slot -> position in cells (for the found flags)
+        std::vector<int64_t> slot_cell;
+        {
+            int64_t mx = -1;
+            for (size_t q = 0; q < cells.size(); q++) mx = std::max(mx, slot_of(cells[q]));
+            slot_cell.assign((size_t)std::max<int64_t>(mx + 1, 0), -1);
+            for (size_t q = 0; q < cells.size(); q++) {
+                const int64_t sl = slot_of(cells[q]);
+                if (sl >= 0) slot_cell[(size_t)sl] = (int64_t)q;
+            }
+        }
         n_full = n_skip = 0;
-        std::vector<uint32_t> win;
-        for (int j = 0; j < ny; j++) {
+        // tile rows on host threads (each tile is independent; found flags are only ever set to 1),
+        // then merged in row order: records and window entries exactly as a sequential scan
+        struct RowOut {
+            std::vector<uint32_t> code;  // per tile: kFull, kSkip, or 2 + the row-local record
+            std::vector<TileRec> recs;
+            std::vector<double> dev;
+            std::vector<uint32_t> entries;
+            double smin = INFINITY;
+        };
+        std::vector<RowOut> rows((size_t)ny);
+        auto do_row = [&](int j) {
+            RowOut& ro = rows[(size_t)j];
+            ro.code.assign((size_t)nx, kFull);
+            std::vector<uint32_t> win;
             for (int i = 0; i < nx; i++) {
                 // tile bounds exactly as the kernel's index computes them (to rounding)
                 double lon0 = grid.x0 + i * tw, lat0 = grid.y0 + j * th;
@@ -433,7 +456,7 @@ struct Builder {
                 uint32_t code = kFull;
                 double dev = 1.0;
                 if (sample(lon0, lat0, tw, th, res, &s) && (dev = patch_dev(s)) <= 0.05) {
-                    smin = std::min(smin, sigma_min(s, tw, th));
+                    ro.smin = std::min(ro.smin, sigma_min(s, tw, th));
                     double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
                     for (int q = 0; q < 9; q++) {
                         amin = std::min(amin, s.a[q]);
@@ -455,29 +478,60 @@ struct Builder {
                                 if (slot < 0) continue;
                                 win[(size_t)ra * wb + rb] = (uint32_t)slot + 1;
                                 any = true;
-                                if (inner) mark_found(slot, cells, slot_of, found, slot_cell);
+                                if (inner && slot < (int64_t)slot_cell.size() && slot_cell[(size_t)slot] >= 0)
+                                    found[(size_t)slot_cell[(size_t)slot]] = 1;
                             }
                         }
                         if (!any) {
                             code = kSkip;
                         } else {
-                            if (entries.size() + win.size() >= ((size_t)1 << 26)) return fail("window entries");
                             TileRec r;
                             r.a0 = a0;
                             r.b0 = b0;
-                            r.off = (uint32_t)entries.size();
+                            r.off = (uint32_t)ro.entries.size();  // row-local until the merge
                             r.dims = (uint32_t)s.face | ((uint32_t)wa << 8) | ((uint32_t)wb << 20);
-                            entries.insert(entries.end(), win.begin(), win.end());
-                            code = (uint32_t)recs.size() + 2;
-                            recs.push_back(r);
-                            rec_dev.push_back(dev);
+                            ro.entries.insert(ro.entries.end(), win.begin(), win.end());
+                            code = (uint32_t)ro.recs.size() + 2;
+                            ro.recs.push_back(r);
+                            ro.dev.push_back(dev);
                         }
                     }
                 }
+                ro.code[(size_t)i] = code;
+            }
+        };
+        {
+            const int nt = (int)std::max(1, std::min({16, (int)std::max(1u, std::thread::hardware_concurrency()), ny}));
+            std::atomic<int> next(0);
+            auto work = [&]() {
+                for (int j; (j = next.fetch_add(1)) < ny;) do_row(j);
+            };
+            std::vector<std::thread> pool;
+            for (int t = 1; t < nt; t++) pool.emplace_back(work);
+            work();
+            for (auto& th : pool) th.join();
+        }
+        double smin = INFINITY;
+        for (int j = 0; j < ny; j++) {
+            RowOut& ro = rows[(size_t)j];
+            smin = std::min(smin, ro.smin);
+            const uint32_t rec0 = (uint32_t)recs.size();
+            const size_t ent0 = entries.size();
+            if (ent0 + ro.entries.size() >= ((size_t)1 << 26)) return fail("window entries");
+            for (TileRec r : ro.recs) {
+                r.off += (uint32_t)ent0;
+                recs.push_back(r);
+            }
+            rec_dev.insert(rec_dev.end(), ro.dev.begin(), ro.dev.end());
+            entries.insert(entries.end(), ro.entries.begin(), ro.entries.end());
+            for (int i = 0; i < nx; i++) {
+                uint32_t code = ro.code[(size_t)i];
                 if (code == kFull) n_full++;
-                if (code == kSkip) n_skip++;
+                else if (code == kSkip) n_skip++;
+                else code += rec0;
                 tile_idx[(size_t)j * nx + i] = code;
             }
+            std::vector<uint32_t>().swap(ro.entries);
         }
         // coverage: every chip cell found in an inner tile, and k rings span the cell reach
         for (size_t q = 0; q < cells.size(); q++)
@@ -524,20 +578,6 @@ struct Builder {
             d = std::max(d, std::max(fabs(pa - s.a[q]), fabs(pb - s.b[q])));
         }
         return d;
-    }
-    static void mark_found(int64_t slot, const std::vector<int64_t>& cells,
-                           const std::function<int64_t(int64_t)>& slot_of, std::vector<uint8_t>& found,
-                           std::vector<int64_t>& slot_cell) {
-        if (slot_cell.empty()) {
-            int64_t mx = -1;
-            for (size_t q = 0; q < cells.size(); q++) mx = std::max(mx, slot_of(cells[q]));
-            slot_cell.assign((size_t)mx + 1, -1);
-            for (size_t q = 0; q < cells.size(); q++) {
-                int64_t sl = slot_of(cells[q]);
-                if (sl >= 0) slot_cell[(size_t)sl] = (int64_t)q;
-            }
-        }
-        if (slot < (int64_t)slot_cell.size() && slot_cell[(size_t)slot] >= 0) found[(size_t)slot_cell[(size_t)slot]] = 1;
     }
 #endif  // !__HIPCC__
 };
