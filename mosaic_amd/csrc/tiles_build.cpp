@@ -438,6 +438,18 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
     const int64_t NX = (int64_t)nx * S, NY = (int64_t)ny * S;
     const size_t SS = (size_t)S * S, CC = (size_t)C * C;
     sub.clear();
+    {
+        // room for the quad level's compact copies too (appended below), so that growing the table
+        // neither moves it nor faults its pages in on one thread
+        int qs = 0;
+        while (qs < 16 && ((NX + (1 << qs) - 1) >> qs) * ((NY + (1 << qs) - 1) >> qs) > quad_max) qs++;
+        int64_t extra = 0;
+        if (qs <= 6) {
+            const int64_t nq = ((NX + (1 << qs) - 1) >> qs) * ((NY + (1 << qs) - 1) >> qs);
+            extra = std::min<int64_t>(nq, kQuadRefMax + 1) << (2 * qs);
+        }
+        sub.reserve((size_t)(NX * NY + extra));
+    }
     sub.resize((size_t)(NX * NY));  // (uninitialised: every tile's entries are written below)
     tile_base.assign((size_t)nx * ny, 0u);
     std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
@@ -609,7 +621,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
         for (uint16_t e : quad) nref += e == kMixed;
         if (qshift <= 6 && nref <= kQuadRefMax + 1 && NX * NY + nref * QQ < ((int64_t)1 << 31)) {
             const size_t base = sub.size();
-            sub.resize(base + (size_t)(nref * QQ), 0);
+            sub.resize(base + (size_t)(nref * QQ));  // (uninitialised: every entry is written below)
             std::vector<int64_t> refq;  // compact quad r -> quad (row-major order)
             refq.reserve((size_t)nref);
             for (int64_t q = 0; q < (int64_t)quad.size(); q++)
@@ -621,7 +633,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
                     for (int64_t dj = 0; dj < QS; dj++)
                         for (int64_t di = 0; di < QS; di++) {
                             const int64_t j = qj * QS + dj, i = qi * QS + di;
-                            if (j < NY && i < NX) dst[dj * QS + di] = sub[(size_t)(j * NX + i)];
+                            dst[dj * QS + di] = j < NY && i < NX ? sub[(size_t)(j * NX + i)] : (uint16_t)0;
                         }
                     quad[(size_t)refq[(size_t)r]] = (uint16_t)(kSubBlock | r);
                 }
