@@ -39,7 +39,8 @@
  *     device memory of the context's GPU (detected per pointer).  Host inputs are staged over PCIe.
  *     Device inputs must be complete when the call's work starts: the context's own streams are
  *     non-blocking (no implicit order with the null stream), so a caller producing columns on another
- *     stream either binds that stream with mosaic_set_stream or synchronises it first.
+ *     stream binds that stream with mosaic_set_stream, records an event on it and passes it to
+ *     mosaic_stream_wait_event before the call, or synchronises it first.
  *   - Calls are synchronous unless the context option "async" is 1, in which case device-pointer
  *     calls only enqueue work on the calling thread's stream (mosaic_sync() waits and reports
  *     deferred errors).
@@ -126,6 +127,11 @@ int mosaic_thread_count(mosaic_ctx* ctx, int64_t* n_threads, int64_t* scratch_by
 /* The calling thread's hipStream_t (created by the context unless set by this thread). */
 int mosaic_get_stream(mosaic_ctx* ctx, void** stream);
 int mosaic_set_stream(mosaic_ctx* ctx, void* stream);
+/* Orders the calling thread's later work after a caller event: enqueues hipStreamWaitEvent(stream,
+ * (hipEvent_t)event) on the thread's stream, so device columns produced on another stream (a cuDF /
+ * Arrow producer, torch) are complete before the next call reads them, without binding that stream
+ * or blocking the host.  The event must have been recorded (hipEventRecord) before this call. */
+int mosaic_stream_wait_event(mosaic_ctx* ctx, void* event);
 /* Wait for enqueued work; reports deferred errors of async calls. */
 int mosaic_sync(mosaic_ctx* ctx);
 /* Counters of the calling thread's last join/index call: [0] rows that needed the exact H3 path,
@@ -284,9 +290,12 @@ int mosaic_pip_join_pairs(mosaic_ctx* ctx, const mosaic_chips* chips, const doub
  * lon/lat for H3, BNG metres for BNG).  Chip rows carry the geometry index as their key.
  * densify >= 1 subdivides H3 cell edges (1 = the 6-vertex h3ToGeoBoundary polygon; border chips keep
  * straight sides between hexagon corners either way).  H3 geometries spanning icosahedron faces are
- * cut into per-face pieces merged per cell (a border chip may then be a MultiPolygon whose parts meet
- * along the face edge); MOSAIC_E_ARG for a geometry with a vertex more than ~78 degrees from the
- * centre of a face it meets.
+ * cut into per-face pieces merged per cell: a core chip's geometry is then the cell boundary
+ * (h3ToGeoBoundary, one Polygon), a border chip over the face edge a MultiPolygon whose parts meet
+ * along that edge (JTS contains -- the join's predicate -- reads it as one region, PointLocator's
+ * Mod-2 rule; JTS overlay operations may reject it: such chips are for the join, not for overlay
+ * fallbacks); MOSAIC_E_ARG for a geometry with a vertex more than ~78 degrees from the centre of a
+ * face it meets.
  * Reference: expressions/index/MosaicExplode.scala:70-79, core/Mosaic.scala:21-87,
  * core/index/IndexSystem.scala:152-186. */
 typedef struct mosaic_chip_set mosaic_chip_set;
@@ -345,9 +354,9 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
  * the quantity the reference's tests check (ST_IntersectionBehaviors.scala:22-135, 1e-8).  out_status
  * 1 marks groups the engine does not answer (a cell holding several chip pairs of the group without a
  * (core, core) pair, a core chip without geometry): evaluate those on the row path.  Sorted by key
- * pair; MOSAIC_E_CAPACITY with *n_out set when more than cap groups exist.  A group's area is summed
- * over its cells with float64 atomics in completion order, so repeated calls can differ in the last
- * bits (always within the reference's 1e-8); the set of groups and their status are deterministic. */
+ * pair; MOSAIC_E_CAPACITY with *n_out set when more than cap groups exist.  Each (group, cell) piece
+ * is written as one record and a group's area is summed on the host in cell-slot order, so repeated
+ * calls return the same bits; the set of groups and their status are deterministic too. */
 int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
                                   int32_t* out_left_key, int32_t* out_right_key, double* out_area, uint8_t* out_status,
                                   int64_t cap, int64_t* n_out);

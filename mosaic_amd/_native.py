@@ -41,7 +41,7 @@ EXPORTS = [
     "mosaic_chip_table_create_arrow", "mosaic_chip_table_build_info", "mosaic_h3_cell_geometry",
     "mosaic_polyfill", "mosaic_cell_lists_info", "mosaic_cell_lists_export", "mosaic_cell_lists_destroy",
     "mosaic_polyfill_last_ms", "mosaic_ctx_exec", "mosaic_buffer_radius", "mosaic_chip_table_create_arrays",
-    "mosaic_intersection_aggregate", "mosaic_thread_release", "mosaic_thread_count",
+    "mosaic_intersection_aggregate", "mosaic_thread_release", "mosaic_thread_count", "mosaic_stream_wait_event",
 ]
 
 GEOM_WKB = 0
@@ -99,6 +99,7 @@ def lib():
         "mosaic_set_option": ([vp, cp, i64], i32),
         "mosaic_get_stream": ([vp, ctypes.POINTER(vp)], i32),
         "mosaic_set_stream": ([vp, vp], i32),
+        "mosaic_stream_wait_event": ([vp, vp], i32),
         "mosaic_sync": ([vp], i32),
         "mosaic_last_stats": ([vp, vp], i32),
         "mosaic_resolution": ([i32, i32, ctypes.POINTER(i32)], i32),

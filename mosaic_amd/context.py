@@ -356,19 +356,28 @@ class MosaicContext:
 
     def set_stream(self, stream_handle):
         N.check(N.lib().mosaic_set_stream(self.handle, stream_handle))
-        self._bound.stream = stream_handle
+        # a null handle binds no caller stream of ours to order against (HIP's null stream)
+        self._bound.stream = stream_handle or None
+
+    def wait_event(self, event_handle):
+        """Order this thread's later calls after a recorded hipEvent_t (mosaic_stream_wait_event)."""
+        N.check(N.lib().mosaic_stream_wait_event(self.handle, event_handle))
 
     def _order(self, *arrays):
         """Device columns written on torch's current stream are complete before the engine's own
-        (non-blocking) stream reads them: without a stream bound with set_stream, wait for torch's
-        current stream (a bound stream orders the work itself)."""
+        (non-blocking) stream reads them: without a stream bound with set_stream, an event recorded
+        on torch's current stream is waited for on the engine's stream (no host block); a bound
+        stream orders the work itself."""
         if getattr(self._bound, "stream", None) is not None:
             return
         for a in arrays:
             if _is_torch(a) and a.is_cuda:
                 import torch
 
-                torch.cuda.current_stream(a.device).synchronize()
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(a.device))
+                self.wait_event(ev.cuda_event)
+                self._bound.last_event = ev  # kept alive until the next ordered call
                 return
 
     def sync(self):
@@ -389,6 +398,8 @@ class MosaicContext:
         """Free the calling thread's execution state on this context (its stream, scratch, events);
         a later call from the thread creates a fresh one (mosaic_thread_release)."""
         N.check(N.lib().mosaic_thread_release(self.handle))
+        # the released state's stream binding is gone: later calls run on a fresh context stream
+        self._bound.stream = None
 
     def thread_states(self):
         """(live per-thread states, scratch bytes they hold) (mosaic_thread_count)."""

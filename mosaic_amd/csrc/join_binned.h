@@ -1,0 +1,61 @@
+// Host interface of the binned chip join (join_binned.hip): scratch owned by a thread state of
+// mosaic_hip.hip and the one launcher run_join calls.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "join_common.h"
+
+namespace binned {
+
+// sorted point values: coordinates, plus the source row for the pairs output
+struct Pt {
+    double x, y;
+};
+struct PtRow {
+    double x, y;
+    long long row;
+};
+__host__ __device__ inline void set_row(Pt&, int64_t) {}
+__host__ __device__ inline void set_row(PtRow& p, int64_t r) { p.row = (long long)r; }
+__host__ __device__ inline int64_t row_of(const Pt&, int64_t i) { return i; }
+__host__ __device__ inline int64_t row_of(const PtRow& p, int64_t) { return (int64_t)p.row; }
+inline const long long* row_map(const Pt*) { return nullptr; }
+inline const long long* row_map(const PtRow* p) { return &p->row; }
+
+struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct Scratch {
+    Buf keys[2], vals[2], temp, n_skip;
+    JoinArgs exact_args;  // the join's arguments as the exact-H3 pass must read them (sorted points)
+    size_t held() const {
+        return keys[0].bytes + keys[1].bytes + vals[0].bytes + vals[1].bytes + temp.bytes + n_skip.bytes;
+    }
+    void release() {
+        for (Buf* b : {&keys[0], &keys[1], &vals[0], &vals[1], &temp, &n_skip}) b->release();
+    }
+};
+
+// Rows [lo, n) of a.x / a.y: key, sort, join (enqueued on stream).  max_code: the largest tile code
+// (tile records + 1).  s.exact_args receives the JoinArgs the exact-H3 pass runs with.
+hipError_t join(const JoinArgs& a, int64_t lo, int64_t n, uint32_t max_code, bool lds_counts, int n_cu, Scratch& s,
+                hipStream_t stream);
+
+}  // namespace binned

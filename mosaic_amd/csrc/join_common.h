@@ -67,13 +67,72 @@ struct JoinArgs {
     long long pair_cap;
     unsigned long long* tests;  // (point, border chip) contains evaluations
     unsigned int* flags;        // bit 0: NaN seen (BNG)
+    // k_join_h3_exact's view of the points: queued row q's coordinates are x[q * cstride],
+    // y[q * cstride] and its source row rowmap[q * cstride] (rowmap == nullptr: q itself) -- the
+    // binned join (join_binned.hip) queues positions in its sorted (x, y[, row]) records
+    int32_t cstride;
+    const long long* rowmap;
 };
 
+// Count modes of the join kernels' hits (template argument CM; a bool true / false reads as 1 / 0):
+// global atomics, the workgroup's LDS count array (n_polygons <= kLdsCountsMax), or a per-wave LDS
+// hash of (key, count) flushed with one global atomic per distinct key (k_join_binned: many
+// polygons, but the few keys of a tile's points).
+static const int kCountGlobal = 0, kCountLds = 1, kCountWaveHash = 2;
+static const int kWaveHashSlots = 256;  // per wave: keys[256] (key + 1, 0 = empty), counts[256], fill
+static const int kWaveHashWords = 2 * kWaveHashSlots + 1;
+
+__device__ inline void wave_hash_add(const JoinArgs& a, uint32_t* t, uint32_t key) {
+    uint32_t h = (key * 0x9E3779B1u) >> 24;
+    for (int p = 0; p < 16; p++) {
+        const uint32_t s = (h + (uint32_t)p) & (kWaveHashSlots - 1);
+        uint32_t k = t[s];
+        if (k == 0) {
+            k = atomicCAS(&t[s], 0u, key + 1u);
+            if (k == 0) {
+                atomicAdd(&t[2 * kWaveHashSlots], 1u);
+                k = key + 1u;
+            }
+        }
+        if (k == key + 1u) {
+            atomicAdd(&t[kWaveHashSlots + s], 1u);
+            return;
+        }
+    }
+    atomicAdd(&a.counts[key], 1ULL);  // probe limit: straight to the global count
+}
+
+// Wave-uniform: adds the wave's hash to the global counts and empties it (always, or only when
+// it is over half full).
+__device__ inline void wave_hash_flush(const JoinArgs& a, uint32_t* t, bool always) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!always && t[2 * kWaveHashSlots] < (uint32_t)(kWaveHashSlots / 2)) return;
+    const int lane = (int)(threadIdx.x & 63);
+    for (int s = lane; s < kWaveHashSlots; s += 64) {
+        const uint32_t k = t[s];
+        if (k) {
+            atomicAdd(&a.counts[k - 1u], (unsigned long long)t[kWaveHashSlots + s]);
+            t[s] = 0;
+            t[kWaveHashSlots + s] = 0;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) t[2 * kWaveHashSlots] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One (row, key) pair: the count, and the pair itself for the pairs output.
-template <bool LDS_COUNTS, bool PAIRS>
+template <int CM, bool PAIRS>
 __device__ inline void emit_hit(const JoinArgs& a, int64_t row, uint32_t key, unsigned int* lds) {
-    if (LDS_COUNTS)
+    if (CM == kCountLds)
         atomicAdd(&lds[key], 1u);
+    else if (CM == kCountWaveHash)
+        wave_hash_add(a, lds, key);
     else
         atomicAdd(&a.counts[key], 1ULL);
     if (PAIRS) {

@@ -36,6 +36,7 @@
 #include "h3_geom.h"
 #include "h3_grid.h"
 #include "isect_area.h"
+#include "join_binned.h"
 #include "join_common.h"
 #include "pip_coop.h"
 #include "pip_device.h"
@@ -62,199 +63,7 @@ static int fail(int code, const std::string& msg) {
         if (_e != hipSuccess) return fail(MOSAIC_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
 
-template <bool LDS_COUNTS, bool PAIRS>
-__device__ inline void join_point(const JoinArgs& a, int64_t row, double x, double y, int64_t cell, unsigned int* lds,
-                                  unsigned int& tests) {
-    if (cell == kEmptyKey) return;
-    uint64_t slot = mix64((uint64_t)cell) & a.mask;
-    HashEntry e;
-    while (true) {
-        e = a.table[slot];
-        if (e.key == cell) break;
-        if (e.key == kEmptyKey) return;
-        slot = (slot + 1) & a.mask;
-    }
-    for (uint32_t c = e.first; c < e.first + e.count; c++) {
-        uint32_t meta = a.chip_meta[c];
-        bool hit = meta & 1u;
-        if (!hit) {
-            tests++;
-            hit = pip::contains(a.store, c, x, y);
-        }
-        if (hit) {
-            uint32_t key = meta >> 1;
-            if (LDS_COUNTS)
-                atomicAdd(&lds[key], 1u);
-            else
-                atomicAdd(&a.counts[key], 1ULL);
-            if (PAIRS) {
-                unsigned long long idx = atomicAdd(a.pair_count, 1ULL);
-                if ((long long)idx < a.pair_cap) {
-                    a.pair_row[idx] = row;
-                    a.pair_key[idx] = (int)key;
-                }
-            }
-        }
-    }
-}
-
-template <bool LDS_COUNTS>
-__device__ inline void counts_init(const JoinArgs& a, unsigned int* lds) {
-    if (LDS_COUNTS) {
-        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x) lds[k] = 0;
-        __syncthreads();
-    }
-}
-
-template <bool LDS_COUNTS>
-__device__ inline void counts_flush(const JoinArgs& a, unsigned int* lds, unsigned int tests) {
-    // one wave-level add for the test counter
-    for (int off = 32; off > 0; off >>= 1) tests += __shfl_down(tests, off, 64);
-    if ((threadIdx.x & 63) == 0 && tests) atomicAdd(a.tests, (unsigned long long)tests);
-    if (LDS_COUNTS) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
-            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
-    }
-}
-
-__device__ inline void probe(const JoinArgs& a, int64_t cell, uint32_t& first, uint32_t& end) {
-    first = end = 0;
-    if (cell == kEmptyKey) return;
-    uint64_t slot = mix64((uint64_t)cell) & a.mask;
-    while (true) {
-        HashEntry e = a.table[slot];
-        if (e.key == cell) {
-            first = e.first;
-            end = e.first + e.count;
-            return;
-        }
-        if (e.key == kEmptyKey) return;
-        slot = (slot + 1) & a.mask;
-    }
-}
-
-// Work items of the wave-cooperative chip evaluation (raster_chips): a general chip (multi-ring /
-// multi-part) or a raster cell's segment list.
-static const uint32_t kGeneralItem = 0xffffffffu;
-
-struct SlabItem {
-    double x, y;
-    uint32_t e0, m;
-};
-
-// ---- raster chip loop: per border chip one ray-parity raster lookup
-// (raster.h); pure cells are decided by the lookup, short cell lists by the owning lane, and only
-// long lists and general (multi-ring / multi-part) chips go to the wave-cooperative evaluation.
-
-// Walks this lane's chips from `cur`: core chips are accepted, border chips decided by the raster
-// where the lane can; stops at the first chip that needs the wave (cur < end on return, with its
-// item (e0, m, par); m == kGeneralItem for general chips).
-template <bool LDS_COUNTS, bool PAIRS>
-__device__ inline void advance_raster(const JoinArgs& a, int64_t row, uint32_t& cur, uint32_t end, double x, double y,
-                                      unsigned int& tests, uint32_t& e0, uint32_t& m, uint32_t& par,
-                                      unsigned int* lds) {
-    for (; cur < end; cur++) {
-        const uint32_t meta = a.chip_meta[cur];
-        if (meta & 1u) {
-            emit_hit<LDS_COUNTS, PAIRS>(a, row, meta >> 1, lds);
-            continue;
-        }
-        tests++;
-        const raster::ChipHdr h = a.hdr[cur];
-        if (pip::box_excludes(h.box, x, y)) continue;
-        if (h.cell_base == raster::kNoRaster) {
-            e0 = 0;
-            m = kGeneralItem;
-            par = 0;
-            return;
-        }
-        const raster::CellRec rec = a.cells[raster::cell_index(h, x, y)];
-        if (rec.m > a.lane_edges) {
-            e0 = rec.word >> 1;
-            m = rec.m;
-            par = rec.word & 1u;
-            return;
-        }
-        if (raster::cell_contains(rec, a.rast_edges, x, y)) emit_hit<LDS_COUNTS, PAIRS>(a, row, meta >> 1, lds);
-    }
-}
-
-// The chips [cur, end) of every lane's point, raster strategy: lane-local where the raster decides,
-// wave-cooperative for long segment lists and general chips.  Wave-uniform call.
-template <bool LDS_COUNTS, bool PAIRS>
-__device__ inline void raster_chips(const JoinArgs& a, int64_t i, uint32_t cur, uint32_t end, double x, double y,
-                                    unsigned int& tests, unsigned int* lds, SlabItem* items) {
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    uint32_t e0 = 0, m = 0, par = 0;
-    advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
-    unsigned long long pending = __ballot(cur < end);
-    while (pending) {
-        int s0 = __ffsll(pending) - 1;
-        uint32_t m0 = pip::readlane_u32(m, s0);
-        if (m0 > 32) {
-            // one item for the whole wave: general chips, or cell lists over 32 records
-            double qx = pip::readlane_f64(x, s0), qy = pip::readlane_f64(y, s0);
-            bool hit;
-            if (m0 == kGeneralItem) {
-                hit = pip::coop_contains(a.store, pip::readlane_u32(cur, s0), qx, qy);
-            } else {
-                uint32_t q0 = pip::readlane_u32(e0, s0);
-                unsigned long long onm = 0;
-                int cross = (int)pip::readlane_u32(par, s0);
-                for (uint32_t b = 0; b < m0; b += 64) {
-                    bool on = false, cr = false;
-                    if (b + lane < m0) pip::edge_rec_flags(a.rast_edges[q0 + b + lane], qx, qy, on, cr);
-                    onm |= __ballot(on);
-                    cross += __popcll(__ballot(cr));
-                }
-                hit = onm == 0 && (cross & 1);
-            }
-            if (lane == s0) {
-                if (hit) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                cur++;
-                advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
-            }
-        } else {
-            const int G = m0 <= 4 ? 4 : (m0 <= 8 ? 8 : (m0 <= 16 ? 16 : 32));
-            const int cap = 64 / G;
-            bool cand = cur < end && m <= (uint32_t)G;
-            unsigned long long cmask = __ballot(cand);
-            int rank = __popcll(cmask & lt_mask);
-            bool chosen = cand && rank < cap;
-            if (chosen) {
-                SlabItem it;
-                it.x = x;
-                it.y = y;
-                it.e0 = e0;
-                it.m = m;
-                items[rank] = it;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            int ng = __popcll(cmask);
-            ng = ng < cap ? ng : cap;
-            int k = lane / G, j = lane - k * G;
-            bool on = false, cr = false;
-            if (k < ng) {
-                SlabItem it = items[k];
-                if ((uint32_t)j < it.m) pip::edge_rec_flags(a.rast_edges[it.e0 + j], it.x, it.y, on, cr);
-            }
-            unsigned long long onm = __ballot(on), crm = __ballot(cr);
-            if (chosen) {
-                const unsigned long long gm = (G == 32) ? 0xffffffffULL : ((1ULL << G) - 1ULL);
-                unsigned long long om = (onm >> (rank * G)) & gm, xm = (crm >> (rank * G)) & gm;
-                if (om == 0 && ((__popcll(xm) + par) & 1)) emit_hit<LDS_COUNTS, PAIRS>(a, i, a.chip_meta[cur] >> 1, lds);
-                cur++;
-                advance_raster<LDS_COUNTS, PAIRS>(a, i, cur, end, x, y, tests, e0, m, par, lds);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        pending = __ballot(cur < end);
-    }
-}
+#include "join_chips.h"
 
 template <int GRID, bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
@@ -293,62 +102,6 @@ __global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
     }
     if (nan_seen) atomicOr(a.flags, 1u);
     counts_flush<LDS_COUNTS>(a, lds, tests);
-}
-
-// ---- tiled variant (default for H3 chip tables with a tile directory, tiles.h).  With the point
-// raster (RASTER), one or two L2-resident lookups give the whole answer of most points (no pair, or
-// one pair with a known polygon key).  Otherwise, or for raster cells marked mixed, the point's
-// tile decides whether it can join at all; points that can are compacted per wave in LDS (so the
-// lanes of a wave all carry work), then get their hexagon from the tile's face and window (no
-// index arithmetic, no hash probe) and go through the raster chip loop.
-static const int kQueue = 128;  // per-wave LDS queue (entries)
-
-struct TileQueue {
-    double x[kQueue], y[kQueue];
-    long long row[kQueue];
-    uint32_t code[kQueue];
-};
-
-// Chips of one queued point: tile path (certified hexagon -> window slot) or the generic
-// fast path + probe (kFull tiles, window misses).  Uncertified points go to the exact queue.
-__device__ inline void tiled_cell(const JoinArgs& a, int64_t i, double x, double y, uint32_t code, uint32_t& cur,
-                                  uint32_t& end) {
-    cur = end = 0;
-    int64_t cell;
-    if (code >= 2) {
-        const tiles::TileRec r = a.tile_rec[code - 2];
-        const int face = (int)(r.dims & 0xffu);
-        const int wa = (int)((r.dims >> 8) & 0xfffu), wb = (int)(r.dims >> 20);
-        double px, py, pz, vx, vy, best;
-        h3::fast_unit(y, x, &px, &py, &pz);
-        h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
-        int ba, bb;
-        if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
-            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-            return;
-        }
-        const int ra = ba - r.a0, rb = bb - r.b0;
-        if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
-            const uint32_t e = a.tile_ent[r.off + (uint32_t)(ra * wb + rb)];
-            if (e) {
-                const HashEntry he = a.table[e - 1];
-                cur = he.first;
-                end = he.first + he.count;
-            }
-            return;
-        }
-        cell = (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res);
-    } else {
-        bool amb;
-        cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
-        if (amb) {
-            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-            return;
-        }
-    }
-    probe(a, cell, cur, end);
 }
 
 template <bool LDS_COUNTS, bool PAIRS>
@@ -1675,9 +1428,10 @@ __global__ void __launch_bounds__(256) k_join_h3_exact(JoinArgs a, int all_rows)
     for (unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
         int64_t i = all_rows ? (int64_t)t : (int64_t)a.amb_queue[t];
         if (a.valid && !a.valid[i]) continue;
-        double x = a.x[i], y = a.y[i];
+        const int64_t k = i * a.cstride;
+        double x = a.x[k], y = a.y[k];
         int64_t cell = (int64_t)h3::h3_exact(h3::to_radians(y, a.jdk), h3::to_radians(x, a.jdk), a.res);
-        join_point<false, PAIRS>(a, i, x, y, cell, nullptr, tests);
+        join_point<false, PAIRS>(a, a.rowmap ? (int64_t)a.rowmap[k] : i, x, y, cell, nullptr, tests);
     }
     counts_flush<false>(a, nullptr, tests);
 }
@@ -1926,6 +1680,11 @@ struct Options {
     // a calling thread keeps its scratch (queues, staging) between calls up to this many bytes; above
     // it the scratch is freed when the call returns (0: always kept, the default)
     int64_t scratch_limit = 0;
+    // the binned join (join_binned.hip) for tile-directory tables without a usable point raster
+    // (border-chip-heavy chip sets): points sorted by tile before the chip loop; rows per sort chunk
+    int bin_points = 1;
+    int64_t bin_min_rows = (int64_t)1 << 18;
+    int64_t bin_chunk = (int64_t)1 << 28;
 };
 
 // Execution state of one calling thread on one context: its HIP stream (created on first use, or
@@ -1944,6 +1703,7 @@ struct ThreadCtx : Options {
     DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
     hipStream_t copy_stream = nullptr;
     DevBuf hx[2], hy[2], hcounts;
+    binned::Scratch bins;  // the binned join's keys, sorted points and sort temp
     int64_t stats[3] = {0, 0, 0};
     unsigned int deferred_flags = 0;
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -1956,7 +1716,7 @@ struct ThreadCtx : Options {
     size_t held() {
         size_t n = 0;
         for (DevBuf* b : scratch()) n += b->bytes;
-        return n;
+        return n + bins.held();
     }
     // free the scratch once the thread's queued work is done (scratch_limit)
     void trim() {
@@ -1964,12 +1724,14 @@ struct ThreadCtx : Options {
         if (stream) (void)hipStreamSynchronize(stream);
         if (copy_stream) (void)hipStreamSynchronize(copy_stream);
         for (DevBuf* b : scratch()) b->release();
+        bins.release();
     }
     void release() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (copy_stream) (void)hipStreamSynchronize(copy_stream);
         for (DevBuf* b : scratch()) b->release();
+        bins.release();
         scalars.release();
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         for (size_t i = 0; i < ev_start.size(); i++) {
@@ -1993,7 +1755,9 @@ struct mosaic_ctx {
     std::unordered_map<uint64_t, std::unique_ptr<ThreadCtx>> threads;
 };
 
-static const int kScalars = 5;
+// join scalars: [0] exact-queue rows, [1] pairs, [2] contains tests, [3] flags, [4] mixed-queue rows,
+// [5] exact rows summed over the binned join's chunks, [6] a binned chunk overflowed the exact queue
+static const int kScalars = 7;
 // the join's counts and scalars zeroed by one launch (two hipMemsetAsync calls of odd sizes took four
 // fill kernels, ~20 us per call on the stream)
 __global__ void __launch_bounds__(256) k_zero_join(unsigned long long* counts, int64_t n_counts, unsigned long long* scalars) {
@@ -2001,6 +1765,15 @@ __global__ void __launch_bounds__(256) k_zero_join(unsigned long long* counts, i
         if (k < n_counts) counts[k] = 0ull;
         else scalars[k - n_counts] = 0ull;
     }
+}
+
+// After a binned chunk's exact pass: its queue rows are added to scalars[5], an overflow is noted in
+// scalars[6], and the queue starts over for the next chunk (whose sorted positions reuse the buffers).
+__global__ void k_amb_roll(unsigned long long* sc, unsigned long long cap) {
+    const unsigned long long q = sc[0];
+    sc[5] += q;
+    if (q > cap) sc[6] = 1;
+    sc[0] = 0;
 }
 
 // Lifetime of per-thread states.  A thread's state on a context is freed by mosaic_thread_release,
@@ -2405,6 +2178,14 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "timing") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
         o.timing = (int)v;
+    } else if (k == "bin_points") {
+        o.bin_points = v ? 1 : 0;
+    } else if (k == "bin_min_rows") {
+        if (v < 0) return fail(MOSAIC_E_ARG, "bin_min_rows must be >= 0");
+        o.bin_min_rows = v;
+    } else if (k == "bin_chunk") {
+        if (v < 1024 || v > ((int64_t)1 << 30)) return fail(MOSAIC_E_ARG, "bin_chunk must be in [1024, 2^30]");
+        o.bin_chunk = v;
     } else if (k == "scratch_limit") {
         if (v < 0) return fail(MOSAIC_E_ARG, "scratch_limit must be >= 0");
         o.scratch_limit = v;
@@ -2437,6 +2218,14 @@ int mosaic_set_stream(mosaic_ctx* ctx, void* s) {
     }
     c->stream = (hipStream_t)s;
     c->own_stream = false;
+    return MOSAIC_OK;
+}
+
+int mosaic_stream_wait_event(mosaic_ctx* ctx, void* ev) {
+    ENTER(ctx);
+    if (!ev) return fail(MOSAIC_E_ARG, "null event");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamWaitEvent(c->stream, (hipEvent_t)ev, 0));
     return MOSAIC_OK;
 }
 
@@ -3813,9 +3602,12 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
     a.pair_cap = cap;
     a.tests = sc + 2;
     a.flags = (unsigned int*)(sc + 3);
+    a.cstride = 1;
+    a.rowmap = nullptr;
     bool lds = ch->n_polygons <= kLdsCountsMax;
     size_t shm = lds ? (size_t)ch->n_polygons * 4 : 0;
     int g = grid_size(c, n);
+    bool binned_used = false;
     if (n > 0) {
         hipEvent_t tstop;
         if ((rc = timing_begin(c, &tstop))) return rc;
@@ -3832,6 +3624,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
         sa.tb_lds = shm_s + (size_t)sa.n_tiles * 4 <= kStreamLdsMax ? 1 : 0;
         if (sa.tb_lds) shm_s += (size_t)sa.n_tiles * 4;
         const bool stream = praster && ch->stream_ok && shm_s <= kStreamLdsMax;
+        // border-chip-heavy tables (no point raster to stream): points binned by tile first
+        binned_used = tiled && !stream && c->bin_points && n >= c->bin_min_rows;
         if (bngdense) {
             a.bng_cells = (const uint32_t*)ch->bng_cells.p;
             a.bng_e0 = ch->bng_e0;
@@ -3982,6 +3776,23 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 if (mstop) HIP_TRY(hipEventRecord(mstop, c->stream));
             }
             tstop = nullptr;  // recorded after the first stream launch
+        } else if (binned_used) {
+            c->last_kernel = "k_join_binned";
+            const uint32_t max_code = (uint32_t)ch->tile_stats[2] + 1u;
+            for (int64_t lo = 0; lo < n; lo += c->bin_chunk) {
+                const int64_t hi = std::min<int64_t>(n, lo + c->bin_chunk);
+                hipError_t e = binned::join(a, lo, hi, max_code, lds && !pairs, c->n_cu, c->bins, c->stream);
+                if (e == hipErrorOutOfMemory) return fail(MOSAIC_E_NOMEM, "binned join: device allocation failed");
+                if (e != hipSuccess) return fail(MOSAIC_E_HIP, std::string("binned join: ") + hipGetErrorString(e));
+                // this chunk's exact-H3 rows, before the next chunk reuses the sorted buffers
+                const int ge = std::min(grid_size(c, (int64_t)qcap), std::max(1, c->n_cu * 2));
+                if (pairs)
+                    hipLaunchKernelGGL((k_join_h3_exact<true>), dim3(ge), dim3(c->block), 0, c->stream, c->bins.exact_args, 0);
+                else
+                    hipLaunchKernelGGL((k_join_h3_exact<false>), dim3(ge), dim3(c->block), 0, c->stream, c->bins.exact_args, 0);
+                hipLaunchKernelGGL(k_amb_roll, dim3(1), dim3(1), 0, c->stream, sc, (unsigned long long)qcap);
+                HIP_TRY(hipGetLastError());
+            }
         } else if (tiled) {
             c->last_kernel = "k_join_tiled";
             if (pairs) MOSAIC_LAUNCH((k_join_tiled<false, true>), 0);
@@ -4001,7 +3812,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
 #undef MOSAIC_LAUNCH
         HIP_TRY(hipGetLastError());
         if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
-        if (h3g) {
+        if (h3g && !binned_used) {
             // the margin queue is nearly always a handful of rows: a grid of 2 workgroups per CU keeps
             // the launch short (a 2048-workgroup grid cost ~40 us of dispatch for ~1 row)
             int ge = std::min(grid_size(c, (int64_t)qcap), std::max(1, c->n_cu * 2));
@@ -4016,6 +3827,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
     HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned long long s[kScalars];
     HIP_TRY(hipMemcpy(s, c->scalars.p, sizeof s, hipMemcpyDeviceToHost));
+    if (binned_used) s[0] = s[6] ? qcap + 1 : s[5];  // (the queue was drained chunk by chunk)
     if (ch->grid == MOSAIC_GRID_H3 && s[0] > qcap) {
         // queue overflow (adversarial input): recompute the whole batch on the exact path
         HIP_TRY(hipMemsetAsync(dcounts, 0, cbytes, c->stream));

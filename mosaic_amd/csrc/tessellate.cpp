@@ -35,6 +35,9 @@
 #include "tess_gpu.h"
 #include "bng_device.h"
 #include "h3_device.h"
+#include "h3_geom.h"
+
+#include <unordered_map>
 
 using namespace mosaic;
 
@@ -526,14 +529,14 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
     };
     std::vector<int64_t> order;  // cell ids in first-seen order (faces ascending, lattice order)
     std::vector<std::vector<Piece>> pieces;
-    std::vector<std::pair<int64_t, size_t>> index;  // id -> slot (sorted at the end of each face)
+    std::unordered_map<int64_t, size_t> index;  // id -> slot (O(1) per piece: country-scale inputs)
     auto slot_of = [&](int64_t id) -> size_t {
-        for (auto& e : index)
-            if (e.first == id) return e.second;
-        index.push_back({id, order.size()});
-        order.push_back(id);
-        pieces.emplace_back();
-        return order.size() - 1;
+        auto ins = index.emplace(id, order.size());
+        if (ins.second) {
+            order.push_back(id);
+            pieces.emplace_back();
+        }
+        return ins.first->second;
     };
     const double s60 = 0.86602540378443864676, R = 0.57735026918962576451;
     int faces_used = 0;
@@ -570,11 +573,19 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
                 if (a.size() >= 3) met += fabs(open_area(a));
             }
         } else {
-            // refuse only when the geometry could reach this face: some vertex on it
+            // refuse when the geometry could reach this face: some vertex on it, or some edge
+            // crossing its territory between vertices (edges sampled every <= 0.25 degrees; a face
+            // territory is ~40 degrees across, so an edge that crosses one has samples on it)
             for (auto& part : geo)
                 for (auto& ring : part)
-                    for (auto& p : ring)
-                        if (face_of(p.x, p.y) == f) return MOSAIC_E_ARG;
+                    for (size_t v = 0; v < ring.size(); v++) {
+                        if (face_of(ring[v].x, ring[v].y) == f) return MOSAIC_E_ARG;
+                        if (v == 0) continue;
+                        const P2 a = ring[v - 1], b = ring[v];
+                        const int m = (int)std::min(1e6, ceil(std::max(fabs(b.x - a.x), fabs(b.y - a.y)) / 0.25));
+                        for (int t = 1; t < m; t++)
+                            if (face_of(a.x + (b.x - a.x) * t / m, a.y + (b.y - a.y) * t / m) == f) return MOSAIC_E_ARG;
+                    }
             continue;
         }
         if (!(met > 1e-12)) continue;
@@ -642,8 +653,27 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
         }
         if (!any) continue;
         std::vector<std::vector<std::vector<P2>>> parts;
+        if (all_core) {
+            // a core cell over a face edge: its geometry is the one polygon of the cell boundary
+            // (h3ToGeoBoundary, what the reference's indexToGeometry returns for a core chip,
+            // H3IndexSystem.scala:93-100), not the per-face pieces (parts sharing the face edge
+            // would make an invalid MultiPolygon)
+            if (keep_core_geom) {
+                double b[20];
+                const int nb = h3geom::h3_to_geo_boundary((uint64_t)order[k], b);
+                if (nb < 3) return MOSAIC_E_ARG;
+                std::vector<P2> ring;
+                for (int v = 0; v <= nb; v++) {
+                    const int q = v % nb;
+                    ring.push_back({h3geom::to_degrees(b[2 * q + 1], 8), h3geom::to_degrees(b[2 * q], 8)});
+                }
+                parts.push_back({ring});
+            }
+            cs->add(true, order[k], key, keep_core_geom ? to_wkb(parts) : std::vector<uint8_t>());
+            continue;
+        }
         for (const Piece& p : ps) {
-            if (p.cls == 1 && (keep_core_geom || !all_core)) {
+            if (p.cls == 1) {
                 FacePlane fp;
                 fp.init(p.face, res);
                 parts.push_back({cell_ring(p.cell, [&](P2 h) { return fp.to_geo(h); })});
@@ -651,8 +681,7 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
                 for (auto& q : p.parts) parts.push_back(q);
             }
         }
-        if (all_core) cs->add(true, order[k], key, keep_core_geom ? to_wkb(parts) : std::vector<uint8_t>());
-        else if (!parts.empty()) cs->add(false, order[k], key, to_wkb(parts));
+        if (!parts.empty()) cs->add(false, order[k], key, to_wkb(parts));
     }
     return MOSAIC_OK;
 }

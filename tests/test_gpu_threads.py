@@ -134,3 +134,57 @@ def test_short_lived_threads_release_their_state(h3ctx):
     h3ctx.pip_join_count(table, x, y)
     assert h3ctx.thread_states()[1] > 0
     table.close()
+
+
+def test_stream_order_after_release_and_wait_event(h3ctx):
+    """after set_stream + thread_release the next call runs on a fresh context stream, so
+    columns torch writes on its own stream must still be ordered before the engine reads them (the
+    mirror records an event on torch's stream and the engine's stream waits for it,
+    mosaic_stream_wait_event).  The columns are produced by a long chain of torch kernels right
+    before each call, so reading them early would see zeros."""
+    import torch
+
+    zones = PolygonSet.load("nyc_taxi_zones_35")
+    chips = tessellate("H3", zones, 9)
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
+                             n_polygons=len(zones))
+    offs, data = chips["wkb"]
+    oc = dict(index_id=chips["index_id"], is_core=chips["is_core"], polygon_key=chips["polygon_key"],
+              wkb_offsets=offs, wkb=data)
+    x, y = quickstart_points(zones, 2_000_000, seed=11)
+    want, _ = oracle.pip_join(oc, oracle.GRID_H3, 9, x, y, len(zones), threads=8)
+    side = torch.cuda.Stream()
+
+    def produce():
+        with torch.cuda.stream(side):
+            xt = torch.zeros(len(x), dtype=torch.float64, device="cuda")
+            yt = torch.zeros(len(y), dtype=torch.float64, device="cuda")
+            big = torch.ones(1 << 26, dtype=torch.float64, device="cuda")
+            for _ in range(20):  # delay the columns' final write
+                big.mul_(1.0000001)
+            xt.copy_(torch.from_numpy(x).pin_memory(), non_blocking=True)
+            yt.copy_(torch.from_numpy(y).pin_memory(), non_blocking=True)
+        return xt, yt, big
+
+    h3ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    h3ctx.thread_release()
+    assert getattr(h3ctx._bound, "stream", "unset") is None
+    with torch.cuda.stream(side):
+        xt, yt, big = produce()
+        got = h3ctx.pip_join_count(table, xt, yt)  # ordered after `side` by the mirror's event
+        got = got.cpu().numpy() if hasattr(got, "cpu") else got
+    assert np.array_equal(got, want)
+    # the raw ABI: an event recorded on the producer stream, waited for by the engine's stream
+    xt, yt, big = produce()
+    ev = torch.cuda.Event()
+    ev.record(side)
+    h3ctx.wait_event(ev.cuda_event)
+    h3ctx._bound.stream = "bound"  # bypass the mirror's own ordering: only the event orders the call
+    try:
+        got = h3ctx.pip_join_count(table, xt, yt)
+    finally:
+        h3ctx._bound.stream = None
+    got = got.cpu().numpy() if hasattr(got, "cpu") else got
+    assert np.array_equal(got, want)
+    del big
+    table.close()

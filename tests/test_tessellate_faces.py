@@ -188,3 +188,27 @@ def test_gpu_producer_face_spanning_identical():
             assert np.array_equal(host["wkb"][0], gpu["wkb"][0]) and np.array_equal(host["wkb"][1], gpu["wkb"][1])
     finally:
         ctx.close()
+
+
+def test_face_spanning_core_chip_is_cell_boundary():
+    """a core chip of a face-spanning geometry is one Polygon -- the cell boundary
+    h3ToGeoBoundary in degrees, closed (what indexToGeometry gives the reference's core chips,
+    H3IndexSystem.scala:93-100) -- never the per-face pieces as a MultiPolygon sharing the face edge."""
+    from mosaic_amd.wkb import read_wkb
+
+    ps = face_cases()
+    chips = tessellate("H3", ps, 7)
+    offs, data = chips["wkb"]
+    n = 0
+    for k in range(len(chips["index_id"])):
+        if not chips["is_core"][k] or chips["polygon_key"][k] == 2:  # (geometry 2: single-face control)
+            continue
+        kind, parts = read_wkb(data[offs[k]:offs[k + 1]])
+        assert kind == "polygon" and len(parts) == 1 and len(parts[0]) == 1
+        ring = parts[0][0]
+        b = oracle.h3_to_geo_boundary(int(chips["index_id"][k]))
+        want = [(lng * 180.0 / math.pi, lat * 180.0 / math.pi) for lat, lng in b]
+        want.append(want[0])
+        assert ring == want
+        n += 1
+    assert n > 20
