@@ -48,7 +48,8 @@ def parse():
     p.add_argument("--res", type=int, default=9)
     p.add_argument("--cpu-sample", type=float, default=2e8,
                    help="prefix of the device points joined by the CPU oracle (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the CPU baseline (0 = every CPU this process may run on)")
     p.add_argument("--pmc", type=int, default=1, help="1: measure HBM traffic with a rocprofv3 PMC child pass")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
@@ -86,7 +87,34 @@ def host_info():
                 break
         except OSError:
             pass
-    return {"cpu_model": cpu, "nproc": os.cpu_count(), "rocm": rocm}
+    return {"cpu_model": cpu, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cgroup_cpus": cgroup_cpus(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "usable_cpus": usable_cpus(), "rocm": rocm}
+
+
+def cgroup_cpus():
+    """The CPU quota of this process's cgroup (cpu.max quota / period), or None when unlimited."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = [l.strip().split(":", 2)[2] for l in f if l.startswith("0::")][0]
+        with open(os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max")) as f:
+            quota, period = f.read().split()
+        return None if quota == "max" else float(quota) / float(period)
+    except (OSError, IndexError, ValueError):
+        return None
+
+
+def usable_cpus():
+    """CPUs this process may use: its affinity mask, capped by its cgroup's CPU quota and by the
+    lease's declared share (OMP_NUM_THREADS, which the GPU box sets to its CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpus()
+    if q:
+        n = min(n, int(q))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
 
 
 def build_chips(ctx, res, rank, world):
@@ -245,12 +273,13 @@ def main():
         m = int(min(args.cpu_sample, n))
         gpu_prefix = ctx.pip_join_count(table, x[:m], y[:m]).cpu().numpy()
         hx, hy = x[:m].cpu().numpy(), y[:m].cpu().numpy()
-        want, total, dt = cpu_baseline(chips, args.res, len(zones), hx, hy, args.cpu_threads)
+        threads = args.cpu_threads or usable_cpus()
+        want, total, dt = cpu_baseline(chips, args.res, len(zones), hx, hy, threads)
         match = bool(np.array_equal(gpu_prefix, want))
         parity = {"points": m, "pairs": int(total), "match": match,
                   "against": "oracle/join.c (CPU restatement of the reference's join) on the first "
                              f"{m} of this rank's device points"}
-        cpu = {"value": m / dt, "unit": "points/s", "cores": args.cpu_threads, "kind": "port",
+        cpu = {"value": m / dt, "unit": "points/s", "cores": threads, "kind": "port",
                "sample": f"the first {m:.0f} of the benchmarked device points (uniform over the NYC zone bbox), "
                          f"H3 res {args.res}, same chips ({total} pairs), {dt:.1f} s, CPU restatement "
                          "(oracle/join.c), not Spark"}

@@ -106,11 +106,16 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
  * host-resident coordinates: the next chunk's copy overlaps the current chunk's join; 0 = stage the
  * whole batch; default 2^25), "mixed_rows" (1/2/4, default 2), "mixed_blocks_per_cu", "stream_pipe"
- * (0/1: the software-pipelined H3 stream kernel where it applies; default 1), "bng_pipe" (0/1: the
- * software-pipelined BNG stream kernel; default 0, slower at C5), "bng_lds" (0/1: BNG tables
+ * (0: k_join_stream; 1: the software-pipelined H3 stream kernel; 2: it with the gathering rows
+ * compacted, k_join_stream_cpt, the default -- each where it applies), "bng_cpt" (0/1: the compacted
+ * BNG stream kernel where it applies; default 1), "bng_lds" (0/1: BNG tables
  * built afterwards carry an LDS cell level for the BNG stream kernel; default 1), "bng_cell" (sub-cells
  * per BNG border cell side in those tables, a power of two <= 64; default 32), "scratch_limit" (see
- * the per-thread state below). */
+ * the per-thread state below), "bin_points" (0/1: H3 joins on a tile directory without a usable point
+ * raster sort the points by tile before the chip loop -- the border-chip-heavy C4 shape; default 1),
+ * "bin_min_rows" (smallest batch that is binned; default 2^18), "bin_chunk" (rows per sort chunk;
+ * default 2^28), "tile_images" (0: none; 1: tables built without a point raster carry per-tile chip
+ * images the binned join copies into LDS, the default; 2: every tile-directory table carries them). */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* Per-thread state.  Each calling thread gets its own execution state on a context (HIP stream,
  * copy stream, timing events, scratch queues and staging sized by its largest call).  It is freed
@@ -266,8 +271,10 @@ int mosaic_chip_table_tiles(const mosaic_chips* chips, int64_t* out13);
 int mosaic_chip_table_tile_grid(const mosaic_chips* chips, double* out4);
 /* Point raster detail: out5 = sub-blocks stored as line records (option "raster_lines"), LDS quad
  * level entries (0: none), quad shift (sub-blocks per quad side = 1 << shift), raster bytes on the
- * device, 1 if joins run the stream kernel on it (quad level with compact copies, edges clamp-safe). */
-int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out5);
+ * device, 1 if joins run the stream kernel on it (quad level with compact copies, edges clamp-safe);
+ * then the binned join's per-tile LDS chip images (option "tile_images"): records with an image,
+ * image bytes on the device, bytes of the largest image. */
+int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out8);
 /* Build cost of the table in ms (ms4): chip hash + geometry + chip rasters, tile directory (host),
  * point-raster classification (GPU with option "raster_build" = 1, the default; host threads with
  * 0), point-raster assembly (host); *digest = FNV-1a 64 of the point raster's arrays (0: no raster),
@@ -368,9 +375,11 @@ int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, con
  * order (bottom, right, top, left; cells failing isValid dropped).  Reference: BNGIndexSystem.kRing /
  * kLoop / isValid (core/index/BNGIndexSystem.scala:216-263).
  * H3: stride = max(6k, 1) (loop) or 1 + 3k(k + 1) (ring), in H3 v3.7's hexRange / hexRing order
- * (reference H3IndexSystem.kRing / kLoop, core/index/H3IndexSystem.scala:154-177); a row whose
- * ring walk reaches a pentagon (where H3 falls back to its hash-ordered _kRingInternal) or whose id
- * is not a valid cell gets out_count[i] = -2 (unsupported, no cells written). */
+ * (reference H3IndexSystem.kRing / kLoop, core/index/H3IndexSystem.scala:154-177); where the walk
+ * meets a pentagon, kRing is H3's _kRingInternal hash table read in slot order (as h3-java returns
+ * it) and kLoop the reference's own fallback, kRing(k).toSet diff kRing(k - 1).toSet in Scala
+ * HashSet order (:169-176); such rows need k <= 60 (MOSAIC_E_ARG otherwise).  A row whose id is
+ * not a valid cell gets out_count[i] = -2 (no cells written). */
 int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k,
                       int loop, int64_t* out, int32_t* out_count);
 

@@ -297,10 +297,10 @@ class ChipTable:
         g = np.zeros(4, np.float64)
         N.check(N.lib().mosaic_chip_table_tile_grid(self.handle, N.ptr(g)))
         d.update(x0=float(g[0]), y0=float(g[1]), sx=float(g[2]), sy=float(g[3]))
-        r = np.zeros(5, np.int64)
+        r = np.zeros(8, np.int64)
         N.check(N.lib().mosaic_chip_table_raster(self.handle, N.ptr(r)))
         d.update(line_sub_blocks=int(r[0]), quad_entries=int(r[1]), quad_shift=int(r[2]), raster_bytes=int(r[3]),
-                 stream=int(r[4]))
+                 stream=int(r[4]), image_records=int(r[5]), image_bytes=int(r[6]), image_max_bytes=int(r[7]))
         return d
 
     def build_info(self):
@@ -697,8 +697,8 @@ class MosaicContext:
         bad = np.nonzero(cnt[:n] == -2)[0]
         if len(bad):
             raise N.MosaicError(
-                N.MOSAIC_E_ARG, f"grid_cellkring / grid_cellkloop: the H3 ring of row {int(bad[0])} (cell {int(ids[bad[0]])}) reaches a "
-                "pentagon, where H3 falls back to its hash-ordered kRing; not supported by this engine")
+                N.MOSAIC_E_ARG, f"grid_cellkring / grid_cellkloop: row {int(bad[0])} (cell {int(ids[bad[0]])}) is not a valid "
+                "H3 cell id")
         rows = [out[i * stride:i * stride + cnt[i]] for i in range(n)]
         if raw or self.index_system.cell_id_type != "string":
             return rows
@@ -707,13 +707,15 @@ class MosaicContext:
     def grid_cellkring(self, cells, k, raw=False):
         """grid_cellkring(cellId, k) (MosaicContext.scala:692-693 -> CellKRing.nullSafeEval ->
         IndexSystem.kRing; BNG: BNGIndexSystem.scala:216-222, the cell and its loops 1..k; H3:
-        H3IndexSystem.scala:154-160, h3.kRing in hexRange order -- rings reaching a pentagon raise)."""
+        H3IndexSystem.scala:154-160, h3.kRing: hexRange order, or H3's hash-table order where the ring
+        meets a pentagon)."""
         return self._kring(cells, k, False, raw)
 
     def grid_cellkloop(self, cells, k, raw=False):
         """grid_cellkloop(cellId, k) (MosaicContext.scala:696-697 -> CellKLoop -> IndexSystem.kLoop;
         BNG: BNGIndexSystem.scala:234-246, the valid cells at distance k; H3: H3IndexSystem.scala:
-        171-177, h3.hexRing order)."""
+        171-177, h3.hexRing order, or the reference's kRing set-difference fallback (Scala HashSet
+        order) where the ring meets a pentagon)."""
         return self._kring(cells, k, True, raw)
 
     def grid_cellkringexplode(self, cells, k):

@@ -19,6 +19,7 @@
 
 #include "h3_geom.h"
 #include "h3_grid.h"
+#include "h3_neighbors.h"
 
 namespace mosaic {
 namespace h3fill {
@@ -155,40 +156,17 @@ MOSAIC_HD void unit3(double lat, double lon, double* v) {
     v[2] = sl;
 }
 
-// kRing(h, 1) as polyfill's search uses it: H3's hexRange order (h3_grid.h) where the walk
-// succeeds (7 cells).  Where H3 falls back to _kRingInternal (a pentagon within the ring, or a
-// vertex region), the same set is found geometrically instead: h, then for each boundary edge the
-// cell just beyond the edge's midpoint on the sphere (m + (m - c) / 8); those rows may differ from
-// H3 only in the order of cells that collide in its output table.  Cells of pentagon base cells
-// below res 0 are not answered: returns -1.
+// kRing(h, 1) as polyfill's search uses it (H3 v3.7 _polyfillInternal: kRing(searchHex, 1, ring)
+// and the ring's non-zero entries in array order): H3's hexRange order where the walk succeeds,
+// else its _kRingInternal table of maxKringSize(1) = 7 slots read in slot order (h3_neighbors.h).
+// Returns the cell count (5 or 7 with a pentagon in reach; -1 for an invalid index).
 MOSAIC_HD int kring1(uint64_t h, int res, int64_t* out) {
-    const int n = h3grid::kring(h, 1, 0, out);
-    if (n == 7) return 7;
-    const int bc = (int)((h >> 45) & 127);
-    if (res > 0 && h3::kH3BaseCellData[bc][4]) return -1;
-    double clat, clon, v[20], c[3], a[3], b[3];
-    if (!h3geom::h3_to_geo(h, &clat, &clon)) return -1;
-    const int nv = h3geom::h3_to_geo_boundary(h, v);
-    int m = 0;
-    out[m++] = (int64_t)h;
-    unit3(clat, clon, c);
-    for (int k = 0; k < nv; k++) {
-        const int k2 = (k + 1) % nv;
-        unit3(v[2 * k], v[2 * k + 1], a);
-        unit3(v[2 * k2], v[2 * k2 + 1], b);
-        double mm[3], q[3];
-        for (int d = 0; d < 3; d++) mm[d] = a[d] + b[d];
-        const double mn = sqrt(mm[0] * mm[0] + mm[1] * mm[1] + mm[2] * mm[2]);
-        for (int d = 0; d < 3; d++) q[d] = mm[d] / mn + (mm[d] / mn - c[d]) / 8;
-        const double lat = glibc::atan2(q[2], sqrt(q[0] * q[0] + q[1] * q[1])), lon = glibc::atan2(q[1], q[0]);
-        const int64_t nb = (int64_t)h3::h3_exact(lat, lon, res);
-        bool seen = nb == 0;
-        for (int t = 0; t < m && !seen; t++) seen = out[t] == nb;
-        if (seen) continue;
-        if (m == 7) return -1;
-        out[m++] = nb;
-    }
-    return m;
+    (void)res;
+    const int n = h3nb::kring_fast(h, 1, 0, out);
+    if (n != -3) return n < 0 ? -1 : n;
+    int64_t tab[8];
+    int32_t dist[7];
+    return h3nb::kring_slow(h, 1, 0, out, tab, dist);
 }
 
 }  // namespace h3fill

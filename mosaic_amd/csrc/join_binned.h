@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "join_common.h"
 
 namespace binned {
@@ -53,9 +55,42 @@ struct Scratch {
     }
 };
 
+// ---- per-tile chip images (the LDS tiles of k_join_tiles)
+// One image per tile record, copied whole into a workgroup's LDS for the sorted points of that
+// tile: its window's chip ranges, per chip (meta, geometry reference, f32 envelope rounded
+// outwards), and the rings of its one-ring border chips.  Layout (32-bit words):
+//   [0] n_slots | n_chips << 16   [1] n_verts   [2] chip word offset   [3] vertex word offset
+//   [4 ..] slot_first: n_slots + 1 uint16 (chip index range of window slot s: [first[s], first[s+1]))
+//   chips (at a multiple of 4 words): 8 words each -- meta (polygon_key << 1 | is_core), vinfo
+//     (vertex offset | count << 16; count 0: no geometry (core chip), kImgGlobal: tested from the
+//     global geometry store), global chip index, 0, f32 minx, miny, maxx, maxy (outward rounded)
+//   vertices (at a multiple of 4 words): double2, ring after ring (closed)
+static const uint32_t kImgCapWords = 6144;     // 24 KB of LDS per workgroup
+static const uint32_t kNoImage = 0xFFFFFFFFu;  // the record's chip records do not fit: generic path
+static const uint32_t kImgGlobal = 0xFFFFu;
+struct ImageSource {
+    const tiles::TileRec* recs;
+    size_t n_recs;
+    const uint32_t* entries;
+    const HashEntry* table;
+    const uint32_t* meta;
+    pip::GeomStore store;
+    int threads;
+};
+// words: the images back to back; off[r]: word offset of record r's image or kNoImage; max_words:
+// the largest image.  False when the images would pass 2^32 words.
+bool build_tile_images(const ImageSource& s, std::vector<uint32_t>& words, std::vector<uint32_t>& off,
+                       uint32_t& max_words);
+
+struct Images {
+    const uint32_t* words = nullptr;  // nullptr: no images (k_join_binned runs)
+    const uint32_t* off = nullptr;
+    uint32_t max_words = 0;
+};
+
 // Rows [lo, n) of a.x / a.y: key, sort, join (enqueued on stream).  max_code: the largest tile code
 // (tile records + 1).  s.exact_args receives the JoinArgs the exact-H3 pass runs with.
-hipError_t join(const JoinArgs& a, int64_t lo, int64_t n, uint32_t max_code, bool lds_counts, int n_cu, Scratch& s,
-                hipStream_t stream);
+hipError_t join(const JoinArgs& a, int64_t lo, int64_t n, uint32_t max_code, bool lds_counts, int n_cu,
+                const Images& img, Scratch& s, hipStream_t stream);
 
 }  // namespace binned

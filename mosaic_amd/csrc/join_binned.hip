@@ -16,7 +16,13 @@
 // pairs, their source rows) through JoinArgs::cstride / rowmap.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <math.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
 
 #include "join_binned.h"
 #include "join_chips.h"
@@ -24,20 +30,38 @@
 using namespace mosaic;
 
 template <class P>
+__device__ __forceinline__ void bin_one(const JoinArgs& a, int64_t i, int64_t lo, double x, double y, uint32_t* keys, P* pts,
+                                        unsigned int& skipped) {
+    const uint32_t code = tiles::tile_of(a.tgrid, a.tile_idx, x, y);
+    keys[i - lo] = code;
+    P p;
+    p.x = x;
+    p.y = y;
+    binned::set_row(p, i);
+    pts[i - lo] = p;
+    skipped += code == tiles::kSkip;
+}
+
+// VEC: two consecutive points per lane and step (16-byte loads of x and y; lo even and the columns
+// 16-byte aligned)
+template <class P, bool VEC>
 __global__ void __launch_bounds__(256) k_bin_keys(JoinArgs a, int64_t lo, int64_t n, uint32_t* keys, P* pts,
                                                   unsigned long long* n_skip) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     unsigned int skipped = 0;
-    for (int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const double x = a.x[i], y = a.y[i];
-        const uint32_t code = tiles::tile_of(a.tgrid, a.tile_idx, x, y);
-        keys[i - lo] = code;
-        P p;
-        p.x = x;
-        p.y = y;
-        binned::set_row(p, i);
-        pts[i - lo] = p;
-        skipped += code == tiles::kSkip;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (VEC) {
+        const int64_t np = (n - lo) / 2;
+        const v2d* X = (const v2d*)(a.x + lo);
+        const v2d* Y = (const v2d*)(a.y + lo);
+        for (int64_t k = t0; k < np; k += stride) {
+            const v2d x = __builtin_nontemporal_load(&X[k]), y = __builtin_nontemporal_load(&Y[k]);
+            bin_one(a, lo + 2 * k, lo, x.x, y.x, keys, pts, skipped);
+            bin_one(a, lo + 2 * k + 1, lo, x.y, y.y, keys, pts, skipped);
+        }
+        if (t0 == 0 && ((n - lo) & 1)) bin_one(a, n - 1, lo, a.x[n - 1], a.y[n - 1], keys, pts, skipped);
+    } else {
+        for (int64_t i = lo + t0; i < n; i += stride) bin_one(a, i, lo, a.x[i], a.y[i], keys, pts, skipped);
     }
     for (int off = 32; off > 0; off >>= 1) skipped += __shfl_down(skipped, off, 64);
     if ((threadIdx.x & 63) == 0 && skipped) atomicAdd(n_skip, (unsigned long long)skipped);
@@ -96,11 +120,194 @@ __global__ void __launch_bounds__(256) k_join_binned(JoinArgs a, const uint32_t*
     }
 }
 
+// ---- k_join_tiles: the binned join over per-tile chip images in LDS (north_star kernel (c): chip
+// rings tiled into LDS).  A workgroup takes kSegPoints consecutive sorted points and walks their
+// runs of equal tile code; per run it copies the tile's image (join_binned.h) into LDS once, then
+// each lane finds its point's hexagon from the tile record (tiled_cell's face-plane rounding: the
+// same certified hexagon) and tests the hexagon's chips from LDS: core chips count, border chips
+// get the f32 envelope pre-test and JTS's ray-crossing ring walk (pip::locate_in_ring's
+// arithmetic) on LDS vertices.  Chips kept in the global store (multi-ring / multi-part, or past
+// the image's vertex budget) take pip::contains; runs without an image (kFull tiles, records over
+// the image cap) and hexagons outside the window take the generic chip loop (raster_chips).
+static const int kSegPoints = 2048;
+
+// false only when (x, y) lies outside the chip's f64 envelope (the f32 box is rounded outwards and
+// rounding is monotone, so fx, fy of a point inside the f64 box are inside the f32 box)
+__device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) {
+    return fx >= __uint_as_float(cr[4]) && fy >= __uint_as_float(cr[5]) && fx <= __uint_as_float(cr[6]) &&
+           fy <= __uint_as_float(cr[7]);
+}
+
+// PointLocation.locateInRing(p, ring) == INTERIOR for a closed ring of n vertices (x, y pairs):
+// pip::locate_in_ring's RayCrossingCounter steps and CGAlgorithmsDD orientation, operation for
+// operation.  A point outside the ring's envelope gets EXTERIOR from the walk itself (no crossing
+// counted twice), so the envelope pre-test of locate_in_polygon changes no answer.
+__device__ __forceinline__ bool ring_interior(const double* v, uint32_t n, double px, double py) {
+    int crossings = 0;
+    double p2x = v[0], p2y = v[1];
+    for (uint32_t i = 1; i < n; i++) {
+        const double p1x = v[2 * i], p1y = v[2 * i + 1];
+        if (!(p1x < px && p2x < px)) {
+            if (px == p2x && py == p2y) return false;
+            if (p1y == py && p2y == py) {
+                const double mnx = p1x < p2x ? p1x : p2x, mxx = p1x < p2x ? p2x : p1x;
+                if (px >= mnx && px <= mxx) return false;
+            } else if (((p1y > py) && (p2y <= py)) || ((p2y > py) && (p1y <= py))) {
+                int orient = pip::orientation_index(p1x, p1y, p2x, p2y, px, py);
+                if (orient == 0) return false;
+                if (p2y < p1y) orient = -orient;
+                if (orient == 1) crossings++;
+            }
+        }
+        p2x = p1x;
+        p2y = p1y;
+    }
+    return crossings & 1;
+}
+
+template <int CM, bool PAIRS, class P>
+__global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys,
+                                                    const P* __restrict__ pts, int64_t n, const unsigned long long* n_skip,
+                                                    binned::Images img, uint32_t img_words) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_t[];
+    __shared__ SlabItem items[4][16];
+    __shared__ uint32_t pairs_all[4 * 64];  // per wave: a window of (point lane, chip) pairs
+    __shared__ unsigned long long run_end_s;
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = (int)(threadIdx.x >> 6) & 3;
+    uint32_t* im = lds_t;
+    unsigned int* cnt = lds_t + img_words;
+    if (CM == kCountLds) {
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x) cnt[k] = 0;
+    } else if (CM == kCountWaveHash) {
+        cnt += wv * kWaveHashWords;
+        for (int k = lane; k < kWaveHashWords; k += 64) cnt[k] = 0;
+    }
+    __syncthreads();
+    unsigned int tests = 0;
+    const int64_t s0 = (int64_t)*n_skip + (int64_t)blockIdx.x * kSegPoints;
+    const int64_t s1 = s0 + kSegPoints < n ? s0 + kSegPoints : n;
+    for (int64_t pos = s0; pos < s1;) {  // block-uniform: one run of equal tile code per iteration
+        const uint32_t code = keys[pos];
+        if (threadIdx.x == 0) run_end_s = (unsigned long long)s1;
+        __syncthreads();
+        for (int64_t b = pos + 1; b < s1; b += 256) {
+            const int64_t i = b + threadIdx.x;
+            if (i < s1 && keys[i] != code) atomicMin(&run_end_s, (unsigned long long)i);
+            __syncthreads();
+            const bool found = run_end_s < (unsigned long long)s1;
+            __syncthreads();
+            if (found) break;
+        }
+        const int64_t r1 = (int64_t)run_end_s;
+        const uint32_t ioff = (code >= 2 && img.off) ? img.off[code - 2] : binned::kNoImage;
+        tiles::TileRec tr{0, 0, 0, 0};
+        if (ioff != binned::kNoImage) {
+            tr = a.tile_rec[code - 2];
+            const uint32_t* src = img.words + ioff;
+            const uint32_t nw = src[3] + 4u * src[1];  // vertex offset + vertex words
+            for (uint32_t k = 4u * threadIdx.x; k < nw; k += 4u * blockDim.x)
+                *(uint4*)(im + k) = *(const uint4*)(src + k);
+            __syncthreads();
+        }
+        const int face = (int)(tr.dims & 0xffu);
+        const int wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
+        const uint32_t* chips = im + im[2];
+        const double* V = (const double*)(im + im[3]);
+        for (int64_t g = pos + wv * 64; g < r1; g += 256) {  // wave-uniform
+            const int64_t i = g + lane;
+            double x = 0.0, y = 0.0;
+            int64_t row = -1;
+            uint32_t cur = 0, end = 0;  // chips left to the generic loop
+            uint32_t c0 = 0, c1 = 0;    // the point's chips in the image
+            if (i < r1) {
+                const P p = pts[i];
+                x = p.x;
+                y = p.y;
+                row = binned::row_of(p, i);
+                if (ioff == binned::kNoImage) {
+                    tiled_cell(a, i, x, y, code, cur, end);
+                } else {
+                    double px, py, pz, vx, vy, best;
+                    h3::fast_unit(y, x, &px, &py, &pz);
+                    h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
+                    int ba, bb;
+                    if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
+                        const unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+                        if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+                    } else {
+                        const int ra = ba - tr.a0, rb = bb - tr.b0;
+                        if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
+                            const uint32_t slot = (uint32_t)(ra * wb + rb);
+                            const uint16_t* sf = (const uint16_t*)(im + 4);
+                            c0 = sf[slot];
+                            c1 = sf[slot + 1];
+                        } else {
+                            probe(a, (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res), cur, end);
+                        }
+                    }
+                }
+            }
+            // the group's (point, chip) pairs, 64 at a time, one per lane: the work is spread over
+            // the wave whatever the points' chip counts (a lane per point would run the wave for
+            // its most crowded cell)
+            const uint32_t n = c1 - c0;
+            uint32_t incl = n;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += t;
+            }
+            const uint32_t off = incl - n, T = __shfl(incl, 63, 64);
+            uint32_t* pb = pairs_all + wv * 64;
+            for (uint32_t w0 = 0; w0 < T; w0 += 64) {  // wave-uniform
+                const uint32_t e0 = off > w0 ? off : w0, e1 = off + n < w0 + 64 ? off + n : w0 + 64;
+                for (uint32_t e = e0; e < e1; e++) pb[e - w0] = (uint32_t)lane | (c0 + (e - off)) << 6;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const bool live = w0 + (uint32_t)lane < T;
+                const uint32_t ent = live ? pb[lane] : 0u;
+                const int owner = (int)(ent & 63u);
+                const double qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64);
+                const int64_t qrow = PAIRS ? (int64_t)__shfl((long long)row, owner, 64) : -1;
+                if (live) {
+                    const uint32_t* cr = chips + 8u * (ent >> 6);
+                    const uint32_t meta = cr[0];
+                    bool hit = true;
+                    if (!(meta & 1u)) {
+                        tests++;
+                        const uint32_t vi = cr[1], vc = vi >> 16;
+                        if (vc == binned::kImgGlobal) hit = pip::contains(a.store, cr[2], qx, qy);
+                        else hit = fbox_in(cr, (float)qx, (float)qy) && ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
+                    }
+                    if (hit) emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            raster_chips<CM, PAIRS>(a, row, cur, end, x, y, tests, cnt, items[wv]);
+            if (CM == kCountWaveHash) wave_hash_flush(a, cnt, false);
+        }
+        __syncthreads();  // every wave is done with this run's image
+        pos = r1;
+    }
+    if (CM == kCountWaveHash) wave_hash_flush(a, cnt, true);
+    for (int off = 32; off > 0; off >>= 1) tests += __shfl_down(tests, off, 64);
+    if (lane == 0 && tests) atomicAdd(a.tests, (unsigned long long)tests);
+    if (CM == kCountLds) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (cnt[k]) atomicAdd(&a.counts[k], (unsigned long long)cnt[k]);
+    }
+}
+
 namespace binned {
 
 template <class P>
 static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint32_t max_code, int cm, int n_cu,
-                                Scratch& s, hipStream_t stream) {
+                                const Images& img, Scratch& s, hipStream_t stream) {
     const int64_t m = n - lo;
     const size_t vb = sizeof(P);
     hipError_t e;
@@ -109,9 +316,13 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
         return e;
     if ((e = hipMemsetAsync(s.n_skip.p, 0, 8, stream))) return e;
     unsigned long long* nsk = (unsigned long long*)s.n_skip.p;
-    const int gk = (int)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, (int64_t)n_cu * 8));
-    hipLaunchKernelGGL((k_bin_keys<P>), dim3(gk), dim3(256), 0, stream, a0, lo, n, (uint32_t*)s.keys[0].p,
-                       (P*)s.vals[0].p, nsk);
+    const int gk = (int)std::max<int64_t>(1, std::min<int64_t>((m + 511) / 512, (int64_t)n_cu * 16));
+    if ((((uintptr_t)(a0.x + lo) | (uintptr_t)(a0.y + lo)) & 15) == 0)
+        hipLaunchKernelGGL((k_bin_keys<P, true>), dim3(gk), dim3(256), 0, stream, a0, lo, n, (uint32_t*)s.keys[0].p,
+                           (P*)s.vals[0].p, nsk);
+    else
+        hipLaunchKernelGGL((k_bin_keys<P, false>), dim3(gk), dim3(256), 0, stream, a0, lo, n, (uint32_t*)s.keys[0].p,
+                           (P*)s.vals[0].p, nsk);
     if ((e = hipGetLastError())) return e;
     // the key's significant bits (codes <= max_code)
     int end_bit = 1;
@@ -134,7 +345,20 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
     const uint32_t* keys = kb.Current();
     const P* pts = pb.Current();
     const bool pairs = a.pair_row != nullptr;
-    if (pairs) {
+    if (img.words) {
+        // one workgroup per kSegPoints sorted points (those past the kSkip prefix exit at once)
+        const uint32_t iw = (img.max_words + 3u) & ~3u;
+        const int gt = (int)std::max<int64_t>(1, (m + kSegPoints - 1) / kSegPoints);
+        const size_t cw = pairs ? 0 : (cm == kCountLds ? (size_t)a.n_polygons : (size_t)(blk / 64) * kWaveHashWords);
+        const size_t shm = ((size_t)iw + cw) * 4;
+        if (pairs)
+            hipLaunchKernelGGL((k_join_tiles<kCountGlobal, true, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw);
+        else if (cm == kCountLds)
+            hipLaunchKernelGGL((k_join_tiles<kCountLds, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw);
+        else
+            hipLaunchKernelGGL((k_join_tiles<kCountWaveHash, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk,
+                               img, iw);
+    } else if (pairs) {
         hipLaunchKernelGGL((k_join_binned<kCountGlobal, true, P>), dim3(gj), dim3(blk), 0, stream, a, keys, pts, m, nsk);
     } else if (cm == kCountLds) {
         hipLaunchKernelGGL((k_join_binned<kCountLds, false, P>), dim3(gj), dim3(blk), (size_t)a.n_polygons * 4, stream, a,
@@ -148,11 +372,124 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
     return hipSuccess;
 }
 
-hipError_t join(const JoinArgs& a, int64_t lo, int64_t n, uint32_t max_code, bool lds_counts, int n_cu, Scratch& s,
-                hipStream_t stream) {
+hipError_t join(const JoinArgs& a, int64_t lo, int64_t n, uint32_t max_code, bool lds_counts, int n_cu,
+                const Images& img, Scratch& s, hipStream_t stream) {
     const int cm = lds_counts ? kCountLds : kCountWaveHash;
-    if (a.pair_row) return sort_and_join<PtRow>(a, lo, n, max_code, cm, n_cu, s, stream);
-    return sort_and_join<Pt>(a, lo, n, max_code, cm, n_cu, s, stream);
+    if (a.pair_row) return sort_and_join<PtRow>(a, lo, n, max_code, cm, n_cu, img, s, stream);
+    return sort_and_join<Pt>(a, lo, n, max_code, cm, n_cu, img, s, stream);
+}
+
+// ---- tile images (host)
+static inline float f32_down(double v) {
+    float f = (float)v;
+    if ((double)f > v) f = nextafterf(f, -INFINITY);
+    return f;
+}
+static inline float f32_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// image of record r: its words (empty: kNoImage)
+static void tile_image(const ImageSource& s, size_t r, std::vector<uint32_t>& w) {
+    w.clear();
+    const tiles::TileRec& tr = s.recs[r];
+    const uint32_t wa = (tr.dims >> 8) & 0xfffu, wb = tr.dims >> 20, ns = wa * wb;
+    if (ns == 0 || ns >= 0xffffu) return;
+    std::vector<uint32_t> first(ns + 1, 0);
+    uint32_t nc = 0;
+    for (uint32_t k = 0; k < ns; k++) {
+        first[k] = nc;
+        const uint32_t e = s.entries[tr.off + k];
+        if (e) nc += s.table[e - 1].count;
+    }
+    first[ns] = nc;
+    const uint32_t slot_words = (ns + 2) / 2;
+    const uint32_t chip_off = (4u + slot_words + 3u) & ~3u;
+    const uint32_t vert_off = chip_off + 8u * nc;
+    if (nc >= 0xffffu || vert_off > kImgCapWords) return;
+    w.assign(vert_off, 0u);
+    w[0] = ns | nc << 16;
+    w[2] = chip_off;
+    w[3] = vert_off;
+    uint16_t* sf = (uint16_t*)(w.data() + 4);
+    for (uint32_t k = 0; k <= ns; k++) sf[k] = (uint16_t)first[k];
+    uint32_t nv = 0, c = 0;
+    for (uint32_t k = 0; k < ns; k++) {
+        const uint32_t e = s.entries[tr.off + k];
+        if (!e) continue;
+        const HashEntry& he = s.table[e - 1];
+        for (uint32_t g = he.first; g < he.first + he.count; g++, c++) {
+            uint32_t* cr = &w[chip_off + 8u * c];
+            cr[0] = s.meta[g];
+            cr[2] = g;
+            const pip::Box& bx = s.store.geom_bbox[g];
+            const float fb[4] = {f32_down(bx.minx), f32_down(bx.miny), f32_up(bx.maxx), f32_up(bx.maxy)};
+            memcpy(cr + 4, fb, 16);
+            if (s.meta[g] & 1u) continue;  // core: no geometry read
+            cr[1] = kImgGlobal << 16;
+            const uint32_t p0 = s.store.geom_part[g], p1 = s.store.geom_part[g + 1];
+            if (p1 - p0 != 1) continue;
+            const uint32_t r0 = s.store.part_ring[p0], r1 = s.store.part_ring[p0 + 1];
+            if (r1 - r0 != 1) continue;
+            const uint32_t v0 = s.store.ring_start[r0], v1 = s.store.ring_start[r0 + 1], m = v1 - v0;
+            // (a ring of < 4 vertices stays global: pip::contains' own handling of degenerate rings)
+            if (m < 4 || m >= kImgGlobal || vert_off + 4u * (nv + m) > kImgCapWords) continue;
+            cr[1] = nv | m << 16;
+            for (uint32_t v = 0; v < m; v++) {
+                const pip::Vec2 q = s.store.verts[v0 + v];
+                uint32_t qw[4];
+                memcpy(qw, &q, 16);
+                w.insert(w.end(), qw, qw + 4);
+            }
+            nv += m;
+        }
+    }
+    w[1] = nv;
+}
+
+bool build_tile_images(const ImageSource& s, std::vector<uint32_t>& words, std::vector<uint32_t>& off,
+                       uint32_t& max_words) {
+    const size_t nr = s.n_recs;
+    const int nt = std::max(1, std::min<int>(s.threads, (int)(nr / 64) + 1));
+    std::vector<std::vector<uint32_t>> part((size_t)nt);
+    std::vector<std::vector<uint32_t>> part_off((size_t)nt);
+    std::vector<uint32_t> part_max((size_t)nt, 0);
+    auto work = [&](int t) {
+        std::vector<uint32_t> w;
+        auto& pw = part[(size_t)t];
+        auto& po = part_off[(size_t)t];
+        for (size_t r = nr * t / nt; r < nr * (t + 1) / nt; r++) {
+            tile_image(s, r, w);
+            if (w.empty()) {
+                po.push_back(kNoImage);
+                continue;
+            }
+            po.push_back((uint32_t)pw.size());
+            pw.insert(pw.end(), w.begin(), w.end());
+            part_max[(size_t)t] = std::max(part_max[(size_t)t], (uint32_t)w.size());
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    size_t total = 0;
+    for (auto& p : part) total += p.size();
+    if (total >= (size_t)kNoImage) return false;
+    words.clear();
+    words.reserve(total);
+    off.clear();
+    off.reserve(nr);
+    max_words = 0;
+    for (int t = 0; t < nt; t++) {
+        const uint32_t base = (uint32_t)words.size();
+        for (uint32_t o : part_off[(size_t)t]) off.push_back(o == kNoImage ? kNoImage : o + base);
+        words.insert(words.end(), part[(size_t)t].begin(), part[(size_t)t].end());
+        max_words = std::max(max_words, part_max[(size_t)t]);
+    }
+    return true;
 }
 
 }  // namespace binned

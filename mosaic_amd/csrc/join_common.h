@@ -297,5 +297,4 @@ struct BngStreamArgs {
 // The stream kernels (join_stream.hip), by template arguments: the host picks one and launches it
 // with hipLaunchKernel.  pipe: k_join_stream_pipe (needs vec); else k_join_stream<lds, pairs, vec>.
 const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec);
-const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool pipe, bool cpt);  // pipe: k_join_stream_bng_pipe (needs vec)
-static const int kBngPipeBlock = 768;  // k_join_stream_bng_pipe's workgroup size (its launch bound)
+const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool cpt);  // cpt: k_join_stream_bng_cpt (needs vec)

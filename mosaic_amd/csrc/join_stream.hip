@@ -1254,219 +1254,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     }
 }
 
-// ---- k_join_stream_bng_pipe: k_join_stream_bng as a four-stage software pipeline over each wave's
-// groups of 256 rows (the H3 kernel's scheme, one stage longer: the BNG answer can take three
-// dependent gathers).  Iteration t: D finishes group t - 3 (its line records arrived), C turns group
-// t - 2's sub-cell codes into line-record gathers, B turns group t - 1's cell entries into sub-cell
-// gathers, A runs group t's coordinates through the integer cell arithmetic and the LDS cell level
-// and gathers its cell entries, then group t + 1's coordinates are loaded -- issued in that order,
-// so every wait is on the oldest loads in flight.  Gathers only by the lanes that need them.  Same
-// answers as k_join_stream_bng, point for point.  Three groups in flight take ~160 VGPRs: 768-thread
-// workgroups, three waves per SIMD (kBngPipeBlock).
-struct BngGroup {
-    uint32_t uv[4];      // the point's offset in its sub-cell, 16-bit fixed point (sub-cell units) per axis
-    uint32_t e[4];       // A -> B: gathered cell entry; B -> C: gathered sub-cell code; C -> D: -
-    uint32_t p[4];       // A -> B: the entry of rows without a gather (0 / kBngPure | code / 1 = kMixed);
-                         // B -> C: the answer if no sub-cell code is needed, else kBngLeaf;
-                         // C -> D: the answer, or kPipeLine (line record)
-    uint32_t q[4];       // A -> B: sub-cell index; B -> C: the cell's leaf base
-    v4u lrec[4];         // C -> D: gathered line record
-};
-
-template <bool LDS_COUNTS, bool PAIRS>
-__global__ void __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(3))) k_join_stream_bng_pipe(JoinArgs a, BngStreamArgs s) {
-    extern __shared__ unsigned int lds[];
-    const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
-    uint32_t* stage = lds + ncw;
-    uint32_t* lcw = stage + (int)(blockDim.x >> 6) * kStageWords;
-    const uint8_t* lcell = (const uint8_t*)lcw;
-    const bool use_lc = s.lcell_words > 0;  // (uniform)
-    for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
-    lds_fill(lcw, s.lcell, s.lcell_words);
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t rcell = stream_rsrc(s.cells, s.cells_bytes);
-    const __amdgpu_buffer_rsrc_t rleaf = stream_rsrc(s.leaf, s.leaf_bytes);
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint32_t* wq = stage + wave * kStageWords;
-    uint32_t wn = 0;
-    bool nan_seen = false;
-    const uint32_t C = (uint32_t)s.C;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    const int64_t wbase = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
-    const int64_t T = wbase + 256 <= a.n ? (a.n - 256 - wbase) / stride + 1 : 0;
-    auto row_of = [&](int64_t wb, int k) -> int64_t { return wb + (k >> 1) * 128 + 2 * lane + (k & 1); };
-    // A: coordinates -> cell, LDS cell level, cell-entry gathers
-    auto stage_a = [&](const double* x, const double* y, const bool* live, bool valid, BngGroup& g) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool lv = valid && live[k];
-            const bool nan = x[k] != x[k] || y[k] != y[k];
-            nan_seen |= lv && nan;
-            const int32_t eI = bng::jvm_d2i(x[k]), nI = bng::jvm_d2i(y[k]);
-            const bool inr = (uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u;
-            const int32_t qe = (int32_t)fma((double)eI, s.inv_div, 1e-7), qn = (int32_t)fma((double)nI, s.inv_div, 1e-7);
-            const int32_t ce = qe - s.e0, cn = qn - s.n0;
-            const bool ok = lv && !nan;  // rows that can join (NaN: flagged, no pair)
-            const bool cell_in = ok && inr && (uint32_t)ce < (uint32_t)s.ne && (uint32_t)cn < (uint32_t)s.nn;
-            const uint32_t li = cell_in ? __umul24((uint32_t)cn >> s.lsh, (uint32_t)s.lnx) + ((uint32_t)ce >> s.lsh) : 0u;
-            const uint32_t lb = use_lc ? (uint32_t)lcell[li] : kBngLdsGather;
-            const bool gth = cell_in && lb == kBngLdsGather;
-            uint32_t ev = 0u;
-            if (gth) ev = __builtin_amdgcn_raw_buffer_load_b32(rcell, (uint32_t)(cn * s.ne + ce) << 2, 0, 0);
-            g.e[k] = ev;
-            // rows outside the one-to-one range take the generic path (an entry with neither flag
-            // answers kMixed); empty or pure LDS blocks answer without a gather
-            g.p[k] = !ok ? 0u : (!inr ? 1u : (gth || !cell_in ? 0u : (lb ? (kBngPure | lb) : 0u)));
-            const double gxs = (x[k] - (double)qe * s.div) * s.f, gys = (y[k] - (double)qn * s.div) * s.f;
-            int sx = (int)gxs, sy = (int)gys;
-            sx = min(max(sx, 0), (int)C - 1);
-            sy = min(max(sy, 0), (int)C - 1);
-            // 16-bit fixed point, rounded: the offset moves by <= 2^-17 sub-cells, far inside the
-            // 1e-4 sub-cell slack the line records were certified with (tiles_build.cpp)
-            const uint32_t fu = min((uint32_t)((gxs - (double)sx) * 65536.0 + 0.5), 65535u);
-            const uint32_t fv = min((uint32_t)((gys - (double)sy) * 65536.0 + 0.5), 65535u);
-            g.uv[k] = fu | (fv << 16);
-            g.q[k] = (uint32_t)(sy * (int)C + sx);
-        }
-    };
-    // B: cell entries -> sub-cell code gathers
-    auto stage_b = [&](BngGroup& g) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t e = g.e[k] | g.p[k];
-            const bool leafc = (e & (kBngPure | kBngLeaf)) == kBngLeaf;
-            const uint32_t base = e & ~kBngLeaf;
-            uint32_t code = 0u;
-            if (leafc) code = __builtin_amdgcn_raw_buffer_load_b16(rleaf, (base + g.q[k]) << 1, 0, MOSAIC_AUX_BNG);
-            g.e[k] = code;
-            g.q[k] = base;
-            g.p[k] = (e & kBngPure) ? (e & ~kBngPure) : (leafc ? kBngLeaf : (e ? (uint32_t)tiles::kMixed : 0u));
-        }
-    };
-    // C: sub-cell codes -> line-record gathers
-    auto stage_c = [&](BngGroup& g) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t code = g.e[k];
-            const bool leafc = g.p[k] == kBngLeaf;
-            const bool line = leafc && (code & 0xC000u) == 0xC000u && code != (uint32_t)tiles::kMixed;
-            v4u r = {0u, 0u, 0u, 0u};
-            if (line) r = __builtin_amdgcn_raw_buffer_load_b128(rleaf, (g.q[k] - 8u * ((code & 0x3fffu) + 1u)) << 1, 0, 0);
-            g.lrec[k] = r;
-            g.p[k] = line ? kPipeLine : (leafc ? code : g.p[k]);
-        }
-    };
-    // D: answers -> counts and the mixed-row stage
-    auto stage_d = [&](BngGroup& g, int64_t wb) {
-        uint32_t code[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float su = (float)(g.uv[k] & 0xffffu) * (1.0f / 65536.0f), sv = (float)(g.uv[k] >> 16) * (1.0f / 65536.0f);
-            const float lv = fmaf(__uint_as_float(g.lrec[k].x), su, fmaf(__uint_as_float(g.lrec[k].y), sv, __uint_as_float(g.lrec[k].z)));
-            uint32_t lc = lv >= 1.0f ? (g.lrec[k].w & 0xffffu) : (uint32_t)tiles::kMixed;
-            lc = lv <= -1.0f ? (g.lrec[k].w >> 16) : lc;
-            code[k] = g.p[k] == kPipeLine ? lc : g.p[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (LDS_COUNTS && !PAIRS) {
-                const uint32_t slot = code[k] - 1u < 0xfffeu ? code[k] - 1u : (uint32_t)(a.n_polygons + lane);
-                atomicAdd(&lds[slot], 1u);
-            } else if (code[k] - 1u < 0xfffeu) {
-                emit_hit<LDS_COUNTS, PAIRS>(a, row_of(wb, k), code[k] - 1u, lds);
-            }
-        }
-        const bool anym = code[0] == tiles::kMixed || code[1] == tiles::kMixed || code[2] == tiles::kMixed ||
-                          code[3] == tiles::kMixed;
-        if (__ballot(anym)) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const bool m = code[k] == tiles::kMixed;
-                const unsigned long long mm = __ballot(m);
-                if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row_of(wb, k) - a.row_lo);
-                wn += (uint32_t)__popcll(mm);
-                stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
-            }
-        }
-    };
-    struct Coords {
-        v2d px[2], py[2];
-    };
-    auto load4 = [&](Coords& cb, int64_t wb, bool valid) {  // invalid groups re-read the wave's first rows
-        const int64_t r = valid ? wb + 2 * lane : wbase + 2 * lane;
-        cb.px[0] = __builtin_nontemporal_load((const v2d*)(a.x + r));
-        cb.px[1] = __builtin_nontemporal_load((const v2d*)(a.x + r + 128));
-        cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
-        cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
-    };
-    // three group slots used in turn: iteration t finishes the slot holding t - 3 (D), advances
-    // t - 2 (C) and t - 1 (B), and refills the finished slot with group t (A)
-    BngGroup g0, g1, g2;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        g0.e[k] = g1.e[k] = g2.e[k] = 0u;
-        g0.p[k] = g1.p[k] = g2.p[k] = 0u;
-        g0.q[k] = g1.q[k] = g2.q[k] = 0u;
-        g0.uv[k] = g1.uv[k] = g2.uv[k] = 0u;
-        g0.lrec[k] = g1.lrec[k] = g2.lrec[k] = v4u{0u, 0u, 0u, 0u};
-    }
-    Coords cb0, cb1;
-    // gd: holds t - 3, then group t; gc: t - 2; gb: t - 1
-    auto step = [&](int64_t t, BngGroup& gd, BngGroup& gc, BngGroup& gb, Coords& cb, Coords& cn) {
-        const bool all[4] = {true, true, true, true};
-        if (t >= 3) stage_d(gd, wbase + (t - 3) * stride);
-        stage_c(gc);  // (invalid groups gather nothing)
-        stage_b(gb);
-        const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
-        const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
-        stage_a(x, y, all, t < T, gd);
-        load4(cn, wbase + (t + 1) * stride, t + 1 < T);
-    };
-    if (T > 0) {
-        load4(cb0, wbase, true);
-        for (int64_t t = 0; t < T + 3; t += 6) {
-            step(t, g0, g1, g2, cb0, cb1);
-            if (t + 1 >= T + 3) break;
-            step(t + 1, g1, g2, g0, cb1, cb0);
-            if (t + 2 >= T + 3) break;
-            step(t + 2, g2, g0, g1, cb0, cb1);
-            if (t + 3 >= T + 3) break;
-            step(t + 3, g0, g1, g2, cb1, cb0);
-            if (t + 4 >= T + 3) break;
-            step(t + 4, g1, g2, g0, cb0, cb1);
-            if (t + 5 >= T + 3) break;
-            step(t + 5, g2, g0, g1, cb1, cb0);
-        }
-    }
-    // the wave's partial group, unpipelined
-    const int64_t wt = wbase + T * stride;
-    if (wt < a.n) {
-        double x[4], y[4];
-        bool live[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int64_t r = row_of(wt, k);
-            live[k] = r < a.n;
-            x[k] = live[k] ? a.x[r] : 0.0;
-            y[k] = live[k] ? a.y[r] : 0.0;
-        }
-        BngGroup g;
-        stage_a(x, y, live, true, g);
-        stage_b(g);
-        stage_c(g);
-        stage_d(g, wt);
-    }
-    stage_flush(a, wq, wn, lane, 1);
-    if (__ballot(nan_seen) && lane == 0) atomicOr(a.flags, 1u);
-    if (LDS_COUNTS) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
-            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
-    }
-}
-
 const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec) {
     if (pipe == 2 && vec) {
         if (pairs) return (const void*)k_join_stream_cpt<false, true>;
@@ -1483,16 +1270,11 @@ const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec) {
     return vec ? (const void*)k_join_stream<false, false, true> : (const void*)k_join_stream<false, false, false>;
 }
 
-const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool pipe, bool cpt) {
+const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool cpt) {
     if (cpt && vec) {
         if (pairs) return (const void*)k_join_stream_bng_cpt<false, true>;
         if (lds) return (const void*)k_join_stream_bng_cpt<true, false>;
         return (const void*)k_join_stream_bng_cpt<false, false>;
-    }
-    if (pipe && vec) {
-        if (pairs) return (const void*)k_join_stream_bng_pipe<false, true>;
-        if (lds) return (const void*)k_join_stream_bng_pipe<true, false>;
-        return (const void*)k_join_stream_bng_pipe<false, false>;
     }
     if (pairs) return vec ? (const void*)k_join_stream_bng<false, true, true> : (const void*)k_join_stream_bng<false, true, false>;
     if (lds) return vec ? (const void*)k_join_stream_bng<true, false, true> : (const void*)k_join_stream_bng<true, false, false>;

@@ -35,6 +35,7 @@
 #include "h3_device.h"
 #include "h3_geom.h"
 #include "h3_grid.h"
+#include "h3_neighbors.h"
 #include "isect_area.h"
 #include "join_binned.h"
 #include "join_common.h"
@@ -1023,8 +1024,9 @@ __global__ void __launch_bounds__(256) k_bng_kring(KringArgs a) {
     if (bad) atomicOr(a.flags, 1u);
 }
 
-// grid_cellkring / grid_cellkloop over H3 cells (h3_grid.h): one lane per row, H3's hexRange /
-// hexRing order; rows whose walk reaches a pentagon (or an invalid id) get count -2.
+// grid_cellkring / grid_cellkloop over H3 cells (h3_neighbors.h): one lane per row, H3's hexRange /
+// hexRing walk; rows where H3 meets a pentagon get count -3 and are finished by k_h3_kring_slow
+// (H3's _kRingInternal; the reference's set-difference fallback for kLoop); invalid ids -2.
 __global__ void __launch_bounds__(256) k_h3_kring(KringArgs a) {
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
@@ -1032,8 +1034,18 @@ __global__ void __launch_bounds__(256) k_h3_kring(KringArgs a) {
             a.count[i] = -1;
             continue;
         }
-        a.count[i] = h3grid::kring((uint64_t)a.cells[i], a.k, a.loop, a.out + i * a.stride);
+        a.count[i] = h3nb::kring_fast((uint64_t)a.cells[i], a.k, a.loop, a.out + i * a.stride);
     }
+}
+
+// the -3 rows of k_h3_kring (rows[0 .. n_rows)), one lane each, with per-lane scratch
+__global__ void __launch_bounds__(64) k_h3_kring_slow(KringArgs a, const int64_t* rows, int64_t n_rows, int64_t* tab,
+                                                      int64_t tab_stride, int32_t* dist, int64_t dist_stride) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_rows) return;
+    const int64_t i = rows[t];
+    a.count[i] = h3nb::kring_slow((uint64_t)a.cells[i], a.k, a.loop, a.out + i * a.stride, tab + t * tab_stride,
+                                  dist + t * dist_stride);
 }
 
 
@@ -1668,7 +1680,6 @@ struct Options {
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
     int bng_cpt = 1;          // k_join_stream_bng_cpt (rows needing gathers compacted) where it applies
     int stream_pipe = 2;      // 1: k_join_stream_pipe (software-pipelined), 2: k_join_stream_cpt (+ compacted gathers)
-    int bng_pipe = 0;         // k_join_stream_bng_pipe (measured slower at C5: 6.30 vs 4.53 ms, profiles/r03_kbench_bng_pipe.txt)
     int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
     int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
     int mixed_blocks_per_cu = 4;  // k_join_mixed grid: the workgroups resident at once (~120 VGPRs: 4 per CU)
@@ -1685,6 +1696,9 @@ struct Options {
     int bin_points = 1;
     int64_t bin_min_rows = (int64_t)1 << 18;
     int64_t bin_chunk = (int64_t)1 << 28;
+    // per-tile chip images in LDS for the binned join: 0 off, 1 for tables without a point raster
+    // (built with the table; joins use them when present), 2 built for every tile-directory table
+    int tile_images = 1;
 };
 
 // Execution state of one calling thread on one context: its HIP stream (created on first use, or
@@ -1943,6 +1957,9 @@ struct mosaic_chips {
     bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
     StreamArgs stream{};
     DevBuf rsub, rmid, rblocks, rquad, rqrec;  // rmid: per-tile leaf block bases; rqrec: quad records
+    DevBuf img_words, img_off;  // per-tile chip images of the binned join (join_binned.h); empty: none
+    uint32_t img_max_words = 0;
+    int64_t img_records = 0;
     int64_t raster_stats[6] = {0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
                                                    // line sub-blocks
     // build cost (ms): chip table core (hash, geometry, chip rasters), tile directory, point-raster
@@ -1952,7 +1969,8 @@ struct mosaic_chips {
     size_t raster_parts[6] = {0, 0, 0, 0, 0, 0};  // bytes of sub, blocks, tile_base, quad, qrec masks, qrec codes
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell})
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell,
+                          &img_words, &img_off})
             b->release();
         store.release();
     }
@@ -2166,8 +2184,6 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "stream_pipe") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "stream_pipe must be 0, 1 or 2");
         o.stream_pipe = (int)v;
-    } else if (k == "bng_pipe") {
-        o.bng_pipe = v ? 1 : 0;
     } else if (k == "bng_cpt") {
         o.bng_cpt = v ? 1 : 0;
     } else if (k == "bng_lds") {
@@ -2180,6 +2196,9 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.timing = (int)v;
     } else if (k == "bin_points") {
         o.bin_points = v ? 1 : 0;
+    } else if (k == "tile_images") {
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "tile_images must be 0, 1 or 2");
+        o.tile_images = (int)v;
     } else if (k == "bin_min_rows") {
         if (v < 0) return fail(MOSAIC_E_ARG, "bin_min_rows must be >= 0");
         o.bin_min_rows = v;
@@ -3430,6 +3449,34 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 }
             }
         }
+        // per-tile chip images for the binned join's LDS tiles (join_binned.h): tables without a
+        // point raster to stream (option tile_images 1), or always (2)
+        if (ch->tiles_ok && (c->tile_images == 2 || (c->tile_images == 1 && !ch->raster_ok))) {
+            binned::ImageSource is;
+            is.recs = tb.recs.data();
+            is.n_recs = tb.recs.size();
+            is.entries = tb.entries.data();
+            is.table = table.data();
+            is.meta = meta.data();
+            is.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(), gb.part_ring.data(),
+                                      gb.geom_part.data(), gb.geom_bbox.data()};
+            is.threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+            std::vector<uint32_t> iwords, ioff;
+            uint32_t imax = 0;
+            if (binned::build_tile_images(is, iwords, ioff, imax) && !iwords.empty()) {
+                if ((rc = ch->img_words.reserve(iwords.size() * 4)) || (rc = ch->img_off.reserve(ioff.size() * 4))) {
+                    ch->release_all();
+                    delete ch;
+                    return rc;
+                }
+                HIP_TRY(hipMemcpy(ch->img_words.p, iwords.data(), iwords.size() * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(ch->img_off.p, ioff.data(), ioff.size() * 4, hipMemcpyHostToDevice));
+                ch->img_max_words = imax;
+                ch->img_records = (int64_t)std::count_if(ioff.begin(), ioff.end(), [](uint32_t o) { return o != binned::kNoImage; });
+                total += iwords.size() * 4 + ioff.size() * 4;
+            }
+            trace.mark("tile images");
+        }
         defer_free(std::move(tb));
         trace.mark("(tile builder handed off)");
     }
@@ -3495,6 +3542,9 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
     o[2] = ch->praster.quad ? ch->praster.qshift : 0;
     o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes + ch->rqrec.bytes) : 0;
     o[4] = ch->stream_ok ? 1 : 0;
+    o[5] = ch->img_records;  // binned join: tile records with an LDS chip image, their bytes, the largest image
+    o[6] = (int64_t)(ch->img_words.bytes + ch->img_off.bytes);
+    o[7] = (int64_t)ch->img_max_words * 4;
     return MOSAIC_OK;
 }
 
@@ -3655,8 +3705,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
-            const bool bpipe = c->bng_pipe && aligned;  // k_join_stream_bng_pipe (768-thread workgroups)
-            const int blkb = bpipe ? std::min(c->stream_block, kBngPipeBlock) : c->stream_block;
+            const int blkb = c->stream_block;
             size_t shm_b = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blkb / 64) * kStageWords * 4;
             // the LDS cell level when it fits this launch's LDS
             bs.lcell = (const uint32_t*)ch->bng_lcell.p;
@@ -3667,13 +3716,13 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             // k_join_stream_bng_cpt (option bng_cpt): with the LDS cell level, a 24-bit cell index and
             // room for its per-wave compaction buffers
             const size_t cpt_bytes = (size_t)(blkb / 64) * kCptBufWords * 4;
-            const bool bcpt = c->bng_cpt && !bpipe && aligned && bs.lcell_words > 0 &&
+            const bool bcpt = c->bng_cpt && aligned && bs.lcell_words > 0 &&
                               (int64_t)ch->bng_ne * ch->bng_nn < ((int64_t)1 << 24) && shm_b + cpt_bytes <= kStreamLdsMax;
             if (bcpt) shm_b += cpt_bytes;
             auto kernel_for = [&](bool vec) -> const void* {
-                return stream_kernel_bng(lds, pairs, vec, bpipe, bcpt);
+                return stream_kernel_bng(lds, pairs, vec, bcpt);
             };
-            c->last_kernel = bcpt ? "k_join_stream_bng_cpt" : (bpipe ? "k_join_stream_bng_pipe" : "k_join_stream_bng");
+            c->last_kernel = bcpt ? "k_join_stream_bng_cpt" : "k_join_stream_bng";
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blkb, shm_b) != hipSuccess || per_cu < 1)
                 per_cu = 1;
@@ -3777,11 +3826,17 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             }
             tstop = nullptr;  // recorded after the first stream launch
         } else if (binned_used) {
-            c->last_kernel = "k_join_binned";
+            c->last_kernel = (c->tile_images && ch->img_words.p) ? "k_join_tiles" : "k_join_binned";
             const uint32_t max_code = (uint32_t)ch->tile_stats[2] + 1u;
             for (int64_t lo = 0; lo < n; lo += c->bin_chunk) {
                 const int64_t hi = std::min<int64_t>(n, lo + c->bin_chunk);
-                hipError_t e = binned::join(a, lo, hi, max_code, lds && !pairs, c->n_cu, c->bins, c->stream);
+                binned::Images img;
+                if (c->tile_images && ch->img_words.p) {
+                    img.words = (const uint32_t*)ch->img_words.p;
+                    img.off = (const uint32_t*)ch->img_off.p;
+                    img.max_words = ch->img_max_words;
+                }
+                hipError_t e = binned::join(a, lo, hi, max_code, lds && !pairs, c->n_cu, img, c->bins, c->stream);
                 if (e == hipErrorOutOfMemory) return fail(MOSAIC_E_NOMEM, "binned join: device allocation failed");
                 if (e != hipSuccess) return fail(MOSAIC_E_HIP, std::string("binned join: ") + hipGetErrorString(e));
                 // this chunk's exact-H3 rows, before the next chunk reuses the sorted buffers
@@ -4202,6 +4257,39 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
     if (h3g) hipLaunchKernelGGL(k_h3_kring, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
     else hipLaunchKernelGGL(k_bng_kring, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
+    if (h3g) {
+        // rows where H3 meets a pentagon (count -3): H3's fallback search, with scratch per row
+        std::vector<int32_t> cnt((size_t)n);
+        HIP_TRY(hipMemcpyAsync(cnt.data(), a.count, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        std::vector<int64_t> rows;
+        for (int64_t i = 0; i < n; i++)
+            if (cnt[(size_t)i] == -3) rows.push_back(i);
+        if (!rows.empty()) {
+            if (k > h3nb::kSlowMaxK)
+                return done(fail(MOSAIC_E_ARG, "H3 k-ring with k > " + std::to_string(h3nb::kSlowMaxK) +
+                                                   " around a pentagon is not supported"));
+            const int64_t m = h3nb::max_kring_size(k), m1 = k ? h3nb::max_kring_size(k - 1) : 1;
+            const int64_t per = std::max<int64_t>(1, ((int64_t)1 << 30) / ((m + m1) * 8 + m * 4));
+            DevBuf s_rows, s_tab, s_dist;
+            auto done2 = [&](int r2) {
+                for (DevBuf* b : {&s_rows, &s_tab, &s_dist}) b->release();
+                return done(r2);
+            };
+            for (size_t r0 = 0; r0 < rows.size(); r0 += (size_t)per) {
+                const int64_t nr = std::min<int64_t>(per, (int64_t)(rows.size() - r0));
+                if ((rc = s_rows.reserve((size_t)nr * 8)) || (rc = s_tab.reserve((size_t)(nr * (m + m1)) * 8)) ||
+                    (rc = s_dist.reserve((size_t)(nr * m) * 4)))
+                    return done2(rc);
+                HIP_TRY(hipMemcpyAsync(s_rows.p, rows.data() + r0, (size_t)nr * 8, hipMemcpyHostToDevice, c->stream));
+                hipLaunchKernelGGL(k_h3_kring_slow, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, c->stream, a,
+                                   (const int64_t*)s_rows.p, nr, (int64_t*)s_tab.p, m + m1, (int32_t*)s_dist.p, m);
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipStreamSynchronize(c->stream));
+            }
+            for (DevBuf* b : {&s_rows, &s_tab, &s_dist}) b->release();
+        }
+    }
     unsigned int flags = 0;
     HIP_TRY(hipMemcpyAsync(&flags, s_flags.p, 4, hipMemcpyDeviceToHost, c->stream));
     if (!dev_out && slots > 0)

@@ -517,33 +517,49 @@ void oracle_h3_to_geo(int64_t h3, double* lat, double* lon) {
     hex2d_to_geo(i - 0.5 * j, j * M_SQRT3_2_L, f.face, get_res((uint64_t)h3), 0, lat, lon);
 }
 
-/* neighbours of h (sphere search): out[0..n), n <= 12 */
+int oracle_h3_to_geo_boundary(int64_t h3, double* out);
+
+/* neighbours of h (sphere search): the cells just beyond the midpoint of every edge of h's boundary
+ * (h3ToGeoBoundary, Class III distortion vertices included), found with geoToH3 -- exact for
+ * hexagons and pentagons alike, independent of H3's neighbour tables.  out[0..n), n <= 12 */
 static int oracle_h3_neighbors(uint64_t h, uint64_t* out) {
     int res = get_res(h), n = 0;
-    double lat, lon;
+    double lat, lon, b[20];
     oracle_h3_to_geo((int64_t)h, &lat, &lon);
-    double step = 0.02;
-    for (int q = 0; q < res; q++) step /= 2.6457513110645906;
-    for (int d = 0; d < 48; d++) {
-        double az = (d + 0.37) * (2 * M_PI / 48), lo = 0, hi = step, la, ln;
-        for (int it = 0; it < 60; it++) {
-            geo_az_distance(lat, lon, az, hi, &la, &ln);
-            if ((uint64_t)oracle_h3_geo_to_h3(la, ln, res) != h) break;
-            lo = hi;
-            hi *= 1.5;
+    const int nv = oracle_h3_to_geo_boundary((int64_t)h, b);
+    double c[3] = {cos(lat) * cos(lon), cos(lat) * sin(lon), sin(lat)};
+    for (int v = 0; v < nv; v++) {
+        const int w = (v + 1) % nv;
+        double p[3] = {cos(b[2 * v]) * cos(b[2 * v + 1]), cos(b[2 * v]) * sin(b[2 * v + 1]), sin(b[2 * v])};
+        double q[3] = {cos(b[2 * w]) * cos(b[2 * w + 1]), cos(b[2 * w]) * sin(b[2 * w + 1]), sin(b[2 * w])};
+        double m[3], e = 0, mn = 0;
+        for (int a = 0; a < 3; a++) {
+            m[a] = 0.5 * (p[a] + q[a]);
+            e += (p[a] - q[a]) * (p[a] - q[a]);
         }
-        for (int it = 0; it < 60; it++) {
-            double mid = 0.5 * (lo + hi);
-            geo_az_distance(lat, lon, az, mid, &la, &ln);
-            if ((uint64_t)oracle_h3_geo_to_h3(la, ln, res) == h) lo = mid;
-            else hi = mid;
+        for (int a = 0; a < 3; a++) mn += m[a] * m[a];
+        mn = sqrt(mn);
+        e = sqrt(e);
+        /* beyond the edge midpoint, away from the centre, by 2 % of the edge length */
+        double d[3], dn = 0;
+        for (int a = 0; a < 3; a++) {
+            m[a] /= mn;
+            d[a] = m[a] - c[a];
         }
-        geo_az_distance(lat, lon, az, hi * 1.3, &la, &ln);
-        uint64_t c = (uint64_t)oracle_h3_geo_to_h3(la, ln, res);
-        if (c == h || c == 0) continue;
+        for (int a = 0; a < 3; a++) dn += d[a] * d[a];
+        dn = sqrt(dn);
+        double t[3], tn = 0;
+        for (int a = 0; a < 3; a++) {
+            t[a] = m[a] + 0.02 * e * d[a] / dn;
+            tn += t[a] * t[a];
+        }
+        tn = sqrt(tn);
+        const double la = asin(t[2] / tn), ln = atan2(t[1], t[0]);
+        uint64_t cell = (uint64_t)oracle_h3_geo_to_h3(la, ln, res);
+        if (cell == h || cell == 0) continue;
         int seen = 0;
-        for (int m = 0; m < n; m++) seen |= out[m] == c;
-        if (!seen && n < 12) out[n++] = c;
+        for (int k = 0; k < n; k++) seen |= out[k] == cell;
+        if (!seen && n < 12) out[n++] = cell;
     }
     return n;
 }

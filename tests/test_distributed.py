@@ -73,3 +73,49 @@ def test_gloo_world2_sharded_join_equals_single_process():
     assert got == want
     assert elapsed == 2.0  # max over ranks
     assert shard == 20_000
+
+
+class _HostTessellator:
+    """Stands in for the GPU context in bench.build_chips on CPU: the host producer."""
+
+    def grid_tessellateexplode(self, zones, res):
+        from mosaic_amd.context import tessellate
+
+        return tessellate("H3", zones, res)
+
+
+def _bench_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from mosaic_amd import distributed as D
+
+    D.init("gloo")
+    # only rank 0 may tessellate: the other ranks get the chip rows over the process group
+    ctx = _HostTessellator() if rank == 0 else None
+    zones, chips, _ = bench.build_chips(ctx, 9, rank, world)
+    offs, data = chips["wkb"]
+    q.put((rank, len(zones), chips["index_id"].tobytes(), chips["is_core"].tobytes(),
+           chips["polygon_key"].tobytes(), bytes(np.asarray(offs).tobytes()), bytes(np.asarray(data).tobytes())))
+    D.finalize()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_bench_chip_broadcast():
+    """bench.py's multi-rank build: rank 0 tessellates the 263 zones and
+    broadcasts the chip set; every rank ends with identical chip rows (ids, is_core, keys, WKB)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=240), q.get(timeout=240)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1]
+    assert got[0][0] == 263 and len(got[0][1]) > 8 * 10_000

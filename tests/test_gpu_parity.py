@@ -493,13 +493,14 @@ def test_join_bng_dense_table(bngctx, res, every):
         assert np.array_equal(bngctx.pip_join_count(table, x, y), want)
     finally:
         bngctx.set_option("tiles", 1)
-    bngctx.set_option("bng_pipe", 1)  # the software-pipelined BNG stream kernel (not the default)
+    bngctx.set_option("bng_cpt", 0)  # the uncompacted BNG stream kernel (not the default)
     try:
         assert np.array_equal(bngctx.pip_join_count(table, x, y), want)
+        assert bngctx.last_kernel() == "k_join_stream_bng"
         r1, k1 = bngctx.pip_join_pairs(table, x, y)
         assert np.array_equal(np.sort(r1 * len(ids) + k1), np.sort(rows * len(ids) + keys))
     finally:
-        bngctx.set_option("bng_pipe", 0)
+        bngctx.set_option("bng_cpt", 1)
     bngctx.set_option("point_raster", 0)  # dense cell table without the border-cell leaf blocks
     try:
         t2 = bngctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], res,

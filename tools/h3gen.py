@@ -418,6 +418,14 @@ def main(out_path):
         for f in around:
             r = 0
             cur, idx = hface, i0
+            if cw[0] >= 0 and order[(i0 - step) % 5] == f:
+                # the face next to the home face across the pentagon's deleted k sector: its frame
+                # is one edge crossing from the home face's, not four around the vertex (fixed by
+                # H3's round trip geoToH3(h3ToGeo(h)) == h over every cell of the base cell,
+                # tools/probes/pent_rot_probe.cpp; the four-step path overshoots by the vertex's
+                # 60-degree deficit)
+                r = rot_between(f, hface)
+                cur = f
             while cur != f:
                 idx = (idx + step) % 5
                 nxt = order[idx]
