@@ -195,22 +195,7 @@ static const int kCptBufWords = 192;
 static const uint32_t kNoLoad = 0x7ffffff0u;  // out-of-range buffer offset (every table is < 2 GiB)
 // cache-policy bits (aux) of the stream kernels' gathers: sub-block entries, line records, leaf
 // codes, BNG sub-cell entries (build-time A/B knobs; 2 = nt)
-#ifndef MOSAIC_AUX_SUB
-#define MOSAIC_AUX_SUB 0
-#endif
-#ifndef MOSAIC_AUX_LINE
-#define MOSAIC_AUX_LINE 0
-#endif
-#ifndef MOSAIC_AUX_LEAF
-#define MOSAIC_AUX_LEAF 0
-#endif
-#ifndef MOSAIC_AUX_BNG
-#define MOSAIC_AUX_BNG 0
-#endif
 // k_join_stream_pipe: groups of coordinates in flight ahead of the one being looked up (1 or 2)
-#ifndef MOSAIC_PIPE_DEPTH
-#define MOSAIC_PIPE_DEPTH 1
-#endif
 
 typedef double v2d __attribute__((ext_vector_type(2)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));

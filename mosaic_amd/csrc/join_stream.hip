@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         for (int k = 0; k < 4; k++) {
             const uint32_t local = (((iyC[k] >> s.cs) & qm) << s.qs) | ((ixC[k] >> s.cs) & qm);
             const uint32_t off = ((((qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
-            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, qv[k] >= 0x8000u ? off : kNoLoad, 0, MOSAIC_AUX_SUB);
+            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rsub, qv[k] >= 0x8000u ? off : kNoLoad, 0, 0);
         }
         // stage C: leaf codes and line records of the points in mixed sub-blocks
         uint32_t leaf[4];
@@ -165,30 +165,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 }
 
 
-// measurement builds only (tools/ab_build.sh): MOSAIC_ABL 1 drops every lookup (coordinates ->
-// fine cell -> count), 2 keeps the LDS levels but no gathers, 3 adds the sub-block gathers, 4 is
-// the full kernel without the LDS count atomics.  Answers are wrong in ablation builds.
-#ifndef MOSAIC_ABL
-#define MOSAIC_ABL 0
-#endif
-
-// Gathers of the pipelined stream kernel, only by the lanes that need one (exec-masked; a wave with
+// Gathers of the pipelined stream kernels, only by the lanes that need one (exec-masked; a wave with
 // no such lane skips the instruction).  Measured against passing an out-of-range offset from the
-// other lanes (branch-free; MOSAIC_GATHER_MODE 0) and against that plus a wave-uniform skip (1):
-// C2 stream 3.47 / 3.52 -> 3.40 ms (profiles/r03_kbench_gather_modes.txt) -- the texture units
-// and the data return path do no work for inactive lanes.
-#ifndef MOSAIC_GATHER_MODE
-#define MOSAIC_GATHER_MODE 2
-#endif
+// other lanes (branch-free) and against that plus a wave-uniform skip: C2 stream 3.47 / 3.52 ->
+// 3.40 ms (profiles/r03_kbench_gather_modes.txt) -- the texture units and the data return path do
+// no work for inactive lanes.
 template <int aux>
 __device__ inline uint32_t gather_b16(__amdgpu_buffer_rsrc_t r, bool need, uint32_t off) {
-    if (MOSAIC_GATHER_MODE == 2) {
-        uint32_t v = 0u;
-        if (need) v = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, aux);
-        return v;
-    }
-    if (MOSAIC_GATHER_MODE == 1 && !__ballot(need)) return 0u;
-    return __builtin_amdgcn_raw_buffer_load_b16(r, need ? off : kNoLoad, 0, aux);
+    uint32_t v = 0u;
+    if (need) v = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, aux);
+    return v;
 }
 __device__ inline uint32_t gather_b32(__amdgpu_buffer_rsrc_t r, bool need, uint32_t off) {
     uint32_t v = 0u;
@@ -197,13 +183,9 @@ __device__ inline uint32_t gather_b32(__amdgpu_buffer_rsrc_t r, bool need, uint3
 }
 template <int aux>
 __device__ inline v4u gather_b128(__amdgpu_buffer_rsrc_t r, bool need, uint32_t off) {
-    if (MOSAIC_GATHER_MODE == 2) {
-        v4u v = {0u, 0u, 0u, 0u};
-        if (need) v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, aux);
-        return v;
-    }
-    if (MOSAIC_GATHER_MODE == 1 && !__ballot(need)) return v4u{0u, 0u, 0u, 0u};
-    return __builtin_amdgcn_raw_buffer_load_b128(r, need ? off : kNoLoad, 0, aux);
+    v4u v = {0u, 0u, 0u, 0u};
+    if (need) v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, aux);
+    return v;
 }
 
 // ---- k_join_stream_pipe: k_join_stream's per-point computation as a three-stage software
@@ -214,25 +196,12 @@ __device__ inline v4u gather_b128(__amdgpu_buffer_rsrc_t r, bool need, uint32_t 
 // t + 1's coordinates -- issued in that order, so every wait is on the oldest loads in flight
 // (vector-memory returns retire in order per wave).  Needs 16-byte aligned columns, tile_base in
 // LDS and at least one full group; the wave's last partial group runs unpipelined.  Same answers
-// as k_join_stream, point for point.
-// MOSAIC_FIXED 1 (default): fine-cell coordinates in fixed point (tiles::raster_code_fixed) -- one
-// f64 fma, one saturating conversion and an integer clamp per axis, every index a bit-field of the
-// result; 0: the f64 clamp / floor / fract form (tiles::raster_code; measurement builds)
-#ifndef MOSAIC_FIXED
-#define MOSAIC_FIXED 1
-#endif
-// MOSAIC_LATE_ISSUE 1: every gather issued at the end of the iteration (see issue_leaf); measured
-// slower (C2 stream 3.33 -> 3.47 ms, profiles/r03_kbench_late_issue.txt), kept for measurement builds
-#ifndef MOSAIC_LATE_ISSUE
-#define MOSAIC_LATE_ISSUE 0
-#endif
+// as k_join_stream, point for point.  Fine-cell coordinates in fixed point
+// (tiles::raster_code_fixed): one f64 fma, one saturating conversion and an integer clamp per axis,
+// every index a bit-field of the result.  The pipe kernel serves the rasters k_join_stream_cpt
+// cannot take (cs + qs > 8, more than 65,536 tiles, no LDS room for the compaction buffers).
 struct PipeGroup {
-#if MOSAIC_FIXED
     uint32_t gx[4], gy[4];  // fixed-point fine-cell coordinates (kFixBits fraction bits)
-#else
-    float u[4], v[4];     // offset in the sub-block, leaf cells
-    uint32_t lf[4];       // leaf cell index within the leaf block
-#endif
     uint32_t tbv[4];      // tile base
     uint32_t qv[4];       // quad-level entry
     uint32_t code[4];     // sub-block entry (gathered), then the answer
@@ -257,7 +226,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint16_t* quad = (const uint16_t*)quadw;
     uint32_t* qmask = quadw + s.n_quad_words;
     const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
-    uint32_t abl_acc = 0;  // (MOSAIC_ABL 4)
     lds_fill(quadw, s.quad, s.n_quad_words);
     lds_fill(qmask, s.qrec, s.n_qrec_words);
     lds_fill(tb, s.tile_base, s.n_tiles);
@@ -283,49 +251,23 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const bool lv = valid && live[k];
-#if MOSAIC_FIXED
             // fixed point (tiles::raster_code_fixed): saturating conversion (negative, NaN -> 0), clamp
             const uint32_t ixC = min(tiles::fix_cvt(fma(x[k], s.sxF, s.gx0F)), (uint32_t)s.gxmaxF);
             const uint32_t iyC = min(tiles::fix_cvt(fma(y[k], s.syF, s.gy0F)), (uint32_t)s.gymaxF);
             g.gx[k] = ixC;
             g.gy[k] = iyC;
             constexpr int SH0 = tiles::kFixBits;
-#else
-            constexpr int SH0 = 0;
-            // (x - x0) sxC as one fma (x sxC - x0 sxC): within the raster's 1e-6-cell widening
-            const double gx = fmin(fmax(fma(x[k], s.sxC, gx0), 0.0), s.gxmax);  // NaN -> 0
-            const double gy = fmin(fmax(fma(y[k], s.syC, gy0), 0.0), s.gymax);
-            const uint32_t ixC = (uint32_t)(int)gx, iyC = (uint32_t)(int)gy;
-            // the offset in the sub-block, leaf cells: (ixC & cm) + fract(gx) (gx >= 0)
-            g.u[k] = (float)(ixC & cm) + (float)__builtin_amdgcn_fract(gx);
-            g.v[k] = (float)(iyC & cm) + (float)__builtin_amdgcn_fract(gy);
-            g.lf[k] = ((iyC & cm) << s.cs) | (ixC & cm);
-#endif
-#if MOSAIC_ABL == 1
-            const uint32_t q = (ixC ^ iyC) & 7u;  // ablation: no LDS lookups
-#else
             const uint32_t q = quad_lookup<SH0>(s, quad, qmask, qcode, ixC, iyC);
-#endif
             // dead rows answer 0.  Non-finite coordinates need no test: fmax / fmin clamp them onto
             // the grid's edge ring, whose sub-blocks are all 0 or kMixed (PointRaster edge_ok, a
             // precondition of this kernel), and a non-finite point joins nothing in the reference
             // (geoToH3 gives H3_NULL) -- 0 is its answer, kMixed sends it to the exact path.
             g.qv[k] = lv ? q : 0u;
-#if MOSAIC_ABL == 1
-            g.tbv[k] = ixC;
-#else
             g.tbv[k] = tb[__umul24(iyC >> (s.tsh + SH0), (uint32_t)s.tnx) + (ixC >> (s.tsh + SH0))];
-#endif
             const uint32_t local = (__builtin_amdgcn_ubfe(iyC, (uint32_t)(s.cs + SH0), (uint32_t)s.qs) << s.qs) |
                                    __builtin_amdgcn_ubfe(ixC, (uint32_t)(s.cs + SH0), (uint32_t)s.qs);
             const uint32_t off = ((((g.qv[k] & 0x7fffu) << (2 * s.qs)) + local) << 1);
-#if MOSAIC_ABL == 1 || MOSAIC_ABL == 2
-            g.code[k] = off & 1u;  // ablation: no sub-block gathers
-#elif MOSAIC_LATE_ISSUE
-            g.code[k] = g.qv[k] >= 0x8000u ? off : kNoLoad;  // gathered by issue_gathers
-#else
-            g.code[k] = gather_b16<MOSAIC_AUX_SUB>(rsub, g.qv[k] >= 0x8000u, off);
-#endif
+            g.code[k] = gather_b16<0>(rsub, g.qv[k] >= 0x8000u, off);
         }
     };
     // stage B: sub-block entries -> leaf and line gathers
@@ -336,24 +278,12 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const bool blk = c - 0x8000u < 0x7fffu;  // kSubBlock | n, not kMixed
             const bool line = blk && (c & 0x4000u);
             const uint32_t n = c & 0x3fffu;
-#if MOSAIC_FIXED
             const uint32_t lf = (__builtin_amdgcn_ubfe(g.gy[k], (uint32_t)tiles::kFixBits, (uint32_t)s.cs) << s.cs) |
                                 __builtin_amdgcn_ubfe(g.gx[k], (uint32_t)tiles::kFixBits, (uint32_t)s.cs);
-#else
-            const uint32_t lf = g.lf[k];
-#endif
             const uint32_t loff = (g.tbv[k] + (n << (2 * s.cs)) + lf) << 1;
             const uint32_t roff = (g.tbv[k] - 8u * (n + 1u)) << 1;
-#if MOSAIC_ABL >= 1 && MOSAIC_ABL <= 3
-            g.leaf[k] = loff & 1u;  // ablation: no leaf / line gathers
-            g.lrec[k] = v4u{roff, loff, 0u, 0u};
-#elif MOSAIC_LATE_ISSUE
-            g.leaf[k] = blk && !line ? loff : kNoLoad;  // gathered by issue_gathers
-            g.lrec[k].x = line ? roff : kNoLoad;
-#else
-            g.leaf[k] = gather_b16<MOSAIC_AUX_LEAF>(rblk, blk && !line, loff);
-            g.lrec[k] = gather_b128<MOSAIC_AUX_LINE>(rblk, line, roff);
-#endif
+            g.leaf[k] = gather_b16<0>(rblk, blk && !line, loff);
+            g.lrec[k] = gather_b128<0>(rblk, line, roff);
             // for stage D: kPipeLine for a line row, else the code to OR with the gathered leaf code
             // (0 for leaf rows; out-of-range gathers return 0)
             g.code[k] = line ? kPipeLine : (blk ? 0u : c);
@@ -364,14 +294,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         uint32_t code[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-#if MOSAIC_FIXED
             // the offset in the sub-block, leaf cells, truncated to 2^-kFixBits (exact in f32)
             const uint32_t fb = (uint32_t)(s.cs + tiles::kFixBits);
             const float u = (float)__builtin_amdgcn_ubfe(g.gx[k], 0u, fb) * (1.0f / (float)(1 << tiles::kFixBits));
             const float v = (float)__builtin_amdgcn_ubfe(g.gy[k], 0u, fb) * (1.0f / (float)(1 << tiles::kFixBits));
-#else
-            const float u = g.u[k], v = g.v[k];
-#endif
             const float sv = fmaf(__uint_as_float(g.lrec[k].x), u,
                                   fmaf(__uint_as_float(g.lrec[k].y), v, __uint_as_float(g.lrec[k].z)));
             const uint32_t pos = g.lrec[k].w & 0xffffu, neg = g.lrec[k].w >> 16;
@@ -389,11 +315,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
                 // keys are < n_polygons <= 8192; 0 (no pair) wraps to 0xffffffff and kMixed / non-finite
                 // codes are >= kPipeNonFinite: both land on the lane's spill word
                 const uint32_t slot = min(code[k] - 1u, spill);
-#if MOSAIC_ABL == 4
-                abl_acc += slot;  // ablation: no LDS count atomics
-#else
                 atomicAdd(&lds[slot], 1u);
-#endif
             } else if (code[k] - 1u < kPipeNonFinite - 1u) {
                 emit_hit<LDS_COUNTS, PAIRS>(a, row_of(wb, k), code[k] - 1u, lds);
             }
@@ -410,7 +332,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             }
         }
     };
-    // coordinates of the next MOSAIC_PIPE_DEPTH groups (1: loaded one iteration ahead; 2: two)
+    // coordinates of the next group (loaded one iteration ahead; two ahead measured slower:
+    // registers, profiles/r03_kbench_pipe_depth.txt)
     struct Coords {
         v2d px[2], py[2];
     };
@@ -430,38 +353,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         g0.qv[k] = g1.qv[k] = 0u;
         g0.code[k] = g1.code[k] = 0u;
         g0.tbv[k] = g1.tbv[k] = 0u;
-#if MOSAIC_FIXED
         g0.gx[k] = g1.gx[k] = g0.gy[k] = g1.gy[k] = 0u;
-#else
-        g0.lf[k] = g1.lf[k] = 0u;
-        g0.u[k] = g1.u[k] = g0.v[k] = g1.v[k] = 0.0f;
-#endif
     }
-    // MOSAIC_LATE_ISSUE: stages B and A only compute their gather offsets (kNoLoad: none); the
-    // gathers of both are issued here, after every wait of the iteration.  A gather issued only by
-    // the lanes that need it is a branch, so the compiler cannot count it in vmcnt: any wait placed
-    // after one becomes vmcnt(0).  Issued in the middle of the iteration (stage B before stage A),
-    // the leaf / line gathers were waited for by stage A's wait on the coordinates, i.e. they had no
-    // latency budget at all; issued last, every load has the whole next iteration's latency budget.
-    auto issue_leaf = [&](PipeGroup& g) {
-#if MOSAIC_LATE_ISSUE && MOSAIC_ABL == 0
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t lo = g.leaf[k], ro = g.lrec[k].x;
-            g.leaf[k] = gather_b16<MOSAIC_AUX_LEAF>(rblk, lo != kNoLoad, lo);
-            g.lrec[k] = gather_b128<MOSAIC_AUX_LINE>(rblk, ro != kNoLoad, ro);
-        }
-#endif
-    };
-    auto issue_sub = [&](PipeGroup& g) {
-#if MOSAIC_LATE_ISSUE && MOSAIC_ABL == 0
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t so = g.code[k];
-            g.code[k] = gather_b16<MOSAIC_AUX_SUB>(rsub, so != kNoLoad, so);
-        }
-#endif
-    };
     // VALID: group t is a full group of this wave (t < T) -- a compile-time constant, so the main loop
     // carries no per-point validity test (only the two drain steps run with VALID false)
     auto step = [&](auto VALID, int64_t t, PipeGroup& gfin, PipeGroup& gadv, Coords& cb, Coords& cn) {
@@ -471,14 +364,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
         const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
         stage_a(x, y, all, decltype(VALID)::value, gfin);
-        issue_leaf(gadv);
-        issue_sub(gfin);
-        if (MOSAIC_PIPE_DEPTH == 2) load4(cb, wbase + (t + 2) * stride, t + 2 < T);  // cb is free again
-        else load4(cn, wbase + (t + 1) * stride, t + 1 < T);
+        load4(cn, wbase + (t + 1) * stride, t + 1 < T);
     };
     if (T > 0) {
         load4(cb0, wbase, true);
-        if (MOSAIC_PIPE_DEPTH == 2) load4(cb1, wbase + stride, 1 < T);
         const std::true_type full;
         const std::false_type drain;
         int64_t t = 0;
@@ -510,12 +399,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         }
         PipeGroup g;
         stage_a(x, y, live, true, g);
-        issue_sub(g);
         stage_b(g);
-        issue_leaf(g);
         stage_d(g, wt);
     }
-    if (MOSAIC_ABL == 4 && abl_acc == 0xdeadbeefu) lds[0] = 1u;
     stage_flush(a, wq, wn, lane, 1);
     if (LDS_COUNTS) {
         __syncthreads();
@@ -541,13 +427,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 // sub-block within the quad; L <= 20), the source lane and row slot, the quad entry and the tile.
 // Same answers as k_join_stream_pipe, point for point.
 // 1: a group's second set of pending rows (65 - 128) is pipelined like the first
-#ifndef MOSAIC_CPT_TWO
-#define MOSAIC_CPT_TWO 1
-#endif
 // 1: compaction through a per-wave LDS buffer; 0: ds_permute (no LDS memory)
-#ifndef MOSAIC_CPT_LDS
-#define MOSAIC_CPT_LDS 1
-#endif
 struct CptSet {
     uint32_t a;     // ix low bits | source lane << 20 | row slot k << 26
     uint32_t b;     // iy low bits
@@ -563,7 +443,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const int nwaves = (int)(blockDim.x >> 6);
     const int ncw = LDS_COUNTS ? a.n_polygons + 64 : 0;
     uint32_t* stage = lds + ncw;
-    // per-wave compaction buffers (MOSAIC_CPT_LDS): 64 slots x 3 words, structure of arrays
+    // per-wave compaction buffers: 64 slots x 3 words, structure of arrays
     uint32_t* cbuf_all = stage + nwaves * s.stage_words;
     uint32_t* tb = cbuf_all + nwaves * kCptBufWords;
     uint32_t* quadw = tb + s.n_tiles;
@@ -610,7 +490,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         const uint32_t q = z.c & 0xffffu;
         const uint32_t local = (__builtin_amdgcn_ubfe(z.b, cs + F, qs) << qs) | __builtin_amdgcn_ubfe(z.a, cs + F, qs);
         const uint32_t off = (((q & 0x7fffu) << (2 * qs)) + local) << 1;
-        z.code = gather_b16<MOSAIC_AUX_SUB>(rsub, q >= 0x8000u, off);
+        z.code = gather_b16<0>(rsub, q >= 0x8000u, off);
     };
     // B: sub-block entry -> leaf / line gather
     auto set_b = [&](CptSet& z) {
@@ -623,8 +503,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         const uint32_t tbv = tb[z.c >> 16];
         const uint32_t loff = (tbv + (n << (2 * cs)) + lf) << 1;
         const uint32_t roff = (tbv - 8u * (n + 1u)) << 1;
-        z.leaf = gather_b16<MOSAIC_AUX_LEAF>(rblk, blk && !line, loff);
-        z.lrec = gather_b128<MOSAIC_AUX_LINE>(rblk, line, roff);
+        z.leaf = gather_b16<0>(rblk, blk && !line, loff);
+        z.lrec = gather_b128<0>(rblk, line, roff);
         z.code = line ? kPipeLine : (blk ? 0u : c);
     };
     // D: answers of the set's rows (group base wb)
@@ -670,7 +550,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             fb[k] = iyC & lowm;
             fc[k] = q | (tile << 16);
         }
-#if MOSAIC_CPT_LDS
         // compaction through the wave's LDS buffer: row slot k's pending rows take set slots base_k ..
         // base_k + n_k - 1; the rows of set sv (slots 64 sv .. 64 sv + 63) are stored, then read back
         // one per lane
@@ -701,47 +580,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             o.c = ok ? cbuf[128 + lane] : 0u;
             __builtin_amdgcn_wave_barrier();
         };
-#else
-        // compaction: row slot k's pending rows go to set slots base_k .. base_k + n_k - 1 (lane =
-        // slot mod 64), its other rows behind them (a rotation of the stable partition: a permutation)
-        uint32_t va[4], vb[4], vc[4], bases[4];
-        uint32_t base = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const unsigned long long m = __ballot(pend[k]);
-            const uint32_t n = (uint32_t)__popcll(m);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            // (a select written as bit operations: pending iff bit 15 of the quad entry, a u16)
-            const uint32_t alt = n + ((uint32_t)lane - rank), pm = 0u - ((fc[k] >> 15) & 1u);
-            const uint32_t dst = ((base + (alt ^ ((rank ^ alt) & pm))) & 63u) << 2;
-            va[k] = (uint32_t)__builtin_amdgcn_ds_permute((int)dst, (int)fa[k]);
-            vb[k] = (uint32_t)__builtin_amdgcn_ds_permute((int)dst, (int)fb[k]);
-            vc[k] = (uint32_t)__builtin_amdgcn_ds_permute((int)dst, (int)fc[k]);
-            bases[k] = base;
-            base += n;
-        }
-        const uint32_t P = base;  // pending rows of the group (wave-uniform)
-        // set sv (slots 64 sv .. 64 sv + 63): lane j takes slot 64 sv + j from the row slot whose range holds it
-        auto gather_set = [&](uint32_t sv, CptSet& o) {
-            const uint32_t slot = 64u * sv + (uint32_t)lane;
-            uint32_t ra = va[0], rb = vb[0], rc = vc[0];
-#pragma unroll
-            for (int k = 1; k < 4; k++) {
-                const bool tk = slot >= bases[k];
-                ra = tk ? va[k] : ra;
-                rb = tk ? vb[k] : rb;
-                rc = tk ? vc[k] : rc;
-            }
-            const bool ok = slot < P;  // empty slots: quad entry 0, answer 0 (the spill word)
-            o.a = ok ? ra : 0u;
-            o.b = ok ? rb : 0u;
-            o.c = ok ? rc : 0u;
-        };
-#endif
         gather_set(0u, z);
         set_a(z);
-        // a second set (65 - 128 pending rows, clustered input) is pipelined too (MOSAIC_CPT_TWO)
-        two = MOSAIC_CPT_TWO && P > 64u;
+        // a second set (65 - 128 pending rows, clustered input) is pipelined too
+        two = P > 64u;
         if (two) {
             gather_set(1u, z2);
             set_a(z2);
@@ -935,7 +777,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         for (int k = 0; k < 4; k++) {
             leafc[k] = (e[k] & (kBngPure | kBngLeaf)) == kBngLeaf;
             const uint32_t off = ((e[k] & ~kBngLeaf) + loff[k]) << 1;
-            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rleaf, leafc[k] ? off : kNoLoad, 0, MOSAIC_AUX_BNG);
+            code[k] = __builtin_amdgcn_raw_buffer_load_b16(rleaf, leafc[k] ? off : kNoLoad, 0, 0);
         }
         v4u lrec[4];
 #pragma unroll
@@ -1069,7 +911,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         base = e & ~kBngLeaf;
         float su, sv;
         const uint32_t q = subcell(z, &su, &sv);
-        z.e = gather_b16<MOSAIC_AUX_BNG>(rleaf, leafc, (base + q) << 1);
+        z.e = gather_b16<0>(rleaf, leafc, (base + q) << 1);
         z.p = z.p == 0u ? 0u : ((e & kBngPure) ? (e & ~kBngPure) : (leafc ? kBngLeaf : (e ? (uint32_t)tiles::kMixed : 0u)));
     };
     // C': sub-cell code -> line-record gather

@@ -1317,25 +1317,8 @@ __global__ void __launch_bounds__(256) k_join_mixed_bng(JoinArgs a) {
 // window entries, hash entries -- R independent chains in flight per lane instead of one), then the
 // raster chip loop runs once per row slot (wave-cooperative, so wave-uniform).  Rows the fast path
 // cannot certify, kFull tiles and window misses take tiled_cell (the generic path).
-#ifndef MOSAIC_MIXED_WPE
-#define MOSAIC_MIXED_WPE 4
-#endif
-// measurement build only (-DMOSAIC_MIXED_TRACE): per-wave phase timestamps of k_join_mixed
-#ifdef MOSAIC_MIXED_TRACE
-__device__ unsigned long long g_mtrace[16384 * 8];
-#define MTRACE(slot)                                                                       \
-    do {                                                                                   \
-        const unsigned wid_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);         \
-        if ((threadIdx.x & 63) == 0 && wid_ < 16384) g_mtrace[wid_ * 8 + (slot)] = wall_clock64(); \
-    } while (0)
-extern "C" int mosaic_debug_mtrace(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mtrace), sizeof(g_mtrace)) == hipSuccess ? 0 : -1;
-}
-#else
-#define MTRACE(slot)
-#endif
 template <bool LDS_COUNTS, bool PAIRS, int R>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOSAIC_MIXED_WPE))) k_join_mixed(JoinArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_join_mixed(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     __shared__ SlabItem items[4][16];
     counts_init<LDS_COUNTS>(a, lds);
@@ -1344,8 +1327,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOSAIC
     const int wv = (int)(threadIdx.x >> 6) & 3;
     const unsigned long long total = *a.mixq_count;
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x * R;
-    MTRACE(0);
-    int iters_ = 0;
     // wave-uniform loop: the wave's rows are [w0, w0 + 64 R), slot k of lane l is w0 + k * 64 + l
     for (unsigned long long w0 = ((unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * R; w0 < total;
          w0 += stride) {
@@ -1410,25 +1391,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOSAIC
                 tiled_cell(a, row[k], x[k], y[k], code[k], cur[k], end[k]);
             }
         }
-        if (iters_ == 0) MTRACE(1);
 #pragma unroll
         for (int k = 0; k < R; k++) {
             raster_chips<LDS_COUNTS, PAIRS>(a, live[k] ? row[k] : -1, cur[k], end[k], x[k], y[k], tests, lds, items[wv]);
-            if (iters_ == 0 && k < 2) MTRACE(2 + k);
         }
-        iters_++;
     }
-    MTRACE(4);
     counts_flush<LDS_COUNTS>(a, lds, tests);
-    MTRACE(5);
-#ifdef MOSAIC_MIXED_TRACE
-    if ((threadIdx.x & 63) == 0) {
-        const unsigned wid_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        if (wid_ < 16384) g_mtrace[wid_ * 8 + 6] = (unsigned long long)iters_;
-    }
-#else
-    (void)iters_;
-#endif
 }
 
 // Exact H3 for the queued rows (or for every row when all_rows is set: queue overflow fallback).

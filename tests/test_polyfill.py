@@ -71,22 +71,43 @@ def test_oracle_docs_example_res0():
     assert b.tolist() == [578360708396220415]
 
 
+PENTAGON_BASE_CELLS = (4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117)
+
+
+def pentagon_cell(bc, res):
+    h = (1 << 59) | (res << 52) | (bc << 45)
+    for r in range(res + 1, 16):
+        h |= 7 << (3 * (15 - r))
+    return h
+
+
 def test_oracle_ring1_matches_sphere_kring():
     rng = np.random.default_rng(7)
-    pent = {4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117}
-    checked = 0
+    cells = []
     for _ in range(120):
         lat, lon = math.degrees(math.asin(rng.uniform(-1, 1))), rng.uniform(-180, 180)
         res = int(rng.integers(0, 13))
-        c = int(oracle.h3_point_to_index(np.array([lon]), np.array([lat]), res)[0])
-        if (c >> 45) & 127 in pent:
-            continue
-        want = set(int(k) for k in oracle.h3_kring_set(c, 1))
-        if any((k >> 45) & 127 in pent for k in want):
-            continue  # the sphere search overshoots around pentagons
-        assert set(oracle.h3_ring1(c).tolist()) == want
-        checked += 1
-    assert checked > 80
+        cells.append(int(oracle.h3_point_to_index(np.array([lon]), np.array([lat]), res)[0]))
+    for bc in PENTAGON_BASE_CELLS:
+        for res in (0, 2, 5):
+            cells += sorted(oracle.h3_kring_set(pentagon_cell(bc, res), 1))
+    for c in cells:
+        assert set(oracle.h3_ring1(c).tolist()) == set(int(k) for k in oracle.h3_kring_set(c, 1)), c
+
+
+def pentagon_polygons(radius_deg):
+    """an octagon around each pentagon's centre (degrees; lon spread by 1 / cos(lat))"""
+    out = []
+    for bc in PENTAGON_BASE_CELLS:
+        la, lo = (math.degrees(v) for v in oracle.h3_to_geo(pentagon_cell(bc, 0)))
+        ring = []
+        for i in range(8):
+            a = 2 * math.pi * (i + 0.3) / 8
+            x = lo + radius_deg * math.cos(a) / math.cos(math.radians(la))
+            ring.append((x if x <= 180 else x - 360, la + radius_deg * math.sin(a)))
+        ring.append(ring[0])
+        out.append((bc, ring))
+    return out
 
 
 def h3_inside(parts, lon, lat):
@@ -205,6 +226,21 @@ def test_kernel_code_on_host_matches_oracle(host_polyfill, res):
     assert n_ordered >= len(cases) // 4
 
 
+@pytest.mark.parametrize("res", [1, 2, 3, 4])
+def test_kernel_code_on_host_pentagons(host_polyfill, res):
+    """searches through the 12 pentagon base cells (H3's kRing falls back to _kRingInternal there):
+    the kernel's code on the host gives the oracle's set, and its order when collision-free"""
+    n_ordered = 0
+    for bc, ring in pentagon_polygons((12.0, 6.0, 3.0, 1.5)[res - 1]):
+        got = host_polyfill([ring], res)
+        want, cf = oracle.h3_polyfill_part([ring], res)
+        assert len(want) > 5 and pentagon_cell(bc, res) in set(want.tolist()), (bc, res)
+        assert sorted(got.tolist()) == sorted(want.tolist()), (bc, res)
+        if cf:
+            assert got.tolist() == want.tolist(), (bc, res)
+            n_ordered += 1
+
+
 # ---- GPU ----
 @pytest.fixture(scope="module")
 def h3ctx():
@@ -285,16 +321,21 @@ def test_gpu_large_res_and_global(h3ctx):
 
 
 @pytest.mark.gpu
-def test_gpu_pentagon_rows_unsupported(h3ctx):
-    """a search entering a pentagon base cell below res 0 is refused (status -2), never answered
-    approximately; at res 0 the geometric ring set answers it (same set as the oracle)"""
-    from mosaic_amd import MosaicError
+def test_gpu_pentagon_searches(h3ctx):
+    """searches entering pentagon base cells (africa at res 0-3, an octagon around each of the 12
+    pentagons at res 1-4): the oracle's sets, its order when collision-free"""
     africa = [(-17.0, 14.0), (10.0, 35.0), (32.0, 30.0), (51.0, 11.0), (40.0, -15.0), (20.0, -35.0),
               (12.0, -5.0), (-17.0, 14.0)]
     ps = polygon_set([[[africa]]])
-    _check_h3(h3ctx.grid_polyfill(ps, 0), ps, 0)
-    with pytest.raises(MosaicError):
-        h3ctx.grid_polyfill(ps, 2)
+    for res in (0, 1, 2, 3):
+        _check_h3(h3ctx.grid_polyfill(ps, res), ps, res)
+    for res in (1, 2, 3, 4):
+        rings = pentagon_polygons((12.0, 6.0, 3.0, 1.5)[res - 1])
+        ps = polygon_set([[[r]] for _, r in rings])
+        rows = h3ctx.grid_polyfill(ps, res)
+        _check_h3(rows, ps, res)
+        for (bc, _), row in zip(rings, rows):
+            assert pentagon_cell(bc, res) in set(row.tolist())
 
 
 @pytest.mark.gpu
