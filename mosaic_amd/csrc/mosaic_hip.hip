@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(256) k_join_tiled(JoinArgs a) {
 struct RBuildArgs {
     const tiles::TileRec* recs;
     const int32_t* tile_of_rec;
-    const double* rec_dev;
+    const tiles::TileCurv* rec_curv;
     const uint32_t* entries;  // tile-window entries: chip-hash slot + 1
     int32_t n_recs, tnx;
     double gx0, gy0, tw, th;
@@ -202,7 +202,8 @@ struct RBuildArgs {
 struct RTile {  // one tile record, as the builder's per-record lambda sees it
     int face, wa, wb, a0, b0;
     uint32_t off;
-    double lon0, lat0, dev, exd, eyd;
+    double lon0, lat0, exd, eyd;
+    tiles::TileCurv cv;
 };
 
 __device__ inline bool rtile_of(const RBuildArgs& a, int r, RTile& t) {
@@ -218,7 +219,7 @@ __device__ inline bool rtile_of(const RBuildArgs& a, int r, RTile& t) {
     t.off = tr.off;
     t.lon0 = a.gx0 + ti * a.tw;
     t.lat0 = a.gy0 + tj * a.th;
-    t.dev = a.rec_dev[r];
+    t.cv = a.rec_curv[r];
     const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
     t.exd = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
     t.eyd = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
@@ -278,11 +279,10 @@ __device__ inline int rhex_answer(const RBuildArgs& a, const RTile& t, int k, bo
 // with the sub-block's tolerance).
 __device__ inline uint16_t rclassify_rect(const RBuildArgs& a, const RTile& t, int i0, int j0, int i1, int j1,
                                           const rbuild::P2* q, const rbuild::P2* sq, double stol) {
-    const double frac = rbuild::dmax((double)(i1 - i0), (double)(j1 - j0)) / a.N;
-    const double tol = 4.0 * t.dev * frac * frac + 1e-7;
     const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
     const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
     const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
+    const double tol = tiles::rect_tol(t.cv, cell_deg_x * (i1 - i0), cell_deg_y * (j1 - j0), rbuild::dmax(ex, ey));
     const double x0 = t.lon0 + a.tw * i0 / a.N - ex, x1 = t.lon0 + a.tw * i1 / a.N + ex;
     const double y0 = t.lat0 + a.th * j0 / a.N - ey, y1 = t.lat0 + a.th * j1 / a.N + ey;
     const double cxm = t.lon0 + a.tw * (i0 + i1) / (2.0 * a.N), cym = t.lat0 + a.th * (j0 + j1) / (2.0 * a.N);
@@ -314,8 +314,8 @@ __device__ inline double rsub_quad(const RBuildArgs& a, const RTile& t, int si, 
     q[1] = rimage(a, t, (si + 1) * C, sj * C);
     q[2] = rimage(a, t, (si + 1) * C, (sj + 1) * C);
     q[3] = rimage(a, t, si * C, (sj + 1) * C);
-    const double frac = rbuild::dmax((double)C, (double)C) / a.N;
-    return 4.0 * t.dev * frac * frac + 1e-7;
+    const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;  // (as the host's classify)
+    return tiles::rect_tol(t.cv, cell_deg_x * C, cell_deg_y * C, rbuild::dmax(t.exd, t.eyd));
 }
 
 // tiles_build.cpp classify_poly(): convex region uv[n] of sub-block (si, sj), candidates those
@@ -344,9 +344,8 @@ __device__ inline uint16_t rclassify_poly(const RBuildArgs& a, const RTile& t, i
     }
     mx /= n;
     my /= n;
-    const double frac = dmax(u1 - u0, v1 - v0) / S;
-    const double tol = 4.0 * t.dev * frac * frac + 1e-7;
     const double eps = dmax(t.exd, t.eyd);
+    const double tol = tiles::poly_tol(t.cv, a.tw * (u1 - u0) / S, a.th * (v1 - v0) / S, eps);
     bool any = false;
     int acnt = 0, akey = -1;
     for (int k = 0; k < t.wa * t.wb; k++) {
@@ -547,9 +546,8 @@ __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile&
     }
     mx /= n;
     my /= n;
-    const double frac = dmax(u1 - u0, v1 - v0) / S;
-    const double tol = 4.0 * t.dev * frac * frac + 1e-7;
     const double eps = dmax(t.exd, t.eyd);
+    const double tol = tiles::poly_tol(t.cv, a.tw * (u1 - u0) / S, a.th * (v1 - v0) / S, eps);
     bool any = false;
     int acnt = 0, akey = -1;
     const int W = t.wa * t.wb, lane = (int)(threadIdx.x & 63);
@@ -2774,19 +2772,20 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     BuildTrace trace;
     const size_t n_recs = tb.recs.size(), SS = (size_t)tb.S * tb.S, CC = (size_t)tb.C * tb.C;
     const int64_t n_sub = (int64_t)(n_recs * SS);
-    if (tb.tile_of_rec.size() != n_recs || tb.rec_dev.size() != n_recs || !ch->tile_rec.p || !ch->tile_ent.p)
+    if (tb.tile_of_rec.size() != n_recs || tb.rec_curv.size() != n_recs || !ch->tile_rec.p || !ch->tile_ent.p)
         return fail(MOSAIC_E_ARG, "raster build: tile directory not on the device");
     TmpBuf d_tor, d_dev, d_code, d_list, d_kind, d_line, d_cells;
     int e;
-    if ((e = d_tor.reserve(std::max<size_t>(n_recs * 4, 16))) || (e = d_dev.reserve(std::max<size_t>(n_recs * 8, 16))) ||
+    if ((e = d_tor.reserve(std::max<size_t>(n_recs * 4, 16))) || (e = d_dev.reserve(std::max<size_t>(n_recs * sizeof(tiles::TileCurv), 16))) ||
         (e = d_code.reserve(std::max<size_t>((size_t)n_sub * 2, 16))))
         return e;
     HIP_TRY(hipMemcpyAsync(d_tor.p, tb.tile_of_rec.data(), n_recs * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_dev.p, tb.rec_dev.data(), n_recs * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_dev.p, tb.rec_curv.data(), n_recs * sizeof(tiles::TileCurv), hipMemcpyHostToDevice,
+                           c->stream));
     RBuildArgs a{};
     a.recs = (const tiles::TileRec*)ch->tile_rec.p;
     a.tile_of_rec = (const int32_t*)d_tor.p;
-    a.rec_dev = (const double*)d_dev.p;
+    a.rec_curv = (const tiles::TileCurv*)d_dev.p;
     a.entries = (const uint32_t*)ch->tile_ent.p;
     a.n_recs = (int32_t)n_recs;
     a.tnx = tb.grid.nx;

@@ -11,24 +11,37 @@
 // window of axial coordinates its points can round to, with the chip-table slot of every hexagon
 // in the window.  A point then costs: tile lookup, projection, rounding, one window read.
 //
-// Why it is exact (every claim is checked on the host while building; any doubt marks the tile
-// kFull, which runs the unchanged h3_fast + probe path):
-//  * face: the 9 samples (corners, edge midpoints, centre) of the tile all have the same closest
-//    face with a dot-product gap >= 1e-4 to every other face.  The gap is a near-linear function
-//    of position; over a tile of <= 0.25 degrees it deviates from linear by < 3e-6, so the whole
-//    tile is inside the face's region by far more than the fast path's error.
-//  * window: a point's hexagon centre differs from its fractional axial coordinates by < 2/3 in
-//    each axial coordinate; the tile's image is within 0.05 hex units (checked at the edge
-//    midpoints and the centre) of the bilinear patch through its corner images, so the window
-//    [floor(min) - 1, floor(max) + 1] per axis contains every hexagon a tile point can have, under
-//    H3 or the fast path.  A certified point outside the window (impossible by this argument)
+// Why it is exact (every condition is checked on the host while building; any doubt marks the
+// tile kFull, which runs the unchanged h3_fast + probe path).  The map of a tile's points to its
+// face plane, F(lon, lat) = S (EI.p, EP.p) / (FC.p) (hex units; p the unit vector, FC the face
+// centre, EI / EP the plane's orthonormal axes), has derivatives bounded over the tile in closed
+// form (TileCurv below).  From them:
+//  * face: the 4 corners of the tile have the same closest face, with a dot-product gap >= 1e-4
+//    to every other face.  Each gap (FC_f - FC_g).p has second derivatives <= |FC_f - FC_g| |p''|
+//    <= 2 rad^-2 along lon and lat lines, so over a tile of <= 0.25 degrees it stays within
+//    2 k^2 (tw^2 + th^2) / 8 < 1e-5 of the bilinear interpolant of its corner values (k = pi / 180),
+//    which is >= the smallest corner gap: the whole tile is on the face.
+//  * window: every image point lies within rect_tol(tile) <= 0.25 hex units of the bilinear patch
+//    through the corner images, which lies in their convex hull; 0.25 hex units are < 0.29 in each
+//    axial coordinate, and a point's hexagon centre is within 2/3 of its fractional axial
+//    coordinates (the Voronoi hexagon's vertices are at axial offsets (2/3, 1/3) and rotations),
+//    so the window [floor(min) - 1, floor(max) + 1] per axis (min / max over the samples) contains
+//    every hexagon a tile point can have, under H3 or the fast path (their images differ by
+//    < 1e-9 hex units).  A certified point outside the window (impossible by this argument)
 //    still takes the index + probe path.
 //  * skip: a tile whose window holds no chip cell is kSkip: none of its points can join.
 //  * outside the grid: the grid is the region of the chip cells (from a rough cell -> lon/lat
-//    inverse) widened by k tile rings, and every chip cell must be found in the window of a tile
-//    at least k rings inside the grid, where k rings span >= 1.5x the 2.5 hex units from a tile's
-//    image to any point of a cell in its window (measured hex-units-per-degree scales).  So every
-//    point of every chip cell lies inside the grid and a finite point outside joins nothing.
+//    inverse, placement only) widened by k tile rings, and every chip cell must be found in the
+//    window of a tile T at least k rings inside the grid, with its hexagon at least 2/sqrt(3) hex
+//    units inside the territory of T's face (the bisector lines with every other face in T's
+//    plane).  A point P of such a cell whose closest face is T's rounds to that hexagon, so F(P)
+//    lies within 1/sqrt(3) of its centre and within 2.5 hex units of T's image; F is expanding by
+//    at least S k cos(lat_max) per degree (the gnomonic map expands the sphere, 1 / D >= 1, and
+//    lon / lat -> sphere has singular values cos(lat) and 1), and k rings are >= 1.5 x 2.5 hex
+//    units under that bound, so P is inside the grid.  P cannot have another closest face: H3's
+//    grids of adjacent faces continue each other across the shared edge (the faceNeighbors ijk
+//    transforms), so the cell's position on another face's grid is outside that face's triangle by
+//    more than a rounding radius.  So a finite point outside the grid joins nothing.
 //    Non-finite points take the full path (H3 returns 0 for them, which a chip could carry).
 //
 // HBM layout (per chip table): tile_idx u32[nx * ny] (kSkip, kFull or record + 2), TileRec 16 B
@@ -230,6 +243,34 @@ struct Grid {
     int32_t nx, ny;
 };
 
+// Bounds of F (above) over one tile, for paths of unit speed in (lon, lat) degrees.  With D = FC.p
+// >= D_min and s = |p - D FC| = sin(angle to FC) <= s_max over the tile, S = kH3FastScale[res] and
+// k = pi / 180 (F = S M p / D, M = (EI; EP) of norm 1, |M p| = s, D' = FC.p' with |D'| <= s |p'| as
+// p' is tangent, and |p'| <= 1; |p''| <= 1 along lon / lat lines, <= 2 along any straight line):
+//   |F'|  <= jac  = S k (1 / D + s^2 / D^2)
+//   |F''| <= kax  = S k^2 (1 / D + 3 s / D^2 + 2 s^3 / D^3)   (lon / lat lines)
+//   |F''| <= kdir = S k^2 (2 / D + 4 s / D^2 + 2 s^3 / D^3)   (any straight line)
+// from F'' = S (M p'' / D - 2 M p' D' / D^2 - M p D'' / D^2 + 2 M p D'^2 / D^3).
+struct TileCurv {
+    double kax, kdir, jac;
+};
+// A rectangle w x h (degrees) widened by e per side: every point's image lies within this distance
+// (hex units) of the quadrilateral of its corner images -- the bilinear interpolant maps the
+// rectangle onto that quadrilateral and differs from F by <= (w^2 + h^2) kax / 8 (its error along
+// each axis is <= length^2 / 8 times the second derivative; bilinear interpolation is the two in
+// turn, each non-expanding), the widening moves an image by <= sqrt(2) e jac, and 1e-7 covers the
+// corner images' rounding.
+MOSAIC_HD double rect_tol(const TileCurv& c, double w, double h, double e) {
+    return 0.125 * c.kax * (w * w + h * h) + 1.5 * c.jac * e + 1e-7;
+}
+// A convex polygon with bounding box w x h (degrees), widened by e: within this distance of the
+// polygon of its vertex images -- F differs from its first-order Taylor polynomial A at the box
+// centre by <= kdir r^2 / 2 (r^2 <= (w^2 + h^2) / 4), and A(polygon) = hull(A(vertices)) is within
+// that of hull(F(vertices)), hence twice that.
+MOSAIC_HD double poly_tol(const TileCurv& c, double w, double h, double e) {
+    return 0.25 * c.kdir * (w * w + h * h) + 1.5 * c.jac * e + 1e-7;
+}
+
 // Tile code of (x = lon, y = lat): kSkip outside the grid (finite points), kFull for non-finite.
 MOSAIC_HD uint32_t tile_of(const Grid& g, const uint32_t* idx, double x, double y) {
     double fx = (x - g.x0) * g.sx, fy = (y - g.y0) * g.sy;
@@ -291,7 +332,7 @@ struct Builder {
     int64_t n_full = 0, n_skip = 0;
     const char* why = nullptr;  // reason the directory was not built
     int res_ = 0;
-    std::vector<double> rec_dev;  // per record: patch deviation of the tile (axial units)
+    std::vector<TileCurv> rec_curv;  // per record: the bounds of F over the tile
 
     // ---- point raster (second stage, optional): per sub-block of a tile (S x S per tile, S a power
     // of two) a uint16 entry: a code, kMixed, kSubBlock | tile-local leaf block, or kSubBlock |
@@ -387,27 +428,30 @@ struct Builder {
             y0 = std::min(y0, cy[k]);
             y1 = std::max(y1, cy[k]);
         }
-        // hex units per degree at the region centre (lon and lat directions)
+        // hex units per degree at the region centre (lon and lat directions): placement only
         double mx = 0.5 * (x0 + x1), my = 0.5 * (y0 + y1);
         Samples c0;
         double dd = 1e-4;
         if (!sample(mx - dd, my - dd, 2 * dd, 2 * dd, res, &c0)) return fail("region centre near a face edge");
         double slon = axis_scale(c0, 3, 5, 2 * dd), slat = axis_scale(c0, 1, 7, 2 * dd);
-        double sig0 = sigma_min(c0, 2 * dd, 2 * dd);
-        if (!(slon > 0 && slat > 0 && sig0 > 0)) return fail("degenerate scale");
+        if (!(slon > 0 && slat > 0)) return fail("degenerate scale");
         // pad by 3 hex units (cells are ~0.6 hex units around their centres)
         x0 -= 6.0 / slon;
         x1 += 6.0 / slon;
         y0 -= 6.0 / slat;
         y1 += 6.0 / slat;
-        if (y0 < -85.0 || y1 > 85.0) return fail("polar region");
+        if (y0 < -80.0 || y1 > 80.0) return fail("polar region");
         if (x1 - x0 > 90.0 || y1 - y0 > 60.0) return fail("region too large");
         double tw = std::min(0.25, 4.0 / slon), th = std::min(0.25, 4.0 / slat);
         // tile budget: at most 2^24 tiles and 2^26 window entries
         double ntiles = ((x1 - x0) / tw + 4) * ((y1 - y0) / th + 4);
         if (ntiles > (double)(1 << 24)) return fail("too many tiles");
-        // rings: 2x the cell reach (2.5 hex units, x1.5) at the centre's scale; verified below
-        int k = std::max(2, (int)ceil(2.0 * 3.75 / (std::min(tw, th) * sig0)));
+        // rings: 1.5x the cell reach (2.5 hex units) under the lower bound S k cos(lat_max) on F's
+        // expansion per degree, lat_max over the grid (<= 64 rings past the padded region)
+        const double kdeg = 3.141592653589793 / 180.0;
+        const double lat_max = std::min(89.0, std::max(fabs(y0), fabs(y1)) + 64.0 * th);
+        const double sig_lo = h3::kH3FastScale[res] * kdeg * cos(lat_max * kdeg) * (1.0 - 1e-9);
+        int k = std::max(2, (int)ceil(3.75 / (std::min(tw, th) * sig_lo)));
         if (k > 64) return fail("ring count");
         rings = k;
         int nx = (int)ceil((x1 - x0) / tw) + 2 * k, ny = (int)ceil((y1 - y0) / th) + 2 * k;
@@ -420,7 +464,7 @@ struct Builder {
         tile_idx.assign((size_t)nx * ny, kSkip);
         recs.clear();
         entries.clear();
-        rec_dev.clear();
+        rec_curv.clear();
         res_ = res;
         std::vector<uint8_t> found(cells.size(), 0);
         // slot -> position in cells (for the found flags)
@@ -440,9 +484,8 @@ struct Builder {
         struct RowOut {
             std::vector<uint32_t> code;  // per tile: kFull, kSkip, or 2 + the row-local record
             std::vector<TileRec> recs;
-            std::vector<double> dev;
+            std::vector<TileCurv> curv;
             std::vector<uint32_t> entries;
-            double smin = INFINITY;
         };
         std::vector<RowOut> rows((size_t)ny);
         auto do_row = [&](int j) {
@@ -454,9 +497,9 @@ struct Builder {
                 double lon0 = grid.x0 + i * tw, lat0 = grid.y0 + j * th;
                 Samples s;
                 uint32_t code = kFull;
-                double dev = 1.0;
-                if (sample(lon0, lat0, tw, th, res, &s) && (dev = patch_dev(s)) <= 0.05) {
-                    ro.smin = std::min(ro.smin, sigma_min(s, tw, th));
+                TileCurv cv;
+                if (sample(lon0, lat0, tw, th, res, &s) && tile_curv(s.face, lon0, lat0, tw, th, res, &cv) &&
+                    rect_tol(cv, tw, th, 0.0) <= 0.25) {
                     double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
                     for (int q = 0; q < 9; q++) {
                         amin = std::min(amin, s.a[q]);
@@ -478,8 +521,10 @@ struct Builder {
                                 if (slot < 0) continue;
                                 win[(size_t)ra * wb + rb] = (uint32_t)slot + 1;
                                 any = true;
-                                if (inner && slot < (int64_t)slot_cell.size() && slot_cell[(size_t)slot] >= 0)
-                                    found[(size_t)slot_cell[(size_t)slot]] = 1;
+                                if (inner && slot < (int64_t)slot_cell.size() && slot_cell[(size_t)slot] >= 0) {
+                                    uint8_t& fd = found[(size_t)slot_cell[(size_t)slot]];
+                                    if (!fd && deep_inside(s.face, a0 + ra, b0 + rb, res)) fd = 1;
+                                }
                             }
                         }
                         if (!any) {
@@ -493,7 +538,7 @@ struct Builder {
                             ro.entries.insert(ro.entries.end(), win.begin(), win.end());
                             code = (uint32_t)ro.recs.size() + 2;
                             ro.recs.push_back(r);
-                            ro.dev.push_back(dev);
+                            ro.curv.push_back(cv);
                         }
                     }
                 }
@@ -511,10 +556,8 @@ struct Builder {
             work();
             for (auto& th : pool) th.join();
         }
-        double smin = INFINITY;
         for (int j = 0; j < ny; j++) {
             RowOut& ro = rows[(size_t)j];
-            smin = std::min(smin, ro.smin);
             const uint32_t rec0 = (uint32_t)recs.size();
             const size_t ent0 = entries.size();
             if (ent0 + ro.entries.size() >= ((size_t)1 << 26)) return fail("window entries");
@@ -522,7 +565,7 @@ struct Builder {
                 r.off += (uint32_t)ent0;
                 recs.push_back(r);
             }
-            rec_dev.insert(rec_dev.end(), ro.dev.begin(), ro.dev.end());
+            rec_curv.insert(rec_curv.end(), ro.curv.begin(), ro.curv.end());
             entries.insert(entries.end(), ro.entries.begin(), ro.entries.end());
             for (int i = 0; i < nx; i++) {
                 uint32_t code = ro.code[(size_t)i];
@@ -533,10 +576,12 @@ struct Builder {
             }
             std::vector<uint32_t>().swap(ro.entries);
         }
-        // coverage: every chip cell found in an inner tile, and k rings span the cell reach
+        // coverage: every chip cell found in an inner tile, deep inside its face, and k rings span
+        // 1.5x the cell reach under the expansion bound over the whole grid
         for (size_t q = 0; q < cells.size(); q++)
-            if (!found[q]) return fail("a chip cell was not found inside the grid");
-        if (!(k * std::min(tw, th) * smin >= 3.75)) return fail("ring margin below the cell reach");
+            if (!found[q]) return fail("a chip cell was not found inside the grid, away from face edges");
+        const double glat = std::max(fabs(grid.y0), fabs(grid.y0 + ny * th));
+        if (!(glat <= lat_max && k * std::min(tw, th) * sig_lo >= 3.75)) return fail("ring margin below the cell reach");
         if (recs.empty()) recs.push_back(TileRec{0, 0, 0, 0});
         if (entries.empty()) entries.push_back(0);
         return true;
@@ -549,16 +594,6 @@ struct Builder {
         double da = s.a[k1] - s.a[k0], db = s.b[k1] - s.b[k0];
         return hypot(da - 0.5 * db, s60 * db) / span;
     }
-    // smallest singular value of d(vx, vy)/d(lon, lat) at the tile centre (hex units per degree)
-    static double sigma_min(const Samples& s, double tw, double th) {
-        const double s60 = 0.86602540378443864676;
-        double ax = (s.a[5] - s.a[3]) / tw, bx = (s.b[5] - s.b[3]) / tw;
-        double ay = (s.a[7] - s.a[1]) / th, by = (s.b[7] - s.b[1]) / th;
-        double j00 = ax - 0.5 * bx, j10 = s60 * bx, j01 = ay - 0.5 * by, j11 = s60 * by;
-        double f = j00 * j00 + j01 * j01 + j10 * j10 + j11 * j11, d = fabs(j00 * j11 - j01 * j10);
-        double disc = std::max(0.0, f * f - 4.0 * d * d);
-        return sqrt(std::max(0.0, 0.5 * (f - sqrt(disc))));
-    }
     bool fail(const char* w) {
         why = w;
         tile_idx.clear();
@@ -566,18 +601,50 @@ struct Builder {
         entries.clear();
         return false;
     }
-    // largest distance (axial units) of the tile's samples from the bilinear patch through its
-    // corner images: the second-order term of the map over the tile
-    static double patch_dev(const Samples& s) {
-        // sample k = (u, v) with u = k % 3, v = k / 3 (0, 1/2, 1); corners 0, 2, 6, 8
-        double d = 0.0;
-        for (int q = 0; q < 9; q++) {
-            double u = 0.5 * (q % 3), v = 0.5 * (q / 3);
-            double pa = (1 - u) * (1 - v) * s.a[0] + u * (1 - v) * s.a[2] + (1 - u) * v * s.a[6] + u * v * s.a[8];
-            double pb = (1 - u) * (1 - v) * s.b[0] + u * (1 - v) * s.b[2] + (1 - u) * v * s.b[6] + u * v * s.b[8];
-            d = std::max(d, std::max(fabs(pa - s.a[q]), fabs(pb - s.b[q])));
+#endif  // !__HIPCC__
+
+  public:
+#if !defined(__HIPCC__)
+    // TileCurv of tile [lon0, lon0 + tw] x [lat0, lat0 + th] on `face`: D and s at the centre, moved
+    // by at most the tile's angular radius rho <= (tw + th) / 2 degrees (a meridian then a parallel
+    // path; D and s are 1-Lipschitz in angle); false when D_min <= 0.5 (never on a face's own tile)
+    static bool tile_curv(int face, double lon0, double lat0, double tw, double th, int res, TileCurv* c) {
+        const double k = 3.141592653589793 / 180.0;
+        double px, py, pz;
+        h3::fast_unit(lat0 + 0.5 * th, lon0 + 0.5 * tw, &px, &py, &pz);
+        const double* fc = h3::kH3FastBasis[face];
+        const double dc = fc[0] * px + fc[1] * py + fc[2] * pz;
+        const double rho = 0.5 * (tw + th) * k * (1.0 + 1e-9) + 1e-12;
+        const double D = dc - rho, s = std::min(1.0, sqrt(std::max(0.0, 1.0 - dc * dc)) + rho);
+        if (!(D > 0.5)) return false;
+        const double S = h3::kH3FastScale[res] * (1.0 + 1e-12), up = 1.0 + 1e-9;
+        const double D2 = D * D, D3 = D2 * D, s3 = s * s * s;
+        c->kax = S * k * k * (1.0 / D + 3.0 * s / D2 + 2.0 * s3 / D3) * up;
+        c->kdir = S * k * k * (2.0 / D + 4.0 * s / D2 + 2.0 * s3 / D3) * up;
+        c->jac = S * k * (1.0 / D + s * s / D2) * up;
+        return true;
+    }
+    // the hexagon at axial (a, b) on `face` (resolution res) lies at least 2 / sqrt(3) hex units
+    // inside the face's territory: its centre's distance (face plane, hex units) from the line
+    // (FC_f - FC_g).(FC_f + (x EI + y EP) / S) = 0 of every other face g
+    static bool deep_inside(int face, int a, int b, int res) {
+        const double* fb = h3::kH3FastBasis[face];
+        const double* ei = fb + ((res & 1) ? 9 : 3);
+        const double* ep = fb + ((res & 1) ? 12 : 6);
+        const double S = h3::kH3FastScale[res];
+        const double x = (double)a - 0.5 * (double)b, y = (double)b * 0.86602540378443864676;
+        for (int g = 0; g < 20; g++) {
+            if (g == face) continue;
+            const double* gc = h3::kH3FastBasis[g];
+            const double n[3] = {fb[0] - gc[0], fb[1] - gc[1], fb[2] - gc[2]};
+            const double c0 = n[0] * fb[0] + n[1] * fb[1] + n[2] * fb[2];
+            const double gx = (n[0] * ei[0] + n[1] * ei[1] + n[2] * ei[2]) / S;
+            const double gy = (n[0] * ep[0] + n[1] * ep[1] + n[2] * ep[2]) / S;
+            const double gn = sqrt(gx * gx + gy * gy);
+            if (gn == 0.0) continue;  // (the opposite face: its bisector plane misses the face's plane)
+            if (!((c0 + gx * x + gy * y) / gn >= 1.1547005383792515 + 1e-6)) return false;
         }
-        return d;
+        return true;
     }
 #endif  // !__HIPCC__
 };

@@ -5,7 +5,8 @@
 // sub-block into C x C cells.  A rectangle R (sub-block or cell, widened by eps) gets a code
 // valid for EVERY point of R:
 //   * the hexagons R can reach: R's image on the tile's face is the quadrilateral of its corner
-//     images to within the tile's measured second-order term (scaled to R's size); every window
+//     images to within rect_tol (tiles.h: the tile's closed-form bound on the map's second
+//     derivatives, scaled by R's size, plus R's widening); every window
 //     hexagon (exact Voronoi hexagon of the face lattice, H3's _hex2dToCoordIJK rounding) that the
 //     quadrilateral meets within a tolerance (separating-axis test) is a candidate.  H3 assigns
 //     each point of R one of them.
@@ -179,21 +180,20 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                     }
                     std::sort(h.core.begin(), h.core.end());
                 }
-            const double dev = rec_dev[(size_t)ri];
+            const TileCurv cv = rec_curv[(size_t)ri];
             const double cell_deg_x = tw / N, cell_deg_y = th / N;
             // classification of the fine-lattice rectangle [i0, i1] x [j0, j1] whose corner images
             // are q (counter-clockwise), with candidate hexagons `cin` -> code; `cout` receives the
             // candidates it meets
             auto classify = [&](int i0, int j0, int i1, int j1, const P2* q, const std::vector<int>& cin,
                                 std::vector<int>& cout) -> uint16_t {
-                double frac = std::max((double)(i1 - i0), (double)(j1 - j0)) / N;
-                double tol = 4.0 * dev * frac * frac + 1e-7;
+                double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(lon0) + 1.0);
+                double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(lat0) + 1.0);
+                const double tol = rect_tol(cv, cell_deg_x * (i1 - i0), cell_deg_y * (j1 - j0), std::max(ex, ey));
                 cout.clear();
                 for (int k : cin)
                     if (rbuild::poly_meets_hex(q, 4, hexes[(size_t)k].c, tol, ht)) cout.push_back(k);
                 Rect r;
-                double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(lon0) + 1.0);
-                double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(lat0) + 1.0);
                 r.x0 = lon0 + tw * i0 / N - ex;
                 r.x1 = lon0 + tw * i1 / N + ex;
                 r.y0 = lat0 + th * j0 / N - ey;
@@ -248,9 +248,8 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                 }
                 mx /= n;  // a point inside the (convex) region
                 my /= n;
-                const double frac = std::max(u1 - u0, v1 - v0) / S;
-                const double tol = 4.0 * dev * frac * frac + 1e-7;
                 const double eps = std::max(exd, eyd);
+                const double tol = poly_tol(cv, tw * (u1 - u0) / S, th * (v1 - v0) / S, eps);
                 bool first = true, mixed_ans = false, any = false;
                 for (int k : cin) {
                     const Hex& h = hexes[(size_t)k];
