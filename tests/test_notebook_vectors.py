@@ -126,10 +126,13 @@ def _ring_ulps(ring, want):
 
 # The docs notebooks were rendered on a Databricks runtime whose libh3 build is not known; on 24 of
 # the 47 core rings below one or two vertex latitudes differ from this image's glibc-linked H3 C by
-# 1-2 ulp.  Tried and ruled out as the cause: a correctly rounded libm (quad precision sin / cos /
-# tan / asin / acos / atan / atan2), FMA contraction, 128-bit or 64-bit long double, and +-3 ulp on
-# face 2's faceCenterGeo / faceAxesAzRadsCII literals.  Ulp-level boundary vertices are therefore
-# parity-unpinned against the docs; cell ids, polyfill order, chip sets and is_core are exact.
+# 1-2 ulp.  Tried and ruled out (tools/probes/kepler_ulp/run.sh): x87 excess precision
+# through the r chain, double constants, binary128 long double with and without FMA contraction,
+# every subset of correctly rounded atan / atan2 / sin / cos / asin, +-1 ulp on r / atan(r) / the
+# azimuth, other degree conversions, printing artefacts, and +-3 ulp on face 2's faceCenterGeo /
+# faceAxesAzRadsCII literals -- the oracle's arithmetic is the closest of all.  Ulp-level boundary
+# vertices are therefore parity-unpinned against the docs; cell ids, polyfill order, chip sets and
+# is_core are exact.
 BOUNDARY_EXACT_RINGS = 23
 BOUNDARY_MAX_ULPS = 2
 
