@@ -412,7 +412,8 @@ int mosaic_h3_cell_geometry(mosaic_ctx* ctx, int mode, const int64_t* cells, con
  * the vertex and centroid cells whose square's centroid the geometry contains (JTS), ordered as
  * the reference's Scala immutable HashSet iterates them.
  * status[g]: MOSAIC_POLYFILL_OK, or MOSAIC_POLYFILL_UNSUPPORTED (no cells written) for an H3 row
- * whose search meets a pentagon or holds a non-finite vertex, or a BNG row without area.  An empty
+ * holding a non-finite vertex, or a BNG row without area (searches through the 12 pentagon base
+ * cells follow H3's _kRingInternal fallback, as h3-java does).  An empty
  * geometry gives no cells.  Errors: MOSAIC_E_RES, MOSAIC_E_NAN (BNG NaN vertex), MOSAIC_E_CAPACITY. */
 #define MOSAIC_POLYFILL_OK 0
 #define MOSAIC_POLYFILL_UNSUPPORTED (-2)

@@ -129,7 +129,13 @@ __global__ void __launch_bounds__(256) k_join_binned(JoinArgs a, const uint32_t*
 // arithmetic) on LDS vertices.  Chips kept in the global store (multi-ring / multi-part, or past
 // the image's vertex budget) take pip::contains; runs without an image (kFull tiles, records over
 // the image cap) and hexagons outside the window take the generic chip loop (raster_chips).
+// The (point, chip) pairs of 64 points are taken 64 at a time, one per lane; core chips count at
+// once, border chips get the f32 envelope test, and the pairs that pass it (a fraction: a point
+// near a building lies in few of its cell's chip envelopes) are compacted into a per-wave LDS
+// buffer whose full sets of 64 run the ring walk -- no lane of a ring-walking wave idles on a pair
+// the envelope already rejected.
 static const int kSegPoints = 2048;
+static const int kSurv = 128;  // per wave: surviving pairs (64 appended at most before a flush)
 
 // false only when (x, y) lies outside the chip's f64 envelope (the f32 box is rounded outwards and
 // rounding is monotone, so fx, fy of a point inside the f64 box are inside the f32 box)
@@ -172,9 +178,13 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_t[];
     __shared__ SlabItem items[4][16];
     __shared__ uint32_t pairs_all[4 * 64];  // per wave: a window of (point lane, chip) pairs
+    __shared__ double surv_x[4][kSurv], surv_y[4][kSurv];
+    __shared__ uint32_t surv_c[4][kSurv];
+    __shared__ long long surv_r[PAIRS ? 4 : 1][PAIRS ? kSurv : 1];
     __shared__ unsigned long long run_end_s;
     const int lane = (int)(threadIdx.x & 63);
     const int wv = (int)(threadIdx.x >> 6) & 3;
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     uint32_t* im = lds_t;
     unsigned int* cnt = lds_t + img_words;
     if (CM == kCountLds) {
@@ -214,6 +224,27 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
         const int wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
         const uint32_t* chips = im + im[2];
         const double* V = (const double*)(im + im[3]);
+        // the ring walk over the wave's buffered pairs, 64 at a time from the top of the buffer
+        // (all of them when `all`); wave-uniform
+        uint32_t sn = 0;
+        auto ring_tests = [&](bool all) {
+            while (sn >= 64 || (all && sn > 0)) {
+                const uint32_t m = sn < 64u ? sn : 64u;
+                if ((uint32_t)lane < m) {
+                    const uint32_t e = sn - m + (uint32_t)lane;
+                    const double qx = surv_x[wv][e], qy = surv_y[wv][e];
+                    const uint32_t* cr = chips + 8u * surv_c[wv][e];
+                    const uint32_t vi = cr[1], vc = vi >> 16;
+                    const bool hit = vc == binned::kImgGlobal ? pip::contains(a.store, cr[2], qx, qy)
+                                                              : ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
+                    if (hit) emit_hit<CM, PAIRS>(a, PAIRS ? (int64_t)surv_r[wv][e] : -1, cr[0] >> 1, cnt);
+                }
+                sn -= m;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        };
         for (int64_t g = pos + wv * 64; g < r1; g += 256) {  // wave-uniform
             const int64_t i = g + lane;
             double x = 0.0, y = 0.0;
@@ -271,25 +302,36 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                 const int owner = (int)(ent & 63u);
                 const double qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64);
                 const int64_t qrow = PAIRS ? (int64_t)__shfl((long long)row, owner, 64) : -1;
+                bool surv = false;
                 if (live) {
                     const uint32_t* cr = chips + 8u * (ent >> 6);
                     const uint32_t meta = cr[0];
-                    bool hit = true;
-                    if (!(meta & 1u)) {
+                    if (meta & 1u) {
+                        emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
+                    } else {
                         tests++;
-                        const uint32_t vi = cr[1], vc = vi >> 16;
-                        if (vc == binned::kImgGlobal) hit = pip::contains(a.store, cr[2], qx, qy);
-                        else hit = fbox_in(cr, (float)qx, (float)qy) && ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
+                        surv = fbox_in(cr, (float)qx, (float)qy);
                     }
-                    if (hit) emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
                 }
+                const unsigned long long sm = __ballot(surv);
+                if (surv) {
+                    const uint32_t e = sn + (uint32_t)__popcll(sm & lt_mask);
+                    surv_x[wv][e] = qx;
+                    surv_y[wv][e] = qy;
+                    surv_c[wv][e] = ent >> 6;
+                    if (PAIRS) surv_r[wv][e] = (long long)qrow;
+                }
+                sn += (uint32_t)__popcll(sm);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (sn >= 64) ring_tests(false);
             }
             raster_chips<CM, PAIRS>(a, row, cur, end, x, y, tests, cnt, items[wv]);
             if (CM == kCountWaveHash) wave_hash_flush(a, cnt, false);
         }
+        ring_tests(true);  // the run's last buffered pairs, while its image is in LDS
+        if (CM == kCountWaveHash) wave_hash_flush(a, cnt, false);
         __syncthreads();  // every wave is done with this run's image
         pos = r1;
     }

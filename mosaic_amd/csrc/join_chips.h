@@ -222,8 +222,15 @@ struct TileQueue {
     uint32_t code[kQueue];
 };
 
+// H3's own cell of a point the fast path cannot certify (a call, so the exact path's registers do
+// not count against the kernels that rarely take it)
+__device__ __noinline__ int64_t exact_cell(double x, double y, int res, int jdk) {
+    return (int64_t)h3::h3_exact(h3::to_radians(y, jdk), h3::to_radians(x, jdk), res);
+}
+
 // Chips of one queued point: tile path (certified hexagon -> window slot) or the generic
-// fast path + probe (kFull tiles, window misses).  Uncertified points go to the exact queue.
+// fast path + probe (kFull tiles, window misses).  Uncertified points go to the exact queue, or
+// (exact_inline) get h3_exact's cell here.
 __device__ inline void tiled_cell(const JoinArgs& a, int64_t i, double x, double y, uint32_t code, uint32_t& cur,
                                   uint32_t& end) {
     cur = end = 0;
@@ -238,7 +245,11 @@ __device__ inline void tiled_cell(const JoinArgs& a, int64_t i, double x, double
         int ba, bb;
         if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
             unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+            if (a.exact_inline) {
+                probe(a, exact_cell(x, y, a.res, a.jdk), cur, end);
+            } else if (q < a.amb_cap) {
+                a.amb_queue[q] = (unsigned long long)i;
+            }
             return;
         }
         const int ra = ba - r.a0, rb = bb - r.b0;
@@ -257,8 +268,11 @@ __device__ inline void tiled_cell(const JoinArgs& a, int64_t i, double x, double
         cell = (int64_t)h3::h3_fast(y, x, a.res, &amb);
         if (amb) {
             unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-            return;
+            if (!a.exact_inline) {
+                if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
+                return;
+            }
+            cell = exact_cell(x, y, a.res, a.jdk);
         }
     }
     probe(a, cell, cur, end);

@@ -61,6 +61,9 @@ struct JoinArgs {
     unsigned long long* amb_queue;  // rows for the exact H3 pass
     unsigned long long* amb_count;
     unsigned long long amb_cap;
+    // tiled_cell: rows the fast path cannot certify are answered in place with h3_exact (counted
+    // in amb_count, not queued) -- k_join_mixed behind a stream kernel, so no exact pass follows
+    int exact_inline = 0;
     long long* pair_row;
     int* pair_key;
     unsigned long long* pair_count;

@@ -3624,7 +3624,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
     bool lds = ch->n_polygons <= kLdsCountsMax;
     size_t shm = lds ? (size_t)ch->n_polygons * 4 : 0;
     int g = grid_size(c, n);
-    bool binned_used = false;
+    bool binned_used = false, exact_inline = false;
     if (n > 0) {
         hipEvent_t tstop;
         if ((rc = timing_begin(c, &tstop))) return rc;
@@ -3729,6 +3729,9 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
             a.mixq_count = sc + 4;
+            // the mixed kernel answers its uncertified rows itself: no exact pass after it
+            a.exact_inline = 1;
+            exact_inline = true;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             auto mode_for = [&](bool vec) -> int {
                 // the pipelined forms where they apply (the compacted one, k_join_stream_cpt, carries
@@ -3834,7 +3837,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
 #undef MOSAIC_LAUNCH
         HIP_TRY(hipGetLastError());
         if (tstop) HIP_TRY(hipEventRecord(tstop, c->stream));
-        if (h3g && !binned_used) {
+        if (h3g && !binned_used && !exact_inline) {
             // the margin queue is nearly always a handful of rows: a grid of 2 workgroups per CU keeps
             // the launch short (a 2048-workgroup grid cost ~40 us of dispatch for ~1 row)
             int ge = std::min(grid_size(c, (int64_t)qcap), std::max(1, c->n_cu * 2));
@@ -3850,7 +3853,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
     unsigned long long s[kScalars];
     HIP_TRY(hipMemcpy(s, c->scalars.p, sizeof s, hipMemcpyDeviceToHost));
     if (binned_used) s[0] = s[6] ? qcap + 1 : s[5];  // (the queue was drained chunk by chunk)
-    if (ch->grid == MOSAIC_GRID_H3 && s[0] > qcap) {
+    if (ch->grid == MOSAIC_GRID_H3 && s[0] > qcap && !exact_inline) {
         // queue overflow (adversarial input): recompute the whole batch on the exact path
         HIP_TRY(hipMemsetAsync(dcounts, 0, cbytes, c->stream));
         HIP_TRY(hipMemsetAsync(sc + 1, 0, 2 * 8, c->stream));

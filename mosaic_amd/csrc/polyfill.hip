@@ -16,10 +16,9 @@
 //   3. host: that sequence inserted into an open-addressing table of maxPolyfillSize slots (home
 //      slot cell % size, linear probing), read in slot order -- the order h3-java returns.  The
 //      parts' lists are concatenated per geometry (H3IndexSystem.scala:118-124).
-// Where H3's ring walk falls back to _kRingInternal (near the 12 pentagons) kring1 finds the same
-// ring set geometrically, so such rows can differ from H3 only in the order of cells that collide
-// in its output table.  Rows whose search enters a pentagon base cell below res 0, or that hold a
-// non-finite vertex, get status MOSAIC_POLYFILL_UNSUPPORTED.
+// Where H3's ring walk falls back to _kRingInternal (near the 12 pentagons) kring1 runs that
+// fallback too (h3_neighbors.h), in H3's table order.  Rows that hold a non-finite vertex get status
+// MOSAIC_POLYFILL_UNSUPPORTED.
 //
 // BNG (BNGIndexSystem.polyfill, core/index/BNGIndexSystem.scala:185-204): breadth-first from the
 // cells of every vertex and of the JTS centroid; a visited cell is kept when the geometry contains

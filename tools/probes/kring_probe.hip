@@ -1,40 +1,47 @@
-// GPU probe: H3 hexRange steps (h3_neighbors.h) for one cell, device vs host, step by step.
+// GPU probe: H3 kRing fast walk (h3_neighbors.h kring_fast) over a list of cells, one lane per row as
+// in k_h3_kring; prints "row count first" per row.  Host build: g++ -DHOST_WALK -x c++ kring_probe.hip
+//   usage: kring_probe CELLS_FILE K
+#ifndef HOST_WALK
 #include <hip/hip_runtime.h>
+#else
+#define __global__
+#endif
 #include <stdio.h>
+#include <stdlib.h>
+#include <vector>
 #include "../../mosaic_amd/csrc/h3_neighbors.h"
 using namespace mosaic;
-struct Step { unsigned long long in, out; int dir, rot_in, rot_out; };
-__host__ __device__ int walk(uint64_t origin, int k, Step* st) {
-    int n = 0, ring = 1, dir = 0, i = 0, rotations = 0;
-    while (ring <= k && n < 60) {
-        if (dir == 0 && i == 0) {
-            Step& s = st[n++]; s.in = origin; s.dir = h3nb::kNextRing; s.rot_in = rotations;
-            origin = h3nb::neighbor_rotations(origin, h3nb::kNextRing, &rotations);
-            s.out = origin; s.rot_out = rotations;
-        }
-        Step& s = st[n++]; s.in = origin; s.dir = h3nb::direction(dir); s.rot_in = rotations;
-        origin = h3nb::neighbor_rotations(origin, h3nb::direction(dir), &rotations);
-        s.out = origin; s.rot_out = rotations;
-        if (++i == ring) { i = 0; if (++dir == 6) { dir = 0; ring++; } }
-    }
-    return n;
+__global__ void kk(const int64_t* cells, int64_t n, int k, int64_t* out, int stride, int* cnt) {
+#ifndef HOST_WALK
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+#else
+    for (int64_t i = 0; i < n; i++)
+#endif
+        cnt[i] = h3nb::kring_fast((uint64_t)cells[i], k, 0, out + i * stride);
 }
-__global__ void kk(uint64_t c, int k, Step* st, int* n, int64_t* fast) {
-    *n = walk(c, k, st);
-    fast[0] = h3nb::kring_fast(c, k, 0, fast + 1);
-}
-int main() {
-    const uint64_t c = 632242071332407807ULL;
-    Step* d; int* dn; int64_t* df;
-    hipMalloc(&d, 64 * sizeof(Step)); hipMalloc(&dn, 4); hipMalloc(&df, 64 * 8);
-    kk<<<1, 1>>>(c, 1, d, dn, df);
-    Step hs[64], gs[64]; int gn; int64_t gf[64];
-    hipMemcpy(gs, d, sizeof(gs), hipMemcpyDeviceToHost); hipMemcpy(&gn, dn, 4, hipMemcpyDeviceToHost);
-    hipMemcpy(gf, df, sizeof(gf), hipMemcpyDeviceToHost);
-    int hn = walk(c, 1, hs);
-    printf("host steps %d gpu steps %d gpu kring_fast %ld\n", hn, gn, gf[0]);
-    for (int i = 0; i < gn && i < hn; i++)
-        printf("%2d dir %d in %llu rot %d -> host %llu rot %d | gpu %llu rot %d%s\n", i, hs[i].dir, hs[i].in, hs[i].rot_in,
-               hs[i].out, hs[i].rot_out, gs[i].out, gs[i].rot_out, (hs[i].out != gs[i].out || hs[i].rot_out != gs[i].rot_out) ? "  <<<" : "");
+int main(int argc, char** argv) {
+    if (argc < 3) return 1;
+    FILE* f = fopen(argv[1], "r");
+    if (!f) return 1;
+    const int k = atoi(argv[2]), stride = 1 + 3 * k * (k + 1);
+    std::vector<int64_t> cells;
+    long long c;
+    while (fscanf(f, "%lld", &c) == 1) cells.push_back(c);
+    fclose(f);
+    const int64_t n = (int64_t)cells.size();
+    std::vector<int64_t> out((size_t)n * stride);
+    std::vector<int> cnt((size_t)n);
+#ifndef HOST_WALK
+    int64_t *dc, *dout;
+    int* dcnt;
+    if (hipMalloc(&dc, n * 8) || hipMalloc(&dout, n * stride * 8) || hipMalloc(&dcnt, n * 4)) return 2;
+    if (hipMemcpy(dc, cells.data(), n * 8, hipMemcpyHostToDevice)) return 2;
+    kk<<<(unsigned)((n + 255) / 256), 256>>>(dc, n, k, dout, stride, dcnt);
+    if (hipDeviceSynchronize() || hipMemcpy(out.data(), dout, n * stride * 8, hipMemcpyDeviceToHost) ||
+        hipMemcpy(cnt.data(), dcnt, n * 4, hipMemcpyDeviceToHost)) return 3;
+#else
+    kk(cells.data(), n, k, out.data(), stride, cnt.data());
+#endif
+    for (int64_t i = 0; i < n; i++) printf("%ld %d %ld\n", (long)i, cnt[i], (long)(cnt[i] > 0 ? out[i * stride + 1] : 0));
     return 0;
 }
