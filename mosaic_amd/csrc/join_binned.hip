@@ -26,6 +26,7 @@
 
 #include "join_binned.h"
 #include "join_chips.h"
+#include "ring_walk.h"
 
 using namespace mosaic;
 
@@ -144,33 +145,6 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
            fy <= __uint_as_float(cr[7]);
 }
 
-// PointLocation.locateInRing(p, ring) == INTERIOR for a closed ring of n vertices (x, y pairs):
-// pip::locate_in_ring's RayCrossingCounter steps and CGAlgorithmsDD orientation, operation for
-// operation.  A point outside the ring's envelope gets EXTERIOR from the walk itself (no crossing
-// counted twice), so the envelope pre-test of locate_in_polygon changes no answer.
-__device__ __forceinline__ bool ring_interior(const double* v, uint32_t n, double px, double py) {
-    int crossings = 0;
-    double p2x = v[0], p2y = v[1];
-    for (uint32_t i = 1; i < n; i++) {
-        const double p1x = v[2 * i], p1y = v[2 * i + 1];
-        if (!(p1x < px && p2x < px)) {
-            if (px == p2x && py == p2y) return false;
-            if (p1y == py && p2y == py) {
-                const double mnx = p1x < p2x ? p1x : p2x, mxx = p1x < p2x ? p2x : p1x;
-                if (px >= mnx && px <= mxx) return false;
-            } else if (((p1y > py) && (p2y <= py)) || ((p2y > py) && (p1y <= py))) {
-                int orient = pip::orientation_index(p1x, p1y, p2x, p2y, px, py);
-                if (orient == 0) return false;
-                if (p2y < p1y) orient = -orient;
-                if (orient == 1) crossings++;
-            }
-        }
-        p2x = p1x;
-        p2y = p1y;
-    }
-    return crossings & 1;
-}
-
 template <int CM, bool PAIRS, class P>
 __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys,
                                                     const P* __restrict__ pts, int64_t n, const unsigned long long* n_skip,
@@ -236,7 +210,7 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                     const uint32_t* cr = chips + 8u * surv_c[wv][e];
                     const uint32_t vi = cr[1], vc = vi >> 16;
                     const bool hit = vc == binned::kImgGlobal ? pip::contains(a.store, cr[2], qx, qy)
-                                                              : ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
+                                                              : ringwalk::ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
                     if (hit) emit_hit<CM, PAIRS>(a, PAIRS ? (int64_t)surv_r[wv][e] : -1, cr[0] >> 1, cnt);
                 }
                 sn -= m;

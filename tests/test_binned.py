@@ -118,3 +118,4 @@ def test_binned_many_polygons_wave_hash(h3ctx):
         del xd, yd
         torch.cuda.empty_cache()
         table.close()
+

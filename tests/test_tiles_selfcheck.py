@@ -109,3 +109,14 @@ def test_tile_map_bounds(tmp_path):
     assert r_jac <= 1.0 and r_ax <= 1.0 and r_dir <= 1.0 and r_rect <= 1.0
     # and not vacuous: the first-derivative bound is attained (radial direction), the others within 3x
     assert r_jac > 0.9 and r_ax > 0.3 and r_rect > 0.1
+
+
+def test_ring_walks_match_jts(tmp_path):
+    """CPU: the tile join's ring walks (ring_walk.h: branch-free with its filter fallback, and the
+    exact walk) equal JTS locateInRing == INTERIOR (pip_device.h) on ~1.1 M adversarial cases"""
+    root = ROOT
+    exe = tmp_path / "rwc"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(root, "mosaic_amd", "csrc"),
+                    "-o", str(exe), os.path.join(root, "tests", "native", "ring_walk_check.cpp")], check=True)
+    cases, bad = map(int, subprocess.run([str(exe), "20000"], check=True, capture_output=True, text=True).stdout.split())
+    assert cases > 1_000_000 and bad == 0

@@ -1,6 +1,6 @@
 """C4-shape chip join timing (GPU box): synthetic OSM-style buildings (mosaic_amd.data.
 synthetic_buildings: rectangles / L-shapes, 8-40 m sides, clustered over the NYC bbox) chipped at
-H3 res 11 by the host tessellator, points 70 % within 25 m of a building and 30 % uniform
+H3 res 11 (grid_tessellateexplode on the GPU; --host-tess: the host producer), points 70 % within 25 m of a building and 30 % uniform
 (building_points_device).  BASELINE's C4 is 5e6 buildings x 2.5e8 points per GPU; --buildings
 scales the build side (host tessellation ~30 us per building).  Prints one JSON line per variant.
 
@@ -23,6 +23,7 @@ def main():
     p.add_argument("--n", type=float, default=2.5e8)
     p.add_argument("--res", type=int, default=11)
     p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--host-tess", action="store_true", help="host tessellator (default: this context's GPU)")
     p.add_argument("--variants", nargs="*", default=["default"],
                    help="default | tiles0 (generic path) | praster0 (tile path without the point raster)")
     args = p.parse_args()
@@ -36,14 +37,14 @@ def main():
     t0 = time.perf_counter()
     b = synthetic_buildings(nb)
     t_gen = time.perf_counter() - t0
+    ctx = MosaicContext.build("H3", "JTS")
     t0 = time.perf_counter()
-    chips = tessellate("H3", b, args.res)
+    chips = tessellate("H3", b, args.res, ctx=None if args.host_tess else ctx)
     t_tess = time.perf_counter() - t0
     print(json.dumps({"buildings": nb, "chips": len(chips["index_id"]), "core_chips": int(chips["is_core"].sum()),
                       "generate_s": round(t_gen, 2), "tessellate_s": round(t_tess, 2)}), flush=True)
     n = int(args.n)
     x, y = building_points_device(b, n, seed=9)
-    ctx = MosaicContext.build("H3", "JTS")
     counts = torch.zeros(nb, dtype=torch.int64, device="cuda")
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     for v in args.variants:
