@@ -94,7 +94,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * raster cells per border chip side, 1..64, for tables built afterwards), "raster_adaptive" (0/1: rings
  * with few segments get 2 ceil(sqrt(segments)) cells a side instead, at most "raster"; default 1),
  * "raster_min_segments" (rings with fewer segments get no raster: their contains test walks the
- * segments; default 0),
+ * segments; default 0, and at least 16 for H3 tables with more polygons than point-raster codes,
+ * whose joins test chips from tile images instead),
  * "lane_edges" (raster cell lists up to this long are evaluated by the owning lane), "tiles" (0/1: H3
  * tile directory for tables built afterwards, and its use by joins), "point_raster" (0/1: the point
  * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile

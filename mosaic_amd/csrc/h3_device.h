@@ -158,12 +158,15 @@ MOSAIC_HD uint64_t set_digit(uint64_t h, int r, int d) {
     int s = (15 - r) * 3;
     return (h & ~((uint64_t)7 << s)) | ((uint64_t)d << s);
 }
+// The first nonzero digit of 1 .. res (0 if none): the most significant nonzero 3-bit group of the
+// used digits.  Written without a loop exit on purpose: gfx950 code for the loop-with-early-return
+// form read the exit condition of the wave's last iteration after the loop, so a lane that had
+// left the loop early saw "no nonzero digit" when other lanes of its wave iterated longer
+// (tools/probes/kring_reason.hip found it; tests/test_h3_kring.py covers mixed waves).
 MOSAIC_HD int leading_nonzero_digit(uint64_t h, int res) {
-    for (int r = 1; r <= res; r++) {
-        int d = get_digit(h, r);
-        if (d) return d;
-    }
-    return 0;
+    const uint64_t d = (h & 0x1fffffffffffULL) >> (3 * (15 - res));  // digits 1 .. res, digit res lowest
+    const int msb = d ? 63 - __builtin_clzll(d) : 0;
+    return (int)((d >> (3 * (msb / 3))) & 7u);
 }
 MOSAIC_HD uint64_t rotate_all(uint64_t h, int res, bool ccw) {
     for (int r = 1; r <= res; r++) h = set_digit(h, r, ccw ? rotate60ccw(get_digit(h, r)) : rotate60cw(get_digit(h, r)));

@@ -247,20 +247,13 @@ MOSAIC_HD bool is_valid_cell(uint64_t h) {
     if (((h >> 56) & 7) != 0) return false;
     const int bc = base_cell_of(h), res = res_of(h);
     if (bc >= 122) return false;
-    bool found_first = false;
-    for (int r = 1; r <= 15; r++) {
-        const int d = h3::get_digit(h, r);
-        if (r <= res) {
-            if (d == 7) return false;
-            if (!found_first && d != 0) {
-                found_first = true;
-                if (base_is_pentagon(bc) && d == 1) return false;
-            }
-        } else if (d != 7) {
-            return false;
-        }
-    }
-    return true;
+    // digits 1 .. res are not 7, digits res + 1 .. 15 are 7 (bit tests, no loop: see
+    // h3::leading_nonzero_digit)
+    const uint64_t low = 0x1249249249249ULL, D = h & 0x1fffffffffffULL;
+    const uint64_t seven = D & (D >> 1) & (D >> 2) & low;  // bit 3j: digit 15 - j is 7
+    const uint64_t unused = low & ((1ULL << (3 * (15 - res))) - 1ULL);
+    if ((seven & unused) != unused || (seven & ~unused) != 0) return false;
+    return !(base_is_pentagon(bc) && h3::leading_nonzero_digit(h, res) == 1);
 }
 
 // Scala 2.12 immutable.HashSet iteration order of Long elements (the hash trie walks 5-bit groups

@@ -129,7 +129,9 @@ __global__ void __launch_bounds__(256) k_join_binned(JoinArgs a, const uint32_t*
 // get the f32 envelope pre-test and JTS's ray-crossing ring walk (pip::locate_in_ring's
 // arithmetic) on LDS vertices.  Chips kept in the global store (multi-ring / multi-part, or past
 // the image's vertex budget) take pip::contains; runs without an image (kFull tiles, records over
-// the image cap) and hexagons outside the window take the generic chip loop (raster_chips).
+// the image cap) and hexagons outside the window take the same pair path over the chip table
+// (envelope from geom_bbox, then pip::contains; the sorted order keeps those reads in L1 / L2).
+// Chip indices fit 26 bits (the caller's condition).
 // The (point, chip) pairs of 64 points are taken 64 at a time, one per lane; core chips count at
 // once, border chips get the f32 envelope test, and the pairs that pass it (a fraction: a point
 // near a building lies in few of its cell's chip envelopes) are compacted into a per-wave LDS
@@ -137,6 +139,7 @@ __global__ void __launch_bounds__(256) k_join_binned(JoinArgs a, const uint32_t*
 // the envelope already rejected.
 static const int kSegPoints = 2048;
 static const int kSurv = 128;  // per wave: surviving pairs (64 appended at most before a flush)
+static const uint32_t kSurvGlobal = 0x80000000u;  // a buffered pair's chip is in the chip table
 
 // false only when (x, y) lies outside the chip's f64 envelope (the f32 box is rounded outwards and
 // rounding is monotone, so fx, fy of a point inside the f64 box are inside the f32 box)
@@ -150,7 +153,6 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                                                     const P* __restrict__ pts, int64_t n, const unsigned long long* n_skip,
                                                     binned::Images img, uint32_t img_words) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_t[];
-    __shared__ SlabItem items[4][16];
     __shared__ uint32_t pairs_all[4 * 64];  // per wave: a window of (point lane, chip) pairs
     __shared__ double surv_x[4][kSurv], surv_y[4][kSurv];
     __shared__ uint32_t surv_c[4][kSurv];
@@ -207,11 +209,21 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                 if ((uint32_t)lane < m) {
                     const uint32_t e = sn - m + (uint32_t)lane;
                     const double qx = surv_x[wv][e], qy = surv_y[wv][e];
-                    const uint32_t* cr = chips + 8u * surv_c[wv][e];
-                    const uint32_t vi = cr[1], vc = vi >> 16;
-                    const bool hit = vc == binned::kImgGlobal ? pip::contains(a.store, cr[2], qx, qy)
-                                                              : ringwalk::ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
-                    if (hit) emit_hit<CM, PAIRS>(a, PAIRS ? (int64_t)surv_r[wv][e] : -1, cr[0] >> 1, cnt);
+                    const uint32_t sc = surv_c[wv][e];
+                    bool hit;
+                    uint32_t key;
+                    if (sc & kSurvGlobal) {  // a chip of the table (a run without an image, a hexagon off the window)
+                        const uint32_t c = sc & ~kSurvGlobal;
+                        hit = pip::contains(a.store, c, qx, qy);
+                        key = a.chip_meta[c] >> 1;
+                    } else {
+                        const uint32_t* cr = chips + 8u * sc;
+                        const uint32_t vi = cr[1], vc = vi >> 16;
+                        hit = vc == binned::kImgGlobal ? pip::contains(a.store, cr[2], qx, qy)
+                                                       : ringwalk::ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
+                        key = cr[0] >> 1;
+                    }
+                    if (hit) emit_hit<CM, PAIRS>(a, PAIRS ? (int64_t)surv_r[wv][e] : -1, key, cnt);
                 }
                 sn -= m;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -223,15 +235,16 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
             const int64_t i = g + lane;
             double x = 0.0, y = 0.0;
             int64_t row = -1;
-            uint32_t cur = 0, end = 0;  // chips left to the generic loop
-            uint32_t c0 = 0, c1 = 0;    // the point's chips in the image
+            uint32_t c0 = 0, c1 = 0;  // the point's chips: in the image, or (glob) in the chip table
+            bool glob = false;
             if (i < r1) {
                 const P p = pts[i];
                 x = p.x;
                 y = p.y;
                 row = binned::row_of(p, i);
                 if (ioff == binned::kNoImage) {
-                    tiled_cell(a, i, x, y, code, cur, end);
+                    tiled_cell(a, i, x, y, code, c0, c1);
+                    glob = true;
                 } else {
                     double px, py, pz, vx, vy, best;
                     h3::fast_unit(y, x, &px, &py, &pz);
@@ -248,7 +261,8 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                             c0 = sf[slot];
                             c1 = sf[slot + 1];
                         } else {
-                            probe(a, (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res), cur, end);
+                            probe(a, (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res), c0, c1);
+                            glob = true;
                         }
                     }
                 }
@@ -276,15 +290,17 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                 const int owner = (int)(ent & 63u);
                 const double qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64);
                 const int64_t qrow = PAIRS ? (int64_t)__shfl((long long)row, owner, 64) : -1;
+                const bool qg = __shfl((int)glob, owner, 64) != 0;
                 bool surv = false;
                 if (live) {
-                    const uint32_t* cr = chips + 8u * (ent >> 6);
-                    const uint32_t meta = cr[0];
+                    const uint32_t c = ent >> 6;
+                    const uint32_t* cr = chips + 8u * c;
+                    const uint32_t meta = qg ? a.chip_meta[c] : cr[0];
                     if (meta & 1u) {
                         emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
                     } else {
                         tests++;
-                        surv = fbox_in(cr, (float)qx, (float)qy);
+                        surv = qg ? !pip::box_excludes(a.store.geom_bbox[c], qx, qy) : fbox_in(cr, (float)qx, (float)qy);
                     }
                 }
                 const unsigned long long sm = __ballot(surv);
@@ -292,7 +308,7 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                     const uint32_t e = sn + (uint32_t)__popcll(sm & lt_mask);
                     surv_x[wv][e] = qx;
                     surv_y[wv][e] = qy;
-                    surv_c[wv][e] = ent >> 6;
+                    surv_c[wv][e] = (ent >> 6) | (qg ? kSurvGlobal : 0u);
                     if (PAIRS) surv_r[wv][e] = (long long)qrow;
                 }
                 sn += (uint32_t)__popcll(sm);
@@ -301,7 +317,6 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if (sn >= 64) ring_tests(false);
             }
-            raster_chips<CM, PAIRS>(a, row, cur, end, x, y, tests, cnt, items[wv]);
             if (CM == kCountWaveHash) wave_hash_flush(a, cnt, false);
         }
         ring_tests(true);  // the run's last buffered pairs, while its image is in LDS

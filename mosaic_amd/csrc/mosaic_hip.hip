@@ -53,6 +53,15 @@ using namespace mosaic;
 // errors
 static thread_local std::string g_last_error;
 
+// f(0) .. f(n - 1) on n host threads (the caller's thread runs f(0))
+template <class F>
+static void parallel_for(int n, F f) {
+    std::vector<std::thread> pool;
+    for (int k = 1; k < n; k++) pool.emplace_back(f, k);
+    if (n > 0) f(0);
+    for (auto& t : pool) t.join();
+}
+
 static int fail(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
@@ -2896,28 +2905,110 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     if (!valid_res(grid, res)) return res_error(grid, res);
     if (n_chips >= (int64_t)1 << 31) return fail(MOSAIC_E_ARG, "too many chips");
     HIP_TRY(hipSetDevice(c->device));
-    // chips grouped by cell, original order kept within a cell
+    // chips grouped by cell, original order kept within a cell: (cell, position) pairs sorted on
+    // host threads (sorted runs, then pairwise merges), which is the stable order by cell
+    const int n_thr = (int)std::max<int64_t>(
+        1, std::min<int64_t>(std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), n_chips / 65536));
     std::vector<uint32_t> order(n_chips);
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t a, uint32_t b) { return index_id[a] < index_id[b]; });
+    {
+        std::vector<std::pair<int64_t, uint32_t>> kv((size_t)n_chips), tmp;
+        auto range = [&](int k, int parts) { return (int64_t)((__int128)n_chips * k / parts); };
+        parallel_for(n_thr, [&](int k) {
+            for (int64_t t = range(k, n_thr); t < range(k + 1, n_thr); t++) kv[(size_t)t] = {index_id[t], (uint32_t)t};
+            std::sort(kv.begin() + range(k, n_thr), kv.begin() + range(k + 1, n_thr));
+        });
+        if (n_thr > 1) tmp.resize(kv.size());
+        for (int w = 1; w < n_thr; w *= 2) {  // merge runs [k w, (k + 1) w) pairwise
+            const int groups = (n_thr + 2 * w - 1) / (2 * w);
+            parallel_for(groups, [&](int g) {
+                const int64_t a0 = range(2 * g * w, n_thr), a1 = range(std::min(2 * g * w + w, n_thr), n_thr),
+                              b1 = range(std::min(2 * g * w + 2 * w, n_thr), n_thr);
+                std::merge(kv.begin() + a0, kv.begin() + a1, kv.begin() + a1, kv.begin() + b1, tmp.begin() + a0);
+            });
+            kv.swap(tmp);
+        }
+        parallel_for(n_thr, [&](int k) {
+            for (int64_t t = range(k, n_thr); t < range(k + 1, n_thr); t++) order[(size_t)t] = kv[(size_t)t].second;
+        });
+    }
     trace.mark("sort by cell");
+    // WKB parse on host threads, contiguous ranges of the sorted order, then concatenated: the same
+    // arrays (and the same first error) as one sequential pass
     GeomBuilder gb;
     std::vector<uint32_t> meta(std::max<int64_t>(n_chips, 1));
     int64_t n_border = 0;
-    for (int64_t t = 0; t < n_chips; t++) {
-        uint32_t i = order[t];
-        if (polygon_key[i] < 0 || polygon_key[i] >= n_polygons)
-            return fail(MOSAIC_E_ARG, "polygon_key out of range at chip " + std::to_string(i));
-        if (index_id[i] == kEmptyKey) return fail(MOSAIC_E_ARG, "reserved index_id at chip " + std::to_string(i));
-        bool core = is_core[i] != 0;
-        meta[t] = ((uint32_t)polygon_key[i] << 1) | (core ? 1u : 0u);
-        int64_t a = wkb_offsets(i), b = wkb_offsets(i + 1);
-        if (b < a || (b > a && !wkb)) return fail(MOSAIC_E_ARG, "bad wkb offsets at chip " + std::to_string(i));
-        // core chips are accepted without a test: their geometry is never read
-        if (!gb.add(core ? nullptr : wkb + a, core ? 0 : (size_t)(b - a)))
-            return fail(MOSAIC_E_WKB, "chip " + std::to_string(i) + ": " + gb.error);
-        n_border += !core;
+    {
+        struct Part {
+            GeomBuilder gb;
+            int64_t n_border = 0, bad_t = -1;
+            int bad_code = 0;
+            std::string bad_msg;
+        };
+        std::vector<Part> parts((size_t)n_thr);
+        auto range = [&](int k) { return (int64_t)((__int128)n_chips * k / n_thr); };
+        parallel_for(n_thr, [&](int k) {
+            Part& pt = parts[(size_t)k];
+            for (int64_t t = range(k); t < range(k + 1); t++) {
+                uint32_t i = order[t];
+                auto bad = [&](int code, const std::string& msg) {
+                    pt.bad_t = t;
+                    pt.bad_code = code;
+                    pt.bad_msg = msg;
+                };
+                if (polygon_key[i] < 0 || polygon_key[i] >= n_polygons) {
+                    bad(MOSAIC_E_ARG, "polygon_key out of range at chip " + std::to_string(i));
+                    return;
+                }
+                if (index_id[i] == kEmptyKey) {
+                    bad(MOSAIC_E_ARG, "reserved index_id at chip " + std::to_string(i));
+                    return;
+                }
+                bool core = is_core[i] != 0;
+                meta[t] = ((uint32_t)polygon_key[i] << 1) | (core ? 1u : 0u);
+                int64_t a = wkb_offsets(i), b = wkb_offsets(i + 1);
+                if (b < a || (b > a && !wkb)) {
+                    bad(MOSAIC_E_ARG, "bad wkb offsets at chip " + std::to_string(i));
+                    return;
+                }
+                // core chips are accepted without a test: their geometry is never read
+                if (!pt.gb.add(core ? nullptr : wkb + a, core ? 0 : (size_t)(b - a))) {
+                    bad(MOSAIC_E_WKB, "chip " + std::to_string(i) + ": " + pt.gb.error);
+                    return;
+                }
+                pt.n_border += !core;
+            }
+        });
+        for (const Part& pt : parts)  // the first failing chip in the sorted order, as a sequential pass
+            if (pt.bad_t >= 0) return fail(pt.bad_code, pt.bad_msg);
+        size_t nv = 0, nr = 0, np = 0, ng = 0;
+        std::vector<size_t> v0(parts.size()), r0(parts.size()), p0(parts.size()), g0(parts.size());
+        for (size_t k = 0; k < parts.size(); k++) {
+            v0[k] = nv;
+            r0[k] = nr;
+            p0[k] = np;
+            g0[k] = ng;
+            nv += parts[k].gb.verts.size();
+            nr += parts[k].gb.ring_bbox.size();
+            np += parts[k].gb.part_ring.size() - 1;
+            ng += parts[k].gb.geom_bbox.size();
+            n_border += parts[k].n_border;
+        }
+        if (nv > std::numeric_limits<uint32_t>::max()) return fail(MOSAIC_E_WKB, "too many vertices");
+        gb.verts.resize(nv);
+        gb.ring_bbox.resize(nr);
+        gb.ring_start.resize(nr + 1);
+        gb.part_ring.resize(np + 1);
+        gb.geom_part.resize(ng + 1);
+        gb.geom_bbox.resize(ng);
+        parallel_for((int)parts.size(), [&](int k) {
+            const GeomBuilder& q = parts[(size_t)k].gb;
+            std::copy(q.verts.begin(), q.verts.end(), gb.verts.begin() + v0[k]);
+            std::copy(q.ring_bbox.begin(), q.ring_bbox.end(), gb.ring_bbox.begin() + r0[k]);
+            std::copy(q.geom_bbox.begin(), q.geom_bbox.end(), gb.geom_bbox.begin() + g0[k]);
+            for (size_t j = 1; j < q.ring_start.size(); j++) gb.ring_start[r0[k] + j] = q.ring_start[j] + (uint32_t)v0[k];
+            for (size_t j = 1; j < q.part_ring.size(); j++) gb.part_ring[p0[k] + j] = q.part_ring[j] + (uint32_t)r0[k];
+            for (size_t j = 1; j < q.geom_part.size(); j++) gb.geom_part[g0[k] + j] = q.geom_part[j] + (uint32_t)p0[k];
+        });
     }
     trace.mark("wkb parse");
     // distinct cells -> [first, count)
@@ -2968,6 +3059,12 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     raster::Builder rb;
     rb.hdr.resize(meta.size());
     bool rb_overflow = false;
+    // too many polygons for point-raster codes (H3): the join sorts points by tile and tests chips
+    // from LDS tile images or the chip table (join_binned.hip), not through chip rasters, so small
+    // rings (buildings) get none -- their direct ring walk is as short as a raster lookup
+    const int64_t min_segments = (grid == MOSAIC_GRID_H3 && n_polygons > (int32_t)tiles::kMaxRasterKeys)
+                                     ? std::max<int64_t>(c->raster_min_segments, 16)
+                                     : c->raster_min_segments;
     auto chip_rasters = [&]() {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
             std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), n_chips / 256));
@@ -2980,7 +3077,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 h.box = gb.geom_bbox[t];
                 h.cell_base = raster::kNoRaster;
                 uint2 d = ring_desc[t];
-                if (!(meta[t] & 1u) && d.y >= 2 && (int64_t)d.y - 1 >= c->raster_min_segments) {
+                if (!(meta[t] & 1u) && d.y >= 2 && (int64_t)d.y - 1 >= min_segments) {
                     // option raster_adaptive: small rings get small rasters (2 ceil(sqrt(segments))
                     // cells a side, at most "raster"), so tables of millions of small chips stay compact
                     int dims = c->raster;
@@ -3796,12 +3893,14 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             }
             tstop = nullptr;  // recorded after the first stream launch
         } else if (binned_used) {
-            c->last_kernel = (c->tile_images && ch->img_words.p) ? "k_join_tiles" : "k_join_binned";
+            // (k_join_tiles packs a chip index and a lane into 32 bits)
+            const bool use_img = c->tile_images && ch->img_words.p && ch->n_chips < ((int64_t)1 << 26);
+            c->last_kernel = use_img ? "k_join_tiles" : "k_join_binned";
             const uint32_t max_code = (uint32_t)ch->tile_stats[2] + 1u;
             for (int64_t lo = 0; lo < n; lo += c->bin_chunk) {
                 const int64_t hi = std::min<int64_t>(n, lo + c->bin_chunk);
                 binned::Images img;
-                if (c->tile_images && ch->img_words.p) {
+                if (use_img) {
                     img.words = (const uint32_t*)ch->img_words.p;
                     img.off = (const uint32_t*)ch->img_off.p;
                     img.max_words = ch->img_max_words;
