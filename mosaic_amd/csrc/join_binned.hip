@@ -148,8 +148,24 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
            fy <= __uint_as_float(cr[7]);
 }
 
+// the tile join's rare paths, as calls: their registers (the general JTS walk over the chip table,
+// the generic point -> chips path) do not count against the kernel's occupancy
+__device__ __noinline__ bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
+    return pip::contains(s, c, x, y);
+}
+__device__ __noinline__ uint2 tiled_cell_call(const JoinArgs& a, int64_t i, double x, double y, uint32_t code) {
+    uint32_t c0, c1;
+    tiled_cell(a, i, x, y, code, c0, c1);
+    return make_uint2(c0, c1);
+}
+__device__ __noinline__ uint2 probe_call(const JoinArgs& a, int64_t cell) {
+    uint32_t c0, c1;
+    probe(a, cell, c0, c1);
+    return make_uint2(c0, c1);
+}
+
 template <int CM, bool PAIRS, class P>
-__global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys,
                                                     const P* __restrict__ pts, int64_t n, const unsigned long long* n_skip,
                                                     binned::Images img, uint32_t img_words) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_t[];
@@ -200,6 +216,7 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
         const int wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
         const uint32_t* chips = im + im[2];
         const double* V = (const double*)(im + im[3]);
+        const uint16_t* rl = (const uint16_t*)(im + im[4]);  // envelope raster: list offsets, lists
         // the ring walk over the wave's buffered pairs, 64 at a time from the top of the buffer
         // (all of them when `all`); wave-uniform
         uint32_t sn = 0;
@@ -214,12 +231,12 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                     uint32_t key;
                     if (sc & kSurvGlobal) {  // a chip of the table (a run without an image, a hexagon off the window)
                         const uint32_t c = sc & ~kSurvGlobal;
-                        hit = pip::contains(a.store, c, qx, qy);
+                        hit = contains_call(a.store, c, qx, qy);
                         key = a.chip_meta[c] >> 1;
                     } else {
                         const uint32_t* cr = chips + 8u * sc;
                         const uint32_t vi = cr[1], vc = vi >> 16;
-                        hit = vc == binned::kImgGlobal ? pip::contains(a.store, cr[2], qx, qy)
+                        hit = vc == binned::kImgGlobal ? contains_call(a.store, cr[2], qx, qy)
                                                        : ringwalk::ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
                         key = cr[0] >> 1;
                     }
@@ -235,7 +252,8 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
             const int64_t i = g + lane;
             double x = 0.0, y = 0.0;
             int64_t row = -1;
-            uint32_t c0 = 0, c1 = 0;  // the point's chips: in the image, or (glob) in the chip table
+            uint32_t c0 = 0, c1 = 0;  // the point's candidates: envelope-raster list positions, or (glob) chips of the table
+            uint32_t slot = 0;        // its hexagon's window slot (image runs)
             bool glob = false;
             if (i < r1) {
                 const P p = pts[i];
@@ -243,26 +261,37 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                 y = p.y;
                 row = binned::row_of(p, i);
                 if (ioff == binned::kNoImage) {
-                    tiled_cell(a, i, x, y, code, c0, c1);
+                    const uint2 r = tiled_cell_call(a, i, x, y, code);
+                    c0 = r.x;
+                    c1 = r.y;
                     glob = true;
                 } else {
-                    double px, py, pz, vx, vy, best;
-                    h3::fast_unit(y, x, &px, &py, &pz);
-                    h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
-                    int ba, bb;
-                    if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
-                        const unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-                        if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-                    } else {
-                        const int ra = ba - tr.a0, rb = bb - tr.b0;
-                        if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
-                            const uint32_t slot = (uint32_t)(ra * wb + rb);
-                            const uint16_t* sf = (const uint16_t*)(im + 4);
-                            c0 = sf[slot];
-                            c1 = sf[slot + 1];
+                    // the raster cell (tile_of's arithmetic): chips whose envelope may hold the point
+                    const double fx = (x - a.tgrid.x0) * a.tgrid.sx, fy = (y - a.tgrid.y0) * a.tgrid.sy;
+                    const int gx = (int)((fx - (double)(int)fx) * (double)binned::kImgRaster);
+                    const int gy = (int)((fy - (double)(int)fy) * (double)binned::kImgRaster);
+                    const int q = min(gy, binned::kImgRaster - 1) * binned::kImgRaster + min(gx, binned::kImgRaster - 1);
+                    c0 = rl[q];
+                    c1 = rl[q + 1];
+                    if (c1 > c0) {  // (a point no envelope holds joins nothing: its hexagon is not needed)
+                        double px, py, pz, vx, vy, best;
+                        h3::fast_unit(y, x, &px, &py, &pz);
+                        h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
+                        int ba, bb;
+                        if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
+                            const unsigned long long qe = atomicAdd(a.amb_count, 1ULL);
+                            if (qe < a.amb_cap) a.amb_queue[qe] = (unsigned long long)i;
+                            c0 = c1 = 0;
                         } else {
-                            probe(a, (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res), c0, c1);
-                            glob = true;
+                            const int ra = ba - tr.a0, rb = bb - tr.b0;
+                            if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
+                                slot = (uint32_t)(ra * wb + rb);
+                            } else {
+                                const uint2 r = probe_call(a, (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res));
+                                c0 = r.x;
+                                c1 = r.y;
+                                glob = true;
+                            }
                         }
                     }
                 }
@@ -291,10 +320,12 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                 const double qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64);
                 const int64_t qrow = PAIRS ? (int64_t)__shfl((long long)row, owner, 64) : -1;
                 const bool qg = __shfl((int)glob, owner, 64) != 0;
+                const uint32_t qslot = (uint32_t)__shfl((int)slot, owner, 64);
                 bool surv = false;
-                if (live) {
-                    const uint32_t c = ent >> 6;
-                    const uint32_t* cr = chips + 8u * c;
+                uint32_t c = ent >> 6;  // glob: a chip of the table; else a list position
+                if (live && !qg) c = rl[c];
+                const uint32_t* cr = chips + 8u * c;
+                if (live && (qg || cr[3] == qslot)) {  // (image chips of another hexagon: no pair)
                     const uint32_t meta = qg ? a.chip_meta[c] : cr[0];
                     if (meta & 1u) {
                         emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
@@ -308,7 +339,7 @@ __global__ void __launch_bounds__(256) k_join_tiles(JoinArgs a, const uint32_t* 
                     const uint32_t e = sn + (uint32_t)__popcll(sm & lt_mask);
                     surv_x[wv][e] = qx;
                     surv_y[wv][e] = qy;
-                    surv_c[wv][e] = (ent >> 6) | (qg ? kSurvGlobal : 0u);
+                    surv_c[wv][e] = c | (qg ? kSurvGlobal : 0u);
                     if (PAIRS) surv_r[wv][e] = (long long)qrow;
                 }
                 sn += (uint32_t)__popcll(sm);
@@ -422,12 +453,12 @@ static inline float f32_up(double v) {
     return f;
 }
 
-// image of record r: its words (empty: kNoImage)
-static void tile_image(const ImageSource& s, size_t r, std::vector<uint32_t>& w) {
+// image of record r (tile (ti, tj) of the grid): its words (empty: kNoImage)
+static void tile_image(const ImageSource& s, size_t r, int ti, int tj, std::vector<uint32_t>& w) {
     w.clear();
     const tiles::TileRec& tr = s.recs[r];
     const uint32_t wa = (tr.dims >> 8) & 0xfffu, wb = tr.dims >> 20, ns = wa * wb;
-    if (ns == 0 || ns >= 0xffffu) return;
+    if (ns == 0 || ns >= 0xffffu || ti < 0) return;
     std::vector<uint32_t> first(ns + 1, 0);
     uint32_t nc = 0;
     for (uint32_t k = 0; k < ns; k++) {
@@ -436,17 +467,59 @@ static void tile_image(const ImageSource& s, size_t r, std::vector<uint32_t>& w)
         if (e) nc += s.table[e - 1].count;
     }
     first[ns] = nc;
+    if (nc >= 0xffffu) return;
+    // the envelope raster: per cell the chips whose envelope meets it (cell range of an envelope
+    // through tile_of's arithmetic; see join_binned.h)
+    const int G = kImgRaster;
+    auto cell_of = [&](double v, double v0, double sc, int t) {
+        const double f = (v - v0) * sc - (double)t;
+        const double c = floor(f * G);
+        return (int)std::min<double>(G - 1, std::max<double>(0.0, c));
+    };
+    std::vector<std::vector<uint16_t>> lists((size_t)G * G);
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < ns; k++) {
+        const uint32_t e = s.entries[tr.off + k];
+        if (!e) continue;
+        const HashEntry& he = s.table[e - 1];
+        for (uint32_t g = he.first; g < he.first + he.count; g++, c++) {
+            int x0 = 0, x1 = G - 1, y0 = 0, y1 = G - 1;
+            if (!(s.meta[g] & 1u)) {
+                const pip::Box& bx = s.store.geom_bbox[g];
+                if (!(bx.minx <= bx.maxx && bx.miny <= bx.maxy)) continue;  // empty: never contains
+                x0 = cell_of(bx.minx, s.grid.x0, s.grid.sx, ti);
+                x1 = cell_of(bx.maxx, s.grid.x0, s.grid.sx, ti);
+                y0 = cell_of(bx.miny, s.grid.y0, s.grid.sy, tj);
+                y1 = cell_of(bx.maxy, s.grid.y0, s.grid.sy, tj);
+            }
+            for (int gy = y0; gy <= y1; gy++)
+                for (int gx = x0; gx <= x1; gx++) lists[(size_t)gy * G + gx].push_back((uint16_t)c);
+        }
+    }
+    uint32_t n_ent = 0;
+    for (auto& l : lists) n_ent += (uint32_t)l.size();
     const uint32_t slot_words = (ns + 2) / 2;
-    const uint32_t chip_off = (4u + slot_words + 3u) & ~3u;
+    const uint32_t rast_off = kImgHdrWords + slot_words;
+    const uint32_t rast_words = ((uint32_t)(G * G + 1) + n_ent + 1) / 2;
+    const uint32_t chip_off = (rast_off + rast_words + 3u) & ~3u;
     const uint32_t vert_off = chip_off + 8u * nc;
-    if (nc >= 0xffffu || vert_off > kImgCapWords) return;
+    if (vert_off > kImgCapWords || (uint32_t)(G * G + 1) + n_ent >= 0xffffu) return;
     w.assign(vert_off, 0u);
     w[0] = ns | nc << 16;
     w[2] = chip_off;
     w[3] = vert_off;
-    uint16_t* sf = (uint16_t*)(w.data() + 4);
+    w[4] = rast_off;
+    uint16_t* sf = (uint16_t*)(w.data() + kImgHdrWords);
     for (uint32_t k = 0; k <= ns; k++) sf[k] = (uint16_t)first[k];
-    uint32_t nv = 0, c = 0;
+    uint16_t* rl = (uint16_t*)(w.data() + rast_off);
+    uint32_t pos = (uint32_t)(G * G + 1);
+    for (int q = 0; q < G * G; q++) {
+        rl[q] = (uint16_t)pos;
+        for (uint16_t v : lists[(size_t)q]) rl[pos++] = v;
+    }
+    rl[G * G] = (uint16_t)pos;
+    uint32_t nv = 0;
+    c = 0;
     for (uint32_t k = 0; k < ns; k++) {
         const uint32_t e = s.entries[tr.off + k];
         if (!e) continue;
@@ -455,6 +528,7 @@ static void tile_image(const ImageSource& s, size_t r, std::vector<uint32_t>& w)
             uint32_t* cr = &w[chip_off + 8u * c];
             cr[0] = s.meta[g];
             cr[2] = g;
+            cr[3] = k;
             const pip::Box& bx = s.store.geom_bbox[g];
             const float fb[4] = {f32_down(bx.minx), f32_down(bx.miny), f32_up(bx.maxx), f32_up(bx.maxy)};
             memcpy(cr + 4, fb, 16);
@@ -484,6 +558,9 @@ bool build_tile_images(const ImageSource& s, std::vector<uint32_t>& words, std::
                        uint32_t& max_words) {
     const size_t nr = s.n_recs;
     const int nt = std::max(1, std::min<int>(s.threads, (int)(nr / 64) + 1));
+    std::vector<int> tile_of_rec(nr, -1);  // record -> tile (ti + tj nx)
+    for (int64_t t = 0; t < (int64_t)s.grid.nx * s.grid.ny; t++)
+        if (s.tile_idx[t] >= 2 && s.tile_idx[t] - 2 < nr) tile_of_rec[s.tile_idx[t] - 2] = (int)t;
     std::vector<std::vector<uint32_t>> part((size_t)nt);
     std::vector<std::vector<uint32_t>> part_off((size_t)nt);
     std::vector<uint32_t> part_max((size_t)nt, 0);
@@ -492,7 +569,8 @@ bool build_tile_images(const ImageSource& s, std::vector<uint32_t>& words, std::
         auto& pw = part[(size_t)t];
         auto& po = part_off[(size_t)t];
         for (size_t r = nr * t / nt; r < nr * (t + 1) / nt; r++) {
-            tile_image(s, r, w);
+            const int t = tile_of_rec[r];
+            tile_image(s, r, t < 0 ? -1 : t % s.grid.nx, t < 0 ? -1 : t / s.grid.nx, w);
             if (w.empty()) {
                 po.push_back(kNoImage);
                 continue;

@@ -3519,6 +3519,8 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             binned::ImageSource is;
             is.recs = tb.recs.data();
             is.n_recs = tb.recs.size();
+            is.grid = tb.grid;
+            is.tile_idx = tb.tile_idx.data();
             is.entries = tb.entries.data();
             is.table = table.data();
             is.meta = meta.data();
