@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "join_common.h"
+#include "tile_images.h"
 
 namespace binned {
 
@@ -54,47 +55,6 @@ struct Scratch {
         for (Buf* b : {&keys[0], &keys[1], &vals[0], &vals[1], &temp, &n_skip}) b->release();
     }
 };
-
-// ---- per-tile chip images (the LDS tiles of k_join_tiles)
-// One image per tile record, copied whole into a workgroup's LDS for the sorted points of that
-// tile: its window's chip ranges, per chip (meta, geometry reference, hexagon, f32 envelope
-// rounded outwards), an envelope raster, and the rings of its one-ring border chips.  Layout
-// (32-bit words):
-//   [0] n_slots | n_chips << 16   [1] n_verts   [2] chip word offset   [3] vertex word offset
-//   [4] envelope-raster word offset   [5..7] 0
-//   [8 ..] slot_first: n_slots + 1 uint16 (chip index range of window slot s: [first[s], first[s+1]))
-//   envelope raster: kImgRaster^2 + 1 uint16 list offsets, then the lists (uint16 chip indices):
-//     cell (gx, gy) of the tile's kImgRaster x kImgRaster split lists every chip whose f64 envelope
-//     meets it (core chips: every cell), so a point tests only the chips listed for its cell
-//   chips (at a multiple of 4 words): 8 words each -- meta (polygon_key << 1 | is_core), vinfo
-//     (vertex offset | count << 16; count 0: no geometry (core chip), kImgGlobal: tested from the
-//     global geometry store), global chip index, window slot of its hexagon, f32 minx, miny, maxx,
-//     maxy (outward rounded)
-//   vertices (at a multiple of 4 words): double2, ring after ring (closed)
-// A point's raster cell is computed from its grid position exactly as its tile is
-// (tiles::tile_of): f = (x - x0) sx, cell floor((f - floor(f)) kImgRaster); the builder maps
-// envelope corners through the same arithmetic, which is monotone, so a point inside an envelope
-// lands in a cell that lists the chip.
-static const uint32_t kImgCapWords = 5120;     // 20 KB of LDS per workgroup: 4 workgroups per CU
-static const uint32_t kImgHdrWords = 8;
-static const int kImgRaster = 16;
-static const uint32_t kNoImage = 0xFFFFFFFFu;  // the record's chip records do not fit: generic path
-static const uint32_t kImgGlobal = 0xFFFFu;
-struct ImageSource {
-    const tiles::TileRec* recs;
-    size_t n_recs;
-    tiles::Grid grid;
-    const uint32_t* tile_idx;  // per tile: kSkip, kFull or record + 2
-    const uint32_t* entries;
-    const HashEntry* table;
-    const uint32_t* meta;
-    pip::GeomStore store;
-    int threads;
-};
-// words: the images back to back; off[r]: word offset of record r's image or kNoImage; max_words:
-// the largest image.  False when the images would pass 2^32 words.
-bool build_tile_images(const ImageSource& s, std::vector<uint32_t>& words, std::vector<uint32_t>& off,
-                       uint32_t& max_words);
 
 struct Images {
     const uint32_t* words = nullptr;  // nullptr: no images (k_join_binned runs)

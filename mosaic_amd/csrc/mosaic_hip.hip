@@ -3522,7 +3522,14 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             is.grid = tb.grid;
             is.tile_idx = tb.tile_idx.data();
             is.entries = tb.entries.data();
-            is.table = table.data();
+            std::vector<uint32_t> sfirst(capacity, 0), scount(capacity, 0);
+            for (uint64_t q = 0; q < capacity; q++)
+                if (table[q].key != kEmptyKey) {
+                    sfirst[q] = table[q].first;
+                    scount[q] = table[q].count;
+                }
+            is.slot_first = sfirst.data();
+            is.slot_count = scount.data();
             is.meta = meta.data();
             is.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(), gb.part_ring.data(),
                                       gb.geom_part.data(), gb.geom_bbox.data()};

@@ -120,3 +120,29 @@ def test_ring_walks_match_jts(tmp_path):
                     "-o", str(exe), os.path.join(root, "tests", "native", "ring_walk_check.cpp")], check=True)
     cases, bad = map(int, subprocess.run([str(exe), "20000"], check=True, capture_output=True, text=True).stdout.split())
     assert cases > 1_000_000 and bad == 0
+
+
+def test_tile_images(tmp_path):
+    """CPU: the binned join's tile images (tile_images.h) for 20k C4-style buildings at H3 res 11
+    and the NYC zones at res 10 -- chip records equal the chip table, and every chip whose envelope
+    holds a point (random tile points, tile edges, envelope corners and edge midpoints) is listed in
+    the point's envelope-raster cell as k_join_tiles computes it"""
+    from mosaic_amd.data import synthetic_buildings
+    exe = tmp_path / "tic"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wno-unknown-pragmas", "-pthread", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "native", "tile_images_check.cpp")], check=True)
+    for name, polys, res in (("bld", synthetic_buildings(20000), 11),
+                             ("nyc", PolygonSet.load("nyc_taxi_zones_35"), 10)):
+        chips = tessellate("H3", polys, res)
+        path = tmp_path / f"{name}.bin"
+        offs, data = chips["wkb"]
+        with open(path, "wb") as f:
+            f.write(struct.pack("<iI", res, len(chips["index_id"])))
+            for i in range(len(chips["index_id"])):
+                w = bytes(data[offs[i]:offs[i + 1]])
+                f.write(struct.pack("<qBiI", int(chips["index_id"][i]), int(chips["is_core"][i]),
+                                    int(chips["polygon_key"][i]), len(w)))
+                f.write(w)
+        out = subprocess.run([str(exe), str(path), "32"], check=True, capture_output=True, text=True).stdout.split()
+        recs, imaged, checked, bad = map(int, out)
+        assert recs > 100 and imaged > recs // 2 and checked > 20_000 and bad == 0, (name, out)
