@@ -46,20 +46,25 @@ struct Buf {
 };
 
 struct Scratch {
-    Buf keys[2], vals[2], temp, n_skip;
+    Buf keys[2], vals[2], temp, n_skip, status;
     JoinArgs exact_args;  // the join's arguments as the exact-H3 pass must read them (sorted points)
     size_t held() const {
-        return keys[0].bytes + keys[1].bytes + vals[0].bytes + vals[1].bytes + temp.bytes + n_skip.bytes;
+        return keys[0].bytes + keys[1].bytes + vals[0].bytes + vals[1].bytes + temp.bytes + n_skip.bytes + status.bytes;
     }
     void release() {
-        for (Buf* b : {&keys[0], &keys[1], &vals[0], &vals[1], &temp, &n_skip}) b->release();
+        for (Buf* b : {&keys[0], &keys[1], &vals[0], &vals[1], &temp, &n_skip, &status}) b->release();
     }
 };
 
+// the device copy of a tile_images.h ImageSet
 struct Images {
-    const uint32_t* words = nullptr;  // nullptr: no images (k_join_binned runs)
-    const uint32_t* off = nullptr;
+    const uint32_t* words = nullptr;  // nullptr: no images (k_bin_keys and k_join_binned run)
+    const uint32_t* off = nullptr;    // per image key - 2
+    const uint32_t* rec = nullptr;    // per image key - 2: the tile record
+    const uint32_t* rec_key = nullptr;  // per record: first image << 2 | level
+    const uint32_t* cover = nullptr;  // kImgCoverWords per record
     uint32_t max_words = 0;
+    uint32_t n_images = 0;
 };
 
 // Rows [lo, n) of a.x / a.y: key, sort, join (enqueued on stream).  max_code: the largest tile code

@@ -68,6 +68,197 @@ __global__ void __launch_bounds__(256) k_bin_keys(JoinArgs a, int64_t lo, int64_
     if ((threadIdx.x & 63) == 0 && skipped) atomicAdd(n_skip, (unsigned long long)skipped);
 }
 
+// ---- k_bin_cover: k_bin_keys for tile-image tables, keeping only the points some chip may hold
+// (tile code not kSkip, and for an imaged record a set cover bit of the point's envelope-raster cell,
+// tile_images.h), compacted in one pass: workgroup b takes kBinChunk consecutive points, counts the
+// kept ones and finds its output offset by decoupled look-back over the earlier workgroups' status
+// words (flag | count: an aggregate published at once, then the inclusive prefix), so the sort and
+// the join see only the kept points.  Workgroups are dispatched in index order, so every status a
+// workgroup waits on belongs to a running workgroup that publishes its aggregate without waiting on
+// anything; the wait is still bounded (kBinSpinCap polls; then *err is set and the caller reruns
+// the uncompacted k_bin_keys).
+static const int kBinPPT = 8;  // points per thread
+static const int kBinChunk = 256 * kBinPPT;
+static const unsigned long long kStAgg = 1ULL << 62, kStPre = 2ULL << 62, kStVal = (1ULL << 62) - 1;
+static const int kBinSpinCap = 1 << 20;
+
+// status words: one 8-byte word carries flag and count, so there is no payload to order; stores and
+// polls go to memory (system scope: sc0 sc1), never to a stale L2 line of another XCD
+__device__ __forceinline__ void st_publish(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long st_poll(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// (explicit pointers and grid, not JoinArgs: they stay in scalar registers; every load is issued
+// before the first use, with clamped indices instead of branches)
+// Keys: kSkip (dropped), kFull, or the image key of the point's record part (tile_images.h:
+// 2 + first image of the record + image_part of its raster cell).  COMPACT false (the fallback
+// after a look-back failure): every point at its own position, dropped ones keyed kSkip (sorted
+// first; *total counts them).
+template <class P, bool VEC, bool COMPACT>
+__global__ void __launch_bounds__(256) k_bin_cover(const double* __restrict__ X, const double* __restrict__ Y,
+                                                   tiles::Grid g, const uint32_t* __restrict__ tidx,
+                                                   const uint32_t* __restrict__ cover, const uint32_t* __restrict__ rec_key,
+                                                   int64_t lo, int64_t n, uint32_t* keys, P* pts,
+                                                   unsigned long long* status, unsigned long long* total, unsigned int* err) {
+    __shared__ uint32_t woff[kBinPPT * 4];  // per (item, wave): kept count, then output offset in the workgroup
+    __shared__ unsigned long long base_s;
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int64_t b = blockIdx.x;
+    const int64_t cs = lo + b * kBinChunk;
+    // item k of this thread: point cs + 2 (k/2 256 + t) + k%2 (VEC: 16-byte loads of both columns)
+    // or cs + k 256 + t
+    auto item = [&](int k) -> int64_t {
+        return VEC ? cs + 2 * ((int64_t)(k >> 1) * 256 + threadIdx.x) + (k & 1) : cs + (int64_t)k * 256 + threadIdx.x;
+    };
+    double xs[kBinPPT], ys[kBinPPT];
+    if (VEC) {
+        // (n - lo >= 2: the caller's condition) the last pair start with both points in range
+        const int64_t vlast = lo + (((n - lo) >> 1) - 1) * 2;
+#pragma unroll
+        for (int k = 0; k < kBinPPT; k += 2) {
+            const int64_t i0 = item(k), li = i0 < vlast ? i0 : vlast;
+            const v2d x = __builtin_nontemporal_load((const v2d*)(X + li)), y = __builtin_nontemporal_load((const v2d*)(Y + li));
+            xs[k] = x.x;
+            xs[k + 1] = x.y;
+            ys[k] = y.x;
+            ys[k + 1] = y.y;
+        }
+        if ((n - lo) & 1) {  // an odd last point: its own loads (last workgroup only)
+#pragma unroll
+            for (int k = 0; k < kBinPPT; k += 2)
+                if (item(k) == n - 1) {
+                    xs[k] = X[n - 1];
+                    ys[k] = Y[n - 1];
+                }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kBinPPT; k++) {
+            const int64_t i = item(k) < n ? item(k) : n - 1;
+            xs[k] = X[i];
+            ys[k] = Y[i];
+        }
+    }
+    // tile codes (tiles::tile_of, its gather issued for every item before any is used)
+    uint32_t code[kBinPPT], cw[kBinPPT];
+    int q[kBinPPT];
+#pragma unroll
+    for (int k = 0; k < kBinPPT; k++) {
+        // (tiles::tile_of's code; the envelope-raster cell as k_join_tiles computes it)
+        const binned::BinCell bc = binned::bin_cell(g, xs[k], ys[k]);
+        code[k] = tidx[bc.slot];
+        if (!bc.in) code[k] = (isfinite(xs[k]) && isfinite(ys[k])) ? tiles::kSkip : tiles::kFull;
+        if (item(k) >= n) code[k] = tiles::kSkip;
+        q[k] = bc.q;
+    }
+    // cover words and image keys (records: codes >= 2)
+    uint32_t rk[kBinPPT];
+#pragma unroll
+    for (int k = 0; k < kBinPPT; k++) {
+        const bool rec = code[k] >= 2u;
+        const uint32_t r = rec ? code[k] - 2u : 0u;
+        cw[k] = cover[(size_t)r * binned::kImgCoverWords + (uint32_t)(q[k] >> 5)];
+        rk[k] = rec_key[r];
+        if (!rec) cw[k] = ~0u;
+    }
+    unsigned long long mk[kBinPPT];
+#pragma unroll
+    for (int k = 0; k < kBinPPT; k++) {
+        const bool keep = code[k] != tiles::kSkip && ((cw[k] >> (q[k] & 31)) & 1u);
+        code[k] = binned::bin_key(code[k], rk[k], q[k]);
+        if (!COMPACT) {
+            if (!keep) code[k] = tiles::kSkip;
+            mk[k] = __ballot(item(k) < n && !keep);  // (dropped, counted)
+            continue;
+        }
+        mk[k] = __ballot(keep);
+        if (lane == 0) woff[k * 4 + wv] = (uint32_t)__popcll(mk[k]);
+    }
+    if (!COMPACT) {
+        unsigned int dropped = 0;
+#pragma unroll
+        for (int k = 0; k < kBinPPT; k++) {
+            dropped += (uint32_t)__popcll(mk[k]);
+            const int64_t i = item(k);
+            if (i < n) {
+                keys[i - lo] = code[k];
+                P p;
+                p.x = xs[k];
+                p.y = ys[k];
+                binned::set_row(p, i);
+                pts[i - lo] = p;
+            }
+        }
+        if (lane == 0 && dropped) atomicAdd(total, (unsigned long long)dropped);
+        return;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        // offsets in (item, wave) order, the workgroup's count T
+        const uint32_t c = lane < kBinPPT * 4 ? woff[lane] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (int d = 1; d < 32; d <<= 1) {
+            const uint32_t t = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += t;
+        }
+        if (lane < kBinPPT * 4) woff[lane] = incl - c;
+        const unsigned long long T = (unsigned long long)__shfl(incl, 31, 64);
+        // decoupled look-back: lane l reads workgroup j - l's status
+        unsigned long long excl = 0;
+        if (b > 0) {
+            if (lane == 0) st_publish(&status[b], kStAgg | T);
+            int64_t j = b - 1;
+            int spins = 0;
+            for (;;) {  // wave-uniform
+                const int64_t k = j - lane;
+                unsigned long long st = k >= 0 ? st_poll(&status[k]) : kStPre;
+                while (__ballot((st >> 62) == 0)) {
+                    if (++spins > kBinSpinCap) {  // (never expected: see above)
+                        if (lane == 0) atomicOr(err, 1u);
+                        if ((st >> 62) == 0) st = kStPre;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    if ((st >> 62) == 0) st = st_poll(&status[k]);
+                }
+                const unsigned long long pm = __ballot((st >> 62) == 2);
+                const int stop = pm ? __ffsll((long long)pm) - 1 : 63;
+                unsigned long long v = lane <= stop ? (st & kStVal) : 0ULL;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+                excl += v;
+                if (pm) break;
+                j -= 64;
+            }
+        }
+        if (lane == 0) {
+            st_publish(&status[b], kStPre | (excl + T));
+            base_s = excl;
+            if (b == (int64_t)gridDim.x - 1) *total = excl + T;
+        }
+    }
+    __syncthreads();
+    const unsigned long long base = base_s;
+#pragma unroll
+    for (int k = 0; k < kBinPPT; k++) {
+        if ((mk[k] >> lane) & 1ULL) {
+            const int64_t i = item(k);
+            const unsigned long long o = base + woff[k * 4 + wv] + (unsigned long long)__popcll(mk[k] & lt_mask);
+            keys[o] = code[k];
+            P p;
+            p.x = xs[k];
+            p.y = ys[k];
+            binned::set_row(p, i);
+            pts[o] = p;
+        }
+    }
+}
+
 // Waves take chunks of kChunkIters x 64 consecutive sorted points (chunk c by wave c mod W), so a
 // wave stays inside one tile for many groups and its per-wave count hash sees few keys.
 static const int kChunkIters = 16;
@@ -138,8 +329,16 @@ __global__ void __launch_bounds__(256) k_join_binned(JoinArgs a, const uint32_t*
 // buffer whose full sets of 64 run the ring walk -- no lane of a ring-walking wave idles on a pair
 // the envelope already rejected.
 static const int kSegPoints = 2048;
+
 static const int kSurv = 128;  // per wave: surviving pairs (64 appended at most before a flush)
 static const uint32_t kSurvGlobal = 0x80000000u;  // a buffered pair's chip is in the chip table
+// a hit of the tile join's count mode kCountChips: image chip sc (kSurvGlobal: chip of the table)
+__device__ __forceinline__ void tile_hit(const JoinArgs& a, unsigned int* ccnt, uint32_t sc, uint32_t key) {
+    if (sc & 0x80000000u)
+        atomicAdd(&a.counts[key], 1ULL);
+    else
+        atomicAdd(&ccnt[sc], 1u);
+}
 
 // false only when (x, y) lies outside the chip's f64 envelope (the f32 box is rounded outwards and
 // rounding is monotone, so fx, fy of a point inside the f64 box are inside the f32 box)
@@ -148,26 +347,28 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
            fy <= __uint_as_float(cr[7]);
 }
 
-// the tile join's rare paths, as calls: their registers (the general JTS walk over the chip table,
-// the generic point -> chips path) do not count against the kernel's occupancy
-__device__ __noinline__ bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
+// the tile join's rare paths (inlined: as calls they cost the kernel 18 % -- call-site register
+// saves and spills -- on C4)
+#define MOSAIC_TJ_NOINLINE __device__ __forceinline__
+MOSAIC_TJ_NOINLINE bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
     return pip::contains(s, c, x, y);
 }
-__device__ __noinline__ uint2 tiled_cell_call(const JoinArgs& a, int64_t i, double x, double y, uint32_t code) {
+MOSAIC_TJ_NOINLINE uint2 tiled_cell_call(const JoinArgs& a, int64_t i, double x, double y, uint32_t code) {
     uint32_t c0, c1;
     tiled_cell(a, i, x, y, code, c0, c1);
     return make_uint2(c0, c1);
 }
-__device__ __noinline__ uint2 probe_call(const JoinArgs& a, int64_t cell) {
+MOSAIC_TJ_NOINLINE uint2 probe_call(const JoinArgs& a, int64_t cell) {
     uint32_t c0, c1;
     probe(a, cell, c0, c1);
     return make_uint2(c0, c1);
 }
 
+// (occupancy 4: 128 VGPRs; C4 1e6 measured 23.4 ms against 28.7 unconstrained and 27.1 at 5)
 template <int CM, bool PAIRS, class P>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys,
-                                                    const P* __restrict__ pts, int64_t n, const unsigned long long* n_skip,
-                                                    binned::Images img, uint32_t img_words) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict__ pts, int64_t n,
+             const unsigned long long* n_skip, binned::Images img, uint32_t img_words) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_t[];
     __shared__ uint32_t pairs_all[4 * 64];  // per wave: a window of (point lane, chip) pairs
     __shared__ double surv_x[4][kSurv], surv_y[4][kSurv];
@@ -178,15 +379,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     const int wv = (int)(threadIdx.x >> 6) & 3;
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     uint32_t* im = lds_t;
-    unsigned int* cnt = lds_t + img_words;
+    unsigned int* cnt = lds_t + img_words;  // kCountLds: per polygon; kCountChips: per image chip
     if (CM == kCountLds) {
         for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x) cnt[k] = 0;
-    } else if (CM == kCountWaveHash) {
-        cnt += wv * kWaveHashWords;
-        for (int k = lane; k < kWaveHashWords; k += 64) cnt[k] = 0;
+    } else if (CM == kCountChips) {
+        for (int k = threadIdx.x; k < (int)binned::kImgMaxChips; k += blockDim.x) cnt[k] = 0;
     }
     __syncthreads();
     unsigned int tests = 0;
+#ifdef MOSAIC_TJ_STAT
+    unsigned int stat = 0;
+#endif
     const int64_t s0 = (int64_t)*n_skip + (int64_t)blockIdx.x * kSegPoints;
     const int64_t s1 = s0 + kSegPoints < n ? s0 + kSegPoints : n;
     for (int64_t pos = s0; pos < s1;) {  // block-uniform: one run of equal tile code per iteration
@@ -202,12 +405,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             if (found) break;
         }
         const int64_t r1 = (int64_t)run_end_s;
-        const uint32_t ioff = (code >= 2 && img.off) ? img.off[code - 2] : binned::kNoImage;
+        // the run's image key -> image, tile record (tcode: its tile code, for the generic path)
+        const uint32_t ioff = code >= 2 ? img.off[code - 2] : binned::kNoImage;
+        const uint32_t tcode = code >= 2 ? img.rec[code - 2] + 2u : code;
         tiles::TileRec tr{0, 0, 0, 0};
         if (ioff != binned::kNoImage) {
-            tr = a.tile_rec[code - 2];
+            tr = a.tile_rec[tcode - 2];
             const uint32_t* src = img.words + ioff;
-            const uint32_t nw = src[3] + 4u * src[1];  // vertex offset + vertex words
+            const uint32_t nw = (src[3] + 2u * src[1] + 3u) & ~3u;  // vertex offset + vertex words (padded)
             for (uint32_t k = 4u * threadIdx.x; k < nw; k += 4u * blockDim.x)
                 *(uint4*)(im + k) = *(const uint4*)(src + k);
             __syncthreads();
@@ -215,7 +420,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         const int face = (int)(tr.dims & 0xffu);
         const int wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
         const uint32_t* chips = im + im[2];
-        const double* V = (const double*)(im + im[3]);
+        const float* V = (const float*)(im + im[3]);
         const uint16_t* rl = (const uint16_t*)(im + im[4]);  // envelope raster: list offsets, lists
         // the ring walk over the wave's buffered pairs, 64 at a time from the top of the buffer
         // (all of them when `all`); wave-uniform
@@ -224,6 +429,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             while (sn >= 64 || (all && sn > 0)) {
                 const uint32_t m = sn < 64u ? sn : 64u;
                 if ((uint32_t)lane < m) {
+#ifdef MOSAIC_TJ_STAT
+                    if (MOSAIC_TJ_STAT == 1) stat++;
+#endif
                     const uint32_t e = sn - m + (uint32_t)lane;
                     const double qx = surv_x[wv][e], qy = surv_y[wv][e];
                     const uint32_t sc = surv_c[wv][e];
@@ -231,16 +439,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
                     uint32_t key;
                     if (sc & kSurvGlobal) {  // a chip of the table (a run without an image, a hexagon off the window)
                         const uint32_t c = sc & ~kSurvGlobal;
+#ifdef MOSAIC_TJ_STAT
+                        if (MOSAIC_TJ_STAT == 2) stat++;
+                        hit = MOSAIC_TJ_STAT == 3 ? false : contains_call(a.store, c, qx, qy);
+#else
                         hit = contains_call(a.store, c, qx, qy);
+#endif
                         key = a.chip_meta[c] >> 1;
                     } else {
                         const uint32_t* cr = chips + 8u * sc;
                         const uint32_t vi = cr[1], vc = vi >> 16;
-                        hit = vc == binned::kImgGlobal ? contains_call(a.store, cr[2], qx, qy)
-                                                       : ringwalk::ring_interior(V + 2u * (vi & 0xffffu), vc, qx, qy);
+                        int r = 2;
+                        if (vc != binned::kImgGlobal)
+                            r = ringwalk::ring_interior_f32(V + 2u * (vi & 0xffffu), vc,
+                                                            ringwalk::f32_frame(__uint_as_float(cr[4]), __uint_as_float(cr[5]),
+                                                                                __uint_as_float(cr[6]), __uint_as_float(cr[7]), qx, qy));
+                        // (global geometry, or a point the f32 walk leaves undecided: the f64 test)
+#ifdef MOSAIC_TJ_STAT
+                        if (MOSAIC_TJ_STAT == 2 && r == 2) stat++;
+                        if (MOSAIC_TJ_STAT == 4 && vc == binned::kImgGlobal) stat++;
+                        hit = r == 2 ? (MOSAIC_TJ_STAT == 3 ? false : contains_call(a.store, cr[2], qx, qy)) : r == 1;
+#else
+                        hit = r == 2 ? contains_call(a.store, cr[2], qx, qy) : r == 1;
+#endif
                         key = cr[0] >> 1;
                     }
-                    if (hit) emit_hit<CM, PAIRS>(a, PAIRS ? (int64_t)surv_r[wv][e] : -1, key, cnt);
+                    if (hit) {
+                        if (CM == kCountChips)
+                            tile_hit(a, cnt, sc, key);
+                        else
+                            emit_hit<CM, PAIRS>(a, PAIRS ? (int64_t)surv_r[wv][e] : -1, key, cnt);
+                    }
                 }
                 sn -= m;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -261,16 +490,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
                 y = p.y;
                 row = binned::row_of(p, i);
                 if (ioff == binned::kNoImage) {
-                    const uint2 r = tiled_cell_call(a, i, x, y, code);
+                    const uint2 r = tiled_cell_call(a, i, x, y, tcode);
                     c0 = r.x;
                     c1 = r.y;
                     glob = true;
                 } else {
-                    // the raster cell (tile_of's arithmetic): chips whose envelope may hold the point
-                    const double fx = (x - a.tgrid.x0) * a.tgrid.sx, fy = (y - a.tgrid.y0) * a.tgrid.sy;
-                    const int gx = (int)((fx - (double)(int)fx) * (double)binned::kImgRaster);
-                    const int gy = (int)((fy - (double)(int)fy) * (double)binned::kImgRaster);
-                    const int q = min(gy, binned::kImgRaster - 1) * binned::kImgRaster + min(gx, binned::kImgRaster - 1);
+                    // the raster cell (k_bin_cover's arithmetic): chips whose envelope may hold the point
+                    const int q = binned::bin_cell(a.tgrid, x, y).q;
                     c0 = rl[q];
                     c1 = rl[q + 1];
                     if (c1 > c0) {  // (a point no envelope holds joins nothing: its hexagon is not needed)
@@ -328,7 +554,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
                 if (live && (qg || cr[3] == qslot)) {  // (image chips of another hexagon: no pair)
                     const uint32_t meta = qg ? a.chip_meta[c] : cr[0];
                     if (meta & 1u) {
-                        emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
+                        if (CM == kCountChips)
+                            tile_hit(a, cnt, c | (qg ? kSurvGlobal : 0u), meta >> 1);
+                        else
+                            emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
                     } else {
                         tests++;
                         surv = qg ? !pip::box_excludes(a.store.geom_bbox[c], qx, qy) : fbox_in(cr, (float)qx, (float)qy);
@@ -348,14 +577,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if (sn >= 64) ring_tests(false);
             }
-            if (CM == kCountWaveHash) wave_hash_flush(a, cnt, false);
         }
         ring_tests(true);  // the run's last buffered pairs, while its image is in LDS
-        if (CM == kCountWaveHash) wave_hash_flush(a, cnt, false);
         __syncthreads();  // every wave is done with this run's image
+        if (CM == kCountChips && ioff != binned::kNoImage) {
+            // the run's chip counts to their polygons (before the next run's image replaces the chips)
+            const uint32_t nc = im[0];
+            for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
+                const uint32_t v = cnt[k];
+                if (v) {
+                    atomicAdd(&a.counts[chips[8u * k] >> 1], (unsigned long long)v);
+                    cnt[k] = 0;
+                }
+            }
+        }
         pos = r1;
     }
-    if (CM == kCountWaveHash) wave_hash_flush(a, cnt, true);
+#ifdef MOSAIC_TJ_STAT
+    tests = MOSAIC_TJ_STAT == 3 ? tests : stat;
+#endif
     for (int off = 32; off > 0; off >>= 1) tests += __shfl_down(tests, off, 64);
     if (lane == 0 && tests) atomicAdd(a.tests, (unsigned long long)tests);
     if (CM == kCountLds) {
@@ -370,22 +610,60 @@ namespace binned {
 template <class P>
 static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint32_t max_code, int cm, int n_cu,
                                 const Images& img, Scratch& s, hipStream_t stream) {
-    const int64_t m = n - lo;
+    int64_t m = n - lo;
     const size_t vb = sizeof(P);
     hipError_t e;
+    const int64_t nb = (m + kBinChunk - 1) / kBinChunk;
     if ((e = s.keys[0].reserve((size_t)m * 4)) || (e = s.keys[1].reserve((size_t)m * 4)) ||
-        (e = s.vals[0].reserve((size_t)m * vb)) || (e = s.vals[1].reserve((size_t)m * vb)) || (e = s.n_skip.reserve(8)))
+        (e = s.vals[0].reserve((size_t)m * vb)) || (e = s.vals[1].reserve((size_t)m * vb)) || (e = s.n_skip.reserve(32)) ||
+        (img.words && (e = s.status.reserve((size_t)std::max<int64_t>(nb, 1) * 8))))
         return e;
-    if ((e = hipMemsetAsync(s.n_skip.p, 0, 8, stream))) return e;
+    // n_skip words: [0] kSkip rows (k_bin_keys) or kept rows (k_bin_cover), [1] 0, [2] look-back failure
+    if ((e = hipMemsetAsync(s.n_skip.p, 0, 32, stream))) return e;
     unsigned long long* nsk = (unsigned long long*)s.n_skip.p;
-    const int gk = (int)std::max<int64_t>(1, std::min<int64_t>((m + 511) / 512, (int64_t)n_cu * 16));
-    if ((((uintptr_t)(a0.x + lo) | (uintptr_t)(a0.y + lo)) & 15) == 0)
-        hipLaunchKernelGGL((k_bin_keys<P, true>), dim3(gk), dim3(256), 0, stream, a0, lo, n, (uint32_t*)s.keys[0].p,
-                           (P*)s.vals[0].p, nsk);
-    else
-        hipLaunchKernelGGL((k_bin_keys<P, false>), dim3(gk), dim3(256), 0, stream, a0, lo, n, (uint32_t*)s.keys[0].p,
-                           (P*)s.vals[0].p, nsk);
-    if ((e = hipGetLastError())) return e;
+    const bool vec = (((uintptr_t)(a0.x + lo) | (uintptr_t)(a0.y + lo)) & 15) == 0;
+    bool keyed = false;  // keys from k_bin_cover (image keys)
+    if (img.words && m > 0) {
+        if ((e = hipMemsetAsync(s.status.p, 0, (size_t)nb * 8, stream))) return e;
+        unsigned int* err = (unsigned int*)(nsk + 2);
+        unsigned long long* st = (unsigned long long*)s.status.p;
+#define MOSAIC_BIN_COVER(VEC, COMPACT)                                                                                \
+    hipLaunchKernelGGL((k_bin_cover<P, VEC, COMPACT>), dim3(nb), dim3(256), 0, stream, a0.x, a0.y, a0.tgrid, a0.tile_idx, \
+                       img.cover, img.rec_key, lo, n, (uint32_t*)s.keys[0].p, (P*)s.vals[0].p, st, nsk, err)
+        if (vec && m >= 2)
+            MOSAIC_BIN_COVER(true, true);
+        else
+            MOSAIC_BIN_COVER(false, true);
+        if ((e = hipGetLastError())) return e;
+        unsigned long long hw[3];
+        if ((e = hipMemcpyAsync(hw, nsk, sizeof hw, hipMemcpyDeviceToHost, stream)) || (e = hipStreamSynchronize(stream)))
+            return e;
+        if (hw[2] == 0 && hw[0] <= (unsigned long long)m) {
+            m = (int64_t)hw[0];
+            nsk += 1;  // the join starts at sorted row 0
+        } else {
+            // the look-back gave up: every row in place, dropped rows keyed kSkip (counted in word 0)
+            if ((e = hipMemsetAsync(s.n_skip.p, 0, 32, stream))) return e;
+            if (vec && m >= 2)
+                MOSAIC_BIN_COVER(true, false);
+            else
+                MOSAIC_BIN_COVER(false, false);
+            if ((e = hipGetLastError())) return e;
+        }
+#undef MOSAIC_BIN_COVER
+        keyed = true;
+        max_code = img.n_images + 1u;
+    }
+    if (!keyed) {
+        const int gk = (int)std::max<int64_t>(1, std::min<int64_t>((m + 511) / 512, (int64_t)n_cu * 16));
+        if (vec)
+            hipLaunchKernelGGL((k_bin_keys<P, true>), dim3(gk), dim3(256), 0, stream, a0, lo, n, (uint32_t*)s.keys[0].p,
+                               (P*)s.vals[0].p, nsk);
+        else
+            hipLaunchKernelGGL((k_bin_keys<P, false>), dim3(gk), dim3(256), 0, stream, a0, lo, n, (uint32_t*)s.keys[0].p,
+                               (P*)s.vals[0].p, nsk);
+        if ((e = hipGetLastError())) return e;
+    }
     // the key's significant bits (codes <= max_code)
     int end_bit = 1;
     while (end_bit < 32 && (max_code >> end_bit)) end_bit++;
@@ -411,14 +689,14 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
         // one workgroup per kSegPoints sorted points (those past the kSkip prefix exit at once)
         const uint32_t iw = (img.max_words + 3u) & ~3u;
         const int gt = (int)std::max<int64_t>(1, (m + kSegPoints - 1) / kSegPoints);
-        const size_t cw = pairs ? 0 : (cm == kCountLds ? (size_t)a.n_polygons : (size_t)(blk / 64) * kWaveHashWords);
+        const size_t cw = pairs ? 0 : (cm == kCountLds ? (size_t)a.n_polygons : (size_t)binned::kImgMaxChips);
         const size_t shm = ((size_t)iw + cw) * 4;
         if (pairs)
             hipLaunchKernelGGL((k_join_tiles<kCountGlobal, true, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw);
         else if (cm == kCountLds)
             hipLaunchKernelGGL((k_join_tiles<kCountLds, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw);
         else
-            hipLaunchKernelGGL((k_join_tiles<kCountWaveHash, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk,
+            hipLaunchKernelGGL((k_join_tiles<kCountChips, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk,
                                img, iw);
     } else if (pairs) {
         hipLaunchKernelGGL((k_join_binned<kCountGlobal, true, P>), dim3(gj), dim3(blk), 0, stream, a, keys, pts, m, nsk);

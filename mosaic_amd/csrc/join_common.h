@@ -82,6 +82,9 @@ struct JoinArgs {
 // hash of (key, count) flushed with one global atomic per distinct key (k_join_binned: many
 // polygons, but the few keys of a tile's points).
 static const int kCountGlobal = 0, kCountLds = 1, kCountWaveHash = 2;
+// k_join_tiles only: per image chip LDS counters, added to the chip's polygon count when the run
+// ends (hits on chips of the table: global atomics)
+static const int kCountChips = 3;
 static const int kWaveHashSlots = 256;  // per wave: keys[256] (key + 1, 0 = empty), counts[256], fill
 static const int kWaveHashWords = 2 * kWaveHashSlots + 1;
 

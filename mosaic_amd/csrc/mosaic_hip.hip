@@ -1932,9 +1932,11 @@ struct mosaic_chips {
     bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
     StreamArgs stream{};
     DevBuf rsub, rmid, rblocks, rquad, rqrec;  // rmid: per-tile leaf block bases; rqrec: quad records
-    DevBuf img_words, img_off;  // per-tile chip images of the binned join (join_binned.h); empty: none
+    // per-tile chip images of the binned join (tile_images.h ImageSet); empty: none
+    DevBuf img_words, img_off, img_rec, img_key, img_cover;
     uint32_t img_max_words = 0;
-    int64_t img_records = 0;
+    int64_t img_records = 0;  // images built (parts of tile records; tile_images.h)
+    int64_t img_count = 0;    // image keys (with the parts that have no image)
     int64_t raster_stats[6] = {0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
                                                    // line sub-blocks
     // build cost (ms): chip table core (hash, geometry, chip rasters), tile directory, point-raster
@@ -1945,7 +1947,7 @@ struct mosaic_chips {
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
                           &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell,
-                          &img_words, &img_off})
+                          &img_words, &img_off, &img_rec, &img_key, &img_cover})
             b->release();
         store.release();
     }
@@ -3534,19 +3536,23 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             is.store = pip::GeomStore{gb.verts.data(), gb.ring_start.data(), gb.ring_bbox.data(), gb.part_ring.data(),
                                       gb.geom_part.data(), gb.geom_bbox.data()};
             is.threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-            std::vector<uint32_t> iwords, ioff;
-            uint32_t imax = 0;
-            if (binned::build_tile_images(is, iwords, ioff, imax) && !iwords.empty()) {
-                if ((rc = ch->img_words.reserve(iwords.size() * 4)) || (rc = ch->img_off.reserve(ioff.size() * 4))) {
-                    ch->release_all();
-                    delete ch;
-                    return rc;
+            binned::ImageSet iset;
+            if (binned::build_tile_images(is, iset) && !iset.words.empty()) {
+                const std::vector<uint32_t>* src[5] = {&iset.words, &iset.off, &iset.rec, &iset.rec_key, &iset.cover};
+                DevBuf* dst[5] = {&ch->img_words, &ch->img_off, &ch->img_rec, &ch->img_key, &ch->img_cover};
+                for (int k = 0; k < 5; k++) {
+                    if ((rc = dst[k]->reserve(src[k]->size() * 4))) {
+                        ch->release_all();
+                        delete ch;
+                        return rc;
+                    }
+                    HIP_TRY(hipMemcpy(dst[k]->p, src[k]->data(), src[k]->size() * 4, hipMemcpyHostToDevice));
+                    total += src[k]->size() * 4;
                 }
-                HIP_TRY(hipMemcpy(ch->img_words.p, iwords.data(), iwords.size() * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(ch->img_off.p, ioff.data(), ioff.size() * 4, hipMemcpyHostToDevice));
-                ch->img_max_words = imax;
-                ch->img_records = (int64_t)std::count_if(ioff.begin(), ioff.end(), [](uint32_t o) { return o != binned::kNoImage; });
-                total += iwords.size() * 4 + ioff.size() * 4;
+                ch->img_max_words = iset.max_words;
+                ch->img_count = (int64_t)iset.off.size();
+                ch->img_records = (int64_t)std::count_if(iset.off.begin(), iset.off.end(),
+                                                         [](uint32_t o) { return o != binned::kNoImage; });
             }
             trace.mark("tile images");
         }
@@ -3615,7 +3621,7 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
     o[2] = ch->praster.quad ? ch->praster.qshift : 0;
     o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes + ch->rqrec.bytes) : 0;
     o[4] = ch->stream_ok ? 1 : 0;
-    o[5] = ch->img_records;  // binned join: tile records with an LDS chip image, their bytes, the largest image
+    o[5] = ch->img_records;  // binned join: LDS chip images (record parts), their bytes, the largest image
     o[6] = (int64_t)(ch->img_words.bytes + ch->img_off.bytes);
     o[7] = (int64_t)ch->img_max_words * 4;
     return MOSAIC_OK;
@@ -3912,7 +3918,11 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 if (use_img) {
                     img.words = (const uint32_t*)ch->img_words.p;
                     img.off = (const uint32_t*)ch->img_off.p;
+                    img.cover = (const uint32_t*)ch->img_cover.p;
+                    img.rec = (const uint32_t*)ch->img_rec.p;
+                    img.rec_key = (const uint32_t*)ch->img_key.p;
                     img.max_words = ch->img_max_words;
+                    img.n_images = (uint32_t)ch->img_count;
                 }
                 hipError_t e = binned::join(a, lo, hi, max_code, lds && !pairs, c->n_cu, img, c->bins, c->stream);
                 if (e == hipErrorOutOfMemory) return fail(MOSAIC_E_NOMEM, "binned join: device allocation failed");

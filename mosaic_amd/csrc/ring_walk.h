@@ -77,5 +77,57 @@ MOSAIC_HD bool ring_interior(const double* v, uint32_t n, double px, double py) 
     return !on && (cross & 1u);
 }
 
+// ---- the f32 walk: the same decisions from single-precision differences, each certified by an
+// error bound or reported undecided (the caller then takes a double-precision walk).
+// Frame: coordinates relative to the chip's outward-rounded f32 envelope minimum (fminx, fminy),
+// vertices stored as float(v - fmin) (round to nearest), the point as float(p - fmin) with p - fmin
+// in double.  M bounds |relative coordinate| of the vertices (within the f32 envelope) and of a
+// point that passed the f32 envelope test (float(p) within the envelope, |p - float(p)| <= 2^-24
+// |p| <= 1.1e-5 for |p| <= 184).  Each stored / converted value is within u M of the exact
+// difference (u = 2^-24), so a computed difference d = fl(a - q), |a - q| <= 2M, is within
+// 2uM + 2uM = 4uM of the exact one: |d| > tol = 5uM fixes its sign (and with it JTS's strict
+// comparisons p1.y > p.y, p1.x < p.x).  The orientation determinant x1 y2 - y1 x2 of such
+// differences (|.| <= 2M) is within 2 (2M 4uM + 2M 4uM) (products of perturbed factors)
+// + 2 u 4M^2 (product roundings) + u 8M^2 (subtraction) = 48uM^2 of the exact one: |det| > 52uM^2
+// fixes its sign.  Constants are rounded up.
+struct F32Frame {
+    float qx, qy, tol, bound;
+};
+MOSAIC_HD F32Frame f32_frame(float fminx, float fminy, float fmaxx, float fmaxy, double px, double py) {
+    F32Frame f;
+    const float m = fmaxf(fmaxx - fminx, fmaxy - fminy) * 1.000001f + 1.1e-5f;
+    f.qx = (float)(px - (double)fminx);
+    f.qy = (float)(py - (double)fminy);
+    f.tol = m * 3.0e-7f;          // 5 u M
+    f.bound = m * m * 3.2e-6f;    // 52 u M^2
+    return f;
+}
+
+// 1: interior, 0: not, 2: undecided (an edge whose decisions the bounds cannot certify: the
+// point near a vertex's y, an edge's x, or an edge's line).  JTS's walk with p1 = v[i], p2 = v[i-1]:
+// an edge with both ends certainly left of the point, or both certainly above / below its y, is
+// skipped (as there, where such an edge changes nothing); a certainly straddling edge with a
+// certain orientation counts a crossing as there; any other edge leaves the answer undecided
+// (which covers every boundary case: vertex, horizontal edge, point on an edge).
+MOSAIC_HD int ring_interior_f32(const float* v, uint32_t n, const F32Frame& f) {
+    bool amb = false;
+    uint32_t cross = 0;
+    float x2 = v[0] - f.qx, y2 = v[1] - f.qy;
+    for (uint32_t i = 1; i < n; i++) {
+        const float x1 = v[2 * i] - f.qx, y1 = v[2 * i + 1] - f.qy;
+        const bool a1 = y1 > f.tol, b1 = y1 < -f.tol, a2 = y2 > f.tol, b2 = y2 < -f.tol;
+        const bool skip = (x1 < -f.tol && x2 < -f.tol) || (a1 && a2) || (b1 && b2);
+        const bool strad = (a1 && b2) || (b1 && a2);
+        const float det = x1 * y2 - y1 * x2;
+        const bool pos = det > f.bound, neg = det < -f.bound;
+        amb |= !skip && !(strad && (pos || neg));
+        // orientation sign(det), negated when p2.y < p1.y (p1 above): a crossing when the result is 1
+        cross += (!skip && strad && (a1 ? neg : pos)) ? 1u : 0u;
+        x2 = x1;
+        y2 = y1;
+    }
+    return amb ? 2 : (int)(cross & 1u);
+}
+
 }  // namespace ringwalk
 }  // namespace mosaic

@@ -113,26 +113,35 @@ def test_tile_map_bounds(tmp_path):
 
 def test_ring_walks_match_jts(tmp_path):
     """CPU: the tile join's ring walks (ring_walk.h: branch-free with its filter fallback, and the
-    exact walk) equal JTS locateInRing == INTERIOR (pip_device.h) on ~1.1 M adversarial cases"""
+    exact walk) equal JTS locateInRing == INTERIOR (pip_device.h) on ~1.1 M adversarial cases, and
+    the certified f32 walk equals it wherever it decides"""
     root = ROOT
     exe = tmp_path / "rwc"
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(root, "mosaic_amd", "csrc"),
                     "-o", str(exe), os.path.join(root, "tests", "native", "ring_walk_check.cpp")], check=True)
-    cases, bad = map(int, subprocess.run([str(exe), "20000"], check=True, capture_output=True, text=True).stdout.split())
+    cases, bad, f32_cases, f32_undecided, f32_random, f32_random_undecided = map(
+        int, subprocess.run([str(exe), "20000"], check=True, capture_output=True, text=True).stdout.split())
     assert cases > 1_000_000 and bad == 0
+    # the f32 walk leaves the boundary cases undecided (vertices, points on edges and on rays
+    # through vertices: most adversarial points) and decides nearly every random point
+    assert f32_cases > 500_000 and f32_random > 100_000 and f32_random_undecided < 1e-3 * f32_random
 
 
 def test_tile_images(tmp_path):
     """CPU: the binned join's tile images (tile_images.h) for 20k C4-style buildings at H3 res 11
-    and the NYC zones at res 10 -- chip records equal the chip table, and every chip whose envelope
-    holds a point (random tile points, tile edges, envelope corners and edge midpoints) is listed in
-    the point's envelope-raster cell as k_join_tiles computes it"""
+    and the NYC zones at res 10 -- image headers and chip records equal the chip table, and every
+    window chip whose envelope holds a point of the tile (random tile points, tile edges, envelope
+    corners and edge midpoints) is listed in the point's envelope-raster cell of its part's image as
+    k_join_tiles computes it, with the record's cover bit set exactly for non-empty cells"""
     from mosaic_amd.data import synthetic_buildings
     exe = tmp_path / "tic"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wno-unknown-pragmas", "-pthread", "-o", str(exe),
+    # (sanitized: an out-of-range index in the builder or the keygen arithmetic fails the run)
+    subprocess.run(["g++", "-O1", "-std=c++17", "-ffp-contract=off", "-Wno-unknown-pragmas", "-pthread",
+                    "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-o", str(exe),
                     os.path.join(ROOT, "tests", "native", "tile_images_check.cpp")], check=True)
-    for name, polys, res in (("bld", synthetic_buildings(20000), 11),
-                             ("nyc", PolygonSet.load("nyc_taxi_zones_35"), 10)):
+    for name, polys, res, cap in (("bld", synthetic_buildings(20000), 11, None),
+                                  ("bld_split", synthetic_buildings(20000, sigma=0.0005), 11, 1024),
+                                  ("nyc", PolygonSet.load("nyc_taxi_zones_35"), 10, None)):
         chips = tessellate("H3", polys, res)
         path = tmp_path / f"{name}.bin"
         offs, data = chips["wkb"]
@@ -143,6 +152,10 @@ def test_tile_images(tmp_path):
                 f.write(struct.pack("<qBiI", int(chips["index_id"][i]), int(chips["is_core"][i]),
                                     int(chips["polygon_key"][i]), len(w)))
                 f.write(w)
-        out = subprocess.run([str(exe), str(path), "32"], check=True, capture_output=True, text=True).stdout.split()
-        recs, imaged, checked, bad = map(int, out)
-        assert recs > 100 and imaged > recs // 2 and checked > 20_000 and bad == 0, (name, out)
+        args = [str(exe), str(path), "32"] + ([str(cap)] if cap else [])
+        out = subprocess.run(args, check=True, capture_output=True, text=True).stdout.split()
+        recs, images, checked, bad, lv0, lv1, lv2 = map(int, out)
+        assert recs > 100 and images > recs // 2 and checked > 20_000 and bad == 0, (name, out)
+        assert lv0 + lv1 + lv2 == recs, (name, out)
+        if cap:  # (dense buildings, small images: records split into 2 x 2 and 4 x 4 parts)
+            assert lv1 > 0 and lv2 > 0, (name, out)
