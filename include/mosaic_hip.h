@@ -144,6 +144,9 @@ int mosaic_sync(mosaic_ctx* ctx);
  * [1] (point, border chip) contains tests, [2] matched pairs (pairs calls only).
  * Filled only by sync calls. */
 int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3);
+/* Rows the calling thread's last join sorted on its binned path (the points some chip may hold:
+ * k_bin_cover's keep count), 0 when the join took another path. */
+int mosaic_last_binned_rows(mosaic_ctx* ctx, int64_t* out);
 /* With option "timing" = 1, every join call brackets its fused kernel with HIP events on the
  * context stream.  Waits for the stream, writes up to cap elapsed times (ms) in call order, reports
  * how many calls were timed in *n_out, and resets the list. */

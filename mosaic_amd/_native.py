@@ -28,7 +28,7 @@ GRID_BNG = 1
 
 EXPORTS = [
     "mosaic_abi_version", "mosaic_last_error", "mosaic_init", "mosaic_destroy", "mosaic_set_option",
-    "mosaic_get_stream", "mosaic_set_stream", "mosaic_sync", "mosaic_last_stats", "mosaic_resolution",
+    "mosaic_get_stream", "mosaic_set_stream", "mosaic_sync", "mosaic_last_stats", "mosaic_last_binned_rows", "mosaic_resolution",
     "mosaic_resolution_str", "mosaic_point_to_cell", "mosaic_bng_format", "mosaic_bng_parse",
     "mosaic_chip_table_create", "mosaic_chip_table_destroy", "mosaic_chip_table_info", "mosaic_chip_table_tiles",
     "mosaic_chip_table_tile_grid", "mosaic_chip_table_raster", "mosaic_pip_join_count",
@@ -102,6 +102,7 @@ def lib():
         "mosaic_stream_wait_event": ([vp, vp], i32),
         "mosaic_sync": ([vp], i32),
         "mosaic_last_stats": ([vp, vp], i32),
+        "mosaic_last_binned_rows": ([vp, vp], i32),
         "mosaic_resolution": ([i32, i32, ctypes.POINTER(i32)], i32),
         "mosaic_resolution_str": ([i32, cp, ctypes.POINTER(i32)], i32),
         "mosaic_point_to_cell": ([vp, i32, i32, vp, vp, vp, i64, vp, vp], i32),

@@ -407,6 +407,12 @@ class MosaicContext:
         N.check(N.lib().mosaic_thread_count(self.handle, ctypes.byref(n), ctypes.byref(b)))
         return n.value, b.value
 
+    def last_binned_rows(self):
+        """Rows the last join on this thread sorted on its binned path (0: another path)."""
+        out = np.zeros(1, np.int64)
+        N.check(N.lib().mosaic_last_binned_rows(self.handle, N.ptr(out)))
+        return int(out[0])
+
     def last_stats(self):
         out = np.zeros(3, np.int64)
         N.check(N.lib().mosaic_last_stats(self.handle, N.ptr(out)))

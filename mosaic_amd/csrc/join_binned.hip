@@ -77,7 +77,10 @@ __global__ void __launch_bounds__(256) k_bin_keys(JoinArgs a, int64_t lo, int64_
 // workgroup waits on belongs to a running workgroup that publishes its aggregate without waiting on
 // anything; the wait is still bounded (kBinSpinCap polls; then *err is set and the caller reruns
 // the uncompacted k_bin_keys).
-static const int kBinPPT = 8;  // points per thread
+#ifndef MOSAIC_BIN_PPT
+#define MOSAIC_BIN_PPT 8
+#endif
+static const int kBinPPT = MOSAIC_BIN_PPT;  // points per thread
 static const int kBinChunk = 256 * kBinPPT;
 static const unsigned long long kStAgg = 1ULL << 62, kStPre = 2ULL << 62, kStVal = (1ULL << 62) - 1;
 static const int kBinSpinCap = 1 << 20;
@@ -349,7 +352,18 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
 
 // the tile join's rare paths (inlined: as calls they cost the kernel 18 % -- call-site register
 // saves and spills -- on C4)
+#ifdef MOSAIC_TJ_CALLS
+#define MOSAIC_TJ_NOINLINE __device__ __noinline__
+#else
 #define MOSAIC_TJ_NOINLINE __device__ __forceinline__
+#endif
+#ifdef MOSAIC_TJ_NORARE  // (timing probe: the rare paths removed -- wrong answers)
+MOSAIC_TJ_NOINLINE bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) { return x == 1e300; }
+MOSAIC_TJ_NOINLINE uint2 tiled_cell_call(const JoinArgs& a, int64_t i, double x, double y, uint32_t code) {
+    return make_uint2(0, 0);
+}
+MOSAIC_TJ_NOINLINE uint2 probe_call(const JoinArgs& a, int64_t cell) { return make_uint2(0, 0); }
+#else
 MOSAIC_TJ_NOINLINE bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
     return pip::contains(s, c, x, y);
 }
@@ -363,6 +377,7 @@ MOSAIC_TJ_NOINLINE uint2 probe_call(const JoinArgs& a, int64_t cell) {
     probe(a, cell, c0, c1);
     return make_uint2(c0, c1);
 }
+#endif
 
 // (occupancy 4: 128 VGPRs; C4 1e6 measured 23.4 ms against 28.7 unconstrained and 27.1 at 5)
 template <int CM, bool PAIRS, class P>
@@ -387,9 +402,6 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
     }
     __syncthreads();
     unsigned int tests = 0;
-#ifdef MOSAIC_TJ_STAT
-    unsigned int stat = 0;
-#endif
     const int64_t s0 = (int64_t)*n_skip + (int64_t)blockIdx.x * kSegPoints;
     const int64_t s1 = s0 + kSegPoints < n ? s0 + kSegPoints : n;
     for (int64_t pos = s0; pos < s1;) {  // block-uniform: one run of equal tile code per iteration
@@ -429,9 +441,6 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
             while (sn >= 64 || (all && sn > 0)) {
                 const uint32_t m = sn < 64u ? sn : 64u;
                 if ((uint32_t)lane < m) {
-#ifdef MOSAIC_TJ_STAT
-                    if (MOSAIC_TJ_STAT == 1) stat++;
-#endif
                     const uint32_t e = sn - m + (uint32_t)lane;
                     const double qx = surv_x[wv][e], qy = surv_y[wv][e];
                     const uint32_t sc = surv_c[wv][e];
@@ -439,12 +448,7 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                     uint32_t key;
                     if (sc & kSurvGlobal) {  // a chip of the table (a run without an image, a hexagon off the window)
                         const uint32_t c = sc & ~kSurvGlobal;
-#ifdef MOSAIC_TJ_STAT
-                        if (MOSAIC_TJ_STAT == 2) stat++;
-                        hit = MOSAIC_TJ_STAT == 3 ? false : contains_call(a.store, c, qx, qy);
-#else
                         hit = contains_call(a.store, c, qx, qy);
-#endif
                         key = a.chip_meta[c] >> 1;
                     } else {
                         const uint32_t* cr = chips + 8u * sc;
@@ -455,13 +459,7 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                                                             ringwalk::f32_frame(__uint_as_float(cr[4]), __uint_as_float(cr[5]),
                                                                                 __uint_as_float(cr[6]), __uint_as_float(cr[7]), qx, qy));
                         // (global geometry, or a point the f32 walk leaves undecided: the f64 test)
-#ifdef MOSAIC_TJ_STAT
-                        if (MOSAIC_TJ_STAT == 2 && r == 2) stat++;
-                        if (MOSAIC_TJ_STAT == 4 && vc == binned::kImgGlobal) stat++;
-                        hit = r == 2 ? (MOSAIC_TJ_STAT == 3 ? false : contains_call(a.store, cr[2], qx, qy)) : r == 1;
-#else
                         hit = r == 2 ? contains_call(a.store, cr[2], qx, qy) : r == 1;
-#endif
                         key = cr[0] >> 1;
                     }
                     if (hit) {
@@ -593,9 +591,6 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
         }
         pos = r1;
     }
-#ifdef MOSAIC_TJ_STAT
-    tests = MOSAIC_TJ_STAT == 3 ? tests : stat;
-#endif
     for (int off = 32; off > 0; off >>= 1) tests += __shfl_down(tests, off, 64);
     if (lane == 0 && tests) atomicAdd(a.tests, (unsigned long long)tests);
     if (CM == kCountLds) {
@@ -630,6 +625,9 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
 #define MOSAIC_BIN_COVER(VEC, COMPACT)                                                                                \
     hipLaunchKernelGGL((k_bin_cover<P, VEC, COMPACT>), dim3(nb), dim3(256), 0, stream, a0.x, a0.y, a0.tgrid, a0.tile_idx, \
                        img.cover, img.rec_key, lo, n, (uint32_t*)s.keys[0].p, (P*)s.vals[0].p, st, nsk, err)
+#ifdef MOSAIC_BIN_NOLB
+        bool ok = false;
+#else
         if (vec && m >= 2)
             MOSAIC_BIN_COVER(true, true);
         else
@@ -638,10 +636,13 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
         unsigned long long hw[3];
         if ((e = hipMemcpyAsync(hw, nsk, sizeof hw, hipMemcpyDeviceToHost, stream)) || (e = hipStreamSynchronize(stream)))
             return e;
-        if (hw[2] == 0 && hw[0] <= (unsigned long long)m) {
+        const bool ok = hw[2] == 0 && hw[0] <= (unsigned long long)m;
+        if (ok) {
             m = (int64_t)hw[0];
             nsk += 1;  // the join starts at sorted row 0
-        } else {
+        }
+#endif
+        if (!ok) {
             // the look-back gave up: every row in place, dropped rows keyed kSkip (counted in word 0)
             if ((e = hipMemsetAsync(s.n_skip.p, 0, 32, stream))) return e;
             if (vec && m >= 2)
@@ -664,6 +665,7 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
                                (P*)s.vals[0].p, nsk);
         if ((e = hipGetLastError())) return e;
     }
+    s.sorted_rows = m;
     // the key's significant bits (codes <= max_code)
     int end_bit = 1;
     while (end_bit < 32 && (max_code >> end_bit)) end_bit++;

@@ -1694,6 +1694,7 @@ struct ThreadCtx : Options {
     DevBuf hx[2], hy[2], hcounts;
     binned::Scratch bins;  // the binned join's keys, sorted points and sort temp
     int64_t stats[3] = {0, 0, 0};
+    int64_t binned_rows = 0;  // rows the last join's binned path sorted (mosaic_last_binned_rows)
     unsigned int deferred_flags = 0;
     std::vector<hipEvent_t> ev_start, ev_stop;
     size_t ev_used = 0;
@@ -2263,6 +2264,13 @@ int mosaic_kernel_times(mosaic_ctx* ctx, double* out_ms, int64_t cap, int64_t* n
 const char* mosaic_last_kernel(mosaic_ctx* ctx) {
     ThreadCtx* c = ctx ? enter(ctx) : nullptr;
     return c ? c->last_kernel : "";
+}
+
+int mosaic_last_binned_rows(mosaic_ctx* ctx, int64_t* out) {
+    if (!ctx || !out) return fail(MOSAIC_E_ARG, "null argument");
+    ENTER(ctx);
+    *out = c->binned_rows;
+    return MOSAIC_OK;
 }
 
 int mosaic_last_stats(mosaic_ctx* ctx, int64_t* out3) {
@@ -3692,6 +3700,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
         if ((rc = c->stage_out2.reserve((size_t)std::max<int64_t>(cap, 1) * 4))) return rc;
     }
     unsigned long long* sc = (unsigned long long*)c->scalars.p;
+    c->binned_rows = 0;
     JoinArgs a;
     a.x = (const double*)dx;
     a.y = (const double*)dy;
@@ -3927,6 +3936,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 hipError_t e = binned::join(a, lo, hi, max_code, lds && !pairs, c->n_cu, img, c->bins, c->stream);
                 if (e == hipErrorOutOfMemory) return fail(MOSAIC_E_NOMEM, "binned join: device allocation failed");
                 if (e != hipSuccess) return fail(MOSAIC_E_HIP, std::string("binned join: ") + hipGetErrorString(e));
+                c->binned_rows += c->bins.sorted_rows;
                 // this chunk's exact-H3 rows, before the next chunk reuses the sorted buffers
                 const int ge = std::min(grid_size(c, (int64_t)qcap), std::max(1, c->n_cu * 2));
                 if (pairs)

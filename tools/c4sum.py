@@ -18,6 +18,12 @@ for f in sorted(glob.glob(os.path.join(d, "c4*.txt"))):
 tl = os.path.join(d, "tests.log")
 if os.path.exists(tl):
     print([l.strip() for l in open(tl) if "passed" in l or "failed" in l or "error" in l.lower()][-1:])
+for st in sorted(glob.glob(os.path.join(d, "stats*.csv"))):
+    import csv
+    print(os.path.basename(st))
+    rows = sorted(csv.DictReader(open(st)), key=lambda r: -float(r["TotalDurationNs"]))[:6]
+    for r in rows:
+        print(f"  {float(r['AverageNs']) / 1e6:8.3f} ms x{int(r['Calls']):3d}  {r['Name'][:100]}")
 for db in glob.glob(os.path.join(d, "prof", "*.db")):
     c = sqlite3.connect(db)
     tabs = [r[0] for r in c.execute("select name from sqlite_master where type='table'")]

@@ -15,6 +15,7 @@ for v in $AB; do
 done
 if [ "$2" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o c4 -- python3 -u $R/tools/kbench_c4.py --buildings 1e6 --n 2.5e8 --reps 5 > $O/prof.txt 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_c4 -o c4 -- python3 -u $R/tools/kbench_c4.py --buildings 1e6 --n 2.5e8 --reps 5 > $O/prof.txt 2>&1 || exit 1
+  find /tmp/prof_c4 -name "*kernel_stats.csv" -exec cp {} $O/stats.csv \;
   echo prof done
 fi

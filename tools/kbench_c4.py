@@ -72,12 +72,14 @@ def main():
         ctx.set_option("async", 0)
         ctx.pip_join_count(table, x, y, out=counts)
         st = ctx.last_stats()
+        sorted_rows = ctx.last_binned_rows()
         ms = float(np.median(ts))
         print(json.dumps({"workload": f"C4 shape: {nb} buildings, H3 res {args.res}, {n} points", "variant": v,
                           "ms": ms, "points_per_s": n / ms * 1e3,
                           "contains_tests_per_s": st["contains_tests"] / ms * 1e3,
                           "pairs": int(counts.sum().item()), "contains_tests": st["contains_tests"],
-                          "exact_path_rows": st["exact_path_rows"], "build_s": round(t_build, 2),
+                          "exact_path_rows": st["exact_path_rows"], "binned_rows": sorted_rows,
+                          "build_s": round(t_build, 2),
                           "chips": table.info(), "tiles": table.tiles()}), flush=True)
         table.close()
 
