@@ -62,8 +62,7 @@ struct Images {
     const uint32_t* words = nullptr;  // nullptr: no images (k_bin_keys and k_join_binned run)
     const uint32_t* off = nullptr;    // per image key - 2
     const uint32_t* rec = nullptr;    // per image key - 2: the tile record
-    const uint32_t* rec_key = nullptr;  // per record: first image << 2 | level
-    const uint32_t* cover = nullptr;  // kImgCoverWords per record
+    const uint32_t* bin_map = nullptr;  // per tile: kBinMapWords (k_bin_cover)
     uint32_t max_words = 0;
     uint32_t n_images = 0;
 };

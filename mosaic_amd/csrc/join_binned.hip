@@ -77,10 +77,7 @@ __global__ void __launch_bounds__(256) k_bin_keys(JoinArgs a, int64_t lo, int64_
 // workgroup waits on belongs to a running workgroup that publishes its aggregate without waiting on
 // anything; the wait is still bounded (kBinSpinCap polls; then *err is set and the caller reruns
 // the uncompacted k_bin_keys).
-#ifndef MOSAIC_BIN_PPT
-#define MOSAIC_BIN_PPT 8
-#endif
-static const int kBinPPT = MOSAIC_BIN_PPT;  // points per thread
+static const int kBinPPT = 8;  // points per thread (4: the pass 20 % slower)
 static const int kBinChunk = 256 * kBinPPT;
 static const unsigned long long kStAgg = 1ULL << 62, kStPre = 2ULL << 62, kStVal = (1ULL << 62) - 1;
 static const int kBinSpinCap = 1 << 20;
@@ -96,16 +93,16 @@ __device__ __forceinline__ unsigned long long st_poll(unsigned long long* p) {
 
 // (explicit pointers and grid, not JoinArgs: they stay in scalar registers; every load is issued
 // before the first use, with clamped indices instead of branches)
-// Keys: kSkip (dropped), kFull, or the image key of the point's record part (tile_images.h:
-// 2 + first image of the record + image_part of its raster cell).  COMPACT false (the fallback
-// after a look-back failure): every point at its own position, dropped ones keyed kSkip (sorted
-// first; *total counts them).
+// Keys: kSkip (dropped), kFull, or the image key of the point's record part (tile_images.h
+// bin_map_key); one table read per point and kept word (the tile's bin map record: key word and
+// the cover word of the point's cell, one cache line).  COMPACT false (the fallback after a
+// look-back failure): every point at its own position, dropped ones keyed kSkip (sorted first;
+// *total counts them).
 template <class P, bool VEC, bool COMPACT>
 __global__ void __launch_bounds__(256) k_bin_cover(const double* __restrict__ X, const double* __restrict__ Y,
-                                                   tiles::Grid g, const uint32_t* __restrict__ tidx,
-                                                   const uint32_t* __restrict__ cover, const uint32_t* __restrict__ rec_key,
-                                                   int64_t lo, int64_t n, uint32_t* keys, P* pts,
-                                                   unsigned long long* status, unsigned long long* total, unsigned int* err) {
+                                                   tiles::Grid g, const uint32_t* __restrict__ bin_map, int64_t lo,
+                                                   int64_t n, uint32_t* keys, P* pts, unsigned long long* status,
+                                                   unsigned long long* total, unsigned int* err) {
     __shared__ uint32_t woff[kBinPPT * 4];  // per (item, wave): kept count, then output offset in the workgroup
     __shared__ unsigned long long base_s;
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
@@ -146,33 +143,30 @@ __global__ void __launch_bounds__(256) k_bin_cover(const double* __restrict__ X,
             ys[k] = Y[i];
         }
     }
-    // tile codes (tiles::tile_of, its gather issued for every item before any is used)
-    uint32_t code[kBinPPT], cw[kBinPPT];
+    // the tile's bin map record: key word and the cover word of the point's envelope-raster cell
+    // (binned::bin_cell: the cell as k_join_tiles computes it; both reads issued for every item
+    // before any is used)
+    uint32_t kw[kBinPPT], cw[kBinPPT];
     int q[kBinPPT];
 #pragma unroll
     for (int k = 0; k < kBinPPT; k++) {
-        // (tiles::tile_of's code; the envelope-raster cell as k_join_tiles computes it)
         const binned::BinCell bc = binned::bin_cell(g, xs[k], ys[k]);
-        code[k] = tidx[bc.slot];
-        if (!bc.in) code[k] = (isfinite(xs[k]) && isfinite(ys[k])) ? tiles::kSkip : tiles::kFull;
-        if (item(k) >= n) code[k] = tiles::kSkip;
+        const uint32_t* m = bin_map + (size_t)bc.slot * binned::kBinMapWords;
+        kw[k] = m[0];
+        cw[k] = m[1 + (bc.q >> 5)];
         q[k] = bc.q;
+        if (!bc.in) {  // off the grid: never kept, unless not finite (kFull: the generic path)
+            kw[k] = (isfinite(xs[k]) && isfinite(ys[k])) ? tiles::kSkip : tiles::kFull;
+            cw[k] = ~0u;
+        }
+        if (item(k) >= n) kw[k] = tiles::kSkip;
     }
-    // cover words and image keys (records: codes >= 2)
-    uint32_t rk[kBinPPT];
-#pragma unroll
-    for (int k = 0; k < kBinPPT; k++) {
-        const bool rec = code[k] >= 2u;
-        const uint32_t r = rec ? code[k] - 2u : 0u;
-        cw[k] = cover[(size_t)r * binned::kImgCoverWords + (uint32_t)(q[k] >> 5)];
-        rk[k] = rec_key[r];
-        if (!rec) cw[k] = ~0u;
-    }
+    uint32_t code[kBinPPT];
     unsigned long long mk[kBinPPT];
 #pragma unroll
     for (int k = 0; k < kBinPPT; k++) {
-        const bool keep = code[k] != tiles::kSkip && ((cw[k] >> (q[k] & 31)) & 1u);
-        code[k] = binned::bin_key(code[k], rk[k], q[k]);
+        const bool keep = binned::bin_map_keep(kw[k], cw[k], q[k]);
+        code[k] = binned::bin_map_key(kw[k], q[k]);
         if (!COMPACT) {
             if (!keep) code[k] = tiles::kSkip;
             mk[k] = __ballot(item(k) < n && !keep);  // (dropped, counted)
@@ -350,20 +344,9 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
            fy <= __uint_as_float(cr[7]);
 }
 
-// the tile join's rare paths (inlined: as calls they cost the kernel 18 % -- call-site register
-// saves and spills -- on C4)
-#ifdef MOSAIC_TJ_CALLS
-#define MOSAIC_TJ_NOINLINE __device__ __noinline__
-#else
+// the tile join's rare paths, inlined (as calls, the C4 1e6 kernel went 8.87 -> 10.88 ms: call-site
+// register saves and spills)
 #define MOSAIC_TJ_NOINLINE __device__ __forceinline__
-#endif
-#ifdef MOSAIC_TJ_NORARE  // (timing probe: the rare paths removed -- wrong answers)
-MOSAIC_TJ_NOINLINE bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) { return x == 1e300; }
-MOSAIC_TJ_NOINLINE uint2 tiled_cell_call(const JoinArgs& a, int64_t i, double x, double y, uint32_t code) {
-    return make_uint2(0, 0);
-}
-MOSAIC_TJ_NOINLINE uint2 probe_call(const JoinArgs& a, int64_t cell) { return make_uint2(0, 0); }
-#else
 MOSAIC_TJ_NOINLINE bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
     return pip::contains(s, c, x, y);
 }
@@ -377,7 +360,6 @@ MOSAIC_TJ_NOINLINE uint2 probe_call(const JoinArgs& a, int64_t cell) {
     probe(a, cell, c0, c1);
     return make_uint2(c0, c1);
 }
-#endif
 
 // (occupancy 4: 128 VGPRs; C4 1e6 measured 23.4 ms against 28.7 unconstrained and 27.1 at 5)
 template <int CM, bool PAIRS, class P>
@@ -623,11 +605,8 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
         unsigned int* err = (unsigned int*)(nsk + 2);
         unsigned long long* st = (unsigned long long*)s.status.p;
 #define MOSAIC_BIN_COVER(VEC, COMPACT)                                                                                \
-    hipLaunchKernelGGL((k_bin_cover<P, VEC, COMPACT>), dim3(nb), dim3(256), 0, stream, a0.x, a0.y, a0.tgrid, a0.tile_idx, \
-                       img.cover, img.rec_key, lo, n, (uint32_t*)s.keys[0].p, (P*)s.vals[0].p, st, nsk, err)
-#ifdef MOSAIC_BIN_NOLB
-        bool ok = false;
-#else
+    hipLaunchKernelGGL((k_bin_cover<P, VEC, COMPACT>), dim3(nb), dim3(256), 0, stream, a0.x, a0.y, a0.tgrid,              \
+                       img.bin_map, lo, n, (uint32_t*)s.keys[0].p, (P*)s.vals[0].p, st, nsk, err)
         if (vec && m >= 2)
             MOSAIC_BIN_COVER(true, true);
         else
@@ -641,7 +620,6 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
             m = (int64_t)hw[0];
             nsk += 1;  // the join starts at sorted row 0
         }
-#endif
         if (!ok) {
             // the look-back gave up: every row in place, dropped rows keyed kSkip (counted in word 0)
             if ((e = hipMemsetAsync(s.n_skip.p, 0, 32, stream))) return e;

@@ -1934,7 +1934,7 @@ struct mosaic_chips {
     StreamArgs stream{};
     DevBuf rsub, rmid, rblocks, rquad, rqrec;  // rmid: per-tile leaf block bases; rqrec: quad records
     // per-tile chip images of the binned join (tile_images.h ImageSet); empty: none
-    DevBuf img_words, img_off, img_rec, img_key, img_cover;
+    DevBuf img_words, img_off, img_rec, img_binmap;
     uint32_t img_max_words = 0;
     int64_t img_records = 0;  // images built (parts of tile records; tile_images.h)
     int64_t img_count = 0;    // image keys (with the parts that have no image)
@@ -1948,7 +1948,7 @@ struct mosaic_chips {
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
                           &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell,
-                          &img_words, &img_off, &img_rec, &img_key, &img_cover})
+                          &img_words, &img_off, &img_rec, &img_binmap})
             b->release();
         store.release();
     }
@@ -3546,9 +3546,9 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             is.threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
             binned::ImageSet iset;
             if (binned::build_tile_images(is, iset) && !iset.words.empty()) {
-                const std::vector<uint32_t>* src[5] = {&iset.words, &iset.off, &iset.rec, &iset.rec_key, &iset.cover};
-                DevBuf* dst[5] = {&ch->img_words, &ch->img_off, &ch->img_rec, &ch->img_key, &ch->img_cover};
-                for (int k = 0; k < 5; k++) {
+                const std::vector<uint32_t>* src[4] = {&iset.words, &iset.off, &iset.rec, &iset.bin_map};
+                DevBuf* dst[4] = {&ch->img_words, &ch->img_off, &ch->img_rec, &ch->img_binmap};
+                for (int k = 0; k < 4; k++) {
                     if ((rc = dst[k]->reserve(src[k]->size() * 4))) {
                         ch->release_all();
                         delete ch;
@@ -3927,9 +3927,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 if (use_img) {
                     img.words = (const uint32_t*)ch->img_words.p;
                     img.off = (const uint32_t*)ch->img_off.p;
-                    img.cover = (const uint32_t*)ch->img_cover.p;
                     img.rec = (const uint32_t*)ch->img_rec.p;
-                    img.rec_key = (const uint32_t*)ch->img_key.p;
+                    img.bin_map = (const uint32_t*)ch->img_binmap.p;
                     img.max_words = ch->img_max_words;
                     img.n_images = (uint32_t)ch->img_count;
                 }

@@ -70,6 +70,7 @@ struct ImageSet {
     std::vector<uint32_t> rec;      // per image: its tile record
     std::vector<uint32_t> rec_key;  // per record: first image index << 2 | level
     std::vector<uint32_t> cover;    // per record: kImgCoverWords
+    std::vector<uint32_t> bin_map;  // per tile: kBinMapWords (k_bin_cover's one table)
     uint32_t max_words = 0;
     uint32_t levels[kImgMaxLevel + 1] = {0, 0, 0};  // records per level
 };
@@ -103,6 +104,17 @@ MOSAIC_HD BinCell bin_cell(const tiles::Grid& g, double x, double y) {
 // rec_key (ignored for codes < 2)
 MOSAIC_HD uint32_t bin_key(uint32_t code, uint32_t rk, int q) {
     return code < 2u ? code : 2u + (rk >> 2) + image_part(q, (int)(rk & 3u));
+}
+// k_bin_cover's table, per tile of the grid (one cache-line-sized record, so a point's two reads
+// share a line): [0] key word -- tiles::kSkip, tiles::kFull, or (2 + first image of the tile's
+// record) << 2 | level -- and [1 ..] the record's cover bits (kFull: all set)
+static const int kBinMapWords = 1 + kImgCoverWords;
+// a point's key and whether it is kept, from its tile's key word kw and cover word cw of cell q
+MOSAIC_HD uint32_t bin_map_key(uint32_t kw, int q) {
+    return kw < 2u ? kw : (kw >> 2) + image_part(q, (int)(kw & 3u));
+}
+MOSAIC_HD bool bin_map_keep(uint32_t kw, uint32_t cw, int q) {
+    return kw != tiles::kSkip && ((cw >> (q & 31)) & 1u);
 }
 
 // ---- building the images (host)
@@ -310,7 +322,7 @@ inline bool build_tile_images(const ImageSource& s, ImageSet& out) {
         total += p.words.size();
         n_img += p.off.size();
     }
-    if (total >= (size_t)kNoImage || n_img >= ((size_t)1 << 30)) return false;
+    if (total >= (size_t)kNoImage || n_img >= ((size_t)1 << 29)) return false;
     out.words.clear();
     out.words.reserve(total);
     out.off.clear();
@@ -332,6 +344,20 @@ inline bool build_tile_images(const ImageSource& s, ImageSet& out) {
     for (size_t r = 0; r < nr; r++) {
         out.rec_key[r] |= (uint32_t)level[r];
         out.levels[level[r]]++;
+    }
+    const int64_t ntiles = (int64_t)s.grid.nx * s.grid.ny;
+    out.bin_map.assign((size_t)ntiles * kBinMapWords, 0u);
+    for (int64_t t = 0; t < ntiles; t++) {
+        uint32_t* m = &out.bin_map[(size_t)t * kBinMapWords];
+        const uint32_t code = s.tile_idx[t];
+        if (code >= 2 && code - 2 < nr) {
+            const uint32_t r = code - 2;
+            m[0] = (2u + (out.rec_key[r] >> 2)) << 2 | (out.rec_key[r] & 3u);
+            for (int q = 0; q < kImgCoverWords; q++) m[1 + q] = out.cover[(size_t)r * kImgCoverWords + q];
+        } else {
+            m[0] = code == tiles::kFull ? tiles::kFull : tiles::kSkip;
+            for (int q = 0; q < kImgCoverWords; q++) m[1 + q] = m[0] == tiles::kFull ? ~0u : 0u;
+        }
     }
     return true;
 }

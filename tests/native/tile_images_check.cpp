@@ -207,7 +207,8 @@ int main(int argc, char** argv) {
     }
     // k_bin_cover's per-point arithmetic on adversarial coordinates (off the grid on every side,
     // fractions below zero, huge, NaN, infinities, tile corners): every gather in range, every key
-    // within the image keys, and an in-grid point's key an image of its own record
+    // within the image keys, an in-grid point's key an image of its own record, and the bin map's
+    // key and keep equal to those of the record tables
     {
         std::vector<double> vx = {g.x0, g.x0 - 1e-9, g.x0 - 0.5 / g.sx, g.x0 - 5.5 / g.sx, g.x0 + (g.nx - 1e-9) / g.sx,
                                   g.x0 + (double)g.nx / g.sx, 1e300, -1e300, NAN, INFINITY, -INFINITY, 0.0};
@@ -236,6 +237,21 @@ int main(int argc, char** argv) {
                 const uint32_t key = binned::bin_key(code, set.rec_key[r], bc.q);
                 if (code >= 2) bad += key < 2 || key - 2 >= set.off.size() || set.rec[key - 2] != r;
                 else bad += key != code;
+                const bool keep = code != tiles::kSkip &&
+                                  (code < 2 || ((set.cover[(size_t)r * binned::kImgCoverWords + (bc.q >> 5)] >> (bc.q & 31)) & 1u));
+                // k_bin_cover's reads: the tile's bin map record (in range), then the same key and keep
+                const size_t mi = (size_t)bc.slot * binned::kBinMapWords;
+                if (mi + binned::kBinMapWords > set.bin_map.size()) {
+                    bad++;
+                    continue;
+                }
+                uint32_t kw = set.bin_map[mi], cw = set.bin_map[mi + 1 + (bc.q >> 5)];
+                if (!bc.in) {
+                    kw = (std::isfinite(x) && std::isfinite(y)) ? tiles::kSkip : tiles::kFull;
+                    cw = ~0u;
+                }
+                bad += binned::bin_map_keep(kw, cw, bc.q) != keep;
+                if (keep) bad += binned::bin_map_key(kw, bc.q) != key;
             }
     }
     printf("%zu %ld %ld %ld %u %u %u\n", nr, imaged, checked, bad, set.levels[0], set.levels[1], set.levels[2]);
