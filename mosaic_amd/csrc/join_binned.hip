@@ -15,7 +15,10 @@
 // The exact-H3 queue carries sorted positions; k_join_h3_exact reads their coordinates (and, for
 // pairs, their source rows) through JoinArgs::cstride / rowmap.
 #include <hip/hip_runtime.h>
+#include <string.h>
+
 #include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -584,6 +587,30 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
 
 namespace binned {
 
+// Onesweep radix sort of (key, point) over bits [0, end_bit) with R bits per pass: keys of 17-22
+// bits (image keys of large tables) sort in two passes instead of hipcub's three 8-bit ones.
+template <unsigned R>
+using OnesweepR = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 12>, rocprim::kernel_config<1024, 12>, R,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+template <unsigned R, class P>
+static hipError_t sort_r(void* tmp, size_t& tb, uint32_t* const k[2], P* const v[2], int64_t m, int end_bit,
+                         hipStream_t stream, int& cur) {
+    rocprim::double_buffer<uint32_t> kb(k[0], k[1]);
+    rocprim::double_buffer<P> vb(v[0], v[1]);
+    const hipError_t e = rocprim::radix_sort_pairs<OnesweepR<R>>(tmp, tb, kb, vb, (size_t)m, 0u, (unsigned)end_bit, stream);
+    cur = kb.current() == k[0] ? 0 : 1;
+    return e;
+}
+template <class P>
+static hipError_t sort_wide(void* tmp, size_t& tb, uint32_t* const k[2], P* const v[2], int64_t m, int end_bit,
+                            hipStream_t stream, int& cur) {
+    if (end_bit <= 18) return sort_r<9, P>(tmp, tb, k, v, m, end_bit, stream, cur);
+    if (end_bit <= 20) return sort_r<10, P>(tmp, tb, k, v, m, end_bit, stream, cur);
+    return sort_r<11, P>(tmp, tb, k, v, m, end_bit, stream, cur);
+}
+
 template <class P>
 static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint32_t max_code, int cm, int n_cu,
                                 const Images& img, Scratch& s, hipStream_t stream) {
@@ -650,9 +677,20 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
     hipcub::DoubleBuffer<uint32_t> kb((uint32_t*)s.keys[0].p, (uint32_t*)s.keys[1].p);
     hipcub::DoubleBuffer<P> pb((P*)s.vals[0].p, (P*)s.vals[1].p);
     size_t tb = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, pb, (int)m, 0, end_bit, stream))) return e;
-    if ((e = s.temp.reserve(tb))) return e;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp.p, tb, kb, pb, (int)m, 0, end_bit, stream))) return e;
+    if (end_bit > 16 && end_bit <= 22) {
+        uint32_t* const k2[2] = {(uint32_t*)s.keys[0].p, (uint32_t*)s.keys[1].p};
+        P* const v2[2] = {(P*)s.vals[0].p, (P*)s.vals[1].p};
+        int cur = 0;
+        if ((e = sort_wide<P>(nullptr, tb, k2, v2, m, end_bit, stream, cur))) return e;
+        if ((e = s.temp.reserve(tb))) return e;
+        if ((e = sort_wide<P>(s.temp.p, tb, k2, v2, m, end_bit, stream, cur))) return e;
+        kb = hipcub::DoubleBuffer<uint32_t>(k2[cur], k2[1 - cur]);
+        pb = hipcub::DoubleBuffer<P>(v2[cur], v2[1 - cur]);
+    } else {
+        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, pb, (int)m, 0, end_bit, stream))) return e;
+        if ((e = s.temp.reserve(tb))) return e;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp.p, tb, kb, pb, (int)m, 0, end_bit, stream))) return e;
+    }
     JoinArgs a = a0;
     a.x = &pb.Current()->x;
     a.y = &pb.Current()->y;

@@ -424,12 +424,12 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 // compact it and gather its sub-block entries, load group t + 1).  Pending rows beyond 64 in a group
 // (clustered input) are finished at once, unpipelined.  Per pending row the set carries: the low L =
 // cs + kFixBits + qs bits of both fixed-point fine-cell coordinates (leaf cell, line offsets and the
-// sub-block within the quad; L <= 20), the source lane and row slot, the quad entry and the tile.
+// sub-block within the quad; L <= 24), the source lane and row slot, the quad entry and the tile.
 // Same answers as k_join_stream_pipe, point for point.
 // 1: a group's second set of pending rows (65 - 128) is pipelined like the first
 // 1: compaction through a per-wave LDS buffer; 0: ds_permute (no LDS memory)
 struct CptSet {
-    uint32_t a;     // ix low bits | source lane << 20 | row slot k << 26
+    uint32_t a;     // ix low bits | source lane << 24 | row slot k << 30
     uint32_t b;     // iy low bits
     uint32_t c;     // quad entry | tile index << 16
     uint32_t code;  // A -> B: gathered sub-block entry; B -> D: the answer, 0 for leaf rows, or kPipeLine
@@ -517,7 +517,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
         lc = sv <= -1.0f ? neg : lc;
         const uint32_t code = z.code == kPipeLine ? lc : (z.code | z.leaf);
-        const uint32_t src = (z.a >> 20) & 63u, k = z.a >> 26;
+        const uint32_t src = (z.a >> 24) & 63u, k = z.a >> 30;
         const int64_t row = wb + (int64_t)((k >> 1) * 128u + 2u * src + (k & 1u));
         answer(code, row);
         const bool m = code >= kPipeNonFinite;
@@ -546,7 +546,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             if (LDS_COUNTS && !PAIRS) atomicAdd(&lds[min(q - 1u, spill)], 1u);
             else if (q - 1u < kPipeNonFinite - 1u) emit_hit<LDS_COUNTS, PAIRS>(a, wb + (k >> 1) * 128 + 2 * lane + (k & 1), q - 1u, lds);
             pend[k] = q >= 0x8000u;
-            fa[k] = (ixC & lowm) | ((uint32_t)lane << 20) | ((uint32_t)k << 26);
+            fa[k] = (ixC & lowm) | ((uint32_t)lane << 24) | ((uint32_t)k << 30);
             fb[k] = iyC & lowm;
             fc[k] = q | (tile << 16);
         }

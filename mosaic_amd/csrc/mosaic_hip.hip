@@ -3856,11 +3856,10 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             auto mode_for = [&](bool vec) -> int {
                 // the pipelined forms where they apply (the compacted one, k_join_stream_cpt, carries
-                // cs + kFixBits + qs <= 20 low bits of the fine-cell coordinates and a 16-bit tile index
-                // per pending row)
+                // cs + kFixBits + qs <= 24 low bits of the fine-cell coordinates and a 16-bit tile index
                 // per pending row, and per wave a kCptBufWords compaction buffer in LDS)
                 int mode = vec && sa.tb_lds && sa.fix_ok ? c->stream_pipe : 0;
-                if (mode == 2 && !(sa.cs + sa.qs <= 8 && sa.n_tiles <= 65536 &&
+                if (mode == 2 && !(sa.cs + tiles::kFixBits + sa.qs <= 24 && sa.n_tiles <= 65536 &&
                                    shm_s + (size_t)(blk / 64) * kCptBufWords * 4 <= kStreamLdsMax))
                     mode = 1;
                 return mode;
