@@ -436,7 +436,7 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                         hit = contains_call(a.store, c, qx, qy);
                         key = a.chip_meta[c] >> 1;
                     } else {
-                        const uint32_t* cr = chips + 8u * sc;
+                        const uint32_t* cr = chips + binned::kImgChipWords * sc;
                         const uint32_t vi = cr[1], vc = vi >> 16;
                         int r = 2;
                         if (vc != binned::kImgGlobal)
@@ -533,7 +533,7 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                 bool surv = false;
                 uint32_t c = ent >> 6;  // glob: a chip of the table; else a list position
                 if (live && !qg) c = rl[c];
-                const uint32_t* cr = chips + 8u * c;
+                const uint32_t* cr = chips + binned::kImgChipWords * c;
                 if (live && (qg || cr[3] == qslot)) {  // (image chips of another hexagon: no pair)
                     const uint32_t meta = qg ? a.chip_meta[c] : cr[0];
                     if (meta & 1u) {
@@ -569,7 +569,7 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
             for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
                 const uint32_t v = cnt[k];
                 if (v) {
-                    atomicAdd(&a.counts[chips[8u * k] >> 1], (unsigned long long)v);
+                    atomicAdd(&a.counts[chips[binned::kImgChipWords * k] >> 1], (unsigned long long)v);
                     cnt[k] = 0;
                 }
             }

@@ -27,10 +27,10 @@ using namespace mosaic;
 //   envelope raster (at word 8): kImgRaster^2 + 1 uint16 list offsets, then the lists (uint16 chip
 //     indices): cell (gx, gy) of the tile's kImgRaster x kImgRaster split lists every chip of the
 //     image whose f64 envelope meets it (core chips: every cell); cells outside the part: empty
-//   chips (at a multiple of 4 words): 8 words each -- meta (polygon_key << 1 | is_core), vinfo
+//   chips (at a multiple of 4 words): kImgChipWords each -- meta (polygon_key << 1 | is_core), vinfo
 //     (vertex offset | count << 16; count 0: no geometry (core chip), kImgGlobal: tested from the
 //     global geometry store), global chip index, window slot of its hexagon, f32 minx, miny, maxx,
-//     maxy (outward rounded)
+//     maxy (outward rounded), a pad word
 //   vertices (at a multiple of 4 words): float2 in the chip's f32 frame (ring_walk.h f32_frame:
 //     float(v - envelope minimum)), ring after ring (closed); the image is padded to 4 words
 // A point's raster cell is computed from its grid position exactly as its tile is
@@ -42,7 +42,10 @@ static const uint32_t kImgCapWords = 6144;  // 24 KB of LDS per workgroup (4 wor
 static const uint32_t kImgHdrWords = 8;
 static const int kImgRaster = 16;
 static const uint32_t kImgRasterWords = (kImgRaster * kImgRaster + 2) / 2;  // the list offsets
-static const uint32_t kImgMaxChips = (kImgCapWords - kImgHdrWords - kImgRasterWords) / 8;  // (8 words per chip)
+// chip records: 8 words and a pad word (a stride of 9 words spreads the records of random chips over
+// the 64 LDS banks; at 8 words every record started in one of 8 banks)
+static const uint32_t kImgChipWords = 9;
+static const uint32_t kImgMaxChips = (kImgCapWords - kImgHdrWords - kImgRasterWords) / kImgChipWords;
 static const int kImgMaxLevel = 2;
 // per tile record: kImgRaster^2 bits, bit q set when some chip's envelope meets envelope-raster cell
 // q (all set for a record without images); k_bin_cover drops the points of clear cells, which no
@@ -176,7 +179,7 @@ inline bool block_image(const ImageSource& s, uint32_t r, uint32_t level_part, c
     for (uint32_t k = 0; k < (uint32_t)tc.size(); k++)
         if (tc[k].x1 >= bx0 && tc[k].x0 <= bx1 && tc[k].y1 >= by0 && tc[k].y0 <= by1) sel.push_back(k);
     const uint32_t nc = (uint32_t)sel.size();
-    if (nc > kImgMaxChips || 8u * nc > s.cap_words) return false;
+    if (nc > kImgMaxChips || kImgChipWords * nc > s.cap_words) return false;
     std::vector<std::vector<uint16_t>> lists((size_t)G * G);
     uint32_t n_ent = 0;
     for (uint32_t c = 0; c < nc; c++) {
@@ -190,7 +193,7 @@ inline bool block_image(const ImageSource& s, uint32_t r, uint32_t level_part, c
     const uint32_t rast_off = kImgHdrWords;
     const uint32_t rast_words = ((uint32_t)(G * G + 1) + n_ent + 1) / 2;
     const uint32_t chip_off = (rast_off + rast_words + 3u) & ~3u;
-    const uint32_t vert_off = chip_off + 8u * nc;
+    const uint32_t vert_off = (chip_off + kImgChipWords * nc + 3u) & ~3u;
     if (vert_off > s.cap_words || (uint32_t)(G * G + 1) + n_ent >= 0xffffu) return false;
     w.assign(vert_off, 0u);
     w[0] = nc;
@@ -209,7 +212,7 @@ inline bool block_image(const ImageSource& s, uint32_t r, uint32_t level_part, c
     uint32_t nv = 0, glob = 0;
     for (uint32_t c = 0; c < nc; c++) {
         const uint32_t g = tc[sel[c]].g;
-        uint32_t* cr = &w[chip_off + 8u * c];
+        uint32_t* cr = &w[chip_off + kImgChipWords * c];
         cr[0] = s.meta[g];
         cr[2] = g;
         cr[3] = tc[sel[c]].slot;

@@ -116,7 +116,7 @@ int main(int argc, char** argv) {
         const uint32_t* chips = im + im[2];
         const float* V = (const float*)(im + im[3]);
         for (uint32_t c = 0; c < nc; c++) {
-            const uint32_t* cr = chips + 8u * c;
+            const uint32_t* cr = chips + binned::kImgChipWords * c;
             const uint32_t q = cr[2], e = tb.entries[tr.off + cr[3]];
             bool ok = e != 0 && q >= first_of(e) && q < first_of(e) + count[e - 1] && cr[0] == meta[q];
             if (!ok) {
@@ -196,7 +196,7 @@ int main(int argc, char** argv) {
             const uint32_t* chips = im + im[2];
             const uint16_t* rl = (const uint16_t*)(im + im[4]);
             std::vector<uint32_t> lst;
-            for (uint32_t p = rl[cell]; p < rl[cell + 1]; p++) lst.push_back(chips[8u * rl[p] + 2]);
+            for (uint32_t p = rl[cell]; p < rl[cell + 1]; p++) lst.push_back(chips[binned::kImgChipWords * rl[p] + 2]);
             bad += covered != !lst.empty();
             for (uint32_t q : wchips) {
                 const pip::Box& bx = gb.geom_bbox[q];

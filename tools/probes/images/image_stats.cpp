@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
         const uint32_t* im = set.words.data() + set.off[k];
         chips += im[0];
         for (uint32_t c = 0; c < im[0]; c++)
-            if (!(im[im[2] + 8u * c] & 1u) && (im[im[2] + 8u * c + 1] >> 16) == binned::kImgGlobal) glob++;
+            if (!(im[im[2] + binned::kImgChipWords * c] & 1u) && (im[im[2] + binned::kImgChipWords * c + 1] >> 16) == binned::kImgGlobal) glob++;
         w_rast += im[2] - im[4];
         w_chip += im[3] - im[2];
         w_vert += 2.0 * im[1];
