@@ -2027,6 +2027,28 @@ int mosaic_ctx_exec(mosaic_ctx* ctx, int* device, void** stream, int* jdk, int* 
 int mosaic_abi_version(void) { return MOSAIC_ABI_VERSION; }
 const char* mosaic_last_error(void) { return g_last_error.c_str(); }
 
+// Context entry pays the device's one-time costs so that the first table build and join do not: a
+// 4 MB pageable upload (the HIP runtime's setup for megabyte-sized pageable copies, 5.5 ms on its
+// first use in a process) and ~3 ms of work on every CU (the GPU leaves its idle clock state; the
+// build's first kernels ran up to 5x slower on a fresh box without it).  Bounded: s_memrealtime
+// runs at 100 MHz, and the loop stops after 2^22 reads whatever the clock says.
+__global__ void __launch_bounds__(256) k_warm_up(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned int spins = 0; spins < (1u << 22) && __builtin_amdgcn_s_memrealtime() - t0 < ticks; spins++) {
+    }
+}
+
+static void warm_up(int n_cu) {
+    const size_t bytes = (size_t)4 << 20;
+    void* d = nullptr;
+    if (hipMalloc(&d, bytes) != hipSuccess) return;
+    std::vector<uint8_t> h(bytes, 0);
+    (void)hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_warm_up, dim3((unsigned)std::max(1, n_cu * 4)), dim3(256), 0, 0, 300000ULL);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(d);
+}
+
 int mosaic_init(int device, mosaic_ctx** out) {
     if (!out) return fail(MOSAIC_E_ARG, "out is null");
     int count = 0;
@@ -2046,6 +2068,7 @@ int mosaic_init(int device, mosaic_ctx** out) {
         mosaic_destroy(c);
         return MOSAIC_E_HIP;
     }
+    warm_up(c->n_cu);
     *out = c;
     return MOSAIC_OK;
 }
