@@ -3811,6 +3811,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             bs.leaf = (const uint16_t*)ch->bng_leaf.p;
             bs.cells_bytes = (uint32_t)((size_t)ch->bng_ne * ch->bng_nn * 4);
             bs.leaf_bytes = (uint32_t)std::min<size_t>(ch->bng_leaf_bytes, kNoLoad);
+            bs.lvl_off = (uint32_t)tiles::bng_level_offset(ch->bng_C);
+            bs.lvl_cb = tiles::bng_level_side(ch->bng_C);
             const int64_t chunk = ((int64_t)1 << 32) - 256;
             const int64_t rows = std::min<int64_t>(n, chunk);
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;

@@ -662,6 +662,14 @@ struct BngBorderCell {
 // kMixed, or kSubBlock | kLineBit | n for a sub-cell split by one straight chip edge (LineRec n of
 // the cell, evaluated at the point's offset in the sub-cell in sub-cell units, stored at
 // blocks[base - 8 (n + 1)]); base[k] = element offset of cell k's block (a multiple of 8).
+// After each block, at base + bng_level_offset(C) (a multiple of 64 elements: one 128-byte line for
+// C <= 32), the cell's sub-block level: per 4 x 4 group of sub-cells (bng_level_side(C) groups per
+// row, row-major) the group's code when all its sub-cells carry the same code that is not a line
+// code, else kSubBlock ("read the sub-cell's own code").  k_join_stream_bng_cpt reads the level
+// first and the leaf code only for kSubBlock groups, so the rows of uniform groups touch one line
+// per border cell (L2-resident) instead of a line of the cell's 2 KB leaf block.
+inline size_t bng_level_offset(int C) { return ((size_t)C * C + 7) & ~(size_t)7; }
+inline int bng_level_side(int C) { return (C + 3) / 4; }
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
                      bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base);
 
