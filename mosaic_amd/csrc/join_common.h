@@ -270,8 +270,8 @@ __device__ inline uint32_t quad_lookup(const StreamArgs& s, const uint16_t* quad
 // Border cells carry kBngLeaf | base: C x C sub-cell entries at leaf[base] (the H3 point raster's
 // codes, tiles_build.cpp bng_leaf_blocks) -- a code, kMixed (the row goes to the mixed queue) or
 // kSubBlock | kLineBit | n: the sub-cell is split by one straight chip edge, LineRec n of the cell at
-// leaf[base - 8 (n + 1)] decides the point from its offset in the sub-cell.  A sub-block level
-// (one code per 4 x 4 group of sub-cells, or kSubBlock: read the leaf code) follows each block.
+// leaf[base - 8 (n + 1)] decides the point from its offset in the sub-cell.  A dense sub-block level
+// (per cell one code per 4 x 4 group of sub-cells, or kSubBlock: read the leaf code) sits beside.
 static const uint32_t kBngPure = 0x80000000u, kBngLeaf = 0x40000000u;
 static const uint32_t kBngLdsGather = 0xFFu;
 struct BngStreamArgs {
@@ -284,8 +284,9 @@ struct BngStreamArgs {
     uint32_t cells_bytes, leaf_bytes;
     const uint32_t* lcell;   // LDS cell level (bytes packed in words); nullptr / lcell_words == 0: none
     int32_t lcell_words, lsh, lnx;
-    uint32_t lvl_off;        // a border cell's sub-block level at leaf[base + lvl_off] (tiles.h
-    int32_t lvl_cb;          // bng_level_offset), lvl_cb groups of 4 x 4 sub-cells per row
+    const uint16_t* lvl;     // sub-block levels: cell index i's at lvl[i lvl_stride] (tiles.h
+    uint32_t lvl_bytes;      // bng_level_code), lvl_cb groups of 4 x 4 sub-cells per row; only
+    int32_t lvl_stride, lvl_cb;  // k_join_stream_bng_cpt reads them
 };
 
 // The stream kernels (join_stream.hip), by template arguments: the host picks one and launches it

@@ -836,23 +836,26 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 // cell level; rows in empty or pure blocks (82 % of uniform C5 points), rows outside the one-to-one
 // range (kMixed) and NaN rows (flagged) are answered there.  The others ("pending": in a border cell)
 // go through a per-wave LDS buffer into one 64-lane set -- per row the cell index with the source
-// lane and row slot, and the f32 sub-cell coordinates -- whose cell-entry, sub-block-level,
-// sub-cell-code and line-record gathers and answers take one lane per pending row, as a five-stage
-// software pipeline over the sets (iteration t: answers of the set of t - 4, line-record gathers of
-// t - 3, sub-cell-code gathers of t - 2 (only rows whose 4 x 4 group the level does not decide),
-// sub-block-level gathers of t - 1, group t's LDS level + compaction + cell-entry gathers,
-// coordinates of t + 1).  The level (128 B per border cell, tiles.h bng_level_offset) stays in L2
-// where the 2 KB leaf blocks do not.  More than 64 pending rows in a group are finished at once.
-// Needs ne nn < 2^24 (cell index in 24 bits).  The sub-cell arithmetic is k_join_stream_bng's and a
-// level code is the code of every sub-cell of its group, so the answers are the same point for point.
+// lane and row slot, and the f32 sub-cell coordinates -- whose cell-entry + sub-block-level,
+// sub-cell-code and line-record gathers and answers take one lane per pending row, as a four-stage
+// software pipeline over the sets (iteration t: answers of the set of t - 3, line-record gathers of
+// t - 2, sub-cell gathers of t - 1, group t's LDS level + compaction + cell-entry and level gathers,
+// coordinates of t + 1).  The sub-block level (BngStreamArgs::lvl: per table cell one code per 4 x 4
+// group of sub-cells, 128 B, read only for border cells, so the lines touched -- 2.6 MB for C5 --
+// stay in L2) is gathered beside the cell entry, from the cell index alone; the 2-byte leaf code
+// (2 KB leaf blocks over 41 MB) only for the rows whose group the level does not decide.
+// More than 64 pending rows in a group are finished at once.  Needs ne nn < 2^24 (cell index in 24
+// bits).  The sub-cell arithmetic is k_join_stream_bng's and a level code is the code of each
+// sub-cell of its group, so the answers are the same point for point.
 struct BngCptSet {
     uint32_t a;     // cell index | source lane << 24 | row slot k << 30
     uint32_t b, c;  // f32 sub-cell coordinates gxs, gys
-    uint32_t e;     // A -> B: gathered cell entry; B -> L: gathered level code; L -> C: sub-cell code
+    uint32_t e;     // A -> B: gathered cell entry; B -> C: the sub-cell code
+    uint32_t l;     // A -> B: gathered sub-block level code
     uint32_t p;     // 0: empty slot; B -> C: the answer, or kBngLeaf; C -> D: the answer or kPipeLine
 };
-// (the cell's leaf base, B -> L and L -> C, and the line record, C -> D, are held by one set at a
-// time: one register copy each instead of one per set slot)
+// (the cell's leaf base, B -> C, and the line record, C -> D, are held by one set at a time: one
+// register copy each instead of one per set slot)
 
 template <bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_bng_cpt(JoinArgs a, BngStreamArgs s) {
@@ -869,6 +872,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rcell = stream_rsrc(s.cells, s.cells_bytes);
     const __amdgpu_buffer_rsrc_t rleaf = stream_rsrc(s.leaf, s.leaf_bytes);
+    const __amdgpu_buffer_rsrc_t rlvl = stream_rsrc(s.lvl, s.lvl_bytes);
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -905,26 +909,24 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     };
     // A': cell-entry gathers
     auto set_a = [&](BngCptSet& z) {
-        z.e = gather_b32(rcell, z.p != 0u, (z.a & 0xffffffu) << 2);
+        const uint32_t ci = z.a & 0xffffffu;
+        z.e = gather_b32(rcell, z.p != 0u, ci << 2);
+        const int sx = min(max((int)__uint_as_float(z.b), 0), (int)C - 1);  // (subcell's clamp)
+        const int sy = min(max((int)__uint_as_float(z.c), 0), (int)C - 1);
+        const uint32_t g = __umul24((uint32_t)sy >> 2, (uint32_t)s.lvl_cb) + ((uint32_t)sx >> 2);
+        z.l = gather_b16<0>(rlvl, z.p != 0u, (ci * (uint32_t)s.lvl_stride + g) << 1);
     };
-    // B': cell entry -> sub-block level gather (the point's 4 x 4 group of sub-cells)
+    // B': cell entry + level code -> sub-cell code gather (rows of undecided groups)
     auto set_b = [&](BngCptSet& z, uint32_t& base) {
         const uint32_t e = z.e;
         const bool leafc = z.p != 0u && (e & (kBngPure | kBngLeaf)) == kBngLeaf;
         base = e & ~kBngLeaf;
-        const int sx = min(max((int)__uint_as_float(z.b), 0), (int)C - 1);  // (subcell's clamp)
-        const int sy = min(max((int)__uint_as_float(z.c), 0), (int)C - 1);
-        const uint32_t g = __umul24((uint32_t)sy >> 2, (uint32_t)s.lvl_cb) + ((uint32_t)sx >> 2);
-        z.e = gather_b16<0>(rleaf, leafc, (base + s.lvl_off + g) << 1);
-        z.p = z.p == 0u ? 0u : ((e & kBngPure) ? (e & ~kBngPure) : (leafc ? kBngLeaf : (e ? (uint32_t)tiles::kMixed : 0u)));
-    };
-    // L': level code -> sub-cell code gather, for the rows whose group the level does not decide
-    auto set_l = [&](BngCptSet& z, uint32_t base) {
-        const bool see = z.p == kBngLeaf && z.e == (uint32_t)tiles::kSubBlock;
         float su, sv;
         const uint32_t q = subcell(z, &su, &sv);
+        const bool see = leafc && z.l == (uint32_t)tiles::kSubBlock;  // the level does not decide
         const uint32_t v = gather_b16<0>(rleaf, see, (base + q) << 1);
-        z.e = see ? v : z.e;
+        z.e = see ? v : z.l;
+        z.p = z.p == 0u ? 0u : ((e & kBngPure) ? (e & ~kBngPure) : (leafc ? kBngLeaf : (e ? (uint32_t)tiles::kMixed : 0u)));
     };
     // C': sub-cell code -> line-record gather
     auto set_c = [&](BngCptSet& z, uint32_t base, v4u& lrec) {
@@ -1020,7 +1022,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
                 gather_set(sv, o);
                 set_a(o);
                 set_b(o, ob);
-                set_l(o, ob);
                 set_c(o, ob, orec);
                 set_d(o, orec, wb);
             }
@@ -1036,20 +1037,17 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         cb.py[0] = __builtin_nontemporal_load((const v2d*)(a.y + r));
         cb.py[1] = __builtin_nontemporal_load((const v2d*)(a.y + r + 128));
     };
-    BngCptSet z0, z1, z2, z3;
-    z0.a = z1.a = z2.a = z3.a = z0.b = z1.b = z2.b = z3.b = z0.c = z1.c = z2.c = z3.c = 0u;
-    z0.e = z1.e = z2.e = z3.e = z0.p = z1.p = z2.p = z3.p = 0u;
-    uint32_t base_bl = 0u, base_lc = 0u;  // the leaf base of the set between stages B and L, L and C
-    v4u lrec_cd = {0u, 0u, 0u, 0u};       // the line record of the set between stages C and D
-    // zd: the set of t - 4, refilled with group t; zc: t - 3; zl: t - 2; zb: t - 1
-    auto step = [&](bool valid, int64_t t, BngCptSet& zd, BngCptSet& zc, BngCptSet& zl, BngCptSet& zb, Coords& cb,
-                    Coords& cn) {
+    BngCptSet z0, z1, z2;
+    z0.a = z1.a = z2.a = z0.b = z1.b = z2.b = z0.c = z1.c = z2.c = 0u;
+    z0.e = z1.e = z2.e = z0.p = z1.p = z2.p = z0.l = z1.l = z2.l = 0u;
+    uint32_t base_bc = 0u;            // the leaf base of the set between stages B and C
+    v4u lrec_cd = {0u, 0u, 0u, 0u};   // the line record of the set between stages C and D
+    // zd: the set of t - 3, refilled with group t; zc: t - 2; zb: t - 1
+    auto step = [&](bool valid, int64_t t, BngCptSet& zd, BngCptSet& zc, BngCptSet& zb, Coords& cb, Coords& cn) {
         const bool all[4] = {true, true, true, true};
-        if (t >= 4) set_d(zd, lrec_cd, wbase + (t - 4) * stride);
-        set_c(zc, base_lc, lrec_cd);
-        set_l(zl, base_bl);
-        base_lc = base_bl;
-        set_b(zb, base_bl);
+        if (t >= 3) set_d(zd, lrec_cd, wbase + (t - 3) * stride);
+        set_c(zc, base_bc, lrec_cd);
+        set_b(zb, base_bc);
         const double x[4] = {cb.px[0].x, cb.px[0].y, cb.px[1].x, cb.px[1].y};
         const double y[4] = {cb.py[0].x, cb.py[0].y, cb.py[1].x, cb.py[1].y};
         stage_a(x, y, all, valid, zd, wbase + t * stride);
@@ -1059,25 +1057,28 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         Coords cb0, cb1;
         load4(cb0, wbase, true);
         int64_t t = 0;
-        for (; t + 4 <= T; t += 4) {
-            step(true, t, z0, z1, z2, z3, cb0, cb1);
-            step(true, t + 1, z1, z2, z3, z0, cb1, cb0);
-            step(true, t + 2, z2, z3, z0, z1, cb0, cb1);
-            step(true, t + 3, z3, z0, z1, z2, cb1, cb0);
+        for (; t + 6 <= T; t += 6) {
+            step(true, t, z0, z1, z2, cb0, cb1);
+            step(true, t + 1, z1, z2, z0, cb1, cb0);
+            step(true, t + 2, z2, z0, z1, cb0, cb1);
+            step(true, t + 3, z0, z1, z2, cb1, cb0);
+            step(true, t + 4, z1, z2, z0, cb0, cb1);
+            step(true, t + 5, z2, z0, z1, cb1, cb0);
         }
-        // the remaining groups (<= 3) and the four drain steps, in the same slot sequence
-#define MOSAIC_BCPT_TAIL(ZD, ZC, ZL, ZB, CB, CN) \
-    if (t < T + 4) {                           \
-        step(t < T, t, ZD, ZC, ZL, ZB, CB, CN); \
-        t++;                                   \
+        // the remaining groups (<= 5) and the three drain steps, in the same slot sequence
+#define MOSAIC_BCPT_TAIL(ZD, ZC, ZB, CB, CN) \
+    if (t < T + 3) {                       \
+        step(t < T, t, ZD, ZC, ZB, CB, CN); \
+        t++;                               \
     }
-        MOSAIC_BCPT_TAIL(z0, z1, z2, z3, cb0, cb1)
-        MOSAIC_BCPT_TAIL(z1, z2, z3, z0, cb1, cb0)
-        MOSAIC_BCPT_TAIL(z2, z3, z0, z1, cb0, cb1)
-        MOSAIC_BCPT_TAIL(z3, z0, z1, z2, cb1, cb0)
-        MOSAIC_BCPT_TAIL(z0, z1, z2, z3, cb0, cb1)
-        MOSAIC_BCPT_TAIL(z1, z2, z3, z0, cb1, cb0)
-        MOSAIC_BCPT_TAIL(z2, z3, z0, z1, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z0, z1, z2, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z1, z2, z0, cb1, cb0)
+        MOSAIC_BCPT_TAIL(z2, z0, z1, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z0, z1, z2, cb1, cb0)
+        MOSAIC_BCPT_TAIL(z1, z2, z0, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z2, z0, z1, cb1, cb0)
+        MOSAIC_BCPT_TAIL(z0, z1, z2, cb0, cb1)
+        MOSAIC_BCPT_TAIL(z1, z2, z0, cb1, cb0)
 #undef MOSAIC_BCPT_TAIL
     }
     // the wave's partial group, unpipelined
@@ -1097,7 +1098,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         v4u zrec;
         stage_a(x, y, live, true, z, wt);
         set_b(z, zb);
-        set_l(z, zb);
         set_c(z, zb, zrec);
         set_d(z, zrec, wt);
     }

@@ -1924,8 +1924,9 @@ struct mosaic_chips {
     int64_t tile_stats[6] = {0, 0, 0, 0, 0, 0};  // nx, ny, records, entries, kFull tiles, rings
     bool bng_ok = false;  // BNG dense cell table (k_join_stream_bng)
     int32_t bng_e0 = 0, bng_n0 = 0, bng_ne = 0, bng_nn = 0, bng_div = 1, bng_C = 0;
-    DevBuf bng_cells, bng_leaf, bng_lcell;
-    size_t bng_leaf_bytes = 0;
+    DevBuf bng_cells, bng_leaf, bng_lcell, bng_lvl;
+    size_t bng_leaf_bytes = 0, bng_lvl_bytes = 0;  // bng_lvl: sub-block levels (tiles.h bng_level_code); 0: none
+    bool bng_cpt_ok = false;  // levels built, or no border cell has a leaf block (k_join_stream_bng_cpt applies)
     int32_t bng_lwords = 0, bng_lsh = 0, bng_lnx = 0;  // LDS cell level (BngStreamArgs::lcell); 0 words: none
     int64_t bng_sub_stats[2] = {0, 0};                 // border-cell sub-cells: kMixed, line records
     bool raster_ok = false;                       // point raster (tiles.h)
@@ -1947,7 +1948,7 @@ struct mosaic_chips {
     size_t raster_parts[6] = {0, 0, 0, 0, 0, 0};  // bytes of sub, blocks, tile_base, quad, qrec masks, qrec codes
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell,
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell, &bng_lvl,
                           &img_words, &img_off, &img_rec, &img_binmap})
             b->release();
         store.release();
@@ -3239,6 +3240,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             // leaf blocks of the border cells (C x C sub-cell entries, C = option bng_cell: 3.1 m
             // sub-cells at 100 m resolution with the default 32; line records with option raster_lines)
             std::vector<uint16_t> leaf;
+            std::vector<uint32_t> lbase_kept;  // border cell b's leaf block at leaf[lbase_kept[b]]
             const int C = c->bng_cell;
             if (!border.empty()) {
                 std::vector<uint32_t> sfirst(capacity, 0), scount(capacity, 0);
@@ -3256,7 +3258,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 src.n_polygons = n_polygons;
                 int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
                 // (leaf offsets are 32-bit buffer offsets in k_join_stream_bng)
-                std::vector<uint32_t> lbase;
+                std::vector<uint32_t>& lbase = lbase_kept;
                 // (leaf element offsets < 2^30, byte offsets below kNoLoad)
                 if (tiles::bng_leaf_blocks(src, border, (double)div, C, c->raster_lines != 0, threads, leaf, lbase) &&
                     leaf.size() * 2 < (size_t)kNoLoad) {
@@ -3274,6 +3276,18 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 }
             }
             if (leaf.empty()) leaf.assign((size_t)C * C, tiles::kMixed);
+            // sub-block levels, dense over the table's cells (only border cells' lines are ever read:
+            // k_join_stream_bng_cpt gathers them beside the cell entry); tables too large for a
+            // 512 MB level array take k_join_stream_bng
+            std::vector<uint16_t> lvl;
+            const int LV = tiles::bng_level_stride(C), CB = tiles::bng_level_side(C);
+            if (ch->bng_C && (size_t)tab.size() * LV * 2 <= ((size_t)512 << 20)) {
+                lvl.assign(tab.size() * (size_t)LV, tiles::kMixed);
+                for (size_t b = 0; b < border.size(); b++)
+                    for (int bj = 0; bj < CB; bj++)
+                        for (int bi = 0; bi < CB; bi++)
+                            lvl[border_at[b] * LV + (size_t)bj * CB + bi] = tiles::bng_level_code(&leaf[lbase_kept[b]], C, bi, bj);
+            }
             // LDS cell level (BngStreamArgs::lcell): the finest block size 2^lsh whose byte table fits
             // the stream kernel's LDS beside its counts and 16 per-wave stages
             std::vector<uint8_t> lcell;
@@ -3307,6 +3321,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             }
             size_t bb = tab.size() * 4, lb = leaf.size() * 2;
             if ((rc = ch->bng_cells.reserve(bb)) || (rc = ch->bng_leaf.reserve(lb)) ||
+                (!lvl.empty() && (rc = ch->bng_lvl.reserve(lvl.size() * 2))) ||
                 (!lcell.empty() && (rc = ch->bng_lcell.reserve(lcell.size())))) {
                 ch->release_all();
                 delete ch;
@@ -3314,6 +3329,12 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             }
             HIP_TRY(hipMemcpy(ch->bng_cells.p, tab.data(), bb, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(ch->bng_leaf.p, leaf.data(), lb, hipMemcpyHostToDevice));
+            if (!lvl.empty()) {
+                HIP_TRY(hipMemcpy(ch->bng_lvl.p, lvl.data(), lvl.size() * 2, hipMemcpyHostToDevice));
+                ch->bng_lvl_bytes = lvl.size() * 2;
+                total += lvl.size() * 2;
+            }
+            ch->bng_cpt_ok = !lvl.empty() || !ch->bng_C;
             if (!lcell.empty()) {
                 HIP_TRY(hipMemcpy(ch->bng_lcell.p, lcell.data(), lcell.size(), hipMemcpyHostToDevice));
                 ch->bng_lwords = (int32_t)(lcell.size() / 4);
@@ -3811,7 +3832,9 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             bs.leaf = (const uint16_t*)ch->bng_leaf.p;
             bs.cells_bytes = (uint32_t)((size_t)ch->bng_ne * ch->bng_nn * 4);
             bs.leaf_bytes = (uint32_t)std::min<size_t>(ch->bng_leaf_bytes, kNoLoad);
-            bs.lvl_off = (uint32_t)tiles::bng_level_offset(ch->bng_C);
+            bs.lvl = (const uint16_t*)ch->bng_lvl.p;
+            bs.lvl_bytes = (uint32_t)ch->bng_lvl_bytes;
+            bs.lvl_stride = tiles::bng_level_stride(ch->bng_C);
             bs.lvl_cb = tiles::bng_level_side(ch->bng_C);
             const int64_t chunk = ((int64_t)1 << 32) - 256;
             const int64_t rows = std::min<int64_t>(n, chunk);
@@ -3829,7 +3852,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             // k_join_stream_bng_cpt (option bng_cpt): with the LDS cell level, a 24-bit cell index and
             // room for its per-wave compaction buffers
             const size_t cpt_bytes = (size_t)(blkb / 64) * kCptBufWords * 4;
-            const bool bcpt = c->bng_cpt && aligned && bs.lcell_words > 0 &&
+            const bool bcpt = c->bng_cpt && aligned && bs.lcell_words > 0 && ch->bng_cpt_ok &&
                               (int64_t)ch->bng_ne * ch->bng_nn < ((int64_t)1 << 24) && shm_b + cpt_bytes <= kStreamLdsMax;
             if (bcpt) shm_b += cpt_bytes;
             auto kernel_for = [&](bool vec) -> const void* {

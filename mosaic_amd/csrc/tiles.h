@@ -662,14 +662,22 @@ struct BngBorderCell {
 // kMixed, or kSubBlock | kLineBit | n for a sub-cell split by one straight chip edge (LineRec n of
 // the cell, evaluated at the point's offset in the sub-cell in sub-cell units, stored at
 // blocks[base - 8 (n + 1)]); base[k] = element offset of cell k's block (a multiple of 8).
-// After each block, at base + bng_level_offset(C) (a multiple of 64 elements: one 128-byte line for
-// C <= 32), the cell's sub-block level: per 4 x 4 group of sub-cells (bng_level_side(C) groups per
-// row, row-major) the group's code when all its sub-cells carry the same code that is not a line
-// code, else kSubBlock ("read the sub-cell's own code").  k_join_stream_bng_cpt reads the level
-// first and the leaf code only for kSubBlock groups, so the rows of uniform groups touch one line
-// per border cell (L2-resident) instead of a line of the cell's 2 KB leaf block.
-inline size_t bng_level_offset(int C) { return ((size_t)C * C + 7) & ~(size_t)7; }
+// The cells' sub-block levels (BngStreamArgs::lvl): per border cell, per 4 x 4 group of sub-cells
+// (bng_level_side(C) groups per row, row-major, bng_level_stride(C) entries per cell) the group's
+// code when all its sub-cells carry the same code that is not a line code, else kSubBlock ("read the
+// sub-cell's own code").  k_join_stream_bng_cpt gathers the level beside the cell entry and the leaf
+// code only for kSubBlock groups, so the rows of uniform groups touch one 128-byte line per border
+// cell (L2-resident) instead of a line of the cell's 2 KB leaf block.
 inline int bng_level_side(int C) { return (C + 3) / 4; }
+inline int bng_level_stride(int C) { return ((bng_level_side(C) * bng_level_side(C) + 63) / 64) * 64; }
+inline uint16_t bng_level_code(const uint16_t* e, int C, int bi, int bj) {
+    const uint16_t v = e[(size_t)(4 * bj) * C + 4 * bi];
+    if (v != kMixed && (v & 0xC000u) == 0xC000u) return kSubBlock;  // a line code: per sub-cell
+    for (int j = 4 * bj; j < std::min(C, 4 * bj + 4); j++)
+        for (int i = 4 * bi; i < std::min(C, 4 * bi + 4); i++)
+            if (e[(size_t)j * C + i] != v) return kSubBlock;
+    return v;
+}
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
                      bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base);
 

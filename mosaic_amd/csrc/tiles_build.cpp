@@ -842,37 +842,21 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
     for (int t = 1; t < nt; t++) pool.emplace_back(work);
     work();
     for (auto& t : pool) t.join();
-    // layout per border cell: padding (kMixed) that puts its level on a 128-byte boundary, its line
-    // records (8 elements each, record n at base - 8 (n + 1)), its leaf block at base, its sub-block
-    // level at base + CCp (tiles.h bng_level_offset)
-    const int CB = bng_level_side(C);
-    const size_t LVp = ((size_t)CB * CB + 63) & ~(size_t)63;
-    auto level_of = [&](const std::vector<uint16_t>& e, int bi, int bj) -> uint16_t {
-        const uint16_t v = e[(size_t)(4 * bj) * C + 4 * bi];
-        if (v != kMixed && (v & 0xC000u) == 0xC000u) return kSubBlock;  // a line code: per sub-cell
-        for (int j = 4 * bj; j < std::min(C, 4 * bj + 4); j++)
-            for (int i = 4 * bi; i < std::min(C, 4 * bi + 4); i++)
-                if (e[(size_t)j * C + i] != v) return kSubBlock;
-        return v;
-    };
-    auto pad_of = [&](size_t at, size_t nl) -> size_t { return (64 - (at + 8 * nl + CCp) % 64) % 64; };
+    // layout per border cell: its line records (8 elements each, record n at base - 8 (n + 1)),
+    // then its leaf block at base
     size_t total = 0;
-    for (size_t k = 0; k < cells.size(); k++) total += pad_of(total, lrec[k].size()) + lrec[k].size() * 8 + CCp + LVp;
+    for (size_t k = 0; k < cells.size(); k++) total += lrec[k].size() * 8 + CCp;
     if (total >= ((size_t)1 << 30)) return false;  // element offsets share a word with the table's flags
     blocks.assign(total, kMixed);
     base.assign(cells.size(), 0);
     size_t at = 0;
     for (size_t k = 0; k < cells.size(); k++) {
         const size_t nl = lrec[k].size();
-        at += pad_of(at, nl);
         for (size_t n = 0; n < nl; n++) memcpy(&blocks[at + 8 * (nl - 1 - n)], &lrec[k][n], sizeof(LineRec));
         at += 8 * nl;
         base[k] = (uint32_t)at;
         memcpy(&blocks[at], ent[k].data(), CCp * 2);
         at += CCp;
-        for (int bj = 0; bj < CB; bj++)
-            for (int bi = 0; bi < CB; bi++) blocks[at + (size_t)bj * CB + bi] = level_of(ent[k], bi, bj);
-        at += LVp;
     }
     return true;
 }
