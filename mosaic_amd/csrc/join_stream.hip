@@ -913,7 +913,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         z.e = gather_b32(rcell, z.p != 0u, ci << 2);
         const int sx = min(max((int)__uint_as_float(z.b), 0), (int)C - 1);  // (subcell's clamp)
         const int sy = min(max((int)__uint_as_float(z.c), 0), (int)C - 1);
-        const uint32_t g = __umul24((uint32_t)sy >> 2, (uint32_t)s.lvl_cb) + ((uint32_t)sx >> 2);
+        const uint32_t g = __umul24((uint32_t)sy >> tiles::kBngLvlShift, (uint32_t)s.lvl_cb) + ((uint32_t)sx >> tiles::kBngLvlShift);
         z.l = gather_b16<0>(rlvl, z.p != 0u, (ci * (uint32_t)s.lvl_stride + g) << 1);
     };
     // B': cell entry + level code -> sub-cell code gather (rows of undecided groups)

@@ -668,13 +668,18 @@ struct BngBorderCell {
 // sub-cell's own code").  k_join_stream_bng_cpt gathers the level beside the cell entry and the leaf
 // code only for kSubBlock groups, so the rows of uniform groups touch one 128-byte line per border
 // cell (L2-resident) instead of a line of the cell's 2 KB leaf block.
-inline int bng_level_side(int C) { return (C + 3) / 4; }
+#ifndef MOSAIC_BNG_LVL_SHIFT
+#define MOSAIC_BNG_LVL_SHIFT 2  // groups of 4 x 4 sub-cells
+#endif
+static const int kBngLvlShift = MOSAIC_BNG_LVL_SHIFT, kBngLvlG = 1 << MOSAIC_BNG_LVL_SHIFT;
+inline int bng_level_side(int C) { return (C + kBngLvlG - 1) / kBngLvlG; }
 inline int bng_level_stride(int C) { return ((bng_level_side(C) * bng_level_side(C) + 63) / 64) * 64; }
 inline uint16_t bng_level_code(const uint16_t* e, int C, int bi, int bj) {
-    const uint16_t v = e[(size_t)(4 * bj) * C + 4 * bi];
+    const int G = kBngLvlG;
+    const uint16_t v = e[(size_t)(G * bj) * C + G * bi];
     if (v != kMixed && (v & 0xC000u) == 0xC000u) return kSubBlock;  // a line code: per sub-cell
-    for (int j = 4 * bj; j < std::min(C, 4 * bj + 4); j++)
-        for (int i = 4 * bi; i < std::min(C, 4 * bi + 4); i++)
+    for (int j = G * bj; j < std::min(C, G * bj + G); j++)
+        for (int i = G * bi; i < std::min(C, G * bi + G); i++)
             if (e[(size_t)j * C + i] != v) return kSubBlock;
     return v;
 }
