@@ -43,7 +43,9 @@
  *     mosaic_stream_wait_event before the call, or synchronises it first.
  *   - Calls are synchronous unless the context option "async" is 1, in which case device-pointer
  *     calls only enqueue work on the calling thread's stream (mosaic_sync() waits and reports
- *     deferred errors).
+ *     deferred errors).  Exception: a binned join (option "bin_points", tables without a usable point
+ *     raster) reads its kept-row count back once per sort chunk, so it blocks the calling thread
+ *     until each chunk's cover pass has run; its results are still reported through mosaic_sync.
  *   - Threads: a context is bound to one GPU and every entry point is thread-safe (SURVEY.md §8(b),
  *     the executor's task threads sharing one context; the reference's index systems are JVM
  *     singletons, H3IndexSystem.scala:22-27).  Each calling thread gets its own HIP stream (created
@@ -62,7 +64,8 @@
 extern "C" {
 #endif
 
-#define MOSAIC_ABI_VERSION 1
+/* 2: mosaic_chip_table_raster writes 8 values (was 5); option "exact_cap". */
+#define MOSAIC_ABI_VERSION 2
 
 typedef enum {
     MOSAIC_OK = 0,
@@ -116,7 +119,10 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * raster sort the points by tile before the chip loop -- the border-chip-heavy C4 shape; default 1),
  * "bin_min_rows" (smallest batch that is binned; default 2^18), "bin_chunk" (rows per sort chunk;
  * default 2^28), "tile_images" (0: none; 1: tables built without a point raster carry per-tile chip
- * images the binned join copies into LDS, the default; 2: every tile-directory table carries them). */
+ * images the binned join copies into LDS, the default; 2: every tile-directory table carries them),
+ * "exact_cap" (rows of the exact-H3 queue; 0 = the default max(n / 8, 2^20) capped at n; an overflow
+ * reruns the batch on the exact path, or is reported as MOSAIC_E_CAPACITY by mosaic_sync after an
+ * async call). */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);
 /* Per-thread state.  Each calling thread gets its own execution state on a context (HIP stream,
  * copy stream, timing events, scratch queues and staging sized by its largest call).  It is freed
@@ -382,8 +388,10 @@ int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, con
  * (reference H3IndexSystem.kRing / kLoop, core/index/H3IndexSystem.scala:154-177); where the walk
  * meets a pentagon, kRing is H3's _kRingInternal hash table read in slot order (as h3-java returns
  * it) and kLoop the reference's own fallback, kRing(k).toSet diff kRing(k - 1).toSet in Scala
- * HashSet order (:169-176); such rows need k <= 60 (MOSAIC_E_ARG otherwise).  A row whose id is
- * not a valid cell gets out_count[i] = -2 (no cells written). */
+ * HashSet order (:169-176).  That search makes ~5 k^3 dependent steps per row: such rows with
+ * k > 128 are not evaluated and get out_count[i] = -4 (evaluate them on the row path); the other rows
+ * of the call are answered.  A row whose id is not a valid cell gets out_count[i] = -2 (no cells
+ * written). */
 int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k,
                       int loop, int64_t* out, int32_t* out_count);
 

@@ -198,12 +198,14 @@ MOSAIC_HD bool hex_ring(uint64_t origin, int k, int64_t* out) {
 
 // _kRingInternal(origin, k, out, distances, maxIdx, 0) into a zeroed table out[maxIdx] with
 // distances dist[maxIdx]: the same depth-first visiting order as H3's recursion, on an explicit
-// stack (frames: cell, depth, next direction index)
-MOSAIC_HD void kring_internal(uint64_t origin, int k, int64_t* out, int32_t* dist, int max_idx) {
-    const int kMaxDepth = 64;
-    uint64_t st_cell[kMaxDepth];
-    int8_t st_next[kMaxDepth];
-    int sp = 0;
+// stack of k + 1 frames.  A frame is one word: the cell with its next direction index in the
+// reserved bits 56-58 (zero in every valid cell index).  stack: k + 1 words of scratch, or null for
+// k < kLocalDepth (a private array).
+static const int kLocalDepth = 63;
+MOSAIC_HD void kring_internal(uint64_t origin, int k, int64_t* out, int32_t* dist, int max_idx, uint64_t* stack) {
+    uint64_t local[kLocalDepth + 1];
+    uint64_t* st = stack ? stack : local;
+    const uint64_t kDirMask = 7ULL << 56;
     // visit(cell, cur_k): true if its neighbours are to be searched
     auto visit = [&](uint64_t cell, int cur_k) -> bool {
         if (cell == 0) return false;
@@ -218,24 +220,21 @@ MOSAIC_HD void kring_internal(uint64_t origin, int k, int64_t* out, int32_t* dis
         dist[off] = cur_k;
         return cur_k < k;
     };
+    if (!stack && k > kLocalDepth) return;  // (callers pass scratch beyond kLocalDepth)
     if (!visit(origin, 0)) return;
-    st_cell[0] = origin;
-    st_next[0] = 0;
-    sp = 1;
+    st[0] = origin;
+    int sp = 1;
     while (sp > 0) {
-        const int top = sp - 1;
-        if (st_next[top] == 6) {
+        const uint64_t f = st[sp - 1];
+        const int i = (int)((f >> 56) & 7);
+        if (i == 6) {
             sp--;
             continue;
         }
-        const int i = st_next[top]++;
+        st[sp - 1] = f + (1ULL << 56);
         int rotations = 0;
-        const uint64_t nb = neighbor_rotations(st_cell[top], direction(i), &rotations);
-        if (visit(nb, sp) && sp < kMaxDepth) {  // (the new frame's depth: cur_k + 1 = sp)
-            st_cell[sp] = nb;
-            st_next[sp] = 0;
-            sp++;
-        }
+        const uint64_t nb = neighbor_rotations(f & ~kDirMask, direction(i), &rotations);
+        if (visit(nb, sp)) st[sp++] = nb;  // (the new frame's depth: cur_k + 1 = sp <= k)
     }
 }
 
@@ -279,16 +278,21 @@ MOSAIC_HD int kring_fast(uint64_t origin, int k, int loop, int64_t* out) {
     return hex_range(origin, k, out) ? max_kring_size(k) : -3;
 }
 
-// The fallback rows (kring_fast == -3), k <= kSlowMaxK: kRing = _kRingInternal's table read in slot
-// order (h3-java drops its zeros); kLoop = the reference's kRing(k).toSet diff kRing(k - 1).toSet in
-// Scala HashSet order (H3IndexSystem.scala:169-176).  Scratch: tab[max_kring_size(k) +
-// max_kring_size(k - 1)] (int64), dist[max_kring_size(k)] (int32).  Returns the count in out.
-static const int kSlowMaxK = 60;
-MOSAIC_HD int kring_slow(uint64_t origin, int k, int loop, int64_t* out, int64_t* tab, int32_t* dist) {
-    if (k > kSlowMaxK) return -2;
+// The engine runs the fallback for k <= kSlowMaxK (H3's search makes ~5 k^3 dependent visits: ~5e6
+// at k = 100, 1e7 at 128); rows beyond it are returned unsupported (-4), not evaluated.
+static const int kSlowMaxK = 128;
+
+// The fallback rows (kring_fast == -3): kRing = _kRingInternal's table read in slot order (h3-java
+// drops its zeros); kLoop = the reference's kRing(k).toSet diff kRing(k - 1).toSet in Scala HashSet
+// order (H3IndexSystem.scala:169-176).  Scratch: tab[max_kring_size(k) + max_kring_size(k - 1)]
+// (int64), dist[max_kring_size(k)] (int32), stack[k + 1] (null for k <= kLocalDepth).  Returns the
+// count in out.
+MOSAIC_HD int kring_slow(uint64_t origin, int k, int loop, int64_t* out, int64_t* tab, int32_t* dist,
+                         uint64_t* stack = nullptr) {
+    if (!stack && k > kLocalDepth) return -2;
     const int m = max_kring_size(k);
     for (int i = 0; i < m; i++) tab[i] = 0, dist[i] = 0;
-    kring_internal(origin, k, tab, dist, m);
+    kring_internal(origin, k, tab, dist, m, stack);
     int n = 0;
     if (!loop) {
         for (int i = 0; i < m; i++)
@@ -299,7 +303,7 @@ MOSAIC_HD int kring_slow(uint64_t origin, int k, int loop, int64_t* out, int64_t
     const int m1 = k ? max_kring_size(k - 1) : 1;
     int64_t* tab1 = tab + m;
     for (int i = 0; i < m1; i++) tab1[i] = 0, dist[i] = 0;
-    if (k) kring_internal(origin, k - 1, tab1, dist, m1);
+    if (k) kring_internal(origin, k - 1, tab1, dist, m1, stack);
     for (int i = 0; i < m; i++) {
         const int64_t c = tab[i];
         if (!c) continue;

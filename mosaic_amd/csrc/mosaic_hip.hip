@@ -1045,14 +1045,18 @@ __global__ void __launch_bounds__(256) k_h3_kring(KringArgs a) {
     }
 }
 
-// the -3 rows of k_h3_kring (rows[0 .. n_rows)), one lane each, with per-lane scratch
-__global__ void __launch_bounds__(64) k_h3_kring_slow(KringArgs a, const int64_t* rows, int64_t n_rows, int64_t* tab,
-                                                      int64_t tab_stride, int32_t* dist, int64_t dist_stride) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// the -3 rows of k_h3_kring (rows[0 .. n_rows)), with per-row scratch (tables, distances, the
+// depth-first stack), `lanes` rows per 64-lane workgroup: 64 for small k, 1 for large k (H3's
+// search makes ~5 k^3 dependent visits per row, so rows sharing a wave would serialise)
+__global__ void __launch_bounds__(64) k_h3_kring_slow(KringArgs a, const int64_t* rows, int64_t n_rows, int lanes,
+                                                      int64_t* tab, int64_t tab_stride, int32_t* dist,
+                                                      int64_t dist_stride, uint64_t* stack) {
+    if ((int)threadIdx.x >= lanes) return;
+    const int64_t t = (int64_t)blockIdx.x * lanes + threadIdx.x;
     if (t >= n_rows) return;
     const int64_t i = rows[t];
     a.count[i] = h3nb::kring_slow((uint64_t)a.cells[i], a.k, a.loop, a.out + i * a.stride, tab + t * tab_stride,
-                                  dist + t * dist_stride);
+                                  dist + t * dist_stride, stack + t * (int64_t)(a.k + 1));
 }
 
 
@@ -1674,6 +1678,9 @@ struct Options {
     // per-tile chip images in LDS for the binned join: 0 off, 1 for tables without a point raster
     // (built with the table; joins use them when present), 2 built for every tile-directory table
     int tile_images = 1;
+    // exact-H3 queue capacity in rows (0: the default, max(n / 8, 2^20) capped at n); a small value
+    // exercises the overflow -> rerun path
+    int64_t exact_cap = 0;
 };
 
 // Execution state of one calling thread on one context: its HIP stream (created on first use, or
@@ -1696,6 +1703,7 @@ struct ThreadCtx : Options {
     int64_t stats[3] = {0, 0, 0};
     int64_t binned_rows = 0;  // rows the last join's binned path sorted (mosaic_last_binned_rows)
     unsigned int deferred_flags = 0;
+    uint64_t last_qcap = 0;  // the exact-H3 queue capacity of the last join (sync_impl's overflow test)
     std::vector<hipEvent_t> ev_start, ev_stop;
     size_t ev_used = 0;
     // the scratch buffers sized by the calls (not `scalars`, which every call needs)
@@ -1765,6 +1773,9 @@ __global__ void k_amb_roll(unsigned long long* sc, unsigned long long cap) {
     if (q > cap) sc[6] = 1;
     sc[0] = 0;
 }
+// After the last binned chunk: scalars[0] holds the rows of all chunks, or cap + 1 when one chunk
+// overflowed, so an async caller's sync (mosaic_sync, the host-chunked join) sees the overflow.
+__global__ void k_amb_final(unsigned long long* sc, unsigned long long cap) { sc[0] = sc[6] ? cap + 1 : sc[5]; }
 
 // Lifetime of per-thread states.  A thread's state on a context is freed by mosaic_thread_release,
 // by mosaic_destroy, or when the thread exits (ThreadExit below) -- so an executor whose worker pool
@@ -2039,14 +2050,19 @@ __global__ void __launch_bounds__(256) k_warm_up(unsigned long long ticks) {
     }
 }
 
-static void warm_up(int n_cu) {
+// On the creating thread's own stream (never the null stream: context creation must not wait for
+// other contexts' or torch's queued work); MOSAIC_NO_WARMUP=1 in the environment skips it.
+static void warm_up(ThreadCtx* t) {
+    const char* off = getenv("MOSAIC_NO_WARMUP");
+    if (off && off[0] == '1') return;
     const size_t bytes = (size_t)4 << 20;
     void* d = nullptr;
     if (hipMalloc(&d, bytes) != hipSuccess) return;
     std::vector<uint8_t> h(bytes, 0);
-    (void)hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice);
-    hipLaunchKernelGGL(k_warm_up, dim3((unsigned)std::max(1, n_cu * 4)), dim3(256), 0, 0, 300000ULL);
-    (void)hipDeviceSynchronize();
+    (void)hipMemcpyAsync(d, h.data(), bytes, hipMemcpyHostToDevice, t->stream);
+    hipLaunchKernelGGL(k_warm_up, dim3((unsigned)std::max(1, t->n_cu * 4)), dim3(256), 0, t->stream, 300000ULL);
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(t->stream);
     (void)hipFree(d);
 }
 
@@ -2065,11 +2081,12 @@ int mosaic_init(int device, mosaic_ctx** out) {
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-    if (!enter(c)) {  // the creating thread's state: fails early if the device cannot make a stream
+    ThreadCtx* t = enter(c);
+    if (!t) {  // the creating thread's state: fails early if the device cannot make a stream
         mosaic_destroy(c);
         return MOSAIC_E_HIP;
     }
-    warm_up(c->n_cu);
+    warm_up(t);
     *out = c;
     return MOSAIC_OK;
 }
@@ -2210,6 +2227,9 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "scratch_limit") {
         if (v < 0) return fail(MOSAIC_E_ARG, "scratch_limit must be >= 0");
         o.scratch_limit = v;
+    } else if (k == "exact_cap") {
+        if (v < 0) return fail(MOSAIC_E_ARG, "exact_cap must be >= 0");
+        o.exact_cap = v;
     } else {
         return fail(MOSAIC_E_ARG, "unknown option " + k);
     }
@@ -2264,7 +2284,7 @@ static int sync_impl(ThreadCtx* c) {
     unsigned int flags = c->deferred_flags | (unsigned int)s[3];
     c->deferred_flags = 0;
     if (flags & 1u) return fail(MOSAIC_E_NAN, "NaN coordinates are not supported.");
-    if ((flags & 2u) || s[0] > c->amb_queue.bytes / 8)
+    if ((flags & 2u) || s[0] > c->last_qcap)
         return fail(MOSAIC_E_CAPACITY, "exact-path queue overflowed in an async call; rerun synchronously");
     return MOSAIC_OK;
 }
@@ -3737,6 +3757,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
         HIP_TRY(hipGetLastError());
     }
     uint64_t qcap = (uint64_t)std::max<int64_t>(std::min<int64_t>(n, std::max<int64_t>(n / 8, 1 << 20)), 1);
+    if (c->exact_cap > 0) qcap = (uint64_t)c->exact_cap;
+    c->last_qcap = qcap;
     if ((rc = c->amb_queue.reserve(qcap * 8))) return rc;
     bool dev_pairs = pairs && is_device_ptr(out_row) && is_device_ptr(out_key);
     if (pairs && !dev_pairs) {
@@ -3992,6 +4014,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 hipLaunchKernelGGL(k_amb_roll, dim3(1), dim3(1), 0, c->stream, sc, (unsigned long long)qcap);
                 HIP_TRY(hipGetLastError());
             }
+            hipLaunchKernelGGL(k_amb_final, dim3(1), dim3(1), 0, c->stream, sc, (unsigned long long)qcap);
+            HIP_TRY(hipGetLastError());
         } else if (tiled) {
             c->last_kernel = "k_join_tiled";
             if (pairs) MOSAIC_LAUNCH((k_join_tiled<false, true>), 0);
@@ -4026,7 +4050,6 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
     HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned long long s[kScalars];
     HIP_TRY(hipMemcpy(s, c->scalars.p, sizeof s, hipMemcpyDeviceToHost));
-    if (binned_used) s[0] = s[6] ? qcap + 1 : s[5];  // (the queue was drained chunk by chunk)
     if (ch->grid == MOSAIC_GRID_H3 && s[0] > qcap && !exact_inline) {
         // queue overflow (adversarial input): recompute the whole batch on the exact path
         HIP_TRY(hipMemsetAsync(dcounts, 0, cbytes, c->stream));
@@ -4409,29 +4432,36 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
         std::vector<int64_t> rows;
         for (int64_t i = 0; i < n; i++)
             if (cnt[(size_t)i] == -3) rows.push_back(i);
+        if (!rows.empty() && k > h3nb::kSlowMaxK) {
+            // beyond kSlowMaxK H3's search (~5 k^3 visits) is not run: those rows only are marked
+            // unsupported (count -4) for the caller's row path; the rest of the batch is answered
+            for (int64_t i : rows) cnt[(size_t)i] = -4;
+            HIP_TRY(hipMemcpyAsync(a.count, cnt.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            rows.clear();
+        }
         if (!rows.empty()) {
-            if (k > h3nb::kSlowMaxK)
-                return done(fail(MOSAIC_E_ARG, "H3 k-ring with k > " + std::to_string(h3nb::kSlowMaxK) +
-                                                   " around a pentagon is not supported"));
             const int64_t m = h3nb::max_kring_size(k), m1 = k ? h3nb::max_kring_size(k - 1) : 1;
-            const int64_t per = std::max<int64_t>(1, ((int64_t)1 << 30) / ((m + m1) * 8 + m * 4));
-            DevBuf s_rows, s_tab, s_dist;
+            const int64_t per = std::max<int64_t>(1, ((int64_t)1 << 30) / ((m + m1) * 8 + m * 4 + (k + 1) * 8));
+            const int lanes = k >= 16 ? 1 : 64;
+            DevBuf s_rows, s_tab, s_dist, s_stack;
             auto done2 = [&](int r2) {
-                for (DevBuf* b : {&s_rows, &s_tab, &s_dist}) b->release();
+                for (DevBuf* b : {&s_rows, &s_tab, &s_dist, &s_stack}) b->release();
                 return done(r2);
             };
             for (size_t r0 = 0; r0 < rows.size(); r0 += (size_t)per) {
                 const int64_t nr = std::min<int64_t>(per, (int64_t)(rows.size() - r0));
                 if ((rc = s_rows.reserve((size_t)nr * 8)) || (rc = s_tab.reserve((size_t)(nr * (m + m1)) * 8)) ||
-                    (rc = s_dist.reserve((size_t)(nr * m) * 4)))
+                    (rc = s_dist.reserve((size_t)(nr * m) * 4)) || (rc = s_stack.reserve((size_t)(nr * (k + 1)) * 8)))
                     return done2(rc);
                 HIP_TRY(hipMemcpyAsync(s_rows.p, rows.data() + r0, (size_t)nr * 8, hipMemcpyHostToDevice, c->stream));
-                hipLaunchKernelGGL(k_h3_kring_slow, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, c->stream, a,
-                                   (const int64_t*)s_rows.p, nr, (int64_t*)s_tab.p, m + m1, (int32_t*)s_dist.p, m);
+                hipLaunchKernelGGL(k_h3_kring_slow, dim3((unsigned)((nr + lanes - 1) / lanes)), dim3(64), 0, c->stream, a,
+                                   (const int64_t*)s_rows.p, nr, lanes, (int64_t*)s_tab.p, m + m1, (int32_t*)s_dist.p, m,
+                                   (uint64_t*)s_stack.p);
                 HIP_TRY(hipGetLastError());
                 HIP_TRY(hipStreamSynchronize(c->stream));
             }
-            for (DevBuf* b : {&s_rows, &s_tab, &s_dist}) b->release();
+            for (DevBuf* b : {&s_rows, &s_tab, &s_dist, &s_stack}) b->release();
         }
     }
     unsigned int flags = 0;

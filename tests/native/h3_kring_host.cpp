@@ -16,7 +16,8 @@ extern "C" int h3_kring_host(int64_t cell, int k, int loop, int64_t* out, int* s
     const int m = mosaic::h3nb::max_kring_size(k), m1 = k ? mosaic::h3nb::max_kring_size(k - 1) : 1;
     std::vector<int64_t> tab((size_t)(m + m1));
     std::vector<int32_t> dist((size_t)m);
-    return mosaic::h3nb::kring_slow((uint64_t)cell, k, loop, out, tab.data(), dist.data());
+    std::vector<uint64_t> stack((size_t)k + 1);
+    return mosaic::h3nb::kring_slow((uint64_t)cell, k, loop, out, tab.data(), dist.data(), stack.data());
 }
 
 extern "C" int64_t h3_neighbor_host(int64_t cell, int dir) {

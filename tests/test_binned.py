@@ -79,6 +79,38 @@ def test_binned_zones_pairs_counts_chunks(h3ctx):
             t.close()
 
 
+def test_binned_host_chunked_exact_queue_overflow(h3ctx):
+    """Host-resident points through the binned join in async chunks (join_count_host_chunked): a
+    chunk whose exact-H3 rows exceed the queue (option exact_cap, tiny here) must be rerun, not
+    returned short; the chunks' exact rows must reach last_stats."""
+    zones = PolygonSet.load("nyc_taxi_zones_35")
+    chips = tessellate("H3", zones, 9)
+    rng = np.random.default_rng(23)
+    x0, y0, x1, y1 = zones.bbox()
+    bx, by = _chip_boundary_points(chips, rng)
+    x = np.concatenate([rng.uniform(x0, x1, 300_000), bx])
+    y = np.concatenate([rng.uniform(y0, y1, 300_000), by])
+    perm = rng.permutation(len(x))
+    x, y = np.ascontiguousarray(x[perm]), np.ascontiguousarray(y[perm])
+    want, _ = oracle.pip_join(_oracle_chips(chips), oracle.GRID_H3, 9, x, y, len(zones))
+    _set(h3ctx, tile_images=2)
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
+                             n_polygons=len(zones))
+    try:
+        _set(h3ctx, point_raster=0, bin_points=1, bin_min_rows=0, host_chunk=100_000)
+        got = h3ctx.pip_join_count(table, x, y)
+        assert h3ctx.last_kernel() == "k_join_tiles"
+        assert np.array_equal(got, want)
+        assert h3ctx.last_stats()["exact_path_rows"] > 0
+        for cap in (1, 3):
+            _set(h3ctx, exact_cap=cap)
+            assert np.array_equal(h3ctx.pip_join_count(table, x, y), want), cap
+    finally:
+        _set(h3ctx, point_raster=1, bin_points=1, bin_min_rows=1 << 18, host_chunk=1 << 25, tile_images=1,
+             exact_cap=0)
+        table.close()
+
+
 def test_binned_many_polygons_wave_hash(h3ctx):
     """60k building footprints at res 11 (n_polygons above the LDS count array: the per-wave hash
     of (key, count)), device points near the buildings."""

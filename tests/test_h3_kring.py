@@ -147,6 +147,23 @@ def test_pentagon_neighbourhoods(host_kring, host_lib):
     assert slow > 500
 
 
+K_BIG = 100
+
+
+def test_pentagon_large_k(host_kring):
+    """k = 100 around all 12 pentagons (the k > 60 limit lifted): H3's _kRingInternal
+    search with its depth-first stack in scratch; kRing / kLoop sets equal the oracle's sphere
+    search (1 + 5 k (k + 1) / 2 cells around a pentagon)."""
+    for i, bc in enumerate(PENTAGON_BASE_CELLS):
+        p = pentagon_cell(bc, 7 + i % 4)
+        ring, slow = host_kring(p, K_BIG, 0, want_slow=True)
+        want = oracle.h3_kring_set(p, K_BIG)
+        assert slow and len(ring) == len(set(ring)) == 1 + 5 * K_BIG * (K_BIG + 1) // 2
+        assert set(ring) == set(want), bc
+        loop = host_kring(p, K_BIG, 1)
+        assert set(loop) == {c for c, d in want.items() if d == K_BIG} and len(loop) == 5 * K_BIG
+
+
 def test_pentagon_cell_itself(host_kring):
     # a pentagon's ring: 5 neighbours (H3's fallback table of 7 slots, 6 filled)
     for bc in PENTAGON_BASE_CELLS:
@@ -162,6 +179,35 @@ def test_invalid_cells(host_kring):
     assert host_kring(0, 1, 0) is None
     bad_pent = pentagon_cell(4, 2) & ~(7 << (3 * 14)) | (1 << (3 * 14))  # leading k digit
     assert host_kring(bad_pent, 1, 0) is None
+
+
+@pytest.mark.gpu
+def test_gpu_kring_pentagons_large_k(host_kring):
+    """k = 100 around all 12 pentagons on the GPU (k_h3_kring_slow, one row per wave, stack in
+    scratch): element for element the host build, sets equal the oracle's; beyond k = 128 such a
+    row alone is marked unsupported (count -4) and the rest of the batch is answered."""
+    import ctypes
+
+    from mosaic_amd import MosaicContext, MosaicError
+    from mosaic_amd import _native as N
+
+    h3 = MosaicContext.build("H3", "JTS")
+    pents = [pentagon_cell(bc, 7 + i % 4) for i, bc in enumerate(PENTAGON_BASE_CELLS)]
+    for loop in (0, 1):
+        got = (h3.grid_cellkloop if loop else h3.grid_cellkring)(pents, K_BIG)
+        for p, g in zip(pents, got):
+            assert g.tolist() == host_kring(p, K_BIG, loop), (p, loop)
+    for p, g in zip(pents[:3], h3.grid_cellkring(pents[:3], K_BIG)):
+        assert set(g.tolist()) == set(oracle.h3_kring_set(p, K_BIG))
+    k = 129
+    cells = np.array([DOC_CELL, pents[0]], np.int64)
+    out = np.zeros(2 * (1 + 3 * k * (k + 1)), np.int64)
+    cnt = np.zeros(2, np.int32)
+    N.check(N.lib().mosaic_cell_kring(h3.handle, N.GRID_H3, N.ptr(cells), None, 2, k, 0, N.ptr(out), N.ptr(cnt)))
+    assert cnt.tolist() == [1 + 3 * k * (k + 1), -4]
+    with pytest.raises(MosaicError, match="row path"):
+        h3.grid_cellkring(cells.tolist(), k)
+    h3.close()
 
 
 @pytest.mark.gpu
