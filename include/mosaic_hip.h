@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-/* 2: mosaic_chip_table_raster writes 8 values (was 5); option "exact_cap". */
+/* 2: mosaic_chip_table_raster writes 8 values (was 5); option "exact_cap"; the aggregate geometry. */
 #define MOSAIC_ABI_VERSION 2
 
 typedef enum {
@@ -363,20 +363,39 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
                                 int32_t* out_left_key, int32_t* out_right_key, uint8_t* out_flag, int64_t cap,
                                 int64_t* n_out);
 
-/* ---- st_intersection_aggregate over the chip join of two chip tables (area) ---- */
-/* For every (left polygon_key, right polygon_key) pair whose chip sets share a cell id: the area of
- * the geometry ST_IntersectionAggregate.update / merge (expressions/geometry/
- * ST_IntersectionAggregate.scala) builds as the union of, per joined chip pair, the cell (both core),
- * the other chip (one core) or the two chips' intersection -- st_area(st_intersection_aggregate(..)),
- * the quantity the reference's tests check (ST_IntersectionBehaviors.scala:22-135, 1e-8).  out_status
- * 1 marks groups the engine does not answer (a cell holding several chip pairs of the group without a
- * (core, core) pair, a core chip without geometry): evaluate those on the row path.  Sorted by key
- * pair; MOSAIC_E_CAPACITY with *n_out set when more than cap groups exist.  Each (group, cell) piece
- * is written as one record and a group's area is summed on the host in cell-slot order, so repeated
- * calls return the same bits; the set of groups and their status are deterministic too. */
+/* ---- st_intersection_aggregate over the chip join of two chip tables ---- */
+/* For every (left polygon_key, right polygon_key) pair whose chip sets share a cell id: the union
+ * ST_IntersectionAggregate.update / merge (expressions/geometry/ST_IntersectionAggregate.scala:40-72)
+ * builds from, per joined chip pair, the cell (both core: indexToGeometry), the other chip (one core)
+ * or the two chips' intersection.  Per cell that union is (the group's left chips there, or the
+ * cell when one is core) n (its right chips, likewise); a cell with one pair is the pair's piece.
+ * mosaic_intersection_aggregate returns its area per group -- st_area(st_intersection_aggregate(..)),
+ * the quantity the reference's tests check (ST_IntersectionBehaviors.scala:22-135, 1e-8): per cell the
+ * area of that piece from the cell overlay (overlay.h, one GPU lane per (group, cell)).  out_status 1
+ * marks groups the engine does not answer (an overlay capacity exceeded, a cell without geometry):
+ * evaluate those on the row path.  Sorted by key pair;
+ * MOSAIC_E_CAPACITY with *n_out set when more than cap groups exist.  Each (group, cell) piece is one
+ * record and a group's area is summed on the host in cell-slot order, so repeated calls return the
+ * same bits. */
 int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
                                   int32_t* out_left_key, int32_t* out_right_key, double* out_area, uint8_t* out_status,
                                   int64_t cap, int64_t* n_out);
+/* The aggregate's geometry: per group the union as the WKB JTS writes (big-endian 2D Polygon, or
+ * MultiPolygon for several polygons; POLYGON EMPTY when the pieces have no area), dissolved across
+ * cells (pieces of adjacent cells form one polygon; shells clockwise, holes counter-clockwise).  The
+ * per-cell boundaries come from the GPU (overlay.h, one lane per (group, cell)); the host joins them
+ * (isect_geom.cpp).  Lower-dimensional parts of the reference's result (chips that only touch, whose
+ * JTS intersection is a line or a point) are not emitted: the polygonal part is.  Vertex order and
+ * ring starts are not JTS's (the reference's own depend on Spark's aggregation order).  area = the
+ * sum of the cells' piece areas (cell-slot order); status 1 = not answered (area NaN, no WKB). */
+typedef struct mosaic_isect_geoms mosaic_isect_geoms;
+int mosaic_intersection_aggregate_geometry(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
+                                           mosaic_isect_geoms** out);
+int mosaic_isect_geoms_info(const mosaic_isect_geoms* g, int64_t* n_groups, int64_t* wkb_bytes);
+/* left_key[n], right_key[n], area[n], status[n], wkb_offsets[n + 1], wkb[wkb_bytes] (any may be null) */
+int mosaic_isect_geoms_export(const mosaic_isect_geoms* g, int32_t* left_key, int32_t* right_key, double* area,
+                              uint8_t* status, int64_t* wkb_offsets, uint8_t* wkb);
+int mosaic_isect_geoms_destroy(mosaic_isect_geoms* g);
 
 /* ---- grid_cellkring / grid_cellkloop over a cell column (BNG, H3) ---- */
 /* loop = 0: kRing(cell, k); loop = 1: kLoop(cell, k).  Row i's cells go to out[i * stride ..] and

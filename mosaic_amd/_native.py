@@ -42,6 +42,8 @@ EXPORTS = [
     "mosaic_polyfill", "mosaic_cell_lists_info", "mosaic_cell_lists_export", "mosaic_cell_lists_destroy",
     "mosaic_polyfill_last_ms", "mosaic_ctx_exec", "mosaic_buffer_radius", "mosaic_chip_table_create_arrays",
     "mosaic_intersection_aggregate", "mosaic_thread_release", "mosaic_thread_count", "mosaic_stream_wait_event",
+    "mosaic_intersection_aggregate_geometry", "mosaic_isect_geoms_info", "mosaic_isect_geoms_export",
+    "mosaic_isect_geoms_destroy",
 ]
 
 GEOM_WKB = 0
@@ -149,6 +151,10 @@ def lib():
         "mosaic_buffer_radius": ([vp, i32, i32, i64, vp, vp, vp, vp, vp], i32),
         "mosaic_chip_table_create_arrays": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, ctypes.POINTER(vp)], i32),
         "mosaic_intersection_aggregate": ([vp, vp, vp, vp, vp, vp, vp, i64, ctypes.POINTER(i64)], i32),
+        "mosaic_intersection_aggregate_geometry": ([vp, vp, vp, ctypes.POINTER(vp)], i32),
+        "mosaic_isect_geoms_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "mosaic_isect_geoms_export": ([vp, vp, vp, vp, vp, vp, vp], i32),
+        "mosaic_isect_geoms_destroy": ([vp], i32),
         "mosaic_thread_release": ([vp], i32),
         "mosaic_thread_count": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
         "mosaic_ctx_exec": ([vp, ctypes.POINTER(i32), ctypes.POINTER(vp), ctypes.POINTER(i32), ctypes.POINTER(i32)],

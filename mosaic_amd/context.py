@@ -844,13 +844,38 @@ class MosaicContext:
             k = int(n_out.value)
             return lk[:k], rk[:k], fl[:k].astype(bool)
 
+    def st_intersection_aggregate(self, left, right):
+        """st_intersection_aggregate(left_index, right_index) grouped by (left_key, right_key) over the
+        chip join (MosaicContext st_intersection_aggregate -> ST_IntersectionAggregate.scala:40-72):
+        (left_key int32, right_key int32, area float64, status uint8, wkb list of bytes) sorted by key
+        pair.  The WKB is the union's polygonal part as JTS writes it (big-endian; POLYGON EMPTY when
+        the pieces have no area); status 1 = not answered (wkb None, area NaN): the row path."""
+        h = ctypes.c_void_p()
+        N.check(N.lib().mosaic_intersection_aggregate_geometry(self.handle, left.handle, right.handle, ctypes.byref(h)))
+        try:
+            n, nb = ctypes.c_int64(0), ctypes.c_int64(0)
+            N.check(N.lib().mosaic_isect_geoms_info(h, ctypes.byref(n), ctypes.byref(nb)))
+            k = int(n.value)
+            lk = np.empty(k, np.int32)
+            rk = np.empty(k, np.int32)
+            ar = np.empty(k, np.float64)
+            st = np.empty(k, np.uint8)
+            off = np.empty(k + 1, np.int64)
+            data = np.empty(max(int(nb.value), 1), np.uint8)
+            N.check(N.lib().mosaic_isect_geoms_export(h, N.ptr(lk), N.ptr(rk), N.ptr(ar), N.ptr(st), N.ptr(off),
+                                                      N.ptr(data)))
+        finally:
+            N.lib().mosaic_isect_geoms_destroy(h)
+        wkb = [None if st[i] else bytes(data[off[i]:off[i + 1]]) for i in range(k)]
+        return lk, rk, ar, st, wkb
+
     def st_intersection_aggregate_area(self, left, right):
         """st_area(st_intersection_aggregate(left_index, right_index)) per (left_key, right_key) group of
         the chip join (ST_IntersectionAggregate.scala; the quantity ST_IntersectionBehaviors.scala:22-135
         checks): arrays (left_key, right_key, area float64, status uint8) sorted by key pair; status 1
-        marks groups the engine does not answer (several chip pairs of the group in one cell without a
-        (core, core) pair, or a core chip without geometry)."""
-        cap = 1024
+        marks groups the engine does not answer (a core chip without geometry, an overlay capacity
+        exceeded)."""
+        cap = 1 << 16  # (a call that finds more groups reports the count and is repeated once)
         while True:
             lk = np.empty(cap, np.int32)
             rk = np.empty(cap, np.int32)

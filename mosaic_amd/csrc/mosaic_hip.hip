@@ -36,7 +36,8 @@
 #include "h3_geom.h"
 #include "h3_grid.h"
 #include "h3_neighbors.h"
-#include "isect_area.h"
+#include "isect_geom.h"
+#include "overlay.h"
 #include "join_binned.h"
 #include "join_common.h"
 #include "pip_coop.h"
@@ -837,107 +838,32 @@ __global__ void __launch_bounds__(256) k_isect_agg(IsectArgs a) {
 }
 
 
-// ---- st_intersection_aggregate's area over the chip join of two chip tables (isect_area.h) ----
-// Per (left key, right key) group: the area of the union of the chip-pair pieces the reference's
-// ST_IntersectionAggregate.update folds (expressions/geometry/ST_IntersectionAggregate.scala).  One
-// wave per cell of the left table, as k_isect_agg; pieces of different cells meet in zero area, so
-// a group's area is the sum over its cells.  Within a cell: a (core, core) pair makes the piece the
-// whole cell (every other piece lies inside it); otherwise the cell must hold one pair of the group
-// (the usual case: one chip per polygon and cell), whose piece is the other chip (one core side) or
-// the intersection of the two chips (wave-parallel sum of triangle overlaps, isect_area.h).  A cell
-// with several pairs and no (core, core) pair sets the group's status bit (the caller evaluates such
-// groups on the row path); a (core, core) pair's cell is the cell polygon (indexToGeometry, as the
-// reference's getCellGeom): H3 h3ToGeoBoundary in degrees, BNG the cell square.
-// Each (group, cell) piece is written as one record (group slot << 32 | left cell slot, area); the
-// host sums a group's records in (group, cell) order, so the area is the same bits on every run
-// (an atomic float add would sum in the order the waves finish).
-struct IsectAreaArgs {
-    IsectArgs base;
-    unsigned long long* rkey;
-    double* rarea;
-    unsigned long long* rcount;
-    unsigned long long rcap;
-    int grid, jdk;
+// ---- st_intersection_aggregate's union by cell (overlay.h): units = (group, left cell slot) ----
+// A unit holds the group's chip pairs of one cell.  Its piece of the union the reference folds is
+// the cell for a (core, core) pair, else (the group's left chips in the cell, or the whole cell when
+// one of them is core) n (its right chips, likewise).  k_isect_units lists the units (one wave per
+// left cell slot, as k_isect_agg; lane 0 writes) with their edge counts, which size each unit's
+// scratch; k_isect_overlay runs overlay::unit_boundary one lane per unit.
+struct IsectUnit {
+    uint32_t gs, slot, fb, eb;
+    uint32_t flags;    // bit 0: a (core, core) pair; bit 1: a left core chip; bit 2: a right core chip
+    uint32_t n_edges;  // edges of the chips the overlay reads (0 for a (core, core) unit)
+    uint32_t n_parts, pad;
 };
 
-// indexToGeometry(cell).getArea (the reference's getCellGeom for a (core, core) pair): H3 the
-// h3ToGeoBoundary ring in degrees (h3-java's Math.toDegrees), BNG the cell square
-__device__ double cell_area(int grid, int64_t id, int jdk) {
-    if (grid == MOSAIC_GRID_BNG) {
-        int r;
-        int32_t e, x, y;
-        if (!bng::cell_origin(id, &r, &e, &x, &y)) return NAN;
-        return (double)e * (double)e;
-    }
-    double v[20];
-    const int n = h3geom::h3_to_geo_boundary((uint64_t)id, v);
-    if (n <= 0) return NAN;
-    const double ox = h3geom::to_degrees(v[1], jdk), oy = h3geom::to_degrees(v[0], jdk);
-    double a = 0, px = 0, py = 0;
-    for (int k = 1; k <= n; k++) {
-        const double x = k == n ? 0.0 : h3geom::to_degrees(v[2 * k + 1], jdk) - ox;
-        const double y = k == n ? 0.0 : h3geom::to_degrees(v[2 * k], jdk) - oy;
-        a += px * y - x * py;
-        px = x;
-        py = y;
-    }
-    return 0.5 * fabs(a);
+__device__ uint32_t chip_edges(const pip::GeomStore& s, uint32_t g, uint32_t* parts) {
+    uint32_t n = 0;
+    for (uint32_t p = s.geom_part[g]; p < s.geom_part[g + 1]; p++) n += (uint32_t)overlay::part_edges(s, p);
+    *parts += s.geom_part[g + 1] - s.geom_part[g];
+    return n;
 }
 
-__device__ inline double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// Area of geometry g (shells counter-clockwise positive, holes negative): JTS getArea
-__device__ double wave_geom_area(const pip::GeomStore& s, uint32_t g, int lane) {
-    const uint32_t ne = isect::edge_count(s, g);
-    if (ne == 0) return 0.0;
-    const pip::Vec2 o = s.verts[s.ring_start[s.part_ring[s.geom_part[g]]]];
-    double sum = 0;
-    for (uint32_t e = (uint32_t)lane; e < ne; e += 64) {
-        uint32_t r, v;
-        bool shell;
-        isect::edge_at(s, g, e, &r, &v, &shell);
-        const double sg = isect::ring_sign(s, r, shell);
-        const pip::Vec2 a = s.verts[v], b = s.verts[v + 1];
-        sum += sg * ((a.x - o.x) * (b.y - o.y) - (b.x - o.x) * (a.y - o.y));
-    }
-    return 0.5 * wave_sum(sum);
-}
-
-// area(A n B): lanes over A's edges, each against every edge of B (isect_area.h)
-__device__ double wave_isect_area(const pip::GeomStore& sa, uint32_t a, const pip::GeomStore& sb, uint32_t b, int lane) {
-    if (sa.geom_part[a + 1] <= sa.geom_part[a] || sb.geom_part[b + 1] <= sb.geom_part[b]) return 0.0;
-    if (!pip::boxes_meet(sa.geom_bbox[a], sb.geom_bbox[b])) return 0.0;
-    const uint32_t na = isect::edge_count(sa, a);
-    if (na == 0) return 0.0;
-    const pip::Vec2 o{fmin(sa.geom_bbox[a].minx, sb.geom_bbox[b].minx), fmin(sa.geom_bbox[a].miny, sb.geom_bbox[b].miny)};
-    double sum = 0;
-    for (uint32_t e = (uint32_t)lane; e < na; e += 64) {
-        uint32_t r, v;
-        bool shell;
-        isect::edge_at(sa, a, e, &r, &v, &shell);
-        const double sga = isect::ring_sign(sa, r, shell);
-        const double p0x = sa.verts[v].x - o.x, p0y = sa.verts[v].y - o.y;
-        const double p1x = sa.verts[v + 1].x - o.x, p1y = sa.verts[v + 1].y - o.y;
-        for (uint32_t p = sb.geom_part[b]; p < sb.geom_part[b + 1]; p++)
-            for (uint32_t rb = sb.part_ring[p]; rb < sb.part_ring[p + 1]; rb++) {
-                const double sgb = isect::ring_sign(sb, rb, rb == sb.part_ring[p]);
-                for (uint32_t i = sb.ring_start[rb]; i + 1 < sb.ring_start[rb + 1]; i++)
-                    sum += isect::pair_term(p0x, p0y, p1x, p1y, sga, sb.verts[i].x - o.x, sb.verts[i].y - o.y,
-                                            sb.verts[i + 1].x - o.x, sb.verts[i + 1].y - o.y, sgb);
-            }
-    }
-    return wave_sum(sum);
-}
-
-__global__ void __launch_bounds__(256) k_isect_area(IsectAreaArgs x) {
-    const IsectArgs& a = x.base;
+__global__ void __launch_bounds__(256) k_isect_units(IsectArgs a, IsectUnit* units, unsigned long long* n_units,
+                                                     unsigned long long cap) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t slot = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; slot < a.capa; slot += nw) {
+        if (lane != 0) continue;
         const HashEntry e = a.ta[slot];
         if (e.key == kEmptyKey) continue;
         uint32_t fb = 0, eb = 0;
@@ -952,52 +878,140 @@ __global__ void __launch_bounds__(256) k_isect_area(IsectAreaArgs x) {
         }
         for (uint32_t ca = e.first; ca < e.first + e.count; ca++)
             for (uint32_t cb = fb; cb < eb; cb++) {
-                const uint32_t ma = a.meta_a[ca], mb = a.meta_b[cb];
-                const unsigned long long key = ((unsigned long long)(ma >> 1) << 32) | (unsigned long long)(mb >> 1);
-                // the group's pairs in this cell: is this the first, how many, a (core, core) one
+                const uint32_t L = a.meta_a[ca] >> 1, R = a.meta_b[cb] >> 1;
+                // first pair of its group in this cell?
                 bool first = true;
-                uint32_t n = 0, cc = ~0u;
-                for (uint32_t ca2 = e.first; ca2 < e.first + e.count; ca2++)
+                for (uint32_t ca2 = e.first; ca2 <= ca && first; ca2++)
                     for (uint32_t cb2 = fb; cb2 < eb; cb2++) {
-                        const uint32_t ma2 = a.meta_a[ca2], mb2 = a.meta_b[cb2];
-                        if (((unsigned long long)(ma2 >> 1) << 32 | (unsigned long long)(mb2 >> 1)) != key) continue;
-                        n++;
-                        if ((ma2 & mb2 & 1u) && cc == ~0u) cc = ca2;
-                        if (ca2 < ca || (ca2 == ca && cb2 < cb)) first = false;
-                    }
-                if (!first) continue;
-                uint64_t gs = 0;
-                if (lane == 0) gs = group_slot(a, key);
-                gs = __shfl(gs, 0, 64);
-                if (gs == ~0ULL) continue;
-                double area = 0;
-                uint32_t flag = 0;
-                if (cc != ~0u) {
-                    area = cell_area(x.grid, e.key, x.jdk);
-                } else if (n > 1) {
-                    flag = 1;
-                } else if (ma & 1u) {
-                    area = wave_geom_area(a.sb, cb, lane);
-                } else if (mb & 1u) {
-                    area = wave_geom_area(a.sa, ca, lane);
-                } else {
-                    area = wave_isect_area(a.sa, ca, a.sb, cb, lane);
-                }
-                if (area != area) flag = 1;
-                if (lane == 0) {
-                    if (flag) {
-                        atomicOr(&a.gflag[gs], flag);
-                    } else {
-                        const unsigned long long r = atomicAdd(x.rcount, 1ULL);
-                        if (r < x.rcap) {
-                            x.rkey[r] = (gs << 32) | slot;
-                            x.rarea[r] = area;
-                        } else {
-                            atomicOr(a.overflow, 1);
+                        if (ca2 == ca && cb2 >= cb) break;
+                        if ((a.meta_a[ca2] >> 1) == L && (a.meta_b[cb2] >> 1) == R) {
+                            first = false;
+                            break;
                         }
                     }
+                if (!first) continue;
+                uint32_t acore = 0, bcore = 0;
+                for (uint32_t c = e.first; c < e.first + e.count; c++)
+                    if ((a.meta_a[c] >> 1) == L) acore |= a.meta_a[c] & 1u;
+                for (uint32_t c = fb; c < eb; c++)
+                    if ((a.meta_b[c] >> 1) == R) bcore |= a.meta_b[c] & 1u;
+                const bool cc = acore && bcore;
+                uint32_t ne = 0, np = 0;
+                if (!cc) {
+                    if (!acore)
+                        for (uint32_t c = e.first; c < e.first + e.count; c++)
+                            if ((a.meta_a[c] >> 1) == L) ne += chip_edges(a.sa, c, &np);
+                    if (!bcore)
+                        for (uint32_t c = fb; c < eb; c++)
+                            if ((a.meta_b[c] >> 1) == R) ne += chip_edges(a.sb, c, &np);
+                }
+                const uint64_t gs = group_slot(a, ((unsigned long long)L << 32) | R);
+                if (gs == ~0ULL) continue;
+                const unsigned long long u = atomicAdd(n_units, 1ULL);
+                if (u < cap) {
+                    IsectUnit x;
+                    x.gs = (uint32_t)gs;
+                    x.slot = (uint32_t)slot;
+                    x.fb = fb;
+                    x.eb = eb;
+                    x.flags = (cc ? 1u : 0u) | (acore ? 2u : 0u) | (bcore ? 4u : 0u);
+                    x.n_edges = ne;
+                    x.n_parts = np;
+                    x.pad = 0;
+                    units[u] = x;
                 }
             }
+    }
+}
+
+struct OverlayArgs {
+    IsectArgs base;
+    const IsectUnit* units;
+    const uint32_t* order;  // processing order: largest units first
+    uint64_t n_units;
+    const int64_t* scratch_off;  // bytes into scratch, per unit
+    char* scratch;
+    const int64_t* out_off;  // edges into out, per unit
+    double* out;             // 4 doubles per edge
+    int32_t* out_count;      // edges, -1: a capacity exceeded
+    double* out_area;
+    int grid, jdk;
+};
+
+__device__ int cell_ring(int grid, int64_t id, int jdk, double* xy) {  // indexToGeometry's ring, open, ccw
+    int n = 0;
+    if (grid == MOSAIC_GRID_BNG) {
+        int r;
+        int32_t e, x, y;
+        if (!bng::cell_origin(id, &r, &e, &x, &y)) return 0;
+        const double X = x, Y = y, E = e;
+        const double v[8] = {X, Y, X + E, Y, X + E, Y + E, X, Y + E};
+        for (int i = 0; i < 8; i++) xy[i] = v[i];
+        return 4;
+    }
+    double v[20];
+    n = h3geom::h3_to_geo_boundary((uint64_t)id, v);
+    if (n <= 0) return 0;
+    for (int k = 0; k < n; k++) xy[2 * k] = h3geom::to_degrees(v[2 * k + 1], jdk), xy[2 * k + 1] = h3geom::to_degrees(v[2 * k], jdk);
+    double s = 0;
+    for (int k = 0; k < n; k++) {
+        const int j = k + 1 == n ? 0 : k + 1;
+        s += (xy[2 * k] - xy[0]) * (xy[2 * j + 1] - xy[1]) - (xy[2 * j] - xy[0]) * (xy[2 * k + 1] - xy[1]);
+    }
+    if (s < 0)
+        for (int k = 0; k < n / 2; k++) {
+            const double tx = xy[2 * k], ty = xy[2 * k + 1];
+            xy[2 * k] = xy[2 * (n - 1 - k)], xy[2 * k + 1] = xy[2 * (n - 1 - k) + 1];
+            xy[2 * (n - 1 - k)] = tx, xy[2 * (n - 1 - k) + 1] = ty;
+        }
+    return n;
+}
+
+// one unit per wave (lane 0): a unit's overlay is sequential, data-dependent work, so units that
+// shared a wave would serialise behind its largest; largest units first, for the tail
+__global__ void __launch_bounds__(64) k_isect_overlay(OverlayArgs x) {
+    const IsectArgs& a = x.base;
+    if ((threadIdx.x & 63) != 0) return;
+    const uint64_t step = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < x.n_units; i += step) {
+        const uint64_t u = x.order[i];
+        const IsectUnit un = x.units[u];
+        double* out = x.out + 4 * x.out_off[u];
+        const int out_cap = (int)(x.out_off[u + 1] - x.out_off[u]);
+        const HashEntry e = a.ta[un.slot];
+        if (un.flags & 1u) {
+            double xy[20];
+            const int n = cell_ring(x.grid, e.key, x.jdk, xy);
+            double acc = 0;
+            for (int k = 0; k < n && k < out_cap; k++) {
+                const int j = k + 1 == n ? 0 : k + 1;
+                out[4 * k] = xy[2 * k], out[4 * k + 1] = xy[2 * k + 1], out[4 * k + 2] = xy[2 * j], out[4 * k + 3] = xy[2 * j + 1];
+                acc += (xy[2 * k] - xy[0]) * (xy[2 * j + 1] - xy[1]) - (xy[2 * j] - xy[0]) * (xy[2 * k + 1] - xy[1]);
+            }
+            x.out_count[u] = n > 0 && n <= out_cap ? n : -1;
+            x.out_area[u] = 0.5 * acc;
+            continue;
+        }
+        const unsigned long long key = a.gkey[un.gs];
+        const uint32_t L = (uint32_t)(key >> 32), R = (uint32_t)key;
+        char* base = x.scratch + x.scratch_off[u];
+        overlay::PartRef* parts = (overlay::PartRef*)base;
+        int np = 0;
+        if (!(un.flags & 2u))
+            for (uint32_t c = e.first; c < e.first + e.count; c++)
+                if ((a.meta_a[c] >> 1) == L)
+                    for (uint32_t p = a.sa.geom_part[c]; p < a.sa.geom_part[c + 1]; p++) parts[np++] = overlay::PartRef{p, 0, 0, 0};
+        if (!(un.flags & 4u))
+            for (uint32_t c = un.fb; c < un.eb; c++)
+                if ((a.meta_b[c] >> 1) == R)
+                    for (uint32_t p = a.sb.geom_part[c]; p < a.sb.geom_part[c + 1]; p++) parts[np++] = overlay::PartRef{p, 1, 0, 0};
+        overlay::Scratch sc = overlay::make_scratch(base + (((int64_t)un.n_parts * sizeof(overlay::PartRef) + 63) & ~(int64_t)63),
+                                                    un.n_edges);
+        const pip::GeomStore st[2] = {a.sa, a.sb};
+        const int need = ((un.flags & 2u) ? 0 : overlay::kNeedA) | ((un.flags & 4u) ? 0 : overlay::kNeedB);
+        double area = 0;
+        x.out_count[u] = overlay::unit_boundary(st, parts, np, need, sc, out, out_cap, &area);
+        x.out_area[u] = area;
     }
 }
 
@@ -1697,6 +1711,7 @@ struct ThreadCtx : Options {
                                        // last mosaic_tessellate_gpu; 0 when it had no candidates
     DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
+    DevBuf ov[8];  // st_intersection_aggregate's cell overlay (run_unit_overlay)
     hipStream_t copy_stream = nullptr;
     DevBuf hx[2], hy[2], hcounts;
     binned::Scratch bins;  // the binned join's keys, sorted points and sort temp
@@ -1709,7 +1724,8 @@ struct ThreadCtx : Options {
     // the scratch buffers sized by the calls (not `scalars`, which every call needs)
     std::vector<DevBuf*> scratch() {
         return {&amb_queue, &mix_queue, &stage_x, &stage_y, &stage_v, &stage_out, &stage_out2, &stage_idx, &geo_off,
-                &geo_data, &dec_x, &dec_y, &dec_status, &hx[0], &hx[1], &hy[0], &hy[1], &hcounts};
+                &geo_data, &dec_x, &dec_y, &dec_status, &hx[0], &hx[1], &hy[0], &hy[1], &hcounts,
+                &ov[0], &ov[1], &ov[2], &ov[3], &ov[4], &ov[5], &ov[6], &ov[7]};
     }
     size_t held() {
         size_t n = 0;
@@ -4285,17 +4301,134 @@ int mosaic_intersects_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const
     return done(MOSAIC_OK);
 }
 
-int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
-                                  int32_t* out_left_key, int32_t* out_right_key, double* out_area, uint8_t* out_status,
-                                  int64_t cap, int64_t* n_out) {
-    ENTER(ctx);
-    if (!c || !left || !right || !n_out || cap < 0 ||
-        (cap > 0 && (!out_left_key || !out_right_key || !out_area || !out_status)))
-        return fail(MOSAIC_E_ARG, "invalid argument");
-    if (left->grid != right->grid || left->res != right->res)
-        return fail(MOSAIC_E_ARG, "st_intersection_aggregate: both chip tables must use the same grid and resolution");
-    *n_out = 0;
-    HIP_TRY(hipSetDevice(c->device));
+// The units of a chip join (k_isect_units over a's group table) run through
+// k_isect_overlay in batches of <= 2 GB of scratch.  Per unit (sorted by group slot, then left cell
+// slot): its record, edge count (-1: a capacity was exceeded), area, and edges (4 doubles each) at
+// edge_off[u] .. edge_off[u] + count.
+struct OverlayResult {
+    std::vector<IsectUnit> units;
+    std::vector<int32_t> count;
+    std::vector<double> area;
+    std::vector<int64_t> edge_off;
+    std::vector<double> edges;
+};
+
+static int run_unit_overlay(ThreadCtx* c, const IsectArgs& a, int grid_sys, uint64_t unit_cap, OverlayResult& r) {
+    DevBuf du, dn;
+    DevBufGuard guard{{&du, &dn}};
+    int rc;
+    if ((rc = du.reserve(std::max<uint64_t>(unit_cap, 1) * sizeof(IsectUnit))) || (rc = dn.reserve(8))) return rc;
+    HIP_TRY(hipMemsetAsync(dn.p, 0, 8, c->stream));
+    const int64_t waves = (int64_t)a.capa;
+    const int g = (int)std::max<int64_t>(1, std::min<int64_t>((waves * 64 + 255) / 256, (int64_t)c->n_cu * 16));
+    hipLaunchKernelGGL(k_isect_units, dim3(g), dim3(256), 0, c->stream, a, (IsectUnit*)du.p, (unsigned long long*)dn.p,
+                       (unsigned long long)unit_cap);
+    HIP_TRY(hipGetLastError());
+    unsigned long long nu = 0;
+    HIP_TRY(hipMemcpyAsync(&nu, dn.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (nu > unit_cap) return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: unit list overflow");
+    r.units.resize(nu);
+    if (nu) HIP_TRY(hipMemcpy(r.units.data(), du.p, nu * sizeof(IsectUnit), hipMemcpyDeviceToHost));
+    std::sort(r.units.begin(), r.units.end(), [](const IsectUnit& p, const IsectUnit& q) {
+        return p.gs < q.gs || (p.gs == q.gs && p.slot < q.slot);
+    });
+    r.count.assign(nu, 0);
+    r.area.assign(nu, 0.0);
+    r.edge_off.assign(nu + 1, 0);
+    std::vector<int64_t> sbytes(nu);
+    for (size_t u = 0; u < nu; u++) {
+        const IsectUnit& x = r.units[u];
+        const bool cc = x.flags & 1u;
+        r.edge_off[u + 1] = r.edge_off[u] + (cc ? 16 : 5 * (int64_t)x.n_edges + 64);
+        sbytes[u] = cc ? 0 : ((((int64_t)x.n_parts * (int64_t)sizeof(overlay::PartRef) + 63) & ~(int64_t)63) +
+                              ((overlay::scratch_bytes(x.n_edges) + 63) & ~(int64_t)63));
+    }
+    r.edges.assign((size_t)r.edge_off[nu] * 4, 0.0);
+    const int64_t kBatch = (int64_t)2 << 30;
+    // (the calling thread's scratch, kept between calls: fresh multi-GB allocations cost more than
+    // the overlay itself)
+    DevBuf &bu = c->ov[0], &bso = c->ov[1], &bsc = c->ov[2], &boo = c->ov[3], &bout = c->ov[4], &bcnt = c->ov[5],
+           &bar = c->ov[6], &bord = c->ov[7];
+    for (size_t u0 = 0; u0 < nu;) {
+        size_t u1 = u0;
+        int64_t sb = 0;
+        while (u1 < nu && (u1 == u0 || sb + sbytes[u1] <= kBatch) && u1 - u0 < ((size_t)1 << 20)) sb += sbytes[u1++];
+        const size_t m = u1 - u0;
+        std::vector<int64_t> so(m), oo(m + 1);
+        int64_t acc = 0;
+        for (size_t i = 0; i < m; i++) so[i] = acc, acc += sbytes[u0 + i];
+        for (size_t i = 0; i <= m; i++) oo[i] = r.edge_off[u0 + i] - r.edge_off[u0];
+        std::vector<uint32_t> ord(m);
+        for (size_t i = 0; i < m; i++) ord[i] = (uint32_t)i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t p, uint32_t q) {
+            return r.units[u0 + p].n_edges > r.units[u0 + q].n_edges;
+        });
+        if ((rc = bu.reserve(m * sizeof(IsectUnit))) || (rc = bso.reserve(m * 8)) || (rc = bsc.reserve((size_t)std::max<int64_t>(acc, 64))) ||
+            (rc = boo.reserve((m + 1) * 8)) || (rc = bout.reserve((size_t)std::max<int64_t>(oo[m], 1) * 32)) ||
+            (rc = bcnt.reserve(m * 4)) || (rc = bar.reserve(m * 8)) || (rc = bord.reserve(m * 4)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(bord.p, ord.data(), m * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(bu.p, r.units.data() + u0, m * sizeof(IsectUnit), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(bso.p, so.data(), m * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(boo.p, oo.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        OverlayArgs x;
+        x.base = a;
+        x.units = (const IsectUnit*)bu.p;
+        x.order = (const uint32_t*)bord.p;
+        x.n_units = m;
+        x.scratch_off = (const int64_t*)bso.p;
+        x.scratch = (char*)bsc.p;
+        x.out_off = (const int64_t*)boo.p;
+        x.out = (double*)bout.p;
+        x.out_count = (int32_t*)bcnt.p;
+        x.out_area = (double*)bar.p;
+        x.grid = grid_sys;
+        x.jdk = c->jdk;
+        const int go = (int)std::max<size_t>(1, std::min<size_t>(m, (size_t)c->n_cu * 32));
+        hipLaunchKernelGGL(k_isect_overlay, dim3(go), dim3(64), 0, c->stream, x);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(r.count.data() + u0, bcnt.p, m * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(r.area.data() + u0, bar.p, m * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(r.edges.data() + 4 * r.edge_off[u0], bout.p, (size_t)oo[m] * 32, hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        u0 = u1;
+    }
+    return MOSAIC_OK;
+}
+
+// the node tolerance of the host stitching: pieces of adjacent cells meet within it.  H3 chips
+// follow the cells' gnomonic sides, so the same side crossing computed in two cells differs by up to
+// ~5e-3 e^2 degrees (e the cell edge in degrees; measured 1.1e-7 at res 8, 1e-8 at res 9:
+// tools/probes/isect_snap.py); the tolerance is 10x that, and at least 2^-40 of the coordinates.
+static double stitch_snap(int grid, int res) {
+    if (grid == MOSAIC_GRID_BNG) return 1e6 * 9.094947017729282e-13;
+    static const double kEdgeKm[16] = {1107.712591, 418.6760055, 158.2446558, 59.81085794, 22.6063794, 8.544408276,
+                                       3.229482772, 1.220629759, 0.461354684, 0.174375668, 0.065907807, 0.024910561,
+                                       0.009415526, 0.003559893, 0.001348575, 0.000509713};
+    const double e = kEdgeKm[res < 0 ? 0 : (res > 15 ? 15 : res)] / 111.32;
+    return std::max(0.05 * e * e, 180.0 * 9.094947017729282e-13);
+}
+
+struct mosaic_isect_geoms {
+    std::vector<int32_t> lk, rk;
+    std::vector<double> area;
+    std::vector<uint8_t> status;
+    std::vector<int64_t> off;
+    std::vector<uint8_t> wkb;
+};
+
+// The units of the chip join of two tables through the cell overlay; groups are runs of units with
+// one group slot (gstart), keyed by gkey[slot] = left key << 32 | right key.
+struct AggUnits {
+    OverlayResult r;
+    std::vector<unsigned long long> gkey;
+    std::vector<size_t> gstart;  // group g = units [gstart[g], gstart[g + 1])
+};
+
+static int aggregate_units(ThreadCtx* c, const mosaic_chips* left, const mosaic_chips* right, AggUnits& out) {
+    out.gstart.assign(1, 0);
     if (left->n_chips == 0 || right->n_chips == 0) return MOSAIC_OK;
     IsectArgs a;
     a.ta = (const HashEntry*)left->table.p;
@@ -4306,8 +4439,8 @@ int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, con
     a.maskb = right->capacity - 1;
     a.meta_b = (const uint32_t*)right->meta.p;
     a.sb = right->store.view();
-    DevBuf cnt, gkey, gflag, rkey, rarea, ovf;
-    DevBufGuard guard{{&cnt, &gkey, &gflag, &rkey, &rarea, &ovf}};
+    DevBuf cnt, gkey, ovf;
+    DevBufGuard guard{{&cnt, &gkey, &ovf}};
     int rc;
     if ((rc = cnt.reserve(8)) || (rc = ovf.reserve(4))) return rc;
     HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
@@ -4328,62 +4461,154 @@ int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, con
     if (pairs == 0) return MOSAIC_OK;
     uint64_t gcap = 1024;
     while (gcap < 2 * pairs) gcap <<= 1;
-    if (gcap > ((uint64_t)1 << 32) || left->capacity > ((uint64_t)1 << 32))
-        return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: too many chip pairs");
-    if ((rc = gkey.reserve(gcap * 8)) || (rc = gflag.reserve(gcap * 4)) || (rc = rkey.reserve(pairs * 8)) ||
-        (rc = rarea.reserve(pairs * 8)))
-        return rc;
+    if (gcap > ((uint64_t)1 << 32)) return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: too many chip pairs");
+    if ((rc = gkey.reserve(gcap * 8))) return rc;
     HIP_TRY(hipMemsetAsync(gkey.p, 0xff, gcap * 8, c->stream));
-    HIP_TRY(hipMemsetAsync(gflag.p, 0, gcap * 4, c->stream));
-    HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
-    a.pass = 1;
     a.gkey = (unsigned long long*)gkey.p;
-    a.gflag = (uint32_t*)gflag.p;
     a.gmask = gcap - 1;
-    // (pieces <= chip pairs: the record buffer cannot overflow)
-    IsectAreaArgs x{a, (unsigned long long*)rkey.p, (double*)rarea.p, (unsigned long long*)cnt.p, pairs, left->grid, c->jdk};
-    hipLaunchKernelGGL(k_isect_area, dim3(grid), dim3(256), 0, c->stream, x);
-    HIP_TRY(hipGetLastError());
-    std::vector<unsigned long long> hk(gcap);
-    std::vector<uint32_t> hf(gcap);
+    if ((rc = run_unit_overlay(c, a, left->grid, pairs, out.r))) return rc;
     int hov = 0;
-    unsigned long long nrec = 0;
-    HIP_TRY(hipMemcpyAsync(hk.data(), gkey.p, gcap * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(hf.data(), gflag.p, gcap * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&nrec, cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&hov, ovf.p, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (hov || nrec > pairs) return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: group table overflow");
-    std::vector<std::pair<unsigned long long, double>> rec(nrec);
-    {
-        std::vector<unsigned long long> rk(nrec);
-        std::vector<double> ra(nrec);
-        HIP_TRY(hipMemcpyAsync(rk.data(), rkey.p, nrec * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(ra.data(), rarea.p, nrec * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        for (size_t i = 0; i < nrec; i++) rec[i] = {rk[i], ra[i]};
-    }
-    // per group, its pieces summed in cell-slot order: the same bits on every run
-    std::sort(rec.begin(), rec.end(), [](const std::pair<unsigned long long, double>& p,
-                                         const std::pair<unsigned long long, double>& q) { return p.first < q.first; });
-    std::vector<double> ha(gcap, 0.0);
-    for (const auto& r : rec) ha[r.first >> 32] += r.second;
-    std::vector<std::pair<unsigned long long, uint64_t>> groups;
-    for (uint64_t s = 0; s < gcap; s++)
-        if (hk[s] != kEmptyGroup) groups.push_back({hk[s], s});
-    std::sort(groups.begin(), groups.end());
-    *n_out = (int64_t)groups.size();
-    if ((int64_t)groups.size() > cap)
-        return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: " + std::to_string(groups.size()) + " groups");
-    for (size_t i = 0; i < groups.size(); i++) {
-        out_left_key[i] = (int32_t)(groups[i].first >> 32);
-        out_right_key[i] = (int32_t)(groups[i].first & 0xffffffffULL);
-        out_area[i] = ha[groups[i].second];
-        out_status[i] = (uint8_t)(hf[groups[i].second] ? 1 : 0);
-    }
+    out.gkey.resize(gcap);
+    HIP_TRY(hipMemcpy(&hov, ovf.p, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out.gkey.data(), gkey.p, gcap * 8, hipMemcpyDeviceToHost));
+    if (hov) return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: group table overflow");
+    out.gstart.clear();
+    for (size_t u = 0; u < out.r.units.size(); u++)
+        if (u == 0 || out.r.units[u].gs != out.r.units[u - 1].gs) out.gstart.push_back(u);
+    out.gstart.push_back(out.r.units.size());
     return MOSAIC_OK;
 }
 
+// per group: the area (its units' areas summed in cell-slot order: the same bits on every call) or
+// NaN when a unit exceeded a capacity / had no area; the order of groups by key pair
+static void aggregate_areas(const AggUnits& g, std::vector<double>& area, std::vector<size_t>& order) {
+    const size_t ng = g.gstart.size() - 1;
+    area.assign(ng, 0.0);
+    for (size_t k = 0; k < ng; k++)
+        for (size_t u = g.gstart[k]; u < g.gstart[k + 1]; u++)
+            area[k] = (g.r.count[u] < 0 || g.r.area[u] != g.r.area[u]) ? NAN : area[k] + g.r.area[u];
+    order.resize(ng);
+    for (size_t k = 0; k < ng; k++) order[k] = k;
+    std::sort(order.begin(), order.end(), [&](size_t p, size_t q) {
+        return g.gkey[g.r.units[g.gstart[p]].gs] < g.gkey[g.r.units[g.gstart[q]].gs];
+    });
+}
+
+int mosaic_intersection_aggregate_geometry(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
+                                           mosaic_isect_geoms** out) {
+    ENTER(ctx);
+    if (!c || !left || !right || !out) return fail(MOSAIC_E_ARG, "invalid argument");
+    if (left->grid != right->grid || left->res != right->res)
+        return fail(MOSAIC_E_ARG, "st_intersection_aggregate: both chip tables must use the same grid and resolution");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(c->device));
+    AggUnits g;
+    int rc;
+    if ((rc = aggregate_units(c, left, right, g))) return rc;
+    const OverlayResult& r = g.r;
+    const size_t ng = g.gstart.size() - 1;
+    std::vector<double> garea;
+    std::vector<size_t> ord;
+    aggregate_areas(g, garea, ord);
+    // each group's cell boundaries stitched into its polygons, on host threads
+    std::vector<std::vector<uint8_t>> wkbs(ng);
+    std::vector<uint8_t> gst(ng, 0);
+    const double snap = stitch_snap(left->grid, left->res);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        std::vector<double> e;
+        for (size_t k; (k = next.fetch_add(1)) < ng;) {
+            e.clear();
+            if (garea[k] != garea[k]) {
+                gst[k] = 1;
+                continue;
+            }
+            for (size_t u = g.gstart[k]; u < g.gstart[k + 1]; u++)
+                e.insert(e.end(), r.edges.begin() + 4 * r.edge_off[u], r.edges.begin() + 4 * (r.edge_off[u] + r.count[u]));
+            double stitched = 0;
+            if (!isect_geom::stitch_wkb(e.data(), e.size() / 4, snap, wkbs[k], &stitched)) {
+                gst[k] = 1;
+                wkbs[k].clear();
+            }
+        }
+    };
+    {
+        const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt && t < ng; t++) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+    }
+    auto* res = new mosaic_isect_geoms();
+    res->off.push_back(0);
+    for (size_t k : ord) {
+        const unsigned long long key = g.gkey[r.units[g.gstart[k]].gs];
+        res->lk.push_back((int32_t)(key >> 32));
+        res->rk.push_back((int32_t)(key & 0xffffffffULL));
+        res->area.push_back(gst[k] ? NAN : garea[k]);
+        res->status.push_back(gst[k]);
+        res->wkb.insert(res->wkb.end(), wkbs[k].begin(), wkbs[k].end());
+        res->off.push_back((int64_t)res->wkb.size());
+    }
+    *out = res;
+    return MOSAIC_OK;
+}
+
+int mosaic_isect_geoms_info(const mosaic_isect_geoms* g, int64_t* n_groups, int64_t* wkb_bytes) {
+    if (!g || !n_groups || !wkb_bytes) return fail(MOSAIC_E_ARG, "null argument");
+    *n_groups = (int64_t)g->lk.size();
+    *wkb_bytes = (int64_t)g->wkb.size();
+    return MOSAIC_OK;
+}
+
+int mosaic_isect_geoms_export(const mosaic_isect_geoms* g, int32_t* left_key, int32_t* right_key, double* area,
+                              uint8_t* status, int64_t* wkb_offsets, uint8_t* wkb) {
+    if (!g) return fail(MOSAIC_E_ARG, "null argument");
+    const size_t n = g->lk.size();
+    if (left_key) std::copy(g->lk.begin(), g->lk.end(), left_key);
+    if (right_key) std::copy(g->rk.begin(), g->rk.end(), right_key);
+    if (area) std::copy(g->area.begin(), g->area.end(), area);
+    if (status) std::copy(g->status.begin(), g->status.end(), status);
+    if (wkb_offsets) std::copy(g->off.begin(), g->off.begin() + (long)(n + 1), wkb_offsets);
+    if (wkb && !g->wkb.empty()) memcpy(wkb, g->wkb.data(), g->wkb.size());
+    return MOSAIC_OK;
+}
+
+int mosaic_isect_geoms_destroy(mosaic_isect_geoms* g) {
+    delete g;
+    return MOSAIC_OK;
+}
+
+int mosaic_intersection_aggregate(mosaic_ctx* ctx, const mosaic_chips* left, const mosaic_chips* right,
+                                  int32_t* out_left_key, int32_t* out_right_key, double* out_area, uint8_t* out_status,
+                                  int64_t cap, int64_t* n_out) {
+    ENTER(ctx);
+    if (!c || !left || !right || !n_out || cap < 0 ||
+        (cap > 0 && (!out_left_key || !out_right_key || !out_area || !out_status)))
+        return fail(MOSAIC_E_ARG, "invalid argument");
+    if (left->grid != right->grid || left->res != right->res)
+        return fail(MOSAIC_E_ARG, "st_intersection_aggregate: both chip tables must use the same grid and resolution");
+    *n_out = 0;
+    HIP_TRY(hipSetDevice(c->device));
+    AggUnits g;
+    int rc;
+    if ((rc = aggregate_units(c, left, right, g))) return rc;
+    std::vector<double> garea;
+    std::vector<size_t> ord;
+    aggregate_areas(g, garea, ord);
+    *n_out = (int64_t)ord.size();
+    if ((int64_t)ord.size() > cap)
+        return fail(MOSAIC_E_CAPACITY, "st_intersection_aggregate: " + std::to_string(ord.size()) + " groups");
+    for (size_t i = 0; i < ord.size(); i++) {
+        const size_t k = ord[i];
+        const unsigned long long key = g.gkey[g.r.units[g.gstart[k]].gs];
+        out_left_key[i] = (int32_t)(key >> 32);
+        out_right_key[i] = (int32_t)(key & 0xffffffffULL);
+        out_area[i] = garea[k];
+        out_status[i] = (uint8_t)(garea[k] != garea[k] ? 1 : 0);
+    }
+    return MOSAIC_OK;
+}
 
 int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k, int loop,
                       int64_t* out, int32_t* out_count) {

@@ -185,3 +185,94 @@ def polygon_area(parts):
             a = sum(pts[i][0] * pts[i + 1][1] - pts[i + 1][0] * pts[i][1] for i in range(len(pts) - 1)) / 2
             total += abs(a) if k == 0 else -abs(a)
     return total
+
+
+# ---- st_intersection_aggregate's geometry: symmetric difference of an emitted boundary against the
+# exact set (float slabs; the checker of overlay.h / isect_geom.cpp, a different algorithm from the
+# engine's noding + labelling).  The set is X = union over units u of (some part of A_u holds p) and
+# (some part of B_u holds p) -- per joined cell the union of the group's left chips intersected with
+# the union of its right chips (None: that side covers everything); the emitted result is a list of
+# directed edges (x0, y0, x1, y1), interior on the left, whose winding number W is the result's
+# indicator.  Between consecutive abscissae of all vertices and all edge crossings nothing crosses,
+# so the length of {y : W != X} is linear in x and the midpoint rule exact (up to rounding).
+def symdiff_area(edges, units):
+    """(area of {W != X}, area of X, area of {W == 1}); units: [(parts_a, parts_b), ...]"""
+    import numpy as np
+
+    segs, ids = [], []  # ids: (unit, side, part) -> flat part number
+    part_no = {}
+    for u, (pa, pb) in enumerate(units):
+        for side, parts in ((0, pa), (1, pb)):
+            for k, rings in enumerate(parts or []):
+                pid = part_no.setdefault((u, side, k), len(part_no))
+                for r in rings:
+                    for i in range(len(r) - 1):
+                        if tuple(r[i]) != tuple(r[i + 1]):
+                            segs.append((r[i][0], r[i][1], r[i + 1][0], r[i + 1][1]))
+                            ids.append(pid)
+    n_in = len(segs)
+    segs += [tuple(e[:4]) for e in edges]
+    allsegs = np.array(segs, float).reshape(-1, 4)
+    ids = np.array(ids, int)
+    xs = set(allsegs[:, 0].tolist()) | set(allsegs[:, 2].tolist())
+    p, q = allsegs[:, None, :2], allsegs[:, None, 2:]
+    r, s = allsegs[None, :, :2], allsegs[None, :, 2:]
+    d = (q[..., 0] - p[..., 0]) * (s[..., 1] - r[..., 1]) - (q[..., 1] - p[..., 1]) * (s[..., 0] - r[..., 0])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = ((r[..., 0] - p[..., 0]) * (s[..., 1] - r[..., 1]) - (r[..., 1] - p[..., 1]) * (s[..., 0] - r[..., 0])) / d
+        u = ((r[..., 0] - p[..., 0]) * (q[..., 1] - p[..., 1]) - (r[..., 1] - p[..., 1]) * (q[..., 0] - p[..., 0])) / d
+        ok = (d != 0) & (t >= 0) & (t <= 1) & (u >= 0) & (u <= 1)
+        cx = p[..., 0] + t * (q[..., 0] - p[..., 0])
+    xs |= set(cx[ok].tolist())
+    xs = np.array(sorted(xs))
+    unit_of = [None] * len(part_no)
+    for (uu, side, k), pid in part_no.items():
+        unit_of[pid] = (uu, side)
+    inp, outp = allsegs[:n_in], allsegs[n_in:]
+    sg = np.where(outp[:, 2] > outp[:, 0], 1, -1)
+
+    def cross_y(sg4, xm):
+        x0, y0, x1, y1 = sg4[:, 0], sg4[:, 1], sg4[:, 2], sg4[:, 3]
+        m = ((x0 < xm) & (xm < x1)) | ((x1 < xm) & (xm < x0))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            y = y0 + (xm - x0) * (y1 - y0) / (x1 - x0)
+        return m, y
+
+    def member(par):
+        cov = [[units[uu][0] is None, units[uu][1] is None] for uu in range(len(units))]
+        for pid, v in enumerate(par):
+            if v:
+                uu, side = unit_of[pid]
+                cov[uu][side] = True
+        return any(a and b for a, b in cov)
+
+    diff = area_x = area_w = 0.0
+    for i in range(len(xs) - 1):
+        x0, x1 = xs[i], xs[i + 1]
+        if x1 <= x0:
+            continue
+        xm = 0.5 * (x0 + x1)
+        m, y = cross_y(inp, xm)
+        ev = [(yy, 0, k) for yy, k in zip(y[m].tolist(), ids[m].tolist())]
+        m, y = cross_y(outp, xm)
+        ev += [(yy, 1, g) for yy, g in zip(y[m].tolist(), sg[m].tolist())]
+        ev.sort()
+        par = [False] * len(part_no)
+        w = 0
+        lx = lw = ld = 0.0
+        for j, (yy, kind, v) in enumerate(ev):
+            if kind == 0:
+                par[v] = not par[v]
+            else:
+                w += v
+            if j + 1 < len(ev):
+                h = ev[j + 1][0] - yy
+                if h > 0:
+                    f = member(par)
+                    lx += h * f
+                    lw += h * (w == 1)
+                    ld += h * abs(w - int(f))
+        diff += (x1 - x0) * ld
+        area_x += (x1 - x0) * lx
+        area_w += (x1 - x0) * lw
+    return diff, area_x, area_w

@@ -1,14 +1,19 @@
-"""st_intersection_aggregate (§8(f) row 4) as its area: st_area of the union the reference's
-ST_IntersectionAggregate.update / merge builds per (left id, right id) group of the chip join
-(expressions/geometry/ST_IntersectionAggregate.scala) -- the quantity its tests check within 1e-8
-(ST_IntersectionBehaviors.scala:22-71 intersectionBehaviour, :73-135 intersectionAggBehaviour).
+"""st_intersection_aggregate (§8(f) row 4): the union the reference's ST_IntersectionAggregate.update /
+merge builds per (left id, right id) group of the chip join (expressions/geometry/
+ST_IntersectionAggregate.scala:40-72) -- its area, the quantity the reference's tests check within 1e-8
+(ST_IntersectionBehaviors.scala:22-71 intersectionBehaviour, :73-135 intersectionAggBehaviour), and
+its geometry as WKB.  The geometry's vertex order cannot be pinned (the reference's depends on Spark's
+aggregation order), so it is pinned as a set: the symmetric difference between the engine's polygons
+and the exact per-cell union (oracle/exact.py symdiff_area, float slabs) must be ~0, and pieces of
+adjacent cells must be dissolved into one polygon.
 
-The engine (mosaic_intersection_aggregate, isect_area.h) sums per cell: the cell for a (core, core)
-pair, the other chip for one core side, and area(left n right) otherwise as the signed sum of the
-overlaps of the two chips' edge triangles fanned from a common origin.
-The checker (oracle/exact.py intersection_area) is a different algorithm in exact rationals:
-vertical slabs between all vertex and crossing abscissae, where the section length is linear and the
-midpoint rule exact.  Pins: intersectionAggBehaviour's chip rows (H3 cells with vertex 2 dropped)
+The engine computes per (group, cell) the piece of the union -- the cell for a (core, core) pair, else
+(the group's left chips there, or the cell when one is core) n (its right chips, likewise) -- by an
+arrangement overlay (overlay.h, one GPU lane per cell) whose boundary edges the host stitches across
+cells (isect_geom.cpp); the area is the sum of the pieces' areas.  The checkers are different
+algorithms: exact rational vertical slabs (oracle/exact.py intersection_area) and float slabs of the
+symmetric difference (symdiff_area), between all vertex and crossing abscissae, where section lengths
+are linear and the midpoint rule exact.  Pins: intersectionAggBehaviour's chip rows (H3 cells with vertex 2 dropped)
 must give the union area of the four geometries, and intersectionBehaviour's invariant -- the
 aggregate over the chips of two polygons equals the area of the polygons' flat intersection --
 on NYC zones against a translated copy."""
@@ -60,51 +65,6 @@ def _parts_arrays(parts):
     return xy, ro, pr
 
 
-@pytest.fixture(scope="module")
-def host_area(tmp_path_factory):
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    so = tmp_path_factory.mktemp("ia") / "libia.so"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-I",
-                    os.path.join(root, "mosaic_amd", "csrc"), "-o", str(so),
-                    os.path.join(root, "tests", "native", "isect_area_host.cpp")], check=True)
-    lib = ctypes.CDLL(str(so))
-    lib.isect_area_host.restype = ctypes.c_double
-    vp, i = ctypes.c_void_p, ctypes.c_int
-    lib.isect_area_host.argtypes = [vp, vp, i, vp, i, vp, vp, i, vp, i]
-
-    def run(a, b):
-        xa, ra, pa = _parts_arrays(a)
-        xb, rb, pb = _parts_arrays(b)
-        return lib.isect_area_host(xa.ctypes.data, ra.ctypes.data, len(ra) - 1, pa.ctypes.data, len(pa) - 1,
-                                   xb.ctypes.data, rb.ctypes.data, len(rb) - 1, pb.ctypes.data, len(pb) - 1)
-    return run
-
-
-def test_kernel_code_on_host_matches_exact(host_area):
-    """the device area code compiled for the host against the exact slab oracle: squares, holes,
-    L-shapes, shared edges, opposite orientations, and tessellated chip pairs of valid NYC zones
-    against a translated copy"""
-    sq = lambda x0, y0, s: [(x0, y0), (x0 + s, y0), (x0 + s, y0 + s), (x0, y0 + s), (x0, y0)]
-    ell = [(0, 0), (3, 0), (3, 1), (1, 1), (1, 3), (0, 3), (0, 0)]
-    cases = [([[sq(0, 0, 2)]], [[sq(1, 1, 2)]]), ([[sq(0, 0, 2)]], [[sq(2, 0, 2)]]),
-             ([[sq(0, 0, 4), sq(1, 1, 1)]], [[sq(0, 0, 4)]]), ([[ell]], [[sq(0.5, 0.5, 2)]]),
-             ([[ell]], [[ell[::-1]]]), ([[sq(0, 0, 1)], [sq(2, 0, 1)]], [[sq(0.5, 0, 2)]])]
-    for a, b in cases:
-        assert abs(host_area(a, b) - float(exact.intersection_area(a, b))) < 1e-12
-    zones = PolygonSet.load("nyc_taxi_zones").subset([3, 7, 9, 11])
-    moved = _translated(zones)
-    li, ri = _chip_index(tessellate("H3", zones, 8)), _chip_index(tessellate("H3", moved, 8))
-    n = 0
-    for (k, cell), lv in li.items():
-        rv = ri.get((k, cell))
-        if not rv or lv[0][0] or rv[0][0]:
-            continue
-        got, want = host_area(lv[0][1], rv[0][1]), float(exact.intersection_area(lv[0][1], rv[0][1]))
-        assert abs(got - want) <= 1e-13 + 1e-9 * want, (cell, got, want)
-        n += 1
-    assert n >= 5
-
-
 def _chip_index(chips):
     """(key, cell) -> [(is_core, parts)] in row order"""
     offs, data = chips["wkb"]
@@ -117,30 +77,20 @@ def _chip_index(chips):
 
 
 def oracle_aggregate(left, right):
-    """{(left key, right key): (area, supported)} with the engine's per-cell rules, areas exact"""
-    li, ri = _chip_index(left), _chip_index(right)
-    by_cell_r = {}
-    for (k, cell), v in ri.items():
-        by_cell_r.setdefault(cell, []).append((k, v))
+    """{(left key, right key): area} of the union of the cells' increments: exact rationals for cells
+    with one pair, the float slab area of the union for cells with several"""
     out = {}
-    for (lk, cell), lv in li.items():
-        for rk, rv in by_cell_r.get(cell, []):
-            pairs = [(a, b) for a in lv for b in rv]
-            area, ok = out.get((lk, rk), (0, True))
-            cc = [a for a, b in pairs if a[0] and b[0]]
-            if cc:
-                area += exact.polygon_area(cc[0][1])
-            elif len(pairs) > 1:
-                ok = False
+    for g, units in _units(_chip_index(left), _chip_index(right)).items():
+        area = 0
+        for cell, lv, rv in units:
+            a, b, need = _increments(lv, rv, cell)
+            if len(lv) * len(rv) > 1 and need == 3:
+                area += exact.symdiff_area([], [(a, b)])[1]
+            elif need == 3:
+                area += float(exact.intersection_area(a, b))
             else:
-                a, b = pairs[0]
-                if a[0]:
-                    area += exact.polygon_area(b[1])
-                elif b[0]:
-                    area += exact.polygon_area(a[1])
-                else:
-                    area += exact.intersection_area(a[1], b[1])
-            out[(lk, rk)] = (area, ok)
+                area += float(exact.polygon_area(a if need == 1 else b))
+        out[g] = area
     return out
 
 
@@ -185,10 +135,16 @@ def test_gpu_intersection_agg_reference_rows(h3ctx):
     assert list(lk) == [0] and list(rk) == [0] and list(st) == [0]
     union = float(exact.polygon_area([[polys[0]]]) + exact.polygon_area([[polys[1]]]))
     assert abs(area[0] - union) < 1e-7  # the reference's bound (10e-8)
-    # a cell holding two border-chip pairs of one group and no (core, core) pair is refused
+    # a cell holding two border-chip pairs of one group and no (core, core) pair: the union of the
+    # two (identical) pieces, through the cell overlay (round 4 refused it)
     left2 = h3ctx.chip_table([0, 0], [ids[0], ids[0]], [rows_wkb[2], rows_wkb[2]], [0, 0], res, n_polygons=1)
     right2 = h3ctx.chip_table([0], [ids[0]], [rows_wkb[2]], [0], res, n_polygons=1)
-    assert list(h3ctx.st_intersection_aggregate_area(left2, right2)[3]) == [1]
+    _, _, a2, s2 = h3ctx.st_intersection_aggregate_area(left2, right2)
+    assert list(s2) == [0] and abs(a2[0] - float(exact.polygon_area([[chips[0]]]))) < 1e-12
+    lk, rk, area, st, wkb = h3ctx.st_intersection_aggregate(left, right)
+    assert list(st) == [0] and abs(area[0] - union) < 1e-7
+    kind, parts = read_wkb(wkb[0])
+    assert len(parts) == 1 and abs(float(exact.polygon_area(parts)) - union) < 1e-7  # the two cells, dissolved
     for t in (left, right, left2, right2):
         t.close()
 
@@ -198,8 +154,7 @@ def test_gpu_intersection_agg_nyc_zones(h3ctx):
     """intersectionBehaviour on NYC zones at res 8: engine == exact per-cell aggregate for every
     group; aggregate == the flat intersection area of the original polygons (the reference's
     invariant, 1e-8) for the groups of a polygon with its own translated copy"""
-    # valid single-polygon zones (no self-crossing ring: on invalid rings JTS's union and the
-    # winding-number area of the engine are not defined the same way)
+    # valid single-polygon zones (the flat-intersection invariant below needs JTS-valid input)
     zones = PolygonSet.load("nyc_taxi_zones").subset([3, 7, 9, 11, 15, 23, 24, 40])
     moved = _translated(zones)
     res = 8
@@ -212,12 +167,10 @@ def test_gpu_intersection_agg_nyc_zones(h3ctx):
     lk, rk, area, st = h3ctx.st_intersection_aggregate_area(left, right)
     want = oracle_aggregate(lc, rc)
     assert set(zip(lk.tolist(), rk.tolist())) == set(want)
-    assert len(want) > 0
-    for a, b, v, s in zip(lk, rk, area, st):
-        w, ok = want[(int(a), int(b))]
-        assert bool(s) == (not ok)
-        if ok:
-            assert abs(v - float(w)) <= 1e-12 + 1e-9 * abs(float(w)), (a, b, v, float(w))
+    assert len(want) > 0 and not st.any()
+    for a, b, v in zip(lk, rk, area):
+        w = want[(int(a), int(b))]
+        assert abs(v - w) <= 1e-13 + 1e-9 * abs(w), (a, b, v, w)
     checked = 0
     for a, b, v, s in zip(lk, rk, area, st):
         if a == b and not s:
@@ -237,3 +190,285 @@ def test_gpu_intersection_agg_nyc_zones(h3ctx):
 def _wkb_list(chips):
     offs, data = chips["wkb"]
     return [bytes(data[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+
+
+# ---- the union's geometry (overlay.h per cell, isect_geom.cpp across cells) ----
+
+def _build_so(tmp_path_factory, name, sources):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = tmp_path_factory.mktemp(name) / f"lib{name}.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-I",
+                    os.path.join(root, "mosaic_amd", "csrc"), "-o", str(so)] + [os.path.join(root, s) for s in sources],
+                   check=True)
+    return ctypes.CDLL(str(so))
+
+
+def _flat(parts):
+    if not parts:
+        return np.zeros(2), np.zeros(1, np.int64), np.zeros(1, np.int64)
+    return _parts_arrays(parts)
+
+
+@pytest.fixture(scope="module")
+def host_overlay(tmp_path_factory):
+    """overlay.h compiled for the host: (A parts, B parts, need) -> (directed edges, area)"""
+    lib = _build_so(tmp_path_factory, "ov", ["tests/native/overlay_host.cpp"])
+    vp, i = ctypes.c_void_p, ctypes.c_int
+    lib.overlay_host.restype = ctypes.c_int
+    lib.overlay_host.argtypes = [vp, vp, i, vp, i, vp, vp, i, vp, i, i, vp, i, vp]
+
+    def run(a, b, need):
+        xa, ra, pa = _flat(a)
+        xb, rb, pb = _flat(b)
+        out = np.zeros(4 * 65536)
+        ar = ctypes.c_double()
+        n = lib.overlay_host(xa.ctypes.data, ra.ctypes.data, len(ra) - 1, pa.ctypes.data, len(pa) - 1, xb.ctypes.data,
+                             rb.ctypes.data, len(rb) - 1, pb.ctypes.data, len(pb) - 1, need, out.ctypes.data, 65536,
+                             ctypes.byref(ar))
+        assert n >= 0
+        return out[:4 * n].reshape(-1, 4).tolist(), ar.value
+    return run
+
+
+@pytest.fixture(scope="module")
+def host_stitch(tmp_path_factory):
+    """isect_geom.cpp: edges -> WKB (None when the edges do not close)"""
+    lib = _build_so(tmp_path_factory, "st", ["tests/native/stitch_host.cpp", "mosaic_amd/csrc/isect_geom.cpp"])
+    lib.stitch_host.restype = ctypes.c_long
+    lib.stitch_host.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_double, ctypes.c_void_p, ctypes.c_long,
+                                ctypes.c_void_p]
+
+    def run(edges, snap):
+        e = np.ascontiguousarray(np.array(edges, float).reshape(-1, 4))
+        buf = np.zeros(1 << 22, np.uint8)
+        ar = ctypes.c_double()
+        n = lib.stitch_host(e.ctypes.data, len(e), snap, buf.ctypes.data, len(buf), ctypes.byref(ar))
+        return (bytes(buf[:n]) if n >= 0 else None), ar.value
+    return run
+
+
+def h3_snap(res):
+    """isect_geom's node tolerance for H3 (mosaic_hip.hip stitch_snap)"""
+    e = [1107.712591, 418.6760055, 158.2446558, 59.81085794, 22.6063794, 8.544408276, 3.229482772, 1.220629759,
+         0.461354684, 0.174375668, 0.065907807, 0.024910561, 0.009415526, 0.003559893, 0.001348575, 0.000509713][res]
+    return max(0.05 * (e / 111.32) ** 2, 180.0 * 2.0 ** -40)
+
+
+def _sq(x0, y0, s):
+    return [(x0, y0), (x0 + s, y0), (x0 + s, y0 + s), (x0, y0 + s), (x0, y0)]
+
+
+def test_overlay_unit_cases(host_overlay):
+    """one cell's overlay against the exact set: squares, holes, L-shapes, shared edges, overlapping
+    parts on one side (the union before the intersection), identical and ulp-shifted edges"""
+    ell = [(0, 0), (3, 0), (3, 1), (1, 1), (1, 3), (0, 3), (0, 0)]
+    sq = _sq
+    cases = [([[sq(0, 0, 2)]], [[sq(1, 1, 2)]]), ([[sq(0, 0, 2)]], [[sq(2, 0, 2)]]),
+             ([[sq(0, 0, 4), sq(1, 1, 1)]], [[sq(0, 0, 4)]]), ([[ell]], [[sq(0.5, 0.5, 2)]]), ([[ell]], [[ell[::-1]]]),
+             ([[sq(0, 0, 1)], [sq(2, 0, 1)]], [[sq(0.5, 0, 2)]]), ([[sq(0, 0, 2)], [sq(1, 1, 2)]], [[sq(0.5, 0.5, 2)]]),
+             ([[sq(0, 0, 2)], [sq(1, 0, 2)]], [[sq(0, 0, 3)], [sq(2, -1, 1)]]), ([[sq(0, 0, 2)]], [[sq(0, 0, 2)]]),
+             ([[sq(0, 0, 2)], [sq(0, 0, 2)]], [[sq(1, 0, 2)]]), ([[sq(0, 0, 1)], [sq(1, 0, 1)]], [[sq(0, 0, 2)]])]
+    for a, b in cases:
+        e, ar = host_overlay(a, b, 3)
+        d, ax, aw = exact.symdiff_area(e, [(a, b)])
+        assert d < 1e-12 and abs(ar - ax) < 1e-12, (a, b, d, ar, ax)
+    e, ar = host_overlay([[sq(0, 0, 2)], [sq(1, 1, 2)]], [], 1)  # B core: the union of A
+    assert abs(ar - 7) < 1e-12 and exact.symdiff_area(e, [([[sq(0, 0, 2)], [sq(1, 1, 2)]], None)])[0] < 1e-12
+    a = [[sq(-74.0, 40.7, 0.01)]]
+    b = [[[(x + math.ulp(x), y) for x, y in sq(-74.0, 40.7, 0.01)]]]
+    e, ar = host_overlay(a, b, 3)
+    assert len(e) == 4 and exact.symdiff_area(e, [(a, b)])[0] < 1e-18
+
+
+def _units(li, ri):
+    """(left key, right key) -> [(cell, left chips, right chips)] of the chip join"""
+    by_cell = {}
+    for (k, cell), v in ri.items():
+        by_cell.setdefault(cell, []).append((k, v))
+    groups = {}
+    for (lk, cell), lv in li.items():
+        for rk, rv in by_cell.get(cell, []):
+            groups.setdefault((lk, rk), []).append((cell, lv, rv))
+    return groups
+
+
+def _increments(lv, rv, cell):
+    """the reference's increments of one cell as an overlay unit (A parts | None, B parts | None, need)"""
+    acore, bcore = any(c for c, _ in lv), any(c for c, _ in rv)
+    A = [p for _, ps in lv for p in ps]
+    B = [p for _, ps in rv for p in ps]
+    if acore and bcore:
+        ring = [(math.degrees(lo), math.degrees(la)) for la, lo in oracle.h3_to_geo_boundary(cell)]
+        return [[ring + ring[:1]]], None, 1
+    if acore:
+        return None, B, 2
+    if bcore:
+        return A, None, 1
+    return A, B, 3
+
+
+def _wkb_edges(w):
+    """edges of the engine's WKB, interior on the left (its shells are clockwise)"""
+    _, parts = read_wkb(w)
+    out = []
+    for p in parts:
+        for r in p:
+            out += [(r[i + 1][0], r[i + 1][1], r[i][0], r[i][1]) for i in range(len(r) - 1)]
+    return parts, out
+
+
+def _shares_edge(parts):
+    """two polygons of a MultiPolygon with a common edge (not dissolved)"""
+    def keys(p):
+        return {tuple(sorted([(round(r[i][0], 9), round(r[i][1], 9)), (round(r[i + 1][0], 9), round(r[i + 1][1], 9))]))
+                for r in p for i in range(len(r) - 1)}
+    ks = [keys(p) for p in parts]
+    return any(ks[i] & ks[j] for i in range(len(ks)) for j in range(i + 1, len(ks)))
+
+
+def _check_group(units, wkb, area, snap):
+    """the group's WKB against the exact union of its cells' increments.  Chips of adjacent cells
+    meet along their shared side only within the stitching tolerance `snap` (each follows its own
+    cell's gnomonic side), so the exact union X has slivers of that width between cells -- gaps or
+    overlaps -- that the dissolved polygons close: the symmetric difference is bounded by snap x the
+    polygons' perimeter, and is ~0 for a group within one cell.  The area (the sum of the cells'
+    pieces) is X's within the same bound."""
+    us = [(a, b) for a, b, _ in units]
+    parts, e = _wkb_edges(wkb)
+    d, ax, aw = exact.symdiff_area(e, us)
+    per = sum(math.hypot(x1 - x0, y1 - y0) for x0, y0, x1, y1 in e)
+    # (the overlay's node tolerance, 2^-40 of the coordinates, moves vertices by <= 7e-11 degrees:
+    # 1e-13 of absolute slack; the float slab checker's own precision: 1e-8 relative)
+    bound = (snap * per if len(units) > 1 else 0.0) + 1e-9 * ax + 1e-13
+    assert d <= bound, (d, bound, ax)
+    # (the area sums the cells' pieces, so a sliver where two cells' chips overlap counts twice there)
+    assert abs(area - ax) <= bound + 1e-8 * ax, (area, ax)
+    assert not _shares_edge(parts)
+    return len(parts)
+
+
+@pytest.mark.parametrize("res", [8, 9])
+def test_overlay_stitch_nyc_groups(host_overlay, host_stitch, res):
+    """zones against a translated copy: per cell the overlay (host build of the device code), across
+    cells the stitching; every group's polygons equal the exact union (symmetric difference ~0) and
+    pieces of adjacent cells are dissolved (no polygon shares an edge with another)"""
+    zones = PolygonSet.load("nyc_taxi_zones").subset([3, 7, 9, 11, 15, 23, 24, 40])
+    moved = _translated(zones)
+    groups = _units(_chip_index(tessellate("H3", zones, res)), _chip_index(tessellate("H3", moved, res)))
+    assert len(groups) >= 10
+    multi_cell = 0
+    for g, units in sorted(groups.items()):
+        edges, area, us = [], 0.0, []
+        for cell, lv, rv in units:
+            a, b, need = _increments(lv, rv, cell)
+            e, ar = host_overlay(a or [], b or [], need)
+            edges += e
+            area += ar
+            us.append((a, b, need))
+        w, _ = host_stitch(edges, h3_snap(res))
+        assert w is not None, g
+        _check_group(us, w, area, h3_snap(res))
+        multi_cell += len(units) > 1
+    assert multi_cell >= 5
+
+
+def _overlapping_left(zones, k, res):
+    """a chip set whose key 0 holds zone k and a copy shifted by a fraction of a cell: overlapping
+    chips of one key in one cell (the case the union exists for)"""
+    a = zones.subset([k])
+    xy = a.xy.copy()
+    xy[:, 0] += 0.0013
+    xy[:, 1] += 0.0007
+    b = PolygonSet(xy, a.ring_offsets, a.part_rings, a.geom_parts)
+    ca, cb = tessellate("H3", a, res), tessellate("H3", b, res)
+    out = {}
+    for c in (ca, cb):
+        offs, data = c["wkb"]
+        out.setdefault("is_core", []).extend(c["is_core"].tolist())
+        out.setdefault("index_id", []).extend(c["index_id"].tolist())
+        out.setdefault("wkb", []).extend(bytes(data[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1))
+    out["polygon_key"] = [0] * len(out["index_id"])
+    return out
+
+
+def _index_rows(rows):
+    d = {}
+    for core, cid, w, k in zip(rows["is_core"], rows["index_id"], rows["wkb"], rows["polygon_key"]):
+        d.setdefault((int(k), int(cid)), []).append((int(core), read_wkb(w)[1] if len(w) else []))
+    return d
+
+
+def test_overlay_overlapping_chips(host_overlay, host_stitch):
+    """a key whose chips overlap within cells (two overlapping polygons under one key) against a
+    translated zone: the union of the overlapping pieces, exact, dissolved"""
+    zones = PolygonSet.load("nyc_taxi_zones")
+    res = 9
+    left = _overlapping_left(zones, 3, res)
+    moved = _translated(zones.subset([3]))
+    groups = _units(_index_rows(left), _chip_index(tessellate("H3", moved, res)))
+    (g, units), = groups.items()
+    assert sum(len(lv) > 1 for _, lv, _ in units) >= 5
+    edges, area, us = [], 0.0, []
+    for cell, lv, rv in units:
+        a, b, need = _increments(lv, rv, cell)
+        e, ar = host_overlay(a or [], b or [], need)
+        edges += e
+        area += ar
+        us.append((a, b, need))
+    w, _ = host_stitch(edges, h3_snap(res))
+    assert w is not None
+    _check_group(us, w, area, h3_snap(res))
+
+
+def _table(ctx, rows, res, n):
+    return ctx.chip_table(rows["is_core"], rows["index_id"], list(rows["wkb"]), rows["polygon_key"], res, n_polygons=n)
+
+
+def _rows(chips):
+    return dict(is_core=chips["is_core"], index_id=chips["index_id"], wkb=_wkb_list(chips), polygon_key=chips["polygon_key"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("res", [8, 9, 10])
+def test_gpu_intersection_agg_geometry_nyc(h3ctx, res):
+    """all 263 NYC zones against a translated copy: no group refused; the area API and
+    the geometry API agree; sampled groups' polygons equal the exact union of their cells' increments
+    (symmetric difference ~0), dissolved across cells"""
+    zones = PolygonSet.load("nyc_taxi_zones")
+    moved = _translated(zones)
+    lc, rc = tessellate("H3", zones, res, ctx=h3ctx), tessellate("H3", moved, res, ctx=h3ctx)
+    left, right = _table(h3ctx, _rows(lc), res, len(zones)), _table(h3ctx, _rows(rc), res, len(zones))
+    lk, rk, area, st, wkb = h3ctx.st_intersection_aggregate(left, right)
+    lk2, rk2, area2, st2 = h3ctx.st_intersection_aggregate_area(left, right)
+    assert len(lk) > 500 and not st.any() and not st2.any()
+    assert np.array_equal(lk, lk2) and np.array_equal(rk, rk2)
+    assert np.array_equal(area.view(np.uint64), area2.view(np.uint64))  # (one unit pipeline)
+    groups = _units(_chip_index(lc), _chip_index(rc))
+    assert set(zip(lk.tolist(), rk.tolist())) == set(groups)
+    idx = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(lk, rk))}
+    rng = np.random.default_rng(res)
+    sample = [k for k in sorted(groups) if len(groups[k]) > 1 and len(groups[k]) <= 40]
+    for g in [sample[i] for i in rng.choice(len(sample), min(12, len(sample)), replace=False)]:
+        us = [_increments(lv, rv, cell) for cell, lv, rv in groups[g]]
+        _check_group(us, wkb[idx[g]], area[idx[g]], h3_snap(res))
+    left.close()
+    right.close()
+
+
+@pytest.mark.gpu
+def test_gpu_intersection_agg_overlapping_chips(h3ctx):
+    """the overlapping chip set on the GPU: no refusal, geometry exact and dissolved, the area API
+    equal to the geometry API"""
+    zones = PolygonSet.load("nyc_taxi_zones")
+    res = 9
+    rows = _overlapping_left(zones, 3, res)
+    moved = _translated(zones.subset([3]))
+    rc = tessellate("H3", moved, res)
+    left, right = _table(h3ctx, rows, res, 1), _table(h3ctx, _rows(rc), res, 1)
+    lk, rk, area, st, wkb = h3ctx.st_intersection_aggregate(left, right)
+    _, _, area2, st2 = h3ctx.st_intersection_aggregate_area(left, right)
+    assert list(st) == [0] and list(st2) == [0] and abs(area[0] - area2[0]) <= 1e-12 * area[0]
+    (g, units), = _units(_index_rows(rows), _chip_index(rc)).items()
+    _check_group([_increments(lv, rv, cell) for cell, lv, rv in units], wkb[0], area[0], h3_snap(res))
+    left.close()
+    right.close()

@@ -1,5 +1,6 @@
 """Timing of st_intersects_aggregate (mosaic_intersects_aggregate) and of st_intersection_aggregate's
-area (mosaic_intersection_aggregate) on the GPU box: the 263 NYC zones chipped at H3 res 9 and 10
+area (mosaic_intersection_aggregate) and geometry (mosaic_intersection_aggregate_geometry: GPU cell
+overlay + host stitching into WKB) on the GPU box: the 263 NYC zones chipped at H3 res 9 and 10
 joined with a translated copy.  Prints one JSON line per case (groups, true groups, refused groups,
 ms for each whole call incl. D2H)."""
 import json
@@ -37,10 +38,17 @@ def main():
             t0 = time.perf_counter()
             _, _, area, st = ctx.st_intersection_aggregate_area(tl, tr)
             ta.append((time.perf_counter() - t0) * 1e3)
+        tg = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, _, garea, gst, wkb = ctx.st_intersection_aggregate(tl, tr)
+            tg.append((time.perf_counter() - t0) * 1e3)
         print(json.dumps({"case": f"{name} res {res} shift {shift}", "chips": [len(l["index_id"]), len(r["index_id"])],
                           "groups": int(len(fl)), "true": int(fl.sum()), "ms_median": float(np.median(ts)),
                           "area_ms_median": float(np.median(ta)), "area_refused_groups": int(st.sum()),
-                          "area_total": float(area[st == 0].sum())}), flush=True)
+                          "area_total": float(area[st == 0].sum()), "geometry_ms_median": float(np.median(tg)),
+                          "geometry_refused_groups": int(gst.sum()),
+                          "wkb_bytes": int(sum(len(w) for w in wkb if w is not None))}), flush=True)
         tl.close()
         tr.close()
 
