@@ -118,8 +118,9 @@ def usable_cpus():
 
 
 def build_chips(ctx, res, rank, world):
-    """Rank 0 tessellates (grid_tessellateexplode, cell classification on its GPU); the chip rows go
-    to the other ranks over the process group (one build per node instead of one per rank)."""
+    """Rank 0 tessellates (grid_tessellateexplode, cell classification on its GPU); the chip columns go
+    to the other ranks as raw buffers over the process group (broadcast_chip_set: one build per node
+    instead of one per rank, no pickling)."""
     from mosaic_amd.data import PolygonSet
 
     zones = PolygonSet.load("nyc_taxi_zones")
@@ -128,11 +129,13 @@ def build_chips(ctx, res, rank, world):
     if rank == 0:
         chips = ctx.grid_tessellateexplode(zones, res)
     if world > 1:
+        import torch
         import torch.distributed as dist
 
-        obj = [chips]
-        dist.broadcast_object_list(obj, src=0)
-        chips = obj[0]
+        from mosaic_amd.distributed import broadcast_chip_set
+
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else None
+        chips = broadcast_chip_set(chips, src=0, device=dev)
     return zones, chips, time.perf_counter() - t0
 
 

@@ -120,7 +120,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * "bin_min_rows" (smallest batch that is binned; default 2^18), "bin_chunk" (rows per sort chunk;
  * default 2^28), "tile_images" (0: none; 1: tables built without a point raster carry per-tile chip
  * images the binned join copies into LDS, the default; 2: every tile-directory table carries them),
- * "exact_cap" (rows of the exact-H3 queue; 0 = the default max(n / 8, 2^20) capped at n; an overflow
+ * "bin_spin_cap" (the binned join's look-back poll limit; < 0 forces its uncompacted fallback -- a test
+ * knob), "exact_cap" (rows of the exact-H3 queue; 0 = the default max(n / 8, 2^20) capped at n; an overflow
  * reruns the batch on the exact path, or is reported as MOSAIC_E_CAPACITY by mosaic_sync after an
  * async call). */
 int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t value);

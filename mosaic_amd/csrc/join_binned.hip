@@ -76,14 +76,15 @@ __global__ void __launch_bounds__(256) k_bin_keys(JoinArgs a, int64_t lo, int64_
 // tile_images.h), compacted in one pass: workgroup b takes kBinChunk consecutive points, counts the
 // kept ones and finds its output offset by decoupled look-back over the earlier workgroups' status
 // words (flag | count: an aggregate published at once, then the inclusive prefix), so the sort and
-// the join see only the kept points.  Workgroups are dispatched in index order, so every status a
-// workgroup waits on belongs to a running workgroup that publishes its aggregate without waiting on
-// anything; the wait is still bounded (kBinSpinCap polls; then *err is set and the caller reruns
-// the uncompacted k_bin_keys).
+// the join see only the kept points.  A workgroup's chunk is its ordered ticket (an atomic counter
+// taken at start, status[gridDim.x]), not its blockIdx: every status it waits on belongs to a
+// workgroup that took an earlier ticket, so is already running and publishes its aggregate without
+// waiting on anything -- whatever order the hardware dispatches workgroups in.  The wait is still
+// bounded (spin_cap polls; then *err is set and the caller reruns the pass uncompacted; spin_cap < 0
+// forces that fallback, for its test).
 static const int kBinPPT = 8;  // points per thread (4: the pass 20 % slower)
 static const int kBinChunk = 256 * kBinPPT;
 static const unsigned long long kStAgg = 1ULL << 62, kStPre = 2ULL << 62, kStVal = (1ULL << 62) - 1;
-static const int kBinSpinCap = 1 << 20;
 
 // status words: one 8-byte word carries flag and count, so there is no payload to order; stores and
 // polls go to memory (system scope: sc0 sc1), never to a stale L2 line of another XCD
@@ -105,12 +106,16 @@ template <class P, bool VEC, bool COMPACT>
 __global__ void __launch_bounds__(256) k_bin_cover(const double* __restrict__ X, const double* __restrict__ Y,
                                                    tiles::Grid g, const uint32_t* __restrict__ bin_map, int64_t lo,
                                                    int64_t n, uint32_t* keys, P* pts, unsigned long long* status,
-                                                   unsigned long long* total, unsigned int* err) {
+                                                   unsigned long long* total, unsigned int* err, int spin_cap) {
     __shared__ uint32_t woff[kBinPPT * 4];  // per (item, wave): kept count, then output offset in the workgroup
-    __shared__ unsigned long long base_s;
+    __shared__ unsigned long long base_s, ticket_s;
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int64_t b = blockIdx.x;
+    if (COMPACT) {
+        if (threadIdx.x == 0) ticket_s = atomicAdd(&status[gridDim.x], 1ULL);
+        __syncthreads();
+    }
+    const int64_t b = COMPACT ? (int64_t)ticket_s : (int64_t)blockIdx.x;
     const int64_t cs = lo + b * kBinChunk;
     // item k of this thread: point cs + 2 (k/2 256 + t) + k%2 (VEC: 16-byte loads of both columns)
     // or cs + k 256 + t
@@ -210,6 +215,7 @@ __global__ void __launch_bounds__(256) k_bin_cover(const double* __restrict__ X,
         const unsigned long long T = (unsigned long long)__shfl(incl, 31, 64);
         // decoupled look-back: lane l reads workgroup j - l's status
         unsigned long long excl = 0;
+        if (spin_cap < 0 && lane == 0) atomicOr(err, 1u);
         if (b > 0) {
             if (lane == 0) st_publish(&status[b], kStAgg | T);
             int64_t j = b - 1;
@@ -218,7 +224,7 @@ __global__ void __launch_bounds__(256) k_bin_cover(const double* __restrict__ X,
                 const int64_t k = j - lane;
                 unsigned long long st = k >= 0 ? st_poll(&status[k]) : kStPre;
                 while (__ballot((st >> 62) == 0)) {
-                    if (++spins > kBinSpinCap) {  // (never expected: see above)
+                    if (++spins > spin_cap) {  // (never expected: see above)
                         if (lane == 0) atomicOr(err, 1u);
                         if ((st >> 62) == 0) st = kStPre;
                         break;
@@ -620,20 +626,21 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
     const int64_t nb = (m + kBinChunk - 1) / kBinChunk;
     if ((e = s.keys[0].reserve((size_t)m * 4)) || (e = s.keys[1].reserve((size_t)m * 4)) ||
         (e = s.vals[0].reserve((size_t)m * vb)) || (e = s.vals[1].reserve((size_t)m * vb)) || (e = s.n_skip.reserve(32)) ||
-        (img.words && (e = s.status.reserve((size_t)std::max<int64_t>(nb, 1) * 8))))
+        (img.words && (e = s.status.reserve((size_t)std::max<int64_t>(nb + 1, 1) * 8))))
         return e;
     // n_skip words: [0] kSkip rows (k_bin_keys) or kept rows (k_bin_cover), [1] 0, [2] look-back failure
     if ((e = hipMemsetAsync(s.n_skip.p, 0, 32, stream))) return e;
     unsigned long long* nsk = (unsigned long long*)s.n_skip.p;
+    s.lookback_failed = 0;
     const bool vec = (((uintptr_t)(a0.x + lo) | (uintptr_t)(a0.y + lo)) & 15) == 0;
     bool keyed = false;  // keys from k_bin_cover (image keys)
     if (img.words && m > 0) {
-        if ((e = hipMemsetAsync(s.status.p, 0, (size_t)nb * 8, stream))) return e;
+        if ((e = hipMemsetAsync(s.status.p, 0, (size_t)(nb + 1) * 8, stream))) return e;  // (+ the ticket)
         unsigned int* err = (unsigned int*)(nsk + 2);
         unsigned long long* st = (unsigned long long*)s.status.p;
 #define MOSAIC_BIN_COVER(VEC, COMPACT)                                                                                \
     hipLaunchKernelGGL((k_bin_cover<P, VEC, COMPACT>), dim3(nb), dim3(256), 0, stream, a0.x, a0.y, a0.tgrid,              \
-                       img.bin_map, lo, n, (uint32_t*)s.keys[0].p, (P*)s.vals[0].p, st, nsk, err)
+                       img.bin_map, lo, n, (uint32_t*)s.keys[0].p, (P*)s.vals[0].p, st, nsk, err, s.spin_cap)
         if (vec && m >= 2)
             MOSAIC_BIN_COVER(true, true);
         else
@@ -643,6 +650,7 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
         if ((e = hipMemcpyAsync(hw, nsk, sizeof hw, hipMemcpyDeviceToHost, stream)) || (e = hipStreamSynchronize(stream)))
             return e;
         const bool ok = hw[2] == 0 && hw[0] <= (unsigned long long)m;
+        s.lookback_failed = !ok;
         if (ok) {
             m = (int64_t)hw[0];
             nsk += 1;  // the join starts at sorted row 0

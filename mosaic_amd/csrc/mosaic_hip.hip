@@ -1695,6 +1695,8 @@ struct Options {
     // exact-H3 queue capacity in rows (0: the default, max(n / 8, 2^20) capped at n); a small value
     // exercises the overflow -> rerun path
     int64_t exact_cap = 0;
+    // k_bin_cover's look-back poll limit (< 0: the uncompacted fallback at once, for its test)
+    int bin_spin_cap = 1 << 20;
 };
 
 // Execution state of one calling thread on one context: its HIP stream (created on first use, or
@@ -2217,7 +2219,7 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, 1024]");
         o.stream_block = (int)v;
     } else if (k == "stream_pipe") {
-        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "stream_pipe must be 0, 1 or 2");
+        if (v < 0 || v > 3) return fail(MOSAIC_E_ARG, "stream_pipe must be 0, 1, 2 or 3");
         o.stream_pipe = (int)v;
     } else if (k == "bng_cpt") {
         o.bng_cpt = v ? 1 : 0;
@@ -2243,6 +2245,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "scratch_limit") {
         if (v < 0) return fail(MOSAIC_E_ARG, "scratch_limit must be >= 0");
         o.scratch_limit = v;
+    } else if (k == "bin_spin_cap") {
+        o.bin_spin_cap = (int)std::max<int64_t>(-1, std::min<int64_t>(v, (int64_t)1 << 30));
     } else if (k == "exact_cap") {
         if (v < 0) return fail(MOSAIC_E_ARG, "exact_cap must be >= 0");
         o.exact_cap = v;
@@ -3945,14 +3949,14 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 // cs + kFixBits + qs <= 24 low bits of the fine-cell coordinates and a 16-bit tile index
                 // per pending row, and per wave a kCptBufWords compaction buffer in LDS)
                 int mode = vec && sa.tb_lds && sa.fix_ok ? c->stream_pipe : 0;
-                if (mode == 2 && !(sa.cs + tiles::kFixBits + sa.qs <= 24 && sa.n_tiles <= 65536 &&
+                if (mode >= 2 && !(sa.cs + tiles::kFixBits + sa.qs <= 24 && sa.n_tiles <= 65536 &&
                                    shm_s + (size_t)(blk / 64) * kCptBufWords * 4 <= kStreamLdsMax))
                     mode = 1;
                 return mode;
             };
             auto kernel_for = [&](bool vec) -> const void* { return stream_kernel_h3(mode_for(vec), lds, pairs, vec); };
             auto shm_for = [&](bool vec) -> size_t {
-                return shm_s + (mode_for(vec) == 2 ? (size_t)(blk / 64) * kCptBufWords * 4 : 0);
+                return shm_s + (mode_for(vec) >= 2 ? (size_t)(blk / 64) * kCptBufWords * 4 : 0);
             };
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(true), blk, shm_for(true)) != hipSuccess ||
@@ -3965,9 +3969,11 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 // 16-byte loads need aligned columns and >= 256 rows (the prefetch past the end
                 // re-reads the chunk's first 256)
                 const void* kfn = kernel_for(aligned && ac.n - lo >= 256);
+                const int mode = mode_for(aligned && ac.n - lo >= 256);
                 if (lo == 0) {
-                    static const char* const names[3] = {"k_join_stream", "k_join_stream_pipe", "k_join_stream_cpt"};
-                    c->last_kernel = names[mode_for(aligned && ac.n - lo >= 256)];
+                    static const char* const names[4] = {"k_join_stream", "k_join_stream_pipe", "k_join_stream_cpt",
+                                                         "k_join_stream_cpt"};
+                    c->last_kernel = names[mode];
                 }
                 if (lo > 0) HIP_TRY(hipMemsetAsync(ac.mixq_count, 0, 8, c->stream));
                 // persistent grid: the workgroups resident at once (each fills its LDS once)
@@ -3981,6 +3987,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                                                                            (int64_t)c->n_cu * c->mixed_blocks_per_cu));
 #define MOSAIC_MIXED(KERNEL, SHM) \
     hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac)
+                if (mode == 3) continue;  // (the stream kernel answered its mixed rows itself)
                 hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
                 if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
                 if (c->mixed_rows == 4) {
@@ -4017,6 +4024,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                     img.max_words = ch->img_max_words;
                     img.n_images = (uint32_t)ch->img_count;
                 }
+                c->bins.spin_cap = c->bin_spin_cap;
                 hipError_t e = binned::join(a, lo, hi, max_code, lds && !pairs, c->n_cu, img, c->bins, c->stream);
                 if (e == hipErrorOutOfMemory) return fail(MOSAIC_E_NOMEM, "binned join: device allocation failed");
                 if (e != hipSuccess) return fail(MOSAIC_E_HIP, std::string("binned join: ") + hipGetErrorString(e));

@@ -63,6 +63,43 @@ def sharded_join_count(count_fn, x, y, n_polygons, device=None):
     return counts[:n_polygons]
 
 
+def broadcast_chip_set(chips, src=0, device=None):
+    """Replicate a chip set (tessellate()'s columns) from rank `src` to every rank as raw buffers --
+    one size message, then is_core, index_id, polygon_key, the WKB offsets and the WKB bytes, each a
+    single broadcast -- instead of a pickled object (C4: 12 M chips, GBs of WKB).  The chip table is
+    then built on every rank from identical columns (chips replicated per
+    GPU).  `device`: where the collective's tensors live (a CUDA device for RCCL, None for gloo).
+    Returns the chip set on every rank (numpy columns; on `src` the input itself)."""
+    import numpy as np
+
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return chips
+    me = dist.get_rank()
+    sizes = torch.zeros(2, dtype=torch.int64, device=device)
+    if me == src:
+        sizes[0] = len(chips["index_id"])
+        sizes[1] = int(chips["wkb"][0][-1])
+    dist.broadcast(sizes, src=src)
+    n, nb = int(sizes[0]), int(sizes[1])
+    cols = [("is_core", torch.uint8, n), ("index_id", torch.int64, n), ("polygon_key", torch.int32, n),
+            ("wkb_offsets", torch.int64, n + 1), ("wkb", torch.uint8, nb)]
+    out = {}
+    for name, dt, m in cols:
+        if me == src:
+            src_arr = chips["wkb"][0] if name == "wkb_offsets" else (chips["wkb"][1][:nb] if name == "wkb" else chips[name])
+            npdt = {torch.uint8: np.uint8, torch.int64: np.int64, torch.int32: np.int32}[dt]
+            t = torch.from_numpy(np.ascontiguousarray(src_arr, dtype=npdt)).to(device) if m else torch.empty(0, dtype=dt, device=device)
+        else:
+            t = torch.empty(m, dtype=dt, device=device)
+        if m:
+            dist.broadcast(t, src=src)
+        out[name] = t.cpu().numpy() if me != src else None
+    if me == src:
+        return chips
+    return dict(is_core=out["is_core"], index_id=out["index_id"], polygon_key=out["polygon_key"],
+                wkb=(out["wkb_offsets"], out["wkb"]))
+
+
 def finalize():
     if dist.is_initialized():
         dist.barrier()

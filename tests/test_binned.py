@@ -151,3 +151,37 @@ def test_binned_many_polygons_wave_hash(h3ctx):
         torch.cuda.empty_cache()
         table.close()
 
+
+
+def test_binned_lookback_fallback(h3ctx):
+    """k_bin_cover's compaction takes ordered tickets; its bounded wait's fallback (rerun in place,
+    dropped rows keyed kSkip) is forced with bin_spin_cap < 0 and must give the same counts and pairs
+    (every row then goes through the sort: last_binned_rows == n)."""
+    zones = PolygonSet.load("nyc_taxi_zones_35")
+    chips = tessellate("H3", zones, 9)
+    rng = np.random.default_rng(31)
+    x0, y0, x1, y1 = zones.bbox()
+    x = rng.uniform(x0 - 0.05, x1 + 0.05, 700_001)
+    y = rng.uniform(y0 - 0.05, y1 + 0.05, 700_001)
+    want, total = oracle.pip_join(_oracle_chips(chips), oracle.GRID_H3, 9, x, y, len(zones))
+    _set(h3ctx, tile_images=2)
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
+                             n_polygons=len(zones))
+    try:
+        _set(h3ctx, point_raster=0, bin_points=1)
+        kept = None
+        for cap in (1 << 20, -1):
+            _set(h3ctx, bin_spin_cap=cap)
+            assert np.array_equal(h3ctx.pip_join_count(table, x, y), want), cap
+            assert h3ctx.last_kernel() == "k_join_tiles"
+            rows = h3ctx.last_binned_rows()
+            if cap > 0:
+                kept = rows
+                assert 0 < kept < len(x)
+            else:
+                assert rows == len(x)
+            r, k = h3ctx.pip_join_pairs(table, x, y)
+            assert len(r) == total and np.array_equal(np.bincount(k, minlength=len(zones)), want)
+    finally:
+        _set(h3ctx, point_raster=1, bin_points=1, tile_images=1, bin_spin_cap=1 << 20)
+        table.close()
