@@ -1,7 +1,6 @@
 // The stream kernels of the point-raster join: k_join_stream / k_join_stream_pipe (H3 tile
 // directory + point raster, tiles.h) and k_join_stream_bng (BNG dense cell table).  A translation
 // unit of their own (the host side that builds their arguments and launches them is mosaic_hip.hip).
-#include "join_chips.h"
 #include "join_common.h"
 
 // ---- k_join_stream (default with a point raster, tiles.h): the point raster's answer for every
@@ -438,63 +437,7 @@ struct CptSet {
     v4u lrec;       // gathered line record
 };
 
-// The mixed rows of one wave (stage entries wq[0 .. n), n <= 64: one row per lane), answered inside
-// the stream kernel (stream_pipe = 3): the path of k_join_mixed (tile record, certified hexagon,
-// window entry, hash entry, raster chip loop; rows the fast path cannot certify take tiled_cell's
-// exact cell in place) -- so the rows' dependent load chains run while the SIMD's other waves stream,
-// instead of in a separate launch behind the whole stream.  A call: its registers are not the
-// stream loop's.
-#ifndef MOSAIC_MIX_INLINE
-#define MOSAIC_MIX_ATTR __noinline__
-#else
-#define MOSAIC_MIX_ATTR inline
-#endif
-template <bool CM, bool PAIRS>
-__device__ MOSAIC_MIX_ATTR void mixed_batch(const JoinArgs& a, const uint32_t* wq, uint32_t n, unsigned int* lds,
-                                            SlabItem* items, unsigned int* tests) {
-    const int lane = (int)(threadIdx.x & 63);
-    const bool live = (uint32_t)lane < n;
-    const int64_t row = a.row_lo + (live ? (int64_t)wq[lane] : 0);
-    __builtin_amdgcn_wave_barrier();
-    const double x = a.x[row], y = a.y[row];
-    const uint32_t code = tiles::tile_of(a.tgrid, a.tile_idx, x, y);
-    const tiles::TileRec rec = a.tile_rec[code >= 2 ? code - 2 : 0];
-    bool fast = false;
-    uint32_t ent_idx = 0;
-    if (live && code >= 2) {
-        const int face = (int)(rec.dims & 0xffu);
-        const int wa = (int)((rec.dims >> 8) & 0xfffu), wb = (int)(rec.dims >> 20);
-        double px, py, pz, vx, vy, best;
-        h3::fast_unit(y, x, &px, &py, &pz);
-        h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
-        int ba, bb;
-        if (h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
-            const int ra = ba - rec.a0, rb = bb - rec.b0;
-            if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
-                fast = true;
-                ent_idx = rec.off + (uint32_t)(ra * wb + rb);
-            }
-        }
-    }
-    const uint32_t ent = a.tile_ent[ent_idx];
-    const HashEntry he = a.table[fast && ent ? ent - 1 : 0];
-    uint32_t cur = 0, end = 0;
-    if (live) {
-        if (fast) {
-            if (ent) {
-                cur = he.first;
-                end = he.first + he.count;
-            }
-        } else {
-            tiled_cell(a, row, x, y, code, cur, end);
-        }
-    }
-    unsigned int t = 0;
-    raster_chips<CM, PAIRS>(a, live ? row : -1, cur, end, x, y, t, lds, items);
-    *tests += t;
-}
-
-template <bool LDS_COUNTS, bool PAIRS, bool MIX>
+template <bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) k_join_stream_cpt(JoinArgs a, StreamArgs s) {
     extern __shared__ unsigned int lds[];
     const int nwaves = (int)(blockDim.x >> 6);
@@ -519,24 +462,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     uint32_t* wq = stage + wave * s.stage_words;
     uint32_t* cbuf = cbuf_all + wave * kCptBufWords;
-    // (MIX) the chip loop's work items of this wave, in its compaction buffer (free between sets)
-    SlabItem* items = (SlabItem*)(((uintptr_t)cbuf + 7) & ~(uintptr_t)7);
-    unsigned int tests = 0;
     uint32_t wn = 0;
-    // a full stage (>= 64 rows): to the global queue, or (MIX) answered here, 64 at a time
-    auto flush64 = [&]() {
-        if (!MIX) {
-            stage_flush(a, wq, wn, lane, 64);
-        } else if (wn >= 64) {
-            mixed_batch<LDS_COUNTS, PAIRS>(a, wq, 64u, lds, items, &tests);
-            const uint32_t rest = wn - 64u;  // (< 64)
-            const uint32_t v = (uint32_t)lane < rest ? wq[64 + lane] : 0u;
-            __builtin_amdgcn_wave_barrier();
-            if ((uint32_t)lane < rest) wq[lane] = v;
-            __builtin_amdgcn_wave_barrier();
-            wn = rest;
-        }
-    };
     constexpr int F = tiles::kFixBits;
     const uint32_t cs = (uint32_t)s.cs, qs = (uint32_t)s.qs;
     const uint32_t lowm = (1u << (cs + F + qs)) - 1u;
@@ -599,7 +525,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const unsigned long long mm = __ballot(m);
             if (m) wq[wn + __popcll(mm & lt_mask)] = (uint32_t)(row - a.row_lo);
             wn += (uint32_t)__popcll(mm);
-            flush64();  // the stage holds < 128
+            stage_flush(a, wq, wn, lane, 64);  // the stage holds < 128
         }
     };
     // --- stage A of a group: LDS levels, resolved rows answered, pending rows compacted into z (the
@@ -742,13 +668,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             set_d(z2, wt);
         }
     }
-    if (!MIX) {
-        stage_flush(a, wq, wn, lane, 1);
-    } else {
-        if (wn) mixed_batch<LDS_COUNTS, PAIRS>(a, wq, wn, lds, items, &tests);
-        for (int off = 32; off > 0; off >>= 1) tests += __shfl_down(tests, off, 64);
-        if (lane == 0 && tests) atomicAdd(a.tests, (unsigned long long)tests);
-    }
+    stage_flush(a, wq, wn, lane, 1);
     if (LDS_COUNTS) {
         __syncthreads();
         for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
@@ -1191,15 +1111,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 }
 
 const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec) {
-    if (pipe == 3 && vec) {
-        if (pairs) return (const void*)k_join_stream_cpt<false, true, true>;
-        if (lds) return (const void*)k_join_stream_cpt<true, false, true>;
-        return (const void*)k_join_stream_cpt<false, false, true>;
-    }
     if (pipe == 2 && vec) {
-        if (pairs) return (const void*)k_join_stream_cpt<false, true, false>;
-        if (lds) return (const void*)k_join_stream_cpt<true, false, false>;
-        return (const void*)k_join_stream_cpt<false, false, false>;
+        if (pairs) return (const void*)k_join_stream_cpt<false, true>;
+        if (lds) return (const void*)k_join_stream_cpt<true, false>;
+        return (const void*)k_join_stream_cpt<false, false>;
     }
     if (pipe && vec) {
         if (pairs) return (const void*)k_join_stream_pipe<false, true>;

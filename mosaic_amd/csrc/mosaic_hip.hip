@@ -2219,7 +2219,7 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         if (v < 64 || v > 1024 || v % 64) return fail(MOSAIC_E_ARG, "stream_block must be a multiple of 64 in [64, 1024]");
         o.stream_block = (int)v;
     } else if (k == "stream_pipe") {
-        if (v < 0 || v > 3) return fail(MOSAIC_E_ARG, "stream_pipe must be 0, 1, 2 or 3");
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "stream_pipe must be 0, 1 or 2");
         o.stream_pipe = (int)v;
     } else if (k == "bng_cpt") {
         o.bng_cpt = v ? 1 : 0;
@@ -3971,8 +3971,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 const void* kfn = kernel_for(aligned && ac.n - lo >= 256);
                 const int mode = mode_for(aligned && ac.n - lo >= 256);
                 if (lo == 0) {
-                    static const char* const names[4] = {"k_join_stream", "k_join_stream_pipe", "k_join_stream_cpt",
-                                                         "k_join_stream_cpt"};
+                    static const char* const names[3] = {"k_join_stream", "k_join_stream_pipe", "k_join_stream_cpt"};
                     c->last_kernel = names[mode];
                 }
                 if (lo > 0) HIP_TRY(hipMemsetAsync(ac.mixq_count, 0, 8, c->stream));
@@ -3987,7 +3986,6 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                                                                            (int64_t)c->n_cu * c->mixed_blocks_per_cu));
 #define MOSAIC_MIXED(KERNEL, SHM) \
     hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac)
-                if (mode == 3) continue;  // (the stream kernel answered its mixed rows itself)
                 hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
                 if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
                 if (c->mixed_rows == 4) {

@@ -274,10 +274,10 @@ def test_join_tessellated_chips_every_strategy(h3ctx):
             table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
                                      n_polygons=len(zones35))
             assert table.tiles()["built"] == 1
-            # (stream_pipe 2: k_join_stream_cpt, the default; 3: it answering its mixed rows itself -- the boundary points fill whole groups
+            # (stream_pipe 2: k_join_stream_cpt, the default -- the boundary points fill whole groups
             # with pending rows, so its > 64-row overflow path runs too; 1: k_join_stream_pipe; 0:
             # k_join_stream, the unpipelined float-coordinate stream kernel)
-            for tiles, praster, pipe in ((1, 1, 2), (1, 1, 3), (1, 1, 1), (1, 1, 0), (1, 0, 1), (0, 0, 1)):
+            for tiles, praster, pipe in ((1, 1, 2), (1, 1, 1), (1, 1, 0), (1, 0, 1), (0, 0, 1)):
                 h3ctx.set_option("tiles", tiles)
                 h3ctx.set_option("point_raster", praster)
                 h3ctx.set_option("stream_pipe", pipe)
