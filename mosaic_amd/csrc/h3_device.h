@@ -159,10 +159,18 @@ MOSAIC_HD uint64_t set_digit(uint64_t h, int r, int d) {
     return (h & ~((uint64_t)7 << s)) | ((uint64_t)d << s);
 }
 // The first nonzero digit of 1 .. res (0 if none): the most significant nonzero 3-bit group of the
-// used digits.  Written without a loop exit on purpose: gfx950 code for the loop-with-early-return
-// form read the exit condition of the wave's last iteration after the loop, so a lane that had
-// left the loop early saw "no nonzero digit" when other lanes of its wave iterated longer
-// (tools/probes/kring_reason.hip found it; tests/test_h3_kring.py covers mixed waves).
+// used digits.  Written without a loop exit on purpose.  Root cause of the round-4 failure (a
+// compiler bug, not a source bug; tools/probes/early_exit/): with H3 C's loop-with-early-return form
+// inlined into is_pentagon inside hex_range, the gfx950 code computes the exit test `d != 0` into an
+// SGPR lane mask each iteration (v_cmp_ne_u32 s[0:1]) and, after the loop, reads that mask as the
+// result (s_and_b64 s[2:3], s[0:1], exec) -- but a VOPC compare writes 0 for inactive lanes, so every
+// lane that had left the loop in an earlier iteration read "no nonzero digit"
+// (isa_old_is_pentagon.txt).  The same source gives correct code in isolation (the i1 is merged per
+// lane: s_andn2 / s_and / s_or with exec each iteration), so the miscompile depends on the
+// surrounding control flow; 446 of 1,476 k-ring rows near pentagons differed with the round-4
+// headers, 0 with these.  Device code keeps such "bool decided inside a loop" checks loop-free where
+// it can (is_valid_cell, h3_geom's digit check); the remaining loops are covered by mixed-wave GPU
+// tests against the oracle.
 MOSAIC_HD int leading_nonzero_digit(uint64_t h, int res) {
     const uint64_t d = (h & 0x1fffffffffffULL) >> (3 * (15 - res));  // digits 1 .. res, digit res lowest
     const int msb = d ? 63 - __builtin_clzll(d) : 0;

@@ -162,8 +162,11 @@ MOSAIC_HD bool h3_to_faceijk(uint64_t h, FaceIJK* f) {
     if (((h >> 59) & 15) != 1) return false;
     const int res = res_of(h), bc = base_cell_of(h);
     if (bc >= 122) return false;
-    for (int q = 1; q <= res; q++)
-        if (h3::get_digit(h, q) == 7) return false;
+    // digits 1 .. res must not be 7: bit tests, no loop exit (a bool decided inside a divergent loop
+    // and read after it is what gfx950 code got wrong in round 4: h3_device.h leading_nonzero_digit)
+    const uint64_t low = 0x1249249249249ULL, D = h & 0x1fffffffffffULL;
+    const uint64_t used = low & ~((1ULL << (3 * (15 - res))) - 1ULL);  // digit groups 1 .. res
+    if (D & (D >> 1) & (D >> 2) & used) return false;
     const bool pent = h3::kH3BaseCellData[bc][4] != 0;
     if (pent && h3::leading_nonzero_digit(h, res) == 5) h = h3::rotate_all(h, res, false);
     f->face = h3::kH3BaseCellData[bc][0];

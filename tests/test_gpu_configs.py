@@ -1,5 +1,10 @@
 """BASELINE.json configs at (or near) full size on one MI355X, checked against the oracle.
 
+* C1 (configs[0], the Quickstart shape): 1e7 points -- 80 % Gaussian mixture around
+  32 zone centres (sigma 0.005 deg), 20 % uniform, rounded to 1e-6 deg like the taxi GPS -- plus 0.1 %
+  adversarial points on the zones' vertices and edge midpoints, the 263 zones tessellated at H3 res
+  9: cells of every point, counts and pairs equal the oracle's; the WKT geometry column of the first
+  1e6 points gives the same cells (grid_pointascellid over pickup_geom, QuickstartNotebook.py:162-165).
 * C2 (configs[1], the bench workload): 1e9 uniform points over the NYC bbox, 263 zones at H3 res 9.
   Counts of the point-raster path (k_join_stream) equal those of the generic path (tile directory
   and point raster off: hash probe + per-chip rasters) on all 1e9 points, and the oracle's on a
@@ -45,6 +50,37 @@ def h3ctx():
 @pytest.fixture(scope="module")
 def zones():
     return PolygonSet.load("nyc_taxi_zones")
+
+
+def test_c1_quickstart_shape_vs_oracle(h3ctx, zones):
+    from mosaic_amd.data import quickstart_points
+
+    chips = h3ctx.grid_tessellateexplode(zones, 9)
+    table = h3ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
+                             n_polygons=len(zones))
+    x, y = quickstart_points(zones, 10_000_000, config=1)
+    # 0.1 %: zone vertices and edge midpoints (boundary points: JTS leaves them out of both zones)
+    rng = np.random.default_rng(1)
+    vi = rng.choice(len(zones.xy) - 1, 5_000, replace=False)
+    vx, vy = zones.xy[vi, 0], zones.xy[vi, 1]
+    mx, my = 0.5 * (zones.xy[vi, 0] + zones.xy[vi + 1, 0]), 0.5 * (zones.xy[vi, 1] + zones.xy[vi + 1, 1])
+    x = np.concatenate([x, vx, mx])
+    y = np.concatenate([y, vy, my])
+    perm = rng.permutation(len(x))
+    x, y = np.ascontiguousarray(x[perm]), np.ascontiguousarray(y[perm])
+    cells = h3ctx.grid_longlatascellid(x, y, 9, raw=True)
+    assert np.array_equal(cells, oracle.h3_point_to_index(x, y, 9))
+    oc = chips_to_oracle(chips)
+    want, total, orow, okey = oracle.pip_join(oc, oracle.GRID_H3, 9, x, y, len(zones), pairs=True, threads=16)
+    assert total > 8e6
+    assert np.array_equal(h3ctx.pip_join_count(table, x, y), want)
+    rows, keys = h3ctx.pip_join_pairs(table, x, y)
+    o = np.lexsort((okey, orow))
+    assert np.array_equal(rows, orow[o]) and np.array_equal(keys, okey[o])
+    m = 1_000_000
+    wkt = [f"POINT ({a!r} {b!r})" for a, b in zip(x[:m].tolist(), y[:m].tolist())]
+    assert np.array_equal(h3ctx.grid_pointascellid(wkt, 9, raw=True), cells[:m])
+    table.close()
 
 
 def test_c2_full_size_raster_vs_generic_vs_oracle(h3ctx, zones):

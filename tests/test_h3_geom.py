@@ -134,4 +134,22 @@ def test_gpu_h3_geometry_equals_oracle(host_geom):
         assert wkb[i] == struct.pack(">BIII", 0, 3, 1, len(ring)) + b"".join(struct.pack(">dd", x, y) for x, y in ring)
     with pytest.raises(MosaicError):
         h3.grid_boundaryaswkb([cells[0], 12345])
+    # mixed waves (tools/probes/early_exit: a bool decided inside a divergent loop was misread by
+    # lanes that left it early): 64 cells of every resolution with one digit-7 id at each lane in
+    # turn -- its lane leaves the digit check first -- must raise every time, and the valid batch
+    # must still equal the oracle
+    rng = np.random.default_rng(64)
+    lat, lon = np.degrees(np.arcsin(rng.uniform(-1, 1, 64))), rng.uniform(-180, 180, 64)
+    wave = [int(oracle.h3_point_to_index(lon[r:r + 1], lat[r:r + 1], 1 + r % 15)[0]) for r in range(64)]
+    for lane in range(64):
+        bad = list(wave)
+        c = bad[lane]
+        res = (c >> 52) & 15
+        bad[lane] = c | (7 << (3 * (15 - max(1, res // 2))))  # digit res / 2 (>= 1) set to 7
+        with pytest.raises(MosaicError):
+            h3.grid_cellcenter(bad)
+    cen = h3.grid_cellcenter(wave)
+    for i, c in enumerate(wave):
+        lat, lon = oracle.h3_to_geo(c)
+        assert (cen[i, 0], cen[i, 1]) == (deg(lon), deg(lat))
     h3.close()
