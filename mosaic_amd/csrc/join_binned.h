@@ -46,17 +46,16 @@ struct Buf {
 };
 
 struct Scratch {
-    Buf keys[2], vals[2], temp, n_skip, status, slots;
+    Buf keys[2], vals[2], temp, n_skip, status;
     JoinArgs exact_args;  // the join's arguments as the exact-H3 pass must read them (sorted points)
     int64_t sorted_rows = 0;  // rows the last join() sorted (after k_bin_cover's drops)
     int spin_cap = 1 << 20;   // k_bin_cover's look-back polls before it gives up (< 0: give up at once)
     int lookback_failed = 0;  // the last join() reran k_bin_cover uncompacted
     size_t held() const {
-        return keys[0].bytes + keys[1].bytes + vals[0].bytes + vals[1].bytes + temp.bytes + n_skip.bytes + status.bytes +
-               slots.bytes;
+        return keys[0].bytes + keys[1].bytes + vals[0].bytes + vals[1].bytes + temp.bytes + n_skip.bytes + status.bytes;
     }
     void release() {
-        for (Buf* b : {&keys[0], &keys[1], &vals[0], &vals[1], &temp, &n_skip, &status, &slots}) b->release();
+        for (Buf* b : {&keys[0], &keys[1], &vals[0], &vals[1], &temp, &n_skip, &status}) b->release();
     }
 };
 

@@ -359,74 +359,22 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
 MOSAIC_TJ_NOINLINE bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
     return pip::contains(s, c, x, y);
 }
-// ---- k_tile_slots: each sorted point's candidates for k_join_tiles, computed in a pass of their own
-// so the join kernel's registers hold no H3 arithmetic (with it inlined the join spilled 3.8 GB of
-// scratch per C4 launch at 128 VGPRs).  Per point one word: image runs -- the envelope-raster list
-// positions [c0, c1) of its cell and its hexagon's window slot (c0 | c1 << 16 | slot << 32; c0 == c1
-// when no envelope holds the point, or the point took the exact-H3 queue); runs without an image and
-// hexagons outside the window -- kSlotGlobal | first chip | end chip << 26 (chips of the table,
-// from tiled_cell or the probe).  Sorted order: consecutive points share their run's image and tile
-// record, so those reads stay in L1 / L2.
-static const uint64_t kSlotGlobal = 1ULL << 63;
-
-template <class P>
-__global__ void __launch_bounds__(256) k_tile_slots(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict__ pts,
-                                                    int64_t n, const unsigned long long* n_skip, binned::Images img,
-                                                    uint64_t* __restrict__ slots) {
-    const int64_t lo = (int64_t)*n_skip;
-    const int64_t step = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
-        const uint32_t code = keys[i];
-        const P p = pts[i];
-        const double x = p.x, y = p.y;
-        const uint32_t ioff = code >= 2 ? img.off[code - 2] : binned::kNoImage;
-        const uint32_t tcode = code >= 2 ? img.rec[code - 2] + 2u : code;
-        uint64_t w;
-        if (ioff == binned::kNoImage) {
-            uint32_t c0, c1;
-            tiled_cell(a, i, x, y, tcode, c0, c1);
-            w = kSlotGlobal | (uint64_t)c0 | (uint64_t)c1 << 26;
-        } else {
-            const uint32_t* im = img.words + ioff;
-            const uint16_t* rl = (const uint16_t*)(im + im[4]);
-            const int q = binned::bin_cell(a.tgrid, x, y).q;
-            uint32_t c0 = rl[q], c1 = rl[q + 1];
-            uint32_t slot = 0;
-            w = 0;
-            if (c1 > c0) {  // (a point no envelope holds joins nothing: its hexagon is not needed)
-                const tiles::TileRec tr = a.tile_rec[tcode - 2];
-                const int face = (int)(tr.dims & 0xffu);
-                const int wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
-                double px, py, pz, vx, vy, best;
-                h3::fast_unit(y, x, &px, &py, &pz);
-                h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
-                int ba, bb;
-                if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
-                    const unsigned long long qe = atomicAdd(a.amb_count, 1ULL);
-                    if (qe < a.amb_cap) a.amb_queue[qe] = (unsigned long long)i;
-                    c0 = c1 = 0;
-                } else {
-                    const int ra = ba - tr.a0, rb = bb - tr.b0;
-                    if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
-                        slot = (uint32_t)(ra * wb + rb);
-                    } else {
-                        uint32_t g0, g1;
-                        probe(a, (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res), g0, g1);
-                        w = kSlotGlobal | (uint64_t)g0 | (uint64_t)g1 << 26;
-                    }
-                }
-            }
-            if (!w) w = (uint64_t)c0 | (uint64_t)c1 << 16 | (uint64_t)slot << 32;
-        }
-        slots[i] = w;
-    }
+MOSAIC_TJ_NOINLINE uint2 tiled_cell_call(const JoinArgs& a, int64_t i, double x, double y, uint32_t code) {
+    uint32_t c0, c1;
+    tiled_cell(a, i, x, y, code, c0, c1);
+    return make_uint2(c0, c1);
+}
+MOSAIC_TJ_NOINLINE uint2 probe_call(const JoinArgs& a, int64_t cell) {
+    uint32_t c0, c1;
+    probe(a, cell, c0, c1);
+    return make_uint2(c0, c1);
 }
 
 // (occupancy 4: 128 VGPRs; C4 1e6 measured 23.4 ms against 28.7 unconstrained and 27.1 at 5)
 template <int CM, bool PAIRS, class P>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict__ pts, int64_t n,
-             const unsigned long long* n_skip, binned::Images img, uint32_t img_words, const uint64_t* __restrict__ slots) {
+             const unsigned long long* n_skip, binned::Images img, uint32_t img_words) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_t[];
     __shared__ uint32_t pairs_all[4 * 64];  // per wave: a window of (point lane, chip) pairs
     __shared__ double surv_x[4][kSurv], surv_y[4][kSurv];
@@ -460,15 +408,20 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
             if (found) break;
         }
         const int64_t r1 = (int64_t)run_end_s;
-        // the run's image key -> image
+        // the run's image key -> image, tile record (tcode: its tile code, for the generic path)
         const uint32_t ioff = code >= 2 ? img.off[code - 2] : binned::kNoImage;
+        const uint32_t tcode = code >= 2 ? img.rec[code - 2] + 2u : code;
+        tiles::TileRec tr{0, 0, 0, 0};
         if (ioff != binned::kNoImage) {
+            tr = a.tile_rec[tcode - 2];
             const uint32_t* src = img.words + ioff;
             const uint32_t nw = (src[3] + 2u * src[1] + 3u) & ~3u;  // vertex offset + vertex words (padded)
             for (uint32_t k = 4u * threadIdx.x; k < nw; k += 4u * blockDim.x)
                 *(uint4*)(im + k) = *(const uint4*)(src + k);
             __syncthreads();
         }
+        const int face = (int)(tr.dims & 0xffu);
+        const int wa = (int)((tr.dims >> 8) & 0xfffu), wb = (int)(tr.dims >> 20);
         const uint32_t* chips = im + im[2];
         const float* V = (const float*)(im + im[3]);
         const uint16_t* rl = (const uint16_t*)(im + im[4]);  // envelope raster: list offsets, lists
@@ -525,15 +478,37 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                 x = p.x;
                 y = p.y;
                 row = binned::row_of(p, i);
-                const uint64_t w = slots[i];  // (k_tile_slots)
-                glob = (w & kSlotGlobal) != 0;
-                if (glob) {
-                    c0 = (uint32_t)w & 0x3ffffffu;
-                    c1 = (uint32_t)(w >> 26) & 0x3ffffffu;
+                if (ioff == binned::kNoImage) {
+                    const uint2 r = tiled_cell_call(a, i, x, y, tcode);
+                    c0 = r.x;
+                    c1 = r.y;
+                    glob = true;
                 } else {
-                    c0 = (uint32_t)w & 0xffffu;
-                    c1 = (uint32_t)(w >> 16) & 0xffffu;
-                    slot = (uint32_t)(w >> 32) & 0xffffffu;
+                    // the raster cell (k_bin_cover's arithmetic): chips whose envelope may hold the point
+                    const int q = binned::bin_cell(a.tgrid, x, y).q;
+                    c0 = rl[q];
+                    c1 = rl[q + 1];
+                    if (c1 > c0) {  // (a point no envelope holds joins nothing: its hexagon is not needed)
+                        double px, py, pz, vx, vy, best;
+                        h3::fast_unit(y, x, &px, &py, &pz);
+                        h3::fast_plane(px, py, pz, face, a.res, &vx, &vy, &best);
+                        int ba, bb;
+                        if (!h3::fast_hex(vx, vy, a.res, &ba, &bb)) {
+                            const unsigned long long qe = atomicAdd(a.amb_count, 1ULL);
+                            if (qe < a.amb_cap) a.amb_queue[qe] = (unsigned long long)i;
+                            c0 = c1 = 0;
+                        } else {
+                            const int ra = ba - tr.a0, rb = bb - tr.b0;
+                            if ((unsigned)ra < (unsigned)wa && (unsigned)rb < (unsigned)wb) {
+                                slot = (uint32_t)(ra * wb + rb);
+                            } else {
+                                const uint2 r = probe_call(a, (int64_t)h3::face_axial_to_h3(face, ba, bb, a.res));
+                                c0 = r.x;
+                                c1 = r.y;
+                                glob = true;
+                            }
+                        }
+                    }
                 }
             }
             // the group's (point, chip) pairs, 64 at a time, one per lane: the work is spread over
@@ -742,19 +717,13 @@ static hipError_t sort_and_join(const JoinArgs& a0, int64_t lo, int64_t n, uint3
         const int gt = (int)std::max<int64_t>(1, (m + kSegPoints - 1) / kSegPoints);
         const size_t cw = pairs ? 0 : (cm == kCountLds ? (size_t)a.n_polygons : (size_t)binned::kImgMaxChips);
         const size_t shm = ((size_t)iw + cw) * 4;
-        if ((e = s.slots.reserve((size_t)std::max<int64_t>(m, 1) * 8))) return e;
-        uint64_t* sl = (uint64_t*)s.slots.p;
-        const int gsl = (int)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, (int64_t)n_cu * 16));
-        hipLaunchKernelGGL((k_tile_slots<P>), dim3(gsl), dim3(256), 0, stream, a, keys, pts, m, nsk, img, sl);
         if (pairs)
-            hipLaunchKernelGGL((k_join_tiles<kCountGlobal, true, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw,
-                               sl);
+            hipLaunchKernelGGL((k_join_tiles<kCountGlobal, true, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw);
         else if (cm == kCountLds)
-            hipLaunchKernelGGL((k_join_tiles<kCountLds, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw,
-                               sl);
+            hipLaunchKernelGGL((k_join_tiles<kCountLds, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk, img, iw);
         else
             hipLaunchKernelGGL((k_join_tiles<kCountChips, false, P>), dim3(gt), dim3(blk), shm, stream, a, keys, pts, m, nsk,
-                               img, iw, sl);
+                               img, iw);
     } else if (pairs) {
         hipLaunchKernelGGL((k_join_binned<kCountGlobal, true, P>), dim3(gj), dim3(blk), 0, stream, a, keys, pts, m, nsk);
     } else if (cm == kCountLds) {
