@@ -65,7 +65,7 @@ extern "C" {
 #endif
 
 /* 2: mosaic_chip_table_raster writes 8 values (was 5); option "exact_cap"; the aggregate geometry. */
-#define MOSAIC_ABI_VERSION 2
+#define MOSAIC_ABI_VERSION 3
 
 typedef enum {
     MOSAIC_OK = 0,
@@ -104,7 +104,10 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * raster over the tile directory, likewise), "raster_sub" / "raster_cell" (its sub-blocks per tile
  * side and leaf cells per sub-block side, powers of two, for tables built afterwards; default 64 /
  * 16), "raster_lines" (0/1: sub-blocks crossed by one straight chip edge store a line record instead
- * of a leaf block; default 1), "raster_build" (1: the point raster is classified on the GPU, the
+ * of a leaf block; default 1), "raster_leaf_lines" (0/1: leaf cells of the other mixed sub-blocks
+ * crossed by one straight chip edge store a line record too, answered by k_join_leaf before
+ * k_join_mixed; default 0), "leaf_join" (0/1: joins run k_join_leaf on the mixed queue; default 1),
+ * "raster_build" (1: the point raster is classified on the GPU, the
  * default; 0: on host threads -- identical bytes), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768
  * entries, or an entry budget <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of
  * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
@@ -284,8 +287,9 @@ int mosaic_chip_table_tile_grid(const mosaic_chips* chips, double* out4);
  * level entries (0: none), quad shift (sub-blocks per quad side = 1 << shift), raster bytes on the
  * device, 1 if joins run the stream kernel on it (quad level with compact copies, edges clamp-safe);
  * then the binned join's per-tile LDS chip images (option "tile_images"): records with an image,
- * image bytes on the device, bytes of the largest image. */
-int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out8);
+ * image bytes on the device, bytes of the largest image; leaf cells stored as line records (option
+ * "raster_leaf_lines"). */
+int mosaic_chip_table_raster(const mosaic_chips* chips, int64_t* out9);
 /* Build cost of the table in ms (ms4): chip hash + geometry + chip rasters, tile directory (host),
  * point-raster classification (GPU with option "raster_build" = 1, the default; host threads with
  * 0), point-raster assembly (host); *digest = FNV-1a 64 of the point raster's arrays (0: no raster),

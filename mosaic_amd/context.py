@@ -297,10 +297,11 @@ class ChipTable:
         g = np.zeros(4, np.float64)
         N.check(N.lib().mosaic_chip_table_tile_grid(self.handle, N.ptr(g)))
         d.update(x0=float(g[0]), y0=float(g[1]), sx=float(g[2]), sy=float(g[3]))
-        r = np.zeros(8, np.int64)
+        r = np.zeros(9, np.int64)
         N.check(N.lib().mosaic_chip_table_raster(self.handle, N.ptr(r)))
         d.update(line_sub_blocks=int(r[0]), quad_entries=int(r[1]), quad_shift=int(r[2]), raster_bytes=int(r[3]),
-                 stream=int(r[4]), image_records=int(r[5]), image_bytes=int(r[6]), image_max_bytes=int(r[7]))
+                 stream=int(r[4]), image_records=int(r[5]), image_bytes=int(r[6]), image_max_bytes=int(r[7]),
+                 leaf_lines=int(r[8]))
         return d
 
     def build_info(self):

@@ -292,4 +292,6 @@ struct BngStreamArgs {
 // The stream kernels (join_stream.hip), by template arguments: the host picks one and launches it
 // with hipLaunchKernel.  pipe: k_join_stream_pipe (needs vec); else k_join_stream<lds, pairs, vec>.
 const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec);
+// k_join_leaf<lds, pairs> (join_stream.hip): the mixed queue's leaf-line rows, before k_join_mixed
+const void* leaf_kernel(bool lds, bool pairs);
 const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool cpt);  // cpt: k_join_stream_bng_cpt (needs vec)

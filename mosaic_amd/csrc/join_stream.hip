@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
             lc = sv <= -1.0f ? neg : lc;
             uint32_t c = line[k] ? lc : (blk[k] ? leaf[k] : code[k]);
-            c = fin[k] ? c : (uint32_t)tiles::kMixed;
+            c = fin[k] && c < 0x8000u ? c : (uint32_t)tiles::kMixed;  // (leaf lines: the mixed kernel)
             code[k] = live[k] ? c : 0u;
         }
         // counts: one LDS add per point (points without a pair add to the lane's spill word)
@@ -1108,6 +1108,86 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
             if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
     }
+}
+
+// ---- k_join_leaf: the mixed queue's rows whose leaf cell is a leaf line (tiles.h leaf_is_line: the
+// cell is split by one straight chip edge) are answered from the line record; the others -- the
+// line's band, mixed leaf cells, line sub-blocks' bands, non-finite rows -- move to queue q2, which
+// k_join_mixed then takes.  One lane per row: tiles::raster_code_fixed's chain from global memory
+// (quad level, quad record, compact sub-block entry, tile base, leaf code, line record), the same
+// fine cell and line offsets as the stream kernels.  ~95 % of NYC res-9 mixed leaf cells are leaf
+// lines (tools/raster_stats.cpp), so the mixed kernel's H3 cell + chip loop runs on ~1/5 of the rows.
+template <bool LDS_COUNTS, bool PAIRS>
+__global__ void __launch_bounds__(256) k_join_leaf(JoinArgs a, StreamArgs s, uint32_t* q2, unsigned long long* q2_count) {
+    extern __shared__ unsigned int lds[];
+    if (LDS_COUNTS) {
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x) lds[k] = 0;
+        __syncthreads();
+    }
+    constexpr int F = tiles::kFixBits;
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const uint16_t* quad = (const uint16_t*)s.quad;
+    const uint32_t* qmask = s.qrec;
+    const uint16_t* qcode = (const uint16_t*)(s.qrec + 2 * s.n_qrec);
+    const uint32_t cs = (uint32_t)s.cs, qs = (uint32_t)s.qs, cm = (1u << cs) - 1u, qm = (1u << qs) - 1u;
+    const unsigned long long total = *a.mixq_count;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    // wave-uniform loop (the q2 append is a wave ballot)
+    for (unsigned long long t0 = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); t0 < total; t0 += stride) {
+        const unsigned long long t = t0 + (unsigned long long)lane;
+        const bool live = t < total;
+        const uint32_t off = live ? a.mixq[t] : 0u;
+        const int64_t row = a.row_lo + (int64_t)off;
+        uint32_t code = tiles::kMixed;
+        if (live) {
+            const double x = a.x[row], y = a.y[row];
+            if (isfinite(x + y)) {
+                const uint32_t gix = min(tiles::fix_cvt(fma(x, s.sxF, s.gx0F)), (uint32_t)s.gxmaxF);
+                const uint32_t giy = min(tiles::fix_cvt(fma(y, s.syF, s.gy0F)), (uint32_t)s.gymaxF);
+                const uint32_t ixC = gix >> F, iyC = giy >> F, ix = ixC >> cs, iy = iyC >> cs;
+                const uint32_t q = quad_lookup<F>(s, quad, qmask, qcode, gix, giy);
+                const uint32_t e = q < 0x8000u ? q : s.csub[((q & 0x7fffu) << (2 * qs)) + (((iy & qm) << qs) | (ix & qm))];
+                code = e;
+                if (tiles::sub_is_block(e) && !(e & tiles::kLineBit)) {
+                    const uint32_t base = s.tile_base[(iyC >> s.tsh) * (uint32_t)s.tnx + (ixC >> s.tsh)];
+                    const uint32_t lc = s.blocks[base + ((e & 0x3fffu) << (2 * cs)) + (((iyC & cm) << cs) | (ixC & cm))];
+                    code = lc;
+                    if (tiles::leaf_is_line(lc)) {
+                        const tiles::LineRec lr = *(const tiles::LineRec*)(s.blocks + base - 8u * ((lc & 0x3fffu) + 1u));
+                        const uint32_t fm = (1u << (cs + F)) - 1u;
+                        const float sc = 1.0f / (float)(1 << F);
+                        code = tiles::line_code(lr, (float)(gix & fm) * sc, (float)(giy & fm) * sc);
+                    }
+                } else if (tiles::sub_is_block(e)) {
+                    code = tiles::kMixed;  // a line sub-block's band (the stream kernel's answer)
+                }
+            }
+        }
+        const bool keep = live && code >= 0x8000u;  // kMixed (or a code the chain cannot decide)
+        if (live && !keep && code != 0u) {
+            if (LDS_COUNTS && !PAIRS) atomicAdd(&lds[code - 1u], 1u);
+            else emit_hit<LDS_COUNTS, PAIRS>(a, row, code - 1u, lds);
+        }
+        const unsigned long long km = __ballot(keep);
+        if (km) {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(q2_count, (unsigned long long)__popcll(km));
+            base = __shfl(base, 0, 64);
+            if (keep) q2[base + __popcll(km & lt_mask)] = off;
+        }
+    }
+    if (LDS_COUNTS) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)
+            if (lds[k]) atomicAdd(&a.counts[k], (unsigned long long)lds[k]);
+    }
+}
+
+const void* leaf_kernel(bool lds, bool pairs) {
+    if (pairs) return (const void*)k_join_leaf<false, true>;
+    if (lds) return (const void*)k_join_leaf<true, false>;
+    return (const void*)k_join_leaf<false, false>;
 }
 
 const void* stream_kernel_h3(int pipe, bool lds, bool pairs, bool vec) {

@@ -532,8 +532,11 @@ __device__ inline int rhex_answer_wave(const RBuildArgs& a, const RTile& t, int 
     return cnt;
 }
 
+// (qc, ctol): for a leaf line, the leaf cell's corner images and tolerance -- the candidates are then
+// those of the cell (tiles_build.cpp classify's cand2), as try_line's cin
 __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* uv,
-                                               int n, const rbuild::P2* sq, double stol) {
+                                               int n, const rbuild::P2* sq, double stol, const rbuild::P2* qc = nullptr,
+                                               double ctol = 0.0) {
     using rbuild::dmax;
     using rbuild::dmin;
     rbuild::P2 img[8], ll[8];
@@ -567,7 +570,8 @@ __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile&
         bool is_c = false;
         if (kl < W) {
             const rbuild::P2 c = rhex_centre(t, kl);
-            is_c = rbuild::poly_meets_hex(sq, 4, c, stol, a.ht) && rbuild::poly_meets_hex(img, n, c, tol, a.ht);
+            is_c = rbuild::poly_meets_hex(sq, 4, c, stol, a.ht) && (!qc || rbuild::poly_meets_hex(qc, 4, c, ctol, a.ht)) &&
+                   rbuild::poly_meets_hex(img, n, c, tol, a.ht);
         }
         for (unsigned long long mask = __ballot(is_c); mask; mask &= mask - 1) {
             const int k = k0 + __builtin_ctzll(mask);
@@ -587,13 +591,19 @@ __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile&
     return acnt == 0 ? (uint16_t)0 : (uint16_t)(akey + 1);
 }
 
+// tiles_build.cpp try_line() over the box [u0, u1] x [v0, v1] (sub-block units; the whole sub-block
+// or, for a leaf line, one leaf cell whose corner images and tolerance are qc, ctol), margins
+// 0 .. mk_end - 1
 __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* sq,
-                                      double stol, tiles::LineRec& out) {
+                                      double stol, tiles::LineRec& out, double u0 = 0.0, double v0 = 0.0,
+                                      double u1 = 1.0, double v1 = 1.0, int mk_end = 4, const rbuild::P2* qc = nullptr,
+                                      double ctol = 0.0) {
     const int S = a.S, lane = (int)(threadIdx.x & 63);
     const double wR = a.tw / S, hR = a.th / S;
     const double lonR0 = t.lon0 + a.tw * si / S, latR0 = t.lat0 + a.th * sj / S;
     const double exu = t.exd / wR, eyv = t.eyd / hR;
-    const double bx0 = lonR0 - t.exd, bx1 = lonR0 + wR + t.exd, by0 = latR0 - t.eyd, by1 = latR0 + hR + t.eyd;
+    const double bx0 = lonR0 + wR * u0 - t.exd, bx1 = lonR0 + wR * u1 + t.exd, by0 = latR0 + hR * v0 - t.eyd,
+                 by1 = latR0 + hR * v1 + t.eyd;
     // pass 0: this lane's longest clipped segment (first in (hexagon, vertex) order on ties); pass
     // 1: this lane's largest deviation; then wave reductions
     double best = 0.0, dev_max = 0.0, la = 0.0, lb = 0.0, lc = 0.0;
@@ -605,7 +615,8 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
         for (int k0 = 0; k0 < W; k0 += 64) {
         const int kl = k0 + lane;
         const bool is_c = kl < W && a.entries[t.off + (uint32_t)kl] &&
-                          rbuild::poly_meets_hex(sq, 4, rhex_centre(t, kl), stol, a.ht);
+                          rbuild::poly_meets_hex(sq, 4, rhex_centre(t, kl), stol, a.ht) &&
+                          (!qc || rbuild::poly_meets_hex(qc, 4, rhex_centre(t, kl), ctol, a.ht));
         for (unsigned long long mask = __ballot(is_c); mask; mask &= mask - 1) {
             const int k = k0 + __builtin_ctzll(mask);
             const uint32_t e = a.entries[t.off + (uint32_t)k];
@@ -621,7 +632,7 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
                             const pip::Vec2 s0 = a.store.verts[v - 1], s1 = a.store.verts[v];
                             double ax = (s0.x - lonR0) / wR, ay = (s0.y - latR0) / hR;
                             double qx = (s1.x - lonR0) / wR, qy = (s1.y - latR0) / hR;
-                            if (!rbuild::clip_seg(ax, ay, qx, qy, -exu, -eyv, 1.0 + exu, 1.0 + eyv)) continue;
+                            if (!rbuild::clip_seg(ax, ay, qx, qy, u0 - exu, v0 - eyv, u1 + exu, v1 + eyv)) continue;
                             if (pass == 0) {
                                 const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
                                 if (l2 > best) {  // a lane's segments come in increasing order
@@ -665,8 +676,8 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
         }
     }
     dev_max = wave_max_f64(dev_max);
-    const rbuild::P2 sqb[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
-    for (int mk = 0; mk < 4; mk++) {
+    const rbuild::P2 sqb[4] = {{u0 - exu, v0 - eyv}, {u1 + exu, v0 - eyv}, {u1 + exu, v1 + eyv}, {u0 - exu, v1 + eyv}};
+    for (int mk = 0; mk < mk_end; mk++) {
         const double margin = rbuild::line_margin(mk);
         if (dev_max > margin - 2.0 * tiles::kLineSlack) continue;
         out.a = (float)(la / margin);
@@ -675,9 +686,9 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
         const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - tiles::kLineSlack / margin;
         rbuild::P2 hp[8], hn[8];
         const int np = rbuild::clip_half(sqb, 4, A, B, Cf - m, hp), nn = rbuild::clip_half(sqb, 4, -A, -B, -Cf - m, hn);
-        const uint16_t cp = np >= 3 ? rclassify_poly_wave(a, t, si, sj, hp, np, sq, stol) : (uint16_t)0;
+        const uint16_t cp = np >= 3 ? rclassify_poly_wave(a, t, si, sj, hp, np, sq, stol, qc, ctol) : (uint16_t)0;
         if (cp == tiles::kMixed) continue;
-        const uint16_t cn = nn >= 3 ? rclassify_poly_wave(a, t, si, sj, hn, nn, sq, stol) : (uint16_t)0;
+        const uint16_t cn = nn >= 3 ? rclassify_poly_wave(a, t, si, sj, hn, nn, sq, stol, qc, ctol) : (uint16_t)0;
         if (cn == tiles::kMixed) continue;
         out.pos = cp;
         out.neg = cn;
@@ -730,6 +741,47 @@ __global__ void __launch_bounds__(256) k_raster_cells(RBuildArgs a) {
         a.cells[w] = code;
     }
 }
+
+// Leaf lines (tiles_build.cpp, the cell loop of classify_raster_host): one wave per kMixed leaf
+// cell (mlist: its index in `cells`, ascending), the line fit of k_raster_line_wave over the cell's
+// box with the cell's candidates; ok[m] = 1 and out[m] = the record when one certifies.
+__global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const uint32_t* mlist, int64_t n_ml,
+                                                           uint8_t* ok, tiles::LineRec* out) {
+    const int64_t m = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (m >= n_ml) return;
+    const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
+    const int64_t w = mlist[m];
+    const int64_t msb = w / CC;
+    const int cc = (int)(w - msb * CC), cj = cc / a.C, ci = cc - cj * a.C;
+    const int64_t g = a.cell_sb[msb];
+    const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
+    RTile t;
+    tiles::LineRec lr{0, 0, 0, 0, 0};
+    bool found = false;
+    if (rtile_of(a, r, t)) {
+        rbuild::P2 sq[4];
+        const double stol = rsub_quad(a, t, si, sj, sq);
+        const int i0 = si * a.C + ci, j0 = sj * a.C + cj;
+        const rbuild::P2 qc[4] = {rimage(a, t, i0, j0), rimage(a, t, i0 + 1, j0), rimage(a, t, i0 + 1, j0 + 1),
+                                  rimage(a, t, i0, j0 + 1)};
+        // the cell's tolerance as rclassify_rect computes it (tiles_build.cpp classify)
+        const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
+        const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
+        const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
+        const double ctol = tiles::rect_tol(t.cv, cell_deg_x * 1, cell_deg_y * 1, rbuild::dmax(ex, ey));
+        found = rtry_line_wave(a, t, si, sj, sq, stol, lr, (double)ci / a.C, (double)cj / a.C, (double)(ci + 1) / a.C,
+                               (double)(cj + 1) / a.C, tiles::kLeafLineMargins, qc, ctol);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ok[m] = found ? 1 : 0;
+        out[m] = found ? lr : tiles::LineRec{0, 0, 0, 0, 0};
+    }
+}
+
+struct RasterMixedCell {  // hipcub select predicate: leaf cell w is kMixed
+    const uint16_t* cells;
+    __host__ __device__ bool operator()(uint32_t w) const { return cells[w] == tiles::kMixed; }
+};
 
 // ---- st_intersects_aggregate over the chip join of two chip tables ----------------------------
 // ST_IntersectsAggregate.update (expressions/geometry/ST_IntersectsAggregate.scala:28-39) folds
@@ -1635,6 +1687,58 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging for the table build's host <-> device copies (h2d / d2h below).  A copy
+// from or to pageable memory of a megabyte or more makes the HIP runtime pin that memory (a
+// user-pointer registration with the kernel driver); when the range is later invalidated -- the
+// vector freed, its pages moved or collapsed into a huge page -- the driver evicts every queue of
+// the process, restores them tens of ms later, and whatever kernel was running stretches by that
+// much.  Measured: the raster classification kernels' active cycles identical in every build
+// (GRBM_GUI_ACTIVE, profiles/r05_build_var_pmc/), their wall time 6 ms in a process's first build
+// and 32-42 ms in later ones, the 5 MB k_raster_sub copy 3 -> 30 ms.  Two 8 MB buffers allocated
+// once per thread state, used in turn (an event per buffer), so no build copy touches pageable
+// memory on the device side.
+struct HostStage {
+    static const size_t kBytes = (size_t)8 << 20;
+    void* p[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    int next = 0;  // the buffer the next chunk takes
+    int ensure() {
+        if (p[0]) return MOSAIC_OK;
+        for (int k = 0; k < 2; k++) {
+            if (hipHostMalloc(&p[k], kBytes, hipHostMallocDefault) != hipSuccess) {
+                p[k] = nullptr;
+                release();
+                return fail(MOSAIC_E_NOMEM, "hipHostMalloc(staging) failed");
+            }
+            if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+                ev[k] = nullptr;
+                release();
+                return fail(MOSAIC_E_HIP, "hipEventCreate(staging) failed");
+            }
+        }
+        return MOSAIC_OK;
+    }
+    // wait until buffer k's last copy has finished
+    int wait(int k) {
+        if (busy[k]) {
+            busy[k] = false;
+            if (hipEventSynchronize(ev[k]) != hipSuccess) return fail(MOSAIC_E_HIP, "staging event");
+        }
+        return MOSAIC_OK;
+    }
+    void release() {
+        for (int k = 0; k < 2; k++) {
+            if (busy[k] && ev[k]) (void)hipEventSynchronize(ev[k]);
+            busy[k] = false;
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
+            if (p[k]) (void)hipHostFree(p[k]);
+            ev[k] = nullptr;
+            p[k] = nullptr;
+        }
+    }
+};
+
 // Scope guards of entry points: staged buffers and timing events are released
 // on every return path (errors after allocation included)
 struct DevBufGuard {
@@ -1668,6 +1772,8 @@ struct Options {
     int raster_cell = 16;     // point raster: leaf cells per sub-block side (a power of two)
     int raster_quad = 1;      // point raster: LDS quad level
     int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
+    int raster_leaf_lines = 0;  // point raster: line records for single-edge leaf cells (leaf lines)
+    int leaf_join = 1;        // k_join_leaf answers the mixed queue's leaf-line rows before k_join_mixed
     int raster_build = 1;     // point raster classification: 1 on the GPU (k_raster_*), 0 on host threads
     int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
@@ -1711,9 +1817,10 @@ struct ThreadCtx : Options {
     const char* last_kernel = "";      // the dominant kernel of the last join call (mosaic_last_kernel)
     double last_tess_classify_ms = 0;  // classification kernel (k_bng_tess_classify / k_tess_classify_poly) of the
                                        // last mosaic_tessellate_gpu; 0 when it had no candidates
-    DevBuf amb_queue, mix_queue, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
+    DevBuf amb_queue, mix_queue, mix_queue2, scalars, stage_x, stage_y, stage_v, stage_out, stage_out2, stage_idx;
     DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
     DevBuf ov[8];  // st_intersection_aggregate's cell overlay (run_unit_overlay)
+    HostStage hstage;  // pinned staging of the table build's copies (h2d / d2h)
     hipStream_t copy_stream = nullptr;
     DevBuf hx[2], hy[2], hcounts;
     binned::Scratch bins;  // the binned join's keys, sorted points and sort temp
@@ -1725,7 +1832,7 @@ struct ThreadCtx : Options {
     size_t ev_used = 0;
     // the scratch buffers sized by the calls (not `scalars`, which every call needs)
     std::vector<DevBuf*> scratch() {
-        return {&amb_queue, &mix_queue, &stage_x, &stage_y, &stage_v, &stage_out, &stage_out2, &stage_idx, &geo_off,
+        return {&amb_queue, &mix_queue, &mix_queue2, &stage_x, &stage_y, &stage_v, &stage_out, &stage_out2, &stage_idx, &geo_off,
                 &geo_data, &dec_x, &dec_y, &dec_status, &hx[0], &hx[1], &hy[0], &hy[1], &hcounts,
                 &ov[0], &ov[1], &ov[2], &ov[3], &ov[4], &ov[5], &ov[6], &ov[7]};
     }
@@ -1749,6 +1856,7 @@ struct ThreadCtx : Options {
         for (DevBuf* b : scratch()) b->release();
         bins.release();
         scalars.release();
+        hstage.release();
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         for (size_t i = 0; i < ev_start.size(); i++) {
             (void)hipEventDestroy(ev_start[i]);
@@ -1773,7 +1881,7 @@ struct mosaic_ctx {
 
 // join scalars: [0] exact-queue rows, [1] pairs, [2] contains tests, [3] flags, [4] mixed-queue rows,
 // [5] exact rows summed over the binned join's chunks, [6] a binned chunk overflowed the exact queue
-static const int kScalars = 7;
+static const int kScalars = 8;  // [7]: k_join_leaf's second queue count
 // the join's counts and scalars zeroed by one launch (two hipMemsetAsync calls of odd sizes took four
 // fill kernels, ~20 us per call on the stream)
 __global__ void __launch_bounds__(256) k_zero_join(unsigned long long* counts, int64_t n_counts, unsigned long long* scalars) {
@@ -1896,6 +2004,8 @@ static int timing_begin(ThreadCtx* c, hipEvent_t* stop_out) {
     return MOSAIC_OK;
 }
 
+static int h2d(ThreadCtx* c, void* dst, const void* src, size_t n);
+
 struct GeomStoreDev {
     DevBuf verts, ring_start, ring_bbox, part_ring, geom_part, geom_bbox;
     pip::GeomStore view() const {
@@ -1908,11 +2018,11 @@ struct GeomStoreDev {
         s.geom_bbox = (const pip::Box*)geom_bbox.p;
         return s;
     }
-    int upload(const GeomBuilder& b, hipStream_t st, size_t* total) {
+    int upload(const GeomBuilder& b, ThreadCtx* c, size_t* total) {
         auto up = [&](DevBuf& d, const void* src, size_t bytes) -> int {
             int rc = d.reserve(std::max<size_t>(bytes, 16));
             if (rc) return rc;
-            if (bytes) HIP_TRY(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, st));
+            if ((rc = h2d(c, d.p, src, bytes))) return rc;
             *total += bytes;
             return MOSAIC_OK;
         };
@@ -1923,7 +2033,7 @@ struct GeomStoreDev {
         if ((rc = up(part_ring, b.part_ring.data(), b.part_ring.size() * 4))) return rc;
         if ((rc = up(geom_part, b.geom_part.data(), b.geom_part.size() * 4))) return rc;
         if ((rc = up(geom_bbox, b.geom_bbox.data(), b.geom_bbox.size() * sizeof(pip::Box)))) return rc;
-        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipStreamSynchronize(c->stream));
         return MOSAIC_OK;
     }
     void release() {
@@ -1968,8 +2078,8 @@ struct mosaic_chips {
     uint32_t img_max_words = 0;
     int64_t img_records = 0;  // images built (parts of tile records; tile_images.h)
     int64_t img_count = 0;    // image keys (with the parts that have no image)
-    int64_t raster_stats[6] = {0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
-                                                   // line sub-blocks
+    int64_t raster_stats[7] = {0, 0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
+                                                      // line sub-blocks, leaf lines
     // build cost (ms): chip table core (hash, geometry, chip rasters), tile directory, point-raster
     // classification (GPU or host), point-raster assembly; FNV-1a digest of the point raster
     double build_ms[4] = {0, 0, 0, 0};
@@ -2068,6 +2178,60 @@ __global__ void __launch_bounds__(256) k_warm_up(unsigned long long ticks) {
     }
 }
 
+// Host -> device through the pinned staging buffers, ordered on c->stream: `src` may be freed or
+// reused as soon as this returns (its bytes are in a staging buffer or already copied).
+static int h2d(ThreadCtx* c, void* dst, const void* src, size_t n) {
+    if (!n) return MOSAIC_OK;
+    HostStage& h = c->hstage;
+    int e;
+    if ((e = h.ensure())) return e;
+    for (size_t off = 0; off < n; off += HostStage::kBytes) {
+        const size_t m = std::min(HostStage::kBytes, n - off);
+        const int k = h.next;
+        h.next ^= 1;
+        if ((e = h.wait(k))) return e;
+        memcpy(h.p[k], (const char*)src + off, m);
+        HIP_TRY(hipMemcpyAsync((char*)dst + off, h.p[k], m, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(h.ev[k], c->stream));
+        h.busy[k] = true;
+    }
+    return MOSAIC_OK;
+}
+
+// Device -> host through the pinned staging buffers after the work queued on c->stream; returns
+// when `dst` holds the bytes.  Chunk i + 1's copy runs while chunk i is copied out on the host.
+static int d2h(ThreadCtx* c, void* dst, const void* src, size_t n) {
+    if (!n) return MOSAIC_OK;
+    HostStage& h = c->hstage;
+    int e;
+    if ((e = h.ensure())) return e;
+    int pk = -1;
+    size_t poff = 0, pm = 0;
+    for (size_t off = 0;; off += HostStage::kBytes) {
+        const bool more = off < n;
+        int k = -1;
+        size_t m = 0;
+        if (more) {
+            m = std::min(HostStage::kBytes, n - off);
+            k = h.next;
+            h.next ^= 1;
+            if ((e = h.wait(k))) return e;
+            HIP_TRY(hipMemcpyAsync(h.p[k], (const char*)src + off, m, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipEventRecord(h.ev[k], c->stream));
+            h.busy[k] = true;
+        }
+        if (pk >= 0) {
+            if ((e = h.wait(pk))) return e;
+            memcpy((char*)dst + poff, h.p[pk], pm);
+        }
+        if (!more) break;
+        pk = k;
+        poff = off;
+        pm = m;
+    }
+    return MOSAIC_OK;
+}
+
 // On the creating thread's own stream (never the null stream: context creation must not wait for
 // other contexts' or torch's queued work); MOSAIC_NO_WARMUP=1 in the environment skips it.
 static void warm_up(ThreadCtx* t) {
@@ -2078,6 +2242,7 @@ static void warm_up(ThreadCtx* t) {
     if (hipMalloc(&d, bytes) != hipSuccess) return;
     std::vector<uint8_t> h(bytes, 0);
     (void)hipMemcpyAsync(d, h.data(), bytes, hipMemcpyHostToDevice, t->stream);
+    (void)h2d(t, d, h.data(), bytes);  // (allocates the build's pinned staging)
     hipLaunchKernelGGL(k_warm_up, dim3((unsigned)std::max(1, t->n_cu * 4)), dim3(256), 0, t->stream, 300000ULL);
     (void)hipGetLastError();
     (void)hipStreamSynchronize(t->stream);
@@ -2207,6 +2372,10 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.raster_min_segments = (int)v;
     } else if (k == "raster_lines") {
         o.raster_lines = v ? 1 : 0;
+    } else if (k == "raster_leaf_lines") {
+        o.raster_leaf_lines = v ? 1 : 0;
+    } else if (k == "leaf_join") {
+        o.leaf_join = v ? 1 : 0;
     } else if (k == "raster_quad_records") {
         o.raster_quad_records = v ? 1 : 0;
     } else if (k == "raster_build") {
@@ -2862,9 +3031,9 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     if ((e = d_tor.reserve(std::max<size_t>(n_recs * 4, 16))) || (e = d_dev.reserve(std::max<size_t>(n_recs * sizeof(tiles::TileCurv), 16))) ||
         (e = d_code.reserve(std::max<size_t>((size_t)n_sub * 2, 16))))
         return e;
-    HIP_TRY(hipMemcpyAsync(d_tor.p, tb.tile_of_rec.data(), n_recs * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_dev.p, tb.rec_curv.data(), n_recs * sizeof(tiles::TileCurv), hipMemcpyHostToDevice,
-                           c->stream));
+    if ((e = h2d(c, d_tor.p, tb.tile_of_rec.data(), n_recs * 4)) ||
+        (e = h2d(c, d_dev.p, tb.rec_curv.data(), n_recs * sizeof(tiles::TileCurv))))
+        return e;
     RBuildArgs a{};
     a.recs = (const tiles::TileRec*)ch->tile_rec.p;
     a.tile_of_rec = (const int32_t*)d_tor.p;
@@ -2892,8 +3061,7 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     if (n_sub) {
         hipLaunchKernelGGL(k_raster_sub, grid_of(n_sub), dim3(256), 0, c->stream, a);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(rc.code.data(), d_code.p, (size_t)n_sub * 2, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((e = d2h(c, rc.code.data(), d_code.p, (size_t)n_sub * 2))) return e;
     }
     trace.mark("  k_raster_sub + copy");
     // mixed sub-blocks in record, then scan order (the order assemble_raster consumes them)
@@ -2909,7 +3077,7 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     if ((e = d_list.reserve(list.size() * 4)) || (e = d_kind.reserve(list.size())) ||
         (e = d_line.reserve(list.size() * sizeof(tiles::LineRec))))
         return e;
-    HIP_TRY(hipMemcpyAsync(d_list.p, list.data(), list.size() * 4, hipMemcpyHostToDevice, c->stream));
+    if ((e = h2d(c, d_list.p, list.data(), list.size() * 4))) return e;
     a.mixed = (const uint32_t*)d_list.p;
     a.n_mixed = n_mixed;
     a.kind = (uint8_t*)d_kind.p;
@@ -2919,10 +3087,9 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     else  // one wave per sub-block
         hipLaunchKernelGGL(k_raster_line_wave, dim3((unsigned)((n_mixed + 3) / 4)), dim3(256), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(rc.kind.data(), d_kind.p, list.size(), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(rc.line.data(), d_line.p, list.size() * sizeof(tiles::LineRec), hipMemcpyDeviceToHost,
-                           c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((e = d2h(c, rc.kind.data(), d_kind.p, list.size())) ||
+        (e = d2h(c, rc.line.data(), d_line.p, list.size() * sizeof(tiles::LineRec))))
+        return e;
     trace.mark("  mixed list + line kernel");
     // the other mixed sub-blocks: C x C leaf cells each
     std::vector<uint32_t> cell_sb;
@@ -2934,7 +3101,7 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     if (cell_sb.empty()) return MOSAIC_OK;
     const int64_t n_cells = (int64_t)(cell_sb.size() * CC);
     if ((e = d_cells.reserve((size_t)n_cells * 2))) return e;
-    HIP_TRY(hipMemcpyAsync(d_list.p, cell_sb.data(), cell_sb.size() * 4, hipMemcpyHostToDevice, c->stream));
+    if ((e = h2d(c, d_list.p, cell_sb.data(), cell_sb.size() * 4))) return e;
     a.cell_sb = (const uint32_t*)d_list.p;
     a.n_cell_sb = (int64_t)cell_sb.size();
     a.cells = (uint16_t*)d_cells.p;
@@ -2944,9 +3111,40 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     HIP_TRY(hipGetLastError());
     rc.cells.resize((size_t)n_cells);
     prefault(rc.cells.data(), rc.cells.size() * 2);
-    HIP_TRY(hipMemcpyAsync(rc.cells.data(), d_cells.p, (size_t)n_cells * 2, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((e = d2h(c, rc.cells.data(), d_cells.p, (size_t)n_cells * 2))) return e;
     trace.mark("  k_raster_cells + copy");
+    rc.cline_at.clear();
+    rc.cline.clear();
+    if (!tb.leaf_lines) return MOSAIC_OK;
+    // leaf lines: the kMixed cells in index order (hipcub select), one line fit per cell
+    TmpBuf d_ml, d_nml, d_tmp, d_ok, d_lrec;
+    if ((e = d_ml.reserve((size_t)n_cells * 4)) || (e = d_nml.reserve(8))) return e;
+    hipcub::CountingInputIterator<uint32_t> idx(0u);
+    size_t tmp_bytes = 0;
+    HIP_TRY(hipcub::DeviceSelect::If(nullptr, tmp_bytes, idx, (uint32_t*)d_ml.p, (int64_t*)d_nml.p, n_cells,
+                                     RasterMixedCell{(const uint16_t*)d_cells.p}, c->stream));
+    if ((e = d_tmp.reserve(std::max<size_t>(tmp_bytes, 16)))) return e;
+    HIP_TRY(hipcub::DeviceSelect::If(d_tmp.p, tmp_bytes, idx, (uint32_t*)d_ml.p, (int64_t*)d_nml.p, n_cells,
+                                     RasterMixedCell{(const uint16_t*)d_cells.p}, c->stream));
+    int64_t n_ml = 0;
+    if ((e = d2h(c, &n_ml, d_nml.p, 8))) return e;
+    if (n_ml <= 0) return MOSAIC_OK;
+    if ((e = d_ok.reserve((size_t)n_ml)) || (e = d_lrec.reserve((size_t)n_ml * sizeof(tiles::LineRec)))) return e;
+    hipLaunchKernelGGL(k_raster_cell_lines, dim3((unsigned)((n_ml + 3) / 4)), dim3(256), 0, c->stream, a,
+                       (const uint32_t*)d_ml.p, n_ml, (uint8_t*)d_ok.p, (tiles::LineRec*)d_lrec.p);
+    HIP_TRY(hipGetLastError());
+    std::vector<uint32_t> ml((size_t)n_ml);
+    std::vector<uint8_t> okv((size_t)n_ml);
+    std::vector<tiles::LineRec> lrec((size_t)n_ml);
+    if ((e = d2h(c, okv.data(), d_ok.p, (size_t)n_ml)) || (e = d2h(c, ml.data(), d_ml.p, (size_t)n_ml * 4)) ||
+        (e = d2h(c, lrec.data(), d_lrec.p, (size_t)n_ml * sizeof(tiles::LineRec))))
+        return e;
+    for (int64_t m = 0; m < n_ml; m++)
+        if (okv[(size_t)m]) {
+            rc.cline_at.push_back(ml[(size_t)m]);
+            rc.cline.push_back(lrec[(size_t)m]);
+        }
+    trace.mark("  leaf lines");
     return MOSAIC_OK;
 }
 
@@ -3197,13 +3395,14 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
     size_t total = 0;
     int rc;
     if ((rc = ch->table.reserve(capacity * sizeof(HashEntry))) || (rc = ch->meta.reserve(meta.size() * 4)) ||
-        (rc = ch->store.upload(gb, c->stream, &total))) {
+        (rc = ch->store.upload(gb, c, &total))) {
         ch->release_all();
         delete ch;
         return rc;
     }
-    HIP_TRY(hipMemcpy(ch->table.p, table.data(), capacity * sizeof(HashEntry), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ch->meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
+    if ((rc = h2d(c, ch->table.p, table.data(), capacity * sizeof(HashEntry))) ||
+        (rc = h2d(c, ch->meta.p, meta.data(), meta.size() * 4)))
+        return rc;
     // the chip rasters: joined here when the build has no point raster to classify, else after it
     bool rb_uploaded = false;
     auto upload_chip_rasters = [&]() -> int {
@@ -3220,9 +3419,10 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             (e = ch->cells.reserve(rb.cells.size() * sizeof(raster::CellRec))) ||
             (e = ch->rast_edges.reserve(rb.edges.size() * sizeof(pip::Edge))))
             return e;
-        HIP_TRY(hipMemcpy(ch->hdr.p, rb.hdr.data(), rb.hdr.size() * sizeof(raster::ChipHdr), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge), hipMemcpyHostToDevice));
+        if ((e = h2d(c, ch->hdr.p, rb.hdr.data(), rb.hdr.size() * sizeof(raster::ChipHdr))) ||
+            (e = h2d(c, ch->cells.p, rb.cells.data(), rb.cells.size() * sizeof(raster::CellRec))) ||
+            (e = h2d(c, ch->rast_edges.p, rb.edges.data(), rb.edges.size() * sizeof(pip::Edge))))
+            return e;
         return MOSAIC_OK;
     };
     trace.mark("core uploads");
@@ -3367,16 +3567,16 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 delete ch;
                 return rc;
             }
-            HIP_TRY(hipMemcpy(ch->bng_cells.p, tab.data(), bb, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(ch->bng_leaf.p, leaf.data(), lb, hipMemcpyHostToDevice));
+            if ((rc = h2d(c, ch->bng_cells.p, tab.data(), bb))) return rc;
+            if ((rc = h2d(c, ch->bng_leaf.p, leaf.data(), lb))) return rc;
             if (!lvl.empty()) {
-                HIP_TRY(hipMemcpy(ch->bng_lvl.p, lvl.data(), lvl.size() * 2, hipMemcpyHostToDevice));
+                if ((rc = h2d(c, ch->bng_lvl.p, lvl.data(), lvl.size() * 2))) return rc;
                 ch->bng_lvl_bytes = lvl.size() * 2;
                 total += lvl.size() * 2;
             }
             ch->bng_cpt_ok = !lvl.empty() || !ch->bng_C;
             if (!lcell.empty()) {
-                HIP_TRY(hipMemcpy(ch->bng_lcell.p, lcell.data(), lcell.size(), hipMemcpyHostToDevice));
+                if ((rc = h2d(c, ch->bng_lcell.p, lcell.data(), lcell.size()))) return rc;
                 ch->bng_lwords = (int32_t)(lcell.size() / 4);
                 ch->bng_lsh = lsh;
                 ch->bng_lnx = (int32_t)lnx;
@@ -3420,9 +3620,9 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 delete ch;
                 return rc;
             }
-            HIP_TRY(hipMemcpy(ch->tile_idx.p, tb.tile_idx.data(), b0, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(ch->tile_rec.p, tb.recs.data(), b1, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(ch->tile_ent.p, tb.entries.data(), b2, hipMemcpyHostToDevice));
+            if ((rc = h2d(c, ch->tile_idx.p, tb.tile_idx.data(), b0))) return rc;
+            if ((rc = h2d(c, ch->tile_rec.p, tb.recs.data(), b1))) return rc;
+            if ((rc = h2d(c, ch->tile_ent.p, tb.entries.data(), b2))) return rc;
             ch->tiles_ok = true;
             ch->tgrid = tb.grid;
             ch->tile_stats[0] = tb.grid.nx;
@@ -3462,6 +3662,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     tb.quad_lds_bytes = 0;
                 }
                 tb.lines = c->raster_lines != 0;
+                tb.leaf_lines = c->raster_leaf_lines != 0;
                 bool raster_built = false;
                 auto t_cls = std::chrono::steady_clock::now();
                 if (tb.raster_setup(src, c->raster_sub, c->raster_cell)) {
@@ -3502,9 +3703,9 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         return rc;
                     }
                     trace.mark("  raster reserve");
-                    HIP_TRY(hipMemcpy(ch->rsub.p, tb.sub.data(), r0, hipMemcpyHostToDevice));
-                    HIP_TRY(hipMemcpy(ch->rmid.p, tb.tile_base.data(), rm, hipMemcpyHostToDevice));
-                    HIP_TRY(hipMemcpy(ch->rblocks.p, tb.blocks.data(), r1, hipMemcpyHostToDevice));
+                    if ((rc = h2d(c, ch->rsub.p, tb.sub.data(), r0))) return rc;
+                    if ((rc = h2d(c, ch->rmid.p, tb.tile_base.data(), rm))) return rc;
+                    if ((rc = h2d(c, ch->rblocks.p, tb.blocks.data(), r1))) return rc;
                     trace.mark("  raster copies (sub, blocks)");
                     total += rm;
                     ch->raster_ok = true;
@@ -3527,7 +3728,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                             delete ch;
                             return rc;
                         }
-                        HIP_TRY(hipMemcpy(ch->rquad.p, tb.quad.data(), tb.quad.size() * 2, hipMemcpyHostToDevice));
+                        if ((rc = h2d(c, ch->rquad.p, tb.quad.data(), tb.quad.size() * 2))) return rc;
                         ch->praster.quad = (const uint16_t*)ch->rquad.p;
                         ch->praster.qnx = tb.qnx;
                         ch->praster.qny = tb.qny;
@@ -3585,7 +3786,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                             delete ch;
                             return rc;
                         }
-                        HIP_TRY(hipMemcpy(ch->rqrec.p, qw.data(), qw.size() * 4, hipMemcpyHostToDevice));
+                        if ((rc = h2d(c, ch->rqrec.p, qw.data(), qw.size() * 4))) return rc;
                         sa.qrec = (const uint32_t*)ch->rqrec.p;
                         sa.n_qrec = (int32_t)nrec;
                         sa.n_qrec_words = (int32_t)qw.size();
@@ -3603,6 +3804,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     ch->raster_stats[3] = tb.n_sub_mixed;
                     ch->raster_stats[4] = tb.n_cell_mixed;
                     ch->raster_stats[5] = tb.n_sub_line;
+                    ch->raster_stats[6] = tb.n_cell_line;
                     total += r0 + r1;
                 }
             }
@@ -3638,7 +3840,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         delete ch;
                         return rc;
                     }
-                    HIP_TRY(hipMemcpy(dst[k]->p, src[k]->data(), src[k]->size() * 4, hipMemcpyHostToDevice));
+                    if ((rc = h2d(c, dst[k]->p, src[k]->data(), src[k]->size() * 4))) return rc;
                     total += src[k]->size() * 4;
                 }
                 ch->img_max_words = iset.max_words;
@@ -3657,6 +3859,8 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
         delete ch;
         return rc;
     }
+    // the staged uploads are ordered on this thread's stream: complete before any stream joins the table
+    HIP_TRY(hipStreamSynchronize(c->stream));
     trace.mark("chip rasters uploaded");
     ch->device_bytes = total + capacity * sizeof(HashEntry) + meta.size() * 4 + rb.hdr.size() * sizeof(raster::ChipHdr) +
                        rb.cells.size() * sizeof(raster::CellRec) + rb.edges.size() * sizeof(pip::Edge);
@@ -3716,6 +3920,7 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
     o[5] = ch->img_records;  // binned join: LDS chip images (record parts), their bytes, the largest image
     o[6] = (int64_t)(ch->img_words.bytes + ch->img_off.bytes);
     o[7] = (int64_t)ch->img_max_words * 4;
+    o[8] = ch->raster_stats[6];  // leaf lines
     return MOSAIC_OK;
 }
 
@@ -3940,6 +4145,10 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             if ((rc = c->mix_queue.reserve((size_t)rows * 4 + 16))) return rc;
             a.mixq = (uint32_t*)c->mix_queue.p;
             a.mixq_count = sc + 4;
+            // k_join_leaf between the stream and mixed kernels: tables with leaf lines, fixed-point
+            // coordinates (tiles::raster_code_fixed's chain)
+            const bool leafq = c->leaf_join && ch->raster_stats[6] > 0 && sa.fix_ok;
+            if (leafq && (rc = c->mix_queue2.reserve((size_t)rows * 4 + 16))) return rc;
             // the mixed kernel answers its uncertified rows itself: no exact pass after it
             a.exact_inline = 1;
             exact_inline = true;
@@ -3988,6 +4197,16 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
     hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac)
                 hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
                 if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
+                if (leafq) {
+                    uint32_t* q2 = (uint32_t*)c->mix_queue2.p;
+                    unsigned long long* q2c = sc + 7;
+                    HIP_TRY(hipMemsetAsync(q2c, 0, 8, c->stream));
+                    void* largs[] = {&ac, &sa, &q2, &q2c};
+                    HIP_TRY(hipLaunchKernel(leaf_kernel(lds, pairs), dim3((unsigned)std::max(1, c->n_cu * 8)), dim3(256), largs,
+                                            lds && !pairs ? shm : 0, c->stream));
+                    ac.mixq = q2;
+                    ac.mixq_count = q2c;
+                }
                 if (c->mixed_rows == 4) {
                     if (pairs) MOSAIC_MIXED((k_join_mixed<false, true, 4>), 0);
                     else if (lds) MOSAIC_MIXED((k_join_mixed<true, false, 4>), shm);
@@ -4195,7 +4414,7 @@ int mosaic_st_contains(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* wkb_offs
     if (n == 0) return MOSAIC_OK;
     GeomStoreDev st;
     size_t total = 0;
-    int rc = st.upload(gb, c->stream, &total);
+    int rc = st.upload(gb, c, &total);
     if (rc) {
         st.release();
         return rc;

@@ -121,6 +121,11 @@ static const int kQuadRefMax = 0x7ffe;  // quad entries kSubBlock | r, r <= kQua
 static const int kQuadLimit = 65536;  // option raster_quad: largest entry budget
 
 MOSAIC_HD bool sub_is_block(uint32_t e) { return (e & kSubBlock) && e != kMixed; }
+// Leaf codes are 0, key + 1, kMixed or -- a leaf line -- kSubBlock | kLineBit | n: the cell is split
+// by one straight chip edge, LineRec n of the tile (sub-block frame), as for a line sub-block.
+// Every consumer that does not evaluate leaf lines treats codes >= kSubBlock as kMixed.
+MOSAIC_HD bool leaf_is_line(uint32_t c) { return (c & 0xC000u) == 0xC000u && c != kMixed; }
+static const int kLeafLineMargins = 3;  // leaf lines try line_margin(0 .. 2): at most 1/128 sub-block
 
 // The point raster's code of (x, y), grid origin (x0, y0) shared with the tile grid; the kernel
 // k_join_stream computes exactly this, lane-parallel.  Fine-cell coordinates g = (x - x0) sx C
@@ -157,7 +162,11 @@ MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, doubl
     if (e & kLineBit)
         return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)(gx - (double)(ixC & ~cm)),
                          (float)(gy - (double)(iyC & ~cm)));
-    return r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
+    const uint16_t lc = r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
+    if (leaf_is_line(lc))
+        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)((lc & 0x3fffu) + 1)),
+                         (float)(gx - (double)(ixC & ~cm)), (float)(gy - (double)(iyC & ~cm)));
+    return lc;
 }
 
 // Fixed-point fine-cell coordinates (k_join_stream_pipe): gi = floor(g 2^kFixBits) with g the
@@ -207,7 +216,14 @@ MOSAIC_HD uint16_t raster_code_fixed(const PointRaster& r, double ax, double bx,
         return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)((uint32_t)gix & fm) * sc,
                          (float)((uint32_t)giy & fm) * sc);
     }
-    return r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
+    const uint16_t lc = r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
+    if (leaf_is_line(lc)) {
+        const uint32_t fm = (1u << (r.cshift + F)) - 1u;
+        const float sc = 1.0f / (float)(1 << F);
+        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)((lc & 0x3fffu) + 1)),
+                         (float)((uint32_t)gix & fm) * sc, (float)((uint32_t)giy & fm) * sc);
+    }
+    return lc;
 }
 
 // std::vector allocator whose resize() leaves trivial elements uninitialised (host builders only)
@@ -356,8 +372,9 @@ struct Builder {
     std::vector<uint32_t> qrec_mask;
     std::vector<uint16_t> qrec_code;
     int qrec_shift = 0;
-    int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0, n_sub_line = 0;
+    int64_t n_sub_pure = 0, n_sub_mixed = 0, n_cell_mixed = 0, n_sub_line = 0, n_cell_line = 0;
     bool lines = true;  // split single-feature sub-blocks by a line (set before build_raster)
+    bool leaf_lines = false;  // and single-feature leaf cells of the other mixed sub-blocks
     // Chip access for the raster classification (host memory)
     struct ChipSource {
         const uint32_t* slot_first;  // per hash slot: first chip, chip count (0 for empty slots)
@@ -379,6 +396,10 @@ struct Builder {
         std::vector<LineRec> line;      // per mixed sub-block (kind 1)
         std::vector<uint32_t> cell_at;  // per mixed sub-block (kind 0): its block of C x C codes in cells
         std::vector<uint16_t, NoInitAlloc<uint16_t>> cells;
+        // leaf lines: the kMixed leaf cells (index into cells, ascending) that one straight chip edge
+        // splits, and their line records (sub-block frame, as the sub-block line records)
+        std::vector<uint32_t> cline_at;
+        std::vector<LineRec> cline;
     };
     std::vector<int> tile_of_rec;  // record -> tile (raster_setup)
     bool raster_setup(const ChipSource& src, int S_, int C_);

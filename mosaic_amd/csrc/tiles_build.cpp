@@ -127,6 +127,8 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
     std::vector<std::vector<uint8_t>> r_kind(recs.size());
     std::vector<std::vector<LineRec>> r_line(recs.size());
     std::vector<std::vector<uint16_t>> r_cells(recs.size());
+    std::vector<std::vector<uint32_t>> r_cline_at(recs.size());  // leaf lines: cell (record-local) ...
+    std::vector<std::vector<LineRec>> r_cline(recs.size());      // ... and its record
     std::atomic<int64_t> next(0);
 
     auto work = [&]() {
@@ -278,12 +280,16 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
             };
             // a mixed sub-block whose chip edges all lie along one line: the line through the
             // longest clipped edge; both sides (beyond a margin, less the slack) must classify
+            // The box is [u0, u1] x [v0, v1] in sub-block units: the whole sub-block, or one leaf cell
+            // (a leaf line, tried margins 0 .. mk_end - 1) in the sub-block's frame.
             std::vector<P2> ends;
-            auto try_line = [&](int si, int sj, const std::vector<int>& cin, LineRec& out) -> bool {
+            auto try_line = [&](int si, int sj, double u0, double v0, double u1, double v1, int mk_end,
+                                const std::vector<int>& cin, LineRec& out) -> bool {
                 const double wR = tw / S, hR = th / S;
                 const double lonR0 = lon0 + tw * si / S, latR0 = lat0 + th * sj / S;
                 const double exu = exd / wR, eyv = eyd / hR;
-                const double bx0 = lonR0 - exd, bx1 = lonR0 + wR + exd, by0 = latR0 - eyd, by1 = latR0 + hR + eyd;
+                const double bx0 = lonR0 + wR * u0 - exd, bx1 = lonR0 + wR * u1 + exd, by0 = latR0 + hR * v0 - eyd,
+                             by1 = latR0 + hR * v1 + eyd;
                 double best = 0.0;
                 P2 pa{0, 0}, pb{0, 0};
                 ends.clear();
@@ -295,7 +301,7 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                         for (const Seg& e : h.segs[b]) {
                             double ax = (e.ax - lonR0) / wR, ay = (e.ay - latR0) / hR;
                             double qx = (e.bx - lonR0) / wR, qy = (e.by - latR0) / hR;
-                            if (!clip_seg(ax, ay, qx, qy, -exu, -eyv, 1.0 + exu, 1.0 + eyv)) continue;
+                            if (!clip_seg(ax, ay, qx, qy, u0 - exu, v0 - eyv, u1 + exu, v1 + eyv)) continue;
                             ends.push_back(P2{ax, ay});
                             ends.push_back(P2{qx, qy});
                             const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
@@ -313,9 +319,9 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                 const double c = -(a * 0.5 * (pa.x + pb.x) + b * 0.5 * (pa.y + pb.y));
                 double dev_max = 0.0;
                 for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * p.x + b * p.y + c));
-                const P2 sq[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
+                const P2 sq[4] = {{u0 - exu, v0 - eyv}, {u1 + exu, v0 - eyv}, {u1 + exu, v1 + eyv}, {u0 - exu, v1 + eyv}};
                 // the narrowest band (fewest rows to the mixed kernel) whose two sides certify
-                for (int mk = 0; mk < 4; mk++) {
+                for (int mk = 0; mk < mk_end; mk++) {
                     const double margin = rbuild::line_margin(mk);
                     if (dev_max > margin - 2.0 * kLineSlack) continue;
                     out.a = (float)(a / margin);
@@ -352,7 +358,7 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                     rcode[(size_t)sj * S + si] = code;
                     if (code != kMixed) continue;
                     LineRec lr;
-                    if (lines && try_line(si, sj, cand, lr)) {
+                    if (lines && try_line(si, sj, 0.0, 0.0, 1.0, 1.0, 4, cand, lr)) {
                         r_kind[(size_t)ri].push_back(1);
                         r_line[(size_t)ri].push_back(lr);
                         continue;
@@ -367,7 +373,14 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                             int i0 = si * C + ci, j0 = sj * C + cj;
                             const P2 qc[4] = {clat[(size_t)cj * (C + 1) + ci], clat[(size_t)cj * (C + 1) + ci + 1],
                                               clat[(size_t)(cj + 1) * (C + 1) + ci + 1], clat[(size_t)(cj + 1) * (C + 1) + ci]};
-                            cellc[(size_t)cj * C + ci] = classify(i0, j0, i0 + 1, j0 + 1, qc, cand, cand2);
+                            uint16_t cc = classify(i0, j0, i0 + 1, j0 + 1, qc, cand, cand2);
+                            if (cc == kMixed && leaf_lines &&
+                                try_line(si, sj, (double)ci / C, (double)cj / C, (double)(ci + 1) / C, (double)(cj + 1) / C,
+                                         kLeafLineMargins, cand2, lr)) {
+                                r_cline_at[(size_t)ri].push_back((uint32_t)(r_cells[(size_t)ri].size() + (size_t)cj * C + ci));
+                                r_cline[(size_t)ri].push_back(lr);
+                            }
+                            cellc[(size_t)cj * C + ci] = cc;
                         }
                     r_kind[(size_t)ri].push_back(0);
                     r_line[(size_t)ri].push_back(LineRec{0, 0, 0, 0, 0});
@@ -384,8 +397,14 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
     rc.line.clear();
     rc.cell_at.clear();
     rc.cells.clear();
+    rc.cline_at.clear();
+    rc.cline.clear();
     for (size_t r = 0; r < recs.size(); r++) {
         size_t c0 = 0;
+        for (size_t k = 0; k < r_cline_at[r].size(); k++) {
+            rc.cline_at.push_back((uint32_t)(rc.cells.size() + r_cline_at[r][k]));
+            rc.cline.push_back(r_cline[r][k]);
+        }
         for (size_t k = 0; k < r_kind[r].size(); k++) {
             rc.kind.push_back(r_kind[r][k]);
             rc.line.push_back(r_line[r][k]);
@@ -470,9 +489,9 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
     for (int64_t ri = 0; ri < nrec; ri++) mk0[(size_t)ri + 1] += mk0[(size_t)ri];
     if (mk0[(size_t)nrec] > rc.kind.size()) return false;
     trace.mark("alloc + mixed counts");
-    std::atomic<int64_t> pure(0), mixed(0), cmixed(0), nline(0);
+    std::atomic<int64_t> pure(0), mixed(0), cmixed(0), nline(0), ncline(0);
     parallel_for(nrec, threads, [&](int64_t b, int64_t e) {
-        int64_t l_pure = 0, l_mixed = 0, l_cmixed = 0, l_line = 0;
+        int64_t l_pure = 0, l_mixed = 0, l_cmixed = 0, l_line = 0, l_cline = 0;
         for (int64_t ri = b; ri < e; ri++) {
             if (!rec_ok(ri)) continue;
             const int t = tile_of_rec[(size_t)ri];
@@ -507,7 +526,18 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
                             } else {
                                 // tile-local leaf block number (< S * S <= kLineBit)
                                 entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / CC));
+                                const size_t b0 = outb.size();
                                 outb.insert(outb.end(), cellc, cellc + CC);
+                                // leaf lines: kSubBlock | kLineBit | n, n the tile-local line record
+                                // (while n fits 14 bits; the others stay kMixed)
+                                const uint32_t g0 = rc.cell_at[mk] * (uint32_t)CC;
+                                for (auto it = std::lower_bound(rc.cline_at.begin(), rc.cline_at.end(), g0);
+                                     it != rc.cline_at.end() && *it < g0 + (uint32_t)CC && outl.size() < kLineBit; ++it) {
+                                    outb[b0 + (*it - g0)] = (uint16_t)(kSubBlock | kLineBit | (uint32_t)outl.size());
+                                    outl.push_back(rc.cline[(size_t)(it - rc.cline_at.begin())]);
+                                    l_cline++;
+                                    l_cmixed--;
+                                }
                             }
                         }
                         mk++;
@@ -519,6 +549,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
         mixed += l_mixed;
         cmixed += l_cmixed;
         nline += l_line;
+        ncline += l_cline;
     });
     trace.mark("sub entries");
     // tiles without a record: kFull (every point takes the tile path) or kSkip (no pair: 0)
@@ -583,6 +614,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
     n_sub_pure = pure.load();
     n_sub_mixed = mixed.load();
     n_cell_mixed = cmixed.load();
+    n_cell_line = ncline.load();
     // quad level: the smallest power-of-two group of sub-blocks whose table fits quad_max entries
     qshift = 0;
     while (qshift < 16 && ((NX + (1 << qshift) - 1) >> qshift) * ((NY + (1 << qshift) - 1) >> qshift) > quad_max)

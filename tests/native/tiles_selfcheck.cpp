@@ -102,6 +102,7 @@ int main(int argc, char** argv) {
     src.n_polygons = npoly;
     // the stream kernel's LDS shape: quad level in half of ~130 KB, quad records in the rest
     tb.quad_max = 16384;
+    tb.leaf_lines = getenv("TILES_NO_LEAF_LINES") == nullptr;  // leaf lines certified too (every pure code is checked)
     tb.quad_lds_bytes = 130 * 1024;
     bool rok = tb.build_raster(src, S, Cc, 8);
     tiles::PointRaster pr{};

@@ -80,6 +80,7 @@ int main(int argc, char** argv) {
     const int threads = argc > 9 ? atoi(argv[9]) : 8;
     auto t0 = std::chrono::steady_clock::now();
     tiles::Builder tb;
+    tb.leaf_lines = getenv("NO_LEAF_LINES") == nullptr;
     if (!tb.build(res, cells, slot_of)) {
         fprintf(stderr, "directory not built: %s\n", tb.why);
         return 1;
@@ -114,6 +115,7 @@ int main(int argc, char** argv) {
            "blocks %zu elements; quad %d x %d shift %d\n",
            tb.grid.nx, tb.grid.ny, (long long)NX, (long long)NY, tb.recs.size(), (long long)tb.n_sub_pure,
            (long long)tb.n_sub_mixed, (long long)tb.n_sub_line, tb.blocks.size(), tb.qnx, tb.qny, tb.qshift);
+    printf("leaf cells: mixed %lld, leaf lines %lld\n", (long long)tb.n_cell_mixed, (long long)tb.n_cell_line);
     const uint16_t* sub = tb.sub.data();
     auto sub_at = [&](int64_t i, int64_t j) { return sub[(size_t)(j * NX + i)]; };
     // per quad shift q: uniform quads (one pure code over all their sub-blocks)
