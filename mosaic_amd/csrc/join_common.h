@@ -192,6 +192,9 @@ struct StreamArgs {
     // clamp(cvt_i32(fma(x, sxF, gx0F)), 0, gxmaxF) with F = tiles::kFixBits fraction bits
     double sxF, syF, gx0F, gy0F;
     int32_t gxmaxF, gymaxF, fix_ok;  // fix_ok: (NX C) 2^F and (NY C) 2^F fit an int32
+    // leaf lines (tiles::PointRaster::tile_lbase / llines; nullptr: none): k_join_leaf only
+    const uint32_t* tile_lbase;
+    const tiles::LineRec* llines;
 };
 // per-wave mixed-row stage of the stream kernels (words): rows are appended one slot (<= 64 rows)
 // at a time and flushed at >= 64

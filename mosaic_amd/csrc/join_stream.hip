@@ -1124,6 +1124,13 @@ __global__ void __launch_bounds__(256) k_join_leaf(JoinArgs a, StreamArgs s, uin
         for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x) lds[k] = 0;
         __syncthreads();
     }
+    // kept rows through a per-wave stage (one q2 atomic per >= 64 rows: a per-wave atomic on one
+    // counter from every wave at once serialises the kernel)
+    JoinArgs aq = a;
+    aq.mixq = q2;
+    aq.mixq_count = q2_count;
+    uint32_t* wq = lds + (LDS_COUNTS ? a.n_polygons : 0) + (threadIdx.x >> 6) * kStageWords;
+    uint32_t wn = 0;
     constexpr int F = tiles::kFixBits;
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
@@ -1150,11 +1157,12 @@ __global__ void __launch_bounds__(256) k_join_leaf(JoinArgs a, StreamArgs s, uin
                 const uint32_t e = q < 0x8000u ? q : s.csub[((q & 0x7fffu) << (2 * qs)) + (((iy & qm) << qs) | (ix & qm))];
                 code = e;
                 if (tiles::sub_is_block(e) && !(e & tiles::kLineBit)) {
-                    const uint32_t base = s.tile_base[(iyC >> s.tsh) * (uint32_t)s.tnx + (ixC >> s.tsh)];
+                    const uint32_t tile = (iyC >> s.tsh) * (uint32_t)s.tnx + (ixC >> s.tsh);
+                    const uint32_t base = s.tile_base[tile];
                     const uint32_t lc = s.blocks[base + ((e & 0x3fffu) << (2 * cs)) + (((iyC & cm) << cs) | (ixC & cm))];
                     code = lc;
                     if (tiles::leaf_is_line(lc)) {
-                        const tiles::LineRec lr = *(const tiles::LineRec*)(s.blocks + base - 8u * ((lc & 0x3fffu) + 1u));
+                        const tiles::LineRec lr = s.llines[s.tile_lbase[tile] + (lc & 0x3fffu)];
                         const uint32_t fm = (1u << (cs + F)) - 1u;
                         const float sc = 1.0f / (float)(1 << F);
                         code = tiles::line_code(lr, (float)(gix & fm) * sc, (float)(giy & fm) * sc);
@@ -1169,14 +1177,10 @@ __global__ void __launch_bounds__(256) k_join_leaf(JoinArgs a, StreamArgs s, uin
             if (LDS_COUNTS && !PAIRS) atomicAdd(&lds[code - 1u], 1u);
             else emit_hit<LDS_COUNTS, PAIRS>(a, row, code - 1u, lds);
         }
-        const unsigned long long km = __ballot(keep);
-        if (km) {
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(q2_count, (unsigned long long)__popcll(km));
-            base = __shfl(base, 0, 64);
-            if (keep) q2[base + __popcll(km & lt_mask)] = off;
-        }
+        stage_push(wq, wn, keep, off, lt_mask);
+        stage_flush(aq, wq, wn, lane, 64);
     }
+    stage_flush(aq, wq, wn, lane, 1);
     if (LDS_COUNTS) {
         __syncthreads();
         for (int k = threadIdx.x; k < a.n_polygons; k += blockDim.x)

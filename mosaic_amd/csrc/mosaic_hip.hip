@@ -25,6 +25,7 @@
 #include <numeric>
 #include <string>
 #include <sys/mman.h>
+#include <dirent.h>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -536,7 +537,7 @@ __device__ inline int rhex_answer_wave(const RBuildArgs& a, const RTile& t, int 
 // those of the cell (tiles_build.cpp classify's cand2), as try_line's cin
 __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* uv,
                                                int n, const rbuild::P2* sq, double stol, const rbuild::P2* qc = nullptr,
-                                               double ctol = 0.0) {
+                                               double ctol = 0.0, int nc = -1, int ck = 0) {
     using rbuild::dmax;
     using rbuild::dmin;
     rbuild::P2 img[8], ll[8];
@@ -564,17 +565,20 @@ __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile&
     bool any = false;
     int acnt = 0, akey = -1;
     const int W = t.wa * t.wb, lane = (int)(threadIdx.x & 63);
-    for (int k0 = 0; k0 < W; k0 += 64) {
+    // nc >= 0: the candidates are given (lane j < nc holds window hexagon ck, ascending), the sq / qc
+    // filters already applied
+    const bool listm = nc >= 0;
+    for (int k0 = 0; k0 < (listm ? 1 : W); k0 += 64) {
         // the window hexagons of this chunk that are candidates, one lane each, in order
-        const int kl = k0 + lane;
+        const int kl = listm ? (lane < nc ? ck : -1) : k0 + lane;
         bool is_c = false;
-        if (kl < W) {
+        if (listm ? kl >= 0 : kl < W) {
             const rbuild::P2 c = rhex_centre(t, kl);
-            is_c = rbuild::poly_meets_hex(sq, 4, c, stol, a.ht) && (!qc || rbuild::poly_meets_hex(qc, 4, c, ctol, a.ht)) &&
+            is_c = (listm || (rbuild::poly_meets_hex(sq, 4, c, stol, a.ht) && (!qc || rbuild::poly_meets_hex(qc, 4, c, ctol, a.ht)))) &&
                    rbuild::poly_meets_hex(img, n, c, tol, a.ht);
         }
         for (unsigned long long mask = __ballot(is_c); mask; mask &= mask - 1) {
-            const int k = k0 + __builtin_ctzll(mask);
+            const int k = listm ? __shfl(ck, __builtin_ctzll(mask), 64) : k0 + __builtin_ctzll(mask);
             int key;
             const int cnt = rhex_answer_wave(a, t, k, x0, y0, x1, y1, ll, n, eps, mx, my, &key);
             if (cnt < 0 || cnt > 1) return tiles::kMixed;
@@ -597,7 +601,8 @@ __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile&
 __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* sq,
                                       double stol, tiles::LineRec& out, double u0 = 0.0, double v0 = 0.0,
                                       double u1 = 1.0, double v1 = 1.0, int mk_end = 4, const rbuild::P2* qc = nullptr,
-                                      double ctol = 0.0) {
+                                      double ctol = 0.0, int nc = -1, int ck = 0) {
+    const bool listm = nc >= 0;  // the candidates given (rclassify_poly_wave's nc, ck)
     const int S = a.S, lane = (int)(threadIdx.x & 63);
     const double wR = a.tw / S, hR = a.th / S;
     const double lonR0 = t.lon0 + a.tw * si / S, latR0 = t.lat0 + a.th * sj / S;
@@ -612,13 +617,13 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
     const int W = t.wa * t.wb;
     if (W <= 0) return false;
     for (int pass = 0; pass < 2; pass++)
-        for (int k0 = 0; k0 < W; k0 += 64) {
-        const int kl = k0 + lane;
-        const bool is_c = kl < W && a.entries[t.off + (uint32_t)kl] &&
-                          rbuild::poly_meets_hex(sq, 4, rhex_centre(t, kl), stol, a.ht) &&
-                          (!qc || rbuild::poly_meets_hex(qc, 4, rhex_centre(t, kl), ctol, a.ht));
+        for (int k0 = 0; k0 < (listm ? 1 : W); k0 += 64) {
+        const int kl = listm ? (lane < nc ? ck : -1) : k0 + lane;
+        const bool is_c = (listm ? kl >= 0 : kl < W) && a.entries[t.off + (uint32_t)kl] &&
+                          (listm || (rbuild::poly_meets_hex(sq, 4, rhex_centre(t, kl), stol, a.ht) &&
+                                     (!qc || rbuild::poly_meets_hex(qc, 4, rhex_centre(t, kl), ctol, a.ht))));
         for (unsigned long long mask = __ballot(is_c); mask; mask &= mask - 1) {
-            const int k = k0 + __builtin_ctzll(mask);
+            const int k = listm ? __shfl(ck, __builtin_ctzll(mask), 64) : k0 + __builtin_ctzll(mask);
             const uint32_t e = a.entries[t.off + (uint32_t)k];
             const HashEntry he = a.table[e - 1];
             for (uint32_t c = he.first; c < he.first + he.count; c++) {
@@ -649,7 +654,7 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
                     }
             }
         }
-        if (pass == 0 && k0 + 64 >= W) {
+        if (pass == 0 && (listm || k0 + 64 >= W)) {
             // the sequential choice: the largest l2, and of equal ones the first in order
             double bl = best;
             uint64_t bk = best_key;
@@ -686,9 +691,9 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
         const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - tiles::kLineSlack / margin;
         rbuild::P2 hp[8], hn[8];
         const int np = rbuild::clip_half(sqb, 4, A, B, Cf - m, hp), nn = rbuild::clip_half(sqb, 4, -A, -B, -Cf - m, hn);
-        const uint16_t cp = np >= 3 ? rclassify_poly_wave(a, t, si, sj, hp, np, sq, stol, qc, ctol) : (uint16_t)0;
+        const uint16_t cp = np >= 3 ? rclassify_poly_wave(a, t, si, sj, hp, np, sq, stol, qc, ctol, nc, ck) : (uint16_t)0;
         if (cp == tiles::kMixed) continue;
-        const uint16_t cn = nn >= 3 ? rclassify_poly_wave(a, t, si, sj, hn, nn, sq, stol, qc, ctol) : (uint16_t)0;
+        const uint16_t cn = nn >= 3 ? rclassify_poly_wave(a, t, si, sj, hn, nn, sq, stol, qc, ctol, nc, ck) : (uint16_t)0;
         if (cn == tiles::kMixed) continue;
         out.pos = cp;
         out.neg = cn;
@@ -742,39 +747,90 @@ __global__ void __launch_bounds__(256) k_raster_cells(RBuildArgs a) {
     }
 }
 
-// Leaf lines (tiles_build.cpp, the cell loop of classify_raster_host): one wave per kMixed leaf
-// cell (mlist: its index in `cells`, ascending), the line fit of k_raster_line_wave over the cell's
-// box with the cell's candidates; ok[m] = 1 and out[m] = the record when one certifies.
-__global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const uint32_t* mlist, int64_t n_ml,
-                                                           uint8_t* ok, tiles::LineRec* out) {
-    const int64_t m = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+// Leaf lines (tiles_build.cpp, the cell loop of classify_raster_host).  mlist: the kMixed leaf
+// cells (index in `cells`, ascending); first[msb]: the first entry of kind-0 sub-block msb's cells in
+// mlist, -1 when it has none (k_ml_first).  One wave per such sub-block: its candidate hexagons
+// (the window hexagons meeting the sub-block quad, as classify's `cand`) once, then per mixed cell
+// the cell's candidates among them (cand2) and the line fit of k_raster_line_wave over the cell's
+// box with those; ok[m] = 1 and out[m] = the record when one certifies.  (More than 64 sub-block
+// candidates: the window form per cell.)
+__global__ void k_ml_first(const uint32_t* mlist, int64_t n_ml, int64_t CC, int32_t* first) {
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n_ml) return;
+    const int64_t msb = mlist[m] / CC;
+    if (m == 0 || (int64_t)(mlist[m - 1] / CC) != msb) first[msb] = (int32_t)m;
+}
+
+__global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const uint32_t* mlist, int64_t n_ml,
+                                                           const int32_t* first, uint8_t* ok, tiles::LineRec* out) {
+    __shared__ int cbuf[4][64];
+    const int64_t msb = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (msb >= a.n_cell_sb) return;
+    const int64_t m0 = first[msb];
+    if (m0 < 0) return;
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6) & 3;
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
-    const int64_t w = mlist[m];
-    const int64_t msb = w / CC;
-    const int cc = (int)(w - msb * CC), cj = cc / a.C, ci = cc - cj * a.C;
     const int64_t g = a.cell_sb[msb];
     const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
     RTile t;
-    tiles::LineRec lr{0, 0, 0, 0, 0};
-    bool found = false;
-    if (rtile_of(a, r, t)) {
-        rbuild::P2 sq[4];
-        const double stol = rsub_quad(a, t, si, sj, sq);
-        const int i0 = si * a.C + ci, j0 = sj * a.C + cj;
-        const rbuild::P2 qc[4] = {rimage(a, t, i0, j0), rimage(a, t, i0 + 1, j0), rimage(a, t, i0 + 1, j0 + 1),
-                                  rimage(a, t, i0, j0 + 1)};
-        // the cell's tolerance as rclassify_rect computes it (tiles_build.cpp classify)
-        const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
-        const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
-        const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
-        const double ctol = tiles::rect_tol(t.cv, cell_deg_x * 1, cell_deg_y * 1, rbuild::dmax(ex, ey));
-        found = rtry_line_wave(a, t, si, sj, sq, stol, lr, (double)ci / a.C, (double)cj / a.C, (double)(ci + 1) / a.C,
-                               (double)(cj + 1) / a.C, tiles::kLeafLineMargins, qc, ctol);
+    const bool tok = rtile_of(a, r, t);
+    rbuild::P2 sq[4];
+    double stol = 0.0;
+    int nsc = 0, sck = -1;
+    bool over = false;
+    if (tok) {
+        stol = rsub_quad(a, t, si, sj, sq);
+        const int W = t.wa * t.wb;
+        for (int k0 = 0; k0 < W && !over; k0 += 64) {
+            const int kl = k0 + lane;
+            const bool is_c = kl < W && rbuild::poly_meets_hex(sq, 4, rhex_centre(t, kl), stol, a.ht);
+            const unsigned long long mk = __ballot(is_c);
+            const int cnt = __popcll(mk);
+            if (nsc + cnt > 64) {
+                over = true;
+            } else {
+                if (is_c) cbuf[wv][nsc + __popcll(mk & lt_mask)] = kl;
+                nsc += cnt;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        sck = lane < nsc ? cbuf[wv][lane] : -1;
+        __builtin_amdgcn_wave_barrier();
     }
-    if ((threadIdx.x & 63) == 0) {
-        ok[m] = found ? 1 : 0;
-        out[m] = found ? lr : tiles::LineRec{0, 0, 0, 0, 0};
+    const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
+    for (int64_t m = m0; m < n_ml && (int64_t)(mlist[m] / CC) == msb; m++) {
+        const int cc = (int)(mlist[m] - msb * CC), cj = cc / a.C, ci = cc - cj * a.C;
+        tiles::LineRec lr{0, 0, 0, 0, 0};
+        bool found = false;
+        if (tok) {
+            const int i0 = si * a.C + ci, j0 = sj * a.C + cj;
+            const rbuild::P2 qc[4] = {rimage(a, t, i0, j0), rimage(a, t, i0 + 1, j0), rimage(a, t, i0 + 1, j0 + 1),
+                                      rimage(a, t, i0, j0 + 1)};
+            // the cell's tolerance as rclassify_rect computes it (tiles_build.cpp classify)
+            const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
+            const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
+            const double ctol = tiles::rect_tol(t.cv, cell_deg_x * 1, cell_deg_y * 1, rbuild::dmax(ex, ey));
+            const double u0 = (double)ci / a.C, v0 = (double)cj / a.C, u1 = (double)(ci + 1) / a.C, v1 = (double)(cj + 1) / a.C;
+            if (over) {
+                found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol);
+            } else {
+                // the cell's candidates: the sub-block's that meet the cell quad, ascending
+                const bool cin = lane < nsc && rbuild::poly_meets_hex(qc, 4, rhex_centre(t, sck), ctol, a.ht);
+                const unsigned long long mk = __ballot(cin);
+                if (cin) cbuf[wv][__popcll(mk & lt_mask)] = sck;
+                __builtin_amdgcn_wave_barrier();
+                const int ncc = __popcll(mk);
+                const int cck = lane < ncc ? cbuf[wv][lane] : -1;
+                __builtin_amdgcn_wave_barrier();
+                found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol, ncc,
+                                       cck);
+            }
+        }
+        if (lane == 0) {
+            ok[m] = found ? 1 : 0;
+            out[m] = found ? lr : tiles::LineRec{0, 0, 0, 0, 0};
+        }
     }
 }
 
@@ -2073,6 +2129,7 @@ struct mosaic_chips {
     bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
     StreamArgs stream{};
     DevBuf rsub, rmid, rblocks, rquad, rqrec;  // rmid: per-tile leaf block bases; rqrec: quad records
+    DevBuf rlbase, rllines;                    // leaf lines: per-tile first record, the records
     // per-tile chip images of the binned join (tile_images.h ImageSet); empty: none
     DevBuf img_words, img_off, img_rec, img_binmap;
     uint32_t img_max_words = 0;
@@ -2084,10 +2141,11 @@ struct mosaic_chips {
     // classification (GPU or host), point-raster assembly; FNV-1a digest of the point raster
     double build_ms[4] = {0, 0, 0, 0};
     uint64_t raster_digest = 0;  // computed on first request (mosaic_chip_table_build_info), not in the build
-    size_t raster_parts[6] = {0, 0, 0, 0, 0, 0};  // bytes of sub, blocks, tile_base, quad, qrec masks, qrec codes
+    size_t raster_parts[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // bytes of sub, blocks, tile_base, quad, qrec masks, qrec
+                                                        // codes, leaf-line bases, leaf lines
     void release_all() {
         for (DevBuf* b : {&table, &meta, &hdr, &cells, &rast_edges,
-                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &bng_cells, &bng_leaf, &bng_lcell, &bng_lvl,
+                          &tile_idx, &tile_rec, &tile_ent, &rsub, &rmid, &rblocks, &rquad, &rqrec, &rlbase, &rllines, &bng_cells, &bng_leaf, &bng_lcell, &bng_lvl,
                           &img_words, &img_off, &img_rec, &img_binmap})
             b->release();
         store.release();
@@ -2988,12 +3046,32 @@ static double ms_since(std::chrono::steady_clock::time_point t0) {
 
 // Build-side phase trace (measurement only): MOSAIC_BUILD_TRACE=1 prints each phase's wall time of
 // a chip-table build to stderr.
+// With the driver's per-process statistics readable, each line also shows the time the process's
+// queues have spent evicted so far (KFD sysfs stats_<gpu>/evicted_ms, summed over GPUs).
+static long long kfd_evicted_ms() {
+    char dir[96];
+    snprintf(dir, sizeof dir, "/sys/class/kfd/kfd/proc/%d", (int)getpid());
+    long long total = -1;
+    if (DIR* d = opendir(dir)) {
+        while (dirent* e = readdir(d)) {
+            if (strncmp(e->d_name, "stats_", 6) != 0) continue;
+            std::string f = std::string(dir) + "/" + e->d_name + "/evicted_ms";
+            if (FILE* fp = fopen(f.c_str(), "r")) {
+                long long v = 0;
+                if (fscanf(fp, "%lld", &v) == 1) total = (total < 0 ? 0 : total) + v;
+                fclose(fp);
+            }
+        }
+        closedir(d);
+    }
+    return total;
+}
 struct BuildTrace {
     bool on = getenv("MOSAIC_BUILD_TRACE") != nullptr;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
     void mark(const char* what) {
         if (!on) return;
-        fprintf(stderr, "[build] %-28s %8.3f ms\n", what, ms_since(t));
+        fprintf(stderr, "[build] %-28s %8.3f ms  (evicted %lld ms)\n", what, ms_since(t), kfd_evicted_ms());
         t = std::chrono::steady_clock::now();
     }
 };
@@ -3129,9 +3207,15 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     int64_t n_ml = 0;
     if ((e = d2h(c, &n_ml, d_nml.p, 8))) return e;
     if (n_ml <= 0) return MOSAIC_OK;
-    if ((e = d_ok.reserve((size_t)n_ml)) || (e = d_lrec.reserve((size_t)n_ml * sizeof(tiles::LineRec)))) return e;
-    hipLaunchKernelGGL(k_raster_cell_lines, dim3((unsigned)((n_ml + 3) / 4)), dim3(256), 0, c->stream, a,
-                       (const uint32_t*)d_ml.p, n_ml, (uint8_t*)d_ok.p, (tiles::LineRec*)d_lrec.p);
+    TmpBuf d_first;
+    if ((e = d_ok.reserve((size_t)n_ml)) || (e = d_lrec.reserve((size_t)n_ml * sizeof(tiles::LineRec))) ||
+        (e = d_first.reserve(cell_sb.size() * 4)))
+        return e;
+    HIP_TRY(hipMemsetAsync(d_first.p, 0xff, cell_sb.size() * 4, c->stream));
+    hipLaunchKernelGGL(k_ml_first, dim3((unsigned)((n_ml + 255) / 256)), dim3(256), 0, c->stream, (const uint32_t*)d_ml.p,
+                       n_ml, (int64_t)CC, (int32_t*)d_first.p);
+    hipLaunchKernelGGL(k_raster_cell_lines, dim3((unsigned)((cell_sb.size() + 3) / 4)), dim3(256), 0, c->stream, a,
+                       (const uint32_t*)d_ml.p, n_ml, (const int32_t*)d_first.p, (uint8_t*)d_ok.p, (tiles::LineRec*)d_lrec.p);
     HIP_TRY(hipGetLastError());
     std::vector<uint32_t> ml((size_t)n_ml);
     std::vector<uint8_t> okv((size_t)n_ml);
@@ -3696,6 +3780,8 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     ch->raster_parts[3] = tb.quad.size() * 2;
                     ch->raster_parts[4] = tb.qrec_mask.size() * 4;
                     ch->raster_parts[5] = tb.qrec_code.size() * 2;
+                    ch->raster_parts[6] = tb.llines.empty() ? 0 : tb.tile_lbase.size() * 4;
+                    ch->raster_parts[7] = tb.llines.size() * sizeof(tiles::LineRec);
                     size_t r0 = tb.sub.size() * 2, r1 = tb.blocks.size() * 2, rm = tb.tile_base.size() * 4;
                     if ((rc = ch->rsub.reserve(r0)) || (rc = ch->rblocks.reserve(r1)) || (rc = ch->rmid.reserve(rm))) {
                         ch->release_all();
@@ -3706,6 +3792,16 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     if ((rc = h2d(c, ch->rsub.p, tb.sub.data(), r0))) return rc;
                     if ((rc = h2d(c, ch->rmid.p, tb.tile_base.data(), rm))) return rc;
                     if ((rc = h2d(c, ch->rblocks.p, tb.blocks.data(), r1))) return rc;
+                    if (!tb.llines.empty()) {
+                        if ((rc = ch->rlbase.reserve(ch->raster_parts[6])) || (rc = ch->rllines.reserve(ch->raster_parts[7])) ||
+                            (rc = h2d(c, ch->rlbase.p, tb.tile_lbase.data(), ch->raster_parts[6])) ||
+                            (rc = h2d(c, ch->rllines.p, tb.llines.data(), ch->raster_parts[7]))) {
+                            ch->release_all();
+                            delete ch;
+                            return rc;
+                        }
+                        total += ch->raster_parts[6] + ch->raster_parts[7];
+                    }
                     trace.mark("  raster copies (sub, blocks)");
                     total += rm;
                     ch->raster_ok = true;
@@ -3714,6 +3810,8 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                     ch->praster.sshift = tb.sshift;
                     ch->praster.tnx = tb.grid.nx;
                     ch->praster.blocks = (const uint16_t*)ch->rblocks.p;
+                    ch->praster.tile_lbase = tb.llines.empty() ? nullptr : (const uint32_t*)ch->rlbase.p;
+                    ch->praster.llines = tb.llines.empty() ? nullptr : (const tiles::LineRec*)ch->rllines.p;
                     ch->praster.sx = tb.grid.sx * tb.S;
                     ch->praster.sy = tb.grid.sy * tb.S;
                     ch->praster.nx = tb.grid.nx * tb.S;
@@ -3772,6 +3870,8 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         sa.tile_base = (const uint32_t*)ch->rmid.p;
                         sa.csub = (const uint16_t*)ch->rsub.p + nsub;
                         sa.blocks = (const uint16_t*)ch->rblocks.p;
+                        sa.tile_lbase = ch->praster.tile_lbase;
+                        sa.llines = ch->praster.llines;
                         sa.csub_bytes = (uint32_t)csub_bytes;
                         sa.blocks_bytes = (uint32_t)blocks_bytes;
                         sa.tile_base_bytes = (uint32_t)rm;
@@ -3915,7 +4015,8 @@ int mosaic_chip_table_raster(const mosaic_chips* ch, int64_t* o) {
     o[0] = ch->raster_stats[5];
     o[1] = ch->praster.quad ? (int64_t)ch->praster.qnx * ch->praster.qny : 0;
     o[2] = ch->praster.quad ? ch->praster.qshift : 0;
-    o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes + ch->rqrec.bytes) : 0;
+    o[3] = ch->raster_ok ? (int64_t)(ch->rsub.bytes + ch->rmid.bytes + ch->rblocks.bytes + ch->rquad.bytes + ch->rqrec.bytes +
+                                     ch->rlbase.bytes + ch->rllines.bytes) : 0;
     o[4] = ch->stream_ok ? 1 : 0;
     o[5] = ch->img_records;  // binned join: LDS chip images (record parts), their bytes, the largest image
     o[6] = (int64_t)(ch->img_words.bytes + ch->img_off.bytes);
@@ -3933,11 +4034,12 @@ int mosaic_chip_table_build_info(const mosaic_chips* ch, double* ms4, uint64_t* 
         // FNV-1a over the raster arrays as uploaded (sub-block table, blocks, tile bases, quad level,
         // quad-record masks and codes): read back from the device on request, off the build's path
         HIP_TRY(hipSetDevice(ch->device));
-        const void* src[6] = {ch->rsub.p, ch->rblocks.p, ch->rmid.p, ch->rquad.p, ch->rqrec.p,
-                              ch->rqrec.p ? (const void*)((const uint8_t*)ch->rqrec.p + ch->raster_parts[4]) : nullptr};
+        const void* src[8] = {ch->rsub.p, ch->rblocks.p, ch->rmid.p, ch->rquad.p, ch->rqrec.p,
+                              ch->rqrec.p ? (const void*)((const uint8_t*)ch->rqrec.p + ch->raster_parts[4]) : nullptr,
+                              ch->rlbase.p, ch->rllines.p};
         uint64_t h = 1469598103934665603ull;
         std::vector<uint8_t> buf;
-        for (int k = 0; k < 6; k++) {
+        for (int k = 0; k < 8; k++) {
             buf.resize(src[k] ? ch->raster_parts[k] : 0);  // (parts not uploaded: quad level or records off)
             if (!buf.empty()) HIP_TRY(hipMemcpy(buf.data(), src[k], buf.size(), hipMemcpyDeviceToHost));
             h = fnv1a(h, buf.data(), buf.size());
@@ -4147,7 +4249,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             a.mixq_count = sc + 4;
             // k_join_leaf between the stream and mixed kernels: tables with leaf lines, fixed-point
             // coordinates (tiles::raster_code_fixed's chain)
-            const bool leafq = c->leaf_join && ch->raster_stats[6] > 0 && sa.fix_ok;
+            const bool leafq = c->leaf_join && sa.llines && sa.fix_ok;
             if (leafq && (rc = c->mix_queue2.reserve((size_t)rows * 4 + 16))) return rc;
             // the mixed kernel answers its uncertified rows itself: no exact pass after it
             a.exact_inline = 1;
@@ -4202,8 +4304,8 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                     unsigned long long* q2c = sc + 7;
                     HIP_TRY(hipMemsetAsync(q2c, 0, 8, c->stream));
                     void* largs[] = {&ac, &sa, &q2, &q2c};
-                    HIP_TRY(hipLaunchKernel(leaf_kernel(lds, pairs), dim3((unsigned)std::max(1, c->n_cu * 8)), dim3(256), largs,
-                                            lds && !pairs ? shm : 0, c->stream));
+                    HIP_TRY(hipLaunchKernel(leaf_kernel(lds, pairs), dim3((unsigned)std::max(1, c->n_cu * 2)), dim3(256), largs,
+                                            (lds && !pairs ? shm : 0) + 4 * kStageWords * 4, c->stream));
                     ac.mixq = q2;
                     ac.mixq_count = q2c;
                 }

