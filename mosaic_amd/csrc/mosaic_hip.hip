@@ -748,39 +748,28 @@ __global__ void __launch_bounds__(256) k_raster_cells(RBuildArgs a) {
 }
 
 // Leaf lines (tiles_build.cpp, the cell loop of classify_raster_host).  mlist: the kMixed leaf
-// cells (index in `cells`, ascending); first[msb]: the first entry of kind-0 sub-block msb's cells in
-// mlist, -1 when it has none (k_ml_first).  One wave per such sub-block: its candidate hexagons
-// (the window hexagons meeting the sub-block quad, as classify's `cand`) once, then per mixed cell
-// the cell's candidates among them (cand2) and the line fit of k_raster_line_wave over the cell's
-// box with those; ok[m] = 1 and out[m] = the record when one certifies.  (More than 64 sub-block
-// candidates: the window form per cell.)
-__global__ void k_ml_first(const uint32_t* mlist, int64_t n_ml, int64_t CC, int32_t* first) {
-    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= n_ml) return;
-    const int64_t msb = mlist[m] / CC;
-    if (m == 0 || (int64_t)(mlist[m - 1] / CC) != msb) first[msb] = (int32_t)m;
-}
-
-__global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const uint32_t* mlist, int64_t n_ml,
-                                                           const int32_t* first, uint8_t* ok, tiles::LineRec* out) {
+// cells (index in `cells`, ascending).  k_sub_cands: one wave per kind-0 sub-block, its candidate
+// hexagons (the window hexagons meeting the sub-block quad, as classify's `cand`) into
+// cands[64 msb ..], their number in ncand[msb] (-1: more than 64).  k_raster_cell_lines: one wave
+// per mixed cell, the cell's candidates among its sub-block's (cand2, ascending) and the line fit of
+// k_raster_line_wave over the cell's box with those; ok[m] = 1 and out[m] = the record when one
+// certifies.  (One wave per sub-block for all its cells measured slower: 83 ms for NYC res 9, the
+// sub-blocks with hundreds of mixed cells serialise.)
+__global__ void __launch_bounds__(256) k_sub_cands(RBuildArgs a, int32_t* cands, int32_t* ncand) {
     __shared__ int cbuf[4][64];
     const int64_t msb = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (msb >= a.n_cell_sb) return;
-    const int64_t m0 = first[msb];
-    if (m0 < 0) return;
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6) & 3;
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
+    const int64_t SS = (int64_t)a.S * a.S;
     const int64_t g = a.cell_sb[msb];
     const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
     RTile t;
-    const bool tok = rtile_of(a, r, t);
-    rbuild::P2 sq[4];
-    double stol = 0.0;
-    int nsc = 0, sck = -1;
+    int nsc = 0;
     bool over = false;
-    if (tok) {
-        stol = rsub_quad(a, t, si, sj, sq);
+    if (rtile_of(a, r, t)) {
+        rbuild::P2 sq[4];
+        const double stol = rsub_quad(a, t, si, sj, sq);
         const int W = t.wa * t.wb;
         for (int k0 = 0; k0 < W && !over; k0 += 64) {
             const int kl = k0 + lane;
@@ -794,43 +783,59 @@ __global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const u
                 nsc += cnt;
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        sck = lane < nsc ? cbuf[wv][lane] : -1;
-        __builtin_amdgcn_wave_barrier();
     }
-    const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
-    for (int64_t m = m0; m < n_ml && (int64_t)(mlist[m] / CC) == msb; m++) {
-        const int cc = (int)(mlist[m] - msb * CC), cj = cc / a.C, ci = cc - cj * a.C;
-        tiles::LineRec lr{0, 0, 0, 0, 0};
-        bool found = false;
-        if (tok) {
-            const int i0 = si * a.C + ci, j0 = sj * a.C + cj;
-            const rbuild::P2 qc[4] = {rimage(a, t, i0, j0), rimage(a, t, i0 + 1, j0), rimage(a, t, i0 + 1, j0 + 1),
-                                      rimage(a, t, i0, j0 + 1)};
-            // the cell's tolerance as rclassify_rect computes it (tiles_build.cpp classify)
-            const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
-            const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
-            const double ctol = tiles::rect_tol(t.cv, cell_deg_x * 1, cell_deg_y * 1, rbuild::dmax(ex, ey));
-            const double u0 = (double)ci / a.C, v0 = (double)cj / a.C, u1 = (double)(ci + 1) / a.C, v1 = (double)(cj + 1) / a.C;
-            if (over) {
-                found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol);
-            } else {
-                // the cell's candidates: the sub-block's that meet the cell quad, ascending
-                const bool cin = lane < nsc && rbuild::poly_meets_hex(qc, 4, rhex_centre(t, sck), ctol, a.ht);
-                const unsigned long long mk = __ballot(cin);
-                if (cin) cbuf[wv][__popcll(mk & lt_mask)] = sck;
-                __builtin_amdgcn_wave_barrier();
-                const int ncc = __popcll(mk);
-                const int cck = lane < ncc ? cbuf[wv][lane] : -1;
-                __builtin_amdgcn_wave_barrier();
-                found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol, ncc,
-                                       cck);
-            }
+    __builtin_amdgcn_wave_barrier();
+    if (!over && lane < nsc) cands[msb * 64 + lane] = cbuf[wv][lane];
+    if (lane == 0) ncand[msb] = over ? -1 : nsc;
+}
+
+__global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const uint32_t* mlist, int64_t n_ml,
+                                                           const int32_t* cands, const int32_t* ncand, uint8_t* ok,
+                                                           tiles::LineRec* out) {
+    __shared__ int cbuf[4][64];
+    const int64_t m = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (m >= n_ml) return;
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6) & 3;
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
+    const int64_t w = mlist[m];
+    const int64_t msb = w / CC;
+    const int cc = (int)(w - msb * CC), cj = cc / a.C, ci = cc - cj * a.C;
+    const int64_t g = a.cell_sb[msb];
+    const int r = (int)(g / SS), sb = (int)(g - (int64_t)r * SS), sj = sb / a.S, si = sb - sj * a.S;
+    RTile t;
+    tiles::LineRec lr{0, 0, 0, 0, 0};
+    bool found = false;
+    if (rtile_of(a, r, t)) {
+        rbuild::P2 sq[4];
+        const double stol = rsub_quad(a, t, si, sj, sq);
+        const int i0 = si * a.C + ci, j0 = sj * a.C + cj;
+        const rbuild::P2 qc[4] = {rimage(a, t, i0, j0), rimage(a, t, i0 + 1, j0), rimage(a, t, i0 + 1, j0 + 1),
+                                  rimage(a, t, i0, j0 + 1)};
+        // the cell's tolerance as rclassify_rect computes it (tiles_build.cpp classify)
+        const double cell_deg_x = a.tw / a.N, cell_deg_y = a.th / a.N;
+        const double ex = 1e-6 * cell_deg_x + 1e-12 * (fabs(t.lon0) + 1.0);
+        const double ey = 1e-6 * cell_deg_y + 1e-12 * (fabs(t.lat0) + 1.0);
+        const double ctol = tiles::rect_tol(t.cv, cell_deg_x * 1, cell_deg_y * 1, rbuild::dmax(ex, ey));
+        const double u0 = (double)ci / a.C, v0 = (double)cj / a.C, u1 = (double)(ci + 1) / a.C, v1 = (double)(cj + 1) / a.C;
+        const int nsc = ncand[msb];
+        if (nsc < 0) {
+            found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol);
+        } else {
+            // the cell's candidates: the sub-block's that meet the cell quad, ascending
+            const int sck = lane < nsc ? cands[msb * 64 + lane] : -1;
+            const bool cin = lane < nsc && rbuild::poly_meets_hex(qc, 4, rhex_centre(t, sck), ctol, a.ht);
+            const unsigned long long mk = __ballot(cin);
+            if (cin) cbuf[wv][__popcll(mk & lt_mask)] = sck;
+            __builtin_amdgcn_wave_barrier();
+            const int ncc = __popcll(mk);
+            const int cck = lane < ncc ? cbuf[wv][lane] : -1;
+            found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol, ncc, cck);
         }
-        if (lane == 0) {
-            ok[m] = found ? 1 : 0;
-            out[m] = found ? lr : tiles::LineRec{0, 0, 0, 0, 0};
-        }
+    }
+    if (lane == 0) {
+        ok[m] = found ? 1 : 0;
+        out[m] = found ? lr : tiles::LineRec{0, 0, 0, 0, 0};
     }
 }
 
@@ -1830,6 +1835,7 @@ struct Options {
     int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
     int raster_leaf_lines = 0;  // point raster: line records for single-edge leaf cells (leaf lines)
     int leaf_join = 1;        // k_join_leaf answers the mixed queue's leaf-line rows before k_join_mixed
+    int leaf_blocks_per_cu = 2;  // k_join_leaf grid
     int raster_build = 1;     // point raster classification: 1 on the GPU (k_raster_*), 0 on host threads
     int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
@@ -1877,6 +1883,7 @@ struct ThreadCtx : Options {
     DevBuf geo_off, geo_data, dec_x, dec_y, dec_status;  // point geometry decode
     DevBuf ov[8];  // st_intersection_aggregate's cell overlay (run_unit_overlay)
     HostStage hstage;  // pinned staging of the table build's copies (h2d / d2h)
+    DevBuf rbuild[14];  // the raster classification's device scratch, kept between builds (raster_classify_gpu)
     hipStream_t copy_stream = nullptr;
     DevBuf hx[2], hy[2], hcounts;
     binned::Scratch bins;  // the binned join's keys, sorted points and sort temp
@@ -1890,7 +1897,9 @@ struct ThreadCtx : Options {
     std::vector<DevBuf*> scratch() {
         return {&amb_queue, &mix_queue, &mix_queue2, &stage_x, &stage_y, &stage_v, &stage_out, &stage_out2, &stage_idx, &geo_off,
                 &geo_data, &dec_x, &dec_y, &dec_status, &hx[0], &hx[1], &hy[0], &hy[1], &hcounts,
-                &ov[0], &ov[1], &ov[2], &ov[3], &ov[4], &ov[5], &ov[6], &ov[7]};
+                &ov[0], &ov[1], &ov[2], &ov[3], &ov[4], &ov[5], &ov[6], &ov[7], &rbuild[0], &rbuild[1], &rbuild[2],
+                &rbuild[3], &rbuild[4], &rbuild[5], &rbuild[6], &rbuild[7], &rbuild[8], &rbuild[9], &rbuild[10],
+                &rbuild[11], &rbuild[12], &rbuild[13]};
     }
     size_t held() {
         size_t n = 0;
@@ -2299,7 +2308,6 @@ static void warm_up(ThreadCtx* t) {
     void* d = nullptr;
     if (hipMalloc(&d, bytes) != hipSuccess) return;
     std::vector<uint8_t> h(bytes, 0);
-    (void)hipMemcpyAsync(d, h.data(), bytes, hipMemcpyHostToDevice, t->stream);
     (void)h2d(t, d, h.data(), bytes);  // (allocates the build's pinned staging)
     hipLaunchKernelGGL(k_warm_up, dim3((unsigned)std::max(1, t->n_cu * 4)), dim3(256), 0, t->stream, 300000ULL);
     (void)hipGetLastError();
@@ -2434,6 +2442,9 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.raster_leaf_lines = v ? 1 : 0;
     } else if (k == "leaf_join") {
         o.leaf_join = v ? 1 : 0;
+    } else if (k == "leaf_blocks_per_cu") {
+        if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "leaf_blocks_per_cu must be in [1, 64]");
+        o.leaf_blocks_per_cu = (int)v;
     } else if (k == "raster_quad_records") {
         o.raster_quad_records = v ? 1 : 0;
     } else if (k == "raster_build") {
@@ -3046,32 +3057,39 @@ static double ms_since(std::chrono::steady_clock::time_point t0) {
 
 // Build-side phase trace (measurement only): MOSAIC_BUILD_TRACE=1 prints each phase's wall time of
 // a chip-table build to stderr.
-// With the driver's per-process statistics readable, each line also shows the time the process's
-// queues have spent evicted so far (KFD sysfs stats_<gpu>/evicted_ms, summed over GPUs).
-static long long kfd_evicted_ms() {
-    char dir[96];
-    snprintf(dir, sizeof dir, "/sys/class/kfd/kfd/proc/%d", (int)getpid());
-    long long total = -1;
-    if (DIR* d = opendir(dir)) {
+// With the driver's per-process statistics readable, each line also shows the time the queues of
+// every KFD process visible here have spent evicted so far (sysfs proc/<pid>/stats_<gpu>/evicted_ms;
+// the pids are the host's, so all are listed).
+static std::string kfd_evicted_ms() {
+    std::string out;
+    const char* root = "/sys/class/kfd/kfd/proc";
+    if (DIR* d = opendir(root)) {
         while (dirent* e = readdir(d)) {
-            if (strncmp(e->d_name, "stats_", 6) != 0) continue;
-            std::string f = std::string(dir) + "/" + e->d_name + "/evicted_ms";
-            if (FILE* fp = fopen(f.c_str(), "r")) {
-                long long v = 0;
-                if (fscanf(fp, "%lld", &v) == 1) total = (total < 0 ? 0 : total) + v;
-                fclose(fp);
+            if (e->d_name[0] == '.') continue;
+            std::string pdir = std::string(root) + "/" + e->d_name;
+            if (DIR* d2 = opendir(pdir.c_str())) {
+                while (dirent* s = readdir(d2)) {
+                    if (strncmp(s->d_name, "stats_", 6) != 0) continue;
+                    std::string f = pdir + "/" + s->d_name + "/evicted_ms";
+                    if (FILE* fp = fopen(f.c_str(), "r")) {
+                        long long v = 0;
+                        if (fscanf(fp, "%lld", &v) == 1) out += std::string(" ") + e->d_name + ":" + (s->d_name + 6) + "=" + std::to_string(v);
+                        fclose(fp);
+                    }
+                }
+                closedir(d2);
             }
         }
         closedir(d);
     }
-    return total;
+    return out;
 }
 struct BuildTrace {
     bool on = getenv("MOSAIC_BUILD_TRACE") != nullptr;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
     void mark(const char* what) {
         if (!on) return;
-        fprintf(stderr, "[build] %-28s %8.3f ms  (evicted %lld ms)\n", what, ms_since(t), kfd_evicted_ms());
+        fprintf(stderr, "[build] %-28s %8.3f ms  (evicted ms:%s)\n", what, ms_since(t), kfd_evicted_ms().c_str());
         t = std::chrono::steady_clock::now();
     }
 };
@@ -3083,7 +3101,10 @@ struct BuildTrace {
 static void prefault(void* p, size_t bytes) {
     if (bytes < ((size_t)4 << 20)) return;
     const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)4095, a1 = (uintptr_t)p + bytes;
-    (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
+    // (huge pages only on request, MOSAIC_THP=1: collapsing or migrating pages of a range the GPU
+    // driver tracks evicts the process's queues -- see HostStage)
+    static const bool thp = getenv("MOSAIC_THP") && getenv("MOSAIC_THP")[0] == '1';
+    if (thp) (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
     const int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
     std::vector<std::thread> pool;
     for (int t = 0; t < nt; t++)
@@ -3104,7 +3125,9 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     const int64_t n_sub = (int64_t)(n_recs * SS);
     if (tb.tile_of_rec.size() != n_recs || tb.rec_curv.size() != n_recs || !ch->tile_rec.p || !ch->tile_ent.p)
         return fail(MOSAIC_E_ARG, "raster build: tile directory not on the device");
-    TmpBuf d_tor, d_dev, d_code, d_list, d_kind, d_line, d_cells;
+    // (device scratch held by the thread state and reused: a build allocates and frees nothing here)
+    DevBuf &d_tor = c->rbuild[0], &d_dev = c->rbuild[1], &d_code = c->rbuild[2], &d_list = c->rbuild[3],
+           &d_kind = c->rbuild[4], &d_line = c->rbuild[5], &d_cells = c->rbuild[6];
     int e;
     if ((e = d_tor.reserve(std::max<size_t>(n_recs * 4, 16))) || (e = d_dev.reserve(std::max<size_t>(n_recs * sizeof(tiles::TileCurv), 16))) ||
         (e = d_code.reserve(std::max<size_t>((size_t)n_sub * 2, 16))))
@@ -3195,7 +3218,8 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     rc.cline.clear();
     if (!tb.leaf_lines) return MOSAIC_OK;
     // leaf lines: the kMixed cells in index order (hipcub select), one line fit per cell
-    TmpBuf d_ml, d_nml, d_tmp, d_ok, d_lrec;
+    DevBuf &d_ml = c->rbuild[7], &d_nml = c->rbuild[8], &d_tmp = c->rbuild[9], &d_ok = c->rbuild[10],
+           &d_lrec = c->rbuild[11];
     if ((e = d_ml.reserve((size_t)n_cells * 4)) || (e = d_nml.reserve(8))) return e;
     hipcub::CountingInputIterator<uint32_t> idx(0u);
     size_t tmp_bytes = 0;
@@ -3207,15 +3231,15 @@ static int raster_classify_gpu(ThreadCtx* c, const mosaic_chips* ch, const tiles
     int64_t n_ml = 0;
     if ((e = d2h(c, &n_ml, d_nml.p, 8))) return e;
     if (n_ml <= 0) return MOSAIC_OK;
-    TmpBuf d_first;
+    DevBuf &d_cands = c->rbuild[12], &d_ncand = c->rbuild[13];
     if ((e = d_ok.reserve((size_t)n_ml)) || (e = d_lrec.reserve((size_t)n_ml * sizeof(tiles::LineRec))) ||
-        (e = d_first.reserve(cell_sb.size() * 4)))
+        (e = d_cands.reserve(cell_sb.size() * 64 * 4)) || (e = d_ncand.reserve(cell_sb.size() * 4)))
         return e;
-    HIP_TRY(hipMemsetAsync(d_first.p, 0xff, cell_sb.size() * 4, c->stream));
-    hipLaunchKernelGGL(k_ml_first, dim3((unsigned)((n_ml + 255) / 256)), dim3(256), 0, c->stream, (const uint32_t*)d_ml.p,
-                       n_ml, (int64_t)CC, (int32_t*)d_first.p);
-    hipLaunchKernelGGL(k_raster_cell_lines, dim3((unsigned)((cell_sb.size() + 3) / 4)), dim3(256), 0, c->stream, a,
-                       (const uint32_t*)d_ml.p, n_ml, (const int32_t*)d_first.p, (uint8_t*)d_ok.p, (tiles::LineRec*)d_lrec.p);
+    hipLaunchKernelGGL(k_sub_cands, dim3((unsigned)((cell_sb.size() + 3) / 4)), dim3(256), 0, c->stream, a,
+                       (int32_t*)d_cands.p, (int32_t*)d_ncand.p);
+    hipLaunchKernelGGL(k_raster_cell_lines, dim3((unsigned)((n_ml + 3) / 4)), dim3(256), 0, c->stream, a,
+                       (const uint32_t*)d_ml.p, n_ml, (const int32_t*)d_cands.p, (const int32_t*)d_ncand.p,
+                       (uint8_t*)d_ok.p, (tiles::LineRec*)d_lrec.p);
     HIP_TRY(hipGetLastError());
     std::vector<uint32_t> ml((size_t)n_ml);
     std::vector<uint8_t> okv((size_t)n_ml);
@@ -4299,12 +4323,13 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
     hipLaunchKernelGGL(KERNEL, dim3(gm), dim3(c->block), SHM, c->stream, ac)
                 hipEvent_t mstop = nullptr;  // option timing = 2: the mixed kernel is timed too
                 if (c->timing == 2 && lo == 0 && (rc = timing_begin(c, &mstop))) return rc;
+                const int lb = leafq ? std::max(1, c->n_cu * c->leaf_blocks_per_cu) : 0;
                 if (leafq) {
                     uint32_t* q2 = (uint32_t*)c->mix_queue2.p;
                     unsigned long long* q2c = sc + 7;
                     HIP_TRY(hipMemsetAsync(q2c, 0, 8, c->stream));
                     void* largs[] = {&ac, &sa, &q2, &q2c};
-                    HIP_TRY(hipLaunchKernel(leaf_kernel(lds, pairs), dim3((unsigned)std::max(1, c->n_cu * 2)), dim3(256), largs,
+                    HIP_TRY(hipLaunchKernel(leaf_kernel(lds, pairs), dim3((unsigned)lb), dim3(256), largs,
                                             (lds && !pairs ? shm : 0) + 4 * kStageWords * 4, c->stream));
                     ac.mixq = q2;
                     ac.mixq_count = q2c;
@@ -5835,7 +5860,7 @@ static int launch_clip_kernels(ThreadCtx* c, tessgpu::ClipArgs a, int64_t n_task
     std::reverse(sel.begin() + n_small, sel.end());  // large ones in task order
     int e = d_sel.reserve(std::max<size_t>((size_t)n_tasks * 8, 16));
     if (e) return e;
-    if (n_tasks) HIP_TRY(hipMemcpyAsync(d_sel.p, sel.data(), (size_t)n_tasks * 8, hipMemcpyHostToDevice, c->stream));
+    if (n_tasks && (e = h2d(c, d_sel.p, sel.data(), (size_t)n_tasks * 8))) return e;
     if (n_small) {
         a.tsel = (const int64_t*)d_sel.p;
         a.n_sel = n_small;
@@ -5886,7 +5911,7 @@ int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_
     auto up = [&](TmpBuf& b, const void* src, size_t bytes) -> int {
         int e = b.reserve(std::max<size_t>(bytes, 16));
         if (e) return e;
-        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        if (bytes) if (int e_ = h2d(c, b.p, src, bytes)) return e_;
         return MOSAIC_OK;
     };
     if ((rc = up(s_gp, geom_parts, (size_t)(n_geoms + 1) * 8)) || (rc = up(s_pr, part_rings, (size_t)(n_parts + 1) * 8)) ||
@@ -5940,17 +5965,17 @@ int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_
         if (le) return le;
         HIP_TRY(hipEventRecord(e1, c->stream));
         unsigned long long cnt[3];
-        HIP_TRY(hipMemcpyAsync(cnt, s_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(out->redo.data(), s_redo.p, (size_t)n_tasks, hipMemcpyDeviceToHost, c->stream));
+        if (int e_ = d2h(c, cnt, s_cnt.p, sizeof cnt)) return e_;
+        if (int e_ = d2h(c, out->redo.data(), s_redo.p, (size_t)n_tasks)) return e_;
         HIP_TRY(hipStreamSynchronize(c->stream));
         const int64_t nv_out = std::min<int64_t>((int64_t)cnt[0], out_cap), nr = std::min<int64_t>((int64_t)cnt[1], ring_cap),
                       np = std::min<int64_t>((int64_t)cnt[2], part_cap);
         out->verts.resize((size_t)nv_out * 2);
         out->rings.resize((size_t)nr);
         out->parts.resize((size_t)np);
-        if (nv_out) HIP_TRY(hipMemcpyAsync(out->verts.data(), s_out.p, (size_t)nv_out * 16, hipMemcpyDeviceToHost, c->stream));
-        if (nr) HIP_TRY(hipMemcpyAsync(out->rings.data(), s_rings.p, (size_t)nr * sizeof(tessclip::ClipRing), hipMemcpyDeviceToHost, c->stream));
-        if (np) HIP_TRY(hipMemcpyAsync(out->parts.data(), s_parts.p, (size_t)np * sizeof(tessclip::ClipPart), hipMemcpyDeviceToHost, c->stream));
+        if (nv_out) if (int e_ = d2h(c, out->verts.data(), s_out.p, (size_t)nv_out * 16)) return e_;
+        if (nr) if (int e_ = d2h(c, out->rings.data(), s_rings.p, (size_t)nr * sizeof(tessclip::ClipRing))) return e_;
+        if (np) if (int e_ = d2h(c, out->parts.data(), s_parts.p, (size_t)np * sizeof(tessclip::ClipPart))) return e_;
         HIP_TRY(hipStreamSynchronize(c->stream));
         float ms = 0;
         (void)hipEventElapsedTime(&ms, e0, e1);
@@ -6008,7 +6033,7 @@ int tessclip::h3_session_begin(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* 
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
         int e = b.reserve(std::max<size_t>(bytes, 16));
         if (e) return e;
-        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        if (bytes) if (int e_ = h2d(c, b.p, src, bytes)) return e_;
         return MOSAIC_OK;
     };
     int rc;
@@ -6051,7 +6076,7 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
         int e = b.reserve(std::max<size_t>(bytes, 16));
         if (e) return e;
-        if (bytes) HIP_TRY(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        if (bytes) if (int e_ = h2d(c, b.p, src, bytes)) return e_;
         return MOSAIC_OK;
     };
     if ((rc = up(S->d_cg, cand_geom, (size_t)nc * 4)) || (rc = up(S->d_cxy, cxy, (size_t)nc * 16)) ||
@@ -6089,7 +6114,7 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     hipLaunchKernelGGL(tessgpu::k_tess_classify_poly, dim3((unsigned)blocks), dim3(256), 0, c->stream, ca);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev.e[1], c->stream));
-    HIP_TRY(hipMemcpyAsync(cls, S->d_cls.p, (size_t)nc, hipMemcpyDeviceToHost, c->stream));
+    if (int e_ = d2h(c, cls, S->d_cls.p, (size_t)nc)) return e_;
     HIP_TRY(hipStreamSynchronize(c->stream));
     float cms = 0;
     (void)hipEventElapsedTime(&cms, ev.e[0], ev.e[1]);
@@ -6156,17 +6181,17 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
         return rc;
     HIP_TRY(hipEventRecord(ev.e[1], c->stream));
     unsigned long long cnt[3];
-    HIP_TRY(hipMemcpyAsync(cnt, S->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out->redo.data(), S->d_redo.p, (size_t)n_tasks, hipMemcpyDeviceToHost, c->stream));
+    if (int e_ = d2h(c, cnt, S->d_cnt.p, sizeof cnt)) return e_;
+    if (int e_ = d2h(c, out->redo.data(), S->d_redo.p, (size_t)n_tasks)) return e_;
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int64_t nv_out = std::min<int64_t>((int64_t)cnt[0], out_cap), nr = std::min<int64_t>((int64_t)cnt[1], ring_cap),
                   np = std::min<int64_t>((int64_t)cnt[2], part_cap);
     out->verts.resize((size_t)nv_out * 2);
     out->rings.resize((size_t)nr);
     out->parts.resize((size_t)np);
-    if (nv_out) HIP_TRY(hipMemcpyAsync(out->verts.data(), S->d_out.p, (size_t)nv_out * 16, hipMemcpyDeviceToHost, c->stream));
-    if (nr) HIP_TRY(hipMemcpyAsync(out->rings.data(), S->d_rings.p, (size_t)nr * sizeof(ClipRing), hipMemcpyDeviceToHost, c->stream));
-    if (np) HIP_TRY(hipMemcpyAsync(out->parts.data(), S->d_parts.p, (size_t)np * sizeof(ClipPart), hipMemcpyDeviceToHost, c->stream));
+    if (nv_out) if (int e_ = d2h(c, out->verts.data(), S->d_out.p, (size_t)nv_out * 16)) return e_;
+    if (nr) if (int e_ = d2h(c, out->rings.data(), S->d_rings.p, (size_t)nr * sizeof(ClipRing))) return e_;
+    if (np) if (int e_ = d2h(c, out->parts.data(), S->d_parts.p, (size_t)np * sizeof(ClipPart))) return e_;
     HIP_TRY(hipStreamSynchronize(c->stream));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ev.e[0], ev.e[1]);
@@ -6225,7 +6250,7 @@ int mosaic_tess_classify_poly(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* g
     hipLaunchKernelGGL(tessgpu::k_tess_classify_poly, dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(t1, c->stream));
-    HIP_TRY(hipMemcpyAsync(cls, s_cls.p, (size_t)n_cand, hipMemcpyDeviceToHost, c->stream));
+    if (int e_ = d2h(c, cls, s_cls.p, (size_t)n_cand)) return e_;
     HIP_TRY(hipStreamSynchronize(c->stream));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, t0, t1);

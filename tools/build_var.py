@@ -24,26 +24,14 @@ def main():
     t0 = time.perf_counter()
     chips = ctx.grid_tessellateexplode(zones, 9)
     tess = time.perf_counter() - t0
-    def evicted_ms():
-        import glob
-        tot = None
-        for f in glob.glob(f"/sys/class/kfd/kfd/proc/{os.getpid()}/stats_*/evicted_ms"):
-            try:
-                tot = (tot or 0) + int(open(f).read().split()[0])
-            except (OSError, ValueError, IndexError):
-                pass
-        return tot
-
     for r in range(args.reps):
         if args.sleep:
             time.sleep(args.sleep)
-        ev0 = evicted_ms()
         t0 = time.perf_counter()
         table = ctx.chip_table(chips["is_core"], chips["index_id"], chips["wkb"], chips["polygon_key"], 9,
                                n_polygons=len(zones))
         wall = time.perf_counter() - t0
-        ev1 = evicted_ms()
-        print(json.dumps({"rep": r, "evicted_ms": None if ev0 is None else ev1 - ev0, "sleep": args.sleep, "tess_s": round(tess, 4), "build_s": round(wall, 4),
+        print(json.dumps({"rep": r, "sleep": args.sleep, "tess_s": round(tess, 4), "build_s": round(wall, 4),
                           **{k: round(v, 2) for k, v in table.build_info().items() if k.endswith("_ms")}}), flush=True)
         table.close()
 
