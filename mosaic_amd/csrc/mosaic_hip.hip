@@ -1836,6 +1836,7 @@ struct Options {
     int raster_leaf_lines = 0;  // point raster: line records for single-edge leaf cells (leaf lines)
     int leaf_join = 1;        // k_join_leaf answers the mixed queue's leaf-line rows before k_join_mixed
     int leaf_blocks_per_cu = 2;  // k_join_leaf grid
+    int exact_defer = 0;      // stream joins: uncertified rows to k_join_h3_exact after k_join_mixed
     int raster_build = 1;     // point raster classification: 1 on the GPU (k_raster_*), 0 on host threads
     int raster_quad_records = 1;  // point raster: LDS quad records beside the quad level
     int stream_block = 1024;  // k_join_stream workgroup size (a multiple of 64, <= 1024)
@@ -2442,6 +2443,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.raster_leaf_lines = v ? 1 : 0;
     } else if (k == "leaf_join") {
         o.leaf_join = v ? 1 : 0;
+    } else if (k == "exact_defer") {
+        o.exact_defer = v ? 1 : 0;
     } else if (k == "leaf_blocks_per_cu") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "leaf_blocks_per_cu must be in [1, 64]");
         o.leaf_blocks_per_cu = (int)v;
@@ -4275,9 +4278,10 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             // coordinates (tiles::raster_code_fixed's chain)
             const bool leafq = c->leaf_join && sa.llines && sa.fix_ok;
             if (leafq && (rc = c->mix_queue2.reserve((size_t)rows * 4 + 16))) return rc;
-            // the mixed kernel answers its uncertified rows itself: no exact pass after it
-            a.exact_inline = 1;
-            exact_inline = true;
+            // the mixed kernel answers its uncertified rows itself: no exact pass after it (option
+            // exact_defer: it queues them for k_join_h3_exact instead)
+            a.exact_inline = c->exact_defer ? 0 : 1;
+            exact_inline = !c->exact_defer;
             const bool aligned = (((uintptr_t)dx | (uintptr_t)dy) & 15) == 0;
             auto mode_for = [&](bool vec) -> int {
                 // the pipelined forms where they apply (the compacted one, k_join_stream_cpt, carries
