@@ -445,18 +445,22 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     uint32_t* stage = lds + ncw;
     // per-wave compaction buffers: 64 slots x 3 words, structure of arrays
     uint32_t* cbuf_all = stage + nwaves * s.stage_words;
+    // tile bases in LDS (s.tb_lds), or gathered beside the sub-block entry (large tile grids: their
+    // LDS goes to a finer quad level instead)
     uint32_t* tb = cbuf_all + nwaves * kCptBufWords;
-    uint32_t* quadw = tb + s.n_tiles;
+    uint32_t* quadw = tb + (s.tb_lds ? s.n_tiles : 0);
     const uint16_t* quad = (const uint16_t*)quadw;
     uint32_t* qmask = quadw + s.n_quad_words;
     const uint16_t* qcode = (const uint16_t*)(qmask + 2 * s.n_qrec);
     lds_fill(quadw, s.quad, s.n_quad_words);
     lds_fill(qmask, s.qrec, s.n_qrec_words);
-    lds_fill(tb, s.tile_base, s.n_tiles);
+    if (s.tb_lds) lds_fill(tb, s.tile_base, s.n_tiles);
     for (int k = threadIdx.x; k < ncw; k += blockDim.x) lds[k] = 0;
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rsub = stream_rsrc(s.csub, s.csub_bytes);
     const __amdgpu_buffer_rsrc_t rblk = stream_rsrc(s.blocks, s.blocks_bytes);
+    const __amdgpu_buffer_rsrc_t rtb = stream_rsrc(s.tile_base, s.tile_base_bytes);
+    const bool tb_lds = s.tb_lds != 0;
     const int lane = (int)(threadIdx.x & 63);
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -485,12 +489,14 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         }
     };
     // --- set stages
-    // A: the sub-block gather (pending rows: quad entry >= 0x8000)
+    // A: the sub-block gather (pending rows: quad entry >= 0x8000), and without tile bases in LDS
+    // the tile base beside it (carried to B in z.leaf)
     auto set_a = [&](CptSet& z) {
         const uint32_t q = z.c & 0xffffu;
         const uint32_t local = (__builtin_amdgcn_ubfe(z.b, cs + F, qs) << qs) | __builtin_amdgcn_ubfe(z.a, cs + F, qs);
         const uint32_t off = (((q & 0x7fffu) << (2 * qs)) + local) << 1;
         z.code = gather_b16<0>(rsub, q >= 0x8000u, off);
+        if (!tb_lds) z.leaf = gather_b32(rtb, q >= 0x8000u, (z.c >> 16) << 2);
     };
     // B: sub-block entry -> leaf / line gather
     auto set_b = [&](CptSet& z) {
@@ -500,7 +506,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         const bool line = blk && (c & 0x4000u);
         const uint32_t n = c & 0x3fffu;
         const uint32_t lf = (__builtin_amdgcn_ubfe(z.b, (uint32_t)F, cs) << cs) | __builtin_amdgcn_ubfe(z.a, (uint32_t)F, cs);
-        const uint32_t tbv = tb[z.c >> 16];
+        const uint32_t tbv = tb_lds ? tb[z.c >> 16] : z.leaf;
         const uint32_t loff = (tbv + (n << (2 * cs)) + lf) << 1;
         const uint32_t roff = (tbv - 8u * (n + 1u)) << 1;
         z.leaf = gather_b16<0>(rblk, blk && !line, loff);

@@ -1833,6 +1833,7 @@ struct Options {
     int raster_cell = 16;     // point raster: leaf cells per sub-block side (a power of two)
     int raster_quad = 1;      // point raster: LDS quad level
     int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
+    int raster_tb_lds = 1;    // tile bases in the stream kernels' LDS: 1 up to 1/3 of it, 2 only when small (1/16), 0 never
     int raster_leaf_lines = 0;  // point raster: line records for single-edge leaf cells (leaf lines)
     int leaf_join = 1;        // k_join_leaf answers the mixed queue's leaf-line rows before k_join_mixed
     int leaf_blocks_per_cu = 2;  // k_join_leaf grid
@@ -2145,6 +2146,7 @@ struct mosaic_chips {
     uint32_t img_max_words = 0;
     int64_t img_records = 0;  // images built (parts of tile records; tile_images.h)
     int64_t img_count = 0;    // image keys (with the parts that have no image)
+    bool tb_lds_budget = true;  // the build's LDS budget left room for the tile bases (k_join_stream_*)
     int64_t raster_stats[7] = {0, 0, 0, 0, 0, 0, 0};  // S, C, pure sub-blocks, mixed sub-blocks, mixed cells,
                                                       // line sub-blocks, leaf lines
     // build cost (ms): chip table core (hash, geometry, chip rasters), tile directory, point-raster
@@ -2439,6 +2441,9 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.raster_min_segments = (int)v;
     } else if (k == "raster_lines") {
         o.raster_lines = v ? 1 : 0;
+    } else if (k == "raster_tb_lds") {
+        if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "raster_tb_lds must be 0, 1 or 2");
+        o.raster_tb_lds = (int)v;
     } else if (k == "raster_leaf_lines") {
         o.raster_leaf_lines = v ? 1 : 0;
     } else if (k == "leaf_join") {
@@ -3762,8 +3767,13 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 // beside its counts, its per-wave stages (1024 threads) and, when small, tile_base
                 size_t avail = kStreamLdsMax - 16 * kStageWords * 4 - 1024 -
                                (n_polygons <= kLdsCountsMax ? ((size_t)n_polygons + 64) * 4 : 0);
+                // (option raster_tb_lds 2 / 0: the tile bases of a large tile grid out of LDS, a finer
+                // quad level in their place, k_join_stream_cpt gathering the tile base beside the
+                // sub-block entry -- at C3 quad shift 6 -> 5, pending rows 28 % -> 18 %, but the extra
+                // gathers cost more than the saved ones: stream 3.80 -> 3.87 ms)
                 const size_t tbytes = tb.tile_idx.size() * 4;
-                if (tbytes <= avail / 3) avail -= tbytes;
+                ch->tb_lds_budget = c->raster_tb_lds == 1 ? tbytes <= avail / 3 : (c->raster_tb_lds == 2 && tbytes <= avail / 16);
+                if (ch->tb_lds_budget) avail -= tbytes;
                 // quad level in at most half of it, quad records in the rest (option raster_quad_records)
                 if (c->raster_quad_records && c->raster_quad == 1) {
                     tb.quad_max = (int)std::min<size_t>(tiles::kQuadLimit, avail / 4);
@@ -4179,7 +4189,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
         const int blk = c->stream_block;
         size_t shm_s = (lds && !pairs ? ((size_t)ch->n_polygons + 64) * 4 : 0) + (size_t)(blk / 64) * sa.stage_words * 4 +
                        (size_t)sa.n_quad_words * 4 + (size_t)sa.n_qrec_words * 4;
-        sa.tb_lds = shm_s + (size_t)sa.n_tiles * 4 <= kStreamLdsMax ? 1 : 0;
+        sa.tb_lds = ch->tb_lds_budget && shm_s + (size_t)sa.n_tiles * 4 <= kStreamLdsMax ? 1 : 0;
         if (sa.tb_lds) shm_s += (size_t)sa.n_tiles * 4;
         const bool stream = praster && ch->stream_ok && shm_s <= kStreamLdsMax;
         // border-chip-heavy tables (no point raster to stream): points binned by tile first
@@ -4287,10 +4297,12 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 // the pipelined forms where they apply (the compacted one, k_join_stream_cpt, carries
                 // cs + kFixBits + qs <= 24 low bits of the fine-cell coordinates and a 16-bit tile index
                 // per pending row, and per wave a kCptBufWords compaction buffer in LDS)
-                int mode = vec && sa.tb_lds && sa.fix_ok ? c->stream_pipe : 0;
+                // (k_join_stream_pipe reads tile bases from LDS; k_join_stream_cpt from LDS or memory)
+                int mode = vec && sa.fix_ok ? c->stream_pipe : 0;
                 if (mode >= 2 && !(sa.cs + tiles::kFixBits + sa.qs <= 24 && sa.n_tiles <= 65536 &&
                                    shm_s + (size_t)(blk / 64) * kCptBufWords * 4 <= kStreamLdsMax))
                     mode = 1;
+                if (mode == 1 && !sa.tb_lds) mode = 0;
                 return mode;
             };
             auto kernel_for = [&](bool vec) -> const void* { return stream_kernel_h3(mode_for(vec), lds, pairs, vec); };

@@ -85,6 +85,15 @@ int main(int argc, char** argv) {
         fprintf(stderr, "directory not built: %s\n", tb.why);
         return 1;
     }
+    if (getenv("DEVICE_QUAD")) {
+        // the quad-level budget of a chip table built for the stream kernels (mosaic_hip.hip): the
+        // LDS of one 1024-thread workgroup beside its counts, stages and (when small) tile_base
+        size_t avail = 160 * 1024 - 16 * 128 * 4 - 1024 - ((size_t)npoly + 64) * 4;
+        const size_t tbytes = tb.tile_idx.size() * 4;
+        if (tbytes <= avail / 3 && !getenv("NO_TB_LDS")) avail -= tbytes;
+        tb.quad_max = (int)std::min<size_t>(tiles::kQuadLimit, avail / 4);
+        tb.quad_lds_bytes = avail;
+    }
     auto t1 = std::chrono::steady_clock::now();
     tiles::Builder::ChipSource src;
     src.slot_first = slot_first.data();
@@ -273,5 +282,82 @@ int main(int argc, char** argv) {
            "line %.4f (mixed band %.5f), leaf %.4f (mixed cell %.5f)\n",
            npts, (double)c_out / npts, (double)c_quad / npts, (double)c_sub / npts, (double)c_submixed / npts,
            (double)c_line / npts, (double)c_line_mixed / npts, (double)c_leaf / npts, (double)c_leaf_mixed / npts);
+    // POINTS=file (float64 x[n] then y[n]): the stream kernel's groups of 256 consecutive rows --
+    // rows whose quad entry (after the quad records) is not a code are "pending" (k_join_stream_cpt
+    // compacts them into 64-row sets: P <= 64 one pipelined set, <= 128 two, more: unpipelined sets)
+    if (const char* pf = getenv("POINTS")) {
+        FILE* fp = fopen(pf, "rb");
+        if (!fp) return 4;
+        fseek(fp, 0, SEEK_END);
+        const long nb = ftell(fp);
+        fseek(fp, 0, SEEK_SET);
+        const size_t np = (size_t)nb / 16;
+        std::vector<double> px(np), py(np);
+        if (fread(px.data(), 8, np, fp) != np || fread(py.data(), 8, np, fp) != np) return 4;
+        fclose(fp);
+        tiles::PointRaster pr{};
+        pr.sub = tb.sub.data();
+        pr.tile_base = tb.tile_base.data();
+        pr.blocks = tb.blocks.data();
+        pr.sx = tb.grid.sx * S;
+        pr.sy = tb.grid.sy * S;
+        pr.nx = (int32_t)NX;
+        pr.ny = (int32_t)NY;
+        pr.C = C;
+        pr.sshift = tb.sshift;
+        pr.tnx = tb.grid.nx;
+        pr.cshift = tb.cshift;
+        pr.quad = tb.quad.data();
+        pr.qnx = tb.qnx;
+        pr.qny = tb.qny;
+        pr.qshift = tb.qshift;
+        pr.qrec_mask = tb.qrec_mask.empty() ? nullptr : tb.qrec_mask.data();
+        pr.qrec_code = tb.qrec_code.empty() ? nullptr : tb.qrec_code.data();
+        pr.n_qrec = (int32_t)tb.qrec_code.size();
+        pr.qrec_shift = tb.qrec_shift;
+        const int F = tiles::kFixBits;
+        const double ax = pr.sx * C * (double)(1 << F), ay = pr.sy * C * (double)(1 << F);
+        const double bx = -tb.grid.x0 * ax, by = -tb.grid.y0 * ay;
+        const uint32_t gxmax = (uint32_t)(((int64_t)NX * C - 1) << F), gymax = (uint32_t)(((int64_t)NY * C - 1) << F);
+        long groups = 0, g64 = 0, g128 = 0, pend = 0, line = 0, leaf = 0, mixed = 0, extra_sets = 0;
+        long hist[5] = {0, 0, 0, 0, 0};  // P: 0, 1-16, 17-64, 65-128, > 128
+        for (size_t g0 = 0; g0 + 256 <= np; g0 += 256) {
+            int P = 0;
+            for (size_t r = g0; r < g0 + 256; r++) {
+                uint32_t gix = tiles::fix_cvt(fma(px[r], ax, bx)), giy = tiles::fix_cvt(fma(py[r], ay, by));
+                gix = gix > gxmax ? gxmax : gix;
+                giy = giy > gymax ? gymax : giy;
+                const int ixC = (int)(gix >> F), iyC = (int)(giy >> F), ix = ixC >> tb.cshift, iy = iyC >> tb.cshift;
+                uint32_t q = pr.quad[(uint32_t)(iy >> pr.qshift) * (uint32_t)pr.qnx + (uint32_t)(ix >> pr.qshift)];
+                if (q >= tiles::kSubBlock && (q & 0x7fffu) < (uint32_t)pr.n_qrec) {
+                    const uint32_t rr = q & 0x7fffu;
+                    const uint32_t b = (uint32_t)((((iy >> pr.qrec_shift) & 7) << 3) | ((ix >> pr.qrec_shift) & 7));
+                    if ((pr.qrec_mask[2 * rr + (b >> 5)] >> (b & 31)) & 1u) q = pr.qrec_code[rr];
+                }
+                if (q < tiles::kSubBlock) continue;
+                P++;
+                const int qm = (1 << pr.qshift) - 1;
+                const uint32_t e = pr.sub[(size_t)pr.nx * pr.ny + ((size_t)(q & 0x7fffu) << (2 * pr.qshift)) +
+                                          (size_t)(((iy & qm) << pr.qshift) | (ix & qm))];
+                if (tiles::sub_is_block(e)) (e & tiles::kLineBit) ? line++ : leaf++;
+                const uint16_t code = tiles::raster_code_fixed(pr, ax, bx, ay, by, gxmax, gymax, px[r], py[r]);
+                mixed += code == tiles::kMixed;
+            }
+            groups++;
+            pend += P;
+            g64 += P > 64;
+            g128 += P > 128;
+            if (P > 128) extra_sets += (P + 63) / 64 - 2;
+            hist[P == 0 ? 0 : (P <= 16 ? 1 : (P <= 64 ? 2 : (P <= 128 ? 3 : 4)))]++;
+        }
+        printf("points %zu in %ld groups of 256: pending rows (sub-block gathers) %.4f per point; groups with "
+               "P > 64 (second set) %.4f, P > 128 (unpipelined sets) %.4f, unpipelined sets per group %.4f; "
+               "P histogram 0 / 1-16 / 17-64 / 65-128 / >128: %.4f %.4f %.4f %.4f %.4f; line gathers %.4f, leaf "
+               "gathers %.4f, mixed rows %.5f per point\n",
+               np, groups, (double)pend / (groups * 256.0), (double)g64 / groups, (double)g128 / groups,
+               (double)extra_sets / groups, (double)hist[0] / groups, (double)hist[1] / groups, (double)hist[2] / groups,
+               (double)hist[3] / groups, (double)hist[4] / groups, (double)line / (groups * 256.0),
+               (double)leaf / (groups * 256.0), (double)mixed / (groups * 256.0));
+    }
     return 0;
 }
