@@ -26,6 +26,7 @@
 #include <string>
 #include <sys/mman.h>
 #include <dirent.h>
+#include <sys/prctl.h>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -2318,8 +2319,22 @@ static void warm_up(ThreadCtx* t) {
     (void)hipFree(d);
 }
 
+// Transparent huge pages off for the process (unless MOSAIC_THP=1): khugepaged collapsing pages of a
+// range the GPU driver tracks evicts every queue of the process for tens of ms -- measured on the
+// table build (build side: 21.6-23.4 ms raster classification without, 70-84 ms with
+// huge pages; the first geometry upload 0.5 vs 12.5 ms).  Boxes whose kernel setting is "always"
+// would collapse pages without any advice, so the process opts out once, at its first context.
+static void thp_off_once() {
+    static std::once_flag once;
+    std::call_once(once, []() {
+        const char* e = getenv("MOSAIC_THP");
+        if (!(e && e[0] == '1')) (void)prctl(PR_SET_THP_DISABLE, 1, 0, 0, 0);
+    });
+}
+
 int mosaic_init(int device, mosaic_ctx** out) {
     if (!out) return fail(MOSAIC_E_ARG, "out is null");
+    thp_off_once();
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(MOSAIC_E_HIP, "no HIP device available");
     if (device < 0 || device >= count) return fail(MOSAIC_E_ARG, "device ordinal out of range");
@@ -5427,6 +5442,7 @@ struct ClassifyPolyArgs {
     const int32_t* cand_geom;
     const double* clip;  // [n_cand][nv][2]
     int nv;
+    const int32_t* clip_n;  // per candidate: its clip polygon's vertices (<= nv); nullptr: nv each
     int64_t n_cand;
     double eps;
     uint8_t* cls;
@@ -5438,6 +5454,7 @@ __global__ void __launch_bounds__(256) k_tess_classify_poly(ClassifyPolyArgs a) 
     for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < a.n_cand; c += n_waves) {
         const int g = a.cand_geom[c];
         const double* P = a.clip + 2 * (int64_t)a.nv * c;
+        const int nvk = a.clip_n ? a.clip_n[c] : a.nv;
         const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
         bool near = false;
         for (int64_t p = p0; p < p1 && !near; p++)
@@ -5446,7 +5463,7 @@ __global__ void __launch_bounds__(256) k_tess_classify_poly(ClassifyPolyArgs a) 
                 bool hit = false;
                 for (int64_t v = lane; v + 1 < n && !hit; v += 64) {
                     const double* s = a.xy + 2 * (b + v);
-                    hit = seg_near_poly(s[0], s[1], s[2], s[3], P, a.nv, a.eps);
+                    hit = seg_near_poly(s[0], s[1], s[2], s[3], P, nvk, a.eps);
                 }
                 if (__ballot(hit)) {
                     near = true;
@@ -5456,12 +5473,12 @@ __global__ void __launch_bounds__(256) k_tess_classify_poly(ClassifyPolyArgs a) 
         uint8_t out = 2;
         if (!near) {
             double cx = 0, cy = 0;  // centroid of the clip vertex list, summed in order as the host does
-            for (int i = 0; i < a.nv; i++) {
+            for (int i = 0; i < nvk; i++) {
                 cx += P[2 * i];
                 cy += P[2 * i + 1];
             }
-            cx /= (double)a.nv;
-            cy /= (double)a.nv;
+            cx /= (double)nvk;
+            cy /= (double)nvk;
             bool inside = false;
             for (int64_t p = p0; p < p1 && !inside; p++) {
                 bool par = false;
@@ -5497,6 +5514,7 @@ struct ClipArgs {
     const int32_t* gface;
     const double* clip;
     int nv, res, mode;
+    const int32_t* clip_n;  // per candidate: its clip polygon's vertices (<= nv, stride nv); nullptr: nv
     double area_eps;
     const int64_t* tasks;
     int64_t n_tasks;
@@ -5625,6 +5643,7 @@ __global__ void __launch_bounds__(256) k_tess_clip(ClipArgs a) {
         const int64_t k = a.tasks[t];
         const int g = a.cand_geom[k];
         const double* P = a.clip + 2 * (int64_t)a.nv * k;
+        const int nvk = a.clip_n ? a.clip_n[k] : a.nv;
         const int face = a.mode == 0 ? a.gface[g] : 0;
         bool redo = false;
         const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
@@ -5648,8 +5667,8 @@ __global__ void __launch_bounds__(256) k_tess_clip(ClipArgs a) {
                 wave_sync_global();
                 int cur = 0;
                 int64_t m = n;
-                for (int e = 0; e < a.nv && m > 0; e++) {
-                    const int f = e + 1 == a.nv ? 0 : e + 1;
+                for (int e = 0; e < nvk && m > 0; e++) {
+                    const int f = e + 1 == nvk ? 0 : e + 1;
                     m = clip_pass(bxy[cur], btag[cur], m, P[2 * e], P[2 * e + 1], P[2 * f], P[2 * f + 1], bxy[cur ^ 1],
                                   btag[cur ^ 1], a.cap);
                     wave_sync_global();
@@ -5735,8 +5754,9 @@ __global__ void __launch_bounds__(256) k_tess_clip_lane(ClipArgs a) {
         const int64_t k = a.tasks[t];
         const int g = a.cand_geom[k];
         const double* P = a.clip + 2 * (int64_t)a.nv * k;
+        const int nvk = a.clip_n ? a.clip_n[k] : a.nv;
         const int face = a.mode == 0 ? a.gface[g] : 0;
-        bool redo = a.nv > kClipLaneClip;
+        bool redo = nvk > kClipLaneClip;
         const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
         for (int64_t p = p0; p < p1 && !redo; p++) {
             bool any = false;
@@ -5757,8 +5777,8 @@ __global__ void __launch_bounds__(256) k_tess_clip_lane(ClipArgs a) {
                 }
                 int cur = 0;
                 int64_t m = n;
-                for (int e = 0; e < a.nv && m > 0; e++) {
-                    const int f = e + 1 == a.nv ? 0 : e + 1;
+                for (int e = 0; e < nvk && m > 0; e++) {
+                    const int f = e + 1 == nvk ? 0 : e + 1;
                     const double ax = P[2 * e], ay = P[2 * e + 1], bx_ = P[2 * f], by_ = P[2 * f + 1];
                     int64_t o = 0;
                     for (int64_t i = 0; i < m; i++) {
@@ -5951,6 +5971,7 @@ int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_
     a.gface = (const int32_t*)s_gf.p;
     a.clip = (const double*)s_clip.p;
     a.nv = nv;
+    a.clip_n = nullptr;
     a.res = res;
     a.mode = mode;
     a.area_eps = area_eps;
@@ -6014,11 +6035,11 @@ struct tessclip::H3Session {
     const int64_t *geom_parts, *part_rings, *ring_offsets;
     int res, D;
     double dx[6], dy[6];
-    DevBuf d_gp, d_pr, d_ro, d_pxy, d_gxy, d_gf, d_cg, d_cxy, d_clip, d_cls, d_tasks;
+    DevBuf d_gp, d_pr, d_ro, d_pxy, d_gxy, d_gf, d_cg, d_cxy, d_clip, d_cls, d_tasks, d_cn;
     DevBuf d_sxy, d_stag, d_out, d_cnt, d_rings, d_parts, d_redo, d_sel;
     void release() {
         for (DevBuf* b : {&d_gp, &d_pr, &d_ro, &d_pxy, &d_gxy, &d_gf, &d_cg, &d_cxy, &d_clip, &d_cls, &d_tasks, &d_sxy, &d_stag,
-                          &d_out, &d_cnt, &d_rings, &d_parts, &d_redo, &d_sel})
+                          &d_out, &d_cnt, &d_rings, &d_parts, &d_redo, &d_sel, &d_cn})
             b->release();
     }
 };
@@ -6077,9 +6098,11 @@ void tessclip::h3_session_end(H3Session* S) {
 }
 
 int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geom, const double* cxy, double eps,
-                               double area_eps, uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out) {
+                               double area_eps, uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out,
+                               const double* clip_xy, const int32_t* clip_n, int nv_max) {
     ENTER(S->ctx);
-    const int nv = 6 * S->D;
+    const bool given = clip_xy != nullptr;  // explicit clip polygons (face pieces) instead of hexagons
+    const int nv = given ? nv_max : 6 * S->D;
     tasks.clear();
     out->redo.clear();
     out->rings.clear();
@@ -6095,9 +6118,14 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
         if (bytes) if (int e_ = h2d(c, b.p, src, bytes)) return e_;
         return MOSAIC_OK;
     };
-    if ((rc = up(S->d_cg, cand_geom, (size_t)nc * 4)) || (rc = up(S->d_cxy, cxy, (size_t)nc * 16)) ||
-        (rc = S->d_clip.reserve((size_t)nc * nv * 16)) || (rc = S->d_cls.reserve((size_t)nc)))
+    if ((rc = up(S->d_cg, cand_geom, (size_t)nc * 4)) || (rc = S->d_clip.reserve((size_t)nc * nv * 16)) ||
+        (rc = S->d_cls.reserve((size_t)nc)))
         return rc;
+    if (given) {
+        if ((rc = up(S->d_clip, clip_xy, (size_t)nc * nv * 16)) || (rc = up(S->d_cn, clip_n, (size_t)nc * 4))) return rc;
+    } else if ((rc = up(S->d_cxy, cxy, (size_t)nc * 16))) {
+        return rc;
+    }
     tessgpu::FillClipArgs fa;
     fa.cxy = (const double*)S->d_cxy.p;
     fa.n_cand = nc;
@@ -6108,8 +6136,9 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     }
     fa.clip = (double*)S->d_clip.p;
     const int64_t nfill = nc * nv;
-    hipLaunchKernelGGL(tessgpu::k_tess_fill_clip, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((nfill + 255) / 256, 1 << 20))),
-                       dim3(256), 0, c->stream, fa);
+    if (!given)
+        hipLaunchKernelGGL(tessgpu::k_tess_fill_clip, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((nfill + 255) / 256, 1 << 20))),
+                           dim3(256), 0, c->stream, fa);
     HIP_TRY(hipGetLastError());
     tessgpu::ClassifyPolyArgs ca;
     ca.xy = (const double*)S->d_pxy.p;
@@ -6119,6 +6148,7 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     ca.cand_geom = (const int32_t*)S->d_cg.p;
     ca.clip = (const double*)S->d_clip.p;
     ca.nv = nv;
+    ca.clip_n = given ? (const int32_t*)S->d_cn.p : nullptr;
     ca.n_cand = nc;
     ca.eps = eps;
     ca.cls = (uint8_t*)S->d_cls.p;
@@ -6173,6 +6203,7 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     a.gface = (const int32_t*)S->d_gf.p;
     a.clip = (const double*)S->d_clip.p;
     a.nv = nv;
+    a.clip_n = given ? (const int32_t*)S->d_cn.p : nullptr;
     a.res = S->res;
     a.mode = 0;
     a.area_eps = area_eps;
@@ -6254,6 +6285,7 @@ int mosaic_tess_classify_poly(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* g
     a.cand_geom = (const int32_t*)dcg;
     a.clip = (const double*)dclip;
     a.nv = nv;
+    a.clip_n = nullptr;
     a.n_cand = n_cand;
     a.eps = eps;
     a.cls = (uint8_t*)s_cls.p;

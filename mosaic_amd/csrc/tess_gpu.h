@@ -50,8 +50,12 @@ struct H3Session;
 int h3_session_begin(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                      const int64_t* ring_offsets, const double* pxy, const double* gxy, const int32_t* gface, int res, int D,
                      const double* dx, const double* dy, H3Session** out);
+// clip_xy / clip_n / nv_max: explicit clip polygons instead of the hexagons of cxy (the per-face
+// pieces of cells of face-spanning geometries): clip_n[k] open counter-clockwise vertices of
+// candidate k at clip_xy + 2 nv_max k.
 int h3_session_chunk(H3Session* s, int64_t n_cand, const int32_t* cand_geom, const double* cxy, double eps,
-                     double area_eps, uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out);
+                     double area_eps, uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out,
+                     const double* clip_xy = nullptr, const int32_t* clip_n = nullptr, int nv_max = 0);
 void h3_session_end(H3Session* s);
 
 }  // namespace tessclip

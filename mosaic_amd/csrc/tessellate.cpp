@@ -519,23 +519,38 @@ double open_area(const std::vector<P2>& r) {
     return 0.5 * a;
 }
 
-// Chips of geometry g (lon/lat rings geo) that spans faces: 0, or MOSAIC_E_ARG for geometries no
-// face plane can hold (a vertex more than ~78 degrees from a face centre whose territory it meets).
-int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, int keep_core_geom,
-                            const std::vector<std::vector<std::vector<P2>>>& geo) {
-    struct Piece {
-        int face, cls;
-        Cell cell;
-        std::vector<std::vector<std::vector<P2>>> parts;  // border: the clipped geometry
-    };
-    std::vector<int64_t> order;  // cell ids in first-seen order (faces ascending, lattice order)
-    std::vector<std::vector<Piece>> pieces;
+using Geo3 = std::vector<std::vector<std::vector<P2>>>;  // parts -> rings -> points
+
+// The per-face pieces of one face-spanning geometry: made by multiface_pieces, classified and
+// clipped by multiface_classify_host (tessellate_h3_multiface) or on the GPU (mosaic_tessellate_gpu,
+// the same arithmetic), turned into chips by multiface_emit.
+struct MultiPiece {
+    int face, cls = -1;
+    Cell cell;
+    Geo3 parts;  // border: the clipped geometry
+};
+struct MultiFace {
+    std::vector<int64_t> order;                   // cell ids in first-seen order (faces ascending, lattice order)
+    std::vector<std::vector<size_t>> slot_pieces;  // per cell id: its pieces (indices into pieces)
+    std::vector<MultiPiece> pieces;
+    std::vector<int> faces;                       // faces with pieces, ascending
+    std::vector<Geo3> pl;                         // per face of `faces`: the geometry in its plane
+    int face_slot(int f) const {
+        for (size_t k = 0; k < faces.size(); k++)
+            if (faces[k] == f) return (int)k;
+        return -1;
+    }
+};
+
+// Pieces of geometry geo (lon/lat rings) that spans faces: 0, or MOSAIC_E_ARG for geometries no face
+// plane can hold (a vertex more than ~78 degrees from a face centre whose territory it meets).
+int multiface_pieces(int res, int D, const Geo3& geo, MultiFace& mf) {
     std::unordered_map<int64_t, size_t> index;  // id -> slot (O(1) per piece: country-scale inputs)
     auto slot_of = [&](int64_t id) -> size_t {
-        auto ins = index.emplace(id, order.size());
+        auto ins = index.emplace(id, mf.order.size());
         if (ins.second) {
-            order.push_back(id);
-            pieces.emplace_back();
+            mf.order.push_back(id);
+            mf.slot_pieces.emplace_back();
         }
         return ins.first->second;
     };
@@ -591,6 +606,8 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
         }
         if (!(met > 1e-12)) continue;
         faces_used++;
+        mf.faces.push_back(f);
+        mf.pl.push_back(pl);
         P2 tc[3];
         ft.corners(tc);
         double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
@@ -633,22 +650,41 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
                 h3::ijk_normalize(ijk);
                 const int64_t id = (int64_t)h3::face_ijk_to_h3(f, ijk, res);
                 if (id == 0) return MOSAIC_E_ARG;  // (a lattice cell H3 has no id for: not expected)
-                Piece pc;
+                MultiPiece pc;
                 pc.face = f;
                 pc.cell.id = id;
                 pc.cell.clip = hex;
                 pc.cell.outline = hex;
-                pc.cls = classify_cell(pc.cell, pl, 1e-3);
-                if (pc.cls == 2) clip_cell(pc.cell, pl, geo, [&](P2 h) { return fp.to_geo(h); }, 1e-12, pc.parts);
-                pieces[slot_of(id)].push_back(std::move(pc));
+                mf.slot_pieces[slot_of(id)].push_back(mf.pieces.size());
+                mf.pieces.push_back(std::move(pc));
             }
         }
     }
-    if (faces_used == 0) return MOSAIC_OK;
-    for (size_t k = 0; k < order.size(); k++) {
-        const std::vector<Piece>& ps = pieces[k];
+    return MOSAIC_OK;
+}
+
+// classify_cell and clip_cell of every piece against the geometry in its face's plane
+void multiface_classify_host(MultiFace& mf, const Geo3& geo, int res) {
+    for (size_t k = 0; k < mf.faces.size(); k++) {
+        FacePlane fp;
+        fp.init(mf.faces[k], res);
+        for (MultiPiece& pc : mf.pieces) {
+            if (pc.face != mf.faces[k]) continue;
+            pc.cls = classify_cell(pc.cell, mf.pl[k], 1e-3);
+            if (pc.cls == 2) clip_cell(pc.cell, mf.pl[k], geo, [&](P2 h) { return fp.to_geo(h); }, 1e-12, pc.parts);
+        }
+    }
+}
+
+// The chips of the classified pieces, in cell first-seen order.
+void multiface_emit(mosaic_chip_set* cs, int32_t key, int res, int keep_core_geom, const MultiFace& mf) {
+    for (size_t k = 0; k < mf.order.size(); k++) {
+        std::vector<const MultiPiece*> ps;
+        for (size_t q : mf.slot_pieces[k]) ps.push_back(&mf.pieces[q]);
+        const std::vector<int64_t>& order = mf.order;
         bool all_core = true, any = false;
-        for (const Piece& p : ps) {
+        for (const MultiPiece* pp : ps) {
+            const MultiPiece& p = *pp;
             all_core = all_core && p.cls == 1;
             any = any || p.cls == 1 || (p.cls == 2 && !p.parts.empty());
         }
@@ -662,7 +698,7 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
             if (keep_core_geom) {
                 double b[20];
                 const int nb = h3geom::h3_to_geo_boundary((uint64_t)order[k], b);
-                if (nb < 3) return MOSAIC_E_ARG;
+                if (nb < 3) continue;  // (not expected: a valid H3 id)
                 std::vector<P2> ring;
                 for (int v = 0; v <= nb; v++) {
                     const int q = v % nb;
@@ -675,7 +711,8 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
         }
         int face_mask_n = 0;
         uint32_t face_mask = 0;
-        for (const Piece& p : ps) {
+        for (const MultiPiece* pp : ps) {
+            const MultiPiece& p = *pp;
             const size_t before = parts.size();
             if (p.cls == 1) {
                 FacePlane fp;
@@ -725,6 +762,15 @@ int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, in
         }
         cs->add(false, order[k], key, to_wkb(parts));
     }
+}
+
+// Chips of geometry g (lon/lat rings geo) that spans faces, on the host: 0, or MOSAIC_E_ARG (see
+// multiface_pieces).
+int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, int keep_core_geom, const Geo3& geo) {
+    MultiFace mf;
+    if (int rc = multiface_pieces(res, D, geo, mf)) return rc;
+    multiface_classify_host(mf, geo, res);
+    multiface_emit(cs, key, res, keep_core_geom, mf);
     return MOSAIC_OK;
 }
 
