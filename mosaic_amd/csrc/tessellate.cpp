@@ -805,6 +805,26 @@ struct ClippedChips {
         for (size_t t = 0; t < tasks.size(); t++) task_of[(size_t)tasks[t]] = (int64_t)t;
     }
     bool redo(int64_t k) const { return task_of[(size_t)k] < 0 || r.redo[(size_t)task_of[(size_t)k]]; }
+    // candidate k's clipped geometry as clip_cell's out_parts (kept parts with rings, closed rings)
+    void parts_of(int64_t k, Geo3& out) const {
+        out.clear();
+        size_t jr = (size_t)ring_at[(size_t)k];
+        for (size_t jp = (size_t)part_at[(size_t)k]; jp < r.parts.size() && r.parts[jp].cand == k; jp++) {
+            const int32_t part = r.parts[jp].part;
+            while (jr < r.rings.size() && r.rings[jr].cand == k && r.rings[jr].part < part) jr++;
+            const size_t r0 = jr;
+            while (jr < r.rings.size() && r.rings[jr].cand == k && r.rings[jr].part == part) jr++;
+            if (!r.parts[jp].keep || jr == r0) continue;
+            std::vector<std::vector<P2>> rings;
+            for (size_t q = r0; q < jr; q++) {
+                const tessclip::ClipRing& cr = r.rings[q];
+                std::vector<P2> ring((size_t)cr.n);
+                for (int32_t v = 0; v < cr.n; v++) ring[(size_t)v] = {r.verts[2 * (cr.off + v)], r.verts[2 * (cr.off + v) + 1]};
+                rings.push_back(std::move(ring));
+            }
+            out.push_back(std::move(rings));
+        }
+    }
     // candidate k's chip as WKB appended to w (to_wkb's bytes); false (nothing written): no chip
     template <class W>
     bool chip(int64_t k, W& w) const {
@@ -847,6 +867,118 @@ struct ClippedChips {
         return true;
     }
 };
+
+// The face-spanning geometries' chips on the device (mosaic_tessellate_gpu): per-face pieces made on
+// host threads (multiface_pieces), then one session over virtual geometries -- (geometry, face): the
+// geometry's rings in that face's plane (MultiFace::pl, the host routine's doubles) and in lon / lat,
+// computed vertices mapped back through that face -- with the pieces as explicit clip polygons,
+// classified and clipped by the same kernels as the single-face cells (k_tess_classify_poly /
+// k_tess_clip: tessellate.cpp's classify_cell / clip_cell arithmetic), so multiface_emit writes the
+// host routine's chips.  Tasks the kernels hand back (scratch) are clipped on the host.
+int multiface_gpu(mosaic_ctx* ctx, const std::vector<int64_t>& multi_geoms, const int64_t* geom_parts,
+                  const int64_t* part_rings, const int64_t* ring_offsets, const double* xy, int res, int D,
+                  std::vector<MultiFace>& mfs) {
+    const size_t nm = multi_geoms.size();
+    std::vector<Geo3> geos(nm);
+    std::atomic<size_t> next(0);
+    std::atomic<int> bad(0);
+    auto work = [&]() {
+        for (size_t m; (m = next.fetch_add(1)) < nm;) {
+            const int64_t g = multi_geoms[m];
+            for (int64_t p = geom_parts[g]; p < geom_parts[g + 1]; p++) {
+                std::vector<std::vector<P2>> rings;
+                for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
+                    std::vector<P2> ring;
+                    for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) ring.push_back({xy[2 * v], xy[2 * v + 1]});
+                    rings.push_back(std::move(ring));
+                }
+                geos[m].push_back(std::move(rings));
+            }
+            if (multiface_pieces(res, D, geos[m], mfs[m])) bad = 1;
+        }
+    };
+    {
+        const int nt = (int)std::max<size_t>(1, std::min<size_t>(std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())), nm));
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
+    }
+    if (bad) return mosaic_tess_fail(MOSAIC_E_ARG, "geometry too large for a gnomonic face plane "
+                                                  "(a vertex more than 78 degrees from a face centre it meets)");
+    // virtual geometries and the pieces as candidates
+    std::vector<int64_t> vgp(1, 0), vpr(1, 0), vro(1, 0);
+    std::vector<double> vpxy, vxy;
+    std::vector<int32_t> vgf;
+    const int nvmax = 6 * D + 3;  // a 6D-gon cut by the three sides of a face triangle
+    std::vector<int32_t> pcg, pcn;
+    std::vector<double> pclip;
+    std::vector<std::pair<size_t, size_t>> pref;  // candidate -> (geometry m, piece q)
+    for (size_t m = 0; m < nm; m++) {
+        const MultiFace& mf = mfs[m];
+        std::vector<int32_t> vid(mf.faces.size());
+        for (size_t k = 0; k < mf.faces.size(); k++) {
+            vid[k] = (int32_t)vgf.size();
+            vgf.push_back(mf.faces[k]);
+            for (size_t pi = 0; pi < geos[m].size(); pi++) {
+                for (size_t ri = 0; ri < geos[m][pi].size(); ri++) {
+                    const std::vector<P2>& gr = geos[m][pi][ri];
+                    const std::vector<P2>& pr = mf.pl[k][pi][ri];
+                    for (size_t v = 0; v < gr.size(); v++) {
+                        vxy.push_back(gr[v].x);
+                        vxy.push_back(gr[v].y);
+                        vpxy.push_back(pr[v].x);
+                        vpxy.push_back(pr[v].y);
+                    }
+                    vro.push_back(vro.back() + (int64_t)gr.size());
+                }
+                vpr.push_back(vro.size() - 1);
+            }
+            vgp.push_back(vpr.size() - 1);
+        }
+        for (size_t q = 0; q < mf.pieces.size(); q++) {
+            const MultiPiece& pc = mf.pieces[q];
+            const int n = (int)pc.cell.clip.size();
+            if (n > nvmax) return mosaic_tess_fail(MOSAIC_E_ARG, "face piece with more vertices than expected");
+            pcg.push_back(vid[(size_t)mf.face_slot(pc.face)]);
+            pcn.push_back(n);
+            for (int v = 0; v < nvmax; v++) {
+                pclip.push_back(v < n ? pc.cell.clip[(size_t)v].x : 0.0);
+                pclip.push_back(v < n ? pc.cell.clip[(size_t)v].y : 0.0);
+            }
+            pref.push_back({m, q});
+        }
+    }
+    const int64_t n_pieces = (int64_t)pcg.size();
+    if (n_pieces == 0) return MOSAIC_OK;
+    tessclip::H3Session* S = nullptr;
+    if (int rc = tessclip::h3_session_begin(ctx, (int64_t)vgf.size(), vgp.data(), vpr.data(), vro.data(), vpxy.data(),
+                                            vxy.data(), vgf.data(), res, D, hex_corners().dx, hex_corners().dy, &S))
+        return rc;
+    std::vector<uint8_t> cls((size_t)n_pieces, 0);
+    std::vector<int64_t> tasks;
+    ClippedChips cc;
+    int rc = tessclip::h3_session_chunk(S, n_pieces, pcg.data(), nullptr, 1e-3, 1e-12, cls.data(), tasks, &cc.r,
+                                        pclip.data(), pcn.data(), nvmax);
+    tessclip::h3_session_end(S);
+    if (rc) return rc;
+    cc.index(n_pieces, tasks);
+    for (int64_t i = 0; i < n_pieces; i++) {
+        MultiFace& mf = mfs[pref[(size_t)i].first];
+        MultiPiece& pc = mf.pieces[pref[(size_t)i].second];
+        pc.cls = cls[(size_t)i];
+        if (pc.cls != 2) continue;
+        if (cc.redo(i)) {
+            FacePlane fp;
+            fp.init(pc.face, res);
+            clip_cell(pc.cell, mf.pl[(size_t)mf.face_slot(pc.face)], geos[pref[(size_t)i].first],
+                      [&](P2 h) { return fp.to_geo(h); }, 1e-12, pc.parts);
+        } else {
+            cc.parts_of(i, pc.parts);
+        }
+    }
+    return MOSAIC_OK;
+}
 
 }  // namespace
 
@@ -1113,23 +1245,21 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     mosaic_chip_set* cs = new mosaic_chip_set();
     // the face-spanning geometries before geometry `upto`, emitted where the host producer emits them
     size_t next_multi = 0;
-    auto flush_multi = [&](int64_t upto) -> int {
-        for (; next_multi < multi_geoms.size() && multi_geoms[next_multi] < upto; next_multi++) {
-            const int64_t g = multi_geoms[next_multi];
-            std::vector<std::vector<std::vector<P2>>> mg;
-            for (int64_t p = geom_parts[g]; p < geom_parts[g + 1]; p++) {
-                std::vector<std::vector<P2>> rings;
-                for (int64_t r = part_rings[p]; r < part_rings[p + 1]; r++) {
-                    std::vector<P2> ring;
-                    for (int64_t v = ring_offsets[r]; v < ring_offsets[r + 1]; v++) ring.push_back({xy[2 * v], xy[2 * v + 1]});
-                    rings.push_back(std::move(ring));
-                }
-                mg.push_back(std::move(rings));
-            }
-            if (tessellate_h3_multiface(cs, (int32_t)g, res, D, keep_core_geom, mg))
-                return mosaic_tess_fail(MOSAIC_E_ARG, "geometry too large for a gnomonic face plane "
-                                                      "(a vertex more than 78 degrees from a face centre it meets)");
+    // face-spanning geometries: their per-face pieces made on the host (multiface_pieces), classified
+    // and clipped on the device like every other candidate -- one session over virtual geometries
+    // (geometry, face), the pieces as explicit clip polygons -- and emitted in geometry order
+    // (multiface_emit), so the chips are the host producer's
+    std::vector<MultiFace> mfs(multi_geoms.size());
+    if (!multi_geoms.empty()) {
+        if (int rc = multiface_gpu(ctx, multi_geoms, geom_parts, part_rings, ring_offsets, xy, res, D, mfs)) {
+            delete cs;
+            return rc;
         }
+    }
+    trace.mark("face-spanning pieces (GPU)");
+    auto flush_multi = [&](int64_t upto) -> int {
+        for (; next_multi < multi_geoms.size() && multi_geoms[next_multi] < upto; next_multi++)
+            multiface_emit(cs, (int32_t)multi_geoms[next_multi], res, keep_core_geom, mfs[next_multi]);
         return MOSAIC_OK;
     };
     // one device session for the batch: geometry uploaded once, per chunk only the candidate centres;

@@ -175,6 +175,9 @@ def test_face_spanning_core_cells_are_whole_cells():
 
 @pytest.mark.gpu
 def test_gpu_producer_face_spanning_identical():
+    """The GPU producer classifies and clips the per-face pieces on the device (multiface_gpu:
+    virtual (geometry, face) geometries, the pieces as explicit clip polygons); its chips equal the
+    host routine's byte for byte."""
     from mosaic_amd import MosaicContext
 
     ps = face_cases()
