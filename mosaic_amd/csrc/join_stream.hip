@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     uint32_t* wq = stage + wave * s.stage_words;
     uint32_t wn = 0;  // wave-uniform fill level of the stage
-    const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u;
+    const uint32_t cm = (1u << s.cs) - 1u, qm = (1u << s.qs) - 1u, tm = (1u << s.tsh) - 1u;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
     int64_t w0 = a.row_lo + ((int64_t)blockIdx.x * blockDim.x + (int64_t)wave * 64) * 4;
     // rows of slot k: w0 + (k >> 1) 128 + 2 lane + (k & 1)
@@ -123,7 +123,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             // tiles::line_code, as selects
-            const float u = (float)(gx[k] - (double)(ixC[k] & ~cm)), v = (float)(gy[k] - (double)(iyC[k] & ~cm));
+            // (offsets from the tile's corner: line records are in the tile frame)
+            const float u = (float)(gx[k] - (double)(ixC[k] & ~tm)), v = (float)(gy[k] - (double)(iyC[k] & ~tm));
             const float sv = fmaf(__uint_as_float(lrec[k].x), u, fmaf(__uint_as_float(lrec[k].y), v, __uint_as_float(lrec[k].z)));
             const uint32_t pos = lrec[k].w & 0xffffu, neg = lrec[k].w >> 16;
             uint32_t lc = sv >= 1.0f ? pos : (uint32_t)tiles::kMixed;
@@ -294,8 +295,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         uint32_t code[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            // the offset in the sub-block, leaf cells, truncated to 2^-kFixBits (exact in f32)
-            const uint32_t fb = (uint32_t)(s.cs + tiles::kFixBits);
+            // the offset in the tile (line records are in the tile frame), leaf cells, truncated to
+            // 2^-kFixBits (exact in f32)
+            const uint32_t fb = (uint32_t)(s.tsh + tiles::kFixBits);
             const float u = (float)__builtin_amdgcn_ubfe(g.gx[k], 0u, fb) * (1.0f / (float)(1 << tiles::kFixBits));
             const float v = (float)__builtin_amdgcn_ubfe(g.gy[k], 0u, fb) * (1.0f / (float)(1 << tiles::kFixBits));
             const float sv = fmaf(__uint_as_float(g.lrec[k].x), u,
@@ -469,7 +471,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     uint32_t wn = 0;
     constexpr int F = tiles::kFixBits;
     const uint32_t cs = (uint32_t)s.cs, qs = (uint32_t)s.qs;
-    const uint32_t lowm = (1u << (cs + F + qs)) - 1u;
+    // low bits carried per pending row: the sub-block within the quad and, for the line test, the
+    // offset in the tile (line records are in the tile frame)
+    const uint32_t lowm = (1u << max(cs + F + qs, (uint32_t)s.tsh + F)) - 1u;
     const uint32_t spill = (uint32_t)(a.n_polygons + lane);
     // the fixed-point offsets in VGPRs for the whole kernel (an fma reads one scalar operand; as
     // scalars they would be copied into VGPRs at every point)
@@ -494,7 +498,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     auto set_a = [&](CptSet& z) {
         const uint32_t q = z.c & 0xffffu;
         const uint32_t local = (__builtin_amdgcn_ubfe(z.b, cs + F, qs) << qs) | __builtin_amdgcn_ubfe(z.a, cs + F, qs);
-        const uint32_t off = (((q & 0x7fffu) << (2 * qs)) + local) << 1;
+        uint32_t off = (((q & 0x7fffu) << (2 * qs)) + local) << 1;
+#ifdef MOSAIC_ABL_GATHER_HIT
+        if (MOSAIC_ABL_GATHER_HIT & 4) off &= 0xffeu;
+#endif
         z.code = gather_b16<0>(rsub, q >= 0x8000u, off);
         if (!tb_lds) z.leaf = gather_b32(rtb, q >= 0x8000u, (z.c >> 16) << 2);
     };
@@ -507,15 +514,28 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         const uint32_t n = c & 0x3fffu;
         const uint32_t lf = (__builtin_amdgcn_ubfe(z.b, (uint32_t)F, cs) << cs) | __builtin_amdgcn_ubfe(z.a, (uint32_t)F, cs);
         const uint32_t tbv = tb_lds ? tb[z.c >> 16] : z.leaf;
-        const uint32_t loff = (tbv + (n << (2 * cs)) + lf) << 1;
-        const uint32_t roff = (tbv - 8u * (n + 1u)) << 1;
+        uint32_t loff = (tbv + (n << (2 * cs)) + lf) << 1;
+        uint32_t roff = (tbv - 8u * (n + 1u)) << 1;
+#ifdef MOSAIC_ABL_GATHER_HIT  // measurement builds only: the leaf / line gathers within 4 KB (wrong answers)
+#ifdef MOSAIC_ABL_LMASK
+        if (MOSAIC_ABL_GATHER_HIT & 1) roff &= (uint32_t)MOSAIC_ABL_LMASK;
+#else
+        if (MOSAIC_ABL_GATHER_HIT & 1) roff &= 0xff0u;
+#endif
+        if (MOSAIC_ABL_GATHER_HIT & 2) loff &= 0xffeu;
+#endif
         z.leaf = gather_b16<0>(rblk, blk && !line, loff);
         z.lrec = gather_b128<0>(rblk, line, roff);
         z.code = line ? kPipeLine : (blk ? 0u : c);
     };
     // D: answers of the set's rows (group base wb)
     auto set_d = [&](CptSet& z, int64_t wb) {
-        const uint32_t fb = cs + (uint32_t)F;
+        const uint32_t fb = (uint32_t)s.tsh + (uint32_t)F;
+#ifdef MOSAIC_ABL_GATHER_HIT  // (measurement builds) wait for the gathers, then answer key 0
+        __asm__ volatile("" ::"v"(z.lrec.x), "v"(z.lrec.y), "v"(z.lrec.z), "v"(z.lrec.w), "v"(z.leaf));
+        if (MOSAIC_ABL_GATHER_HIT & 9) z.lrec = v4u{0u, 0u, __float_as_uint(2.0f), 0x00010001u};
+        if (MOSAIC_ABL_GATHER_HIT & 10) z.leaf = z.code == kPipeLine ? z.leaf : 1u;
+#endif
         const float u = (float)__builtin_amdgcn_ubfe(z.a, 0u, fb) * (1.0f / (float)(1 << F));
         const float v = (float)__builtin_amdgcn_ubfe(z.b, 0u, fb) * (1.0f / (float)(1 << F));
         const float sv = fmaf(__uint_as_float(z.lrec.x), u, fmaf(__uint_as_float(z.lrec.y), v, __uint_as_float(z.lrec.z)));

@@ -406,7 +406,7 @@ __device__ inline bool rtry_line(const RBuildArgs& a, const RTile& t, int si, in
     // pass 0: the longest clipped border-chip segment; pass 1: the largest distance of any clipped
     // end from its line
     double best = 0.0, dev_max = 0.0, la = 0.0, lb = 0.0, lc = 0.0;
-    rbuild::P2 pa{0, 0}, pb{0, 0};
+    rbuild::P2 ta{0, 0}, tb{0, 0};  // the longest piece's whole segment, tile frame
     for (int pass = 0; pass < 2; pass++) {
         for (int k = 0; k < t.wa * t.wb; k++) {
             if (!rbuild::poly_meets_hex(sq, 4, rhex_centre(t, k), stol, a.ht)) continue;
@@ -428,22 +428,22 @@ __device__ inline bool rtry_line(const RBuildArgs& a, const RTile& t, int si, in
                                 const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
                                 if (l2 > best) {
                                     best = l2;
-                                    pa = rbuild::P2{ax, ay};
-                                    pb = rbuild::P2{qx, qy};
+                                    ta = rbuild::P2{(s0.x - t.lon0) / wR, (s0.y - t.lat0) / hR};
+                                    tb = rbuild::P2{(s1.x - t.lon0) / wR, (s1.y - t.lat0) / hR};
                                 }
                             } else {
-                                dev_max = rbuild::dmax(dev_max, fabs(la * ax + lb * ay + lc));
-                                dev_max = rbuild::dmax(dev_max, fabs(la * qx + lb * qy + lc));
+                                dev_max = rbuild::dmax(dev_max, fabs(la * (ax + si) + lb * (ay + sj) + lc));
+                                dev_max = rbuild::dmax(dev_max, fabs(la * (qx + si) + lb * (qy + sj) + lc));
                             }
                         }
             }
         }
         if (pass == 0) {
             if (!(best > 1e-6)) return false;
-            const double l = sqrt(best);
-            la = -(pb.y - pa.y) / l;
-            lb = (pb.x - pa.x) / l;
-            lc = -(la * 0.5 * (pa.x + pb.x) + lb * 0.5 * (pa.y + pb.y));
+            const double lt = sqrt((tb.x - ta.x) * (tb.x - ta.x) + (tb.y - ta.y) * (tb.y - ta.y));
+            la = -(tb.y - ta.y) / lt;
+            lb = (tb.x - ta.x) / lt;
+            lc = -(la * 0.5 * (ta.x + tb.x) + lb * 0.5 * (ta.y + tb.y));
         }
     }
     const rbuild::P2 sqb[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
@@ -453,7 +453,9 @@ __device__ inline bool rtry_line(const RBuildArgs& a, const RTile& t, int si, in
         out.a = (float)(la / margin);
         out.b = (float)(lb / margin);
         out.c = (float)(lc / margin);
-        const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - tiles::kLineSlack / margin;
+        const double A = out.a, B = out.b;
+        const double Cf = (double)out.c + A * si + B * sj;
+        const double m = 1.0 - rbuild::line_slack_tile(A, B, out.c, S, tiles::kLineSlack);
         rbuild::P2 hp[8], hn[8];
         const int np = rbuild::clip_half(sqb, 4, A, B, Cf - m, hp), nn = rbuild::clip_half(sqb, 4, -A, -B, -Cf - m, hn);
         const uint16_t cp = np >= 3 ? rclassify_poly(a, t, si, sj, hp, np, sq, stol) : (uint16_t)0;
@@ -602,7 +604,8 @@ __device__ inline uint16_t rclassify_poly_wave(const RBuildArgs& a, const RTile&
 __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int si, int sj, const rbuild::P2* sq,
                                       double stol, tiles::LineRec& out, double u0 = 0.0, double v0 = 0.0,
                                       double u1 = 1.0, double v1 = 1.0, int mk_end = 4, const rbuild::P2* qc = nullptr,
-                                      double ctol = 0.0, int nc = -1, int ck = 0) {
+                                      double ctol = 0.0, int nc = -1, int ck = 0, bool tf = true) {
+    // tf: a sub-block line, tile frame (rbuild::line_slack_tile); else a leaf line, sub-block frame
     const bool listm = nc >= 0;  // the candidates given (rclassify_poly_wave's nc, ck)
     const int S = a.S, lane = (int)(threadIdx.x & 63);
     const double wR = a.tw / S, hR = a.th / S;
@@ -614,7 +617,7 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
     // 1: this lane's largest deviation; then wave reductions
     double best = 0.0, dev_max = 0.0, la = 0.0, lb = 0.0, lc = 0.0;
     uint64_t best_key = ~0ull;
-    rbuild::P2 pa{0, 0}, pb{0, 0};
+    rbuild::P2 pa{0, 0}, pb{0, 0}, ta{0, 0}, tb{0, 0};
     const int W = t.wa * t.wb;
     if (W <= 0) return false;
     for (int pass = 0; pass < 2; pass++)
@@ -646,7 +649,12 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
                                     best_key = ((uint64_t)(uint32_t)k << 32) | v;
                                     pa = rbuild::P2{ax, ay};
                                     pb = rbuild::P2{qx, qy};
+                                    ta = rbuild::P2{(s0.x - t.lon0) / wR, (s0.y - t.lat0) / hR};
+                                    tb = rbuild::P2{(s1.x - t.lon0) / wR, (s1.y - t.lat0) / hR};
                                 }
+                            } else if (tf) {
+                                dev_max = rbuild::dmax(dev_max, fabs(la * (ax + si) + lb * (ay + sj) + lc));
+                                dev_max = rbuild::dmax(dev_max, fabs(la * (qx + si) + lb * (qy + sj) + lc));
                             } else {
                                 dev_max = rbuild::dmax(dev_max, fabs(la * ax + lb * ay + lc));
                                 dev_max = rbuild::dmax(dev_max, fabs(la * qx + lb * qy + lc));
@@ -673,12 +681,21 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
             }
             best = bl;
             if (!(best > 1e-6)) return false;
-            pa = rbuild::P2{__shfl(pa.x, bw, 64), __shfl(pa.y, bw, 64)};
-            pb = rbuild::P2{__shfl(pb.x, bw, 64), __shfl(pb.y, bw, 64)};
-            const double l = sqrt(best);
-            la = -(pb.y - pa.y) / l;
-            lb = (pb.x - pa.x) / l;
-            lc = -(la * 0.5 * (pa.x + pb.x) + lb * 0.5 * (pa.y + pb.y));
+            if (tf) {
+                ta = rbuild::P2{__shfl(ta.x, bw, 64), __shfl(ta.y, bw, 64)};
+                tb = rbuild::P2{__shfl(tb.x, bw, 64), __shfl(tb.y, bw, 64)};
+                const double lt = sqrt((tb.x - ta.x) * (tb.x - ta.x) + (tb.y - ta.y) * (tb.y - ta.y));
+                la = -(tb.y - ta.y) / lt;
+                lb = (tb.x - ta.x) / lt;
+                lc = -(la * 0.5 * (ta.x + tb.x) + lb * 0.5 * (ta.y + tb.y));
+            } else {
+                pa = rbuild::P2{__shfl(pa.x, bw, 64), __shfl(pa.y, bw, 64)};
+                pb = rbuild::P2{__shfl(pb.x, bw, 64), __shfl(pb.y, bw, 64)};
+                const double l = sqrt(best);
+                la = -(pb.y - pa.y) / l;
+                lb = (pb.x - pa.x) / l;
+                lc = -(la * 0.5 * (pa.x + pb.x) + lb * 0.5 * (pa.y + pb.y));
+            }
         }
     }
     dev_max = wave_max_f64(dev_max);
@@ -689,7 +706,9 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
         out.a = (float)(la / margin);
         out.b = (float)(lb / margin);
         out.c = (float)(lc / margin);
-        const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - tiles::kLineSlack / margin;
+        const double A = out.a, B = out.b;
+        const double Cf = tf ? (double)out.c + A * si + B * sj : (double)out.c;
+        const double m = 1.0 - (tf ? rbuild::line_slack_tile(A, B, out.c, S, tiles::kLineSlack) : tiles::kLineSlack / margin);
         rbuild::P2 hp[8], hn[8];
         const int np = rbuild::clip_half(sqb, 4, A, B, Cf - m, hp), nn = rbuild::clip_half(sqb, 4, -A, -B, -Cf - m, hn);
         const uint16_t cp = np >= 3 ? rclassify_poly_wave(a, t, si, sj, hp, np, sq, stol, qc, ctol, nc, ck) : (uint16_t)0;
@@ -821,7 +840,7 @@ __global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const u
         const double u0 = (double)ci / a.C, v0 = (double)cj / a.C, u1 = (double)(ci + 1) / a.C, v1 = (double)(cj + 1) / a.C;
         const int nsc = ncand[msb];
         if (nsc < 0) {
-            found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol);
+            found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol, -1, 0, false);
         } else {
             // the cell's candidates: the sub-block's that meet the cell quad, ascending
             const int sck = lane < nsc ? cands[msb * 64 + lane] : -1;
@@ -831,7 +850,7 @@ __global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const u
             __builtin_amdgcn_wave_barrier();
             const int ncc = __popcll(mk);
             const int cck = lane < ncc ? cbuf[wv][lane] : -1;
-            found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol, ncc, cck);
+            found = rtry_line_wave(a, t, si, sj, sq, stol, lr, u0, v0, u1, v1, tiles::kLeafLineMargins, qc, ctol, ncc, cck, false);
         }
     }
     if (lane == 0) {
@@ -4314,7 +4333,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 // per pending row, and per wave a kCptBufWords compaction buffer in LDS)
                 // (k_join_stream_pipe reads tile bases from LDS; k_join_stream_cpt from LDS or memory)
                 int mode = vec && sa.fix_ok ? c->stream_pipe : 0;
-                if (mode >= 2 && !(sa.cs + tiles::kFixBits + sa.qs <= 24 && sa.n_tiles <= 65536 &&
+                if (mode >= 2 && !(sa.cs + tiles::kFixBits + sa.qs <= 24 && sa.tsh + tiles::kFixBits <= 24 && sa.n_tiles <= 65536 &&
                                    shm_s + (size_t)(blk / 64) * kCptBufWords * 4 <= kStreamLdsMax))
                     mode = 1;
                 if (mode == 1 && !sa.tb_lds) mode = 0;

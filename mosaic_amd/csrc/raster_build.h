@@ -151,5 +151,20 @@ MOSAIC_HD int clip_half(const P2* q, int n, double a, double b, double c, P2* ou
 // The line-record margins tried, narrowest first (sub-block units)
 MOSAIC_HD double line_margin(int k) { return k == 0 ? 1.0 / 2048 : (k == 1 ? 1.0 / 512 : (k == 2 ? 1.0 / 128 : 1.0 / 32)); }
 
+// Sub-block line records live in the TILE frame: s = A ut + B vt + Ct with (ut, vt) the point's
+// offset from the tile's corner in sub-block units (0 <= ut, vt <= S), the line through the chip
+// segment that holds the longest clipped piece -- so every sub-block one edge splits gets the same
+// record and the tile keeps one copy.  The device evaluates fmaf(A / C, u, fmaf(B / C, v, Ct)) with
+// (u, v) the tile-local leaf-cell offsets (exact in f32: S C 2^kFixBits <= 2^24 fixed-point units,
+// truncated to one unit; the float kernels round to less than one).  A sub-block's two sides are
+// certified beyond 1 - line_slack_tile: kLineSlack sub-block units per axis (the offsets' error,
+// as in the sub-block frame) plus the two f32 roundings of the evaluation (each <= 2^-24 of its
+// result, |inner| <= |B| S + |Ct|, |outer| <= |A| S + |inner|).
+MOSAIC_HD double line_slack_tile(double A, double B, double Ct, int S, double kslack) {
+    const double aa = fabs(A), ab = fabs(B);
+    const double inner = ab * S + fabs(Ct), outer = aa * S + inner;
+    return (aa + ab) * kslack + (inner + outer) * (1.0 / 8388608.0);
+}
+
 }  // namespace rbuild
 }  // namespace mosaic

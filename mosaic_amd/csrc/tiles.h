@@ -71,15 +71,18 @@ static const uint32_t kFull = 1;  // run the generic fast path + probe
 // kMixed, kSubBlock | n (n < kLineBit): the C x C leaf block at blocks[tile_base[tile] + n C^2],
 // or kSubBlock | kLineBit | n: the line record at blocks[tile_base[tile] - 8 (n + 1)] (a tile's
 // line records precede its leaf blocks, last first; tile_base counts uint16 elements and is a
-// multiple of 8).
+// multiple of 8).  Sub-block line records are in the tile frame (rbuild::line_slack_tile): u, v
+// are the point's offsets from the TILE's corner in leaf cells, and the sub-blocks one edge splits
+// share one record.
 static const uint16_t kMixed = 0xffffu;
 static const uint16_t kSubBlock = 0x8000u;
 static const uint16_t kLineBit = 0x4000u;
 static const int32_t kMaxRasterKeys = 0x7ffd;  // polygon keys 0 .. kMaxRasterKeys - 1
 
 // A sub-block split by one straight feature (a chip edge: a zone boundary or a hexagon side):
-// s = a u + b v + c with (u, v) the point's offset from the sub-block's lower-left corner in leaf
-// cells (0 <= u, v < C), (a, b) scaled to 1 / (margin C), so points with s >= 1 get code pos,
+// s = a u + b v + c with (u, v) the point's offset from the tile's lower-left corner in leaf cells
+// (0 <= u, v < S C; leaf lines: from the sub-block's corner, 0 <= u, v < C), (a, b) scaled to
+// 1 / (margin C), so points with s >= 1 get code pos,
 // s <= -1 code neg and the band of half-width `margin` (sub-block units, chosen per record)
 // between is mixed.  The host certifies the two half-planes widened by kLineSlack sub-block units,
 // far more than the float evaluation's error.
@@ -164,9 +167,11 @@ MOSAIC_HD uint16_t raster_code(const PointRaster& r, double x0, double y0, doubl
     if (!sub_is_block(e)) return (uint16_t)e;
     const size_t base = r.tile_base[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)];
     const uint32_t n = e & 0x3fffu;
-    if (e & kLineBit)
-        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)(gx - (double)(ixC & ~cm)),
-                         (float)(gy - (double)(iyC & ~cm)));
+    if (e & kLineBit) {  // tile frame
+        const int tm = (1 << (r.sshift + r.cshift)) - 1;
+        return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)(gx - (double)(ixC & ~tm)),
+                         (float)(gy - (double)(iyC & ~tm)));
+    }
     const uint16_t lc = r.blocks[base + ((size_t)n << (2 * r.cshift)) + (size_t)(((iyC & cm) << r.cshift) | (ixC & cm))];
     if (leaf_is_line(lc) && r.llines)
         return line_code(r.llines[r.tile_lbase[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)] + (lc & 0x3fffu)],
@@ -215,8 +220,8 @@ MOSAIC_HD uint16_t raster_code_fixed(const PointRaster& r, double ax, double bx,
     if (!sub_is_block(e)) return (uint16_t)e;
     const size_t base = r.tile_base[(iy >> r.sshift) * r.tnx + (ix >> r.sshift)];
     const uint32_t n = e & 0x3fffu;
-    if (e & kLineBit) {
-        const uint32_t fm = (1u << (r.cshift + F)) - 1u;
+    if (e & kLineBit) {  // tile frame
+        const uint32_t fm = (1u << (r.sshift + r.cshift + F)) - 1u;
         const float sc = 1.0f / (float)(1 << F);
         return line_code(*(const LineRec*)(r.blocks + base - 8 * (size_t)(n + 1)), (float)((uint32_t)gix & fm) * sc,
                          (float)((uint32_t)giy & fm) * sc);

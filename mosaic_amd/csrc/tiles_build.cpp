@@ -26,7 +26,9 @@
 
 #include <atomic>
 #include <cstring>
+#include <string>
 #include <thread>
+#include <unordered_map>
 
 namespace mosaic {
 namespace tiles {
@@ -284,16 +286,18 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
             // longest clipped edge; both sides (beyond a margin, less the slack) must classify
             // The box is [u0, u1] x [v0, v1] in sub-block units: the whole sub-block, or one leaf cell
             // (a leaf line, tried margins 0 .. mk_end - 1) in the sub-block's frame.
+            // tf: a sub-block line, in the tile frame (rbuild::line_slack_tile); else a leaf line in
+            // the sub-block frame
             std::vector<P2> ends;
             auto try_line = [&](int si, int sj, double u0, double v0, double u1, double v1, int mk_end,
-                                const std::vector<int>& cin, LineRec& out) -> bool {
+                                const std::vector<int>& cin, LineRec& out, bool tf) -> bool {
                 const double wR = tw / S, hR = th / S;
                 const double lonR0 = lon0 + tw * si / S, latR0 = lat0 + th * sj / S;
                 const double exu = exd / wR, eyv = eyd / hR;
                 const double bx0 = lonR0 + wR * u0 - exd, bx1 = lonR0 + wR * u1 + exd, by0 = latR0 + hR * v0 - eyd,
                              by1 = latR0 + hR * v1 + eyd;
                 double best = 0.0;
-                P2 pa{0, 0}, pb{0, 0};
+                P2 pa{0, 0}, pb{0, 0}, ta{0, 0}, tb{0, 0};
                 ends.clear();
                 for (int k : cin) {
                     const Hex& h = hexes[(size_t)k];
@@ -311,16 +315,27 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                                 best = l2;
                                 pa = P2{ax, ay};
                                 pb = P2{qx, qy};
+                                ta = P2{(e.ax - lon0) / wR, (e.ay - lat0) / hR};
+                                tb = P2{(e.bx - lon0) / wR, (e.by - lat0) / hR};
                             }
                         }
                     }
                 }
                 if (!(best > 1e-6)) return false;
-                const double l = sqrt(best);
-                const double a = -(pb.y - pa.y) / l, b = (pb.x - pa.x) / l;
-                const double c = -(a * 0.5 * (pa.x + pb.x) + b * 0.5 * (pa.y + pb.y));
-                double dev_max = 0.0;
-                for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * p.x + b * p.y + c));
+                double a, b, c, dev_max = 0.0;
+                if (tf) {  // the whole segment's line, tile frame
+                    const double lt = sqrt((tb.x - ta.x) * (tb.x - ta.x) + (tb.y - ta.y) * (tb.y - ta.y));
+                    a = -(tb.y - ta.y) / lt;
+                    b = (tb.x - ta.x) / lt;
+                    c = -(a * 0.5 * (ta.x + tb.x) + b * 0.5 * (ta.y + tb.y));
+                    for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * (p.x + si) + b * (p.y + sj) + c));
+                } else {
+                    const double l = sqrt(best);
+                    a = -(pb.y - pa.y) / l;
+                    b = (pb.x - pa.x) / l;
+                    c = -(a * 0.5 * (pa.x + pb.x) + b * 0.5 * (pa.y + pb.y));
+                    for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * p.x + b * p.y + c));
+                }
                 const P2 sq[4] = {{u0 - exu, v0 - eyv}, {u1 + exu, v0 - eyv}, {u1 + exu, v1 + eyv}, {u0 - exu, v1 + eyv}};
                 // the narrowest band (fewest rows to the mixed kernel) whose two sides certify
                 for (int mk = 0; mk < mk_end; mk++) {
@@ -330,8 +345,11 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                     out.b = (float)(b / margin);
                     out.c = (float)(c / margin);
                     // certify with the coefficients the device uses: device side + implies
-                    // A u + B v + C >= 1 - (float error) >= 1 - kLineSlack / margin
-                    const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - kLineSlack / margin;
+                    // A u + B v + C >= 1 - (float error) >= 1 - kLineSlack / margin (tile frame:
+                    // the sub-block's own C = Ct + A si + B sj, and line_slack_tile)
+                    const double A = out.a, B = out.b;
+                    const double Cf = tf ? (double)out.c + A * si + B * sj : (double)out.c;
+                    const double m = 1.0 - (tf ? rbuild::line_slack_tile(A, B, out.c, S, kLineSlack) : kLineSlack / margin);
                     P2 hp[8], hn[8];
                     const int np = clip_half(sq, 4, A, B, Cf - m, hp), nn = clip_half(sq, 4, -A, -B, -Cf - m, hn);
                     const uint16_t cp = np >= 3 ? classify_poly(si, sj, hp, np, cin) : 0;
@@ -360,7 +378,7 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                     rcode[(size_t)sj * S + si] = code;
                     if (code != kMixed) continue;
                     LineRec lr;
-                    if (lines && try_line(si, sj, 0.0, 0.0, 1.0, 1.0, 4, cand, lr)) {
+                    if (lines && try_line(si, sj, 0.0, 0.0, 1.0, 1.0, 4, cand, lr, true)) {
                         r_kind[(size_t)ri].push_back(1);
                         r_line[(size_t)ri].push_back(lr);
                         continue;
@@ -378,7 +396,7 @@ void Builder::classify_raster_host(const ChipSource& src, int threads, RasterCla
                             uint16_t cc = classify(i0, j0, i0 + 1, j0 + 1, qc, cand, cand2);
                             if (cc == kMixed && leaf_lines &&
                                 try_line(si, sj, (double)ci / C, (double)cj / C, (double)(ci + 1) / C, (double)(cj + 1) / C,
-                                         kLeafLineMargins, cand2, lr)) {
+                                         kLeafLineMargins, cand2, lr, false)) {
                                 r_cline_at[(size_t)ri].push_back((uint32_t)(r_cells[(size_t)ri].size() + (size_t)cj * C + ci));
                                 r_cline[(size_t)ri].push_back(lr);
                             }
@@ -504,6 +522,9 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
             std::vector<LineRec>& outl = tile_lines[(size_t)ri];
             std::vector<LineRec>& outll = tile_llines[(size_t)ri];
             size_t mk = mk0[(size_t)ri];  // next mixed sub-block
+            // the tile's distinct line records (tile frame: every sub-block one edge splits with
+            // the same margin and sides shares its record), first occurrence first
+            std::unordered_map<std::string, uint32_t> lidx;
             for (int sj = 0; sj < S; sj++)
                 for (int si = 0; si < S; si++) {
                     const uint16_t code = rcode[(size_t)sj * S + si];
@@ -515,8 +536,10 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
                         l_mixed++;
                         if (rc.kind[mk]) {
                             // tile-local line record number (< S * S <= kLineBit)
-                            entry = (uint16_t)(kSubBlock | kLineBit | (uint32_t)outl.size());
-                            outl.push_back(rc.line[mk]);
+                            const auto ins = lidx.emplace(std::string((const char*)&rc.line[mk], sizeof(LineRec)),
+                                                          (uint32_t)outl.size());
+                            if (ins.second) outl.push_back(rc.line[mk]);
+                            entry = (uint16_t)(kSubBlock | kLineBit | ins.first->second);
                             l_line++;
                         } else {
                             const uint16_t* cellc = rc.cells.data() + (size_t)rc.cell_at[mk] * CC;
