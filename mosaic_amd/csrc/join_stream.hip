@@ -766,7 +766,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             }
         }
         uint32_t code[4], e[4], loff[4];
-        float su[4], sv[4];
+        float gu[4], gv[4];
         bool inr[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -794,8 +794,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             int sx = (int)gxs, sy = (int)gys;
             sx = min(max(sx, 0), (int)C - 1);
             sy = min(max(sy, 0), (int)C - 1);
-            su[k] = gxs - (float)sx;  // offset in the sub-cell (sub-cell units)
-            sv[k] = gys - (float)sy;
+            gu[k] = gxs;  // offset in the cell (sub-cell units)
+            gv[k] = gys;
             loff[k] = (uint32_t)(sy * (int)C + sx);
         }
         bool leafc[4], line[4];
@@ -816,7 +816,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             // tiles::line_code, as selects
-            const float lv = fmaf(__uint_as_float(lrec[k].x), su[k], fmaf(__uint_as_float(lrec[k].y), sv[k], __uint_as_float(lrec[k].z)));
+            // (line records in the cell frame: the offsets from the cell's corner)
+            const float lv = fmaf(__uint_as_float(lrec[k].x), gu[k], fmaf(__uint_as_float(lrec[k].y), gv[k], __uint_as_float(lrec[k].z)));
             uint32_t lc = lv >= 1.0f ? (lrec[k].w & 0xffffu) : (uint32_t)tiles::kMixed;
             lc = lv <= -1.0f ? (lrec[k].w >> 16) : lc;
             code[k] = line[k] ? lc : code[k];
@@ -964,9 +965,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
     };
     // D': answers of the set's rows (group base wb)
     auto set_d = [&](BngCptSet& z, const v4u& lrec, int64_t wb) {
-        float su, sv;
-        (void)subcell(z, &su, &sv);
-        const float lv = fmaf(__uint_as_float(lrec.x), su, fmaf(__uint_as_float(lrec.y), sv, __uint_as_float(lrec.z)));
+        // (line records in the cell frame: the offsets from the cell's corner)
+        const float lv = fmaf(__uint_as_float(lrec.x), __uint_as_float(z.b), fmaf(__uint_as_float(lrec.y), __uint_as_float(z.c), __uint_as_float(lrec.z)));
         uint32_t lc = lv >= 1.0f ? (lrec.w & 0xffffu) : (uint32_t)tiles::kMixed;
         lc = lv <= -1.0f ? (lrec.w >> 16) : lc;
         const uint32_t code = z.p == kPipeLine ? lc : z.p;

@@ -821,13 +821,15 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                 return ans.empty() ? (uint16_t)0 : (ans.size() == 1 ? (uint16_t)(ans[0] + 1) : kMixed);
             };
             // a mixed sub-cell whose chip edges all lie along one line (tiles_build try_line, in
-            // sub-cell units): the line through the longest clipped edge, both sides certified
+            // sub-cell units): the line through the chip segment holding the longest clipped piece,
+            // in the CELL frame (offsets from the cell's corner, 0 <= u, v <= C: the sub-cells one
+            // edge splits share the record; rbuild::line_slack_tile), both sides certified
             auto try_line = [&](int i, int j, LineRec& out) -> bool {
                 const double rx0 = bc.x0 + h * i, ry0 = bc.y0 + h * j;
                 const double exu = ex / h, eyv = ey / h;
                 const double bx0 = rx0 - ex, bx1 = rx0 + h + ex, by0 = ry0 - ey, by1 = ry0 + h + ey;
                 double best = 0.0;
-                P2 pa{0, 0}, pb{0, 0};
+                P2 ta{0, 0}, tb{0, 0};
                 ends.clear();
                 for (size_t b = 0; b < border.size(); b++) {
                     const pip::Box& bx = src.store.geom_bbox[border[b]];
@@ -841,17 +843,17 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                         const double l2 = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
                         if (l2 > best) {
                             best = l2;
-                            pa = P2{ax, ay};
-                            pb = P2{qx, qy};
+                            ta = P2{(e.ax - bc.x0) / h, (e.ay - bc.y0) / h};
+                            tb = P2{(e.bx - bc.x0) / h, (e.by - bc.y0) / h};
                         }
                     }
                 }
                 if (!(best > 1e-6)) return false;
-                const double l = sqrt(best);
-                const double a = -(pb.y - pa.y) / l, b = (pb.x - pa.x) / l;
-                const double c = -(a * 0.5 * (pa.x + pb.x) + b * 0.5 * (pa.y + pb.y));
+                const double lt = sqrt((tb.x - ta.x) * (tb.x - ta.x) + (tb.y - ta.y) * (tb.y - ta.y));
+                const double a = -(tb.y - ta.y) / lt, b = (tb.x - ta.x) / lt;
+                const double c = -(a * 0.5 * (ta.x + tb.x) + b * 0.5 * (ta.y + tb.y));
                 double dev_max = 0.0;
-                for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * p.x + b * p.y + c));
+                for (const P2& p : ends) dev_max = std::max(dev_max, fabs(a * (p.x + i) + b * (p.y + j) + c));
                 const P2 sq[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
                 for (int mk = 0; mk < 4; mk++) {
                     const double margin = rbuild::line_margin(mk);
@@ -859,8 +861,10 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                     out.a = (float)(a / margin);
                     out.b = (float)(b / margin);
                     out.c = (float)(c / margin);
-                    // certify with the coefficients the device uses (as try_line)
-                    const double A = out.a, B = out.b, Cf = out.c, m = 1.0 - kLineSlack / margin;
+                    // certify with the coefficients the device uses (as try_line): the sub-cell's
+                    // own C = Ct + A i + B j
+                    const double A = out.a, B = out.b, Cf = (double)out.c + A * i + B * j;
+                    const double m = 1.0 - rbuild::line_slack_tile(A, B, out.c, C, kLineSlack);
                     P2 hp[8], hn[8];
                     const int np = clip_half(sq, 4, A, B, Cf - m, hp), nn = clip_half(sq, 4, -A, -B, -Cf - m, hn);
                     for (int v = 0; v < np; v++) hp[v] = P2{rx0 + h * hp[v].x, ry0 + h * hp[v].y};
@@ -896,8 +900,11 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                     if (!mixed) code = ans.empty() ? (uint16_t)0 : (ans.size() == 1 ? (uint16_t)(ans[0] + 1) : kMixed);
                     LineRec lr;
                     if (code == kMixed && lines && try_line(i, j, lr)) {
-                        code = (uint16_t)(kSubBlock | kLineBit | lrec[(size_t)k].size());
-                        lrec[(size_t)k].push_back(lr);
+                        // the cell's distinct records, first occurrence first
+                        size_t n = 0;
+                        while (n < lrec[(size_t)k].size() && memcmp(&lrec[(size_t)k][n], &lr, sizeof(LineRec))) n++;
+                        code = (uint16_t)(kSubBlock | kLineBit | n);
+                        if (n == lrec[(size_t)k].size()) lrec[(size_t)k].push_back(lr);
                     }
                     e[(size_t)j * C + i] = code;
                 }
