@@ -290,6 +290,33 @@ int main(int argc, char** argv) {
         rbad++;
         fprintf(stderr, "an edge sub-block answers a pair\n");
     }
+    // tile-frame line records: one copy per tile and edge -- the records a tile's line sub-blocks
+    // name are pairwise distinct (the assembly's deduplication) and fewer than those sub-blocks
+    if (rok && !tb.sub.empty()) {
+        const int64_t NXs = (int64_t)g.nx << tb.sshift, NYs = (int64_t)g.ny << tb.sshift;
+        long nrec = 0, dup = 0;
+        for (int64_t tj = 0; tj < g.ny; tj++)
+            for (int64_t ti = 0; ti < g.nx; ti++) {
+                uint32_t nmax = 0;
+                bool any = false;
+                for (int64_t sj = tj << tb.sshift; sj < (tj + 1) << tb.sshift && sj < NYs; sj++)
+                    for (int64_t si = ti << tb.sshift; si < (ti + 1) << tb.sshift && si < NXs; si++) {
+                        const uint16_t e = tb.sub[(size_t)(sj * NXs + si)];
+                        if (tiles::sub_is_block(e) && (e & tiles::kLineBit)) {
+                            nmax = std::max<uint32_t>(nmax, (uint32_t)(e & 0x3fffu) + 1u);
+                            any = true;
+                        }
+                    }
+                if (!any) continue;
+                nrec += nmax;
+                const size_t base = tb.tile_base[(size_t)(tj * g.nx + ti)];
+                for (uint32_t p = 0; p < nmax; p++)
+                    for (uint32_t q = p + 1; q < nmax; q++)
+                        dup += memcmp(tb.blocks.data() + base - 8 * (size_t)(p + 1), tb.blocks.data() + base - 8 * (size_t)(q + 1),
+                                      sizeof(tiles::LineRec)) == 0;
+            }
+        fprintf(stderr, "line records %ld for %lld line sub-blocks, duplicates %ld\n", nrec, (long long)tb.n_sub_line, dup);
+    }
     fprintf(stderr, "pure codes: float form %ld, fixed-point form %ld\n", rpure, rfpure);
     printf("1 %ld %ld %ld %ld %ld %ld %d %ld %ld %ld\n", bad, checked, skipped, full, unc, miss, rok ? 1 : 0, rbad, rpure,
            rmixed);

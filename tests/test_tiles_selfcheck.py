@@ -63,6 +63,12 @@ def test_tiles_nyc_tessellation(exe, tmp_path, res, sc):
     # against the exact answer like the float form's) decides as many points
     m = re.search(r"pure codes: float form (\d+), fixed-point form (\d+)", r["log"])
     assert m and int(m.group(2)) >= 0.999 * int(m.group(1)), r["log"]
+    # line records in the tile frame: one copy per tile and edge (no duplicates within a tile, and
+    # sub-blocks along one edge share a record)
+    m = re.search(r"line records (\d+) for (\d+) line sub-blocks, duplicates (\d+)", r["log"])
+    assert m and int(m.group(3)) == 0, r["log"]
+    if int(m.group(2)) > 20_000:
+        assert int(m.group(1)) < 0.9 * int(m.group(2)), r["log"]
 
 
 def _disc_chips(lon, lat, radius_deg, res, n=20000, seed=0):
