@@ -1865,6 +1865,7 @@ struct Options {
     int stream_pipe = 2;      // 1: k_join_stream_pipe (software-pipelined), 2: k_join_stream_cpt (+ compacted gathers)
     int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
     int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
+    int bng_group_lines = 1;  // BNG levels carry a line code where one line record decides a whole group
     int mixed_blocks_per_cu = 4;  // k_join_mixed grid: the workgroups resident at once (~120 VGPRs: 4 per CU)
     int mixed_rows = 2;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
@@ -2508,6 +2509,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "bng_cell") {
         if (v > 64 || !pow2(v)) return fail(MOSAIC_E_ARG, "bng_cell must be a power of two in [1, 64]");
         o.bng_cell = (int)v;
+    } else if (k == "bng_group_lines") {
+        o.bng_group_lines = v ? 1 : 0;
     } else if (k == "timing") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
         o.timing = (int)v;
@@ -3631,6 +3634,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
             // sub-cells at 100 m resolution with the default 32; line records with option raster_lines)
             std::vector<uint16_t> leaf;
             std::vector<uint32_t> lbase_kept;  // border cell b's leaf block at leaf[lbase_kept[b]]
+            std::vector<uint16_t> bng_glines;  // group-level line codes (tiles.h bng_leaf_blocks glines)
             const int C = c->bng_cell;
             if (!border.empty()) {
                 std::vector<uint32_t> sfirst(capacity, 0), scount(capacity, 0);
@@ -3650,7 +3654,8 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 // (leaf offsets are 32-bit buffer offsets in k_join_stream_bng)
                 std::vector<uint32_t>& lbase = lbase_kept;
                 // (leaf element offsets < 2^30, byte offsets below kNoLoad)
-                if (tiles::bng_leaf_blocks(src, border, (double)div, C, c->raster_lines != 0, threads, leaf, lbase) &&
+                if (tiles::bng_leaf_blocks(src, border, (double)div, C, c->raster_lines != 0, threads, leaf, lbase,
+                                           c->bng_group_lines ? &bng_glines : nullptr) &&
                     leaf.size() * 2 < (size_t)kNoLoad) {
                     for (size_t b = 0; b < border.size(); b++) {
                         tab[border_at[b]] = kBngLeaf | lbase[b];
@@ -3676,7 +3681,12 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 for (size_t b = 0; b < border.size(); b++)
                     for (int bj = 0; bj < CB; bj++)
                         for (int bi = 0; bi < CB; bi++)
-                            lvl[border_at[b] * LV + (size_t)bj * CB + bi] = tiles::bng_level_code(&leaf[lbase_kept[b]], C, bi, bj);
+                        {
+                            uint16_t v = tiles::bng_level_code(&leaf[lbase_kept[b]], C, bi, bj);
+                            // a group certified for one line record: that line code (tiles.h glines)
+                            if (v == tiles::kSubBlock && !bng_glines.empty()) v = bng_glines[b * (size_t)CB * CB + (size_t)bj * CB + bi];
+                            lvl[border_at[b] * LV + (size_t)bj * CB + bi] = v;
+                        }
             }
             // LDS cell level (BngStreamArgs::lcell): the finest block size 2^lsh whose byte table fits
             // the stream kernel's LDS beside its counts and 16 per-wave stages

@@ -716,8 +716,15 @@ inline uint16_t bng_level_code(const uint16_t* e, int C, int bi, int bj) {
             if (e[(size_t)j * C + i] != v) return kSubBlock;
     return v;
 }
+// glines (optional): per border cell bng_level_side(C)^2 group codes -- a line code kSubBlock |
+// kLineBit | n where the cell's line record n (cell frame) is certified over the whole group (every
+// line sub-cell of the group names n, none is kMixed, and both half-planes of the record clipped to
+// the widened group square classify to its pos / neg), else kSubBlock.  The level then carries that
+// line code, so k_join_stream_bng_cpt gathers the record without the leaf code (a level code is a
+// valid answer for every point of its group, as before).
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
-                     bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base);
+                     bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base,
+                     std::vector<uint16_t>* glines = nullptr);
 
 }  // namespace tiles
 }  // namespace mosaic

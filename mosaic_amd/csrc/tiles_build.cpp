@@ -764,8 +764,11 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
 }
 
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
-                     bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base) {
+                     bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base,
+                     std::vector<uint16_t>* glines) {
     if (C < 1 || C > 64) return false;
+    const int CB = bng_level_side(C), G = kBngLvlG;
+    if (glines) glines->assign(cells.size() * (size_t)CB * CB, kSubBlock);
     const size_t CC = (size_t)C * C, CCp = (CC + 7) & ~(size_t)7;  // leaf block padded to 16 bytes
     std::vector<std::vector<uint16_t>> ent(cells.size());
     std::vector<std::vector<LineRec>> lrec(cells.size());
@@ -908,6 +911,37 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                     }
                     e[(size_t)j * C + i] = code;
                 }
+            // group-level line codes (glines): a group whose line sub-cells all name record n and
+            // whose other sub-cells are pure, with n certified over the whole widened group
+            if (glines && lines && !lrec[(size_t)k].empty())
+                for (int bj = 0; bj < CB; bj++)
+                    for (int bi = 0; bi < CB; bi++) {
+                        uint32_t n = ~0u;
+                        bool ok = true;
+                        for (int j = G * bj; ok && j < std::min(C, G * bj + G); j++)
+                            for (int i = G * bi; ok && i < std::min(C, G * bi + G); i++) {
+                                const uint16_t v = e[(size_t)j * C + i];
+                                if (v == kMixed) ok = false;
+                                else if ((v & 0xC000u) == 0xC000u) {
+                                    if (n == ~0u) n = v & 0x3fffu;
+                                    else if (n != (uint32_t)(v & 0x3fffu)) ok = false;
+                                }
+                            }
+                        if (!ok || n == ~0u) continue;
+                        const LineRec& lr = lrec[(size_t)k][n];
+                        const double exu = ex / h, eyv = ey / h;
+                        const double u0 = G * bi, v0 = G * bj, u1 = std::min(C, G * bi + G), v1 = std::min(C, G * bj + G);
+                        const P2 sq[4] = {{u0 - exu, v0 - eyv}, {u1 + exu, v0 - eyv}, {u1 + exu, v1 + eyv}, {u0 - exu, v1 + eyv}};
+                        const double A = lr.a, B = lr.b, Ct = lr.c;
+                        const double m = 1.0 - rbuild::line_slack_tile(A, B, Ct, C, kLineSlack);
+                        P2 hp[8], hn[8];
+                        const int np = clip_half(sq, 4, A, B, Ct - m, hp), nn = clip_half(sq, 4, -A, -B, -Ct - m, hn);
+                        for (int v = 0; v < np; v++) hp[v] = P2{bc.x0 + h * hp[v].x, bc.y0 + h * hp[v].y};
+                        for (int v = 0; v < nn; v++) hn[v] = P2{bc.x0 + h * hn[v].x, bc.y0 + h * hn[v].y};
+                        if (np >= 3 && classify_poly(hp, np) != lr.pos) continue;
+                        if (nn >= 3 && classify_poly(hn, nn) != lr.neg) continue;
+                        (*glines)[(size_t)k * CB * CB + (size_t)bj * CB + bi] = (uint16_t)(kSubBlock | kLineBit | n);
+                    }
         }
     };
     const int nt = std::max(1, threads);
