@@ -105,3 +105,11 @@ def test_bng_format_matches_oracle_random():
             if (s.startswith("SZ") and str(int(v))[3:5] == "10") or s in ("SW", "NW", "NE", "SE") or res == -1:
                 continue
             assert bng.parse(s) == int(v)
+
+
+def test_graft_build_entry():
+    """__graft_entry__.build() (the driver's build check): make is a no-op on a built tree, and its
+    ABI check reads the version from include/mosaic_hip.h, so it cannot fall behind the header."""
+    import __graft_entry__ as g
+
+    g.build()
