@@ -119,7 +119,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * built afterwards carry an LDS cell level for the BNG stream kernel; default 1), "bng_cell" (sub-cells
  * per BNG border cell side in those tables, a power of two <= 64; default 32), "bng_group_lines" (0/1:
  * those tables' sub-block levels name a line record wherever one decides a whole 4 x 4 group; default
- * 1), "scratch_limit" (see
+ * 1), "bng_wedges" (0/1: those tables carry wedge records for sub-cells split at a chip vertex,
+ * answered by the BNG mixed-row kernel before its chip loop; default 1), "scratch_limit" (see
  * the per-thread state below), "bin_points" (0/1: H3 joins on a tile directory without a usable point
  * raster sort the points by tile before the chip loop -- the border-chip-heavy C4 shape; default 1),
  * "bin_min_rows" (smallest batch that is binned; default 2^18), "bin_chunk" (rows per sort chunk;

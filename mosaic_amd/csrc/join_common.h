@@ -53,6 +53,7 @@ struct JoinArgs {
     const uint32_t* bng_cells;        // BNG dense cell table (k_join_stream_bng); nullptr: none
     const uint16_t* bng_leaf;         // its leaf blocks (C x C codes per border cell)
     int32_t bng_e0, bng_n0, bng_ne, bng_nn, bng_div, bng_C;
+    int32_t bng_wedge;                // k_join_mixed_bng answers wedge sub-cells first (tiles.h)
     int64_t row_lo;                   // k_join_stream / k_join_mixed: rows [row_lo, n)
     uint32_t* mixq;                   // rows (- row_lo) in mixed raster cells, dense, in
     unsigned long long* mixq_count;   //   mixq[0 .. *mixq_count)

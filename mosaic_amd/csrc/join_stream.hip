@@ -820,7 +820,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
             const float lv = fmaf(__uint_as_float(lrec[k].x), gu[k], fmaf(__uint_as_float(lrec[k].y), gv[k], __uint_as_float(lrec[k].z)));
             uint32_t lc = lv >= 1.0f ? (lrec[k].w & 0xffffu) : (uint32_t)tiles::kMixed;
             lc = lv <= -1.0f ? (lrec[k].w >> 16) : lc;
-            code[k] = line[k] ? lc : code[k];
+            code[k] = line[k] ? lc : (code[k] - 0x8000u < 0x4000u ? (uint32_t)tiles::kMixed : code[k]);  // (wedges)
             uint32_t c = (e[k] & kBngPure) ? (e[k] & ~kBngPure) : ((e[k] & kBngLeaf) ? code[k] : (e[k] ? (uint32_t)tiles::kMixed : 0u));
             c = inr[k] ? c : (uint32_t)tiles::kMixed;      // outside the one-to-one range: generic path
             c = (x[k] != x[k] || y[k] != y[k]) ? 0u : c;  // NaN: flagged, no pair
@@ -961,7 +961,8 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) 
         const bool leafc = z.p == kBngLeaf;
         const bool line = leafc && (code & 0xC000u) == 0xC000u && code != (uint32_t)tiles::kMixed;
         lrec = gather_b128<0>(rleaf, line, (base - 8u * ((code & 0x3fffu) + 1u)) << 1);
-        z.p = line ? kPipeLine : (leafc ? code : z.p);
+        // (wedge codes kSubBlock | n: the mixed queue, k_join_mixed_bng)
+        z.p = line ? kPipeLine : (leafc ? (code - 0x8000u < 0x4000u ? (uint32_t)tiles::kMixed : code) : z.p);
     };
     // D': answers of the set's rows (group base wb)
     auto set_d = [&](BngCptSet& z, const v4u& lrec, int64_t wb) {

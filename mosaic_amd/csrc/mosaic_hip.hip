@@ -1441,10 +1441,41 @@ __global__ void __launch_bounds__(256) k_join_mixed_bng(JoinArgs a) {
             x[k] = a.x[row[k]];
             y[k] = a.y[row[k]];
         }
+        // wedge sub-cells (tiles.h bng_leaf_blocks wedges): the stream kernels' cell and sub-cell
+        // arithmetic, the leaf code, and for a wedge code the two records -- a point outside both
+        // bands is answered here and skips the chip loop
+        bool done[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            done[k] = false;
+            if (!a.bng_wedge || !live[k] || x[k] != x[k] || y[k] != y[k]) continue;
+            const int32_t eI = bng::jvm_d2i(x[k]), nI = bng::jvm_d2i(y[k]);
+            if (!((uint32_t)eI < 10000000u && (uint32_t)nI < 10000000u)) continue;
+            const double xe = (double)eI, ye = (double)nI, inv_div = 1.0 / (double)a.bng_div;
+            const int32_t qe = (int32_t)fma(xe, inv_div, 1e-7), qn = (int32_t)fma(ye, inv_div, 1e-7);
+            const int32_t ce = qe - a.bng_e0, cn = qn - a.bng_n0;
+            if (!((uint32_t)ce < (uint32_t)a.bng_ne && (uint32_t)cn < (uint32_t)a.bng_nn)) continue;
+            const uint32_t e = a.bng_cells[(int64_t)cn * a.bng_ne + ce];
+            if ((e & (kBngPure | kBngLeaf)) != kBngLeaf) continue;
+            const uint32_t base = e & ~kBngLeaf;
+            const float ff = (float)((double)a.bng_C / (double)a.bng_div);
+            const float gxs = fmaf((float)(eI - (int32_t)__umul24((uint32_t)qe, (uint32_t)a.bng_div)), ff, (float)(x[k] - xe) * ff);
+            const float gys = fmaf((float)(nI - (int32_t)__umul24((uint32_t)qn, (uint32_t)a.bng_div)), ff, (float)(y[k] - ye) * ff);
+            const int sx = min(max((int)gxs, 0), a.bng_C - 1), sy = min(max((int)gys, 0), a.bng_C - 1);
+            const uint32_t code = a.bng_leaf[base + (uint32_t)(sy * a.bng_C + sx)];
+            if (code - 0x8000u >= 0x4000u) continue;
+            const uint32_t nrec = code & 0x3fffu;
+            const tiles::LineRec r1 = *(const tiles::LineRec*)(a.bng_leaf + base - 8u * (nrec + 1u));
+            const tiles::LineRec r2 = *(const tiles::LineRec*)(a.bng_leaf + base - 8u * (nrec + 2u));
+            const uint32_t w = tiles::bng_wedge_code(r1, r2, gxs, gys);
+            if (w == (uint32_t)tiles::kMixed) continue;
+            if (w) emit_hit<LDS_COUNTS, PAIRS>(a, row[k], w - 1u, lds);
+            done[k] = true;
+        }
 #pragma unroll
         for (int k = 0; k < R; k++) {
             // NaN: flagged by the stream kernel, no pair
-            if (!live[k] || !bng::point_to_index(x[k], y[k], a.res, &cell[k])) cell[k] = kEmptyKey;
+            if (!live[k] || done[k] || !bng::point_to_index(x[k], y[k], a.res, &cell[k])) cell[k] = kEmptyKey;
             slot[k] = mix64((uint64_t)cell[k]) & a.mask;
         }
         HashEntry he[R];
@@ -1866,6 +1897,7 @@ struct Options {
     int bng_lds = 1;          // BNG dense table: LDS cell level for k_join_stream_bng (chip tables built later)
     int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
     int bng_group_lines = 1;  // BNG levels carry a line code where one line record decides a whole group
+    int bng_wedges = 1;       // BNG tables: wedge records for sub-cells split at a chip vertex
     int mixed_blocks_per_cu = 4;  // k_join_mixed grid: the workgroups resident at once (~120 VGPRs: 4 per CU)
     int mixed_rows = 2;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
@@ -2156,6 +2188,7 @@ struct mosaic_chips {
     bool bng_cpt_ok = false;  // levels built, or no border cell has a leaf block (k_join_stream_bng_cpt applies)
     int32_t bng_lwords = 0, bng_lsh = 0, bng_lnx = 0;  // LDS cell level (BngStreamArgs::lcell); 0 words: none
     int64_t bng_sub_stats[2] = {0, 0};                 // border-cell sub-cells: kMixed, line records
+    int bng_wedges = 0;                                // leaf blocks carry wedge codes (tiles.h)
     bool raster_ok = false;                       // point raster (tiles.h)
     tiles::PointRaster praster{};
     bool stream_ok = false;  // k_join_stream can run on the raster (quad level with compact copies, clamp-safe edges)
@@ -2511,6 +2544,8 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
         o.bng_cell = (int)v;
     } else if (k == "bng_group_lines") {
         o.bng_group_lines = v ? 1 : 0;
+    } else if (k == "bng_wedges") {
+        o.bng_wedges = v ? 1 : 0;
     } else if (k == "timing") {
         if (v < 0 || v > 2) return fail(MOSAIC_E_ARG, "timing must be 0, 1 or 2");
         o.timing = (int)v;
@@ -3655,7 +3690,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                 std::vector<uint32_t>& lbase = lbase_kept;
                 // (leaf element offsets < 2^30, byte offsets below kNoLoad)
                 if (tiles::bng_leaf_blocks(src, border, (double)div, C, c->raster_lines != 0, threads, leaf, lbase,
-                                           c->bng_group_lines ? &bng_glines : nullptr) &&
+                                           c->bng_group_lines ? &bng_glines : nullptr, c->bng_wedges != 0) &&
                     leaf.size() * 2 < (size_t)kNoLoad) {
                     for (size_t b = 0; b < border.size(); b++) {
                         tab[border_at[b]] = kBngLeaf | lbase[b];
@@ -3666,6 +3701,7 @@ static int chip_table_create(ThreadCtx* c, int grid, int res, int64_t n_chips, c
                         }
                     }
                     ch->bng_C = C;
+                    ch->bng_wedges = c->bng_wedges && c->raster_lines ? 1 : 0;
                 } else {
                     leaf.clear();
                 }
@@ -4247,6 +4283,7 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
             a.bng_div = ch->bng_div;
             a.bng_leaf = (const uint16_t*)ch->bng_leaf.p;
             a.bng_C = ch->bng_C;
+            a.bng_wedge = ch->bng_C > 0 && ch->bng_wedges ? 1 : 0;
             BngStreamArgs bs;
             bs.e0 = ch->bng_e0;
             bs.n0 = ch->bng_n0;

@@ -722,9 +722,21 @@ inline uint16_t bng_level_code(const uint16_t* e, int C, int bi, int bj) {
 // the widened group square classify to its pos / neg), else kSubBlock.  The level then carries that
 // line code, so k_join_stream_bng_cpt gathers the record without the leaf code (a level code is a
 // valid answer for every point of its group, as before).
+// wedges: a sub-cell split by two chip segments that share a vertex gets the leaf code
+// kSubBlock | n (no line bit): records n and n + 1 (cell frame) are the two segments' lines, oriented
+// so that the convex wedge is s >= 1 on both; its code is record n's pos, the reflex side's (s <= -1
+// on either line) its neg; both regions certified like a line record's sides.  The stream kernels
+// send such rows to the mixed queue and k_join_mixed_bng answers them from the two records when the
+// point lies outside both bands (bng_wedge_code), before any chip test.
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
                      bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base,
-                     std::vector<uint16_t>* glines = nullptr);
+                     std::vector<uint16_t>* glines = nullptr, bool wedges = false);
+MOSAIC_HD uint32_t bng_wedge_code(const LineRec& r1, const LineRec& r2, float u, float v) {
+    const float s1 = fmaf(r1.a, u, fmaf(r1.b, v, r1.c)), s2 = fmaf(r2.a, u, fmaf(r2.b, v, r2.c));
+    if (s1 >= 1.0f && s2 >= 1.0f) return r1.pos;
+    if (s1 <= -1.0f || s2 <= -1.0f) return r1.neg;
+    return kMixed;
+}
 
 }  // namespace tiles
 }  // namespace mosaic

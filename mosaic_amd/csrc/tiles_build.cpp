@@ -765,7 +765,7 @@ bool Builder::assemble_raster(const RasterClass& rc, int threads) {
 
 bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorderCell>& cells, double side, int C,
                      bool lines, int threads, std::vector<uint16_t>& blocks, std::vector<uint32_t>& base,
-                     std::vector<uint16_t>* glines) {
+                     std::vector<uint16_t>* glines, bool wedges) {
     if (C < 1 || C > 64) return false;
     const int CB = bng_level_side(C), G = kBngLvlG;
     if (glines) glines->assign(cells.size() * (size_t)CB * CB, kSubBlock);
@@ -882,6 +882,109 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                 }
                 return false;
             };
+            // a mixed sub-cell split by two segments sharing a vertex (tiles.h bng_leaf_blocks wedges):
+            // the two longest clipped pieces' segments, their lines oriented so that the convex
+            // wedge is s >= 0 on both, both regions certified
+            auto try_wedge = [&](int i, int j, LineRec& o1, LineRec& o2) -> bool {
+                const double rx0 = bc.x0 + h * i, ry0 = bc.y0 + h * j;
+                const double exu = ex / h, eyv = ey / h;
+                const double bx0 = rx0 - ex, bx1 = rx0 + h + ex, by0 = ry0 - ey, by1 = ry0 + h + ey;
+                // the longest clipped piece's segment, then the longest piece of a different segment
+                // (adjacent zones' chips carry the same boundary segment: equal ends either way round)
+                double l1 = 0.0, l2 = 0.0;
+                const Seg* s1 = nullptr;
+                const Seg* s2 = nullptr;
+                auto same = [](const Seg* p, const Seg& q) {
+                    return (p->ax == q.ax && p->ay == q.ay && p->bx == q.bx && p->by == q.by) ||
+                           (p->ax == q.bx && p->ay == q.by && p->bx == q.ax && p->by == q.ay);
+                };
+                for (int pass = 0; pass < 2; pass++) {
+                    if (pass == 1 && !s1) return false;
+                    for (size_t b = 0; b < border.size(); b++) {
+                        const pip::Box& bx = src.store.geom_bbox[border[b]];
+                        if (bx.maxx < bx0 || bx.minx > bx1 || bx.maxy < by0 || bx.miny > by1) continue;
+                        for (const Seg& e : csegs[b]) {
+                            if (pass == 1 && same(s1, e)) continue;
+                            double ax = (e.ax - rx0) / h, ay = (e.ay - ry0) / h;
+                            double qx = (e.bx - rx0) / h, qy = (e.by - ry0) / h;
+                            if (!clip_seg(ax, ay, qx, qy, -exu, -eyv, 1.0 + exu, 1.0 + eyv)) continue;
+                            const double l = (qx - ax) * (qx - ax) + (qy - ay) * (qy - ay);
+                            if (pass == 0 && l > l1) {
+                                l1 = l;
+                                s1 = &e;
+                            } else if (pass == 1 && l > l2) {
+                                l2 = l;
+                                s2 = &e;
+                            }
+                        }
+                    }
+                }
+                if (!s1 || !s2 || !(l2 > 1e-6)) return false;
+                P2 V, A1, A2;  // the shared vertex and the segments' other ends (metres)
+                if (s1->bx == s2->ax && s1->by == s2->ay) {
+                    V = P2{s1->bx, s1->by}; A1 = P2{s1->ax, s1->ay}; A2 = P2{s2->bx, s2->by};
+                } else if (s1->ax == s2->bx && s1->ay == s2->by) {
+                    V = P2{s1->ax, s1->ay}; A1 = P2{s1->bx, s1->by}; A2 = P2{s2->ax, s2->ay};
+                } else if (s1->ax == s2->ax && s1->ay == s2->ay) {
+                    V = P2{s1->ax, s1->ay}; A1 = P2{s1->bx, s1->by}; A2 = P2{s2->bx, s2->by};
+                } else if (s1->bx == s2->bx && s1->by == s2->by) {
+                    V = P2{s1->bx, s1->by}; A1 = P2{s1->ax, s1->ay}; A2 = P2{s2->ax, s2->ay};
+                } else {
+                    return false;
+                }
+                auto cf = [&](P2 p) { return P2{(p.x - bc.x0) / h, (p.y - bc.y0) / h}; };  // cell frame
+                V = cf(V);
+                A1 = cf(A1);
+                A2 = cf(A2);
+                auto line_of = [&](P2 A, P2 O, double* a, double* b, double* c) -> bool {  // through V, A; O on the + side
+                    const double L = sqrt((A.x - V.x) * (A.x - V.x) + (A.y - V.y) * (A.y - V.y));
+                    if (!(L > 0.0)) return false;
+                    *a = -(A.y - V.y) / L;
+                    *b = (A.x - V.x) / L;
+                    *c = -(*a * V.x + *b * V.y);
+                    const double so = *a * O.x + *b * O.y + *c;
+                    if (so < 0) {
+                        *a = -*a;
+                        *b = -*b;
+                        *c = -*c;
+                    }
+                    return fabs(so) > 1e-9;  // (collinear: a line record's case)
+                };
+                double a1, b1, c1, a2, b2, c2;
+                if (!line_of(A1, A2, &a1, &b1, &c1) || !line_of(A2, A1, &a2, &b2, &c2)) return false;
+                const P2 sq[4] = {{-exu, -eyv}, {1.0 + exu, -eyv}, {1.0 + exu, 1.0 + eyv}, {-exu, 1.0 + eyv}};
+                for (int mk = 0; mk < 4; mk++) {
+                    const double margin = rbuild::line_margin(mk);
+                    o1 = LineRec{(float)(a1 / margin), (float)(b1 / margin), (float)(c1 / margin), 0, 0};
+                    o2 = LineRec{(float)(a2 / margin), (float)(b2 / margin), (float)(c2 / margin), 0, 0};
+                    const double A1c = o1.a, B1c = o1.b, C1 = (double)o1.c + A1c * i + B1c * j;
+                    const double A2c = o2.a, B2c = o2.b, C2 = (double)o2.c + A2c * i + B2c * j;
+                    const double m1 = 1.0 - rbuild::line_slack_tile(A1c, B1c, o1.c, C, kLineSlack);
+                    const double m2 = 1.0 - rbuild::line_slack_tile(A2c, B2c, o2.c, C, kLineSlack);
+                    P2 t[8], w[8], r1[8], r2[8];
+                    const int nt = clip_half(sq, 4, A1c, B1c, C1 - m1, t);
+                    const int nw = nt >= 3 ? clip_half(t, nt, A2c, B2c, C2 - m2, w) : 0;
+                    const int n1 = clip_half(sq, 4, -A1c, -B1c, -C1 - m1, r1), n2 = clip_half(sq, 4, -A2c, -B2c, -C2 - m2, r2);
+                    auto metres = [&](P2* q, int n) {
+                        for (int v = 0; v < n; v++) q[v] = P2{rx0 + h * q[v].x, ry0 + h * q[v].y};
+                    };
+                    metres(w, nw);
+                    metres(r1, n1);
+                    metres(r2, n2);
+                    const uint16_t cw = nw >= 3 ? classify_poly(w, nw) : 0;
+                    if (cw == kMixed) continue;
+                    const uint16_t cr1 = n1 >= 3 ? classify_poly(r1, n1) : kSubBlock;
+                    if (cr1 == kMixed) continue;
+                    const uint16_t cr2 = n2 >= 3 ? classify_poly(r2, n2) : kSubBlock;
+                    if (cr2 == kMixed) continue;
+                    if (cr1 != kSubBlock && cr2 != kSubBlock && cr1 != cr2) return false;
+                    const uint16_t cr = cr1 != kSubBlock ? cr1 : (cr2 != kSubBlock ? cr2 : (uint16_t)0);
+                    o1.pos = o2.pos = cw;
+                    o1.neg = o2.neg = cr;
+                    return true;
+                }
+                return false;
+            };
             std::vector<uint16_t>& e = ent[(size_t)k];
             e.assign(CCp, 0);
             for (int j = 0; j < C; j++)
@@ -908,6 +1011,13 @@ bool bng_leaf_blocks(const Builder::ChipSource& src, const std::vector<BngBorder
                         while (n < lrec[(size_t)k].size() && memcmp(&lrec[(size_t)k][n], &lr, sizeof(LineRec))) n++;
                         code = (uint16_t)(kSubBlock | kLineBit | n);
                         if (n == lrec[(size_t)k].size()) lrec[(size_t)k].push_back(lr);
+                    } else if (code == kMixed && lines && wedges && lrec[(size_t)k].size() + 2 <= 0x3fffu) {
+                        LineRec w2;
+                        if (try_wedge(i, j, lr, w2)) {
+                            code = (uint16_t)(kSubBlock | lrec[(size_t)k].size());
+                            lrec[(size_t)k].push_back(lr);
+                            lrec[(size_t)k].push_back(w2);
+                        }
                     }
                     e[(size_t)j * C + i] = code;
                 }

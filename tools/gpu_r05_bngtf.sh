@@ -11,6 +11,6 @@ timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thre
 echo tests done
 for k in ${REPS:-1 2}; do
   timeout -k 10 200 python3 -u tools/kbench_bng.py --reps 5 --sweep bng_group_lines=1 > $O/c5_new$k.txt 2>&1 || exit 1
-  timeout -k 10 200 python3 -u tools/kbench_bng.py --reps 5 --build-opts bng_group_lines=0 > $O/c5_old$k.txt 2>&1 || exit 1
+  timeout -k 10 200 python3 -u tools/kbench_bng.py --reps 5 --build-opts ${OLD_OPTS:-bng_wedges=0} > $O/c5_old$k.txt 2>&1 || exit 1
 done
 echo kbench done
