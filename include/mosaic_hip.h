@@ -64,8 +64,13 @@
 extern "C" {
 #endif
 
-/* 2: mosaic_chip_table_raster writes 8 values (was 5); option "exact_cap"; the aggregate geometry. */
-#define MOSAIC_ABI_VERSION 3
+/* 2: mosaic_chip_table_raster writes 8 values (was 5); option "exact_cap"; the aggregate geometry.
+ * 3: mosaic_chip_table_raster writes 9 values (out9[8] = leaf_lines; callers must pass 9 slots);
+ *    mosaic_intersection_aggregate_geometry; mosaic_cell_kring count -4 for rows with k > 128 near a
+ *    pentagon (now answered, see 4).
+ * 4: border chips are the reference's planar clip against indexToGeometry (mosaic_tessellate);
+ *    mosaic_tess_counters; mosaic_cell_kring answers every row (no -4). */
+#define MOSAIC_ABI_VERSION 4
 
 typedef enum {
     MOSAIC_OK = 0,
@@ -313,16 +318,21 @@ int mosaic_pip_join_pairs(mosaic_ctx* ctx, const mosaic_chips* chips, const doub
  * flat rings: geometry g = parts [geom_parts[g], geom_parts[g+1]); part p = rings
  * [part_rings[p], part_rings[p+1]); ring r = vertices xy[2*ring_offsets[r] ..] (x, y interleaved,
  * lon/lat for H3, BNG metres for BNG).  Chip rows carry the geometry index as their key.
- * densify >= 1 subdivides H3 cell edges (1 = the 6-vertex h3ToGeoBoundary polygon; border chips keep
- * straight sides between hexagon corners either way).  H3 geometries spanning icosahedron faces are
- * cut into per-face pieces merged per cell: a core chip's geometry is then the cell boundary
- * (h3ToGeoBoundary, one Polygon), a border chip over the face edge a MultiPolygon whose parts meet
- * along that edge (JTS contains -- the join's predicate -- reads it as one region, PointLocator's
- * Mod-2 rule; JTS overlay operations may reject it: such chips are for the join, not for overlay
- * fallbacks); MOSAIC_E_ARG for a geometry with a vertex more than ~78 degrees from the centre of a
- * face it meets.
+ * Cells are enumerated and classified (core / border / none) in the plane where they are exact
+ * (H3: the icosahedron face's gnomonic plane; BNG: metres).  A border chip is the reference's
+ * `geometry.intersection(indexToGeometry(cell))` (IndexSystem.getBorderChips): the geometry clipped
+ * in its own coordinates against the cell polygon -- H3: the h3ToGeoBoundary ring in degrees (JDK 8
+ * Math.toDegrees) with straight sides, face-edge vertices included; BNG: the square -- with JTS
+ * 1.19's crossing arithmetic (RobustLineIntersector / Intersection.intersection), every ring written
+ * from its lowest vertex, shells counter-clockwise, holes clockwise, polygons by lowest vertex (the
+ * order of the reference's rendered chips); a border chip equal to its cell is a core chip
+ * (`intersect.equals(indexGeom)`).  A core chip's geometry is indexToGeometry(cell) (densify > 1: H3
+ * core outlines follow the cell's arcs with `densify` points a side instead).  Cells the planar clip
+ * cannot take (over the antimeridian or a pole) are clipped in the face plane instead
+ * (mosaic_tess_counters counts them).  MOSAIC_E_ARG for a geometry with a vertex more than ~78 degrees
+ * from the centre of a face it meets.
  * Reference: expressions/index/MosaicExplode.scala:70-79, core/Mosaic.scala:21-87,
- * core/index/IndexSystem.scala:152-186. */
+ * core/index/IndexSystem.scala:152-186, core/index/H3IndexSystem.scala:93-100. */
 typedef struct mosaic_chip_set mosaic_chip_set;
 int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                       const int64_t* ring_offsets, const double* xy, int keep_core_geom, int densify,
@@ -344,14 +354,17 @@ int mosaic_chip_set_destroy(mosaic_chip_set* cs);
  * IndexSystem.getBorderChips / getCoreChips (core/index/IndexSystem.scala:152-186, via
  * Mosaic.mosaicFill core/Mosaic.scala:60-87).  BNG: k_bng_tess_classify on the cell squares; H3:
  * k_tess_classify_poly on the (densify-subdivided) hexagons in the icosahedron face plane.  Border
- * cells are clipped on the GPU as well (k_tess_clip); candidate enumeration and the chip WKB
- * assembly are host code, as is the per-face routine for H3 geometries spanning faces.  Errors as
- * mosaic_tessellate. */
+ * cells are clipped on the GPU as well (k_tess_clip_ll, one lane per cell, the host routine's
+ * arithmetic); candidate enumeration, the per-face pieces of H3 geometries spanning faces and the
+ * chip WKB assembly are host code.  Errors as mosaic_tessellate. */
 int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
                           const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
                           int keep_core_geom, int densify, mosaic_chip_set** out);
 /* Duration (HIP events on the context stream) of the last classification launch, ms. */
 double mosaic_tess_last_classify_ms(const mosaic_ctx* ctx);
+/* Process-wide counters of the chip producers' host clip: border chips clipped (ll_chips) and cells
+ * that fell back to the face-plane clip (ll_fallbacks). */
+int mosaic_tess_counters(int64_t* ll_chips, int64_t* ll_fallbacks);
 
 /* ---- st_contains per row ---- */
 /* out[i] = JTS contains(geometry[geom_index[i]], POINT(px[i] py[i])); geometries given as WKB. */

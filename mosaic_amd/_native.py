@@ -33,7 +33,7 @@ EXPORTS = [
     "mosaic_chip_table_create", "mosaic_chip_table_destroy", "mosaic_chip_table_info", "mosaic_chip_table_tiles",
     "mosaic_chip_table_tile_grid", "mosaic_chip_table_raster", "mosaic_pip_join_count",
     "mosaic_pip_join_pairs", "mosaic_st_contains", "mosaic_tessellate", "mosaic_tessellate_gpu",
-    "mosaic_tess_last_classify_ms", "mosaic_chip_set_info",
+    "mosaic_tess_last_classify_ms", "mosaic_tess_counters", "mosaic_chip_set_info",
     "mosaic_chip_set_export", "mosaic_chip_set_columns", "mosaic_chip_set_destroy", "mosaic_kernel_times", "mosaic_last_kernel", "mosaic_point_geom_to_cell",
     "mosaic_point_geom_decode", "mosaic_intersects_aggregate",
     "mosaic_cell_kring", "mosaic_bng_format_column", "mosaic_cell_boundary_wkb", "mosaic_point_to_cell_exact",
@@ -136,6 +136,7 @@ def lib():
         "mosaic_h3_cell_geometry": ([vp, i32, vp, vp, i64, vp, vp], i32),
         "mosaic_tessellate_gpu": ([vp, i32, i32, i64, vp, vp, vp, vp, i32, i32, ctypes.POINTER(vp)], i32),
         "mosaic_tess_last_classify_ms": ([vp], ctypes.c_double),
+        "mosaic_tess_counters": ([ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
         "mosaic_point_to_cell_exact": ([vp, i32, vp, vp, i64, vp], i32),
         "mosaic_diag_libm": ([vp, i32, vp, vp, i64, vp], i32),
         "mosaic_point_coords_to_cell": ([vp, i32, i32, vp, vp, vp, vp, vp, vp, i64, vp, vp, ctypes.POINTER(i64)], i32),

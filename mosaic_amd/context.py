@@ -933,6 +933,14 @@ def tessellate(index_system, polygons, resolution, keep_core_geom=True, densify=
     return dict(is_core=is_core, index_id=index_id, polygon_key=key, wkb=(offs, data))
 
 
+def tessellate_counters():
+    """(border chips clipped by the reference-style planar clip on the host, cells that fell back to
+    the face-plane clip): process-wide counters of the chip producers (mosaic_tess_counters)."""
+    a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+    N.check(N.lib().mosaic_tess_counters(ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
+
+
 class _ChipSetOwner:
     """Holds a mosaic_chip_set whose columns numpy arrays view; destroyed with the last of them."""
 

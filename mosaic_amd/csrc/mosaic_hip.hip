@@ -47,6 +47,7 @@
 #include "point_decode.h"
 #include "raster.h"
 #include "raster_build.h"
+#include "tess_clip.h"
 #include "tess_gpu.h"
 #include "tiles.h"
 
@@ -5565,115 +5566,6 @@ __global__ void __launch_bounds__(256) k_tess_classify_poly(ClassifyPolyArgs a) 
     }
 }
 
-// ---- k_tess_clip: border chips of mosaic_tessellate_gpu (tess_gpu.h), one wave per task.  Per ring
-// of the candidate's geometry: Sutherland-Hodgman against each edge of the clip polygon as a
-// wave-parallel pass (lane i emits the output of input vertex i -- intersection and / or the vertex,
-// as tessellate.cpp's clip_edge -- at its ballot prefix, so the output order is the sequential
-// one), ping-ponging between two scratch buffers of the wave; then the ring's area (summed in order,
-// redundantly on every lane), the degenerate / net-area tests and the output vertices (original
-// vertices copied, computed ones mapped back).
-struct ClipArgs {
-    const double* pxy;  // rings in the clip plane
-    const double* gxy;  // rings in output coordinates (lon / lat or metres)
-    const int64_t *ring_offsets, *part_rings, *geom_parts;
-    const int32_t* cand_geom;
-    const int32_t* gface;
-    const double* clip;
-    int nv, res, mode;
-    const int32_t* clip_n;  // per candidate: its clip polygon's vertices (<= nv, stride nv); nullptr: nv
-    double area_eps;
-    const int64_t* tasks;
-    int64_t n_tasks;
-    const int64_t* tsel;  // when set: the kernel takes the tasks tsel[0 .. n_sel) (positions in tasks)
-    int64_t n_sel;
-    double* sxy;      // per wave: 2 x cap points
-    int32_t* stag;    // per wave: 2 x cap tags
-    int64_t cap;
-    double* out;      // output vertices (interleaved)
-    unsigned long long* counters;  // [0] vertices, [1] rings, [2] parts
-    int64_t out_cap, ring_cap, part_cap;
-    tessclip::ClipRing* rings;
-    tessclip::ClipPart* parts;
-    uint8_t* redo;  // per task
-};
-
-__device__ inline void wave_sync_global() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-// tessellate.cpp FacePlane::to_geo (mode 0) / identity (mode 1)
-__device__ inline void clip_to_geo(const ClipArgs& a, int face, double hx, double hy, double* ox, double* oy) {
-    if (a.mode == 1) {
-        *ox = hx;
-        *oy = hy;
-        return;
-    }
-    const double* b = h3::kH3FastBasis[face];
-    const double* ei = b + ((a.res & 1) ? 9 : 3);
-    const double* ep = b + ((a.res & 1) ? 12 : 6);
-    const double S = h3::kH3FastScale[a.res];
-    double t[3];
-    for (int k = 0; k < 3; k++) t[k] = b[k] + (hx * ei[k] + hy * ep[k]) / S;
-    *ox = glibc::atan2(t[1], t[0]) * (180.0 / M_PI);
-    *oy = glibc::atan2(t[2], sqrt(t[0] * t[0] + t[1] * t[1])) * (180.0 / M_PI);
-}
-
-// one Sutherland-Hodgman pass (clip_edge): returns the output size, or -1 when it exceeds cap
-__device__ inline int64_t clip_pass(const double* ixy, const int32_t* itag, int64_t n, double ax, double ay, double bx,
-                                    double by, double* oxy, int32_t* otag, int64_t cap) {
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    int64_t m = 0;
-    for (int64_t base = 0; base < n; base += 64) {
-        const int64_t i = base + lane;
-        int cnt = 0;
-        double qx = 0, qy = 0, cx = 0, cy = 0;
-        int32_t ct = -1;
-        if (i < n) {
-            const int64_t j = i == 0 ? n - 1 : i - 1;
-            cx = ixy[2 * i];
-            cy = ixy[2 * i + 1];
-            ct = itag[i];
-            const double px = ixy[2 * j], py = ixy[2 * j + 1];
-            const double sc = (bx - ax) * (cy - ay) - (by - ay) * (cx - ax);
-            const double sp = (bx - ax) * (py - ay) - (by - ay) * (px - ax);
-            const bool ic = sc >= 0, ip = sp >= 0;
-            if (ic != ip) {
-                const double t = sp / (sp - sc);
-                qx = px + t * (cx - px);
-                qy = py + t * (cy - py);
-            }
-            cnt = ic ? (ip ? 1 : 2) : (ip ? 1 : 0);
-            // emitted: ic && !ip: [q, cur]; ic && ip: [cur]; !ic && ip: [q]
-            if (!ic && ip) {
-                cx = qx;
-                cy = qy;
-                ct = -1;
-            }
-        }
-        const unsigned long long b1 = __ballot(cnt >= 1), b2 = __ballot(cnt == 2);
-        const int64_t pre = m + __popcll(b1 & lt) + __popcll(b2 & lt);
-        const int64_t tot = __popcll(b1) + __popcll(b2);
-        if (m + tot > cap) return -1;
-        if (cnt == 2) {
-            oxy[2 * pre] = qx;
-            oxy[2 * pre + 1] = qy;
-            otag[pre] = -1;
-            oxy[2 * pre + 2] = cx;
-            oxy[2 * pre + 3] = cy;
-            otag[pre + 1] = ct;
-        } else if (cnt == 1) {
-            oxy[2 * pre] = cx;
-            oxy[2 * pre + 1] = cy;
-            otag[pre] = ct;
-        }
-        m += tot;
-    }
-    return m;
-}
-
 // mosaic_tessellate_gpu's H3 clip polygons generated on the device: candidate k's hexagon around its
 // face-plane centre (cxy), each side cut into D pieces -- tessellate.cpp fill_clip's arithmetic
 // (corner = centre + offset; a + (b - a) t / D, no contraction), so the same doubles.
@@ -5697,416 +5589,164 @@ __global__ void __launch_bounds__(256) k_tess_fill_clip(FillClipArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_tess_clip(ClipArgs a) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    double* bxy[2] = {a.sxy + wave * 4 * a.cap, a.sxy + wave * 4 * a.cap + 2 * a.cap};
-    int32_t* btag[2] = {a.stag + wave * 2 * a.cap, a.stag + wave * 2 * a.cap + a.cap};
-    const int64_t n_work = a.tsel ? a.n_sel : a.n_tasks;
-    for (int64_t u = wave; u < n_work; u += n_waves) {
-        const int64_t t = a.tsel ? a.tsel[u] : u;
-        const int64_t k = a.tasks[t];
-        const int g = a.cand_geom[k];
-        const double* P = a.clip + 2 * (int64_t)a.nv * k;
-        const int nvk = a.clip_n ? a.clip_n[k] : a.nv;
-        const int face = a.mode == 0 ? a.gface[g] : 0;
-        bool redo = false;
-        const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
-        for (int64_t p = p0; p < p1 && !redo; p++) {
-            bool any = false;
-            double net = 0;
-            const int64_t r0 = a.part_rings[p];
-            for (int64_t r = r0; r < a.part_rings[p + 1]; r++) {
-                const int64_t vb = a.ring_offsets[r], n_closed = a.ring_offsets[r + 1] - vb;
-                if (n_closed < 4) continue;
-                const int64_t n = n_closed - 1;  // open vertex list
-                if (n > a.cap) {
-                    redo = true;
-                    break;
-                }
-                for (int64_t i = lane; i < n; i += 64) {
-                    bxy[0][2 * i] = a.pxy[2 * (vb + i)];
-                    bxy[0][2 * i + 1] = a.pxy[2 * (vb + i) + 1];
-                    btag[0][i] = (int32_t)i;
-                }
-                wave_sync_global();
-                int cur = 0;
-                int64_t m = n;
-                for (int e = 0; e < nvk && m > 0; e++) {
-                    const int f = e + 1 == nvk ? 0 : e + 1;
-                    m = clip_pass(bxy[cur], btag[cur], m, P[2 * e], P[2 * e + 1], P[2 * f], P[2 * f + 1], bxy[cur ^ 1],
-                                  btag[cur ^ 1], a.cap);
-                    wave_sync_global();
-                    if (m < 0) break;
-                    cur ^= 1;
-                }
-                if (m < 0) {
-                    redo = true;
-                    break;
-                }
-                const bool shell = r == r0;
-                if (m < 3) {
-                    if (shell) break;  // the shell misses the cell
-                    continue;
-                }
-                const double* vx = bxy[cur];
-                double ar = 0;  // ring_area of the closed ring, in order
-                for (int64_t i = 0; i < m; i++) {
-                    const int64_t j = i + 1 == m ? 0 : i + 1;
-                    ar += vx[2 * i] * vx[2 * j + 1] - vx[2 * j] * vx[2 * i + 1];
-                }
-                ar = 0.5 * ar;
-                if (fabs(ar) <= a.area_eps) {
-                    if (shell) break;
-                    continue;
-                }
-                net += shell ? fabs(ar) : -fabs(ar);
-                any = true;
-                unsigned long long off = 0, rid = 0;
-                if (lane == 0) {
-                    off = atomicAdd(&a.counters[0], (unsigned long long)(m + 1));
-                    rid = atomicAdd(&a.counters[1], 1ull);
-                }
-                off = __shfl(off, 0, 64);
-                rid = __shfl(rid, 0, 64);
-                if ((int64_t)(off + m + 1) > a.out_cap || (int64_t)rid >= a.ring_cap) {
-                    redo = true;
-                    break;
-                }
-                const int32_t* tg = btag[cur];
-                for (int64_t i = lane; i <= m; i += 64) {
-                    const int64_t s_ = i == m ? 0 : i;
-                    double ox, oy;
-                    if (tg[s_] >= 0) {
-                        ox = a.gxy[2 * (vb + tg[s_])];
-                        oy = a.gxy[2 * (vb + tg[s_]) + 1];
-                    } else {
-                        clip_to_geo(a, face, vx[2 * s_], vx[2 * s_ + 1], &ox, &oy);
-                    }
-                    a.out[2 * (off + i)] = ox;
-                    a.out[2 * (off + i) + 1] = oy;
-                }
-                if (lane == 0) a.rings[rid] = tessclip::ClipRing{k, (int32_t)(p - p0), (int32_t)(r - r0), (int64_t)off, (int32_t)(m + 1), 0};
-            }
-            if (any && !redo) {
-                unsigned long long pid = 0;
-                if (lane == 0) pid = atomicAdd(&a.counters[2], 1ull);
-                pid = __shfl(pid, 0, 64);
-                if ((int64_t)pid >= a.part_cap) {
-                    redo = true;
-                } else if (lane == 0) {
-                    a.parts[pid] = tessclip::ClipPart{k, (int32_t)(p - p0), net > a.area_eps ? 1 : 0};
-                }
-            }
-        }
-        if (lane == 0) a.redo[t] = redo ? 1 : 0;
-    }
-}
-
-// ---- k_tess_clip_lane: k_tess_clip for small tasks (every ring of the geometry <= kClipLaneRing
-// vertices, clip polygon <= kClipLaneClip vertices: building-scale inputs), one LANE per task -- the
-// same Sutherland-Hodgman passes run sequentially in the lane's private buffers, so the output
-// vertices, their order, the area sums and the tests are k_tess_clip's (and clip_edge's) exactly.
-// (k_tess_clip spends a wave, global scratch and an agent-scope fence per pass on rings of ~5-13
-// vertices there.)
-static constexpr int kClipLaneRing = 24, kClipLaneClip = 12, kClipLaneCap = kClipLaneRing + kClipLaneClip + 2;
-__global__ void __launch_bounds__(256) k_tess_clip_lane(ClipArgs a) {
-    const int64_t n_work = a.tsel ? a.n_sel : a.n_tasks;
-    double bx[2][kClipLaneCap], by[2][kClipLaneCap];
-    int32_t bt[2][kClipLaneCap];
-    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_work; u += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = a.tsel ? a.tsel[u] : u;
-        const int64_t k = a.tasks[t];
-        const int g = a.cand_geom[k];
-        const double* P = a.clip + 2 * (int64_t)a.nv * k;
-        const int nvk = a.clip_n ? a.clip_n[k] : a.nv;
-        const int face = a.mode == 0 ? a.gface[g] : 0;
-        bool redo = nvk > kClipLaneClip;
-        const int64_t p0 = a.geom_parts[g], p1 = a.geom_parts[g + 1];
-        for (int64_t p = p0; p < p1 && !redo; p++) {
-            bool any = false;
-            double net = 0;
-            const int64_t r0 = a.part_rings[p];
-            for (int64_t r = r0; r < a.part_rings[p + 1]; r++) {
-                const int64_t vb = a.ring_offsets[r], n_closed = a.ring_offsets[r + 1] - vb;
-                if (n_closed < 4) continue;
-                const int64_t n = n_closed - 1;  // open vertex list
-                if (n > kClipLaneRing) {
-                    redo = true;
-                    break;
-                }
-                for (int64_t i = 0; i < n; i++) {
-                    bx[0][i] = a.pxy[2 * (vb + i)];
-                    by[0][i] = a.pxy[2 * (vb + i) + 1];
-                    bt[0][i] = (int32_t)i;
-                }
-                int cur = 0;
-                int64_t m = n;
-                for (int e = 0; e < nvk && m > 0; e++) {
-                    const int f = e + 1 == nvk ? 0 : e + 1;
-                    const double ax = P[2 * e], ay = P[2 * e + 1], bx_ = P[2 * f], by_ = P[2 * f + 1];
-                    int64_t o = 0;
-                    for (int64_t i = 0; i < m; i++) {
-                        const int64_t j = i == 0 ? m - 1 : i - 1;
-                        double cx = bx[cur][i], cy = by[cur][i];
-                        int32_t ct = bt[cur][i];
-                        const double px = bx[cur][j], py = by[cur][j];
-                        const double sc = (bx_ - ax) * (cy - ay) - (by_ - ay) * (cx - ax);
-                        const double sp = (bx_ - ax) * (py - ay) - (by_ - ay) * (px - ax);
-                        const bool ic = sc >= 0, ip = sp >= 0;
-                        double qx = 0, qy = 0;
-                        if (ic != ip) {
-                            const double tt = sp / (sp - sc);
-                            qx = px + tt * (cx - px);
-                            qy = py + tt * (cy - py);
-                        }
-                        const int cnt = ic ? (ip ? 1 : 2) : (ip ? 1 : 0);
-                        if (!ic && ip) {
-                            cx = qx;
-                            cy = qy;
-                            ct = -1;
-                        }
-                        if (o + cnt > kClipLaneCap) {
-                            o = -1;
-                            break;
-                        }
-                        if (cnt == 2) {
-                            bx[cur ^ 1][o] = qx;
-                            by[cur ^ 1][o] = qy;
-                            bt[cur ^ 1][o] = -1;
-                            o++;
-                        }
-                        if (cnt >= 1) {
-                            bx[cur ^ 1][o] = cx;
-                            by[cur ^ 1][o] = cy;
-                            bt[cur ^ 1][o] = ct;
-                            o++;
-                        }
-                    }
-                    m = o;
-                    if (m < 0) break;
-                    cur ^= 1;
-                }
-                if (m < 0) {
-                    redo = true;
-                    break;
-                }
-                const bool shell = r == r0;
-                if (m < 3) {
-                    if (shell) break;  // the shell misses the cell
-                    continue;
-                }
-                double ar = 0;  // ring_area of the closed ring, in order
-                for (int64_t i = 0; i < m; i++) {
-                    const int64_t j = i + 1 == m ? 0 : i + 1;
-                    ar += bx[cur][i] * by[cur][j] - bx[cur][j] * by[cur][i];
-                }
-                ar = 0.5 * ar;
-                if (fabs(ar) <= a.area_eps) {
-                    if (shell) break;
-                    continue;
-                }
-                net += shell ? fabs(ar) : -fabs(ar);
-                any = true;
-                const unsigned long long off = atomicAdd(&a.counters[0], (unsigned long long)(m + 1));
-                const unsigned long long rid = atomicAdd(&a.counters[1], 1ull);
-                if ((int64_t)(off + m + 1) > a.out_cap || (int64_t)rid >= a.ring_cap) {
-                    redo = true;
-                    break;
-                }
-                for (int64_t i = 0; i <= m; i++) {
-                    const int64_t s_ = i == m ? 0 : i;
-                    double ox, oy;
-                    if (bt[cur][s_] >= 0) {
-                        ox = a.gxy[2 * (vb + bt[cur][s_])];
-                        oy = a.gxy[2 * (vb + bt[cur][s_]) + 1];
-                    } else {
-                        clip_to_geo(a, face, bx[cur][s_], by[cur][s_], &ox, &oy);
-                    }
-                    a.out[2 * (off + i)] = ox;
-                    a.out[2 * (off + i) + 1] = oy;
-                }
-                a.rings[rid] = tessclip::ClipRing{k, (int32_t)(p - p0), (int32_t)(r - r0), (int64_t)off, (int32_t)(m + 1), 0};
-            }
-            if (any && !redo) {
-                const unsigned long long pid = atomicAdd(&a.counters[2], 1ull);
-                if ((int64_t)pid >= a.part_cap) redo = true;
-                else a.parts[pid] = tessclip::ClipPart{k, (int32_t)(p - p0), net > a.area_eps ? 1 : 0};
-            }
-        }
-        a.redo[t] = redo ? 1 : 0;
-    }
-}
-
 }  // namespace tessgpu
 
 // host side of the border clipping (tess_gpu.h)
 
-// The tasks split for k_tess_clip_lane (every ring of the geometry and the clip polygon small) and
-// k_tess_clip (the rest), uploaded as one selection list [small..., large...]; both kernels launched
-// (they append to the same outputs).
-static int launch_clip_kernels(ThreadCtx* c, tessgpu::ClipArgs a, int64_t n_tasks, const int64_t* tasks,
-                               const int32_t* cand_geom, const int64_t* geom_parts, const int64_t* part_rings,
-                               const int64_t* ring_offsets, int nv, int64_t n_waves, DevBuf& d_sel) {
-    std::vector<int64_t> sel((size_t)n_tasks);
-    int64_t n_small = 0, n_large = 0;
-    for (int64_t t = 0; t < n_tasks; t++) {
-        const int g = cand_geom[tasks[t]];
-        bool small = nv <= tessgpu::kClipLaneClip;
-        for (int64_t r = part_rings[geom_parts[g]]; small && r < part_rings[geom_parts[g + 1]]; r++)
-            small = ring_offsets[r + 1] - ring_offsets[r] - 1 <= tessgpu::kClipLaneRing;
-        if (small) sel[(size_t)n_small++] = t;
-        else sel[(size_t)(n_tasks - 1 - n_large++)] = t;
+// The border candidates `tasks` clipped on the device by k_tess_clip_ll (tess_clip.hip) -- geometry
+// arrays already on the device (d*), cell polygons from the candidates' H3 ids (d_cid, mode 0) or
+// given (d_clip, nv vertices per candidate, mode 1).  Output space: a few points per task beyond the
+// typical chip (a task that does not fit goes to the host, status 1), workspaces for at most
+// n_cu x 128 lanes.
+struct ClipLLBufs {
+    DevBuf tasks, wch, wout, out, cnt, rings, parts, status;
+    void release() {
+        for (DevBuf* b : {&tasks, &wch, &wout, &out, &cnt, &rings, &parts, &status}) b->release();
     }
-    std::reverse(sel.begin() + n_small, sel.end());  // large ones in task order
-    int e = d_sel.reserve(std::max<size_t>((size_t)n_tasks * 8, 16));
-    if (e) return e;
-    if (n_tasks && (e = h2d(c, d_sel.p, sel.data(), (size_t)n_tasks * 8))) return e;
-    if (n_small) {
-        a.tsel = (const int64_t*)d_sel.p;
-        a.n_sel = n_small;
-        const int64_t blocks = std::min<int64_t>((n_small + 255) / 256, (int64_t)c->n_cu * 8);
-        hipLaunchKernelGGL(tessgpu::k_tess_clip_lane, dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
-    }
-    if (n_large) {
-        a.tsel = (const int64_t*)d_sel.p + n_small;
-        a.n_sel = n_large;
-        const int64_t w = std::max<int64_t>(1, std::min<int64_t>(n_waves, n_large));
-        hipLaunchKernelGGL(tessgpu::k_tess_clip, dim3((unsigned)((w + 3) / 4)), dim3(256), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
-    }
-    return MOSAIC_OK;
-}
-int tessclip::clip_border(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
-                         const int64_t* ring_offsets, const double* pxy, const double* gxy, const int32_t* gface, int res,
-                         int mode, int64_t n_tasks, const int64_t* tasks, const int32_t* cand_geom, int64_t n_cand,
-                         const double* clip, int nv, double area_eps, ClipResult* out) {
-    ENTER(ctx);
-    if (!out || n_geoms < 0 || n_tasks < 0 || nv < 3 || (mode == 0 && (res < 0 || res > 15)))
-        return fail(MOSAIC_E_ARG, "invalid argument");
-    out->redo.assign((size_t)n_tasks, 0);
+};
+static int run_clip_ll(ThreadCtx* c, ClipLLBufs& B, const void* d_gxy, const void* d_ro, const void* d_pr, const void* d_gp,
+                       const void* d_cg, const void* d_cid, const void* d_clip, int nv, int mode,
+                       const std::vector<int64_t>& tasks, const int32_t* cand_geom, const int64_t* geom_parts,
+                       const int64_t* part_rings, const int64_t* ring_offsets, tessclip::ClipResult* out) {
+    const int64_t n_tasks = (int64_t)tasks.size();
+    out->status.assign((size_t)n_tasks, 0);
     out->rings.clear();
     out->parts.clear();
     out->verts.clear();
     out->kernel_ms = 0;
     if (n_tasks == 0) return MOSAIC_OK;
-    const int64_t n_parts = geom_parts[n_geoms], n_rings = part_rings[n_parts], n_verts = ring_offsets[n_rings];
-    int64_t maxn = 1, ring_cap = 0, part_cap = 0;
-    for (int64_t r = 0; r < n_rings; r++) maxn = std::max<int64_t>(maxn, ring_offsets[r + 1] - ring_offsets[r]);
+    // output bound per task: its geometry's vertices + events and cell vertices, capped near the
+    // typical chip size (the rest to the host)
+    int64_t bound = 0;
     for (int64_t t = 0; t < n_tasks; t++) {
-        if (tasks[t] < 0 || tasks[t] >= n_cand) return fail(MOSAIC_E_ARG, "task out of range");
-        const int g = cand_geom[tasks[t]];
-        if (g < 0 || g >= n_geoms || (mode == 0 && (gface[g] < 0 || gface[g] >= 20)))
-            return fail(MOSAIC_E_ARG, "candidate geometry out of range");
-        part_cap += geom_parts[g + 1] - geom_parts[g];
-        ring_cap += part_rings[geom_parts[g + 1]] - part_rings[geom_parts[g]];
+        const int g = cand_geom[tasks[(size_t)t]];
+        bound += ring_offsets[part_rings[geom_parts[g + 1]]] - ring_offsets[part_rings[geom_parts[g]]] + 4 * mosaic::tessll::kLLChains + 32;
+    }
+    const int64_t out_cap = std::min<int64_t>(bound, n_tasks * 96 + ((int64_t)1 << 20));
+    const int64_t ring_cap = n_tasks * mosaic::tessll::kLLOut, part_cap = ring_cap;
+    const int64_t lanes = std::max<int64_t>(64, std::min<int64_t>(n_tasks, (int64_t)c->n_cu * 128));
+    int rc;
+    if ((rc = B.tasks.reserve((size_t)n_tasks * 8)) || (rc = B.wch.reserve((size_t)lanes * mosaic::tessll::kLLChains * sizeof(llclip::Chain))) ||
+        (rc = B.wout.reserve((size_t)lanes * mosaic::tessll::kLLOut * sizeof(llclip::Out))) || (rc = B.out.reserve((size_t)out_cap * 16)) ||
+        (rc = B.cnt.reserve(32)) || (rc = B.rings.reserve((size_t)ring_cap * sizeof(tessclip::ClipRing))) ||
+        (rc = B.parts.reserve((size_t)part_cap * sizeof(tessclip::ClipPart))) || (rc = B.status.reserve((size_t)n_tasks)))
+        return rc;
+    if ((rc = h2d(c, B.tasks.p, tasks.data(), (size_t)n_tasks * 8))) return rc;
+    HIP_TRY(hipMemsetAsync(B.cnt.p, 0, 32, c->stream));
+    mosaic::tessll::ClipLLArgs a;
+    a.gxy = (const double*)d_gxy;
+    a.ring_offsets = (const int64_t*)d_ro;
+    a.part_rings = (const int64_t*)d_pr;
+    a.geom_parts = (const int64_t*)d_gp;
+    a.cand_geom = (const int32_t*)d_cg;
+    a.cand_id = (const int64_t*)d_cid;
+    a.clip = (const double*)d_clip;
+    a.nv = nv;
+    a.mode = mode;
+    a.tasks = (const int64_t*)B.tasks.p;
+    a.n_tasks = n_tasks;
+    a.wch = (llclip::Chain*)B.wch.p;
+    a.wout = (llclip::Out*)B.wout.p;
+    a.out = (double*)B.out.p;
+    a.counters = (unsigned long long*)B.cnt.p;
+    a.out_cap = out_cap;
+    a.ring_cap = ring_cap;
+    a.part_cap = part_cap;
+    a.rings = (tessclip::ClipRing*)B.rings.p;
+    a.parts = (tessclip::ClipPart*)B.parts.p;
+    a.status = (uint8_t*)B.status.p;
+    EventGuard ev;
+    HIP_TRY(hipEventCreate(&ev.e[0]));
+    HIP_TRY(hipEventCreate(&ev.e[1]));
+    HIP_TRY(hipEventRecord(ev.e[0], c->stream));
+    HIP_TRY(mosaic::tessll::launch_clip_ll(a, lanes, c->stream));
+    HIP_TRY(hipEventRecord(ev.e[1], c->stream));
+    unsigned long long cnt[3];
+    if ((rc = d2h(c, cnt, B.cnt.p, sizeof cnt))) return rc;
+    if ((rc = d2h(c, out->status.data(), B.status.p, (size_t)n_tasks))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // (counters past a cap: those tasks came back with status 1; the space before is valid)
+    const int64_t nv_out = std::min<int64_t>((int64_t)cnt[0], out_cap), nr = std::min<int64_t>((int64_t)cnt[1], ring_cap),
+                  np = std::min<int64_t>((int64_t)cnt[2], part_cap);
+    out->verts.resize((size_t)nv_out * 2);
+    out->rings.resize((size_t)nr);
+    out->parts.resize((size_t)np);
+    if (nv_out && (rc = d2h(c, out->verts.data(), B.out.p, (size_t)nv_out * 16))) return rc;
+    if (nr && (rc = d2h(c, out->rings.data(), B.rings.p, (size_t)nr * sizeof(tessclip::ClipRing)))) return rc;
+    if (np && (rc = d2h(c, out->parts.data(), B.parts.p, (size_t)np * sizeof(tessclip::ClipPart)))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // drop the records of tasks that went to the host (an overflowing task may have taken ring / part
+    // slots before its check failed: it wrote nothing into them)
+    {
+        std::vector<uint8_t> host(out->status.size());
+        std::unordered_map<int64_t, int64_t> pos;
+        for (int64_t t = 0; t < n_tasks; t++) pos[tasks[(size_t)t]] = t;
+        auto keep_ring = [&](const tessclip::ClipRing& r) { auto it = pos.find(r.cand); return it != pos.end() && out->status[(size_t)it->second] != 1; };
+        auto keep_part = [&](const tessclip::ClipPart& r) { auto it = pos.find(r.cand); return it != pos.end() && out->status[(size_t)it->second] != 1; };
+        out->rings.erase(std::remove_if(out->rings.begin(), out->rings.end(), [&](const tessclip::ClipRing& r) { return !keep_ring(r); }), out->rings.end());
+        out->parts.erase(std::remove_if(out->parts.begin(), out->parts.end(), [&](const tessclip::ClipPart& r) { return !keep_part(r); }), out->parts.end());
+    }
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ev.e[0], ev.e[1]);
+    out->kernel_ms = ms;
+    return MOSAIC_OK;
+}
+
+int tessclip::clip_ll(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
+                      const int64_t* ring_offsets, const double* xy, const std::vector<int64_t>& tasks,
+                      const int32_t* cand_geom, int64_t n_cand, const double* clip, int nv, ClipResult* out) {
+    ENTER(ctx);
+    if (!out || n_geoms < 0 || nv < 3 || nv > 16) return fail(MOSAIC_E_ARG, "invalid argument");
+    for (int64_t k : tasks)
+        if (k < 0 || k >= n_cand || cand_geom[k] < 0 || cand_geom[k] >= n_geoms) return fail(MOSAIC_E_ARG, "task out of range");
+    if (tasks.empty()) {
+        out->status.clear();
+        out->rings.clear();
+        out->parts.clear();
+        out->verts.clear();
+        out->kernel_ms = 0;
+        return MOSAIC_OK;
     }
     HIP_TRY(hipSetDevice(c->device));
-    // per-wave scratch: 2 buffers of cap points; as many waves as a 2 GiB budget holds
-    const int64_t cap = 2 * maxn + 4 * (int64_t)nv + 64, per_wave = 2 * cap * (16 + 4);
-    const int64_t n_waves = std::max<int64_t>(1, std::min<int64_t>({n_tasks, (int64_t)c->n_cu * 8, ((int64_t)2 << 30) / per_wave}));
-    const int64_t out_cap = 2 * n_verts + n_tasks * (3 * (int64_t)nv + 8) + 1024;
-    TmpBuf s_gp, s_pr, s_ro, s_pxy, s_gxy, s_gf, s_cg, s_clip, s_tasks, s_sxy, s_stag, s_out, s_cnt, s_rings, s_parts, s_redo, s_sel;
-    int rc;
+    const int64_t n_parts = geom_parts[n_geoms], n_rings = part_rings[n_parts], n_verts = ring_offsets[n_rings];
+    TmpBuf s_gp, s_pr, s_ro, s_xy, s_cg, s_clip;
+    ClipLLBufs B;
+    struct Rel {
+        ClipLLBufs& b;
+        ~Rel() { b.release(); }
+    } rel{B};
     auto up = [&](TmpBuf& b, const void* src, size_t bytes) -> int {
         int e = b.reserve(std::max<size_t>(bytes, 16));
         if (e) return e;
         if (bytes) if (int e_ = h2d(c, b.p, src, bytes)) return e_;
         return MOSAIC_OK;
     };
+    int rc;
     if ((rc = up(s_gp, geom_parts, (size_t)(n_geoms + 1) * 8)) || (rc = up(s_pr, part_rings, (size_t)(n_parts + 1) * 8)) ||
-        (rc = up(s_ro, ring_offsets, (size_t)(n_rings + 1) * 8)) || (rc = up(s_pxy, pxy, (size_t)n_verts * 16)) ||
-        (rc = up(s_gxy, gxy, (size_t)n_verts * 16)) || (rc = up(s_gf, gface, mode == 0 ? (size_t)n_geoms * 4 : 0)) ||
-        (rc = up(s_cg, cand_geom, (size_t)n_cand * 4)) || (rc = up(s_clip, clip, (size_t)n_cand * nv * 16)) ||
-        (rc = up(s_tasks, tasks, (size_t)n_tasks * 8)) || (rc = s_sxy.reserve((size_t)(n_waves * 4 * cap) * 8)) ||
-        (rc = s_stag.reserve((size_t)(n_waves * 2 * cap) * 4)) || (rc = s_out.reserve((size_t)out_cap * 16)) ||
-        (rc = s_cnt.reserve(32)) || (rc = s_rings.reserve((size_t)std::max<int64_t>(ring_cap, 1) * sizeof(tessclip::ClipRing))) ||
-        (rc = s_parts.reserve((size_t)std::max<int64_t>(part_cap, 1) * sizeof(tessclip::ClipPart))) ||
-        (rc = s_redo.reserve((size_t)n_tasks)))
+        (rc = up(s_ro, ring_offsets, (size_t)(n_rings + 1) * 8)) || (rc = up(s_xy, xy, (size_t)n_verts * 16)) ||
+        (rc = up(s_cg, cand_geom, (size_t)n_cand * 4)) || (rc = up(s_clip, clip, (size_t)n_cand * nv * 16)))
         return rc;
-    HIP_TRY(hipMemsetAsync(s_cnt.p, 0, 32, c->stream));
-    tessgpu::ClipArgs a;
-    a.pxy = (const double*)s_pxy.p;
-    a.gxy = (const double*)s_gxy.p;
-    a.ring_offsets = (const int64_t*)s_ro.p;
-    a.part_rings = (const int64_t*)s_pr.p;
-    a.geom_parts = (const int64_t*)s_gp.p;
-    a.cand_geom = (const int32_t*)s_cg.p;
-    a.gface = (const int32_t*)s_gf.p;
-    a.clip = (const double*)s_clip.p;
-    a.nv = nv;
-    a.clip_n = nullptr;
-    a.res = res;
-    a.mode = mode;
-    a.area_eps = area_eps;
-    a.tasks = (const int64_t*)s_tasks.p;
-    a.n_tasks = n_tasks;
-    a.sxy = (double*)s_sxy.p;
-    a.stag = (int32_t*)s_stag.p;
-    a.cap = cap;
-    a.out = (double*)s_out.p;
-    a.counters = (unsigned long long*)s_cnt.p;
-    a.out_cap = out_cap;
-    a.ring_cap = ring_cap;
-    a.part_cap = part_cap;
-    a.rings = (tessclip::ClipRing*)s_rings.p;
-    a.parts = (tessclip::ClipPart*)s_parts.p;
-    a.redo = (uint8_t*)s_redo.p;
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    if (hipEventCreate(&e1) != hipSuccess) {
-        (void)hipEventDestroy(e0);
-        return fail(MOSAIC_E_HIP, "hipEventCreate failed");
-    }
-    a.tsel = nullptr;
-    a.n_sel = 0;
-    auto run = [&]() -> int {
-        HIP_TRY(hipEventRecord(e0, c->stream));
-        int le = launch_clip_kernels(c, a, n_tasks, tasks, cand_geom, geom_parts, part_rings, ring_offsets, nv, n_waves, s_sel);
-        if (le) return le;
-        HIP_TRY(hipEventRecord(e1, c->stream));
-        unsigned long long cnt[3];
-        if (int e_ = d2h(c, cnt, s_cnt.p, sizeof cnt)) return e_;
-        if (int e_ = d2h(c, out->redo.data(), s_redo.p, (size_t)n_tasks)) return e_;
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        const int64_t nv_out = std::min<int64_t>((int64_t)cnt[0], out_cap), nr = std::min<int64_t>((int64_t)cnt[1], ring_cap),
-                      np = std::min<int64_t>((int64_t)cnt[2], part_cap);
-        out->verts.resize((size_t)nv_out * 2);
-        out->rings.resize((size_t)nr);
-        out->parts.resize((size_t)np);
-        if (nv_out) if (int e_ = d2h(c, out->verts.data(), s_out.p, (size_t)nv_out * 16)) return e_;
-        if (nr) if (int e_ = d2h(c, out->rings.data(), s_rings.p, (size_t)nr * sizeof(tessclip::ClipRing))) return e_;
-        if (np) if (int e_ = d2h(c, out->parts.data(), s_parts.p, (size_t)np * sizeof(tessclip::ClipPart))) return e_;
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        out->kernel_ms = ms;
-        return MOSAIC_OK;
-    };
-    rc = run();
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    return rc;
+    return run_clip_ll(c, B, s_xy.p, s_ro.p, s_pr.p, s_gp.p, s_cg.p, nullptr, s_clip.p, nv, 1, tasks, cand_geom, geom_parts,
+                       part_rings, ring_offsets, out);
 }
 
 // ---- mosaic_tessellate_gpu's H3 branch as one device session: the geometry batch is uploaded once,
-// each chunk of candidates uploads only its centres (16 B each); clip polygons are generated on the
-// device (k_tess_fill_clip), classified (k_tess_classify_poly) and the border ones clipped
-// (k_tess_clip) from the same device arrays.
+// each chunk of candidates uploads only its centres (16 B each) and ids (8 B); clip polygons are
+// generated on the device (k_tess_fill_clip), classified in the face plane (k_tess_classify_poly)
+// and the border ones clipped in lon / lat against their cells' boundaries (k_tess_clip_ll) from the
+// same device arrays.
 struct tessclip::H3Session {
     mosaic_ctx* ctx;
     int64_t n_geoms, n_parts, n_rings, n_verts, maxn;
     const int64_t *geom_parts, *part_rings, *ring_offsets;
     int res, D;
     double dx[6], dy[6];
-    DevBuf d_gp, d_pr, d_ro, d_pxy, d_gxy, d_gf, d_cg, d_cxy, d_clip, d_cls, d_tasks, d_cn;
-    DevBuf d_sxy, d_stag, d_out, d_cnt, d_rings, d_parts, d_redo, d_sel;
+    DevBuf d_gp, d_pr, d_ro, d_pxy, d_gxy, d_gf, d_cg, d_cxy, d_clip, d_cls, d_cn, d_cid, d_cnt;
+    ClipLLBufs ll;
     void release() {
-        for (DevBuf* b : {&d_gp, &d_pr, &d_ro, &d_pxy, &d_gxy, &d_gf, &d_cg, &d_cxy, &d_clip, &d_cls, &d_tasks, &d_sxy, &d_stag,
-                          &d_out, &d_cnt, &d_rings, &d_parts, &d_redo, &d_sel, &d_cn})
+        for (DevBuf* b : {&d_gp, &d_pr, &d_ro, &d_pxy, &d_gxy, &d_gf, &d_cg, &d_cxy, &d_clip, &d_cls, &d_cn, &d_cid, &d_cnt})
             b->release();
+        ll.release();
     }
 };
 
@@ -6164,13 +5804,13 @@ void tessclip::h3_session_end(H3Session* S) {
 }
 
 int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geom, const double* cxy, double eps,
-                               double area_eps, uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out,
+                               uint8_t* cls, std::vector<int64_t>& tasks, ClipResult* out, const int64_t* cand_id,
                                const double* clip_xy, const int32_t* clip_n, int nv_max) {
     ENTER(S->ctx);
     const bool given = clip_xy != nullptr;  // explicit clip polygons (face pieces) instead of hexagons
     const int nv = given ? nv_max : 6 * S->D;
     tasks.clear();
-    out->redo.clear();
+    out->status.clear();
     out->rings.clear();
     out->parts.clear();
     out->verts.clear();
@@ -6192,6 +5832,7 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     } else if ((rc = up(S->d_cxy, cxy, (size_t)nc * 16))) {
         return rc;
     }
+    if (cand_id && (rc = up(S->d_cid, cand_id, (size_t)nc * 8))) return rc;
     tessgpu::FillClipArgs fa;
     fa.cxy = (const double*)S->d_cxy.p;
     fa.n_cand = nc;
@@ -6231,85 +5872,12 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     float cms = 0;
     (void)hipEventElapsedTime(&cms, ev.e[0], ev.e[1]);
     c->last_tess_classify_ms = cms;
-    // the border candidates, clipped on the device (tessclip::clip_border's kernel and sizing)
-    int64_t ring_cap = 0, part_cap = 0;
-    for (int64_t k = 0; k < nc; k++) {
-        if (cls[k] != 2) continue;
-        tasks.push_back(k);
-        const int g = cand_geom[k];
-        part_cap += S->geom_parts[g + 1] - S->geom_parts[g];
-        ring_cap += S->part_rings[S->geom_parts[g + 1]] - S->part_rings[S->geom_parts[g]];
-    }
-    const int64_t n_tasks = (int64_t)tasks.size();
-    out->redo.assign((size_t)n_tasks, 0);
-    if (n_tasks == 0) return MOSAIC_OK;
-    const int64_t cap = 2 * S->maxn + 4 * (int64_t)nv + 64, per_wave = 2 * cap * (16 + 4);
-    const int64_t n_waves = std::max<int64_t>(1, std::min<int64_t>({n_tasks, (int64_t)c->n_cu * 8, ((int64_t)2 << 30) / per_wave}));
-    // output bound: every ring of a task's geometry clipped by a convex nv-gon
-    int64_t task_verts = 0;
-    for (int64_t t = 0; t < n_tasks; t++) {
-        const int g = cand_geom[tasks[(size_t)t]];
-        task_verts += S->ring_offsets[S->part_rings[S->geom_parts[g + 1]]] - S->ring_offsets[S->part_rings[S->geom_parts[g]]];
-    }
-    const int64_t out_cap = 2 * task_verts + n_tasks * (3 * (int64_t)nv + 8) + 1024;
-    if ((rc = up(S->d_tasks, tasks.data(), (size_t)n_tasks * 8)) || (rc = S->d_sxy.reserve((size_t)(n_waves * 4 * cap) * 8)) ||
-        (rc = S->d_stag.reserve((size_t)(n_waves * 2 * cap) * 4)) || (rc = S->d_out.reserve((size_t)out_cap * 16)) ||
-        (rc = S->d_rings.reserve((size_t)std::max<int64_t>(ring_cap, 1) * sizeof(ClipRing))) ||
-        (rc = S->d_parts.reserve((size_t)std::max<int64_t>(part_cap, 1) * sizeof(ClipPart))) ||
-        (rc = S->d_redo.reserve((size_t)n_tasks)))
-        return rc;
-    HIP_TRY(hipMemsetAsync(S->d_cnt.p, 0, 32, c->stream));
-    tessgpu::ClipArgs a;
-    a.pxy = (const double*)S->d_pxy.p;
-    a.gxy = (const double*)S->d_gxy.p;
-    a.ring_offsets = (const int64_t*)S->d_ro.p;
-    a.part_rings = (const int64_t*)S->d_pr.p;
-    a.geom_parts = (const int64_t*)S->d_gp.p;
-    a.cand_geom = (const int32_t*)S->d_cg.p;
-    a.gface = (const int32_t*)S->d_gf.p;
-    a.clip = (const double*)S->d_clip.p;
-    a.nv = nv;
-    a.clip_n = given ? (const int32_t*)S->d_cn.p : nullptr;
-    a.res = S->res;
-    a.mode = 0;
-    a.area_eps = area_eps;
-    a.tasks = (const int64_t*)S->d_tasks.p;
-    a.n_tasks = n_tasks;
-    a.sxy = (double*)S->d_sxy.p;
-    a.stag = (int32_t*)S->d_stag.p;
-    a.cap = cap;
-    a.out = (double*)S->d_out.p;
-    a.counters = (unsigned long long*)S->d_cnt.p;
-    a.out_cap = out_cap;
-    a.ring_cap = ring_cap;
-    a.part_cap = part_cap;
-    a.rings = (ClipRing*)S->d_rings.p;
-    a.parts = (ClipPart*)S->d_parts.p;
-    a.redo = (uint8_t*)S->d_redo.p;
-    a.tsel = nullptr;
-    a.n_sel = 0;
-    HIP_TRY(hipEventRecord(ev.e[0], c->stream));
-    if ((rc = launch_clip_kernels(c, a, n_tasks, tasks.data(), cand_geom, S->geom_parts, S->part_rings, S->ring_offsets, nv,
-                                  n_waves, S->d_sel)))
-        return rc;
-    HIP_TRY(hipEventRecord(ev.e[1], c->stream));
-    unsigned long long cnt[3];
-    if (int e_ = d2h(c, cnt, S->d_cnt.p, sizeof cnt)) return e_;
-    if (int e_ = d2h(c, out->redo.data(), S->d_redo.p, (size_t)n_tasks)) return e_;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    const int64_t nv_out = std::min<int64_t>((int64_t)cnt[0], out_cap), nr = std::min<int64_t>((int64_t)cnt[1], ring_cap),
-                  np = std::min<int64_t>((int64_t)cnt[2], part_cap);
-    out->verts.resize((size_t)nv_out * 2);
-    out->rings.resize((size_t)nr);
-    out->parts.resize((size_t)np);
-    if (nv_out) if (int e_ = d2h(c, out->verts.data(), S->d_out.p, (size_t)nv_out * 16)) return e_;
-    if (nr) if (int e_ = d2h(c, out->rings.data(), S->d_rings.p, (size_t)nr * sizeof(ClipRing))) return e_;
-    if (np) if (int e_ = d2h(c, out->parts.data(), S->d_parts.p, (size_t)np * sizeof(ClipPart))) return e_;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, ev.e[0], ev.e[1]);
-    out->kernel_ms = ms;
-    return MOSAIC_OK;
+    if (!cand_id) return MOSAIC_OK;  // classification only (face pieces)
+    // the border candidates, clipped in lon / lat on the device
+    for (int64_t k = 0; k < nc; k++)
+        if (cls[k] == 2) tasks.push_back(k);
+    return run_clip_ll(c, S->ll, S->d_gxy.p, S->d_ro.p, S->d_pr.p, S->d_gp.p, S->d_cg.p, S->d_cid.p, nullptr, 0, 0, tasks,
+                       cand_geom, S->geom_parts, S->part_rings, S->ring_offsets, out);
 }
 
 extern "C" {

@@ -37,6 +37,7 @@
 #include "h3_device.h"
 #include "h3_geom.h"
 #include "isect_geom.h"
+#include "llclip.h"
 
 #include <unordered_map>
 
@@ -440,6 +441,120 @@ void emit_cell(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::ve
     cs->add(false, cell.id, key, to_wkb(out_parts));
 }
 
+// ---- border chips as the reference builds them (llclip.h): geometry n cell polygon in output
+// coordinates, with JTS's crossing arithmetic.  Cells the planar clip cannot take (a cell over the
+// antimeridian or a pole; a ring walk whose labels do not pair up) fall back to clip_cell in the
+// plane of `pl` and are counted (mosaic_tess_counters).
+std::atomic<int64_t> g_ll_fallbacks{0}, g_ll_chips{0};
+
+// H3 cell id -> its indexToGeometry polygon (h3ToGeoBoundary, degrees via JDK 8 Math.toDegrees, as
+// H3IndexSystem.scala:93-100 builds it); false when it is not a planar counter-clockwise polygon
+bool h3_cell_ll(int64_t id, llclip::Cell& C) {
+    double b[20];
+    const int nb = h3geom::h3_to_geo_boundary((uint64_t)id, b);
+    if (nb < 3 || nb > 16) return false;
+    C.nc = nb;
+    for (int v = 0; v < nb; v++) C.v[v] = {h3geom::to_degrees(b[2 * v + 1], 8), h3geom::to_degrees(b[2 * v], 8)};
+    llclip::cell_init(C);
+    return llclip::cell_ok(C, true);
+}
+// BNG square (BNGIndexSystem.indexToGeometry: (x, y), (x + e, y), (x + e, y + e), (x, y + e))
+bool bng_cell_ll(double x0, double y0, double e, llclip::Cell& C) {
+    C.nc = 4;
+    C.v[0] = {x0, y0};
+    C.v[1] = {x0 + e, y0};
+    C.v[2] = {x0 + e, y0 + e};
+    C.v[3] = {x0, y0 + e};
+    llclip::cell_init(C);
+    return llclip::cell_ok(C, false);
+}
+
+// The chip of geometry gg against C as WKB (empty: no chip); llclip status.  Host scratch grows on
+// overflow, so only kInconsistent / kBadCell come back non-zero.
+int ll_chip(const llclip::Geom& gg, const llclip::Cell& C, bool* is_cell, std::vector<uint8_t>& wkb) {
+    thread_local std::vector<llclip::Chain> ch;
+    thread_local std::vector<llclip::Out> out;
+    thread_local std::vector<double> buf;
+    const double eps2 = 1e-12 * llclip::cell_area2(C);
+    for (size_t cap = 64;; cap *= 4) {
+        if (ch.size() < cap) ch.resize(cap);
+        if (out.size() < cap) out.resize(cap);
+        llclip::Work w{ch.data(), (int32_t)cap, out.data(), (int32_t)cap, 0, 0};
+        int32_t polys = 0;
+        const int st = llclip::clip(gg, C, w, eps2, &polys, is_cell);
+        if (st == llclip::kOverflow && cap < ((size_t)1 << 22)) continue;
+        if (st) return st;
+        wkb.clear();
+        if (polys == 0) return llclip::kOk;
+        WkbOut wo;
+        if (polys > 1) {
+            wo.u8(0);
+            wo.u32(6);
+            wo.u32((uint32_t)polys);
+        }
+        for (int32_t i = 0; i < w.n_out;) {
+            int32_t j = i + 1;
+            while (j < w.n_out && w.out[j].hole) j++;
+            wo.u8(0);
+            wo.u32(3);
+            wo.u32((uint32_t)(j - i));
+            for (int32_t k = i; k < j; k++) {
+                const int32_t n = w.out[k].npts;
+                buf.resize(2 * (size_t)(n + 1));
+                llclip::write_ring(gg, C, w, w.out[k], buf.data());
+                wo.u32((uint32_t)(n + 1));
+                for (int32_t v = 0; v <= n; v++) {
+                    wo.f64(buf[2 * (size_t)v]);
+                    wo.f64(buf[2 * (size_t)v + 1]);
+                }
+            }
+            i = j;
+        }
+        wkb.swap(wo.b);
+        g_ll_chips++;
+        return llclip::kOk;
+    }
+}
+
+// C as a closed ring (a core chip's indexToGeometry)
+std::vector<P2> cell_ll_ring(const llclip::Cell& C) {
+    std::vector<P2> r;
+    for (int v = 0; v <= C.nc; v++) r.push_back({C.v[v % C.nc].x, C.v[v % C.nc].y});
+    return r;
+}
+
+// emit_cell with the reference's border chips: classification in the plane of pl (as emit_cell),
+// border cells clipped against C (make_c(C) fills it; false: no planar polygon) in output coordinates;
+// core chips carry C itself when core_from_c (H3 without densify, BNG), else the plane outline.
+template <class ToGeo, class MakeC>
+void emit_cell_ll(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std::vector<std::vector<std::vector<P2>>>& pl,
+                  const std::vector<std::vector<std::vector<P2>>>& geo, const llclip::Geom& gg, double core_eps,
+                  int keep_core_geom, ToGeo to_geo, double area_eps, MakeC make_c, bool core_from_c, int pre = -1) {
+    const int cls = pre >= 0 ? pre : classify_cell(cell, pl, core_eps);
+    if (cls == 0) return;
+    llclip::Cell C;
+    const bool cok = make_c(C);
+    if (cls == 1) {
+        std::vector<uint8_t> blob;
+        if (keep_core_geom) blob = to_wkb({{core_from_c && cok ? cell_ll_ring(C) : cell_ring(cell, to_geo)}});
+        cs->add(true, cell.id, key, blob);
+        return;
+    }
+    if (cok) {
+        bool is_cell = false;
+        std::vector<uint8_t> blob;
+        if (ll_chip(gg, C, &is_cell, blob) == llclip::kOk) {
+            if (!blob.empty()) cs->add(is_cell, cell.id, key, is_cell && !keep_core_geom ? std::vector<uint8_t>() : blob);
+            return;
+        }
+    }
+    g_ll_fallbacks++;
+    std::vector<std::vector<std::vector<P2>>> out_parts;
+    clip_cell(cell, pl, geo, to_geo, area_eps, out_parts);
+    if (out_parts.empty()) return;
+    cs->add(false, cell.id, key, to_wkb(out_parts));
+}
+
 // ---- H3 polygons that span icosahedron faces ----
 // geoToH3 projects a point onto its closest face (largest fc . p) and rounds in that face's
 // gnomonic plane, so a cell is, on the sphere, the union over faces f of (hexagon of its lattice
@@ -671,30 +786,34 @@ void multiface_classify_host(MultiFace& mf, const Geo3& geo, int res) {
         for (MultiPiece& pc : mf.pieces) {
             if (pc.face != mf.faces[k]) continue;
             pc.cls = classify_cell(pc.cell, mf.pl[k], 1e-3);
-            if (pc.cls == 2) clip_cell(pc.cell, mf.pl[k], geo, [&](P2 h) { return fp.to_geo(h); }, 1e-12, pc.parts);
         }
     }
 }
 
-// The chips of the classified pieces, in cell first-seen order.
-void multiface_emit(mosaic_chip_set* cs, int32_t key, int res, int keep_core_geom, const MultiFace& mf) {
+// The chips of the classified pieces, in cell first-seen order: a cell whose pieces are all core is a
+// core chip (indexToGeometry); any other cell with a piece in the polygon gets the reference's border
+// chip -- the whole geometry clipped against the cell's boundary polygon in lon / lat (llclip.h), which
+// needs no per-face pieces (the boundary carries H3's face-edge vertices).  A cell the planar clip
+// cannot take falls back to the pieces clipped in their faces' planes, dissolved along the face edge.
+void multiface_emit(mosaic_chip_set* cs, int32_t key, int res, int keep_core_geom, MultiFace& mf, const Geo3& geo,
+                    const llclip::Geom& gg) {
     for (size_t k = 0; k < mf.order.size(); k++) {
-        std::vector<const MultiPiece*> ps;
+        std::vector<MultiPiece*> ps;
         for (size_t q : mf.slot_pieces[k]) ps.push_back(&mf.pieces[q]);
         const std::vector<int64_t>& order = mf.order;
         bool all_core = true, any = false;
         for (const MultiPiece* pp : ps) {
-            const MultiPiece& p = *pp;
-            all_core = all_core && p.cls == 1;
-            any = any || p.cls == 1 || (p.cls == 2 && !p.parts.empty());
+            all_core = all_core && pp->cls == 1;
+            any = any || pp->cls == 1 || pp->cls == 2;
         }
         if (!any) continue;
         std::vector<std::vector<std::vector<P2>>> parts;
+        llclip::Cell C;
+        const bool cok = h3_cell_ll(order[k], C);
         if (all_core) {
             // a core cell over a face edge: its geometry is the one polygon of the cell boundary
             // (h3ToGeoBoundary, what the reference's indexToGeometry returns for a core chip,
-            // H3IndexSystem.scala:93-100), not the per-face pieces (parts sharing the face edge
-            // would make an invalid MultiPolygon)
+            // H3IndexSystem.scala:93-100), not the per-face pieces
             if (keep_core_geom) {
                 double b[20];
                 const int nb = h3geom::h3_to_geo_boundary((uint64_t)order[k], b);
@@ -709,16 +828,28 @@ void multiface_emit(mosaic_chip_set* cs, int32_t key, int res, int keep_core_geo
             cs->add(true, order[k], key, keep_core_geom ? to_wkb(parts) : std::vector<uint8_t>());
             continue;
         }
+        if (cok) {
+            bool is_cell = false;
+            std::vector<uint8_t> blob;
+            if (ll_chip(gg, C, &is_cell, blob) == llclip::kOk) {
+                if (!blob.empty()) cs->add(is_cell, order[k], key, is_cell && !keep_core_geom ? std::vector<uint8_t>() : blob);
+                continue;
+            }
+        }
+        g_ll_fallbacks++;
         int face_mask_n = 0;
         uint32_t face_mask = 0;
-        for (const MultiPiece* pp : ps) {
-            const MultiPiece& p = *pp;
+        for (MultiPiece* pp : ps) {
+            MultiPiece& p = *pp;
             const size_t before = parts.size();
+            FacePlane fp;
+            fp.init(p.face, res);
             if (p.cls == 1) {
-                FacePlane fp;
-                fp.init(p.face, res);
                 parts.push_back({cell_ring(p.cell, [&](P2 h) { return fp.to_geo(h); })});
             } else if (p.cls == 2) {
+                if (p.parts.empty())
+                    clip_cell(p.cell, mf.pl[(size_t)mf.face_slot(p.face)], geo, [&](P2 h) { return fp.to_geo(h); }, 1e-12,
+                              p.parts);
                 for (auto& q : p.parts) parts.push_back(q);
             }
             if (parts.size() > before && !(face_mask & (1u << p.face))) {
@@ -728,12 +859,8 @@ void multiface_emit(mosaic_chip_set* cs, int32_t key, int res, int keep_core_geo
         }
         if (parts.empty()) continue;
         if (face_mask_n > 1) {
-            // the pieces of several faces meet along the face edge: as members of one MultiPolygon
-            // they would share those segments (not a valid OGC geometry, which JTS consumers reject).
-            // Their union instead: every ring as directed edges with the interior on the left
-            // (shells counter-clockwise, holes clockwise), dissolved by the stitcher of
-            // st_intersection_aggregate (isect_geom.cpp).  The two faces compute a shared vertex in
-            // their own planes, ~1e-13 degrees apart; the snap is far below any chip feature.
+            // pieces of several faces meet along the face edge: dissolved into one geometry (every ring
+            // as directed edges, interior on the left, through st_intersection_aggregate's stitcher)
             std::vector<double> e;
             for (const auto& part : parts)
                 for (size_t r = 0; r < part.size(); r++) {
@@ -766,11 +893,12 @@ void multiface_emit(mosaic_chip_set* cs, int32_t key, int res, int keep_core_geo
 
 // Chips of geometry g (lon/lat rings geo) that spans faces, on the host: 0, or MOSAIC_E_ARG (see
 // multiface_pieces).
-int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, int keep_core_geom, const Geo3& geo) {
+int tessellate_h3_multiface(mosaic_chip_set* cs, int32_t key, int res, int D, int keep_core_geom, const Geo3& geo,
+                            const llclip::Geom& gg) {
     MultiFace mf;
     if (int rc = multiface_pieces(res, D, geo, mf)) return rc;
     multiface_classify_host(mf, geo, res);
-    multiface_emit(cs, key, res, keep_core_geom, mf);
+    multiface_emit(cs, key, res, keep_core_geom, mf, geo, gg);
     return MOSAIC_OK;
 }
 
@@ -804,7 +932,8 @@ struct ClippedChips {
         task_of.assign((size_t)n_cand, -1);
         for (size_t t = 0; t < tasks.size(); t++) task_of[(size_t)tasks[t]] = (int64_t)t;
     }
-    bool redo(int64_t k) const { return task_of[(size_t)k] < 0 || r.redo[(size_t)task_of[(size_t)k]]; }
+    bool redo(int64_t k) const { return task_of[(size_t)k] < 0 || r.status[(size_t)task_of[(size_t)k]] == 1; }
+    bool is_cell(int64_t k) const { return task_of[(size_t)k] >= 0 && r.status[(size_t)task_of[(size_t)k]] == 2; }
     // candidate k's clipped geometry as clip_cell's out_parts (kept parts with rings, closed rings)
     void parts_of(int64_t k, Geo3& out) const {
         out.clear();
@@ -869,17 +998,16 @@ struct ClippedChips {
 };
 
 // The face-spanning geometries' chips on the device (mosaic_tessellate_gpu): per-face pieces made on
-// host threads (multiface_pieces), then one session over virtual geometries -- (geometry, face): the
-// geometry's rings in that face's plane (MultiFace::pl, the host routine's doubles) and in lon / lat,
-// computed vertices mapped back through that face -- with the pieces as explicit clip polygons,
-// classified and clipped by the same kernels as the single-face cells (k_tess_classify_poly /
-// k_tess_clip: tessellate.cpp's classify_cell / clip_cell arithmetic), so multiface_emit writes the
-// host routine's chips.  Tasks the kernels hand back (scratch) are clipped on the host.
+// host threads (multiface_pieces), then classified by one session over virtual geometries --
+// (geometry, face): the geometry's rings in that face's plane (MultiFace::pl, the host routine's
+// doubles) -- with the pieces as explicit clip polygons (k_tess_classify_poly: tessellate.cpp's
+// classify_cell arithmetic); multiface_emit then clips each border cell in lon / lat (llclip.h), as
+// the host routine does.
 int multiface_gpu(mosaic_ctx* ctx, const std::vector<int64_t>& multi_geoms, const int64_t* geom_parts,
                   const int64_t* part_rings, const int64_t* ring_offsets, const double* xy, int res, int D,
-                  std::vector<MultiFace>& mfs) {
+                  std::vector<MultiFace>& mfs, std::vector<Geo3>& geos) {
     const size_t nm = multi_geoms.size();
-    std::vector<Geo3> geos(nm);
+    geos.assign(nm, Geo3());
     std::atomic<size_t> next(0);
     std::atomic<int> bad(0);
     auto work = [&]() {
@@ -957,26 +1085,12 @@ int multiface_gpu(mosaic_ctx* ctx, const std::vector<int64_t>& multi_geoms, cons
         return rc;
     std::vector<uint8_t> cls((size_t)n_pieces, 0);
     std::vector<int64_t> tasks;
-    ClippedChips cc;
-    int rc = tessclip::h3_session_chunk(S, n_pieces, pcg.data(), nullptr, 1e-3, 1e-12, cls.data(), tasks, &cc.r,
+    tessclip::ClipResult cr;
+    int rc = tessclip::h3_session_chunk(S, n_pieces, pcg.data(), nullptr, 1e-3, cls.data(), tasks, &cr, nullptr,
                                         pclip.data(), pcn.data(), nvmax);
     tessclip::h3_session_end(S);
     if (rc) return rc;
-    cc.index(n_pieces, tasks);
-    for (int64_t i = 0; i < n_pieces; i++) {
-        MultiFace& mf = mfs[pref[(size_t)i].first];
-        MultiPiece& pc = mf.pieces[pref[(size_t)i].second];
-        pc.cls = cls[(size_t)i];
-        if (pc.cls != 2) continue;
-        if (cc.redo(i)) {
-            FacePlane fp;
-            fp.init(pc.face, res);
-            clip_cell(pc.cell, mf.pl[(size_t)mf.face_slot(pc.face)], geos[pref[(size_t)i].first],
-                      [&](P2 h) { return fp.to_geo(h); }, 1e-12, pc.parts);
-        } else {
-            cc.parts_of(i, pc.parts);
-        }
-    }
+    for (int64_t i = 0; i < n_pieces; i++) mfs[pref[(size_t)i].first].pieces[pref[(size_t)i].second].cls = cls[(size_t)i];
     return MOSAIC_OK;
 }
 
@@ -1024,7 +1138,8 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                         multi = multi || f != face;
                     }
             if (multi) {  // cells on several faces: per-face pieces (tessellate_h3_multiface)
-                if (tessellate_h3_multiface(cs, (int32_t)g, res, D, keep_core_geom, geo)) {
+                const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+                if (tessellate_h3_multiface(cs, (int32_t)g, res, D, keep_core_geom, geo, gg)) {
                     delete cs;
                     return mosaic_tess_fail(MOSAIC_E_ARG, "geometry too large for a gnomonic face plane "
                                                           "(a vertex more than 78 degrees from a face centre it meets)");
@@ -1066,8 +1181,10 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                     // densified clip polygon: SH on the densified (still convex) hexagon keeps the
                     // cell boundary within ~1/D^2 of the great-circle arcs once mapped back
                     cell.clip = cell.outline;
-                    emit_cell(cs, (int32_t)g, cell, pl, geo, 1e-3, keep_core_geom,
-                              [&](P2 h) { return fp.to_geo(h); }, 1e-12);
+                    const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+                    emit_cell_ll(cs, (int32_t)g, cell, pl, geo, gg, 1e-3, keep_core_geom,
+                                 [&](P2 h) { return fp.to_geo(h); }, 1e-12,
+                                 [&](llclip::Cell& C) { return h3_cell_ll(cell.id, C); }, D == 1);
                 }
             }
         } else {
@@ -1094,8 +1211,9 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                     int64_t id;
                     if (!bng::point_to_index(cx0 + 0.5 * e, cy0 + 0.5 * e, res, &id)) continue;
                     cell.id = id;
-                    emit_cell(cs, (int32_t)g, cell, geo, geo, 1e-9 * e, keep_core_geom, [](P2 h) { return h; },
-                              1e-12 * e * e);
+                    const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+                    emit_cell_ll(cs, (int32_t)g, cell, geo, geo, gg, 1e-9 * e, keep_core_geom, [](P2 h) { return h; },
+                                 1e-12 * e * e, [&](llclip::Cell& C) { return bng_cell_ll(cx0, cy0, e, C); }, true);
                 }
         }
     }
@@ -1250,8 +1368,9 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     // (geometry, face), the pieces as explicit clip polygons -- and emitted in geometry order
     // (multiface_emit), so the chips are the host producer's
     std::vector<MultiFace> mfs(multi_geoms.size());
+    std::vector<Geo3> mgeos;
     if (!multi_geoms.empty()) {
-        if (int rc = multiface_gpu(ctx, multi_geoms, geom_parts, part_rings, ring_offsets, xy, res, D, mfs)) {
+        if (int rc = multiface_gpu(ctx, multi_geoms, geom_parts, part_rings, ring_offsets, xy, res, D, mfs, mgeos)) {
             delete cs;
             return rc;
         }
@@ -1259,7 +1378,11 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
     trace.mark("face-spanning pieces (GPU)");
     auto flush_multi = [&](int64_t upto) -> int {
         for (; next_multi < multi_geoms.size() && multi_geoms[next_multi] < upto; next_multi++)
-            multiface_emit(cs, (int32_t)multi_geoms[next_multi], res, keep_core_geom, mfs[next_multi]);
+        {
+            const int64_t g = multi_geoms[next_multi];
+            const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+            multiface_emit(cs, (int32_t)g, res, keep_core_geom, mfs[next_multi], mgeos[next_multi], gg);
+        }
         return MOSAIC_OK;
     };
     // one device session for the batch: geometry uploaded once, per chunk only the candidate centres;
@@ -1283,8 +1406,8 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         cls.assign((size_t)nc, 0);
         trace.add(0);
         ClippedChips cc;
-        int rc = tessclip::h3_session_chunk(S, nc, cg.data() + k0, cxy.data() + 2 * (size_t)k0, 1e-3, 1e-12, cls.data(),
-                                            tasks, &cc.r);
+        int rc = tessclip::h3_session_chunk(S, nc, cg.data() + k0, cxy.data() + 2 * (size_t)k0, 1e-3, cls.data(), tasks,
+                                            &cc.r, cid.data() + k0);
         trace.add(1);
         clip_kernel_ms += cc.r.kernel_ms;
         if (rc) {
@@ -1325,7 +1448,12 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
                     if (!cls[kk]) continue;
                     o.off = (int64_t)w.b.size();
                     if (cls[kk] == 2 && !cc.redo(kk)) {
-                        if (direct) {
+                        // (a chip equal to its cell is a core chip, geometry kept only with keep_core_geom)
+                        o.core = cc.is_cell(kk);
+                        if (o.core && !keep_core_geom) {
+                            WkbSize z;
+                            if (cc.chip(kk, z)) o.len = 0;
+                        } else if (direct) {
                             WkbSize z;
                             if (cc.chip(kk, z)) o.len = (int32_t)z.n;
                         } else {
@@ -1365,8 +1493,9 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
                     tmp.key.clear();
                     tmp.wkb_offsets.assign(1, 0);
                     tmp.wkb.clear();
-                    emit_cell(&tmp, (int32_t)cur, cell, pl, geo, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); },
-                              1e-12, (int)cls[kk]);
+                    const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[cur], geom_parts[cur + 1]};
+                    emit_cell_ll(&tmp, (int32_t)cur, cell, pl, geo, gg, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); },
+                                 1e-12, [&](llclip::Cell& C) { return h3_cell_ll(cell.id, C); }, D == 1, (int)cls[kk]);
                     if (!tmp.index_id.empty()) {
                         o.core = tmp.is_core[0] != 0;
                         w.b.insert(w.b.end(), tmp.wkb.begin(), tmp.wkb.end());
@@ -1524,31 +1653,33 @@ int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, c
     int rc = mosaic_tess_classify_bng(ctx, n_geoms, geom_parts, part_rings, ring_offsets, xy, n_cand, cg.data(),
                                       cij.data(), e, 1e-9 * e, cls.data());
     if (rc) return rc;
-    // border cells clipped on the GPU (k_tess_clip, identity mapping) against the squares emit_cell uses
+    // border cells clipped on the GPU (k_tess_clip_ll) against their squares, as emit_cell_ll does
     std::vector<int64_t> tasks;
     for (int64_t k = 0; k < n_cand; k++)
         if (cls[k] == 2) tasks.push_back(k);
     std::vector<double> sq((size_t)n_cand * 8);
     for (int64_t k = 0; k < n_cand; k++) {
-        const double cx0 = cij[2 * k] * e, cy0 = cij[2 * k + 1] * e;
-        const double v[8] = {cx0, cy0, cx0 + e, cy0, cx0 + e, cy0 + e, cx0, cy0 + e};
-        memcpy(sq.data() + 8 * k, v, sizeof v);
+        llclip::Cell C;
+        bng_cell_ll(cij[2 * k] * e, cij[2 * k + 1] * e, e, C);
+        for (int v = 0; v < 4; v++) {
+            sq[8 * (size_t)k + 2 * v] = C.v[v].x;
+            sq[8 * (size_t)k + 2 * v + 1] = C.v[v].y;
+        }
     }
     ClippedChips cc;
-    if ((rc = tessclip::clip_border(ctx, n_geoms, geom_parts, part_rings, ring_offsets, xy, xy, nullptr, 0, 1,
-                                    (int64_t)tasks.size(), tasks.data(), cg.data(), n_cand, sq.data(), 4, 1e-12 * e * e,
-                                    &cc.r)))
+    if ((rc = tessclip::clip_ll(ctx, n_geoms, geom_parts, part_rings, ring_offsets, xy, tasks, cg.data(), n_cand, sq.data(), 4,
+                                &cc.r)))
         return rc;
     cc.index(n_cand, tasks);
     mosaic_chip_set* cs = new mosaic_chip_set();
     std::vector<std::vector<std::vector<P2>>> geo;
-    std::vector<uint8_t> blob;
     int64_t cur = -1;
     for (int64_t k = 0; k < n_cand; k++) {
         if (!cls[k]) continue;
         if (cls[k] == 2 && !cc.redo(k)) {
             WkbOut w;
-            if (cc.chip(k, w)) cs->add(false, cid[k], cg[k], w.b);
+            const bool core = cc.is_cell(k);
+            if (cc.chip(k, w)) cs->add(core, cid[k], cg[k], core && !keep_core_geom ? std::vector<uint8_t>() : w.b);
             continue;
         }
         if (cg[k] != cur) {
@@ -1569,10 +1700,19 @@ int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, c
         cell.clip = {{cx0, cy0}, {cx0 + e, cy0}, {cx0 + e, cy0 + e}, {cx0, cy0 + e}};
         cell.outline = cell.clip;
         cell.id = cid[k];
-        emit_cell(cs, (int32_t)cur, cell, geo, geo, 1e-9 * e, keep_core_geom, [](P2 h) { return h; }, 1e-12 * e * e,
-                  (int)cls[k]);
+        const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[cur], geom_parts[cur + 1]};
+        emit_cell_ll(cs, (int32_t)cur, cell, geo, geo, gg, 1e-9 * e, keep_core_geom, [](P2 h) { return h; }, 1e-12 * e * e,
+                     [&](llclip::Cell& C) { return bng_cell_ll(cx0, cy0, e, C); }, true, (int)cls[k]);
     }
     *out = cs;
+    return MOSAIC_OK;
+}
+
+// chips clipped by the reference-style clip on the host, and cells that fell back to the plane clip
+// (process-wide counters; tests assert no fallback on their inputs)
+int mosaic_tess_counters(int64_t* ll_chips, int64_t* ll_fallbacks) {
+    if (ll_chips) *ll_chips = g_ll_chips.load();
+    if (ll_fallbacks) *ll_fallbacks = g_ll_fallbacks.load();
     return MOSAIC_OK;
 }
 

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
     assert set(names) == set(N.EXPORTS)
-    assert lib.mosaic_abi_version() == 3
+    assert lib.mosaic_abi_version() == 4
 
 
 def test_no_gpu_init_fails_cleanly():

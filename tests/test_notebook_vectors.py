@@ -32,13 +32,19 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 NB = json.load(open(os.path.join(_HERE, "golden", "notebook_vectors.json")))
 POINT_SETS = ["grid_indexes_points_res9", "quickstart_points_res10"]
 POLYFILLS = ["homecrest_polyfill_res9", "freshkills_polyfill_res10"]
-# JTS overlay (planar lon/lat: zone edge x the cell's straight-chord hexagon) vs this engine's
-# clipping in the face plane: the vertices where a zone edge crosses a cell edge
-# differ by the sagitta of the zone edge's gnomonic image (up to ~1e-7 degrees for kilometre-long
-# zone edges); original zone vertices are kept bit for bit.  Measured max 1.0e-7 degrees (~1 cm).
-CHIP_VERTEX_TOL = 2e-7
-
-
+# Border chips are the reference's planar clip (llclip.h): JTS's crossing arithmetic on the zone edge
+# and the cell's h3ToGeoBoundary chord, original vertices copied.  Against the rendered chips the
+# vertex sequences agree to CHIP_VERTEX_ULPS -- the cells' own boundary vertices differ from the
+# reference's libh3 by 1-2 ulp on about half the cells (BOUNDARY_EXACT_RINGS below), and the crossings
+# computed from them inherit that -- with one exception: one crossing of Freshkills Park's cell
+# 0x8a2a10605197fff is 23 ulp (1.6e-13 degrees) away.  Its hexagon vertices in the rendered ring are
+# bit-exact, the crossing is well conditioned (77 degrees between the segments), and none of five
+# intersection formulas (JTS 1.19 conditioned homogeneous, CGAlgorithmsDD double-double, HCoordinate
+# with normalisation, exact rational, Sutherland-Hodgman's parametric form) nor +-3 ulp on either
+# hexagon vertex reproduces it: an input outside the chip (the notebook downloaded the zones afresh)
+# differs, not the arithmetic (scratch probe recorded in DESIGN.md section 6).
+CHIP_VERTEX_ULPS = 3
+CHIP_VERTEX_EXCEPTIONS = {("Freshkills Park", 0x8A2A10605197FFF): 23}
 @pytest.fixture(scope="module")
 def zones():
     return PolygonSet.load("nyc_taxi_zones")
@@ -210,43 +216,59 @@ def _wkb_prefix_vertices(b):
         return np.array(out), False
 
 
+def _seq(parts):
+    """all vertices of a Polygon / MultiPolygon in WKB order (closing vertices included)"""
+    return [tuple(map(float, v)) for p in parts for r in p for v in np.asarray(r)]
+
+
+def _ulps(a, b):
+    return max((abs(u - v) / math.ulp(u) for p, q in zip(a, b) for u, v in zip(p, q)), default=0.0)
+
+
 def test_host_tessellation_quickstart_border_geometry(zones):
-    """Border chips of quickstart cell 32 (JTS overlay, little-endian WKB) against the engine's:
-    every reference vertex within CHIP_VERTEX_TOL of an engine vertex (for the 133 WKB values the
-    display cut, the shown prefix), and for the 118 complete ones the same area up to that gap along
-    the perimeter."""
+    """Border chips of quickstart cell 32 (the reference's rendered WKB, little-endian) against the
+    engine's: the same vertex sequence -- counter-clockwise from the lowest vertex, crossings where
+    the zone edge meets the cell's chord -- within CHIP_VERTEX_ULPS (the shown prefix for the 133
+    values the display cut), the same rings for the 118 complete ones."""
     names = list(zones.names)
-    worst, worst_area, full, cut = 0.0, 0.0, 0, 0
+    worst, full, cut = 0.0, 0, 0
     for zone, rows in _ref_chips().items():
         chips = _chip_map(tessellate("H3", zones.subset([names.index(zone)]), 10))
         for cid, core, w in rows:
             if w is None:
                 continue
             rv, complete = _wkb_prefix_vertices(w)
+            rv = [tuple(map(float, v)) for v in rv]
             _, oparts = W.read_wkb(chips[cid][1])
-            ov = _vertices(oparts)
-            d = np.hypot(rv[:, None, 0] - ov[None, :, 0], rv[:, None, 1] - ov[None, :, 1])
-            worst = max(worst, d.min(1).max())
+            ev = _seq(oparts)
             if complete:
-                a_ref, a_eng = _parts_area(W.read_wkb(w)[1]), _parts_area(oparts)
-                # the area between the two boundaries: at most the vertex gap along the perimeter
-                worst_area = max(worst_area, abs(a_ref - a_eng) / (CHIP_VERTEX_TOL * _parts_perimeter(oparts)))
+                _, rparts = W.read_wkb(w)
+                assert [len(r) for p in rparts for r in p] == [len(r) for p in oparts for r in p], hex(cid)
                 full += 1
             else:
+                assert len(ev) >= len(rv)
                 cut += 1
+            u = _ulps(rv, ev[:len(rv)])
+            allowed = CHIP_VERTEX_EXCEPTIONS.get((zone, cid), CHIP_VERTEX_ULPS)
+            assert u <= allowed, (zone, hex(cid), u)
+            if (zone, cid) not in CHIP_VERTEX_EXCEPTIONS:
+                worst = max(worst, u)
     assert (full, cut) == (118, 133), (full, cut)
-    assert worst < CHIP_VERTEX_TOL and worst_area < 1.0, (worst, worst_area)
+    assert worst <= CHIP_VERTEX_ULPS
 
 
 def test_host_tessellation_kepler_newark(zones):
     """kepler.ipynb: the first zone (Newark Airport; the notebook's GeoJSON equals the fixture's
     coordinates) tessellated at res 9: the same 92 chip ids; core chips are exactly the chips whose
-    reference geometry is the whole cell; border chips match within CHIP_VERTEX_TOL."""
+    reference geometry is the whole cell, with that ring up to its start vertex (the rendered WKT
+    starts each at h3ToGeoBoundary's last vertex -- the geometry API that rendered the notebook
+    reverses rings twice -- the engine writes indexToGeometry's order); border chips equal the
+    rendered ones vertex for vertex within CHIP_VERTEX_ULPS."""
     k = NB["kepler_tessellation_res9"]
     assert np.array_equal(np.array(k["geometry"]["coordinates"][0][0]), np.array(zones.parts(0)[0][0]))
     chips = _chip_map(tessellate("H3", zones.subset([0]), 9))
     assert set(chips) == {c for c, _ in k["rows"]}
-    worst = 0.0
+    n_border = 0
     for cid, wkt in k["rows"]:
         _, rparts = W.read_wkt(wkt)
         want = [(_deg(g), _deg(a)) for a, g in oracle.h3_to_geo_boundary(cid)]
@@ -255,8 +277,13 @@ def test_host_tessellation_kepler_newark(zones):
         core, blob = chips[cid]
         assert core == ref_core, hex(cid)
         _, oparts = W.read_wkb(blob)
-        worst = max(worst, _vertex_gap(_vertices(rparts), _vertices(oparts)))
-    assert worst < CHIP_VERTEX_TOL
+        if core:
+            assert _ring_ulps(oparts[0][0], [tuple(v) for v in np.asarray(rparts[0][0])[:-1]]) <= BOUNDARY_MAX_ULPS
+        else:
+            n_border += 1
+            rs, es = _seq(rparts), _seq(oparts)
+            assert len(rs) == len(es) and _ulps(rs, es) <= CHIP_VERTEX_ULPS, hex(cid)
+    assert n_border == 45
 
 
 def test_join_rows_are_border_candidates(zones):

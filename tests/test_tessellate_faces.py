@@ -211,8 +211,11 @@ def test_face_spanning_core_chip_is_cell_boundary():
         ring = parts[0][0]
         b = oracle.h3_to_geo_boundary(int(chips["index_id"][k]))
         want = [(lng * 180.0 / math.pi, lat * 180.0 / math.pi) for lat, lng in b]
-        want.append(want[0])
-        assert ring == want
+        # a border candidate whose clip is the whole cell is a core chip too (IndexSystem.scala:160:
+        # isCore = intersect.equals(indexGeom)); its geometry is the clip, written from its lowest vertex
+        lo = min(range(len(want)), key=lambda i: (want[i][1], want[i][0]))
+        rot = want[lo:] + want[:lo]
+        assert ring in (want + [want[0]], rot + [rot[0]])
         n += 1
     assert n > 20
 
