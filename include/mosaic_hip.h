@@ -428,10 +428,9 @@ int mosaic_isect_geoms_destroy(mosaic_isect_geoms* g);
  * (reference H3IndexSystem.kRing / kLoop, core/index/H3IndexSystem.scala:154-177); where the walk
  * meets a pentagon, kRing is H3's _kRingInternal hash table read in slot order (as h3-java returns
  * it) and kLoop the reference's own fallback, kRing(k).toSet diff kRing(k - 1).toSet in Scala
- * HashSet order (:169-176).  That search makes ~5 k^3 dependent steps per row: such rows with
- * k > 128 are not evaluated and get out_count[i] = -4 (evaluate them on the row path); the other rows
- * of the call are answered.  A row whose id is not a valid cell gets out_count[i] = -2 (no cells
- * written). */
+ * HashSet order (:169-176).  That search makes ~5 k^3 dependent steps per row: it runs on the GPU for
+ * k <= 128 and on host threads beyond (the same code), so every row is answered.  A row whose id is
+ * not a valid cell gets out_count[i] = -2 (no cells written). */
 int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uint8_t* valid, int64_t n, int k,
                       int loop, int64_t* out, int32_t* out_count);
 

@@ -706,11 +706,6 @@ class MosaicContext:
             raise N.MosaicError(
                 N.MOSAIC_E_ARG, f"grid_cellkring / grid_cellkloop: row {int(bad[0])} (cell {int(ids[bad[0]])}) is not a valid "
                 "H3 cell id")
-        unsup = np.nonzero(cnt[:n] == -4)[0]
-        if len(unsup):
-            raise N.MosaicError(
-                N.MOSAIC_E_ARG, f"grid_cellkring / grid_cellkloop: row {int(unsup[0])} (cell {int(ids[unsup[0]])}) meets a "
-                f"pentagon with k = {k} > 128: evaluate it on the row path")
         rows = [out[i * stride:i * stride + cnt[i]] for i in range(n)]
         if raw or self.index_system.cell_id_type != "string":
             return rows

@@ -356,42 +356,80 @@ MOSAIC_HD int face_search(double px, double py, double pz, double* best_out, dou
 }
 
 // round(n / 7) for |n| < 2^27: floor((n + 3) / 7), via an unsigned division of a shifted numerator
-MOSAIC_HD int div7r(int n) {
+MOSAIC_HD constexpr int div7r(int n) {
     const unsigned off = 7u << 25;
-    return (int)((unsigned)(n + 3) + off) / 7 - (1 << 25);
+    return (int)(((unsigned)(n + 3) + off) / 7u) - (1 << 25);
+}
+// floor(n / 7) for |n| < 2^27
+MOSAIC_HD constexpr int div7f(int n) {
+    const unsigned off = 7u << 25;
+    return (int)(((unsigned)n + off) / 7u) - (1 << 25);
 }
 
 // digit <- axial (i - k, j - k) offset of a child from its parent's centre; 7 = invalid.
 // The 3x3 table {1, 3, 7, 5, 0, 2, 7, 4, 6} packed 3 bits per entry.
-MOSAIC_HD int axial_digit(int da, int db) {
+MOSAIC_HD constexpr int axial_digit(int da, int db) {
     const unsigned kPacked = 0x69d0bd9u;
     unsigned ia = (unsigned)(da + 1), ib = (unsigned)(db + 1);
     return (ia < 3 && ib < 3) ? (int)((kPacked >> (3u * (ia * 3u + ib))) & 7u) : 7;
 }
 
+// One level of _faceIjkToH3 in axial coordinates: the parent (a, b) <- child (a, b) at level r, and
+// the child's digit.  Class III (r odd): _upAp7, centre _downAp7 = axial (2I + J, 3J - I); Class II:
+// _upAp7r, centre _downAp7r = axial (3I - J, I + 2J).
+MOSAIC_HD constexpr int axial_up(int& a, int& b, bool class3) {
+    int I = 0, J = 0, da = 0, db = 0;
+    if (class3) {
+        I = div7r(3 * a - b);
+        J = div7r(a + 2 * b);
+        da = a - (2 * I + J);
+        db = b - (3 * J - I);
+    } else {
+        I = div7r(2 * a + b);
+        J = div7r(3 * b - a);
+        da = a - (3 * I - J);
+        db = b - (I + 2 * J);
+    }
+    a = I;
+    b = J;
+    return axial_digit(da, db);
+}
+
+// Two levels at once.  The two steps' centre maps compose to 7 x identity -- (2I + J, 3J - I) of
+// (3I - J, I + 2J) is (7I, 7J), in either order -- and each step's rounding commutes with
+// translations by its parent lattice, so with (a, b) = 7 (qa, qb) + (ra, rb), 0 <= ra, rb < 7, the two
+// digits depend on (ra, rb) alone and the grandparent is (qa, qb) + a small offset from (ra, rb).
+// Table [first level is Class III][7 ra + rb]: bits 0-2 the first (finer) level's digit, 3-5 the
+// second's, 6-8 / 9-11 the grandparent offset + 2.  Built at compile time from axial_up itself.
+struct AxialPairTab {
+    uint16_t v[2][49];
+};
+MOSAIC_HD constexpr AxialPairTab make_axial_pair_tab() {
+    AxialPairTab t{};
+    for (int c3 = 0; c3 < 2; c3++)
+        for (int ra = 0; ra < 7; ra++)
+            for (int rb = 0; rb < 7; rb++) {
+                int a = ra, b = rb;
+                const int d1 = axial_up(a, b, c3 != 0);
+                const int d2 = axial_up(a, b, c3 == 0);
+                t.v[c3][7 * ra + rb] = (uint16_t)(d1 | d2 << 3 | (a + 2) << 6 | (b + 2) << 9);
+            }
+    return t;
+}
+#if defined(__HIPCC__)
+static __constant__ const AxialPairTab kAxialPairs = make_axial_pair_tab();
+#else
+static const AxialPairTab kAxialPairs = make_axial_pair_tab();
+#endif
+
 // _faceIjkToH3 in axial coordinates (a, b) = (i - k, j - k) of the res-`res` cell on `face`.
 // Same arithmetic as face_ijk_to_h3 (the axial pair is invariant under _ijkNormalize, and
-// _downAp7 / _downAp7r are linear), with the three normalisations per level removed.
-MOSAIC_HD uint64_t face_axial_to_h3(int face, int a, int b, int res) {
-    uint64_t h = 0x00001fffffffffffULL | (1ULL << 59) | ((uint64_t)res << 52);
-    for (int r = res; r >= 1; r--) {
-        int I, J, da, db;
-        if (r & 1) {  // Class III child: _upAp7, centre _downAp7 = axial (2I + J, 3J - I)
-            I = div7r(3 * a - b);
-            J = div7r(a + 2 * b);
-            da = a - (2 * I + J);
-            db = b - (3 * J - I);
-        } else {  // Class II child: _upAp7r, centre _downAp7r = axial (3I - J, I + 2J)
-            I = div7r(2 * a + b);
-            J = div7r(3 * b - a);
-            da = a - (3 * I - J);
-            db = b - (I + 2 * J);
-        }
-        int s = (15 - r) * 3;
-        h = (h & ~((uint64_t)7 << s)) | ((uint64_t)axial_digit(da, db) << s);
-        a = I;
-        b = J;
-    }
+// _downAp7 / _downAp7r are linear), with the three normalisations per level removed and the levels
+// taken two at a time (kAxialPairs: two floor divisions by 7 and one table read per pair instead of
+// four rounding divisions and two digit decodings); face_axial_to_h3_levels is the one-level form,
+// kept for the self-check (tests/native/h3_pairs_check.cpp: identical on every input).
+MOSAIC_HD uint64_t axial_base_to_h3(int face, int a, int b, int res, uint64_t digits) {
+    uint64_t h = digits | (1ULL << 59) | ((uint64_t)res << 52);
     IJK ijk = {a, b, 0};
     ijk_normalize(ijk);
     if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
@@ -409,6 +447,31 @@ MOSAIC_HD uint64_t face_axial_to_h3(int face, int a, int b, int res) {
         for (int i = 0; i < rots; i++) h = rotate_all_digits(h, true);
     }
     return h;
+}
+MOSAIC_HD uint64_t face_axial_to_h3_levels(int face, int a, int b, int res) {
+    uint64_t h = 0x00001fffffffffffULL;
+    for (int r = res; r >= 1; r--) {
+        const int s = (15 - r) * 3;
+        h = (h & ~((uint64_t)7 << s)) | ((uint64_t)axial_up(a, b, (r & 1) != 0) << s);
+    }
+    return axial_base_to_h3(face, a, b, res, h);
+}
+MOSAIC_HD uint64_t face_axial_to_h3(int face, int a, int b, int res) {
+    // digits of levels res .. 1 gathered with level res lowest, placed above the unused 7s at the end
+    uint64_t d = 0;
+    int sh = 0, r = res;
+    const int c3 = res & 1;  // every pair starts on a level of res's parity
+    for (; r >= 2; r -= 2, sh += 6) {
+        const int qa = div7f(a), qb = div7f(b);
+        const unsigned e = kAxialPairs.v[c3][7 * (a - 7 * qa) + (b - 7 * qb)];
+        d |= (uint64_t)(e & 63u) << sh;
+        a = qa + (int)((e >> 6) & 7u) - 2;
+        b = qb + (int)((e >> 9) & 7u) - 2;
+    }
+    if (r == 1) d |= (uint64_t)axial_up(a, b, true) << sh;
+    const int low = 3 * (15 - res);
+    const uint64_t digits = (d << low) | ((1ULL << low) - 1ULL);
+    return axial_base_to_h3(face, a, b, res, digits);
 }
 
 // The unit vector of (lat_deg, lon_deg) for the fast path: radians by one multiply (within 2 ulp of

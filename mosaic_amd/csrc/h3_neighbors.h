@@ -278,8 +278,8 @@ MOSAIC_HD int kring_fast(uint64_t origin, int k, int loop, int64_t* out) {
     return hex_range(origin, k, out) ? max_kring_size(k) : -3;
 }
 
-// The engine runs the fallback for k <= kSlowMaxK (H3's search makes ~5 k^3 dependent visits: ~5e6
-// at k = 100, 1e7 at 128); rows beyond it are returned unsupported (-4), not evaluated.
+// The device runs the fallback for k <= kSlowMaxK (H3's search makes ~5 k^3 dependent visits: ~5e6
+// at k = 100, 1e7 at 128); rows beyond it run this same code on host threads (mosaic_cell_kring).
 static const int kSlowMaxK = 128;
 
 // The fallback rows (kring_fast == -3): kRing = _kRingInternal's table read in slot order (h3-java

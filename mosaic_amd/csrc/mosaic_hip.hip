@@ -1103,6 +1103,8 @@ __device__ int cell_ring(int grid, int64_t id, int jdk, double* xy) {  // indexT
 
 // one unit per wave (lane 0): a unit's overlay is sequential, data-dependent work, so units that
 // shared a wave would serialise behind its largest; largest units first, for the tail
+// the largest unit (edges of its chip parts) one lane overlays: 4096^2 noding steps, ~0.1 s
+static constexpr uint32_t kMaxUnitEdges = 4096;
 __global__ void __launch_bounds__(64) k_isect_overlay(OverlayArgs x) {
     const IsectArgs& a = x.base;
     if ((threadIdx.x & 63) != 0) return;
@@ -1124,6 +1126,13 @@ __global__ void __launch_bounds__(64) k_isect_overlay(OverlayArgs x) {
             }
             x.out_count[u] = n > 0 && n <= out_cap ? n : -1;
             x.out_area[u] = 0.5 * acc;
+            continue;
+        }
+        if (un.n_edges > kMaxUnitEdges) {
+            // one lane's noding is O(E^2) dependent steps: a unit beyond the limit is not answered
+            // (count -1: its group gets status 1, area NaN) instead of holding the lane for seconds
+            x.out_count[u] = -1;
+            x.out_area[u] = NAN;
             continue;
         }
         const unsigned long long key = a.gkey[un.gs];
@@ -4789,10 +4798,10 @@ static int run_unit_overlay(ThreadCtx* c, const IsectArgs& a, int grid_sys, uint
     std::vector<int64_t> sbytes(nu);
     for (size_t u = 0; u < nu; u++) {
         const IsectUnit& x = r.units[u];
-        const bool cc = x.flags & 1u;
-        r.edge_off[u + 1] = r.edge_off[u] + (cc ? 16 : 5 * (int64_t)x.n_edges + 64);
-        sbytes[u] = cc ? 0 : ((((int64_t)x.n_parts * (int64_t)sizeof(overlay::PartRef) + 63) & ~(int64_t)63) +
-                              ((overlay::scratch_bytes(x.n_edges) + 63) & ~(int64_t)63));
+        const bool cc = x.flags & 1u, skip = !cc && x.n_edges > kMaxUnitEdges;  // (skip: not answered)
+        r.edge_off[u + 1] = r.edge_off[u] + (cc || skip ? 16 : 5 * (int64_t)x.n_edges + 64);
+        sbytes[u] = cc || skip ? 0 : ((((int64_t)x.n_parts * (int64_t)sizeof(overlay::PartRef) + 63) & ~(int64_t)63) +
+                                      ((overlay::scratch_bytes(x.n_edges) + 63) & ~(int64_t)63));
     }
     r.edges.assign((size_t)r.edge_off[nu] * 4, 0.0);
     const int64_t kBatch = (int64_t)2 << 30;
@@ -4848,17 +4857,28 @@ static int run_unit_overlay(ThreadCtx* c, const IsectArgs& a, int grid_sys, uint
     return MOSAIC_OK;
 }
 
-// the node tolerance of the host stitching: pieces of adjacent cells meet within it.  H3 chips
-// follow the cells' gnomonic sides, so the same side crossing computed in two cells differs by up to
-// ~5e-3 e^2 degrees (e the cell edge in degrees; measured 1.1e-7 at res 8, 1e-8 at res 9:
-// tools/probes/isect_snap.py); the tolerance is 10x that, and at least 2^-40 of the coordinates.
+// Node tolerance of the stitch: chips are the reference's planar clips (llclip.h), so the same cell
+// side crossing computed in two adjacent cells is the same double (the cells share their
+// h3ToGeoBoundary vertices bit for bit and JTS's crossing arithmetic is symmetric in its segments);
+// what is left are the overlay's own node positions (tol 2^-40 of the coordinates, overlay.h).  A
+// fixed tolerance of that scale -- 180 x 2^-40 degrees (1.6e-10, ~16 um), 1e6 x 2^-40 metres for BNG
+// -- never merges distinct chip vertices at any resolution (until round 5 it was 0.05 e^2 for the
+// gnomonic-plane chips, kilometres at res 3).
 static double stitch_snap(int grid, int res) {
-    if (grid == MOSAIC_GRID_BNG) return 1e6 * 9.094947017729282e-13;
+    (void)res;
+    return (grid == MOSAIC_GRID_BNG ? 1e6 : 180.0) * 9.094947017729282e-13;
+}
+// cell edge in output units (stitch check scale): H3 edge length in degrees, BNG the square's edge
+static double agg_cell_edge(int grid, int res) {
+    if (grid == MOSAIC_GRID_BNG) {
+        static const double e_by_res[] = {0, 100000, 10000, 1000, 100, 10, 1};
+        const int ar = res < 0 ? -res : res;
+        return res == -1 ? 500000 : (res > 0 ? e_by_res[ar > 6 ? 6 : ar] : e_by_res[ar > 6 ? 6 : ar - 1] / 2.0);
+    }
     static const double kEdgeKm[16] = {1107.712591, 418.6760055, 158.2446558, 59.81085794, 22.6063794, 8.544408276,
                                        3.229482772, 1.220629759, 0.461354684, 0.174375668, 0.065907807, 0.024910561,
                                        0.009415526, 0.003559893, 0.001348575, 0.000509713};
-    const double e = kEdgeKm[res < 0 ? 0 : (res > 15 ? 15 : res)] / 111.32;
-    return std::max(0.05 * e * e, 180.0 * 9.094947017729282e-13);
+    return kEdgeKm[res < 0 ? 0 : (res > 15 ? 15 : res)] / 111.32;
 }
 
 struct mosaic_isect_geoms {
@@ -4963,7 +4983,7 @@ int mosaic_intersection_aggregate_geometry(mosaic_ctx* ctx, const mosaic_chips* 
     // each group's cell boundaries stitched into its polygons, on host threads
     std::vector<std::vector<uint8_t>> wkbs(ng);
     std::vector<uint8_t> gst(ng, 0);
-    const double snap = stitch_snap(left->grid, left->res);
+    const double snap = stitch_snap(left->grid, left->res), edge = agg_cell_edge(left->grid, left->res);
     std::atomic<size_t> next{0};
     auto work = [&]() {
         std::vector<double> e;
@@ -4976,7 +4996,11 @@ int mosaic_intersection_aggregate_geometry(mosaic_ctx* ctx, const mosaic_chips* 
             for (size_t u = g.gstart[k]; u < g.gstart[k + 1]; u++)
                 e.insert(e.end(), r.edges.begin() + 4 * r.edge_off[u], r.edges.begin() + 4 * (r.edge_off[u] + r.count[u]));
             double stitched = 0;
-            if (!isect_geom::stitch_wkb(e.data(), e.size() / 4, snap, wkbs[k], &stitched)) {
+            // the dissolved polygons must keep the units' area: a stitch that merged or lost pieces
+            // is flagged (status 1), not returned distorted
+            const double bound = 1e-9 * std::max(fabs(garea[k]), edge * edge);
+            if (!isect_geom::stitch_wkb(e.data(), e.size() / 4, snap, wkbs[k], &stitched) ||
+                !(fabs(stitched - garea[k]) <= bound)) {
                 gst[k] = 1;
                 wkbs[k].clear();
             }
@@ -5108,9 +5132,42 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
         for (int64_t i = 0; i < n; i++)
             if (cnt[(size_t)i] == -3) rows.push_back(i);
         if (!rows.empty() && k > h3nb::kSlowMaxK) {
-            // beyond kSlowMaxK H3's search (~5 k^3 visits) is not run: those rows only are marked
-            // unsupported (count -4) for the caller's row path; the rest of the batch is answered
-            for (int64_t i : rows) cnt[(size_t)i] = -4;
+            // beyond kSlowMaxK H3's search (~5 k^3 dependent visits per row: seconds for one lane at
+            // k ~ 200, the device form would hold a wave that long) runs on host threads -- the same
+            // h3nb::kring_slow (h3_neighbors.h, host build of the device code), so the rows equal
+            // h3-java's _kRingInternal tables as the device rows do
+            const int64_t m = h3nb::max_kring_size(k), m1 = h3nb::max_kring_size(k - 1);
+            std::vector<int64_t> origin(rows.size());
+            if (is_device_ptr(cells)) {
+                std::vector<int64_t> all((size_t)n);
+                HIP_TRY(hipMemcpy(all.data(), cells, (size_t)n * 8, hipMemcpyDeviceToHost));
+                for (size_t j = 0; j < rows.size(); j++) origin[j] = all[(size_t)rows[j]];
+            } else {
+                for (size_t j = 0; j < rows.size(); j++) origin[j] = cells[(size_t)rows[j]];
+            }
+            std::vector<int64_t> res((size_t)rows.size() * (size_t)stride, 0);
+            std::atomic<size_t> next{0};
+            auto work = [&]() {
+                std::vector<int64_t> tab((size_t)(m + m1));
+                std::vector<int32_t> dist((size_t)m);
+                std::vector<uint64_t> stack((size_t)k + 1);
+                for (size_t j; (j = next.fetch_add(1)) < rows.size();)
+                    cnt[(size_t)rows[j]] = h3nb::kring_slow((uint64_t)origin[j], k, loop, res.data() + j * (size_t)stride,
+                                                             tab.data(), dist.data(), stack.data());
+            };
+            {
+                // (tables of ~3 k^2 cells per thread: at most 16 threads, fewer for huge k)
+                const size_t per = (size_t)(m + m1) * 8 + (size_t)m * 4;
+                const unsigned cap = (unsigned)std::max<size_t>(1, ((size_t)4 << 30) / std::max<size_t>(per, 1));
+                const unsigned nt = std::max(1u, std::min({16u, std::thread::hardware_concurrency(), cap, (unsigned)rows.size()}));
+                std::vector<std::thread> th;
+                for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+                work();
+                for (auto& t : th) t.join();
+            }
+            for (size_t j = 0; j < rows.size(); j++)
+                HIP_TRY(hipMemcpyAsync(a.out + rows[j] * stride, res.data() + j * (size_t)stride, (size_t)stride * 8,
+                                       hipMemcpyHostToDevice, c->stream));
             HIP_TRY(hipMemcpyAsync(a.count, cnt.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
             rows.clear();

@@ -184,12 +184,8 @@ def test_invalid_cells(host_kring):
 @pytest.mark.gpu
 def test_gpu_kring_pentagons_large_k(host_kring):
     """k = 100 around all 12 pentagons on the GPU (k_h3_kring_slow, one row per wave, stack in
-    scratch): element for element the host build, sets equal the oracle's; beyond k = 128 such a
-    row alone is marked unsupported (count -4) and the rest of the batch is answered."""
-    import ctypes
-
-    from mosaic_amd import MosaicContext, MosaicError
-    from mosaic_amd import _native as N
+    scratch): element for element the host build, sets equal the oracle's."""
+    from mosaic_amd import MosaicContext
 
     h3 = MosaicContext.build("H3", "JTS")
     pents = [pentagon_cell(bc, 7 + i % 4) for i, bc in enumerate(PENTAGON_BASE_CELLS)]
@@ -199,14 +195,42 @@ def test_gpu_kring_pentagons_large_k(host_kring):
             assert g.tolist() == host_kring(p, K_BIG, loop), (p, loop)
     for p, g in zip(pents[:3], h3.grid_cellkring(pents[:3], K_BIG)):
         assert set(g.tolist()) == set(oracle.h3_kring_set(p, K_BIG))
-    k = 129
-    cells = np.array([DOC_CELL, pents[0]], np.int64)
-    out = np.zeros(2 * (1 + 3 * k * (k + 1)), np.int64)
-    cnt = np.zeros(2, np.int32)
-    N.check(N.lib().mosaic_cell_kring(h3.handle, N.GRID_H3, N.ptr(cells), None, 2, k, 0, N.ptr(out), N.ptr(cnt)))
-    assert cnt.tolist() == [1 + 3 * k * (k + 1), -4]
-    with pytest.raises(MosaicError, match="row path"):
-        h3.grid_cellkring(cells.tolist(), k)
+    h3.close()
+
+
+def _digest(cells):
+    m = (1 << 64) - 1
+    cells = [int(c) & m for c in cells]
+    s = x = q = 0
+    for c in cells:
+        s, x, q = (s + c) & m, x ^ c, (q + c * c) & m
+    return dict(n=len(cells), sum=s, xor=x, sumsq=q)
+
+
+@pytest.mark.gpu
+def test_gpu_kring_pentagons_k200(host_kring):
+    """k = 200 around all 12 pentagons -- past the device search's k <= 128, answered
+    by the same H3 _kRingInternal code on host threads inside mosaic_cell_kring (no -4 / row path any
+    more): kRing and kLoop sets equal the oracle's sphere search (order-free digests committed by
+    tests/golden/make_kring_k200.py), in a batch with a row H3's fast walk serves; the element order
+    equals the host build of the device code on two pentagons."""
+    import json
+    import os
+
+    from mosaic_amd import MosaicContext
+
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kring_k200_pentagons.json")))
+    k = fx["k"]
+    h3 = MosaicContext.build("H3", "JTS")
+    cells = [DOC_CELL] + [r["cell"] for r in fx["rows"]]
+    for loop, name in ((0, "ring"), (1, "loop")):
+        got = (h3.grid_cellkloop if loop else h3.grid_cellkring)(cells, k)
+        assert len(got[0]) == (6 * k if loop else 1 + 3 * k * (k + 1))  # the hexagon row: H3's walk
+        for r, g in zip(fx["rows"], got[1:]):
+            assert len(set(g.tolist())) == len(g)
+            assert _digest(g.tolist()) == r[name], (hex(r["cell"]), name)
+        for r, g in zip(fx["rows"][:2], got[1:3]):
+            assert g.tolist() == host_kring(r["cell"], k, loop)
     h3.close()
 
 

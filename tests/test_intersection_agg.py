@@ -248,10 +248,10 @@ def host_stitch(tmp_path_factory):
 
 
 def h3_snap(res):
-    """isect_geom's node tolerance for H3 (mosaic_hip.hip stitch_snap)"""
-    e = [1107.712591, 418.6760055, 158.2446558, 59.81085794, 22.6063794, 8.544408276, 3.229482772, 1.220629759,
-         0.461354684, 0.174375668, 0.065907807, 0.024910561, 0.009415526, 0.003559893, 0.001348575, 0.000509713][res]
-    return max(0.05 * (e / 111.32) ** 2, 180.0 * 2.0 ** -40)
+    """isect_geom's node tolerance for H3 (mosaic_hip.hip stitch_snap): since the chips are the
+    reference's planar clips, adjacent cells' chips meet exactly and the tolerance is the overlay's
+    own node scale, 180 x 2^-40 degrees at every resolution"""
+    return 180.0 * 2.0 ** -40
 
 
 def _sq(x0, y0, s):
@@ -292,14 +292,16 @@ def _units(li, ri):
     return groups
 
 
-def _increments(lv, rv, cell):
+def _increments(lv, rv, cell, bng_res=None):
     """the reference's increments of one cell as an overlay unit (A parts | None, B parts | None, need)"""
     acore, bcore = any(c for c, _ in lv), any(c for c, _ in rv)
     A = [p for _, ps in lv for p in ps]
     B = [p for _, ps in rv for p in ps]
     if acore and bcore:
-        ring = [(math.degrees(lo), math.degrees(la)) for la, lo in oracle.h3_to_geo_boundary(cell)]
-        return [[ring + ring[:1]]], None, 1
+        if bng_res is None:
+            ring = [(math.degrees(lo), math.degrees(la)) for la, lo in oracle.h3_to_geo_boundary(cell)]
+            return [[ring + ring[:1]]], None, 1
+        return [read_wkb(oracle.bng_cell_wkb(cell))[1][0]], None, 1
     if acore:
         return None, B, 2
     if bcore:
@@ -328,11 +330,10 @@ def _shares_edge(parts):
 
 def _check_group(units, wkb, area, snap):
     """the group's WKB against the exact union of its cells' increments.  Chips of adjacent cells
-    meet along their shared side only within the stitching tolerance `snap` (each follows its own
-    cell's gnomonic side), so the exact union X has slivers of that width between cells -- gaps or
-    overlaps -- that the dissolved polygons close: the symmetric difference is bounded by snap x the
-    polygons' perimeter, and is ~0 for a group within one cell.  The area (the sum of the cells'
-    pieces) is X's within the same bound."""
+    meet along their shared side exactly (the reference's planar clips against cell polygons that
+    share their vertices), up to the overlay's node scale `snap`: the symmetric difference is bounded
+    by snap x the polygons' perimeter, and is ~0 for a group within one cell.  The area (the sum of
+    the cells' pieces) is X's within the same bound."""
     us = [(a, b) for a, b, _ in units]
     parts, e = _wkb_edges(wkb)
     d, ax, aw = exact.symdiff_area(e, us)
@@ -472,3 +473,55 @@ def test_gpu_intersection_agg_overlapping_chips(h3ctx):
     _check_group([_increments(lv, rv, cell) for cell, lv, rv in units], wkb[0], area[0], h3_snap(res))
     left.close()
     right.close()
+
+
+def _bng_zones(n=4, size=300.0):
+    """London postcode zones (EPSG:27700) scaled about their vertex mean to ~`size` metres across:
+    small enough for the reference's BNG resolutions 5 (10 m) and 6 (1 m)"""
+    z = PolygonSet.load("london_postcode_zones")
+    xy = []
+    ro, pr, gp = [0], [0], [0]
+    for g in range(n):
+        parts = z.parts(g * 7)
+        allv = np.array([v for p in parts for r in p for v in r])
+        c = allv.mean(axis=0)
+        f = size / max(np.ptp(allv[:, 0]), np.ptp(allv[:, 1]))
+        for p in parts:
+            for r in p:
+                xy += [tuple(c + (np.asarray(v) - c) * f + np.array([450.0 * g, 0.0])) for v in r]
+                ro.append(len(xy))
+            pr.append(len(ro) - 1)
+        gp.append(len(pr) - 1)
+    return PolygonSet(np.array(xy), ro, pr, gp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("res", [5, 6])
+def test_gpu_intersection_agg_bng(res):
+    """st_intersection_aggregate on BNG at the reference's resolutions (intersectionBehaviour
+    on BNG res 5, selfIntersectionBehaviour on BNG res 6, ST_IntersectionTest.scala:27-32): zones
+    against a translated copy and against themselves -- no group refused, the area API equal to the
+    geometry API, sampled groups' polygons equal to the exact union of their cells' increments
+    (symmetric difference within the node scale), dissolved across cells."""
+    from mosaic_amd import MosaicContext
+
+    ctx = MosaicContext.build("BNG", "JTS")
+    zones = _bng_zones(size={5: 300.0, 6: 30.0}[res])  # (~900 cells a zone)
+    snap = 1e6 * 2.0 ** -40
+    for other in (_translated(zones), zones):
+        lc, rc = tessellate("BNG", zones, res, ctx=ctx), tessellate("BNG", other, res, ctx=ctx)
+        left, right = _table(ctx, _rows(lc), res, len(zones)), _table(ctx, _rows(rc), res, len(other))
+        lk, rk, area, st, wkb = ctx.st_intersection_aggregate(left, right)
+        lk2, rk2, area2, st2 = ctx.st_intersection_aggregate_area(left, right)
+        assert len(lk) >= len(zones) and not st.any() and not st2.any()
+        assert np.array_equal(lk, lk2) and np.array_equal(rk, rk2)
+        assert np.array_equal(area.view(np.uint64), area2.view(np.uint64))
+        groups = _units(_chip_index(lc), _chip_index(rc))
+        assert set(zip(lk.tolist(), rk.tolist())) == set(groups)
+        idx = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(lk, rk))}
+        for g in sorted(groups)[:3]:
+            us = [_increments(lv, rv, cell, bng_res=res) for cell, lv, rv in groups[g]]
+            _check_group(us, wkb[idx[g]], area[idx[g]], snap)
+        left.close()
+        right.close()
+    ctx.close()

@@ -35,3 +35,15 @@ def test_glibc_math_restatement_is_bit_exact(tmp_path):
     for name, n, bad in rows:
         assert int(n) > 1000000 and int(bad) == 0, (name, n, bad, res.stderr)
     assert res.returncode == 0
+
+
+def test_h3_digit_pairs_equal_single_levels(tmp_path):
+    """h3_device.h face_axial_to_h3 takes _faceIjkToH3's aperture-7 levels two at a time (the two
+    centre maps compose to 7 x identity, so the digit pair depends only on the axial coordinates
+    mod 7: kAxialPairs); it must equal the one-level form on every face and resolution."""
+    exe = tmp_path / "pairs"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wno-unknown-pragmas", "-I",
+                    os.path.join(ROOT, "mosaic_amd", "csrc"), "-o", str(exe),
+                    os.path.join(ROOT, "tests", "native", "h3_pairs_check.cpp")], check=True)
+    n, bad = map(int, subprocess.run([str(exe), "2000000"], check=True, capture_output=True, text=True).stdout.split())
+    assert n > 6_000_000 and bad == 0
