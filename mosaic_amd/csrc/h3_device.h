@@ -581,6 +581,62 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
     return face_axial_to_h3(face, ba, bb, res);
 }
 
+// h3_fast for two points at once (the cell kernel's two rows per lane): the same arithmetic stage by
+// stage for both, so the two independent chains interleave in one instruction stream.  Points off the
+// common path (non-finite, beyond the table sine's range, outside the face lookup table's cells) take
+// h3_fast itself.  out / amb exactly as h3_fast's for each point (host self-check:
+// tests/native/h3_host_selfcheck.cpp).
+MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2]) {
+    if (res < 0 || res > 15) {
+        out[0] = out[1] = 0;
+        amb[0] = amb[1] = false;
+        return;
+    }
+    bool common[2], ok[2];
+    int face[2], a[2], b[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const double d2r = 0.017453292519943295;
+        const double la = lat[k] * d2r, lo = lon[k] * d2r;
+        common[k] = fabs(lo) < 3.1484375 && fabs(la) < 3.1484375;  // (false for NaN and infinities)
+        double slat, clat, slon, clon;
+        fast_sincos(common[k] ? la : 0.0, &slat, &clat);
+        fast_sincos(common[k] ? lo : 0.0, &slon, &clon);
+        const double px = clon * clat, py = slon * clat, pz = slat;
+        const int li = common[k] ? (int)floor(lat[k] + 90.0) : -1, lj = common[k] ? (int)floor(lon[k] + 180.0) : -1;
+        const int f = (li >= 0 && li < 180 && lj >= 0 && lj < 360) ? (int)kH3FaceLut[li][lj] : 255;
+        common[k] = f != 255;
+        face[k] = common[k] ? f : 0;
+        double vx, vy, best;
+        fast_plane(px, py, pz, face[k], res, &vx, &vy, &best);
+        a[k] = b[k] = 0;
+        ok[k] = fast_hex(vx, vy, res, &a[k], &b[k]);
+        if (!ok[k]) a[k] = b[k] = 0;
+    }
+    uint64_t d[2] = {0, 0};
+    int sh = 0, r = res;
+    const int c3 = res & 1;
+    for (; r >= 2; r -= 2, sh += 6) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int qa = div7f(a[k]), qb = div7f(b[k]);
+            const unsigned e = kAxialPairs.v[c3][7 * (a[k] - 7 * qa) + (b[k] - 7 * qb)];
+            d[k] |= (uint64_t)(e & 63u) << sh;
+            a[k] = qa + (int)((e >> 6) & 7u) - 2;
+            b[k] = qb + (int)((e >> 9) & 7u) - 2;
+        }
+    }
+    const int low = 3 * (15 - res);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (r == 1) d[k] |= (uint64_t)axial_up(a[k], b[k], true) << sh;
+        const uint64_t h = axial_base_to_h3(face[k], a[k], b[k], res, (d[k] << low) | ((1ULL << low) - 1ULL));
+        out[k] = ok[k] ? h : 0;
+        amb[k] = !ok[k];
+        if (!common[k]) out[k] = h3_fast(lat[k], lon[k], res, &amb[k]);
+    }
+}
+
 // java.lang.Math.toRadians (h3-java converts degrees in Java before calling H3 C)
 MOSAIC_HD double to_radians(double deg, int jdk) {
     if (jdk <= 8) return deg / 180.0 * 3.141592653589793;

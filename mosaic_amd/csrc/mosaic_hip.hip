@@ -79,6 +79,10 @@ static int fail(int code, const std::string& msg) {
 
 #include "join_chips.h"
 
+namespace mosaic {
+int kring_slow_host(uint64_t origin, int k, int loop, int64_t* out, int64_t* tab, int32_t* dist, uint64_t* stack);  // kring_host.cpp
+}
+
 template <int GRID, bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
     extern __shared__ unsigned int lds[];
@@ -1628,30 +1632,57 @@ struct CellArgs {
     unsigned long long* amb_count;
     unsigned long long amb_cap;
     unsigned int* flags;
+    int vec;  // x, y, out 16-byte aligned: two rows per lane as 16-byte loads / stores
 };
 
 __device__ __forceinline__ bool cell_row_present(const CellArgs& a, int64_t i) {
     return (!a.valid || a.valid[i]) && (!a.status || a.status[i] == 1);
 }
 
+// grid_longlatascellid / grid_pointascellid's cell step: two consecutive rows per lane (16-byte loads
+// of x and y, one 16-byte store), the two fast paths interleaved (h3::h3_fast2); rows the fast path
+// cannot certify are queued for k_cell_h3_exact.
 __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        bool v = cell_row_present(a, i);
-        if (a.out_valid) a.out_valid[i] = v;
-        if (!v) {
-            a.out[i] = 0;
-            continue;
+    const int64_t np = (a.n + 1) >> 1;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np; p += stride) {
+        const int64_t i = 2 * p;
+        const bool two = i + 1 < a.n;
+        double lat[2], lon[2];
+        if (two && a.vec) {
+            const v2d xv = __builtin_nontemporal_load((const v2d*)(a.x + i));
+            const v2d yv = __builtin_nontemporal_load((const v2d*)(a.y + i));
+            lon[0] = xv.x, lon[1] = xv.y, lat[0] = yv.x, lat[1] = yv.y;
+        } else {
+            lon[0] = a.x[i], lat[0] = a.y[i];
+            lon[1] = two ? a.x[i + 1] : 0.0, lat[1] = two ? a.y[i + 1] : 0.0;
         }
-        bool amb;
-        double xd = a.x[i], yd = a.y[i];
-        uint64_t cell = h3::h3_fast(yd, xd, a.res, &amb);
-        if (amb) {
-            unsigned long long q = atomicAdd(a.amb_count, 1ULL);
-            if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)i;
-            else atomicOr(a.flags, 2u);
+        uint64_t cell[2];
+        bool amb[2];
+        h3::h3_fast2(lat, lon, a.res, cell, amb);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (k == 1 && !two) break;
+            const bool v = cell_row_present(a, i + k);
+            if (a.out_valid) a.out_valid[i + k] = v;
+            if (!v) {
+                cell[k] = 0;
+            } else if (amb[k]) {
+                unsigned long long q = atomicAdd(a.amb_count, 1ULL);
+                if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)(i + k);
+                else atomicOr(a.flags, 2u);
+            }
         }
-        a.out[i] = (long long)cell;
+        if (two && a.vec) {
+            typedef long long v2ll __attribute__((ext_vector_type(2)));
+            v2ll o;
+            o.x = (long long)cell[0];
+            o.y = (long long)cell[1];
+            __builtin_nontemporal_store(o, (v2ll*)(a.out + i));
+        } else {
+            a.out[i] = (long long)cell[0];
+            if (two) a.out[i + 1] = (long long)cell[1];
+        }
     }
 }
 
@@ -2739,6 +2770,7 @@ static int point_to_cell_impl(ThreadCtx* c, int grid, int res, const double* x, 
     a.amb_count = sc + 0;
     a.amb_cap = cap;
     a.flags = (unsigned int*)(sc + 3);
+    a.vec = (((uintptr_t)dx | (uintptr_t)dy | (uintptr_t)dout) & 15) == 0;
     int g = grid_size(c, n);
     if (grid == MOSAIC_GRID_H3) {
         hipLaunchKernelGGL(k_cell_h3, dim3(g), dim3(c->block), 0, c->stream, a);
@@ -5134,7 +5166,7 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
         if (!rows.empty() && k > h3nb::kSlowMaxK) {
             // beyond kSlowMaxK H3's search (~5 k^3 dependent visits per row: seconds for one lane at
             // k ~ 200, the device form would hold a wave that long) runs on host threads -- the same
-            // h3nb::kring_slow (h3_neighbors.h, host build of the device code), so the rows equal
+            // h3nb::kring_slow (h3_neighbors.h) compiled by g++ (kring_host.cpp), so the rows equal
             // h3-java's _kRingInternal tables as the device rows do
             const int64_t m = h3nb::max_kring_size(k), m1 = h3nb::max_kring_size(k - 1);
             std::vector<int64_t> origin(rows.size());
@@ -5152,8 +5184,8 @@ int mosaic_cell_kring(mosaic_ctx* ctx, int grid, const int64_t* cells, const uin
                 std::vector<int32_t> dist((size_t)m);
                 std::vector<uint64_t> stack((size_t)k + 1);
                 for (size_t j; (j = next.fetch_add(1)) < rows.size();)
-                    cnt[(size_t)rows[j]] = h3nb::kring_slow((uint64_t)origin[j], k, loop, res.data() + j * (size_t)stride,
-                                                             tab.data(), dist.data(), stack.data());
+                    cnt[(size_t)rows[j]] = mosaic::kring_slow_host((uint64_t)origin[j], k, loop, res.data() + j * (size_t)stride,
+                                                                    tab.data(), dist.data(), stack.data());
             };
             {
                 // (tables of ~3 k^2 cells per thread: at most 16 threads, fewer for huge k)

@@ -84,6 +84,22 @@ int main(int argc, char** argv) {
         }
         bool a = false;
         int64_t fa = (int64_t)mosaic::h3::h3_fast(lat, lon, res, &a);
+        {
+            // the two-point form (k_cell_h3): this point beside the previous one, both as h3_fast
+            static double plat = 40.7, plon = -74.0;
+            const double la2[2] = {plat, lat}, lo2[2] = {plon, lon};
+            uint64_t c2[2];
+            bool a2[2];
+            mosaic::h3::h3_fast2(la2, lo2, res, c2, a2);
+            bool ap = false;
+            const uint64_t cp = mosaic::h3::h3_fast(plat, plon, res, &ap);
+            if (c2[1] != (uint64_t)fa || a2[1] != a || c2[0] != cp || a2[0] != ap) {
+                if (bad_fast < 5) fprintf(stderr, "fast2 mismatch lat %.17g lon %.17g res %d\n", lat, lon, res);
+                bad_fast++;
+            }
+            plat = lat;
+            plon = lon;
+        }
         if (a) {
             amb++;
         } else if (fa != want) {
