@@ -2,6 +2,7 @@
 // mosaic_hip.hip and the one launcher run_join calls.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include <vector>
@@ -75,3 +76,28 @@ hipError_t join(const JoinArgs& a, int64_t lo, int64_t n, uint32_t max_code, boo
                 const Images& img, Scratch& s, hipStream_t stream);
 
 }  // namespace binned
+
+// Layout fingerprint of the structs the translation units hand each other (JoinArgs, StreamArgs,
+// BngStreamArgs, binned::Scratch / Images, by size and the offsets the other side reads).  Every TU
+// reports the value its own compilation of these headers gives (mosaic_layout_*); mosaic_init refuses
+// to run when they differ.  Round 5's A/B library linked a join_binned.o built against an older
+// join_binned.h (Scratch without `slots`: 16 bytes shorter) into a mosaic_hip.o built against the new
+// one: join() wrote s.exact_args where mosaic_hip.o did not read it, and the exact-H3 pass ran with
+// shifted pointers -- the illegal-address fault of gpurun_out/r05h.
+#define MOSAIC_FP_MIX(h, v) ((h) * 0x100000001b3ULL ^ (uint64_t)(v))
+static constexpr uint64_t mosaic_layout_fingerprint() {
+    uint64_t h = 0xcbf29ce484222325ULL;
+    h = MOSAIC_FP_MIX(h, sizeof(JoinArgs));
+    h = MOSAIC_FP_MIX(h, sizeof(StreamArgs));
+    h = MOSAIC_FP_MIX(h, sizeof(BngStreamArgs));
+    h = MOSAIC_FP_MIX(h, sizeof(binned::Scratch));
+    h = MOSAIC_FP_MIX(h, offsetof(binned::Scratch, exact_args));
+    h = MOSAIC_FP_MIX(h, offsetof(binned::Scratch, sorted_rows));
+    h = MOSAIC_FP_MIX(h, offsetof(binned::Scratch, spin_cap));
+    h = MOSAIC_FP_MIX(h, offsetof(binned::Scratch, lookback_failed));
+    h = MOSAIC_FP_MIX(h, sizeof(binned::Images));
+    h = MOSAIC_FP_MIX(h, offsetof(JoinArgs, res));
+    h = MOSAIC_FP_MIX(h, offsetof(JoinArgs, counts));
+    return h;
+}
+#undef MOSAIC_FP_MIX

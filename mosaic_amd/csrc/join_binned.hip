@@ -746,3 +746,5 @@ hipError_t join(const JoinArgs& a, int64_t lo, int64_t n, uint32_t max_code, boo
 }
 
 }  // namespace binned
+
+extern "C" uint64_t mosaic_layout_join_binned(void) { return mosaic_layout_fingerprint(); }

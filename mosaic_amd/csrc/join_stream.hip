@@ -1,6 +1,7 @@
 // The stream kernels of the point-raster join: k_join_stream / k_join_stream_pipe (H3 tile
 // directory + point raster, tiles.h) and k_join_stream_bng (BNG dense cell table).  A translation
 // unit of their own (the host side that builds their arguments and launches them is mosaic_hip.hip).
+#include "join_binned.h"
 #include "join_common.h"
 
 // ---- k_join_stream (default with a point raster, tiles.h): the point raster's answer for every
@@ -1247,3 +1248,5 @@ const void* stream_kernel_bng(bool lds, bool pairs, bool vec, bool cpt) {
     if (lds) return vec ? (const void*)k_join_stream_bng<true, false, true> : (const void*)k_join_stream_bng<true, false, false>;
     return vec ? (const void*)k_join_stream_bng<false, false, true> : (const void*)k_join_stream_bng<false, false, false>;
 }
+
+extern "C" uint64_t mosaic_layout_join_stream(void) { return mosaic_layout_fingerprint(); }

@@ -82,6 +82,10 @@ static int fail(int code, const std::string& msg) {
 namespace mosaic {
 int kring_slow_host(uint64_t origin, int k, int loop, int64_t* out, int64_t* tab, int32_t* dist, uint64_t* stack);  // kring_host.cpp
 }
+// the other translation units' view of the shared structs (join_binned.h, tess_clip.h)
+extern "C" uint64_t mosaic_layout_join_binned(void);
+extern "C" uint64_t mosaic_layout_join_stream(void);
+extern "C" uint64_t mosaic_layout_tess_clip(void);
 
 template <int GRID, bool LDS_COUNTS, bool PAIRS>
 __global__ void __launch_bounds__(256) k_join_raster(JoinArgs a) {
@@ -2428,6 +2432,11 @@ static void thp_off_once() {
 
 int mosaic_init(int device, mosaic_ctx** out) {
     if (!out) return fail(MOSAIC_E_ARG, "out is null");
+    // objects compiled against different revisions of the shared headers (a hand-linked A/B library)
+    // would pass structs with shifted fields between translation units: refuse to run
+    if (mosaic_layout_join_binned() != mosaic_layout_fingerprint() || mosaic_layout_join_stream() != mosaic_layout_fingerprint() ||
+        mosaic_layout_tess_clip() != mosaic::tessll::layout_fingerprint())
+        return fail(MOSAIC_E_ARG, "libmosaic_hip.so links objects built against different struct layouts (rebuild every object)");
     thp_off_once();
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(MOSAIC_E_HIP, "no HIP device available");

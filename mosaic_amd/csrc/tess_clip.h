@@ -3,6 +3,7 @@
 // tess_clip.hip and the host orchestration in mosaic_hip.hip.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "llclip.h"
@@ -35,6 +36,16 @@ struct ClipLLArgs {
 
 // launch over `lanes` lanes (grid-stride over the tasks)
 hipError_t launch_clip_ll(const ClipLLArgs& a, int64_t lanes, hipStream_t stream);
+
+// layout fingerprint of the records mosaic_hip.hip and tess_clip.hip share (join_binned.h's rationale)
+static constexpr uint64_t layout_fingerprint() {
+    uint64_t h = 0xcbf29ce484222325ULL;
+    for (uint64_t v : {(uint64_t)sizeof(ClipLLArgs), (uint64_t)sizeof(llclip::Chain), (uint64_t)sizeof(llclip::Out),
+                       (uint64_t)sizeof(tessclip::ClipRing), (uint64_t)sizeof(tessclip::ClipPart),
+                       (uint64_t)offsetof(ClipLLArgs, status), (uint64_t)kLLChains, (uint64_t)kLLOut})
+        h = h * 0x100000001b3ULL ^ v;
+    return h;
+}
 
 }  // namespace tessll
 }  // namespace mosaic

@@ -95,3 +95,5 @@ hipError_t launch_clip_ll(const ClipLLArgs& a, int64_t lanes, hipStream_t stream
 
 }  // namespace tessll
 }  // namespace mosaic
+
+extern "C" uint64_t mosaic_layout_tess_clip(void) { return mosaic::tessll::layout_fingerprint(); }

@@ -113,3 +113,22 @@ def test_graft_build_entry():
     import __graft_entry__ as g
 
     g.build()
+
+
+def test_translation_units_agree_on_struct_layouts():
+    """The objects of libmosaic_hip.so were compiled against the same shared headers: each reports the
+    layout fingerprint of the structs it exchanges (join_binned.h / tess_clip.h), and mosaic_init refuses
+    a library whose objects disagree (round 5's hand-linked A/B library faulted that way, DESIGN.md
+    section 8).  Host functions: no GPU needed."""
+    import ctypes
+
+    from mosaic_amd import _native as N
+
+    lib = N.lib()
+    fps = []
+    for name in ("mosaic_layout_join_binned", "mosaic_layout_join_stream", "mosaic_layout_tess_clip"):
+        f = getattr(lib, name)
+        f.restype = ctypes.c_uint64
+        f.argtypes = []
+        fps.append(f())
+    assert fps[0] == fps[1] and all(fps)

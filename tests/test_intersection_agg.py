@@ -478,7 +478,7 @@ def test_gpu_intersection_agg_overlapping_chips(h3ctx):
 def _bng_zones(n=4, size=300.0):
     """London postcode zones (EPSG:27700) scaled about their vertex mean to ~`size` metres across:
     small enough for the reference's BNG resolutions 5 (10 m) and 6 (1 m)"""
-    z = PolygonSet.load("london_postcode_zones")
+    z = PolygonSet.load("london_postcodes_bng")
     xy = []
     ro, pr, gp = [0], [0], [0]
     for g in range(n):
