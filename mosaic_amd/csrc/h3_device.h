@@ -583,13 +583,16 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
 
 // h3_fast for two points at once (the cell kernel's two rows per lane): the same arithmetic stage by
 // stage for both, so the two independent chains interleave in one instruction stream.  Points off the
-// common path (non-finite, beyond the table sine's range, outside the face lookup table's cells) take
-// h3_fast itself.  out / amb exactly as h3_fast's for each point (host self-check:
-// tests/native/h3_host_selfcheck.cpp).
-MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2]) {
+// common path (non-finite, beyond the table sine's range, outside the face lookup table's cells) are
+// reported in rare[] (out 0) for the caller to run h3_fast on -- out of this instruction stream: its
+// glibc sincos and 20-face search, inlined here, cost the common path registers.  Otherwise out /
+// amb exactly as h3_fast's (host self-check: tests/native/h3_host_selfcheck.cpp).
+MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2], bool rare[2],
+                        const AxialPairTab* pairs = nullptr) {
+    const AxialPairTab& P = pairs ? *pairs : kAxialPairs;  // (a kernel may pass its LDS copy)
     if (res < 0 || res > 15) {
         out[0] = out[1] = 0;
-        amb[0] = amb[1] = false;
+        amb[0] = amb[1] = rare[0] = rare[1] = false;
         return;
     }
     bool common[2], ok[2];
@@ -620,7 +623,7 @@ MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint6
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const int qa = div7f(a[k]), qb = div7f(b[k]);
-            const unsigned e = kAxialPairs.v[c3][7 * (a[k] - 7 * qa) + (b[k] - 7 * qb)];
+            const unsigned e = P.v[c3][7 * (a[k] - 7 * qa) + (b[k] - 7 * qb)];
             d[k] |= (uint64_t)(e & 63u) << sh;
             a[k] = qa + (int)((e >> 6) & 7u) - 2;
             b[k] = qb + (int)((e >> 9) & 7u) - 2;
@@ -631,9 +634,9 @@ MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint6
     for (int k = 0; k < 2; k++) {
         if (r == 1) d[k] |= (uint64_t)axial_up(a[k], b[k], true) << sh;
         const uint64_t h = axial_base_to_h3(face[k], a[k], b[k], res, (d[k] << low) | ((1ULL << low) - 1ULL));
-        out[k] = ok[k] ? h : 0;
-        amb[k] = !ok[k];
-        if (!common[k]) out[k] = h3_fast(lat[k], lon[k], res, &amb[k]);
+        out[k] = ok[k] && common[k] ? h : 0;
+        amb[k] = !ok[k] && common[k];
+        rare[k] = !common[k];
     }
 }
 

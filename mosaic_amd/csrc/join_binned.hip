@@ -356,7 +356,11 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
 // the tile join's rare paths, inlined (as calls, the C4 1e6 kernel went 8.87 -> 10.88 ms: call-site
 // register saves and spills)
 #define MOSAIC_TJ_NOINLINE __device__ __forceinline__
+#if defined(MOSAIC_TJ_CONTAINS_CALL)  // measurement build: only the f64 walk (undecided pairs) as a call
+__device__ __attribute__((noinline)) bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
+#else
 MOSAIC_TJ_NOINLINE bool contains_call(const pip::GeomStore& s, uint32_t c, double x, double y) {
+#endif
     return pip::contains(s, c, x, y);
 }
 MOSAIC_TJ_NOINLINE uint2 tiled_cell_call(const JoinArgs& a, int64_t i, double x, double y, uint32_t code) {

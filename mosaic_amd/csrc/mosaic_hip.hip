@@ -1647,6 +1647,14 @@ __device__ __forceinline__ bool cell_row_present(const CellArgs& a, int64_t i) {
 // of x and y, one 16-byte store), the two fast paths interleaved (h3::h3_fast2); rows the fast path
 // cannot certify are queued for k_cell_h3_exact.
 __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
+#if defined(MOSAIC_CELL_LDS_PAIRS)  // measurement build: the digit-pair table read from LDS
+    __shared__ h3::AxialPairTab lpairs;
+    for (int k = threadIdx.x; k < 98; k += blockDim.x) (&lpairs.v[0][0])[k] = (&h3::kAxialPairs.v[0][0])[k];
+    __syncthreads();
+    const h3::AxialPairTab* ptab = &lpairs;
+#else
+    const h3::AxialPairTab* ptab = nullptr;
+#endif
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t np = (a.n + 1) >> 1;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np; p += stride) {
@@ -1662,8 +1670,8 @@ __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
             lon[1] = two ? a.x[i + 1] : 0.0, lat[1] = two ? a.y[i + 1] : 0.0;
         }
         uint64_t cell[2];
-        bool amb[2];
-        h3::h3_fast2(lat, lon, a.res, cell, amb);
+        bool amb[2], rare[2];
+        h3::h3_fast2(lat, lon, a.res, cell, amb, rare, ptab);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             if (k == 1 && !two) break;
@@ -1671,7 +1679,9 @@ __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
             if (a.out_valid) a.out_valid[i + k] = v;
             if (!v) {
                 cell[k] = 0;
-            } else if (amb[k]) {
+            } else if (amb[k] || rare[k]) {
+                // (rare rows -- off the face table, beyond the table sine, non-finite -- get h3_fast in
+                // k_cell_h3_exact, then h3_exact if that is ambiguous too)
                 unsigned long long q = atomicAdd(a.amb_count, 1ULL);
                 if (q < a.amb_cap) a.amb_queue[q] = (unsigned long long)(i + k);
                 else atomicOr(a.flags, 2u);
@@ -1696,7 +1706,11 @@ __global__ void __launch_bounds__(256) k_cell_h3_exact(CellArgs a, int all_rows)
     for (unsigned long long t = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
         int64_t i = all_rows ? (int64_t)t : (int64_t)a.amb_queue[t];
         if (!cell_row_present(a, i)) continue;
-        a.out[i] = (long long)h3::h3_exact(h3::to_radians(a.y[i], a.jdk), h3::to_radians(a.x[i], a.jdk), a.res);
+        // queued rows: k_cell_h3's rare rows take the full fast path first (face search, glibc sincos)
+        bool amb = true;
+        uint64_t cell = all_rows ? 0 : h3::h3_fast(a.y[i], a.x[i], a.res, &amb);
+        if (amb) cell = h3::h3_exact(h3::to_radians(a.y[i], a.jdk), h3::to_radians(a.x[i], a.jdk), a.res);
+        a.out[i] = (long long)cell;
     }
 }
 

@@ -89,8 +89,10 @@ int main(int argc, char** argv) {
             static double plat = 40.7, plon = -74.0;
             const double la2[2] = {plat, lat}, lo2[2] = {plon, lon};
             uint64_t c2[2];
-            bool a2[2];
-            mosaic::h3::h3_fast2(la2, lo2, res, c2, a2);
+            bool a2[2], r2[2];
+            mosaic::h3::h3_fast2(la2, lo2, res, c2, a2, r2);
+            for (int k = 0; k < 2; k++)
+                if (r2[k]) c2[k] = mosaic::h3::h3_fast(la2[k], lo2[k], res, &a2[k]);  // (the caller's rare path)
             bool ap = false;
             const uint64_t cp = mosaic::h3::h3_fast(plat, plon, res, &ap);
             if (c2[1] != (uint64_t)fa || a2[1] != a || c2[0] != cp || a2[0] != ap) {
