@@ -587,41 +587,73 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
 // reported in rare[] (out 0) for the caller to run h3_fast on -- out of this instruction stream: its
 // glibc sincos and 20-face search, inlined here, cost the common path registers.  Otherwise out /
 // amb exactly as h3_fast's (host self-check: tests/native/h3_host_selfcheck.cpp).
-MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2], bool rare[2],
+template <int K>
+MOSAIC_HD void h3_fastk(const double lat[K], const double lon[K], int res, uint64_t out[K], bool amb[K], bool rare[K],
                         const AxialPairTab* pairs = nullptr) {
     const AxialPairTab& P = pairs ? *pairs : kAxialPairs;  // (a kernel may pass its LDS copy)
     if (res < 0 || res > 15) {
-        out[0] = out[1] = 0;
-        amb[0] = amb[1] = rare[0] = rare[1] = false;
+        for (int k = 0; k < K; k++) out[k] = 0, amb[k] = rare[k] = false;
         return;
     }
-    bool common[2], ok[2];
-    int face[2], a[2], b[2];
+    bool common[K], ok[K];
+    int face[K], a[K], b[K];
+    double px[K], py[K], pz[K];
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < K; k++) {
         const double d2r = 0.017453292519943295;
         const double la = lat[k] * d2r, lo = lon[k] * d2r;
         common[k] = fabs(lo) < 3.1484375 && fabs(la) < 3.1484375;  // (false for NaN and infinities)
         double slat, clat, slon, clon;
         fast_sincos(common[k] ? la : 0.0, &slat, &clat);
         fast_sincos(common[k] ? lo : 0.0, &slon, &clon);
-        const double px = clon * clat, py = slon * clat, pz = slat;
+        px[k] = clon * clat, py[k] = slon * clat, pz[k] = slat;
         const int li = common[k] ? (int)floor(lat[k] + 90.0) : -1, lj = common[k] ? (int)floor(lon[k] + 180.0) : -1;
         const int f = (li >= 0 && li < 180 && lj >= 0 && lj < 360) ? (int)kH3FaceLut[li][lj] : 255;
         common[k] = f != 255;
         face[k] = common[k] ? f : 0;
-        double vx, vy, best;
-        fast_plane(px, py, pz, face[k], res, &vx, &vy, &best);
+    }
+    double vx[K], vy[K];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // a wave whose points all lie on one face (nearly every wave of a regional batch) reads that face's
+    // basis with scalar loads into SGPRs instead of 15 vector gathers per point
+    const int f0 = __builtin_amdgcn_readfirstlane(face[0]);
+    bool other = false;
+#pragma unroll
+    for (int k = 0; k < K; k++) other = other || face[k] != f0;
+    if (__ballot(other) == 0) {
+        const double* fb = kH3FastBasis[f0];
+        const double* ei = fb + ((res & 1) ? 9 : 3);
+        const double* ep = fb + ((res & 1) ? 12 : 6);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double bb = fma(fb[0], px[k], fma(fb[1], py[k], fb[2] * pz[k]));
+            const double sc = kH3FastScale[res] / bb;
+            vx[k] = sc * fma(ei[0], px[k], fma(ei[1], py[k], ei[2] * pz[k]));
+            vy[k] = sc * fma(ep[0], px[k], fma(ep[1], py[k], ep[2] * pz[k]));
+        }
+    } else
+#endif
+    {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            double best;
+            fast_plane(px[k], py[k], pz[k], face[k], res, &vx[k], &vy[k], &best);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
         a[k] = b[k] = 0;
-        ok[k] = fast_hex(vx, vy, res, &a[k], &b[k]);
+        ok[k] = fast_hex(vx[k], vy[k], res, &a[k], &b[k]);
         if (!ok[k]) a[k] = b[k] = 0;
     }
-    uint64_t d[2] = {0, 0};
+    uint64_t d[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) d[k] = 0;
     int sh = 0, r = res;
     const int c3 = res & 1;
     for (; r >= 2; r -= 2, sh += 6) {
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < K; k++) {
             const int qa = div7f(a[k]), qb = div7f(b[k]);
             const unsigned e = P.v[c3][7 * (a[k] - 7 * qa) + (b[k] - 7 * qb)];
             d[k] |= (uint64_t)(e & 63u) << sh;
@@ -631,13 +663,17 @@ MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint6
     }
     const int low = 3 * (15 - res);
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < K; k++) {
         if (r == 1) d[k] |= (uint64_t)axial_up(a[k], b[k], true) << sh;
         const uint64_t h = axial_base_to_h3(face[k], a[k], b[k], res, (d[k] << low) | ((1ULL << low) - 1ULL));
         out[k] = ok[k] && common[k] ? h : 0;
         amb[k] = !ok[k] && common[k];
         rare[k] = !common[k];
     }
+}
+MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2], bool rare[2],
+                        const AxialPairTab* pairs = nullptr) {
+    h3_fastk<2>(lat, lon, res, out, amb, rare, pairs);
 }
 
 // java.lang.Math.toRadians (h3-java converts degrees in Java before calling H3 C)

@@ -1643,38 +1643,49 @@ __device__ __forceinline__ bool cell_row_present(const CellArgs& a, int64_t i) {
     return (!a.valid || a.valid[i]) && (!a.status || a.status[i] == 1);
 }
 
+// rows per lane of k_cell_h3 (compile-time; 2 unless a measurement build sets MOSAIC_CELL_ROWS)
+#if defined(MOSAIC_CELL_ROWS)
+static constexpr int kCellRows = MOSAIC_CELL_ROWS;
+#else
+static constexpr int kCellRows = 2;
+#endif
 // grid_longlatascellid / grid_pointascellid's cell step: two consecutive rows per lane (16-byte loads
 // of x and y, one 16-byte store), the two fast paths interleaved (h3::h3_fast2); rows the fast path
 // cannot certify are queued for k_cell_h3_exact.
 __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
-#if defined(MOSAIC_CELL_LDS_PAIRS)  // measurement build: the digit-pair table read from LDS
+    // the digit-pair table read from LDS (12.8 vs 13.6 ms per 1e9 points from the constant table:
+    // gpurun_out/r06f, profiles/r06_cell_*)
     __shared__ h3::AxialPairTab lpairs;
     for (int k = threadIdx.x; k < 98; k += blockDim.x) (&lpairs.v[0][0])[k] = (&h3::kAxialPairs.v[0][0])[k];
     __syncthreads();
     const h3::AxialPairTab* ptab = &lpairs;
-#else
-    const h3::AxialPairTab* ptab = nullptr;
-#endif
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t np = (a.n + 1) >> 1;
+    constexpr int R = kCellRows;
+    const int64_t np = (a.n + R - 1) / R;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np; p += stride) {
-        const int64_t i = 2 * p;
-        const bool two = i + 1 < a.n;
-        double lat[2], lon[2];
-        if (two && a.vec) {
-            const v2d xv = __builtin_nontemporal_load((const v2d*)(a.x + i));
-            const v2d yv = __builtin_nontemporal_load((const v2d*)(a.y + i));
-            lon[0] = xv.x, lon[1] = xv.y, lat[0] = yv.x, lat[1] = yv.y;
-        } else {
-            lon[0] = a.x[i], lat[0] = a.y[i];
-            lon[1] = two ? a.x[i + 1] : 0.0, lat[1] = two ? a.y[i + 1] : 0.0;
-        }
-        uint64_t cell[2];
-        bool amb[2], rare[2];
-        h3::h3_fast2(lat, lon, a.res, cell, amb, rare, ptab);
+        const int64_t i = R * p;
+        const bool full = i + R <= a.n;
+        double lat[R], lon[R];
+        if (full && a.vec) {
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            if (k == 1 && !two) break;
+            for (int h = 0; h < R / 2; h++) {
+                const v2d xv = __builtin_nontemporal_load((const v2d*)(a.x + i) + h);
+                const v2d yv = __builtin_nontemporal_load((const v2d*)(a.y + i) + h);
+                lon[2 * h] = xv.x, lon[2 * h + 1] = xv.y, lat[2 * h] = yv.x, lat[2 * h + 1] = yv.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                lon[k] = i + k < a.n ? a.x[i + k] : 0.0;
+                lat[k] = i + k < a.n ? a.y[i + k] : 0.0;
+            }
+        }
+        uint64_t cell[R];
+        bool amb[R], rare[R];
+        h3::h3_fastk<R>(lat, lon, a.res, cell, amb, rare, ptab);
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            if (i + k >= a.n) continue;
             const bool v = cell_row_present(a, i + k);
             if (a.out_valid) a.out_valid[i + k] = v;
             if (!v) {
@@ -1687,15 +1698,19 @@ __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
                 else atomicOr(a.flags, 2u);
             }
         }
-        if (two && a.vec) {
+        if (full && a.vec) {
             typedef long long v2ll __attribute__((ext_vector_type(2)));
-            v2ll o;
-            o.x = (long long)cell[0];
-            o.y = (long long)cell[1];
-            __builtin_nontemporal_store(o, (v2ll*)(a.out + i));
+#pragma unroll
+            for (int h = 0; h < R / 2; h++) {
+                v2ll o;
+                o.x = (long long)cell[2 * h];
+                o.y = (long long)cell[2 * h + 1];
+                __builtin_nontemporal_store(o, (v2ll*)(a.out + i) + h);
+            }
         } else {
-            a.out[i] = (long long)cell[0];
-            if (two) a.out[i + 1] = (long long)cell[1];
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if (i + k < a.n) a.out[i + k] = (long long)cell[k];
         }
     }
 }
@@ -2793,7 +2808,7 @@ static int point_to_cell_impl(ThreadCtx* c, int grid, int res, const double* x, 
     a.amb_count = sc + 0;
     a.amb_cap = cap;
     a.flags = (unsigned int*)(sc + 3);
-    a.vec = (((uintptr_t)dx | (uintptr_t)dy | (uintptr_t)dout) & 15) == 0;
+    a.vec = (((uintptr_t)dx | (uintptr_t)dy | (uintptr_t)dout) & 15) == 0;  // (every group of rows starts 16-byte aligned: kCellRows even)
     int g = grid_size(c, n);
     if (grid == MOSAIC_GRID_H3) {
         hipLaunchKernelGGL(k_cell_h3, dim3(g), dim3(c->block), 0, c->stream, a);
