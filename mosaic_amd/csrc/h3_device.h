@@ -422,6 +422,40 @@ static __constant__ const AxialPairTab kAxialPairs = make_axial_pair_tab();
 static const AxialPairTab kAxialPairs = make_axial_pair_tab();
 #endif
 
+// Four levels at once, by the same argument twice: the two pair steps compose to 49 x identity, so
+// with (a, b) = 49 (qa, qb) + (ra, rb), 0 <= ra, rb < 49, the four digits depend on (ra, rb) alone and
+// the level-4 ancestor is (qa, qb) + an offset in [-3, 3].  Table [first level is Class III][49 ra + rb]:
+// bits 0-11 the four digits (finest lowest), 12-14 / 15-17 the ancestor offset + 3.  Built at compile
+// time from the pair table (tests/native/h3_pairs_check.cpp: identical to the one-level form).
+struct AxialQuadTab {
+    uint32_t v[2][2401];
+};
+MOSAIC_HD constexpr AxialQuadTab make_axial_quad_tab() {
+    AxialQuadTab t{};
+    const AxialPairTab P = make_axial_pair_tab();
+    for (int c3 = 0; c3 < 2; c3++)
+        for (int ra = 0; ra < 49; ra++)
+            for (int rb = 0; rb < 49; rb++) {
+                const unsigned e1 = P.v[c3][7 * (ra % 7) + rb % 7];
+                const int a1 = ra / 7 + (int)((e1 >> 6) & 7u) - 2, b1 = rb / 7 + (int)((e1 >> 9) & 7u) - 2;
+                const int qa = div7f(a1), qb = div7f(b1);
+                const unsigned e2 = P.v[c3][7 * (a1 - 7 * qa) + (b1 - 7 * qb)];
+                const int a2 = qa + (int)((e2 >> 6) & 7u) - 2, b2 = qb + (int)((e2 >> 9) & 7u) - 2;
+                t.v[c3][49 * ra + rb] = (e1 & 63u) | (e2 & 63u) << 6 | (unsigned)(a2 + 3) << 12 | (unsigned)(b2 + 3) << 15;
+            }
+    return t;
+}
+#if defined(__HIPCC__)
+static __constant__ const AxialQuadTab kAxialQuads = make_axial_quad_tab();
+#else
+static const AxialQuadTab kAxialQuads = make_axial_quad_tab();
+#endif
+// floor(n / 49) for |n| < 2^27
+MOSAIC_HD constexpr int div49f(int n) {
+    const unsigned off = 49u << 22;
+    return (int)(((unsigned)n + off) / 49u) - (1 << 22);
+}
+
 // _faceIjkToH3 in axial coordinates (a, b) = (i - k, j - k) of the res-`res` cell on `face`.
 // Same arithmetic as face_ijk_to_h3 (the axial pair is invariant under _ijkNormalize, and
 // _downAp7 / _downAp7r are linear), with the three normalisations per level removed and the levels
@@ -472,6 +506,30 @@ MOSAIC_HD uint64_t face_axial_to_h3(int face, int a, int b, int res) {
     const int low = 3 * (15 - res);
     const uint64_t digits = (d << low) | ((1ULL << low) - 1ULL);
     return axial_base_to_h3(face, a, b, res, digits);
+}
+// face_axial_to_h3 with the levels four at a time (kAxialQuads), then at most one pair and one level.
+MOSAIC_HD uint64_t face_axial_to_h3_quad(int face, int a, int b, int res, const uint32_t* Q) {
+    uint64_t d = 0;
+    int sh = 0, r = res;
+    const int c3 = res & 1;
+    for (; r >= 4; r -= 4, sh += 12) {
+        const int qa = div49f(a), qb = div49f(b);
+        const unsigned e = Q[49 * (a - 49 * qa) + (b - 49 * qb)];
+        d |= (uint64_t)(e & 4095u) << sh;
+        a = qa + (int)((e >> 12) & 7u) - 3;
+        b = qb + (int)((e >> 15) & 7u) - 3;
+    }
+    if (r >= 2) {
+        const int qa = div7f(a), qb = div7f(b);
+        const unsigned e = kAxialPairs.v[c3][7 * (a - 7 * qa) + (b - 7 * qb)];
+        d |= (uint64_t)(e & 63u) << sh;
+        a = qa + (int)((e >> 6) & 7u) - 2;
+        b = qb + (int)((e >> 9) & 7u) - 2;
+        r -= 2, sh += 6;
+    }
+    if (r == 1) d |= (uint64_t)axial_up(a, b, true) << sh;
+    const int low = 3 * (15 - res);
+    return axial_base_to_h3(face, a, b, res, (d << low) | ((1ULL << low) - 1ULL));
 }
 
 // The unit vector of (lat_deg, lon_deg) for the fast path: radians by one multiply (within 2 ulp of
@@ -587,10 +645,13 @@ MOSAIC_HD uint64_t h3_fast(double lat_deg, double lon_deg, int res, bool* ambigu
 // reported in rare[] (out 0) for the caller to run h3_fast on -- out of this instruction stream: its
 // glibc sincos and 20-face search, inlined here, cost the common path registers.  Otherwise out /
 // amb exactly as h3_fast's (host self-check: tests/native/h3_host_selfcheck.cpp).
-template <int K>
-MOSAIC_HD void h3_fastk(const double lat[K], const double lon[K], int res, uint64_t out[K], bool amb[K], bool rare[K],
-                        const AxialPairTab* pairs = nullptr) {
-    const AxialPairTab& P = pairs ? *pairs : kAxialPairs;  // (a kernel may pass its LDS copy)
+// The digit tables are parameters (a kernel passes its LDS copies, referenced directly so that the
+// reads compile to LDS loads -- a pointer chosen at run time between LDS and the constant table is a
+// flat pointer, and the loads go through the vector memory path); Q = the four-level table of res's
+// parity (kAxialQuads.v[res & 1] or a copy), used when kQuad.
+template <int K, bool kQuad>
+MOSAIC_HD void h3_fastk_tab(const double lat[K], const double lon[K], int res, uint64_t out[K], bool amb[K], bool rare[K],
+                            const AxialPairTab& P, const uint32_t* Q) {
     if (res < 0 || res > 15) {
         for (int k = 0; k < K; k++) out[k] = 0, amb[k] = rare[k] = false;
         return;
@@ -651,6 +712,18 @@ MOSAIC_HD void h3_fastk(const double lat[K], const double lon[K], int res, uint6
     for (int k = 0; k < K; k++) d[k] = 0;
     int sh = 0, r = res;
     const int c3 = res & 1;
+    if (kQuad) {
+        for (; r >= 4; r -= 4, sh += 12) {
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int qa = div49f(a[k]), qb = div49f(b[k]);
+                const unsigned e = Q[49 * (a[k] - 49 * qa) + (b[k] - 49 * qb)];
+                d[k] |= (uint64_t)(e & 4095u) << sh;
+                a[k] = qa + (int)((e >> 12) & 7u) - 3;
+                b[k] = qb + (int)((e >> 15) & 7u) - 3;
+            }
+        }
+    }
     for (; r >= 2; r -= 2, sh += 6) {
 #pragma unroll
         for (int k = 0; k < K; k++) {
@@ -671,9 +744,15 @@ MOSAIC_HD void h3_fastk(const double lat[K], const double lon[K], int res, uint6
         rare[k] = !common[k];
     }
 }
-MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2], bool rare[2],
-                        const AxialPairTab* pairs = nullptr) {
-    h3_fastk<2>(lat, lon, res, out, amb, rare, pairs);
+template <int K>
+MOSAIC_HD void h3_fastk(const double lat[K], const double lon[K], int res, uint64_t out[K], bool amb[K], bool rare[K]) {
+    h3_fastk_tab<K, false>(lat, lon, res, out, amb, rare, kAxialPairs, nullptr);
+}
+MOSAIC_HD void h3_fast2(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2], bool rare[2]) {
+    h3_fastk<2>(lat, lon, res, out, amb, rare);
+}
+MOSAIC_HD void h3_fast2_quad(const double lat[2], const double lon[2], int res, uint64_t out[2], bool amb[2], bool rare[2]) {
+    h3_fastk_tab<2, true>(lat, lon, res, out, amb, rare, kAxialPairs, res >= 0 && res <= 15 ? kAxialQuads.v[res & 1] : nullptr);
 }
 
 // java.lang.Math.toRadians (h3-java converts degrees in Java before calling H3 C)

@@ -1649,16 +1649,32 @@ static constexpr int kCellRows = MOSAIC_CELL_ROWS;
 #else
 static constexpr int kCellRows = 2;
 #endif
+// digits four levels per step (h3::kAxialQuads) in k_cell_h3 (compile-time; a measurement build may set
+// MOSAIC_CELL_QUAD=0 for the pair steps alone)
+#if defined(MOSAIC_CELL_QUAD)
+static constexpr bool kCellQuad = MOSAIC_CELL_QUAD != 0;
+#else
+static constexpr bool kCellQuad = true;
+#endif
 // grid_longlatascellid / grid_pointascellid's cell step: two consecutive rows per lane (16-byte loads
-// of x and y, one 16-byte store), the two fast paths interleaved (h3::h3_fast2); rows the fast path
+// of x and y, one 16-byte store), the two fast paths interleaved (h3::h3_fastk_tab); rows the fast path
 // cannot certify are queued for k_cell_h3_exact.
-__global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
-    // the digit-pair table read from LDS (12.8 vs 13.6 ms per 1e9 points from the constant table:
-    // gpurun_out/r06f, profiles/r06_cell_*)
+#if defined(MOSAIC_CELL_WAVES)
+#define MOSAIC_CELL_ATTR __attribute__((amdgpu_waves_per_eu(MOSAIC_CELL_WAVES, MOSAIC_CELL_WAVES)))
+#else
+#define MOSAIC_CELL_ATTR
+#endif
+__global__ void __launch_bounds__(256) MOSAIC_CELL_ATTR k_cell_h3(CellArgs a) {
+    // the digit tables read from LDS (12.8 vs 13.6 ms per 1e9 points for the pair table from the
+    // constant table: gpurun_out/r06f, profiles/r06_cell_*), the four-level table of res's parity too
     __shared__ h3::AxialPairTab lpairs;
+    __shared__ uint32_t lquad[kCellQuad ? 2401 : 1];
     for (int k = threadIdx.x; k < 98; k += blockDim.x) (&lpairs.v[0][0])[k] = (&h3::kAxialPairs.v[0][0])[k];
+    if (kCellQuad) {
+        const uint32_t* gq = h3::kAxialQuads.v[a.res & 1];
+        for (int k = threadIdx.x; k < 2401; k += blockDim.x) lquad[k] = gq[k];
+    }
     __syncthreads();
-    const h3::AxialPairTab* ptab = &lpairs;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     constexpr int R = kCellRows;
     const int64_t np = (a.n + R - 1) / R;
@@ -1682,7 +1698,7 @@ __global__ void __launch_bounds__(256) k_cell_h3(CellArgs a) {
         }
         uint64_t cell[R];
         bool amb[R], rare[R];
-        h3::h3_fastk<R>(lat, lon, a.res, cell, amb, rare, ptab);
+        h3::h3_fastk_tab<R, kCellQuad>(lat, lon, a.res, cell, amb, rare, lpairs, lquad);
 #pragma unroll
         for (int k = 0; k < R; k++) {
             if (i + k >= a.n) continue;
@@ -1972,6 +1988,7 @@ struct Options {
     int bng_cell = 32;        // BNG dense table: sub-cells per border cell side (a power of two)
     int bng_group_lines = 1;  // BNG levels carry a line code where one line record decides a whole group
     int bng_wedges = 1;       // BNG tables: wedge records for sub-cells split at a chip vertex
+    int cell_blocks_per_cu = 256;  // k_cell_h3 grid: n_cu x this, grid-strided (0 = one lane per group of kCellRows rows)
     int mixed_blocks_per_cu = 4;  // k_join_mixed grid: the workgroups resident at once (~120 VGPRs: 4 per CU)
     int mixed_rows = 2;           // k_join_mixed: queued rows per lane and iteration (1, 2 or 4)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
@@ -2554,6 +2571,9 @@ int mosaic_set_option(mosaic_ctx* ctx, const char* key, int64_t v) {
     } else if (k == "blocks_per_cu") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "blocks_per_cu must be in [1, 64]");
         o.blocks_per_cu = (int)v;
+    } else if (k == "cell_blocks_per_cu") {
+        if (v < 0 || v > 4096) return fail(MOSAIC_E_ARG, "cell_blocks_per_cu must be in [0, 4096]");
+        o.cell_blocks_per_cu = (int)v;
     } else if (k == "raster") {
         if (v < 1 || v > 64) return fail(MOSAIC_E_ARG, "raster must be in [1, 64]");
         o.raster = (int)v;
@@ -2811,7 +2831,13 @@ static int point_to_cell_impl(ThreadCtx* c, int grid, int res, const double* x, 
     a.vec = (((uintptr_t)dx | (uintptr_t)dy | (uintptr_t)dout) & 15) == 0;  // (every group of rows starts 16-byte aligned: kCellRows even)
     int g = grid_size(c, n);
     if (grid == MOSAIC_GRID_H3) {
-        hipLaunchKernelGGL(k_cell_h3, dim3(g), dim3(c->block), 0, c->stream, a);
+        // k_cell_h3's grid: 256 blocks per CU by default -- at the common 8 (occupancy 7 at 66 VGPRs) it
+        // ran 11.1 ms per 1e9 points, 9.3 ms at 128-1024, 9.6 ms with one lane per row pair
+        // (gpurun_out/r06s, r06s2; profiles/r06_cell_grid_sweep.txt)
+        const int64_t groups = (n + kCellRows - 1) / kCellRows, want = (groups + c->block - 1) / c->block;
+        const int64_t gc = c->cell_blocks_per_cu ? std::min<int64_t>(want, (int64_t)c->n_cu * c->cell_blocks_per_cu) : want;
+        hipLaunchKernelGGL(k_cell_h3, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(gc, 0x7fffffff))), dim3(c->block),
+                           0, c->stream, a);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_cell_h3_exact, dim3(grid_size(c, (int64_t)cap)), dim3(c->block), 0, c->stream, a, 0);
         HIP_TRY(hipGetLastError());

@@ -90,7 +90,10 @@ int main(int argc, char** argv) {
             const double la2[2] = {plat, lat}, lo2[2] = {plon, lon};
             uint64_t c2[2];
             bool a2[2], r2[2];
-            mosaic::h3::h3_fast2(la2, lo2, res, c2, a2, r2);
+            if ((i >> 6) & 1)
+                mosaic::h3::h3_fast2(la2, lo2, res, c2, a2, r2);
+            else  // the four-level digit form (k_cell_h3's)
+                mosaic::h3::h3_fast2_quad(la2, lo2, res, c2, a2, r2);
             for (int k = 0; k < 2; k++)
                 if (r2[k]) c2[k] = mosaic::h3::h3_fast(la2[k], lo2[k], res, &a2[k]);  // (the caller's rare path)
             bool ap = false;

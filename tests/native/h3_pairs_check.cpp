@@ -1,5 +1,5 @@
-// CPU check of h3_device.h's two-level digit step (face_axial_to_h3, kAxialPairs) against the one-level
-// form (face_axial_to_h3_levels): every res 0..15 on every face, axial coordinates over the face's
+// CPU check of h3_device.h's two-level and four-level digit steps (face_axial_to_h3 with kAxialPairs,
+// face_axial_to_h3_quad with kAxialQuads) against the one-level form (face_axial_to_h3_levels): every res 0..15 on every face, axial coordinates over the face's
 // range (a dense block around the origin and random samples out to the res-15 face radius).  Prints
 // the number of inputs and of differences.
 #include <stdint.h>
@@ -9,6 +9,12 @@
 #include <random>
 
 #include "h3_device.h"
+
+static int check(int face, int a, int b, int res) {
+    const uint64_t want = mosaic::h3::face_axial_to_h3_levels(face, a, b, res);
+    return (mosaic::h3::face_axial_to_h3(face, a, b, res) != want) +
+           (mosaic::h3::face_axial_to_h3_quad(face, a, b, res, mosaic::h3::kAxialQuads.v[res & 1]) != want);
+}
 
 int main(int argc, char** argv) {
     const long n_rand = argc > 1 ? atol(argv[1]) : 1000000;
@@ -23,13 +29,13 @@ int main(int argc, char** argv) {
             for (int a = -60; a <= 60; a++)
                 for (int b = -60; b <= 60; b++) {
                     n++;
-                    bad += mosaic::h3::face_axial_to_h3(face, a, b, res) != mosaic::h3::face_axial_to_h3_levels(face, a, b, res);
+                    bad += check(face, a, b, res);
                 }
             std::uniform_int_distribution<int> u(-lim, lim);
             for (long t = 0; t < n_rand / 320; t++) {
                 const int a = u(rng), b = u(rng);
                 n++;
-                bad += mosaic::h3::face_axial_to_h3(face, a, b, res) != mosaic::h3::face_axial_to_h3_levels(face, a, b, res);
+                bad += check(face, a, b, res);
             }
         }
     }
