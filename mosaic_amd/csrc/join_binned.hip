@@ -353,6 +353,14 @@ __device__ __forceinline__ bool fbox_in(const uint32_t* cr, float fx, float fy) 
            fy <= __uint_as_float(cr[7]);
 }
 
+// the tile join's f32 ring walk: rolled (no scratch; 152 bytes per lane with the unrolled form);
+// a measurement build may set MOSAIC_TJ_UNROLLED_WALK
+#if defined(MOSAIC_TJ_UNROLLED_WALK)
+#define MOSAIC_TJ_WALK ringwalk::ring_interior_f32
+#else
+#define MOSAIC_TJ_WALK ringwalk::ring_interior_f32_rolled
+#endif
+
 // the tile join's rare paths, inlined (as calls, the C4 1e6 kernel went 8.87 -> 10.88 ms: call-site
 // register saves and spills)
 #define MOSAIC_TJ_NOINLINE __device__ __forceinline__
@@ -450,7 +458,7 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                         const uint32_t vi = cr[1], vc = vi >> 16;
                         int r = 2;
                         if (vc != binned::kImgGlobal)
-                            r = ringwalk::ring_interior_f32(V + 2u * (vi & 0xffffu), vc,
+                            r = MOSAIC_TJ_WALK(V + 2u * (vi & 0xffffu), vc,
                                                             ringwalk::f32_frame(__uint_as_float(cr[4]), __uint_as_float(cr[5]),
                                                                                 __uint_as_float(cr[6]), __uint_as_float(cr[7]), qx, qy));
                         // (global geometry, or a point the f32 walk leaves undecided: the f64 test)

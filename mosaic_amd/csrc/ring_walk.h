@@ -128,6 +128,32 @@ MOSAIC_HD int ring_interior_f32(const float* v, uint32_t n, const F32Frame& f) {
     }
     return amb ? 2 : (int)(cross & 1u);
 }
+// ring_interior_f32 as a rolled loop that reads the next vertex one step ahead (the walk the tile join
+// inlines: the unrolled form's registers made k_join_tiles spill, 152 bytes of scratch per lane).
+// Same decisions edge by edge; v must hold n >= 1 vertices.
+MOSAIC_HD int ring_interior_f32_rolled(const float* v, uint32_t n, const F32Frame& f) {
+    bool amb = false;
+    uint32_t cross = 0;
+    float x2 = v[0] - f.qx, y2 = v[1] - f.qy;
+    float nx = n > 1 ? v[2] : 0.0f, ny = n > 1 ? v[3] : 0.0f;
+#pragma unroll 1
+    for (uint32_t i = 1; i < n; i++) {
+        const float x1 = nx - f.qx, y1 = ny - f.qy;
+        const uint32_t j = i + 1 < n ? i + 1 : i;
+        nx = v[2 * j];
+        ny = v[2 * j + 1];
+        const bool a1 = y1 > f.tol, b1 = y1 < -f.tol, a2 = y2 > f.tol, b2 = y2 < -f.tol;
+        const bool skip = (x1 < -f.tol && x2 < -f.tol) || (a1 && a2) || (b1 && b2);
+        const bool strad = (a1 && b2) || (b1 && a2);
+        const float det = x1 * y2 - y1 * x2;
+        const bool pos = det > f.bound, neg = det < -f.bound;
+        amb |= !skip && !(strad && (pos || neg));
+        cross += (!skip && strad && (a1 ? neg : pos)) ? 1u : 0u;
+        x2 = x1;
+        y2 = y1;
+    }
+    return amb ? 2 : (int)(cross & 1u);
+}
 
 }  // namespace ringwalk
 }  // namespace mosaic
