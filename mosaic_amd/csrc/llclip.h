@@ -237,11 +237,19 @@ MOSAIC_HD bool pos_of(const Cell& C, Pt q, Pos* out) {
 }
 
 // ---- the geometry: closed rings as in the chip producer's flat arrays
+// Optional ring indexes (ring_blocks below; null: none): per ring, the envelopes of its stored edges
+// in blocks of kBlk -- the walks skip a block whose envelope cannot meet C (ring_chains) or the ray of
+// a point (locate_part), with the same comparisons the skipped edges would make, so the result does
+// not depend on them -- and Orientation.isCCW of every ring.
+static constexpr int kBlk = 16;
 struct Geom {
     const double* xy;             // interleaved vertices
     const int64_t* ring_offsets;  // ring r = vertices [ring_offsets[r], ring_offsets[r + 1]) (closed)
     const int64_t* part_rings;    // part p = rings [part_rings[p], part_rings[p + 1]); first = shell
     int64_t p0, p1;               // the geometry's parts
+    const double* blk = nullptr;        // block envelopes (x0, y0, x1, y1), ring r's from ring_blk[r]
+    const int64_t* ring_blk = nullptr;
+    const uint8_t* ring_ccw = nullptr;  // isCCW per ring
 };
 MOSAIC_HD Pt gv(const Geom& g, int64_t v) { return Pt{g.xy[2 * v], g.xy[2 * v + 1]}; }
 
@@ -275,11 +283,33 @@ MOSAIC_HD bool ring_is_ccw(const Geom& g, int64_t vb, int n) {
     return down_hi.x - up_hi.x < 0;
 }
 
+// The ring indexes of Geom: per ring its number of blocks; then per ring (host loop or one device lane
+// per ring) its block envelopes from blk = Geom::blk + 4 ring_blk[r] and its orientation.
+MOSAIC_HD int64_t ring_block_count(const int64_t* ro, int64_t r) {
+    const int64_t n = ro[r + 1] - ro[r] - 1;
+    return n > 0 ? (n + kBlk - 1) / kBlk : 0;
+}
+MOSAIC_HD void ring_blocks_one(const int64_t* ro, const double* xy, int64_t r, double* blk, uint8_t* ccw) {
+    const Geom g{xy, ro, nullptr, 0, 0};
+    const int64_t vb = ro[r], n = ro[r + 1] - vb - 1;
+    *ccw = n >= 3 && n <= 0x7fffffff && ring_is_ccw(g, vb, (int)n) ? 1 : 0;
+    for (int64_t j = 0; n > 0 && j * kBlk < n; j++) {
+        double x0 = xy[2 * (vb + j * kBlk)], y0 = xy[2 * (vb + j * kBlk) + 1], x1 = x0, y1 = y0;
+        const int64_t e = j * kBlk + kBlk < n ? j * kBlk + kBlk : n;
+        for (int64_t v = vb + j * kBlk + 1; v <= vb + e; v++) {
+            const double x = xy[2 * v], y = xy[2 * v + 1];
+            x0 = x < x0 ? x : x0, x1 = x > x1 ? x : x1, y0 = y < y0 ? y : y0, y1 = y > y1 ? y : y1;
+        }
+        blk[4 * j] = x0, blk[4 * j + 1] = y0, blk[4 * j + 2] = x1, blk[4 * j + 3] = y1;
+    }
+}
+
 // one ring walked with the interior on its left: oriented vertex k -> the stored vertex
 struct RingRef {
     int64_t vb;  // first stored vertex
     int32_t n;   // open vertex count
     int32_t rev; // walk reversed
+    int64_t blk = -1;  // the ring's first block envelope (Geom::blk), -1 without
 };
 MOSAIC_HD Pt rv(const Geom& g, const RingRef& r, int32_t k) {
     k %= r.n;
@@ -438,6 +468,14 @@ MOSAIC_HD int locate_part(Pt p, const Geom& g, int64_t part) {
         if (n < 3) continue;
         bool odd = false;
         for (int64_t i = 0; i < n; i++) {
+            if (g.blk && i % kBlk == 0) {
+                // a block wholly above or below p: no edge of it holds p or crosses its ray
+                const double* b = g.blk + 4 * (g.ring_blk[r] + i / kBlk);
+                if (b[1] > p.y || b[3] < p.y) {
+                    i += kBlk - 1;
+                    continue;
+                }
+            }
             const Pt a = gv(g, vb + i), b = gv(g, vb + i + 1);
             if (orient(a, b, p) == 0 && in_env(p, a, b)) return 1;
             if ((a.y > p.y) != (b.y > p.y)) {
@@ -470,6 +508,27 @@ MOSAIC_HD int ring_chains(const Geom& g, const Cell& C, const RingRef& R, int32_
     Pos evp[40];
     double evt[40];
     for (int32_t k = 0; k < n; k++) {
+        if (R.blk >= 0 && cur != 1) {
+            // a stored block of edges starting at oriented edge k whose envelope misses C's: each of
+            // its edges is a single piece outside C (the walk cannot be inside at its first vertex,
+            // which lies outside C's envelope)
+            int32_t j = -1, m = 0;
+            if (!R.rev) {
+                if (k % kBlk == 0) j = k / kBlk, m = n - k < kBlk ? n - k : kBlk;
+            } else if ((n - k) % kBlk == 0) {
+                j = (n - k) / kBlk - 1, m = kBlk;  // stored edges n - k - kBlk .. n - k - 1
+            }
+            if (j >= 0) {
+                const double* e = g.blk + 4 * (R.blk + j);
+                if (e[2] < C.x0 || e[0] > C.x1 || e[3] < C.y0 || e[1] > C.y1) {
+                    any_out = true;
+                    if (cur == -1) first_lab = 0;
+                    cur = 0;
+                    k += m - 1;
+                    continue;
+                }
+            }
+        }
         const Pt a = rv(g, R, k), b = rv(g, R, k + 1);
         if (same(a, b)) continue;
         int ne = 0;
@@ -621,8 +680,8 @@ MOSAIC_HD int clip(const Geom& g, const Cell& C, Work& w, double area_eps2, int3
             const int32_t n = (int32_t)(g.ring_offsets[r + 1] - vb - 1);
             if (n < 3) continue;
             const bool shell = r == g.part_rings[p];
-            const bool ccw = ring_is_ccw(g, vb, n);
-            RingRef R{vb, n, (int32_t)(ccw != shell)};
+            const bool ccw = g.ring_ccw ? g.ring_ccw[r] != 0 : ring_is_ccw(g, vb, n);
+            RingRef R{vb, n, (int32_t)(ccw != shell), g.blk ? g.ring_blk[r] : -1};
             int whole = 0;
             const int st = ring_chains(g, C, R, (int32_t)p, w, &whole);
             if (st) return st;

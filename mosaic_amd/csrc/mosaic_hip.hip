@@ -5757,10 +5757,34 @@ struct ClipLLBufs {
         for (DevBuf* b : {&tasks, &wch, &wout, &out, &cnt, &rings, &parts, &status}) b->release();
     }
 };
+// the ring indexes of the lon / lat clip on the device (llclip::Geom::blk / ring_blk / ring_ccw): block
+// offsets by a prefix over the host's ring offsets, envelopes and orientations by k_ring_blocks
+struct RingIdxDev {
+    DevBuf blk, rblk, ccw;
+    int build(ThreadCtx* c, int64_t n_rings, const int64_t* ro, const void* d_ro, const void* d_xy) {
+        std::vector<int64_t> rb((size_t)std::max<int64_t>(1, n_rings));
+        int64_t t = 0;
+        for (int64_t r = 0; r < n_rings; r++) rb[(size_t)r] = t, t += llclip::ring_block_count(ro, r);
+        int rc;
+        if ((rc = rblk.reserve(rb.size() * 8)) || (rc = blk.reserve((size_t)std::max<int64_t>(1, t) * 32)) ||
+            (rc = ccw.reserve((size_t)std::max<int64_t>(16, n_rings))) || (rc = h2d(c, rblk.p, rb.data(), (size_t)n_rings * 8)))
+            return rc;
+        HIP_TRY(mosaic::tessll::launch_ring_blocks((const int64_t*)d_ro, (const double*)d_xy, n_rings, (const int64_t*)rblk.p,
+                                                   (double*)blk.p, (uint8_t*)ccw.p, c->stream));
+        return MOSAIC_OK;
+    }
+    void release() {
+        blk.release();
+        rblk.release();
+        ccw.release();
+    }
+};
+
 static int run_clip_ll(ThreadCtx* c, ClipLLBufs& B, const void* d_gxy, const void* d_ro, const void* d_pr, const void* d_gp,
                        const void* d_cg, const void* d_cid, const void* d_clip, int nv, int mode,
                        const std::vector<int64_t>& tasks, const int32_t* cand_geom, const int64_t* geom_parts,
-                       const int64_t* part_rings, const int64_t* ring_offsets, tessclip::ClipResult* out) {
+                       const int64_t* part_rings, const int64_t* ring_offsets, tessclip::ClipResult* out,
+                       const RingIdxDev* ri) {
     const int64_t n_tasks = (int64_t)tasks.size();
     out->status.assign((size_t)n_tasks, 0);
     out->rings.clear();
@@ -5808,6 +5832,9 @@ static int run_clip_ll(ThreadCtx* c, ClipLLBufs& B, const void* d_gxy, const voi
     a.rings = (tessclip::ClipRing*)B.rings.p;
     a.parts = (tessclip::ClipPart*)B.parts.p;
     a.status = (uint8_t*)B.status.p;
+    a.blk = ri ? (const double*)ri->blk.p : nullptr;
+    a.ring_blk = ri ? (const int64_t*)ri->rblk.p : nullptr;
+    a.ring_ccw = ri ? (const uint8_t*)ri->ccw.p : nullptr;
     EventGuard ev;
     HIP_TRY(hipEventCreate(&ev.e[0]));
     HIP_TRY(hipEventCreate(&ev.e[1]));
@@ -5879,8 +5906,14 @@ int tessclip::clip_ll(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_part
         (rc = up(s_ro, ring_offsets, (size_t)(n_rings + 1) * 8)) || (rc = up(s_xy, xy, (size_t)n_verts * 16)) ||
         (rc = up(s_cg, cand_geom, (size_t)n_cand * 4)) || (rc = up(s_clip, clip, (size_t)n_cand * nv * 16)))
         return rc;
+    RingIdxDev ri;
+    struct RelRi {
+        RingIdxDev& r;
+        ~RelRi() { r.release(); }
+    } rel_ri{ri};
+    if ((rc = ri.build(c, n_rings, ring_offsets, s_ro.p, s_xy.p))) return rc;
     return run_clip_ll(c, B, s_xy.p, s_ro.p, s_pr.p, s_gp.p, s_cg.p, nullptr, s_clip.p, nv, 1, tasks, cand_geom, geom_parts,
-                       part_rings, ring_offsets, out);
+                       part_rings, ring_offsets, out, &ri);
 }
 
 // ---- mosaic_tessellate_gpu's H3 branch as one device session: the geometry batch is uploaded once,
@@ -5896,10 +5929,12 @@ struct tessclip::H3Session {
     double dx[6], dy[6];
     DevBuf d_gp, d_pr, d_ro, d_pxy, d_gxy, d_gf, d_cg, d_cxy, d_clip, d_cls, d_cn, d_cid, d_cnt;
     ClipLLBufs ll;
+    RingIdxDev ri;
     void release() {
         for (DevBuf* b : {&d_gp, &d_pr, &d_ro, &d_pxy, &d_gxy, &d_gf, &d_cg, &d_cxy, &d_clip, &d_cls, &d_cn, &d_cid, &d_cnt})
             b->release();
         ll.release();
+        ri.release();
     }
 };
 
@@ -5936,7 +5971,7 @@ int tessclip::h3_session_begin(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* 
     if ((rc = up(S->d_gp, geom_parts, (size_t)(n_geoms + 1) * 8)) || (rc = up(S->d_pr, part_rings, (size_t)(S->n_parts + 1) * 8)) ||
         (rc = up(S->d_ro, ring_offsets, (size_t)(S->n_rings + 1) * 8)) || (rc = up(S->d_pxy, pxy, (size_t)S->n_verts * 16)) ||
         (rc = up(S->d_gxy, gxy, (size_t)S->n_verts * 16)) || (rc = up(S->d_gf, gface, (size_t)n_geoms * 4)) ||
-        (rc = S->d_cnt.reserve(32))) {
+        (rc = S->d_cnt.reserve(32)) || (rc = S->ri.build(c, S->n_rings, ring_offsets, S->d_ro.p, S->d_gxy.p))) {
         S->release();
         delete S;
         return rc;
@@ -6030,7 +6065,29 @@ int tessclip::h3_session_chunk(H3Session* S, int64_t nc, const int32_t* cand_geo
     for (int64_t k = 0; k < nc; k++)
         if (cls[k] == 2) tasks.push_back(k);
     return run_clip_ll(c, S->ll, S->d_gxy.p, S->d_ro.p, S->d_pr.p, S->d_gp.p, S->d_cg.p, S->d_cid.p, nullptr, 0, 0, tasks,
-                       cand_geom, S->geom_parts, S->part_rings, S->ring_offsets, out);
+                       cand_geom, S->geom_parts, S->part_rings, S->ring_offsets, out, &S->ri);
+}
+
+int tessclip::h3_cell_vertices(H3Session* S, const std::vector<int64_t>& ids, std::vector<double>& v, std::vector<int32_t>& cnt) {
+    ENTER(S->ctx);
+    const int64_t n = (int64_t)ids.size();
+    v.resize((size_t)n * 20);
+    cnt.resize((size_t)n);
+    if (n == 0) return MOSAIC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    TmpBuf d_i, d_o, d_c, d_f;
+    int rc;
+    if ((rc = d_i.reserve((size_t)n * 8)) || (rc = d_o.reserve((size_t)n * 160)) || (rc = d_c.reserve((size_t)n * 4)) ||
+        (rc = d_f.reserve(16)) || (rc = h2d(c, d_i.p, ids.data(), (size_t)n * 8)))
+        return rc;
+    HIP_TRY(hipMemsetAsync(d_f.p, 0, 16, c->stream));
+    // k_h3_geom mode 1 with JDK 8's toDegrees: the vertices tessellate.cpp's h3_cell_ll computes
+    hipLaunchKernelGGL(k_h3_geom, dim3(grid_size(c, n)), dim3(c->block), 0, c->stream, (const int64_t*)d_i.p,
+                       (const uint8_t*)nullptr, n, 1, 8, d_o.p, (int32_t*)d_c.p, (unsigned int*)d_f.p);
+    HIP_TRY(hipGetLastError());
+    if ((rc = d2h(c, cnt.data(), d_c.p, (size_t)n * 4)) || (rc = d2h(c, v.data(), d_o.p, (size_t)n * 160))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MOSAIC_OK;
 }
 
 extern "C" {

@@ -32,10 +32,16 @@ struct ClipLLArgs {
     tessclip::ClipRing* rings;
     tessclip::ClipPart* parts;
     uint8_t* status;  // per task: 0 chip written (or none), 1 to the host, 2 written and equal to the cell
+    const double* blk;         // ring indexes (llclip::Geom; null: none)
+    const int64_t* ring_blk;
+    const uint8_t* ring_ccw;
 };
 
 // launch over `lanes` lanes (grid-stride over the tasks)
 hipError_t launch_clip_ll(const ClipLLArgs& a, int64_t lanes, hipStream_t stream);
+// the ring indexes of rings [0, n_rings) (llclip::ring_blocks_one, one lane per ring); ring_blk given
+hipError_t launch_ring_blocks(const int64_t* ro, const double* xy, int64_t n_rings, const int64_t* ring_blk, double* blk,
+                              uint8_t* ccw, hipStream_t stream);
 
 // layout fingerprint of the records mosaic_hip.hip and tess_clip.hip share (join_binned.h's rationale)
 static constexpr uint64_t layout_fingerprint() {

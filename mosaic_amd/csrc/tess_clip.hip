@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(256) k_tess_clip_ll(ClipLLArgs a) {
             a.status[t] = 1;
             continue;
         }
-        const llclip::Geom gg{a.gxy, a.ring_offsets, a.part_rings, a.geom_parts[g], a.geom_parts[g + 1]};
+        const llclip::Geom gg{a.gxy, a.ring_offsets, a.part_rings, a.geom_parts[g], a.geom_parts[g + 1], a.blk, a.ring_blk, a.ring_ccw};
         int32_t polys = 0;
         bool is_cell = false;
         const int st = llclip::clip(gg, C, w, 1e-12 * llclip::cell_area2(C), &polys, &is_cell);
@@ -85,6 +85,21 @@ __global__ void __launch_bounds__(256) k_tess_clip_ll(ClipLLArgs a) {
         }
         a.status[t] = is_cell ? 2 : 0;
     }
+}
+
+__global__ void __launch_bounds__(256) k_ring_blocks(const int64_t* ro, const double* xy, int64_t n_rings, const int64_t* ring_blk,
+                                                     double* blk, uint8_t* ccw) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_rings; r += step)
+        llclip::ring_blocks_one(ro, xy, r, blk + 4 * ring_blk[r], ccw + r);
+}
+
+hipError_t launch_ring_blocks(const int64_t* ro, const double* xy, int64_t n_rings, const int64_t* ring_blk, double* blk,
+                              uint8_t* ccw, hipStream_t stream) {
+    if (n_rings <= 0) return hipSuccess;
+    const int64_t blocks = (n_rings + 255) / 256 < 65536 ? (n_rings + 255) / 256 : 65536;
+    hipLaunchKernelGGL(k_ring_blocks, dim3((unsigned)blocks), dim3(256), 0, stream, ro, xy, n_rings, ring_blk, blk, ccw);
+    return hipGetLastError();
 }
 
 hipError_t launch_clip_ll(const ClipLLArgs& a, int64_t lanes, hipStream_t stream) {

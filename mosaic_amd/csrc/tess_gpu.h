@@ -53,6 +53,10 @@ int h3_session_begin(mosaic_ctx* ctx, int64_t n_geoms, const int64_t* geom_parts
 int h3_session_chunk(H3Session* s, int64_t n_cand, const int32_t* cand_geom, const double* cxy, double eps, uint8_t* cls,
                      std::vector<int64_t>& tasks, ClipResult* out, const int64_t* cand_id,
                      const double* clip_xy = nullptr, const int32_t* clip_n = nullptr, int nv_max = 0);
+// h3ToGeoBoundary of cells on the device (JDK 8 toDegrees, (lng, lat) degrees): v gets 20 doubles per id,
+// cnt the vertex count (0: not a valid cell) -- the core chips' geometry, which costs ~56 us per cell
+// on the host (x87-exact steps emulated)
+int h3_cell_vertices(H3Session* s, const std::vector<int64_t>& ids, std::vector<double>& v, std::vector<int32_t>& cnt);
 void h3_session_end(H3Session* s);
 
 }  // namespace tessclip

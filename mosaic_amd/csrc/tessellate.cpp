@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -449,6 +450,34 @@ std::atomic<int64_t> g_ll_fallbacks{0}, g_ll_chips{0};
 
 // H3 cell id -> its indexToGeometry polygon (h3ToGeoBoundary, degrees via JDK 8 Math.toDegrees, as
 // H3IndexSystem.scala:93-100 builds it); false when it is not a planar counter-clockwise polygon
+// the batch's ring indexes for the lon / lat clip (llclip::ring_blocks_one), built on first use (host
+// threads may call geom() at once)
+struct RingIdx {
+    int64_t n_rings = 0;
+    const double* xy;
+    const int64_t *ro, *pr;
+    mutable std::vector<double> blk;
+    mutable std::vector<int64_t> ring_blk;
+    mutable std::vector<uint8_t> ccw;
+    mutable std::once_flag once;
+    RingIdx(int64_t n_geoms, const int64_t* gp, const int64_t* pr_, const int64_t* ro_, const double* xy_)
+        : xy(xy_), ro(ro_), pr(pr_) {
+        if (n_geoms > 0 && gp && pr_ && ro_ && xy_) n_rings = pr_[gp[n_geoms]];
+    }
+    llclip::Geom geom(int64_t p0, int64_t p1) const {
+        std::call_once(once, [&] {
+            ring_blk.resize((size_t)std::max<int64_t>(1, n_rings));
+            ccw.resize((size_t)std::max<int64_t>(1, n_rings));
+            int64_t t = 0;
+            for (int64_t r = 0; r < n_rings; r++) ring_blk[(size_t)r] = t, t += llclip::ring_block_count(ro, r);
+            blk.resize((size_t)std::max<int64_t>(1, t) * 4);
+            for (int64_t r = 0; r < n_rings; r++)
+                llclip::ring_blocks_one(ro, xy, r, blk.data() + 4 * ring_blk[(size_t)r], ccw.data() + r);
+        });
+        return llclip::Geom{xy, ro, pr, p0, p1, blk.data(), ring_blk.data(), ccw.data()};
+    }
+};
+
 bool h3_cell_ll(int64_t id, llclip::Cell& C) {
     double b[20];
     const int nb = h3geom::h3_to_geo_boundary((uint64_t)id, b);
@@ -533,13 +562,13 @@ void emit_cell_ll(mosaic_chip_set* cs, int32_t key, const Cell& cell, const std:
     const int cls = pre >= 0 ? pre : classify_cell(cell, pl, core_eps);
     if (cls == 0) return;
     llclip::Cell C;
-    const bool cok = make_c(C);
     if (cls == 1) {
         std::vector<uint8_t> blob;
-        if (keep_core_geom) blob = to_wkb({{core_from_c && cok ? cell_ll_ring(C) : cell_ring(cell, to_geo)}});
+        if (keep_core_geom) blob = to_wkb({{core_from_c && make_c(C) ? cell_ll_ring(C) : cell_ring(cell, to_geo)}});
         cs->add(true, cell.id, key, blob);
         return;
     }
+    const bool cok = make_c(C);
     if (cok) {
         bool is_cell = false;
         std::vector<uint8_t> blob;
@@ -1101,6 +1130,7 @@ extern "C" {
 int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_parts, const int64_t* part_rings,
                       const int64_t* ring_offsets, const double* xy, int keep_core_geom, int densify,
                       mosaic_chip_set** out) {
+    const RingIdx ri(n_geoms, geom_parts, part_rings, ring_offsets, xy);
     if (!out || n_geoms < 0 || (n_geoms > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy)))
         return mosaic_tess_fail(MOSAIC_E_ARG, "invalid argument");
     if (grid == MOSAIC_GRID_H3 && (res < 0 || res > 15))
@@ -1138,7 +1168,7 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                         multi = multi || f != face;
                     }
             if (multi) {  // cells on several faces: per-face pieces (tessellate_h3_multiface)
-                const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+                const llclip::Geom gg = ri.geom(geom_parts[g], geom_parts[g + 1]);
                 if (tessellate_h3_multiface(cs, (int32_t)g, res, D, keep_core_geom, geo, gg)) {
                     delete cs;
                     return mosaic_tess_fail(MOSAIC_E_ARG, "geometry too large for a gnomonic face plane "
@@ -1181,7 +1211,7 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                     // densified clip polygon: SH on the densified (still convex) hexagon keeps the
                     // cell boundary within ~1/D^2 of the great-circle arcs once mapped back
                     cell.clip = cell.outline;
-                    const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+                    const llclip::Geom gg = ri.geom(geom_parts[g], geom_parts[g + 1]);
                     emit_cell_ll(cs, (int32_t)g, cell, pl, geo, gg, 1e-3, keep_core_geom,
                                  [&](P2 h) { return fp.to_geo(h); }, 1e-12,
                                  [&](llclip::Cell& C) { return h3_cell_ll(cell.id, C); }, D == 1);
@@ -1211,7 +1241,7 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
                     int64_t id;
                     if (!bng::point_to_index(cx0 + 0.5 * e, cy0 + 0.5 * e, res, &id)) continue;
                     cell.id = id;
-                    const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+                    const llclip::Geom gg = ri.geom(geom_parts[g], geom_parts[g + 1]);
                     emit_cell_ll(cs, (int32_t)g, cell, geo, geo, gg, 1e-9 * e, keep_core_geom, [](P2 h) { return h; },
                                  1e-12 * e * e, [&](llclip::Cell& C) { return bng_cell_ll(cx0, cy0, e, C); }, true);
                 }
@@ -1226,6 +1256,7 @@ int mosaic_tessellate(int grid, int res, int64_t n_geoms, const int64_t* geom_pa
 static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const int64_t* geom_parts,
                              const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
                              int keep_core_geom, int densify, mosaic_chip_set** out) {
+    const RingIdx ri(n_geoms, geom_parts, part_rings, ring_offsets, xy);
     if (res < 0 || res > 15)
         return mosaic_tess_fail(MOSAIC_E_RES, ("H3 resolution has to be between 0 and 15; found " + std::to_string(res)).c_str());
     if (densify < 1 || densify > 64) return mosaic_tess_fail(MOSAIC_E_ARG, "densify must be in [1, 64]");
@@ -1380,7 +1411,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         for (; next_multi < multi_geoms.size() && multi_geoms[next_multi] < upto; next_multi++)
         {
             const int64_t g = multi_geoms[next_multi];
-            const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[g], geom_parts[g + 1]};
+            const llclip::Geom gg = ri.geom(geom_parts[g], geom_parts[g + 1]);
             multiface_emit(cs, (int32_t)g, res, keep_core_geom, mfs[next_multi], mgeos[next_multi], gg);
         }
         return MOSAIC_OK;
@@ -1416,6 +1447,20 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
         }
         trace.add(2);
         cc.index(nc, tasks);
+        // core chips' geometry (indexToGeometry of the cell) from the device: h3ToGeoBoundary costs ~56
+        // us per cell on the host (x87-exact steps emulated), the whole res-11 NYC build on 16 threads
+        std::vector<int64_t> core_ids;
+        std::vector<int32_t> core_idx, core_cnt;
+        std::vector<double> core_v;
+        if (keep_core_geom && D == 1) {
+            core_idx.assign((size_t)nc, -1);
+            for (int64_t kk = 0; kk < nc; kk++)
+                if (cls[kk] == 1) core_idx[(size_t)kk] = (int32_t)core_ids.size(), core_ids.push_back(cid[k0 + kk]);
+            if ((rc = tessclip::h3_cell_vertices(S, core_ids, core_v, core_cnt))) {
+                delete cs;
+                return rc;
+            }
+        }
         trace.add(3);
         // the chunk's chips on host threads (each candidate's chip is independent: GPU-clipped border
         // chips to WKB, core chips' outlines, cells the GPU clipper left to the host).  Thread t takes
@@ -1463,6 +1508,24 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
                         continue;
                     }
                     o.built = 1;
+                    if (cls[kk] == 1 && !core_idx.empty()) {
+                        // (h3_cell_ll's cell from the device's vertices; a cell that is not a planar polygon
+                        // takes emit_cell_ll below, whose core chip is then the face-plane outline)
+                        const int32_t ci = core_idx[(size_t)kk], nb = core_cnt[(size_t)ci];
+                        llclip::Cell C;
+                        if (nb >= 3 && nb <= 10) {
+                            C.nc = nb;
+                            for (int q = 0; q < nb; q++) C.v[q] = {core_v[20 * (size_t)ci + 2 * q], core_v[20 * (size_t)ci + 2 * q + 1]};
+                            llclip::cell_init(C);
+                            if (llclip::cell_ok(C, true)) {
+                                const std::vector<uint8_t> blob = to_wkb({{cell_ll_ring(C)}});
+                                o.core = 1;
+                                w.b.insert(w.b.end(), blob.begin(), blob.end());
+                                o.len = (int32_t)blob.size();
+                                continue;
+                            }
+                        }
+                    }
                     if (cg[k] != cur) {
                         cur = cg[k];
                         fp.init(gface[cur], res);
@@ -1493,7 +1556,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
                     tmp.key.clear();
                     tmp.wkb_offsets.assign(1, 0);
                     tmp.wkb.clear();
-                    const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[cur], geom_parts[cur + 1]};
+                    const llclip::Geom gg = ri.geom(geom_parts[cur], geom_parts[cur + 1]);
                     emit_cell_ll(&tmp, (int32_t)cur, cell, pl, geo, gg, 1e-3, keep_core_geom, [&](P2 h) { return fp.to_geo(h); },
                                  1e-12, [&](llclip::Cell& C) { return h3_cell_ll(cell.id, C); }, D == 1, (int)cls[kk]);
                     if (!tmp.index_id.empty()) {
@@ -1608,6 +1671,7 @@ static int tessellate_gpu_h3(mosaic_ctx* ctx, int res, int64_t n_geoms, const in
 int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, const int64_t* geom_parts,
                           const int64_t* part_rings, const int64_t* ring_offsets, const double* xy,
                           int keep_core_geom, int densify, mosaic_chip_set** out) {
+    const RingIdx ri(n_geoms, geom_parts, part_rings, ring_offsets, xy);
     if (!ctx || !out || n_geoms < 0 || (n_geoms > 0 && (!geom_parts || !part_rings || !ring_offsets || !xy)))
         return mosaic_tess_fail(MOSAIC_E_ARG, "invalid argument");
     if (grid == MOSAIC_GRID_H3)
@@ -1700,7 +1764,7 @@ int mosaic_tessellate_gpu(mosaic_ctx* ctx, int grid, int res, int64_t n_geoms, c
         cell.clip = {{cx0, cy0}, {cx0 + e, cy0}, {cx0 + e, cy0 + e}, {cx0, cy0 + e}};
         cell.outline = cell.clip;
         cell.id = cid[k];
-        const llclip::Geom gg{xy, ring_offsets, part_rings, geom_parts[cur], geom_parts[cur + 1]};
+        const llclip::Geom gg = ri.geom(geom_parts[cur], geom_parts[cur + 1]);
         emit_cell_ll(cs, (int32_t)cur, cell, geo, geo, gg, 1e-9 * e, keep_core_geom, [](P2 h) { return h; }, 1e-12 * e * e,
                      [&](llclip::Cell& C) { return bng_cell_ll(cx0, cy0, e, C); }, true, (int)cls[k]);
     }
