@@ -111,7 +111,8 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * 16), "raster_lines" (0/1: sub-blocks crossed by one straight chip edge store a line record instead
  * of a leaf block; default 1), "raster_leaf_lines" (0/1: leaf cells of the other mixed sub-blocks
  * crossed by one straight chip edge store a line record too, answered by k_join_leaf before
- * k_join_mixed; default 0), "leaf_join" (0/1: joins run k_join_leaf on the mixed queue; default 1),
+ * k_join_mixed; default 1 since round 6: the reference's chord-edged border chips leave ~1.6x more
+ * mixed leaf rows than face-plane chips did), "leaf_join" (0/1: joins run k_join_leaf on the mixed queue; default 1),
  * "raster_build" (1: the point raster is classified on the GPU, the
  * default; 0: on host threads -- identical bytes), "raster_quad" (its LDS level: 0 off, 1 default budget of 32768
  * entries, or an entry budget <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of

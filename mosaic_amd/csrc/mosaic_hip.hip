@@ -1975,7 +1975,7 @@ struct Options {
     int raster_quad = 1;      // point raster: LDS quad level
     int raster_lines = 1;     // point raster: line records for single-edge sub-blocks
     int raster_tb_lds = 1;    // tile bases in the stream kernels' LDS: 1 up to 1/3 of it, 2 only when small (1/16), 0 never
-    int raster_leaf_lines = 0;  // point raster: line records for single-edge leaf cells (leaf lines)
+    int raster_leaf_lines = 1;  // point raster: line records for single-edge leaf cells (leaf lines; default since round 6)
     int leaf_join = 1;        // k_join_leaf answers the mixed queue's leaf-line rows before k_join_mixed
     int leaf_blocks_per_cu = 2;  // k_join_leaf grid
     int exact_defer = 0;      // stream joins: uncertified rows to k_join_h3_exact after k_join_mixed

@@ -35,7 +35,7 @@ def _build(ctx, chips, res, npoly, gpu, **opts):
     finally:
         ctx.set_option("raster_build", 1)
         for k in opts:
-            ctx.set_option(k, {"raster_sub": 64, "raster_cell": 16, "raster_lines": 1, "raster_leaf_lines": 0}[k])
+            ctx.set_option(k, {"raster_sub": 64, "raster_cell": 16, "raster_lines": 1, "raster_leaf_lines": 1}[k])
 
 
 @pytest.mark.parametrize("res,ids,opts", [
@@ -44,7 +44,7 @@ def _build(ctx, chips, res, npoly, gpu, **opts):
     (8, None, {"raster_lines": 0}),
     (10, range(0, 263, 5), {"raster_sub": 16, "raster_cell": 8}),
     (11, range(0, 263, 29), {"raster_sub": 32, "raster_cell": 4}),
-    (9, None, {"raster_leaf_lines": 1}),
+    (9, None, {"raster_leaf_lines": 0}),
     (10, range(0, 263, 5), {"raster_sub": 16, "raster_cell": 8, "raster_leaf_lines": 1}),
 ])
 def test_gpu_raster_equals_host_raster(ctx, zones, res, ids, opts):

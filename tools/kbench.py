@@ -31,6 +31,8 @@ def main():
     p.add_argument("--sweep", nargs="*", default=[""], help="option sets to time, e.g. stream_pipe=0 stream_pipe=1")
     p.add_argument("--build-opts", nargs="*", default=[""],
                    help="option sets applied before each table build, e.g. raster_quad_records=0")
+    p.add_argument("--save-chips", default="", help="write the chip set to this .npz (A/B of chips against code)")
+    p.add_argument("--chips", default="", help="join these chips (.npz from --save-chips) instead of tessellating")
     args = p.parse_args()
     import torch
 
@@ -40,7 +42,15 @@ def main():
 
     zones = PolygonSet.load(args.zones)
     t0 = time.perf_counter()
-    chips = tessellate("H3", zones, args.res)
+    if args.chips:
+        z = np.load(args.chips)
+        chips = {"is_core": z["is_core"], "index_id": z["index_id"], "polygon_key": z["polygon_key"],
+                 "wkb": (z["wkb_offsets"], z["wkb_data"])}
+    else:
+        chips = tessellate("H3", zones, args.res)
+    if args.save_chips:
+        np.savez(args.save_chips, is_core=chips["is_core"], index_id=chips["index_id"], polygon_key=chips["polygon_key"],
+                 wkb_offsets=chips["wkb"][0], wkb_data=chips["wkb"][1])
     tess_s = time.perf_counter() - t0
     ctx = MosaicContext.build("H3")
     n = int(args.n)
