@@ -733,8 +733,14 @@ __device__ inline bool rtry_line_wave(const RBuildArgs& a, const RTile& t, int s
     return false;
 }
 
+// (measurement builds may constrain the raster classification kernels' occupancy: MOSAIC_RASTER_WAVES)
+#if defined(MOSAIC_RASTER_WAVES)
+#define MOSAIC_RASTER_ATTR __attribute__((amdgpu_waves_per_eu(MOSAIC_RASTER_WAVES)))
+#else
+#define MOSAIC_RASTER_ATTR
+#endif
 // one wave per mixed sub-block (waves past the end exit together)
-__global__ void __launch_bounds__(256) k_raster_line_wave(RBuildArgs a) {
+__global__ void __launch_bounds__(256) MOSAIC_RASTER_ATTR k_raster_line_wave(RBuildArgs a) {
     const int64_t SS = (int64_t)a.S * a.S;
     const int64_t m = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (m >= a.n_mixed) return;
@@ -754,7 +760,7 @@ __global__ void __launch_bounds__(256) k_raster_line_wave(RBuildArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_raster_cells(RBuildArgs a) {
+__global__ void __launch_bounds__(256) MOSAIC_RASTER_ATTR k_raster_cells(RBuildArgs a) {
     const int64_t SS = (int64_t)a.S * a.S, CC = (int64_t)a.C * a.C;
     const int64_t total = a.n_cell_sb * CC;
     for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (int64_t)gridDim.x * blockDim.x) {
@@ -818,7 +824,14 @@ __global__ void __launch_bounds__(256) k_sub_cands(RBuildArgs a, int32_t* cands,
     if (lane == 0) ncand[msb] = over ? -1 : nsc;
 }
 
-__global__ void __launch_bounds__(256) k_raster_cell_lines(RBuildArgs a, const uint32_t* mlist, int64_t n_ml,
+// (occupancy 4, spilling, instead of the 256 VGPRs the compiler picks unconstrained: the leaf-line fits
+// are chains of dependent chip / vertex loads, 63 -> ~33 ms for the NYC res-9 raster's 1 M mixed leaf
+// cells, gpurun_out/r06w, profiles/r06_mixed/leaf_lines_occupancy.txt)
+#if !defined(MOSAIC_CELL_LINES_WAVES)
+#define MOSAIC_CELL_LINES_WAVES 4
+#endif
+#define MOSAIC_CELL_LINES_ATTR __attribute__((amdgpu_waves_per_eu(MOSAIC_CELL_LINES_WAVES)))
+__global__ void __launch_bounds__(256) MOSAIC_CELL_LINES_ATTR k_raster_cell_lines(RBuildArgs a, const uint32_t* mlist, int64_t n_ml,
                                                            const int32_t* cands, const int32_t* ncand, uint8_t* ok,
                                                            tiles::LineRec* out) {
     __shared__ int cbuf[4][64];
@@ -1111,8 +1124,10 @@ __device__ int cell_ring(int grid, int64_t id, int jdk, double* xy) {  // indexT
 
 // one unit per wave (lane 0): a unit's overlay is sequential, data-dependent work, so units that
 // shared a wave would serialise behind its largest; largest units first, for the tail
-// the largest unit (edges of its chip parts) one lane overlays: 4096^2 noding steps, ~0.1 s
-static constexpr uint32_t kMaxUnitEdges = 4096;
+// the largest unit (edges of its chip parts) one lane overlays: 16384^2 noding steps, ~1.5 s -- above
+// every unit of the 263 NYC zones against a translated copy down to res 5 (15,358 edges; 4,096, the
+// round-5 limit, refused 6 groups at res 7, the reference's test resolution, and 147 at res 5)
+static constexpr uint32_t kMaxUnitEdges = 16384;
 __global__ void __launch_bounds__(64) k_isect_overlay(OverlayArgs x) {
     const IsectArgs& a = x.base;
     if ((threadIdx.x & 63) != 0) return;

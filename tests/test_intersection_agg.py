@@ -430,9 +430,10 @@ def _rows(chips):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("res", [8, 9, 10])
+@pytest.mark.parametrize("res", [5, 7, 8, 9, 10])
 def test_gpu_intersection_agg_geometry_nyc(h3ctx, res):
-    """all 263 NYC zones against a translated copy: no group refused; the area API and
+    """all 263 NYC zones against a translated copy (res 7 the reference's test resolution,
+    res 5 a coarse one where the stitch tolerance must stay bounded): no group refused; the area API and
     the geometry API agree; sampled groups' polygons equal the exact union of their cells' increments
     (symmetric difference ~0), dissolved across cells"""
     zones = PolygonSet.load("nyc_taxi_zones")
@@ -441,14 +442,21 @@ def test_gpu_intersection_agg_geometry_nyc(h3ctx, res):
     left, right = _table(h3ctx, _rows(lc), res, len(zones)), _table(h3ctx, _rows(rc), res, len(zones))
     lk, rk, area, st, wkb = h3ctx.st_intersection_aggregate(left, right)
     lk2, rk2, area2, st2 = h3ctx.st_intersection_aggregate_area(left, right)
-    assert len(lk) > 500 and not st.any() and not st2.any()
+    assert len(lk) > 500 and np.array_equal(st, st2)
+    if res >= 7:
+        assert not st.any()
+    else:
+        # coarse cells hold whole zones: a unit past the overlay's per-unit edge limit, or a stitch
+        # whose area disagrees with the units', is refused (status 1, area NaN), never returned
+        # distorted; the rest are exact
+        assert st.mean() < 0.05 and np.isnan(area[st != 0]).all(), (int(st.sum()), len(st))
     assert np.array_equal(lk, lk2) and np.array_equal(rk, rk2)
     assert np.array_equal(area.view(np.uint64), area2.view(np.uint64))  # (one unit pipeline)
     groups = _units(_chip_index(lc), _chip_index(rc))
     assert set(zip(lk.tolist(), rk.tolist())) == set(groups)
     idx = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(lk, rk))}
     rng = np.random.default_rng(res)
-    sample = [k for k in sorted(groups) if len(groups[k]) > 1 and len(groups[k]) <= 40]
+    sample = [k for k in sorted(groups) if len(groups[k]) > 1 and len(groups[k]) <= 40 and st[idx[k]] == 0]
     for g in [sample[i] for i in rng.choice(len(sample), min(12, len(sample)), replace=False)]:
         us = [_increments(lv, rv, cell) for cell, lv, rv in groups[g]]
         _check_group(us, wkb[idx[g]], area[idx[g]], h3_snap(res))
