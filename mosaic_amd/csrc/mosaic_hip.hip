@@ -4545,7 +4545,9 @@ static int run_join(ThreadCtx* c, const mosaic_chips* ch, const double* x, const
                 if (leafq) {
                     uint32_t* q2 = (uint32_t*)c->mix_queue2.p;
                     unsigned long long* q2c = sc + 7;
-                    HIP_TRY(hipMemsetAsync(q2c, 0, 8, c->stream));
+                    // (k_zero_join cleared it for the first chunk: no fill dispatch between the stream and
+                    // leaf kernels)
+                    if (lo > 0) HIP_TRY(hipMemsetAsync(q2c, 0, 8, c->stream));
                     void* largs[] = {&ac, &sa, &q2, &q2c};
                     HIP_TRY(hipLaunchKernel(leaf_kernel(lds, pairs), dim3((unsigned)lb), dim3(256), largs,
                                             (lds && !pairs ? shm : 0) + 4 * kStageWords * 4, c->stream));
