@@ -82,7 +82,14 @@ __global__ void __launch_bounds__(256) k_bin_keys(JoinArgs a, int64_t lo, int64_
 // waiting on anything -- whatever order the hardware dispatches workgroups in.  The wait is still
 // bounded (spin_cap polls; then *err is set and the caller reruns the pass uncompacted; spin_cap < 0
 // forces that fallback, for its test).
-static const int kBinPPT = 8;  // points per thread (4: the pass 20 % slower)
+#if defined(MOSAIC_BIN_PPT)
+static const int kBinPPT = MOSAIC_BIN_PPT;  // (measurement builds: 2 .. 16)
+#else
+// points per thread (4: the pass 20 % slower than 8; 16, the most the per-(item, wave) scan of one wave
+// holds: C4 at 1e6 buildings 15.12 -> 14.18 ms, gpurun_out/r06p)
+static const int kBinPPT = 16;
+#endif
+static_assert(kBinPPT % 2 == 0 && kBinPPT * 4 <= 64, "k_bin_cover's offsets scan is one wave");
 static const int kBinChunk = 256 * kBinPPT;
 static const unsigned long long kStAgg = 1ULL << 62, kStPre = 2ULL << 62, kStVal = (1ULL << 62) - 1;
 
@@ -207,12 +214,12 @@ __global__ void __launch_bounds__(256) k_bin_cover(const double* __restrict__ X,
         const uint32_t c = lane < kBinPPT * 4 ? woff[lane] : 0u;
         uint32_t incl = c;
 #pragma unroll
-        for (int d = 1; d < 32; d <<= 1) {
+        for (int d = 1; d < kBinPPT * 4; d <<= 1) {
             const uint32_t t = __shfl_up(incl, d, 64);
             if (lane >= d) incl += t;
         }
         if (lane < kBinPPT * 4) woff[lane] = incl - c;
-        const unsigned long long T = (unsigned long long)__shfl(incl, 31, 64);
+        const unsigned long long T = (unsigned long long)__shfl(incl, kBinPPT * 4 - 1, 64);
         // decoupled look-back: lane l reads workgroup j - l's status
         unsigned long long excl = 0;
         if (spin_cap < 0 && lane == 0) atomicOr(err, 1u);
