@@ -341,7 +341,11 @@ __global__ void __launch_bounds__(256) k_join_binned(JoinArgs a, const uint32_t*
 // near a building lies in few of its cell's chip envelopes) are compacted into a per-wave LDS
 // buffer whose full sets of 64 run the ring walk -- no lane of a ring-walking wave idles on a pair
 // the envelope already rejected.
+#if defined(MOSAIC_TJ_SEG)
+static const int kSegPoints = MOSAIC_TJ_SEG;  // (measurement builds)
+#else
 static const int kSegPoints = 2048;
+#endif
 
 static const int kSurv = 128;  // per wave: surviving pairs (64 appended at most before a flush)
 static const uint32_t kSurvGlobal = 0x80000000u;  // a buffered pair's chip is in the chip table
