@@ -72,7 +72,7 @@ def test_concurrent_joins_on_one_context(h3ctx):
     for th in threads:
         th.join(timeout=300)
     h3ctx.set_option("stream_block", 1024)
-    h3ctx.set_option("mixed_rows", 2)
+    h3ctx.set_option("mixed_rows", 1)
     table.close()
     assert not any(th.is_alive() for th in threads)
     assert not errors, errors[:5]
