@@ -1540,7 +1540,10 @@ __global__ void __launch_bounds__(256) k_join_mixed_bng(JoinArgs a) {
 // raster chip loop runs once per row slot (wave-cooperative, so wave-uniform).  Rows the fast path
 // cannot certify, kFull tiles and window misses take tiled_cell (the generic path).
 template <bool LDS_COUNTS, bool PAIRS, int R>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_join_mixed(JoinArgs a) {
+#if !defined(MOSAIC_MIXED_WAVES)
+#define MOSAIC_MIXED_WAVES 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MOSAIC_MIXED_WAVES))) k_join_mixed(JoinArgs a) {
     extern __shared__ unsigned int lds[];
     __shared__ SlabItem items[4][16];
     counts_init<LDS_COUNTS>(a, lds);
