@@ -118,7 +118,7 @@ int mosaic_destroy(mosaic_ctx* ctx);
  * entries, or an entry budget <= 65536), "stream_block" (k_join_stream workgroup size, a multiple of
  * 64 up to 1024, default 1024), "host_chunk" (rows per chunk when mosaic_pip_join_count gets
  * host-resident coordinates: the next chunk's copy overlaps the current chunk's join; 0 = stage the
- * whole batch; default 2^25), "mixed_rows" (1/2/4, default 1), "mixed_blocks_per_cu", "cell_blocks_per_cu" (k_cell_h3 grid, default 256; 0 = one lane per row pair), "stream_pipe"
+ * whole batch; default 2^25), "mixed_rows" (1/2/4, default 1), "mixed_blocks_per_cu" (default 16), "cell_blocks_per_cu" (k_cell_h3 grid, default 256; 0 = one lane per row pair), "stream_pipe"
  * (0: k_join_stream; 1: the software-pipelined H3 stream kernel; 2: it with the gathering rows
  * compacted, k_join_stream_cpt, the default -- each where it applies), "bng_cpt" (0/1: the compacted
  * BNG stream kernel where it applies; default 1), "bng_lds" (0/1: BNG tables

@@ -2007,7 +2007,7 @@ struct Options {
     int bng_group_lines = 1;  // BNG levels carry a line code where one line record decides a whole group
     int bng_wedges = 1;       // BNG tables: wedge records for sub-cells split at a chip vertex
     int cell_blocks_per_cu = 256;  // k_cell_h3 grid: n_cu x this, grid-strided (0 = one lane per group of kCellRows rows)
-    int mixed_blocks_per_cu = 4;  // k_join_mixed grid: the workgroups resident at once (~120 VGPRs: 4 per CU)
+    int mixed_blocks_per_cu = 16;  // k_join_mixed(_bng) grid (16 since round 6: BNG mixed 0.68 -> 0.59 ms at C5, H3 unchanged; gpurun_out/r06bm2)
     int mixed_rows = 1;  // k_join_mixed rows per lane (1 since round 6: 0.278 -> 0.235 ms at C2 on the reference's chips, gpurun_out/r06mr2)
     // host-resident coordinates (mosaic_pip_join_count): chunks of host_chunk rows, the next chunk's
     // copy on copy_stream overlapping the current chunk's join (0: stage the whole batch first)
