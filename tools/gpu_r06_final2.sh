@@ -17,3 +17,5 @@ echo bench done
 echo prof done
 timeout -k 10 200 python3 -u tools/kbench.py --reps 10 --clustered --res 10 > $O/c3.txt 2>&1 || exit 1
 echo c3 done
+timeout -k 10 200 python3 -u tools/kbench_bng.py --reps 5 > $O/c5.txt 2>&1 || exit 1
+echo c5 done
