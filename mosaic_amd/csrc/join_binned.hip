@@ -553,6 +553,9 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 const bool live = w0 + (uint32_t)lane < T;
+#if defined(MOSAIC_TJ_COUNT_FORMED)  // measurement build: the stat counts every pair formed instead
+                tests += live ? 1u : 0u;
+#endif
                 const uint32_t ent = live ? pb[lane] : 0u;
                 const int owner = (int)(ent & 63u);
                 const double qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64);
@@ -571,7 +574,9 @@ k_join_tiles(JoinArgs a, const uint32_t* __restrict__ keys, const P* __restrict_
                         else
                             emit_hit<CM, PAIRS>(a, qrow, meta >> 1, cnt);
                     } else {
+#if !defined(MOSAIC_TJ_COUNT_FORMED)
                         tests++;
+#endif
                         surv = qg ? !pip::box_excludes(a.store.geom_bbox[c], qx, qy) : fbox_in(cr, (float)qx, (float)qy);
                     }
                 }
