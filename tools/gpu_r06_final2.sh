@@ -19,3 +19,6 @@ timeout -k 10 200 python3 -u tools/kbench.py --reps 10 --clustered --res 10 > $O
 echo c3 done
 timeout -k 10 200 python3 -u tools/kbench_bng.py --reps 5 > $O/c5.txt 2>&1 || exit 1
 echo c5 done
+timeout -k 10 300 python3 -u tools/kbench_c4.py --buildings 1e6 --n 2.5e8 --reps 5 > $O/c4_1e6.txt 2>&1 || exit 1
+timeout -k 10 400 python3 -u tools/kbench_c4.py --buildings 5e6 --n 2.5e8 --reps 3 > $O/c4_5e6.txt 2>&1 || exit 1
+echo c4 done
