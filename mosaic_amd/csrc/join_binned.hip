@@ -644,10 +644,15 @@ namespace binned {
 
 // Onesweep radix sort of (key, point) over bits [0, end_bit) with R bits per pass: keys of 17-22
 // bits (image keys of large tables) sort in two passes instead of hipcub's three 8-bit ones.
+#if !defined(MOSAIC_SORT_BLOCK)  // (measurement builds may set the onesweep block and items per thread)
+#define MOSAIC_SORT_BLOCK 1024
+#define MOSAIC_SORT_ITEMS 12
+#endif
 template <unsigned R>
 using OnesweepR = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 12>, rocprim::kernel_config<1024, 12>, R,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<MOSAIC_SORT_BLOCK, MOSAIC_SORT_ITEMS>,
+                                        rocprim::kernel_config<MOSAIC_SORT_BLOCK, MOSAIC_SORT_ITEMS>, R,
                                         rocprim::block_radix_rank_algorithm::match>>;
 template <unsigned R, class P>
 static hipError_t sort_r(void* tmp, size_t& tb, uint32_t* const k[2], P* const v[2], int64_t m, int end_bit,
